@@ -1,0 +1,146 @@
+/*
+ * grk.h -- C ABI of libgrk.so, the MI355X (gfx950) hot path of the TencentGR
+ * sequence-recommender training step.
+ *
+ * The reference (Puiching-Memory/Tencent_Recommendation_2025) has no native
+ * code and no FFI: its hot path is PyTorch ops called from Python
+ * (SURVEY.md §8(b)).  Each entry point below replaces the device work of one
+ * reference call site, cited per function; the Python host layer
+ * (tencent_recommendation_2025_amd/kernels.py) binds them with ctypes and
+ * exposes them as torch.library ops under the reference's nn.Module surface.
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers unless noted; the caller (the torch
+ *    caching allocator) owns every buffer, including workspace.  The library
+ *    never allocates, frees or synchronises, so every call can be captured
+ *    into a hipGraph.
+ *  - Work is enqueued on `stream` (a hipStream_t passed as void*).
+ *  - Return 0 on success, else a GRK_E* code; grk_last_error() returns the
+ *    thread-local message.  Shape/argument errors are detected on the host
+ *    before any launch.  Out-of-range indices are detected on the device: the
+ *    offending lookup reads/writes nothing and, if `err_flag` is non-NULL,
+ *    *err_flag is set to 1 (the torch layer checks it lazily).
+ *  - Matrices are row-major with an explicit leading dimension in elements.
+ */
+#ifndef GRK_H_
+#define GRK_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { GRK_OK = 0, GRK_EINVAL = 1, GRK_EHIP = 2, GRK_EUNSUPPORTED = 3 };
+enum { GRK_F32 = 0, GRK_BF16 = 1 };                 /* floating dtypes */
+enum { GRK_I32 = 0, GRK_I64 = 1 };                  /* index dtypes */
+
+/* How a lookup derives its row id from the index tensor value v at token
+ * (n = b*T + t):  model/BaseLine/model.py:240-247 and :326-328. */
+enum {
+  GRK_IDX_PLAIN = 0,      /* row = v                                   */
+  GRK_IDX_ITEM_MASK = 1,  /* row = v * (token_type[n] == 1)            */
+  GRK_IDX_USER_MASK = 2,  /* row = v * (token_type[n] == 2)            */
+  GRK_IDX_POSITION = 3    /* row = (t + 1) * (v != 0)                  */
+};
+
+#define GRK_MAX_FEATURES 48
+#define GRK_MAX_LOOKUPS 8
+
+/* Returns the last error message of the calling thread ("" if none). */
+const char* grk_last_error(void);
+/* Library version string. */
+const char* grk_version(void);
+
+/* ------------------------------------------------------------------------
+ * Embedding tables
+ * ------------------------------------------------------------------------ */
+
+/* One feature of a fused multi-table lookup.  Replaces one
+ * `nn.Embedding.__call__` (model/BaseLine/model.py:242,243,247,275,328) or one
+ * `sparse_emb[k](t).sum(2)` bag-sum (model/BaseLine/model.py:277). */
+typedef struct grk_feature {
+  const void* table;     /* [num_rows, dim], call dtype                     */
+  const void* idx;       /* [num_tokens, idx_ld] index tensor, call itype   */
+  int64_t num_rows;
+  int64_t idx_ld;        /* elements between consecutive tokens            */
+  int32_t bag;           /* index columns per token: 1 = gather, >1 = sum  */
+  int32_t out_col;       /* first output column (elements)                 */
+  int32_t idx_mode;      /* GRK_IDX_*                                       */
+  int32_t pad_;
+} grk_feature;
+
+/* out[n, f.out_col : f.out_col+dim] = sum_a table_f[row(n, a)] for every
+ * feature f and token n < num_tokens.  Bag sums accumulate in fp32 from slot
+ * 0 upward and round once.  Bit-exact with the reference lookups.
+ * token_type: int32 [num_tokens] (needed by *_MASK modes), seq_len = T
+ * (needed by GRK_IDX_POSITION). */
+int grk_embedding_gather(const grk_feature* features, int num_features, int dim, int dtype, int itype,
+                         int64_t num_tokens, const int32_t* token_type, int32_t seq_len, void* out,
+                         int64_t out_ld, int32_t* err_flag, void* stream);
+
+/* One lookup that received a gradient (source of gradient rows).  The item
+ * table has three (seq, pos, neg: model/BaseLine/model.py:243,376-377). */
+typedef struct grk_lookup {
+  const void* idx;       /* index tensor as in grk_feature                 */
+  const void* grad;      /* [num_tokens, grad_ld] upstream grad, grad dtype */
+  int64_t num_tokens;
+  int64_t idx_ld;
+  int64_t grad_ld;
+  int32_t bag;
+  int32_t grad_col;      /* first column of this lookup's grad rows        */
+  int32_t idx_mode;
+  int32_t pad_;
+} grk_lookup;
+
+/* Workspace bytes for grk_embedding_backward with `num_occurrences` =
+ * sum over lookups of num_tokens * bag. */
+size_t grk_embedding_backward_workspace(int64_t num_occurrences, int64_t num_rows); /* 0 = query failed */
+
+/* Deterministic scatter-add gradient of one table, replacing autograd's
+ * embedding_dense_backward.  Occurrences (lookup order,
+ * then token, then bag slot) are stably sorted by row id and each row is
+ * summed sequentially in fp32 in occurrence order: bit-identical to the
+ * reference CPU backward for a single lookup.  Rows == padding_idx are
+ * skipped (padding_idx < 0: none).
+ *
+ * Outputs (any may be NULL):
+ *   dense_out  [num_rows, dim] fp32: zero-filled then written (drop-in mode)
+ *   uniq_ids   int64 [num_occurrences]: sorted unique row ids
+ *   uniq_rows  fp32  [num_occurrences, dim]: their gradient rows
+ *   uniq_count int32 [1]: number of unique rows
+ *   row_slot   int32 [num_rows]: row_slot[id] = position in uniq_*;
+ *              entries of untouched rows are left as they were (-1 by
+ *              contract; grk_table_adamw restores them). */
+int grk_embedding_backward(const grk_lookup* lookups, int num_lookups, int dim, int grad_dtype, int itype,
+                           const int32_t* token_type, int32_t seq_len, int64_t num_rows, int64_t padding_idx,
+                           float* dense_out, int64_t* uniq_ids, float* uniq_rows, int32_t* uniq_count,
+                           int32_t* row_slot, void* workspace, size_t workspace_bytes, int32_t* err_flag,
+                           void* stream);
+
+/* ------------------------------------------------------------------------
+ * Table optimizer: AdamW (model/BaseLine/main.py:131,189;
+ * model/BaseLineO1/main.py:174,249), torch single-tensor update order.
+ * ------------------------------------------------------------------------ */
+enum { GRK_ADAM_DENSE = 0, GRK_ADAM_LAZY = 1 };
+
+typedef struct grk_adamw_hparams {
+  float lr, beta1, beta2, eps, weight_decay;
+  float step_size;        /* lr / (1 - beta1^t)                             */
+  float bias_corr2_sqrt;  /* sqrt(1 - beta2^t)                              */
+  float pad_;
+} grk_adamw_hparams;
+
+/* mode GRK_ADAM_DENSE: every row of the table moves (reference semantics:
+ * rows without gradient see g = 0), gradient rows found via row_slot.
+ * mode GRK_ADAM_LAZY: only the uniq_count rows are updated (documented
+ * deviation).  Both restore row_slot[uniq_ids[*]] = -1. */
+int grk_table_adamw(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows, int dim,
+                    const int64_t* uniq_ids, const float* uniq_rows, const int32_t* uniq_count, int64_t max_uniq,
+                    int32_t* row_slot, grk_adamw_hparams hp, int mode, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GRK_H_ */

@@ -1,0 +1,75 @@
+"""HSTU pointwise-aggregated attention oracle (numpy).  TEST INFRASTRUCTURE ONLY.
+
+**Parity unpinned.**  The reference has no HSTU (its blocks are
+softmax MHA only, ``model/BaseLine/model.py:10-62``).  This restates the HSTU
+layer of Zhai et al., "Actions Speak Louder than Words" (ICML 2024), eq. (1)-(3),
+as the north star (BASELINE.json) specifies it, with the reference's own
+masking convention (``model/BaseLine/model.py:331-335``: causal AND
+key-not-padding):
+
+    S[i,j] = alpha * <q_i, k_j> + rab[h, min(i - j, NB - 1)]          (j <= i)
+    A[i,j] = SiLU(S[i,j]) * inv_n * mask[i,j]
+    O[i]   = sum_j A[i,j] v_j
+
+``rab`` is a learned relative-position bias, one value per (head, distance
+bucket).  The time bias of the paper is omitted: the reference's dataset drops
+timestamps (``model/BaseLine/dataset.py:117``).  It is pinned by its own fp64
+closed form here and by finite-difference gradient checks in
+``tests/test_oracle_selfcheck.py``.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .attention import build_mask
+
+
+def silu(x):
+    return x / (1.0 + np.exp(-x))
+
+
+def dsilu(x):
+    s = 1.0 / (1.0 + np.exp(-x))
+    return s * (1.0 + x * (1.0 - s))
+
+
+def _bias(rab, T):
+    rab = np.asarray(rab, np.float64)
+    nb = rab.shape[1]
+    i = np.arange(T)[:, None]
+    j = np.arange(T)[None, :]
+    bucket = np.clip(i - j, 0, nb - 1)
+    return rab[:, bucket], bucket  # [H,T,T], [T,T]
+
+
+def forward(q, k, v, key_valid, rab, alpha, inv_n):
+    """Returns ``(out [B,H,T,hd], s [B,H,T,T] pre-activation, mask [B,1,T,T])``."""
+    q = np.asarray(q, np.float64); k = np.asarray(k, np.float64); v = np.asarray(v, np.float64)
+    T = q.shape[2]
+    bias, _ = _bias(rab, T)
+    mask = build_mask(key_valid, True)[:, None]
+    s = alpha * np.einsum('bhid,bhjd->bhij', q, k) + bias[None]
+    a = np.where(mask, silu(s) * inv_n, 0.0)
+    out = np.einsum('bhij,bhjd->bhid', a, v)
+    return out, s, mask
+
+
+def backward(q, k, v, key_valid, rab, alpha, inv_n, dout):
+    """Returns ``(dq, dk, dv, drab [H, NB])``."""
+    q = np.asarray(q, np.float64); k = np.asarray(k, np.float64); v = np.asarray(v, np.float64)
+    dout = np.asarray(dout, np.float64)
+    T = q.shape[2]
+    _, s, mask = forward(q, k, v, key_valid, rab, alpha, inv_n)
+    a = np.where(mask, silu(s) * inv_n, 0.0)
+    dv = np.einsum('bhij,bhid->bhjd', a, dout)
+    da = np.einsum('bhid,bhjd->bhij', dout, v)
+    ds = np.where(mask, da * dsilu(s) * inv_n, 0.0)
+    dq = alpha * np.einsum('bhij,bhjd->bhid', ds, k)
+    dk = alpha * np.einsum('bhij,bhid->bhjd', ds, q)
+    nb = np.asarray(rab).shape[1]
+    _, bucket = _bias(rab, T)
+    drab = np.zeros((q.shape[1], nb), np.float64)
+    dsh = ds.sum(axis=0)  # [H,T,T]
+    for h in range(q.shape[1]):
+        np.add.at(drab[h], bucket.reshape(-1), dsh[h].reshape(-1))
+    return dq, dk, dv, drab

@@ -1,0 +1,129 @@
+"""ctypes binding of libgrk.so (the C ABI declared in include/grk.h).
+
+The library is built in-tree (``make`` at the repo root, or
+``__graft_entry__.build()``) and loaded from this package directory.  There is
+no fallback: if the library is missing or fails to load, every op raises.
+torch is imported first so that the HIP runtime libgrk.so links against
+(``libamdhip64.so.7``) resolves to the one torch already loaded -- one runtime,
+shared streams.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+LIB_PATH = PKG_DIR / 'libgrk.so'
+
+GRK_OK, GRK_EINVAL, GRK_EHIP, GRK_EUNSUPPORTED = 0, 1, 2, 3
+GRK_F32, GRK_BF16 = 0, 1
+GRK_I32, GRK_I64 = 0, 1
+IDX_PLAIN, IDX_ITEM_MASK, IDX_USER_MASK, IDX_POSITION = 0, 1, 2, 3
+ADAM_DENSE, ADAM_LAZY = 0, 1
+MAX_FEATURES, MAX_LOOKUPS = 48, 8
+
+
+class GrkFeature(C.Structure):
+    _fields_ = [('table', C.c_void_p), ('idx', C.c_void_p), ('num_rows', C.c_int64), ('idx_ld', C.c_int64),
+                ('bag', C.c_int32), ('out_col', C.c_int32), ('idx_mode', C.c_int32), ('pad_', C.c_int32)]
+
+
+class GrkLookup(C.Structure):
+    _fields_ = [('idx', C.c_void_p), ('grad', C.c_void_p), ('num_tokens', C.c_int64), ('idx_ld', C.c_int64),
+                ('grad_ld', C.c_int64), ('bag', C.c_int32), ('grad_col', C.c_int32), ('idx_mode', C.c_int32),
+                ('pad_', C.c_int32)]
+
+
+class GrkAdamwHparams(C.Structure):
+    _fields_ = [('lr', C.c_float), ('beta1', C.c_float), ('beta2', C.c_float), ('eps', C.c_float),
+                ('weight_decay', C.c_float), ('step_size', C.c_float), ('bias_corr2_sqrt', C.c_float),
+                ('pad_', C.c_float)]
+
+
+class GrkError(RuntimeError):
+    pass
+
+
+_P, _I, _I64, _SZ, _F = C.c_void_p, C.c_int, C.c_int64, C.c_size_t, C.c_float
+
+# name -> (restype, argtypes).  Kept in sync with include/grk.h; the CPU test
+# suite checks that every symbol the header declares is exported and listed.
+SIGNATURES = {
+    'grk_last_error': (C.c_char_p, []),
+    'grk_version': (C.c_char_p, []),
+    'grk_embedding_gather': (_I, [C.POINTER(GrkFeature), _I, _I, _I, _I, _I64, _P, C.c_int32, _P, _I64, _P, _P]),
+    'grk_embedding_backward_workspace': (_SZ, [_I64, _I64]),
+    'grk_embedding_backward': (_I, [C.POINTER(GrkLookup), _I, _I, _I, _I, _P, C.c_int32, _I64, _I64, _P, _P, _P,
+                                    _P, _P, _P, _SZ, _P, _P]),
+    'grk_table_adamw': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _P, _I64, _P, GrkAdamwHparams, _I, _P]),
+}
+
+_lib = None
+
+
+def build(verbose: bool = False) -> Path:
+    """Compile libgrk.so in-tree with hipcc (make)."""
+    jobs = str(min(16, os.cpu_count() or 4))
+    r = subprocess.run(['make', '-j', jobs], cwd=REPO_DIR, capture_output=not verbose, text=True)
+    if r.returncode != 0:
+        raise GrkError(f'building libgrk.so failed:\n{r.stdout}\n{r.stderr}')
+    return LIB_PATH
+
+
+def lib():
+    """The loaded library (raises if it is not built)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise GrkError(f'{LIB_PATH} is missing: run `make` (or __graft_entry__.build()) first')
+        handle = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != GRK_OK:
+        msg = lib().grk_last_error().decode(errors='replace')
+        raise GrkError(f'{what} failed (code {rc}): {msg}')
+
+
+def stream_ptr(device=None) -> int:
+    """Raw hipStream_t of torch's current stream."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def dtype_code(t: torch.dtype) -> int:
+    if t == torch.float32:
+        return GRK_F32
+    if t == torch.bfloat16:
+        return GRK_BF16
+    raise GrkError(f'unsupported dtype {t} (float32 / bfloat16 only)')
+
+
+def itype_code(t: torch.dtype) -> int:
+    if t == torch.int64:
+        return GRK_I64
+    if t == torch.int32:
+        return GRK_I32
+    raise GrkError(f'unsupported index dtype {t} (int32 / int64 only)')
+
+
+def loaded_path() -> str | None:
+    """Path of libgrk.so as mapped in this process (None if not loaded)."""
+    try:
+        with open('/proc/self/maps') as f:
+            for line in f:
+                if line.rstrip().endswith('libgrk.so'):
+                    return line.split()[-1]
+    except OSError:
+        pass
+    return None

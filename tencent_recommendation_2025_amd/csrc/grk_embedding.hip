@@ -1,0 +1,384 @@
+// Embedding-table hot path for gfx950: fused multi-table gather / bag-sum and
+// the deterministic scatter-add gradient.
+//
+// Reference call sites replaced:
+//   forward : nn.Embedding lookups in feat2emb / log2feats
+//             (model/BaseLine/model.py:242-247,275,277,328;
+//              model/BaseLineO1/model.py:345-350,380,383,439)
+//   backward: autograd embedding_dense_backward of those lookups.
+//
+// Both directions are HBM-bound byte movers: one 16-byte vector per lane,
+// consecutive lanes on consecutive bytes of one row, no LDS, no MFMA.
+#include <string.h>  // rocprim/iterator/texture_cache_iterator.hpp uses memset without it
+#include <rocprim/rocprim.hpp>
+
+#include "grk_common.h"
+
+namespace grk {
+
+struct FeatArgs {
+  grk_feature f[GRK_MAX_FEATURES];
+};
+
+struct LookupArgs {
+  grk_lookup l[GRK_MAX_LOOKUPS];
+  int64_t occ_off[GRK_MAX_LOOKUPS + 1];
+  int num;
+};
+
+template <typename I>
+__device__ __forceinline__ int64_t resolve_row(const I* idx, int64_t n, int32_t a, int64_t ld, int mode,
+                                               const int32_t* token_type, int32_t T) {
+  int64_t v = (int64_t)idx[n * ld + a];
+  switch (mode) {
+    case GRK_IDX_ITEM_MASK: return token_type[n] == 1 ? v : 0;
+    case GRK_IDX_USER_MASK: return token_type[n] == 2 ? v : 0;
+    case GRK_IDX_POSITION: return v != 0 ? (int64_t)(n % T) + 1 : 0;
+    default: return v;
+  }
+}
+
+// ---------------------------------------------------------------- gather ----
+// grid.y = feature; grid.x strides over (token, 16-byte chunk) units of that
+// feature.  Each lane moves one 16-byte vector per unit; UNROLL units are in
+// flight per lane.
+template <typename T, typename I, int UNROLL>
+__global__ void __launch_bounds__(256) k_gather(FeatArgs args, int dim, int64_t num_tokens,
+                                                const int32_t* __restrict__ token_type, int32_t T_len,
+                                                T* __restrict__ out, int64_t out_ld, int32_t* err_flag) {
+  constexpr int VEC = Vec16<T>::N;
+  const grk_feature& f = args.f[blockIdx.y];
+  const int chunks = dim / VEC;
+  const int64_t units = num_tokens * chunks;
+  const T* table = reinterpret_cast<const T*>(f.table);
+  const I* idx = reinterpret_cast<const I*>(f.idx);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; base < units; base += stride * UNROLL) {
+    Vec16<T> acc[UNROLL];
+    int64_t nn[UNROLL];
+    int cc[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      int64_t unit = base + u * stride;
+      nn[u] = unit / chunks;
+      cc[u] = (int)(unit - nn[u] * chunks);
+      if (unit >= units) continue;
+      if (f.bag == 1) {
+        int64_t row = resolve_row(idx, nn[u], 0, f.idx_ld, f.idx_mode, token_type, T_len);
+        if (row < 0 || row >= f.num_rows) {
+          if (err_flag) *err_flag = 1;
+          acc[u].v = {};
+        } else {
+          acc[u].load(table + row * dim + cc[u] * VEC);
+        }
+      } else {
+        float s[VEC];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) s[e] = 0.f;
+        for (int a = 0; a < f.bag; ++a) {
+          int64_t row = resolve_row(idx, nn[u], a, f.idx_ld, f.idx_mode, token_type, T_len);
+          if (row < 0 || row >= f.num_rows) {
+            if (err_flag) *err_flag = 1;
+            continue;
+          }
+          Vec16<T> r;
+          r.load(table + row * dim + cc[u] * VEC);
+          if (a == 0) {
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) s[e] = r.get(e);
+          } else {
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) s[e] = s[e] + r.get(e);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[u].set(e, s[e]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      int64_t unit = base + u * stride;
+      if (unit >= units) continue;
+      acc[u].store(out + nn[u] * out_ld + f.out_col + cc[u] * VEC);
+    }
+  }
+}
+
+// -------------------------------------------------------------- backward ----
+template <typename I>
+__global__ void k_build_keys(LookupArgs la, const int32_t* __restrict__ token_type, int32_t T_len,
+                             int64_t num_rows, int64_t padding_idx, unsigned* __restrict__ keys,
+                             int* __restrict__ vals, int64_t total, int32_t* err_flag) {
+  int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= total) return;
+  int l = 0;
+  while (l + 1 < la.num && o >= la.occ_off[l + 1]) ++l;
+  const grk_lookup& L = la.l[l];
+  int64_t rel = o - la.occ_off[l];
+  int64_t n = rel / L.bag;
+  int a = (int)(rel - n * L.bag);
+  int64_t row = resolve_row(reinterpret_cast<const I*>(L.idx), n, a, L.idx_ld, L.idx_mode, token_type, T_len);
+  unsigned key = (unsigned)num_rows;  // sentinel: sorts after every real row
+  if (row < 0 || row >= num_rows) {
+    if (err_flag) *err_flag = 1;
+  } else if (row != padding_idx) {
+    key = (unsigned)row;
+  }
+  keys[o] = key;
+  vals[o] = (int)o;
+}
+
+__global__ void k_mark_heads(const unsigned* __restrict__ keys, int* __restrict__ flags, int64_t n, unsigned sentinel) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  unsigned k = keys[i];
+  flags[i] = (k != sentinel && (i == 0 || keys[i - 1] != k)) ? 1 : 0;
+}
+
+__global__ void k_segments(const unsigned* __restrict__ keys, const int* __restrict__ pos, int64_t n,
+                           unsigned sentinel, int* __restrict__ seg_start, int* __restrict__ seg_end,
+                           unsigned* __restrict__ seg_key, int64_t* __restrict__ uniq_ids,
+                           int32_t* __restrict__ count) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  unsigned k = keys[i];
+  if (k == sentinel) return;
+  int u = pos[i] - 1;
+  if (i == 0 || keys[i - 1] != k) {
+    seg_start[u] = (int)i;
+    seg_key[u] = k;
+    if (uniq_ids) uniq_ids[u] = (int64_t)k;
+  }
+  bool last_of_seg = (i == n - 1) || keys[i + 1] != k;
+  if (last_of_seg) {
+    seg_end[u] = (int)(i + 1);
+    if (i == n - 1 || keys[i + 1] == sentinel) *count = u + 1;
+  }
+}
+
+// One group of dim/4 lanes per unique row; each lane owns 4 consecutive
+// columns and adds the occurrence rows strictly in sorted (= occurrence)
+// order in fp32 -- bitwise what the CPU reference does.
+template <typename G>
+__global__ void __launch_bounds__(256) k_segment_reduce(LookupArgs la, int dim, const int* __restrict__ vals,
+                                                        const int* __restrict__ seg_start,
+                                                        const int* __restrict__ seg_end,
+                                                        const unsigned* __restrict__ seg_key,
+                                                        const int32_t* __restrict__ count, int64_t max_rows,
+                                                        float* __restrict__ dense_out,
+                                                        float* __restrict__ uniq_rows,
+                                                        int32_t* __restrict__ row_slot) {
+  const int tpr = dim / 4;
+  const int rows_per_block = blockDim.x / tpr;
+  const int64_t u = (int64_t)blockIdx.x * rows_per_block + threadIdx.x / tpr;
+  const int c = (threadIdx.x % tpr) * 4;
+  if ((int)(threadIdx.x / tpr) >= rows_per_block || u >= max_rows || u >= *count) return;
+  const int s = seg_start[u], e = seg_end[u];
+  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+  for (int p = s; p < e; ++p) {
+    const int64_t o = vals[p];
+    int l = 0;
+    while (l + 1 < la.num && o >= la.occ_off[l + 1]) ++l;
+    const grk_lookup& L = la.l[l];
+    const int64_t n = (o - la.occ_off[l]) / L.bag;
+    const G* g = reinterpret_cast<const G*>(L.grad) + n * L.grad_ld + L.grad_col + c;
+    acc0 += Elem<G>::load(g + 0);
+    acc1 += Elem<G>::load(g + 1);
+    acc2 += Elem<G>::load(g + 2);
+    acc3 += Elem<G>::load(g + 3);
+  }
+  const unsigned key = seg_key[u];
+  float4 r = make_float4(acc0, acc1, acc2, acc3);
+  if (dense_out) *reinterpret_cast<float4*>(dense_out + (int64_t)key * dim + c) = r;
+  if (uniq_rows) *reinterpret_cast<float4*>(uniq_rows + u * dim + c) = r;
+  if (row_slot && c == 0) row_slot[key] = (int32_t)u;
+}
+
+// ------------------------------------------------------------ workspace ----
+struct BwdWs {
+  unsigned *keys_in, *keys_out, *seg_key;
+  int *vals_in, *vals_out, *flags, *pos, *seg_start, *seg_end;
+  void* sort_tmp;
+  size_t sort_bytes;
+  void* scan_tmp;
+  size_t scan_bytes;
+  size_t total;
+};
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int plan_ws(int64_t n, int64_t num_rows, char* base, BwdWs* ws) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) -> char* {
+    char* p = base ? base + off : nullptr;
+    off += align256(bytes);
+    return p;
+  };
+  ws->keys_in = (unsigned*)take(n * 4);
+  ws->keys_out = (unsigned*)take(n * 4);
+  ws->seg_key = (unsigned*)take(n * 4);
+  ws->vals_in = (int*)take(n * 4);
+  ws->vals_out = (int*)take(n * 4);
+  ws->flags = (int*)take(n * 4);
+  ws->pos = (int*)take(n * 4);
+  ws->seg_start = (int*)take(n * 4);
+  ws->seg_end = (int*)take(n * 4);
+  unsigned end_bit = 1;
+  while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
+  size_t sb = 0, cb = 0;
+  if (n > 0) {
+    if (rocprim::radix_sort_pairs(nullptr, sb, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
+                                  (int*)nullptr, (size_t)n, 0, end_bit) != hipSuccess)
+      return GRK_EHIP;
+    if (rocprim::inclusive_scan(nullptr, cb, (int*)nullptr, (int*)nullptr, (size_t)n, rocprim::plus<int>()) !=
+        hipSuccess)
+      return GRK_EHIP;
+  }
+  ws->sort_bytes = sb;
+  ws->sort_tmp = take(sb);
+  ws->scan_bytes = cb;
+  ws->scan_tmp = take(cb);
+  ws->total = off;
+  return GRK_OK;
+}
+
+}  // namespace grk
+
+using namespace grk;
+
+extern "C" int grk_embedding_gather(const grk_feature* features, int num_features, int dim, int dtype, int itype,
+                                    int64_t num_tokens, const int32_t* token_type, int32_t seq_len, void* out,
+                                    int64_t out_ld, int32_t* err_flag, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(features && num_features > 0 && num_features <= GRK_MAX_FEATURES,
+                "num_features must be in [1, %d]", GRK_MAX_FEATURES);
+  GRK_CHECK_ARG(dtype == GRK_F32 || dtype == GRK_BF16, "dtype must be GRK_F32 or GRK_BF16");
+  GRK_CHECK_ARG(itype == GRK_I32 || itype == GRK_I64, "itype must be GRK_I32 or GRK_I64");
+  const int vec = dtype == GRK_F32 ? 4 : 8;
+  GRK_CHECK_ARG(dim > 0 && dim % vec == 0, "dim (%d) must be a positive multiple of %d", dim, vec);
+  GRK_CHECK_ARG(out != nullptr && num_tokens >= 0, "bad output");
+  GRK_CHECK_ARG(out_ld % vec == 0 && ((uintptr_t)out % 16) == 0, "output must be 16-byte aligned per row");
+  FeatArgs fa;
+  memset(&fa, 0, sizeof(fa));
+  for (int i = 0; i < num_features; ++i) {
+    const grk_feature& f = features[i];
+    GRK_CHECK_ARG(f.table && f.idx && f.bag >= 1 && f.num_rows > 0, "feature %d: bad table/idx/bag", i);
+    GRK_CHECK_ARG(f.out_col >= 0 && f.out_col + dim <= out_ld && f.out_col % vec == 0,
+                  "feature %d: out_col %d out of range / misaligned", i, f.out_col);
+    GRK_CHECK_ARG(((uintptr_t)f.table % 16) == 0, "feature %d: table must be 16-byte aligned", i);
+    GRK_CHECK_ARG(f.idx_mode >= 0 && f.idx_mode <= 3, "feature %d: bad idx_mode", i);
+    GRK_CHECK_ARG(f.idx_mode == GRK_IDX_PLAIN || f.idx_mode == GRK_IDX_POSITION || token_type,
+                  "feature %d: masked mode needs token_type", i);
+    GRK_CHECK_ARG(f.idx_mode != GRK_IDX_POSITION || seq_len > 0, "position mode needs seq_len");
+    fa.f[i] = f;
+  }
+  if (num_tokens == 0) return GRK_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t units = num_tokens * (dim / vec);
+  constexpr int UNROLL = 4;
+  int gx = grid_for((units + UNROLL - 1) / UNROLL, 256, 4096 / (num_features > 8 ? 8 : num_features) + 1);
+  dim3 grid(gx, num_features);
+  if (dtype == GRK_BF16) {
+    if (itype == GRK_I64)
+      k_gather<bf16_t, int64_t, UNROLL><<<grid, 256, 0, s>>>(fa, dim, num_tokens, token_type, seq_len,
+                                                               (bf16_t*)out, out_ld, err_flag);
+    else
+      k_gather<bf16_t, int32_t, UNROLL><<<grid, 256, 0, s>>>(fa, dim, num_tokens, token_type, seq_len,
+                                                               (bf16_t*)out, out_ld, err_flag);
+  } else {
+    if (itype == GRK_I64)
+      k_gather<float, int64_t, UNROLL><<<grid, 256, 0, s>>>(fa, dim, num_tokens, token_type, seq_len,
+                                                              (float*)out, out_ld, err_flag);
+    else
+      k_gather<float, int32_t, UNROLL><<<grid, 256, 0, s>>>(fa, dim, num_tokens, token_type, seq_len,
+                                                              (float*)out, out_ld, err_flag);
+  }
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+extern "C" size_t grk_embedding_backward_workspace(int64_t num_occurrences, int64_t num_rows) {
+  BwdWs ws;
+  if (plan_ws(num_occurrences, num_rows, nullptr, &ws) != GRK_OK) return 0;
+  return ws.total + 256;
+}
+
+extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups, int dim, int grad_dtype,
+                                      int itype, const int32_t* token_type, int32_t seq_len, int64_t num_rows,
+                                      int64_t padding_idx, float* dense_out, int64_t* uniq_ids, float* uniq_rows,
+                                      int32_t* uniq_count, int32_t* row_slot, void* workspace,
+                                      size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(lookups && num_lookups > 0 && num_lookups <= GRK_MAX_LOOKUPS, "num_lookups must be in [1, %d]",
+                GRK_MAX_LOOKUPS);
+  GRK_CHECK_ARG(grad_dtype == GRK_F32 || grad_dtype == GRK_BF16, "grad_dtype must be GRK_F32 or GRK_BF16");
+  GRK_CHECK_ARG(itype == GRK_I32 || itype == GRK_I64, "bad itype");
+  GRK_CHECK_ARG(dim > 0 && dim % 4 == 0 && dim <= 1024, "dim (%d) must be a multiple of 4 and <= 1024", dim);
+  GRK_CHECK_ARG(num_rows > 0 && num_rows < 0xFFFFFFFFLL, "num_rows out of range");
+  GRK_CHECK_ARG(uniq_count != nullptr, "uniq_count is required");
+  LookupArgs la;
+  memset(&la, 0, sizeof(la));
+  la.num = num_lookups;
+  int64_t total = 0;
+  for (int i = 0; i < num_lookups; ++i) {
+    const grk_lookup& L = lookups[i];
+    GRK_CHECK_ARG(L.idx && L.grad && L.bag >= 1 && L.num_tokens >= 0, "lookup %d: bad idx/grad/bag", i);
+    GRK_CHECK_ARG(L.idx_mode >= 0 && L.idx_mode <= 3, "lookup %d: bad idx_mode", i);
+    GRK_CHECK_ARG(L.idx_mode == GRK_IDX_PLAIN || L.idx_mode == GRK_IDX_POSITION || token_type,
+                  "lookup %d: masked mode needs token_type", i);
+    la.l[i] = L;
+    la.occ_off[i] = total;
+    total += L.num_tokens * L.bag;
+  }
+  la.occ_off[num_lookups] = total;
+  GRK_CHECK_ARG(total < 0x7FFFFFFFLL, "too many occurrences");
+  BwdWs ws;
+  if (plan_ws(total, num_rows, nullptr, &ws) != GRK_OK) {
+    set_error("rocprim workspace query failed");
+    return GRK_EHIP;
+  }
+  GRK_CHECK_ARG(workspace_bytes >= ws.total + 256 && workspace, "workspace too small (%zu < %zu)", workspace_bytes,
+                ws.total + 256);
+  char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  plan_ws(total, num_rows, base, &ws);
+  hipStream_t s = (hipStream_t)stream;
+  GRK_CHECK_HIP(hipMemsetAsync(uniq_count, 0, sizeof(int32_t), s));
+  if (dense_out) GRK_CHECK_HIP(hipMemsetAsync(dense_out, 0, (size_t)num_rows * dim * sizeof(float), s));
+  if (total == 0) return GRK_OK;
+  const int B = 256;
+  const int g = (int)((total + B - 1) / B);
+  if (itype == GRK_I64)
+    k_build_keys<int64_t><<<g, B, 0, s>>>(la, token_type, seq_len, num_rows, padding_idx, ws.keys_in, ws.vals_in,
+                                          total, err_flag);
+  else
+    k_build_keys<int32_t><<<g, B, 0, s>>>(la, token_type, seq_len, num_rows, padding_idx, ws.keys_in, ws.vals_in,
+                                          total, err_flag);
+  GRK_LAUNCH_CHECK();
+  unsigned end_bit = 1;
+  while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
+  size_t sb = ws.sort_bytes;
+  GRK_CHECK_HIP(rocprim::radix_sort_pairs(ws.sort_tmp, sb, ws.keys_in, ws.keys_out, ws.vals_in, ws.vals_out,
+                                          (size_t)total, 0, end_bit, s));
+  const unsigned sentinel = (unsigned)num_rows;
+  k_mark_heads<<<g, B, 0, s>>>(ws.keys_out, ws.flags, total, sentinel);
+  GRK_LAUNCH_CHECK();
+  size_t cb = ws.scan_bytes;
+  GRK_CHECK_HIP(rocprim::inclusive_scan(ws.scan_tmp, cb, ws.flags, ws.pos, (size_t)total, rocprim::plus<int>(), s));
+  k_segments<<<g, B, 0, s>>>(ws.keys_out, ws.pos, total, sentinel, ws.seg_start, ws.seg_end, ws.seg_key, uniq_ids,
+                             uniq_count);
+  GRK_LAUNCH_CHECK();
+  const int tpr = dim / 4;
+  const int rows_per_block = tpr >= 256 ? 1 : 256 / tpr;
+  const int block = tpr >= 256 ? tpr : rows_per_block * tpr;
+  const int64_t gr = (total + rows_per_block - 1) / rows_per_block;
+  if (grad_dtype == GRK_BF16)
+    k_segment_reduce<bf16_t><<<(unsigned)gr, block, 0, s>>>(la, dim, ws.vals_out, ws.seg_start, ws.seg_end,
+                                                            ws.seg_key, uniq_count, total, dense_out, uniq_rows,
+                                                            row_slot);
+  else
+    k_segment_reduce<float><<<(unsigned)gr, block, 0, s>>>(la, dim, ws.vals_out, ws.seg_start, ws.seg_end,
+                                                           ws.seg_key, uniq_count, total, dense_out, uniq_rows,
+                                                           row_slot);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}

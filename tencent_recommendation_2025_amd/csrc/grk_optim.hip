@@ -1,0 +1,142 @@
+// Table AdamW for gfx950.
+//
+// Replaces torch.optim.AdamW's update of the embedding tables
+// (model/BaseLine/main.py:131,189; model/BaseLineO1/main.py:174,249) in the
+// torch single-tensor order:
+//   p *= 1 - lr*wd;  m = m + (1-b1)(g - m);  v = v*b2 + (1-b2) g g;
+//   p -= step_size * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+// Dense mode streams every row (reference semantics, HBM-bound:
+// 10 B/elem read + 10 B/elem written for bf16 params + fp32 moments); the
+// gradient is row-sparse and found through row_slot.  Lazy mode touches only
+// rows with a gradient.
+#include "grk_common.h"
+
+namespace grk {
+
+template <typename P>
+__device__ __forceinline__ void adam4(P* p, float* m, float* v, const float g[4], const grk_adamw_hparams& hp) {
+  float pv[4], mv[4], vv[4];
+  if constexpr (sizeof(P) == 4) {
+    float4 t = *reinterpret_cast<const float4*>(p);
+    pv[0] = t.x; pv[1] = t.y; pv[2] = t.z; pv[3] = t.w;
+  } else {
+    uint2 t = *reinterpret_cast<const uint2*>(p);
+    pv[0] = __uint_as_float(t.x << 16); pv[1] = __uint_as_float(t.x & 0xFFFF0000u);
+    pv[2] = __uint_as_float(t.y << 16); pv[3] = __uint_as_float(t.y & 0xFFFF0000u);
+  }
+  float4 mt = *reinterpret_cast<const float4*>(m);
+  float4 vt = *reinterpret_cast<const float4*>(v);
+  mv[0] = mt.x; mv[1] = mt.y; mv[2] = mt.z; mv[3] = mt.w;
+  vv[0] = vt.x; vv[1] = vt.y; vv[2] = vt.z; vv[3] = vt.w;
+  const float decay = 1.0f - hp.lr * hp.weight_decay;
+  const float w1 = 1.0f - hp.beta1, w2 = 1.0f - hp.beta2;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float pe = pv[e] * decay;
+    float me = mv[e] + w1 * (g[e] - mv[e]);
+    float ve = vv[e] * hp.beta2 + w2 * g[e] * g[e];
+    float denom = sqrtf(ve) / hp.bias_corr2_sqrt + hp.eps;
+    pe = pe - hp.step_size * (me / denom);
+    pv[e] = pe; mv[e] = me; vv[e] = ve;
+  }
+  if constexpr (sizeof(P) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+  } else {
+    uint2 t;
+    t.x = (unsigned)f32_to_bf16(pv[0]) | ((unsigned)f32_to_bf16(pv[1]) << 16);
+    t.y = (unsigned)f32_to_bf16(pv[2]) | ((unsigned)f32_to_bf16(pv[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = t;
+  }
+  *reinterpret_cast<float4*>(m) = make_float4(mv[0], mv[1], mv[2], mv[3]);
+  *reinterpret_cast<float4*>(v) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+}
+
+template <typename P>
+__global__ void __launch_bounds__(256) k_adamw_dense(P* __restrict__ param, float* __restrict__ m,
+                                                     float* __restrict__ v, int64_t num_rows, int dim,
+                                                     const float* __restrict__ uniq_rows,
+                                                     const int32_t* __restrict__ row_slot, grk_adamw_hparams hp) {
+  const int q = dim / 4;
+  const int64_t total = num_rows * q;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / q;
+    const int c = (int)(i - row * q) * 4;
+    const int32_t slot = row_slot ? row_slot[row] : -1;
+    float g[4] = {0.f, 0.f, 0.f, 0.f};
+    if (slot >= 0) {
+      float4 t = *reinterpret_cast<const float4*>(uniq_rows + (int64_t)slot * dim + c);
+      g[0] = t.x; g[1] = t.y; g[2] = t.z; g[3] = t.w;
+    }
+    const int64_t off = row * dim + c;
+    adam4<P>(param + off, m + off, v + off, g, hp);
+  }
+}
+
+template <typename P>
+__global__ void __launch_bounds__(256) k_adamw_lazy(P* __restrict__ param, float* __restrict__ m,
+                                                    float* __restrict__ v, int dim,
+                                                    const int64_t* __restrict__ uniq_ids,
+                                                    const float* __restrict__ uniq_rows,
+                                                    const int32_t* __restrict__ count, int64_t max_uniq,
+                                                    grk_adamw_hparams hp) {
+  const int q = dim / 4;
+  const int64_t n = *count;
+  const int64_t total = (n < max_uniq ? n : max_uniq) * q;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t u = i / q;
+    const int c = (int)(i - u * q) * 4;
+    float4 t = *reinterpret_cast<const float4*>(uniq_rows + u * dim + c);
+    float g[4] = {t.x, t.y, t.z, t.w};
+    const int64_t off = uniq_ids[u] * dim + c;
+    adam4<P>(param + off, m + off, v + off, g, hp);
+  }
+}
+
+__global__ void k_reset_slots(int32_t* __restrict__ row_slot, const int64_t* __restrict__ uniq_ids,
+                              const int32_t* __restrict__ count, int64_t max_uniq) {
+  const int64_t n = *count < max_uniq ? *count : max_uniq;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n; u += (int64_t)gridDim.x * blockDim.x)
+    row_slot[uniq_ids[u]] = -1;
+}
+
+}  // namespace grk
+
+using namespace grk;
+
+extern "C" int grk_table_adamw(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows,
+                               int dim, const int64_t* uniq_ids, const float* uniq_rows, const int32_t* uniq_count,
+                               int64_t max_uniq, int32_t* row_slot, grk_adamw_hparams hp, int mode, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(param && exp_avg && exp_avg_sq, "param / exp_avg / exp_avg_sq required");
+  GRK_CHECK_ARG(param_dtype == GRK_F32 || param_dtype == GRK_BF16, "bad param dtype");
+  GRK_CHECK_ARG(dim > 0 && dim % 4 == 0, "dim must be a multiple of 4");
+  GRK_CHECK_ARG(mode == GRK_ADAM_DENSE || mode == GRK_ADAM_LAZY, "bad mode");
+  GRK_CHECK_ARG(mode == GRK_ADAM_DENSE || (uniq_ids && uniq_rows && uniq_count), "lazy mode needs uniq_* inputs");
+  GRK_CHECK_ARG(!row_slot || (uniq_ids && uniq_count), "row_slot needs uniq_ids/uniq_count");
+  GRK_CHECK_ARG(mode == GRK_ADAM_LAZY || !row_slot || uniq_rows, "dense mode with row_slot needs uniq_rows");
+  GRK_CHECK_ARG(hp.bias_corr2_sqrt > 0.f, "bias_corr2_sqrt must be > 0");
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == GRK_ADAM_DENSE) {
+    const int g = grid_for(num_rows * (dim / 4), 256, 256 * 32);
+    if (param_dtype == GRK_BF16)
+      k_adamw_dense<bf16_t><<<g, 256, 0, s>>>((bf16_t*)param, exp_avg, exp_avg_sq, num_rows, dim, uniq_rows,
+                                              row_slot, hp);
+    else
+      k_adamw_dense<float><<<g, 256, 0, s>>>((float*)param, exp_avg, exp_avg_sq, num_rows, dim, uniq_rows,
+                                             row_slot, hp);
+  } else {
+    const int g = grid_for(max_uniq * (dim / 4), 256, 256 * 32);
+    if (param_dtype == GRK_BF16)
+      k_adamw_lazy<bf16_t><<<g, 256, 0, s>>>((bf16_t*)param, exp_avg, exp_avg_sq, dim, uniq_ids, uniq_rows,
+                                             uniq_count, max_uniq, hp);
+    else
+      k_adamw_lazy<float><<<g, 256, 0, s>>>((float*)param, exp_avg, exp_avg_sq, dim, uniq_ids, uniq_rows,
+                                            uniq_count, max_uniq, hp);
+  }
+  GRK_LAUNCH_CHECK();
+  if (row_slot) {
+    k_reset_slots<<<grid_for(max_uniq, 256, 1024), 256, 0, s>>>(row_slot, uniq_ids, uniq_count, max_uniq);
+    GRK_LAUNCH_CHECK();
+  }
+  return GRK_OK;
+}

@@ -1,0 +1,171 @@
+"""Thin torch-facing wrappers over the libgrk.so C ABI (include/grk.h).
+
+Each function validates shapes on the host, passes raw device pointers and
+torch's current HIP stream, and raises ``GrkError`` on any failure.  There is
+no CPU / eager fallback: these functions require CUDA(HIP) tensors and the
+built library.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib as L
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _require_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise L.GrkError('grk kernels need device (HIP) tensors; there is no CPU path')
+
+
+@dataclass
+class Lookup:
+    """One table lookup feeding a fused gather (see grk_feature / grk_lookup).
+
+    ``idx`` is ``[..., bag]`` when ``bag > 1`` (array feature) else ``[...]``;
+    tokens are the leading dims flattened (``n = b*T + t``).
+    """
+    table: torch.Tensor
+    idx: torch.Tensor
+    out_col: int
+    mode: int = L.IDX_PLAIN
+    bag: int = 1
+
+    def idx_ld(self):
+        return self.bag
+
+
+def _idx_contig(idx, bag):
+    idx = idx if idx.is_contiguous() else idx.contiguous()
+    n = idx.numel() // bag
+    return idx, n
+
+
+def embedding_gather(lookups, out, num_tokens, token_type=None, seq_len=0, err_flag=None):
+    """out[n, col:col+D] = sum_a table[row(n, a)]  for every lookup (grk_embedding_gather)."""
+    if not lookups:
+        return out
+    if len(lookups) > L.MAX_FEATURES:
+        raise L.GrkError(f'at most {L.MAX_FEATURES} features per gather call')
+    dim = lookups[0].table.shape[1]
+    dt = lookups[0].table.dtype
+    it = lookups[0].idx.dtype
+    _require_cuda(out, token_type, err_flag, *[lk.table for lk in lookups])
+    if out.dtype != dt or out.dim() != 2 or out.stride(1) != 1:
+        raise L.GrkError('out must be a row-major [N, ld] tensor of the table dtype')
+    feats = (L.GrkFeature * len(lookups))()
+    keep = []
+    for i, lk in enumerate(lookups):
+        if lk.table.shape[1] != dim or lk.table.dtype != dt or lk.idx.dtype != it:
+            raise L.GrkError('all lookups of one call share dim, table dtype and index dtype')
+        if not lk.table.is_contiguous():
+            raise L.GrkError('tables must be contiguous')
+        idx, n = _idx_contig(lk.idx, lk.bag)
+        if n != num_tokens:
+            raise L.GrkError(f'lookup {i}: {n} tokens, expected {num_tokens}')
+        keep.append(idx)
+        feats[i] = L.GrkFeature(lk.table.data_ptr(), idx.data_ptr(), lk.table.shape[0], lk.bag, lk.bag,
+                                lk.out_col, lk.mode, 0)
+    if token_type is not None:
+        token_type = token_type.to(torch.int32).contiguous()
+        keep.append(token_type)
+    rc = L.lib().grk_embedding_gather(feats, len(lookups), dim, L.dtype_code(dt), L.itype_code(it), num_tokens,
+                                      _ptr(token_type), seq_len, out.data_ptr(), out.stride(0), _ptr(err_flag),
+                                      L.stream_ptr(out.device))
+    L.check(rc, 'grk_embedding_gather')
+    return out
+
+
+@dataclass
+class GradSource:
+    """One lookup's upstream gradient for a table (grk_lookup)."""
+    idx: torch.Tensor
+    grad: torch.Tensor      # [N, ld]
+    grad_col: int
+    mode: int = L.IDX_PLAIN
+    bag: int = 1
+
+
+class BackwardResult:
+    __slots__ = ('dense', 'ids', 'rows', 'count', 'capacity')
+
+    def __init__(self, dense, ids, rows, count, capacity):
+        self.dense, self.ids, self.rows, self.count, self.capacity = dense, ids, rows, count, capacity
+
+
+def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, seq_len=0, dense=True,
+                       sparse=False, row_slot=None, err_flag=None):
+    """Deterministic scatter-add table gradient (grk_embedding_backward).
+
+    Returns a ``BackwardResult`` with ``dense`` ([num_rows, dim] fp32) when
+    ``dense`` and ``ids``/``rows``/``count`` (row-sparse form, capacity =
+    number of occurrences) when ``sparse``.
+    """
+    if len(sources) > L.MAX_LOOKUPS:
+        raise L.GrkError(f'at most {L.MAX_LOOKUPS} gradient sources per table')
+    dev = sources[0].grad.device
+    gdt = sources[0].grad.dtype
+    it = sources[0].idx.dtype
+    _require_cuda(*[s.grad for s in sources], token_type, row_slot, err_flag)
+    lk = (L.GrkLookup * len(sources))()
+    keep = []
+    total = 0
+    for i, s in enumerate(sources):
+        if s.grad.dtype != gdt or s.idx.dtype != it:
+            raise L.GrkError('all sources of one table share grad dtype and index dtype')
+        if s.grad.stride(-1) != 1 or s.grad.dim() != 2:
+            raise L.GrkError('grad must be a row-major [N, ld] tensor')
+        idx, n = _idx_contig(s.idx, s.bag)
+        if n != s.grad.shape[0]:
+            raise L.GrkError(f'source {i}: {n} index tokens vs {s.grad.shape[0]} grad rows')
+        if s.grad_col + dim > s.grad.shape[1]:
+            raise L.GrkError(f'source {i}: grad_col out of range')
+        keep.append(idx)
+        lk[i] = L.GrkLookup(idx.data_ptr(), s.grad.data_ptr(), n, s.bag, s.grad.stride(0), s.bag, s.grad_col,
+                            s.mode, 0)
+        total += n * s.bag
+    if token_type is not None:
+        token_type = token_type.to(torch.int32).contiguous()
+        keep.append(token_type)
+    ws_bytes = L.lib().grk_embedding_backward_workspace(total, num_rows)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    dense_out = torch.empty((num_rows, dim), dtype=torch.float32, device=dev) if dense else None
+    cap = max(total, 1)
+    ids = torch.empty(cap, dtype=torch.int64, device=dev) if sparse else None
+    rows = torch.empty((cap, dim), dtype=torch.float32, device=dev) if sparse else None
+    count = torch.empty(1, dtype=torch.int32, device=dev)
+    rc = L.lib().grk_embedding_backward(lk, len(sources), dim, L.dtype_code(gdt), L.itype_code(it),
+                                        _ptr(token_type), seq_len, num_rows, -1 if padding_idx is None else padding_idx,
+                                        _ptr(dense_out), _ptr(ids), _ptr(rows), count.data_ptr(), _ptr(row_slot),
+                                        ws.data_ptr(), ws.numel(), _ptr(err_flag), L.stream_ptr(dev))
+    L.check(rc, 'grk_embedding_backward')
+    return BackwardResult(dense_out, ids, rows, count, cap)
+
+
+def adamw_hparams(lr, beta1, beta2, eps, weight_decay, step):
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    return L.GrkAdamwHparams(lr, beta1, beta2, eps, weight_decay, lr / bc1, math.sqrt(bc2), 0.0)
+
+
+def table_adamw(param, exp_avg, exp_avg_sq, hp, ids=None, rows=None, count=None, capacity=0, row_slot=None,
+                lazy=False):
+    """AdamW update of one table from a row-sparse gradient (grk_table_adamw)."""
+    _require_cuda(param, exp_avg, exp_avg_sq, ids, rows, count, row_slot)
+    if exp_avg.dtype != torch.float32 or exp_avg_sq.dtype != torch.float32:
+        raise L.GrkError('optimizer moments must be float32')
+    if not (param.is_contiguous() and exp_avg.is_contiguous() and exp_avg_sq.is_contiguous()):
+        raise L.GrkError('param and moments must be contiguous')
+    rc = L.lib().grk_table_adamw(param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(),
+                                 exp_avg_sq.data_ptr(), param.shape[0], param.shape[1], _ptr(ids), _ptr(rows),
+                                 _ptr(count), capacity, _ptr(row_slot), hp,
+                                 L.ADAM_LAZY if lazy else L.ADAM_DENSE, L.stream_ptr(param.device))
+    L.check(rc, 'grk_table_adamw')

@@ -1,0 +1,218 @@
+"""GPU parity of the embedding kernels (grk_embedding_gather / _backward,
+grk_table_adamw) against the oracle, which is itself pinned to the reference's
+golden vectors (tests/test_oracle_golden.py).  Integer/byte work is checked
+bit-exact; the fp32 order-defined sums too."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import adamw as oadam
+from oracle import embedding as oemb
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+@pytest.fixture(scope='module')
+def K():
+    from tencent_recommendation_2025_amd import _lib, kernels
+    _lib.lib()
+    return kernels
+
+
+def T(x, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+    return t if dtype is None else t.to(dtype)
+
+
+def gather1(K, table, idx, bag=1, mode=0, token_type=None, seq_len=0, dtype=torch.float32):
+    D = table.shape[1]
+    n = idx.numel() // bag
+    out = torch.full((n, D), float('nan'), dtype=dtype, device=DEV)
+    K.embedding_gather([K.Lookup(table, idx, 0, mode, bag)], out, n, token_type, seq_len)
+    torch.cuda.synchronize()
+    return out
+
+
+def test_gather_golden_bitexact(K, golden):
+    g = golden('emb_ops.npz')
+    table = T(g['table'])
+    out = gather1(K, table, T(g['idx']))
+    assert np.array_equal(out.cpu().numpy().reshape(g['out'].shape), g['out'])
+    out32 = gather1(K, table, T(g['idx']).int())
+    assert torch.equal(out32, out)
+
+
+def test_bag_sum_golden_bitexact(K, golden):
+    g = golden('emb_ops.npz')
+    out = gather1(K, T(g['table']), T(g['idx_arr']), bag=4)
+    assert np.array_equal(out.cpu().numpy().reshape(g['bag'].shape), g['bag'])
+
+
+def test_backward_golden_bitexact(K, golden):
+    g = golden('emb_ops.npz')
+    D = g['table'].shape[1]
+    res = K.embedding_backward([K.GradSource(T(g['idx']), T(g['gout']).reshape(-1, D), 0)], 1001, D)
+    assert np.array_equal(res.dense.cpu().numpy(), g['dgrad'])
+    res = K.embedding_backward([K.GradSource(T(g['idx_arr']), T(g['gbag']).reshape(-1, D), 0, bag=4)], 1001, D)
+    assert np.array_equal(res.dense.cpu().numpy(), g['dgrad_bag'])
+
+
+def test_backward_multi_source(K, golden):
+    g = golden('emb_ops.npz')
+    D = 64
+    src = [K.GradSource(T(g['item_idx'][i]), T(g['item_gout'][i]).reshape(-1, D), 0) for i in range(3)]
+    res = K.embedding_backward(src, 1001, D)
+    want = oemb.multi_source_backward([(g['item_gout'][i], g['item_idx'][i]) for i in range(3)], 1001)
+    assert np.array_equal(res.dense.cpu().numpy(), want)
+    # vs the reference's autograd (sums three dense grads): equal to rounding
+    np.testing.assert_allclose(res.dense.cpu().numpy(), g['item_dgrad'], rtol=1e-6, atol=1e-6)
+
+
+def test_bf16_gather_bagsum_backward(K):
+    rng = np.random.default_rng(0)
+    R, D, N, A = 5000, 128, 777, 3
+    tab = oemb.to_bf16_f32(rng.standard_normal((R, D)).astype(np.float32))
+    idx = rng.integers(0, R, (N,))
+    idx[:50] = 0
+    arr = rng.integers(0, R, (N, A))
+    tb = T(tab).to(torch.bfloat16)
+    out = gather1(K, tb, T(idx), dtype=torch.bfloat16)
+    assert np.array_equal(out.float().cpu().numpy(), oemb.gather(tab, idx))
+    out = gather1(K, tb, T(arr), bag=A, dtype=torch.bfloat16)
+    assert np.array_equal(out.float().cpu().numpy(), oemb.bag_sum(tab, arr, out_bf16=True))
+    gr = oemb.to_bf16_f32(rng.standard_normal((N, D)).astype(np.float32))
+    res = K.embedding_backward([K.GradSource(T(arr), T(gr).to(torch.bfloat16), 0, bag=A)], R, D)
+    want = oemb.dense_backward(np.repeat(gr[:, None, :], A, axis=1), arr, R)
+    assert np.array_equal(res.dense.cpu().numpy(), want)
+
+
+def test_index_modes_and_fused_features(K):
+    rng = np.random.default_rng(1)
+    B, Tn, D = 6, 17, 64
+    item = rng.standard_normal((300, D)).astype(np.float32)
+    user = rng.standard_normal((50, D)).astype(np.float32)
+    pos = rng.standard_normal((2 * 16 + 1, D)).astype(np.float32)
+    sp = rng.standard_normal((20, D)).astype(np.float32)
+    seq = np.zeros((B, Tn), np.int64)
+    tt = np.zeros((B, Tn), np.int32)
+    for b in range(B):
+        n = int(rng.integers(1, Tn + 1))
+        seq[b, Tn - n] = rng.integers(1, 50)
+        tt[b, Tn - n] = 2
+        seq[b, Tn - n + 1:] = rng.integers(1, 300, n - 1)
+        tt[b, Tn - n + 1:] = 1
+    f = rng.integers(0, 20, (B, Tn))
+    arr = rng.integers(0, 20, (B, Tn, 3))
+    out = torch.full((B * Tn, 5 * D + 8), -7.0, device=DEV)
+    ttd = T(tt)
+    lk = [K.Lookup(T(item), T(seq), 0, 1), K.Lookup(T(user), T(seq), D, 2), K.Lookup(T(pos), T(seq), 2 * D, 3),
+          K.Lookup(T(sp), T(f), 3 * D), K.Lookup(T(sp), T(arr), 4 * D, bag=3)]
+    K.embedding_gather(lk, out, B * Tn, ttd, Tn)
+    o = out.cpu().numpy().reshape(B, Tn, -1)
+    posidx = np.arange(1, Tn + 1)[None, :] * (seq != 0)
+    assert np.array_equal(o[..., :D], item[(tt == 1) * seq])
+    assert np.array_equal(o[..., D:2 * D], user[(tt == 2) * seq])
+    assert np.array_equal(o[..., 2 * D:3 * D], pos[posidx])
+    assert np.array_equal(o[..., 3 * D:4 * D], sp[f])
+    assert np.array_equal(o[..., 4 * D:5 * D], oemb.bag_sum(sp, arr))
+    assert np.all(o[..., 5 * D:] == -7.0)  # columns outside every feature untouched
+    # backward through the masked / positional modes
+    gout = rng.standard_normal((B * Tn, 5 * D)).astype(np.float32)
+    gd = T(gout)
+    res = K.embedding_backward([K.GradSource(T(seq), gd, 0, 1)], 300, D, token_type=ttd, seq_len=Tn)
+    assert np.array_equal(res.dense.cpu().numpy(), oemb.dense_backward(gout[:, :D], ((tt == 1) * seq), 300))
+    res = K.embedding_backward([K.GradSource(T(seq), gd, 2 * D, 3)], 33, D, token_type=ttd, seq_len=Tn)
+    assert np.array_equal(res.dense.cpu().numpy(), oemb.dense_backward(gout[:, 2 * D:3 * D], posidx, 33))
+
+
+def test_sparse_output_row_slot_and_adamw(K):
+    rng = np.random.default_rng(2)
+    R, D, N = 2000, 64, 3000
+    idx = rng.integers(0, R, (N,))
+    idx[rng.random(N) < 0.3] = 7  # hot row
+    gr = rng.standard_normal((N, D)).astype(np.float32)
+    slot = torch.full((R,), -1, dtype=torch.int32, device=DEV)
+    res = K.embedding_backward([K.GradSource(T(idx), T(gr), 0)], R, D, dense=True, sparse=True, row_slot=slot)
+    cnt = int(res.count.item())
+    uniq = oemb.unique_rows(idx)
+    assert cnt == len(uniq)
+    assert np.array_equal(res.ids[:cnt].cpu().numpy(), uniq)
+    dense = oemb.dense_backward(gr, idx, R)
+    assert np.array_equal(res.rows[:cnt].cpu().numpy(), dense[uniq])
+    s = slot.cpu().numpy()
+    assert np.array_equal(s[uniq], np.arange(cnt)) and np.all(np.delete(s, uniq) == -1)
+    p0 = rng.standard_normal((R, D)).astype(np.float32)
+    m0 = rng.standard_normal((R, D)).astype(np.float32) * 0.01
+    v0 = np.abs(rng.standard_normal((R, D)).astype(np.float32)) * 0.01
+    for lazy in (False, True):
+        p, m, v = T(p0), T(m0), T(v0)
+        slot2 = slot.clone()
+        hp = K.adamw_hparams(1e-3, 0.9, 0.98, 1e-8, 0.01, 3)
+        K.table_adamw(p, m, v, hp, res.ids, res.rows, res.count, res.capacity, None if lazy else slot2, lazy=lazy)
+        fn = oadam.lazy_rows if lazy else oadam.dense_rows
+        wp, wm, wv = fn(p0, m0, v0, uniq, dense[uniq], 3, 1e-3, 0.9, 0.98, 1e-8, 0.01)
+        np.testing.assert_allclose(p.cpu().numpy(), wp, rtol=2e-6, atol=1e-7)
+        np.testing.assert_allclose(m.cpu().numpy(), wm, rtol=2e-6, atol=1e-8)
+        np.testing.assert_allclose(v.cpu().numpy(), wv, rtol=2e-6, atol=1e-10)
+        if not lazy:
+            assert torch.all(slot2 == -1)
+
+
+def test_adamw_bf16_param(K):
+    rng = np.random.default_rng(3)
+    R, D = 300, 32
+    p0 = oemb.to_bf16_f32(rng.standard_normal((R, D)).astype(np.float32))
+    ids = np.arange(0, R, 3)
+    g = rng.standard_normal((len(ids), D)).astype(np.float32)
+    p = T(p0).to(torch.bfloat16)
+    m = torch.zeros(R, D, device=DEV); v = torch.zeros(R, D, device=DEV)
+    slot = torch.full((R,), -1, dtype=torch.int32, device=DEV)
+    slot[T(ids)] = torch.arange(len(ids), dtype=torch.int32, device=DEV)
+    K.table_adamw(p, m, v, K.adamw_hparams(1e-2, 0.9, 0.98, 1e-8, 0.01, 1), T(ids), T(g),
+                  torch.tensor([len(ids)], dtype=torch.int32, device=DEV), len(ids), slot)
+    wp, _, _ = oadam.dense_rows(p0, np.zeros((R, D), np.float32), np.zeros((R, D), np.float32), ids, g, 1, 1e-2)
+    got = p.float().cpu().numpy()
+    # fp32 math then one RNE rounding: equal to the rounded oracle up to 1 bf16 ulp (fma contraction)
+    np.testing.assert_allclose(got, oemb.to_bf16_f32(wp), rtol=2 ** -7, atol=1e-30)
+    assert np.mean(got == oemb.to_bf16_f32(wp)) > 0.99
+
+
+def test_out_of_range_flag_and_empty(K):
+    table = torch.randn(10, 16, device=DEV)
+    idx = torch.tensor([1, 2, 10, -1], device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out = torch.full((4, 16), 5.0, device=DEV)
+    K.embedding_gather([K.Lookup(table, idx, 0)], out, 4, err_flag=err)
+    assert err.item() == 1
+    assert torch.all(out[2:] == 0) and torch.equal(out[:2], table[1:3])
+    empty = torch.empty(0, 16, device=DEV)
+    K.embedding_gather([K.Lookup(table, idx[:0], 0)], empty, 0)
+    res = K.embedding_backward([K.GradSource(idx[:0], empty, 0)], 10, 16)
+    assert res.count.item() == 0 and torch.all(res.dense == 0)
+
+
+def test_full_size_c2_properties(K):
+    """BASELINE config 2 sizes: 1M x 512 bf16 item table, B=128, T=201, 16 lookups."""
+    g = torch.Generator(device=DEV).manual_seed(0)
+    R, D, B, Tn = 1_000_001, 512, 128, 201
+    N = B * Tn
+    table = torch.randn(R, D, device=DEV, generator=g).to(torch.bfloat16)
+    idx = torch.randint(0, R, (16, N), device=DEV, generator=g)
+    out = torch.empty(N, 16 * D, dtype=torch.bfloat16, device=DEV)
+    K.embedding_gather([K.Lookup(table, idx[f], f * D) for f in range(16)], out, N)
+    sel = torch.randint(0, N, (2048,), device=DEV, generator=g)
+    want = table.float().cpu().numpy()[idx[:, sel].cpu().numpy()]          # [16, S, D]
+    got = out[sel].float().cpu().numpy().reshape(len(sel), 16, D).transpose(1, 0, 2)
+    assert np.array_equal(got, want)
+    # backward: three sources on one table; checksum of the dense grad == sum of all grad rows
+    grad = torch.randn(N, 3 * D, device=DEV, generator=g).to(torch.bfloat16)
+    src = [K.GradSource(idx[f], grad, f * D) for f in range(3)]
+    res = K.embedding_backward(src, R, D, padding_idx=None, dense=True, sparse=True)
+    total = res.dense.double().sum(0)
+    want_total = grad.double().reshape(N, 3, D).sum((0, 1))
+    torch.testing.assert_close(total, want_total, rtol=1e-6, atol=1e-3)
+    cnt = int(res.count.item())
+    assert cnt == torch.unique(idx[:3]).numel()
+    ids = res.ids[:cnt]
+    assert torch.all(ids[1:] > ids[:-1])
