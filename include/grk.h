@@ -140,6 +140,48 @@ int grk_table_adamw(void* param, int param_dtype, float* exp_avg, float* exp_avg
                     const int64_t* uniq_ids, const float* uniq_rows, const int32_t* uniq_count, int64_t max_uniq,
                     int32_t* row_slot, grk_adamw_hparams hp, int mode, void* stream);
 
+
+/* ------------------------------------------------------------------------
+ * Causal attention (MFMA 32x32x16 bf16)
+ *   GRK_ATTN_SOFTMAX: softmax(scale * QK^T + mask) V with dropout -- the
+ *     reference's F.scaled_dot_product_attention with log2feats' mask
+ *     (model/BaseLine/model.py:39-43,331-335); fully-masked rows give 0.
+ *   GRK_ATTN_HSTU: SiLU(scale * QK^T + rab[h, min(i-j, nb-1)]) * inv_n * mask,
+ *     times V (north star; no reference -- oracle/hstu.py).
+ * mask[b,i,j] = (j <= i) && key_valid[b,j]  (key_valid NULL = all valid).
+ * Q/K/V are bf16 [B*T, ld] with head h at columns [h*hd, (h+1)*hd).
+ * ------------------------------------------------------------------------ */
+enum { GRK_ATTN_SOFTMAX = 0, GRK_ATTN_HSTU = 1 };
+
+typedef struct grk_attn_args {
+  int32_t kind;                    /* GRK_ATTN_*                                  */
+  int32_t batch, heads, seq_len, head_dim;   /* head_dim in {16, 32, 64, 128}  */
+  int32_t num_buckets;             /* hstu: rab columns                           */
+  const void* q; const void* k; const void* v;   /* bf16                        */
+  int64_t ldq, ldk, ldv;           /* row strides (elements), multiples of 8      */
+  const uint8_t* key_valid;        /* [batch, seq_len] or NULL                    */
+  const float* rab;                /* hstu: [heads, num_buckets] fp32             */
+  float scale;                     /* softmax: 1/sqrt(hd); hstu: alpha            */
+  float inv_n;                     /* hstu: 1/n                                   */
+  float dropout_p;                 /* softmax training dropout                    */
+  int32_t precise;                 /* 1: P / dS fed to MFMA as bf16 hi+lo pairs   */
+  uint64_t seed;                   /* dropout stream                              */
+  int32_t out_dtype;               /* GRK_F32 / GRK_BF16 for out, dq, dk, dv      */
+  int32_t pad_;
+} grk_attn_args;
+
+/* out [B*T, ldo] (out_dtype); lse fp32 [B, H, T] (softmax: natural-log
+ * logsumexp of the masked scaled scores, -inf for fully-masked rows). */
+int grk_attention_fwd(const grk_attn_args* a, void* out, int64_t ldo, float* lse, void* stream);
+
+/* Gradients of grk_attention_fwd for upstream dout (dout_dtype).  Softmax
+ * needs the forward out/lse and a delta workspace fp32 [B, H, T]; hstu
+ * accumulates drab fp32 [H, nb] (caller zero-fills).  dq/dk/dv are written
+ * (not accumulated) in out_dtype; deterministic except drab. */
+int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
+                      int dout_dtype, const float* lse, float* delta_ws, void* dq, int64_t lddq, void* dk,
+                      int64_t lddk, void* dv, int64_t lddv, float* drab, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,6 +45,18 @@ class GrkAdamwHparams(C.Structure):
                 ('pad_', C.c_float)]
 
 
+class GrkAttnArgs(C.Structure):
+    _fields_ = [('kind', C.c_int32), ('batch', C.c_int32), ('heads', C.c_int32), ('seq_len', C.c_int32),
+                ('head_dim', C.c_int32), ('num_buckets', C.c_int32), ('q', C.c_void_p), ('k', C.c_void_p),
+                ('v', C.c_void_p), ('ldq', C.c_int64), ('ldk', C.c_int64), ('ldv', C.c_int64),
+                ('key_valid', C.c_void_p), ('rab', C.c_void_p), ('scale', C.c_float), ('inv_n', C.c_float),
+                ('dropout_p', C.c_float), ('precise', C.c_int32), ('seed', C.c_uint64), ('out_dtype', C.c_int32),
+                ('pad_', C.c_int32)]
+
+
+ATTN_SOFTMAX, ATTN_HSTU = 0, 1
+
+
 class GrkError(RuntimeError):
     pass
 
@@ -61,6 +73,9 @@ SIGNATURES = {
     'grk_embedding_backward': (_I, [C.POINTER(GrkLookup), _I, _I, _I, _I, _P, C.c_int32, _I64, _I64, _P, _P, _P,
                                     _P, _P, _P, _SZ, _P, _P]),
     'grk_table_adamw': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _P, _I64, _P, GrkAdamwHparams, _I, _P]),
+    'grk_attention_fwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _P]),
+    'grk_attention_bwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64, _P, _I64,
+                               _P, _P]),
 }
 
 _lib = None

@@ -1,0 +1,660 @@
+// Causal attention for gfx950 with MFMA 32x32x16 bf16: the reference's
+// softmax MHA core and the north-star HSTU pointwise attention.
+//
+// Replaces:
+//   softmax: F.scaled_dot_product_attention(Q, K, V, dropout_p, attn_mask)
+//            with log2feats' mask (causal AND key-not-padding)
+//            (model/BaseLine/model.py:39-43,331-335;
+//             model/BaseLineO1/model.py:73-77,443-447)
+//   hstu:    A = SiLU(alpha QK^T + rab[i-j]) * inv_n * mask ; O = A V
+//            (no reference; oracle/hstu.py)
+//
+// Layout: Q/K/V/O/dO are [B*T, ld] row-major with head h at columns
+// [h*HD, (h+1)*HD) -- the natural output of the fused projection GEMM, no
+// transposes.  One workgroup = 4 waves = 128 consecutive queries (forward,
+// dQ) or keys (dK/dV) of one (batch, head); K/V (or Q/dO) chunks of 64 rows
+// are staged through LDS with an XOR-swizzled row image that serves both the
+// row reads (ds_read_b128) and the transposed reads (ds_read_b64_tr_b16).
+//
+// MFMA operand conventions (lane l: r = l&31, hh = l>>5):
+//   A[r][8hh+j], B[8hh+j][r], D[(i&3)+8(i>>2)+4hh][r].
+// The forward computes S^T = K Q^T so a lane owns one query column; P^T is
+// then directly the B operand of O^T = V^T P^T (permuted k order, see
+// cdna_hip_programming.md §3).  Backward = dQ kernel (S^T, dP^T, dQ^T) +
+// dK/dV kernel (S, dP, dV^T, dK^T): no atomics on dQ/dK/dV, deterministic.
+#include "grk_common.h"
+
+namespace grk {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+constexpr int kChunk = 64;      // rows staged per LDS chunk
+constexpr int kBlockRows = 128; // queries (fwd/dQ) or keys (dKdV) per workgroup
+constexpr int kRabMax = 2048;
+
+struct AttnParams {
+  int kind, B, H, T;
+  const bf16_t *q, *k, *v;
+  int64_t ldq, ldk, ldv;
+  const uint8_t* key_valid;
+  float scale, inv_n, dropout_p;
+  unsigned long long seed;
+  const float* rab;
+  int nb;
+  int precise;
+  int out_f32;
+  // forward
+  void* out; int64_t ldo; float* lse;
+  // backward
+  const void* dout; int64_t lddo; int dout_f32;
+  const float* delta;
+  void *dq, *dk, *dv; int64_t lddq, lddk, lddv;
+  float* drab;
+};
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Swizzled LDS row image: row of HD bf16 = HD/8 16-byte chunks; chunk c of
+// row r lives at chunk position c ^ (r & MASK).
+template <int HD>
+__device__ __forceinline__ int lds_off(int row, int col) {
+  constexpr int NCH = HD / 8;
+  constexpr int MASK = NCH >= 8 ? 7 : NCH - 1;
+  const int c = col >> 3;
+  return row * (HD * 2) + ((c ^ (row & MASK)) << 4) + ((col & 7) << 1);
+}
+
+template <int HD>
+__device__ __forceinline__ bf16x8 lds_row8(const char* base, int row, int col) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + lds_off<HD>(row, col)));
+}
+
+// Transposed fragment: element j of lane (r, hh) = M[row0 + 8(j>>2) + 4hh + (j&3)][col0 + r].
+template <int HD>
+__device__ __forceinline__ bf16x8 lds_tr8(const char* base, int row0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int q4 = i >> 2, p = i & 3;
+  const int hh = g >> 1;
+  const int col = col0 + 16 * (g & 1) + 4 * p;
+  const int ra = row0 + 4 * hh + q4;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + lds_off<HD>(ra, col)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + lds_off<HD>(ra + 8, col)));
+  bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
+  bf16x8 r;
+  r[0] = l4[0]; r[1] = l4[1]; r[2] = l4[2]; r[3] = l4[3];
+  r[4] = h4[0]; r[5] = h4[1]; r[6] = h4[2]; r[7] = h4[3];
+  return r;
+}
+
+// Accumulator registers 8s..8s+7 as a bf16 operand (hi part, and the
+// residual lo part for the precise mode).
+__device__ __forceinline__ void pack_acc(const float* x, int s, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    __bf16 hb = static_cast<__bf16>(x[8 * s + j]);
+    hi[j] = hb;
+    lo[j] = static_cast<__bf16>(x[8 * s + j] - static_cast<float>(hb));
+  }
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float dsilu(float x) {
+  const float sg = 1.0f / (1.0f + __expf(-x));
+  return sg * (1.0f + x * (1.0f - sg));
+}
+
+// Counter-based dropout keep decision for element (b*H+h, q, k): identical
+// in forward and backward.
+__device__ __forceinline__ bool drop_keep(unsigned long long seed, int bh, int q, int k, int T, float p) {
+  unsigned long long x = seed ^ (((unsigned long long)bh * (unsigned)T + (unsigned)q) * (unsigned)T + (unsigned)k) *
+                                    0x9E3779B97F4A7C15ull;
+  x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27; x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  const float u = (float)(x >> 40) * (1.0f / 16777216.0f);
+  return u >= p;
+}
+
+__device__ __forceinline__ int acc_row(int i, int hh) { return (i & 3) + 8 * (i >> 2) + 4 * hh; }
+
+// Load a [HD] bf16 row slice as an 8-wide fragment from global; zero if !ok.
+__device__ __forceinline__ bf16x8 gload8(const bf16_t* p, bool ok) {
+  uint4 v = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 gload8_any(const void* base, int64_t off, bool f32, bool ok) {
+  if (!ok) return __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+  if (!f32) return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>((const bf16_t*)base + off));
+  const float4* fp = reinterpret_cast<const float4*>((const float*)base + off);
+  float4 a = fp[0], b = fp[1];
+  bf16x8 r;
+  r[0] = (__bf16)a.x; r[1] = (__bf16)a.y; r[2] = (__bf16)a.z; r[3] = (__bf16)a.w;
+  r[4] = (__bf16)b.x; r[5] = (__bf16)b.y; r[6] = (__bf16)b.z; r[7] = (__bf16)b.w;
+  return r;
+}
+
+// Stage rows [r0, r0+kChunk) of a [B*T, ld] head slice into a swizzled LDS
+// image (zeros outside [0, T)).
+template <int HD>
+__device__ __forceinline__ void stage_rows(char* dst, const void* src, int64_t ld, int b, int T, int h, int r0,
+                                           bool f32) {
+  constexpr int NCH = HD / 8;
+  for (int u = threadIdx.x; u < kChunk * NCH; u += blockDim.x) {
+    const int row = u / NCH, c = u % NCH;
+    const int t = r0 + row;
+    const bool ok = t >= 0 && t < T;
+    bf16x8 v = gload8_any(src, ((int64_t)b * T + (ok ? t : 0)) * ld + h * HD + c * 8, f32, ok);
+    *reinterpret_cast<uint4*>(dst + lds_off<HD>(row, c * 8)) = __builtin_bit_cast(uint4, v);
+  }
+}
+
+__device__ __forceinline__ int seq_start(const uint8_t* kv, int b, int T, int* s_start) {
+  if (!kv) return 0;
+  if (threadIdx.x == 0) *s_start = T;
+  __syncthreads();
+  for (int j = threadIdx.x; j < T; j += blockDim.x)
+    if (kv[(int64_t)b * T + j]) atomicMin(s_start, j);
+  __syncthreads();
+  return *s_start;
+}
+
+template <typename OutT>
+__device__ __forceinline__ void store4(OutT* p, const float* v);
+template <>
+__device__ __forceinline__ void store4<float>(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <>
+__device__ __forceinline__ void store4<bf16_t>(bf16_t* p, const float* v) {
+  uint2 t;
+  t.x = (unsigned)f32_to_bf16(v[0]) | ((unsigned)f32_to_bf16(v[1]) << 16);
+  t.y = (unsigned)f32_to_bf16(v[2]) | ((unsigned)f32_to_bf16(v[3]) << 16);
+  *reinterpret_cast<uint2*>(p) = t;
+}
+
+// Store an accumulated D^T tile set acc[NDT] (rows = feature d, lane = token)
+// to row `tok` of a [B*T, ld] output: lane holds d = dt*32 + 8g + 4hh + 0..3.
+template <int HD, int NDT>
+__device__ __forceinline__ void store_rows(void* out, int64_t ld, bool f32, int64_t tok, int h, int hh,
+                                           const f32x16* acc, float mul, bool ok) {
+  if (!ok) return;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = dt * 32 + 8 * g + 4 * hh;
+      if (d >= HD) continue;
+      float v[4] = {acc[dt][4 * g] * mul, acc[dt][4 * g + 1] * mul, acc[dt][4 * g + 2] * mul, acc[dt][4 * g + 3] * mul};
+      const int64_t off = tok * ld + h * HD + d;
+      if (f32) store4<float>((float*)out + off, v);
+      else store4<bf16_t>((bf16_t*)out + off, v);
+    }
+}
+
+// ================================================================ forward ====
+template <int HD, int KIND>
+__global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
+  constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
+  constexpr int IMG = kChunk * HD * 2;
+  constexpr int RAB = KIND == 1 ? kRabMax : 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 64 + RAB * 4 + 16];
+  char* Ks = smem;
+  char* Vs = smem + IMG;
+  uint8_t* kvs = reinterpret_cast<uint8_t*>(smem + 2 * IMG);
+  float* rabs = reinterpret_cast<float*>(smem + 2 * IMG + 64);
+  int* s_start = reinterpret_cast<int*>(smem + 2 * IMG + 64 + RAB * 4);
+
+  const int b = blockIdx.z, h = blockIdx.y, T = p.T;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int q0 = blockIdx.x * kBlockRows, qw = q0 + wave * 32, myq = qw + r;
+  const bool qok = myq < T;
+  const int start = seq_start(p.key_valid, b, T, s_start);
+  if (KIND == 1)
+    for (int j = threadIdx.x; j < p.nb; j += blockDim.x) rabs[j] = p.rab[h * p.nb + j];
+
+  bf16x8 qf[KS];
+  const bf16_t* qrow = p.q + ((int64_t)b * T + (qok ? myq : 0)) * p.ldq + h * HD;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) qf[ks] = gload8(qrow + 16 * ks + 8 * hh, qok);
+
+  f32x16 o[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+  const float sl2 = p.scale * kLog2e;
+  const float rdrop = 1.0f / (1.0f - p.dropout_p);
+  const bool drop = KIND == 0 && p.dropout_p > 0.f;
+  const int bh = b * p.H + h;
+
+  const int kbeg = (start / 32) * 32;
+  const int kend = min(T, q0 + kBlockRows);
+  for (int kc = kbeg; kc < kend; kc += kChunk) {
+    __syncthreads();
+    stage_rows<HD>(Ks, p.k, p.ldk, b, T, h, kc, false);
+    stage_rows<HD>(Vs, p.v, p.ldv, b, T, h, kc, false);
+    if (threadIdx.x < kChunk) {
+      const int t = kc + threadIdx.x;
+      kvs[threadIdx.x] = (t < T) && (!p.key_valid || p.key_valid[(int64_t)b * T + t]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int kb = kc + 32 * sub;
+      if (kb > qw + 31 || kb >= kend || kb + 32 <= start) continue;  // wave-uniform causal/padding skip
+      f32x16 s = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s = mfma(lds_row8<HD>(Ks, 32 * sub + r, 16 * ks + 8 * hh), qf[ks], s);
+      float pr[16], pd[16];
+      if (KIND == 0) {
+        float x[16], tmax = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kr = 32 * sub + acc_row(i, hh), key = kc + kr;
+          const bool ok = qok && key <= myq && kvs[kr];
+          x[i] = ok ? s[i] * sl2 : -INFINITY;
+          tmax = fmaxf(tmax, x[i]);
+        }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+        const float mn = fmaxf(m, tmax);
+        const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
+        float rs = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          pr[i] = (x[i] == -INFINITY) ? 0.f : exp2f(x[i] - mn);
+          rs += pr[i];
+        }
+        rs += __shfl_xor(rs, 32);
+        l = l * alpha + rs;
+        m = mn;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) o[dt] *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          pd[i] = pr[i];
+          if (drop) {
+            const int key = kc + 32 * sub + acc_row(i, hh);
+            pd[i] = drop_keep(p.seed, bh, myq, key, T, p.dropout_p) ? pr[i] * rdrop : 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kr = 32 * sub + acc_row(i, hh), key = kc + kr;
+          const bool ok = qok && key <= myq && kvs[kr];
+          const float sp = s[i] * p.scale + rabs[ok ? min(myq - key, p.nb - 1) : 0];
+          pd[i] = ok ? silu(sp) * p.inv_n : 0.f;
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 ph, pl;
+        pack_acc(pd, s2, ph, pl);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          bf16x8 vf = lds_tr8<HD>(Vs, 32 * sub + 16 * s2, dt * 32, lane);
+          o[dt] = mfma(vf, ph, o[dt]);
+          if (p.precise) o[dt] = mfma(vf, pl, o[dt]);
+        }
+      }
+    }
+  }
+  float mul = 1.f;
+  if (KIND == 0) {
+    mul = l > 0.f ? 1.0f / l : 0.f;
+    if (hh == 0 && qok && p.lse) p.lse[(int64_t)bh * T + myq] = l > 0.f ? (m + log2f(l)) * kLn2 : -INFINITY;
+  }
+  store_rows<HD, NDT>(p.out, p.ldo, p.out_f32, (int64_t)b * T + myq, h, hh, o, mul, qok);
+}
+
+// ========================================================== delta (softmax) ==
+// delta[bh, t] = sum_d dO[t, d] * O[t, d]  (fp32), one wave per (b, t, h).
+template <int HD>
+__global__ void __launch_bounds__(256) k_attn_delta(AttnParams p) {
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t total = (int64_t)p.B * p.T * p.H;
+  if (wid >= total) return;
+  const int h = (int)(wid % p.H);
+  const int64_t tok = wid / p.H;
+  float acc = 0.f;
+  for (int d = lane; d < HD; d += 64) {
+    const int64_t oo = tok * p.ldo + h * HD + d, od = tok * p.lddo + h * HD + d;
+    const float ov = p.out_f32 ? ((const float*)p.out)[oo] : bf16_to_f32(((const bf16_t*)p.out)[oo]);
+    const float dv = p.dout_f32 ? ((const float*)p.dout)[od] : bf16_to_f32(((const bf16_t*)p.dout)[od]);
+    acc += ov * dv;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if (lane == 0) {
+    const int b = (int)(tok / p.T), t = (int)(tok % p.T);
+    const_cast<float*>(p.delta)[((int64_t)b * p.H + h) * p.T + t] = acc;
+  }
+}
+
+// ================================================================ dQ =========
+template <int HD, int KIND>
+__global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
+  constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
+  constexpr int IMG = kChunk * HD * 2;
+  constexpr int RAB = KIND == 1 ? kRabMax : 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 64 + 2 * RAB * 4 + 16];
+  char* Ks = smem;
+  char* Vs = smem + IMG;
+  uint8_t* kvs = reinterpret_cast<uint8_t*>(smem + 2 * IMG);
+  float* rabs = reinterpret_cast<float*>(smem + 2 * IMG + 64);
+  float* bins = rabs + RAB;
+  int* s_start = reinterpret_cast<int*>(smem + 2 * IMG + 64 + 2 * RAB * 4);
+
+  const int b = blockIdx.z, h = blockIdx.y, T = p.T;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int q0 = blockIdx.x * kBlockRows, qw = q0 + wave * 32, myq = qw + r;
+  const bool qok = myq < T;
+  const int start = seq_start(p.key_valid, b, T, s_start);
+  if (KIND == 1)
+    for (int j = threadIdx.x; j < p.nb; j += blockDim.x) {
+      rabs[j] = p.rab[h * p.nb + j];
+      bins[j] = 0.f;
+    }
+  const int bh = b * p.H + h;
+  const int64_t tok = (int64_t)b * T + (qok ? myq : 0);
+
+  bf16x8 qf[KS], dof[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    qf[ks] = gload8(p.q + tok * p.ldq + h * HD + 16 * ks + 8 * hh, qok);
+    dof[ks] = gload8_any(p.dout, tok * p.lddo + h * HD + 16 * ks + 8 * hh, p.dout_f32, qok);
+  }
+  float lse2 = 0.f, dlt = 0.f;
+  if (KIND == 0 && qok) {
+    lse2 = p.lse[(int64_t)bh * T + myq] * kLog2e;
+    dlt = p.delta[(int64_t)bh * T + myq];
+  }
+  const bool row_live = KIND == 1 || lse2 != -INFINITY;
+  f32x16 acc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) acc[dt] = f32x16{};
+  const float sl2 = p.scale * kLog2e;
+  const float rdrop = 1.0f / (1.0f - p.dropout_p);
+  const bool drop = KIND == 0 && p.dropout_p > 0.f;
+
+  const int kbeg = (start / 32) * 32;
+  const int kend = min(T, q0 + kBlockRows);
+  for (int kc = kbeg; kc < kend; kc += kChunk) {
+    __syncthreads();
+    stage_rows<HD>(Ks, p.k, p.ldk, b, T, h, kc, false);
+    stage_rows<HD>(Vs, p.v, p.ldv, b, T, h, kc, false);
+    if (threadIdx.x < kChunk) {
+      const int t = kc + threadIdx.x;
+      kvs[threadIdx.x] = (t < T) && (!p.key_valid || p.key_valid[(int64_t)b * T + t]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int kb = kc + 32 * sub;
+      if (kb > qw + 31 || kb >= kend || kb + 32 <= start) continue;
+      f32x16 s = f32x16{}, dp = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s = mfma(lds_row8<HD>(Ks, 32 * sub + r, 16 * ks + 8 * hh), qf[ks], s);
+        dp = mfma(lds_row8<HD>(Vs, 32 * sub + r, 16 * ks + 8 * hh), dof[ks], dp);
+      }
+      float ds[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int kr = 32 * sub + acc_row(i, hh), key = kc + kr;
+        const bool ok = qok && row_live && key <= myq && kvs[kr];
+        if (KIND == 0) {
+          const float pv = ok ? exp2f(s[i] * sl2 - lse2) : 0.f;
+          float dpv = dp[i];
+          if (drop) dpv = drop_keep(p.seed, bh, myq, key, T, p.dropout_p) ? dpv * rdrop : 0.f;
+          ds[i] = pv * (dpv - dlt);
+        } else {
+          const int bk = min(myq - key, p.nb - 1);
+          const float sp = s[i] * p.scale + rabs[ok ? bk : 0];
+          ds[i] = ok ? dp[i] * dsilu(sp) * p.inv_n : 0.f;
+          if (ok && ds[i] != 0.f) atomicAdd(&bins[bk], ds[i]);
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 dh, dl;
+        pack_acc(ds, s2, dh, dl);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          bf16x8 kf = lds_tr8<HD>(Ks, 32 * sub + 16 * s2, dt * 32, lane);
+          acc[dt] = mfma(kf, dh, acc[dt]);
+          if (p.precise) acc[dt] = mfma(kf, dl, acc[dt]);
+        }
+      }
+    }
+  }
+  store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, (int64_t)b * T + myq, h, hh, acc, p.scale, qok);
+  if (KIND == 1) {
+    __syncthreads();
+    for (int j = threadIdx.x; j < p.nb; j += blockDim.x)
+      if (bins[j] != 0.f) atomicAdd(&p.drab[h * p.nb + j], bins[j]);
+  }
+}
+
+// ============================================================== dK / dV =====
+template <int HD, int KIND>
+__global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
+  constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
+  constexpr int IMG = kChunk * HD * 2;
+  constexpr int RAB = KIND == 1 ? kRabMax : 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 2 * kChunk * 4 + RAB * 4 + 16];
+  char* Qs = smem;
+  char* Ds = smem + IMG;
+  float* lses = reinterpret_cast<float*>(smem + 2 * IMG);
+  float* dlts = lses + kChunk;
+  float* rabs = dlts + kChunk;
+  int* s_start = reinterpret_cast<int*>(smem + 2 * IMG + 2 * kChunk * 4 + RAB * 4);
+
+  const int b = blockIdx.z, h = blockIdx.y, T = p.T;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int k0 = blockIdx.x * kBlockRows, kw = k0 + wave * 32, myk = kw + r;
+  const int start = seq_start(p.key_valid, b, T, s_start);
+  const bool kok = myk < T && myk >= start && (!p.key_valid || p.key_valid[(int64_t)b * T + myk]);
+  if (KIND == 1)
+    for (int j = threadIdx.x; j < p.nb; j += blockDim.x) rabs[j] = p.rab[h * p.nb + j];
+  const int bh = b * p.H + h;
+  const int64_t tok = (int64_t)b * T + (myk < T ? myk : 0);
+
+  bf16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    kf[ks] = gload8(p.k + tok * p.ldk + h * HD + 16 * ks + 8 * hh, myk < T);
+    vf[ks] = gload8(p.v + tok * p.ldv + h * HD + 16 * ks + 8 * hh, myk < T);
+  }
+  f32x16 dk[NDT], dv[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) { dk[dt] = f32x16{}; dv[dt] = f32x16{}; }
+  const float sl2 = p.scale * kLog2e;
+  const float rdrop = 1.0f / (1.0f - p.dropout_p);
+  const bool drop = KIND == 0 && p.dropout_p > 0.f;
+
+  // queries that can see this block's keys: q >= k0 and q >= start
+  const int qbeg = (max(k0, start) / 32) * 32;
+  for (int qc = qbeg; qc < T; qc += kChunk) {
+    __syncthreads();
+    stage_rows<HD>(Qs, p.q, p.ldq, b, T, h, qc, false);
+    stage_rows<HD>(Ds, p.dout, p.lddo, b, T, h, qc, p.dout_f32);
+    if (threadIdx.x < kChunk) {
+      const int t = qc + threadIdx.x;
+      float lv = -INFINITY, dl = 0.f;
+      if (KIND == 0 && t < T) {
+        lv = p.lse[(int64_t)bh * T + t] * kLog2e;
+        dl = p.delta[(int64_t)bh * T + t];
+      }
+      lses[threadIdx.x] = lv;
+      dlts[threadIdx.x] = dl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int qb = qc + 32 * sub;
+      if (qb + 31 < kw || qb >= T) continue;  // wave-uniform: every query precedes this wave's keys
+      f32x16 s = f32x16{}, dp = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s = mfma(lds_row8<HD>(Qs, 32 * sub + r, 16 * ks + 8 * hh), kf[ks], s);
+        dp = mfma(lds_row8<HD>(Ds, 32 * sub + r, 16 * ks + 8 * hh), vf[ks], dp);
+      }
+      float pd[16], ds[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qr = 32 * sub + acc_row(i, hh), q = qc + qr;
+        const bool ok = kok && q < T && myk <= q;
+        if (KIND == 0) {
+          const float lv = lses[qr];
+          const float pv = (ok && lv != -INFINITY) ? exp2f(s[i] * sl2 - lv) : 0.f;
+          float dpv = dp[i];
+          pd[i] = pv;
+          if (drop) {
+            const bool keep = drop_keep(p.seed, bh, q, myk, T, p.dropout_p);
+            pd[i] = keep ? pv * rdrop : 0.f;
+            dpv = keep ? dpv * rdrop : 0.f;
+          }
+          ds[i] = pv * (dpv - dlts[qr]);
+        } else {
+          const float sp = s[i] * p.scale + rabs[ok ? min(q - myk, p.nb - 1) : 0];
+          pd[i] = ok ? silu(sp) * p.inv_n : 0.f;
+          ds[i] = ok ? dp[i] * dsilu(sp) * p.inv_n : 0.f;
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 ph, pl, dh, dl;
+        pack_acc(pd, s2, ph, pl);
+        pack_acc(ds, s2, dh, dl);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          bf16x8 dof = lds_tr8<HD>(Ds, 32 * sub + 16 * s2, dt * 32, lane);
+          bf16x8 qf = lds_tr8<HD>(Qs, 32 * sub + 16 * s2, dt * 32, lane);
+          dv[dt] = mfma(dof, ph, dv[dt]);
+          dk[dt] = mfma(qf, dh, dk[dt]);
+          if (p.precise) {
+            dv[dt] = mfma(dof, pl, dv[dt]);
+            dk[dt] = mfma(qf, dl, dk[dt]);
+          }
+        }
+      }
+    }
+  }
+  const int64_t otok = (int64_t)b * T + myk;
+  store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, otok, h, hh, dk, p.scale, myk < T);
+  store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, 1.f, myk < T);
+}
+
+template <int HD>
+static int launch_hd(const AttnParams& p, int which, hipStream_t s) {
+  dim3 grid((p.T + kBlockRows - 1) / kBlockRows, p.H, p.B);
+  if (which == 0) {
+    if (p.kind == GRK_ATTN_SOFTMAX) k_attn_fwd<HD, 0><<<grid, 256, 0, s>>>(p);
+    else k_attn_fwd<HD, 1><<<grid, 256, 0, s>>>(p);
+  } else if (which == 1) {
+    const int64_t waves = (int64_t)p.B * p.T * p.H;
+    k_attn_delta<HD><<<(unsigned)((waves + 3) / 4), 256, 0, s>>>(p);
+  } else if (which == 2) {
+    if (p.kind == GRK_ATTN_SOFTMAX) k_attn_bwd_dq<HD, 0><<<grid, 256, 0, s>>>(p);
+    else k_attn_bwd_dq<HD, 1><<<grid, 256, 0, s>>>(p);
+  } else {
+    if (p.kind == GRK_ATTN_SOFTMAX) k_attn_bwd_dkdv<HD, 0><<<grid, 256, 0, s>>>(p);
+    else k_attn_bwd_dkdv<HD, 1><<<grid, 256, 0, s>>>(p);
+  }
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
+  switch (hd) {
+    case 16: return launch_hd<16>(p, which, s);
+    case 32: return launch_hd<32>(p, which, s);
+    case 64: return launch_hd<64>(p, which, s);
+    case 128: return launch_hd<128>(p, which, s);
+  }
+  set_error("head_dim %d unsupported (16, 32, 64, 128)", hd);
+  return GRK_EUNSUPPORTED;
+}
+
+static int fill_params(const grk_attn_args* a, AttnParams* p) {
+  GRK_CHECK_ARG(a != nullptr, "args is NULL");
+  GRK_CHECK_ARG(a->kind == GRK_ATTN_SOFTMAX || a->kind == GRK_ATTN_HSTU, "bad kind");
+  GRK_CHECK_ARG(a->batch > 0 && a->heads > 0 && a->seq_len > 0, "batch/heads/seq_len must be > 0");
+  GRK_CHECK_ARG(a->head_dim == 16 || a->head_dim == 32 || a->head_dim == 64 || a->head_dim == 128,
+                "head_dim %d unsupported (16, 32, 64, 128)", a->head_dim);
+  GRK_CHECK_ARG(a->q && a->k && a->v, "q/k/v required");
+  const int64_t need = (int64_t)a->heads * a->head_dim;
+  GRK_CHECK_ARG(a->ldq >= need && a->ldk >= need && a->ldv >= need, "row strides smaller than heads*head_dim");
+  GRK_CHECK_ARG(a->ldq % 8 == 0 && a->ldk % 8 == 0 && a->ldv % 8 == 0, "row strides must be multiples of 8");
+  GRK_CHECK_ARG(((uintptr_t)a->q | (uintptr_t)a->k | (uintptr_t)a->v) % 16 == 0, "q/k/v must be 16-byte aligned");
+  GRK_CHECK_ARG(a->kind == GRK_ATTN_SOFTMAX || (a->rab && a->num_buckets > 0 && a->num_buckets <= kRabMax),
+                "hstu needs rab with 1..%d buckets", kRabMax);
+  GRK_CHECK_ARG(a->dropout_p >= 0.f && a->dropout_p < 1.f, "dropout_p must be in [0, 1)");
+  GRK_CHECK_ARG(a->kind == GRK_ATTN_SOFTMAX || a->dropout_p == 0.f, "hstu attention has no dropout");
+  GRK_CHECK_ARG(a->out_dtype == GRK_F32 || a->out_dtype == GRK_BF16, "out_dtype must be GRK_F32 / GRK_BF16");
+  memset(p, 0, sizeof(*p));
+  p->kind = a->kind; p->B = a->batch; p->H = a->heads; p->T = a->seq_len;
+  p->q = (const bf16_t*)a->q; p->k = (const bf16_t*)a->k; p->v = (const bf16_t*)a->v;
+  p->ldq = a->ldq; p->ldk = a->ldk; p->ldv = a->ldv;
+  p->key_valid = a->key_valid;
+  p->scale = a->scale; p->inv_n = a->inv_n; p->dropout_p = a->dropout_p; p->seed = a->seed;
+  p->rab = a->rab; p->nb = a->num_buckets;
+  p->precise = a->precise; p->out_f32 = a->out_dtype == GRK_F32;
+  return GRK_OK;
+}
+
+}  // namespace grk
+
+using namespace grk;
+
+extern "C" int grk_attention_fwd(const grk_attn_args* a, void* out, int64_t ldo, float* lse, void* stream) {
+  clear_error();
+  AttnParams p;
+  int rc = fill_params(a, &p);
+  if (rc) return rc;
+  GRK_CHECK_ARG(out && ldo >= (int64_t)a->heads * a->head_dim, "bad out / ldo");
+  GRK_CHECK_ARG(a->kind == GRK_ATTN_HSTU || lse, "softmax forward needs lse [B, H, T]");
+  p.out = out; p.ldo = ldo; p.lse = lse;
+  return launch(p, a->head_dim, 0, (hipStream_t)stream);
+}
+
+extern "C" int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout,
+                                 int64_t lddo, int dout_dtype, const float* lse, float* delta_ws, void* dq,
+                                 int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv, float* drab,
+                                 void* stream) {
+  clear_error();
+  AttnParams p;
+  int rc = fill_params(a, &p);
+  if (rc) return rc;
+  const int64_t need = (int64_t)a->heads * a->head_dim;
+  GRK_CHECK_ARG(dout && lddo >= need && lddo % 8 == 0, "bad dout / lddo");
+  GRK_CHECK_ARG(dout_dtype == GRK_F32 || dout_dtype == GRK_BF16, "bad dout dtype");
+  GRK_CHECK_ARG(dq && dk && dv && lddq >= need && lddk >= need && lddv >= need, "bad dq/dk/dv");
+  GRK_CHECK_ARG(a->kind == GRK_ATTN_HSTU || (out && lse && delta_ws && ldo >= need),
+                "softmax backward needs out, lse and delta_ws [B, H, T]");
+  GRK_CHECK_ARG(a->kind == GRK_ATTN_SOFTMAX || drab, "hstu backward needs drab (zero-initialised)");
+  p.out = const_cast<void*>(out); p.ldo = ldo;
+  p.dout = dout; p.lddo = lddo; p.dout_f32 = dout_dtype == GRK_F32;
+  p.lse = const_cast<float*>(lse); p.delta = delta_ws;
+  p.dq = dq; p.lddq = lddq; p.dk = dk; p.lddk = lddk; p.dv = dv; p.lddv = lddv;
+  p.drab = drab;
+  hipStream_t s = (hipStream_t)stream;
+  if (a->kind == GRK_ATTN_SOFTMAX) {
+    // out dtype of the forward output equals out_dtype of these args
+    rc = launch(p, a->head_dim, 1, s);
+    if (rc) return rc;
+  }
+  rc = launch(p, a->head_dim, 2, s);
+  if (rc) return rc;
+  return launch(p, a->head_dim, 3, s);
+}

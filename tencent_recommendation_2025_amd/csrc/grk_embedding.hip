@@ -256,13 +256,14 @@ extern "C" int grk_embedding_gather(const grk_feature* features, int num_feature
   GRK_CHECK_ARG(itype == GRK_I32 || itype == GRK_I64, "itype must be GRK_I32 or GRK_I64");
   const int vec = dtype == GRK_F32 ? 4 : 8;
   GRK_CHECK_ARG(dim > 0 && dim % vec == 0, "dim (%d) must be a positive multiple of %d", dim, vec);
-  GRK_CHECK_ARG(out != nullptr && num_tokens >= 0, "bad output");
+  GRK_CHECK_ARG(num_tokens >= 0 && (out != nullptr || num_tokens == 0), "bad output");
   GRK_CHECK_ARG(out_ld % vec == 0 && ((uintptr_t)out % 16) == 0, "output must be 16-byte aligned per row");
   FeatArgs fa;
   memset(&fa, 0, sizeof(fa));
   for (int i = 0; i < num_features; ++i) {
     const grk_feature& f = features[i];
-    GRK_CHECK_ARG(f.table && f.idx && f.bag >= 1 && f.num_rows > 0, "feature %d: bad table/idx/bag", i);
+    GRK_CHECK_ARG(f.table && (f.idx || num_tokens == 0) && f.bag >= 1 && f.num_rows > 0,
+                  "feature %d: bad table/idx/bag", i);
     GRK_CHECK_ARG(f.out_col >= 0 && f.out_col + dim <= out_ld && f.out_col % vec == 0,
                   "feature %d: out_col %d out of range / misaligned", i, f.out_col);
     GRK_CHECK_ARG(((uintptr_t)f.table % 16) == 0, "feature %d: table must be 16-byte aligned", i);
@@ -322,7 +323,8 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   int64_t total = 0;
   for (int i = 0; i < num_lookups; ++i) {
     const grk_lookup& L = lookups[i];
-    GRK_CHECK_ARG(L.idx && L.grad && L.bag >= 1 && L.num_tokens >= 0, "lookup %d: bad idx/grad/bag", i);
+    GRK_CHECK_ARG(L.bag >= 1 && L.num_tokens >= 0 && ((L.idx && L.grad) || L.num_tokens == 0),
+                  "lookup %d: bad idx/grad/bag", i);
     GRK_CHECK_ARG(L.idx_mode >= 0 && L.idx_mode <= 3, "lookup %d: bad idx_mode", i);
     GRK_CHECK_ARG(L.idx_mode == GRK_IDX_PLAIN || L.idx_mode == GRK_IDX_POSITION || token_type,
                   "lookup %d: masked mode needs token_type", i);

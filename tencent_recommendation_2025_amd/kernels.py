@@ -169,3 +169,55 @@ def table_adamw(param, exp_avg, exp_avg_sq, hp, ids=None, rows=None, count=None,
                                  _ptr(count), capacity, _ptr(row_slot), hp,
                                  L.ADAM_LAZY if lazy else L.ADAM_DENSE, L.stream_ptr(param.device))
     L.check(rc, 'grk_table_adamw')
+
+
+# ------------------------------------------------------------------ attention
+def _col_view_ok(t, name):
+    if t.dim() != 2 or t.stride(1) != 1 or t.dtype != torch.bfloat16:
+        raise L.GrkError(f'{name} must be a bf16 [B*T, >=H*hd] row-major view')
+    if t.stride(0) % 8 or t.data_ptr() % 16:
+        raise L.GrkError(f'{name}: row stride must be a multiple of 8 and the view 16-byte aligned')
+
+
+def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, inv_n=1.0, dropout_p=0.0, seed=0,
+              precise=False, out_dtype=torch.bfloat16):
+    """Build grk_attn_args for bf16 [B*T, ld] column views q/k/v (head h at cols h*hd)."""
+    for t, n in ((q, 'q'), (k, 'k'), (v, 'v')):
+        _col_view_ok(t, n)
+        if t.shape[0] != B * T or t.shape[1] < H * hd:
+            raise L.GrkError(f'{n}: shape {tuple(t.shape)} does not fit B*T={B * T}, H*hd={H * hd}')
+    if key_valid is not None:
+        if key_valid.dtype != torch.uint8 or key_valid.shape != (B, T) or not key_valid.is_contiguous():
+            raise L.GrkError('key_valid must be a contiguous uint8 [B, T] tensor')
+    nb = 0
+    if kind == L.ATTN_HSTU:
+        if rab is None or rab.dtype != torch.float32 or rab.dim() != 2 or rab.shape[0] != H or not rab.is_contiguous():
+            raise L.GrkError('hstu needs a contiguous fp32 rab [H, num_buckets]')
+        nb = rab.shape[1]
+    if scale is None:
+        scale = hd ** -0.5
+    return L.GrkAttnArgs(kind, B, H, T, hd, nb, q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0),
+                         v.stride(0), _ptr(key_valid), _ptr(rab), float(scale), float(inv_n), float(dropout_p),
+                         int(bool(precise)), int(seed) & (2 ** 64 - 1), L.dtype_code(out_dtype), 0)
+
+
+def attention_fwd(args, out, lse=None):
+    """grk_attention_fwd: out [B*T, >=H*hd] (args.out_dtype); lse fp32 [B, H, T] (softmax)."""
+    _require_cuda(out, lse)
+    if out.stride(1) != 1 or out.stride(0) % 8:
+        raise L.GrkError('out must be row-major with a row stride multiple of 8')
+    rc = L.lib().grk_attention_fwd(C.byref(args), out.data_ptr(), out.stride(0), _ptr(lse), L.stream_ptr(out.device))
+    L.check(rc, 'grk_attention_fwd')
+
+
+def attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab=None):
+    """grk_attention_bwd: writes dq/dk/dv (args.out_dtype) and accumulates drab."""
+    _require_cuda(dout, dq, dk, dv, drab)
+    for t, n in ((dout, 'dout'), (dq, 'dq'), (dk, 'dk'), (dv, 'dv')):
+        if t.stride(1) != 1 or t.stride(0) % 8:
+            raise L.GrkError(f'{n} must be row-major with a row stride multiple of 8')
+    rc = L.lib().grk_attention_bwd(C.byref(args), _ptr(out), 0 if out is None else out.stride(0), dout.data_ptr(),
+                                   dout.stride(0), L.dtype_code(dout.dtype), _ptr(lse), _ptr(delta), dq.data_ptr(),
+                                   dq.stride(0), dk.data_ptr(), dk.stride(0), dv.data_ptr(), dv.stride(0), _ptr(drab),
+                                   L.stream_ptr(dout.device))
+    L.check(rc, 'grk_attention_bwd')

@@ -1,0 +1,172 @@
+"""GPU parity of grk_attention_fwd/bwd against the oracle (oracle/attention.py
+is pinned to the reference's SDPA in tests/test_oracle_golden.py; oracle/hstu.py
+is parity-unpinned, checked by finite differences in test_oracle_selfcheck.py).
+
+Tolerance (BASELINE.json north star): 1e-3 normwise relative error for bf16
+attention, against the fp64 oracle fed the SAME bf16-rounded inputs, fp32
+outputs, with the precise (hi/lo) probability operands.  The fast mode
+(probabilities rounded to bf16) is held to 1e-2."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import attention as oatt
+from oracle import hstu as ohstu
+from oracle.embedding import to_bf16_f32
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+TOL_PRECISE = 1e-3
+TOL_FAST = 1e-2
+
+
+@pytest.fixture(scope='module')
+def K():
+    from tencent_recommendation_2025_amd import _lib, kernels
+    _lib.lib()
+    return kernels
+
+
+def nrel(got, want):
+    want = np.asarray(want, np.float64)
+    den = np.linalg.norm(want)
+    return float(np.linalg.norm(np.asarray(got, np.float64) - want) / (den if den > 0 else 1.0))
+
+
+def make_inputs(B, T, H, hd, lens, seed, width_mult=3):
+    """Packed bf16 qkv [B*T, 3*H*hd] (q|k|v column blocks) + key_valid from left-padded lengths."""
+    rng = np.random.default_rng(seed)
+    D = H * hd
+    x = to_bf16_f32(rng.standard_normal((B * T, width_mult * D)).astype(np.float32))
+    valid = np.zeros((B, T), np.uint8)
+    for b, n in enumerate(lens):
+        valid[b, T - n:] = 1
+    return x, valid
+
+
+def heads(x, B, T, H, hd):
+    return x.reshape(B, T, H, hd).transpose(0, 2, 1, 3)
+
+
+def flat(x):
+    B, H, T, hd = x.shape
+    return x.transpose(0, 2, 1, 3).reshape(B * T, H * hd)
+
+
+def drop_mask_np(seed, B, H, T, p):
+    """numpy replica of drop_keep() in grk_attention.hip (test infrastructure)."""
+    with np.errstate(over='ignore'):
+        bh = np.arange(B * H, dtype=np.uint64)[:, None, None]
+        q = np.arange(T, dtype=np.uint64)[None, :, None]
+        k = np.arange(T, dtype=np.uint64)[None, None, :]
+        T64 = np.uint64(T)
+        x = np.uint64(seed) ^ (((bh * T64 + q) * T64 + k) * np.uint64(0x9E3779B97F4A7C15))
+        x ^= x >> np.uint64(30); x *= np.uint64(0xBF58476D1CE4E5B9)
+        x ^= x >> np.uint64(27); x *= np.uint64(0x94D049BB133111EB)
+        x ^= x >> np.uint64(31)
+    u = (x >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return (u >= np.float32(p)).reshape(B, H, T, T)
+
+
+def run(K, kind, B, T, H, hd, lens, precise, seed=0, dropout=0.0, nb=None, out_dtype=torch.float32):
+    from tencent_recommendation_2025_amd import _lib as L
+    D = H * hd
+    x, valid = make_inputs(B, T, H, hd, lens, seed)
+    xd = torch.from_numpy(x).to(DEV).to(torch.bfloat16)
+    q, k, v = xd[:, :D], xd[:, D:2 * D], xd[:, 2 * D:]
+    kv = torch.from_numpy(valid).to(DEV)
+    rng = np.random.default_rng(seed + 1)
+    rab = None
+    extra = {}
+    if kind == L.ATTN_HSTU:
+        nb = nb or T
+        rab_np = (rng.standard_normal((H, nb)) * 0.5).astype(np.float32)
+        rab = torch.from_numpy(rab_np).to(DEV)
+        extra = dict(rab=rab, inv_n=1.0 / T, scale=hd ** -0.5)
+    args = K.attn_args(kind, q, k, v, B, T, H, hd, key_valid=kv, precise=precise, dropout_p=dropout, seed=1234,
+                       out_dtype=out_dtype, **extra)
+    out = torch.empty(B * T, D, dtype=out_dtype, device=DEV)
+    lse = torch.empty(B, H, T, dtype=torch.float32, device=DEV)
+    K.attention_fwd(args, out, lse)
+    dout_np = to_bf16_f32(rng.standard_normal((B * T, D)).astype(np.float32))
+    dout = torch.from_numpy(dout_np).to(DEV).to(out_dtype)
+    dq, dk, dv = (torch.empty(B * T, D, dtype=out_dtype, device=DEV) for _ in range(3))
+    delta = torch.empty(B, H, T, device=DEV)
+    drab = torch.zeros(H, nb, device=DEV) if kind == L.ATTN_HSTU else None
+    K.attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab)
+    torch.cuda.synchronize()
+    qh, kh, vh = (heads(x[:, i * D:(i + 1) * D], B, T, H, hd) for i in range(3))
+    doh = heads(dout_np, B, T, H, hd)
+    res = dict(out=out.float().cpu().numpy(), dq=dq.float().cpu().numpy(), dk=dk.float().cpu().numpy(),
+               dv=dv.float().cpu().numpy(), lse=lse.cpu().numpy())
+    if kind == L.ATTN_SOFTMAX:
+        keep = drop_mask_np(1234, B, H, T, dropout) if dropout > 0 else None
+        o, lse_ref, _ = oatt.forward(qh, kh, vh, valid.astype(bool), keep=keep, dropout_p=dropout)
+        gq, gk, gv = oatt.backward(qh, kh, vh, valid.astype(bool), doh, keep=keep, dropout_p=dropout)
+        want = dict(out=flat(o), dq=flat(gq), dk=flat(gk), dv=flat(gv), lse=lse_ref)
+    else:
+        o, _, _ = ohstu.forward(qh, kh, vh, valid.astype(bool), rab_np, hd ** -0.5, 1.0 / T)
+        gq, gk, gv, gr = ohstu.backward(qh, kh, vh, valid.astype(bool), rab_np, hd ** -0.5, 1.0 / T, doh)
+        want = dict(out=flat(o), dq=flat(gq), dk=flat(gk), dv=flat(gv), drab=gr)
+        res['drab'] = drab.cpu().numpy()
+    return res, want, valid
+
+
+@pytest.mark.parametrize('hd', [16, 32, 64, 128])
+@pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
+def test_attention_parity_precise(K, kind, hd):
+    H = 2 if hd >= 64 else 4
+    res, want, valid = run(K, kind, B=3, T=201, H=H, hd=hd, lens=[201, 120, 7], precise=True)
+    for key in ('out', 'dq', 'dk', 'dv') + (('drab',) if kind == 1 else ()):
+        err = nrel(res[key], want[key])
+        assert err < TOL_PRECISE, f'{key}: normwise rel err {err:.2e}'
+    if kind == 0:
+        live = np.isfinite(want['lse'])
+        np.testing.assert_allclose(res['lse'][live], want['lse'][live], rtol=1e-5, atol=1e-4)
+        assert np.all(np.isneginf(res['lse'][~live]))
+
+
+@pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
+def test_attention_parity_fast_bf16(K, kind):
+    res, want, _ = run(K, kind, B=4, T=201, H=8, hd=64, lens=[201, 150, 64, 33], precise=False,
+                       out_dtype=torch.bfloat16)
+    for key in ('out', 'dq', 'dk', 'dv'):
+        err = nrel(res[key], want[key])
+        assert err < TOL_FAST, f'{key}: normwise rel err {err:.2e}'
+
+
+def test_fully_masked_rows_are_zero(K):
+    res, want, valid = run(K, 0, B=2, T=70, H=2, hd=64, lens=[70, 5], precise=True)
+    pad_rows = np.where(valid.reshape(-1) == 0)[0]
+    for key in ('out', 'dq'):
+        assert np.all(res[key][pad_rows] == 0)
+        assert np.all(np.isfinite(res[key]))
+    assert np.all(np.isfinite(res['dk'])) and np.all(np.isfinite(res['dv']))
+
+
+def test_softmax_dropout_matches_masked_oracle(K):
+    res, want, _ = run(K, 0, B=2, T=97, H=2, hd=32, lens=[97, 40], precise=True, dropout=0.2)
+    for key in ('out', 'dq', 'dk', 'dv'):
+        err = nrel(res[key], want[key])
+        assert err < TOL_PRECISE, f'{key}: normwise rel err {err:.2e}'
+
+
+def test_long_sequence_multi_chunk(K):
+    """T=1025 (config 5 length): many K/V chunks and q-blocks."""
+    res, want, _ = run(K, 1, B=1, T=1025, H=1, hd=128, lens=[900], precise=True, nb=1025)
+    for key in ('out', 'dq', 'dk', 'dv', 'drab'):
+        err = nrel(res[key], want[key])
+        assert err < TOL_PRECISE, f'{key}: normwise rel err {err:.2e}'
+
+
+def test_hstu_bucket_clipping(K):
+    res, want, _ = run(K, 1, B=2, T=150, H=2, hd=64, lens=[150, 90], precise=True, nb=33)
+    for key in ('out', 'dq', 'dk', 'dv', 'drab'):
+        assert nrel(res[key], want[key]) < TOL_PRECISE, key
+
+
+def test_determinism(K):
+    a, _, _ = run(K, 0, B=2, T=130, H=2, hd=64, lens=[130, 77], precise=False, seed=5)
+    b, _, _ = run(K, 0, B=2, T=130, H=2, hd=64, lens=[130, 77], precise=False, seed=5)
+    for key in ('out', 'dq', 'dk', 'dv'):
+        assert np.array_equal(a[key], b[key])
