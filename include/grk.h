@@ -46,7 +46,6 @@ enum {
 };
 
 #define GRK_MAX_FEATURES 48
-#define GRK_MAX_LOOKUPS 8
 
 /* Returns the last error message of the calling thread ("" if none). */
 const char* grk_last_error(void);
@@ -81,13 +80,17 @@ int grk_embedding_gather(const grk_feature* features, int num_features, int dim,
                          int64_t out_ld, int32_t* err_flag, void* stream);
 
 /* One lookup that received a gradient (source of gradient rows).  The item
- * table has three (seq, pos, neg: model/BaseLine/model.py:243,376-377). */
+ * table has three (seq, pos, neg: model/BaseLine/model.py:243,376-377).
+ * Several tables stored in one flat buffer (a "table group") are reduced in
+ * one call: lookup rows are shifted by row_offset into the group's rows. */
 typedef struct grk_lookup {
   const void* idx;       /* index tensor as in grk_feature                 */
   const void* grad;      /* [num_tokens, grad_ld] upstream grad, grad dtype */
   int64_t num_tokens;
   int64_t idx_ld;
   int64_t grad_ld;
+  int64_t row_offset;    /* group row of this lookup's table row 0         */
+  int64_t table_rows;    /* rows of this lookup's table (range check)      */
   int32_t bag;
   int32_t grad_col;      /* first column of this lookup's grad rows        */
   int32_t idx_mode;
@@ -110,6 +113,8 @@ size_t grk_embedding_backward_workspace(int64_t num_occurrences, int64_t num_row
  *   uniq_ids   int64 [num_occurrences]: sorted unique row ids
  *   uniq_rows  fp32  [num_occurrences, dim]: their gradient rows
  *   uniq_count int32 [1]: number of unique rows
+ * num_rows = rows of the group; padding_idx is a table-local row (each
+ * lookup's row padding_idx is skipped).  Any number of lookups.
  *   row_slot   int32 [num_rows]: row_slot[id] = position in uniq_*;
  *              entries of untouched rows are left as they were (-1 by
  *              contract; grk_table_adamw restores them). */
@@ -181,6 +186,32 @@ int grk_attention_fwd(const grk_attn_args* a, void* out, int64_t ldo, float* lse
 int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
                       int dout_dtype, const float* lse, float* delta_ws, void* dq, int64_t lddq, void* dk,
                       int64_t lddk, void* dv, int64_t lddv, float* drab, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Pair logits + BCE (model/BaseLine/model.py:379-382; main.py:177-182)
+ * ------------------------------------------------------------------------ */
+/* Floats of `partials` workspace needed for num_rows rows. */
+size_t grk_pair_logits_partials(int64_t num_rows);
+
+/* pos/neg_logits[n] = <h_n, e_pos_n> / <h_n, e_neg_n>, zeroed where
+ * next_token_type[n] != 1 (NULL: every row valid).  If `loss` is non-NULL it
+ * also writes the reference BCE loss (mean over valid rows of
+ * softplus(-pos) plus mean of softplus(neg)) and the valid-row count, reduced
+ * in a fixed order.  Inputs share `dtype`. */
+int grk_pair_logits_fwd(const void* h, int64_t ldh, const void* e_pos, int64_t ldp, const void* e_neg, int64_t ldn,
+                        const int32_t* next_token_type, int64_t num_rows, int dim, int dtype, float* pos_logits,
+                        float* neg_logits, float* partials, float* loss, int32_t* count, void* stream);
+
+/* dh = gp*e_pos + gn*e_neg, de_pos = gp*h, de_neg = gn*h per row.
+ * Either gpos/gneg (fp32 per-row coefficients) are given, or -- when
+ * pos_logits/neg_logits are non-NULL -- the BCE coefficients
+ * gp = g*(sigmoid(pos)-1)/count, gn = g*sigmoid(neg)/count on valid rows,
+ * with g = *grad_loss (device scalar; NULL = 1).  Outputs may be NULL. */
+int grk_pair_logits_bwd(const void* h, int64_t ldh, const void* e_pos, int64_t ldp, const void* e_neg, int64_t ldn,
+                        int64_t num_rows, int dim, int dtype, const float* gpos, const float* gneg,
+                        const float* pos_logits, const float* neg_logits, const int32_t* next_token_type,
+                        const int32_t* count, const float* grad_loss, void* dh, int64_t lddh, void* de_pos,
+                        int64_t lddp, void* de_neg, int64_t lddn, void* stream);
 
 #ifdef __cplusplus
 }

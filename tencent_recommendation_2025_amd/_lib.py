@@ -25,7 +25,7 @@ GRK_F32, GRK_BF16 = 0, 1
 GRK_I32, GRK_I64 = 0, 1
 IDX_PLAIN, IDX_ITEM_MASK, IDX_USER_MASK, IDX_POSITION = 0, 1, 2, 3
 ADAM_DENSE, ADAM_LAZY = 0, 1
-MAX_FEATURES, MAX_LOOKUPS = 48, 8
+MAX_FEATURES = 48
 
 
 class GrkFeature(C.Structure):
@@ -35,8 +35,8 @@ class GrkFeature(C.Structure):
 
 class GrkLookup(C.Structure):
     _fields_ = [('idx', C.c_void_p), ('grad', C.c_void_p), ('num_tokens', C.c_int64), ('idx_ld', C.c_int64),
-                ('grad_ld', C.c_int64), ('bag', C.c_int32), ('grad_col', C.c_int32), ('idx_mode', C.c_int32),
-                ('pad_', C.c_int32)]
+                ('grad_ld', C.c_int64), ('row_offset', C.c_int64), ('table_rows', C.c_int64), ('bag', C.c_int32),
+                ('grad_col', C.c_int32), ('idx_mode', C.c_int32), ('pad_', C.c_int32)]
 
 
 class GrkAdamwHparams(C.Structure):
@@ -76,6 +76,10 @@ SIGNATURES = {
     'grk_attention_fwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _P]),
     'grk_attention_bwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64, _P, _I64,
                                _P, _P]),
+    'grk_pair_logits_partials': (_SZ, [_I64]),
+    'grk_pair_logits_fwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _P]),
+    'grk_pair_logits_bwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _I64, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
+                                 _P, _I64, _P, _I64, _P]),
 }
 
 _lib = None

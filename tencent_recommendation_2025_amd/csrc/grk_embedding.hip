@@ -20,9 +20,11 @@ struct FeatArgs {
   grk_feature f[GRK_MAX_FEATURES];
 };
 
+constexpr int kLookupsPerLaunch = 16;
+
 struct LookupArgs {
-  grk_lookup l[GRK_MAX_LOOKUPS];
-  int64_t occ_off[GRK_MAX_LOOKUPS + 1];
+  grk_lookup l[kLookupsPerLaunch];
+  int64_t occ_off[kLookupsPerLaunch + 1];  // occurrence offsets, absolute
   int num;
 };
 
@@ -105,27 +107,31 @@ __global__ void __launch_bounds__(256) k_gather(FeatArgs args, int dim, int64_t 
 }
 
 // -------------------------------------------------------------- backward ----
+// Occurrences [occ_off[0], occ_off[num]) of one launch batch: sort key =
+// group row (sentinel for padding / out-of-range), payload = occurrence id,
+// gsrc[o] = address of the occurrence's gradient row.
 template <typename I>
-__global__ void k_build_keys(LookupArgs la, const int32_t* __restrict__ token_type, int32_t T_len,
+__global__ void k_build_keys(LookupArgs la, int esize, const int32_t* __restrict__ token_type, int32_t T_len,
                              int64_t num_rows, int64_t padding_idx, unsigned* __restrict__ keys,
-                             int* __restrict__ vals, int64_t total, int32_t* err_flag) {
-  int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= total) return;
+                             int* __restrict__ vals, unsigned long long* __restrict__ gsrc, int32_t* err_flag) {
+  const int64_t o = la.occ_off[0] + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= la.occ_off[la.num]) return;
   int l = 0;
   while (l + 1 < la.num && o >= la.occ_off[l + 1]) ++l;
   const grk_lookup& L = la.l[l];
-  int64_t rel = o - la.occ_off[l];
-  int64_t n = rel / L.bag;
-  int a = (int)(rel - n * L.bag);
-  int64_t row = resolve_row(reinterpret_cast<const I*>(L.idx), n, a, L.idx_ld, L.idx_mode, token_type, T_len);
+  const int64_t rel = o - la.occ_off[l];
+  const int64_t n = rel / L.bag;
+  const int a = (int)(rel - n * L.bag);
+  const int64_t row = resolve_row(reinterpret_cast<const I*>(L.idx), n, a, L.idx_ld, L.idx_mode, token_type, T_len);
   unsigned key = (unsigned)num_rows;  // sentinel: sorts after every real row
-  if (row < 0 || row >= num_rows) {
+  if (row < 0 || row >= L.table_rows || L.row_offset + row >= num_rows) {
     if (err_flag) *err_flag = 1;
   } else if (row != padding_idx) {
-    key = (unsigned)row;
+    key = (unsigned)(L.row_offset + row);
   }
   keys[o] = key;
   vals[o] = (int)o;
+  gsrc[o] = (unsigned long long)((const char*)L.grad + (n * L.grad_ld + L.grad_col) * esize);
 }
 
 __global__ void k_mark_heads(const unsigned* __restrict__ keys, int* __restrict__ flags, int64_t n, unsigned sentinel) {
@@ -160,7 +166,8 @@ __global__ void k_segments(const unsigned* __restrict__ keys, const int* __restr
 // columns and adds the occurrence rows strictly in sorted (= occurrence)
 // order in fp32 -- bitwise what the CPU reference does.
 template <typename G>
-__global__ void __launch_bounds__(256) k_segment_reduce(LookupArgs la, int dim, const int* __restrict__ vals,
+__global__ void __launch_bounds__(256) k_segment_reduce(const unsigned long long* __restrict__ gsrc, int dim,
+                                                        const int* __restrict__ vals,
                                                         const int* __restrict__ seg_start,
                                                         const int* __restrict__ seg_end,
                                                         const unsigned* __restrict__ seg_key,
@@ -176,12 +183,7 @@ __global__ void __launch_bounds__(256) k_segment_reduce(LookupArgs la, int dim, 
   const int s = seg_start[u], e = seg_end[u];
   float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
   for (int p = s; p < e; ++p) {
-    const int64_t o = vals[p];
-    int l = 0;
-    while (l + 1 < la.num && o >= la.occ_off[l + 1]) ++l;
-    const grk_lookup& L = la.l[l];
-    const int64_t n = (o - la.occ_off[l]) / L.bag;
-    const G* g = reinterpret_cast<const G*>(L.grad) + n * L.grad_ld + L.grad_col + c;
+    const G* g = reinterpret_cast<const G*>(gsrc[vals[p]]) + c;
     acc0 += Elem<G>::load(g + 0);
     acc1 += Elem<G>::load(g + 1);
     acc2 += Elem<G>::load(g + 2);
@@ -198,6 +200,7 @@ __global__ void __launch_bounds__(256) k_segment_reduce(LookupArgs la, int dim, 
 struct BwdWs {
   unsigned *keys_in, *keys_out, *seg_key;
   int *vals_in, *vals_out, *flags, *pos, *seg_start, *seg_end;
+  unsigned long long* gsrc;
   void* sort_tmp;
   size_t sort_bytes;
   void* scan_tmp;
@@ -223,6 +226,7 @@ static int plan_ws(int64_t n, int64_t num_rows, char* base, BwdWs* ws) {
   ws->pos = (int*)take(n * 4);
   ws->seg_start = (int*)take(n * 4);
   ws->seg_end = (int*)take(n * 4);
+  ws->gsrc = (unsigned long long*)take(n * 8);
   unsigned end_bit = 1;
   while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
   size_t sb = 0, cb = 0;
@@ -310,16 +314,12 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
                                       int32_t* uniq_count, int32_t* row_slot, void* workspace,
                                       size_t workspace_bytes, int32_t* err_flag, void* stream) {
   clear_error();
-  GRK_CHECK_ARG(lookups && num_lookups > 0 && num_lookups <= GRK_MAX_LOOKUPS, "num_lookups must be in [1, %d]",
-                GRK_MAX_LOOKUPS);
+  GRK_CHECK_ARG(lookups && num_lookups > 0, "need at least one lookup");
   GRK_CHECK_ARG(grad_dtype == GRK_F32 || grad_dtype == GRK_BF16, "grad_dtype must be GRK_F32 or GRK_BF16");
   GRK_CHECK_ARG(itype == GRK_I32 || itype == GRK_I64, "bad itype");
   GRK_CHECK_ARG(dim > 0 && dim % 4 == 0 && dim <= 1024, "dim (%d) must be a multiple of 4 and <= 1024", dim);
   GRK_CHECK_ARG(num_rows > 0 && num_rows < 0xFFFFFFFFLL, "num_rows out of range");
   GRK_CHECK_ARG(uniq_count != nullptr, "uniq_count is required");
-  LookupArgs la;
-  memset(&la, 0, sizeof(la));
-  la.num = num_lookups;
   int64_t total = 0;
   for (int i = 0; i < num_lookups; ++i) {
     const grk_lookup& L = lookups[i];
@@ -328,11 +328,12 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
     GRK_CHECK_ARG(L.idx_mode >= 0 && L.idx_mode <= 3, "lookup %d: bad idx_mode", i);
     GRK_CHECK_ARG(L.idx_mode == GRK_IDX_PLAIN || L.idx_mode == GRK_IDX_POSITION || token_type,
                   "lookup %d: masked mode needs token_type", i);
-    la.l[i] = L;
-    la.occ_off[i] = total;
+    GRK_CHECK_ARG(L.row_offset >= 0 && L.table_rows > 0 && L.row_offset + L.table_rows <= num_rows,
+                  "lookup %d: rows [%lld, +%lld) outside the group's %lld rows", i, (long long)L.row_offset,
+                  (long long)L.table_rows, (long long)num_rows);
+    GRK_CHECK_ARG(L.grad_col >= 0 && L.grad_col + dim <= L.grad_ld, "lookup %d: grad_col out of range", i);
     total += L.num_tokens * L.bag;
   }
-  la.occ_off[num_lookups] = total;
   GRK_CHECK_ARG(total < 0x7FFFFFFFLL, "too many occurrences");
   BwdWs ws;
   if (plan_ws(total, num_rows, nullptr, &ws) != GRK_OK) {
@@ -348,14 +349,30 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   if (dense_out) GRK_CHECK_HIP(hipMemsetAsync(dense_out, 0, (size_t)num_rows * dim * sizeof(float), s));
   if (total == 0) return GRK_OK;
   const int B = 256;
+  const int esize = grad_dtype == GRK_F32 ? 4 : 2;
+  int64_t occ = 0;
+  for (int first = 0; first < num_lookups; first += kLookupsPerLaunch) {
+    LookupArgs la;
+    memset(&la, 0, sizeof(la));
+    la.num = num_lookups - first < kLookupsPerLaunch ? num_lookups - first : kLookupsPerLaunch;
+    for (int i = 0; i < la.num; ++i) {
+      la.l[i] = lookups[first + i];
+      la.occ_off[i] = occ;
+      occ += la.l[i].num_tokens * la.l[i].bag;
+    }
+    la.occ_off[la.num] = occ;
+    const int64_t cnt = occ - la.occ_off[0];
+    if (cnt == 0) continue;
+    const unsigned g = (unsigned)((cnt + B - 1) / B);
+    if (itype == GRK_I64)
+      k_build_keys<int64_t><<<g, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
+                                            ws.vals_in, ws.gsrc, err_flag);
+    else
+      k_build_keys<int32_t><<<g, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
+                                            ws.vals_in, ws.gsrc, err_flag);
+    GRK_LAUNCH_CHECK();
+  }
   const int g = (int)((total + B - 1) / B);
-  if (itype == GRK_I64)
-    k_build_keys<int64_t><<<g, B, 0, s>>>(la, token_type, seq_len, num_rows, padding_idx, ws.keys_in, ws.vals_in,
-                                          total, err_flag);
-  else
-    k_build_keys<int32_t><<<g, B, 0, s>>>(la, token_type, seq_len, num_rows, padding_idx, ws.keys_in, ws.vals_in,
-                                          total, err_flag);
-  GRK_LAUNCH_CHECK();
   unsigned end_bit = 1;
   while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
   size_t sb = ws.sort_bytes;
@@ -374,11 +391,11 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   const int block = tpr >= 256 ? tpr : rows_per_block * tpr;
   const int64_t gr = (total + rows_per_block - 1) / rows_per_block;
   if (grad_dtype == GRK_BF16)
-    k_segment_reduce<bf16_t><<<(unsigned)gr, block, 0, s>>>(la, dim, ws.vals_out, ws.seg_start, ws.seg_end,
+    k_segment_reduce<bf16_t><<<(unsigned)gr, block, 0, s>>>(ws.gsrc, dim, ws.vals_out, ws.seg_start, ws.seg_end,
                                                             ws.seg_key, uniq_count, total, dense_out, uniq_rows,
                                                             row_slot);
   else
-    k_segment_reduce<float><<<(unsigned)gr, block, 0, s>>>(la, dim, ws.vals_out, ws.seg_start, ws.seg_end,
+    k_segment_reduce<float><<<(unsigned)gr, block, 0, s>>>(ws.gsrc, dim, ws.vals_out, ws.seg_start, ws.seg_end,
                                                            ws.seg_key, uniq_count, total, dense_out, uniq_rows,
                                                            row_slot);
   GRK_LAUNCH_CHECK();

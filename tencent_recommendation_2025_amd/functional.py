@@ -1,0 +1,261 @@
+"""Autograd functions over the libgrk.so kernels.
+
+These are the device ops under the reference's nn.Module surface
+(tencent_recommendation_2025_amd/model.py).  Every forward/backward runs a
+hand-written HIP kernel from libgrk.so; dense GEMMs, LayerNorm and the
+elementwise glue stay torch ops (hipBLASLt / MIOpen).  No CPU fallback: the
+kernels require device tensors.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib as L
+from . import kernels as K
+
+_disable = torch._dynamo.disable  # ctypes calls: explicit graph breaks under torch.compile
+
+# Debug hook (bench.py): when a list, every fused gather appends its launch arguments.
+GATHER_TRACE = None
+
+
+# --------------------------------------------------------------- lookups ----
+class TableRef:
+    """Where a lookup's rows live: a plain table weight (drop-in: dense
+    autograd gradient) or a row range of a TableGroup (fused optimizer:
+    row-sparse gradient collected by the group's sink)."""
+    __slots__ = ('weight', 'group', 'row_offset')
+
+    def __init__(self, weight, group=None, row_offset=0):
+        self.weight, self.group, self.row_offset = weight, group, row_offset
+
+
+class LookupSpec:
+    __slots__ = ('ref', 'idx', 'out_col', 'mode', 'bag')
+
+    def __init__(self, ref, idx, out_col, mode=L.IDX_PLAIN, bag=1):
+        self.ref, self.idx, self.out_col, self.mode, self.bag = ref, idx, out_col, mode, bag
+
+
+class _FeatureLookupFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, specs, token_type, seq_len, num_tokens, out_ld, extra, extra_col, *weights):
+        dt = specs[0].ref.weight.dtype
+        dev = specs[0].ref.weight.device
+        out = torch.empty(num_tokens, out_ld, dtype=dt, device=dev)
+        lookups = [K.Lookup(s.ref.weight, s.idx, s.out_col, s.mode, s.bag) for s in specs]
+        for i in range(0, len(lookups), L.MAX_FEATURES):
+            K.embedding_gather(lookups[i:i + L.MAX_FEATURES], out, num_tokens, token_type, seq_len)
+        if GATHER_TRACE is not None:
+            GATHER_TRACE.append((lookups, out, num_tokens, token_type, seq_len))
+        if extra is not None:
+            out[:, extra_col:extra_col + extra.shape[1]] = extra.to(dt)
+        ctx.specs, ctx.token_type, ctx.seq_len = specs, token_type, seq_len
+        ctx.extra_info = None if extra is None else (extra_col, extra.shape[1], extra.dtype)
+        ctx.n_weights = len(weights)
+        ctx.weight_ids = [id(w) for w in weights]
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        gout = gout.contiguous()
+        specs = ctx.specs
+        D = specs[0].ref.weight.shape[1]
+        grads = []
+        # drop-in: one deterministic reduction over every distinct table of the call
+        dense = [s for s in specs if s.ref.group is None]
+        if dense and ctx.n_weights:
+            tables, offs, total = {}, {}, 0
+            for s in dense:
+                w = s.ref.weight
+                if id(w) not in tables:
+                    tables[id(w)] = w
+                    offs[id(w)] = total
+                    total += w.shape[0]
+            src = [K.GradSource(s.idx, gout, s.out_col, s.mode, s.bag, offs[id(s.ref.weight)],
+                                s.ref.weight.shape[0]) for s in dense]
+            res = K.embedding_backward(src, total, D, padding_idx=0, token_type=ctx.token_type,
+                                       seq_len=ctx.seq_len, dense=True)
+            by_id = {k: res.dense[offs[k]:offs[k] + w.shape[0]].to(w.dtype) for k, w in tables.items()}
+            grads = [by_id[wid] for wid in ctx.weight_ids]
+        for s in specs:
+            if s.ref.group is not None:
+                s.ref.group.collect(K.GradSource(s.idx, gout, s.out_col, s.mode, s.bag, s.ref.row_offset,
+                                                 s.ref.weight.shape[0]), ctx.token_type, ctx.seq_len)
+        g_extra = None
+        if ctx.extra_info is not None:
+            c, w, dt = ctx.extra_info
+            g_extra = gout[:, c:c + w].to(dt)
+        return (None, None, None, None, None, g_extra, None, *grads)
+
+
+@_disable
+def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extra=None, extra_col=0):
+    """Fused multi-table gather (+ bag sums) into one [num_tokens, out_ld] buffer.
+
+    Drop-in tables get dense gradients through autograd; grouped tables push
+    row-sparse gradient sources into their group's sink."""
+    weights, seen = [], set()
+    for s in specs:
+        if s.ref.group is None and id(s.ref.weight) not in seen and s.ref.weight.requires_grad:
+            seen.add(id(s.ref.weight))
+            weights.append(s.ref.weight)
+    if token_type is not None:
+        token_type = token_type.to(torch.int32).contiguous()
+    return _FeatureLookupFn.apply(specs, token_type, seq_len, num_tokens, out_ld, extra, extra_col, *weights)
+
+
+# ------------------------------------------------------------- attention ----
+class _SoftmaxMHAFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, key_valid, B, T, H, hd, dropout_p, seed, precise):
+        D = H * hd
+        out_dt = qkv.dtype
+        xb = qkv if qkv.dtype == torch.bfloat16 else qkv.to(torch.bfloat16)
+        xb = xb.contiguous()
+        args = K.attn_args(L.ATTN_SOFTMAX, xb[:, :D], xb[:, D:2 * D], xb[:, 2 * D:3 * D], B, T, H, hd,
+                           key_valid=key_valid, dropout_p=dropout_p, seed=seed, precise=precise, out_dtype=out_dt)
+        out = torch.empty(B * T, D, dtype=out_dt, device=qkv.device)
+        lse = torch.empty(B, H, T, dtype=torch.float32, device=qkv.device)
+        K.attention_fwd(args, out, lse)
+        ctx.save_for_backward(xb, out, lse, key_valid)
+        ctx.meta = (B, T, H, hd, dropout_p, seed, precise, out_dt)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        xb, out, lse, key_valid = ctx.saved_tensors
+        B, T, H, hd, dropout_p, seed, precise, out_dt = ctx.meta
+        D = H * hd
+        args = K.attn_args(L.ATTN_SOFTMAX, xb[:, :D], xb[:, D:2 * D], xb[:, 2 * D:3 * D], B, T, H, hd,
+                           key_valid=key_valid, dropout_p=dropout_p, seed=seed, precise=precise, out_dtype=out_dt)
+        dqkv = torch.empty(B * T, 3 * D, dtype=out_dt, device=xb.device)
+        delta = torch.empty(B, H, T, dtype=torch.float32, device=xb.device)
+        gout = gout.contiguous()
+        if gout.dtype not in (torch.float32, torch.bfloat16):
+            gout = gout.float()
+        K.attention_bwd(args, out, gout, lse, delta, dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:])
+        return dqkv, None, None, None, None, None, None, None, None
+
+
+@_disable
+def softmax_mha(qkv, key_valid, B, T, H, hd, dropout_p=0.0, seed=0, precise=None):
+    """Causal + key-padding softmax attention on a packed [B*T, 3D] (q|k|v) tensor."""
+    if precise is None:
+        precise = qkv.dtype == torch.float32
+    return _SoftmaxMHAFn.apply(qkv, key_valid, B, T, H, hd, float(dropout_p), int(seed), bool(precise))
+
+
+class _HSTUCoreFn(torch.autograd.Function):
+    """y = LayerNorm(HSTU-attention(SiLU(pre))) * u, with u|v|q|k = SiLU(pre)."""
+
+    @staticmethod
+    def forward(ctx, pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps, precise):
+        D = H * hd
+        act = F.silu(pre.to(torch.bfloat16)).contiguous()
+        args = K.attn_args(L.ATTN_HSTU, act[:, 2 * D:3 * D], act[:, 3 * D:], act[:, D:2 * D], B, T, H, hd,
+                           key_valid=key_valid, scale=hd ** -0.5, rab=rab.float().contiguous(), inv_n=inv_n,
+                           precise=precise, out_dtype=torch.bfloat16)
+        o = torch.empty(B * T, D, dtype=torch.bfloat16, device=pre.device)
+        K.attention_fwd(args, o)
+        z = F.layer_norm(o.float(), (D,), ln_w.float(), ln_b.float(), eps)
+        y = (z * act[:, :D].float()).to(pre.dtype if pre.dtype != torch.float32 else torch.float32)
+        ctx.save_for_backward(pre, o, rab, ln_w, ln_b, key_valid)
+        ctx.meta = (B, T, H, hd, inv_n, eps, precise)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        pre, o, rab, ln_w, ln_b, key_valid = ctx.saved_tensors
+        B, T, H, hd, inv_n, eps, precise = ctx.meta
+        D = H * hd
+        act = F.silu(pre.to(torch.bfloat16)).contiguous()
+        u = act[:, :D].float()
+        gy = gy.float()
+        with torch.enable_grad():
+            od = o.detach().float().requires_grad_(True)
+            w = ln_w.detach().float().requires_grad_(True)
+            b = ln_b.detach().float().requires_grad_(True)
+            z = F.layer_norm(od, (D,), w, b, eps)
+            do, dw, db = torch.autograd.grad(z, (od, w, b), gy * u)
+        dact = torch.empty(B * T, 4 * D, dtype=torch.bfloat16, device=pre.device)
+        dact[:, :D] = gy * z.detach()
+        rab32 = rab.float().contiguous()
+        drab = torch.zeros_like(rab32)
+        args = K.attn_args(L.ATTN_HSTU, act[:, 2 * D:3 * D], act[:, 3 * D:], act[:, D:2 * D], B, T, H, hd,
+                           key_valid=key_valid, scale=hd ** -0.5, rab=rab32, inv_n=inv_n, precise=precise,
+                           out_dtype=torch.bfloat16)
+        K.attention_bwd(args, None, do.to(torch.bfloat16), None, None, dact[:, 2 * D:3 * D], dact[:, 3 * D:],
+                        dact[:, D:2 * D], drab)
+        p32 = pre.float()
+        sg = torch.sigmoid(p32)
+        dpre = (dact.float() * (sg * (1 + p32 * (1 - sg)))).to(pre.dtype)
+        return (dpre, drab.to(rab.dtype), dw.to(ln_w.dtype), db.to(ln_b.dtype), None, None, None, None, None, None,
+                None, None)
+
+
+@_disable
+def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, precise=False):
+    return _HSTUCoreFn.apply(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, float(inv_n), float(eps), bool(precise))
+
+
+# ---------------------------------------------------------------- logits ----
+def _rows2d(x):
+    x = x.reshape(-1, x.shape[-1])
+    return x if x.stride(-1) == 1 else x.contiguous()
+
+
+class _PairLogitsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, ep, en, ntt):
+        dt = torch.promote_types(torch.promote_types(h.dtype, ep.dtype), en.dtype)
+        h2, p2, n2 = (_rows2d(x.to(dt)) for x in (h, ep, en))
+        pos, neg = K.pair_logits_fwd(h2, p2, n2, ntt)
+        ctx.save_for_backward(h2, p2, n2)
+        ctx.dtypes = (h.dtype, ep.dtype, en.dtype)
+        return pos, neg
+
+    @staticmethod
+    def backward(ctx, gpos, gneg):
+        h2, p2, n2 = ctx.saved_tensors
+        need = ctx.needs_input_grad[:3]
+        dh, dp, dn = K.pair_logits_bwd(h2, p2, n2, gpos=gpos, gneg=gneg, need=need)
+        cast = lambda g, t: None if g is None else g.to(t)
+        return cast(dh, ctx.dtypes[0]), cast(dp, ctx.dtypes[1]), cast(dn, ctx.dtypes[2]), None
+
+
+@_disable
+def pair_logits(h, e_pos, e_neg, next_token_type):
+    """(pos, neg) logits = rowwise <h, e> masked by next_token_type == 1 (fp32, shape of h[..., 0])."""
+    ntt = next_token_type.reshape(-1).to(torch.int32).contiguous()
+    pos, neg = _PairLogitsFn.apply(h, e_pos, e_neg, ntt)
+    shape = h.shape[:-1]
+    return pos.view(shape), neg.view(shape)
+
+
+class _BCELossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, ep, en, ntt):
+        dt = torch.promote_types(torch.promote_types(h.dtype, ep.dtype), en.dtype)
+        h2, p2, n2 = (_rows2d(x.to(dt)) for x in (h, ep, en))
+        pos, neg, loss, count = K.pair_logits_fwd(h2, p2, n2, ntt, with_loss=True)
+        ctx.save_for_backward(h2, p2, n2, pos, neg, ntt, count)
+        ctx.dtypes = (h.dtype, ep.dtype, en.dtype)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        h2, p2, n2, pos, neg, ntt, count = ctx.saved_tensors
+        need = ctx.needs_input_grad[:3]
+        dh, dp, dn = K.pair_logits_bwd(h2, p2, n2, pos_logits=pos, neg_logits=neg, next_token_type=ntt, count=count,
+                                       grad_loss=gloss, need=need)
+        cast = lambda g, t: None if g is None else g.to(t)
+        return cast(dh, ctx.dtypes[0]), cast(dp, ctx.dtypes[1]), cast(dn, ctx.dtypes[2]), None
+
+
+@_disable
+def bce_loss(h, e_pos, e_neg, next_token_type):
+    """Fused logits + the reference BCE loss (main.py:177-182), no host sync."""
+    ntt = next_token_type.reshape(-1).to(torch.int32).contiguous()
+    return _BCELossFn.apply(h, e_pos, e_neg, ntt)

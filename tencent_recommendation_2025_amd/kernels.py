@@ -86,12 +86,17 @@ def embedding_gather(lookups, out, num_tokens, token_type=None, seq_len=0, err_f
 
 @dataclass
 class GradSource:
-    """One lookup's upstream gradient for a table (grk_lookup)."""
+    """One lookup's upstream gradient for a table (grk_lookup).
+
+    ``row_offset``/``table_rows`` place the lookup's table inside a table
+    group (several tables in one flat buffer); -1 rows = the whole group."""
     idx: torch.Tensor
     grad: torch.Tensor      # [N, ld]
     grad_col: int
     mode: int = L.IDX_PLAIN
     bag: int = 1
+    row_offset: int = 0
+    table_rows: int = -1
 
 
 class BackwardResult:
@@ -109,8 +114,6 @@ def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, s
     ``dense`` and ``ids``/``rows``/``count`` (row-sparse form, capacity =
     number of occurrences) when ``sparse``.
     """
-    if len(sources) > L.MAX_LOOKUPS:
-        raise L.GrkError(f'at most {L.MAX_LOOKUPS} gradient sources per table')
     dev = sources[0].grad.device
     gdt = sources[0].grad.dtype
     it = sources[0].idx.dtype
@@ -129,8 +132,9 @@ def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, s
         if s.grad_col + dim > s.grad.shape[1]:
             raise L.GrkError(f'source {i}: grad_col out of range')
         keep.append(idx)
-        lk[i] = L.GrkLookup(idx.data_ptr(), s.grad.data_ptr(), n, s.bag, s.grad.stride(0), s.bag, s.grad_col,
-                            s.mode, 0)
+        rows = num_rows - s.row_offset if s.table_rows < 0 else s.table_rows
+        lk[i] = L.GrkLookup(idx.data_ptr() if n else None, s.grad.data_ptr() if n else None, n, s.bag,
+                            s.grad.stride(0), s.row_offset, rows, s.bag, s.grad_col, s.mode, 0)
         total += n * s.bag
     if token_type is not None:
         token_type = token_type.to(torch.int32).contiguous()
@@ -221,3 +225,52 @@ def attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab=None):
                                    dq.stride(0), dk.data_ptr(), dk.stride(0), dv.data_ptr(), dv.stride(0), _ptr(drab),
                                    L.stream_ptr(dout.device))
     L.check(rc, 'grk_attention_bwd')
+
+
+# -------------------------------------------------------------- pair logits
+def _rows(t, name):
+    if t is None:
+        return None, 0
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise L.GrkError(f'{name} must be a row-major [N, >=D] matrix')
+    return t.data_ptr(), t.stride(0)
+
+
+def pair_logits_fwd(h, e_pos, e_neg, next_token_type=None, with_loss=False):
+    """Returns (pos_logits, neg_logits[, loss, count]) -- grk_pair_logits_fwd."""
+    _require_cuda(h, e_pos, e_neg, next_token_type)
+    N, D = h.shape
+    dev = h.device
+    pos = torch.empty(N, dtype=torch.float32, device=dev)
+    neg = torch.empty(N, dtype=torch.float32, device=dev)
+    loss = count = part = None
+    if with_loss:
+        part = torch.empty(max(L.lib().grk_pair_logits_partials(N), 1), dtype=torch.float32, device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        count = torch.empty(1, dtype=torch.int32, device=dev)
+    ntt = None if next_token_type is None else next_token_type.to(torch.int32).contiguous()
+    (hp, hl), (pp, pl), (np_, nl) = _rows(h, 'h'), _rows(e_pos, 'e_pos'), _rows(e_neg, 'e_neg')
+    rc = L.lib().grk_pair_logits_fwd(hp, hl, pp, pl, np_, nl, _ptr(ntt), N, D, L.dtype_code(h.dtype),
+                                     pos.data_ptr(), neg.data_ptr(), _ptr(part), _ptr(loss), _ptr(count),
+                                     L.stream_ptr(dev))
+    L.check(rc, 'grk_pair_logits_fwd')
+    return (pos, neg, loss, count) if with_loss else (pos, neg)
+
+
+def pair_logits_bwd(h, e_pos, e_neg, gpos=None, gneg=None, pos_logits=None, neg_logits=None, next_token_type=None,
+                    count=None, grad_loss=None, need=(True, True, True)):
+    """Returns (dh, de_pos, de_neg) -- grk_pair_logits_bwd (None where not needed)."""
+    _require_cuda(h, e_pos, e_neg, gpos, gneg, pos_logits, neg_logits, count, grad_loss)
+    N, D = h.shape
+    outs = [torch.empty(N, D, dtype=h.dtype, device=h.device) if n else None for n in need]
+    ntt = None if next_token_type is None else next_token_type.to(torch.int32).contiguous()
+    gpos = None if gpos is None else gpos.float().contiguous()
+    gneg = None if gneg is None else gneg.float().contiguous()
+    gl = None if grad_loss is None else grad_loss.float().reshape(1).contiguous()
+    (hp, hl), (pp, pl), (np_, nl) = _rows(h, 'h'), _rows(e_pos, 'e_pos'), _rows(e_neg, 'e_neg')
+    (a, al), (b, bl), (c, cl) = _rows(outs[0], 'dh'), _rows(outs[1], 'de_pos'), _rows(outs[2], 'de_neg')
+    rc = L.lib().grk_pair_logits_bwd(hp, hl, pp, pl, np_, nl, N, D, L.dtype_code(h.dtype), _ptr(gpos), _ptr(gneg),
+                                     _ptr(pos_logits), _ptr(neg_logits), _ptr(ntt), _ptr(count), _ptr(gl), a, al, b,
+                                     bl, c, cl, L.stream_ptr(h.device))
+    L.check(rc, 'grk_pair_logits_bwd')
+    return tuple(outs)

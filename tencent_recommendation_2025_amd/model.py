@@ -1,0 +1,359 @@
+"""Drop-in ``BaselineModel`` for the TencentGR training script, on the grk HIP path.
+
+Keeps the reference's module surface:
+``BaselineModel(user_num, item_num, feat_statistics, feat_types, args)``,
+``forward(user_item, pos_seqs, neg_seqs, mask, next_mask, next_action_type,
+seq_feature, pos_feature, neg_feature) -> (pos_logits, neg_logits)``,
+``predict``, ``save_item_emb``, the sub-module contract
+``attention_layers[i](q, k, v, attn_mask=[B,T,T]) -> (out, None)`` and every
+state_dict key (``model/BaseLine/model.py:81-433``,
+``model/BaseLineO1/model.py:167-555``).  ``args`` may carry three optional
+fields the reference does not have:
+
+* ``variant``: "baseline" (Conv1d FFN, default) | "o1" (PackedSwiGLUFFN);
+* ``block``:   "softmax" (reference attention, default) | "hstu" (north-star
+  HSTU layer; no FFN, pre-norm residual);
+* ``hstu_num_buckets``: relative-position buckets (default maxlen + 1).
+
+Device work: all table lookups of a feat2emb call are ONE fused gather
+launch (``grk_embedding_gather``) writing the concatenated itemdnn/userdnn
+operands in place; attention is ``grk_attention_*``; logits are
+``grk_pair_logits_*``.  Features may be the reference's lists of dicts (they
+are tensorised on the host, as ``feat2tensor`` does) or dicts of tensors
+(``MyDataset.collate_tensor_fn``).
+"""
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import _lib as L
+from . import functional as G
+from .dataset import MM_SHAPE, save_emb, tensorize
+
+
+class FlashMultiHeadAttention(torch.nn.Module):
+    """Softmax MHA (model/BaseLine/model.py:10-62) on grk_attention_fwd/bwd.
+
+    Q/K/V come from one GEMM with the three weights concatenated at call time
+    (state_dict keys unchanged); the kernel reads the packed [B*T, 3D] result
+    directly, with the mask given as causal + per-key validity instead of a
+    materialised [B,T,T] tensor."""
+
+    def __init__(self, hidden_units, num_heads, dropout_rate):
+        super().__init__()
+        assert hidden_units % num_heads == 0, 'hidden_units must be divisible by num_heads'
+        self.hidden_units, self.num_heads = hidden_units, num_heads
+        self.head_dim = hidden_units // num_heads
+        self.dropout_rate = dropout_rate
+        self.q_linear = torch.nn.Linear(hidden_units, hidden_units)
+        self.k_linear = torch.nn.Linear(hidden_units, hidden_units)
+        self.v_linear = torch.nn.Linear(hidden_units, hidden_units)
+        self.out_linear = torch.nn.Linear(hidden_units, hidden_units)
+
+    def forward(self, query, key, value, attn_mask=None, key_valid=None):
+        B, T, D = query.shape
+        if key_valid is None:
+            key_valid = key_valid_from_mask(attn_mask, B, T)
+        if query is key and key is value:
+            w = torch.cat([self.q_linear.weight, self.k_linear.weight, self.v_linear.weight], 0)
+            b = torch.cat([self.q_linear.bias, self.k_linear.bias, self.v_linear.bias], 0)
+            qkv = F.linear(query, w, b)
+        else:
+            qkv = torch.cat([self.q_linear(query), self.k_linear(key), self.v_linear(value)], -1)
+        p = self.dropout_rate if self.training else 0.0
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+        o = G.softmax_mha(qkv.reshape(B * T, 3 * D), key_valid, B, T, self.num_heads, self.head_dim, p, seed)
+        return self.out_linear(o.view(B, T, D)), None
+
+
+def key_valid_from_mask(attn_mask, B, T):
+    """Recover per-key validity from a log2feats-style mask (tril AND key_valid)
+    and reject any other mask -- the kernels implement exactly that form."""
+    if attn_mask is None:
+        return None
+    kv = attn_mask[:, -1, :]
+    expect = torch.tril(torch.ones(T, T, dtype=torch.bool, device=attn_mask.device)).unsqueeze(0) & kv.unsqueeze(1)
+    if not torch.equal(attn_mask.bool(), expect):
+        raise NotImplementedError('grk attention supports the causal AND key-padding mask of log2feats only')
+    return kv.to(torch.uint8).contiguous()
+
+
+class HSTUAttention(torch.nn.Module):
+    """HSTU layer (north star; no reference -- oracle/hstu.py, oracle/model_ref.RefHSTU):
+
+        u, v, q, k = split(SiLU(uvqk(x)))
+        y = out_linear(dropout(LayerNorm(HSTU-attn(q, k, v, rab)) * u))
+    """
+
+    def __init__(self, hidden_units, num_heads, dropout_rate, num_buckets):
+        super().__init__()
+        assert hidden_units % num_heads == 0, 'hidden_units must be divisible by num_heads'
+        self.hidden_units, self.num_heads = hidden_units, num_heads
+        self.head_dim = hidden_units // num_heads
+        self.dropout_rate = dropout_rate
+        self.uvqk = torch.nn.Linear(hidden_units, 4 * hidden_units)
+        self.rab = torch.nn.Parameter(torch.zeros(num_heads, num_buckets))
+        self.attn_norm = torch.nn.LayerNorm(hidden_units, eps=1e-8)
+        self.out_linear = torch.nn.Linear(hidden_units, hidden_units)
+
+    def forward(self, query, key=None, value=None, attn_mask=None, key_valid=None):
+        B, T, D = query.shape
+        if key_valid is None:
+            key_valid = key_valid_from_mask(attn_mask, B, T)
+        pre = self.uvqk(query).reshape(B * T, 4 * D)
+        y = G.hstu_core(pre, self.rab, self.attn_norm.weight, self.attn_norm.bias, key_valid, B, T,
+                        self.num_heads, self.head_dim, 1.0 / T, self.attn_norm.eps)
+        y = F.dropout(y, self.dropout_rate, self.training)
+        return self.out_linear(y.view(B, T, D)), None
+
+
+class PointWiseFeedForward(torch.nn.Module):
+    """Conv1d(k=1)-ReLU FFN (model/BaseLine/model.py:65-78)."""
+
+    def __init__(self, hidden_units, dropout_rate):
+        super().__init__()
+        self.conv1 = torch.nn.Conv1d(hidden_units, hidden_units, kernel_size=1)
+        self.dropout1 = torch.nn.Dropout(p=dropout_rate)
+        self.relu = torch.nn.ReLU()
+        self.conv2 = torch.nn.Conv1d(hidden_units, hidden_units, kernel_size=1)
+        self.dropout2 = torch.nn.Dropout(p=dropout_rate)
+
+    def forward(self, x):
+        # k=1 convolutions are GEMMs on the [.., D] rows: F.linear, no transposes
+        h = self.dropout1(F.linear(x, self.conv1.weight.squeeze(-1), self.conv1.bias))
+        return self.dropout2(F.linear(self.relu(h), self.conv2.weight.squeeze(-1), self.conv2.bias))
+
+
+class PackedSwiGLUFFN(torch.nn.Module):
+    """SwiGLU FFN (model/BaseLineO1/model.py:103-164)."""
+
+    def __init__(self, dim, hidden_dim=None, multiple_of=256, ffn_dim_multiplier=None, device=None, dtype=None,
+                 dropout_rate=0.0):
+        super().__init__()
+        if hidden_dim is None:
+            hidden_dim = 4 * dim
+        else:
+            hidden_dim = int(2 * hidden_dim / 3)
+        if ffn_dim_multiplier is not None:
+            hidden_dim = int(ffn_dim_multiplier * hidden_dim)
+        hidden_dim = multiple_of * ((hidden_dim + multiple_of - 1) // multiple_of)
+        kw = {'device': device, 'dtype': dtype}
+        self.w13 = torch.nn.Linear(dim, 2 * hidden_dim, bias=False, **kw)
+        self.w2 = torch.nn.Linear(hidden_dim, dim, bias=False, **kw)
+        self.dropout = torch.nn.Dropout(p=dropout_rate) if dropout_rate > 0.0 else None
+
+    def forward(self, x):
+        a, b = torch.chunk(self.w13(x), 2, dim=-1)
+        y = self.w2(F.silu(a) * b)
+        return self.dropout(y) if self.dropout is not None else y
+
+
+class BaselineModel(torch.nn.Module):
+    """Two-tower sequence recommender (model/BaseLine/model.py:81-433)."""
+
+    def __init__(self, user_num, item_num, feat_statistics, feat_types, args):
+        super().__init__()
+        self.user_num, self.item_num = user_num, item_num
+        self.dev = getattr(args, 'device', 'cuda')
+        self.norm_first = getattr(args, 'norm_first', False)
+        self.maxlen = args.maxlen
+        self.variant = getattr(args, 'variant', 'baseline')
+        self.block = getattr(args, 'block', 'softmax')
+        d = args.hidden_units
+        self.hidden_units = d
+        self.item_emb = torch.nn.Embedding(item_num + 1, d, padding_idx=0)
+        self.user_emb = torch.nn.Embedding(user_num + 1, d, padding_idx=0)
+        self.pos_emb = torch.nn.Embedding(2 * args.maxlen + 1, d, padding_idx=0)
+        self.emb_dropout = torch.nn.Dropout(p=args.dropout_rate)
+        self.sparse_emb = torch.nn.ModuleDict()
+        self.emb_transform = torch.nn.ModuleDict()
+        self.attention_layernorms = torch.nn.ModuleList()
+        self.attention_layers = torch.nn.ModuleList()
+        self.forward_layernorms = torch.nn.ModuleList()
+        self.forward_layers = torch.nn.ModuleList()
+        self._init_feat_info(feat_statistics, feat_types)
+        if self.USER_CONTINUAL_FEAT or self.ITEM_CONTINUAL_FEAT:
+            raise NotImplementedError('continual features are not supported (empty in the TencentGR schema)')
+        userdim = d * (len(self.USER_SPARSE_FEAT) + 1 + len(self.USER_ARRAY_FEAT))
+        itemdim = d * (len(self.ITEM_SPARSE_FEAT) + 1 + len(self.ITEM_ARRAY_FEAT)) + d * len(self.ITEM_EMB_FEAT)
+        self.userdnn = torch.nn.Linear(userdim, d)
+        self.itemdnn = torch.nn.Linear(itemdim, d)
+        self.last_layernorm = torch.nn.LayerNorm(d, eps=1e-8)
+        nb = getattr(args, 'hstu_num_buckets', None) or args.maxlen + 1
+        for _ in range(args.num_blocks):
+            self.attention_layernorms.append(torch.nn.LayerNorm(d, eps=1e-8))
+            if self.block == 'hstu':
+                self.attention_layers.append(HSTUAttention(d, args.num_heads, args.dropout_rate, nb))
+                continue
+            self.attention_layers.append(FlashMultiHeadAttention(d, args.num_heads, args.dropout_rate))
+            self.forward_layernorms.append(torch.nn.LayerNorm(d, eps=1e-8))
+            if self.variant == 'o1':
+                self.forward_layers.append(PackedSwiGLUFFN(d, dropout_rate=args.dropout_rate))
+            else:
+                self.forward_layers.append(PointWiseFeedForward(d, args.dropout_rate))
+        for group in (self.USER_SPARSE_FEAT, self.ITEM_SPARSE_FEAT, self.ITEM_ARRAY_FEAT, self.USER_ARRAY_FEAT):
+            for k in group:
+                self.sparse_emb[k] = torch.nn.Embedding(group[k] + 1, d, padding_idx=0)
+        for k in self.ITEM_EMB_FEAT:
+            self.emb_transform[k] = torch.nn.Linear(self.ITEM_EMB_FEAT[k], d)
+        self._table_refs = None  # set by TableStore (fused optimizer mode)
+
+    def _init_feat_info(self, feat_statistics, feat_types):
+        self.USER_SPARSE_FEAT = {k: feat_statistics[k] for k in feat_types['user_sparse']}
+        self.USER_CONTINUAL_FEAT = feat_types['user_continual']
+        self.ITEM_SPARSE_FEAT = {k: feat_statistics[k] for k in feat_types['item_sparse']}
+        self.ITEM_CONTINUAL_FEAT = feat_types['item_continual']
+        self.USER_ARRAY_FEAT = {k: feat_statistics[k] for k in feat_types['user_array']}
+        self.ITEM_ARRAY_FEAT = {k: feat_statistics[k] for k in feat_types['item_array']}
+        self.ITEM_EMB_FEAT = {k: MM_SHAPE[k] for k in feat_types['item_emb']}
+
+    # ------------------------------------------------------------ tables ----
+    def table_modules(self):
+        """name -> nn.Embedding for every table (state_dict prefix order)."""
+        out = {'item_emb': self.item_emb, 'user_emb': self.user_emb, 'pos_emb': self.pos_emb}
+        for k, m in self.sparse_emb.items():
+            out[f'sparse_emb.{k}'] = m
+        return out
+
+    def _ref(self, name):
+        if self._table_refs is not None:
+            return self._table_refs[name]
+        return G.TableRef(self.table_modules()[name].weight)
+
+    def _device(self):
+        return self.item_emb.weight.device
+
+    def _feats(self, feature_array, fids, B, T):
+        """Device tensors for the requested features (tensorising dict lists on the host)."""
+        dev = self._device()
+        if isinstance(feature_array, dict):
+            out = feature_array
+        else:
+            arr = set(self.ITEM_ARRAY_FEAT) | set(self.USER_ARRAY_FEAT)
+            out = tensorize(list(feature_array), fids, arr, set(self.ITEM_EMB_FEAT))
+        res = {}
+        for k in fids:
+            t = out[k]
+            res[k] = t.to(dev, non_blocking=True) if t.device != dev else t
+        return res
+
+    # -------------------------------------------------- model/BaseLine/model.py:226-310
+    def _embed(self, seq, feature_array, mask=None, include_user=False, with_pos=False):
+        dev = self._device()
+        seq = seq.to(dev, non_blocking=True)
+        B, T = seq.shape
+        N = B * T
+        d = self.hidden_units
+        item_f = list(self.ITEM_SPARSE_FEAT) + list(self.ITEM_ARRAY_FEAT)
+        user_f = (list(self.USER_SPARSE_FEAT) + list(self.USER_ARRAY_FEAT)) if include_user else []
+        feats = self._feats(feature_array, item_f + user_f + list(self.ITEM_EMB_FEAT), B, T)
+        tt = mask.to(dev, non_blocking=True) if mask is not None else None
+        specs = []
+        col = 0
+        specs.append(G.LookupSpec(self._ref('item_emb'), seq, col, L.IDX_ITEM_MASK if include_user else L.IDX_PLAIN))
+        col += d
+        for k in item_f:
+            t = feats[k]
+            bag = t.shape[2] if k in self.ITEM_ARRAY_FEAT else 1
+            specs.append(G.LookupSpec(self._ref(f'sparse_emb.{k}'), t, col, L.IDX_PLAIN, bag))
+            col += d
+        extra_col = col
+        extra = None
+        if self.ITEM_EMB_FEAT:
+            extra = torch.cat([self.emb_transform[k](feats[k]) for k in self.ITEM_EMB_FEAT], -1).reshape(N, -1)
+            col += d * len(self.ITEM_EMB_FEAT)
+        item_w = col
+        if include_user:
+            specs.append(G.LookupSpec(self._ref('user_emb'), seq, col, L.IDX_USER_MASK))
+            col += d
+            for k in user_f:
+                t = feats[k]
+                bag = t.shape[2] if k in self.USER_ARRAY_FEAT else 1
+                specs.append(G.LookupSpec(self._ref(f'sparse_emb.{k}'), t, col, L.IDX_PLAIN, bag))
+                col += d
+        user_end = col
+        if with_pos:
+            specs.append(G.LookupSpec(self._ref('pos_emb'), seq, col, L.IDX_POSITION))
+            col += d
+        buf = G.feature_lookup(specs, N, col, tt, T, extra, extra_col)
+        x = torch.relu(self.itemdnn(buf[:, :item_w]))
+        if include_user:
+            x = x + torch.relu(self.userdnn(buf[:, item_w:user_end]))
+        pos_rows = buf[:, user_end:user_end + d] if with_pos else None
+        return x.view(B, T, d), pos_rows
+
+    def feat2emb(self, seq, feature_array, mask=None, include_user=False):
+        return self._embed(seq, feature_array, mask, include_user)[0]
+
+    # -------------------------------------------------- model/BaseLine/model.py:312-350
+    def log2feats(self, log_seqs, mask, seq_feature):
+        dev = self._device()
+        B, T = log_seqs.shape
+        seqs, pos_rows = self._embed(log_seqs, seq_feature, mask=mask, include_user=True, with_pos=True)
+        seqs = seqs * self.item_emb.embedding_dim ** 0.5 + pos_rows.view(B, T, -1)
+        seqs = self.emb_dropout(seqs)
+        key_valid = (mask.to(dev, non_blocking=True) != 0).to(torch.uint8).contiguous()
+        for i in range(len(self.attention_layers)):
+            if self.block == 'hstu':
+                y, _ = self.attention_layers[i](self.attention_layernorms[i](seqs), key_valid=key_valid)
+                seqs = seqs + y
+            elif self.norm_first:
+                x = self.attention_layernorms[i](seqs)
+                seqs = seqs + self.attention_layers[i](x, x, x, key_valid=key_valid)[0]
+                seqs = seqs + self.forward_layers[i](self.forward_layernorms[i](seqs))
+            else:
+                y, _ = self.attention_layers[i](seqs, seqs, seqs, key_valid=key_valid)
+                seqs = self.attention_layernorms[i](seqs + y)
+                seqs = self.forward_layernorms[i](seqs + self.forward_layers[i](seqs))
+        return self.last_layernorm(seqs)
+
+    # -------------------------------------------------- model/BaseLine/model.py:352-384
+    def forward(self, user_item, pos_seqs, neg_seqs, mask, next_mask, next_action_type, seq_feature, pos_feature,
+                neg_feature):
+        log_feats = self.log2feats(user_item, mask, seq_feature)
+        pos_embs = self.feat2emb(pos_seqs, pos_feature, include_user=False)
+        neg_embs = self.feat2emb(neg_seqs, neg_feature, include_user=False)
+        return G.pair_logits(log_feats, pos_embs, neg_embs, next_mask.to(self._device(), non_blocking=True))
+
+    def encode(self, user_item, pos_seqs, neg_seqs, mask, seq_feature, pos_feature, neg_feature):
+        """(log_feats, pos_embs, neg_embs) -- the operands of the loss."""
+        return (self.log2feats(user_item, mask, seq_feature),
+                self.feat2emb(pos_seqs, pos_feature, include_user=False),
+                self.feat2emb(neg_seqs, neg_feature, include_user=False))
+
+    def predict(self, log_seqs, seq_feature, mask):
+        return self.log2feats(log_seqs, mask, seq_feature)[:, -1, :]
+
+    def save_item_emb(self, item_ids, retrieval_ids, feat_dict, save_path, batch_size=1024):
+        """Candidate item embeddings -> embedding.fbin / id.u64bin (model/BaseLine/model.py:402-433)."""
+        embs = []
+        for s in range(0, len(item_ids), batch_size):
+            e = min(s + batch_size, len(item_ids))
+            seq = torch.tensor(item_ids[s:e], device=self._device()).unsqueeze(0)
+            feats = [np.array([feat_dict[i] for i in range(s, e)], dtype=object)]
+            embs.append(self.feat2emb(seq, feats, include_user=False).squeeze(0).detach().float().cpu().numpy())
+        save_emb(np.concatenate(embs, 0), Path(save_path, 'embedding.fbin'))
+        save_emb(np.array(retrieval_ids, dtype=np.uint64).reshape(-1, 1), Path(save_path, 'id.u64bin'))
+
+
+def init_reference_(model, seed=None):
+    """Parameter init of the training script (model/BaseLine/main.py:95-111):
+    xavier_normal_ for dim >= 2, zeros for 1-D, padding rows of every table zeroed."""
+    g = None
+    if seed is not None:
+        g = torch.Generator(device=model.item_emb.weight.device).manual_seed(seed)
+    with torch.no_grad():
+        for _, p in model.named_parameters():
+            if p.dim() >= 2:
+                fan_in, fan_out = torch.nn.init._calculate_fan_in_and_fan_out(p)
+                std = (2.0 / float(fan_in + fan_out)) ** 0.5
+                p.normal_(0.0, std, generator=g)
+            elif p.dim() == 1:
+                p.zero_()
+        for t in model.table_modules().values():
+            t.weight[0].zero_()
+    return model
