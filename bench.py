@@ -149,7 +149,7 @@ def main():
                         block=a.block)
     torch.manual_seed(0)
     model = BaselineModel(a.users, a.items, stats, types, margs).to(dev)
-    init_reference_(model, seed=0)
+    init_reference_(model, seed=0, live_norms=True)
     if world > 1:
         from tencent_recommendation_2025_amd.sharding import ShardedFusedAdamW
         opt = ShardedFusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)

@@ -206,6 +206,11 @@ def _rows2d(x):
     return x if x.stride(-1) == 1 else x.contiguous()
 
 
+def _shape_grads(ctx, *gs):
+    out = [None if g is None else g.view(shape).to(dt) for g, shape, dt in zip(gs, ctx.shapes, ctx.dtypes)]
+    return (*out, None)
+
+
 class _PairLogitsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, ep, en, ntt):
@@ -214,15 +219,15 @@ class _PairLogitsFn(torch.autograd.Function):
         pos, neg = K.pair_logits_fwd(h2, p2, n2, ntt)
         ctx.save_for_backward(h2, p2, n2)
         ctx.dtypes = (h.dtype, ep.dtype, en.dtype)
+        ctx.shapes = (h.shape, ep.shape, en.shape)
         return pos, neg
 
     @staticmethod
     def backward(ctx, gpos, gneg):
         h2, p2, n2 = ctx.saved_tensors
         need = ctx.needs_input_grad[:3]
-        dh, dp, dn = K.pair_logits_bwd(h2, p2, n2, gpos=gpos, gneg=gneg, need=need)
-        cast = lambda g, t: None if g is None else g.to(t)
-        return cast(dh, ctx.dtypes[0]), cast(dp, ctx.dtypes[1]), cast(dn, ctx.dtypes[2]), None
+        dh, dp, dn = K.pair_logits_bwd(h2, p2, n2, gpos=gpos.contiguous(), gneg=gneg.contiguous(), need=need)
+        return _shape_grads(ctx, dh, dp, dn)
 
 
 @_disable
@@ -242,6 +247,7 @@ class _BCELossFn(torch.autograd.Function):
         pos, neg, loss, count = K.pair_logits_fwd(h2, p2, n2, ntt, with_loss=True)
         ctx.save_for_backward(h2, p2, n2, pos, neg, ntt, count)
         ctx.dtypes = (h.dtype, ep.dtype, en.dtype)
+        ctx.shapes = (h.shape, ep.shape, en.shape)
         return loss
 
     @staticmethod
@@ -250,8 +256,7 @@ class _BCELossFn(torch.autograd.Function):
         need = ctx.needs_input_grad[:3]
         dh, dp, dn = K.pair_logits_bwd(h2, p2, n2, pos_logits=pos, neg_logits=neg, next_token_type=ntt, count=count,
                                        grad_loss=gloss, need=need)
-        cast = lambda g, t: None if g is None else g.to(t)
-        return cast(dh, ctx.dtypes[0]), cast(dp, ctx.dtypes[1]), cast(dn, ctx.dtypes[2]), None
+        return _shape_grads(ctx, dh, dp, dn)
 
 
 @_disable

@@ -238,13 +238,14 @@ class BaselineModel(torch.nn.Module):
         res = {}
         for k in fids:
             t = out[k]
-            res[k] = t.to(dev, non_blocking=True) if t.device != dev else t
+            t = t.to(dev, non_blocking=True) if t.device != dev else t
+            res[k] = t if (t.is_floating_point() or t.dtype == torch.int64) else t.long()
         return res
 
     # -------------------------------------------------- model/BaseLine/model.py:226-310
     def _embed(self, seq, feature_array, mask=None, include_user=False, with_pos=False):
         dev = self._device()
-        seq = seq.to(dev, non_blocking=True)
+        seq = seq.to(dev, non_blocking=True).long()
         B, T = seq.shape
         N = B * T
         d = self.hidden_units
@@ -340,9 +341,12 @@ class BaselineModel(torch.nn.Module):
         save_emb(np.array(retrieval_ids, dtype=np.uint64).reshape(-1, 1), Path(save_path, 'id.u64bin'))
 
 
-def init_reference_(model, seed=None):
+def init_reference_(model, seed=None, live_norms=False):
     """Parameter init of the training script (model/BaseLine/main.py:95-111):
-    xavier_normal_ for dim >= 2, zeros for 1-D, padding rows of every table zeroed."""
+    xavier_normal_ for dim >= 2, zeros for 1-D, padding rows of every table zeroed.
+
+    The reference's rule also zeroes every LayerNorm gamma, which makes the
+    first steps' logits exactly 0; ``live_norms=True`` keeps gamma = 1."""
     g = None
     if seed is not None:
         g = torch.Generator(device=model.item_emb.weight.device).manual_seed(seed)
@@ -356,4 +360,8 @@ def init_reference_(model, seed=None):
                 p.zero_()
         for t in model.table_modules().values():
             t.weight[0].zero_()
+        if live_norms:
+            for mm in model.modules():
+                if isinstance(mm, torch.nn.LayerNorm):
+                    mm.weight.fill_(1.0)
     return model

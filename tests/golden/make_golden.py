@@ -122,10 +122,26 @@ def main():
     # the directory generator is deterministic: tests regenerate it with the same seed.
 
     # ---------------- full training step (BaseLine and O1) --------------------
+    # The reference init zeroes every 1-D parameter, LayerNorm gamma included
+    # (main.py:100-102), which makes the first step's logits and table grads
+    # exactly zero.  The "_live" fixtures apply the same init and then set
+    # gamma = 1 and small random biases so that every gradient is non-zero.
+    runs = []
     for tag, mod, wd, l2 in (('baseline', base_mod, 0.01, args.l2_emb), ('o1', o1_mod, args.l2_emb, 0.0)):
+        runs += [(tag, mod, wd, l2, False), (tag + '_live', mod, wd, l2, True)]
+    for tag, mod, wd, l2, live in runs:
         torch.manual_seed(0)
         m = mod.BaselineModel(dset.usernum, dset.itemnum, dset.feat_statistics, ft, args)
         ref_init(m)
+        if live:
+            gl = torch.Generator().manual_seed(7)
+            with torch.no_grad():
+                for mm in m.modules():
+                    if isinstance(mm, torch.nn.LayerNorm):
+                        mm.weight.fill_(1.0)
+                for _, p in m.named_parameters():
+                    if p.dim() == 1 and not torch.all(p == 1.0):
+                        p.copy_(torch.randn(p.shape, generator=gl) * 0.05)
         before = {k: v.detach().clone().numpy() for k, v in m.state_dict().items()}
         opt = torch.optim.AdamW(m.parameters(), lr=args.lr, betas=(0.9, 0.98), weight_decay=wd)
         m.train()
