@@ -98,15 +98,16 @@ typedef struct grk_lookup {
 } grk_lookup;
 
 /* Workspace bytes for grk_embedding_backward with `num_occurrences` =
- * sum over lookups of num_tokens * bag. */
-size_t grk_embedding_backward_workspace(int64_t num_occurrences, int64_t num_rows); /* 0 = query failed */
+ * sum over lookups of num_tokens * bag (0 = query failed). */
+size_t grk_embedding_backward_workspace(int64_t num_occurrences, int64_t num_rows, int dim);
 
 /* Deterministic scatter-add gradient of one table, replacing autograd's
  * embedding_dense_backward.  Occurrences (lookup order,
- * then token, then bag slot) are stably sorted by row id and each row is
- * summed sequentially in fp32 in occurrence order: bit-identical to the
- * reference CPU backward for a single lookup.  Rows == padding_idx are
- * skipped (padding_idx < 0: none).
+ * then token, then bag slot) are stably sorted by row id and reduced in fp32
+ * by a load-balanced segmented reduction: every row with <= 512 occurrences
+ * is summed sequentially in occurrence order (bit-identical to the reference
+ * CPU backward for a single lookup); hotter rows use a fixed blocked order
+ * (deterministic).  Rows == padding_idx are skipped (padding_idx < 0: none).
  *
  * Outputs (any may be NULL):
  *   dense_out  [num_rows, dim] fp32: zero-filled then written (drop-in mode)

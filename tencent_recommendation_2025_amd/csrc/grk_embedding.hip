@@ -108,12 +108,13 @@ __global__ void __launch_bounds__(256) k_gather(FeatArgs args, int dim, int64_t 
 
 // -------------------------------------------------------------- backward ----
 // Occurrences [occ_off[0], occ_off[num]) of one launch batch: sort key =
-// group row (sentinel for padding / out-of-range), payload = occurrence id,
-// gsrc[o] = address of the occurrence's gradient row.
+// group row (sentinel for padding / out-of-range), payload = address of the
+// occurrence's gradient row.  The radix sort is stable, so after sorting the
+// payloads of one key are in occurrence order.
 template <typename I>
 __global__ void k_build_keys(LookupArgs la, int esize, const int32_t* __restrict__ token_type, int32_t T_len,
                              int64_t num_rows, int64_t padding_idx, unsigned* __restrict__ keys,
-                             int* __restrict__ vals, unsigned long long* __restrict__ gsrc, int32_t* err_flag) {
+                             unsigned long long* __restrict__ gptr, int32_t* err_flag) {
   const int64_t o = la.occ_off[0] + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= la.occ_off[la.num]) return;
   int l = 0;
@@ -130,8 +131,7 @@ __global__ void k_build_keys(LookupArgs la, int esize, const int32_t* __restrict
     key = (unsigned)(L.row_offset + row);
   }
   keys[o] = key;
-  vals[o] = (int)o;
-  gsrc[o] = (unsigned long long)((const char*)L.grad + (n * L.grad_ld + L.grad_col) * esize);
+  gptr[o] = (unsigned long long)((const char*)L.grad + (n * L.grad_ld + L.grad_col) * esize);
 }
 
 __global__ void k_mark_heads(const unsigned* __restrict__ keys, int* __restrict__ flags, int64_t n, unsigned sentinel) {
@@ -162,45 +162,187 @@ __global__ void k_segments(const unsigned* __restrict__ keys, const int* __restr
   }
 }
 
-// One group of dim/4 lanes per unique row; each lane owns 4 consecutive
-// columns and adds the occurrence rows strictly in sorted (= occurrence)
-// order in fp32 -- bitwise what the CPU reference does.
+// ------------------------------------------------- segmented reduction ----
+// The sorted occurrence list is cut into fixed chunks of kRedChunk entries,
+// one row group (dim/VEC lanes, VEC = one 16-byte vector of grads) per chunk,
+// so hot rows (a cardinality-10 feature table gets thousands of occurrences
+// per row) are spread over many row groups instead of serialising one.
+//   * a row whose occurrences all fall in one chunk is summed strictly in
+//     occurrence order and written directly (bit-exact with the CPU order);
+//   * a row crossing a chunk boundary with <= 2*kRedChunk occurrences is
+//     re-summed sequentially by k_seg_combine (still bit-exact);
+//   * longer rows are summed per chunk into partial slots (A: the chunk's
+//     first piece, B: its last piece when that continues past the chunk) and
+//     k_seg_combine adds the partials in chunk order -- deterministic, a
+//     fixed blocked summation order.
+constexpr int kRedChunk = 256;
+constexpr int kRedPipe = 8;  // occurrence rows loaded ahead of the in-order adds
+
 template <typename G>
-__global__ void __launch_bounds__(256) k_segment_reduce(const unsigned long long* __restrict__ gsrc, int dim,
-                                                        const int* __restrict__ vals,
-                                                        const int* __restrict__ seg_start,
-                                                        const int* __restrict__ seg_end,
-                                                        const unsigned* __restrict__ seg_key,
-                                                        const int32_t* __restrict__ count, int64_t max_rows,
-                                                        float* __restrict__ dense_out,
-                                                        float* __restrict__ uniq_rows,
-                                                        int32_t* __restrict__ row_slot) {
-  const int tpr = dim / 4;
-  const int rows_per_block = blockDim.x / tpr;
-  const int64_t u = (int64_t)blockIdx.x * rows_per_block + threadIdx.x / tpr;
-  const int c = (threadIdx.x % tpr) * 4;
-  if ((int)(threadIdx.x / tpr) >= rows_per_block || u >= max_rows || u >= *count) return;
-  const int s = seg_start[u], e = seg_end[u];
-  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-  for (int p = s; p < e; ++p) {
-    const G* g = reinterpret_cast<const G*>(gsrc[vals[p]]) + c;
-    acc0 += Elem<G>::load(g + 0);
-    acc1 += Elem<G>::load(g + 1);
-    acc2 += Elem<G>::load(g + 2);
-    acc3 += Elem<G>::load(g + 3);
+struct RowVec {
+  static constexpr int VEC = 16 / sizeof(G);
+  float v[VEC];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) v[e] = 0.f;
   }
-  const unsigned key = seg_key[u];
-  float4 r = make_float4(acc0, acc1, acc2, acc3);
-  if (dense_out) *reinterpret_cast<float4*>(dense_out + (int64_t)key * dim + c) = r;
-  if (uniq_rows) *reinterpret_cast<float4*>(uniq_rows + u * dim + c) = r;
+};
+
+template <typename G>
+__device__ __forceinline__ void load_row(Vec16<G>& r, unsigned long long ptr, int c) {
+  r.load(reinterpret_cast<const G*>(ptr) + c);
+}
+
+template <typename G>
+__device__ __forceinline__ void store_final(const RowVec<G>& acc, unsigned key, int64_t u, int dim, int c,
+                                            float* dense_out, float* uniq_rows, int32_t* row_slot) {
+  constexpr int VEC = RowVec<G>::VEC;
+#pragma unroll
+  for (int e = 0; e < VEC; e += 4) {
+    float4 r = make_float4(acc.v[e], acc.v[e + 1], acc.v[e + 2], acc.v[e + 3]);
+    if (dense_out) *reinterpret_cast<float4*>(dense_out + (int64_t)key * dim + c + e) = r;
+    if (uniq_rows) *reinterpret_cast<float4*>(uniq_rows + u * dim + c + e) = r;
+  }
   if (row_slot && c == 0) row_slot[key] = (int32_t)u;
+}
+
+template <typename G>
+__device__ __forceinline__ void store_slot(const RowVec<G>& acc, float* slot, int dim, int c) {
+  constexpr int VEC = RowVec<G>::VEC;
+#pragma unroll
+  for (int e = 0; e < VEC; e += 4)
+    *reinterpret_cast<float4*>(slot + c + e) = make_float4(acc.v[e], acc.v[e + 1], acc.v[e + 2], acc.v[e + 3]);
+}
+
+// Sequential in-order sum of the sorted occurrences [s, e) with kRedPipe rows in flight.
+template <typename G>
+__device__ __forceinline__ void seq_sum(RowVec<G>& acc, const unsigned long long* __restrict__ gptr, int s, int e,
+                                        int c) {
+  constexpr int VEC = RowVec<G>::VEC;
+  for (int p = s; p < e; p += kRedPipe) {
+    Vec16<G> r[kRedPipe];
+#pragma unroll
+    for (int j = 0; j < kRedPipe; ++j)
+      if (p + j < e) load_row<G>(r[j], gptr[p + j], c);
+#pragma unroll
+    for (int j = 0; j < kRedPipe; ++j)
+      if (p + j < e)
+#pragma unroll
+        for (int x = 0; x < VEC; ++x) acc.v[x] += r[j].get(x);
+  }
+}
+
+template <typename G>
+__global__ void __launch_bounds__(256) k_seg_chunks(const unsigned* __restrict__ keys,
+                                                    const unsigned long long* __restrict__ gptr,
+                                                    const int* __restrict__ pos, const int* __restrict__ seg_start,
+                                                    const int* __restrict__ seg_end, int64_t n, unsigned sentinel,
+                                                    int dim, float* __restrict__ slotA, float* __restrict__ slotB,
+                                                    float* __restrict__ dense_out, float* __restrict__ uniq_rows,
+                                                    int32_t* __restrict__ row_slot) {
+  constexpr int VEC = RowVec<G>::VEC;
+  const int tpr = dim / VEC;
+  const int groups = blockDim.x / tpr;
+  const int64_t chunk = (int64_t)blockIdx.x * groups + threadIdx.x / tpr;
+  const int c = (threadIdx.x % tpr) * VEC;
+  const int64_t p0 = chunk * kRedChunk;
+  if ((int)(threadIdx.x / tpr) >= groups || p0 >= n) return;
+  const int64_t p1 = min(n, p0 + kRedChunk);
+  RowVec<G> acc;
+  acc.zero();
+  int64_t ps = p0;                 // start of the current piece
+  unsigned cur = keys[p0];
+  if (cur == sentinel) return;
+  auto flush = [&](int64_t pe) {   // piece [ps, pe) of key cur
+    const int u = pos[ps] - 1;
+    const int su = seg_start[u], eu = seg_end[u];
+    if (su >= p0 && eu <= p1) {
+      store_final<G>(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
+    } else if (eu - su > 2 * kRedChunk) {
+      store_slot<G>(acc, (ps == p0 ? slotA : slotB) + chunk * dim, dim, c);
+    }  // else: short row crossing a boundary -- k_seg_combine sums it sequentially
+  };
+  for (int64_t p = p0; p < p1; p += kRedPipe) {
+    Vec16<G> r[kRedPipe];
+    unsigned k[kRedPipe];
+#pragma unroll
+    for (int j = 0; j < kRedPipe; ++j) {
+      k[j] = p + j < p1 ? keys[p + j] : sentinel;
+      if (k[j] != sentinel) load_row<G>(r[j], gptr[p + j], c);
+    }
+#pragma unroll
+    for (int j = 0; j < kRedPipe; ++j) {
+      if (k[j] == sentinel) continue;
+      if (k[j] != cur) {
+        flush(p + j);
+        acc.zero();
+        cur = k[j];
+        ps = p + j;
+      }
+#pragma unroll
+      for (int x = 0; x < VEC; ++x) acc.v[x] += r[j].get(x);
+    }
+    if (k[kRedPipe - 1] == sentinel && p + kRedPipe <= p1) {  // reached the padding tail
+      flush(p + kRedPipe);
+      return;
+    }
+  }
+  flush(p1);
+}
+
+template <typename G>
+__global__ void __launch_bounds__(256) k_seg_combine(const unsigned long long* __restrict__ gptr,
+                                                     const int* __restrict__ seg_start,
+                                                     const int* __restrict__ seg_end,
+                                                     const unsigned* __restrict__ seg_key,
+                                                     const int32_t* __restrict__ count, int64_t max_rows, int dim,
+                                                     const float* __restrict__ slotA, const float* __restrict__ slotB,
+                                                     float* __restrict__ dense_out, float* __restrict__ uniq_rows,
+                                                     int32_t* __restrict__ row_slot) {
+  constexpr int VEC = RowVec<G>::VEC;
+  const int tpr = dim / VEC;
+  const int groups = blockDim.x / tpr;
+  const int64_t u = (int64_t)blockIdx.x * groups + threadIdx.x / tpr;
+  const int c = (threadIdx.x % tpr) * VEC;
+  if ((int)(threadIdx.x / tpr) >= groups || u >= max_rows || u >= *count) return;
+  const int su = seg_start[u], eu = seg_end[u];
+  const int cs = su / kRedChunk, ce = (eu - 1) / kRedChunk;
+  if (cs == ce) return;  // written by k_seg_chunks
+  RowVec<G> acc;
+  acc.zero();
+  if (eu - su <= 2 * kRedChunk) {
+    seq_sum<G>(acc, gptr, su, eu, c);
+  } else {
+    const float* first = ((su % kRedChunk) == 0 ? slotA : slotB) + (int64_t)cs * dim + c;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc.v[e] = first[e];
+    for (int ch = cs + 1; ch <= ce; ch += kRedPipe) {
+      float4 r[kRedPipe][VEC / 4];
+#pragma unroll
+      for (int j = 0; j < kRedPipe; ++j)
+        if (ch + j <= ce)
+#pragma unroll
+          for (int e = 0; e < VEC / 4; ++e)
+            r[j][e] = *reinterpret_cast<const float4*>(slotA + (int64_t)(ch + j) * dim + c + 4 * e);
+#pragma unroll
+      for (int j = 0; j < kRedPipe; ++j)
+        if (ch + j <= ce)
+#pragma unroll
+          for (int e = 0; e < VEC / 4; ++e) {
+            acc.v[4 * e] += r[j][e].x; acc.v[4 * e + 1] += r[j][e].y;
+            acc.v[4 * e + 2] += r[j][e].z; acc.v[4 * e + 3] += r[j][e].w;
+          }
+    }
+  }
+  store_final<G>(acc, seg_key[u], u, dim, c, dense_out, uniq_rows, row_slot);
 }
 
 // ------------------------------------------------------------ workspace ----
 struct BwdWs {
   unsigned *keys_in, *keys_out, *seg_key;
-  int *vals_in, *vals_out, *flags, *pos, *seg_start, *seg_end;
-  unsigned long long* gsrc;
+  int *flags, *pos, *seg_start, *seg_end;
+  unsigned long long *gptr_in, *gptr_out;
+  float *slotA, *slotB;
   void* sort_tmp;
   size_t sort_bytes;
   void* scan_tmp;
@@ -210,7 +352,7 @@ struct BwdWs {
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static int plan_ws(int64_t n, int64_t num_rows, char* base, BwdWs* ws) {
+static int plan_ws(int64_t n, int64_t num_rows, int dim, char* base, BwdWs* ws) {
   size_t off = 0;
   auto take = [&](size_t bytes) -> char* {
     char* p = base ? base + off : nullptr;
@@ -220,19 +362,22 @@ static int plan_ws(int64_t n, int64_t num_rows, char* base, BwdWs* ws) {
   ws->keys_in = (unsigned*)take(n * 4);
   ws->keys_out = (unsigned*)take(n * 4);
   ws->seg_key = (unsigned*)take(n * 4);
-  ws->vals_in = (int*)take(n * 4);
-  ws->vals_out = (int*)take(n * 4);
   ws->flags = (int*)take(n * 4);
   ws->pos = (int*)take(n * 4);
   ws->seg_start = (int*)take(n * 4);
   ws->seg_end = (int*)take(n * 4);
-  ws->gsrc = (unsigned long long*)take(n * 8);
+  ws->gptr_in = (unsigned long long*)take(n * 8);
+  ws->gptr_out = (unsigned long long*)take(n * 8);
+  const int64_t chunks = (n + kRedChunk - 1) / kRedChunk;
+  ws->slotA = (float*)take((size_t)chunks * dim * 4);
+  ws->slotB = (float*)take((size_t)chunks * dim * 4);
   unsigned end_bit = 1;
   while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
   size_t sb = 0, cb = 0;
   if (n > 0) {
-    if (rocprim::radix_sort_pairs(nullptr, sb, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
-                                  (int*)nullptr, (size_t)n, 0, end_bit) != hipSuccess)
+    if (rocprim::radix_sort_pairs(nullptr, sb, (unsigned*)nullptr, (unsigned*)nullptr,
+                                  (unsigned long long*)nullptr, (unsigned long long*)nullptr, (size_t)n, 0,
+                                  end_bit) != hipSuccess)
       return GRK_EHIP;
     if (rocprim::inclusive_scan(nullptr, cb, (int*)nullptr, (int*)nullptr, (size_t)n, rocprim::plus<int>()) !=
         hipSuccess)
@@ -302,9 +447,9 @@ extern "C" int grk_embedding_gather(const grk_feature* features, int num_feature
   return GRK_OK;
 }
 
-extern "C" size_t grk_embedding_backward_workspace(int64_t num_occurrences, int64_t num_rows) {
+extern "C" size_t grk_embedding_backward_workspace(int64_t num_occurrences, int64_t num_rows, int dim) {
   BwdWs ws;
-  if (plan_ws(num_occurrences, num_rows, nullptr, &ws) != GRK_OK) return 0;
+  if (plan_ws(num_occurrences, num_rows, dim, nullptr, &ws) != GRK_OK) return 0;
   return ws.total + 256;
 }
 
@@ -317,7 +462,9 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   GRK_CHECK_ARG(lookups && num_lookups > 0, "need at least one lookup");
   GRK_CHECK_ARG(grad_dtype == GRK_F32 || grad_dtype == GRK_BF16, "grad_dtype must be GRK_F32 or GRK_BF16");
   GRK_CHECK_ARG(itype == GRK_I32 || itype == GRK_I64, "bad itype");
-  GRK_CHECK_ARG(dim > 0 && dim % 4 == 0 && dim <= 1024, "dim (%d) must be a multiple of 4 and <= 1024", dim);
+  const int vec_req = grad_dtype == GRK_BF16 ? 8 : 4;
+  GRK_CHECK_ARG(dim > 0 && dim % vec_req == 0 && dim / vec_req <= 256, "dim (%d) must be a multiple of %d and <= %d",
+                dim, vec_req, 256 * vec_req);
   GRK_CHECK_ARG(num_rows > 0 && num_rows < 0xFFFFFFFFLL, "num_rows out of range");
   GRK_CHECK_ARG(uniq_count != nullptr, "uniq_count is required");
   int64_t total = 0;
@@ -336,14 +483,14 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   }
   GRK_CHECK_ARG(total < 0x7FFFFFFFLL, "too many occurrences");
   BwdWs ws;
-  if (plan_ws(total, num_rows, nullptr, &ws) != GRK_OK) {
+  if (plan_ws(total, num_rows, dim, nullptr, &ws) != GRK_OK) {
     set_error("rocprim workspace query failed");
     return GRK_EHIP;
   }
   GRK_CHECK_ARG(workspace_bytes >= ws.total + 256 && workspace, "workspace too small (%zu < %zu)", workspace_bytes,
                 ws.total + 256);
   char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
-  plan_ws(total, num_rows, base, &ws);
+  plan_ws(total, num_rows, dim, base, &ws);
   hipStream_t s = (hipStream_t)stream;
   GRK_CHECK_HIP(hipMemsetAsync(uniq_count, 0, sizeof(int32_t), s));
   if (dense_out) GRK_CHECK_HIP(hipMemsetAsync(dense_out, 0, (size_t)num_rows * dim * sizeof(float), s));
@@ -366,17 +513,17 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
     const unsigned g = (unsigned)((cnt + B - 1) / B);
     if (itype == GRK_I64)
       k_build_keys<int64_t><<<g, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
-                                            ws.vals_in, ws.gsrc, err_flag);
+                                            ws.gptr_in, err_flag);
     else
       k_build_keys<int32_t><<<g, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
-                                            ws.vals_in, ws.gsrc, err_flag);
+                                            ws.gptr_in, err_flag);
     GRK_LAUNCH_CHECK();
   }
   const int g = (int)((total + B - 1) / B);
   unsigned end_bit = 1;
   while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
   size_t sb = ws.sort_bytes;
-  GRK_CHECK_HIP(rocprim::radix_sort_pairs(ws.sort_tmp, sb, ws.keys_in, ws.keys_out, ws.vals_in, ws.vals_out,
+  GRK_CHECK_HIP(rocprim::radix_sort_pairs(ws.sort_tmp, sb, ws.keys_in, ws.keys_out, ws.gptr_in, ws.gptr_out,
                                           (size_t)total, 0, end_bit, s));
   const unsigned sentinel = (unsigned)num_rows;
   k_mark_heads<<<g, B, 0, s>>>(ws.keys_out, ws.flags, total, sentinel);
@@ -386,18 +533,26 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   k_segments<<<g, B, 0, s>>>(ws.keys_out, ws.pos, total, sentinel, ws.seg_start, ws.seg_end, ws.seg_key, uniq_ids,
                              uniq_count);
   GRK_LAUNCH_CHECK();
-  const int tpr = dim / 4;
-  const int rows_per_block = tpr >= 256 ? 1 : 256 / tpr;
-  const int block = tpr >= 256 ? tpr : rows_per_block * tpr;
-  const int64_t gr = (total + rows_per_block - 1) / rows_per_block;
-  if (grad_dtype == GRK_BF16)
-    k_segment_reduce<bf16_t><<<(unsigned)gr, block, 0, s>>>(ws.gsrc, dim, ws.vals_out, ws.seg_start, ws.seg_end,
-                                                            ws.seg_key, uniq_count, total, dense_out, uniq_rows,
-                                                            row_slot);
-  else
-    k_segment_reduce<float><<<(unsigned)gr, block, 0, s>>>(ws.gsrc, dim, ws.vals_out, ws.seg_start, ws.seg_end,
-                                                           ws.seg_key, uniq_count, total, dense_out, uniq_rows,
-                                                           row_slot);
+  const int vec = grad_dtype == GRK_BF16 ? 8 : 4;
+  const int tpr = dim / vec;
+  const int groups = tpr >= 256 ? 1 : 256 / tpr;
+  const int block = tpr >= 256 ? tpr : groups * tpr;
+  const int64_t chunks = (total + kRedChunk - 1) / kRedChunk;
+  const unsigned gc = (unsigned)((chunks + groups - 1) / groups);
+  const unsigned gu = (unsigned)((total + groups - 1) / groups);
+  if (grad_dtype == GRK_BF16) {
+    k_seg_chunks<bf16_t><<<gc, block, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,
+                                              sentinel, dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot);
+    GRK_LAUNCH_CHECK();
+    k_seg_combine<bf16_t><<<gu, block, 0, s>>>(ws.gptr_out, ws.seg_start, ws.seg_end, ws.seg_key, uniq_count, total,
+                                               dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot);
+  } else {
+    k_seg_chunks<float><<<gc, block, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,
+                                             sentinel, dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot);
+    GRK_LAUNCH_CHECK();
+    k_seg_combine<float><<<gu, block, 0, s>>>(ws.gptr_out, ws.seg_start, ws.seg_end, ws.seg_key, uniq_count, total,
+                                              dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot);
+  }
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }

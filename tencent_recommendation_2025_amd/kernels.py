@@ -139,7 +139,7 @@ def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, s
     if token_type is not None:
         token_type = token_type.to(torch.int32).contiguous()
         keep.append(token_type)
-    ws_bytes = L.lib().grk_embedding_backward_workspace(total, num_rows)
+    ws_bytes = L.lib().grk_embedding_backward_workspace(total, num_rows, dim)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     dense_out = torch.empty((num_rows, dim), dtype=torch.float32, device=dev) if dense else None
     cap = max(total, 1)

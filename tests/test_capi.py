@@ -67,4 +67,4 @@ def test_workspace_query_without_device_fails_cleanly(lib):
     if torch.cuda.is_available():
         pytest.skip('covered by the gpu suite')
     # rocprim sizes its temp storage from the device; with no device the query reports 0
-    assert lib.lib().grk_embedding_backward_workspace(77184, 1_000_001) == 0
+    assert lib.lib().grk_embedding_backward_workspace(77184, 1_000_001, 512) == 0
