@@ -17,7 +17,7 @@ all: $(LIB)
 $(OBJ_DIR):
 	mkdir -p $@
 
-$(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/grk_common.h include/grk.h | $(OBJ_DIR)
+$(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(wildcard $(SRC_DIR)/*.h) include/grk.h | $(OBJ_DIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(OBJ_DIR)/%.cpp.o: $(SRC_DIR)/%.cpp include/grk.h | $(OBJ_DIR)

@@ -214,6 +214,26 @@ int grk_pair_logits_bwd(const void* h, int64_t ldh, const void* e_pos, int64_t l
                         const int32_t* count, const float* grad_loss, void* dh, int64_t lddh, void* de_pos,
                         int64_t lddp, void* de_neg, int64_t lddn, void* stream);
 
+/* ------------------------------------------------------------------------
+ * In-batch sampled softmax (north star; no reference -- oracle/loss.py)
+ *   z_ij = <h_i, e_j> / tau over valid columns j; j != i masked when
+ *   item_ids[j] == item_ids[i]; loss = mean_valid_i (logsumexp_j z_ij - z_ii)
+ * h, e: bf16 [num_rows, ld] (dim in {32, 64, 128, 256, 512}); valid uint8.
+ * ------------------------------------------------------------------------ */
+size_t grk_sampled_softmax_workspace(int64_t num_rows);
+
+/* Writes lse2 fp32 [num_rows] (log2-domain logsumexp, -inf on invalid rows),
+ * the loss and the valid-row count (fixed-order reduction). */
+int grk_sampled_softmax_fwd(const void* h, int64_t ldh, const void* e, int64_t lde, const int64_t* item_ids,
+                            const uint8_t* valid, int64_t num_rows, int dim, float tau, float* lse2, float* loss,
+                            int32_t* count, void* workspace, size_t workspace_bytes, void* stream);
+
+/* G [num_rows, ldg] bf16 = (softmax - I) * grad_loss / (count * tau) on valid
+ * (row, column) pairs, 0 elsewhere; then dh = G e and de = G^T h (GEMMs). */
+int grk_sampled_softmax_grad(const void* h, int64_t ldh, const void* e, int64_t lde, const int64_t* item_ids,
+                             const uint8_t* valid, int64_t num_rows, int dim, float tau, const float* lse2,
+                             const int32_t* count, const float* grad_loss, void* G, int64_t ldg, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

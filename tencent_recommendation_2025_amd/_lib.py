@@ -77,6 +77,9 @@ SIGNATURES = {
     'grk_attention_bwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64, _P, _I64,
                                _P, _P]),
     'grk_pair_logits_partials': (_SZ, [_I64]),
+    'grk_sampled_softmax_workspace': (_SZ, [_I64]),
+    'grk_sampled_softmax_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _I, _F, _P, _P, _P, _P, _SZ, _P]),
+    'grk_sampled_softmax_grad': (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _I, _F, _P, _P, _P, _P, _I64, _P]),
     'grk_pair_logits_fwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _P]),
     'grk_pair_logits_bwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _I64, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
                                  _P, _I64, _P, _I64, _P]),

@@ -23,16 +23,10 @@
 // cdna_hip_programming.md §3).  Backward = dQ kernel (S^T, dP^T, dQ^T) +
 // dK/dV kernel (S, dP, dV^T, dK^T): no atomics on dQ/dK/dV, deterministic.
 #include "grk_common.h"
+#include "grk_mfma.h"
 
 namespace grk {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kLn2 = 0.6931471805599453f;
 constexpr int kChunk = 64;      // rows staged per LDS chunk
 constexpr int kBlockRows = 128; // queries (fwd/dQ) or keys (dKdV) per workgroup
 constexpr int kRabMax = 2048;
@@ -57,54 +51,6 @@ struct AttnParams {
   float* drab;
 };
 
-__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// Swizzled LDS row image: row of HD bf16 = HD/8 16-byte chunks; chunk c of
-// row r lives at chunk position c ^ (r & MASK).
-template <int HD>
-__device__ __forceinline__ int lds_off(int row, int col) {
-  constexpr int NCH = HD / 8;
-  constexpr int MASK = NCH >= 8 ? 7 : NCH - 1;
-  const int c = col >> 3;
-  return row * (HD * 2) + ((c ^ (row & MASK)) << 4) + ((col & 7) << 1);
-}
-
-template <int HD>
-__device__ __forceinline__ bf16x8 lds_row8(const char* base, int row, int col) {
-  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + lds_off<HD>(row, col)));
-}
-
-// Transposed fragment: element j of lane (r, hh) = M[row0 + 8(j>>2) + 4hh + (j&3)][col0 + r].
-template <int HD>
-__device__ __forceinline__ bf16x8 lds_tr8(const char* base, int row0, int col0, int lane) {
-  const int g = lane >> 4, i = lane & 15;
-  const int q4 = i >> 2, p = i & 3;
-  const int hh = g >> 1;
-  const int col = col0 + 16 * (g & 1) + 4 * p;
-  const int ra = row0 + 4 * hh + q4;
-  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + lds_off<HD>(ra, col)));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + lds_off<HD>(ra + 8, col)));
-  bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
-  bf16x8 r;
-  r[0] = l4[0]; r[1] = l4[1]; r[2] = l4[2]; r[3] = l4[3];
-  r[4] = h4[0]; r[5] = h4[1]; r[6] = h4[2]; r[7] = h4[3];
-  return r;
-}
-
-// Accumulator registers 8s..8s+7 as a bf16 operand (hi part, and the
-// residual lo part for the precise mode).
-__device__ __forceinline__ void pack_acc(const float* x, int s, bf16x8& hi, bf16x8& lo) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    __bf16 hb = static_cast<__bf16>(x[8 * s + j]);
-    hi[j] = hb;
-    lo[j] = static_cast<__bf16>(x[8 * s + j] - static_cast<float>(hb));
-  }
-}
-
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float dsilu(float x) {
   const float sg = 1.0f / (1.0f + __expf(-x));
@@ -121,25 +67,6 @@ __device__ __forceinline__ bool drop_keep(unsigned long long seed, int bh, int q
   x ^= x >> 31;
   const float u = (float)(x >> 40) * (1.0f / 16777216.0f);
   return u >= p;
-}
-
-__device__ __forceinline__ int acc_row(int i, int hh) { return (i & 3) + 8 * (i >> 2) + 4 * hh; }
-
-// Load a [HD] bf16 row slice as an 8-wide fragment from global; zero if !ok.
-__device__ __forceinline__ bf16x8 gload8(const bf16_t* p, bool ok) {
-  uint4 v = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-__device__ __forceinline__ bf16x8 gload8_any(const void* base, int64_t off, bool f32, bool ok) {
-  if (!ok) return __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
-  if (!f32) return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>((const bf16_t*)base + off));
-  const float4* fp = reinterpret_cast<const float4*>((const float*)base + off);
-  float4 a = fp[0], b = fp[1];
-  bf16x8 r;
-  r[0] = (__bf16)a.x; r[1] = (__bf16)a.y; r[2] = (__bf16)a.z; r[3] = (__bf16)a.w;
-  r[4] = (__bf16)b.x; r[5] = (__bf16)b.y; r[6] = (__bf16)b.z; r[7] = (__bf16)b.w;
-  return r;
 }
 
 // Stage rows [r0, r0+kChunk) of a [B*T, ld] head slice into a swizzled LDS

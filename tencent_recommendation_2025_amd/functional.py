@@ -264,3 +264,35 @@ def bce_loss(h, e_pos, e_neg, next_token_type):
     """Fused logits + the reference BCE loss (main.py:177-182), no host sync."""
     ntt = next_token_type.reshape(-1).to(torch.int32).contiguous()
     return _BCELossFn.apply(h, e_pos, e_neg, ntt)
+
+
+# -------------------------------------------------------- sampled softmax ----
+class _SampledSoftmaxFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, e, item_ids, valid, tau):
+        D = h.shape[-1]
+        hb = _rows2d(h.to(torch.bfloat16))
+        eb = _rows2d(e.to(torch.bfloat16))
+        loss, lse2, count = K.sampled_softmax_fwd(hb, eb, item_ids, valid, tau)
+        ctx.save_for_backward(hb, eb, item_ids, valid, lse2, count)
+        ctx.meta = (tau, h.shape, e.shape, h.dtype, e.dtype)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        hb, eb, ids, valid, lse2, count = ctx.saved_tensors
+        tau, hs, es, hdt, edt = ctx.meta
+        G = K.sampled_softmax_grad_matrix(hb, eb, ids, valid, tau, lse2, count, gloss)
+        dh = (G @ eb).view(hs).to(hdt) if ctx.needs_input_grad[0] else None
+        de = (G.t() @ hb).view(es).to(edt) if ctx.needs_input_grad[1] else None
+        return dh, de, None, None, None
+
+
+@_disable
+def sampled_softmax_loss(h, pos_emb, pos_ids, next_token_type, tau):
+    """In-batch sampled softmax over every valid position's positive item
+    (north star; oracle/loss.py::sampled_softmax): one flash-style MFMA pass
+    for the loss, a G-matrix pass + two GEMMs for the gradients."""
+    ids = pos_ids.reshape(-1).to(torch.int64).contiguous()
+    valid = (next_token_type.reshape(-1) == 1).to(torch.uint8).contiguous()
+    return _SampledSoftmaxFn.apply(h, pos_emb, ids, valid, float(tau))

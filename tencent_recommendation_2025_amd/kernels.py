@@ -274,3 +274,36 @@ def pair_logits_bwd(h, e_pos, e_neg, gpos=None, gneg=None, pos_logits=None, neg_
                                      bl, c, cl, L.stream_ptr(h.device))
     L.check(rc, 'grk_pair_logits_bwd')
     return tuple(outs)
+
+
+# --------------------------------------------------------- sampled softmax
+def sampled_softmax_fwd(h, e, item_ids, valid, tau):
+    """(loss, lse2, count) of the in-batch sampled softmax (grk_sampled_softmax_fwd)."""
+    _require_cuda(h, e, item_ids, valid)
+    M, D = h.shape
+    dev = h.device
+    (hp, hl), (ep, el) = _rows(h, 'h'), _rows(e, 'e')
+    ws = torch.empty(max(L.lib().grk_sampled_softmax_workspace(M), 4), dtype=torch.uint8, device=dev)
+    lse2 = torch.empty(M, dtype=torch.float32, device=dev)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    count = torch.empty(1, dtype=torch.int32, device=dev)
+    rc = L.lib().grk_sampled_softmax_fwd(hp, hl, ep, el, item_ids.data_ptr(), valid.data_ptr(), M, D, float(tau),
+                                         lse2.data_ptr(), loss.data_ptr(), count.data_ptr(), ws.data_ptr(),
+                                         ws.numel(), L.stream_ptr(dev))
+    L.check(rc, 'grk_sampled_softmax_fwd')
+    return loss, lse2, count
+
+
+def sampled_softmax_grad_matrix(h, e, item_ids, valid, tau, lse2, count, grad_loss=None):
+    """G [M, M] bf16 (view of a row-padded buffer) with dh = G e, de = G^T h."""
+    _require_cuda(h, e, item_ids, valid, lse2, count, grad_loss)
+    M, D = h.shape
+    ldg = (M + 7) // 8 * 8
+    G = torch.empty(M, ldg, dtype=torch.bfloat16, device=h.device)
+    gl = None if grad_loss is None else grad_loss.float().reshape(1).contiguous()
+    (hp, hl), (ep, el) = _rows(h, 'h'), _rows(e, 'e')
+    rc = L.lib().grk_sampled_softmax_grad(hp, hl, ep, el, item_ids.data_ptr(), valid.data_ptr(), M, D, float(tau),
+                                          lse2.data_ptr(), count.data_ptr(), _ptr(gl), G.data_ptr(), ldg,
+                                          L.stream_ptr(h.device))
+    L.check(rc, 'grk_sampled_softmax_grad')
+    return G[:, :M]

@@ -84,15 +84,17 @@ def test_dropin_step_matches_reference(golden, tag):
                             weight_decay=float(g['weight_decay']))
     opt.zero_grad()
     loss.backward()
+    live = tag.endswith('_live')
     worst = {}
     for name, p in m.named_parameters():
         want = g[f'grad.{name}']
         got = p.grad.detach().cpu().numpy() if p.grad is not None else np.zeros_like(want)
-        if np.linalg.norm(want) > 0:
+        # the key bias gets an analytically-zero gradient (softmax is shift-invariant): rounding noise only
+        if np.linalg.norm(want) > 0 and not name.endswith('k_linear.bias'):
             worst[name] = nrel(got, want)
-    bad = {k: v for k, v in worst.items() if v > 2e-2}
-    assert not bad, f'grad normwise errors above 2e-2: {bad}'
-    if tag.endswith('_live'):
+    if live:  # reference init zeroes LayerNorm gamma: only the live fixtures have meaningful grads
+        bad = {k: v for k, v in worst.items() if v > 2e-2}
+        assert not bad, f'grad normwise errors above 2e-2: {bad}'
         assert len(worst) > 40, 'live fixture: (almost) every gradient is non-zero'
     opt.step()
     lr = float(g['lr'])
@@ -101,7 +103,8 @@ def test_dropin_step_matches_reference(golden, tag):
         got = p.detach().cpu().numpy()
         # AdamW's first step moves each element by ~lr*sign(grad): compare to lr
         assert np.max(np.abs(got - want)) <= 2.05 * lr, name
-        assert np.mean(np.abs(got - want) < 1e-6) > 0.97, name
+        if live and not name.endswith('k_linear.bias'):
+            assert np.mean(np.abs(got - want) < 1e-6) > 0.97, name
 
 
 def test_list_of_dicts_input_equals_tensor_input(golden, tmp_path):
@@ -173,7 +176,8 @@ def test_fused_trainer_matches_dropin(golden):
     for k in s1:
         diff = (s1[k].float() - s2[k].float()).abs()
         assert float(diff.max()) <= 2.05 * lr, k
-        assert float((diff < 1e-6).float().mean()) > 0.97, k
+        if not k.endswith('k_linear.bias'):
+            assert float((diff < 1e-6).float().mean()) > 0.97, k
 
 
 def test_fused_trainer_bf16_hstu_learns():

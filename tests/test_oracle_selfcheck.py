@@ -1,0 +1,99 @@
+"""Self-consistency of the parity-UNPINNED oracle pieces (no reference
+implementation exists for them): HSTU attention and in-batch sampled softmax.
+Pinned by finite differences and by agreement of two independent
+restatements (numpy closed form vs torch autograd)."""
+import numpy as np
+import torch
+
+from oracle import attention as oatt
+from oracle import hstu as ohstu
+from oracle import loss as oloss
+from oracle import model_ref
+
+
+def fd_check(f, x, grad, eps=1e-6, n=12, seed=0):
+    rng = np.random.default_rng(seed)
+    for _ in range(n):
+        idx = tuple(rng.integers(0, s) for s in x.shape)
+        xp, xm = x.copy(), x.copy()
+        xp[idx] += eps
+        xm[idx] -= eps
+        num = (f(xp) - f(xm)) / (2 * eps)
+        assert abs(num - grad[idx]) < 1e-6 + 1e-5 * abs(num), (idx, num, grad[idx])
+
+
+def hstu_inputs(seed=0, B=2, H=2, T=9, hd=4, nb=5):
+    rng = np.random.default_rng(seed)
+    q, k, v, do = (rng.standard_normal((B, H, T, hd)) for _ in range(4))
+    valid = np.ones((B, T), bool)
+    valid[1, :3] = False
+    rab = rng.standard_normal((H, nb)) * 0.5
+    return q, k, v, do, valid, rab
+
+
+def test_hstu_backward_finite_differences():
+    q, k, v, do, valid, rab = hstu_inputs()
+    a, n = 0.7, 1.0 / 9
+    dq, dk, dv, drab = ohstu.backward(q, k, v, valid, rab, a, n, do)
+    L = lambda qq=q, kk=k, vv=v, rr=rab: float((ohstu.forward(qq, kk, vv, valid, rr, a, n)[0] * do).sum())
+    fd_check(lambda x: L(qq=x), q, dq)
+    fd_check(lambda x: L(kk=x), k, dk)
+    fd_check(lambda x: L(vv=x), v, dv)
+    fd_check(lambda x: L(rr=x), rab, drab)
+
+
+def test_hstu_numpy_equals_torch_restatement():
+    q, k, v, do, valid, rab = hstu_inputs(seed=1, T=7, nb=7)
+    B, H, T, hd = q.shape
+    m = model_ref.RefHSTU(H * hd, H, 0.0, T).double()
+    x = torch.from_numpy(np.random.default_rng(2).standard_normal((B, T, H * hd)))
+    with torch.no_grad():
+        m.rab.copy_(torch.from_numpy(rab))
+    u, vv, qq, kk = torch.split(torch.nn.functional.silu(m.uvqk(x)), H * hd, dim=-1)
+    sh = lambda t: t.view(B, T, H, hd).transpose(1, 2).numpy()
+    mask = torch.from_numpy(np.tril(np.ones((T, T), bool))[None] & valid[:, None, :])
+    o_np, _, _ = ohstu.forward(sh(qq.detach()), sh(kk.detach()), sh(vv.detach()), valid, rab, hd ** -0.5, 1.0 / T)
+    y, _ = m(x, x, x, attn_mask=mask)
+    o_t = torch.from_numpy(o_np).transpose(1, 2).reshape(B, T, H * hd)
+    want = m.out_linear(m.attn_norm(o_t) * u)
+    np.testing.assert_allclose(y.detach().numpy(), want.detach().numpy(), rtol=1e-10, atol=1e-12)
+
+
+def test_softmax_attention_backward_finite_differences():
+    q, k, v, do, valid, _ = hstu_inputs(seed=3)
+    dq, dk, dv = oatt.backward(q, k, v, valid, do)
+    L = lambda qq=q, kk=k, vv=v: float((oatt.forward(qq, kk, vv, valid)[0] * do).sum())
+    fd_check(lambda x: L(qq=x), q, dq)
+    fd_check(lambda x: L(kk=x), k, dk)
+    fd_check(lambda x: L(vv=x), v, dv)
+
+
+def test_sampled_softmax_numpy_equals_torch_autograd():
+    rng = np.random.default_rng(4)
+    M, D = 40, 8
+    h, e = rng.standard_normal((M, D)), rng.standard_normal((M, D))
+    ids = rng.integers(0, 12, M)
+    valid = rng.random(M) < 0.7
+    loss, dh, de = oloss.sampled_softmax(h, e, ids, valid, 0.3)
+    th, te = torch.from_numpy(h).requires_grad_(True), torch.from_numpy(e).requires_grad_(True)
+    tl = model_ref.sampled_softmax_loss(th, te, torch.from_numpy(ids), torch.from_numpy(valid.astype(np.int64)), 0.3)
+    tl.backward()
+    np.testing.assert_allclose(tl.item(), loss, rtol=1e-12)
+    np.testing.assert_allclose(th.grad.numpy(), dh, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(te.grad.numpy(), de, rtol=1e-9, atol=1e-12)
+
+
+def test_bce_oracle_equals_torch():
+    rng = np.random.default_rng(5)
+    N, D = 30, 6
+    h, ep, en = (rng.standard_normal((N, D)) for _ in range(3))
+    ntt = rng.integers(0, 2, N)
+    loss, _, _, dh, dep, den = oloss.bce(h, ep, en, ntt)
+    th, tp, tn = (torch.from_numpy(x).requires_grad_(True) for x in (h, ep, en))
+    m = torch.from_numpy(ntt == 1)
+    pl = (th * tp).sum(-1) * m
+    nl = (th * tn).sum(-1) * m
+    tl = model_ref.bce_loss(pl, nl, torch.from_numpy(ntt))
+    tl.backward()
+    np.testing.assert_allclose(tl.item(), loss, rtol=1e-12)
+    np.testing.assert_allclose(th.grad.numpy(), dh, rtol=1e-9, atol=1e-12)
