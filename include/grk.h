@@ -204,7 +204,8 @@ int grk_pair_logits_fwd(const void* h, int64_t ldh, const void* e_pos, int64_t l
                         float* neg_logits, float* partials, float* loss, int32_t* count, void* stream);
 
 /* dh = gp*e_pos + gn*e_neg, de_pos = gp*h, de_neg = gn*h per row.
- * Either gpos/gneg (fp32 per-row coefficients) are given, or -- when
+ * Either gpos/gneg (fp32 per-row upstream grads of the logits; rows with
+ * next_token_type != 1 get 0, as the forward masked them) are given, or -- when
  * pos_logits/neg_logits are non-NULL -- the BCE coefficients
  * gp = g*(sigmoid(pos)-1)/count, gn = g*sigmoid(neg)/count on valid rows,
  * with g = *grad_loss (device scalar; NULL = 1).  Outputs may be NULL. */

@@ -253,7 +253,7 @@ def sampled_softmax_loss(h, pos_emb, pos_ids, next_token_type, tau):
     ids = pos_ids.reshape(-1); valid = (next_token_type.reshape(-1) == 1)
     n = hv.shape[0]
     z = hv @ ev.t() / tau
-    same = (ids[:, None] == ids[None, :]) & ~torch.eye(n, dtype=torch.bool)
+    same = (ids[:, None] == ids[None, :]) & ~torch.eye(n, dtype=torch.bool, device=hv.device)
     z = z.masked_fill(~valid[None, :] | same, float('-inf'))
     lse = torch.logsumexp(z, dim=1)
     per = lse - z.diagonal()

@@ -118,8 +118,9 @@ __global__ void __launch_bounds__(256) k_pair_logits_bwd(const T* __restrict__ h
   if (n >= N) return;
   float gp, gn;
   if (mode == 0) {
-    gp = gpos ? gpos[n] : 0.f;
-    gn = gneg ? gneg[n] : 0.f;
+    const bool valid = ntt ? ntt[n] == 1 : true;  // the forward zeroed masked logits
+    gp = (gpos && valid) ? gpos[n] : 0.f;
+    gn = (gneg && valid) ? gneg[n] : 0.f;
   } else {
     const bool valid = ntt ? ntt[n] == 1 : true;
     const float c = (float)max(*count, 1);

@@ -217,16 +217,17 @@ class _PairLogitsFn(torch.autograd.Function):
         dt = torch.promote_types(torch.promote_types(h.dtype, ep.dtype), en.dtype)
         h2, p2, n2 = (_rows2d(x.to(dt)) for x in (h, ep, en))
         pos, neg = K.pair_logits_fwd(h2, p2, n2, ntt)
-        ctx.save_for_backward(h2, p2, n2)
+        ctx.save_for_backward(h2, p2, n2, ntt)
         ctx.dtypes = (h.dtype, ep.dtype, en.dtype)
         ctx.shapes = (h.shape, ep.shape, en.shape)
         return pos, neg
 
     @staticmethod
     def backward(ctx, gpos, gneg):
-        h2, p2, n2 = ctx.saved_tensors
+        h2, p2, n2, ntt = ctx.saved_tensors
         need = ctx.needs_input_grad[:3]
-        dh, dp, dn = K.pair_logits_bwd(h2, p2, n2, gpos=gpos.contiguous(), gneg=gneg.contiguous(), need=need)
+        dh, dp, dn = K.pair_logits_bwd(h2, p2, n2, gpos=gpos.contiguous(), gneg=gneg.contiguous(),
+                                       next_token_type=ntt, need=need)
         return _shape_grads(ctx, dh, dp, dn)
 
 
