@@ -53,6 +53,9 @@ def parse():
     ap.add_argument('--cpu-batch', type=int, default=8)
     ap.add_argument('--cpu-steps', type=int, default=2)
     ap.add_argument('--roofline-reps', type=int, default=20)
+    ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
+                    help='gloo: rehearse N ranks on fewer GPUs (collectives staged via host)')
+    ap.add_argument('--sharded', type=int, default=None, help='force the row-sharded optimizer (default: N > 1)')
     return ap.parse_args()
 
 
@@ -132,10 +135,15 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device('cuda', local % max(ndev, 1))
+    torch.cuda.set_device(dev)
+    sharded = (world > 1) if a.sharded is None else bool(a.sharded)
+    if world > 1 or sharded:
+        if a.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group('gloo')
 
     from tencent_recommendation_2025_amd import functional as G
     from tencent_recommendation_2025_amd import synthetic as S
@@ -150,7 +158,7 @@ def main():
     torch.manual_seed(0)
     model = BaselineModel(a.users, a.items, stats, types, margs).to(dev)
     init_reference_(model, seed=0, live_norms=True)
-    if world > 1:
+    if sharded:
         from tencent_recommendation_2025_amd.sharding import ShardedFusedAdamW
         opt = ShardedFusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
     else:
@@ -199,13 +207,13 @@ def main():
                                    f'({a.blocks} blocks x {a.heads} heads), {a.items}-item bf16 table, '
                                    f'{a.users} users, loss={a.loss}, table AdamW={a.table_mode}',
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch, 'seq_len': a.maxlen + 1,
-                       'parallelism': f'dp{world}' + ('+rowshard' if world > 1 else '')},
+                       'parallelism': f'dp{world}' + ('+rowshard' if sharded else '')},
             'final_loss': round(final_loss, 5),
             'roofline': roof,
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

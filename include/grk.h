@@ -141,7 +141,9 @@ typedef struct grk_adamw_hparams {
 /* mode GRK_ADAM_DENSE: every row of the table moves (reference semantics:
  * rows without gradient see g = 0), gradient rows found via row_slot.
  * mode GRK_ADAM_LAZY: only the uniq_count rows are updated (documented
- * deviation).  Both restore row_slot[uniq_ids[*]] = -1. */
+ * deviation).  Both restore row_slot[uniq_ids[*]] = -1 when
+ * uniq_ids is given; with uniq_ids NULL, row_slot is a caller-owned fixed map
+ * (an identity map + a dense gradient in uniq_rows = plain dense AdamW). */
 int grk_table_adamw(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows, int dim,
                     const int64_t* uniq_ids, const float* uniq_rows, const int32_t* uniq_count, int64_t max_uniq,
                     int32_t* row_slot, grk_adamw_hparams hp, int mode, void* stream);

@@ -112,7 +112,6 @@ extern "C" int grk_table_adamw(void* param, int param_dtype, float* exp_avg, flo
   GRK_CHECK_ARG(dim > 0 && dim % 4 == 0, "dim must be a multiple of 4");
   GRK_CHECK_ARG(mode == GRK_ADAM_DENSE || mode == GRK_ADAM_LAZY, "bad mode");
   GRK_CHECK_ARG(mode == GRK_ADAM_DENSE || (uniq_ids && uniq_rows && uniq_count), "lazy mode needs uniq_* inputs");
-  GRK_CHECK_ARG(!row_slot || (uniq_ids && uniq_count), "row_slot needs uniq_ids/uniq_count");
   GRK_CHECK_ARG(mode == GRK_ADAM_LAZY || !row_slot || uniq_rows, "dense mode with row_slot needs uniq_rows");
   GRK_CHECK_ARG(hp.bias_corr2_sqrt > 0.f, "bias_corr2_sqrt must be > 0");
   hipStream_t s = (hipStream_t)stream;
@@ -134,7 +133,7 @@ extern "C" int grk_table_adamw(void* param, int param_dtype, float* exp_avg, flo
                                             uniq_count, max_uniq, hp);
   }
   GRK_LAUNCH_CHECK();
-  if (row_slot) {
+  if (row_slot && uniq_ids && uniq_count) {  // without uniq_ids row_slot is a fixed map (e.g. identity)
     k_reset_slots<<<grid_for(max_uniq, 256, 1024), 256, 0, s>>>(row_slot, uniq_ids, uniq_count, max_uniq);
     GRK_LAUNCH_CHECK();
   }

@@ -200,7 +200,8 @@ class BaselineModel(torch.nn.Module):
                 self.sparse_emb[k] = torch.nn.Embedding(group[k] + 1, d, padding_idx=0)
         for k in self.ITEM_EMB_FEAT:
             self.emb_transform[k] = torch.nn.Linear(self.ITEM_EMB_FEAT[k], d)
-        self._table_refs = None  # set by TableStore (fused optimizer mode)
+        self._table_refs = None  # set by FusedAdamW (table groups)
+        self._remaps = None      # set by ShardedFusedAdamW.prepare (rows fetched from other ranks)
 
     def _init_feat_info(self, feat_statistics, feat_types):
         self.USER_SPARSE_FEAT = {k: feat_statistics[k] for k in feat_types['user_sparse']}
@@ -280,12 +281,29 @@ class BaselineModel(torch.nn.Module):
         if with_pos:
             specs.append(G.LookupSpec(self._ref('pos_emb'), seq, col, L.IDX_POSITION))
             col += d
+        if self._remaps is not None or self._table_refs is not None:
+            specs = self._remap_specs(specs)
         buf = G.feature_lookup(specs, N, col, tt, T, extra, extra_col)
         x = torch.relu(self.itemdnn(buf[:, :item_w]))
         if include_user:
             x = x + torch.relu(self.userdnn(buf[:, item_w:user_end]))
         pos_rows = buf[:, user_end:user_end + d] if with_pos else None
         return x.view(B, T, d), pos_rows
+
+    def _remap_specs(self, specs):
+        """Row-sharded tables: read the rows prepare() fetched for this step."""
+        out = []
+        for s in specs:
+            name = getattr(s.ref, 'name', None)
+            if name is None:
+                out.append(s)
+                continue
+            hit = (self._remaps or {}).get((name, s.idx.data_ptr(), s.mode))
+            if hit is None:
+                raise RuntimeError(f'{name} is row-sharded: call the optimizer\'s prepare(batch) before forward')
+            ref, inv = hit
+            out.append(G.LookupSpec(ref, inv, s.out_col, L.IDX_PLAIN, 1))
+        return out
 
     def feat2emb(self, seq, feature_array, mask=None, include_user=False):
         return self._embed(seq, feature_array, mask, include_user)[0]

@@ -1,0 +1,274 @@
+"""Multi-GPU training: row-sharded tables over RCCL all-to-all, DP all-reduce.
+
+The reference is single-process (no torch.distributed); this is
+the north star's scale-out:
+
+* one process per GPU, ``torch.distributed`` with the "nccl" backend (RCCL
+  over xGMI); every rank trains on its own batch (data parallel, weak scaling);
+* the big tables (``item_emb``, ``user_emb``) are **row-sharded**: global row
+  ``g`` lives on rank ``g % G`` at local row ``g // G`` (row 0 -- the padding
+  row -- is local row 0 of rank 0).  At the start of a step ``prepare`` routes
+  the batch's unique ids to their owners (``all_to_all``), owners gather the
+  rows, and the rows come back (``all_to_all``); the model's fused gather then
+  reads the fetched rows.  After backward, each rank first reduces its
+  gradients per unique id (deterministic), routes them to the owners
+  (``all_to_all``), and each owner reduces what it received in rank order
+  (deterministic) and runs the table AdamW on its shard;
+* the small tables (pos + feature tables, ~48k rows) are replicated; their
+  dense fp32 gradient and every dense parameter's gradient are averaged with
+  one flat ``all_reduce`` each.
+
+Gradients are averaged over ranks (DP convention: the global loss is the mean
+of the per-rank losses).  One host synchronisation per step remains: the
+all-to-all split sizes.
+
+The collective logic here is device-agnostic (the CPU test suite drives it
+with gloo); the device work is injected: on HIP tensors the row gather and
+the gradient reductions are the grk kernels.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+from . import functional as G
+from . import kernels as K
+from .optim import FusedAdamW, TableGroup
+
+
+# ----------------------------------------------------------- device work ----
+def kernel_gather(shard, local_ids):
+    """rows = shard[local_ids] (grk_embedding_gather)."""
+    out = torch.empty(local_ids.numel(), shard.shape[1], dtype=shard.dtype, device=shard.device)
+    if local_ids.numel():
+        K.embedding_gather([K.Lookup(shard, local_ids, 0)], out, local_ids.numel())
+    return out
+
+
+def kernel_reduce(sources, num_rows, dim, padding_idx, row_slot):
+    """Deterministic row-sparse reduction (grk_embedding_backward)."""
+    return K.embedding_backward(sources, num_rows, dim, padding_idx=padding_idx, dense=False, sparse=True,
+                                row_slot=row_slot)
+
+
+def kernel_dense_reduce(sources, num_rows, dim, token_type=None, seq_len=0, padding_idx=0):
+    return K.embedding_backward(sources, num_rows, dim, padding_idx=padding_idx, token_type=token_type,
+                                seq_len=seq_len, dense=True).dense
+
+
+# ----------------------------------------------------------- collectives ----
+# RCCL ("nccl") takes device tensors directly.  With gloo (CPU tests, and
+# rehearsing several ranks on one GPU) device tensors are staged via host.
+def _staged(pg, *ts):
+    return dist.get_backend(pg) == 'gloo' and any(t.is_cuda for t in ts)
+
+
+def a2a(out, inp, out_split=None, in_split=None, pg=None):
+    if _staged(pg, out, inp):
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu(), out_split, in_split, group=pg)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, out_split, in_split, group=pg)
+
+
+def all_reduce(t, pg=None):
+    if _staged(pg, t):
+        c = t.cpu()
+        dist.all_reduce(c, group=pg)
+        t.copy_(c)
+    else:
+        dist.all_reduce(t, group=pg)
+
+
+# ------------------------------------------------------------- exchange ----
+class ShardedRef(G.TableRef):
+    """Marks a lookup of a row-sharded table (must be remapped by prepare())."""
+    __slots__ = ('name',)
+
+    def __init__(self, name, weight):
+        super().__init__(weight)
+        self.name = name
+
+
+class FetchSink:
+    """Collects the gradient sources of lookups into a fetched-row buffer."""
+
+    def __init__(self):
+        self.sources = []
+
+    def collect(self, src, token_type, seq_len):
+        self.sources.append(src)
+
+
+class ShardExchange:
+    """Routes ids / rows / gradients of one row-sharded table."""
+
+    def __init__(self, name, shard, dim, pg=None, gather_fn=kernel_gather):
+        self.name, self.shard, self.dim, self.pg = name, shard, dim, pg
+        self.world = dist.get_world_size(pg)
+        self.rank = dist.get_rank(pg)
+        self.gather_fn = gather_fn
+        self.plan = None
+
+    def route(self, ids):
+        """Phase 1 (before the single host sync): unique ids, owner order, counts."""
+        uniq, inverse = torch.unique(ids, sorted=True, return_inverse=True)
+        owner = uniq % self.world
+        order = torch.argsort(owner, stable=True)
+        send_ids = uniq[order]
+        send_counts = torch.bincount(owner, minlength=self.world)
+        recv_counts = torch.empty_like(send_counts)
+        a2a(recv_counts, send_counts, pg=self.pg)
+        return dict(uniq=uniq, inverse=inverse, order=order, send_ids=send_ids, send_counts=send_counts,
+                    recv_counts=recv_counts)
+
+    def fetch(self, r, send_split, recv_split):
+        """Phase 2: ids to owners, owners gather, rows back; returns rows in uniq order."""
+        recv_ids = r['send_ids'].new_empty(sum(recv_split))
+        a2a(recv_ids, r['send_ids'], recv_split, send_split, self.pg)
+        local = recv_ids // self.world
+        rows = self.gather_fn(self.shard, local)
+        back = rows.new_empty((len(r['uniq']), self.dim))
+        a2a(back, rows, send_split, recv_split, self.pg)
+        fetched = torch.empty_like(back)
+        fetched[r['order']] = back
+        self.plan = dict(order=r['order'], send_split=send_split, recv_split=recv_split, recv_local=local,
+                         n_uniq=len(r['uniq']))
+        return fetched
+
+    def push_grads(self, uniq_grads):
+        """Route per-unique-id gradients [U, D] to the owners; returns (local ids, rows) received."""
+        p = self.plan
+        send = uniq_grads[p['order']].contiguous()
+        recv = send.new_empty((sum(p['recv_split']), self.dim))
+        a2a(recv, send, p['recv_split'], p['send_split'], self.pg)
+        return p['recv_local'], recv
+
+
+def shard_rows(full_rows, world, rank):
+    return (full_rows - rank + world - 1) // world
+
+
+# ------------------------------------------------------------ optimizer ----
+class ShardedFusedAdamW(FusedAdamW):
+    """FusedAdamW across ranks: sharded item/user tables, replicated small tables, DP dense params."""
+
+    SHARDED = ('item_emb', 'user_emb')
+
+    def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
+                 table_dtype=torch.bfloat16, pg=None, gather_fn=kernel_gather, reduce_fn=kernel_reduce,
+                 dense_reduce_fn=kernel_dense_reduce):
+        self.pg = pg
+        self.world = dist.get_world_size(pg)
+        self.rank = dist.get_rank(pg)
+        self.reduce_fn, self.dense_reduce_fn = reduce_fn, dense_reduce_fn
+        tables = model.table_modules()
+        dev = model.item_emb.weight.device
+        self.shards = {}
+        sharded_refs = {}
+        for name in self.SHARDED:
+            emb = tables[name]
+            full = emb.weight.detach()
+            shard = full[self.rank::self.world].to(dtype=table_dtype).contiguous()
+            grp = TableGroup(f'{name}@{self.rank}', [(name, _Holder(shard))], table_dtype, dev)
+            grp.global_rows = emb.num_embeddings
+            self.shards[name] = (grp, ShardExchange(name, grp.flat, emb.embedding_dim, pg, gather_fn))
+            # the full table is not kept: this rank holds rows rank::world only
+            emb.weight = torch.nn.Parameter(torch.empty(0, emb.embedding_dim, dtype=table_dtype, device=dev),
+                                            requires_grad=False)
+            sharded_refs[name] = ShardedRef(name, emb.weight)
+        small_keys = tuple(k for k in tables if k not in self.SHARDED)
+        super().__init__(model, lr, betas, eps, weight_decay, table_mode, table_dtype,
+                         groups=(('small', small_keys),))
+        model._table_refs.update(sharded_refs)
+        self.small = self.groups[0]
+        self.small_identity = torch.arange(self.small.rows, dtype=torch.int32, device=dev)
+        self.sinks = {}
+
+    # -- input dist -------------------------------------------------------
+    def prepare(self, batch):
+        """Fetch every row of the sharded tables this step's batch reads."""
+        seq, pos, neg, tt = batch[0], batch[1], batch[2], batch[3]
+        seq, pos, neg = seq.long(), pos.long(), neg.long()
+        tt = tt.to(seq.device)
+        parts = {
+            'item_emb': [(seq, L.IDX_ITEM_MASK, seq * (tt == 1)), (pos, L.IDX_PLAIN, pos), (neg, L.IDX_PLAIN, neg)],
+            'user_emb': [(seq, L.IDX_USER_MASK, seq * (tt == 2))],
+        }
+        routed = {}
+        for name, plist in parts.items():
+            ids = torch.cat([v.reshape(-1) for _, _, v in plist])
+            routed[name] = self.shards[name][1].route(ids)
+        counts = torch.stack([torch.stack([routed[n]['send_counts'], routed[n]['recv_counts']]) for n in parts])
+        counts = counts.cpu().tolist()  # the one host sync of the step: all-to-all split sizes
+        remaps = {}
+        self.sinks = {}
+        for gi, (name, plist) in enumerate(parts.items()):
+            grp, ex = self.shards[name]
+            r = routed[name]
+            fetched = ex.fetch(r, counts[gi][0], counts[gi][1])
+            sink = FetchSink()
+            self.sinks[name] = sink
+            ref = G.TableRef(fetched, sink, 0)
+            off = 0
+            for idx, mode, v in plist:
+                n = v.numel()
+                inv = r['inverse'][off:off + n].view(v.shape)
+                off += n
+                remaps[(name, idx.data_ptr(), mode)] = (ref, inv)
+        self.model._remaps = remaps
+
+    # -- gradient sync + update -------------------------------------------
+    @torch.no_grad()
+    def step(self):
+        self.t += 1
+        hp = K.adamw_hparams(self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, self.t)
+        inv_world = 1.0 / self.world
+        # dense parameters: one flat all-reduce (mean)
+        params = [p for grp in self.dense.param_groups for p in grp['params'] if p.grad is not None]
+        if params:
+            flat = torch.cat([p.grad.reshape(-1).float() for p in params])
+            all_reduce(flat, self.pg)
+            flat.mul_(inv_world)
+            off = 0
+            for p in params:
+                n = p.grad.numel()
+                p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                off += n
+        self.dense.step()
+        # replicated small tables: dense fp32 gradient, all-reduce (mean), dense AdamW
+        g = self.small
+        if g.pending:
+            dense = self.dense_reduce_fn(g.pending, g.rows, g.dim, g.token_type, g.seq_len)
+        else:
+            dense = torch.zeros(g.rows, g.dim, dtype=torch.float32, device=g.flat.device)
+        all_reduce(dense, self.pg)
+        dense.mul_(inv_world)
+        K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, None, dense, None, 0, self.small_identity)
+        g.clear()
+        # sharded tables: per-unique-id grads -> owners -> owner reduction -> shard AdamW
+        for name, (grp, ex) in self.shards.items():
+            sink = self.sinks.get(name)
+            if sink is not None and sink.sources and ex.plan is not None:
+                ug = self.dense_reduce_fn(sink.sources, ex.plan['n_uniq'], grp.dim, padding_idx=None)
+                ug.mul_(inv_world)
+                local, rows = ex.push_grads(ug)
+                src = [K.GradSource(local, rows, 0)]
+                res = self.reduce_fn(src, grp.rows, grp.dim, 0 if self.rank == 0 else -1,
+                                     None if self.lazy else grp.row_slot)
+                K.table_adamw(grp.flat, grp.exp_avg, grp.exp_avg_sq, hp, res.ids, res.rows, res.count, res.capacity,
+                              None if self.lazy else grp.row_slot, lazy=self.lazy)
+            elif not self.lazy:
+                K.table_adamw(grp.flat, grp.exp_avg, grp.exp_avg_sq, hp)
+        self.sinks = {}
+        self.model._remaps = None
+
+
+class _Holder:
+    """Minimal nn.Embedding stand-in for TableGroup (a shard buffer)."""
+
+    def __init__(self, w):
+        self.weight = w
+        self.num_embeddings, self.embedding_dim = w.shape

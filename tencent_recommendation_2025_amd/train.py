@@ -37,6 +37,8 @@ class Trainer:
 
     def step(self, batch):
         self.opt.zero_grad()
+        if hasattr(self.opt, 'prepare'):  # row-sharded tables: fetch this batch's rows from their owners
+            self.opt.prepare(batch)
         loss = self.compute_loss(batch)
         loss.backward()
         self.opt.step()
