@@ -7,6 +7,6 @@
 set -euo pipefail
 N=${1:-2}
 cd "$(dirname "$0")/.."
-exec python -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" --master-addr 127.0.0.1 \
+python -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" --master-addr 127.0.0.1 \
     --master-port "${PORT:-29531}" bench.py --gpus "$N" --backend gloo --steps 3 --warmup 1 \
     --cpu-baseline 0 --roofline-reps 2 "${@:2}"
