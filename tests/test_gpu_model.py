@@ -106,7 +106,8 @@ def test_dropin_step_matches_reference(golden, tag):
         # AdamW's first step moves each element by ~lr*sign(grad): compare to lr
         assert np.max(np.abs(got - want)) <= 2.05 * lr, name
         if live and not name.endswith('k_linear.bias'):
-            assert np.mean(np.abs(got - want) < 1e-6) > 0.97, name
+            # near-zero grads may flip AdamW's first-step sign: allow 3% (at least one element)
+            assert np.sum(np.abs(got - want) >= 1e-6) <= max(1, int(0.03 * got.size)), name
 
 
 def test_list_of_dicts_input_equals_tensor_input(golden, tmp_path):
