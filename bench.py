@@ -168,7 +168,10 @@ def main():
     pool = [S.make_batch(cfg, gen, dev) for _ in range(4)]
 
     for i in range(a.warmup):
+        if i == a.warmup - 1:
+            G.GATHER_TRACE = []          # capture the fused-gather launches of one real step
         trainer.step(pool[i % len(pool)])
+    trace, G.GATHER_TRACE = G.GATHER_TRACE, None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -185,12 +188,11 @@ def main():
     elapsed = float(t.item())
     final_loss = float(loss.float().item())
 
-    G.GATHER_TRACE = []
-    with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16):
-        seq, pos, neg, tt, ntt, nat, sf, pf, nf = pool[0]
-        model.log2feats(seq, tt, sf)
-    roof = gather_roofline(G.GATHER_TRACE, a.roofline_reps)
-    G.GATHER_TRACE = None
+    if not trace:  # --warmup 0: trace one extra, untimed step after the timed region
+        G.GATHER_TRACE = []
+        trainer.step(pool[0])
+        trace, G.GATHER_TRACE = G.GATHER_TRACE, None
+    roof = gather_roofline(trace, a.roofline_reps)
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline:

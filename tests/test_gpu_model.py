@@ -105,9 +105,12 @@ def test_dropin_step_matches_reference(golden, tag):
         got = p.detach().cpu().numpy()
         # AdamW's first step moves each element by ~lr*sign(grad): compare to lr
         assert np.max(np.abs(got - want)) <= 2.05 * lr, name
-        if live and not name.endswith('k_linear.bias'):
-            # near-zero grads may flip AdamW's first-step sign: allow 3% (at least one element)
-            assert np.sum(np.abs(got - want) >= 1e-6) <= max(1, int(0.03 * got.size)), name
+        if live and not name.endswith('k_linear.bias') and f'grad.{name}' in g.files:
+            # AdamW's first step moves by ~lr*sign(grad): elements whose reference grad is not tiny
+            # must land on the reference value; near-zero grads may flip sign
+            gr = g[f'grad.{name}']
+            firm = np.abs(gr) >= 0.05 * np.sqrt(np.mean(gr.astype(np.float64) ** 2))
+            assert np.mean(np.abs(got - want)[firm] < 1e-6) > 0.99, name
 
 
 def test_list_of_dicts_input_equals_tensor_input(golden, tmp_path):
