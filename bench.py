@@ -79,10 +79,21 @@ def gather_roofline(trace, reps):
     tt_bytes = n * 4 if tt is not None else 0
     alg = rows * D * es + n * D * len(lookups) * es + idx_bytes + tt_bytes
     gbps = alg / (ms * 1e-3) / 1e9
-    return {'bound': 'hbm', 'kernel': 'grk::k_gather (seq-side fused lookup)', 'achieved': round(gbps, 1),
-            'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': round(gbps / HBM_PEAK_GBPS, 4), 'traffic': None,
-            'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2),
-            'rows_per_launch': int(rows), 'features': len(lookups)}
+    res = {'bound': 'hbm', 'kernel': 'grk::k_gather (seq-side fused lookup)', 'achieved': round(gbps, 1),
+           'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': round(gbps / HBM_PEAK_GBPS, 4), 'traffic': None,
+           'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2),
+           'rows_per_launch': int(rows), 'features': len(lookups)}
+    # HBM bytes per launch from the committed rocprofv3 PMC passes of this same workload
+    pmc = os.path.join(REPO, 'profiles', 'r1_pmc_gather.json')
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            p = json.load(f)
+        if abs(p['write_bytes_per_launch'] - n * out.shape[1] * es) < 1e6:  # same output => same workload
+            res['traffic'] = int(p['traffic_bytes_per_launch'])
+            res['traffic_note'] = ('rocprofv3 PMC (profiles/r1_pmc_gather.json): FETCH_SIZE x2 + WRITE_SIZE; '
+                                   'reads of small/padding rows hit L2, so traffic < algorithmic bytes')
+            res['traffic_gbps'] = round(p['traffic_bytes_per_launch'] / (ms * 1e-3) / 1e9, 1)
+    return res
 
 
 def cpu_baseline(a, stats, types):
