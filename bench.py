@@ -88,7 +88,7 @@ def gather_roofline(trace, reps):
     if os.path.exists(pmc):
         with open(pmc) as f:
             p = json.load(f)
-        if abs(p['write_bytes_per_launch'] - n * out.shape[1] * es) < 1e6:  # same output => same workload
+        if abs(p['write_bytes_per_launch'] - n * D * len(lookups) * es) < 1e6:  # same output bytes => same workload
             res['traffic'] = int(p['traffic_bytes_per_launch'])
             res['traffic_note'] = ('rocprofv3 PMC (profiles/r1_pmc_gather.json): FETCH_SIZE x2 + WRITE_SIZE; '
                                    'reads of small/padding rows hit L2, so traffic < algorithmic bytes')

@@ -160,6 +160,11 @@ int grk_table_adamw(void* param, int param_dtype, float* exp_avg, float* exp_avg
  * Q/K/V are bf16 [B*T, ld] with head h at columns [h*hd, (h+1)*hd).
  * ------------------------------------------------------------------------ */
 enum { GRK_ATTN_SOFTMAX = 0, GRK_ATTN_HSTU = 1 };
+/* GRK_ACT_SILU: q/k/v point at PRE-activations (the uvqk projection output);
+ * the kernels apply SiLU on load (rounded to bf16, as F.silu on bf16) and
+ * the backward writes dq/dk/dv w.r.t. the pre-activations (x dSiLU), i.e.
+ * the HSTU `u, v, q, k = split(SiLU(uvqk(x)))` is fused away. */
+enum { GRK_ACT_NONE = 0, GRK_ACT_SILU = 1 };
 
 typedef struct grk_attn_args {
   int32_t kind;                    /* GRK_ATTN_*                                  */
@@ -175,7 +180,7 @@ typedef struct grk_attn_args {
   int32_t precise;                 /* 1: P / dS fed to MFMA as bf16 hi+lo pairs   */
   uint64_t seed;                   /* dropout stream                              */
   int32_t out_dtype;               /* GRK_F32 / GRK_BF16 for out, dq, dk, dv      */
-  int32_t pad_;
+  int32_t act;                     /* GRK_ACT_*: activation applied to q/k/v      */
 } grk_attn_args;
 
 /* out [B*T, ldo] (out_dtype); lse fp32 [B, H, T] (softmax: natural-log
@@ -189,6 +194,29 @@ int grk_attention_fwd(const grk_attn_args* a, void* out, int64_t ldo, float* lse
 int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
                       int dout_dtype, const float* lse, float* delta_ws, void* dq, int64_t lddq, void* dk,
                       int64_t lddk, void* dv, int64_t lddv, float* drab, void* stream);
+
+/* ------------------------------------------------------------------------
+ * HSTU output gate (north star; no reference -- oracle/hstu.py)
+ *   y = dropout(LayerNorm(o; gamma, beta, eps) * SiLU(u))
+ * the tail of the HSTU layer before out_linear, with u the first D columns of
+ * the uvqk pre-activation.  o, u, y, gy, dout, du: bf16 rows (16-byte
+ * aligned, strides multiples of 8); gamma/beta/dgamma/dbeta fp32 [dim];
+ * dim multiple of 8, <= 2048.  stats fp32 [rows, 2] = (mean, rstd) saved by
+ * the forward for the backward.  Dropout: counter hash of (seed, row, col),
+ * identical in both directions.
+ * ------------------------------------------------------------------------ */
+int grk_norm_gate_fwd(const void* o, int64_t ldo, const void* u, int64_t ldu, const float* gamma,
+                      const float* beta, float eps, int64_t rows, int dim, float dropout_p, uint64_t seed, void* y,
+                      int64_t ldy, float* stats, void* stream);
+
+size_t grk_norm_gate_bwd_workspace(int64_t rows, int dim);
+
+/* dout = dL/do, du = dL/du (w.r.t. the pre-activation u), dgamma/dbeta
+ * written (not accumulated); fixed-order, deterministic reductions. */
+int grk_norm_gate_bwd(const void* gy, int64_t ldgy, const void* o, int64_t ldo, const void* u, int64_t ldu,
+                      const float* gamma, const float* beta, const float* stats, int64_t rows, int dim,
+                      float dropout_p, uint64_t seed, void* dout, int64_t lddo, void* du, int64_t lddu,
+                      float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Pair logits + BCE (model/BaseLine/model.py:379-382; main.py:177-182)

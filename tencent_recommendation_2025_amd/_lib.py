@@ -51,10 +51,11 @@ class GrkAttnArgs(C.Structure):
                 ('v', C.c_void_p), ('ldq', C.c_int64), ('ldk', C.c_int64), ('ldv', C.c_int64),
                 ('key_valid', C.c_void_p), ('rab', C.c_void_p), ('scale', C.c_float), ('inv_n', C.c_float),
                 ('dropout_p', C.c_float), ('precise', C.c_int32), ('seed', C.c_uint64), ('out_dtype', C.c_int32),
-                ('pad_', C.c_int32)]
+                ('act', C.c_int32)]
 
 
 ATTN_SOFTMAX, ATTN_HSTU = 0, 1
+ACT_NONE, ACT_SILU = 0, 1
 
 
 class GrkError(RuntimeError):
@@ -76,6 +77,10 @@ SIGNATURES = {
     'grk_attention_fwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _P]),
     'grk_attention_bwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64, _P, _I64,
                                _P, _P]),
+    'grk_norm_gate_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _F, C.c_uint64, _P, _I64, _P, _P]),
+    'grk_norm_gate_bwd_workspace': (_SZ, [_I64, _I]),
+    'grk_norm_gate_bwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _P, _P, _I64, _I, _F, C.c_uint64, _P, _I64, _P,
+                               _I64, _P, _P, _P, _SZ, _P]),
     'grk_pair_logits_partials': (_SZ, [_I64]),
     'grk_sampled_softmax_workspace': (_SZ, [_I64]),
     'grk_sampled_softmax_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _I, _F, _P, _P, _P, _P, _SZ, _P]),

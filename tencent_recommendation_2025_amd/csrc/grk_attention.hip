@@ -42,6 +42,7 @@ struct AttnParams {
   int nb;
   int precise;
   int out_f32;
+  int act;  // GRK_ACT_SILU: q/k/v are pre-activations
   // forward
   void* out; int64_t ldo; float* lse;
   // backward
@@ -51,11 +52,6 @@ struct AttnParams {
   float* drab;
 };
 
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
-__device__ __forceinline__ float dsilu(float x) {
-  const float sg = 1.0f / (1.0f + __expf(-x));
-  return sg * (1.0f + x * (1.0f - sg));
-}
 
 // Counter-based dropout keep decision for element (b*H+h, q, k): identical
 // in forward and backward.
@@ -73,13 +69,14 @@ __device__ __forceinline__ bool drop_keep(unsigned long long seed, int bh, int q
 // image (zeros outside [0, T)).
 template <int HD>
 __device__ __forceinline__ void stage_rows(char* dst, const void* src, int64_t ld, int b, int T, int h, int r0,
-                                           bool f32) {
+                                           bool f32, bool act = false) {
   constexpr int NCH = HD / 8;
   for (int u = threadIdx.x; u < kChunk * NCH; u += blockDim.x) {
     const int row = u / NCH, c = u % NCH;
     const int t = r0 + row;
     const bool ok = t >= 0 && t < T;
     bf16x8 v = gload8_any(src, ((int64_t)b * T + (ok ? t : 0)) * ld + h * HD + c * 8, f32, ok);
+    if (act) v = silu8(v);
     *reinterpret_cast<uint4*>(dst + lds_off<HD>(row, c * 8)) = __builtin_bit_cast(uint4, v);
   }
 }
@@ -110,9 +107,12 @@ __device__ __forceinline__ void store4<bf16_t>(bf16_t* p, const float* v) {
 
 // Store an accumulated D^T tile set acc[NDT] (rows = feature d, lane = token)
 // to row `tok` of a [B*T, ld] output: lane holds d = dt*32 + 8g + 4hh + 0..3.
+// With dsrc (GRK_ACT_SILU) the value is the gradient w.r.t. the activation
+// and is multiplied by dSiLU(pre) read from the same position of dsrc.
 template <int HD, int NDT>
 __device__ __forceinline__ void store_rows(void* out, int64_t ld, bool f32, int64_t tok, int h, int hh,
-                                           const f32x16* acc, float mul, bool ok) {
+                                           const f32x16* acc, float mul, bool ok, const bf16_t* dsrc = nullptr,
+                                           int64_t ldsrc = 0) {
   if (!ok) return;
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
@@ -121,6 +121,13 @@ __device__ __forceinline__ void store_rows(void* out, int64_t ld, bool f32, int6
       const int d = dt * 32 + 8 * g + 4 * hh;
       if (d >= HD) continue;
       float v[4] = {acc[dt][4 * g] * mul, acc[dt][4 * g + 1] * mul, acc[dt][4 * g + 2] * mul, acc[dt][4 * g + 3] * mul};
+      if (dsrc) {
+        const uint2 pw = *reinterpret_cast<const uint2*>(dsrc + tok * ldsrc + h * HD + d);
+        v[0] *= dsilu(__uint_as_float(pw.x << 16));
+        v[1] *= dsilu(__uint_as_float(pw.x & 0xFFFF0000u));
+        v[2] *= dsilu(__uint_as_float(pw.y << 16));
+        v[3] *= dsilu(__uint_as_float(pw.y & 0xFFFF0000u));
+      }
       const int64_t off = tok * ld + h * HD + d;
       if (f32) store4<float>((float*)out + off, v);
       else store4<bf16_t>((bf16_t*)out + off, v);
@@ -151,7 +158,10 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
   bf16x8 qf[KS];
   const bf16_t* qrow = p.q + ((int64_t)b * T + (qok ? myq : 0)) * p.ldq + h * HD;
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) qf[ks] = gload8(qrow + 16 * ks + 8 * hh, qok);
+  for (int ks = 0; ks < KS; ++ks) {
+    qf[ks] = gload8(qrow + 16 * ks + 8 * hh, qok);
+    if (p.act) qf[ks] = silu8(qf[ks]);
+  }
 
   f32x16 o[NDT];
 #pragma unroll
@@ -166,8 +176,8 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
   const int kend = min(T, q0 + kBlockRows);
   for (int kc = kbeg; kc < kend; kc += kChunk) {
     __syncthreads();
-    stage_rows<HD>(Ks, p.k, p.ldk, b, T, h, kc, false);
-    stage_rows<HD>(Vs, p.v, p.ldv, b, T, h, kc, false);
+    stage_rows<HD>(Ks, p.k, p.ldk, b, T, h, kc, false, p.act);
+    stage_rows<HD>(Vs, p.v, p.ldv, b, T, h, kc, false, p.act);
     if (threadIdx.x < kChunk) {
       const int t = kc + threadIdx.x;
       kvs[threadIdx.x] = (t < T) && (!p.key_valid || p.key_valid[(int64_t)b * T + t]);
@@ -298,6 +308,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     qf[ks] = gload8(p.q + tok * p.ldq + h * HD + 16 * ks + 8 * hh, qok);
+    if (p.act) qf[ks] = silu8(qf[ks]);
     dof[ks] = gload8_any(p.dout, tok * p.lddo + h * HD + 16 * ks + 8 * hh, p.dout_f32, qok);
   }
   float lse2 = 0.f, dlt = 0.f;
@@ -317,8 +328,8 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
   const int kend = min(T, q0 + kBlockRows);
   for (int kc = kbeg; kc < kend; kc += kChunk) {
     __syncthreads();
-    stage_rows<HD>(Ks, p.k, p.ldk, b, T, h, kc, false);
-    stage_rows<HD>(Vs, p.v, p.ldv, b, T, h, kc, false);
+    stage_rows<HD>(Ks, p.k, p.ldk, b, T, h, kc, false, p.act);
+    stage_rows<HD>(Vs, p.v, p.ldv, b, T, h, kc, false, p.act);
     if (threadIdx.x < kChunk) {
       const int t = kc + threadIdx.x;
       kvs[threadIdx.x] = (t < T) && (!p.key_valid || p.key_valid[(int64_t)b * T + t]);
@@ -364,7 +375,8 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
       }
     }
   }
-  store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, (int64_t)b * T + myq, h, hh, acc, p.scale, qok);
+  store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, (int64_t)b * T + myq, h, hh, acc, p.scale, qok,
+                      p.act ? p.q : nullptr, p.ldq);
   if (KIND == 1) {
     __syncthreads();
     for (int j = threadIdx.x; j < p.nb; j += blockDim.x)
@@ -401,6 +413,10 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
   for (int ks = 0; ks < KS; ++ks) {
     kf[ks] = gload8(p.k + tok * p.ldk + h * HD + 16 * ks + 8 * hh, myk < T);
     vf[ks] = gload8(p.v + tok * p.ldv + h * HD + 16 * ks + 8 * hh, myk < T);
+    if (p.act) {
+      kf[ks] = silu8(kf[ks]);
+      vf[ks] = silu8(vf[ks]);
+    }
   }
   f32x16 dk[NDT], dv[NDT];
 #pragma unroll
@@ -413,7 +429,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
   const int qbeg = (max(k0, start) / 32) * 32;
   for (int qc = qbeg; qc < T; qc += kChunk) {
     __syncthreads();
-    stage_rows<HD>(Qs, p.q, p.ldq, b, T, h, qc, false);
+    stage_rows<HD>(Qs, p.q, p.ldq, b, T, h, qc, false, p.act);
     stage_rows<HD>(Ds, p.dout, p.lddo, b, T, h, qc, p.dout_f32);
     if (threadIdx.x < kChunk) {
       const int t = qc + threadIdx.x;
@@ -478,8 +494,8 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
     }
   }
   const int64_t otok = (int64_t)b * T + myk;
-  store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, otok, h, hh, dk, p.scale, myk < T);
-  store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, 1.f, myk < T);
+  store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, otok, h, hh, dk, p.scale, myk < T, p.act ? p.k : nullptr, p.ldk);
+  store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, 1.f, myk < T, p.act ? p.v : nullptr, p.ldv);
 }
 
 template <int HD>
@@ -529,6 +545,7 @@ static int fill_params(const grk_attn_args* a, AttnParams* p) {
   GRK_CHECK_ARG(a->dropout_p >= 0.f && a->dropout_p < 1.f, "dropout_p must be in [0, 1)");
   GRK_CHECK_ARG(a->kind == GRK_ATTN_SOFTMAX || a->dropout_p == 0.f, "hstu attention has no dropout");
   GRK_CHECK_ARG(a->out_dtype == GRK_F32 || a->out_dtype == GRK_BF16, "out_dtype must be GRK_F32 / GRK_BF16");
+  GRK_CHECK_ARG(a->act == GRK_ACT_NONE || a->act == GRK_ACT_SILU, "act must be GRK_ACT_NONE / GRK_ACT_SILU");
   memset(p, 0, sizeof(*p));
   p->kind = a->kind; p->B = a->batch; p->H = a->heads; p->T = a->seq_len;
   p->q = (const bf16_t*)a->q; p->k = (const bf16_t*)a->k; p->v = (const bf16_t*)a->v;
@@ -537,6 +554,7 @@ static int fill_params(const grk_attn_args* a, AttnParams* p) {
   p->scale = a->scale; p->inv_n = a->inv_n; p->dropout_p = a->dropout_p; p->seed = a->seed;
   p->rab = a->rab; p->nb = a->num_buckets;
   p->precise = a->precise; p->out_f32 = a->out_dtype == GRK_F32;
+  p->act = a->act;
   return GRK_OK;
 }
 

@@ -1,0 +1,312 @@
+// HSTU output gate for gfx950: y = dropout(LayerNorm(o) * SiLU(u)), its
+// backward, and the deterministic dgamma/dbeta column sums.
+//
+// Replaces (north star; no reference -- oracle/hstu.py):
+//   y = out_linear(dropout(attn_norm(HSTU-attn(q, k, v)) * u)),  u = SiLU(pre_u)
+// which in eager PyTorch is a silu, a dtype cast, a LayerNorm, a multiply and
+// a dropout (forward) and ~10 elementwise/reduction kernels (backward), each
+// a full [N, D] HBM round trip.  Here: one pass over o / u / y forward, one
+// pass over gy / o / u / do / du backward.
+//
+// Layout: o, u, y, gy, do, du are bf16 rows of length D with row strides
+// (u and du are the first D columns of the [N, 4D] pre-activation / its grad).
+// One 64-lane wave per row; lane owns the 16-byte vectors c = lane + 64 j.
+// LayerNorm statistics (mean, rstd) are saved per row by the forward.
+#include "grk_common.h"
+
+namespace grk {
+
+constexpr int kNgWaves = 4;        // waves per workgroup
+constexpr int kNgBwdBlocks = 512;  // fixed backward grid -> fixed reduction order
+
+struct NGParams {
+  const bf16_t* o; int64_t ldo;
+  const bf16_t* u; int64_t ldu;
+  const float* gamma; const float* beta;
+  float eps;
+  int64_t rows; int dim;
+  float dropout_p; unsigned long long seed;
+  bf16_t* y; int64_t ldy;
+  float* stats;  // [rows, 2] = mean, rstd
+  // backward
+  const bf16_t* gy; int64_t ldgy;
+  bf16_t* dout; int64_t lddo;
+  bf16_t* du; int64_t lddu;
+  float* partial;  // [gridDim.x, 2, dim]
+  float* dgamma; float* dbeta;
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// Counter-based dropout decision for element (row, col); identical in fwd/bwd.
+__device__ __forceinline__ bool ng_keep(unsigned long long seed, int64_t row, int col, int dim, float p) {
+  unsigned long long x = seed ^ ((unsigned long long)(row * dim + col) * 0x9E3779B97F4A7C15ull);
+  x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27; x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (float)(x >> 40) * (1.0f / 16777216.0f) >= p;
+}
+
+__device__ __forceinline__ void load8(const bf16_t* p, float* f) {
+  const uint4 w = *reinterpret_cast<const uint4*>(p);
+  const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(ws[i] << 16);
+    f[2 * i + 1] = __uint_as_float(ws[i] & 0xFFFF0000u);
+  }
+}
+
+__device__ __forceinline__ void store8(bf16_t* p, const float* f) {
+  uint4 w;
+  unsigned* ws = &w.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ws[i] = (unsigned)f32_to_bf16(f[2 * i]) | ((unsigned)f32_to_bf16(f[2 * i + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = w;
+}
+
+__device__ __forceinline__ void load8f(const float* p, float* f) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+// dropout multiplier of the 8 elements starting at column c8
+__device__ __forceinline__ void keep8(const NGParams& p, int64_t row, int c8, float* m) {
+  const float rk = 1.0f / (1.0f - p.dropout_p);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) m[e] = p.dropout_p > 0.f ? (ng_keep(p.seed, row, c8 + e, p.dim, p.dropout_p) ? rk : 0.f) : 1.f;
+}
+
+// ------------------------------------------------------------------ forward --
+template <int VPL>
+__global__ void __launch_bounds__(64 * kNgWaves) k_ng_fwd(NGParams p) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kNgWaves + (threadIdx.x >> 6);
+  if (row >= p.rows) return;
+  const int nv = p.dim >> 3;
+  float x[VPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nv) {
+      load8(p.o + row * p.ldo + 8 * c, x[j]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += x[j][e];
+    }
+  }
+  const float inv_d = 1.0f / (float)p.dim;
+  const float mean = wave_sum(s) * inv_d;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j)
+    if (lane + 64 * j < nv)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = x[j][e] - mean;
+        q += d * d;
+      }
+  const float rstd = rsqrtf(wave_sum(q) * inv_d + p.eps);
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c >= nv) continue;
+    float u[8], g[8], b[8], m[8], y[8];
+    load8(p.u + row * p.ldu + 8 * c, u);
+    load8f(p.gamma + 8 * c, g);
+    load8f(p.beta + 8 * c, b);
+    keep8(p, row, 8 * c, m);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      // SiLU(u) rounded to bf16 first: u is the bf16 activation of the reference formulation
+      const float su = bf16_to_f32(f32_to_bf16(silu(u[e])));
+      y[e] = ((x[j][e] - mean) * rstd * g[e] + b[e]) * su * m[e];
+    }
+    store8(p.y + row * p.ldy + 8 * c, y);
+  }
+  if (lane == 0 && p.stats) {
+    p.stats[2 * row] = mean;
+    p.stats[2 * row + 1] = rstd;
+  }
+}
+
+// ----------------------------------------------------------------- backward --
+// zhat = (o - mean) rstd, z = zhat g + b, su = SiLU(u), m = dropout multiplier
+//   gz = gy su m          du = gy z m dSiLU(u)
+//   dgamma += gz zhat     dbeta += gz
+//   do = rstd (gz g - mean(gz g) - zhat mean(gz g zhat))
+template <int VPL>
+__global__ void __launch_bounds__(64 * kNgWaves) k_ng_bwd(NGParams p) {
+  __shared__ float red[2 * 64 * VPL * 8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nv = p.dim >> 3;
+  const float inv_d = 1.0f / (float)p.dim;
+  float dg[VPL][8], db[VPL][8], g[VPL][8];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { dg[j][e] = 0.f; db[j][e] = 0.f; g[j][e] = 0.f; }
+    if (c < nv) load8f(p.gamma + 8 * c, g[j]);
+  }
+  const int64_t stride = (int64_t)gridDim.x * kNgWaves;
+  for (int64_t row = (int64_t)blockIdx.x * kNgWaves + wave; row < p.rows; row += stride) {
+    const float mean = p.stats[2 * row], rstd = p.stats[2 * row + 1];
+    float zh[VPL][8], gzg[VPL][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c >= nv) continue;
+      float o[8], u[8], gy[8], b[8], m[8], du[8];
+      load8(p.o + row * p.ldo + 8 * c, o);
+      load8(p.u + row * p.ldu + 8 * c, u);
+      load8(p.gy + row * p.ldgy + 8 * c, gy);
+      load8f(p.beta + 8 * c, b);
+      keep8(p, row, 8 * c, m);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float su = bf16_to_f32(f32_to_bf16(silu(u[e])));
+        zh[j][e] = (o[e] - mean) * rstd;
+        const float z = zh[j][e] * g[j][e] + b[e];
+        const float gm = gy[e] * m[e];
+        const float gz = gm * su;
+        du[e] = gm * z * dsilu(u[e]);
+        dg[j][e] += gz * zh[j][e];
+        db[j][e] += gz;
+        gzg[j][e] = gz * g[j][e];
+        s1 += gzg[j][e];
+        s2 += gzg[j][e] * zh[j][e];
+      }
+      store8(p.du + row * p.lddu + 8 * c, du);
+    }
+    s1 = wave_sum(s1) * inv_d;
+    s2 = wave_sum(s2) * inv_d;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c >= nv) continue;
+      float d[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = rstd * (gzg[j][e] - s1 - zh[j][e] * s2);
+      store8(p.dout + row * p.lddo + 8 * c, d);
+    }
+  }
+  // block partials: waves add in fixed order
+  for (int w = 0; w < kNgWaves; ++w) {
+    if (wave == w)
+#pragma unroll
+      for (int j = 0; j < VPL; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int i = (lane + 64 * j) * 8 + e;
+          red[i] = (w == 0 ? 0.f : red[i]) + dg[j][e];
+          red[64 * VPL * 8 + i] = (w == 0 ? 0.f : red[64 * VPL * 8 + i]) + db[j][e];
+        }
+    __syncthreads();
+  }
+  float* part = p.partial + (int64_t)blockIdx.x * 2 * p.dim;
+  for (int i = threadIdx.x; i < p.dim; i += blockDim.x) {
+    part[i] = red[i];
+    part[p.dim + i] = red[64 * VPL * 8 + i];
+  }
+}
+
+// dgamma | dbeta = column sums of the block partials, blocks in order.
+__global__ void __launch_bounds__(256) k_ng_colsum(NGParams p, int nblocks) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * p.dim) return;
+  float acc = 0.f;
+  for (int bk = 0; bk < nblocks; ++bk) acc += p.partial[(int64_t)bk * 2 * p.dim + i];
+  if (i < p.dim) p.dgamma[i] = acc;
+  else p.dbeta[i - p.dim] = acc;
+}
+
+static int ng_blocks_bwd(int64_t rows) {
+  int64_t need = (rows + kNgWaves - 1) / kNgWaves;
+  return (int)(need < kNgBwdBlocks ? (need < 1 ? 1 : need) : kNgBwdBlocks);
+}
+
+static int ng_check(const NGParams& p) {
+  GRK_CHECK_ARG(p.rows >= 0, "rows must be >= 0");
+  GRK_CHECK_ARG(p.dim > 0 && p.dim % 8 == 0 && p.dim <= 2048, "dim must be a multiple of 8 in [8, 2048]");
+  GRK_CHECK_ARG(p.gamma && p.beta, "gamma/beta required");
+  GRK_CHECK_ARG(p.dropout_p >= 0.f && p.dropout_p < 1.f, "dropout_p must be in [0, 1)");
+  GRK_CHECK_ARG(p.rows == 0 || (p.o && p.u), "o/u required");
+  GRK_CHECK_ARG(p.ldo >= p.dim && p.ldu >= p.dim && p.ldo % 8 == 0 && p.ldu % 8 == 0,
+                "row strides must be >= dim and multiples of 8");
+  GRK_CHECK_ARG(((uintptr_t)p.o | (uintptr_t)p.u | (uintptr_t)p.gamma | (uintptr_t)p.beta) % 16 == 0,
+                "o/u/gamma/beta must be 16-byte aligned");
+  return GRK_OK;
+}
+
+}  // namespace grk
+
+using namespace grk;
+
+extern "C" int grk_norm_gate_fwd(const void* o, int64_t ldo, const void* u, int64_t ldu, const float* gamma,
+                                 const float* beta, float eps, int64_t rows, int dim, float dropout_p, uint64_t seed,
+                                 void* y, int64_t ldy, float* stats, void* stream) {
+  clear_error();
+  NGParams p;
+  memset(&p, 0, sizeof(p));
+  p.o = (const bf16_t*)o; p.ldo = ldo; p.u = (const bf16_t*)u; p.ldu = ldu;
+  p.gamma = gamma; p.beta = beta; p.eps = eps; p.rows = rows; p.dim = dim;
+  p.dropout_p = dropout_p; p.seed = seed; p.y = (bf16_t*)y; p.ldy = ldy; p.stats = stats;
+  int rc = ng_check(p);
+  if (rc) return rc;
+  GRK_CHECK_ARG(rows == 0 || (y && ldy >= dim && ldy % 8 == 0 && (uintptr_t)y % 16 == 0), "bad y / ldy");
+  if (rows == 0) return GRK_OK;
+  const unsigned grid = (unsigned)((rows + kNgWaves - 1) / kNgWaves);
+  hipStream_t s = (hipStream_t)stream;
+  const int vpl = (dim / 8 + 63) / 64;
+  if (vpl == 1) k_ng_fwd<1><<<grid, 64 * kNgWaves, 0, s>>>(p);
+  else if (vpl == 2) k_ng_fwd<2><<<grid, 64 * kNgWaves, 0, s>>>(p);
+  else k_ng_fwd<4><<<grid, 64 * kNgWaves, 0, s>>>(p);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+extern "C" size_t grk_norm_gate_bwd_workspace(int64_t rows, int dim) {
+  return (size_t)ng_blocks_bwd(rows) * 2 * (size_t)(dim > 0 ? dim : 0) * sizeof(float);
+}
+
+extern "C" int grk_norm_gate_bwd(const void* gy, int64_t ldgy, const void* o, int64_t ldo, const void* u,
+                                 int64_t ldu, const float* gamma, const float* beta, const float* stats, int64_t rows,
+                                 int dim, float dropout_p, uint64_t seed, void* dout, int64_t lddo, void* du,
+                                 int64_t lddu, float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  NGParams p;
+  memset(&p, 0, sizeof(p));
+  p.o = (const bf16_t*)o; p.ldo = ldo; p.u = (const bf16_t*)u; p.ldu = ldu;
+  p.gamma = gamma; p.beta = beta; p.rows = rows; p.dim = dim;
+  p.dropout_p = dropout_p; p.seed = seed; p.stats = const_cast<float*>(stats);
+  p.gy = (const bf16_t*)gy; p.ldgy = ldgy; p.dout = (bf16_t*)dout; p.lddo = lddo; p.du = (bf16_t*)du; p.lddu = lddu;
+  p.partial = (float*)ws; p.dgamma = dgamma; p.dbeta = dbeta;
+  int rc = ng_check(p);
+  if (rc) return rc;
+  GRK_CHECK_ARG(dgamma && dbeta, "dgamma/dbeta required");
+  GRK_CHECK_ARG(ws && ws_bytes >= grk_norm_gate_bwd_workspace(rows, dim), "workspace too small");
+  GRK_CHECK_ARG(rows == 0 || (gy && dout && du && stats), "gy/dout/du/stats required");
+  GRK_CHECK_ARG(ldgy >= dim && lddo >= dim && lddu >= dim && ldgy % 8 == 0 && lddo % 8 == 0 && lddu % 8 == 0,
+                "row strides must be >= dim and multiples of 8");
+  GRK_CHECK_ARG(((uintptr_t)gy | (uintptr_t)dout | (uintptr_t)du) % 16 == 0, "gy/dout/du must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = ng_blocks_bwd(rows);
+  if (rows > 0) {
+    const int vpl = (dim / 8 + 63) / 64;
+    if (vpl == 1) k_ng_bwd<1><<<nb, 64 * kNgWaves, 0, s>>>(p);
+    else if (vpl == 2) k_ng_bwd<2><<<nb, 64 * kNgWaves, 0, s>>>(p);
+    else k_ng_bwd<4><<<nb, 64 * kNgWaves, 0, s>>>(p);
+    GRK_LAUNCH_CHECK();
+  } else {
+    GRK_CHECK_HIP(hipMemsetAsync(ws, 0, grk_norm_gate_bwd_workspace(rows, dim), s));
+  }
+  k_ng_colsum<<<(2 * dim + 255) / 256, 256, 0, s>>>(p, nb);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}

@@ -82,5 +82,12 @@ __device__ __forceinline__ bf16x8 gload8_any(const void* base, int64_t off, bool
   return r;
 }
 
+// SiLU of each element, computed in fp32 and rounded to bf16 (= F.silu on bf16).
+__device__ __forceinline__ bf16x8 silu8(bf16x8 x) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = static_cast<__bf16>(silu(static_cast<float>(x[j])));
+  return r;
+}
 
 }  // namespace grk

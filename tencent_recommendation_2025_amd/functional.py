@@ -148,56 +148,55 @@ def softmax_mha(qkv, key_valid, B, T, H, hd, dropout_p=0.0, seed=0, precise=None
 
 
 class _HSTUCoreFn(torch.autograd.Function):
-    """y = LayerNorm(HSTU-attention(SiLU(pre))) * u, with u|v|q|k = SiLU(pre)."""
+    """y = dropout(LayerNorm(HSTU-attn(q, k, v)) * u), with u|v|q|k = SiLU(pre).
+
+    Three kernels forward, two backward, no eager elementwise glue:
+      attention (SiLU applied to q/k/v on load)        -> o
+      norm gate (LayerNorm(o) * SiLU(u), dropout)       -> y, (mean, rstd)
+    backward:
+      norm gate bwd -> do, dpre[:, :D] (x dSiLU), dgamma, dbeta
+      attention bwd -> dpre[:, D:] (dq/dk/dv x dSiLU written in place), drab
+    """
 
     @staticmethod
-    def forward(ctx, pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps, precise):
+    def forward(ctx, pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps, precise, dropout_p, seed):
         D = H * hd
-        act = F.silu(pre.to(torch.bfloat16)).contiguous()
-        args = K.attn_args(L.ATTN_HSTU, act[:, 2 * D:3 * D], act[:, 3 * D:], act[:, D:2 * D], B, T, H, hd,
-                           key_valid=key_valid, scale=hd ** -0.5, rab=rab.float().contiguous(), inv_n=inv_n,
-                           precise=precise, out_dtype=torch.bfloat16)
+        pb = pre.to(torch.bfloat16).contiguous()
+        rab32 = rab.float().contiguous()
+        args = K.attn_args(L.ATTN_HSTU, pb[:, 2 * D:3 * D], pb[:, 3 * D:], pb[:, D:2 * D], B, T, H, hd,
+                           key_valid=key_valid, scale=hd ** -0.5, rab=rab32, inv_n=inv_n, precise=precise,
+                           out_dtype=torch.bfloat16, act='silu')
         o = torch.empty(B * T, D, dtype=torch.bfloat16, device=pre.device)
         K.attention_fwd(args, o)
-        z = F.layer_norm(o.float(), (D,), ln_w.float(), ln_b.float(), eps)
-        y = (z * act[:, :D].float()).to(pre.dtype if pre.dtype != torch.float32 else torch.float32)
-        ctx.save_for_backward(pre, o, rab, ln_w, ln_b, key_valid)
-        ctx.meta = (B, T, H, hd, inv_n, eps, precise)
-        return y
+        w32, b32 = ln_w.float().contiguous(), ln_b.float().contiguous()
+        y, stats = K.norm_gate_fwd(o, pb[:, :D], w32, b32, eps, dropout_p, seed)
+        ctx.save_for_backward(pb, o, stats, rab32, w32, b32, key_valid)
+        ctx.meta = (B, T, H, hd, inv_n, precise, dropout_p, seed, pre.dtype, rab.dtype, ln_w.dtype, ln_b.dtype)
+        return y if pre.dtype == torch.bfloat16 else y.to(pre.dtype)
 
     @staticmethod
     def backward(ctx, gy):
-        pre, o, rab, ln_w, ln_b, key_valid = ctx.saved_tensors
-        B, T, H, hd, inv_n, eps, precise = ctx.meta
+        pb, o, stats, rab32, w32, b32, key_valid = ctx.saved_tensors
+        B, T, H, hd, inv_n, precise, dropout_p, seed, pdt, rdt, wdt, bdt = ctx.meta
         D = H * hd
-        act = F.silu(pre.to(torch.bfloat16)).contiguous()
-        u = act[:, :D].float()
-        gy = gy.float()
-        with torch.enable_grad():
-            od = o.detach().float().requires_grad_(True)
-            w = ln_w.detach().float().requires_grad_(True)
-            b = ln_b.detach().float().requires_grad_(True)
-            z = F.layer_norm(od, (D,), w, b, eps)
-            do, dw, db = torch.autograd.grad(z, (od, w, b), gy * u)
-        dact = torch.empty(B * T, 4 * D, dtype=torch.bfloat16, device=pre.device)
-        dact[:, :D] = gy * z.detach()
-        rab32 = rab.float().contiguous()
+        gy = gy.to(torch.bfloat16)
+        gy = gy if gy.is_contiguous() else gy.contiguous()
+        dpre = torch.empty(B * T, 4 * D, dtype=torch.bfloat16, device=pb.device)
+        do, _, dw, db = K.norm_gate_bwd(gy, o, pb[:, :D], w32, b32, stats, dropout_p, seed, du=dpre[:, :D])
         drab = torch.zeros_like(rab32)
-        args = K.attn_args(L.ATTN_HSTU, act[:, 2 * D:3 * D], act[:, 3 * D:], act[:, D:2 * D], B, T, H, hd,
+        args = K.attn_args(L.ATTN_HSTU, pb[:, 2 * D:3 * D], pb[:, 3 * D:], pb[:, D:2 * D], B, T, H, hd,
                            key_valid=key_valid, scale=hd ** -0.5, rab=rab32, inv_n=inv_n, precise=precise,
-                           out_dtype=torch.bfloat16)
-        K.attention_bwd(args, None, do.to(torch.bfloat16), None, None, dact[:, 2 * D:3 * D], dact[:, 3 * D:],
-                        dact[:, D:2 * D], drab)
-        p32 = pre.float()
-        sg = torch.sigmoid(p32)
-        dpre = (dact.float() * (sg * (1 + p32 * (1 - sg)))).to(pre.dtype)
-        return (dpre, drab.to(rab.dtype), dw.to(ln_w.dtype), db.to(ln_b.dtype), None, None, None, None, None, None,
-                None, None)
+                           out_dtype=torch.bfloat16, act='silu')
+        K.attention_bwd(args, None, do, None, None, dpre[:, 2 * D:3 * D], dpre[:, 3 * D:], dpre[:, D:2 * D], drab)
+        return (dpre if pdt == torch.bfloat16 else dpre.to(pdt), drab.to(rdt), dw.to(wdt), db.to(bdt),
+                None, None, None, None, None, None, None, None, None, None)
 
 
 @_disable
-def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, precise=False):
-    return _HSTUCoreFn.apply(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, float(inv_n), float(eps), bool(precise))
+def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, precise=False, dropout_p=0.0, seed=0):
+    """Fused HSTU layer core on the [B*T, 4D] uvqk pre-activation (see _HSTUCoreFn)."""
+    return _HSTUCoreFn.apply(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, float(inv_n), float(eps), bool(precise),
+                             float(dropout_p), int(seed))
 
 
 # ---------------------------------------------------------------- logits ----

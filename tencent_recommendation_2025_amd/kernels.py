@@ -184,8 +184,11 @@ def _col_view_ok(t, name):
 
 
 def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, inv_n=1.0, dropout_p=0.0, seed=0,
-              precise=False, out_dtype=torch.bfloat16):
-    """Build grk_attn_args for bf16 [B*T, ld] column views q/k/v (head h at cols h*hd)."""
+              precise=False, out_dtype=torch.bfloat16, act=None):
+    """Build grk_attn_args for bf16 [B*T, ld] column views q/k/v (head h at cols h*hd).
+
+    act="silu": q/k/v are pre-activations; SiLU is applied on load and the
+    backward's dq/dk/dv are gradients w.r.t. the pre-activations."""
     for t, n in ((q, 'q'), (k, 'k'), (v, 'v')):
         _col_view_ok(t, n)
         if t.shape[0] != B * T or t.shape[1] < H * hd:
@@ -202,7 +205,8 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
         scale = hd ** -0.5
     return L.GrkAttnArgs(kind, B, H, T, hd, nb, q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0),
                          v.stride(0), _ptr(key_valid), _ptr(rab), float(scale), float(inv_n), float(dropout_p),
-                         int(bool(precise)), int(seed) & (2 ** 64 - 1), L.dtype_code(out_dtype), 0)
+                         int(bool(precise)), int(seed) & (2 ** 64 - 1), L.dtype_code(out_dtype),
+                         {None: L.ACT_NONE, 'silu': L.ACT_SILU}[act])
 
 
 def attention_fwd(args, out, lse=None):
@@ -225,6 +229,52 @@ def attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab=None):
                                    dq.stride(0), dk.data_ptr(), dk.stride(0), dv.data_ptr(), dv.stride(0), _ptr(drab),
                                    L.stream_ptr(dout.device))
     L.check(rc, 'grk_attention_bwd')
+
+
+# ------------------------------------------------------------- HSTU gate
+def _bf16_rows(t, name, dim):
+    if t.dtype != torch.bfloat16 or t.dim() != 2 or t.stride(1) != 1 or t.stride(0) % 8 or t.shape[1] < dim:
+        raise L.GrkError(f'{name} must be a bf16 row-major [N, >={dim}] matrix with row stride % 8 == 0')
+    if t.data_ptr() % 16:
+        raise L.GrkError(f'{name} must be 16-byte aligned')
+    return t.data_ptr(), t.stride(0)
+
+
+def norm_gate_fwd(o, u, gamma, beta, eps, dropout_p=0.0, seed=0, y=None):
+    """y = dropout(LayerNorm(o) * SiLU(u)) (grk_norm_gate_fwd).  Returns (y bf16 [N, D], stats fp32 [N, 2])."""
+    _require_cuda(o, u, gamma, beta)
+    N, D = o.shape[0], gamma.shape[0]
+    dev = o.device
+    if y is None:
+        y = torch.empty(N, D, dtype=torch.bfloat16, device=dev)
+    stats = torch.empty(N, 2, dtype=torch.float32, device=dev)
+    (op, ol), (up, ul), (yp, yl) = _bf16_rows(o, 'o', D), _bf16_rows(u, 'u', D), _bf16_rows(y, 'y', D)
+    rc = L.lib().grk_norm_gate_fwd(op, ol, up, ul, gamma.data_ptr(), beta.data_ptr(), float(eps), N, D,
+                                   float(dropout_p), int(seed) & (2 ** 64 - 1), yp, yl, stats.data_ptr(),
+                                   L.stream_ptr(dev))
+    L.check(rc, 'grk_norm_gate_fwd')
+    return y, stats
+
+
+def norm_gate_bwd(gy, o, u, gamma, beta, stats, dropout_p=0.0, seed=0, dout=None, du=None):
+    """Gradients of norm_gate_fwd: (dout bf16 [N, D], du bf16 [N, D] w.r.t. pre-activation u, dgamma, dbeta fp32)."""
+    _require_cuda(gy, o, u, gamma, beta, stats)
+    N, D = o.shape[0], gamma.shape[0]
+    dev = o.device
+    if dout is None:
+        dout = torch.empty(N, D, dtype=torch.bfloat16, device=dev)
+    if du is None:
+        du = torch.empty(N, D, dtype=torch.bfloat16, device=dev)
+    dgamma = torch.empty(D, dtype=torch.float32, device=dev)
+    dbeta = torch.empty(D, dtype=torch.float32, device=dev)
+    ws = torch.empty(max(L.lib().grk_norm_gate_bwd_workspace(N, D), 4), dtype=torch.uint8, device=dev)
+    ptrs = [_bf16_rows(t, n, D) for t, n in ((gy, 'gy'), (o, 'o'), (u, 'u'), (dout, 'dout'), (du, 'du'))]
+    (gp, gl), (op, ol), (up, ul), (dp, dl), (dup, dul) = ptrs
+    rc = L.lib().grk_norm_gate_bwd(gp, gl, op, ol, up, ul, gamma.data_ptr(), beta.data_ptr(), stats.data_ptr(), N, D,
+                                   float(dropout_p), int(seed) & (2 ** 64 - 1), dp, dl, dup, dul, dgamma.data_ptr(),
+                                   dbeta.data_ptr(), ws.data_ptr(), ws.numel(), L.stream_ptr(dev))
+    L.check(rc, 'grk_norm_gate_bwd')
+    return dout, du, dgamma, dbeta
 
 
 # -------------------------------------------------------------- pair logits

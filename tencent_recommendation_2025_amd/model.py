@@ -87,6 +87,10 @@ class HSTUAttention(torch.nn.Module):
 
         u, v, q, k = split(SiLU(uvqk(x)))
         y = out_linear(dropout(LayerNorm(HSTU-attn(q, k, v, rab)) * u))
+
+    The SiLU, LayerNorm, gating and dropout run inside the grk kernels
+    (functional.hstu_core); dropout uses grk's counter-hash mask, not torch's
+    Philox stream.
     """
 
     def __init__(self, hidden_units, num_heads, dropout_rate, num_buckets):
@@ -105,9 +109,10 @@ class HSTUAttention(torch.nn.Module):
         if key_valid is None:
             key_valid = key_valid_from_mask(attn_mask, B, T)
         pre = self.uvqk(query).reshape(B * T, 4 * D)
+        p = self.dropout_rate if self.training else 0.0
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
         y = G.hstu_core(pre, self.rab, self.attn_norm.weight, self.attn_norm.bias, key_valid, B, T,
-                        self.num_heads, self.head_dim, 1.0 / T, self.attn_norm.eps)
-        y = F.dropout(y, self.dropout_rate, self.training)
+                        self.num_heads, self.head_dim, 1.0 / T, self.attn_norm.eps, dropout_p=p, seed=seed)
         return self.out_linear(y.view(B, T, D)), None
 
 
