@@ -53,9 +53,14 @@ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+// sigmoid via the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp),
+// no IEEE division; saturates cleanly to 0 / 1 for large |x|.
+__device__ __forceinline__ float sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
+__device__ __forceinline__ float silu(float x) { return x * sigmoid_fast(x); }
 __device__ __forceinline__ float dsilu(float x) {
-  const float sg = 1.0f / (1.0f + __expf(-x));
+  const float sg = sigmoid_fast(x);
   return sg * (1.0f + x * (1.0f - sg));
 }
 

@@ -216,14 +216,28 @@ __global__ void __launch_bounds__(64 * kNgWaves) k_ng_bwd(NGParams p) {
   }
 }
 
-// dgamma | dbeta = column sums of the block partials, blocks in order.
-__global__ void __launch_bounds__(256) k_ng_colsum(NGParams p, int nblocks) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * p.dim) return;
+// dgamma | dbeta = column sums of the block partials in a fixed order: 64
+// columns per workgroup, 16 row groups each summing a strided subset of the
+// blocks, then the 16 group sums added in order.
+constexpr int kColGroups = 16;
+__global__ void __launch_bounds__(64 * kColGroups) k_ng_colsum(NGParams p, int nblocks) {
+  __shared__ float part[kColGroups][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + cl;
   float acc = 0.f;
-  for (int bk = 0; bk < nblocks; ++bk) acc += p.partial[(int64_t)bk * 2 * p.dim + i];
-  if (i < p.dim) p.dgamma[i] = acc;
-  else p.dbeta[i - p.dim] = acc;
+  if (i < 2 * p.dim) {
+#pragma unroll 8
+    for (int bk = grp; bk < nblocks; bk += kColGroups) acc += p.partial[(int64_t)bk * 2 * p.dim + i];
+  }
+  part[grp][cl] = acc;
+  __syncthreads();
+  if (grp == 0 && i < 2 * p.dim) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < kColGroups; ++g) t += part[g][cl];
+    if (i < p.dim) p.dgamma[i] = t;
+    else p.dbeta[i - p.dim] = t;
+  }
 }
 
 static int ng_blocks_bwd(int64_t rows) {
@@ -306,7 +320,7 @@ extern "C" int grk_norm_gate_bwd(const void* gy, int64_t ldgy, const void* o, in
   } else {
     GRK_CHECK_HIP(hipMemsetAsync(ws, 0, grk_norm_gate_bwd_workspace(rows, dim), s));
   }
-  k_ng_colsum<<<(2 * dim + 255) / 256, 256, 0, s>>>(p, nb);
+  k_ng_colsum<<<(2 * dim + 63) / 64, 64 * kColGroups, 0, s>>>(p, nb);
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }

@@ -39,8 +39,13 @@ class LookupSpec:
 
 
 class _FeatureLookupFn(torch.autograd.Function):
+    """One fused gather into a [num_tokens, out_ld] buffer, returned as column
+    blocks (``splits``) so each consumer (itemdnn / userdnn / position add)
+    back-propagates into its own block: no full-width gradient buffer is ever
+    materialised or accumulated."""
+
     @staticmethod
-    def forward(ctx, specs, token_type, seq_len, num_tokens, out_ld, extra, extra_col, *weights):
+    def forward(ctx, specs, token_type, seq_len, num_tokens, out_ld, extra, extra_col, splits, *weights):
         dt = specs[0].ref.weight.dtype
         dev = specs[0].ref.weight.device
         out = torch.empty(num_tokens, out_ld, dtype=dt, device=dev)
@@ -51,51 +56,71 @@ class _FeatureLookupFn(torch.autograd.Function):
             GATHER_TRACE.append((lookups, out, num_tokens, token_type, seq_len))
         if extra is not None:
             out[:, extra_col:extra_col + extra.shape[1]] = extra.to(dt)
-        ctx.specs, ctx.token_type, ctx.seq_len = specs, token_type, seq_len
+        ctx.specs, ctx.token_type, ctx.seq_len, ctx.splits = specs, token_type, seq_len, splits
         ctx.extra_info = None if extra is None else (extra_col, extra.shape[1], extra.dtype)
         ctx.n_weights = len(weights)
         ctx.weight_ids = [id(w) for w in weights]
-        return out
+        return tuple(out[:, a:b] for a, b in splits)
 
     @staticmethod
-    def backward(ctx, gout):
-        gout = gout.contiguous()
-        specs = ctx.specs
+    def backward(ctx, *gsplits):
+        specs, splits = ctx.specs, ctx.splits
         D = specs[0].ref.weight.shape[1]
+
+        def locate(col, width):
+            """(grad block, column inside it) holding output columns [col, col+width); None if no gradient."""
+            for (a, b), g in zip(splits, gsplits):
+                if a <= col and col + width <= b:
+                    if g is None:
+                        return None, 0
+                    return (g if g.stride(-1) == 1 else g.contiguous()), col - a
+            raise RuntimeError(f'output columns [{col}, {col + width}) are not inside one split')
+
+        live = []
+        for s in specs:
+            g, c = locate(s.out_col, D)
+            if g is not None:
+                live.append((s, g, c))
         grads = []
         # drop-in: one deterministic reduction over every distinct table of the call
-        dense = [s for s in specs if s.ref.group is None]
-        if dense and ctx.n_weights:
+        dense = [(s, g, c) for s, g, c in live if s.ref.group is None]
+        if ctx.n_weights:
             tables, offs, total = {}, {}, 0
-            for s in dense:
+            for s in specs:
                 w = s.ref.weight
-                if id(w) not in tables:
+                if s.ref.group is None and id(w) not in tables:
                     tables[id(w)] = w
                     offs[id(w)] = total
                     total += w.shape[0]
-            src = [K.GradSource(s.idx, gout, s.out_col, s.mode, s.bag, offs[id(s.ref.weight)],
-                                s.ref.weight.shape[0]) for s in dense]
-            res = K.embedding_backward(src, total, D, padding_idx=0, token_type=ctx.token_type,
-                                       seq_len=ctx.seq_len, dense=True)
-            by_id = {k: res.dense[offs[k]:offs[k] + w.shape[0]].to(w.dtype) for k, w in tables.items()}
+            if dense:
+                src = [K.GradSource(s.idx, g, c, s.mode, s.bag, offs[id(s.ref.weight)], s.ref.weight.shape[0])
+                       for s, g, c in dense]
+                res = K.embedding_backward(src, total, D, padding_idx=0, token_type=ctx.token_type,
+                                           seq_len=ctx.seq_len, dense=True)
+                by_id = {k: res.dense[offs[k]:offs[k] + w.shape[0]].to(w.dtype) for k, w in tables.items()}
+            else:
+                by_id = {k: None for k in tables}
             grads = [by_id[wid] for wid in ctx.weight_ids]
-        for s in specs:
+        for s, g, c in live:
             if s.ref.group is not None:
-                s.ref.group.collect(K.GradSource(s.idx, gout, s.out_col, s.mode, s.bag, s.ref.row_offset,
+                s.ref.group.collect(K.GradSource(s.idx, g, c, s.mode, s.bag, s.ref.row_offset,
                                                  s.ref.weight.shape[0]), ctx.token_type, ctx.seq_len)
         g_extra = None
         if ctx.extra_info is not None:
-            c, w, dt = ctx.extra_info
-            g_extra = gout[:, c:c + w].to(dt)
-        return (None, None, None, None, None, g_extra, None, *grads)
+            c0, w, dt = ctx.extra_info
+            g, c = locate(c0, w)
+            g_extra = None if g is None else g[:, c:c + w].to(dt)
+        return (None, None, None, None, None, g_extra, None, None, *grads)
 
 
 @_disable
-def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extra=None, extra_col=0):
+def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extra=None, extra_col=0, splits=None):
     """Fused multi-table gather (+ bag sums) into one [num_tokens, out_ld] buffer.
 
-    Drop-in tables get dense gradients through autograd; grouped tables push
-    row-sparse gradient sources into their group's sink."""
+    Returns the buffer's column blocks ``splits`` (list of (start, end);
+    default: the whole buffer, returned as a single tensor).  Drop-in tables
+    get dense gradients through autograd; grouped tables push row-sparse
+    gradient sources into their group's sink."""
     weights, seen = [], set()
     for s in specs:
         if s.ref.group is None and id(s.ref.weight) not in seen and s.ref.weight.requires_grad:
@@ -103,7 +128,10 @@ def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extra=
             weights.append(s.ref.weight)
     if token_type is not None:
         token_type = token_type.to(torch.int32).contiguous()
-    return _FeatureLookupFn.apply(specs, token_type, seq_len, num_tokens, out_ld, extra, extra_col, *weights)
+    single = splits is None
+    splits = tuple((0, out_ld) if single else ((int(a), int(b)) for a, b in splits))
+    outs = _FeatureLookupFn.apply(specs, token_type, seq_len, num_tokens, out_ld, extra, extra_col, splits, *weights)
+    return outs[0] if single else outs
 
 
 # ------------------------------------------------------------- attention ----

@@ -288,11 +288,13 @@ class BaselineModel(torch.nn.Module):
             col += d
         if self._remaps is not None or self._table_refs is not None:
             specs = self._remap_specs(specs)
-        buf = G.feature_lookup(specs, N, col, tt, T, extra, extra_col)
-        x = torch.relu(self.itemdnn(buf[:, :item_w]))
+        splits = [(0, item_w)] + ([(item_w, user_end)] if include_user else []) + \
+                 ([(user_end, user_end + d)] if with_pos else [])
+        blocks = list(G.feature_lookup(specs, N, col, tt, T, extra, extra_col, splits))
+        x = torch.relu(self.itemdnn(blocks.pop(0)))
         if include_user:
-            x = x + torch.relu(self.userdnn(buf[:, item_w:user_end]))
-        pos_rows = buf[:, user_end:user_end + d] if with_pos else None
+            x = x + torch.relu(self.userdnn(blocks.pop(0)))
+        pos_rows = blocks.pop(0) if with_pos else None
         return x.view(B, T, d), pos_rows
 
     def _remap_specs(self, specs):
