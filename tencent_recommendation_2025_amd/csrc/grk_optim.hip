@@ -13,25 +13,42 @@
 
 namespace grk {
 
-template <typename P>
-__device__ __forceinline__ void adam4(P* p, float* m, float* v, const float g[4], const grk_adamw_hparams& hp) {
-  float pv[4], mv[4], vv[4];
+// AdamW on NV consecutive elements (NV = 4 or 8): param via one 8/16-byte
+// access (bf16) or NV/4 float4s, moments via NV/4 float4s each.
+template <typename P, int NV>
+__device__ __forceinline__ void adam_vec(P* p, float* m, float* v, const float* g, const grk_adamw_hparams& hp) {
+  float pv[NV], mv[NV], vv[NV];
   if constexpr (sizeof(P) == 4) {
-    float4 t = *reinterpret_cast<const float4*>(p);
-    pv[0] = t.x; pv[1] = t.y; pv[2] = t.z; pv[3] = t.w;
+#pragma unroll
+    for (int k = 0; k < NV / 4; ++k) {
+      const float4 t = reinterpret_cast<const float4*>(p)[k];
+      pv[4 * k] = t.x; pv[4 * k + 1] = t.y; pv[4 * k + 2] = t.z; pv[4 * k + 3] = t.w;
+    }
   } else {
-    uint2 t = *reinterpret_cast<const uint2*>(p);
-    pv[0] = __uint_as_float(t.x << 16); pv[1] = __uint_as_float(t.x & 0xFFFF0000u);
-    pv[2] = __uint_as_float(t.y << 16); pv[3] = __uint_as_float(t.y & 0xFFFF0000u);
+    unsigned w[NV / 2];
+    if constexpr (NV == 8) {
+      const uint4 t = *reinterpret_cast<const uint4*>(p);
+      w[0] = t.x; w[1] = t.y; w[2] = t.z; w[3] = t.w;
+    } else {
+      const uint2 t = *reinterpret_cast<const uint2*>(p);
+      w[0] = t.x; w[1] = t.y;
+    }
+#pragma unroll
+    for (int k = 0; k < NV / 2; ++k) {
+      pv[2 * k] = __uint_as_float(w[k] << 16);
+      pv[2 * k + 1] = __uint_as_float(w[k] & 0xFFFF0000u);
+    }
   }
-  float4 mt = *reinterpret_cast<const float4*>(m);
-  float4 vt = *reinterpret_cast<const float4*>(v);
-  mv[0] = mt.x; mv[1] = mt.y; mv[2] = mt.z; mv[3] = mt.w;
-  vv[0] = vt.x; vv[1] = vt.y; vv[2] = vt.z; vv[3] = vt.w;
+#pragma unroll
+  for (int k = 0; k < NV / 4; ++k) {
+    const float4 a = reinterpret_cast<const float4*>(m)[k], b = reinterpret_cast<const float4*>(v)[k];
+    mv[4 * k] = a.x; mv[4 * k + 1] = a.y; mv[4 * k + 2] = a.z; mv[4 * k + 3] = a.w;
+    vv[4 * k] = b.x; vv[4 * k + 1] = b.y; vv[4 * k + 2] = b.z; vv[4 * k + 3] = b.w;
+  }
   const float decay = 1.0f - hp.lr * hp.weight_decay;
   const float w1 = 1.0f - hp.beta1, w2 = 1.0f - hp.beta2;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < NV; ++e) {
     float pe = pv[e] * decay;
     float me = mv[e] + w1 * (g[e] - mv[e]);
     float ve = vv[e] * hp.beta2 + w2 * g[e] * g[e];
@@ -40,55 +57,73 @@ __device__ __forceinline__ void adam4(P* p, float* m, float* v, const float g[4]
     pv[e] = pe; mv[e] = me; vv[e] = ve;
   }
   if constexpr (sizeof(P) == 4) {
-    *reinterpret_cast<float4*>(p) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+#pragma unroll
+    for (int k = 0; k < NV / 4; ++k)
+      reinterpret_cast<float4*>(p)[k] = make_float4(pv[4 * k], pv[4 * k + 1], pv[4 * k + 2], pv[4 * k + 3]);
   } else {
-    uint2 t;
-    t.x = (unsigned)f32_to_bf16(pv[0]) | ((unsigned)f32_to_bf16(pv[1]) << 16);
-    t.y = (unsigned)f32_to_bf16(pv[2]) | ((unsigned)f32_to_bf16(pv[3]) << 16);
-    *reinterpret_cast<uint2*>(p) = t;
+    unsigned w[NV / 2];
+#pragma unroll
+    for (int k = 0; k < NV / 2; ++k)
+      w[k] = (unsigned)f32_to_bf16(pv[2 * k]) | ((unsigned)f32_to_bf16(pv[2 * k + 1]) << 16);
+    if constexpr (NV == 8) *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+    else *reinterpret_cast<uint2*>(p) = make_uint2(w[0], w[1]);
   }
-  *reinterpret_cast<float4*>(m) = make_float4(mv[0], mv[1], mv[2], mv[3]);
-  *reinterpret_cast<float4*>(v) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+#pragma unroll
+  for (int k = 0; k < NV / 4; ++k) {
+    reinterpret_cast<float4*>(m)[k] = make_float4(mv[4 * k], mv[4 * k + 1], mv[4 * k + 2], mv[4 * k + 3]);
+    reinterpret_cast<float4*>(v)[k] = make_float4(vv[4 * k], vv[4 * k + 1], vv[4 * k + 2], vv[4 * k + 3]);
+  }
 }
 
-template <typename P>
+template <int NV>
+__device__ __forceinline__ void load_grad(const float* src, float* g) {
+#pragma unroll
+  for (int k = 0; k < NV / 4; ++k) {
+    const float4 t = reinterpret_cast<const float4*>(src)[k];
+    g[4 * k] = t.x; g[4 * k + 1] = t.y; g[4 * k + 2] = t.z; g[4 * k + 3] = t.w;
+  }
+}
+
+// Dense mode: one NV-vector per thread and a grid covering the whole table
+// (no grid-stride loop): measured fastest for this read+write stream on
+// gfx950 (scripts/microbench/adamw_dense.hip: 6.09 TB/s vs 5.66 for a
+// 4-wide grid-stride loop; nontemporal hints were slower).
+template <typename P, int NV>
 __global__ void __launch_bounds__(256) k_adamw_dense(P* __restrict__ param, float* __restrict__ m,
                                                      float* __restrict__ v, int64_t num_rows, int dim,
                                                      const float* __restrict__ uniq_rows,
                                                      const int32_t* __restrict__ row_slot, grk_adamw_hparams hp) {
-  const int q = dim / 4;
-  const int64_t total = num_rows * q;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = i / q;
-    const int c = (int)(i - row * q) * 4;
-    const int32_t slot = row_slot ? row_slot[row] : -1;
-    float g[4] = {0.f, 0.f, 0.f, 0.f};
-    if (slot >= 0) {
-      float4 t = *reinterpret_cast<const float4*>(uniq_rows + (int64_t)slot * dim + c);
-      g[0] = t.x; g[1] = t.y; g[2] = t.z; g[3] = t.w;
-    }
-    const int64_t off = row * dim + c;
-    adam4<P>(param + off, m + off, v + off, g, hp);
-  }
+  const int q = dim / NV;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= num_rows * q) return;
+  const int64_t row = i / q;
+  const int c = (int)(i - row * q) * NV;
+  const int32_t slot = row_slot ? row_slot[row] : -1;
+  float g[NV];
+#pragma unroll
+  for (int e = 0; e < NV; ++e) g[e] = 0.f;
+  if (slot >= 0) load_grad<NV>(uniq_rows + (int64_t)slot * dim + c, g);
+  const int64_t off = row * dim + c;
+  adam_vec<P, NV>(param + off, m + off, v + off, g, hp);
 }
 
-template <typename P>
+template <typename P, int NV>
 __global__ void __launch_bounds__(256) k_adamw_lazy(P* __restrict__ param, float* __restrict__ m,
                                                     float* __restrict__ v, int dim,
                                                     const int64_t* __restrict__ uniq_ids,
                                                     const float* __restrict__ uniq_rows,
                                                     const int32_t* __restrict__ count, int64_t max_uniq,
                                                     grk_adamw_hparams hp) {
-  const int q = dim / 4;
+  const int q = dim / NV;
   const int64_t n = *count;
   const int64_t total = (n < max_uniq ? n : max_uniq) * q;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t u = i / q;
-    const int c = (int)(i - u * q) * 4;
-    float4 t = *reinterpret_cast<const float4*>(uniq_rows + u * dim + c);
-    float g[4] = {t.x, t.y, t.z, t.w};
+    const int c = (int)(i - u * q) * NV;
+    float g[NV];
+    load_grad<NV>(uniq_rows + u * dim + c, g);
     const int64_t off = uniq_ids[u] * dim + c;
-    adam4<P>(param + off, m + off, v + off, g, hp);
+    adam_vec<P, NV>(param + off, m + off, v + off, g, hp);
   }
 }
 
@@ -115,22 +150,24 @@ extern "C" int grk_table_adamw(void* param, int param_dtype, float* exp_avg, flo
   GRK_CHECK_ARG(mode == GRK_ADAM_LAZY || !row_slot || uniq_rows, "dense mode with row_slot needs uniq_rows");
   GRK_CHECK_ARG(hp.bias_corr2_sqrt > 0.f, "bias_corr2_sqrt must be > 0");
   hipStream_t s = (hipStream_t)stream;
+  const bool v8 = dim % 8 == 0;
   if (mode == GRK_ADAM_DENSE) {
-    const int g = grid_for(num_rows * (dim / 4), 256, 256 * 32);
-    if (param_dtype == GRK_BF16)
-      k_adamw_dense<bf16_t><<<g, 256, 0, s>>>((bf16_t*)param, exp_avg, exp_avg_sq, num_rows, dim, uniq_rows,
-                                              row_slot, hp);
-    else
-      k_adamw_dense<float><<<g, 256, 0, s>>>((float*)param, exp_avg, exp_avg_sq, num_rows, dim, uniq_rows,
-                                             row_slot, hp);
+    const int64_t work = num_rows * (dim / (v8 ? 8 : 4));
+    if (work == 0) return GRK_OK;
+    GRK_CHECK_ARG((work + 255) / 256 < (int64_t)1 << 31, "table too large for one launch");
+    const unsigned g = (unsigned)((work + 255) / 256);
+#define GRK_DENSE(P, NV) k_adamw_dense<P, NV><<<g, 256, 0, s>>>((P*)param, exp_avg, exp_avg_sq, num_rows, dim, \
+                                                              uniq_rows, row_slot, hp)
+    if (param_dtype == GRK_BF16) { if (v8) GRK_DENSE(bf16_t, 8); else GRK_DENSE(bf16_t, 4); }
+    else { if (v8) GRK_DENSE(float, 8); else GRK_DENSE(float, 4); }
+#undef GRK_DENSE
   } else {
-    const int g = grid_for(max_uniq * (dim / 4), 256, 256 * 32);
-    if (param_dtype == GRK_BF16)
-      k_adamw_lazy<bf16_t><<<g, 256, 0, s>>>((bf16_t*)param, exp_avg, exp_avg_sq, dim, uniq_ids, uniq_rows,
-                                             uniq_count, max_uniq, hp);
-    else
-      k_adamw_lazy<float><<<g, 256, 0, s>>>((float*)param, exp_avg, exp_avg_sq, dim, uniq_ids, uniq_rows,
-                                            uniq_count, max_uniq, hp);
+    const int g = grid_for(max_uniq * (dim / (v8 ? 8 : 4)), 256, 256 * 32);
+#define GRK_LAZY(P, NV) k_adamw_lazy<P, NV><<<g, 256, 0, s>>>((P*)param, exp_avg, exp_avg_sq, dim, uniq_ids, \
+                                                            uniq_rows, uniq_count, max_uniq, hp)
+    if (param_dtype == GRK_BF16) { if (v8) GRK_LAZY(bf16_t, 8); else GRK_LAZY(bf16_t, 4); }
+    else { if (v8) GRK_LAZY(float, 8); else GRK_LAZY(float, 4); }
+#undef GRK_LAZY
   }
   GRK_LAUNCH_CHECK();
   if (row_slot && uniq_ids && uniq_count) {  // without uniq_ids row_slot is a fixed map (e.g. identity)

@@ -315,6 +315,29 @@ class BaselineModel(torch.nn.Module):
     def feat2emb(self, seq, feature_array, mask=None, include_user=False):
         return self._embed(seq, feature_array, mask, include_user)[0]
 
+    def feat2emb_pair(self, pos_seqs, pos_feature, neg_seqs, neg_feature):
+        """``(feat2emb(pos), feat2emb(neg))`` computed as ONE feat2emb over the
+        two batches stacked ([2B, T]): one fused gather and one itemdnn GEMM
+        with twice the rows.  Every output row depends on its own token only,
+        so this equals the reference's two calls (model/BaseLine/model.py:376-377)."""
+        dev = self._device()
+        pos = pos_seqs.to(dev, non_blocking=True).long()
+        neg = neg_seqs.to(dev, non_blocking=True).long()
+        B, T = pos.shape
+        fids = list(self.ITEM_SPARSE_FEAT) + list(self.ITEM_ARRAY_FEAT) + list(self.ITEM_EMB_FEAT)
+        fp = self._feats(pos_feature, fids, B, T)
+        fn = self._feats(neg_feature, fids, B, T)
+        feats = {k: _stack_padded(fp[k], fn[k]) for k in fids}
+        seq2 = torch.cat([pos, neg], 0)
+        if self._remaps is not None:  # row-sharded tables: the stacked ids read the rows fetched for pos and neg
+            for name in ('item_emb',):
+                a = self._remaps.get((name, pos.data_ptr(), L.IDX_PLAIN))
+                b = self._remaps.get((name, neg.data_ptr(), L.IDX_PLAIN))
+                if a is not None and b is not None and a[0] is b[0]:
+                    self._remaps[(name, seq2.data_ptr(), L.IDX_PLAIN)] = (a[0], torch.cat([a[1], b[1]], 0))
+        x = self._embed(seq2, feats)[0]
+        return x[:B], x[B:]
+
     # -------------------------------------------------- model/BaseLine/model.py:312-350
     def log2feats(self, log_seqs, mask, seq_feature):
         dev = self._device()
@@ -341,15 +364,13 @@ class BaselineModel(torch.nn.Module):
     def forward(self, user_item, pos_seqs, neg_seqs, mask, next_mask, next_action_type, seq_feature, pos_feature,
                 neg_feature):
         log_feats = self.log2feats(user_item, mask, seq_feature)
-        pos_embs = self.feat2emb(pos_seqs, pos_feature, include_user=False)
-        neg_embs = self.feat2emb(neg_seqs, neg_feature, include_user=False)
+        pos_embs, neg_embs = self.feat2emb_pair(pos_seqs, pos_feature, neg_seqs, neg_feature)
         return G.pair_logits(log_feats, pos_embs, neg_embs, next_mask.to(self._device(), non_blocking=True))
 
     def encode(self, user_item, pos_seqs, neg_seqs, mask, seq_feature, pos_feature, neg_feature):
         """(log_feats, pos_embs, neg_embs) -- the operands of the loss."""
         return (self.log2feats(user_item, mask, seq_feature),
-                self.feat2emb(pos_seqs, pos_feature, include_user=False),
-                self.feat2emb(neg_seqs, neg_feature, include_user=False))
+                *self.feat2emb_pair(pos_seqs, pos_feature, neg_seqs, neg_feature))
 
     def predict(self, log_seqs, seq_feature, mask):
         return self.log2feats(log_seqs, mask, seq_feature)[:, -1, :]
@@ -364,6 +385,16 @@ class BaselineModel(torch.nn.Module):
             embs.append(self.feat2emb(seq, feats, include_user=False).squeeze(0).detach().float().cpu().numpy())
         save_emb(np.concatenate(embs, 0), Path(save_path, 'embedding.fbin'))
         save_emb(np.array(retrieval_ids, dtype=np.uint64).reshape(-1, 1), Path(save_path, 'id.u64bin'))
+
+
+def _stack_padded(a, b):
+    """Stack two feature tensors along the batch dim; array features (bag dim 2)
+    are zero-padded to the wider bag (index 0 = the zero padding row)."""
+    if a.dim() == 3 and not a.is_floating_point() and a.shape[2] != b.shape[2]:
+        w = max(a.shape[2], b.shape[2])
+        a = F.pad(a, (0, w - a.shape[2]))
+        b = F.pad(b, (0, w - b.shape[2]))
+    return torch.cat([a, b], 0)
 
 
 def init_reference_(model, seed=None, live_norms=False):
