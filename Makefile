@@ -14,6 +14,10 @@ OBJS := $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(HIP_SRCS)) $(patsubst $(SRC
 
 all: $(LIB)
 
+# whole-sequence attention: MFMA accumulators in VGPRs (no AGPR<->VGPR copies
+# around the S tile; same occupancy -- scripts/isa_loops.py)
+$(OBJ_DIR)/grk_attention_seq.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
+
 $(OBJ_DIR):
 	mkdir -p $@
 

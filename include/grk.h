@@ -181,7 +181,15 @@ typedef struct grk_attn_args {
   uint64_t seed;                   /* dropout stream                              */
   int32_t out_dtype;               /* GRK_F32 / GRK_BF16 for out, dq, dk, dv      */
   int32_t act;                     /* GRK_ACT_*: activation applied to q/k/v      */
+  const int32_t* seq_range;        /* optional [B, 2] from grk_seq_ranges (first
+                                      valid key, contiguous flag); NULL = derived
+                                      from key_valid inside every launch        */
 } grk_attn_args;
+
+/* ranges[b] = (first j with key_valid[b, j], 1 if the valid keys are exactly
+ * [first, T) else 0); first = T for an all-padding row.  One launch per step
+ * serves every attention launch of that step (all layers, fwd and bwd). */
+int grk_seq_ranges(const uint8_t* key_valid, int batch, int seq_len, int32_t* ranges, void* stream);
 
 /* out [B*T, ldo] (out_dtype); lse fp32 [B, H, T] (softmax: natural-log
  * logsumexp of the masked scaled scores, -inf for fully-masked rows). */
@@ -189,7 +197,8 @@ int grk_attention_fwd(const grk_attn_args* a, void* out, int64_t ldo, float* lse
 
 /* Gradients of grk_attention_fwd for upstream dout (dout_dtype).  Softmax
  * needs the forward out/lse and a delta workspace fp32 [B, H, T]; hstu
- * accumulates drab fp32 [H, nb] (caller zero-fills).  dq/dk/dv are written
+ * accumulates drab fp32 [H, nb] (caller zero-fills; NULL = rab is frozen,
+ * its gradient is not computed).  dq/dk/dv are written
  * (not accumulated) in out_dtype; deterministic except drab. */
 int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
                       int dout_dtype, const float* lse, float* delta_ws, void* dq, int64_t lddq, void* dk,

@@ -1,0 +1,132 @@
+// Shared pieces of the gfx950 attention kernels (grk_attention.hip: the
+// chunked kernels for any length; grk_attention_seq.hip: whole-sequence
+// kernels for short sequences).  See grk_attention.hip for the conventions.
+#pragma once
+#include "grk_common.h"
+#include "grk_mfma.h"
+
+namespace grk {
+
+constexpr int kChunk = 64;      // rows staged per LDS chunk
+constexpr int kBlockRows = 128; // queries (fwd/dQ) or keys (dKdV) per workgroup
+constexpr int kRabMax = 2048;
+
+struct AttnParams {
+  int kind, B, H, T;
+  const bf16_t *q, *k, *v;
+  int64_t ldq, ldk, ldv;
+  const uint8_t* key_valid;
+  float scale, inv_n, dropout_p;
+  unsigned long long seed;
+  const float* rab;
+  int nb;
+  int precise;
+  int out_f32;
+  int act;  // GRK_ACT_SILU: q/k/v are pre-activations
+  const int* seq_range;  // optional [B, 2] (first valid key, contiguous flag)
+  // forward
+  void* out; int64_t ldo; float* lse;
+  // backward
+  const void* dout; int64_t lddo; int dout_f32;
+  const float* delta;
+  void *dq, *dk, *dv; int64_t lddq, lddk, lddv;
+  float* drab;
+};
+
+
+// Counter-based dropout keep decision for element (b*H+h, q, k): identical
+// in forward and backward.
+__device__ __forceinline__ bool drop_keep(unsigned long long seed, int bh, int q, int k, int T, float p) {
+  unsigned long long x = seed ^ (((unsigned long long)bh * (unsigned)T + (unsigned)q) * (unsigned)T + (unsigned)k) *
+                                    0x9E3779B97F4A7C15ull;
+  x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27; x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  const float u = (float)(x >> 40) * (1.0f / 16777216.0f);
+  return u >= p;
+}
+
+// Stage rows [r0, r0+kChunk) of a [B*T, ld] head slice into a swizzled LDS
+// image (zeros outside [0, T)).
+// Stage rows [r0, r0 + nrows) of a [B*T, ld] head slice into image rows
+// [dst0, dst0 + nrows) of a swizzled LDS image (zeros outside [0, T));
+// act: apply SiLU on the way (pre-activation inputs).
+template <int HD>
+__device__ __forceinline__ void stage_rows_at(char* dst, const void* src, int64_t ld, int b, int T, int h, int r0,
+                                              int nrows, int dst0, bool f32, bool act) {
+  constexpr int NCH = HD / 8;
+  for (int u = threadIdx.x; u < nrows * NCH; u += blockDim.x) {
+    const int row = u / NCH, c = u % NCH;
+    const int t = r0 + row;
+    const bool ok = t >= 0 && t < T;
+    bf16x8 v = gload8_any(src, ((int64_t)b * T + (ok ? t : 0)) * ld + h * HD + c * 8, f32, ok);
+    if (act) v = silu8(v);
+    *reinterpret_cast<uint4*>(dst + lds_off<HD>(dst0 + row, c * 8)) = __builtin_bit_cast(uint4, v);
+  }
+}
+
+template <int HD>
+__device__ __forceinline__ void stage_rows(char* dst, const void* src, int64_t ld, int b, int T, int h, int r0,
+                                           bool f32, bool act = false) {
+  stage_rows_at<HD>(dst, src, ld, b, T, h, r0, kChunk, 0, f32, act);
+}
+
+__device__ __forceinline__ int seq_start(const uint8_t* kv, int b, int T, int* s_start) {
+  if (!kv) return 0;
+  if (threadIdx.x == 0) *s_start = T;
+  __syncthreads();
+  for (int j = threadIdx.x; j < T; j += blockDim.x)
+    if (kv[(int64_t)b * T + j]) atomicMin(s_start, j);
+  __syncthreads();
+  return *s_start;
+}
+
+template <typename OutT>
+__device__ __forceinline__ void store4(OutT* p, const float* v);
+template <>
+__device__ __forceinline__ void store4<float>(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <>
+__device__ __forceinline__ void store4<bf16_t>(bf16_t* p, const float* v) {
+  uint2 t;
+  t.x = (unsigned)f32_to_bf16(v[0]) | ((unsigned)f32_to_bf16(v[1]) << 16);
+  t.y = (unsigned)f32_to_bf16(v[2]) | ((unsigned)f32_to_bf16(v[3]) << 16);
+  *reinterpret_cast<uint2*>(p) = t;
+}
+
+// Store an accumulated D^T tile set acc[NDT] (rows = feature d, lane = token)
+// to row `tok` of a [B*T, ld] output: lane holds d = dt*32 + 8g + 4hh + 0..3.
+// With dsrc (GRK_ACT_SILU) the value is the gradient w.r.t. the activation
+// and is multiplied by dSiLU(pre) read from the same position of dsrc.
+template <int HD, int NDT>
+__device__ __forceinline__ void store_rows(void* out, int64_t ld, bool f32, int64_t tok, int h, int hh,
+                                           const f32x16* acc, float mul, bool ok, const bf16_t* dsrc = nullptr,
+                                           int64_t ldsrc = 0) {
+  if (!ok) return;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = dt * 32 + 8 * g + 4 * hh;
+      if (d >= HD) continue;
+      float v[4] = {acc[dt][4 * g] * mul, acc[dt][4 * g + 1] * mul, acc[dt][4 * g + 2] * mul, acc[dt][4 * g + 3] * mul};
+      if (dsrc) {
+        const uint2 pw = *reinterpret_cast<const uint2*>(dsrc + tok * ldsrc + h * HD + d);
+        v[0] *= dsilu(__uint_as_float(pw.x << 16));
+        v[1] *= dsilu(__uint_as_float(pw.x & 0xFFFF0000u));
+        v[2] *= dsilu(__uint_as_float(pw.y << 16));
+        v[3] *= dsilu(__uint_as_float(pw.y & 0xFFFF0000u));
+      }
+      const int64_t off = tok * ld + h * HD + d;
+      if (f32) store4<float>((float*)out + off, v);
+      else store4<bf16_t>((bf16_t*)out + off, v);
+    }
+}
+
+// Whole-sequence kernels (grk_attention_seq.hip): one workgroup per
+// (batch, head) with the sequence's K/V (or Q/dO) resident in LDS.
+// Returns true and launches when the shape fits; false = use the chunked path.
+bool attn_seq_launch(const AttnParams& p, int hd, int which, hipStream_t s);
+
+}  // namespace grk

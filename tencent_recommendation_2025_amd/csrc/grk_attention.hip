@@ -22,117 +22,9 @@
 // then directly the B operand of O^T = V^T P^T (permuted k order, see
 // cdna_hip_programming.md §3).  Backward = dQ kernel (S^T, dP^T, dQ^T) +
 // dK/dV kernel (S, dP, dV^T, dK^T): no atomics on dQ/dK/dV, deterministic.
-#include "grk_common.h"
-#include "grk_mfma.h"
+#include "grk_attention.h"
 
 namespace grk {
-
-constexpr int kChunk = 64;      // rows staged per LDS chunk
-constexpr int kBlockRows = 128; // queries (fwd/dQ) or keys (dKdV) per workgroup
-constexpr int kRabMax = 2048;
-
-struct AttnParams {
-  int kind, B, H, T;
-  const bf16_t *q, *k, *v;
-  int64_t ldq, ldk, ldv;
-  const uint8_t* key_valid;
-  float scale, inv_n, dropout_p;
-  unsigned long long seed;
-  const float* rab;
-  int nb;
-  int precise;
-  int out_f32;
-  int act;  // GRK_ACT_SILU: q/k/v are pre-activations
-  // forward
-  void* out; int64_t ldo; float* lse;
-  // backward
-  const void* dout; int64_t lddo; int dout_f32;
-  const float* delta;
-  void *dq, *dk, *dv; int64_t lddq, lddk, lddv;
-  float* drab;
-};
-
-
-// Counter-based dropout keep decision for element (b*H+h, q, k): identical
-// in forward and backward.
-__device__ __forceinline__ bool drop_keep(unsigned long long seed, int bh, int q, int k, int T, float p) {
-  unsigned long long x = seed ^ (((unsigned long long)bh * (unsigned)T + (unsigned)q) * (unsigned)T + (unsigned)k) *
-                                    0x9E3779B97F4A7C15ull;
-  x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
-  x ^= x >> 27; x *= 0x94D049BB133111EBull;
-  x ^= x >> 31;
-  const float u = (float)(x >> 40) * (1.0f / 16777216.0f);
-  return u >= p;
-}
-
-// Stage rows [r0, r0+kChunk) of a [B*T, ld] head slice into a swizzled LDS
-// image (zeros outside [0, T)).
-template <int HD>
-__device__ __forceinline__ void stage_rows(char* dst, const void* src, int64_t ld, int b, int T, int h, int r0,
-                                           bool f32, bool act = false) {
-  constexpr int NCH = HD / 8;
-  for (int u = threadIdx.x; u < kChunk * NCH; u += blockDim.x) {
-    const int row = u / NCH, c = u % NCH;
-    const int t = r0 + row;
-    const bool ok = t >= 0 && t < T;
-    bf16x8 v = gload8_any(src, ((int64_t)b * T + (ok ? t : 0)) * ld + h * HD + c * 8, f32, ok);
-    if (act) v = silu8(v);
-    *reinterpret_cast<uint4*>(dst + lds_off<HD>(row, c * 8)) = __builtin_bit_cast(uint4, v);
-  }
-}
-
-__device__ __forceinline__ int seq_start(const uint8_t* kv, int b, int T, int* s_start) {
-  if (!kv) return 0;
-  if (threadIdx.x == 0) *s_start = T;
-  __syncthreads();
-  for (int j = threadIdx.x; j < T; j += blockDim.x)
-    if (kv[(int64_t)b * T + j]) atomicMin(s_start, j);
-  __syncthreads();
-  return *s_start;
-}
-
-template <typename OutT>
-__device__ __forceinline__ void store4(OutT* p, const float* v);
-template <>
-__device__ __forceinline__ void store4<float>(float* p, const float* v) {
-  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-}
-template <>
-__device__ __forceinline__ void store4<bf16_t>(bf16_t* p, const float* v) {
-  uint2 t;
-  t.x = (unsigned)f32_to_bf16(v[0]) | ((unsigned)f32_to_bf16(v[1]) << 16);
-  t.y = (unsigned)f32_to_bf16(v[2]) | ((unsigned)f32_to_bf16(v[3]) << 16);
-  *reinterpret_cast<uint2*>(p) = t;
-}
-
-// Store an accumulated D^T tile set acc[NDT] (rows = feature d, lane = token)
-// to row `tok` of a [B*T, ld] output: lane holds d = dt*32 + 8g + 4hh + 0..3.
-// With dsrc (GRK_ACT_SILU) the value is the gradient w.r.t. the activation
-// and is multiplied by dSiLU(pre) read from the same position of dsrc.
-template <int HD, int NDT>
-__device__ __forceinline__ void store_rows(void* out, int64_t ld, bool f32, int64_t tok, int h, int hh,
-                                           const f32x16* acc, float mul, bool ok, const bf16_t* dsrc = nullptr,
-                                           int64_t ldsrc = 0) {
-  if (!ok) return;
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = dt * 32 + 8 * g + 4 * hh;
-      if (d >= HD) continue;
-      float v[4] = {acc[dt][4 * g] * mul, acc[dt][4 * g + 1] * mul, acc[dt][4 * g + 2] * mul, acc[dt][4 * g + 3] * mul};
-      if (dsrc) {
-        const uint2 pw = *reinterpret_cast<const uint2*>(dsrc + tok * ldsrc + h * HD + d);
-        v[0] *= dsilu(__uint_as_float(pw.x << 16));
-        v[1] *= dsilu(__uint_as_float(pw.x & 0xFFFF0000u));
-        v[2] *= dsilu(__uint_as_float(pw.y << 16));
-        v[3] *= dsilu(__uint_as_float(pw.y & 0xFFFF0000u));
-      }
-      const int64_t off = tok * ld + h * HD + d;
-      if (f32) store4<float>((float*)out + off, v);
-      else store4<bf16_t>((bf16_t*)out + off, v);
-    }
-}
 
 // ================================================================ forward ====
 template <int HD, int KIND>
@@ -359,7 +251,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
           const int bk = min(myq - key, p.nb - 1);
           const float sp = s[i] * p.scale + rabs[ok ? bk : 0];
           ds[i] = ok ? dp[i] * dsilu(sp) * p.inv_n : 0.f;
-          if (ok && ds[i] != 0.f) atomicAdd(&bins[bk], ds[i]);
+          if (ok && ds[i] != 0.f && p.drab) atomicAdd(&bins[bk], ds[i]);
         }
       }
 #pragma unroll
@@ -377,7 +269,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
   }
   store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, (int64_t)b * T + myq, h, hh, acc, p.scale, qok,
                       p.act ? p.q : nullptr, p.ldq);
-  if (KIND == 1) {
+  if (KIND == 1 && p.drab) {
     __syncthreads();
     for (int j = threadIdx.x; j < p.nb; j += blockDim.x)
       if (bins[j] != 0.f) atomicAdd(&p.drab[h * p.nb + j], bins[j]);
@@ -519,6 +411,10 @@ static int launch_hd(const AttnParams& p, int which, hipStream_t s) {
 }
 
 static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
+  if (which != 1 && attn_seq_launch(p, hd, which, s)) {
+    GRK_LAUNCH_CHECK();
+    return GRK_OK;
+  }
   switch (hd) {
     case 16: return launch_hd<16>(p, which, s);
     case 32: return launch_hd<32>(p, which, s);
@@ -555,6 +451,7 @@ static int fill_params(const grk_attn_args* a, AttnParams* p) {
   p->rab = a->rab; p->nb = a->num_buckets;
   p->precise = a->precise; p->out_f32 = a->out_dtype == GRK_F32;
   p->act = a->act;
+  p->seq_range = a->seq_range;
   return GRK_OK;
 }
 
@@ -587,7 +484,6 @@ extern "C" int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_
   GRK_CHECK_ARG(dq && dk && dv && lddq >= need && lddk >= need && lddv >= need, "bad dq/dk/dv");
   GRK_CHECK_ARG(a->kind == GRK_ATTN_HSTU || (out && lse && delta_ws && ldo >= need),
                 "softmax backward needs out, lse and delta_ws [B, H, T]");
-  GRK_CHECK_ARG(a->kind == GRK_ATTN_SOFTMAX || drab, "hstu backward needs drab (zero-initialised)");
   p.out = const_cast<void*>(out); p.ldo = ldo;
   p.dout = dout; p.lddo = lddo; p.dout_f32 = dout_dtype == GRK_F32;
   p.lse = const_cast<float*>(lse); p.delta = delta_ws;

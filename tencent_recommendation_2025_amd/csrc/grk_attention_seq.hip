@@ -1,0 +1,739 @@
+// Whole-sequence causal attention for gfx950 (short sequences, the
+// TencentGR regime: T <= 256 at head_dim 64).  Same math, operand
+// conventions and outputs as the chunked kernels of grk_attention.hip
+// (softmax MHA and HSTU), restructured for a
+// latency-bound problem:
+//
+//  * one workgroup (4 waves) per (batch, head): the sequence's K/V (forward,
+//    dQ) or Q/dO (dK/dV) are staged into LDS ONCE, from the first valid key
+//    on (left padding is never loaded), behind a single barrier -- the
+//    chunked kernels wait on a load + barrier per 64-row chunk;
+//  * causal 32-row tiles are dealt to the waves in (j, n-1-j) pairs so every
+//    wave gets the same number of 32x32 sub-tiles;
+//  * the relative-position bias is staged as a clamped window rabx[d] so each
+//    score reads it at a compile-time offset from one per-lane base;
+//  * sub-tiles strictly below the diagonal and past the padding skip all
+//    masking (contiguous key validity = the dataset's left padding; any
+//    other key_valid pattern takes the per-key masked path);
+//  * the precise (hi/lo probability) mode is a template parameter.
+#include <stdlib.h>
+
+#include "grk_attention.h"
+
+namespace grk {
+
+constexpr int kSeqWaves = 4;
+
+// Phase timestamps for scripts/microbench/attn_stamps.hip (compiled only there).
+#ifdef GRK_ATTN_STAMPS
+__device__ unsigned long long g_attn_stamps[1 << 16][8];
+#define GRK_STAMP(k) \
+  if ((threadIdx.x & 63) == 0) g_attn_stamps[(blockIdx.x * kSeqWaves + (threadIdx.x >> 6)) & 0xFFFF][k] = __builtin_amdgcn_s_memtime()
+#else
+#define GRK_STAMP(k)
+#endif
+constexpr int kRabPad = 32;
+constexpr int kDqBinArrays = 2;  // dQ kernel: drab bins as int64 fixed point (2 float slots each)
+constexpr double kFixScale = 4294967296.0;  // drab fixed point: value * 2^32
+
+// drab partials are accumulated in LDS as 64-bit fixed point with integer
+// atomics: ds_add_u64 costs ~93 cycles per wave-instruction on gfx950 against
+// ~1150 for ds_add_f32 (scripts/microbench/lds_ops.hip), and integer sums do
+// not depend on the order of the adds.  Range +-2^31, resolution 2^-32.
+__device__ __forceinline__ unsigned long long to_fix(float v) {
+  const double d = fmin(fmax((double)v * kFixScale, -9.0e18), 9.0e18);
+  return (unsigned long long)(long long)d;
+}             // rabx[kRabPad + d], d >= -31 inside a sub-tile
+constexpr int kSeqLdsMax = 80 * 1024;   // LDS per workgroup: 2 per CU fit gfx950's 160 KiB
+
+struct SeqInfo {
+  int start;   // first valid key
+  int contig;  // valid keys are exactly [start, T)
+};
+
+__device__ __forceinline__ SeqInfo seq_info(const AttnParams& p, int b, int T, int* sh) {
+  if (p.seq_range)  // uniform scalar load; clamped so a bad range can never address outside [0, T)
+    return {min(max(p.seq_range[2 * b], 0), T), p.seq_range[2 * b + 1] != 0};
+  const uint8_t* kv = p.key_valid;
+  if (!kv) return {0, 1};
+  int first = T, cnt = 0;
+  for (int j = threadIdx.x; j < T; j += blockDim.x)
+    if (kv[(int64_t)b * T + j]) {
+      first = min(first, j);
+      ++cnt;
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    first = min(first, __shfl_xor(first, off));
+    cnt += __shfl_xor(cnt, off);
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[wave] = first;
+    sh[kSeqWaves + wave] = cnt;
+  }
+  __syncthreads();
+  int f = T, c = 0;
+#pragma unroll
+  for (int w = 0; w < kSeqWaves; ++w) {
+    f = min(f, sh[w]);
+    c += sh[kSeqWaves + w];
+  }
+  return {f, c == T - f};
+}
+
+// grk_seq_ranges: one wave per sequence.
+__global__ void __launch_bounds__(256) k_seq_ranges(const uint8_t* __restrict__ kv, int B, int T,
+                                                    int* __restrict__ out) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= B) return;
+  int first = T, cnt = 0;
+  for (int j = lane; j < T; j += 64)
+    if (kv[(int64_t)b * T + j]) {
+      first = min(first, j);
+      ++cnt;
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    first = min(first, __shfl_xor(first, off));
+    cnt += __shfl_xor(cnt, off);
+  }
+  if (lane == 0) {
+    out[2 * b] = first;
+    out[2 * b + 1] = cnt == T - first;
+  }
+}
+
+// KS 8-wide fragments of row `row` of a head slice (lane hh picks 8hh..8hh+7 of each 16)
+template <int HD>
+__device__ __forceinline__ void load_frag(bf16x8* f, const bf16_t* base, int64_t ld, int b, int T, int h, int row,
+                                          int hh) {
+  const bool ok = row < T;
+  const bf16_t* src = base + ((int64_t)b * T + (ok ? row : 0)) * ld + h * HD + 8 * hh;
+#pragma unroll
+  for (int ks = 0; ks < HD / 16; ++ks) f[ks] = gload8(src + 16 * ks, ok);
+}
+
+template <int HD>
+__device__ __forceinline__ void load_frag_any(bf16x8* f, const void* base, int64_t ld, bool f32, int b, int T, int h,
+                                              int row, int hh) {
+  const bool ok = row < T;
+  const int64_t off = ((int64_t)b * T + (ok ? row : 0)) * ld + h * HD + 8 * hh;
+#pragma unroll
+  for (int ks = 0; ks < HD / 16; ++ks) f[ks] = gload8_any(base, off + 16 * ks, f32, ok);
+}
+
+template <int HD>
+__device__ __forceinline__ void act_frag(bf16x8* f, bool act) {
+  if (act)
+#pragma unroll
+    for (int ks = 0; ks < HD / 16; ++ks) f[ks] = silu8(f[ks]);
+}
+
+// LDS carve-up shared by the three kernels: two row images of Tp x HD,
+// then per-row floats (rabx / lse / delta), key-valid bytes, scratch ints.
+template <int HD>
+struct SeqLds {
+  char* img0;
+  char* img1;
+  float* f0;  // Tp + kRabPad floats
+  float* f1;  // F1 x (Tp + kRabPad) floats (dQ: private drab bins per (wave, half-wave); dK/dV: delta)
+  uint8_t* kvs;
+  int* sh;
+  __device__ SeqLds(char* smem, int Tp, int F1 = 1) {
+    img0 = smem;
+    img1 = smem + Tp * HD * 2;
+    f0 = reinterpret_cast<float*>(smem + 2 * Tp * HD * 2);
+    f1 = f0 + Tp + kRabPad;
+    kvs = reinterpret_cast<uint8_t*>(f1 + F1 * (Tp + kRabPad));
+    sh = reinterpret_cast<int*>(kvs + Tp);
+  }
+  static size_t bytes(int Tp, int F1 = 1) {
+    return (size_t)2 * Tp * HD * 2 + (size_t)((1 + F1) * (Tp + kRabPad)) * 4 + Tp + 16 * 4;
+  }
+};
+
+// Stage rows [r0, Tp) of two [B*T, ld] head slices into the images at the
+// same rows: every load of a batch is in flight before the first use (a
+// load -> SiLU -> ds_write chain per element serialises on HBM latency).
+template <int HD>
+__device__ __forceinline__ void stage_pair(char* img0, const void* src0, int64_t ld0, bool f32_0, bool act0,
+                                           char* img1, const void* src1, int64_t ld1, bool f32_1, bool act1,
+                                           int b, int T, int h, int r0, int Tp) {
+  constexpr int NCH = HD / 8, BATCH = 8;
+  const int nvec = (Tp - r0) * NCH;
+  for (int base = threadIdx.x; base < nvec; base += BATCH * blockDim.x) {
+    bf16x8 v0[BATCH], v1[BATCH];
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const int u = base + k * blockDim.x;
+      const int t = r0 + u / NCH, c = u % NCH;
+      const bool ok = u < nvec && t < T;
+      const int64_t row = (int64_t)b * T + (ok ? t : 0);
+      v0[k] = gload8_any(src0, row * ld0 + h * HD + c * 8, f32_0, ok);
+      v1[k] = gload8_any(src1, row * ld1 + h * HD + c * 8, f32_1, ok);
+    }
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const int u = base + k * blockDim.x;
+      if (u < nvec) {
+        const int row = r0 + u / NCH, c = u % NCH;
+        const bf16x8 a = act0 ? silu8(v0[k]) : v0[k];
+        const bf16x8 bb = act1 ? silu8(v1[k]) : v1[k];
+        *reinterpret_cast<uint4*>(img0 + lds_off<HD>(row, c * 8)) = __builtin_bit_cast(uint4, a);
+        *reinterpret_cast<uint4*>(img1 + lds_off<HD>(row, c * 8)) = __builtin_bit_cast(uint4, bb);
+      }
+    }
+  }
+}
+
+// rabx[kRabPad + d] = rab[h, min(d, nb - 1)] for d >= 0, 0 for d < 0.
+// Tp + kRabPad <= 2 * blockDim for every shape the seq kernels take.
+struct RabRegs {
+  float v[2];
+};
+__device__ __forceinline__ RabRegs load_rab(const AttnParams& p, int h, int Tp) {
+  RabRegs r;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int j = threadIdx.x + k * blockDim.x;
+    const int d = j - kRabPad;
+    r.v[k] = (d < 0 || j >= Tp + kRabPad) ? 0.f : p.rab[h * p.nb + min(d, p.nb - 1)];
+  }
+  return r;
+}
+__device__ __forceinline__ void store_rab(float* rabx, const RabRegs& r, int Tp) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int j = threadIdx.x + k * blockDim.x;
+    if (j < Tp + kRabPad) rabx[j] = r.v[k];
+  }
+}
+
+__device__ __forceinline__ void stage_kvs(uint8_t* kvs, const uint8_t* kv, int b, int T, int Tp) {
+  for (int j = threadIdx.x; j < Tp; j += blockDim.x) kvs[j] = j < T && (!kv || kv[(int64_t)b * T + j]);
+}
+
+// relative-position bias of the 16 scores of lane (r, hh) in the sub-tile of
+// keys [kb, kb+32) for query myq: rabx[kRabPad + myq - key], key = kb + acc_row(i, hh)
+__device__ __forceinline__ void rab16(const float* rabx, int myq, int kb, int hh, float* rb) {
+  const float* base = rabx + kRabPad + (myq - kb - 4 * hh) - 27;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) rb[i] = base[27 - ((i & 3) + 8 * (i >> 2))];
+}
+
+// Branch-free mask of the 16 scores of lane (r, hh) in a sub-tile: row index
+// kb + acc_row(i, hh) valid iff in [lo, hi] (and kvs[row] != 0 when the key
+// validity is not one contiguous run).  A 16-bit mask; each select is then one
+// v_cndmask.  The contiguous case never touches LDS.
+// acc_row(i, hh) = (i & 3) + 8 (i >> 2) + 4 hh increases with i, so the scores
+// whose row lies in [lo, hi] are the contiguous index range [n_le(lo - 1), n_le(hi)).
+__device__ __forceinline__ int n_le(int c, int hh) {  // #{i : acc_row(i, hh) <= c}
+  const int d = c - 4 * hh;
+  return d < 0 ? 0 : min(4 * (d >> 3) + min((d & 7) + 1, 4), 16);
+}
+__device__ __forceinline__ unsigned mask16_range(int kb, int hh, int lo, int hi) {
+  const int a = n_le(lo - 1 - kb, hh), b = n_le(hi - kb, hh);
+  return b > a ? ((0xFFFFu >> (16 - b)) & ~((1u << a) - 1u)) : 0u;
+}
+__device__ __forceinline__ unsigned mask16(int kb, int hh, int lo, int hi, bool contig, const uint8_t* kvs) {
+  unsigned m = mask16_range(kb, hh, lo, hi);
+  if (!contig) {
+    unsigned v = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v |= (unsigned)(kvs[kb + acc_row(i, hh)] != 0) << i;
+    m &= v;
+  }
+  return m;
+}
+
+// Causal tiles are dealt in pairs {u, n-1-u} (work u+1 and n-u sub-tiles:
+// n+1 per pair); wave w takes pairs w, w + kSeqWaves, ...
+
+// Tile list of one wave: pairs {u, n-1-u} for u = wave, wave + kSeqWaves, ...
+// The fragments of the wave's first tile are loaded in the prologue, beside
+// the staging loads, so no tile starts with a global round trip.
+__device__ __forceinline__ int pair_tile(int u, int ps, int n) { return ps == 0 ? u : n - 1 - u; }
+__device__ __forceinline__ bool pair_has(int u, int ps, int n) { return ps == 0 || n - 1 - u != u; }
+
+// ================================================================ forward ====
+template <int HD, int KIND, int PREC>
+__global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
+  const int T = p.T, nq = (T + 31) / 32, Tp = nq * 32;
+  SeqLds<HD> L(smem, Tp);
+  GRK_STAMP(0);
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const SeqInfo si = seq_info(p, b, T, L.sh);
+  const int start = si.start, first = start / 32, kbeg = first * 32;
+  const int ntiles = nq - first, npairs = (ntiles + 1) / 2;
+  GRK_STAMP(1);
+  // prologue: every independent load in flight before the first wait
+  bf16x8 qpre[KS];
+  if (wave < npairs) load_frag<HD>(qpre, p.q, p.ldq, b, T, h, (first + wave) * 32 + r, hh);
+  RabRegs rr;
+  if (KIND == 1) rr = load_rab(p, h, Tp);
+  stage_pair<HD>(L.img0, p.k, p.ldk, false, p.act, L.img1, p.v, p.ldv, false, p.act, b, T, h, kbeg, Tp);
+  if (KIND == 1) store_rab(L.f0, rr, Tp);
+  if (!si.contig) stage_kvs(L.kvs, p.key_valid, b, T, Tp);
+  GRK_STAMP(2);
+  __syncthreads();
+  GRK_STAMP(3);
+
+  const float sl2 = p.scale * kLog2e;
+  const float rdrop = 1.0f / (1.0f - p.dropout_p);
+  const bool drop = KIND == 0 && p.dropout_p > 0.f;
+  const int bh = b * p.H + h;
+
+  // query tiles before the first valid key: every row fully masked -> 0
+  for (int qt = wave; qt < first; qt += kSeqWaves) {
+    const int myq = qt * 32 + r;
+    f32x16 z[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) z[dt] = f32x16{};
+    if (KIND == 0 && hh == 0 && myq < T && p.lse) p.lse[(int64_t)bh * T + myq] = -INFINITY;
+    store_rows<HD, NDT>(p.out, p.ldo, p.out_f32, (int64_t)b * T + myq, h, hh, z, 0.f, myq < T);
+  }
+
+  for (int pu = wave; pu < npairs; pu += kSeqWaves)
+#pragma unroll
+    for (int ps = 0; ps < 2; ++ps) {
+      if (!pair_has(pu, ps, ntiles)) break;
+      const int q0 = (first + pair_tile(pu, ps, ntiles)) * 32, myq = q0 + r;
+      const bool qok = myq < T;
+      bf16x8 qf[KS];
+      if (pu == wave && ps == 0) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) qf[ks] = qpre[ks];
+      } else {
+        load_frag<HD>(qf, p.q, p.ldq, b, T, h, myq, hh);
+      }
+      act_frag<HD>(qf, p.act);
+      f32x16 o[NDT];
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x16{};
+      float m = -INFINITY, l = 0.f;
+      for (int kb = kbeg; kb <= q0; kb += 32) {
+        f32x16 s = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) s = mfma(lds_row8<HD>(L.img0, kb + r, 16 * ks + 8 * hh), qf[ks], s);
+        // strictly below the diagonal and past the padding: nothing to mask
+        const bool fast = si.contig && kb < q0 && kb >= start;
+        float pd[16];
+        if (KIND == 0) {
+          float x[16], tmax = -INFINITY;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) x[i] = s[i] * sl2;
+          if (!fast) {
+            const unsigned mk = qok ? mask16(kb, hh, start, myq, si.contig, L.kvs) : 0u;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[i] = ((mk >> i) & 1) ? x[i] : -INFINITY;
+          }
+#pragma unroll
+          for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, x[i]);
+          tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+          const float mn = fmaxf(m, tmax);
+          const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
+          const float mref = (mn == -INFINITY) ? 0.f : mn;  // exp2(-inf - 0) = 0 for masked scores
+          float rs = 0.f;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            pd[i] = exp2f(x[i] - mref);
+            rs += pd[i];
+          }
+          rs += __shfl_xor(rs, 32);
+          l = l * alpha + rs;
+          m = mn;
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) o[dt] *= alpha;
+          if (drop) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int key = kb + acc_row(i, hh);
+              pd[i] = drop_keep(p.seed, bh, myq, key, T, p.dropout_p) ? pd[i] * rdrop : 0.f;
+            }
+          }
+        } else {
+          float rb[16];
+          rab16(L.f0, myq, kb, hh, rb);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) pd[i] = silu(fmaf(s[i], p.scale, rb[i]));
+          if (!fast) {
+            const unsigned mk = qok ? mask16(kb, hh, start, myq, si.contig, L.kvs) : 0u;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) pd[i] = ((mk >> i) & 1) ? pd[i] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 ph, pl;
+          pack_acc(pd, s2, ph, pl);
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            const bf16x8 vf = lds_tr8<HD>(L.img1, kb + 16 * s2, dt * 32, lane);
+            o[dt] = mfma(vf, ph, o[dt]);
+            if (PREC) o[dt] = mfma(vf, pl, o[dt]);
+          }
+        }
+      }
+      float mul = p.inv_n;
+      if (KIND == 0) {
+        mul = l > 0.f ? 1.0f / l : 0.f;
+        if (hh == 0 && qok && p.lse) p.lse[(int64_t)bh * T + myq] = l > 0.f ? (m + log2f(l)) * kLn2 : -INFINITY;
+      }
+      store_rows<HD, NDT>(p.out, p.ldo, p.out_f32, (int64_t)b * T + myq, h, hh, o, mul, qok);
+      GRK_STAMP(4 + ps);
+    }
+  GRK_STAMP(6);
+}
+
+// ================================================================ dQ =========
+template <int HD, int KIND, int PREC>
+__global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
+  const int T = p.T, nq = (T + 31) / 32, Tp = nq * 32;
+  SeqLds<HD> L(smem, Tp, kDqBinArrays);
+  // drab by distance d in [-kRabPad, Tp): bins[kRabPad + d], int64 fixed point
+  unsigned long long* bins = reinterpret_cast<unsigned long long*>(L.f1);
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const SeqInfo si = seq_info(p, b, T, L.sh);
+  const int start = si.start, first = start / 32, kbeg = first * 32;
+  const int ntiles = nq - first, npairs = (ntiles + 1) / 2;
+  const int bh = b * p.H + h;
+  bf16x8 qpre[KS], dpre[KS];
+  if (wave < npairs) {
+    const int row = (first + wave) * 32 + r;
+    load_frag<HD>(qpre, p.q, p.ldq, b, T, h, row, hh);
+    load_frag_any<HD>(dpre, p.dout, p.lddo, p.dout_f32, b, T, h, row, hh);
+  }
+  RabRegs rr;
+  if (KIND == 1) rr = load_rab(p, h, Tp);
+  stage_pair<HD>(L.img0, p.k, p.ldk, false, p.act, L.img1, p.v, p.ldv, false, p.act, b, T, h, kbeg, Tp);
+  if (KIND == 1) {
+    store_rab(L.f0, rr, Tp);
+    for (int j = threadIdx.x; j < Tp + kRabPad; j += blockDim.x) bins[j] = 0ull;
+  }
+  if (!si.contig) stage_kvs(L.kvs, p.key_valid, b, T, Tp);
+  __syncthreads();
+
+  const float sl2 = p.scale * kLog2e;
+  const float rdrop = 1.0f / (1.0f - p.dropout_p);
+  const bool drop = KIND == 0 && p.dropout_p > 0.f;
+
+  for (int qt = wave; qt < first; qt += kSeqWaves) {  // fully masked query rows: dq = 0
+    const int myq = qt * 32 + r;
+    f32x16 z[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) z[dt] = f32x16{};
+    store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, (int64_t)b * T + myq, h, hh, z, 0.f, myq < T);
+  }
+
+  for (int pu = wave; pu < npairs; pu += kSeqWaves)
+#pragma unroll
+    for (int ps = 0; ps < 2; ++ps) {
+      if (!pair_has(pu, ps, ntiles)) break;
+      const int q0 = (first + pair_tile(pu, ps, ntiles)) * 32, myq = q0 + r;
+      const bool qok = myq < T;
+      bf16x8 qf[KS], dof[KS];
+      if (pu == wave && ps == 0) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          qf[ks] = qpre[ks];
+          dof[ks] = dpre[ks];
+        }
+      } else {
+        load_frag<HD>(qf, p.q, p.ldq, b, T, h, myq, hh);
+        load_frag_any<HD>(dof, p.dout, p.lddo, p.dout_f32, b, T, h, myq, hh);
+      }
+      act_frag<HD>(qf, p.act);
+      float lse2 = 0.f, dlt = 0.f;
+      if (KIND == 0 && qok) {
+        lse2 = p.lse[(int64_t)bh * T + myq] * kLog2e;
+        dlt = p.delta[(int64_t)bh * T + myq];
+      }
+      const bool row_live = KIND == 1 || lse2 != -INFINITY;
+      f32x16 acc[NDT];
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) acc[dt] = f32x16{};
+      for (int kb = kbeg; kb <= q0; kb += 32) {
+        f32x16 s = f32x16{}, dp = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          s = mfma(lds_row8<HD>(L.img0, kb + r, 16 * ks + 8 * hh), qf[ks], s);
+          dp = mfma(lds_row8<HD>(L.img1, kb + r, 16 * ks + 8 * hh), dof[ks], dp);
+        }
+        const bool fast = si.contig && kb < q0 && kb >= start;
+        float ds[16];
+        const unsigned mk = fast ? 0xFFFFu : ((qok && row_live) ? mask16(kb, hh, start, myq, si.contig, L.kvs) : 0u);
+        if (KIND == 0) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float pv = ((mk >> i) & 1) ? exp2f(s[i] * sl2 - lse2) : 0.f;
+            float dpv = dp[i];
+            if (drop) dpv = drop_keep(p.seed, bh, myq, kb + acc_row(i, hh), T, p.dropout_p) ? dpv * rdrop : 0.f;
+            ds[i] = pv * (dpv - dlt);
+          }
+        } else {
+          float rb[16];
+          rab16(L.f0, myq, kb, hh, rb);
+          // d = myq - key >= -31: masked scores add 0 without a branch
+          unsigned long long* bb = bins + kRabPad + (myq - kb - 4 * hh) - 27;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float v = dp[i] * dsilu(fmaf(s[i], p.scale, rb[i])) * p.inv_n;
+            ds[i] = ((mk >> i) & 1) ? v : 0.f;
+          }
+          if (p.drab && __any(mk != 0))
+#pragma unroll
+            for (int i = 0; i < 16; ++i) atomicAdd(&bb[27 - ((i & 3) + 8 * (i >> 2))], to_fix(ds[i]));
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 dh, dl;
+          pack_acc(ds, s2, dh, dl);
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            const bf16x8 kf = lds_tr8<HD>(L.img0, kb + 16 * s2, dt * 32, lane);
+            acc[dt] = mfma(kf, dh, acc[dt]);
+            if (PREC) acc[dt] = mfma(kf, dl, acc[dt]);
+          }
+        }
+      }
+      store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, (int64_t)b * T + myq, h, hh, acc, p.scale, qok,
+                          p.act ? p.q : nullptr, p.ldq);
+    }
+  if (KIND == 1 && p.drab) {
+    __syncthreads();
+    for (int d = threadIdx.x; d < Tp; d += blockDim.x) {
+      const long long q = (long long)bins[kRabPad + d];
+      if (q != 0) atomicAdd(&p.drab[h * p.nb + min(d, p.nb - 1)], (float)((double)q * (1.0 / kFixScale)));
+    }
+  }
+}
+
+// ============================================================== dK / dV =====
+template <int HD, int KIND, int PREC>
+__global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
+  const int T = p.T, nq = (T + 31) / 32, Tp = nq * 32;
+  SeqLds<HD> L(smem, Tp);
+  float* lses = L.f0;  // softmax: per-query log2-domain lse, delta
+  float* dlts = L.f1;
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const SeqInfo si = seq_info(p, b, T, L.sh);
+  const int start = si.start, first = start / 32, kbeg = first * 32;
+  const int ntiles = nq - first, npairs = (ntiles + 1) / 2;
+  const int bh = b * p.H + h;
+  // key tile j (absolute first + j) visits query tiles j .. ntiles-1
+  bf16x8 kpre[KS], vpre[KS];
+  if (wave < npairs) {
+    const int row = (first + wave) * 32 + r;
+    load_frag<HD>(kpre, p.k, p.ldk, b, T, h, row, hh);
+    load_frag<HD>(vpre, p.v, p.ldv, b, T, h, row, hh);
+  }
+  RabRegs rr;
+  float lv[2], dl[2];
+  if (KIND == 1) {
+    rr = load_rab(p, h, Tp);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int j = threadIdx.x + k * blockDim.x;
+      lv[k] = -INFINITY;
+      dl[k] = 0.f;
+      if (j < T) {
+        lv[k] = p.lse[(int64_t)bh * T + j] * kLog2e;
+        dl[k] = p.delta[(int64_t)bh * T + j];
+      }
+    }
+  }
+  stage_pair<HD>(L.img0, p.q, p.ldq, false, p.act, L.img1, p.dout, p.lddo, p.dout_f32, false, b, T, h, kbeg, Tp);
+  if (KIND == 1) {
+    store_rab(L.f0, rr, Tp);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int j = threadIdx.x + k * blockDim.x;
+      if (j < Tp) {
+        lses[j] = lv[k];
+        dlts[j] = dl[k];
+      }
+    }
+  }
+  if (!si.contig) stage_kvs(L.kvs, p.key_valid, b, T, Tp);
+  __syncthreads();
+
+  const float sl2 = p.scale * kLog2e;
+  const float rdrop = 1.0f / (1.0f - p.dropout_p);
+  const bool drop = KIND == 0 && p.dropout_p > 0.f;
+
+  for (int kt = wave; kt < first; kt += kSeqWaves) {  // keys before the first valid one: no gradient
+    const int myk = kt * 32 + r;
+    f32x16 z[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) z[dt] = f32x16{};
+    store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, (int64_t)b * T + myk, h, hh, z, 0.f, myk < T);
+    store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, (int64_t)b * T + myk, h, hh, z, 0.f, myk < T);
+  }
+
+  for (int pu = wave; pu < npairs; pu += kSeqWaves)
+#pragma unroll
+    for (int ps = 0; ps < 2; ++ps) {
+      if (!pair_has(pu, ps, ntiles)) break;
+      const int k0 = (first + pair_tile(pu, ps, ntiles)) * 32, myk = k0 + r;
+      const bool kin = myk < T;
+      const bool kok = kin && myk >= start && (si.contig || L.kvs[myk]);
+      bf16x8 kf[KS], vf[KS];
+      if (pu == wave && ps == 0) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          kf[ks] = kpre[ks];
+          vf[ks] = vpre[ks];
+        }
+      } else {
+        load_frag<HD>(kf, p.k, p.ldk, b, T, h, myk, hh);
+        load_frag<HD>(vf, p.v, p.ldv, b, T, h, myk, hh);
+      }
+      act_frag<HD>(kf, p.act);
+      act_frag<HD>(vf, p.act);
+      f32x16 dk[NDT], dv[NDT];
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        dk[dt] = f32x16{};
+        dv[dt] = f32x16{};
+      }
+      for (int qb = k0; qb < Tp; qb += 32) {
+        f32x16 s = f32x16{}, dp = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          s = mfma(lds_row8<HD>(L.img0, qb + r, 16 * ks + 8 * hh), kf[ks], s);
+          dp = mfma(lds_row8<HD>(L.img1, qb + r, 16 * ks + 8 * hh), vf[ks], dp);
+        }
+        // every query after every key of the tile, all queries < T, keys valid
+        const bool fast = si.contig && qb > k0 && qb + 32 <= T && k0 >= start;
+        float pd[16], ds[16];
+        if (KIND == 0) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int qr = acc_row(i, hh), q = qb + qr;
+            const bool ok = fast | (kok & (q < T) & (myk <= q));
+            const float lq = lses[q];
+            const float e = exp2f(s[i] * sl2 - (lq == -INFINITY ? 0.f : lq));
+            const float pv = (ok & (lq != -INFINITY)) ? e : 0.f;
+            float dpv = dp[i];
+            pd[i] = pv;
+            if (drop) {
+              const bool keep = drop_keep(p.seed, bh, q, myk, T, p.dropout_p);
+              pd[i] = keep ? pv * rdrop : 0.f;
+              dpv = keep ? dpv * rdrop : 0.f;
+            }
+            ds[i] = pv * (dpv - dlts[q]);
+          }
+        } else {
+          // bias of (query qb + acc_row(i, hh), key myk): rabx[kRabPad + q - myk]
+          const float* rbase = L.f0 + kRabPad + (qb - myk + 4 * hh);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int qr = acc_row(i, hh), q = qb + qr;
+            const bool ok = fast | (kok & (q < T) & (myk <= q));
+            const float x = fmaf(s[i], p.scale, rbase[(i & 3) + 8 * (i >> 2)]);
+            const float sg = sigmoid_fast(x);
+            pd[i] = ok ? x * sg * p.inv_n : 0.f;
+            ds[i] = ok ? dp[i] * (sg * (1.0f + x * (1.0f - sg))) * p.inv_n : 0.f;
+          }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 ph, pl, dh, dl2;
+          pack_acc(pd, s2, ph, pl);
+          pack_acc(ds, s2, dh, dl2);
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            const bf16x8 dof = lds_tr8<HD>(L.img1, qb + 16 * s2, dt * 32, lane);
+            const bf16x8 qf = lds_tr8<HD>(L.img0, qb + 16 * s2, dt * 32, lane);
+            dv[dt] = mfma(dof, ph, dv[dt]);
+            dk[dt] = mfma(qf, dh, dk[dt]);
+            if (PREC) {
+              dv[dt] = mfma(dof, pl, dv[dt]);
+              dk[dt] = mfma(qf, dl2, dk[dt]);
+            }
+          }
+        }
+      }
+      const int64_t otok = (int64_t)b * T + myk;
+      store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, otok, h, hh, dk, p.scale, kin, p.act ? p.k : nullptr, p.ldk);
+      store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, 1.f, kin, p.act ? p.v : nullptr, p.ldv);
+    }
+}
+
+// Launch with `lds` bytes of dynamic LDS; above 64 KiB the kernel's limit is
+// raised first (once per kernel and size; gfx950 allows up to 160 KiB).
+static void launch_lds(void (*kernel)(AttnParams), dim3 grid, int threads, size_t lds, hipStream_t s,
+                       const AttnParams& p) {
+  if (lds > 64 * 1024) {
+    static thread_local const void* last_k = nullptr;
+    static thread_local size_t last_b = 0;
+    if (last_k != (const void*)kernel || last_b < lds) {
+      (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      last_k = (const void*)kernel;
+      last_b = lds;
+    }
+  }
+  kernel<<<grid, threads, lds, s>>>(p);
+}
+
+template <int HD>
+static bool seq_launch_hd(const AttnParams& p, int which, hipStream_t s) {
+  const int Tp = (p.T + 31) / 32 * 32;
+  const size_t lds = SeqLds<HD>::bytes(Tp, which == 2 ? kDqBinArrays : 1);
+  if (lds > (size_t)kSeqLdsMax || Tp + kRabPad > 2 * 64 * kSeqWaves) return false;
+  const dim3 grid(p.B * p.H);
+  const int threads = 64 * kSeqWaves;
+#define GRK_SEQ(KERNEL)                                                                                  \
+  do {                                                                                                   \
+    if (p.kind == GRK_ATTN_SOFTMAX) {                                                                    \
+      if (p.precise) launch_lds(KERNEL<HD, 0, 1>, grid, threads, lds, s, p);                             \
+      else launch_lds(KERNEL<HD, 0, 0>, grid, threads, lds, s, p);                                       \
+    } else {                                                                                             \
+      if (p.precise) launch_lds(KERNEL<HD, 1, 1>, grid, threads, lds, s, p);                             \
+      else launch_lds(KERNEL<HD, 1, 0>, grid, threads, lds, s, p);                                       \
+    }                                                                                                    \
+  } while (0)
+  if (which == 0) GRK_SEQ(k_attn_fwd_seq);
+  else if (which == 2) GRK_SEQ(k_attn_dq_seq);
+  else GRK_SEQ(k_attn_dkdv_seq);
+#undef GRK_SEQ
+  return true;
+}
+
+bool attn_seq_launch(const AttnParams& p, int hd, int which, hipStream_t s) {
+  static const bool chunked = getenv("GRK_ATTN_CHUNKED") != nullptr;  // force the chunked kernels (A/B tests)
+  if (chunked) return false;
+  switch (hd) {
+    case 16: return seq_launch_hd<16>(p, which, s);
+    case 32: return seq_launch_hd<32>(p, which, s);
+    case 64: return seq_launch_hd<64>(p, which, s);
+    case 128: return seq_launch_hd<128>(p, which, s);
+  }
+  return false;
+}
+
+}  // namespace grk
+
+using namespace grk;
+
+extern "C" int grk_seq_ranges(const uint8_t* key_valid, int batch, int seq_len, int32_t* ranges, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(batch >= 0 && seq_len > 0, "batch must be >= 0 and seq_len > 0");
+  if (batch == 0) return GRK_OK;
+  GRK_CHECK_ARG(key_valid && ranges, "key_valid and ranges required");
+  k_seq_ranges<<<(batch + 3) / 4, 256, 0, (hipStream_t)stream>>>(key_valid, batch, seq_len, ranges);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}

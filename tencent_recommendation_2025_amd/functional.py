@@ -137,42 +137,44 @@ def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extra=
 # ------------------------------------------------------------- attention ----
 class _SoftmaxMHAFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, key_valid, B, T, H, hd, dropout_p, seed, precise):
+    def forward(ctx, qkv, key_valid, B, T, H, hd, dropout_p, seed, precise, seq_range):
         D = H * hd
         out_dt = qkv.dtype
         xb = qkv if qkv.dtype == torch.bfloat16 else qkv.to(torch.bfloat16)
         xb = xb.contiguous()
         args = K.attn_args(L.ATTN_SOFTMAX, xb[:, :D], xb[:, D:2 * D], xb[:, 2 * D:3 * D], B, T, H, hd,
-                           key_valid=key_valid, dropout_p=dropout_p, seed=seed, precise=precise, out_dtype=out_dt)
+                           key_valid=key_valid, dropout_p=dropout_p, seed=seed, precise=precise, out_dtype=out_dt,
+                           seq_range=seq_range)
         out = torch.empty(B * T, D, dtype=out_dt, device=qkv.device)
         lse = torch.empty(B, H, T, dtype=torch.float32, device=qkv.device)
         K.attention_fwd(args, out, lse)
-        ctx.save_for_backward(xb, out, lse, key_valid)
+        ctx.save_for_backward(xb, out, lse, key_valid, seq_range)
         ctx.meta = (B, T, H, hd, dropout_p, seed, precise, out_dt)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        xb, out, lse, key_valid = ctx.saved_tensors
+        xb, out, lse, key_valid, seq_range = ctx.saved_tensors
         B, T, H, hd, dropout_p, seed, precise, out_dt = ctx.meta
         D = H * hd
         args = K.attn_args(L.ATTN_SOFTMAX, xb[:, :D], xb[:, D:2 * D], xb[:, 2 * D:3 * D], B, T, H, hd,
-                           key_valid=key_valid, dropout_p=dropout_p, seed=seed, precise=precise, out_dtype=out_dt)
+                           key_valid=key_valid, dropout_p=dropout_p, seed=seed, precise=precise, out_dtype=out_dt,
+                           seq_range=seq_range)
         dqkv = torch.empty(B * T, 3 * D, dtype=out_dt, device=xb.device)
         delta = torch.empty(B, H, T, dtype=torch.float32, device=xb.device)
         gout = gout.contiguous()
         if gout.dtype not in (torch.float32, torch.bfloat16):
             gout = gout.float()
         K.attention_bwd(args, out, gout, lse, delta, dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:])
-        return dqkv, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None
 
 
 @_disable
-def softmax_mha(qkv, key_valid, B, T, H, hd, dropout_p=0.0, seed=0, precise=None):
+def softmax_mha(qkv, key_valid, B, T, H, hd, dropout_p=0.0, seed=0, precise=None, seq_range=None):
     """Causal + key-padding softmax attention on a packed [B*T, 3D] (q|k|v) tensor."""
     if precise is None:
         precise = qkv.dtype == torch.float32
-    return _SoftmaxMHAFn.apply(qkv, key_valid, B, T, H, hd, float(dropout_p), int(seed), bool(precise))
+    return _SoftmaxMHAFn.apply(qkv, key_valid, B, T, H, hd, float(dropout_p), int(seed), bool(precise), seq_range)
 
 
 class _HSTUCoreFn(torch.autograd.Function):
@@ -187,24 +189,24 @@ class _HSTUCoreFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps, precise, dropout_p, seed):
+    def forward(ctx, pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps, precise, dropout_p, seed, seq_range):
         D = H * hd
         pb = pre.to(torch.bfloat16).contiguous()
         rab32 = rab.float().contiguous()
         args = K.attn_args(L.ATTN_HSTU, pb[:, 2 * D:3 * D], pb[:, 3 * D:], pb[:, D:2 * D], B, T, H, hd,
                            key_valid=key_valid, scale=hd ** -0.5, rab=rab32, inv_n=inv_n, precise=precise,
-                           out_dtype=torch.bfloat16, act='silu')
+                           out_dtype=torch.bfloat16, act='silu', seq_range=seq_range)
         o = torch.empty(B * T, D, dtype=torch.bfloat16, device=pre.device)
         K.attention_fwd(args, o)
         w32, b32 = ln_w.float().contiguous(), ln_b.float().contiguous()
         y, stats = K.norm_gate_fwd(o, pb[:, :D], w32, b32, eps, dropout_p, seed)
-        ctx.save_for_backward(pb, o, stats, rab32, w32, b32, key_valid)
+        ctx.save_for_backward(pb, o, stats, rab32, w32, b32, key_valid, seq_range)
         ctx.meta = (B, T, H, hd, inv_n, precise, dropout_p, seed, pre.dtype, rab.dtype, ln_w.dtype, ln_b.dtype)
         return y if pre.dtype == torch.bfloat16 else y.to(pre.dtype)
 
     @staticmethod
     def backward(ctx, gy):
-        pb, o, stats, rab32, w32, b32, key_valid = ctx.saved_tensors
+        pb, o, stats, rab32, w32, b32, key_valid, seq_range = ctx.saved_tensors
         B, T, H, hd, inv_n, precise, dropout_p, seed, pdt, rdt, wdt, bdt = ctx.meta
         D = H * hd
         gy = gy.to(torch.bfloat16)
@@ -214,17 +216,18 @@ class _HSTUCoreFn(torch.autograd.Function):
         drab = torch.zeros_like(rab32)
         args = K.attn_args(L.ATTN_HSTU, pb[:, 2 * D:3 * D], pb[:, 3 * D:], pb[:, D:2 * D], B, T, H, hd,
                            key_valid=key_valid, scale=hd ** -0.5, rab=rab32, inv_n=inv_n, precise=precise,
-                           out_dtype=torch.bfloat16, act='silu')
+                           out_dtype=torch.bfloat16, act='silu', seq_range=seq_range)
         K.attention_bwd(args, None, do, None, None, dpre[:, 2 * D:3 * D], dpre[:, 3 * D:], dpre[:, D:2 * D], drab)
         return (dpre if pdt == torch.bfloat16 else dpre.to(pdt), drab.to(rdt), dw.to(wdt), db.to(bdt),
-                None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None)
 
 
 @_disable
-def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, precise=False, dropout_p=0.0, seed=0):
+def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, precise=False, dropout_p=0.0, seed=0,
+              seq_range=None):
     """Fused HSTU layer core on the [B*T, 4D] uvqk pre-activation (see _HSTUCoreFn)."""
     return _HSTUCoreFn.apply(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, float(inv_n), float(eps), bool(precise),
-                             float(dropout_p), int(seed))
+                             float(dropout_p), int(seed), seq_range)
 
 
 # ---------------------------------------------------------------- logits ----

@@ -184,11 +184,12 @@ def _col_view_ok(t, name):
 
 
 def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, inv_n=1.0, dropout_p=0.0, seed=0,
-              precise=False, out_dtype=torch.bfloat16, act=None):
+              precise=False, out_dtype=torch.bfloat16, act=None, seq_range=None):
     """Build grk_attn_args for bf16 [B*T, ld] column views q/k/v (head h at cols h*hd).
 
     act="silu": q/k/v are pre-activations; SiLU is applied on load and the
-    backward's dq/dk/dv are gradients w.r.t. the pre-activations."""
+    backward's dq/dk/dv are gradients w.r.t. the pre-activations.
+    seq_range: optional int32 [B, 2] from seq_ranges(key_valid) (computed once per step)."""
     for t, n in ((q, 'q'), (k, 'k'), (v, 'v')):
         _col_view_ok(t, n)
         if t.shape[0] != B * T or t.shape[1] < H * hd:
@@ -197,16 +198,34 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
         if key_valid.dtype != torch.uint8 or key_valid.shape != (B, T) or not key_valid.is_contiguous():
             raise L.GrkError('key_valid must be a contiguous uint8 [B, T] tensor')
     nb = 0
+    if seq_range is not None and (seq_range.dtype != torch.int32 or seq_range.shape != (B, 2)
+                                  or not seq_range.is_contiguous()):
+        raise L.GrkError('seq_range must be a contiguous int32 [B, 2] tensor (kernels.seq_ranges)')
     if kind == L.ATTN_HSTU:
         if rab is None or rab.dtype != torch.float32 or rab.dim() != 2 or rab.shape[0] != H or not rab.is_contiguous():
             raise L.GrkError('hstu needs a contiguous fp32 rab [H, num_buckets]')
         nb = rab.shape[1]
     if scale is None:
         scale = hd ** -0.5
-    return L.GrkAttnArgs(kind, B, H, T, hd, nb, q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0),
+    args = L.GrkAttnArgs(kind, B, H, T, hd, nb, q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0),
                          v.stride(0), _ptr(key_valid), _ptr(rab), float(scale), float(inv_n), float(dropout_p),
                          int(bool(precise)), int(seed) & (2 ** 64 - 1), L.dtype_code(out_dtype),
-                         {None: L.ACT_NONE, 'silu': L.ACT_SILU}[act])
+                         {None: L.ACT_NONE, 'silu': L.ACT_SILU}[act], _ptr(seq_range))
+    args._keep = (q, k, v, key_valid, rab, seq_range)  # the struct holds raw pointers: keep the tensors alive
+    return args
+
+
+def seq_ranges(key_valid):
+    """int32 [B, 2]: (first valid key, contiguous flag) per sequence (grk_seq_ranges)."""
+    _require_cuda(key_valid)
+    if key_valid.dtype != torch.uint8 or key_valid.dim() != 2 or not key_valid.is_contiguous():
+        raise L.GrkError('key_valid must be a contiguous uint8 [B, T] tensor')
+    B, T = key_valid.shape
+    out = torch.empty(B, 2, dtype=torch.int32, device=key_valid.device)
+    rc = L.lib().grk_seq_ranges(key_valid.data_ptr() if B else None, B, T, out.data_ptr() if B else None,
+                                L.stream_ptr(key_valid.device))
+    L.check(rc, 'grk_seq_ranges')
+    return out
 
 
 def attention_fwd(args, out, lse=None):

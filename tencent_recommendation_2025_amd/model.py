@@ -32,6 +32,7 @@ import torch.nn.functional as F
 
 from . import _lib as L
 from . import functional as G
+from . import kernels as K
 from .dataset import MM_SHAPE, save_emb, tensorize
 
 
@@ -54,7 +55,7 @@ class FlashMultiHeadAttention(torch.nn.Module):
         self.v_linear = torch.nn.Linear(hidden_units, hidden_units)
         self.out_linear = torch.nn.Linear(hidden_units, hidden_units)
 
-    def forward(self, query, key, value, attn_mask=None, key_valid=None):
+    def forward(self, query, key, value, attn_mask=None, key_valid=None, seq_range=None):
         B, T, D = query.shape
         if key_valid is None:
             key_valid = key_valid_from_mask(attn_mask, B, T)
@@ -66,7 +67,8 @@ class FlashMultiHeadAttention(torch.nn.Module):
             qkv = torch.cat([self.q_linear(query), self.k_linear(key), self.v_linear(value)], -1)
         p = self.dropout_rate if self.training else 0.0
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
-        o = G.softmax_mha(qkv.reshape(B * T, 3 * D), key_valid, B, T, self.num_heads, self.head_dim, p, seed)
+        o = G.softmax_mha(qkv.reshape(B * T, 3 * D), key_valid, B, T, self.num_heads, self.head_dim, p, seed,
+                          seq_range=seq_range)
         return self.out_linear(o.view(B, T, D)), None
 
 
@@ -104,7 +106,7 @@ class HSTUAttention(torch.nn.Module):
         self.attn_norm = torch.nn.LayerNorm(hidden_units, eps=1e-8)
         self.out_linear = torch.nn.Linear(hidden_units, hidden_units)
 
-    def forward(self, query, key=None, value=None, attn_mask=None, key_valid=None):
+    def forward(self, query, key=None, value=None, attn_mask=None, key_valid=None, seq_range=None):
         B, T, D = query.shape
         if key_valid is None:
             key_valid = key_valid_from_mask(attn_mask, B, T)
@@ -112,7 +114,8 @@ class HSTUAttention(torch.nn.Module):
         p = self.dropout_rate if self.training else 0.0
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
         y = G.hstu_core(pre, self.rab, self.attn_norm.weight, self.attn_norm.bias, key_valid, B, T,
-                        self.num_heads, self.head_dim, 1.0 / T, self.attn_norm.eps, dropout_p=p, seed=seed)
+                        self.num_heads, self.head_dim, 1.0 / T, self.attn_norm.eps, dropout_p=p, seed=seed,
+                        seq_range=seq_range)
         return self.out_linear(y.view(B, T, D)), None
 
 
@@ -346,16 +349,17 @@ class BaselineModel(torch.nn.Module):
         seqs = seqs * self.item_emb.embedding_dim ** 0.5 + pos_rows.view(B, T, -1)
         seqs = self.emb_dropout(seqs)
         key_valid = (mask.to(dev, non_blocking=True) != 0).to(torch.uint8).contiguous()
+        kw = dict(key_valid=key_valid, seq_range=K.seq_ranges(key_valid))  # one launch serves every layer
         for i in range(len(self.attention_layers)):
             if self.block == 'hstu':
-                y, _ = self.attention_layers[i](self.attention_layernorms[i](seqs), key_valid=key_valid)
+                y, _ = self.attention_layers[i](self.attention_layernorms[i](seqs), **kw)
                 seqs = seqs + y
             elif self.norm_first:
                 x = self.attention_layernorms[i](seqs)
-                seqs = seqs + self.attention_layers[i](x, x, x, key_valid=key_valid)[0]
+                seqs = seqs + self.attention_layers[i](x, x, x, **kw)[0]
                 seqs = seqs + self.forward_layers[i](self.forward_layernorms[i](seqs))
             else:
-                y, _ = self.attention_layers[i](seqs, seqs, seqs, key_valid=key_valid)
+                y, _ = self.attention_layers[i](seqs, seqs, seqs, **kw)
                 seqs = self.attention_layernorms[i](seqs + y)
                 seqs = self.forward_layernorms[i](seqs + self.forward_layers[i](seqs))
         return self.last_layernorm(seqs)

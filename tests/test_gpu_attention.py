@@ -68,12 +68,15 @@ def drop_mask_np(seed, B, H, T, p):
     return (u >= np.float32(p)).reshape(B, H, T, T)
 
 
-def run(K, kind, B, T, H, hd, lens, precise, seed=0, dropout=0.0, nb=None, out_dtype=torch.float32, act=None):
+def run(K, kind, B, T, H, hd, lens, precise, seed=0, dropout=0.0, nb=None, out_dtype=torch.float32, act=None,
+        holes=False, use_ranges=False):
     """act='silu': x holds pre-activations; the oracle sees SiLU(x) rounded to bf16
     and its q/k/v gradients are chained through dSiLU(x)."""
     from tencent_recommendation_2025_amd import _lib as L
     D = H * hd
     x, valid = make_inputs(B, T, H, hd, lens, seed)
+    if holes:  # non-contiguous key validity (not the dataset's left padding): the masked path
+        valid[:, ::7] = 0
     pre = x
     xd = torch.from_numpy(x).to(DEV).to(torch.bfloat16)
     q, k, v = xd[:, :D], xd[:, D:2 * D], xd[:, 2 * D:]
@@ -87,7 +90,7 @@ def run(K, kind, B, T, H, hd, lens, precise, seed=0, dropout=0.0, nb=None, out_d
         rab = torch.from_numpy(rab_np).to(DEV)
         extra = dict(rab=rab, inv_n=1.0 / T, scale=hd ** -0.5)
     args = K.attn_args(kind, q, k, v, B, T, H, hd, key_valid=kv, precise=precise, dropout_p=dropout, seed=1234,
-                       out_dtype=out_dtype, act=act, **extra)
+                       out_dtype=out_dtype, act=act, seq_range=K.seq_ranges(kv) if use_ranges else None, **extra)
     if act == 'silu':
         x = to_bf16_f32((pre / (1.0 + np.exp(-pre.astype(np.float64)))).astype(np.float32))
     out = torch.empty(B * T, D, dtype=out_dtype, device=DEV)
@@ -184,6 +187,40 @@ def test_determinism(K):
 def test_silu_on_load_matches_oracle(K, kind):
     """GRK_ACT_SILU: q/k/v are pre-activations; dq/dk/dv are w.r.t. them."""
     res, want, _ = run(K, kind, B=3, T=201, H=2, hd=64, lens=[201, 120, 7], precise=True, act='silu')
+    for key in ('out', 'dq', 'dk', 'dv') + (('drab',) if kind == 1 else ()):
+        err = nrel(res[key], want[key])
+        assert err < TOL_PRECISE, f'{key}: normwise rel err {err:.2e}'
+
+
+def test_seq_ranges(K):
+    valid = np.zeros((5, 40), np.uint8)
+    valid[0, 10:] = 1          # left padding
+    valid[1, :] = 1            # full
+    valid[2, 5:20] = 1         # hole at the end: not contiguous to T
+    valid[3, [3, 9]] = 1       # scattered
+    got = K.seq_ranges(torch.from_numpy(valid).to(DEV)).cpu().numpy()  # row 4: no valid key
+    np.testing.assert_array_equal(got, [[10, 1], [0, 1], [5, 0], [3, 0], [40, 1]])
+
+
+@pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
+def test_precomputed_ranges_bitwise_equal(K, kind):
+    a, _, _ = run(K, kind, B=3, T=201, H=2, hd=64, lens=[201, 120, 7], precise=False, act='silu' if kind else None)
+    b, _, _ = run(K, kind, B=3, T=201, H=2, hd=64, lens=[201, 120, 7], precise=False, act='silu' if kind else None,
+                  use_ranges=True)
+    for key in a:
+        if key == 'lse' and kind == 1:
+            continue  # HSTU writes no lse
+        if key == 'drab':  # float atomics: order-dependent (documented in include/grk.h)
+            np.testing.assert_allclose(a[key], b[key], rtol=1e-5, atol=1e-7)
+            continue
+        assert np.array_equal(a[key], b[key]), key
+
+
+@pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
+@pytest.mark.parametrize('use_ranges', [False, True])
+def test_non_contiguous_key_valid(K, kind, use_ranges):
+    res, want, _ = run(K, kind, B=3, T=150, H=2, hd=64, lens=[150, 90, 40], precise=True, holes=True,
+                       use_ranges=use_ranges)
     for key in ('out', 'dq', 'dk', 'dv') + (('drab',) if kind == 1 else ()):
         err = nrel(res[key], want[key])
         assert err < TOL_PRECISE, f'{key}: normwise rel err {err:.2e}'
