@@ -149,6 +149,14 @@ int grk_table_adamw(void* param, int param_dtype, float* exp_avg, float* exp_avg
                     int32_t* row_slot, grk_adamw_hparams hp, int mode, void* stream);
 
 
+/* Dense AdamW of num_rows rows from a dense gradient [num_rows, grad_ld]
+ * (grad_dtype GRK_F32 / GRK_BF16): the update of tables whose gradient comes
+ * out of a dense op (the dnn-projected feature tables, model.py).  Same update
+ * order as grk_table_adamw; param / moments may point inside a larger table. */
+int grk_table_adamw_dense(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows,
+                          int dim, const void* grad, int grad_dtype, int64_t grad_ld, grk_adamw_hparams hp,
+                          void* stream);
+
 /* ------------------------------------------------------------------------
  * Causal attention (MFMA 32x32x16 bf16)
  *   GRK_ATTN_SOFTMAX: softmax(scale * QK^T + mask) V with dropout -- the

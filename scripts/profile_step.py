@@ -1,0 +1,74 @@
+"""Where does one bench training step spend its time, host and device?
+
+    python scripts/profile_step.py [--batch 128] [--steps 3] [--trace gpurun_out/step_trace.json]
+
+Prints per-phase wall times (forward / backward / optimizer, each closed by a
+device synchronize, so a phase's wall = max(host issue, device execution))
+and torch.profiler's top host-side ops by self CPU time.
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--batch', type=int, default=128)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--trace', default=None)
+    a = ap.parse_args()
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel, init_reference_
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    cfg = S.SyntheticConfig(batch_size=a.batch)
+    stats, types = S.feature_schema(cfg)
+    torch.manual_seed(0)
+    m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, S.make_args()).cuda()
+    init_reference_(m, seed=0, live_norms=True)
+    opt = FusedAdamW(m, lr=1e-3)
+    tr = Trainer(m, opt, loss='bce')
+    g = torch.Generator(device='cuda').manual_seed(0)
+    batches = [S.make_batch(cfg, g, 'cuda') for _ in range(4)]
+    for i in range(3):
+        tr.step(batches[i % 4])
+    torch.cuda.synchronize()
+
+    def phases(b):
+        t = [time.perf_counter()]
+        opt.zero_grad()
+        loss = tr.compute_loss(b)
+        torch.cuda.synchronize(); t.append(time.perf_counter())
+        loss.backward()
+        torch.cuda.synchronize(); t.append(time.perf_counter())
+        opt.step()
+        torch.cuda.synchronize(); t.append(time.perf_counter())
+        return [1e3 * (y - x) for x, y in zip(t, t[1:])]
+
+    res = [phases(batches[i % 4]) for i in range(a.steps)]
+    for name, k in (('forward', 0), ('backward', 1), ('optimizer', 2)):
+        print(f'{name:10s} {min(r[k] for r in res):8.2f} ms (min of {a.steps})')
+    # host issue time alone: no synchronize inside the step
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        tr.step(batches[i % 4])
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f'async steps: host issue {1e3 * (t1 - t0) / a.steps:.2f} ms/step, wall {1e3 * (t2 - t0) / a.steps:.2f} ms/step')
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU]) as prof:
+        tr.step(batches[0])
+        torch.cuda.synchronize()
+    print(prof.key_averages().table(sort_by='self_cpu_time_total', row_limit=25))
+    if a.trace:
+        prof.export_chrome_trace(a.trace)
+
+
+if __name__ == '__main__':
+    main()

@@ -74,6 +74,7 @@ SIGNATURES = {
     'grk_embedding_backward': (_I, [C.POINTER(GrkLookup), _I, _I, _I, _I, _P, C.c_int32, _I64, _I64, _P, _P, _P,
                                     _P, _P, _P, _SZ, _P, _P]),
     'grk_table_adamw': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _P, _I64, _P, GrkAdamwHparams, _I, _P]),
+    'grk_table_adamw_dense': (_I, [_P, _I, _P, _P, _I64, _I, _P, _I, _I64, GrkAdamwHparams, _P]),
     'grk_attention_fwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _P]),
     'grk_attention_bwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64, _P, _I64,
                                _P, _P]),

@@ -107,6 +107,30 @@ __global__ void __launch_bounds__(256) k_adamw_dense(P* __restrict__ param, floa
   adam_vec<P, NV>(param + off, m + off, v + off, g, hp);
 }
 
+// Dense gradient of any dtype ([rows, grad_ld], GT = float or bf16): every
+// row moves; one NV-vector per thread over a full grid as k_adamw_dense.
+template <typename P, typename GT, int NV>
+__global__ void __launch_bounds__(256) k_adamw_dense_grad(P* __restrict__ param, float* __restrict__ m,
+                                                          float* __restrict__ v, int64_t num_rows, int dim,
+                                                          const GT* __restrict__ grad, int64_t grad_ld,
+                                                          grk_adamw_hparams hp) {
+  const int q = dim / NV;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= num_rows * q) return;
+  const int64_t row = i / q;
+  const int c = (int)(i - row * q) * NV;
+  float g[NV];
+  const GT* src = grad + row * grad_ld + c;
+  if constexpr (sizeof(GT) == 4) {
+    load_grad<NV>(reinterpret_cast<const float*>(src), g);
+  } else {
+#pragma unroll
+    for (int e = 0; e < NV; ++e) g[e] = bf16_to_f32(reinterpret_cast<const bf16_t*>(src)[e]);
+  }
+  const int64_t off = row * dim + c;
+  adam_vec<P, NV>(param + off, m + off, v + off, g, hp);
+}
+
 template <typename P, int NV>
 __global__ void __launch_bounds__(256) k_adamw_lazy(P* __restrict__ param, float* __restrict__ m,
                                                     float* __restrict__ v, int dim,
@@ -174,5 +198,35 @@ extern "C" int grk_table_adamw(void* param, int param_dtype, float* exp_avg, flo
     k_reset_slots<<<grid_for(max_uniq, 256, 1024), 256, 0, s>>>(row_slot, uniq_ids, uniq_count, max_uniq);
     GRK_LAUNCH_CHECK();
   }
+  return GRK_OK;
+}
+
+extern "C" int grk_table_adamw_dense(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
+                                     int64_t num_rows, int dim, const void* grad, int grad_dtype, int64_t grad_ld,
+                                     grk_adamw_hparams hp, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(num_rows >= 0, "num_rows must be >= 0");
+  if (num_rows == 0) return GRK_OK;
+  GRK_CHECK_ARG(param && exp_avg && exp_avg_sq && grad, "param / exp_avg / exp_avg_sq / grad required");
+  GRK_CHECK_ARG(param_dtype == GRK_F32 || param_dtype == GRK_BF16, "bad param dtype");
+  GRK_CHECK_ARG(grad_dtype == GRK_F32 || grad_dtype == GRK_BF16, "bad grad dtype");
+  GRK_CHECK_ARG(dim > 0 && dim % 4 == 0 && grad_ld >= dim && grad_ld % 4 == 0, "dim / grad_ld must be multiples of 4");
+  GRK_CHECK_ARG(hp.bias_corr2_sqrt > 0.f, "bias_corr2_sqrt must be > 0");
+  const bool v8 = dim % 8 == 0 && grad_ld % 8 == 0;
+  const int64_t work = num_rows * (dim / (v8 ? 8 : 4));
+  GRK_CHECK_ARG((work + 255) / 256 < (int64_t)1 << 31, "table too large for one launch");
+  const unsigned g = (unsigned)((work + 255) / 256);
+  hipStream_t s = (hipStream_t)stream;
+#define GRK_DG(P, GT, NV) k_adamw_dense_grad<P, GT, NV><<<g, 256, 0, s>>>((P*)param, exp_avg, exp_avg_sq, num_rows, \
+                                                                         dim, (const GT*)grad, grad_ld, hp)
+  if (param_dtype == GRK_BF16) {
+    if (grad_dtype == GRK_BF16) { if (v8) GRK_DG(bf16_t, bf16_t, 8); else GRK_DG(bf16_t, bf16_t, 4); }
+    else { if (v8) GRK_DG(bf16_t, float, 8); else GRK_DG(bf16_t, float, 4); }
+  } else {
+    if (grad_dtype == GRK_BF16) { if (v8) GRK_DG(float, bf16_t, 8); else GRK_DG(float, bf16_t, 4); }
+    else { if (v8) GRK_DG(float, float, 8); else GRK_DG(float, float, 4); }
+  }
+#undef GRK_DG
+  GRK_LAUNCH_CHECK();
   return GRK_OK;
 }

@@ -45,7 +45,7 @@ class _FeatureLookupFn(torch.autograd.Function):
     materialised or accumulated."""
 
     @staticmethod
-    def forward(ctx, specs, token_type, seq_len, num_tokens, out_ld, extra, extra_col, splits, *weights):
+    def forward(ctx, specs, token_type, seq_len, num_tokens, out_ld, extras, splits, *weights):
         dt = specs[0].ref.weight.dtype
         dev = specs[0].ref.weight.device
         out = torch.empty(num_tokens, out_ld, dtype=dt, device=dev)
@@ -54,10 +54,9 @@ class _FeatureLookupFn(torch.autograd.Function):
             K.embedding_gather(lookups[i:i + L.MAX_FEATURES], out, num_tokens, token_type, seq_len)
         if GATHER_TRACE is not None:
             GATHER_TRACE.append((lookups, out, num_tokens, token_type, seq_len))
-        if extra is not None:
-            out[:, extra_col:extra_col + extra.shape[1]] = extra.to(dt)
+        for col, x in extras:
+            out[:, col:col + x.shape[1]] = x.to(dt)
         ctx.specs, ctx.token_type, ctx.seq_len, ctx.splits = specs, token_type, seq_len, splits
-        ctx.extra_info = None if extra is None else (extra_col, extra.shape[1], extra.dtype)
         ctx.n_weights = len(weights)
         ctx.weight_ids = [id(w) for w in weights]
         return tuple(out[:, a:b] for a, b in splits)
@@ -105,22 +104,20 @@ class _FeatureLookupFn(torch.autograd.Function):
             if s.ref.group is not None:
                 s.ref.group.collect(K.GradSource(s.idx, g, c, s.mode, s.bag, s.ref.row_offset,
                                                  s.ref.weight.shape[0]), ctx.token_type, ctx.seq_len)
-        g_extra = None
-        if ctx.extra_info is not None:
-            c0, w, dt = ctx.extra_info
-            g, c = locate(c0, w)
-            g_extra = None if g is None else g[:, c:c + w].to(dt)
-        return (None, None, None, None, None, g_extra, None, None, *grads)
+        # extras are dense inputs (features, constants): no gradient is propagated to them
+        return (None, None, None, None, None, None, None, *grads)
 
 
 @_disable
-def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extra=None, extra_col=0, splits=None):
+def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extras=(), splits=None):
     """Fused multi-table gather (+ bag sums) into one [num_tokens, out_ld] buffer.
 
-    Returns the buffer's column blocks ``splits`` (list of (start, end);
-    default: the whole buffer, returned as a single tensor).  Drop-in tables
-    get dense gradients through autograd; grouped tables push row-sparse
-    gradient sources into their group's sink."""
+    ``extras``: (column, [num_tokens, w] tensor) blocks copied into the buffer
+    (dense features, constants; treated as non-differentiable).  Returns the
+    buffer's column blocks ``splits`` (list of (start, end); default: the whole
+    buffer, returned as a single tensor).  Drop-in tables get dense gradients
+    through autograd; grouped tables push row-sparse gradient sources into
+    their group's sink."""
     weights, seen = [], set()
     for s in specs:
         if s.ref.group is None and id(s.ref.weight) not in seen and s.ref.weight.requires_grad:
@@ -130,8 +127,43 @@ def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extra=
         token_type = token_type.to(torch.int32).contiguous()
     single = splits is None
     splits = tuple((0, out_ld) if single else ((int(a), int(b)) for a, b in splits))
-    outs = _FeatureLookupFn.apply(specs, token_type, seq_len, num_tokens, out_ld, extra, extra_col, splits, *weights)
+    extras = tuple((int(c), x) for c, x in extras)
+    outs = _FeatureLookupFn.apply(specs, token_type, seq_len, num_tokens, out_ld, extras, splits, *weights)
     return outs[0] if single else outs
+
+
+class _GroupStackFn(torch.autograd.Function):
+    """Equally-sized tables of a TableGroup as one [G, rows, D] tensor for use
+    in differentiable torch ops (a view of the group buffer when the tables
+    are adjacent); the backward hands the dense gradient to the group (fused
+    optimizer) instead of autograd (the group's weight views do not require
+    grad)."""
+
+    @staticmethod
+    def forward(ctx, anchor, group, offsets, rows):
+        ctx.group, ctx.offsets, ctx.rows = group, offsets, rows
+        o0 = offsets[0]
+        ctx.contiguous = all(o == o0 + j * rows for j, o in enumerate(offsets))
+        if ctx.contiguous:
+            return group.flat[o0:o0 + len(offsets) * rows].view(len(offsets), rows, -1)
+        return torch.stack([group.flat[o:o + rows] for o in offsets])
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.contiguous:
+            ctx.group.collect_dense(ctx.offsets[0], g.reshape(-1, g.shape[-1]))
+        else:
+            for j, o in enumerate(ctx.offsets):
+                ctx.group.collect_dense(o, g[j])
+        return None, None, None, None
+
+
+_ANCHOR = torch.zeros((), requires_grad=True)  # makes _GroupStackFn's output part of the graph
+
+
+@_disable
+def group_stack(group, offsets, rows):
+    return _GroupStackFn.apply(_ANCHOR, group, tuple(offsets), rows)
 
 
 # ------------------------------------------------------------- attention ----

@@ -183,6 +183,22 @@ def _col_view_ok(t, name):
         raise L.GrkError(f'{name}: row stride must be a multiple of 8 and the view 16-byte aligned')
 
 
+def table_adamw_dense(param, exp_avg, exp_avg_sq, hp, grad):
+    """AdamW of every row of `param` (a [rows, D] table or row range of one) from a dense
+    gradient (fp32 or bf16, [rows, >= D] row-major) -- grk_table_adamw_dense."""
+    _require_cuda(param, exp_avg, exp_avg_sq, grad)
+    rows, D = param.shape
+    for t, n in ((param, 'param'), (exp_avg, 'exp_avg'), (exp_avg_sq, 'exp_avg_sq')):
+        if t.shape != (rows, D) or not t.is_contiguous():
+            raise L.GrkError(f'{n} must be a contiguous [{rows}, {D}] tensor')
+    if grad.dim() != 2 or grad.shape[0] != rows or grad.shape[1] < D or grad.stride(1) != 1:
+        raise L.GrkError(f'grad must be a row-major [{rows}, >= {D}] tensor')
+    rc = L.lib().grk_table_adamw_dense(param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(),
+                                       exp_avg_sq.data_ptr(), rows, D, grad.data_ptr(), L.dtype_code(grad.dtype),
+                                       grad.stride(0), hp, L.stream_ptr(param.device))
+    L.check(rc, 'grk_table_adamw_dense')
+
+
 def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, inv_n=1.0, dropout_p=0.0, seed=0,
               precise=False, out_dtype=torch.bfloat16, act=None, seq_range=None):
     """Build grk_attn_args for bf16 [B*T, ld] column views q/k/v (head h at cols h*hd).

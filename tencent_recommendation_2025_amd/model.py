@@ -24,6 +24,7 @@ are tensorised on the host, as ``feat2tensor`` does) or dicts of tensors
 """
 from __future__ import annotations
 
+import contextlib
 from pathlib import Path
 
 import numpy as np
@@ -209,6 +210,9 @@ class BaselineModel(torch.nn.Module):
         for k in self.ITEM_EMB_FEAT:
             self.emb_transform[k] = torch.nn.Linear(self.ITEM_EMB_FEAT[k], d)
         self._table_refs = None  # set by FusedAdamW (table groups)
+        self._fwd_id = None      # projections of the small tables are shared within one forward
+        self._proj_cache = {}
+        self._proj_off_cache = {}
         self._remaps = None      # set by ShardedFusedAdamW.prepare (rows fetched from other ranks)
 
     def _init_feat_info(self, feat_statistics, feat_types):
@@ -252,6 +256,92 @@ class BaselineModel(torch.nn.Module):
         return res
 
     # -------------------------------------------------- model/BaseLine/model.py:226-310
+    # feat2emb computes relu(itemdnn(cat(item_emb, sparse/array feature embs,
+    # emb_transform(mm)))) (+ relu(userdnn(cat(user_emb, user feature embs)))).
+    # Restated exactly (up to fp32 summation order) as
+    #     [item_emb rows | mm | 1] @ [W_0 | W_mm Wt | b']^T  +  sum_f P_f[idx_f]
+    # with P_f = E_f @ W_f^T the feature table projected through its itemdnn
+    # block: the small feature tables are projected once per forward (~25
+    # GFLOP at d=512) and their lookups become ONE bag-sum gather of projected
+    # rows, so the dnn GEMMs run with K = d + 40 instead of 16d / 9d.  The
+    # projections are plain torch ops, so autograd produces dE_f and dW_f.
+    def _projection(self, which):
+        """(P [rows, d], {feature: P row of its table's row 0}) for the item or user dnn.
+
+        P[0] (the first table's padding row, zero) is the shared padding row:
+        every feature's index 0 is mapped there (_proj_index), so padding
+        occurrences are skipped by the gradient reduction (padding_idx 0) as
+        nn.Embedding(padding_idx=0) does."""
+        key = (which, self._fwd_id)
+        if self._fwd_id is not None and key in self._proj_cache:
+            return self._proj_cache[key]
+        d = self.hidden_units
+        if which == 'item':
+            feats, dnn = list(self.ITEM_SPARSE_FEAT) + list(self.ITEM_ARRAY_FEAT), self.itemdnn
+        else:
+            feats, dnn = list(self.USER_SPARSE_FEAT) + list(self.USER_ARRAY_FEAT), self.userdnn
+        Wv = dnn.weight.view(d, -1, d)  # [d_out, block, d_in]
+        by_rows = {}
+        for j, k in enumerate(feats):  # block 0 is item_emb / user_emb
+            by_rows.setdefault(self.sparse_emb[k].num_embeddings, []).append((k, j + 1))
+        parts, offs, row = [], {}, 0
+        for rows, group in by_rows.items():
+            refs = {k: self._ref(f'sparse_emb.{k}') for k, _ in group}
+            grp = next(iter(refs.values())).group
+            if grp is not None and all(r.group is grp for r in refs.values()):
+                group = sorted(group, key=lambda kj: refs[kj[0]].row_offset)
+                E = G.group_stack(grp, [refs[k].row_offset for k, _ in group], rows)
+            else:
+                E = torch.stack([refs[k].weight for k, _ in group])
+            # one indexing op for all blocks: its backward is one scatter into the weight gradient
+            js = self._const_index(tuple(j for _, j in group), Wv.device) if len(group) > 1 else group[0][1]
+            Wb = (Wv[:, js, :].permute(1, 0, 2) if len(group) > 1 else Wv[:, js, :][None]).to(E.dtype)
+            parts.append(torch.bmm(E, Wb.transpose(1, 2)).to(E.dtype).reshape(-1, d))
+            for k, _ in group:
+                offs[k] = row
+                row += rows
+        res = (torch.cat(parts) if len(parts) > 1 else parts[0]), offs
+        if self._fwd_id is not None:
+            self._proj_cache[key] = res
+        return res
+
+    def _const_index(self, values, device):
+        """Cached device int64 tensor (built once: no host->device copy per forward)."""
+        t = self._proj_off_cache.get(('idx', values))
+        if t is None:
+            t = torch.tensor(values, dtype=torch.int64).to(device)
+            self._proj_off_cache[('idx', values)] = t
+        return t
+
+    def _proj_index(self, feats, names, offs, N):
+        """[N, sum of bags] rows of P: feature value v of table k -> offs[k] + v, 0 -> 0."""
+        x = torch.cat([feats[k].reshape(N, -1) for k in names], 1)
+        key = tuple((offs[k], feats[k].reshape(N, -1).shape[1]) for k in names)
+        off = self._proj_off_cache.get(key)
+        if off is None:
+            off = torch.tensor([o for o, w in key for _ in range(w)], dtype=x.dtype).to(x.device)
+            self._proj_off_cache[key] = off
+        return torch.where(x > 0, x + off, 0)
+
+    def _dnn_weight(self, which, width):
+        """[d, width] = [W_0 | W_mm Wt | b' | 0] matching the operand [rows | mm | 1 | pad]."""
+        d = self.hidden_units
+        dnn = self.itemdnn if which == 'item' else self.userdnn
+        W, cols, bias = dnn.weight, [dnn.weight[:, :d]], dnn.bias[:, None]
+        if which == 'item':
+            base = (1 + len(self.ITEM_SPARSE_FEAT) + len(self.ITEM_ARRAY_FEAT)) * d
+            for j, k in enumerate(self.ITEM_EMB_FEAT):
+                Wk = W[:, base + j * d:base + (j + 1) * d]
+                et = self.emb_transform[k]
+                # one matrix-matrix product for [Wk Wt | Wk bt] (a matrix-vector product
+                # for Wk bt costs milliseconds of host time in its backward on ROCm)
+                Mk = Wk @ torch.cat([et.weight, et.bias[:, None]], 1)
+                cols.append(Mk[:, :-1])
+                bias = bias + Mk[:, -1:]
+        cols.append(bias)
+        Wc = torch.cat(cols, 1)
+        return F.pad(Wc, (0, width - Wc.shape[1]))
+
     def _embed(self, seq, feature_array, mask=None, include_user=False, with_pos=False):
         dev = self._device()
         seq = seq.to(dev, non_blocking=True).long()
@@ -262,41 +352,58 @@ class BaselineModel(torch.nn.Module):
         user_f = (list(self.USER_SPARSE_FEAT) + list(self.USER_ARRAY_FEAT)) if include_user else []
         feats = self._feats(feature_array, item_f + user_f + list(self.ITEM_EMB_FEAT), B, T)
         tt = mask.to(dev, non_blocking=True) if mask is not None else None
-        specs = []
+        specs, extras, splits = [], [], []
         col = 0
-        specs.append(G.LookupSpec(self._ref('item_emb'), seq, col, L.IDX_ITEM_MASK if include_user else L.IDX_PLAIN))
-        col += d
-        for k in item_f:
-            t = feats[k]
-            bag = t.shape[2] if k in self.ITEM_ARRAY_FEAT else 1
-            specs.append(G.LookupSpec(self._ref(f'sparse_emb.{k}'), t, col, L.IDX_PLAIN, bag))
+        ones = None
+
+        def operand(ref, mode, dense):
+            """gather block [rows | dense | 1 | pad] feeding one dnn GEMM; returns its split."""
+            nonlocal col, ones
+            start = col
+            specs.append(G.LookupSpec(ref, seq, col, mode))
             col += d
-        extra_col = col
-        extra = None
-        if self.ITEM_EMB_FEAT:
-            extra = torch.cat([self.emb_transform[k](feats[k]) for k in self.ITEM_EMB_FEAT], -1).reshape(N, -1)
-            col += d * len(self.ITEM_EMB_FEAT)
-        item_w = col
+            if ones is None:
+                ones = torch.ones(N, 1, device=dev)
+            x = torch.cat(dense + [ones], 1) if dense else ones
+            pad = (-x.shape[1]) % 8
+            extras.append((col, F.pad(x, (0, pad)) if pad else x))
+            col += x.shape[1] + pad
+            splits.append((start, col))
+            return col - start
+
+        def projected(which, names):
+            nonlocal col
+            P, offs = self._projection(which)
+            idx = self._proj_index(feats, names, offs, N)
+            specs.append(G.LookupSpec(G.TableRef(P), idx, col, L.IDX_PLAIN, idx.shape[1]))
+            splits.append((col, col + d))
+            col += d
+
+        mm = [feats[k].reshape(N, -1).float() for k in self.ITEM_EMB_FEAT]
+        wi = operand(self._ref('item_emb'), L.IDX_ITEM_MASK if include_user else L.IDX_PLAIN, mm)
+        if item_f:
+            projected('item', item_f)
         if include_user:
-            specs.append(G.LookupSpec(self._ref('user_emb'), seq, col, L.IDX_USER_MASK))
-            col += d
-            for k in user_f:
-                t = feats[k]
-                bag = t.shape[2] if k in self.USER_ARRAY_FEAT else 1
-                specs.append(G.LookupSpec(self._ref(f'sparse_emb.{k}'), t, col, L.IDX_PLAIN, bag))
-                col += d
-        user_end = col
+            wu = operand(self._ref('user_emb'), L.IDX_USER_MASK, [])
+            if user_f:
+                projected('user', user_f)
         if with_pos:
             specs.append(G.LookupSpec(self._ref('pos_emb'), seq, col, L.IDX_POSITION))
+            splits.append((col, col + d))
             col += d
         if self._remaps is not None or self._table_refs is not None:
             specs = self._remap_specs(specs)
-        splits = [(0, item_w)] + ([(item_w, user_end)] if include_user else []) + \
-                 ([(user_end, user_end + d)] if with_pos else [])
-        blocks = list(G.feature_lookup(specs, N, col, tt, T, extra, extra_col, splits))
-        x = torch.relu(self.itemdnn(blocks.pop(0)))
+        blocks = list(G.feature_lookup(specs, N, col, tt, T, extras, splits))
+
+        def dnn(which, width, has_proj):
+            a = blocks.pop(0)
+            p = blocks.pop(0) if has_proj else None
+            w = self._dnn_weight(which, width).to(a.dtype)
+            return torch.relu(torch.addmm(p, a, w.t()) if p is not None else a @ w.t())
+
+        x = dnn('item', wi, bool(item_f))
         if include_user:
-            x = x + torch.relu(self.userdnn(blocks.pop(0)))
+            x = x + dnn('user', wu, bool(user_f))
         pos_rows = blocks.pop(0) if with_pos else None
         return x.view(B, T, d), pos_rows
 
@@ -367,14 +474,27 @@ class BaselineModel(torch.nn.Module):
     # -------------------------------------------------- model/BaseLine/model.py:352-384
     def forward(self, user_item, pos_seqs, neg_seqs, mask, next_mask, next_action_type, seq_feature, pos_feature,
                 neg_feature):
-        log_feats = self.log2feats(user_item, mask, seq_feature)
-        pos_embs, neg_embs = self.feat2emb_pair(pos_seqs, pos_feature, neg_seqs, neg_feature)
+        with self._shared_projections():
+            log_feats = self.log2feats(user_item, mask, seq_feature)
+            pos_embs, neg_embs = self.feat2emb_pair(pos_seqs, pos_feature, neg_seqs, neg_feature)
         return G.pair_logits(log_feats, pos_embs, neg_embs, next_mask.to(self._device(), non_blocking=True))
 
     def encode(self, user_item, pos_seqs, neg_seqs, mask, seq_feature, pos_feature, neg_feature):
         """(log_feats, pos_embs, neg_embs) -- the operands of the loss."""
-        return (self.log2feats(user_item, mask, seq_feature),
-                *self.feat2emb_pair(pos_seqs, pos_feature, neg_seqs, neg_feature))
+        with self._shared_projections():
+            return (self.log2feats(user_item, mask, seq_feature),
+                    *self.feat2emb_pair(pos_seqs, pos_feature, neg_seqs, neg_feature))
+
+    @contextlib.contextmanager
+    def _shared_projections(self):
+        """One set of projected feature tables for every feat2emb of this forward."""
+        self._fwd_id = object()
+        self._proj_cache = {}
+        try:
+            yield
+        finally:
+            self._fwd_id = None
+            self._proj_cache = {}
 
     def predict(self, log_seqs, seq_feature, mask):
         return self.log2feats(log_seqs, mask, seq_feature)[:, -1, :]

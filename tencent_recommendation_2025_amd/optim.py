@@ -31,6 +31,9 @@ class TableGroup:
 
     def __init__(self, name, tables, dtype, device):
         self.name = name
+        # equal-sized tables adjacent (stable in the given order): the dnn
+        # projections read each size class as one contiguous [G, rows, D] view
+        tables = sorted(tables, key=lambda kv: kv[1].num_embeddings)
         D = tables[0][1].embedding_dim
         self.dim = D
         self.offsets = {}
@@ -56,6 +59,48 @@ class TableGroup:
         self.pending = []
         self.token_type = None
         self.seq_len = 0
+        self.dense_grads = {}  # row offset -> dense gradient of rows [off, off + len) (tables used in dense ops)
+        self._identity = None
+
+    def collect_dense(self, row_offset, grad):
+        """Dense gradient (any float dtype) for rows [row_offset, row_offset + len(grad))."""
+        prev = self.dense_grads.get(row_offset)
+        if prev is not None and prev.shape == grad.shape:
+            grad = prev.float() + grad
+        elif prev is not None:
+            raise RuntimeError(f'table group {self.name}: overlapping dense gradients at row {row_offset}')
+        self.dense_grads[row_offset] = grad
+
+    def identity(self):
+        if self._identity is None:
+            self._identity = torch.arange(self.rows, dtype=torch.int32, device=self.flat.device)
+        return self._identity
+
+    def dense_gradient(self, padding_idx=0):
+        """fp32 [rows, D]: the row-sparse sources reduced densely plus the dense parts."""
+        if self.pending:
+            dense = K.embedding_backward(self.pending, self.rows, self.dim, padding_idx=padding_idx,
+                                         token_type=self.token_type, seq_len=self.seq_len, dense=True).dense
+        else:
+            dense = torch.zeros(self.rows, self.dim, dtype=torch.float32, device=self.flat.device)
+        for off, g in self.dense_grads.items():
+            dense[off:off + g.shape[0]] += g
+        return dense
+
+    def step_dense_ranges(self, hp):
+        """Dense-parity AdamW when every gradient of the group is dense (no
+        row-sparse sources): each range from its own gradient (bf16 or fp32,
+        no fp32 staging buffer), rows without gradient with g = 0."""
+        pos = 0
+        for off in sorted(self.dense_grads):
+            g = self.dense_grads[off]
+            if off > pos:
+                K.table_adamw(self.flat[pos:off], self.exp_avg[pos:off], self.exp_avg_sq[pos:off], hp)
+            end = off + g.shape[0]
+            K.table_adamw_dense(self.flat[off:end], self.exp_avg[off:end], self.exp_avg_sq[off:end], hp, g)
+            pos = end
+        if pos < self.rows:
+            K.table_adamw(self.flat[pos:], self.exp_avg[pos:], self.exp_avg_sq[pos:], hp)
 
     def collect(self, src, token_type, seq_len):
         self.pending.append(src)
@@ -69,9 +114,12 @@ class TableGroup:
     def clear(self):
         self.pending = []
         self.token_type = None
+        self.dense_grads = {}
 
 
-DEFAULT_GROUPS = (('item', ('item_emb',)), ('user', ('user_emb',)), ('small', None))
+# pos_emb (row-sparse gradients) apart from the feature tables, whose gradients
+# are dense (they feed the dnns through projections: model._projection)
+DEFAULT_GROUPS = (('item', ('item_emb',)), ('user', ('user_emb',)), ('pos', ('pos_emb',)), ('small', None))
 
 
 class FusedAdamW:
@@ -112,7 +160,11 @@ class FusedAdamW:
         self.dense.step()
         hp = K.adamw_hparams(self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, self.t)
         for g in self.groups:
-            if g.pending:
+            if g.dense_grads and not g.pending:  # dense gradients only: per-range updates
+                g.step_dense_ranges(hp)
+            elif g.dense_grads:  # mixed: one dense fp32 gradient
+                K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, None, g.dense_gradient(), None, 0, g.identity())
+            elif g.pending:
                 res = K.embedding_backward(g.pending, g.rows, g.dim, padding_idx=0, token_type=g.token_type,
                                            seq_len=g.seq_len, dense=False, sparse=True, row_slot=g.row_slot)
                 K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, res.ids, res.rows, res.count, res.capacity,

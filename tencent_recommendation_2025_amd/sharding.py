@@ -244,6 +244,8 @@ class ShardedFusedAdamW(FusedAdamW):
             dense = self.dense_reduce_fn(g.pending, g.rows, g.dim, g.token_type, g.seq_len)
         else:
             dense = torch.zeros(g.rows, g.dim, dtype=torch.float32, device=g.flat.device)
+        for off, dg in g.dense_grads.items():
+            dense[off:off + dg.shape[0]] += dg
         all_reduce(dense, self.pg)
         dense.mul_(inv_world)
         K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, None, dense, None, 0, self.small_identity)

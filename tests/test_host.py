@@ -46,7 +46,7 @@ def test_table_groups_keep_state_dict(golden):
     for k in sd0:
         assert torch.equal(sd0[k], sd1[k]), k
     names = [grp.name for grp in opt.groups]
-    assert names == ['item', 'user', 'small']
+    assert names == ['item', 'user', 'pos', 'small']
     small = opt.groups[2]
     # every small table is a view into the group's flat buffer
     for key, off in small.offsets.items():
