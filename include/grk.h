@@ -157,6 +157,23 @@ int grk_table_adamw_dense(void* param, int param_dtype, float* exp_avg, float* e
                           int dim, const void* grad, int grad_dtype, int64_t grad_ld, grk_adamw_hparams hp,
                           void* stream);
 
+/* Deferred dense-parity updates.  A table whose rows carry last[row] (int32:
+ * the step the row was last updated at) may skip the g = 0 updates of rows
+ * outside a step's batch; before a row is read it is brought to step t by
+ * replaying the skipped steps (last[row], t] in registers with those steps'
+ * hyper-parameters hp_ring[s % ring_len] (the caller keeps them there), with
+ * the same per-element arithmetic as grk_table_adamw -- bit-identical to
+ * updating every row every step.  ids != NULL: rows ids[0 .. num_ids)
+ * (duplicates allowed, each replayed once); ids == NULL: every row (flush).
+ * Sets last[row] = t. */
+int grk_table_adamw_catchup(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows,
+                            int dim, int32_t* last, const int64_t* ids, int64_t num_ids,
+                            const grk_adamw_hparams* hp_ring, int32_t ring_len, int32_t t, void* stream);
+
+/* last[uniq_ids[0 .. *uniq_count)] = t: the rows a GRK_ADAM_LAZY update of step t moved. */
+int grk_stamp_rows(int32_t* last, const int64_t* uniq_ids, const int32_t* uniq_count, int64_t max_uniq, int32_t t,
+                   void* stream);
+
 /* ------------------------------------------------------------------------
  * Causal attention (MFMA 32x32x16 bf16)
  *   GRK_ATTN_SOFTMAX: softmax(scale * QK^T + mask) V with dropout -- the
@@ -205,12 +222,13 @@ int grk_attention_fwd(const grk_attn_args* a, void* out, int64_t ldo, float* lse
 
 /* Gradients of grk_attention_fwd for upstream dout (dout_dtype).  Softmax
  * needs the forward out/lse and a delta workspace fp32 [B, H, T]; hstu
- * accumulates drab fp32 [H, nb] (caller zero-fills; NULL = rab is frozen,
- * its gradient is not computed).  dq/dk/dv are written
- * (not accumulated) in out_dtype; deterministic except drab. */
+ * accumulates drab fp32 [H, nb] (NULL = rab is frozen, its gradient is not
+ * computed) through drab_ws, an int64 [H, nb] scratch: the partial sums are
+ * 64-bit fixed point (value * 2^32), so drab is deterministic.  dq/dk/dv are written
+ * (not accumulated) in out_dtype; deterministic. */
 int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
                       int dout_dtype, const float* lse, float* delta_ws, void* dq, int64_t lddq, void* dk,
-                      int64_t lddk, void* dv, int64_t lddv, float* drab, void* stream);
+                      int64_t lddk, void* dv, int64_t lddv, float* drab, int64_t* drab_ws, void* stream);
 
 /* ------------------------------------------------------------------------
  * HSTU output gate (north star; no reference -- oracle/hstu.py)

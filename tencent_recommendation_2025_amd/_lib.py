@@ -75,9 +75,11 @@ SIGNATURES = {
                                     _P, _P, _P, _SZ, _P, _P]),
     'grk_table_adamw': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _P, _I64, _P, GrkAdamwHparams, _I, _P]),
     'grk_table_adamw_dense': (_I, [_P, _I, _P, _P, _I64, _I, _P, _I, _I64, GrkAdamwHparams, _P]),
+    'grk_table_adamw_catchup': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _I64, _P, C.c_int32, C.c_int32, _P]),
+    'grk_stamp_rows': (_I, [_P, _P, _P, _I64, C.c_int32, _P]),
     'grk_attention_fwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _P]),
     'grk_attention_bwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64, _P, _I64,
-                               _P, _P]),
+                               _P, _P, _P]),
     'grk_norm_gate_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _F, C.c_uint64, _P, _I64, _P, _P]),
     'grk_norm_gate_bwd_workspace': (_SZ, [_I64, _I]),
     'grk_norm_gate_bwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _P, _P, _I64, _I, _F, C.c_uint64, _P, _I64, _P,

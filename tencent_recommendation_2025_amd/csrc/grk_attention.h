@@ -24,6 +24,7 @@ struct AttnParams {
   int out_f32;
   int act;  // GRK_ACT_SILU: q/k/v are pre-activations
   const int* seq_range;  // optional [B, 2] (first valid key, contiguous flag)
+  unsigned long long* drab_fix;  // [H, nb] int64 fixed-point drab accumulator (deterministic)
   // forward
   void* out; int64_t ldo; float* lse;
   // backward
@@ -122,6 +123,17 @@ __device__ __forceinline__ void store_rows(void* out, int64_t ld, bool f32, int6
       if (f32) store4<float>((float*)out + off, v);
       else store4<bf16_t>((bf16_t*)out + off, v);
     }
+}
+
+// drab is accumulated as 64-bit fixed point (value * 2^32) with integer
+// atomics, in LDS and across workgroups: integer sums do not depend on the
+// order of the adds (deterministic), and ds_add_u64 costs ~93 cycles per
+// wave-instruction on gfx950 against ~1150 for ds_add_f32
+// (scripts/microbench/lds_ops.hip).  Range +-2^31, resolution 2^-32.
+constexpr double kFixScale = 4294967296.0;
+__device__ __forceinline__ unsigned long long to_fix(float v) {
+  const double d = fmin(fmax((double)v * kFixScale, -9.0e18), 9.0e18);
+  return (unsigned long long)(long long)d;
 }
 
 // Whole-sequence kernels (grk_attention_seq.hip): one workgroup per

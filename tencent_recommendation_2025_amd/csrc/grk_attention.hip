@@ -175,13 +175,13 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
   constexpr int IMG = kChunk * HD * 2;
   constexpr int RAB = KIND == 1 ? kRabMax : 4;
-  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 64 + 2 * RAB * 4 + 16];
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 64 + 3 * RAB * 4 + 16];
   char* Ks = smem;
   char* Vs = smem + IMG;
   uint8_t* kvs = reinterpret_cast<uint8_t*>(smem + 2 * IMG);
   float* rabs = reinterpret_cast<float*>(smem + 2 * IMG + 64);
-  float* bins = rabs + RAB;
-  int* s_start = reinterpret_cast<int*>(smem + 2 * IMG + 64 + 2 * RAB * 4);
+  unsigned long long* bins = reinterpret_cast<unsigned long long*>(rabs + RAB);  // int64 fixed point
+  int* s_start = reinterpret_cast<int*>(smem + 2 * IMG + 64 + 3 * RAB * 4);
 
   const int b = blockIdx.z, h = blockIdx.y, T = p.T;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
   if (KIND == 1)
     for (int j = threadIdx.x; j < p.nb; j += blockDim.x) {
       rabs[j] = p.rab[h * p.nb + j];
-      bins[j] = 0.f;
+      bins[j] = 0ull;
     }
   const int bh = b * p.H + h;
   const int64_t tok = (int64_t)b * T + (qok ? myq : 0);
@@ -251,7 +251,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
           const int bk = min(myq - key, p.nb - 1);
           const float sp = s[i] * p.scale + rabs[ok ? bk : 0];
           ds[i] = ok ? dp[i] * dsilu(sp) * p.inv_n : 0.f;
-          if (ok && ds[i] != 0.f && p.drab) atomicAdd(&bins[bk], ds[i]);
+          if (ok && ds[i] != 0.f && p.drab) atomicAdd(&bins[bk], to_fix(ds[i]));
         }
       }
 #pragma unroll
@@ -272,7 +272,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
   if (KIND == 1 && p.drab) {
     __syncthreads();
     for (int j = threadIdx.x; j < p.nb; j += blockDim.x)
-      if (bins[j] != 0.f) atomicAdd(&p.drab[h * p.nb + j], bins[j]);
+      if (bins[j] != 0ull) atomicAdd(&p.drab_fix[h * p.nb + j], bins[j]);
   }
 }
 
@@ -410,6 +410,12 @@ static int launch_hd(const AttnParams& p, int which, hipStream_t s) {
   return GRK_OK;
 }
 
+// drab[i] += fixed-point accumulator (after the dQ kernels)
+__global__ void k_drab_finalize(float* __restrict__ drab, const unsigned long long* __restrict__ fix, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) drab[i] += (float)((double)(long long)fix[i] * (1.0 / kFixScale));
+}
+
 static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
   if (which != 1 && attn_seq_launch(p, hd, which, s)) {
     GRK_LAUNCH_CHECK();
@@ -473,7 +479,7 @@ extern "C" int grk_attention_fwd(const grk_attn_args* a, void* out, int64_t ldo,
 extern "C" int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout,
                                  int64_t lddo, int dout_dtype, const float* lse, float* delta_ws, void* dq,
                                  int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv, float* drab,
-                                 void* stream) {
+                                 int64_t* drab_ws, void* stream) {
   clear_error();
   AttnParams p;
   int rc = fill_params(a, &p);
@@ -488,8 +494,12 @@ extern "C" int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_
   p.dout = dout; p.lddo = lddo; p.dout_f32 = dout_dtype == GRK_F32;
   p.lse = const_cast<float*>(lse); p.delta = delta_ws;
   p.dq = dq; p.lddq = lddq; p.dk = dk; p.lddk = lddk; p.dv = dv; p.lddv = lddv;
-  p.drab = drab;
+  GRK_CHECK_ARG(!drab || drab_ws, "drab needs drab_ws (int64 [H, nb] scratch)");
+  p.drab = a->kind == GRK_ATTN_HSTU ? drab : nullptr;
+  p.drab_fix = reinterpret_cast<unsigned long long*>(drab_ws);
   hipStream_t s = (hipStream_t)stream;
+  const int nfix = a->heads * a->num_buckets;
+  if (p.drab) GRK_CHECK_HIP(hipMemsetAsync(drab_ws, 0, (size_t)nfix * 8, s));
   if (a->kind == GRK_ATTN_SOFTMAX) {
     // out dtype of the forward output equals out_dtype of these args
     rc = launch(p, a->head_dim, 1, s);
@@ -497,5 +507,9 @@ extern "C" int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_
   }
   rc = launch(p, a->head_dim, 2, s);
   if (rc) return rc;
+  if (p.drab) {
+    k_drab_finalize<<<(nfix + 255) / 256, 256, 0, s>>>(p.drab, p.drab_fix, nfix);
+    GRK_LAUNCH_CHECK();
+  }
   return launch(p, a->head_dim, 3, s);
 }

@@ -32,18 +32,8 @@ __device__ unsigned long long g_attn_stamps[1 << 16][8];
 #else
 #define GRK_STAMP(k)
 #endif
-constexpr int kRabPad = 32;
-constexpr int kDqBinArrays = 2;  // dQ kernel: drab bins as int64 fixed point (2 float slots each)
-constexpr double kFixScale = 4294967296.0;  // drab fixed point: value * 2^32
-
-// drab partials are accumulated in LDS as 64-bit fixed point with integer
-// atomics: ds_add_u64 costs ~93 cycles per wave-instruction on gfx950 against
-// ~1150 for ds_add_f32 (scripts/microbench/lds_ops.hip), and integer sums do
-// not depend on the order of the adds.  Range +-2^31, resolution 2^-32.
-__device__ __forceinline__ unsigned long long to_fix(float v) {
-  const double d = fmin(fmax((double)v * kFixScale, -9.0e18), 9.0e18);
-  return (unsigned long long)(long long)d;
-}             // rabx[kRabPad + d], d >= -31 inside a sub-tile
+constexpr int kRabPad = 32;             // rabx[kRabPad + d], d >= -31 inside a sub-tile
+constexpr int kDqBinArrays = 2;         // dQ kernel: drab bins as int64 fixed point (2 float slots each)
 constexpr int kSeqLdsMax = 80 * 1024;   // LDS per workgroup: 2 per CU fit gfx950's 160 KiB
 
 struct SeqInfo {
@@ -509,8 +499,8 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
   if (KIND == 1 && p.drab) {
     __syncthreads();
     for (int d = threadIdx.x; d < Tp; d += blockDim.x) {
-      const long long q = (long long)bins[kRabPad + d];
-      if (q != 0) atomicAdd(&p.drab[h * p.nb + min(d, p.nb - 1)], (float)((double)q * (1.0 / kFixScale)));
+      const unsigned long long q = bins[kRabPad + d];
+      if (q != 0) atomicAdd(&p.drab_fix[h * p.nb + min(d, p.nb - 1)], q);
     }
   }
 }

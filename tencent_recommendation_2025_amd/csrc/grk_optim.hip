@@ -13,6 +13,20 @@
 
 namespace grk {
 
+// One element of the torch single-tensor AdamW step.  Every update path (dense,
+// lazy, dense-gradient, catch-up replay) goes through this function, so a
+// replayed g = 0 step is bit-identical to the step the dense pass would run.
+__device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, const grk_adamw_hparams& hp) {
+  const float decay = 1.0f - hp.lr * hp.weight_decay;
+  const float w1 = 1.0f - hp.beta1, w2 = 1.0f - hp.beta2;
+  float pe = p * decay;
+  const float me = m + w1 * (g - m);
+  const float ve = v * hp.beta2 + w2 * g * g;
+  const float denom = sqrtf(ve) / hp.bias_corr2_sqrt + hp.eps;
+  pe = pe - hp.step_size * (me / denom);
+  p = pe; m = me; v = ve;
+}
+
 // AdamW on NV consecutive elements (NV = 4 or 8): param via one 8/16-byte
 // access (bf16) or NV/4 float4s, moments via NV/4 float4s each.
 template <typename P, int NV>
@@ -45,17 +59,8 @@ __device__ __forceinline__ void adam_vec(P* p, float* m, float* v, const float* 
     mv[4 * k] = a.x; mv[4 * k + 1] = a.y; mv[4 * k + 2] = a.z; mv[4 * k + 3] = a.w;
     vv[4 * k] = b.x; vv[4 * k + 1] = b.y; vv[4 * k + 2] = b.z; vv[4 * k + 3] = b.w;
   }
-  const float decay = 1.0f - hp.lr * hp.weight_decay;
-  const float w1 = 1.0f - hp.beta1, w2 = 1.0f - hp.beta2;
 #pragma unroll
-  for (int e = 0; e < NV; ++e) {
-    float pe = pv[e] * decay;
-    float me = mv[e] + w1 * (g[e] - mv[e]);
-    float ve = vv[e] * hp.beta2 + w2 * g[e] * g[e];
-    float denom = sqrtf(ve) / hp.bias_corr2_sqrt + hp.eps;
-    pe = pe - hp.step_size * (me / denom);
-    pv[e] = pe; mv[e] = me; vv[e] = ve;
-  }
+  for (int e = 0; e < NV; ++e) adam1(pv[e], mv[e], vv[e], g[e], hp);
   if constexpr (sizeof(P) == 4) {
 #pragma unroll
     for (int k = 0; k < NV / 4; ++k)
@@ -129,6 +134,64 @@ __global__ void __launch_bounds__(256) k_adamw_dense_grad(P* __restrict__ param,
   }
   const int64_t off = row * dim + c;
   adam_vec<P, NV>(param + off, m + off, v + off, g, hp);
+}
+
+// Catch-up (deferred dense-parity updates): one wave per row; lane 0 claims
+// the row (last[row] <- t) so duplicate ids replay it once; the skipped g = 0
+// steps (last, t] are replayed in registers with each step's hyper-parameters,
+// rounding bf16 parameters after every step exactly as a store/load would.
+template <typename P, int NV>
+__global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, float* __restrict__ m,
+                                                       float* __restrict__ v, int64_t num_rows, int dim,
+                                                       int32_t* __restrict__ last, const int64_t* __restrict__ ids,
+                                                       int64_t num_ids, const grk_adamw_hparams* __restrict__ ring,
+                                                       int ring_len, int t) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= (ids ? num_ids : num_rows)) return;
+  const int64_t row = ids ? ids[w] : w;
+  if (row < 0 || row >= num_rows) return;
+  int from = 0;
+  if (lane == 0) from = atomicExch(&last[row], t);
+  from = __shfl(from, 0);
+  if (from >= t) return;
+  for (int c = lane * NV; c < dim; c += 64 * NV) {
+    float pv[NV], mv[NV], vv[NV];
+    const int64_t off = row * dim + c;
+    if constexpr (sizeof(P) == 4) {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) pv[e] = reinterpret_cast<const float*>(param + off)[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) pv[e] = bf16_to_f32(reinterpret_cast<const bf16_t*>(param + off)[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < NV; ++e) { mv[e] = m[off + e]; vv[e] = v[off + e]; }
+    for (int st = from + 1; st <= t; ++st) {
+      const grk_adamw_hparams hp = ring[st % ring_len];
+#pragma unroll
+      for (int e = 0; e < NV; ++e) {
+        adam1(pv[e], mv[e], vv[e], 0.0f, hp);
+        if constexpr (sizeof(P) == 2) pv[e] = bf16_to_f32(f32_to_bf16(pv[e]));
+      }
+    }
+    if constexpr (sizeof(P) == 4) {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) reinterpret_cast<float*>(param + off)[e] = pv[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) reinterpret_cast<bf16_t*>(param + off)[e] = f32_to_bf16(pv[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < NV; ++e) { m[off + e] = mv[e]; v[off + e] = vv[e]; }
+  }
+}
+
+__global__ void k_stamp_rows(int32_t* __restrict__ last, const int64_t* __restrict__ ids,
+                             const int32_t* __restrict__ count, int64_t max_uniq, int t) {
+  const int64_t n = *count < max_uniq ? *count : max_uniq;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n; u += (int64_t)gridDim.x * blockDim.x)
+    last[ids[u]] = t;
 }
 
 template <typename P, int NV>
@@ -227,6 +290,41 @@ extern "C" int grk_table_adamw_dense(void* param, int param_dtype, float* exp_av
     else { if (v8) GRK_DG(float, float, 8); else GRK_DG(float, float, 4); }
   }
 #undef GRK_DG
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+
+extern "C" int grk_table_adamw_catchup(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
+                                       int64_t num_rows, int dim, int32_t* last, const int64_t* ids, int64_t num_ids,
+                                       const grk_adamw_hparams* hp_ring, int32_t ring_len, int32_t t, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(num_rows >= 0 && num_ids >= 0, "num_rows / num_ids must be >= 0");
+  const int64_t waves = ids ? num_ids : num_rows;
+  if (waves == 0) return GRK_OK;
+  GRK_CHECK_ARG(param && exp_avg && exp_avg_sq && last && hp_ring, "param / moments / last / hp_ring required");
+  GRK_CHECK_ARG(param_dtype == GRK_F32 || param_dtype == GRK_BF16, "bad param dtype");
+  GRK_CHECK_ARG(dim > 0 && dim % 4 == 0, "dim must be a multiple of 4");
+  GRK_CHECK_ARG(ring_len > 0 && t >= 0, "ring_len must be > 0 and t >= 0");
+  GRK_CHECK_ARG((waves + 3) / 4 < (int64_t)1 << 31, "too many rows for one launch");
+  const unsigned g = (unsigned)((waves + 3) / 4);
+  hipStream_t s = (hipStream_t)stream;
+  const bool v8 = dim % 8 == 0;
+#define GRK_CU(P, NV) k_adamw_catchup<P, NV><<<g, 256, 0, s>>>((P*)param, exp_avg, exp_avg_sq, num_rows, dim, last, \
+                                                               ids, num_ids, hp_ring, ring_len, t)
+  if (param_dtype == GRK_BF16) { if (v8) GRK_CU(bf16_t, 8); else GRK_CU(bf16_t, 4); }
+  else { if (v8) GRK_CU(float, 8); else GRK_CU(float, 4); }
+#undef GRK_CU
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+extern "C" int grk_stamp_rows(int32_t* last, const int64_t* uniq_ids, const int32_t* uniq_count, int64_t max_uniq,
+                              int32_t t, void* stream) {
+  clear_error();
+  if (max_uniq <= 0) return GRK_OK;
+  GRK_CHECK_ARG(last && uniq_ids && uniq_count, "last / uniq_ids / uniq_count required");
+  k_stamp_rows<<<grid_for(max_uniq, 256, 1024), 256, 0, (hipStream_t)stream>>>(last, uniq_ids, uniq_count, max_uniq, t);
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }

@@ -199,6 +199,33 @@ def table_adamw_dense(param, exp_avg, exp_avg_sq, hp, grad):
     L.check(rc, 'grk_table_adamw_dense')
 
 
+def table_adamw_catchup(param, exp_avg, exp_avg_sq, last, hp_ring, t, ids=None):
+    """Replay the skipped g = 0 steps (last[row], t] of rows `ids` (all rows if None) --
+    grk_table_adamw_catchup.  hp_ring: uint8/float tensor holding grk_adamw_hparams[ring_len]."""
+    _require_cuda(param, exp_avg, exp_avg_sq, last, hp_ring, ids)
+    rows, D = param.shape
+    if last.dtype != torch.int32 or last.shape != (rows,):
+        raise L.GrkError('last must be an int32 [rows] tensor')
+    ring_len = hp_ring.numel() * hp_ring.element_size() // C.sizeof(L.GrkAdamwHparams)
+    n = 0
+    if ids is not None:
+        if ids.dtype != torch.int64 or not ids.is_contiguous():
+            raise L.GrkError('ids must be a contiguous int64 tensor')
+        n = ids.numel()
+    rc = L.lib().grk_table_adamw_catchup(param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(),
+                                         exp_avg_sq.data_ptr(), rows, D, last.data_ptr(), _ptr(ids), n,
+                                         hp_ring.data_ptr(), ring_len, int(t), L.stream_ptr(param.device))
+    L.check(rc, 'grk_table_adamw_catchup')
+
+
+def stamp_rows(last, ids, count, capacity, t):
+    """last[ids[:count]] = t (grk_stamp_rows)."""
+    _require_cuda(last, ids, count)
+    rc = L.lib().grk_stamp_rows(last.data_ptr(), ids.data_ptr(), count.data_ptr(), int(capacity), int(t),
+                                L.stream_ptr(last.device))
+    L.check(rc, 'grk_stamp_rows')
+
+
 def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, inv_n=1.0, dropout_p=0.0, seed=0,
               precise=False, out_dtype=torch.bfloat16, act=None, seq_range=None):
     """Build grk_attn_args for bf16 [B*T, ld] column views q/k/v (head h at cols h*hd).
@@ -254,15 +281,16 @@ def attention_fwd(args, out, lse=None):
 
 
 def attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab=None):
-    """grk_attention_bwd: writes dq/dk/dv (args.out_dtype) and accumulates drab."""
+    """grk_attention_bwd: writes dq/dk/dv (args.out_dtype) and accumulates drab (deterministic)."""
     _require_cuda(dout, dq, dk, dv, drab)
     for t, n in ((dout, 'dout'), (dq, 'dq'), (dk, 'dk'), (dv, 'dv')):
         if t.stride(1) != 1 or t.stride(0) % 8:
             raise L.GrkError(f'{n} must be row-major with a row stride multiple of 8')
+    ws = None if drab is None else torch.empty(drab.numel(), dtype=torch.int64, device=drab.device)
     rc = L.lib().grk_attention_bwd(C.byref(args), _ptr(out), 0 if out is None else out.stride(0), dout.data_ptr(),
                                    dout.stride(0), L.dtype_code(dout.dtype), _ptr(lse), _ptr(delta), dq.data_ptr(),
                                    dq.stride(0), dk.data_ptr(), dk.stride(0), dv.data_ptr(), dv.stride(0), _ptr(drab),
-                                   L.stream_ptr(dout.device))
+                                   _ptr(ws), L.stream_ptr(dout.device))
     L.check(rc, 'grk_attention_bwd')
 
 

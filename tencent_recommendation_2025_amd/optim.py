@@ -22,6 +22,9 @@ from __future__ import annotations
 
 import torch
 
+import ctypes as C
+
+from . import _lib as L
 from . import functional as G
 from . import kernels as K
 
@@ -126,7 +129,7 @@ class FusedAdamW:
     """AdamW over a BaselineModel: table groups on grk kernels, dense params on torch fused AdamW."""
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
-                 table_dtype=torch.bfloat16, groups=DEFAULT_GROUPS):
+                 table_dtype=torch.bfloat16, groups=DEFAULT_GROUPS, defer_period=16):
         if table_mode not in ('dense', 'lazy'):
             raise ValueError("table_mode must be 'dense' or 'lazy'")
         self.model = model
@@ -148,6 +151,71 @@ class FusedAdamW:
         self.dense = torch.optim.AdamW(dense, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                                        fused=dev.type == 'cuda')
         self.t = 0
+        # Deferred dense parity for the big item/user tables: a row outside the
+        # step's batch takes a g = 0 update that depends on nothing but (p, m, v)
+        # and the step's hyper-parameters, so it is replayed in registers when
+        # the row is next read (begin_step: the batch rows), at every
+        # `defer_period`-th step for all rows, and before state_dict (flush) --
+        # bit-identical to moving every row every step, without streaming the
+        # whole table through HBM each step.  Needs Trainer.step (begin_step).
+        self.defer = int(defer_period) if (defer_period and not self.lazy and dev.type == 'cuda') else 0
+        self._deferred = {g.name: g for g in self.groups if g.name in ('item', 'user')} if self.defer else {}
+        self._seg = None     # step every deferred row was last brought up to (segment start)
+        self._begun = None   # step for which begin_step caught the batch rows up
+        for g in self._deferred.values():
+            g.last = torch.zeros(g.rows, dtype=torch.int32, device=dev)
+        if self.defer:
+            nf = C.sizeof(L.GrkAdamwHparams) // 4
+            self._ring = torch.zeros(self.defer, nf, dtype=torch.float32, device=dev)
+            self._pinned = [torch.zeros(self.defer, nf, dtype=torch.float32).pin_memory() for _ in range(2)]
+            self._uploads = 0
+            model.register_state_dict_pre_hook(lambda *args, **kw: self.flush())
+
+    def _hp(self, step):
+        return K.adamw_hparams(self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, step)
+
+    def _upload_ring(self, t):
+        """Hyper-parameters of steps t+1 .. t+defer into the device ring (slot s % defer)."""
+        buf = self._pinned[self._uploads % 2]  # alternate: the previous copy may still be in flight
+        self._uploads += 1
+        for step in range(t + 1, t + self.defer + 1):
+            hp = self._hp(step)
+            buf[step % self.defer] = torch.tensor([getattr(hp, f) for f, _ in hp._fields_], dtype=torch.float32)
+        self._ring.copy_(buf, non_blocking=True)
+
+    def _segment(self, t):
+        """Start a new defer segment at step t: bring every row to t, refill the ring."""
+        if self._seg is not None and self._seg < t:
+            for g in self._deferred.values():
+                K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self._ring, t)
+        self._upload_ring(t)
+        self._seg = t
+
+    @torch.no_grad()
+    def begin_step(self, batch):
+        """Bring the rows the coming step reads up to date (deferred tables).
+
+        batch = (seq, pos, neg, token_type, ...) as Trainer.step gets it: the
+        item table's rows are seq (item tokens), pos and neg; the user table's
+        are seq (user tokens)."""
+        if not self._deferred:
+            return
+        t = self.t
+        if self._seg is None or t - self._seg >= self.defer:
+            self._segment(t)
+        seq, pos, neg, tt = (x.long() for x in batch[:4])
+        ids = {'item': torch.cat([(seq * (tt == 1)).reshape(-1), pos.reshape(-1), neg.reshape(-1)]),
+               'user': (seq * (tt == 2)).reshape(-1)}
+        for name, g in self._deferred.items():
+            K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self._ring, t, ids[name])
+        self._begun = t
+
+    @torch.no_grad()
+    def flush(self):
+        """Bring every row of the deferred tables to the current step (before reading them)."""
+        if self._deferred and self._seg is not None:
+            for g in self._deferred.values():
+                K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self._ring, self.t)
 
     def zero_grad(self, set_to_none=True):
         self.dense.zero_grad(set_to_none=set_to_none)
@@ -156,10 +224,26 @@ class FusedAdamW:
 
     @torch.no_grad()
     def step(self):
+        if self._deferred and self._begun != self.t:  # no begin_step: every row to step t, then dense
+            if self._seg is None or self.t - self._seg >= self.defer:
+                self._segment(self.t)
+            self.flush()
+        begun, self._begun = self._begun == self.t, None
         self.t += 1
         self.dense.step()
         hp = K.adamw_hparams(self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, self.t)
         for g in self.groups:
+            if g.name in self._deferred:
+                if begun:  # rows outside the batch stay deferred; the batch rows move now
+                    if g.pending:
+                        res = K.embedding_backward(g.pending, g.rows, g.dim, padding_idx=0, token_type=g.token_type,
+                                                   seq_len=g.seq_len, dense=False, sparse=True, row_slot=g.row_slot)
+                        K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, res.ids, res.rows, res.count,
+                                      res.capacity, g.row_slot, lazy=True)
+                        K.stamp_rows(g.last, res.ids, res.count, res.capacity, self.t)
+                    g.clear()
+                    continue
+                g.last.fill_(self.t)  # dense update below moves every row
             if g.dense_grads and not g.pending:  # dense gradients only: per-range updates
                 g.step_dense_ranges(hp)
             elif g.dense_grads:  # mixed: one dense fp32 gradient

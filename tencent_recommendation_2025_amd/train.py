@@ -39,6 +39,8 @@ class Trainer:
         self.opt.zero_grad()
         if hasattr(self.opt, 'prepare'):  # row-sharded tables: fetch this batch's rows from their owners
             self.opt.prepare(batch)
+        if hasattr(self.opt, 'begin_step'):  # deferred table updates: bring this batch's rows up to date
+            self.opt.begin_step(batch)
         loss = self.compute_loss(batch)
         loss.backward()
         self.opt.step()

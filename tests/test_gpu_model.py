@@ -202,3 +202,34 @@ def test_fused_trainer_bf16_hstu_learns():
     losses = [tr.step(batch).item() for _ in range(6)]
     assert all(np.isfinite(losses))
     assert losses[-1] < losses[0] - 0.05, losses
+
+
+@pytest.mark.parametrize('period', [1, 3])
+def test_deferred_table_updates_are_bit_identical_to_dense(period):
+    """FusedAdamW(defer_period=k): rows outside the batch replayed when next
+    read / every k steps / before state_dict == moving every row every step,
+    bit for bit (tables and moments), across several segment boundaries."""
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    cfg = S.SyntheticConfig(batch_size=8, maxlen=30, num_items=5000, num_users=700, min_len=4)
+    stats, types = S.feature_schema(cfg)
+    args = S.make_args(hidden_units=64, maxlen=30, num_blocks=1, num_heads=2)
+    runs = []
+    for defer in (0, period):
+        torch.manual_seed(0)
+        m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, args).to(DEV)
+        opt = FusedAdamW(m, lr=2e-3, defer_period=defer)
+        tr = Trainer(m, opt, loss='bce')
+        g = torch.Generator(device=DEV).manual_seed(0)
+        for _ in range(7):
+            tr.step(S.make_batch(cfg, g, DEV))
+        sd = m.state_dict()  # flushes deferred rows first
+        torch.cuda.synchronize()
+        runs.append((sd, {grp.name: (grp.exp_avg.clone(), grp.exp_avg_sq.clone()) for grp in opt.groups}))
+    for k in runs[0][0]:
+        assert torch.equal(runs[0][0][k], runs[1][0][k]), k
+    for name in runs[0][1]:
+        for a, b in zip(runs[0][1][name], runs[1][1][name]):
+            assert torch.equal(a, b), name
