@@ -337,6 +337,190 @@ __global__ void __launch_bounds__(256) k_seg_combine(const unsigned long long* _
   store_final<G>(acc, seg_key[u], u, dim, c, dense_out, uniq_rows, row_slot);
 }
 
+// ------------------------------------ segmented reduction, one wave per row ----
+// dim == 64 * VEC (bf16 d=512, fp32 d=256: one 16-byte vector per lane covers
+// a row).  Same chunking and summation order as k_seg_chunks /
+// k_seg_combine, restructured for memory-level parallelism: the chunk's keys,
+// scan positions and gradient-row addresses are loaded into lanes up front and
+// broadcast with readlane, so row loads take scalar base addresses with
+// kWavePipe rows in flight instead of a key -> address -> row chain per
+// step; whether a piece is a whole segment follows from the neighbouring keys
+// (keys[p0-1], keys[p1]), so seg_start / seg_end are read only for the (at
+// most two) pieces that cross the chunk's edges.
+constexpr int kWavePipe = 16;
+
+// (readlane returns int: both halves go through unsigned, or the low word
+// would sign-extend into the high one)
+__device__ __forceinline__ unsigned long long readlane64(unsigned lo, unsigned hi, int l) {
+  return ((unsigned long long)(unsigned)__builtin_amdgcn_readlane(hi, l) << 32) |
+         (unsigned long long)(unsigned)__builtin_amdgcn_readlane(lo, l);
+}
+
+// 16-byte row-vector load through a global-address-space pointer (a flat
+// load would also count against lgkmcnt and serialise with scalar loads).
+template <typename G>
+__device__ __forceinline__ void load_row_global(Vec16<G>& r, unsigned long long ptr, int c) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+  const u32x4 t = *reinterpret_cast<gu32x4*>(ptr + (unsigned long long)c * sizeof(G));
+  if constexpr (sizeof(G) == 2) r.v = make_uint4(t.x, t.y, t.z, t.w);
+  else r.v = make_float4(__uint_as_float(t.x), __uint_as_float(t.y), __uint_as_float(t.z), __uint_as_float(t.w));
+}
+
+template <typename G>
+__global__ void __launch_bounds__(256) k_seg_chunks_wave(const unsigned* __restrict__ keys,
+                                                         const unsigned long long* __restrict__ gptr,
+                                                         const int* __restrict__ pos, const int* __restrict__ seg_start,
+                                                         const int* __restrict__ seg_end, int64_t n, unsigned sentinel,
+                                                         int dim, float* __restrict__ slotA, float* __restrict__ slotB,
+                                                         float* __restrict__ dense_out, float* __restrict__ uniq_rows,
+                                                         int32_t* __restrict__ row_slot) {
+  constexpr int VEC = RowVec<G>::VEC;
+  constexpr int KP = kRedChunk / 64;  // chunk entries per lane
+  const int lane = threadIdx.x & 63;
+  const int64_t chunk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t p0 = chunk * kRedChunk;
+  if (p0 >= n) return;
+  const int64_t p1 = min(n, p0 + kRedChunk);
+  const int c = lane * VEC;
+  unsigned kr[KP], glo[KP], ghi[KP];
+  int pr[KP];
+  const unsigned long long g0 = gptr[p0];  // stands in past p1: every row load stays valid and unconditional
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    const int64_t i = p0 + k * 64 + lane;
+    kr[k] = i < p1 ? keys[i] : sentinel;
+    pr[k] = i < p1 ? pos[i] : 0;
+    const unsigned long long g = i < p1 ? gptr[i] : g0;
+    glo[k] = (unsigned)g;
+    ghi[k] = (unsigned)(g >> 32);
+  }
+  unsigned cur = __builtin_amdgcn_readfirstlane(kr[0]);
+  if (cur == sentinel) return;
+  const unsigned kprev = p0 > 0 ? keys[p0 - 1] : sentinel;
+  const unsigned knext = p1 < n ? keys[p1] : sentinel;
+  RowVec<G> acc;
+  acc.zero();
+  int64_t ps = p0, pe = p0;          // current piece [ps, pe) of key cur
+  int u = __builtin_amdgcn_readfirstlane(pr[0]) - 1;
+  auto flush = [&]() {
+    const bool whole = (ps > p0 || kprev != cur) && (pe < p1 || knext != cur);
+    if (whole) {
+      store_final<G>(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
+    } else if (seg_end[u] - seg_start[u] > 2 * kRedChunk) {
+      store_slot<G>(acc, (ps == p0 ? slotA : slotB) + chunk * dim, dim, c);
+    }  // else: short row crossing an edge -- k_seg_combine_edges sums it sequentially
+  };
+  bool done = false;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    for (int s0 = 0; s0 < 64 && !done; s0 += kWavePipe) {
+      Vec16<G> r[kWavePipe];
+      unsigned kk[kWavePipe];
+#pragma unroll
+      for (int j = 0; j < kWavePipe; ++j) {
+        kk[j] = (unsigned)__builtin_amdgcn_readlane(kr[k], s0 + j);
+        load_row_global<G>(r[j], readlane64(glo[k], ghi[k], s0 + j), c);
+      }
+#pragma unroll
+      for (int j = 0; j < kWavePipe; ++j) {
+        if (done) break;
+        if (kk[j] == sentinel) {  // sorted: the rest of the chunk is padding / past the end
+          done = true;
+          break;
+        }
+        if (kk[j] != cur) {
+          flush();
+          acc.zero();
+          cur = kk[j];
+          ps = p0 + k * 64 + s0 + j;
+          u = __builtin_amdgcn_readlane(pr[k], s0 + j) - 1;  // int: scan positions fit
+        }
+#pragma unroll
+        for (int x = 0; x < VEC; ++x) acc.v[x] += r[j].get(x);
+        pe = p0 + k * 64 + s0 + j + 1;
+      }
+    }
+  }
+  flush();
+}
+
+// seq_sum for one wave: the row addresses of 64 occurrences at a time are
+// loaded into lanes and broadcast, kWavePipe rows in flight, in-order adds.
+template <typename G>
+__device__ __forceinline__ void seq_sum_wave(RowVec<G>& acc, const unsigned long long* __restrict__ gptr, int s, int e,
+                                             int lane, int c) {
+  constexpr int VEC = RowVec<G>::VEC;
+  for (int b = s; b < e; b += 64) {
+    const unsigned long long g = gptr[b + lane < e ? b + lane : s];
+    const unsigned lo = (unsigned)g, hi = (unsigned)(g >> 32);
+    const int m = min(64, e - b);
+    for (int s0 = 0; s0 < m; s0 += kWavePipe) {
+      Vec16<G> r[kWavePipe];
+#pragma unroll
+      for (int j = 0; j < kWavePipe; ++j) load_row_global<G>(r[j], readlane64(lo, hi, s0 + j), c);
+#pragma unroll
+      for (int j = 0; j < kWavePipe; ++j)
+        if (s0 + j < m)
+#pragma unroll
+          for (int x = 0; x < VEC; ++x) acc.v[x] += r[j].get(x);
+    }
+  }
+}
+
+// One wave per chunk edge b (occurrence b * kRedChunk): finishes the row that
+// first crosses a chunk edge at b, i.e. crosses b and starts in chunk b - 1.
+template <typename G>
+__global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __restrict__ keys,
+                                                           const unsigned long long* __restrict__ gptr,
+                                                           const int* __restrict__ pos,
+                                                           const int* __restrict__ seg_start,
+                                                           const int* __restrict__ seg_end, int64_t n,
+                                                           unsigned sentinel, int dim, const float* __restrict__ slotA,
+                                                           const float* __restrict__ slotB,
+                                                           float* __restrict__ dense_out, float* __restrict__ uniq_rows,
+                                                           int32_t* __restrict__ row_slot) {
+  constexpr int VEC = RowVec<G>::VEC;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) + 1;
+  const int64_t pb = b * kRedChunk;
+  if (pb >= n) return;
+  const unsigned key = keys[pb];
+  if (key == sentinel || keys[pb - 1] != key) return;
+  const int u = pos[pb] - 1;
+  const int su = seg_start[u], eu = seg_end[u];
+  if (su / kRedChunk != b - 1) return;  // also crosses an earlier edge: finished there
+  const int c = lane * VEC;
+  const int cs = (int)(b - 1), ce = (eu - 1) / kRedChunk;
+  RowVec<G> acc;
+  acc.zero();
+  if (eu - su <= 2 * kRedChunk) {
+    seq_sum_wave<G>(acc, gptr, su, eu, lane, c);
+  } else {
+    const float* first = ((su % kRedChunk) == 0 ? slotA : slotB) + (int64_t)cs * dim + c;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc.v[e] = first[e];
+    for (int ch = cs + 1; ch <= ce; ch += kRedPipe) {
+      float4 r[kRedPipe][VEC / 4];
+#pragma unroll
+      for (int j = 0; j < kRedPipe; ++j)
+        if (ch + j <= ce)
+#pragma unroll
+          for (int e = 0; e < VEC / 4; ++e)
+            r[j][e] = *reinterpret_cast<const float4*>(slotA + (int64_t)(ch + j) * dim + c + 4 * e);
+#pragma unroll
+      for (int j = 0; j < kRedPipe; ++j)
+        if (ch + j <= ce)
+#pragma unroll
+          for (int e = 0; e < VEC / 4; ++e) {
+            acc.v[4 * e] += r[j][e].x; acc.v[4 * e + 1] += r[j][e].y;
+            acc.v[4 * e + 2] += r[j][e].z; acc.v[4 * e + 3] += r[j][e].w;
+          }
+    }
+  }
+  store_final<G>(acc, key, u, dim, c, dense_out, uniq_rows, row_slot);
+}
+
 // ------------------------------------------------------------ workspace ----
 struct BwdWs {
   unsigned *keys_in, *keys_out, *seg_key;
@@ -538,6 +722,21 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   const int groups = tpr >= 256 ? 1 : 256 / tpr;
   const int block = tpr >= 256 ? tpr : groups * tpr;
   const int64_t chunks = (total + kRedChunk - 1) / kRedChunk;
+  if (tpr == 64) {  // one wave per row
+    const unsigned gw = (unsigned)((chunks + 3) / 4);
+    const unsigned ge = (unsigned)(chunks > 1 ? (chunks - 1 + 3) / 4 : 0);
+#define GRK_SEGW(G)                                                                                                  \
+  k_seg_chunks_wave<G><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,         \
+                                          sentinel, dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot);        \
+  GRK_LAUNCH_CHECK();                                                                                                \
+  if (ge)                                                                                                            \
+    k_seg_combine_edges<G><<<ge, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,     \
+                                              sentinel, dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot)
+    if (grad_dtype == GRK_BF16) { GRK_SEGW(bf16_t); } else { GRK_SEGW(float); }
+#undef GRK_SEGW
+    GRK_LAUNCH_CHECK();
+    return GRK_OK;
+  }
   const unsigned gc = (unsigned)((chunks + groups - 1) / groups);
   const unsigned gu = (unsigned)((total + groups - 1) / groups);
   if (grad_dtype == GRK_BF16) {

@@ -13,25 +13,47 @@
 
 namespace grk {
 
+// Per-step constants of the update (uniform across a launch or a replayed
+// step): 1/sqrt(1-b2^t) is taken once here so the element update has no
+// IEEE division.
+struct AdamStep {
+  float decay, w1, beta2, w2, inv_bc2, eps, step_size;
+};
+__device__ __forceinline__ AdamStep adam_step(const grk_adamw_hparams& hp) {
+  AdamStep s;
+  s.decay = 1.0f - hp.lr * hp.weight_decay;
+  s.w1 = 1.0f - hp.beta1;
+  s.beta2 = hp.beta2;
+  s.w2 = 1.0f - hp.beta2;
+  s.inv_bc2 = 1.0f / hp.bias_corr2_sqrt;
+  s.eps = hp.eps;
+  s.step_size = hp.step_size;
+  return s;
+}
+
 // One element of the torch single-tensor AdamW step.  Every update path (dense,
 // lazy, dense-gradient, catch-up replay) goes through this function, so a
 // replayed g = 0 step is bit-identical to the step the dense pass would run.
-__device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, const grk_adamw_hparams& hp) {
-  const float decay = 1.0f - hp.lr * hp.weight_decay;
-  const float w1 = 1.0f - hp.beta1, w2 = 1.0f - hp.beta2;
-  float pe = p * decay;
-  const float me = m + w1 * (g - m);
-  const float ve = v * hp.beta2 + w2 * g * g;
-  const float denom = sqrtf(ve) / hp.bias_corr2_sqrt + hp.eps;
-  pe = pe - hp.step_size * (me / denom);
-  p = pe; m = me; v = ve;
+// sqrt and the reciprocal are the hardware v_sqrt_f32 / v_rcp_f32 (1 ulp
+// each): the correctly rounded library forms cost ~30 VALU ops per element
+// (scaling, refinement FMAs, denorm-mode switches), which made replayed steps
+// VALU-bound; the difference from torch's rounding is a few ulp of the
+// ~lr-sized update term, far inside the parity tolerances (tests/).
+__device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, const AdamStep& s) {
+  const float pe = p * s.decay;
+  const float me = m + s.w1 * (g - m);
+  const float ve = v * s.beta2 + s.w2 * g * g;
+  const float denom = __builtin_amdgcn_sqrtf(ve) * s.inv_bc2 + s.eps;
+  p = pe - s.step_size * (me * __builtin_amdgcn_rcpf(denom));
+  m = me;
+  v = ve;
 }
 
-// AdamW on NV consecutive elements (NV = 4 or 8): param via one 8/16-byte
-// access (bf16) or NV/4 float4s, moments via NV/4 float4s each.
+// NV consecutive elements (NV = 4 or 8) of param / exp_avg / exp_avg_sq in
+// registers: param via one 8/16-byte access (bf16) or NV/4 float4s, moments
+// via NV/4 float4s each.
 template <typename P, int NV>
-__device__ __forceinline__ void adam_vec(P* p, float* m, float* v, const float* g, const grk_adamw_hparams& hp) {
-  float pv[NV], mv[NV], vv[NV];
+__device__ __forceinline__ void load_pmv(const P* p, const float* m, const float* v, float* pv, float* mv, float* vv) {
   if constexpr (sizeof(P) == 4) {
 #pragma unroll
     for (int k = 0; k < NV / 4; ++k) {
@@ -59,8 +81,10 @@ __device__ __forceinline__ void adam_vec(P* p, float* m, float* v, const float* 
     mv[4 * k] = a.x; mv[4 * k + 1] = a.y; mv[4 * k + 2] = a.z; mv[4 * k + 3] = a.w;
     vv[4 * k] = b.x; vv[4 * k + 1] = b.y; vv[4 * k + 2] = b.z; vv[4 * k + 3] = b.w;
   }
-#pragma unroll
-  for (int e = 0; e < NV; ++e) adam1(pv[e], mv[e], vv[e], g[e], hp);
+}
+
+template <typename P, int NV>
+__device__ __forceinline__ void store_pmv(P* p, float* m, float* v, const float* pv, const float* mv, const float* vv) {
   if constexpr (sizeof(P) == 4) {
 #pragma unroll
     for (int k = 0; k < NV / 4; ++k)
@@ -78,6 +102,16 @@ __device__ __forceinline__ void adam_vec(P* p, float* m, float* v, const float* 
     reinterpret_cast<float4*>(m)[k] = make_float4(mv[4 * k], mv[4 * k + 1], mv[4 * k + 2], mv[4 * k + 3]);
     reinterpret_cast<float4*>(v)[k] = make_float4(vv[4 * k], vv[4 * k + 1], vv[4 * k + 2], vv[4 * k + 3]);
   }
+}
+
+// AdamW on NV consecutive elements.
+template <typename P, int NV>
+__device__ __forceinline__ void adam_vec(P* p, float* m, float* v, const float* g, const AdamStep& s) {
+  float pv[NV], mv[NV], vv[NV];
+  load_pmv<P, NV>(p, m, v, pv, mv, vv);
+#pragma unroll
+  for (int e = 0; e < NV; ++e) adam1(pv[e], mv[e], vv[e], g[e], s);
+  store_pmv<P, NV>(p, m, v, pv, mv, vv);
 }
 
 template <int NV>
@@ -109,7 +143,7 @@ __global__ void __launch_bounds__(256) k_adamw_dense(P* __restrict__ param, floa
   for (int e = 0; e < NV; ++e) g[e] = 0.f;
   if (slot >= 0) load_grad<NV>(uniq_rows + (int64_t)slot * dim + c, g);
   const int64_t off = row * dim + c;
-  adam_vec<P, NV>(param + off, m + off, v + off, g, hp);
+  adam_vec<P, NV>(param + off, m + off, v + off, g, adam_step(hp));
 }
 
 // Dense gradient of any dtype ([rows, grad_ld], GT = float or bf16): every
@@ -133,13 +167,15 @@ __global__ void __launch_bounds__(256) k_adamw_dense_grad(P* __restrict__ param,
     for (int e = 0; e < NV; ++e) g[e] = bf16_to_f32(reinterpret_cast<const bf16_t*>(src)[e]);
   }
   const int64_t off = row * dim + c;
-  adam_vec<P, NV>(param + off, m + off, v + off, g, hp);
+  adam_vec<P, NV>(param + off, m + off, v + off, g, adam_step(hp));
 }
 
 // Catch-up (deferred dense-parity updates): one wave per row; lane 0 claims
 // the row (last[row] <- t) so duplicate ids replay it once; the skipped g = 0
 // steps (last, t] are replayed in registers with each step's hyper-parameters,
 // rounding bf16 parameters after every step exactly as a store/load would.
+// The replayed step range is wave-uniform, so the ring is read with scalar
+// loads and the slot advances without a per-step modulo.
 template <typename P, int NV>
 __global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, float* __restrict__ m,
                                                        float* __restrict__ v, int64_t num_rows, int dim,
@@ -153,37 +189,24 @@ __global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, fl
   if (row < 0 || row >= num_rows) return;
   int from = 0;
   if (lane == 0) from = atomicExch(&last[row], t);
-  from = __shfl(from, 0);
+  from = __builtin_amdgcn_readfirstlane(__shfl(from, 0));
   if (from >= t) return;
+  const int slot0 = (from + 1) % ring_len;
   for (int c = lane * NV; c < dim; c += 64 * NV) {
     float pv[NV], mv[NV], vv[NV];
     const int64_t off = row * dim + c;
-    if constexpr (sizeof(P) == 4) {
-#pragma unroll
-      for (int e = 0; e < NV; ++e) pv[e] = reinterpret_cast<const float*>(param + off)[e];
-    } else {
-#pragma unroll
-      for (int e = 0; e < NV; ++e) pv[e] = bf16_to_f32(reinterpret_cast<const bf16_t*>(param + off)[e]);
-    }
-#pragma unroll
-    for (int e = 0; e < NV; ++e) { mv[e] = m[off + e]; vv[e] = v[off + e]; }
+    load_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
+    int slot = slot0;
     for (int st = from + 1; st <= t; ++st) {
-      const grk_adamw_hparams hp = ring[st % ring_len];
+      const AdamStep s = adam_step(ring[slot]);
+      slot = slot + 1 == ring_len ? 0 : slot + 1;
 #pragma unroll
       for (int e = 0; e < NV; ++e) {
-        adam1(pv[e], mv[e], vv[e], 0.0f, hp);
+        adam1(pv[e], mv[e], vv[e], 0.0f, s);
         if constexpr (sizeof(P) == 2) pv[e] = bf16_to_f32(f32_to_bf16(pv[e]));
       }
     }
-    if constexpr (sizeof(P) == 4) {
-#pragma unroll
-      for (int e = 0; e < NV; ++e) reinterpret_cast<float*>(param + off)[e] = pv[e];
-    } else {
-#pragma unroll
-      for (int e = 0; e < NV; ++e) reinterpret_cast<bf16_t*>(param + off)[e] = f32_to_bf16(pv[e]);
-    }
-#pragma unroll
-    for (int e = 0; e < NV; ++e) { m[off + e] = mv[e]; v[off + e] = vv[e]; }
+    store_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
   }
 }
 
@@ -210,7 +233,7 @@ __global__ void __launch_bounds__(256) k_adamw_lazy(P* __restrict__ param, float
     float g[NV];
     load_grad<NV>(uniq_rows + u * dim + c, g);
     const int64_t off = uniq_ids[u] * dim + c;
-    adam_vec<P, NV>(param + off, m + off, v + off, g, hp);
+    adam_vec<P, NV>(param + off, m + off, v + off, g, adam_step(hp));
   }
 }
 

@@ -181,6 +181,37 @@ def test_adamw_bf16_param(K):
     assert np.mean(got == oemb.to_bf16_f32(wp)) > 0.99
 
 
+@pytest.mark.parametrize('D,dt', [(256, torch.float32), (512, torch.bfloat16)])
+def test_backward_wave_path(K, D, dt):
+    """dim == 64 x 16 bytes (one wave per row: k_seg_chunks_wave +
+    k_seg_combine_edges): rows with <= 512 occurrences -- inside one chunk or
+    crossing chunk edges -- are bit-exact in occurrence order; a 3000-occurrence
+    hot row uses the fixed blocked order; padding is skipped; deterministic."""
+    rng = np.random.default_rng(11)
+    R = 3000
+    idx = np.concatenate([np.full(3000, 5), np.repeat(np.arange(10, 20), rng.integers(300, 513, 10)),
+                          rng.integers(20, R, 20000), np.zeros(2000, np.int64)])
+    rng.shuffle(idx)
+    g = rng.standard_normal((len(idx), D)).astype(np.float32)
+    if dt == torch.bfloat16:
+        g = oemb.to_bf16_f32(g)
+    src = [K.GradSource(T(idx), T(g).to(dt), 0)]
+    res = K.embedding_backward(src, R, D, dense=True, sparse=True)
+    want = oemb.dense_backward(g, idx, R)
+    got = res.dense.cpu().numpy()
+    counts = np.bincount(idx, minlength=R)
+    exact = counts <= 512
+    assert counts[10:20].min() >= 300 and counts[5] == 3000
+    assert np.array_equal(got[exact], want[exact])
+    np.testing.assert_allclose(got[~exact], want[~exact], rtol=1e-5, atol=1e-3)
+    cnt = int(res.count.item())
+    uniq = oemb.unique_rows(idx)
+    assert cnt == len(uniq) and np.array_equal(res.ids[:cnt].cpu().numpy(), uniq)
+    assert np.array_equal(res.rows[:cnt].cpu().numpy(), got[uniq])
+    again = K.embedding_backward(src, R, D, dense=True).dense
+    assert torch.equal(again, res.dense)
+
+
 def test_out_of_range_flag_and_empty(K):
     table = torch.randn(10, 16, device=DEV)
     idx = torch.tensor([1, 2, 10, -1], device=DEV)
