@@ -187,6 +187,9 @@ __global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, fl
   if (w >= (ids ? num_ids : num_rows)) return;
   const int64_t row = ids ? ids[w] : w;
   if (row < 0 || row >= num_rows) return;
+  // A plain read first: later duplicates of a hot row see the claim without
+  // queueing on the atomic; the exchange still decides who replays.
+  if (__builtin_nontemporal_load(&last[row]) >= t) return;
   int from = 0;
   if (lane == 0) from = atomicExch(&last[row], t);
   from = __builtin_amdgcn_readfirstlane(__shfl(from, 0));
