@@ -11,8 +11,9 @@ rank per GPU over RCCL); tables are row-sharded, dense grads all-reduced;
 every rank processes its own 128 sequences (weak scaling).
 
 Prints ONE JSON line (rank 0) with the metric, the live roofline of the
-dominant hand-written kernel (the fused seq-side embedding gather, HBM-bound)
-and the CPU baseline (oracle/model_ref.py, the fp32 torch-CPU restatement of
+dominant hand-written kernel (attention dK/dV; HBM-bound at this shape), the
+other attention kernels and the fused gather under `rooflines`, and the CPU
+baseline (oracle/model_ref.py, the fp32 torch-CPU restatement of
 the same model and step, on a bounded sample).
 """
 from __future__ import annotations
@@ -59,40 +60,137 @@ def parse():
     return ap.parse_args()
 
 
-def gather_roofline(trace, reps):
-    """Time the seq-side fused gather alone with HIP events on its stream."""
-    from tencent_recommendation_2025_amd import kernels as K
-    lookups, out, n, tt, T = max(trace, key=lambda r: r[1].shape[1])  # widest = seq side
+def _time(fn, reps):
+    """Average duration (ms) of fn's launches, HIP events on the stream grk launches on."""
     stream = torch.cuda.current_stream()
-    K.embedding_gather(lookups, out, n, tt, T)
+    fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(reps):
-        K.embedding_gather(lookups, out, n, tt, T)
+        fn()
     e1.record(stream)
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    return e0.elapsed_time(e1) / reps
+
+
+def _pmc(name, match):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary of the same workload (or None)."""
+    path = os.path.join(REPO, 'profiles', name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        p = json.load(f)
+    if any(p.get('workload', {}).get(k) != v for k, v in match.items()):
+        return None
+    return p
+
+
+def attention_rooflines(a, key_valid, reps):
+    """The attention kernels of one layer at the bench shape and the batch's own
+    ragged lengths, timed alone (HIP events on their stream).
+
+    Algorithmic bytes count the rows a kernel must move for VALID tokens
+    (padding rows are skipped by the kernels): fwd reads q, k, v and writes o;
+    dq reads q, k, v, dO and writes dq; dk/dv reads q, k, v, dO and writes dk,
+    dv (bf16, D = H*hd per token; + the fp32 rab row / softmax lse, delta).
+    FLOPs count causal valid pairs P = H * sum_b L_b (L_b + 1) / 2, 2*hd per
+    pair per matmul: fwd 2 matmuls, dq 3 (S, dP, dQ), dk/dv 4 (S, dV, dP, dK).
+    At T = 201, hd = 64 the intensity (~45-65 FLOP/B) is far below the MI355X
+    ridge (2.5 PF / 8 TB/s = 312 FLOP/B): HBM is the bound."""
+    from tencent_recommendation_2025_amd import _lib as L
+    from tencent_recommendation_2025_amd import kernels as K
+    B, T = key_valid.shape
+    H, D = a.heads, a.hidden
+    hd = D // H
+    dev = key_valid.device
+    g = torch.Generator(device=dev).manual_seed(7)
+    pre = torch.randn(B * T, 4 * D, device=dev, generator=g).bfloat16()    # [u | v | q | k] as HSTUAttention
+    kv = key_valid.to(torch.uint8).contiguous()
+    hstu = a.block == 'hstu'
+    kind = L.ATTN_HSTU if hstu else L.ATTN_SOFTMAX
+    extra = dict(rab=0.1 * torch.randn(H, T, device=dev, generator=g), inv_n=1.0 / T, act='silu') if hstu else {}
+    args = K.attn_args(kind, pre[:, 2 * D:3 * D], pre[:, 3 * D:], pre[:, D:2 * D], B, T, H, hd, key_valid=kv,
+                       scale=hd ** -0.5, out_dtype=torch.bfloat16, seq_range=K.seq_ranges(kv), **extra)
+    o = torch.empty(B * T, D, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B, H, T, device=dev)
+    do = torch.randn(B * T, D, device=dev, generator=g).bfloat16()
+    dpre = torch.empty(B * T, 4 * D, dtype=torch.bfloat16, device=dev)
+    delta = torch.empty(B, H, T, device=dev)
+    drab = torch.zeros(H, T, device=dev) if hstu else None
+    K.attention_fwd(args, o, lse)
+    K.attention_bwd(args, o, do, lse, delta, dpre[:, 2 * D:3 * D], dpre[:, 3 * D:], dpre[:, D:2 * D], drab)
+    t_fwd = _time(lambda: K.attention_fwd(args, o, lse), reps)
+    t_dq = _time(lambda: K.attention_bwd(args, o, do, lse, delta, dpre[:, 2 * D:3 * D], None, None, drab,
+                                         parts=L.ATTN_BWD_DQ), reps)
+    t_dkdv = _time(lambda: K.attention_bwd(args, o, do, lse, delta, None, dpre[:, 3 * D:], dpre[:, D:2 * D], None,
+                                           parts=L.ATTN_BWD_DKDV), reps)
+    lens = kv.sum(1).double()
+    n_valid = int(lens.sum().item())
+    pairs = float((lens * (lens + 1) / 2).sum().item()) * H
+    row = D * 2
+    side = H * T * 4 if hstu else n_valid * H * 4            # rab row / lse (+ delta) per kernel
+    ridge = BF16_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBPS * 1e9)
+    name = 'hstu' if hstu else 'softmax'
+    workload = {'B': B, 'T': T, 'D': D, 'H': H, 'kind': name, 'valid_tokens': n_valid}
+
+    def entry(kernel, ms, nbytes, flops, pmc_name):
+        gbps = nbytes / (ms * 1e-3) / 1e9
+        tfs = flops / (ms * 1e-3) / 1e12
+        ai = flops / nbytes
+        bound = 'hbm' if ai < ridge else 'mfma'
+        res = {'bound': bound, 'kernel': kernel,
+               'achieved': round(gbps if bound == 'hbm' else tfs, 1),
+               'peak': HBM_PEAK_GBPS if bound == 'hbm' else BF16_PEAK_TFLOPS,
+               'unit': 'GB/s' if bound == 'hbm' else 'TFLOP/s',
+               'frac': round(gbps / HBM_PEAK_GBPS if bound == 'hbm' else tfs / BF16_PEAK_TFLOPS, 4),
+               'traffic': None, 'alg_bytes_per_launch': int(nbytes), 'flops_per_launch': int(flops),
+               'tflops': round(tfs, 1), 'mfma_frac': round(tfs / BF16_PEAK_TFLOPS, 4),
+               'arith_intensity': round(ai, 1), 'ridge': round(ridge, 1), 'avg_launch_us': round(ms * 1e3, 2),
+               'workload': workload}
+        p = _pmc(pmc_name, workload)
+        if p is not None:
+            res['traffic'] = int(p['traffic_bytes_per_launch'])
+            res['traffic_note'] = (f'rocprofv3 PMC (profiles/{pmc_name}): FETCH_SIZE x2 + WRITE_SIZE '
+                                   '(MI355X_MICROARCH.md gfx950 corrections)')
+        return res
+
+    dkdv = entry(f'grk::k_attn_dkdv_seq ({name} attention dK/dV, one layer)', t_dkdv,
+                 6 * n_valid * row + side, 8 * hd * pairs, f'r1_pmc_attn_dkdv_{name}.json')
+    fwd = entry(f'grk::k_attn_fwd_seq ({name} attention forward, one layer)', t_fwd,
+                4 * n_valid * row + side, 4 * hd * pairs, f'r1_pmc_attn_fwd_{name}.json')
+    dq = entry(f'grk::k_attn_dq_seq ({name} attention dQ{" + drab" if hstu else ""}, one layer)', t_dq,
+               5 * n_valid * row + side, 6 * hd * pairs, f'r1_pmc_attn_dq_{name}.json')
+    fwd['survey_formula_flops'] = int(2 * B * D * T * (T + 1))  # SURVEY.md 8(d): 2*B*D*T(T+1) per layer fwd
+    return dkdv, [fwd, dq]
+
+
+def gather_roofline(trace, reps):
+    """The seq-side fused gather alone (HIP events on its stream).
+
+    Algorithmic bytes per SURVEY.md 8(d): rows x D x elem read + output rows
+    written + index bytes.  Most rows are projected feature-table rows and the
+    padding row, which stay resident in L2 / the Infinity Cache, so this rate
+    is a cache-served gather rate, not an HBM rate: no HBM fraction is given
+    (MI355X_MICROARCH.md measures ~17-19 TB/s for L2-resident and ~8.6 TB/s for
+    Infinity-Cache-resident row gathers)."""
+    from tencent_recommendation_2025_amd import kernels as K
+    lookups, out, n, tt, T = max(trace, key=lambda r: r[1].shape[1])  # widest = seq side
+    ms = _time(lambda: K.embedding_gather(lookups, out, n, tt, T), reps)
     D = lookups[0].table.shape[1]
     es = lookups[0].table.element_size()
     rows = n * sum(lk.bag for lk in lookups)
     idx_bytes = sum(lk.idx.numel() * lk.idx.element_size() for lk in lookups)
     tt_bytes = n * 4 if tt is not None else 0
     alg = rows * D * es + n * D * len(lookups) * es + idx_bytes + tt_bytes
-    gbps = alg / (ms * 1e-3) / 1e9
-    res = {'bound': 'hbm', 'kernel': 'grk::k_gather (seq-side fused lookup)', 'achieved': round(gbps, 1),
-           'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': round(gbps / HBM_PEAK_GBPS, 4), 'traffic': None,
-           'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2),
-           'rows_per_launch': int(rows), 'features': len(lookups)}
-    # HBM bytes per launch from the committed rocprofv3 PMC passes of this same workload
-    pmc = os.path.join(REPO, 'profiles', 'r1_pmc_gather.json')
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            p = json.load(f)
-        if abs(p['write_bytes_per_launch'] - n * D * len(lookups) * es) < 1e6:  # same output bytes => same workload
-            res['traffic'] = int(p['traffic_bytes_per_launch'])
-            res['traffic_note'] = ('rocprofv3 PMC (profiles/r1_pmc_gather.json): FETCH_SIZE x2 + WRITE_SIZE; '
-                                   'reads of small/padding rows hit L2, so traffic < algorithmic bytes')
-            res['traffic_gbps'] = round(p['traffic_bytes_per_launch'] / (ms * 1e-3) / 1e9, 1)
+    res = {'bound': 'l2/infinity-cache', 'kernel': 'grk::k_gather (seq-side fused lookup)',
+           'achieved': round(alg / (ms * 1e-3) / 1e9, 1), 'peak': None, 'unit': 'GB/s', 'frac': None,
+           'traffic': None, 'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2),
+           'rows_per_launch': int(rows), 'features': len(lookups),
+           'workload': {'tokens': int(n), 'rows': int(rows), 'features': len(lookups)}}
+    p = _pmc('r1_pmc_gather.json', res['workload'])
+    if p is not None:
+        res['traffic'] = int(p['traffic_bytes_per_launch'])
+        res['traffic_gbps'] = round(p['traffic_bytes_per_launch'] / (ms * 1e-3) / 1e9, 1)
     return res
 
 
@@ -203,7 +301,9 @@ def main():
         G.GATHER_TRACE = []
         trainer.step(pool[0])
         trace, G.GATHER_TRACE = G.GATHER_TRACE, None
-    roof = gather_roofline(trace, a.roofline_reps)
+    kv = (pool[0][3] != 0).to(torch.uint8)        # the first bench batch's key validity (token_type != 0)
+    roof, more = attention_rooflines(a, kv, a.roofline_reps)
+    more.append(gather_roofline(trace, a.roofline_reps))
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline:
@@ -223,6 +323,7 @@ def main():
                        'parallelism': f'dp{world}' + ('+rowshard' if sharded else '')},
             'final_loss': round(final_loss, 5),
             'roofline': roof,
+            'rooflines': more,
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)

@@ -230,6 +230,20 @@ int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_t ldo, cons
                       int dout_dtype, const float* lse, float* delta_ws, void* dq, int64_t lddq, void* dk,
                       int64_t lddk, void* dv, int64_t lddv, float* drab, int64_t* drab_ws, void* stream);
 
+/* grk_attention_bwd in two independent halves, for callers that schedule
+ * them separately (two streams, or timing one kernel):
+ *   GRK_ATTN_BWD_DQ   -- softmax delta, dq, and drab (with its scratch reset
+ *                        and fixed-point finalize);
+ *   GRK_ATTN_BWD_DKDV -- dk and dv (softmax: reads the delta the DQ half wrote).
+ * parts = GRK_ATTN_BWD_DQ | GRK_ATTN_BWD_DKDV is grk_attention_bwd.  Arguments
+ * a half does not use may be NULL (DQ: dk/dv; DKDV: dq, drab). */
+#define GRK_ATTN_BWD_DQ 1
+#define GRK_ATTN_BWD_DKDV 2
+int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
+                            int dout_dtype, const float* lse, float* delta_ws, void* dq, int64_t lddq, void* dk,
+                            int64_t lddk, void* dv, int64_t lddv, float* drab, int64_t* drab_ws, int parts,
+                            void* stream);
+
 /* ------------------------------------------------------------------------
  * HSTU output gate (north star; no reference -- oracle/hstu.py)
  *   y = dropout(LayerNorm(o; gamma, beta, eps) * SiLU(u))

@@ -1,0 +1,70 @@
+#!/usr/bin/env python
+"""HBM traffic per launch of the bench's roofline kernels from two rocprofv3
+counter passes (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950),
+written to profiles/ for bench.py's `traffic` field.
+
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d <F> -o run -- python bench.py --steps 2 --warmup 1 --cpu-baseline 0
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d <W> -o run -- python bench.py ... > <bench.log>
+    python scripts/pmc_rooflines.py <F> <W> <bench.log> <round tag, e.g. r1>
+
+Corrections (MI355X_MICROARCH.md, HBM / rocprofv3): FETCH_SIZE (KiB) counts
+half the bytes of a wide coalesced stream on gfx950 -> x2; WRITE_SIZE (KiB)
+is exact for 16-B-per-lane stores.  The last `--reps` launches of each kernel
+(bench.py's roofline replays, same shapes as the training launches) are
+averaged; the workload the bench printed is stored with them so bench.py only
+uses the numbers for the same workload.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+fdir, wdir, log, tag = sys.argv[1:5]
+reps = int(sys.argv[5]) if len(sys.argv) > 5 else 5
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counter_rows(d, counter):
+    path = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)[0]
+    return [r for r in csv.DictReader(open(path)) if r['Counter_Name'] == counter]
+
+
+def per_launch(rows, needle, pick_largest_grid):
+    rows = [r for r in rows if needle in r['Kernel_Name']]
+    if pick_largest_grid:
+        big = max(int(r['Grid_Size']) for r in rows)
+        rows = [r for r in rows if int(r['Grid_Size']) == big]
+    # one row per dispatch (a counter may be reported per XCD / instance: sum them)
+    key = next(k for k in ('Dispatch_Id', 'Correlation_Id', 'Kernel_Id') if k in rows[0])
+    by = {}
+    for r in rows:
+        by.setdefault(r[key], 0.0)
+        by[r[key]] += float(r['Counter_Value'])
+    vals = [by[k] for k in sorted(by, key=int)][-reps:]
+    return sum(vals) / len(vals), len(vals)
+
+
+line = [ln for ln in open(log) if ln.startswith('{"metric"')][-1]
+bench = json.loads(line)
+entries = [bench['roofline']] + bench.get('rooflines', [])
+fetch, write = counter_rows(fdir, 'FETCH_SIZE'), counter_rows(wdir, 'WRITE_SIZE')
+for e in entries:
+    k = e['kernel'].split()[0].replace('grk::', '')
+    needle = k + '<' if k.startswith('k_attn') else k
+    f, nf = per_launch(fetch, needle, k == 'k_gather')
+    w, nw = per_launch(write, needle, k == 'k_gather')
+    if k.startswith('k_attn'):
+        name = f"{tag}_pmc_attn_{k[len('k_attn_'):-len('_seq')]}_{e['workload']['kind']}.json"
+    else:
+        name = f'{tag}_pmc_gather.json'
+    out = {'kernel': k, 'workload': e['workload'], 'launches_averaged': min(nf, nw),
+           'fetch_bytes_per_launch': 2 * f * 1024, 'write_bytes_per_launch': w * 1024,
+           'traffic_bytes_per_launch': 2 * f * 1024 + w * 1024,
+           'alg_bytes_per_launch': e['alg_bytes_per_launch'],
+           'method': 'rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH_SIZE x2 '
+                     '(gfx950 wide-stream correction, MI355X_MICROARCH.md HBM), KiB -> bytes'}
+    with open(os.path.join(REPO, 'profiles', name), 'w') as fh:
+        json.dump(out, fh, indent=1)
+    print(f"{name}: traffic {out['traffic_bytes_per_launch'] / 1e6:.1f} MB vs algorithmic "
+          f"{e['alg_bytes_per_launch'] / 1e6:.1f} MB per launch")

@@ -55,6 +55,7 @@ class GrkAttnArgs(C.Structure):
 
 
 ATTN_SOFTMAX, ATTN_HSTU = 0, 1
+ATTN_BWD_DQ, ATTN_BWD_DKDV = 1, 2
 ACT_NONE, ACT_SILU = 0, 1
 
 
@@ -80,6 +81,8 @@ SIGNATURES = {
     'grk_attention_fwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _P]),
     'grk_attention_bwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64, _P, _I64,
                                _P, _P, _P]),
+    'grk_attention_bwd_parts': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64,
+                                     _P, _I64, _P, _P, _I, _P]),
     'grk_norm_gate_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _F, C.c_uint64, _P, _I64, _P, _P]),
     'grk_norm_gate_bwd_workspace': (_SZ, [_I64, _I]),
     'grk_norm_gate_bwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _P, _P, _I64, _I, _F, C.c_uint64, _P, _I64, _P,

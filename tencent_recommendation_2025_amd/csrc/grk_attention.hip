@@ -476,40 +476,53 @@ extern "C" int grk_attention_fwd(const grk_attn_args* a, void* out, int64_t ldo,
   return launch(p, a->head_dim, 0, (hipStream_t)stream);
 }
 
-extern "C" int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout,
-                                 int64_t lddo, int dout_dtype, const float* lse, float* delta_ws, void* dq,
-                                 int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv, float* drab,
-                                 int64_t* drab_ws, void* stream) {
+extern "C" int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout,
+                                       int64_t lddo, int dout_dtype, const float* lse, float* delta_ws, void* dq,
+                                       int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv, float* drab,
+                                       int64_t* drab_ws, int parts, void* stream) {
   clear_error();
   AttnParams p;
   int rc = fill_params(a, &p);
   if (rc) return rc;
+  GRK_CHECK_ARG(parts >= 1 && parts <= (GRK_ATTN_BWD_DQ | GRK_ATTN_BWD_DKDV), "bad parts (%d)", parts);
+  const bool do_dq = parts & GRK_ATTN_BWD_DQ, do_dkdv = parts & GRK_ATTN_BWD_DKDV;
   const int64_t need = (int64_t)a->heads * a->head_dim;
   GRK_CHECK_ARG(dout && lddo >= need && lddo % 8 == 0, "bad dout / lddo");
   GRK_CHECK_ARG(dout_dtype == GRK_F32 || dout_dtype == GRK_BF16, "bad dout dtype");
-  GRK_CHECK_ARG(dq && dk && dv && lddq >= need && lddk >= need && lddv >= need, "bad dq/dk/dv");
+  GRK_CHECK_ARG(!do_dq || (dq && lddq >= need), "bad dq");
+  GRK_CHECK_ARG(!do_dkdv || (dk && dv && lddk >= need && lddv >= need), "bad dk/dv");
   GRK_CHECK_ARG(a->kind == GRK_ATTN_HSTU || (out && lse && delta_ws && ldo >= need),
                 "softmax backward needs out, lse and delta_ws [B, H, T]");
   p.out = const_cast<void*>(out); p.ldo = ldo;
   p.dout = dout; p.lddo = lddo; p.dout_f32 = dout_dtype == GRK_F32;
   p.lse = const_cast<float*>(lse); p.delta = delta_ws;
   p.dq = dq; p.lddq = lddq; p.dk = dk; p.lddk = lddk; p.dv = dv; p.lddv = lddv;
-  GRK_CHECK_ARG(!drab || drab_ws, "drab needs drab_ws (int64 [H, nb] scratch)");
-  p.drab = a->kind == GRK_ATTN_HSTU ? drab : nullptr;
+  GRK_CHECK_ARG(!do_dq || !drab || drab_ws, "drab needs drab_ws (int64 [H, nb] scratch)");
+  p.drab = (a->kind == GRK_ATTN_HSTU && do_dq) ? drab : nullptr;
   p.drab_fix = reinterpret_cast<unsigned long long*>(drab_ws);
   hipStream_t s = (hipStream_t)stream;
-  const int nfix = a->heads * a->num_buckets;
-  if (p.drab) GRK_CHECK_HIP(hipMemsetAsync(drab_ws, 0, (size_t)nfix * 8, s));
-  if (a->kind == GRK_ATTN_SOFTMAX) {
-    // out dtype of the forward output equals out_dtype of these args
-    rc = launch(p, a->head_dim, 1, s);
+  if (do_dq) {
+    const int nfix = a->heads * a->num_buckets;
+    if (p.drab) GRK_CHECK_HIP(hipMemsetAsync(drab_ws, 0, (size_t)nfix * 8, s));
+    if (a->kind == GRK_ATTN_SOFTMAX) {
+      // out dtype of the forward output equals out_dtype of these args
+      rc = launch(p, a->head_dim, 1, s);
+      if (rc) return rc;
+    }
+    rc = launch(p, a->head_dim, 2, s);
     if (rc) return rc;
+    if (p.drab) {
+      k_drab_finalize<<<(nfix + 255) / 256, 256, 0, s>>>(p.drab, p.drab_fix, nfix);
+      GRK_LAUNCH_CHECK();
+    }
   }
-  rc = launch(p, a->head_dim, 2, s);
-  if (rc) return rc;
-  if (p.drab) {
-    k_drab_finalize<<<(nfix + 255) / 256, 256, 0, s>>>(p.drab, p.drab_fix, nfix);
-    GRK_LAUNCH_CHECK();
-  }
-  return launch(p, a->head_dim, 3, s);
+  return do_dkdv ? launch(p, a->head_dim, 3, s) : GRK_OK;
+}
+
+extern "C" int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout,
+                                 int64_t lddo, int dout_dtype, const float* lse, float* delta_ws, void* dq,
+                                 int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv, float* drab,
+                                 int64_t* drab_ws, void* stream) {
+  return grk_attention_bwd_parts(a, out, ldo, dout, lddo, dout_dtype, lse, delta_ws, dq, lddq, dk, lddk, dv, lddv,
+                                 drab, drab_ws, GRK_ATTN_BWD_DQ | GRK_ATTN_BWD_DKDV, stream);
 }

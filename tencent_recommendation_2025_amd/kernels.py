@@ -280,17 +280,25 @@ def attention_fwd(args, out, lse=None):
     L.check(rc, 'grk_attention_fwd')
 
 
-def attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab=None):
-    """grk_attention_bwd: writes dq/dk/dv (args.out_dtype) and accumulates drab (deterministic)."""
+def attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab=None, parts=L.ATTN_BWD_DQ | L.ATTN_BWD_DKDV):
+    """grk_attention_bwd(_parts): writes dq/dk/dv (args.out_dtype) and accumulates drab
+    (deterministic).  ``parts`` selects the dq half (L.ATTN_BWD_DQ: delta, dq, drab)
+    and/or the dk/dv half (L.ATTN_BWD_DKDV); tensors of a half not run may be None."""
     _require_cuda(dout, dq, dk, dv, drab)
     for t, n in ((dout, 'dout'), (dq, 'dq'), (dk, 'dk'), (dv, 'dv')):
-        if t.stride(1) != 1 or t.stride(0) % 8:
+        if t is not None and (t.stride(1) != 1 or t.stride(0) % 8):
             raise L.GrkError(f'{n} must be row-major with a row stride multiple of 8')
-    ws = None if drab is None else torch.empty(drab.numel(), dtype=torch.int64, device=drab.device)
-    rc = L.lib().grk_attention_bwd(C.byref(args), _ptr(out), 0 if out is None else out.stride(0), dout.data_ptr(),
-                                   dout.stride(0), L.dtype_code(dout.dtype), _ptr(lse), _ptr(delta), dq.data_ptr(),
-                                   dq.stride(0), dk.data_ptr(), dk.stride(0), dv.data_ptr(), dv.stride(0), _ptr(drab),
-                                   _ptr(ws), L.stream_ptr(dout.device))
+    ws = None if drab is None or not parts & L.ATTN_BWD_DQ else torch.empty(drab.numel(), dtype=torch.int64,
+                                                                            device=drab.device)
+
+    def p_ld(t):
+        return (None, 0) if t is None else (t.data_ptr(), t.stride(0))
+
+    (q_p, q_ld), (k_p, k_ld), (v_p, v_ld) = p_ld(dq), p_ld(dk), p_ld(dv)
+    rc = L.lib().grk_attention_bwd_parts(C.byref(args), _ptr(out), 0 if out is None else out.stride(0),
+                                         dout.data_ptr(), dout.stride(0), L.dtype_code(dout.dtype), _ptr(lse),
+                                         _ptr(delta), q_p, q_ld, k_p, k_ld, v_p, v_ld, _ptr(drab), _ptr(ws), parts,
+                                         L.stream_ptr(dout.device))
     L.check(rc, 'grk_attention_bwd')
 
 

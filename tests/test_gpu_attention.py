@@ -223,3 +223,41 @@ def test_non_contiguous_key_valid(K, kind, use_ranges):
     for key in ('out', 'dq', 'dk', 'dv') + (('drab',) if kind == 1 else ()):
         err = nrel(res[key], want[key])
         assert err < TOL_PRECISE, f'{key}: normwise rel err {err:.2e}'
+
+
+@pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
+@pytest.mark.parametrize('T', [130, 600])  # whole-sequence and chunked kernels
+def test_bwd_parts_equal_full_backward(K, kind, T):
+    """grk_attention_bwd_parts: the dq half then the dk/dv half (each may run on
+    its own stream) give bitwise the outputs of the one-call backward."""
+    from tencent_recommendation_2025_amd import _lib as L
+    B, H, hd = 3, 2, 64
+    D = H * hd
+    x, valid = make_inputs(B, T, H, hd, [T, T // 2, 7], 5)
+    xd = torch.from_numpy(x).to(DEV).to(torch.bfloat16)
+    kv = torch.from_numpy(valid).to(DEV)
+    extra = dict(rab=0.3 * torch.randn(H, T, device=DEV), inv_n=1.0 / T) if kind == L.ATTN_HSTU else {}
+    args = K.attn_args(kind, xd[:, :D], xd[:, D:2 * D], xd[:, 2 * D:], B, T, H, hd, key_valid=kv,
+                       out_dtype=torch.bfloat16, act='silu' if kind == L.ATTN_HSTU else None, **extra)
+    out = torch.empty(B * T, D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.empty(B, H, T, device=DEV)
+    K.attention_fwd(args, out, lse)
+    dout = torch.randn(B * T, D, device=DEV).bfloat16()
+
+    def bwd(split):
+        g = [torch.full((B * T, D), 7.0, dtype=torch.bfloat16, device=DEV) for _ in range(3)]
+        delta = torch.empty(B, H, T, device=DEV)
+        drab = torch.zeros(H, T, device=DEV) if kind == L.ATTN_HSTU else None
+        if split:
+            K.attention_bwd(args, out, dout, lse, delta, g[0], None, None, drab, parts=L.ATTN_BWD_DQ)
+            assert torch.all(g[1] == 7.0) and torch.all(g[2] == 7.0)
+            K.attention_bwd(args, out, dout, lse, delta, None, g[1], g[2], None, parts=L.ATTN_BWD_DKDV)
+        else:
+            K.attention_bwd(args, out, dout, lse, delta, *g, drab)
+        return g, drab
+
+    (a, ra), (b, rb) = bwd(False), bwd(True)
+    for x1, x2 in zip(a, b):
+        assert torch.equal(x1, x2)
+    if ra is not None:
+        assert torch.equal(ra, rb)
