@@ -28,7 +28,7 @@ $(OBJ_DIR)/%.cpp.o: $(SRC_DIR)/%.cpp include/grk.h | $(OBJ_DIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -L/opt/rocm/lib -lhipblaslt
 
 clean:
 	rm -rf build $(LIB)

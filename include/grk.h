@@ -314,6 +314,30 @@ int grk_sampled_softmax_grad(const void* h, int64_t ldh, const void* e, int64_t 
                              const uint8_t* valid, int64_t num_rows, int dim, float tau, const float* lse2,
                              const int32_t* count, const float* grad_loss, void* G, int64_t ldg, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Plain GEMM for the dense layers around the hot path (HSTU uvqk /
+ * out_linear, itemdnn / userdnn: forward, dX and the weight gradients), on
+ * hipBLASLt with a workspace so its stream-K kernels are eligible
+ * (replaces the torch.nn.Linear / torch.addmm calls of
+ * model/BaseLine/model.py:86-92,129-139 for the fused path).
+ * Row-major, as torch tensors: C[m, n] = alpha * op(A) @ op(B) + beta * C_in
+ * (+ bias[n] broadcast over rows); C_in = c_in, or C itself when c_in is NULL
+ * (c_in has C's dtype and ldc).  op(A) is [m, k]: A stored [m, k] (lda >= k)
+ * or, trans_a, [k, m] (lda >= m); op(B) is [k, n]: B stored [k, n] (ldb >= n)
+ * or, trans_b, [n, k] (ldb >= k).  A, B bf16; C bf16 or fp32 (fp32 C with
+ * beta = 1 accumulates a weight gradient in place); bias bf16 or fp32 or
+ * NULL.  fp32 accumulation.  One plan per shape: the fastest of hipBLASLt's
+ * heuristic candidates, timed on the shape's first call (see
+ * grk_gemm_tuning), then fixed for the process. */
+int grk_gemm(int trans_a, int trans_b, int64_t m, int64_t n, int64_t k, const void* a, int64_t lda, const void* b,
+             int64_t ldb, int ab_dtype, void* c, int64_t ldc, int c_dtype, const void* c_in, float alpha, float beta,
+             const void* bias, int bias_dtype, void* stream);
+
+/* Number of hipBLASLt candidates grk_gemm times for each NEW shape (1..256,
+ * default 256; env GRK_GEMM_TUNE at load).  1 = the heuristic's first pick,
+ * with no timing: the same kernel in every process. */
+int grk_gemm_tuning(int candidates);
+
 #ifdef __cplusplus
 }
 #endif

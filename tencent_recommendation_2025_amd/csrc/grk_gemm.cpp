@@ -1,0 +1,240 @@
+// Plain GEMMs of the dense layers around the hot path (HSTU uvqk /
+// out_linear, itemdnn / userdnn, their dX and dW) on hipBLASLt.
+//
+// torch's matmul path hands hipBLASLt no room for the stream-K kernels, and
+// at this model's shapes -- M = B*T = 25,728 rows against N, K of 512-2,048 --
+// the weight gradients (reduction over M, a 512 x 2,048 output: 32 output
+// tiles for 256 CUs) ran at 110-280 TF/s.  The same library with a workspace
+// picks stream-K kernels: 2-3x faster on the weight gradients and ~2x on the
+// uvqk forward (scripts/microbench/hipblaslt_search.cpp).  This file keeps a
+// handle per device, a workspace per (device, stream) and one plan per
+// problem shape: descriptors + the fastest of hipBLASLt's heuristic
+// candidates, timed once on the shape's first call (the library's first pick
+// is up to 2x slower here: uvqk forward 111 vs 63 us).  The choice is fixed for
+// the process; grk_gemm_tuning(1) keeps the heuristic's first pick (the same
+// kernels in every run).
+//
+// Row-major interface (as torch tensors): C[m, n] = alpha op(A) op(B) + beta C_in
+// (+ bias[n]), computed as the column-major C^T = op(B)^T op(A)^T.
+#include <hipblaslt/hipblaslt-ext.hpp>
+#include <hipblaslt/hipblaslt.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+#include <unordered_map>
+
+#include "grk_common.h"
+
+namespace {
+
+constexpr size_t kWorkspaceBytes = 256ull << 20;  // stream-K partials of the 2,048 x 512 weight gradients
+
+struct Key {
+  int ta, tb, abt, ct, bt, dev;
+  int64_t m, n, k, lda, ldb, ldc;
+  bool operator==(const Key& o) const {
+    return ta == o.ta && tb == o.tb && abt == o.abt && ct == o.ct && bt == o.bt && dev == o.dev && m == o.m &&
+           n == o.n && k == o.k && lda == o.lda && ldb == o.ldb && ldc == o.ldc;
+  }
+};
+struct KeyHash {
+  size_t operator()(const Key& x) const {
+    size_t h = 1469598103934665603ull;
+    const int64_t v[] = {x.ta, x.tb, x.abt, x.ct, x.bt, x.dev, x.m, x.n, x.k, x.lda, x.ldb, x.ldc};
+    for (int64_t e : v) h = (h ^ (size_t)e) * 1099511628211ull;
+    return h;
+  }
+};
+struct Plan {
+  hipblasLtMatmulDesc_t op;
+  hipblasLtMatrixLayout_t A, B, C;
+  hipblasLtMatmulAlgo_t algo;
+  size_t ws;
+};
+struct StreamKey {
+  int dev;
+  hipStream_t s;
+  bool operator==(const StreamKey& o) const { return dev == o.dev && s == o.s; }
+};
+struct StreamKeyHash {
+  size_t operator()(const StreamKey& x) const { return std::hash<void*>()(x.s) * 31 + (size_t)x.dev; }
+};
+
+std::mutex g_mu;
+// Candidates timed per new GEMM shape (grk_gemm_tuning; GRK_GEMM_TUNE overrides at load).
+int g_tune = [] {
+  const char* e = getenv("GRK_GEMM_TUNE");
+  return e ? std::max(1, std::min(256, atoi(e))) : 256;
+}();
+std::unordered_map<int, hipblasLtHandle_t> g_handles;
+std::unordered_map<StreamKey, void*, StreamKeyHash> g_ws;
+std::unordered_map<Key, Plan, KeyHash> g_plans;
+
+hipDataType hip_type(int dt) { return dt == GRK_F32 ? HIP_R_32F : HIP_R_16BF; }
+
+#define GRK_CHECK_BLAS(expr)                                                  \
+  do {                                                                        \
+    hipblasStatus_t _s = (expr);                                              \
+    if (_s != HIPBLAS_STATUS_SUCCESS) {                                       \
+      ::grk::set_error("%s failed: hipblas status %d", #expr, (int)_s);       \
+      return GRK_EHIP;                                                        \
+    }                                                                         \
+  } while (0)
+
+struct Operands {  // the first call's operands, for timing candidate algorithms
+  const void *a, *b, *bias;
+  void* ws;
+  hipStream_t s;
+};
+
+// Average time of `reps` launches of one algorithm into a scratch output (never the caller's C).
+float time_algo(hipblasLtHandle_t h, Plan* p, const hipblasLtMatmulAlgo_t* algo, const Operands& o, void* scratch,
+                int reps) {
+  const float alpha = 1.f, beta = 0.f;
+  for (int i = 0; i < 2; ++i)
+    if (hipblasLtMatmul(h, p->op, &alpha, o.b, p->A, o.a, p->B, &beta, scratch, p->C, scratch, p->C, algo, o.ws,
+                        kWorkspaceBytes, o.s) != HIPBLAS_STATUS_SUCCESS)
+      return -1.f;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return -1.f;
+  if (hipEventCreate(&e1) != hipSuccess) { hipEventDestroy(e0); return -1.f; }
+  hipEventRecord(e0, o.s);
+  for (int i = 0; i < reps; ++i)
+    hipblasLtMatmul(h, p->op, &alpha, o.b, p->A, o.a, p->B, &beta, scratch, p->C, scratch, p->C, algo, o.ws,
+                    kWorkspaceBytes, o.s);
+  hipEventRecord(e1, o.s);
+  float ms = -1.f;
+  if (hipEventSynchronize(e1) == hipSuccess) hipEventElapsedTime(&ms, e0, e1);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  return ms * 1e3f / reps;
+}
+
+int make_plan(hipblasLtHandle_t h, const Key& key, bool has_bias, Plan* p, const Operands& o) {
+  // column-major problem: C'[n, m] = op'(A')[n, k] op'(B')[k, m], A' = B, B' = A
+  const hipblasOperation_t opA = key.tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  const hipblasOperation_t opB = key.ta ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  GRK_CHECK_BLAS(hipblasLtMatmulDescCreate(&p->op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+  GRK_CHECK_BLAS(hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)));
+  GRK_CHECK_BLAS(hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)));
+  if (has_bias) {
+    const hipblasLtEpilogue_t ep = HIPBLASLT_EPILOGUE_BIAS;
+    const hipDataType bt = hip_type(key.bt);
+    GRK_CHECK_BLAS(hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &ep, sizeof(ep)));
+    GRK_CHECK_BLAS(hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+  }
+  const hipDataType ab = hip_type(key.abt);
+  // A' = B: op N -> [n, k] with ld ldb; op T -> stored [k, n]
+  GRK_CHECK_BLAS(hipblasLtMatrixLayoutCreate(&p->A, ab, key.tb ? key.k : key.n, key.tb ? key.n : key.k, key.ldb));
+  // B' = A: op N -> [k, m] with ld lda; op T -> stored [m, k]
+  GRK_CHECK_BLAS(hipblasLtMatrixLayoutCreate(&p->B, ab, key.ta ? key.m : key.k, key.ta ? key.k : key.m, key.lda));
+  GRK_CHECK_BLAS(hipblasLtMatrixLayoutCreate(&p->C, hip_type(key.ct), key.n, key.m, key.ldc));
+  hipblasLtMatmulPreference_t pref;
+  GRK_CHECK_BLAS(hipblasLtMatmulPreferenceCreate(&pref));
+  uint64_t wmax = kWorkspaceBytes;
+  GRK_CHECK_BLAS(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wmax,
+                                                       sizeof(wmax)));
+  // time the heuristic's first g_tune candidates on the first call's operands and keep the fastest
+  const int want = g_tune;
+  std::vector<hipblasLtMatmulHeuristicResult_t> res(want);
+  int n = 0;
+  const hipblasStatus_t st =
+      hipblasLtMatmulAlgoGetHeuristic(h, p->op, p->A, p->B, p->C, p->C, pref, want, res.data(), &n);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (st != HIPBLAS_STATUS_SUCCESS || n < 1) {
+    grk::set_error("hipBLASLt has no algorithm for this GEMM (m=%lld n=%lld k=%lld ta=%d tb=%d)", (long long)key.m,
+                   (long long)key.n, (long long)key.k, key.ta, key.tb);
+    return GRK_EHIP;
+  }
+  int best = 0;
+  float t0 = -1.f, tbest = -1.f;
+  if (n > 1) {
+    void* scratch = nullptr;
+    const size_t cbytes = (size_t)key.ldc * key.m * (key.ct == GRK_F32 ? 4 : 2);
+    if (hipMalloc(&scratch, cbytes) == hipSuccess) {
+      if (has_bias)
+        hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &o.bias, sizeof(o.bias));
+      for (int i = 0; i < n; ++i) {
+        const float t = time_algo(h, p, &res[i].algo, o, scratch, 5);
+        if (i == 0) t0 = t;
+        if (t > 0 && (tbest < 0 || t < tbest)) {
+          tbest = t;
+          best = i;
+        }
+      }
+      hipDeviceSynchronize();
+      hipFree(scratch);
+    }
+  }
+  p->algo = res[best].algo;
+  p->ws = res[best].workspaceSize;
+  if (getenv("GRK_GEMM_LOG"))
+    fprintf(stderr, "grk_gemm plan m=%lld n=%lld k=%lld ta=%d tb=%d c=%s bias=%d ws=%zu: candidate %d of %d "
+            "(%.1f us; first %.1f us): %s\n", (long long)key.m, (long long)key.n, (long long)key.k, key.ta, key.tb,
+            key.ct == GRK_F32 ? "f32" : "bf16", key.bt, p->ws, best, n, tbest, t0,
+            hipblaslt_ext::getKernelNameFromAlgo(h, p->algo).c_str());
+  return GRK_OK;
+}
+
+}  // namespace
+
+using namespace grk;
+
+extern "C" int grk_gemm(int trans_a, int trans_b, int64_t m, int64_t n, int64_t k, const void* a, int64_t lda,
+                        const void* b, int64_t ldb, int ab_dtype, void* c, int64_t ldc, int c_dtype, const void* c_in,
+                        float alpha, float beta, const void* bias, int bias_dtype, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(m >= 0 && n >= 0 && k >= 0, "negative GEMM size");
+  if (m == 0 || n == 0) return GRK_OK;
+  GRK_CHECK_ARG(a && b && c, "a, b and c are required");
+  GRK_CHECK_ARG(ab_dtype == GRK_BF16, "A and B must be bf16");
+  GRK_CHECK_ARG(c_dtype == GRK_BF16 || c_dtype == GRK_F32, "C must be bf16 or fp32");
+  GRK_CHECK_ARG(!bias || bias_dtype == GRK_BF16 || bias_dtype == GRK_F32, "bias must be bf16 or fp32");
+  GRK_CHECK_ARG(lda >= (trans_a ? m : k) && ldb >= (trans_b ? k : n) && ldc >= n, "leading dimension too small");
+  GRK_CHECK_ARG(k > 0 || beta == 1.0f || bias, "k == 0 needs beta == 1 or a bias");
+  int dev = 0;
+  GRK_CHECK_HIP(hipGetDevice(&dev));
+  hipStream_t s = (hipStream_t)stream;
+  std::lock_guard<std::mutex> lock(g_mu);
+  hipblasLtHandle_t h;
+  auto hi = g_handles.find(dev);
+  if (hi == g_handles.end()) {
+    GRK_CHECK_BLAS(hipblasLtCreate(&h));
+    g_handles[dev] = h;
+  } else {
+    h = hi->second;
+  }
+  void* ws;
+  auto wi = g_ws.find({dev, s});
+  if (wi == g_ws.end()) {  // one workspace per (device, stream): GEMMs on different streams never share it
+    GRK_CHECK_HIP(hipMalloc(&ws, kWorkspaceBytes));
+    g_ws[{dev, s}] = ws;
+  } else {
+    ws = wi->second;
+  }
+  const Key key{trans_a ? 1 : 0, trans_b ? 1 : 0, ab_dtype, c_dtype, bias ? bias_dtype : -1, dev,
+                m, n, k, lda, ldb, ldc};
+  auto pi = g_plans.find(key);
+  if (pi == g_plans.end()) {
+    Plan p;
+    const int rc = make_plan(h, key, bias != nullptr, &p, Operands{a, b, bias, ws, s});
+    if (rc) return rc;
+    pi = g_plans.emplace(key, p).first;
+  }
+  Plan& p = pi->second;
+  if (bias)
+    GRK_CHECK_BLAS(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
+  GRK_CHECK_BLAS(hipblasLtMatmul(h, p.op, &alpha, b, p.A, a, p.B, &beta, c_in ? c_in : c, p.C, c, p.C, &p.algo, ws,
+                                 kWorkspaceBytes, s));
+  return GRK_OK;
+}
+
+extern "C" int grk_gemm_tuning(int candidates) {
+  clear_error();
+  GRK_CHECK_ARG(candidates >= 1 && candidates <= 256, "candidates must be in [1, 256]");
+  std::lock_guard<std::mutex> lock(g_mu);
+  g_tune = candidates;
+  return GRK_OK;
+}

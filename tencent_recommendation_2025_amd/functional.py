@@ -132,6 +132,55 @@ def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extras
     return outs[0] if single else outs
 
 
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T + b on grk_gemm (hipBLASLt with stream-K eligible).  bf16
+    operands (the autocast dtype of the reference's training), fp32
+    accumulation; the weight gradient is written by the GEMM in the weight's
+    own dtype (fp32 master weights: no bf16 round trip and no cast kernel)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, addend):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        if x2.dtype != torch.bfloat16:
+            x2 = x2.to(torch.bfloat16)
+        if x2.stride(-1) != 1 or (x2.shape[0] > 1 and x2.stride(0) < x2.shape[1]):
+            x2 = x2.contiguous()
+        wb = weight if weight.dtype == torch.bfloat16 and weight.is_contiguous() else \
+            weight.detach().to(torch.bfloat16).contiguous()
+        if addend is not None:
+            addend = addend.reshape(-1, wb.shape[0])
+            if addend.dtype != torch.bfloat16 or addend.stride(1) != 1 or addend.stride(0) != wb.shape[0]:
+                addend = addend.to(torch.bfloat16).contiguous()
+        y = K.gemm(x2, wb, trans_b=True, bias=None if bias is None else bias.detach().contiguous(),
+                   addend=addend, beta=0.0 if addend is None else 1.0)
+        ctx.save_for_backward(x2, wb)
+        ctx.meta = (shp, weight.dtype, None if bias is None else bias.dtype, ctx.needs_input_grad[3])
+        return y.view(*shp[:-1], wb.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, wb = ctx.saved_tensors
+        shp, wdt, bdt, want_addend = ctx.meta
+        g2 = gy.reshape(-1, gy.shape[-1])
+        if g2.dtype != torch.bfloat16:
+            g2 = g2.to(torch.bfloat16)
+        if not g2.is_contiguous():
+            g2 = g2.contiguous()
+        dx = K.gemm(g2, wb).view(shp) if ctx.needs_input_grad[0] else None
+        dw = K.gemm(g2, x2, trans_a=True, out_dtype=torch.float32 if wdt == torch.float32 else torch.bfloat16) \
+            if ctx.needs_input_grad[1] else None
+        db = g2.sum(0, dtype=torch.float32).to(bdt) if ctx.needs_input_grad[2] else None
+        return dx, dw, db, (gy if want_addend else None)
+
+
+@_disable
+def linear(x, weight, bias=None, addend=None):
+    """torch.nn.functional.linear (+ addend, as torch.addmm) on grk_gemm:
+    bf16 operands, fp32 accumulation, bf16 output."""
+    return _LinearFn.apply(x, weight, bias, addend)
+
+
 class _GroupStackFn(torch.autograd.Function):
     """Equally-sized tables of a TableGroup as one [G, rows, D] tensor for use
     in differentiable torch ops (a view of the group buffer when the tables

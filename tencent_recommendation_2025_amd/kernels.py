@@ -302,6 +302,47 @@ def attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab=None, parts=L.AT
     L.check(rc, 'grk_attention_bwd')
 
 
+# ------------------------------------------------------------------ GEMM
+def gemm(a, b, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat16, alpha=1.0, beta=0.0, bias=None,
+         addend=None):
+    """grk_gemm (hipBLASLt): out[m, n] = alpha op(a) @ op(b) + beta C (+ bias[n]).
+
+    a, b bf16 row-major 2-D (op = transpose when trans_*); out bf16 or fp32.
+    C = ``addend`` (out's dtype and row stride) when given, else ``out``
+    itself (accumulate; an allocated out needs beta == 0 or an addend)."""
+    _require_cuda(a, b, out, bias)
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        raise L.GrkError('gemm operands must be bf16')
+    if a.dim() != 2 or b.dim() != 2 or a.stride(1) != 1 or b.stride(1) != 1:
+        raise L.GrkError('gemm operands must be row-major 2-D matrices')
+    m, k = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    kb, n = (b.shape[1], b.shape[0]) if trans_b else (b.shape[0], b.shape[1])
+    if kb != k:
+        raise L.GrkError(f'gemm inner dimensions differ: {k} vs {kb}')
+    if out is None:
+        if beta != 0.0 and addend is None:
+            raise L.GrkError('beta != 0 needs an output to accumulate into or an addend')
+        out = torch.empty(m, n, dtype=addend.dtype if addend is not None else out_dtype, device=a.device)
+    elif tuple(out.shape) != (m, n) or out.stride(1) != 1 or out.dtype not in (torch.bfloat16, torch.float32):
+        raise L.GrkError(f'gemm output must be a row-major bf16/fp32 [{m}, {n}] matrix')
+    if addend is not None and (tuple(addend.shape) != (m, n) or addend.dtype != out.dtype
+                               or addend.stride(1) != 1 or addend.stride(0) != out.stride(0)):
+        raise L.GrkError("addend must match the output's shape, dtype and row stride")
+    if bias is not None and (bias.numel() != n or not bias.is_contiguous()):
+        raise L.GrkError(f'bias must be a contiguous vector of {n}')
+    rc = L.lib().grk_gemm(int(trans_a), int(trans_b), m, n, k, a.data_ptr(), max(a.stride(0), 1), b.data_ptr(),
+                          max(b.stride(0), 1), L.dtype_code(a.dtype), out.data_ptr(), max(out.stride(0), 1),
+                          L.dtype_code(out.dtype), _ptr(addend), float(alpha), float(beta), _ptr(bias),
+                          L.dtype_code(bias.dtype) if bias is not None else 0, L.stream_ptr(a.device))
+    L.check(rc, 'grk_gemm')
+    return out
+
+
+def gemm_tuning(candidates):
+    """grk_gemm_tuning: hipBLASLt candidates timed per new GEMM shape (1 = heuristic pick, no timing)."""
+    L.check(L.lib().grk_gemm_tuning(int(candidates)), 'grk_gemm_tuning')
+
+
 # ------------------------------------------------------------- HSTU gate
 def _bf16_rows(t, name, dim):
     if t.dtype != torch.bfloat16 or t.dim() != 2 or t.stride(1) != 1 or t.stride(0) % 8 or t.shape[1] < dim:

@@ -233,3 +233,56 @@ def test_deferred_table_updates_are_bit_identical_to_dense(period):
     for name in runs[0][1]:
         for a, b in zip(runs[0][1][name], runs[1][1][name]):
             assert torch.equal(a, b), name
+
+
+def test_grk_gemm_shapes_and_accumulate():
+    """grk_gemm (hipBLASLt, row-major) against a torch fp32 reference of the
+    same bf16 operands: every transpose combination, bias, fp32 output
+    accumulated with beta = 1, a separate addend, and run-to-run determinism."""
+    from tencent_recommendation_2025_amd import kernels as K
+    g = torch.Generator(device=DEV).manual_seed(3)
+    m, n, k = 300, 136, 72
+    A = torch.randn(m, k, device=DEV, generator=g).bfloat16()
+    B = torch.randn(k, n, device=DEV, generator=g).bfloat16()
+    ref = A.float() @ B.float()
+    for ta in (False, True):
+        for tb in (False, True):
+            a = A.t().contiguous() if ta else A
+            b = B.t().contiguous() if tb else B
+            out = K.gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.float32)
+            torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
+            again = K.gemm(a, b, trans_a=ta, trans_b=tb, out_dtype=torch.float32)
+            assert torch.equal(out, again)
+    bias = torch.randn(n, device=DEV, generator=g)
+    y = K.gemm(A, B, bias=bias)
+    torch.testing.assert_close(y.float(), ref + bias, rtol=1e-2, atol=2e-2)
+    acc = torch.randn(m, n, device=DEV, generator=g)
+    want = acc + ref
+    K.gemm(A, B, out=acc, beta=1.0)
+    torch.testing.assert_close(acc, want, rtol=1e-5, atol=1e-4)
+    add = torch.randn(m, n, device=DEV, generator=g).bfloat16()
+    y = K.gemm(A, B, addend=add, beta=1.0)
+    torch.testing.assert_close(y.float(), ref + add.float(), rtol=1e-2, atol=2e-2)
+
+
+def test_grk_linear_matches_torch_linear():
+    """functional.linear (grk_gemm fwd / dX / dW, fp32 weight gradient) against
+    F.linear on the same bf16-rounded operands in fp32."""
+    from tencent_recommendation_2025_amd import functional as G
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn(4, 50, 96, device=DEV, generator=g).bfloat16().float().requires_grad_()
+    w = torch.randn(160, 96, device=DEV, generator=g).bfloat16().float().requires_grad_()
+    b = torch.randn(160, device=DEV, generator=g).requires_grad_()
+    add = torch.randn(4, 50, 160, device=DEV, generator=g).bfloat16()
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y = G.linear(x, w, b, addend=add)
+    gy = torch.randn_like(y.float()).bfloat16()
+    y.backward(gy)
+    x2, w2, b2 = (t.detach().clone().requires_grad_() for t in (x, w, b))
+    y2 = torch.nn.functional.linear(x2, w2, b2) + add.float()
+    y2.backward(gy.float())
+    assert y.dtype == torch.bfloat16 and w.grad.dtype == torch.float32
+    torch.testing.assert_close(y.float(), y2, rtol=1e-2, atol=3e-2)
+    torch.testing.assert_close(x.grad, x2.grad, rtol=1e-2, atol=3e-2)
+    torch.testing.assert_close(w.grad, w2.grad, rtol=1e-3, atol=2e-2)
+    torch.testing.assert_close(b.grad, b2.grad, rtol=1e-4, atol=1e-3)
