@@ -267,6 +267,24 @@ int grk_norm_gate_bwd(const void* gy, int64_t ldgy, const void* o, int64_t ldo, 
                       float dropout_p, uint64_t seed, void* dout, int64_t lddo, void* du, int64_t lddu,
                       float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream);
 
+/* Residual add + LayerNorm of the HSTU block's residual stream (replaces the
+ * `seqs = seqs + mha_outputs` / `attention_layernorms[i](seqs)` /
+ * `last_layernorm(log_feats)` pair of model/BaseLine/model.py:330-345 under
+ * bf16 autocast).  s, y, s_out bf16 [rows, dim]: s_out = bf16(s + y); with y
+ * NULL the LayerNorm reads s and s_out is not written.  x = LN(s_out) * gamma
+ * + beta (fp32 math) stored as x_dtype (bf16: the next GEMM's operand; fp32:
+ * the last norm); stats [rows, 2] = (mean, rstd). */
+int grk_add_norm_fwd(const void* s, int64_t lds, const void* y, int64_t ldy, const float* gamma, const float* beta,
+                     float eps, int64_t rows, int dim, void* s_out, int64_t ldso, void* x, int64_t ldx, int x_dtype,
+                     float* stats, void* stream);
+size_t grk_add_norm_bwd_workspace(int64_t rows, int dim);
+/* ds = gs + dL/ds_out through the LayerNorm for upstream gx (x_dtype) and the
+ * residual stream's own gradient gs (bf16, NULL = 0), rounded once to bf16
+ * (ds is the gradient of both s and y); dgamma/dbeta written, fixed-order. */
+int grk_add_norm_bwd(const void* gx, int64_t ldgx, int gx_dtype, const void* gs, int64_t ldgs, const void* s_new,
+                     int64_t lds, const float* gamma, const float* stats, int64_t rows, int dim, void* ds,
+                     int64_t ldds, float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------------
  * Pair logits + BCE (model/BaseLine/model.py:379-382; main.py:177-182)
  * ------------------------------------------------------------------------ */

@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Per-kernel register / LDS / occupancy table for one HIP source (gfx950).
 
-    python scripts/kernel_resources.py tencent_recommendation_2025_amd/csrc/grk_attention.hip [name-filter]
+    python scripts/kernel_resources.py tencent_recommendation_2025_amd/csrc/grk_attention.hip [name-filter] [hipcc flags...]
 """
 import re
 import subprocess
@@ -10,9 +10,10 @@ import tempfile
 
 src = sys.argv[1]
 filt = sys.argv[2] if len(sys.argv) > 2 else ''
+extra = sys.argv[3:]
 with tempfile.TemporaryDirectory() as d:
     r = subprocess.run(['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-Iinclude', '-x', 'hip',
-                        '-c', src, '-o', f'{d}/k.o', '-Rpass-analysis=kernel-resource-usage'],
+                        '-c', src, '-o', f'{d}/k.o', '-Rpass-analysis=kernel-resource-usage'] + extra,
                        capture_output=True, text=True)
 rows, cur = [], None
 for line in r.stderr.splitlines():

@@ -88,6 +88,9 @@ SIGNATURES = {
     'grk_norm_gate_bwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _P, _P, _I64, _I, _F, C.c_uint64, _P, _I64, _P,
                                _I64, _P, _P, _P, _SZ, _P]),
     'grk_seq_ranges': (_I, [_P, _I, _I, _P, _P]),
+    'grk_add_norm_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _P, _I64, _P, _I64, _I, _P, _P]),
+    'grk_add_norm_bwd_workspace': (_SZ, [_I64, _I]),
+    'grk_add_norm_bwd': (_I, [_P, _I64, _I, _P, _I64, _P, _I64, _P, _P, _I64, _I, _P, _I64, _P, _P, _P, _SZ, _P]),
     'grk_gemm_tuning': (_I, [_I]),
     'grk_gemm': (_I, [_I, _I, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _I, _P, _F, _F, _P, _I, _P]),
     'grk_pair_logits_partials': (_SZ, [_I64]),

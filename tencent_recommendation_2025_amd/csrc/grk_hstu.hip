@@ -240,6 +240,163 @@ __global__ void __launch_bounds__(64 * kColGroups) k_ng_colsum(NGParams p, int n
   }
 }
 
+// ------------------------------------------------- residual add + LayerNorm --
+// The HSTU block's residual stream (model/BaseLine/model.py:330-345 with the
+// HSTU block): s_{i+1} = s_i + y_i, x_{i+1} = LayerNorm_{i+1}(s_{i+1}), which
+// eager autocast runs as a bf16 add, an fp32 LayerNorm of the bf16 sum and a
+// cast of its output for the next GEMM (backward: LayerNorm input grad,
+// gamma/beta reductions, casts and a bf16 add of the two residual grads).
+// Forward: one wave per row, s_new = bf16(s + y) (y may be absent), x =
+// LN(s_new) g + b stored as bf16 or fp32, (mean, rstd) saved.  Backward:
+// ds = gs + rstd (gx g - mean(gx g) - zhat mean(gx g zhat)) rounded once to
+// bf16 (gs may be absent), dgamma/dbeta through fixed-order block partials.
+struct ANParams {
+  const bf16_t* s; int64_t lds;
+  const bf16_t* y; int64_t ldy;
+  const float* gamma; const float* beta;
+  float eps;
+  int64_t rows; int dim;
+  bf16_t* s_out; int64_t ldso;
+  void* x; int64_t ldx; int x_f32;
+  float* stats;
+  // backward
+  const void* gx; int64_t ldgx; int gx_f32;
+  const bf16_t* gs; int64_t ldgs;
+  bf16_t* ds; int64_t ldds;
+  float* partial;
+};
+
+__device__ __forceinline__ void load8_any(const void* base, int64_t off, bool f32, float* f) {
+  if (f32) load8f(reinterpret_cast<const float*>(base) + off, f);
+  else load8(reinterpret_cast<const bf16_t*>(base) + off, f);
+}
+
+template <int VPL>
+__global__ void __launch_bounds__(64 * kNgWaves) k_an_fwd(ANParams p) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kNgWaves + (threadIdx.x >> 6);
+  if (row >= p.rows) return;
+  const int nv = p.dim >> 3;
+  float v[VPL][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c >= nv) continue;
+    load8(p.s + row * p.lds + 8 * c, v[j]);
+    if (p.y) {
+      float t[8];
+      load8(p.y + row * p.ldy + 8 * c, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[j][e] = bf16_to_f32(f32_to_bf16(v[j][e] + t[e]));  // the bf16 residual sum
+      store8(p.s_out + row * p.ldso + 8 * c, v[j]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sum += v[j][e];
+  }
+  const float inv_d = 1.0f / (float)p.dim;
+  const float mean = wave_sum(sum) * inv_d;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j)
+    if (lane + 64 * j < nv)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = v[j][e] - mean;
+        q += d * d;
+      }
+  const float rstd = rsqrtf(wave_sum(q) * inv_d + p.eps);
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c >= nv) continue;
+    float g[8], b[8], x[8];
+    load8f(p.gamma + 8 * c, g);
+    load8f(p.beta + 8 * c, b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = (v[j][e] - mean) * rstd * g[e] + b[e];
+    if (p.x_f32) {
+      float* dst = reinterpret_cast<float*>(p.x) + row * p.ldx + 8 * c;
+      reinterpret_cast<float4*>(dst)[0] = make_float4(x[0], x[1], x[2], x[3]);
+      reinterpret_cast<float4*>(dst)[1] = make_float4(x[4], x[5], x[6], x[7]);
+    } else {
+      store8(reinterpret_cast<bf16_t*>(p.x) + row * p.ldx + 8 * c, x);
+    }
+  }
+  if (lane == 0) {
+    p.stats[2 * row] = mean;
+    p.stats[2 * row + 1] = rstd;
+  }
+}
+
+template <int VPL>
+__global__ void __launch_bounds__(64 * kNgWaves) k_an_bwd(ANParams p) {
+  __shared__ float red[2 * 64 * VPL * 8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nv = p.dim >> 3;
+  const float inv_d = 1.0f / (float)p.dim;
+  float dg[VPL][8], db[VPL][8], g[VPL][8];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { dg[j][e] = 0.f; db[j][e] = 0.f; g[j][e] = 0.f; }
+    if (c < nv) load8f(p.gamma + 8 * c, g[j]);
+  }
+  const int64_t stride = (int64_t)gridDim.x * kNgWaves;
+  for (int64_t row = (int64_t)blockIdx.x * kNgWaves + wave; row < p.rows; row += stride) {
+    const float mean = p.stats[2 * row], rstd = p.stats[2 * row + 1];
+    float zh[VPL][8], gzg[VPL][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c >= nv) continue;
+      float sv[8], gx[8];
+      load8(p.s + row * p.lds + 8 * c, sv);
+      load8_any(p.gx, row * p.ldgx + 8 * c, p.gx_f32, gx);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        zh[j][e] = (sv[e] - mean) * rstd;
+        dg[j][e] += gx[e] * zh[j][e];
+        db[j][e] += gx[e];
+        gzg[j][e] = gx[e] * g[j][e];
+        s1 += gzg[j][e];
+        s2 += gzg[j][e] * zh[j][e];
+      }
+    }
+    s1 = wave_sum(s1) * inv_d;
+    s2 = wave_sum(s2) * inv_d;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c >= nv) continue;
+      float d[8], gs[8];
+      if (p.gs) load8(p.gs + row * p.ldgs + 8 * c, gs);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = rstd * (gzg[j][e] - s1 - zh[j][e] * s2) + (p.gs ? gs[e] : 0.f);
+      store8(p.ds + row * p.ldds + 8 * c, d);
+    }
+  }
+  for (int w = 0; w < kNgWaves; ++w) {
+    if (wave == w)
+#pragma unroll
+      for (int j = 0; j < VPL; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int i = (lane + 64 * j) * 8 + e;
+          red[i] = (w == 0 ? 0.f : red[i]) + dg[j][e];
+          red[64 * VPL * 8 + i] = (w == 0 ? 0.f : red[64 * VPL * 8 + i]) + db[j][e];
+        }
+    __syncthreads();
+  }
+  float* part = p.partial + (int64_t)blockIdx.x * 2 * p.dim;
+  for (int i = threadIdx.x; i < p.dim; i += blockDim.x) {
+    part[i] = red[i];
+    part[p.dim + i] = red[64 * VPL * 8 + i];
+  }
+}
+
 static int ng_blocks_bwd(int64_t rows) {
   int64_t need = (rows + kNgWaves - 1) / kNgWaves;
   return (int)(need < kNgBwdBlocks ? (need < 1 ? 1 : need) : kNgBwdBlocks);
@@ -321,6 +478,75 @@ extern "C" int grk_norm_gate_bwd(const void* gy, int64_t ldgy, const void* o, in
     GRK_CHECK_HIP(hipMemsetAsync(ws, 0, grk_norm_gate_bwd_workspace(rows, dim), s));
   }
   k_ng_colsum<<<(2 * dim + 63) / 64, 64 * kColGroups, 0, s>>>(p, nb);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+extern "C" int grk_add_norm_fwd(const void* s, int64_t lds, const void* y, int64_t ldy, const float* gamma,
+                                const float* beta, float eps, int64_t rows, int dim, void* s_out, int64_t ldso,
+                                void* x, int64_t ldx, int x_dtype, float* stats, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(rows >= 0 && dim > 0 && dim % 8 == 0 && dim <= 2048, "dim must be a multiple of 8 in [8, 2048]");
+  if (rows == 0) return GRK_OK;
+  GRK_CHECK_ARG(s && gamma && beta && x && stats, "s / gamma / beta / x / stats required");
+  GRK_CHECK_ARG(!y || s_out, "y needs s_out (the residual sum)");
+  GRK_CHECK_ARG(x_dtype == GRK_BF16 || x_dtype == GRK_F32, "x must be bf16 or fp32");
+  GRK_CHECK_ARG(lds >= dim && lds % 8 == 0 && ldx >= dim && ldx % 8 == 0 && (!y || (ldy >= dim && ldy % 8 == 0 &&
+                ldso >= dim && ldso % 8 == 0)), "row strides must be >= dim and multiples of 8");
+  GRK_CHECK_ARG(((uintptr_t)s | (uintptr_t)y | (uintptr_t)s_out | (uintptr_t)x | (uintptr_t)gamma |
+                 (uintptr_t)beta) % 16 == 0, "operands must be 16-byte aligned");
+  ANParams p;
+  memset(&p, 0, sizeof(p));
+  p.s = (const bf16_t*)s; p.lds = lds; p.y = (const bf16_t*)y; p.ldy = ldy;
+  p.gamma = gamma; p.beta = beta; p.eps = eps; p.rows = rows; p.dim = dim;
+  p.s_out = (bf16_t*)s_out; p.ldso = ldso; p.x = x; p.ldx = ldx; p.x_f32 = x_dtype == GRK_F32; p.stats = stats;
+  const unsigned grid = (unsigned)((rows + kNgWaves - 1) / kNgWaves);
+  hipStream_t st = (hipStream_t)stream;
+  const int vpl = (dim / 8 + 63) / 64;
+  if (vpl == 1) k_an_fwd<1><<<grid, 64 * kNgWaves, 0, st>>>(p);
+  else if (vpl == 2) k_an_fwd<2><<<grid, 64 * kNgWaves, 0, st>>>(p);
+  else k_an_fwd<4><<<grid, 64 * kNgWaves, 0, st>>>(p);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+extern "C" size_t grk_add_norm_bwd_workspace(int64_t rows, int dim) { return grk_norm_gate_bwd_workspace(rows, dim); }
+
+extern "C" int grk_add_norm_bwd(const void* gx, int64_t ldgx, int gx_dtype, const void* gs, int64_t ldgs,
+                                const void* s_new, int64_t lds, const float* gamma, const float* stats, int64_t rows,
+                                int dim, void* ds, int64_t ldds, float* dgamma, float* dbeta, void* ws,
+                                size_t ws_bytes, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(rows >= 0 && dim > 0 && dim % 8 == 0 && dim <= 2048, "dim must be a multiple of 8 in [8, 2048]");
+  GRK_CHECK_ARG(gamma && dgamma && dbeta, "gamma / dgamma / dbeta required");
+  GRK_CHECK_ARG(ws && ws_bytes >= grk_add_norm_bwd_workspace(rows, dim), "workspace too small");
+  GRK_CHECK_ARG(gx_dtype == GRK_BF16 || gx_dtype == GRK_F32, "gx must be bf16 or fp32");
+  GRK_CHECK_ARG(rows == 0 || (gx && s_new && stats && ds), "gx / s_new / stats / ds required");
+  GRK_CHECK_ARG(ldgx >= dim && ldgx % 8 == 0 && lds >= dim && lds % 8 == 0 && ldds >= dim && ldds % 8 == 0 &&
+                (!gs || (ldgs >= dim && ldgs % 8 == 0)), "row strides must be >= dim and multiples of 8");
+  GRK_CHECK_ARG(((uintptr_t)gx | (uintptr_t)gs | (uintptr_t)s_new | (uintptr_t)ds | (uintptr_t)gamma) % 16 == 0,
+                "operands must be 16-byte aligned");
+  ANParams p;
+  memset(&p, 0, sizeof(p));
+  p.s = (const bf16_t*)s_new; p.lds = lds; p.gamma = gamma; p.rows = rows; p.dim = dim;
+  p.stats = const_cast<float*>(stats);
+  p.gx = gx; p.ldgx = ldgx; p.gx_f32 = gx_dtype == GRK_F32; p.gs = (const bf16_t*)gs; p.ldgs = ldgs;
+  p.ds = (bf16_t*)ds; p.ldds = ldds; p.partial = (float*)ws;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = ng_blocks_bwd(rows);
+  if (rows > 0) {
+    const int vpl = (dim / 8 + 63) / 64;
+    if (vpl == 1) k_an_bwd<1><<<nb, 64 * kNgWaves, 0, st>>>(p);
+    else if (vpl == 2) k_an_bwd<2><<<nb, 64 * kNgWaves, 0, st>>>(p);
+    else k_an_bwd<4><<<nb, 64 * kNgWaves, 0, st>>>(p);
+    GRK_LAUNCH_CHECK();
+  } else {
+    GRK_CHECK_HIP(hipMemsetAsync(ws, 0, grk_add_norm_bwd_workspace(rows, dim), st));
+  }
+  NGParams q;
+  memset(&q, 0, sizeof(q));
+  q.dim = dim; q.partial = (float*)ws; q.dgamma = dgamma; q.dbeta = dbeta;
+  k_ng_colsum<<<(2 * dim + 63) / 64, 64 * kColGroups, 0, st>>>(q, nb);
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }

@@ -181,6 +181,57 @@ def linear(x, weight, bias=None, addend=None):
     return _LinearFn.apply(x, weight, bias, addend)
 
 
+class _AddNormFn(torch.autograd.Function):
+    """HSTU residual stream step on grk_add_norm: s_new = bf16(s + y),
+    x = LayerNorm(s_new) (x_dtype).  Returns (s_new, x), or x alone when y is
+    None (the first block: LayerNorm of s)."""
+
+    @staticmethod
+    def forward(ctx, s, y, weight, bias, eps, x_dtype):
+        shp = s.shape
+        D = shp[-1]
+
+        def rows(t):
+            t = t.reshape(-1, D)
+            return t if t.dtype == torch.bfloat16 and t.stride(-1) == 1 and t.stride(0) % 8 == 0 \
+                else t.to(torch.bfloat16).contiguous()
+
+        s2 = rows(s)
+        y2 = rows(y) if y is not None else None
+        g32 = weight.detach().float().contiguous()
+        b32 = bias.detach().float().contiguous()
+        s_new, x, stats = K.add_norm_fwd(s2, y2, g32, b32, eps, x_dtype)
+        saved = s_new if s_new is not None else s2
+        ctx.save_for_backward(saved, stats, g32)
+        ctx.meta = (shp, y is not None, weight.dtype, bias.dtype, s.dtype, None if y is None else y.dtype)
+        if y is None:
+            return x.view(shp)
+        return s_new.view(shp), x.view(shp)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        saved, stats, g32 = ctx.saved_tensors
+        shp, has_y, wdt, bdt, sdt, ydt = ctx.meta
+        D = shp[-1]
+        gs, gx = (grads if has_y else (None, grads[0]))
+        gx = gx.reshape(-1, D)
+        if gx.stride(-1) != 1 or gx.stride(0) % 8:
+            gx = gx.contiguous()
+        if gs is not None:
+            gs = gs.reshape(-1, D)
+            if gs.dtype != torch.bfloat16 or gs.stride(-1) != 1 or gs.stride(0) % 8:
+                gs = gs.to(torch.bfloat16).contiguous()
+        ds, dg, db = K.add_norm_bwd(gx, gs, saved, g32, stats)
+        ds = ds.view(shp)
+        return (ds.to(sdt), ds.to(ydt) if has_y else None, dg.to(wdt), db.to(bdt), None, None)
+
+
+@_disable
+def add_norm(s, y, weight, bias, eps, x_dtype=torch.bfloat16):
+    """(s + y, LayerNorm(s + y)) with a bf16 residual stream (grk_add_norm); y None -> LayerNorm(s) only."""
+    return _AddNormFn.apply(s, y, weight, bias, float(eps), x_dtype)
+
+
 class _GroupStackFn(torch.autograd.Function):
     """Equally-sized tables of a TableGroup as one [G, rows, D] tensor for use
     in differentiable torch ops (a view of the group buffer when the tables

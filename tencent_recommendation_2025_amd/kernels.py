@@ -352,6 +352,50 @@ def _bf16_rows(t, name, dim):
     return t.data_ptr(), t.stride(0)
 
 
+def _mat_rows(t, name, dim, dtypes=(torch.bfloat16,)):
+    if t.dtype not in dtypes or t.dim() != 2 or t.stride(1) != 1 or t.stride(0) % 8 or t.shape[1] < dim:
+        raise L.GrkError(f'{name} must be a row-major [N, >={dim}] matrix of {dtypes} with row stride % 8 == 0')
+    return t.data_ptr(), t.stride(0)
+
+
+def add_norm_fwd(s, y, gamma, beta, eps, x_dtype=torch.bfloat16):
+    """grk_add_norm_fwd: s_new = bf16(s + y) (y may be None), x = LayerNorm(s_new) in x_dtype.
+
+    Returns (s_new or None, x, stats fp32 [N, 2])."""
+    _require_cuda(s, y, gamma, beta)
+    N, D = s.shape[0], gamma.shape[0]
+    dev = s.device
+    x = torch.empty(N, D, dtype=x_dtype, device=dev)
+    stats = torch.empty(N, 2, dtype=torch.float32, device=dev)
+    s_new = torch.empty(N, D, dtype=torch.bfloat16, device=dev) if y is not None else None
+    (sp, sl), (xp, xl) = _mat_rows(s, 's', D), _mat_rows(x, 'x', D, (torch.bfloat16, torch.float32))
+    yp, yl = _mat_rows(y, 'y', D) if y is not None else (None, 0)
+    op, ol = _mat_rows(s_new, 's_new', D) if s_new is not None else (None, 0)
+    rc = L.lib().grk_add_norm_fwd(sp, sl, yp, yl, gamma.data_ptr(), beta.data_ptr(), float(eps), N, D, op, ol, xp,
+                                  xl, L.dtype_code(x_dtype), stats.data_ptr(), L.stream_ptr(dev))
+    L.check(rc, 'grk_add_norm_fwd')
+    return s_new, x, stats
+
+
+def add_norm_bwd(gx, gs, s_new, gamma, stats):
+    """Gradients of add_norm_fwd: (ds bf16 [N, D] -- for both s and y --, dgamma, dbeta fp32)."""
+    _require_cuda(gx, gs, s_new, gamma, stats)
+    N, D = s_new.shape[0], gamma.shape[0]
+    dev = s_new.device
+    ds = torch.empty(N, D, dtype=torch.bfloat16, device=dev)
+    dgamma = torch.empty(D, dtype=torch.float32, device=dev)
+    dbeta = torch.empty(D, dtype=torch.float32, device=dev)
+    ws = torch.empty(max(L.lib().grk_add_norm_bwd_workspace(N, D), 4), dtype=torch.uint8, device=dev)
+    (gxp, gxl), (sp, sl), (dp, dl) = (_mat_rows(gx, 'gx', D, (torch.bfloat16, torch.float32)), _mat_rows(s_new, 's_new', D),
+                                      _mat_rows(ds, 'ds', D))
+    gsp, gsl = _mat_rows(gs, 'gs', D) if gs is not None else (None, 0)
+    rc = L.lib().grk_add_norm_bwd(gxp, gxl, L.dtype_code(gx.dtype), gsp, gsl, sp, sl, gamma.data_ptr(),
+                                  stats.data_ptr(), N, D, dp, dl, dgamma.data_ptr(), dbeta.data_ptr(), ws.data_ptr(),
+                                  ws.numel(), L.stream_ptr(dev))
+    L.check(rc, 'grk_add_norm_bwd')
+    return ds, dgamma, dbeta
+
+
 def norm_gate_fwd(o, u, gamma, beta, eps, dropout_p=0.0, seed=0, y=None):
     """y = dropout(LayerNorm(o) * SiLU(u)) (grk_norm_gate_fwd).  Returns (y bf16 [N, D], stats fp32 [N, 2])."""
     _require_cuda(o, u, gamma, beta)

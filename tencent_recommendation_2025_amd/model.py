@@ -470,6 +470,21 @@ class BaselineModel(torch.nn.Module):
         seqs = self.emb_dropout(seqs)
         key_valid = (mask.to(dev, non_blocking=True) != 0).to(torch.uint8).contiguous()
         kw = dict(key_valid=key_valid, seq_range=K.seq_ranges(key_valid))  # one launch serves every layer
+        if self.block == 'hstu' and _grk_gemm_ok(seqs) and self.hidden_units % 8 == 0:
+            # bf16 residual stream: each residual add is fused into the next LayerNorm
+            # (grk_add_norm), the last one into last_layernorm (fp32 output, as autocast's)
+            y = None
+            for i in range(len(self.attention_layers)):
+                ln = self.attention_layernorms[i]
+                if y is None:
+                    x = G.add_norm(seqs, None, ln.weight, ln.bias, ln.eps)
+                else:
+                    seqs, x = G.add_norm(seqs, y, ln.weight, ln.bias, ln.eps)
+                y, _ = self.attention_layers[i](x, **kw)
+            ln = self.last_layernorm
+            if y is None:
+                return G.add_norm(seqs, None, ln.weight, ln.bias, ln.eps, x_dtype=torch.float32)
+            return G.add_norm(seqs, y, ln.weight, ln.bias, ln.eps, x_dtype=torch.float32)[1]
         for i in range(len(self.attention_layers)):
             if self.block == 'hstu':
                 y, _ = self.attention_layers[i](self.attention_layernorms[i](seqs), **kw)

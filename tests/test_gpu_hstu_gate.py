@@ -134,3 +134,41 @@ def test_hstu_core_matches_unfused_torch(K):
     assert nrel(y.detach(), yr.detach()) < 2e-2
     for name, a_, b_ in zip(('dpre', 'drab', 'dgamma', 'dbeta'), grads, rg):
         assert nrel(a_, b_) < 2e-2, name
+
+
+@pytest.mark.parametrize('with_y', [False, True])
+@pytest.mark.parametrize('x_dtype', [torch.bfloat16, torch.float32])
+def test_add_norm_matches_torch(with_y, x_dtype):
+    """functional.add_norm (grk_add_norm fwd/bwd) against the eager autocast
+    composition it replaces: s_new = bf16(s + y); x = LayerNorm(s_new) in fp32;
+    gradients of s, y, gamma, beta in fp32."""
+    from tencent_recommendation_2025_amd import functional as G
+    g = torch.Generator(device='cuda').manual_seed(8)
+    N, D = 333, 512
+    s = torch.randn(N, D, device='cuda', generator=g).bfloat16().requires_grad_()
+    y = torch.randn(N, D, device='cuda', generator=g).bfloat16().requires_grad_() if with_y else None
+    w = (1 + 0.1 * torch.randn(D, device='cuda', generator=g)).requires_grad_()
+    b = (0.1 * torch.randn(D, device='cuda', generator=g)).requires_grad_()
+    out = G.add_norm(s, y, w, b, 1e-8, x_dtype=x_dtype)
+    s_new, x = out if with_y else (None, out)
+    gx = torch.randn(N, D, device='cuda', generator=g).to(x_dtype)
+    gs = torch.randn(N, D, device='cuda', generator=g).bfloat16() if with_y else None
+    torch.autograd.backward([x] + ([s_new] if with_y else []), [gx] + ([gs] if with_y else []))
+    # reference: fp32 math on the same bf16 values
+    s2 = s.detach().float().requires_grad_()
+    y2 = y.detach().float().requires_grad_() if with_y else None
+    w2, b2 = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    sn = (s2 + y2) if with_y else s2
+    if with_y:  # autocast adds in bf16: the LayerNorm sees the rounded sum (straight-through gradient)
+        sn = sn + (sn.bfloat16().float() - sn).detach()
+    x2 = torch.nn.functional.layer_norm(sn, (D,), w2, b2, 1e-8)
+    torch.autograd.backward([x2] + ([sn] if with_y else []), [gx.float()] + ([gs.float()] if with_y else []))
+    if with_y:
+        assert torch.equal(s_new, (s.detach().float() + y.detach().float()).bfloat16())
+    tol = dict(rtol=2e-2, atol=2e-2) if x_dtype == torch.bfloat16 else dict(rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(x.float(), x2.detach(), **tol)
+    torch.testing.assert_close(s.grad.float(), s2.grad, rtol=2e-2, atol=3e-2)
+    if with_y:
+        torch.testing.assert_close(y.grad.float(), y2.grad, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(w.grad, w2.grad, rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(b.grad, b2.grad, rtol=1e-3, atol=1e-2)
