@@ -249,6 +249,8 @@ def main():
     torch.cuda.set_device(dev)
     sharded = (world > 1) if a.sharded is None else bool(a.sharded)
     if world > 1 or sharded:
+        for k, v in (('RANK', '0'), ('WORLD_SIZE', '1'), ('MASTER_ADDR', '127.0.0.1'), ('MASTER_PORT', '29533')):
+            os.environ.setdefault(k, v)      # --sharded 1 without a launcher: a world of one
         if a.backend == 'nccl':
             dist.init_process_group('nccl', device_id=dev)
         else:

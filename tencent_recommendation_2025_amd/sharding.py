@@ -124,11 +124,16 @@ class ShardExchange:
         return dict(uniq=uniq, inverse=inverse, order=order, send_ids=send_ids, send_counts=send_counts,
                     recv_counts=recv_counts)
 
-    def fetch(self, r, send_split, recv_split):
-        """Phase 2: ids to owners, owners gather, rows back; returns rows in uniq order."""
+    def fetch(self, r, send_split, recv_split, before_gather=None):
+        """Phase 2: ids to owners, owners gather, rows back; returns rows in uniq order.
+
+        before_gather(local ids) runs on the owner before its gather (the
+        deferred-AdamW catch-up of the requested rows)."""
         recv_ids = r['send_ids'].new_empty(sum(recv_split))
         a2a(recv_ids, r['send_ids'], recv_split, send_split, self.pg)
         local = recv_ids // self.world
+        if before_gather is not None and local.numel():
+            before_gather(local)
         rows = self.gather_fn(self.shard, local)
         back = rows.new_empty((len(r['uniq']), self.dim))
         a2a(back, rows, send_split, recv_split, self.pg)
@@ -151,15 +156,99 @@ def shard_rows(full_rows, world, rank):
     return (full_rows - rank + world - 1) // world
 
 
+# ------------------------------------------------------ DP gradient sync ----
+class GradBuckets:
+    """Dense-parameter gradients averaged over ranks while backward still runs.
+
+    Parameters are bucketed in reverse registration order (the order autograd
+    finishes their gradients); a bucket's ``all_reduce`` is issued from a
+    post-accumulate-grad hook as soon as it and every earlier bucket are
+    complete, so the launch order is the same on every rank and RCCL overlaps
+    the reduction with the rest of backward.  ``finish()`` (in the optimizer
+    step) issues what is left (parameters without a gradient this step count
+    as zero on this rank), waits, and writes the means back into ``p.grad``."""
+
+    def __init__(self, params, pg=None, bucket_bytes=32 << 20):
+        self.pg = pg
+        self.world = dist.get_world_size(pg)
+        self.params = list(params)
+        self.buckets, cur, size = [], [], 0
+        for p in reversed(self.params):
+            cur.append(p)
+            size += p.numel() * 4
+            if size >= bucket_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.where = {id(p): b for b, ps in enumerate(self.buckets) for p in ps}
+        dev = self.params[0].device if self.params else torch.device('cpu')
+        self.flat = [torch.empty(sum(p.numel() for p in ps), dtype=torch.float32, device=dev) for ps in self.buckets]
+        self.async_ok = dev.type == 'cuda' and dist.get_backend(pg) != 'gloo'
+        self._reset()
+        for p in self.params:
+            p.register_post_accumulate_grad_hook(self._hook)
+
+    def _reset(self):
+        self.ready = [0] * len(self.buckets)
+        self.works = [None] * len(self.buckets)
+        self.next = 0
+
+    def _hook(self, p):
+        b = self.where[id(p)]
+        self.ready[b] += 1
+        while self.next < len(self.buckets) and self.ready[self.next] == len(self.buckets[self.next]):
+            self._launch(self.next)
+            self.next += 1
+
+    def _launch(self, b):
+        flat, off = self.flat[b], 0
+        for p in self.buckets[b]:
+            n = p.numel()
+            if p.grad is None:
+                flat[off:off + n].zero_()
+            else:
+                flat[off:off + n].copy_(p.grad.reshape(-1))
+            off += n
+        if self.async_ok:
+            self.works[b] = dist.all_reduce(flat, group=self.pg, async_op=True)
+        else:
+            all_reduce(flat, self.pg)
+
+    def finish(self):
+        while self.next < len(self.buckets):
+            self._launch(self.next)
+            self.next += 1
+        inv = 1.0 / self.world
+        for b, ps in enumerate(self.buckets):
+            if self.works[b] is not None:
+                self.works[b].wait()
+            flat, off = self.flat[b].mul_(inv), 0
+            for p in ps:
+                n = p.numel()
+                if p.grad is None:
+                    p.grad = torch.empty_like(p)
+                p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                off += n
+        self._reset()
+
+
 # ------------------------------------------------------------ optimizer ----
 class ShardedFusedAdamW(FusedAdamW):
-    """FusedAdamW across ranks: sharded item/user tables, replicated small tables, DP dense params."""
+    """FusedAdamW across ranks: sharded item/user tables, replicated small tables, DP dense params.
+
+    Sharded tables keep dense parity the deferred way (optim.FusedAdamW): an
+    owner brings the rows it is asked for up to the current step inside
+    ``prepare`` (catch-up replay) before gathering them, updates the rows it
+    receives gradients for after backward (lazy update + step stamp), and the
+    rows nobody asked for stay deferred until the segment flush -- every
+    ``defer_period`` steps, or before ``state_dict``."""
 
     SHARDED = ('item_emb', 'user_emb')
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
                  table_dtype=torch.bfloat16, pg=None, gather_fn=kernel_gather, reduce_fn=kernel_reduce,
-                 dense_reduce_fn=kernel_dense_reduce):
+                 dense_reduce_fn=kernel_dense_reduce, defer_period=16, bucket_bytes=32 << 20):
         self.pg = pg
         self.world = dist.get_world_size(pg)
         self.rank = dist.get_rank(pg)
@@ -181,11 +270,26 @@ class ShardedFusedAdamW(FusedAdamW):
             sharded_refs[name] = ShardedRef(name, emb.weight)
         small_keys = tuple(k for k in tables if k not in self.SHARDED)
         super().__init__(model, lr, betas, eps, weight_decay, table_mode, table_dtype,
-                         groups=(('small', small_keys),))
+                         groups=(('small', small_keys),), defer_period=defer_period)
         model._table_refs.update(sharded_refs)
         self.small = self.groups[0]
         self.small_identity = torch.arange(self.small.rows, dtype=torch.int32, device=dev)
         self.sinks = {}
+        # the shards are the deferred groups (FusedAdamW machinery: ring, segments, flush)
+        if self.defer:
+            self._deferred = {name: grp for name, (grp, _) in self.shards.items()}
+            for g in self._deferred.values():
+                g.last = torch.zeros(g.rows, dtype=torch.int32, device=dev)
+        params = [p for grp in self.dense.param_groups for p in grp['params']]
+        self.buckets = GradBuckets(params, pg, bucket_bytes) if params else None
+
+    def begin_step(self, batch):
+        """Nothing: prepare() catches up the rows each owner is asked for."""
+
+    def shard_table(self, name):
+        """(rows held by this rank, brought to the current step) -- global rows rank::world."""
+        self.flush()
+        return self.shards[name][0].flat
 
     # -- input dist -------------------------------------------------------
     def prepare(self, batch):
@@ -203,12 +307,19 @@ class ShardedFusedAdamW(FusedAdamW):
             routed[name] = self.shards[name][1].route(ids)
         counts = torch.stack([torch.stack([routed[n]['send_counts'], routed[n]['recv_counts']]) for n in parts])
         counts = counts.cpu().tolist()  # the one host sync of the step: all-to-all split sizes
+        if self.defer and (self._seg is None or self.t - self._seg >= self.defer):
+            self._segment(self.t)
         remaps = {}
         self.sinks = {}
         for gi, (name, plist) in enumerate(parts.items()):
             grp, ex = self.shards[name]
             r = routed[name]
-            fetched = ex.fetch(r, counts[gi][0], counts[gi][1])
+            catchup = None
+            if self.defer:
+                def catchup(local, grp=grp):
+                    K.table_adamw_catchup(grp.flat, grp.exp_avg, grp.exp_avg_sq, grp.last, self._ring, self.t,
+                                          local.contiguous())
+            fetched = ex.fetch(r, counts[gi][0], counts[gi][1], before_gather=catchup)
             sink = FetchSink()
             self.sinks[name] = sink
             ref = G.TableRef(fetched, sink, 0)
@@ -219,26 +330,19 @@ class ShardedFusedAdamW(FusedAdamW):
                 off += n
                 remaps[(name, idx.data_ptr(), mode)] = (ref, inv)
         self.model._remaps = remaps
+        self._begun = self.t
 
     # -- gradient sync + update -------------------------------------------
     @torch.no_grad()
     def step(self):
+        if self._deferred and self._begun != self.t:
+            raise RuntimeError('ShardedFusedAdamW: call prepare(batch) before forward (Trainer.step does)')
+        self._begun = None
         self.t += 1
         hp = K.adamw_hparams(self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, self.t)
         inv_world = 1.0 / self.world
-        # dense parameters: one flat all-reduce (mean)
-        params = [p for grp in self.dense.param_groups for p in grp['params'] if p.grad is not None]
-        if params:
-            flat = torch.cat([p.grad.reshape(-1).float() for p in params])
-            all_reduce(flat, self.pg)
-            flat.mul_(inv_world)
-            off = 0
-            for p in params:
-                n = p.grad.numel()
-                p.grad.copy_(flat[off:off + n].view_as(p.grad))
-                off += n
-        self.dense.step()
-        # replicated small tables: dense fp32 gradient, all-reduce (mean), dense AdamW
+        # replicated small tables: dense fp32 gradient, all-reduce (mean) issued first, so
+        # it runs on RCCL's stream under the dense and shard updates below
         g = self.small
         if g.pending:
             dense = self.dense_reduce_fn(g.pending, g.rows, g.dim, g.token_type, g.seq_len)
@@ -246,24 +350,39 @@ class ShardedFusedAdamW(FusedAdamW):
             dense = torch.zeros(g.rows, g.dim, dtype=torch.float32, device=g.flat.device)
         for off, dg in g.dense_grads.items():
             dense[off:off + dg.shape[0]] += dg
-        all_reduce(dense, self.pg)
-        dense.mul_(inv_world)
-        K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, None, dense, None, 0, self.small_identity)
-        g.clear()
+        small_work = None
+        if self.world > 1:
+            if dense.is_cuda and dist.get_backend(self.pg) != 'gloo':
+                small_work = dist.all_reduce(dense, group=self.pg, async_op=True)
+            else:
+                all_reduce(dense, self.pg)
         # sharded tables: per-unique-id grads -> owners -> owner reduction -> shard AdamW
         for name, (grp, ex) in self.shards.items():
             sink = self.sinks.get(name)
             if sink is not None and sink.sources and ex.plan is not None:
                 ug = self.dense_reduce_fn(sink.sources, ex.plan['n_uniq'], grp.dim, padding_idx=None)
-                ug.mul_(inv_world)
+                if self.world > 1:
+                    ug.mul_(inv_world)
                 local, rows = ex.push_grads(ug)
                 src = [K.GradSource(local, rows, 0)]
                 res = self.reduce_fn(src, grp.rows, grp.dim, 0 if self.rank == 0 else -1,
                                      None if self.lazy else grp.row_slot)
                 K.table_adamw(grp.flat, grp.exp_avg, grp.exp_avg_sq, hp, res.ids, res.rows, res.count, res.capacity,
-                              None if self.lazy else grp.row_slot, lazy=self.lazy)
-            elif not self.lazy:
+                              None if self.lazy else grp.row_slot, lazy=self.lazy or bool(self.defer))
+                if self.defer:
+                    K.stamp_rows(grp.last, res.ids, res.count, res.capacity, self.t)
+            elif not self.lazy and not self.defer:
                 K.table_adamw(grp.flat, grp.exp_avg, grp.exp_avg_sq, hp)
+        # dense parameters: buckets were all-reduced during backward
+        if self.buckets is not None:
+            self.buckets.finish()
+        self.dense.step()
+        if small_work is not None:
+            small_work.wait()
+        if self.world > 1:
+            dense.mul_(inv_world)
+        K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, None, dense, None, 0, self.small_identity)
+        g.clear()
         self.sinks = {}
         self.model._remaps = None
 

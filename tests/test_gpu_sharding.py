@@ -45,10 +45,10 @@ def test_sharded_optimizer_world1_equals_fused(pg):
     from tencent_recommendation_2025_amd.train import Trainer
     m1, cfg = build()
     m2, _ = build()
-    t1 = Trainer(m1, FusedAdamW(m1, lr=2e-3, table_dtype=torch.float32), loss='bce', amp_dtype=None)
-    t2 = Trainer(m2, ShardedFusedAdamW(m2, lr=2e-3, table_dtype=torch.float32), loss='bce', amp_dtype=None)
+    t1 = Trainer(m1, FusedAdamW(m1, lr=2e-3, table_dtype=torch.float32, defer_period=2), loss='bce', amp_dtype=None)
+    t2 = Trainer(m2, ShardedFusedAdamW(m2, lr=2e-3, table_dtype=torch.float32, defer_period=2), loss='bce', amp_dtype=None)
     g = torch.Generator(device=DEV).manual_seed(0)
-    batches = [S.make_batch(cfg, g, DEV) for _ in range(3)]
+    batches = [S.make_batch(cfg, g, DEV) for _ in range(5)]
     for b in batches:
         l1 = t1.step(b)
         l2 = t2.step(b)
@@ -58,5 +58,9 @@ def test_sharded_optimizer_world1_equals_fused(pg):
         if k in ('item_emb.weight', 'user_emb.weight'):
             continue  # held as shards by the sharded optimizer
         torch.testing.assert_close(s1[k].float(), s2[k].float(), rtol=1e-3, atol=2e-5, msg=k)
+    # the shards (deferred rows flushed) == the fused optimizer's full tables at G = 1
+    for k in ('item_emb', 'user_emb'):
+        torch.testing.assert_close(t2.opt.shard_table(k).float(), s1[f'{k}.weight'].float(), rtol=1e-3, atol=2e-5,
+                                   msg=k)
     grp, _ = t2.opt.shards['item_emb']
     torch.testing.assert_close(grp.flat.float(), t1.opt.groups[0].flat.float(), rtol=1e-3, atol=2e-5)
