@@ -57,6 +57,8 @@ def parse():
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='gloo: rehearse N ranks on fewer GPUs (collectives staged via host)')
     ap.add_argument('--sharded', type=int, default=None, help='force the row-sharded optimizer (default: N > 1)')
+    ap.add_argument('--graph', type=int, default=1,
+                    help='capture the training step in a HIP graph and replay it (unsharded path)')
     return ap.parse_args()
 
 
@@ -274,15 +276,17 @@ def main():
         opt = ShardedFusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
     else:
         opt = FusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
-    trainer = Trainer(model, opt, loss=a.loss)
+    trainer = Trainer(model, opt, loss=a.loss, graph=bool(a.graph) and not sharded)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [S.make_batch(cfg, gen, dev) for _ in range(4)]
 
+    trace = None
     for i in range(a.warmup):
-        if i == a.warmup - 1:
-            G.GATHER_TRACE = []          # capture the fused-gather launches of one real step
+        if i == 0:
+            G.GATHER_TRACE = []          # record the fused-gather launches of one real (eager) step
         trainer.step(pool[i % len(pool)])
-    trace, G.GATHER_TRACE = G.GATHER_TRACE, None
+        if i == 0:
+            trace, G.GATHER_TRACE = G.GATHER_TRACE, None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -299,9 +303,9 @@ def main():
     elapsed = float(t.item())
     final_loss = float(loss.float().item())
 
-    if not trace:  # --warmup 0: trace one extra, untimed step after the timed region
+    if not trace:  # --warmup 0: trace one extra, untimed eager step after the timed region
         G.GATHER_TRACE = []
-        trainer.step(pool[0])
+        trainer.eager_step(pool[0])
         trace, G.GATHER_TRACE = G.GATHER_TRACE, None
     kv = (pool[0][3] != 0).to(torch.uint8)        # the first bench batch's key validity (token_type != 0)
     roof, more = attention_rooflines(a, kv, a.roofline_reps)
@@ -322,7 +326,8 @@ def main():
                                    f'({a.blocks} blocks x {a.heads} heads), {a.items}-item bf16 table, '
                                    f'{a.users} users, loss={a.loss}, table AdamW={a.table_mode}',
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch, 'seq_len': a.maxlen + 1,
-                       'parallelism': f'dp{world}' + ('+rowshard' if sharded else '')},
+                       'parallelism': f'dp{world}' + ('+rowshard' if sharded else ''),
+                       'step_launch': 'hip-graph replay' if trainer.graph else 'eager'},
             'final_loss': round(final_loss, 5),
             'roofline': roof,
             'rooflines': more,

@@ -174,6 +174,26 @@ int grk_table_adamw_catchup(void* param, int param_dtype, float* exp_avg, float*
 int grk_stamp_rows(int32_t* last, const int64_t* uniq_ids, const int32_t* uniq_count, int64_t max_uniq, int32_t t,
                    void* stream);
 
+/* Device-clock forms of the four calls above, for a training step captured
+ * once in a HIP graph and replayed (train.Trainer graph mode): the step t is
+ * read at kernel time from *t_dev (int32 in device memory, advanced inside
+ * the graph) and the hyper-parameters from hp_ring[t % ring_len] (filled by
+ * the caller ahead of the steps that use them).  Same arithmetic, same
+ * semantics as the by-value forms with t = *t_dev and hp = hp_ring[t % ring_len]. */
+int grk_table_adamw_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows, int dim,
+                        const int64_t* uniq_ids, const float* uniq_rows, const int32_t* uniq_count, int64_t max_uniq,
+                        int32_t* row_slot, const grk_adamw_hparams* hp_ring, int32_t ring_len, const int32_t* t_dev,
+                        int mode, void* stream);
+int grk_table_adamw_dense_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows,
+                              int dim, const void* grad, int grad_dtype, int64_t grad_ld,
+                              const grk_adamw_hparams* hp_ring, int32_t ring_len, const int32_t* t_dev, void* stream);
+int grk_table_adamw_catchup_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows,
+                                int dim, int32_t* last, const int64_t* ids, int64_t num_ids,
+                                const grk_adamw_hparams* hp_ring, int32_t ring_len, const int32_t* t_dev,
+                                void* stream);
+int grk_stamp_rows_dev(int32_t* last, const int64_t* uniq_ids, const int32_t* uniq_count, int64_t max_uniq,
+                       const int32_t* t_dev, void* stream);
+
 /* ------------------------------------------------------------------------
  * Causal attention (MFMA 32x32x16 bf16)
  *   GRK_ATTN_SOFTMAX: softmax(scale * QK^T + mask) V with dropout -- the

@@ -78,6 +78,10 @@ SIGNATURES = {
     'grk_table_adamw_dense': (_I, [_P, _I, _P, _P, _I64, _I, _P, _I, _I64, GrkAdamwHparams, _P]),
     'grk_table_adamw_catchup': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _I64, _P, C.c_int32, C.c_int32, _P]),
     'grk_stamp_rows': (_I, [_P, _P, _P, _I64, C.c_int32, _P]),
+    'grk_table_adamw_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _P, _I64, _P, _P, C.c_int32, _P, _I, _P]),
+    'grk_table_adamw_dense_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _I, _I64, _P, C.c_int32, _P, _P]),
+    'grk_table_adamw_catchup_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _I64, _P, C.c_int32, _P, _P]),
+    'grk_stamp_rows_dev': (_I, [_P, _P, _P, _I64, _P, _P]),
     'grk_attention_fwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _P]),
     'grk_attention_bwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64, _P, _I64,
                                _P, _P, _P]),

@@ -503,7 +503,7 @@ extern "C" int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, 
   hipStream_t s = (hipStream_t)stream;
   if (do_dq) {
     const int nfix = a->heads * a->num_buckets;
-    if (p.drab) GRK_CHECK_HIP(hipMemsetAsync(drab_ws, 0, (size_t)nfix * 8, s));
+    if (p.drab) GRK_CHECK_HIP(zero_async(drab_ws, (size_t)nfix * 8, s));
     if (a->kind == GRK_ATTN_SOFTMAX) {
       // out dtype of the forward output equals out_dtype of these args
       rc = launch(p, a->head_dim, 1, s);

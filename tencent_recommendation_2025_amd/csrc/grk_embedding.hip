@@ -676,8 +676,8 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
   plan_ws(total, num_rows, dim, base, &ws);
   hipStream_t s = (hipStream_t)stream;
-  GRK_CHECK_HIP(hipMemsetAsync(uniq_count, 0, sizeof(int32_t), s));
-  if (dense_out) GRK_CHECK_HIP(hipMemsetAsync(dense_out, 0, (size_t)num_rows * dim * sizeof(float), s));
+  GRK_CHECK_HIP(zero_async(uniq_count, sizeof(int32_t), s));
+  if (dense_out) GRK_CHECK_HIP(zero_async(dense_out, (size_t)num_rows * dim * sizeof(float), s));
   if (total == 0) return GRK_OK;
   const int B = 256;
   const int esize = grad_dtype == GRK_F32 ? 4 : 2;

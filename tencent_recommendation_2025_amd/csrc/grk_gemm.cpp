@@ -87,6 +87,7 @@ struct Operands {  // the first call's operands, for timing candidate algorithms
   const void *a, *b, *bias;
   void* ws;
   hipStream_t s;
+  bool capturing;
 };
 
 // Average time of `reps` launches of one algorithm into a scratch output (never the caller's C).
@@ -150,7 +151,7 @@ int make_plan(hipblasLtHandle_t h, const Key& key, bool has_bias, Plan* p, const
   }
   int best = 0;
   float t0 = -1.f, tbest = -1.f;
-  if (n > 1) {
+  if (n > 1 && !o.capturing) {  // no timing inside a HIP graph capture: the heuristic's first choice
     void* scratch = nullptr;
     const size_t cbytes = (size_t)key.ldc * key.m * (key.ct == GRK_F32 ? 4 : 2);
     if (hipMalloc(&scratch, cbytes) == hipSuccess) {
@@ -197,6 +198,9 @@ extern "C" int grk_gemm(int trans_a, int trans_b, int64_t m, int64_t n, int64_t 
   int dev = 0;
   GRK_CHECK_HIP(hipGetDevice(&dev));
   hipStream_t s = (hipStream_t)stream;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  GRK_CHECK_HIP(hipStreamIsCapturing(s, &cap));
+  const bool capturing = cap != hipStreamCaptureStatusNone;
   std::lock_guard<std::mutex> lock(g_mu);
   hipblasLtHandle_t h;
   auto hi = g_handles.find(dev);
@@ -209,6 +213,7 @@ extern "C" int grk_gemm(int trans_a, int trans_b, int64_t m, int64_t n, int64_t 
   void* ws;
   auto wi = g_ws.find({dev, s});
   if (wi == g_ws.end()) {  // one workspace per (device, stream): GEMMs on different streams never share it
+    GRK_CHECK_ARG(!capturing, "grk_gemm: first use of a stream inside a graph capture (run one eager step on it first)");
     GRK_CHECK_HIP(hipMalloc(&ws, kWorkspaceBytes));
     g_ws[{dev, s}] = ws;
   } else {
@@ -219,7 +224,7 @@ extern "C" int grk_gemm(int trans_a, int trans_b, int64_t m, int64_t n, int64_t 
   auto pi = g_plans.find(key);
   if (pi == g_plans.end()) {
     Plan p;
-    const int rc = make_plan(h, key, bias != nullptr, &p, Operands{a, b, bias, ws, s});
+    const int rc = make_plan(h, key, bias != nullptr, &p, Operands{a, b, bias, ws, s, capturing});
     if (rc) return rc;
     pi = g_plans.emplace(key, p).first;
   }

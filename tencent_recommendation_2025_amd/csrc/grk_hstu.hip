@@ -475,7 +475,7 @@ extern "C" int grk_norm_gate_bwd(const void* gy, int64_t ldgy, const void* o, in
     else k_ng_bwd<4><<<nb, 64 * kNgWaves, 0, s>>>(p);
     GRK_LAUNCH_CHECK();
   } else {
-    GRK_CHECK_HIP(hipMemsetAsync(ws, 0, grk_norm_gate_bwd_workspace(rows, dim), s));
+    GRK_CHECK_HIP(zero_async(ws, grk_norm_gate_bwd_workspace(rows, dim), s));
   }
   k_ng_colsum<<<(2 * dim + 63) / 64, 64 * kColGroups, 0, s>>>(p, nb);
   GRK_LAUNCH_CHECK();
@@ -541,7 +541,7 @@ extern "C" int grk_add_norm_bwd(const void* gx, int64_t ldgx, int gx_dtype, cons
     else k_an_bwd<4><<<nb, 64 * kNgWaves, 0, st>>>(p);
     GRK_LAUNCH_CHECK();
   } else {
-    GRK_CHECK_HIP(hipMemsetAsync(ws, 0, grk_add_norm_bwd_workspace(rows, dim), st));
+    GRK_CHECK_HIP(zero_async(ws, grk_add_norm_bwd_workspace(rows, dim), st));
   }
   NGParams q;
   memset(&q, 0, sizeof(q));

@@ -170,8 +170,8 @@ extern "C" int grk_pair_logits_fwd(const void* h, int64_t ldh, const void* e_pos
   GRK_CHECK_ARG(!loss || (partials && count), "loss needs partials and count");
   if (num_rows == 0) {
     if (loss) {
-      GRK_CHECK_HIP(hipMemsetAsync(loss, 0, 4, (hipStream_t)stream));
-      GRK_CHECK_HIP(hipMemsetAsync(count, 0, 4, (hipStream_t)stream));
+      GRK_CHECK_HIP(zero_async(loss, 4, (hipStream_t)stream));
+      GRK_CHECK_HIP(zero_async(count, 4, (hipStream_t)stream));
     }
     return GRK_OK;
   }

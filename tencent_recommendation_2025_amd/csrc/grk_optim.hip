@@ -31,6 +31,22 @@ __device__ __forceinline__ AdamStep adam_step(const grk_adamw_hparams& hp) {
   return s;
 }
 
+// Hyper-parameters of a launch: by value (eager callers), or -- for launches
+// captured once in a HIP graph and replayed every step -- read on the device
+// at kernel start from hp_ring[*t % ring_len] with the step counter *t in
+// device memory (the *_dev entry points).  Uniform scalar loads.
+struct HpArg {
+  grk_adamw_hparams hp;
+  const grk_adamw_hparams* ring;
+  const int32_t* t;
+  int ring_len;
+};
+__device__ __forceinline__ grk_adamw_hparams resolve(const HpArg& a) {
+  if (a.ring) return a.ring[*a.t % a.ring_len];
+  return a.hp;
+}
+__device__ __forceinline__ int resolve_t(int t, const int32_t* t_dev) { return t_dev ? *t_dev : t; }
+
 // One element of the torch single-tensor AdamW step.  Every update path (dense,
 // lazy, dense-gradient, catch-up replay) goes through this function, so a
 // replayed g = 0 step is bit-identical to the step the dense pass would run.
@@ -131,7 +147,7 @@ template <typename P, int NV>
 __global__ void __launch_bounds__(256) k_adamw_dense(P* __restrict__ param, float* __restrict__ m,
                                                      float* __restrict__ v, int64_t num_rows, int dim,
                                                      const float* __restrict__ uniq_rows,
-                                                     const int32_t* __restrict__ row_slot, grk_adamw_hparams hp) {
+                                                     const int32_t* __restrict__ row_slot, HpArg hpa) {
   const int q = dim / NV;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= num_rows * q) return;
@@ -143,7 +159,7 @@ __global__ void __launch_bounds__(256) k_adamw_dense(P* __restrict__ param, floa
   for (int e = 0; e < NV; ++e) g[e] = 0.f;
   if (slot >= 0) load_grad<NV>(uniq_rows + (int64_t)slot * dim + c, g);
   const int64_t off = row * dim + c;
-  adam_vec<P, NV>(param + off, m + off, v + off, g, adam_step(hp));
+  adam_vec<P, NV>(param + off, m + off, v + off, g, adam_step(resolve(hpa)));
 }
 
 // Dense gradient of any dtype ([rows, grad_ld], GT = float or bf16): every
@@ -152,7 +168,7 @@ template <typename P, typename GT, int NV>
 __global__ void __launch_bounds__(256) k_adamw_dense_grad(P* __restrict__ param, float* __restrict__ m,
                                                           float* __restrict__ v, int64_t num_rows, int dim,
                                                           const GT* __restrict__ grad, int64_t grad_ld,
-                                                          grk_adamw_hparams hp) {
+                                                          HpArg hpa) {
   const int q = dim / NV;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= num_rows * q) return;
@@ -167,7 +183,7 @@ __global__ void __launch_bounds__(256) k_adamw_dense_grad(P* __restrict__ param,
     for (int e = 0; e < NV; ++e) g[e] = bf16_to_f32(reinterpret_cast<const bf16_t*>(src)[e]);
   }
   const int64_t off = row * dim + c;
-  adam_vec<P, NV>(param + off, m + off, v + off, g, adam_step(hp));
+  adam_vec<P, NV>(param + off, m + off, v + off, g, adam_step(resolve(hpa)));
 }
 
 // Catch-up (deferred dense-parity updates): one wave per row; lane 0 claims
@@ -181,7 +197,8 @@ __global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, fl
                                                        float* __restrict__ v, int64_t num_rows, int dim,
                                                        int32_t* __restrict__ last, const int64_t* __restrict__ ids,
                                                        int64_t num_ids, const grk_adamw_hparams* __restrict__ ring,
-                                                       int ring_len, int t) {
+                                                       int ring_len, int t_host, const int32_t* __restrict__ t_dev) {
+  const int t = resolve_t(t_host, t_dev);
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (w >= (ids ? num_ids : num_rows)) return;
@@ -214,7 +231,9 @@ __global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, fl
 }
 
 __global__ void k_stamp_rows(int32_t* __restrict__ last, const int64_t* __restrict__ ids,
-                             const int32_t* __restrict__ count, int64_t max_uniq, int t) {
+                             const int32_t* __restrict__ count, int64_t max_uniq, int t_host,
+                             const int32_t* __restrict__ t_dev) {
+  const int t = resolve_t(t_host, t_dev);
   const int64_t n = *count < max_uniq ? *count : max_uniq;
   for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n; u += (int64_t)gridDim.x * blockDim.x)
     last[ids[u]] = t;
@@ -226,8 +245,9 @@ __global__ void __launch_bounds__(256) k_adamw_lazy(P* __restrict__ param, float
                                                     const int64_t* __restrict__ uniq_ids,
                                                     const float* __restrict__ uniq_rows,
                                                     const int32_t* __restrict__ count, int64_t max_uniq,
-                                                    grk_adamw_hparams hp) {
+                                                    HpArg hpa) {
   const int q = dim / NV;
+  const AdamStep st = adam_step(resolve(hpa));
   const int64_t n = *count;
   const int64_t total = (n < max_uniq ? n : max_uniq) * q;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -236,7 +256,7 @@ __global__ void __launch_bounds__(256) k_adamw_lazy(P* __restrict__ param, float
     float g[NV];
     load_grad<NV>(uniq_rows + u * dim + c, g);
     const int64_t off = uniq_ids[u] * dim + c;
-    adam_vec<P, NV>(param + off, m + off, v + off, g, adam_step(hp));
+    adam_vec<P, NV>(param + off, m + off, v + off, g, st);
   }
 }
 
@@ -251,9 +271,9 @@ __global__ void k_reset_slots(int32_t* __restrict__ row_slot, const int64_t* __r
 
 using namespace grk;
 
-extern "C" int grk_table_adamw(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows,
-                               int dim, const int64_t* uniq_ids, const float* uniq_rows, const int32_t* uniq_count,
-                               int64_t max_uniq, int32_t* row_slot, grk_adamw_hparams hp, int mode, void* stream) {
+static int table_adamw(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows, int dim,
+                       const int64_t* uniq_ids, const float* uniq_rows, const int32_t* uniq_count, int64_t max_uniq,
+                       int32_t* row_slot, HpArg hp, int mode, void* stream) {
   clear_error();
   GRK_CHECK_ARG(param && exp_avg && exp_avg_sq, "param / exp_avg / exp_avg_sq required");
   GRK_CHECK_ARG(param_dtype == GRK_F32 || param_dtype == GRK_BF16, "bad param dtype");
@@ -261,7 +281,8 @@ extern "C" int grk_table_adamw(void* param, int param_dtype, float* exp_avg, flo
   GRK_CHECK_ARG(mode == GRK_ADAM_DENSE || mode == GRK_ADAM_LAZY, "bad mode");
   GRK_CHECK_ARG(mode == GRK_ADAM_DENSE || (uniq_ids && uniq_rows && uniq_count), "lazy mode needs uniq_* inputs");
   GRK_CHECK_ARG(mode == GRK_ADAM_LAZY || !row_slot || uniq_rows, "dense mode with row_slot needs uniq_rows");
-  GRK_CHECK_ARG(hp.bias_corr2_sqrt > 0.f, "bias_corr2_sqrt must be > 0");
+  GRK_CHECK_ARG(hp.ring ? (hp.t && hp.ring_len > 0) : hp.hp.bias_corr2_sqrt > 0.f,
+                "bias_corr2_sqrt must be > 0 (or a device ring and step)");
   hipStream_t s = (hipStream_t)stream;
   const bool v8 = dim % 8 == 0;
   if (mode == GRK_ADAM_DENSE) {
@@ -290,9 +311,8 @@ extern "C" int grk_table_adamw(void* param, int param_dtype, float* exp_avg, flo
   return GRK_OK;
 }
 
-extern "C" int grk_table_adamw_dense(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
-                                     int64_t num_rows, int dim, const void* grad, int grad_dtype, int64_t grad_ld,
-                                     grk_adamw_hparams hp, void* stream) {
+static int table_adamw_dense(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows,
+                             int dim, const void* grad, int grad_dtype, int64_t grad_ld, HpArg hp, void* stream) {
   clear_error();
   GRK_CHECK_ARG(num_rows >= 0, "num_rows must be >= 0");
   if (num_rows == 0) return GRK_OK;
@@ -300,7 +320,8 @@ extern "C" int grk_table_adamw_dense(void* param, int param_dtype, float* exp_av
   GRK_CHECK_ARG(param_dtype == GRK_F32 || param_dtype == GRK_BF16, "bad param dtype");
   GRK_CHECK_ARG(grad_dtype == GRK_F32 || grad_dtype == GRK_BF16, "bad grad dtype");
   GRK_CHECK_ARG(dim > 0 && dim % 4 == 0 && grad_ld >= dim && grad_ld % 4 == 0, "dim / grad_ld must be multiples of 4");
-  GRK_CHECK_ARG(hp.bias_corr2_sqrt > 0.f, "bias_corr2_sqrt must be > 0");
+  GRK_CHECK_ARG(hp.ring ? (hp.t && hp.ring_len > 0) : hp.hp.bias_corr2_sqrt > 0.f,
+                "bias_corr2_sqrt must be > 0 (or a device ring and step)");
   const bool v8 = dim % 8 == 0 && grad_ld % 8 == 0;
   const int64_t work = num_rows * (dim / (v8 ? 8 : 4));
   GRK_CHECK_ARG((work + 255) / 256 < (int64_t)1 << 31, "table too large for one launch");
@@ -321,9 +342,10 @@ extern "C" int grk_table_adamw_dense(void* param, int param_dtype, float* exp_av
 }
 
 
-extern "C" int grk_table_adamw_catchup(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
-                                       int64_t num_rows, int dim, int32_t* last, const int64_t* ids, int64_t num_ids,
-                                       const grk_adamw_hparams* hp_ring, int32_t ring_len, int32_t t, void* stream) {
+static int table_adamw_catchup(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows,
+                               int dim, int32_t* last, const int64_t* ids, int64_t num_ids,
+                               const grk_adamw_hparams* hp_ring, int32_t ring_len, int32_t t, const int32_t* t_dev,
+                               void* stream) {
   clear_error();
   GRK_CHECK_ARG(num_rows >= 0 && num_ids >= 0, "num_rows / num_ids must be >= 0");
   const int64_t waves = ids ? num_ids : num_rows;
@@ -337,7 +359,7 @@ extern "C" int grk_table_adamw_catchup(void* param, int param_dtype, float* exp_
   hipStream_t s = (hipStream_t)stream;
   const bool v8 = dim % 8 == 0;
 #define GRK_CU(P, NV) k_adamw_catchup<P, NV><<<g, 256, 0, s>>>((P*)param, exp_avg, exp_avg_sq, num_rows, dim, last, \
-                                                               ids, num_ids, hp_ring, ring_len, t)
+                                                               ids, num_ids, hp_ring, ring_len, t, t_dev)
   if (param_dtype == GRK_BF16) { if (v8) GRK_CU(bf16_t, 8); else GRK_CU(bf16_t, 4); }
   else { if (v8) GRK_CU(float, 8); else GRK_CU(float, 4); }
 #undef GRK_CU
@@ -345,12 +367,81 @@ extern "C" int grk_table_adamw_catchup(void* param, int param_dtype, float* exp_
   return GRK_OK;
 }
 
-extern "C" int grk_stamp_rows(int32_t* last, const int64_t* uniq_ids, const int32_t* uniq_count, int64_t max_uniq,
-                              int32_t t, void* stream) {
+static int stamp_rows(int32_t* last, const int64_t* uniq_ids, const int32_t* uniq_count, int64_t max_uniq,
+                      int32_t t, const int32_t* t_dev, void* stream) {
   clear_error();
   if (max_uniq <= 0) return GRK_OK;
   GRK_CHECK_ARG(last && uniq_ids && uniq_count, "last / uniq_ids / uniq_count required");
-  k_stamp_rows<<<grid_for(max_uniq, 256, 1024), 256, 0, (hipStream_t)stream>>>(last, uniq_ids, uniq_count, max_uniq, t);
+  k_stamp_rows<<<grid_for(max_uniq, 256, 1024), 256, 0, (hipStream_t)stream>>>(last, uniq_ids, uniq_count, max_uniq, t,
+                                                                               t_dev);
   GRK_LAUNCH_CHECK();
   return GRK_OK;
+}
+
+static HpArg by_value(grk_adamw_hparams hp) { return HpArg{hp, nullptr, nullptr, 0}; }
+static HpArg on_device(const grk_adamw_hparams* ring, int32_t ring_len, const int32_t* t) {
+  HpArg a{};
+  a.ring = ring;
+  a.t = t;
+  a.ring_len = ring_len;
+  return a;
+}
+
+extern "C" int grk_table_adamw(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows,
+                               int dim, const int64_t* uniq_ids, const float* uniq_rows, const int32_t* uniq_count,
+                               int64_t max_uniq, int32_t* row_slot, grk_adamw_hparams hp, int mode, void* stream) {
+  return table_adamw(param, param_dtype, exp_avg, exp_avg_sq, num_rows, dim, uniq_ids, uniq_rows, uniq_count,
+                     max_uniq, row_slot, by_value(hp), mode, stream);
+}
+
+extern "C" int grk_table_adamw_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows,
+                                   int dim, const int64_t* uniq_ids, const float* uniq_rows, const int32_t* uniq_count,
+                                   int64_t max_uniq, int32_t* row_slot, const grk_adamw_hparams* hp_ring,
+                                   int32_t ring_len, const int32_t* t_dev, int mode, void* stream) {
+  if (!hp_ring || !t_dev || ring_len <= 0) { set_error("hp_ring / t_dev / ring_len required"); return GRK_EINVAL; }
+  return table_adamw(param, param_dtype, exp_avg, exp_avg_sq, num_rows, dim, uniq_ids, uniq_rows, uniq_count,
+                     max_uniq, row_slot, on_device(hp_ring, ring_len, t_dev), mode, stream);
+}
+
+extern "C" int grk_table_adamw_dense(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
+                                     int64_t num_rows, int dim, const void* grad, int grad_dtype, int64_t grad_ld,
+                                     grk_adamw_hparams hp, void* stream) {
+  return table_adamw_dense(param, param_dtype, exp_avg, exp_avg_sq, num_rows, dim, grad, grad_dtype, grad_ld,
+                           by_value(hp), stream);
+}
+
+extern "C" int grk_table_adamw_dense_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
+                                         int64_t num_rows, int dim, const void* grad, int grad_dtype, int64_t grad_ld,
+                                         const grk_adamw_hparams* hp_ring, int32_t ring_len, const int32_t* t_dev,
+                                         void* stream) {
+  if (!hp_ring || !t_dev || ring_len <= 0) { set_error("hp_ring / t_dev / ring_len required"); return GRK_EINVAL; }
+  return table_adamw_dense(param, param_dtype, exp_avg, exp_avg_sq, num_rows, dim, grad, grad_dtype, grad_ld,
+                           on_device(hp_ring, ring_len, t_dev), stream);
+}
+
+extern "C" int grk_table_adamw_catchup(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
+                                       int64_t num_rows, int dim, int32_t* last, const int64_t* ids, int64_t num_ids,
+                                       const grk_adamw_hparams* hp_ring, int32_t ring_len, int32_t t, void* stream) {
+  return table_adamw_catchup(param, param_dtype, exp_avg, exp_avg_sq, num_rows, dim, last, ids, num_ids, hp_ring,
+                             ring_len, t, nullptr, stream);
+}
+
+extern "C" int grk_table_adamw_catchup_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
+                                           int64_t num_rows, int dim, int32_t* last, const int64_t* ids,
+                                           int64_t num_ids, const grk_adamw_hparams* hp_ring, int32_t ring_len,
+                                           const int32_t* t_dev, void* stream) {
+  if (!t_dev) { set_error("t_dev required"); return GRK_EINVAL; }
+  return table_adamw_catchup(param, param_dtype, exp_avg, exp_avg_sq, num_rows, dim, last, ids, num_ids, hp_ring,
+                             ring_len, 0, t_dev, stream);
+}
+
+extern "C" int grk_stamp_rows(int32_t* last, const int64_t* uniq_ids, const int32_t* uniq_count, int64_t max_uniq,
+                              int32_t t, void* stream) {
+  return stamp_rows(last, uniq_ids, uniq_count, max_uniq, t, nullptr, stream);
+}
+
+extern "C" int grk_stamp_rows_dev(int32_t* last, const int64_t* uniq_ids, const int32_t* uniq_count, int64_t max_uniq,
+                                  const int32_t* t_dev, void* stream) {
+  if (!t_dev) { set_error("t_dev required"); return GRK_EINVAL; }
+  return stamp_rows(last, uniq_ids, uniq_count, max_uniq, 0, t_dev, stream);
 }

@@ -160,18 +160,42 @@ def adamw_hparams(lr, beta1, beta2, eps, weight_decay, step):
     return L.GrkAdamwHparams(lr, beta1, beta2, eps, weight_decay, lr / bc1, math.sqrt(bc2), 0.0)
 
 
+class DeviceClock:
+    """The optimizer step in device memory plus a ring of per-step hyper-parameters.
+
+    Passed where a ``GrkAdamwHparams`` (hp) or an int step (t) is expected, the
+    table kernels read the step from ``t`` at execution time and the
+    hyper-parameters from ``ring[t % ring_len]`` (the ``*_dev`` entry points):
+    a launch captured once in a HIP graph then does the right step on every
+    replay.  ``advance()`` (t += 1) is itself a device op, captured with the
+    step.  The owner keeps the ring filled for the steps ahead."""
+
+    def __init__(self, ring_len, device):
+        nf = C.sizeof(L.GrkAdamwHparams) // 4
+        self.ring_len = int(ring_len)
+        self.ring = torch.zeros(self.ring_len, nf, dtype=torch.float32, device=device)
+        self.t = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def advance(self):
+        self.t.add_(1)
+
+
 def table_adamw(param, exp_avg, exp_avg_sq, hp, ids=None, rows=None, count=None, capacity=0, row_slot=None,
                 lazy=False):
-    """AdamW update of one table from a row-sparse gradient (grk_table_adamw)."""
+    """AdamW update of one table from a row-sparse gradient (grk_table_adamw / _dev when hp is a DeviceClock)."""
     _require_cuda(param, exp_avg, exp_avg_sq, ids, rows, count, row_slot)
     if exp_avg.dtype != torch.float32 or exp_avg_sq.dtype != torch.float32:
         raise L.GrkError('optimizer moments must be float32')
     if not (param.is_contiguous() and exp_avg.is_contiguous() and exp_avg_sq.is_contiguous()):
         raise L.GrkError('param and moments must be contiguous')
-    rc = L.lib().grk_table_adamw(param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(),
-                                 exp_avg_sq.data_ptr(), param.shape[0], param.shape[1], _ptr(ids), _ptr(rows),
-                                 _ptr(count), capacity, _ptr(row_slot), hp,
-                                 L.ADAM_LAZY if lazy else L.ADAM_DENSE, L.stream_ptr(param.device))
+    args = (param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(), exp_avg_sq.data_ptr(), param.shape[0],
+            param.shape[1], _ptr(ids), _ptr(rows), _ptr(count), capacity, _ptr(row_slot))
+    mode = L.ADAM_LAZY if lazy else L.ADAM_DENSE
+    if isinstance(hp, DeviceClock):
+        rc = L.lib().grk_table_adamw_dev(*args, hp.ring.data_ptr(), hp.ring_len, hp.t.data_ptr(), mode,
+                                         L.stream_ptr(param.device))
+    else:
+        rc = L.lib().grk_table_adamw(*args, hp, mode, L.stream_ptr(param.device))
     L.check(rc, 'grk_table_adamw')
 
 
@@ -193,15 +217,22 @@ def table_adamw_dense(param, exp_avg, exp_avg_sq, hp, grad):
             raise L.GrkError(f'{n} must be a contiguous [{rows}, {D}] tensor')
     if grad.dim() != 2 or grad.shape[0] != rows or grad.shape[1] < D or grad.stride(1) != 1:
         raise L.GrkError(f'grad must be a row-major [{rows}, >= {D}] tensor')
-    rc = L.lib().grk_table_adamw_dense(param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(),
-                                       exp_avg_sq.data_ptr(), rows, D, grad.data_ptr(), L.dtype_code(grad.dtype),
-                                       grad.stride(0), hp, L.stream_ptr(param.device))
+    args = (param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(), exp_avg_sq.data_ptr(), rows, D,
+            grad.data_ptr(), L.dtype_code(grad.dtype), grad.stride(0))
+    if isinstance(hp, DeviceClock):
+        rc = L.lib().grk_table_adamw_dense_dev(*args, hp.ring.data_ptr(), hp.ring_len, hp.t.data_ptr(),
+                                               L.stream_ptr(param.device))
+    else:
+        rc = L.lib().grk_table_adamw_dense(*args, hp, L.stream_ptr(param.device))
     L.check(rc, 'grk_table_adamw_dense')
 
 
 def table_adamw_catchup(param, exp_avg, exp_avg_sq, last, hp_ring, t, ids=None):
     """Replay the skipped g = 0 steps (last[row], t] of rows `ids` (all rows if None) --
-    grk_table_adamw_catchup.  hp_ring: uint8/float tensor holding grk_adamw_hparams[ring_len]."""
+    grk_table_adamw_catchup.  hp_ring: uint8/float tensor holding grk_adamw_hparams[ring_len];
+    t: an int, or a DeviceClock (its step and ring; hp_ring is then ignored)."""
+    if isinstance(t, DeviceClock):
+        hp_ring = t.ring
     _require_cuda(param, exp_avg, exp_avg_sq, last, hp_ring, ids)
     rows, D = param.shape
     if last.dtype != torch.int32 or last.shape != (rows,):
@@ -212,17 +243,24 @@ def table_adamw_catchup(param, exp_avg, exp_avg_sq, last, hp_ring, t, ids=None):
         if ids.dtype != torch.int64 or not ids.is_contiguous():
             raise L.GrkError('ids must be a contiguous int64 tensor')
         n = ids.numel()
-    rc = L.lib().grk_table_adamw_catchup(param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(),
-                                         exp_avg_sq.data_ptr(), rows, D, last.data_ptr(), _ptr(ids), n,
-                                         hp_ring.data_ptr(), ring_len, int(t), L.stream_ptr(param.device))
+    args = (param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(), exp_avg_sq.data_ptr(), rows, D,
+            last.data_ptr(), _ptr(ids), n, hp_ring.data_ptr(), ring_len)
+    if isinstance(t, DeviceClock):
+        rc = L.lib().grk_table_adamw_catchup_dev(*args, t.t.data_ptr(), L.stream_ptr(param.device))
+    else:
+        rc = L.lib().grk_table_adamw_catchup(*args, int(t), L.stream_ptr(param.device))
     L.check(rc, 'grk_table_adamw_catchup')
 
 
 def stamp_rows(last, ids, count, capacity, t):
-    """last[ids[:count]] = t (grk_stamp_rows)."""
+    """last[ids[:count]] = t (grk_stamp_rows; t may be a DeviceClock)."""
     _require_cuda(last, ids, count)
-    rc = L.lib().grk_stamp_rows(last.data_ptr(), ids.data_ptr(), count.data_ptr(), int(capacity), int(t),
-                                L.stream_ptr(last.device))
+    if isinstance(t, DeviceClock):
+        rc = L.lib().grk_stamp_rows_dev(last.data_ptr(), ids.data_ptr(), count.data_ptr(), int(capacity),
+                                        t.t.data_ptr(), L.stream_ptr(last.device))
+    else:
+        rc = L.lib().grk_stamp_rows(last.data_ptr(), ids.data_ptr(), count.data_ptr(), int(capacity), int(t),
+                                    L.stream_ptr(last.device))
     L.check(rc, 'grk_stamp_rows')
 
 

@@ -148,8 +148,11 @@ class FusedAdamW:
             refs.update(grp.refs)
         model._table_refs = refs
         dense = [p for p in model.parameters() if p.requires_grad]
+        cuda = dev.type == 'cuda'
+        # capturable: the dense AdamW keeps its step count on the device, so the
+        # whole training step can be captured in a HIP graph (train.Trainer)
         self.dense = torch.optim.AdamW(dense, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
-                                       fused=dev.type == 'cuda')
+                                       fused=cuda, capturable=cuda)
         self.t = 0
         # Deferred dense parity for the big item/user tables: a row outside the
         # step's batch takes a g = 0 update that depends on nothing but (p, m, v)
@@ -158,38 +161,64 @@ class FusedAdamW:
         # `defer_period`-th step for all rows, and before state_dict (flush) --
         # bit-identical to moving every row every step, without streaming the
         # whole table through HBM each step.  Needs Trainer.step (begin_step).
-        self.defer = int(defer_period) if (defer_period and not self.lazy and dev.type == 'cuda') else 0
+        self.defer = int(defer_period) if (defer_period and not self.lazy and cuda) else 0
         self._deferred = {g.name: g for g in self.groups if g.name in ('item', 'user')} if self.defer else {}
         self._seg = None     # step every deferred row was last brought up to (segment start)
         self._begun = None   # step for which begin_step caught the batch rows up
         for g in self._deferred.values():
             g.last = torch.zeros(g.rows, dtype=torch.int32, device=dev)
-        if self.defer:
-            nf = C.sizeof(L.GrkAdamwHparams) // 4
-            self._ring = torch.zeros(self.defer, nf, dtype=torch.float32, device=dev)
-            self._pinned = [torch.zeros(self.defer, nf, dtype=torch.float32).pin_memory() for _ in range(2)]
+        # The table kernels read the step and its hyper-parameters on the device
+        # (K.DeviceClock): the ring holds the steps of the current segment,
+        # refilled at segment starts from alternating pinned buffers.
+        self.clock = K.DeviceClock(self.defer or 16, dev) if cuda else None
+        if self.clock is not None:
+            self._pinned = [torch.zeros_like(self.clock.ring, device='cpu').pin_memory() for _ in range(2)]
             self._uploads = 0
+        if self.defer:
             model.register_state_dict_pre_hook(lambda *args, **kw: self.flush())
+
+    @property
+    def _ring(self):
+        return self.clock.ring
 
     def _hp(self, step):
         return K.adamw_hparams(self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, step)
 
     def _upload_ring(self, t):
-        """Hyper-parameters of steps t+1 .. t+defer into the device ring (slot s % defer)."""
-        buf = self._pinned[self._uploads % 2]  # alternate: the previous copy may still be in flight
+        """Hyper-parameters of steps t+1 .. t+ring_len into the device ring (slot s % ring_len)."""
+        n = self.clock.ring_len
+        k = self._uploads % 2  # alternate buffers; the host may run many (graph-replayed) steps ahead
         self._uploads += 1
-        for step in range(t + 1, t + self.defer + 1):
+        done = getattr(self, '_pinned_done', None)
+        if done is None:
+            done = self._pinned_done = [None, None]
+        if done[k] is not None:
+            done[k].synchronize()  # the copy out of this buffer two segments ago has run
+        buf = self._pinned[k]
+        for step in range(t + 1, t + n + 1):
             hp = self._hp(step)
-            buf[step % self.defer] = torch.tensor([getattr(hp, f) for f, _ in hp._fields_], dtype=torch.float32)
-        self._ring.copy_(buf, non_blocking=True)
+            buf[step % n] = torch.tensor([getattr(hp, f) for f, _ in hp._fields_], dtype=torch.float32)
+        self.clock.ring.copy_(buf, non_blocking=True)
+        done[k] = torch.cuda.Event()
+        done[k].record()
 
     def _segment(self, t):
-        """Start a new defer segment at step t: bring every row to t, refill the ring."""
+        """Start a new segment at step t: bring every deferred row to t, refill the ring."""
         if self._seg is not None and self._seg < t:
             for g in self._deferred.values():
-                K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self._ring, t)
+                K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock)
         self._upload_ring(t)
         self._seg = t
+
+    def maybe_segment(self):
+        """Host-side segment bookkeeping due before step self.t + 1 (eager; never inside a captured step)."""
+        if self.clock is not None and (self._seg is None or self.t - self._seg >= self.clock.ring_len):
+            self._segment(self.t)
+
+    def graph_replayed(self):
+        """Host state after a replay of a captured step (the device state advanced inside the graph)."""
+        self.t += 1
+        self._begun = None
 
     @torch.no_grad()
     def begin_step(self, batch):
@@ -198,11 +227,9 @@ class FusedAdamW:
         batch = (seq, pos, neg, token_type, ...) as Trainer.step gets it: the
         item table's rows are seq (item tokens), pos and neg; the user table's
         are seq (user tokens)."""
+        self.maybe_segment()
         if not self._deferred:
             return
-        t = self.t
-        if self._seg is None or t - self._seg >= self.defer:
-            self._segment(t)
         seq, pos, neg, tt = (x.long() for x in batch[:4])
         # Padding (id 0, and tokens of the other type) -> -1, skipped by the kernel:
         # thousands of duplicate claims on row 0 would serialise on one atomic.
@@ -214,15 +241,15 @@ class FusedAdamW:
         ids = {'item': torch.where(item > 0, item, skip),
                'user': torch.where((tt == 2) & (seq > 0), seq, skip).reshape(-1)}
         for name, g in self._deferred.items():
-            K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self._ring, t, ids[name])
-        self._begun = t
+            K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock, ids[name])
+        self._begun = self.t
 
     @torch.no_grad()
     def flush(self):
         """Bring every row of the deferred tables to the current step (before reading them)."""
         if self._deferred and self._seg is not None:
             for g in self._deferred.values():
-                K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self._ring, self.t)
+                K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock)
 
     def zero_grad(self, set_to_none=True):
         self.dense.zero_grad(set_to_none=set_to_none)
@@ -231,14 +258,15 @@ class FusedAdamW:
 
     @torch.no_grad()
     def step(self):
+        self.maybe_segment()
         if self._deferred and self._begun != self.t:  # no begin_step: every row to step t, then dense
-            if self._seg is None or self.t - self._seg >= self.defer:
-                self._segment(self.t)
             self.flush()
         begun, self._begun = self._begun == self.t, None
         self.t += 1
+        if self.clock is not None:
+            self.clock.advance()
         self.dense.step()
-        hp = K.adamw_hparams(self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, self.t)
+        hp = self.clock if self.clock is not None else self._hp(self.t)
         for g in self.groups:
             if g.name in self._deferred:
                 if begun:  # rows outside the batch stay deferred; the batch rows move now
@@ -247,7 +275,7 @@ class FusedAdamW:
                                                    seq_len=g.seq_len, dense=False, sparse=True, row_slot=g.row_slot)
                         K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, res.ids, res.rows, res.count,
                                       res.capacity, g.row_slot, lazy=True)
-                        K.stamp_rows(g.last, res.ids, res.count, res.capacity, self.t)
+                        K.stamp_rows(g.last, res.ids, res.count, res.capacity, self.clock)
                     g.clear()
                     continue
                 g.last.fill_(self.t)  # dense update below moves every row

@@ -202,20 +202,31 @@ class GradBuckets:
             self.next += 1
 
     def _launch(self, b):
-        flat, off = self.flat[b], 0
+        """Bucket b's gradients into its flat buffer (one cat kernel), then its all-reduce."""
+        flat, off, src, alias = self.flat[b], 0, [], 0
         for p in self.buckets[b]:
             n = p.numel()
             if p.grad is None:
-                flat[off:off + n].zero_()
+                src.append(flat.new_zeros(n))
             else:
-                flat[off:off + n].copy_(p.grad.reshape(-1))
+                src.append(p.grad.reshape(-1))
+                alias += src[-1].data_ptr() == flat[off:].data_ptr()
             off += n
+        if alias == 0:
+            torch.cat(src, out=flat)
+        elif alias < len(src):  # zero_grad(set_to_none=False): some grads already live in the bucket
+            off = 0
+            for t in src:
+                if t.data_ptr() != flat[off:].data_ptr():
+                    flat[off:off + t.numel()].copy_(t)
+                off += t.numel()
         if self.async_ok:
             self.works[b] = dist.all_reduce(flat, group=self.pg, async_op=True)
         else:
             all_reduce(flat, self.pg)
 
     def finish(self):
+        """Issue the remaining buckets, wait, and make every p.grad the mean (a view of its bucket)."""
         while self.next < len(self.buckets):
             self._launch(self.next)
             self.next += 1
@@ -223,12 +234,12 @@ class GradBuckets:
         for b, ps in enumerate(self.buckets):
             if self.works[b] is not None:
                 self.works[b].wait()
-            flat, off = self.flat[b].mul_(inv), 0
+            flat, off = self.flat[b], 0
+            if self.world > 1:
+                flat.mul_(inv)
             for p in ps:
                 n = p.numel()
-                if p.grad is None:
-                    p.grad = torch.empty_like(p)
-                p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                p.grad = flat[off:off + n].view_as(p)
                 off += n
         self._reset()
 
@@ -268,12 +279,14 @@ class ShardedFusedAdamW(FusedAdamW):
             emb.weight = torch.nn.Parameter(torch.empty(0, emb.embedding_dim, dtype=table_dtype, device=dev),
                                             requires_grad=False)
             sharded_refs[name] = ShardedRef(name, emb.weight)
-        small_keys = tuple(k for k in tables if k not in self.SHARDED)
+        small_keys = tuple(k for k in tables if k not in self.SHARDED and k != 'pos_emb')
         super().__init__(model, lr, betas, eps, weight_decay, table_mode, table_dtype,
-                         groups=(('small', small_keys),), defer_period=defer_period)
+                         groups=(('pos', ('pos_emb',)), ('small', small_keys)), defer_period=defer_period)
         model._table_refs.update(sharded_refs)
-        self.small = self.groups[0]
-        self.small_identity = torch.arange(self.small.rows, dtype=torch.int32, device=dev)
+        # replicated groups: their fp32 gradients share one buffer (one all-reduce)
+        self.replicated = list(self.groups)
+        self.rep_rows = sum(g.rows for g in self.replicated)
+        self.rep_identity = torch.arange(max(g.rows for g in self.replicated), dtype=torch.int32, device=dev)
         self.sinks = {}
         # the shards are the deferred groups (FusedAdamW machinery: ring, segments, flush)
         if self.defer:
@@ -307,8 +320,7 @@ class ShardedFusedAdamW(FusedAdamW):
             routed[name] = self.shards[name][1].route(ids)
         counts = torch.stack([torch.stack([routed[n]['send_counts'], routed[n]['recv_counts']]) for n in parts])
         counts = counts.cpu().tolist()  # the one host sync of the step: all-to-all split sizes
-        if self.defer and (self._seg is None or self.t - self._seg >= self.defer):
-            self._segment(self.t)
+        self.maybe_segment()
         remaps = {}
         self.sinks = {}
         for gi, (name, plist) in enumerate(parts.items()):
@@ -317,7 +329,7 @@ class ShardedFusedAdamW(FusedAdamW):
             catchup = None
             if self.defer:
                 def catchup(local, grp=grp):
-                    K.table_adamw_catchup(grp.flat, grp.exp_avg, grp.exp_avg_sq, grp.last, self._ring, self.t,
+                    K.table_adamw_catchup(grp.flat, grp.exp_avg, grp.exp_avg_sq, grp.last, None, self.clock,
                                           local.contiguous())
             fetched = ex.fetch(r, counts[gi][0], counts[gi][1], before_gather=catchup)
             sink = FetchSink()
@@ -339,23 +351,23 @@ class ShardedFusedAdamW(FusedAdamW):
             raise RuntimeError('ShardedFusedAdamW: call prepare(batch) before forward (Trainer.step does)')
         self._begun = None
         self.t += 1
-        hp = K.adamw_hparams(self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, self.t)
+        self.clock.advance()
+        hp = self.clock
         inv_world = 1.0 / self.world
-        # replicated small tables: dense fp32 gradient, all-reduce (mean) issued first, so
-        # it runs on RCCL's stream under the dense and shard updates below
-        g = self.small
-        if g.pending:
-            dense = self.dense_reduce_fn(g.pending, g.rows, g.dim, g.token_type, g.seq_len)
-        else:
-            dense = torch.zeros(g.rows, g.dim, dtype=torch.float32, device=g.flat.device)
-        for off, dg in g.dense_grads.items():
-            dense[off:off + dg.shape[0]] += dg
-        small_work = None
+        # replicated tables (pos + feature tables): dense fp32 gradients in one buffer, all-reduce
+        # (mean) issued first, so it runs on RCCL's stream under the shard and dense updates below
+        dev = self.replicated[0].flat.device
+        rep = torch.empty(self.rep_rows, self.replicated[0].dim, dtype=torch.float32, device=dev)
+        row = 0
+        for g in self.replicated:
+            _dense_grad_into(g, rep[row:row + g.rows], self.dense_reduce_fn)
+            row += g.rows
+        rep_work = None
         if self.world > 1:
-            if dense.is_cuda and dist.get_backend(self.pg) != 'gloo':
-                small_work = dist.all_reduce(dense, group=self.pg, async_op=True)
+            if rep.is_cuda and dist.get_backend(self.pg) != 'gloo':
+                rep_work = dist.all_reduce(rep, group=self.pg, async_op=True)
             else:
-                all_reduce(dense, self.pg)
+                all_reduce(rep, self.pg)
         # sharded tables: per-unique-id grads -> owners -> owner reduction -> shard AdamW
         for name, (grp, ex) in self.shards.items():
             sink = self.sinks.get(name)
@@ -370,21 +382,44 @@ class ShardedFusedAdamW(FusedAdamW):
                 K.table_adamw(grp.flat, grp.exp_avg, grp.exp_avg_sq, hp, res.ids, res.rows, res.count, res.capacity,
                               None if self.lazy else grp.row_slot, lazy=self.lazy or bool(self.defer))
                 if self.defer:
-                    K.stamp_rows(grp.last, res.ids, res.count, res.capacity, self.t)
+                    K.stamp_rows(grp.last, res.ids, res.count, res.capacity, self.clock)
             elif not self.lazy and not self.defer:
                 K.table_adamw(grp.flat, grp.exp_avg, grp.exp_avg_sq, hp)
         # dense parameters: buckets were all-reduced during backward
         if self.buckets is not None:
             self.buckets.finish()
         self.dense.step()
-        if small_work is not None:
-            small_work.wait()
+        if rep_work is not None:
+            rep_work.wait()
         if self.world > 1:
-            dense.mul_(inv_world)
-        K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, None, dense, None, 0, self.small_identity)
-        g.clear()
+            rep.mul_(inv_world)
+        row = 0
+        for g in self.replicated:
+            K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, None, rep[row:row + g.rows], None, 0,
+                          self.rep_identity[:g.rows])
+            row += g.rows
+            g.clear()
         self.sinks = {}
         self.model._remaps = None
+
+
+def _dense_grad_into(g, out, dense_reduce_fn):
+    """out (fp32 [g.rows, D]) = the group's gradient: row-sparse sources reduced
+    densely plus the dense ranges (tables used in dense ops), zeros elsewhere."""
+    if g.pending:
+        out.copy_(dense_reduce_fn(g.pending, g.rows, g.dim, g.token_type, g.seq_len))
+        for off, dg in g.dense_grads.items():
+            out[off:off + dg.shape[0]] += dg
+        return
+    pos = 0
+    for off in sorted(g.dense_grads):
+        dg = g.dense_grads[off]
+        if off > pos:
+            out[pos:off].zero_()
+        out[off:off + dg.shape[0]].copy_(dg)
+        pos = off + dg.shape[0]
+    if pos < g.rows:
+        out[pos:].zero_()
 
 
 class _Holder:

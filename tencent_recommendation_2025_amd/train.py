@@ -1,7 +1,17 @@
 """Training step of the TencentGR script on the grk path (model/BaseLine/main.py:163-190;
 model/BaseLineO1/main.py:200-250): forward, loss, backward, optimizer -- with
 no host synchronisation inside the step (the reference's ``np.where`` index
-set and ``loss.item()`` are replaced by device-side counts)."""
+set and ``loss.item()`` are replaced by device-side counts).
+
+Because the step never waits on the device, it can be captured once as a HIP
+graph and replayed (``graph=True``): the ~470 kernel launches and all the
+Python between them collapse into one graph launch per step, so the host no
+longer paces the GPU.  Everything step-dependent lives on the device: the
+table kernels read the step and its hyper-parameters from the optimizer's
+``DeviceClock``, torch's AdamW runs ``capturable``, and the batch is copied
+into the captured input buffers before each replay.  Segment work of the
+deferred table updates (every ``defer_period`` steps) runs eagerly between
+replays."""
 from __future__ import annotations
 
 import contextlib
@@ -11,19 +21,69 @@ import torch
 from . import functional as G
 
 
+def _tensors(batch):
+    """Flat list of the batch's tensors (tuple items and dict values, in order)."""
+    out = []
+    for x in batch:
+        if isinstance(x, torch.Tensor):
+            out.append(x)
+        elif isinstance(x, dict):
+            out.extend(v for _, v in sorted(x.items()) if isinstance(v, torch.Tensor))
+    return out
+
+
+def _clone_batch(batch):
+    res = []
+    for x in batch:
+        if isinstance(x, torch.Tensor):
+            res.append(x.clone())
+        elif isinstance(x, dict):
+            res.append({k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in x.items()})
+        else:
+            res.append(x)
+    return tuple(res)
+
+
 class Trainer:
     """``step(batch)`` = one training step on a tensorised batch
     (``MyDataset.collate_tensor_fn`` layout, tensors on the device).
 
     loss: "bce" -- the reference loss (pos/neg BCE, main.py:177-182);
           "sampled_softmax" -- north-star in-batch sampled softmax.
+    graph: capture the step in a HIP graph after ``graph_warmup`` eager steps
+          and replay it (needs a fused optimizer with a device clock, no
+          attention dropout, and batches of one fixed shape; a batch of another
+          shape runs eagerly).
     """
 
-    def __init__(self, model, optimizer, loss='bce', amp_dtype=torch.bfloat16, temperature=0.05):
+    def __init__(self, model, optimizer, loss='bce', amp_dtype=torch.bfloat16, temperature=0.05, graph=False,
+                 graph_warmup=3):
         if loss not in ('bce', 'sampled_softmax'):
             raise ValueError("loss must be 'bce' or 'sampled_softmax'")
         self.model, self.opt, self.loss_kind = model, optimizer, loss
         self.amp_dtype, self.temperature = amp_dtype, temperature
+        self.graph, self.graph_warmup = bool(graph), int(graph_warmup)
+        if self.graph:
+            why = self._graph_blocker()
+            if why:
+                raise ValueError(f'graph=True: {why}')
+        self._g = None
+        self._static = None
+        self._static_loss = None
+        self._warm = 0
+        self._side = None
+
+    def _graph_blocker(self):
+        if not torch.cuda.is_available():
+            return 'needs a GPU'
+        if getattr(self.opt, 'clock', None) is None:
+            return 'the optimizer must keep a device clock (optim.FusedAdamW on the GPU)'
+        if hasattr(self.opt, 'prepare'):
+            return 'row-sharded tables exchange data-dependent row counts every step (eager only)'
+        for m in self.model.modules():
+            if getattr(m, 'dropout_rate', 0.0) and m.training:
+                return 'attention dropout draws a host-side seed per step'
+        return None
 
     def compute_loss(self, batch):
         seq, pos, neg, tt, ntt, _nat, sf, pf, nf = batch
@@ -35,7 +95,7 @@ class Trainer:
                 return G.bce_loss(h, pe, ne, ntt)
             return G.sampled_softmax_loss(h, pe, pos, ntt, self.temperature)
 
-    def step(self, batch):
+    def eager_step(self, batch):
         self.opt.zero_grad()
         if hasattr(self.opt, 'prepare'):  # row-sharded tables: fetch this batch's rows from their owners
             self.opt.prepare(batch)
@@ -45,3 +105,50 @@ class Trainer:
         loss.backward()
         self.opt.step()
         return loss.detach()
+
+    def step(self, batch):
+        if not self.graph:
+            return self.eager_step(batch)
+        if self._g is None:
+            if self._warm < self.graph_warmup:
+                # warm-up on the stream the capture will use: GEMM plans tuned,
+                # per-stream workspaces and the caching allocator's blocks in place
+                self._warm += 1
+                return self._on_side(lambda: self.eager_step(batch))
+            return self._capture(batch)
+        src = _tensors(batch)
+        dst = _tensors(self._static)
+        if len(src) != len(dst) or any(a.shape != b.shape or a.dtype != b.dtype for a, b in zip(src, dst)):
+            return self.eager_step(batch)
+        for d, s in zip(dst, src):
+            d.copy_(s, non_blocking=True)
+        self.opt.maybe_segment()
+        self._g.replay()
+        self.opt.graph_replayed()
+        return self._static_loss.clone()
+
+    def _on_side(self, fn):
+        cur = torch.cuda.current_stream()
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=cur.device)
+        self._side.wait_stream(cur)
+        with torch.cuda.stream(self._side):
+            out = fn()
+        cur.wait_stream(self._side)
+        return out
+
+    def _capture(self, batch):
+        """Record one step (host state advances once here), then replay it for this batch."""
+        self._static = _clone_batch(batch)
+        self.opt.maybe_segment()
+        self.opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        cur = torch.cuda.current_stream()
+        self._side.wait_stream(cur)
+        with torch.cuda.graph(g, stream=self._side):
+            self._static_loss = self.eager_step(self._static)
+        cur.wait_stream(self._side)
+        self._g = g
+        g.replay()               # the captured step itself (host state already advanced)
+        return self._static_loss.clone()

@@ -286,3 +286,40 @@ def test_grk_linear_matches_torch_linear():
     torch.testing.assert_close(x.grad, x2.grad, rtol=1e-2, atol=3e-2)
     torch.testing.assert_close(w.grad, w2.grad, rtol=1e-3, atol=2e-2)
     torch.testing.assert_close(b.grad, b2.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize('period', [2, 16])
+def test_graph_replayed_steps_equal_eager_steps(period):
+    """Trainer(graph=True): the step captured once in a HIP graph and replayed
+    with new batches (device clock for the table AdamW, capturable dense AdamW,
+    segment work between replays) == the eager step, bit for bit: losses,
+    parameters (deferred rows flushed) and table moments."""
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    cfg = S.SyntheticConfig(batch_size=8, maxlen=30, num_items=5000, num_users=700, min_len=4)
+    stats, types = S.feature_schema(cfg)
+    args = S.make_args(hidden_units=64, maxlen=30, num_blocks=2, num_heads=2)
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, args).to(DEV)
+        opt = FusedAdamW(m, lr=2e-3, defer_period=period)
+        tr = Trainer(m, opt, loss='bce', graph=graph, graph_warmup=2)
+        g = torch.Generator(device=DEV).manual_seed(0)
+        batches = [S.make_batch(cfg, g, DEV) for _ in range(4)]
+        losses = [tr.step(batches[i % 4]).clone() for i in range(9)]
+        if graph:
+            assert tr._g is not None
+        sd = m.state_dict()
+        torch.cuda.synchronize()
+        runs.append((torch.stack(losses), sd, {grp.name: (grp.exp_avg.clone(), grp.exp_avg_sq.clone())
+                                                for grp in opt.groups}, opt.t, int(opt.clock.t.item())))
+    assert runs[0][3] == runs[1][3] == runs[1][4] == 9
+    assert torch.equal(runs[0][0], runs[1][0]), (runs[0][0], runs[1][0])
+    for k in runs[0][1]:
+        assert torch.equal(runs[0][1][k], runs[1][1][k]), k
+    for name in runs[0][2]:
+        for a, b in zip(runs[0][2][name], runs[1][2][name]):
+            assert torch.equal(a, b), name
