@@ -376,6 +376,19 @@ int grk_gemm(int trans_a, int trans_b, int64_t m, int64_t n, int64_t k, const vo
  * with no timing: the same kernel in every process. */
 int grk_gemm_tuning(int candidates);
 
+/* Weight gradient of a dense layer (the dW / db half of autograd for
+ * nn.Linear / Conv1d(k=1), model/BaseLine/model.py:65-78,129-139,302-309 and
+ * the HSTU projections, under bf16 autocast):
+ *   dw[m][n] = sum_k dy[k][m] * x[k][n]      (fp32 accumulation; dw fp32 or bf16)
+ *   db[m]    = sum_k dy[k][m]                (fp32; NULL = not wanted)
+ * dy [k, m] and x [k, n] bf16 row-major (row strides ld_dy, ld_x, multiples of
+ * 8; 16-byte aligned), m and n multiples of 8.  Split-K MFMA kernel + an
+ * in-order slice reduction: deterministic.  workspace: caller-owned device
+ * memory of grk_wgrad_workspace(k, m, n) bytes. */
+size_t grk_wgrad_workspace(int64_t k, int64_t m, int64_t n);
+int grk_wgrad(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, int64_t k, int64_t m, int64_t n, void* dw,
+              int64_t ld_dw, int dw_dtype, float* db, void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

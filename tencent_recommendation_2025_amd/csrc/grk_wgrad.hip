@@ -1,0 +1,267 @@
+// Weight gradients of the dense layers on MFMA (gfx950).
+//
+//   dW[M, N] = dY^T X          db[M] = sum_k dY[k, m]
+//   dY [K, M], X [K, N]: bf16 row-major, K = tokens (25,728 - 51,456 at
+//   BASELINE config 2), M, N = 512 - 2048 features; dW fp32 (the master
+//   weights' dtype) or bf16.
+//
+// Replaces the weight-gradient GEMM autograd runs for every nn.Linear /
+// Conv1d(k=1) of the model under bf16 autocast (model/BaseLine/model.py:65-78,
+// 129-139, 302-309; the HSTU uvqk / output projections) and the bias-gradient
+// column sum beside it.  hipBLASLt tiles this shape (small output, long
+// reduction) with one workgroup per 256-wide output tile: 4 to 16 workgroups
+// for 256 CUs, 140-410 TF/s in the bench step.  Here the reduction is split
+// into S slices so that a launch has ~512 workgroups:
+//  * one 256-thread workgroup = one 128x128 output tile of one K slice; each
+//    wave accumulates a 64x64 quarter in registers (2x2 MFMA 32x32x16 tiles);
+//  * both operands are K-major in memory: 32-row K steps of dY and X are
+//    staged as they lie (coalesced 256-B rows, XOR-swizzled) into a double
+//    LDS buffer (the next step's global loads in flight under the MFMAs) and read as MFMA fragments with ds_read_b64_tr_b16 (the same
+//    k permutation for both operands, so the product still sums over k);
+//  * every slice writes its fp32 partial tile with plain stores and
+//    k_wgrad_reduce sums the slices in slice order -- deterministic, no
+//    atomics; db comes from the dY tiles the n = 0 workgroups stage anyway.
+#include <algorithm>
+
+#include "grk_common.h"
+#include "grk_mfma.h"
+
+namespace grk {
+namespace {
+
+constexpr int kWgTile = 128;                    // output rows / cols per workgroup
+constexpr int kWgK = 32;                        // K rows per step
+constexpr int kWgImg = kWgK * kWgTile * 2;      // one staged [32][128] bf16 image (8 KiB)
+
+// 256-byte rows; the XOR keeps the 16-B row writes and the transposed
+// 32x32x16 fragment reads conflict-free (cdna_hip_programming.md T10, layout (b)).
+__device__ __forceinline__ int wg_off(int row, int ch) {
+  return row * (kWgTile * 2) + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+// Fragment over the 16 k rows [k0, k0+16) for output index c0 + r:
+// element j of lane (r, h) = img[k0 + 8(j>>2) + 4h + (j&3)][c0 + r].
+__device__ __forceinline__ bf16x8 wg_frag(const char* img, int k0, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
+  const int row = k0 + 4 * (g >> 1) + (i >> 2);
+  const int sub = 2 * (col & 7);
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + wg_off(row, col >> 3) + sub));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + wg_off(row + 8, col >> 3) + sub));
+  const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
+  bf16x8 f;
+  f[0] = l4[0]; f[1] = l4[1]; f[2] = l4[2]; f[3] = l4[3];
+  f[4] = h4[0]; f[5] = h4[1]; f[6] = h4[2]; f[7] = h4[3];
+  return f;
+}
+
+template <bool DB>
+__global__ void __launch_bounds__(256) k_wgrad(const bf16_t* __restrict__ A, int64_t lda,
+                                               const bf16_t* __restrict__ B, int64_t ldb, int K, int M, int N,
+                                               int kchunk, float* __restrict__ part, float* __restrict__ dbpart) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * kWgImg];  // [buffer 0 / 1][dY, X]: 32 KiB
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 1, wn = w >> 1, r = lane & 31, hh = lane >> 5;
+  const int n0 = blockIdx.x * kWgTile, m0 = blockIdx.y * kWgTile, s = blockIdx.z;
+  const int kb = s * kchunk, ke = min(K, kb + kchunk);
+  const int nsteps = ke > kb ? (ke - kb + kWgK - 1) / kWgK : 0;
+  const bool do_db = DB && blockIdx.x == 0;
+  const int ch = tid & 15, row0 = tid >> 4;  // this thread's 16-B column chunk and first staged row
+  const bool mok = m0 + 8 * ch < M, nok = n0 + 8 * ch < N;
+  const bf16_t* pa = A + m0 + 8 * ch;
+  const bf16_t* pb = B + n0 + 8 * ch;
+  constexpr int NC = kWgK / 16;  // staged rows per thread per step
+  uint4 ra[NC], rb[NC];
+  float cs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  auto load = [&](int step, uint4* xa, uint4* xb) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int k = kb + step * kWgK + row0 + 16 * c;
+      const bool ok = k < ke;
+      xa[c] = ok && mok ? *reinterpret_cast<const uint4*>(pa + (int64_t)k * lda) : make_uint4(0, 0, 0, 0);
+      xb[c] = ok && nok ? *reinterpret_cast<const uint4*>(pb + (int64_t)k * ldb) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto stage = [&](int buf, const uint4* xa, const uint4* xb) {
+    char* ia = smem + buf * 2 * kWgImg;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      *reinterpret_cast<uint4*>(ia + wg_off(row0 + 16 * c, ch)) = xa[c];
+      *reinterpret_cast<uint4*>(ia + kWgImg + wg_off(row0 + 16 * c, ch)) = xb[c];
+      if (do_db) {
+        const unsigned u[4] = {xa[c].x, xa[c].y, xa[c].z, xa[c].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          cs[2 * e] += __uint_as_float(u[e] << 16);
+          cs[2 * e + 1] += __uint_as_float(u[e] & 0xFFFF0000u);
+        }
+      }
+    }
+  };
+
+  if (nsteps > 0) {
+    load(0, ra, rb);
+    stage(0, ra, rb);
+  }
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    if (step + 1 < nsteps) load(step + 1, ra, rb);
+    const char* ia = smem + cur * 2 * kWgImg;
+    const char* ib = ia + kWgImg;
+#pragma unroll
+    for (int ks = 0; ks < kWgK / 16; ++ks) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = wg_frag(ia, 16 * ks, 64 * wm + 32 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = wg_frag(ib, 16 * ks, 64 * wn + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
+    }
+    if (step + 1 < nsteps) stage(cur ^ 1, ra, rb);
+    __syncthreads();
+  }
+
+  // partial tile of slice s: lane (r, hh) holds rows m = ... + acc_row(e, hh), column n = ... + r
+  float* out = part + (int64_t)s * M * N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + 64 * wn + 32 * j + r;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + 64 * wm + 32 * i + acc_row(e, hh);
+        if (m < M && n < N) out[(int64_t)m * N + n] = acc[i][j][e];
+      }
+    }
+  if (do_db) {  // the 16 threads of one column chunk hold staged rows row0 = 0..15: summed in row order
+    float* red = reinterpret_cast<float*>(smem);  // [16][128], free after the loop's last barrier
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[row0 * kWgTile + 8 * ch + e] = cs[e];
+    __syncthreads();
+    if (tid < kWgTile && m0 + tid < M) {
+      float t = 0.f;
+      for (int q = 0; q < 16; ++q) t += red[q * kWgTile + tid];
+      dbpart[(int64_t)s * M + m0 + tid] = t;
+    }
+  }
+}
+
+__device__ __forceinline__ void wg_store4(float* p, const float4& v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ void wg_store4(bf16_t* p, const float4& v) {
+  uint2 t;
+  t.x = (unsigned)f32_to_bf16(v.x) | ((unsigned)f32_to_bf16(v.y) << 16);
+  t.y = (unsigned)f32_to_bf16(v.z) | ((unsigned)f32_to_bf16(v.w) << 16);
+  *reinterpret_cast<uint2*>(p) = t;
+}
+
+// out[m][n] = sum over slices s = 0, 1, ... of part[s][m][n]; db[m] likewise.
+template <typename OT>
+__global__ void __launch_bounds__(256) k_wgrad_reduce(const float* __restrict__ part, int S, int M, int N,
+                                                      OT* __restrict__ out, int64_t ldo,
+                                                      const float* __restrict__ dbpart, float* __restrict__ db) {
+  const int64_t n4 = N / 4, total = (int64_t)M * n4, mn = (int64_t)M * N;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < total; u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = u / n4;
+    const int64_t n = (u - m * n4) * 4;
+    const float* p = part + m * N + n;
+    float4 a = *reinterpret_cast<const float4*>(p);
+    int s = 1;
+    for (; s + 4 <= S; s += 4) {  // four slices' loads in flight, added in slice order
+      float4 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const float4*>(p + (s + q) * mn);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a.x += v[q].x;
+        a.y += v[q].y;
+        a.z += v[q].z;
+        a.w += v[q].w;
+      }
+    }
+    for (; s < S; ++s) {
+      const float4 v = *reinterpret_cast<const float4*>(p + s * mn);
+      a.x += v.x;
+      a.y += v.y;
+      a.z += v.z;
+      a.w += v.w;
+    }
+    wg_store4(out + m * ldo + n, a);
+  }
+  if (db && blockIdx.x == 0)
+    for (int m = threadIdx.x; m < M; m += blockDim.x) {
+      float t = 0.f;
+      for (int s = 0; s < S; ++s) t += dbpart[(int64_t)s * M + m];
+      db[m] = t;
+    }
+}
+
+// K slices: about two workgroups per CU (latency hiding), slices of >= 512 rows.
+int wgrad_splits(int64_t K, int64_t M, int64_t N) {
+  const int64_t tiles = ((M + kWgTile - 1) / kWgTile) * ((N + kWgTile - 1) / kWgTile);
+  int S = 1;
+  while (S < 64 && tiles * S < 512 && K >= (int64_t)S * 2 * 512) S *= 2;
+  return S;
+}
+
+}  // namespace
+}  // namespace grk
+
+using namespace grk;
+
+extern "C" size_t grk_wgrad_workspace(int64_t k, int64_t m, int64_t n) {
+  if (k < 0 || m <= 0 || n <= 0) return 0;
+  const int S = wgrad_splits(k, m, n);
+  return ((size_t)S * m * n + (size_t)S * m) * sizeof(float);
+}
+
+extern "C" int grk_wgrad(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, int64_t k, int64_t m, int64_t n,
+                         void* dw, int64_t ld_dw, int dw_dtype, float* db, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(k >= 0 && m > 0 && n > 0, "sizes must be k >= 0, m > 0, n > 0");
+  GRK_CHECK_ARG(m % 8 == 0 && n % 8 == 0, "m and n must be multiples of 8");
+  GRK_CHECK_ARG(k < ((int64_t)1 << 31) && m < (1 << 24) && n < (1 << 24), "GEMM too large");
+  GRK_CHECK_ARG(k == 0 || (dy && x), "dy and x are required");
+  GRK_CHECK_ARG(dw && workspace, "dw and workspace are required");
+  GRK_CHECK_ARG(ld_dy >= m && ld_x >= n && ld_dy % 8 == 0 && ld_x % 8 == 0,
+                "row strides must cover the rows and be multiples of 8");
+  GRK_CHECK_ARG((uintptr_t)dy % 16 == 0 && (uintptr_t)x % 16 == 0, "dy / x must be 16-byte aligned");
+  GRK_CHECK_ARG(dw_dtype == GRK_F32 || dw_dtype == GRK_BF16, "dw must be fp32 or bf16");
+  GRK_CHECK_ARG(ld_dw >= n && ld_dw % 4 == 0, "ld_dw must be >= n and a multiple of 4");
+  GRK_CHECK_ARG(workspace_bytes >= grk_wgrad_workspace(k, m, n), "workspace smaller than grk_wgrad_workspace()");
+  const int S = wgrad_splits(k, m, n);
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  float* dbp = part + (size_t)S * m * n;
+  const int kchunk = (int)(((k + S - 1) / S + kWgK - 1) / kWgK * kWgK);
+  const dim3 grid((unsigned)((n + kWgTile - 1) / kWgTile), (unsigned)((m + kWgTile - 1) / kWgTile), (unsigned)S);
+  if (db)
+    k_wgrad<true><<<grid, 256, 0, s>>>((const bf16_t*)dy, ld_dy, (const bf16_t*)x, ld_x, (int)k, (int)m, (int)n,
+                                       kchunk, part, dbp);
+  else
+    k_wgrad<false><<<grid, 256, 0, s>>>((const bf16_t*)dy, ld_dy, (const bf16_t*)x, ld_x, (int)k, (int)m, (int)n,
+                                        kchunk, part, nullptr);
+  GRK_LAUNCH_CHECK();
+  const int64_t work = m * n / 4;
+  const unsigned g = (unsigned)std::min<int64_t>((work + 255) / 256, 4096);
+  if (dw_dtype == GRK_F32)
+    k_wgrad_reduce<float><<<g, 256, 0, s>>>(part, S, (int)m, (int)n, (float*)dw, ld_dw, db ? dbp : nullptr, db);
+  else
+    k_wgrad_reduce<bf16_t><<<g, 256, 0, s>>>(part, S, (int)m, (int)n, (bf16_t*)dw, ld_dw, db ? dbp : nullptr, db);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}

@@ -168,9 +168,16 @@ class _LinearFn(torch.autograd.Function):
         if not g2.is_contiguous():
             g2 = g2.contiguous()
         dx = K.gemm(g2, wb).view(shp) if ctx.needs_input_grad[0] else None
-        dw = K.gemm(g2, x2, trans_a=True, out_dtype=torch.float32 if wdt == torch.float32 else torch.bfloat16) \
-            if ctx.needs_input_grad[1] else None
-        db = g2.sum(0, dtype=torch.float32).to(bdt) if ctx.needs_input_grad[2] else None
+        dw_dt = torch.float32 if wdt == torch.float32 else torch.bfloat16
+        dw = db = None
+        if ctx.needs_input_grad[1] and K.wgrad_ok(g2, x2):
+            # split-K MFMA weight gradient, bias gradient from the same pass over gy
+            dw, db = K.wgrad(g2, x2, out_dtype=dw_dt, want_db=ctx.needs_input_grad[2])
+            db = db.to(bdt) if db is not None else None
+        elif ctx.needs_input_grad[1]:
+            dw = K.gemm(g2, x2, trans_a=True, out_dtype=dw_dt)
+        if ctx.needs_input_grad[2] and db is None:
+            db = g2.sum(0, dtype=torch.float32).to(bdt)
         return dx, dw, db, (gy if want_addend else None)
 
 

@@ -376,6 +376,34 @@ def gemm(a, b, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat16,
     return out
 
 
+def wgrad(dy, x, out_dtype=torch.float32, want_db=False):
+    """grk_wgrad: (dW = dy^T x [M, N] in out_dtype, db = column sums of dy [M] fp32 or None)
+    for dy [K, M] and x [K, N] bf16 row-major (the weight / bias gradients of x @ W^T + b)."""
+    _require_cuda(dy, x)
+    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or dy.dim() != 2 or x.dim() != 2:
+        raise L.GrkError('wgrad operands must be bf16 2-D matrices')
+    if dy.stride(1) != 1 or x.stride(1) != 1 or dy.shape[0] != x.shape[0]:
+        raise L.GrkError('wgrad operands must be row-major with the same number of rows')
+    k, m = dy.shape
+    n = x.shape[1]
+    dev = dy.device
+    ws = torch.empty(max(L.lib().grk_wgrad_workspace(k, m, n), 16), dtype=torch.uint8, device=dev)
+    dw = torch.empty(m, n, dtype=out_dtype, device=dev)
+    db = torch.empty(m, dtype=torch.float32, device=dev) if want_db else None
+    rc = L.lib().grk_wgrad(dy.data_ptr(), max(dy.stride(0), m), x.data_ptr(), max(x.stride(0), n), k, m, n,
+                           dw.data_ptr(), n, L.dtype_code(out_dtype), _ptr(db), ws.data_ptr(), ws.numel(),
+                           L.stream_ptr(dev))
+    L.check(rc, 'grk_wgrad')
+    return dw, db
+
+
+def wgrad_ok(dy, x):
+    """Shapes / strides / alignment grk_wgrad takes (else the hipBLASLt GEMM path)."""
+    return (dy.dim() == 2 and x.dim() == 2 and dy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0
+            and dy.stride(1) == 1 and x.stride(1) == 1 and max(dy.stride(0), dy.shape[1]) % 8 == 0
+            and max(x.stride(0), x.shape[1]) % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
+
+
 def gemm_tuning(candidates):
     """grk_gemm_tuning: hipBLASLt candidates timed per new GEMM shape (1 = heuristic pick, no timing)."""
     L.check(L.lib().grk_gemm_tuning(int(candidates)), 'grk_gemm_tuning')
