@@ -58,7 +58,7 @@ def parse():
                     help='gloo: rehearse N ranks on fewer GPUs (collectives staged via host)')
     ap.add_argument('--sharded', type=int, default=None, help='force the row-sharded optimizer (default: N > 1)')
     ap.add_argument('--graph', type=int, default=1,
-                    help='capture the training step in a HIP graph and replay it (unsharded path)')
+                    help='capture the training step in a HIP graph and replay it (row-sharded: forward + backward)')
     return ap.parse_args()
 
 
@@ -276,7 +276,7 @@ def main():
         opt = ShardedFusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
     else:
         opt = FusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
-    trainer = Trainer(model, opt, loss=a.loss, graph=bool(a.graph) and not sharded)
+    trainer = Trainer(model, opt, loss=a.loss, graph=bool(a.graph))
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [S.make_batch(cfg, gen, dev) for _ in range(4)]
 
@@ -284,7 +284,7 @@ def main():
     for i in range(a.warmup):
         if i == 0:
             G.GATHER_TRACE = []          # record the fused-gather launches of one real (eager) step
-        trainer.step(pool[i % len(pool)])
+        trainer.step(pool[i % len(pool)], next_batch=pool[(i + 1) % len(pool)])
         if i == 0:
             trace, G.GATHER_TRACE = G.GATHER_TRACE, None
     torch.cuda.synchronize()
@@ -292,7 +292,7 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        loss = trainer.step(pool[i % len(pool)])
+        loss = trainer.step(pool[i % len(pool)], next_batch=pool[(i + 1) % len(pool)])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

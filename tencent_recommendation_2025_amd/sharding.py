@@ -28,6 +28,8 @@ the gradient reductions are the grk kernels.
 """
 from __future__ import annotations
 
+import dataclasses
+
 import torch
 import torch.distributed as dist
 
@@ -112,23 +114,26 @@ class ShardExchange:
         self.gather_fn = gather_fn
         self.plan = None
 
-    def route(self, ids):
-        """Phase 1 (before the single host sync): unique ids, owner order, counts."""
+    def route(self, ids, pg=None):
+        """Phase 1 (before the single host sync): unique ids, owner order, counts.
+        pg: communicator for the counts exchange (default: the table's)."""
         uniq, inverse = torch.unique(ids, sorted=True, return_inverse=True)
         owner = uniq % self.world
         order = torch.argsort(owner, stable=True)
         send_ids = uniq[order]
         send_counts = torch.bincount(owner, minlength=self.world)
         recv_counts = torch.empty_like(send_counts)
-        a2a(recv_counts, send_counts, pg=self.pg)
+        a2a(recv_counts, send_counts, pg=self.pg if pg is None else pg)
         return dict(uniq=uniq, inverse=inverse, order=order, send_ids=send_ids, send_counts=send_counts,
                     recv_counts=recv_counts)
 
-    def fetch(self, r, send_split, recv_split, before_gather=None):
+    def fetch(self, r, send_split, recv_split, before_gather=None, out=None):
         """Phase 2: ids to owners, owners gather, rows back; returns rows in uniq order.
 
         before_gather(local ids) runs on the owner before its gather (the
-        deferred-AdamW catch-up of the requested rows)."""
+        deferred-AdamW catch-up of the requested rows).  out: a buffer of at
+        least len(uniq) rows to receive them (a fixed buffer lets a captured
+        forward read the rows of every step)."""
         recv_ids = r['send_ids'].new_empty(sum(recv_split))
         a2a(recv_ids, r['send_ids'], recv_split, send_split, self.pg)
         local = recv_ids // self.world
@@ -137,8 +142,8 @@ class ShardExchange:
         rows = self.gather_fn(self.shard, local)
         back = rows.new_empty((len(r['uniq']), self.dim))
         a2a(back, rows, send_split, recv_split, self.pg)
-        fetched = torch.empty_like(back)
-        fetched[r['order']] = back
+        fetched = torch.empty_like(back) if out is None else out
+        fetched.index_copy_(0, r['order'], back)
         self.plan = dict(order=r['order'], send_split=send_split, recv_split=recv_split, recv_local=local,
                          n_uniq=len(r['uniq']))
         return fetched
@@ -185,6 +190,7 @@ class GradBuckets:
         dev = self.params[0].device if self.params else torch.device('cpu')
         self.flat = [torch.empty(sum(p.numel() for p in ps), dtype=torch.float32, device=dev) for ps in self.buckets]
         self.async_ok = dev.type == 'cuda' and dist.get_backend(pg) != 'gloo'
+        self.enabled = True  # off while a backward is being captured into a HIP graph
         self._reset()
         for p in self.params:
             p.register_post_accumulate_grad_hook(self._hook)
@@ -195,6 +201,8 @@ class GradBuckets:
         self.next = 0
 
     def _hook(self, p):
+        if not self.enabled:
+            return
         b = self.where[id(p)]
         self.ready[b] += 1
         while self.next < len(self.buckets) and self.ready[self.next] == len(self.buckets[self.next]):
@@ -259,7 +267,7 @@ class ShardedFusedAdamW(FusedAdamW):
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
                  table_dtype=torch.bfloat16, pg=None, gather_fn=kernel_gather, reduce_fn=kernel_reduce,
-                 dense_reduce_fn=kernel_dense_reduce, defer_period=16, bucket_bytes=32 << 20):
+                 dense_reduce_fn=kernel_dense_reduce, defer_period=16, bucket_bytes=32 << 20, lookahead=True):
         self.pg = pg
         self.world = dist.get_world_size(pg)
         self.rank = dist.get_rank(pg)
@@ -295,6 +303,15 @@ class ShardedFusedAdamW(FusedAdamW):
                 g.last = torch.zeros(g.rows, dtype=torch.int32, device=dev)
         params = [p for grp in self.dense.param_groups for p in grp['params']]
         self.buckets = GradBuckets(params, pg, bucket_bytes) if params else None
+        # fixed exchange buffers (rows fetched for a step, inverse indices): a captured
+        # forward reads them at the same addresses every step
+        self._fbuf, self._ibuf = {}, {}
+        # lookahead routing: the next batch's counts exchange on its own communicator
+        # and stream, so prepare() needs no device round trip
+        self.meta_pg = dist.new_group(backend=dist.get_backend(pg)) if lookahead else None
+        self._route_stream = None
+        self._ahead = None
+        self._captured = None
 
     def begin_step(self, batch):
         """Nothing: prepare() catches up the rows each owner is asked for."""
@@ -305,25 +322,74 @@ class ShardedFusedAdamW(FusedAdamW):
         return self.shards[name][0].flat
 
     # -- input dist -------------------------------------------------------
-    def prepare(self, batch):
-        """Fetch every row of the sharded tables this step's batch reads."""
+    @staticmethod
+    def _parts(batch):
+        """{table: [(index tensor the model looks up, lookup mode, ids it reads)]}."""
         seq, pos, neg, tt = batch[0], batch[1], batch[2], batch[3]
         seq, pos, neg = seq.long(), pos.long(), neg.long()
         tt = tt.to(seq.device)
-        parts = {
-            'item_emb': [(seq, L.IDX_ITEM_MASK, seq * (tt == 1)), (pos, L.IDX_PLAIN, pos), (neg, L.IDX_PLAIN, neg)],
-            'user_emb': [(seq, L.IDX_USER_MASK, seq * (tt == 2))],
+        return {
+            'item_emb': [(seq, L.IDX_ITEM_MASK, lambda: seq * (tt == 1)), (pos, L.IDX_PLAIN, lambda: pos),
+                         (neg, L.IDX_PLAIN, lambda: neg)],
+            'user_emb': [(seq, L.IDX_USER_MASK, lambda: seq * (tt == 2))],
         }
+
+    def _route_all(self, batch, pg):
         routed = {}
-        for name, plist in parts.items():
-            ids = torch.cat([v.reshape(-1) for _, _, v in plist])
-            routed[name] = self.shards[name][1].route(ids)
-        counts = torch.stack([torch.stack([routed[n]['send_counts'], routed[n]['recv_counts']]) for n in parts])
-        counts = counts.cpu().tolist()  # the one host sync of the step: all-to-all split sizes
+        for name, plist in self._parts(batch).items():
+            ids = torch.cat([v().reshape(-1) for _, _, v in plist])
+            routed[name] = self.shards[name][1].route(ids, pg)
+        counts = torch.stack([torch.stack([r['send_counts'], r['recv_counts']]) for r in routed.values()])
+        return routed, counts
+
+    def prefetch(self, batch):
+        """Route a coming batch ahead of its step (side stream, own communicator):
+        its prepare() then finds the all-to-all split sizes already on the host
+        instead of waiting for the device to drain.  Every rank must prefetch the
+        same sequence of batches."""
+        seq = batch[0]
+        if self.meta_pg is None or not seq.is_cuda or dist.get_backend(self.pg) == 'gloo':
+            return
+        main = torch.cuda.current_stream(seq.device)
+        if self._route_stream is None:
+            self._route_stream = torch.cuda.Stream(device=seq.device)
+        side = self._route_stream
+        side.wait_stream(main)  # the batch's tensors were produced on the main stream
+        with torch.cuda.stream(side):
+            routed, counts = self._route_all(batch, self.meta_pg)
+            host = torch.empty(counts.shape, dtype=counts.dtype, pin_memory=True)
+            host.copy_(counts, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(side)
+        self._ahead = (seq, routed, host, done)
+
+    def _buffer(self, cache, name, shape, dtype, dev):
+        t = cache.get(name)
+        if t is None or t.shape[0] < shape[0]:
+            t = cache[name] = torch.empty(shape, dtype=dtype, device=dev)
+        return t
+
+    def prepare(self, batch, key=None):
+        """Fetch every row of the sharded tables this step's batch reads.
+        key: the tensor prefetch() was given for this batch (default batch[0])."""
+        key = batch[0] if key is None else key
+        ahead, self._ahead = self._ahead, None
+        if ahead is not None and ahead[0] is key:
+            _, routed, host, done = ahead
+            done.synchronize()  # long done: the route ran during the previous step
+            counts = host.tolist()
+            main = torch.cuda.current_stream()
+            main.wait_event(done)
+            for r in routed.values():
+                for t in r.values():
+                    t.record_stream(main)
+        else:
+            routed, counts = self._route_all(batch, self.pg)
+            counts = counts.cpu().tolist()  # the one host sync of the step: all-to-all split sizes
         self.maybe_segment()
         remaps = {}
         self.sinks = {}
-        for gi, (name, plist) in enumerate(parts.items()):
+        for gi, (name, plist) in enumerate(self._parts(batch).items()):
             grp, ex = self.shards[name]
             r = routed[name]
             catchup = None
@@ -331,18 +397,43 @@ class ShardedFusedAdamW(FusedAdamW):
                 def catchup(local, grp=grp):
                     K.table_adamw_catchup(grp.flat, grp.exp_avg, grp.exp_avg_sq, grp.last, None, self.clock,
                                           local.contiguous())
-            fetched = ex.fetch(r, counts[gi][0], counts[gi][1], before_gather=catchup)
+            n_ids = r['inverse'].numel()
+            fbuf = self._buffer(self._fbuf, name, (n_ids, grp.dim), grp.flat.dtype, grp.flat.device)
+            fetched = ex.fetch(r, counts[gi][0], counts[gi][1], before_gather=catchup, out=fbuf)
+            inv_all = self._buffer(self._ibuf, name, (n_ids,), r['inverse'].dtype, grp.flat.device)
+            inv_all[:n_ids].copy_(r['inverse'])
             sink = FetchSink()
             self.sinks[name] = sink
             ref = G.TableRef(fetched, sink, 0)
             off = 0
-            for idx, mode, v in plist:
-                n = v.numel()
-                inv = r['inverse'][off:off + n].view(v.shape)
+            for idx, mode, _ in plist:
+                n = idx.numel()
+                inv = inv_all[off:off + n].view(idx.shape)
                 off += n
                 remaps[(name, idx.data_ptr(), mode)] = (ref, inv)
         self.model._remaps = remaps
         self._begun = self.t
+
+    # -- HIP graph capture of forward + backward (train.Trainer) ------------
+    def capture_state(self):
+        """After the forward + backward of a captured step: what its replays rewrite
+        in place (gradient sources of every group and sink, dense gradients)."""
+        self._captured = dict(
+            groups=[(g, list(g.pending), dict(g.dense_grads), g.token_type, g.seq_len) for g in self.replicated],
+            sinks={k: list(sk.sources) for k, sk in self.sinks.items()},
+            grads=[(p, p.grad) for grp in self.dense.param_groups for p in grp['params']])
+
+    def restore_captured(self):
+        """Before step() after a replay: point the groups, sinks and .grad back at the graph's buffers."""
+        c = self._captured
+        for g, pend, dg, tt, sl in c['groups']:
+            g.pending, g.dense_grads, g.token_type, g.seq_len = list(pend), dict(dg), tt, sl
+        self.sinks = {}
+        for k, src in c['sinks'].items():
+            self.sinks[k] = FetchSink()
+            self.sinks[k].sources = list(src)
+        for p, gr in c['grads']:
+            p.grad = gr
 
     # -- gradient sync + update -------------------------------------------
     @torch.no_grad()
@@ -372,7 +463,11 @@ class ShardedFusedAdamW(FusedAdamW):
         for name, (grp, ex) in self.shards.items():
             sink = self.sinks.get(name)
             if sink is not None and sink.sources and ex.plan is not None:
-                ug = self.dense_reduce_fn(sink.sources, ex.plan['n_uniq'], grp.dim, padding_idx=None)
+                nu = ex.plan['n_uniq']
+                # the lookups read a fixed buffer of >= nu rows; this step's ids index its first nu
+                srcs = [dataclasses.replace(sc, table_rows=nu) if isinstance(sc, K.GradSource) else sc
+                        for sc in sink.sources]
+                ug = self.dense_reduce_fn(srcs, nu, grp.dim, padding_idx=None)
                 if self.world > 1:
                     ug.mul_(inv_world)
                 local, rows = ex.push_grads(ug)

@@ -11,7 +11,14 @@ table kernels read the step and its hyper-parameters from the optimizer's
 ``DeviceClock``, torch's AdamW runs ``capturable``, and the batch is copied
 into the captured input buffers before each replay.  Segment work of the
 deferred table updates (every ``defer_period`` steps) runs eagerly between
-replays."""
+replays.
+
+With row-sharded tables (sharding.ShardedFusedAdamW) the all-to-all sizes
+change every step, so only the forward + backward is captured: the row
+exchange (``prepare``, into fixed buffers) runs eagerly before each replay and
+the gradient exchange + updates (``step``) after it.  Passing the next batch
+(``step(batch, next_batch)``) routes it one step ahead, so no step waits for
+the device to drain before its all-to-alls."""
 from __future__ import annotations
 
 import contextlib
@@ -72,14 +79,13 @@ class Trainer:
         self._static_loss = None
         self._warm = 0
         self._side = None
+        self._sharded = hasattr(optimizer, 'prepare')
 
     def _graph_blocker(self):
         if not torch.cuda.is_available():
             return 'needs a GPU'
         if getattr(self.opt, 'clock', None) is None:
             return 'the optimizer must keep a device clock (optim.FusedAdamW on the GPU)'
-        if hasattr(self.opt, 'prepare'):
-            return 'row-sharded tables exchange data-dependent row counts every step (eager only)'
         for m in self.model.modules():
             if getattr(m, 'dropout_rate', 0.0) and m.training:
                 return 'attention dropout draws a host-side seed per step'
@@ -95,10 +101,12 @@ class Trainer:
                 return G.bce_loss(h, pe, ne, ntt)
             return G.sampled_softmax_loss(h, pe, pos, ntt, self.temperature)
 
-    def eager_step(self, batch):
+    def eager_step(self, batch, next_batch=None):
         self.opt.zero_grad()
         if hasattr(self.opt, 'prepare'):  # row-sharded tables: fetch this batch's rows from their owners
             self.opt.prepare(batch)
+            if next_batch is not None:
+                self.opt.prefetch(next_batch)
         if hasattr(self.opt, 'begin_step'):  # deferred table updates: bring this batch's rows up to date
             self.opt.begin_step(batch)
         loss = self.compute_loss(batch)
@@ -106,25 +114,35 @@ class Trainer:
         self.opt.step()
         return loss.detach()
 
-    def step(self, batch):
+    def step(self, batch, next_batch=None):
+        """One training step; ``next_batch`` (optional) is the batch of the following
+        step, routed ahead when the tables are row-sharded."""
         if not self.graph:
-            return self.eager_step(batch)
+            return self.eager_step(batch, next_batch)
         if self._g is None:
             if self._warm < self.graph_warmup:
                 # warm-up on the stream the capture will use: GEMM plans tuned,
                 # per-stream workspaces and the caching allocator's blocks in place
                 self._warm += 1
-                return self._on_side(lambda: self.eager_step(batch))
-            return self._capture(batch)
+                return self._on_side(lambda: self.eager_step(batch, next_batch))
+            return self._capture(batch, next_batch)
         src = _tensors(batch)
         dst = _tensors(self._static)
         if len(src) != len(dst) or any(a.shape != b.shape or a.dtype != b.dtype for a, b in zip(src, dst)):
-            return self.eager_step(batch)
+            return self.eager_step(batch, next_batch)
         for d, s in zip(dst, src):
             d.copy_(s, non_blocking=True)
-        self.opt.maybe_segment()
-        self._g.replay()
-        self.opt.graph_replayed()
+        if self._sharded:
+            self.opt.prepare(self._static, key=batch[0])
+            if next_batch is not None:
+                self.opt.prefetch(next_batch)
+            self._g.replay()
+            self.opt.restore_captured()
+            self.opt.step()
+        else:
+            self.opt.maybe_segment()
+            self._g.replay()
+            self.opt.graph_replayed()
         return self._static_loss.clone()
 
     def _on_side(self, fn):
@@ -137,18 +155,36 @@ class Trainer:
         cur.wait_stream(self._side)
         return out
 
-    def _capture(self, batch):
+    def _capture(self, batch, next_batch=None):
         """Record one step (host state advances once here), then replay it for this batch."""
         self._static = _clone_batch(batch)
-        self.opt.maybe_segment()
         self.opt.zero_grad(set_to_none=True)
+        if self._sharded:  # exchange eagerly, capture forward + backward only
+            self.opt.prepare(self._static, key=batch[0])
+            if next_batch is not None:
+                self.opt.prefetch(next_batch)
+            buckets = getattr(self.opt, 'buckets', None)
+            if buckets is not None:
+                buckets.enabled = False  # no collectives inside the graph: step() reduces the buckets
+        else:
+            self.opt.maybe_segment()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         cur = torch.cuda.current_stream()
         self._side.wait_stream(cur)
         with torch.cuda.graph(g, stream=self._side):
-            self._static_loss = self.eager_step(self._static)
+            if self._sharded:
+                loss = self.compute_loss(self._static)
+                loss.backward()
+                self._static_loss = loss.detach()
+            else:
+                self._static_loss = self.eager_step(self._static)
         cur.wait_stream(self._side)
         self._g = g
         g.replay()               # the captured step itself (host state already advanced)
+        if self._sharded:
+            if buckets is not None:
+                buckets.enabled = True
+            self.opt.capture_state()
+            self.opt.step()
         return self._static_loss.clone()
