@@ -17,7 +17,8 @@ import sys
 
 def category(name):
     if 'grk::' in name:
-        return 'grk:' + re.search(r'grk::(\w+)', name).group(1)
+        m = re.search(r'grk::(?:\(anonymous namespace\)::)?(\w+)', name)
+        return 'grk:' + (m.group(1) if m else name)
     if name.startswith('Cijk') or name.startswith('Custom_Cijk'):
         return 'GEMM (hipBLASLt)'
     if 'elementwise' in name:

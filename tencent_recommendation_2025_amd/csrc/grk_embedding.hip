@@ -193,10 +193,10 @@ __device__ __forceinline__ void load_row(Vec16<G>& r, unsigned long long ptr, in
   r.load(reinterpret_cast<const G*>(ptr) + c);
 }
 
-template <typename G>
-__device__ __forceinline__ void store_final(const RowVec<G>& acc, unsigned key, int64_t u, int dim, int c,
+template <typename A>
+__device__ __forceinline__ void store_final(const A& acc, unsigned key, int64_t u, int dim, int c,
                                             float* dense_out, float* uniq_rows, int32_t* row_slot) {
-  constexpr int VEC = RowVec<G>::VEC;
+  constexpr int VEC = A::VEC;
 #pragma unroll
   for (int e = 0; e < VEC; e += 4) {
     float4 r = make_float4(acc.v[e], acc.v[e + 1], acc.v[e + 2], acc.v[e + 3]);
@@ -206,9 +206,9 @@ __device__ __forceinline__ void store_final(const RowVec<G>& acc, unsigned key, 
   if (row_slot && c == 0) row_slot[key] = (int32_t)u;
 }
 
-template <typename G>
-__device__ __forceinline__ void store_slot(const RowVec<G>& acc, float* slot, int dim, int c) {
-  constexpr int VEC = RowVec<G>::VEC;
+template <typename A>
+__device__ __forceinline__ void store_slot(const A& acc, float* slot, int dim, int c) {
+  constexpr int VEC = A::VEC;
 #pragma unroll
   for (int e = 0; e < VEC; e += 4)
     *reinterpret_cast<float4*>(slot + c + e) = make_float4(acc.v[e], acc.v[e + 1], acc.v[e + 2], acc.v[e + 3]);
@@ -257,9 +257,9 @@ __global__ void __launch_bounds__(256) k_seg_chunks(const unsigned* __restrict__
     const int u = pos[ps] - 1;
     const int su = seg_start[u], eu = seg_end[u];
     if (su >= p0 && eu <= p1) {
-      store_final<G>(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
+      store_final(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
     } else if (eu - su > 2 * kRedChunk) {
-      store_slot<G>(acc, (ps == p0 ? slotA : slotB) + chunk * dim, dim, c);
+      store_slot(acc, (ps == p0 ? slotA : slotB) + chunk * dim, dim, c);
     }  // else: short row crossing a boundary -- k_seg_combine sums it sequentially
   };
   for (int64_t p = p0; p < p1; p += kRedPipe) {
@@ -334,7 +334,7 @@ __global__ void __launch_bounds__(256) k_seg_combine(const unsigned long long* _
           }
     }
   }
-  store_final<G>(acc, seg_key[u], u, dim, c, dense_out, uniq_rows, row_slot);
+  store_final(acc, seg_key[u], u, dim, c, dense_out, uniq_rows, row_slot);
 }
 
 // ------------------------------------ segmented reduction, one wave per row ----
@@ -367,7 +367,30 @@ __device__ __forceinline__ void load_row_global(Vec16<G>& r, unsigned long long 
   else r.v = make_float4(__uint_as_float(t.x), __uint_as_float(t.y), __uint_as_float(t.z), __uint_as_float(t.w));
 }
 
-template <typename G>
+// One lane's LW consecutive gradient elements of a row in the one-wave-per-row
+// kernels (64 * LW = dim): one 16-byte vector (bf16 x 8, fp32 x 4) or two (fp32 x 8).
+template <typename G, int LW>
+struct WaveVec {
+  static constexpr int PER = 16 / sizeof(G);
+  static constexpr int NV = LW / PER;
+  Vec16<G> r[NV];
+  __device__ __forceinline__ void load(unsigned long long ptr, int c) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) load_row_global<G>(r[i], ptr, c + i * PER);
+  }
+  __device__ __forceinline__ float get(int x) const { return r[x / PER].get(x % PER); }
+};
+template <int LW>
+struct WaveAcc {
+  static constexpr int VEC = LW;
+  float v[LW];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int e = 0; e < LW; ++e) v[e] = 0.f;
+  }
+};
+
+template <typename G, int LW>
 __global__ void __launch_bounds__(256) k_seg_chunks_wave(const unsigned* __restrict__ keys,
                                                          const unsigned long long* __restrict__ gptr,
                                                          const int* __restrict__ pos, const int* __restrict__ seg_start,
@@ -375,7 +398,7 @@ __global__ void __launch_bounds__(256) k_seg_chunks_wave(const unsigned* __restr
                                                          int dim, float* __restrict__ slotA, float* __restrict__ slotB,
                                                          float* __restrict__ dense_out, float* __restrict__ uniq_rows,
                                                          int32_t* __restrict__ row_slot) {
-  constexpr int VEC = RowVec<G>::VEC;
+  constexpr int VEC = LW;
   constexpr int KP = kRedChunk / 64;  // chunk entries per lane
   const int lane = threadIdx.x & 63;
   const int64_t chunk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -399,28 +422,28 @@ __global__ void __launch_bounds__(256) k_seg_chunks_wave(const unsigned* __restr
   if (cur == sentinel) return;
   const unsigned kprev = p0 > 0 ? keys[p0 - 1] : sentinel;
   const unsigned knext = p1 < n ? keys[p1] : sentinel;
-  RowVec<G> acc;
+  WaveAcc<LW> acc;
   acc.zero();
   int64_t ps = p0, pe = p0;          // current piece [ps, pe) of key cur
   int u = __builtin_amdgcn_readfirstlane(pr[0]) - 1;
   auto flush = [&]() {
     const bool whole = (ps > p0 || kprev != cur) && (pe < p1 || knext != cur);
     if (whole) {
-      store_final<G>(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
+      store_final(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
     } else if (seg_end[u] - seg_start[u] > 2 * kRedChunk) {
-      store_slot<G>(acc, (ps == p0 ? slotA : slotB) + chunk * dim, dim, c);
+      store_slot(acc, (ps == p0 ? slotA : slotB) + chunk * dim, dim, c);
     }  // else: short row crossing an edge -- k_seg_combine_edges sums it sequentially
   };
   bool done = false;
 #pragma unroll
   for (int k = 0; k < KP; ++k) {
     for (int s0 = 0; s0 < 64 && !done; s0 += kWavePipe) {
-      Vec16<G> r[kWavePipe];
+      WaveVec<G, LW> r[kWavePipe];
       unsigned kk[kWavePipe];
 #pragma unroll
       for (int j = 0; j < kWavePipe; ++j) {
         kk[j] = (unsigned)__builtin_amdgcn_readlane(kr[k], s0 + j);
-        load_row_global<G>(r[j], readlane64(glo[k], ghi[k], s0 + j), c);
+        r[j].load(readlane64(glo[k], ghi[k], s0 + j), c);
       }
 #pragma unroll
       for (int j = 0; j < kWavePipe; ++j) {
@@ -447,18 +470,18 @@ __global__ void __launch_bounds__(256) k_seg_chunks_wave(const unsigned* __restr
 
 // seq_sum for one wave: the row addresses of 64 occurrences at a time are
 // loaded into lanes and broadcast, kWavePipe rows in flight, in-order adds.
-template <typename G>
-__device__ __forceinline__ void seq_sum_wave(RowVec<G>& acc, const unsigned long long* __restrict__ gptr, int s, int e,
-                                             int lane, int c) {
-  constexpr int VEC = RowVec<G>::VEC;
+template <typename G, int LW>
+__device__ __forceinline__ void seq_sum_wave(WaveAcc<LW>& acc, const unsigned long long* __restrict__ gptr, int s,
+                                             int e, int lane, int c) {
+  constexpr int VEC = LW;
   for (int b = s; b < e; b += 64) {
     const unsigned long long g = gptr[b + lane < e ? b + lane : s];
     const unsigned lo = (unsigned)g, hi = (unsigned)(g >> 32);
     const int m = min(64, e - b);
     for (int s0 = 0; s0 < m; s0 += kWavePipe) {
-      Vec16<G> r[kWavePipe];
+      WaveVec<G, LW> r[kWavePipe];
 #pragma unroll
-      for (int j = 0; j < kWavePipe; ++j) load_row_global<G>(r[j], readlane64(lo, hi, s0 + j), c);
+      for (int j = 0; j < kWavePipe; ++j) r[j].load(readlane64(lo, hi, s0 + j), c);
 #pragma unroll
       for (int j = 0; j < kWavePipe; ++j)
         if (s0 + j < m)
@@ -470,7 +493,7 @@ __device__ __forceinline__ void seq_sum_wave(RowVec<G>& acc, const unsigned long
 
 // One wave per chunk edge b (occurrence b * kRedChunk): finishes the row that
 // first crosses a chunk edge at b, i.e. crosses b and starts in chunk b - 1.
-template <typename G>
+template <typename G, int LW>
 __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __restrict__ keys,
                                                            const unsigned long long* __restrict__ gptr,
                                                            const int* __restrict__ pos,
@@ -480,7 +503,7 @@ __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __res
                                                            const float* __restrict__ slotB,
                                                            float* __restrict__ dense_out, float* __restrict__ uniq_rows,
                                                            int32_t* __restrict__ row_slot) {
-  constexpr int VEC = RowVec<G>::VEC;
+  constexpr int VEC = LW;
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) + 1;
   const int64_t pb = b * kRedChunk;
@@ -492,10 +515,10 @@ __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __res
   if (su / kRedChunk != b - 1) return;  // also crosses an earlier edge: finished there
   const int c = lane * VEC;
   const int cs = (int)(b - 1), ce = (eu - 1) / kRedChunk;
-  RowVec<G> acc;
+  WaveAcc<LW> acc;
   acc.zero();
   if (eu - su <= 2 * kRedChunk) {
-    seq_sum_wave<G>(acc, gptr, su, eu, lane, c);
+    seq_sum_wave<G, LW>(acc, gptr, su, eu, lane, c);
   } else {
     const float* first = ((su % kRedChunk) == 0 ? slotA : slotB) + (int64_t)cs * dim + c;
 #pragma unroll
@@ -518,7 +541,7 @@ __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __res
           }
     }
   }
-  store_final<G>(acc, key, u, dim, c, dense_out, uniq_rows, row_slot);
+  store_final(acc, key, u, dim, c, dense_out, uniq_rows, row_slot);
 }
 
 // ------------------------------------------------------------ workspace ----
@@ -722,17 +745,20 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   const int groups = tpr >= 256 ? 1 : 256 / tpr;
   const int block = tpr >= 256 ? tpr : groups * tpr;
   const int64_t chunks = (total + kRedChunk - 1) / kRedChunk;
-  if (tpr == 64) {  // one wave per row
+  const int lw = dim % 64 == 0 ? dim / 64 : 0;  // elements per lane with one wave per row
+  if ((grad_dtype == GRK_BF16 && lw == 8) || (grad_dtype != GRK_BF16 && (lw == 4 || lw == 8))) {
     const unsigned gw = (unsigned)((chunks + 3) / 4);
     const unsigned ge = (unsigned)(chunks > 1 ? (chunks - 1 + 3) / 4 : 0);
-#define GRK_SEGW(G)                                                                                                  \
-  k_seg_chunks_wave<G><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,         \
-                                          sentinel, dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot);        \
+#define GRK_SEGW(G, LW)                                                                                              \
+  k_seg_chunks_wave<G, LW><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,     \
+                                              sentinel, dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot);    \
   GRK_LAUNCH_CHECK();                                                                                                \
   if (ge)                                                                                                            \
-    k_seg_combine_edges<G><<<ge, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,     \
-                                              sentinel, dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot)
-    if (grad_dtype == GRK_BF16) { GRK_SEGW(bf16_t); } else { GRK_SEGW(float); }
+    k_seg_combine_edges<G, LW><<<ge, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, \
+                                                  sentinel, dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot)
+    if (grad_dtype == GRK_BF16) { GRK_SEGW(bf16_t, 8); }
+    else if (lw == 8) { GRK_SEGW(float, 8); }
+    else { GRK_SEGW(float, 4); }
 #undef GRK_SEGW
     GRK_LAUNCH_CHECK();
     return GRK_OK;

@@ -233,11 +233,15 @@ class GradBuckets:
         else:
             all_reduce(flat, self.pg)
 
-    def finish(self):
-        """Issue the remaining buckets, wait, and make every p.grad the mean (a view of its bucket)."""
+    def launch_rest(self):
+        """Issue every bucket not issued yet (in bucket order)."""
         while self.next < len(self.buckets):
             self._launch(self.next)
             self.next += 1
+
+    def finish(self):
+        """Issue the remaining buckets, wait, and make every p.grad the mean (a view of its bucket)."""
+        self.launch_rest()
         inv = 1.0 / self.world
         for b, ps in enumerate(self.buckets):
             if self.works[b] is not None:
@@ -445,8 +449,24 @@ class ShardedFusedAdamW(FusedAdamW):
         self.clock.advance()
         hp = self.clock
         inv_world = 1.0 / self.world
-        # replicated tables (pos + feature tables): dense fp32 gradients in one buffer, all-reduce
-        # (mean) issued first, so it runs on RCCL's stream under the shard and dense updates below
+        # Order on RCCL's stream: the shard gradients' all-to-alls first (the owner
+        # updates wait on them), then the all-reduces of the replicated tables and the
+        # dense parameters, which run under the owner reductions and updates.
+        pushed = []
+        for name, (grp, ex) in self.shards.items():
+            sink = self.sinks.get(name)
+            if sink is not None and sink.sources and ex.plan is not None:
+                nu = ex.plan['n_uniq']
+                # the lookups read a fixed buffer of >= nu rows; this step's ids index its first nu
+                srcs = [dataclasses.replace(sc, table_rows=nu) if isinstance(sc, K.GradSource) else sc
+                        for sc in sink.sources]
+                ug = self.dense_reduce_fn(srcs, nu, grp.dim, padding_idx=None)
+                if self.world > 1:
+                    ug.mul_(inv_world)
+                pushed.append((grp, ex.push_grads(ug)))
+            elif not self.lazy and not self.defer:
+                K.table_adamw(grp.flat, grp.exp_avg, grp.exp_avg_sq, hp)
+        # replicated tables (pos + feature tables): dense fp32 gradients in one buffer
         dev = self.replicated[0].flat.device
         rep = torch.empty(self.rep_rows, self.replicated[0].dim, dtype=torch.float32, device=dev)
         row = 0
@@ -459,28 +479,17 @@ class ShardedFusedAdamW(FusedAdamW):
                 rep_work = dist.all_reduce(rep, group=self.pg, async_op=True)
             else:
                 all_reduce(rep, self.pg)
-        # sharded tables: per-unique-id grads -> owners -> owner reduction -> shard AdamW
-        for name, (grp, ex) in self.shards.items():
-            sink = self.sinks.get(name)
-            if sink is not None and sink.sources and ex.plan is not None:
-                nu = ex.plan['n_uniq']
-                # the lookups read a fixed buffer of >= nu rows; this step's ids index its first nu
-                srcs = [dataclasses.replace(sc, table_rows=nu) if isinstance(sc, K.GradSource) else sc
-                        for sc in sink.sources]
-                ug = self.dense_reduce_fn(srcs, nu, grp.dim, padding_idx=None)
-                if self.world > 1:
-                    ug.mul_(inv_world)
-                local, rows = ex.push_grads(ug)
-                src = [K.GradSource(local, rows, 0)]
-                res = self.reduce_fn(src, grp.rows, grp.dim, 0 if self.rank == 0 else -1,
-                                     None if self.lazy else grp.row_slot)
-                K.table_adamw(grp.flat, grp.exp_avg, grp.exp_avg_sq, hp, res.ids, res.rows, res.count, res.capacity,
-                              None if self.lazy else grp.row_slot, lazy=self.lazy or bool(self.defer))
-                if self.defer:
-                    K.stamp_rows(grp.last, res.ids, res.count, res.capacity, self.clock)
-            elif not self.lazy and not self.defer:
-                K.table_adamw(grp.flat, grp.exp_avg, grp.exp_avg_sq, hp)
-        # dense parameters: buckets were all-reduced during backward
+        if self.buckets is not None:
+            self.buckets.launch_rest()  # dense parameters (all of them when the backward was a graph replay)
+        # owners: reduce what arrived (rank order: deterministic), update the shard rows
+        for grp, (local, rows) in pushed:
+            src = [K.GradSource(local, rows, 0)]
+            res = self.reduce_fn(src, grp.rows, grp.dim, 0 if self.rank == 0 else -1,
+                                 None if self.lazy else grp.row_slot)
+            K.table_adamw(grp.flat, grp.exp_avg, grp.exp_avg_sq, hp, res.ids, res.rows, res.count, res.capacity,
+                          None if self.lazy else grp.row_slot, lazy=self.lazy or bool(self.defer))
+            if self.defer:
+                K.stamp_rows(grp.last, res.ids, res.count, res.capacity, self.clock)
         if self.buckets is not None:
             self.buckets.finish()
         self.dense.step()

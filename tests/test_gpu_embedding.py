@@ -181,7 +181,7 @@ def test_adamw_bf16_param(K):
     assert np.mean(got == oemb.to_bf16_f32(wp)) > 0.99
 
 
-@pytest.mark.parametrize('D,dt', [(256, torch.float32), (512, torch.bfloat16)])
+@pytest.mark.parametrize('D,dt', [(256, torch.float32), (512, torch.bfloat16), (512, torch.float32)])
 def test_backward_wave_path(K, D, dt):
     """dim == 64 x 16 bytes (one wave per row: k_seg_chunks_wave +
     k_seg_combine_edges): rows with <= 512 occurrences -- inside one chunk or
