@@ -470,16 +470,34 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
         } else {
           float rb[16];
           rab16(L.f0, myq, kb, hh, rb);
-          // d = myq - key >= -31: masked scores add 0 without a branch
-          unsigned long long* bb = bins + kRabPad + (myq - kb - 4 * hh) - 27;
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const float v = dp[i] * dsilu(fmaf(s[i], p.scale, rb[i])) * p.inv_n;
             ds[i] = ((mk >> i) & 1) ? v : 0.f;
           }
-          if (p.drab && __any(mk != 0))
+          if (p.drab && __any(mk != 0)) {
+            // drab bins by distance d = query - key.  The sub-tile's 1024 scores lie on
+            // 63 diagonals: lane r of each half gathers score (key k, query (r + k) & 31)
+            // of each of its 16 keys (one ds_bpermute each), whose distance is
+            // q0 - kb + r (no wrap) or q0 - kb + r - 32 (wrap); the halves are added
+            // and one lane per distance adds the two sums -- 2 LDS atomics per lane
+            // of the first half instead of 16 per lane.  Fixed order: deterministic.
+            float dhi = 0.f, dlo = 0.f;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) atomicAdd(&bb[27 - ((i & 3) + 8 * (i >> 2))], to_fix(ds[i]));
+            for (int i = 0; i < 16; ++i) {
+              const int k = acc_row(i, hh);
+              const float v = __shfl(ds[i], ((r + k) & 31) | (hh << 5));
+              if (r + k < 32) dhi += v;
+              else dlo += v;
+            }
+            dhi += __shfl_xor(dhi, 32);
+            dlo += __shfl_xor(dlo, 32);
+            if (hh == 0) {
+              unsigned long long* bd = bins + kRabPad + (q0 - kb) + r;
+              if (dhi != 0.f) atomicAdd(bd, to_fix(dhi));
+              if (dlo != 0.f) atomicAdd(bd - 32, to_fix(dlo));
+            }
+          }
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
