@@ -196,6 +196,46 @@ def gather_roofline(trace, reps):
     return res
 
 
+def item_gather_roofline(table, batch, reps):
+    """The item-table lookups of one bench batch (item tokens of seq, pos, neg;
+    padding dropped) through grk_embedding_gather from the 1M-row bf16 table:
+    random 1-KiB rows of a 1 GB table, read cold (the Infinity Cache is evicted
+    before every timed launch), so every row comes from HBM -- the north
+    star's "HBM-roofline on embedding gather" figure.  Algorithmic bytes =
+    rows x D x 2 read + rows x D x 2 written + 8 B of index per row."""
+    from tencent_recommendation_2025_amd import kernels as K
+    seq, pos, neg, tt = batch[0], batch[1], batch[2], batch[3]
+    ids = torch.cat([torch.where(tt == 1, seq, 0).reshape(-1), pos.reshape(-1), neg.reshape(-1)]).long()
+    ids = ids[ids > 0].contiguous()
+    n, D = ids.numel(), table.shape[1]
+    out = torch.empty(n, D, dtype=table.dtype, device=table.device)
+    lk = [K.Lookup(table, ids, 0)]
+    K.embedding_gather(lk, out, n)
+    # cold rows every launch: a 512 MiB stream (twice the Infinity Cache) evicts the
+    # table between the timed launches; each launch timed alone with HIP events
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device=table.device)
+    stream = torch.cuda.current_stream()
+    total = 0.0
+    for _ in range(reps):
+        flush.fill_(1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        K.embedding_gather(lk, out, n)
+        e1.record(stream)
+        e1.synchronize()
+        total += e0.elapsed_time(e1)
+    ms = total / reps
+    del flush
+    warm = _time(lambda: K.embedding_gather(lk, out, n), reps)  # same rows again: Infinity-Cache served
+    alg = 2 * n * D * table.element_size() + 8 * n
+    gbps = alg / (ms * 1e-3) / 1e9
+    return {'bound': 'hbm', 'kernel': 'grk::k_gather (item-table rows, 1M x 512 bf16)', 'achieved': round(gbps, 1),
+            'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': round(gbps / HBM_PEAK_GBPS, 4), 'traffic': None,
+            'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2), 'rows_per_launch': int(n),
+            'warm_cache_gbps': round(alg / (warm * 1e-3) / 1e9, 1),
+            'workload': {'rows': int(n), 'table_rows': int(table.shape[0]), 'D': int(D)}}
+
+
 def cpu_baseline(a, stats, types):
     """fp32 torch-CPU restatement (oracle/model_ref.py) of the same model + step, bounded sample."""
     from oracle import model_ref
@@ -310,6 +350,9 @@ def main():
     kv = (pool[0][3] != 0).to(torch.uint8)        # the first bench batch's key validity (token_type != 0)
     roof, more = attention_rooflines(a, kv, a.roofline_reps)
     more.append(gather_roofline(trace, a.roofline_reps))
+    item_table = model.item_emb.weight if model.item_emb.weight.numel() else None
+    if item_table is not None:
+        more.append(item_gather_roofline(item_table.detach(), pool[0], a.roofline_reps))
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline:
