@@ -130,8 +130,7 @@ class Trainer:
         dst = _tensors(self._static)
         if len(src) != len(dst) or any(a.shape != b.shape or a.dtype != b.dtype for a, b in zip(src, dst)):
             return self.eager_step(batch, next_batch)
-        for d, s in zip(dst, src):
-            d.copy_(s, non_blocking=True)
+        torch._foreach_copy_(dst, src, non_blocking=True)  # one multi-tensor kernel, not one copy per tensor
         if self._sharded:
             self.opt.prepare(self._static, key=batch[0])
             if next_batch is not None:
