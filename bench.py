@@ -211,13 +211,17 @@ def item_gather_roofline(table, batch, reps):
     out = torch.empty(n, D, dtype=table.dtype, device=table.device)
     lk = [K.Lookup(table, ids, 0)]
     K.embedding_gather(lk, out, n)
-    # cold rows every launch: a 512 MiB stream (twice the Infinity Cache) evicts the
-    # table between the timed launches; each launch timed alone with HIP events
-    flush = torch.empty(512 << 20, dtype=torch.uint8, device=table.device)
+    # cold rows every launch: READING a 512 MiB buffer (twice the Infinity Cache)
+    # evicts the table between the timed launches; a read leaves clean lines, so
+    # the timed launch pays no write-back of the evicting buffer (a fill would:
+    # it halves even a contiguous copy's rate, scripts/microbench/gather.hip).
+    # Each launch timed alone with HIP events.
+    flush = torch.ones(128 << 20, dtype=torch.int32, device=table.device)
+    sink = torch.empty((), dtype=torch.int64, device=table.device)
     stream = torch.cuda.current_stream()
     total = 0.0
     for _ in range(reps):
-        flush.fill_(1)
+        torch.sum(flush, dim=0, out=sink)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         K.embedding_gather(lk, out, n)
@@ -225,7 +229,7 @@ def item_gather_roofline(table, batch, reps):
         e1.synchronize()
         total += e0.elapsed_time(e1)
     ms = total / reps
-    del flush
+    del flush, sink
     warm = _time(lambda: K.embedding_gather(lk, out, n), reps)  # same rows again: Infinity-Cache served
     alg = 2 * n * D * table.element_size() + 8 * n
     gbps = alg / (ms * 1e-3) / 1e9
