@@ -43,7 +43,7 @@ __device__ __forceinline__ int64_t resolve_row(const I* idx, int64_t n, int32_t 
 // ---------------------------------------------------------------- gather ----
 // grid.y = feature; grid.x strides over (token, 16-byte chunk) units of that
 // feature.  Each lane moves one 16-byte vector per unit; UNROLL units are in
-// flight per lane.
+// flight per lane (the launcher uses 1, see grk_embedding_gather).
 template <typename T, typename I, int UNROLL>
 __global__ void __launch_bounds__(256) k_gather(FeatArgs args, int dim, int64_t num_tokens,
                                                 const int32_t* __restrict__ token_type, int32_t T_len,
@@ -632,28 +632,19 @@ extern "C" int grk_embedding_gather(const grk_feature* features, int num_feature
   if (num_tokens == 0) return GRK_OK;
   hipStream_t s = (hipStream_t)stream;
   const int64_t units = num_tokens * (dim / vec);
-  // Launches whose features are all single lookups take one (row, chunk) unit per
-  // lane over a wide grid: measured faster for cold random rows than 4 units per
-  // lane (scripts/microbench/gather.hip: 19 vs 32 us for 41k rows of 1 KiB);
-  // bag sums keep 4 units in flight per lane.
-  bool single = true;
-  for (int i = 0; i < num_features; ++i) single = single && features[i].bag == 1;
+  // One (row, chunk) unit per lane over a wide grid: measured faster than 4 units
+  // per lane both for cold random rows (scripts/microbench/gather.hip: 19 vs 32 us
+  // for 41k rows of 1 KiB) and for the bag sums of the fused seq-side lookup (97 vs 115 us).
   const int nf = num_features > 8 ? 8 : num_features;
-  dim3 grid(1, num_features);
-#define GRK_GATHER(T, I)                                                                                        \
-  if (single) {                                                                                                 \
-    grid.x = grid_for(units, 256, 8192 / nf + 1);                                                               \
-    k_gather<T, I, 1><<<grid, 256, 0, s>>>(fa, dim, num_tokens, token_type, seq_len, (T*)out, out_ld, err_flag); \
-  } else {                                                                                                      \
-    grid.x = grid_for((units + 3) / 4, 256, 4096 / nf + 1);                                                     \
-    k_gather<T, I, 4><<<grid, 256, 0, s>>>(fa, dim, num_tokens, token_type, seq_len, (T*)out, out_ld, err_flag); \
-  }
+  dim3 grid(grid_for(units, 256, 8192 / nf + 1), num_features);
+#define GRK_GATHER(T, I) \
+  k_gather<T, I, 1><<<grid, 256, 0, s>>>(fa, dim, num_tokens, token_type, seq_len, (T*)out, out_ld, err_flag)
   if (dtype == GRK_BF16) {
-    if (itype == GRK_I64) { GRK_GATHER(bf16_t, int64_t); }
-    else { GRK_GATHER(bf16_t, int32_t); }
+    if (itype == GRK_I64) GRK_GATHER(bf16_t, int64_t);
+    else GRK_GATHER(bf16_t, int32_t);
   } else {
-    if (itype == GRK_I64) { GRK_GATHER(float, int64_t); }
-    else { GRK_GATHER(float, int32_t); }
+    if (itype == GRK_I64) GRK_GATHER(float, int64_t);
+    else GRK_GATHER(float, int32_t);
   }
 #undef GRK_GATHER
   GRK_LAUNCH_CHECK();
