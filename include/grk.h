@@ -389,6 +389,29 @@ size_t grk_wgrad_workspace(int64_t k, int64_t m, int64_t n);
 int grk_wgrad(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, int64_t k, int64_t m, int64_t n, void* dw,
               int64_t ld_dw, int dw_dtype, float* db, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Exact maximum-inner-product top-k retrieval: the ANN step of inference
+ * (model/BaseLine/infer.py:213-225 runs an external faiss HNSW binary with
+ * --faiss_metric_type=0 (inner product) --query_ann_top_k=10 over the
+ * embedding.fbin / id.u64bin written by save_item_emb, model/BaseLine/
+ * model.py:402-433, and query.fbin; results read back by read_result_ids,
+ * infer.py:51-65).  Brute force on the GPU instead of a graph index:
+ *   for each query q: the k items i maximising dot(queries[q], items[i]),
+ *   ordered by score descending, ties by item index ascending.
+ * queries [num_queries, dim] and items [num_items, dim] row-major, both of
+ * `dtype` (GRK_F32 / GRK_BF16), row strides ld_q / ld_i (elements), 16-byte
+ * aligned rows; dim a multiple of 8 and <= 512; 1 <= k <= 16.
+ * Pass 1 scores every (query, item) pair with bf16 MFMA and keeps 16
+ * candidates per query per item slice; pass 2 re-scores the candidates in
+ * fp32 (fixed summation order) and selects the k best, so scores and order
+ * are those of fp32 arithmetic.  out_scores [num_queries, k] fp32, out_ids
+ * [num_queries, k] int64 = item_ids[i] (uint64 retrieval ids; NULL = the
+ * item index i); slots past num_items get id -1 and score -inf (as faiss).
+ * workspace: grk_mips_topk_workspace(num_queries, num_items) bytes. */
+size_t grk_mips_topk_workspace(int64_t num_queries, int64_t num_items);
+int grk_mips_topk(const void* queries, int64_t ld_q, const void* items, int64_t ld_i, int dtype,
+                  int64_t num_queries, int64_t num_items, int dim, int k, const uint64_t* item_ids,
+                  float* out_scores, int64_t* out_ids, void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -404,6 +404,33 @@ def wgrad_ok(dy, x):
             and max(x.stride(0), x.shape[1]) % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
 
 
+def mips_topk(queries, items, k, item_ids=None):
+    """grk_mips_topk: exact inner-product top-k of every query row over all item rows
+    (scores fp32 [Q, k] descending, ids int64 [Q, k]: item_ids[i] (uint64 retrieval
+    ids, as an int64 tensor) or the item row index; -1 / -inf past the item count)."""
+    _require_cuda(queries, items, item_ids)
+    if queries.dtype != items.dtype or queries.dtype not in (torch.float32, torch.bfloat16):
+        raise L.GrkError('queries and items must both be fp32 or both bf16')
+    if queries.dim() != 2 or items.dim() != 2 or queries.shape[1] != items.shape[1]:
+        raise L.GrkError('queries [Q, D] and items [N, D] must share D')
+    queries, items = queries.contiguous(), items.contiguous()
+    q, d = queries.shape
+    n = items.shape[0]
+    if item_ids is not None:
+        if item_ids.dtype not in (torch.int64, torch.uint64) or item_ids.numel() != n:
+            raise L.GrkError('item_ids must be a 64-bit integer tensor with one id per item row')
+        item_ids = item_ids.contiguous()
+    dev = queries.device
+    ws = torch.empty(max(L.lib().grk_mips_topk_workspace(q, n), 16), dtype=torch.uint8, device=dev)
+    scores = torch.empty(q, k, dtype=torch.float32, device=dev)
+    ids = torch.empty(q, k, dtype=torch.int64, device=dev)
+    rc = L.lib().grk_mips_topk(queries.data_ptr(), d, items.data_ptr(), d, L.dtype_code(queries.dtype), q, n, d,
+                               int(k), _ptr(item_ids), scores.data_ptr(), ids.data_ptr(), ws.data_ptr(), ws.numel(),
+                               L.stream_ptr(dev))
+    L.check(rc, 'grk_mips_topk')
+    return scores, ids
+
+
 def gemm_tuning(candidates):
     """grk_gemm_tuning: hipBLASLt candidates timed per new GEMM shape (1 = heuristic pick, no timing)."""
     L.check(L.lib().grk_gemm_tuning(int(candidates)), 'grk_gemm_tuning')

@@ -22,6 +22,13 @@ Fixtures:
   dataset.npz      -- ``MyDataset.__getitem__`` + ``collate_fn`` + ``feat2tensor``
                       outputs on a synthetic TencentGR directory.
   save_emb.bin     -- bytes written by the reference ``save_emb``.
+  retrieval.npz    -- retrieval file formats: item / id / query files written
+                      by the reference ``save_emb`` (as save_item_emb and
+                      infer.py:205-209 write them) and a result-id file read
+                      back by the reference ``read_result_ids`` (infer.py:51-65);
+                      the exact top-10 (float64) the HNSW search approximates.
+                      ``python tests/golden/make_golden.py retrieval`` writes
+                      only this fixture.
 """
 from __future__ import annotations
 
@@ -229,5 +236,31 @@ def main():
     print('torch', torch.__version__)
 
 
+def retrieval_golden():
+    ds_mod, base, _ = ref_modules()
+    sys.modules['model'] = base  # infer.py: `from model import BaselineModel`
+    infer = _load('ref_infer', REF / 'BaseLine' / 'infer.py')
+    from oracle.retrieval import mips_topk
+    rng = np.random.default_rng(7)
+    items = rng.standard_normal((300, 64)).astype(np.float32)
+    queries = rng.standard_normal((9, 64)).astype(np.float32)
+    ids = (rng.permutation(300) + 1000).astype(np.uint64).reshape(-1, 1)
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        for name, arr in (('items', items), ('queries', queries), ('ids', ids)):
+            ds_mod.save_emb(arr, Path(d, name))
+            out[f'{name}_bytes'] = np.frombuffer(Path(d, name).read_bytes(), dtype=np.uint8)
+        scores, top = mips_topk(queries, items, 10, ids.reshape(-1).astype(np.int64))
+        res = np.concatenate([np.array([9, 10], dtype=np.uint32).view(np.uint8),
+                              top.astype(np.uint64).view(np.uint8).reshape(-1)])
+        Path(d, 'res').write_bytes(res.tobytes())
+        read = infer.read_result_ids(Path(d, 'res'))
+    save('retrieval.npz', items=items, queries=queries, ids=ids, top10_scores=scores, top10_ids=top,
+         result_bytes=res, result_read_by_reference=read, **out)
+
+
 if __name__ == '__main__':
-    main()
+    if sys.argv[1:] == ['retrieval']:
+        retrieval_golden()
+    else:
+        main()
