@@ -75,6 +75,9 @@ def _time(fn, reps):
     return e0.elapsed_time(e1) / reps
 
 
+PMC_TAG = 'r1s2'  # round tag of the committed PMC summaries (scripts/pmc_rooflines.py)
+
+
 def _pmc(name, match):
     """HBM bytes per launch from a committed rocprofv3 PMC summary of the same workload (or None)."""
     path = os.path.join(REPO, 'profiles', name)
@@ -157,11 +160,11 @@ def attention_rooflines(a, key_valid, reps):
         return res
 
     dkdv = entry(f'grk::k_attn_dkdv_seq ({name} attention dK/dV, one layer)', t_dkdv,
-                 6 * n_valid * row + side, 8 * hd * pairs, f'r1_pmc_attn_dkdv_{name}.json')
+                 6 * n_valid * row + side, 8 * hd * pairs, f'{PMC_TAG}_pmc_attn_dkdv_{name}.json')
     fwd = entry(f'grk::k_attn_fwd_seq ({name} attention forward, one layer)', t_fwd,
-                4 * n_valid * row + side, 4 * hd * pairs, f'r1_pmc_attn_fwd_{name}.json')
+                4 * n_valid * row + side, 4 * hd * pairs, f'{PMC_TAG}_pmc_attn_fwd_{name}.json')
     dq = entry(f'grk::k_attn_dq_seq ({name} attention dQ{" + drab" if hstu else ""}, one layer)', t_dq,
-               5 * n_valid * row + side, 6 * hd * pairs, f'r1_pmc_attn_dq_{name}.json')
+               5 * n_valid * row + side, 6 * hd * pairs, f'{PMC_TAG}_pmc_attn_dq_{name}.json')
     fwd['survey_formula_flops'] = int(2 * B * D * T * (T + 1))  # 2*B*D*T(T+1) per layer fwd
     return dkdv, [fwd, dq]
 
@@ -189,7 +192,7 @@ def gather_roofline(trace, reps):
            'traffic': None, 'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2),
            'rows_per_launch': int(rows), 'features': len(lookups),
            'workload': {'tokens': int(n), 'rows': int(rows), 'features': len(lookups)}}
-    p = _pmc('r1_pmc_gather.json', res['workload'])
+    p = _pmc(f'{PMC_TAG}_pmc_gather.json', res['workload'])
     if p is not None:
         res['traffic'] = int(p['traffic_bytes_per_launch'])
         res['traffic_gbps'] = round(p['traffic_bytes_per_launch'] / (ms * 1e-3) / 1e9, 1)
@@ -233,11 +236,39 @@ def item_gather_roofline(table, batch, reps):
     warm = _time(lambda: K.embedding_gather(lk, out, n), reps)  # same rows again: Infinity-Cache served
     alg = 2 * n * D * table.element_size() + 8 * n
     gbps = alg / (ms * 1e-3) / 1e9
-    return {'bound': 'hbm', 'kernel': 'grk::k_gather (item-table rows, 1M x 512 bf16)', 'achieved': round(gbps, 1),
-            'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': round(gbps / HBM_PEAK_GBPS, 4), 'traffic': None,
-            'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2), 'rows_per_launch': int(n),
-            'warm_cache_gbps': round(alg / (warm * 1e-3) / 1e9, 1),
-            'workload': {'rows': int(n), 'table_rows': int(table.shape[0]), 'D': int(D)}}
+    res = {'bound': 'hbm', 'kernel': 'grk::k_gather (item-table rows, 1M x 512 bf16)', 'achieved': round(gbps, 1),
+           'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': round(gbps / HBM_PEAK_GBPS, 4), 'traffic': None,
+           'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2), 'rows_per_launch': int(n),
+           'warm_cache_gbps': round(alg / (warm * 1e-3) / 1e9, 1),
+           'workload': {'rows': int(n), 'table_rows': int(table.shape[0]), 'D': int(D)}}
+    p = _pmc(f'{PMC_TAG}_pmc_gather_item.json', res['workload'])
+    if p is not None:
+        res['traffic'] = int(p['traffic_bytes_per_launch'])
+    return res
+
+
+def wgrad_roofline(a, reps):
+    """grk_wgrad on the largest weight gradient of the step: the HSTU uvqk
+    projection (dW [4D, D] = dY^T X over K = B*T tokens, + bias gradient),
+    timed alone (HIP events; k_wgrad + its in-order slice reduction).  MFMA
+    bound: algorithmic FLOPs 2*K*M*N."""
+    from tencent_recommendation_2025_amd import kernels as K
+    k, m, n = a.batch * (a.maxlen + 1), 4 * a.hidden, a.hidden
+    g = torch.Generator(device='cuda').manual_seed(0)
+    dy = torch.randn(k, m, device='cuda', generator=g).bfloat16()
+    x = torch.randn(k, n, device='cuda', generator=g).bfloat16()
+    ms = _time(lambda: K.wgrad(dy, x, want_db=True), reps)
+    flops = 2 * k * m * n
+    tf = flops / (ms * 1e-3) / 1e12
+    res = {'bound': 'mfma', 'kernel': 'grk::k_wgrad + k_wgrad_reduce (uvqk weight + bias gradient)',
+           'achieved': round(tf, 1), 'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+           'frac': round(tf / BF16_PEAK_TFLOPS, 4), 'traffic': None, 'flops_per_launch': int(flops),
+           'alg_bytes_per_launch': int(2 * k * (m + n) + 4 * m * (n + 1)), 'avg_launch_us': round(ms * 1e3, 2),
+           'workload': {'K': int(k), 'M': int(m), 'N': int(n)}}
+    p = _pmc(f'{PMC_TAG}_pmc_wgrad.json', res['workload'])
+    if p is not None:
+        res['traffic'] = int(p['traffic_bytes_per_launch'])
+    return res
 
 
 def cpu_baseline(a, stats, types):
@@ -357,6 +388,7 @@ def main():
     item_table = model.item_emb.weight if model.item_emb.weight.numel() else None
     if item_table is not None:
         more.append(item_gather_roofline(item_table.detach(), pool[0], a.roofline_reps))
+    more.append(wgrad_roofline(a, a.roofline_reps))
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline:

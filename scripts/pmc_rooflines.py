@@ -49,18 +49,34 @@ line = [ln for ln in open(log) if ln.startswith('{"metric"')][-1]
 bench = json.loads(line)
 entries = [bench['roofline']] + bench.get('rooflines', [])
 fetch, write = counter_rows(fdir, 'FETCH_SIZE'), counter_rows(wdir, 'WRITE_SIZE')
+def traffic(needle, pick_largest_grid=False):
+    f, nf = per_launch(fetch, needle, pick_largest_grid)
+    w, nw = per_launch(write, needle, pick_largest_grid)
+    return 2 * f * 1024, w * 1024, min(nf, nw)
+
+
 for e in entries:
     k = e['kernel'].split()[0].replace('grk::', '')
-    needle = k + '<' if k.startswith('k_attn') else k
-    f, nf = per_launch(fetch, needle, k == 'k_gather')
-    w, nw = per_launch(write, needle, k == 'k_gather')
     if k.startswith('k_attn'):
+        fb, wb, n = traffic(k + '<')
         name = f"{tag}_pmc_attn_{k[len('k_attn_'):-len('_seq')]}_{e['workload']['kind']}.json"
-    else:
+    elif k == 'k_gather' and 'item-table' in e['kernel']:
+        fb, wb, n = traffic('k_gather')  # the last launches of the run: the item-table roofline's
+        name = f'{tag}_pmc_gather_item.json'
+    elif k == 'k_gather':
+        fb, wb, n = traffic('k_gather', True)  # widest launch: the seq-side fused lookup
         name = f'{tag}_pmc_gather.json'
-    out = {'kernel': k, 'workload': e['workload'], 'launches_averaged': min(nf, nw),
-           'fetch_bytes_per_launch': 2 * f * 1024, 'write_bytes_per_launch': w * 1024,
-           'traffic_bytes_per_launch': 2 * f * 1024 + w * 1024,
+    elif k == 'k_wgrad':
+        # one grk_wgrad call = k_wgrad + k_wgrad_reduce; the last launches are the roofline's
+        f1, w1, n1 = traffic('k_wgrad<')
+        f2, w2, n2 = traffic('k_wgrad_reduce')
+        fb, wb, n = f1 + f2, w1 + w2, min(n1, n2)
+        name = f'{tag}_pmc_wgrad.json'
+    else:
+        continue
+    out = {'kernel': k, 'workload': e['workload'], 'launches_averaged': n,
+           'fetch_bytes_per_launch': fb, 'write_bytes_per_launch': wb,
+           'traffic_bytes_per_launch': fb + wb,
            'alg_bytes_per_launch': e['alg_bytes_per_launch'],
            'method': 'rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH_SIZE x2 '
                      '(gfx950 wide-stream correction, MI355X_MICROARCH.md HBM), KiB -> bytes'}

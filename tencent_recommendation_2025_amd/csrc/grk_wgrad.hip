@@ -63,10 +63,19 @@ __global__ void __launch_bounds__(256) k_wgrad(const bf16_t* __restrict__ A, int
   __shared__ __attribute__((aligned(16))) char smem[4 * kWgImg];  // [buffer 0 / 1][dY, X]: 32 KiB
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w & 1, wn = w >> 1, r = lane & 31, hh = lane >> 5;
-  const int n0 = blockIdx.x * kWgTile, m0 = blockIdx.y * kWgTile, s = blockIdx.z;
+  // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs
+  // (physical id % 8), so logical tile ids are laid out XCD-major -- the n-tiles
+  // sharing one dY block and the m-tiles sharing one X block of a K-slice run
+  // on the same XCD and read them through its L2 once (PMC: 546 -> see DESIGN).
+  const unsigned nx = gridDim.x, my = gridDim.y;
+  const unsigned total = nx * my * gridDim.z;
+  const unsigned phys = blockIdx.x + nx * (blockIdx.y + my * blockIdx.z);
+  const unsigned logical = total % 8 == 0 ? (phys % 8) * (total / 8) + phys / 8 : phys;
+  const int bx = (int)(logical % nx), by = (int)((logical / nx) % my), s = (int)(logical / (nx * my));
+  const int n0 = bx * kWgTile, m0 = by * kWgTile;
   const int kb = s * kchunk, ke = min(K, kb + kchunk);
   const int nsteps = ke > kb ? (ke - kb + kWgK - 1) / kWgK : 0;
-  const bool do_db = DB && blockIdx.x == 0;
+  const bool do_db = DB && bx == 0;
   const int ch = tid & 15, row0 = tid >> 4;  // this thread's 16-B column chunk and first staged row
   const bool mok = m0 + 8 * ch < M, nok = n0 + 8 * ch < N;
   const bf16_t* pa = A + m0 + 8 * ch;
