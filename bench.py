@@ -52,7 +52,7 @@ def parse():
     ap.add_argument('--zipf', type=float, default=None)
     ap.add_argument('--cpu-baseline', type=int, default=1)
     ap.add_argument('--cpu-batch', type=int, default=8)
-    ap.add_argument('--cpu-steps', type=int, default=2)
+    ap.add_argument('--cpu-steps', type=int, default=6)
     ap.add_argument('--roofline-reps', type=int, default=20)
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='gloo: rehearse N ranks on fewer GPUs (collectives staged via host)')

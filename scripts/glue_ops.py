@@ -51,6 +51,14 @@ def main():
     print(f'device time over 2 steps: {tot / 1e3:.3f} ms (all kernels incl. grk)')
     for e in rows[:a.rows]:
         print(f'{e.self_device_time_total / 2e3:8.3f} ms/step {e.count / 2:5.1f}x  {e.key}  {e.input_shapes}')
+    print('\n# by call site (model-code frames)')
+    ks = prof.key_averages(group_by_stack_n=8)
+    rows = [e for e in ks if e.self_device_time_total > 0 and e.key.startswith('aten::')]
+    rows.sort(key=lambda e: -e.self_device_time_total)
+    for e in rows[:a.rows]:
+        fr = [f for f in e.stack if 'tencent_recommendation_2025_amd' in f or 'bench' in f][:3]
+        print(f'{e.self_device_time_total / 2e3:8.3f} ms/step {e.count / 2:5.1f}x  {e.key}  | ' + ' <- '.join(
+            f.split('/')[-1] for f in fr))
 
 
 if __name__ == '__main__':

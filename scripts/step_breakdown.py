@@ -42,6 +42,11 @@ def main():
           f'{len(sel) / last:.0f} launches/step')
     for k, v in sorted(cat.items(), key=lambda kv: -kv[1]):
         print(f'  {v / last:8.3f}  {100 * v / busy:5.1f}%  {k}')
+    gaps = sorted(((sel[i + 1][0] - sel[i][1], sel[i][2][:60], sel[i + 1][2][:60]) for i in range(len(sel) - 1)
+                   if sel[i + 1][0] > sel[i][1]), reverse=True)
+    print(f'# idle gaps: {sum(g[0] for g in gaps) / 1e6 / last:.3f} ms/step; largest (us, after -> before):')
+    for g, a, b in gaps[:12]:
+        print(f'  {g / 1e3:8.1f}  {a}  ->  {b}')
     print('# top kernels (ms/step, launches/step, avg us)')
     for k, (v, c) in sorted(top.items(), key=lambda kv: -kv[1][0])[:40]:
         print(f'  {v / last:8.3f} {c / last:5.1f} {1e3 * v / c:8.1f}  {k}')

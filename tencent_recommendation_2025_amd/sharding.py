@@ -116,12 +116,31 @@ class ShardExchange:
 
     def route(self, ids, pg=None):
         """Phase 1 (before the single host sync): unique ids, owner order, counts.
-        pg: communicator for the counts exchange (default: the table's)."""
-        uniq, inverse = torch.unique(ids, sorted=True, return_inverse=True)
-        owner = uniq % self.world
+        pg: communicator for the counts exchange (default: the table's).
+
+        Every output has a fixed size (len(ids)), so nothing here waits for the
+        device (torch.unique / bincount would: their output sizes are data
+        dependent): uniq holds the distinct ids ascending in its first n_uniq
+        slots, the tail is padding whose owner is the overflow bin ``world``, so
+        the stable owner order lists every real id first.  n_uniq reaches the
+        host as sum(send_counts) with the split sizes."""
+        n = ids.numel()
+        srt, perm = torch.sort(ids, stable=True)
+        head = torch.ones_like(srt, dtype=torch.bool)
+        if n > 1:
+            head[1:] = srt[1:] != srt[:-1]
+        upos = torch.cumsum(head, 0) - 1                 # unique index of each sorted occurrence
+        inverse = torch.empty_like(upos)
+        inverse[perm] = upos
+        uniq = torch.zeros_like(srt)
+        uniq.scatter_(0, upos, srt)                      # duplicates write the same value
+        n_uniq = upos[-1:] + 1 if n else upos.new_zeros(1)
+        owner = torch.where(torch.arange(n, device=ids.device) < n_uniq, uniq % self.world, self.world)
         order = torch.argsort(owner, stable=True)
         send_ids = uniq[order]
-        send_counts = torch.bincount(owner, minlength=self.world)
+        send_counts = torch.zeros(self.world + 1, dtype=torch.int64, device=ids.device)
+        send_counts.scatter_add_(0, owner, torch.ones_like(owner))
+        send_counts = send_counts[:self.world].contiguous()
         recv_counts = torch.empty_like(send_counts)
         a2a(recv_counts, send_counts, pg=self.pg if pg is None else pg)
         return dict(uniq=uniq, inverse=inverse, order=order, send_ids=send_ids, send_counts=send_counts,
@@ -132,20 +151,22 @@ class ShardExchange:
 
         before_gather(local ids) runs on the owner before its gather (the
         deferred-AdamW catch-up of the requested rows).  out: a buffer of at
-        least len(uniq) rows to receive them (a fixed buffer lets a captured
+        least n_uniq rows to receive them (a fixed buffer lets a captured
         forward read the rows of every step)."""
+        n_uniq = sum(send_split)
+        order = r['order'][:n_uniq]
         recv_ids = r['send_ids'].new_empty(sum(recv_split))
-        a2a(recv_ids, r['send_ids'], recv_split, send_split, self.pg)
+        a2a(recv_ids, r['send_ids'][:n_uniq], recv_split, send_split, self.pg)
         local = recv_ids // self.world
         if before_gather is not None and local.numel():
             before_gather(local)
         rows = self.gather_fn(self.shard, local)
-        back = rows.new_empty((len(r['uniq']), self.dim))
+        back = rows.new_empty((n_uniq, self.dim))
         a2a(back, rows, send_split, recv_split, self.pg)
         fetched = torch.empty_like(back) if out is None else out
-        fetched.index_copy_(0, r['order'], back)
-        self.plan = dict(order=r['order'], send_split=send_split, recv_split=recv_split, recv_local=local,
-                         n_uniq=len(r['uniq']))
+        fetched.index_copy_(0, order, back)
+        self.plan = dict(order=order, send_split=send_split, recv_split=recv_split, recv_local=local,
+                         n_uniq=n_uniq)
         return fetched
 
     def push_grads(self, uniq_grads):
@@ -313,8 +334,8 @@ class ShardedFusedAdamW(FusedAdamW):
         # lookahead routing: the next batch's counts exchange on its own communicator
         # and stream, so prepare() needs no device round trip
         self.meta_pg = dist.new_group(backend=dist.get_backend(pg)) if lookahead else None
-        self._route_stream = None
-        self._ahead = None
+        self.trace = None  # optional list: host-side diagnostics (scripts/host_issue.py)
+        self._ahead = []  # routed batches waiting for their prepare(), oldest first (at most 2)
         self._captured = None
 
     def begin_step(self, batch):
@@ -347,25 +368,35 @@ class ShardedFusedAdamW(FusedAdamW):
         return routed, counts
 
     def prefetch(self, batch):
-        """Route a coming batch ahead of its step (side stream, own communicator):
+        """Route a coming batch ahead of its step (own communicator for the counts):
         its prepare() then finds the all-to-all split sizes already on the host
         instead of waiting for the device to drain.  Every rank must prefetch the
         same sequence of batches."""
         seq = batch[0]
         if self.meta_pg is None or not seq.is_cuda or dist.get_backend(self.pg) == 'gloo':
             return
-        main = torch.cuda.current_stream(seq.device)
-        if self._route_stream is None:
-            self._route_stream = torch.cuda.Stream(device=seq.device)
-        side = self._route_stream
-        side.wait_stream(main)  # the batch's tensors were produced on the main stream
-        with torch.cuda.stream(side):
-            routed, counts = self._route_all(batch, self.meta_pg)
-            host = torch.empty(counts.shape, dtype=counts.dtype, pin_memory=True)
-            host.copy_(counts, non_blocking=True)
-            done = torch.cuda.Event()
-            done.record(side)
-        self._ahead = (seq, routed, host, done)
+        # On the current stream, in order: HIP serialises this process's streams on
+        # shared hardware queues, and a side stream's work waiting on the main
+        # stream was measured to run only after the whole queued step (the host
+        # then waited for it in prepare()); issued first in the step on the main
+        # stream it runs at once and is long done when prepare() reads the counts.
+        routed, counts = self._route_all(batch, self.meta_pg)
+        host = self._pinned_counts(counts)
+        host.copy_(counts, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record()
+        self._ahead = self._ahead[-1:] + [(seq, routed, host, done)]
+
+    def _pinned_counts(self, counts):
+        """Two pinned host buffers used in turn (prepare() has read the older one
+        before the next prefetch writes it)."""
+        ring = getattr(self, '_pinned_ring', None)
+        if ring is None or ring[0].shape != counts.shape:
+            ring = self._pinned_ring = [torch.empty(counts.shape, dtype=counts.dtype, pin_memory=True)
+                                        for _ in range(2)]
+            self._pinned_turn = 0
+        self._pinned_turn ^= 1
+        return ring[self._pinned_turn]
 
     def _buffer(self, cache, name, shape, dtype, dev):
         t = cache.get(name)
@@ -377,9 +408,12 @@ class ShardedFusedAdamW(FusedAdamW):
         """Fetch every row of the sharded tables this step's batch reads.
         key: the tensor prefetch() was given for this batch (default batch[0])."""
         key = batch[0] if key is None else key
-        ahead, self._ahead = self._ahead, None
-        if ahead is not None and ahead[0] is key:
+        ahead = next((a for a in self._ahead if a[0] is key), None)
+        self._ahead = [a for a in self._ahead if a is not ahead]
+        if ahead is not None:
             _, routed, host, done = ahead
+            if self.trace is not None:
+                self.trace.append(('route done at prepare', done.query()))
             done.synchronize()  # long done: the route ran during the previous step
             counts = host.tolist()
             main = torch.cuda.current_stream()

@@ -130,11 +130,14 @@ class Trainer:
         dst = _tensors(self._static)
         if len(src) != len(dst) or any(a.shape != b.shape or a.dtype != b.dtype for a, b in zip(src, dst)):
             return self.eager_step(batch, next_batch)
+        if self._sharded and next_batch is not None:
+            # route the next batch before anything of this step is queued: its side
+            # stream then waits only for the previous step, and prepare(next) finds
+            # the split sizes on the host a whole step early
+            self.opt.prefetch(next_batch)
         torch._foreach_copy_(dst, src, non_blocking=True)  # one multi-tensor kernel, not one copy per tensor
         if self._sharded:
             self.opt.prepare(self._static, key=batch[0])
-            if next_batch is not None:
-                self.opt.prefetch(next_batch)
             self._g.replay()
             self.opt.restore_captured()
             self.opt.step()
@@ -171,7 +174,10 @@ class Trainer:
         g = torch.cuda.CUDAGraph()
         cur = torch.cuda.current_stream()
         self._side.wait_stream(cur)
-        with torch.cuda.graph(g, stream=self._side):
+        # thread_local: the process group's watchdog thread polls its collectives'
+        # events while we capture; under the default global mode that poll is an
+        # illegal call during capture and aborts the process
+        with torch.cuda.graph(g, stream=self._side, capture_error_mode='thread_local'):
             if self._sharded:
                 loss = self.compute_loss(self._static)
                 loss.backward()
