@@ -412,6 +412,26 @@ int grk_mips_topk(const void* queries, int64_t ld_q, const void* items, int64_t 
                   int64_t num_queries, int64_t num_items, int dim, int k, const uint64_t* item_ids,
                   float* out_scores, int64_t* out_ids, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Negative sampling on the device: the per-position random negative of
+ * MyDataset.__getitem__ (model/BaseLine/dataset.py:136-162; _random_neq,
+ * :79-95) for a whole tensorised batch.  For every sequence b and position t
+ * with next_token_type == 1 and pos != 0: neg[b,t] = a uniform id in
+ * [1, num_items] not in excl[b, 0:excl_len] (0 entries ignored), redrawn up to
+ * max_tries (<= 65535) times (the reference redraws without bound; if every try is
+ * excluded the last draw is kept and bit 2 of *err_flag is set); other
+ * positions 0.  Draws are splitmix64(seed, b, t, attempt): deterministic, so
+ * oracle/sampler.py restates them bit-exactly (the reference's np.random
+ * stream is not reproducible on a GPU).  pos / next_token_type / neg int32
+ * [batch, seq_len], seq_len <= 65535; excl int32 [batch, excl_len], excl_len <= 4096.
+ * item_feat (optional, int32 [num_items + 1, num_feat], row 0 = the default
+ * feature values): neg_feat[b,t,:] = item_feat[neg[b,t],:] -- the
+ * fill_missing_feat(item_feat_dict[neg]) rows of dataset.py:161-162,
+ * tensorised. */
+int grk_sample_negatives(const int32_t* pos, const int32_t* next_token_type, int64_t batch, int32_t seq_len,
+                         const int32_t* excl, int32_t excl_len, int64_t num_items, uint64_t seed,
+                         int32_t max_tries, const int32_t* item_feat, int32_t num_feat, int32_t* neg,
+                         int32_t* neg_feat, int32_t* err_flag, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -235,6 +235,23 @@ def tensorize(feat_list, fids, array_fids=(), emb_fids=()):
     return out
 
 
+def sample_negatives(seq, pos, token_type, next_token_type, num_items, seed, item_feat=None, max_tries=1000):
+    """Negatives of a tensorised batch drawn on the device (grk_sample_negatives):
+    the neg / neg_feat of MyDataset.__getitem__ (model/BaseLine/dataset.py:136-162)
+    for every sequence at once, so DataLoader workers need not draw them.
+
+    The exclusion set of sequence b (the reference's ts, dataset.py:136-139) is
+    the item tokens of its window plus its positives -- every item of the user
+    the batch holds (items older than the maxlen window are not in the batch and
+    are not excluded).  item_feat: int32 [num_items + 1, F] item feature ids, row
+    0 = the default values (fill_missing_feat); returns (neg [B, T], neg_feat
+    [B, T, F] or None), int32 on the batch's device."""
+    from . import kernels as K
+    excl = torch.cat([torch.where(token_type == 1, seq, 0), pos], 1)
+    return K.sample_negatives(pos, next_token_type, excl, num_items, seed, max_tries=max_tries,
+                              item_feat=item_feat)
+
+
 class MyTestDataset(MyDataset):
     """Inference sequences (model/BaseLine/dataset.py:296-419)."""
 
