@@ -138,6 +138,12 @@ class ShardExchange:
         owner = torch.where(torch.arange(n, device=ids.device) < n_uniq, uniq % self.world, self.world)
         order = torch.argsort(owner, stable=True)
         send_ids = uniq[order]
+        # fetched rows and per-unique gradients live in owner order (slot s holds
+        # send_ids[s]): rows come back from the owners already in place and the
+        # gradients go out without a permutation; tokens index their id's slot
+        slot = torch.empty_like(order)
+        slot[order] = torch.arange(n, device=ids.device)
+        inverse = slot[inverse]
         send_counts = torch.zeros(self.world + 1, dtype=torch.int64, device=ids.device)
         send_counts.scatter_add_(0, owner, torch.ones_like(owner))
         send_counts = send_counts[:self.world].contiguous()
@@ -147,32 +153,30 @@ class ShardExchange:
                     recv_counts=recv_counts)
 
     def fetch(self, r, send_split, recv_split, before_gather=None, out=None):
-        """Phase 2: ids to owners, owners gather, rows back; returns rows in uniq order.
+        """Phase 2: ids to owners, owners gather, rows back; returns rows in slot (owner) order.
 
         before_gather(local ids) runs on the owner before its gather (the
         deferred-AdamW catch-up of the requested rows).  out: a buffer of at
         least n_uniq rows to receive them (a fixed buffer lets a captured
         forward read the rows of every step)."""
         n_uniq = sum(send_split)
-        order = r['order'][:n_uniq]
         recv_ids = r['send_ids'].new_empty(sum(recv_split))
         a2a(recv_ids, r['send_ids'][:n_uniq], recv_split, send_split, self.pg)
         local = recv_ids // self.world
         if before_gather is not None and local.numel():
             before_gather(local)
         rows = self.gather_fn(self.shard, local)
-        back = rows.new_empty((n_uniq, self.dim))
-        a2a(back, rows, send_split, recv_split, self.pg)
-        fetched = torch.empty_like(back) if out is None else out
-        fetched.index_copy_(0, order, back)
-        self.plan = dict(order=order, send_split=send_split, recv_split=recv_split, recv_local=local,
-                         n_uniq=n_uniq)
+        fetched = rows.new_empty((n_uniq, self.dim)) if out is None else out
+        a2a(fetched[:n_uniq], rows, send_split, recv_split, self.pg)
+        self.plan = dict(send_split=send_split, recv_split=recv_split, recv_local=local, n_uniq=n_uniq)
         return fetched
 
     def push_grads(self, uniq_grads):
-        """Route per-unique-id gradients [U, D] to the owners; returns (local ids, rows) received."""
+        """Route per-slot gradients [>= n_uniq, D] (slot order, as fetch() returned the
+        rows) to the owners; returns (local ids, rows) received."""
         p = self.plan
-        send = uniq_grads[p['order']].contiguous()
+        send = uniq_grads[:p['n_uniq']]
+        send = send if send.is_contiguous() else send.contiguous()
         recv = send.new_empty((sum(p['recv_split']), self.dim))
         a2a(recv, send, p['recv_split'], p['send_split'], self.pg)
         return p['recv_local'], recv
