@@ -22,6 +22,7 @@ the device to drain before its all-to-alls."""
 from __future__ import annotations
 
 import contextlib
+import time
 
 import torch
 
@@ -171,6 +172,11 @@ class Trainer:
         else:
             self.opt.maybe_segment()
         torch.cuda.synchronize()
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            # let the process groups' watchdog threads reap the (complete) collectives
+            # issued so far, so none of their events is polled while we capture (seen
+            # under rocprofv3 as a watchdog abort with a collective still listed)
+            time.sleep(1.0)
         g = torch.cuda.CUDAGraph()
         cur = torch.cuda.current_stream()
         self._side.wait_stream(cur)
