@@ -187,14 +187,28 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(const float* __restrict__ 
     const int64_t m = u / n4;
     const int64_t n = (u - m * n4) * 4;
     const float* p = part + m * N + n;
-    float4 a = *reinterpret_cast<const float4*>(p);
-    int s = 1;
-    for (; s + 4 <= S; s += 4) {  // four slices' loads in flight, added in slice order
-      float4 v[4];
+    // up to eight slices' loads in flight at once (the whole reduction at S <= 8:
+    // one memory latency per output chunk), added in slice order
+    const int c = S < 8 ? S : 8;
+    float4 v[8];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const float4*>(p + (s + q) * mn);
+    for (int q = 0; q < 8; ++q)
+      if (q < c) v[q] = *reinterpret_cast<const float4*>(p + q * mn);
+    float4 a = v[0];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+    for (int q = 1; q < 8; ++q)
+      if (q < c) {
+        a.x += v[q].x;
+        a.y += v[q].y;
+        a.z += v[q].z;
+        a.w += v[q].w;
+      }
+    int s = c;
+    for (; s + 8 <= S; s += 8) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(p + (s + q) * mn);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
         a.x += v[q].x;
         a.y += v[q].y;
         a.z += v[q].z;
@@ -202,18 +216,29 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(const float* __restrict__ 
       }
     }
     for (; s < S; ++s) {
-      const float4 v = *reinterpret_cast<const float4*>(p + s * mn);
-      a.x += v.x;
-      a.y += v.y;
-      a.z += v.z;
-      a.w += v.w;
+      const float4 w = *reinterpret_cast<const float4*>(p + s * mn);
+      a.x += w.x;
+      a.y += w.y;
+      a.z += w.z;
+      a.w += w.w;
     }
     wg_store4(out + m * ldo + n, a);
   }
-  if (db && blockIdx.x == 0)
-    for (int m = threadIdx.x; m < M; m += blockDim.x) {
-      float t = 0.f;
-      for (int s = 0; s < S; ++s) t += dbpart[(int64_t)s * M + m];
+  // db: spread over the grid (one column per thread), slices' loads in flight
+  // together, summed in slice order (a single workgroup walking all M columns
+  // with one dependent load per slice was the reduce kernel's critical path)
+  if (db)
+    for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (int64_t)gridDim.x * blockDim.x) {
+      const int c = S < 8 ? S : 8;
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q < c) v[q] = dbpart[(int64_t)q * M + m];
+      float t = v[0];
+#pragma unroll
+      for (int q = 1; q < 8; ++q)
+        if (q < c) t += v[q];
+      for (int s = c; s < S; ++s) t += dbpart[(int64_t)s * M + m];
       db[m] = t;
     }
 }
