@@ -450,7 +450,7 @@ class BaselineModel(torch.nn.Module):
         fids = list(self.ITEM_SPARSE_FEAT) + list(self.ITEM_ARRAY_FEAT) + list(self.ITEM_EMB_FEAT)
         fp = self._feats(pos_feature, fids, B, T)
         fn = self._feats(neg_feature, fids, B, T)
-        feats = {k: _stack_padded(fp[k], fn[k]) for k in fids}
+        feats = _stack_pairs(fp, fn, fids)
         seq2 = torch.cat([pos, neg], 0)
         if self._remaps is not None:  # row-sharded tables: the stacked ids read the rows fetched for pos and neg
             for name in ('item_emb',):
@@ -537,6 +537,37 @@ class BaselineModel(torch.nn.Module):
             embs.append(self.feat2emb(seq, feats, include_user=False).squeeze(0).detach().float().cpu().numpy())
         save_emb(np.concatenate(embs, 0), Path(save_path, 'embedding.fbin'))
         save_emb(np.array(retrieval_ids, dtype=np.uint64).reshape(-1, 1), Path(save_path, 'id.u64bin'))
+
+
+def _stack_pairs(fa, fb, fids):
+    """{k: _stack_padded(fa[k], fb[k])} for every feature with (at most) one
+    zero-fill and one multi-tensor copy kernel per dtype instead of a cat (and
+    pads) per feature."""
+    out, groups, pad = {}, {}, []
+    for k in fids:
+        a, b = fa[k], fb[k]
+        if a.dim() != b.dim() or a.shape[0] != b.shape[0] or a.shape[1:2] != b.shape[1:2] or a.dtype != b.dtype \
+                or (a.dim() == 3 and a.is_floating_point() and a.shape[2] != b.shape[2]) or a.dim() > 3:
+            out[k] = _stack_padded(a, b)
+            continue
+        w = max(a.shape[2], b.shape[2]) if a.dim() == 3 else None
+        shp = (a.shape[0] + b.shape[0],) + a.shape[1:2] + ((w,) if w is not None else ())
+        o = torch.empty(shp, dtype=a.dtype, device=a.device)
+        if w is not None and (a.shape[2] != w or b.shape[2] != w):
+            pad.append(o)
+        n = a.shape[0]
+        for part, t in ((o[:n], a), (o[n:], b)):
+            d = part[..., :t.shape[2]] if w is not None and t.shape[2] != w else part
+            # one list per (dtype, contiguous destination): the multi-tensor fast path
+            g = groups.setdefault((t.dtype, d.is_contiguous()), ([], []))
+            g[0].append(d)
+            g[1].append(t if t.is_contiguous() else t.contiguous())
+        out[k] = o
+    if pad:
+        torch._foreach_zero_(pad)
+    for dst, src in groups.values():
+        torch._foreach_copy_(dst, src)
+    return out
 
 
 def _stack_padded(a, b):
