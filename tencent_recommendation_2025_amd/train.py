@@ -136,7 +136,7 @@ class Trainer:
             # stream then waits only for the previous step, and prepare(next) finds
             # the split sizes on the host a whole step early
             self.opt.prefetch(next_batch)
-        torch._foreach_copy_(dst, src, non_blocking=True)  # one multi-tensor kernel, not one copy per tensor
+        _copy_batch(dst, src)
         if self._sharded:
             self.opt.prepare(self._static, key=batch[0])
             self._g.replay()
@@ -199,3 +199,17 @@ class Trainer:
             self.opt.capture_state()
             self.opt.step()
         return self._static_loss.clone()
+
+
+def _copy_batch(dst, src):
+    """Batch tensors into the captured step's inputs: one multi-tensor copy per
+    dtype.  A single _foreach_copy_ over the mixed int32 / int64 / fp32 batch
+    leaves the multi-tensor fast path and issues one memcpy per tensor (~50
+    copies of ~5 us each per step, measured)."""
+    groups = {}
+    for d, s in zip(dst, src):
+        g = groups.setdefault((d.dtype, s.dtype, d.device, s.device), ([], []))
+        g[0].append(d)
+        g[1].append(s)
+    for d, s in groups.values():
+        torch._foreach_copy_(d, s, non_blocking=True)
