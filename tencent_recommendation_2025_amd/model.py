@@ -409,7 +409,14 @@ class BaselineModel(torch.nn.Module):
         def dnn(which, width, has_proj):
             a = blocks.pop(0)
             p = blocks.pop(0) if has_proj else None
-            w = self._dnn_weight(which, width).to(a.dtype)
+            # one composed (and cast) dnn weight per forward: the seq-side and the
+            # pos/neg feat2emb share it, so its autograd graph runs once
+            key = ('w', which, width, a.dtype, self._fwd_id)
+            w = self._proj_cache.get(key) if self._fwd_id is not None else None
+            if w is None:
+                w = self._dnn_weight(which, width).to(a.dtype)
+                if self._fwd_id is not None:
+                    self._proj_cache[key] = w
             if _grk_gemm_ok(a):
                 return torch.relu(G.linear(a, w, addend=p))
             return torch.relu(torch.addmm(p, a, w.t()) if p is not None else a @ w.t())
