@@ -306,7 +306,9 @@ class BaselineModel(torch.nn.Module):
                 E = torch.stack([refs[k].weight for k, _ in group])
             # one indexing op for all blocks: its backward is one scatter into the weight gradient
             js = self._const_index(tuple(j for _, j in group), Wv.device) if len(group) > 1 else group[0][1]
-            Wb = (Wv[:, js, :].permute(1, 0, 2) if len(group) > 1 else Wv[:, js, :][None]).to(E.dtype)
+            if Wv.dtype != E.dtype:  # cast the whole weight once, not each group's blocks (bit-identical)
+                Wv = Wv.to(E.dtype)
+            Wb = Wv[:, js, :].permute(1, 0, 2) if len(group) > 1 else Wv[:, js, :][None]
             parts.append(torch.bmm(E, Wb.transpose(1, 2)).to(E.dtype).reshape(-1, d))
             for k, _ in group:
                 offs[k] = row
