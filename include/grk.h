@@ -13,7 +13,12 @@
  *  - All pointers are DEVICE pointers unless noted; the caller (the torch
  *    caching allocator) owns every buffer, including workspace.  The library
  *    never allocates, frees or synchronises, so every call can be captured
- *    into a hipGraph.
+ *    into a hipGraph -- with one exception: grk_gemm, on the FIRST call for a
+ *    new shape, times its hipBLASLt candidates (a scratch buffer is allocated,
+ *    the device synchronised, the buffer freed) and allocates one hipBLASLt
+ *    workspace per stream the first time it sees the stream.  Calls for
+ *    known shapes on known streams allocate nothing (the trainer warms every
+ *    shape up on the capture stream before capturing).
  *  - Work is enqueued on `stream` (a hipStream_t passed as void*).
  *  - Return 0 on success, else a GRK_E* code; grk_last_error() returns the
  *    thread-local message.  Shape/argument errors are detected on the host

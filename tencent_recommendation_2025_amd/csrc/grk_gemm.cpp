@@ -100,16 +100,16 @@ float time_algo(hipblasLtHandle_t h, Plan* p, const hipblasLtMatmulAlgo_t* algo,
       return -1.f;
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess) return -1.f;
-  if (hipEventCreate(&e1) != hipSuccess) { hipEventDestroy(e0); return -1.f; }
-  hipEventRecord(e0, o.s);
+  if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return -1.f; }
+  (void)hipEventRecord(e0, o.s);
   for (int i = 0; i < reps; ++i)
     hipblasLtMatmul(h, p->op, &alpha, o.b, p->A, o.a, p->B, &beta, scratch, p->C, scratch, p->C, algo, o.ws,
                     kWorkspaceBytes, o.s);
-  hipEventRecord(e1, o.s);
+  (void)hipEventRecord(e1, o.s);
   float ms = -1.f;
-  if (hipEventSynchronize(e1) == hipSuccess) hipEventElapsedTime(&ms, e0, e1);
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
+  if (hipEventSynchronize(e1) == hipSuccess) (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
   return ms * 1e3f / reps;
 }
 
@@ -165,8 +165,8 @@ int make_plan(hipblasLtHandle_t h, const Key& key, bool has_bias, Plan* p, const
           best = i;
         }
       }
-      hipDeviceSynchronize();
-      hipFree(scratch);
+      (void)hipDeviceSynchronize();
+      (void)hipFree(scratch);
     }
   }
   p->algo = res[best].algo;
