@@ -15,7 +15,10 @@ OBJS := $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(HIP_SRCS)) $(patsubst $(SRC
 all: $(LIB)
 
 # whole-sequence attention: MFMA accumulators in VGPRs (no AGPR<->VGPR copies
-# around the S tile; same occupancy -- scripts/isa_loops.py)
+# around the S tile).  Every S/dP chain starts from acc_zero() (grk_mfma.h):
+# with a literal zero srcC this form let an MFMA's vdst alias its own srcA/srcB,
+# which gave timing-dependent wrong HSTU rows when two workgroups shared a CU
+# (DESIGN.md §5b); the overlap check below guards the link.
 $(OBJ_DIR)/grk_attention_seq.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
 
 $(OBJ_DIR):
@@ -27,7 +30,11 @@ $(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(wildcard $(SRC_DIR)/*.h) include/grk.h | $(OB
 $(OBJ_DIR)/%.cpp.o: $(SRC_DIR)/%.cpp include/grk.h | $(OBJ_DIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+HIP_OBJS := $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(HIP_SRCS))
+
+# no MFMA may write registers it reads as srcA/srcB (scripts/check_mfma_overlap.py)
 $(LIB): $(OBJS)
+	python3 scripts/check_mfma_overlap.py $(HIP_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -L/opt/rocm/lib -lhipblaslt
 
 clean:

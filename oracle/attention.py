@@ -52,8 +52,13 @@ def forward(q, k, v, key_valid, scale=None, causal=True, keep=None, dropout_p=0.
     return out, lse, p
 
 
-def backward(q, k, v, key_valid, dout, scale=None, causal=True, keep=None, dropout_p=0.0):
-    """Returns ``(dq, dk, dv)`` of ``forward`` for upstream ``dout``."""
+def backward(q, k, v, key_valid, dout, scale=None, causal=True, keep=None, dropout_p=0.0, out_stored=None):
+    """Returns ``(dq, dk, dv)`` of ``forward`` for upstream ``dout``.
+
+    ``out_stored``: the forward output as the caller kept it (e.g. rounded to
+    bf16).  The flash-style backward forms delta = rowsum(dout * out) from the
+    STORED output, so a kernel fed a bf16 output is checked against the same
+    delta (its inputs identically rounded); default: the exact output."""
     q = np.asarray(q, np.float64); k = np.asarray(k, np.float64); v = np.asarray(v, np.float64)
     dout = np.asarray(dout, np.float64)
     hd = q.shape[-1]
@@ -64,6 +69,8 @@ def backward(q, k, v, key_valid, dout, scale=None, causal=True, keep=None, dropo
     dv = np.einsum('bhij,bhid->bhjd', pd, dout)
     dpd = np.einsum('bhid,bhjd->bhij', dout, v)
     dp = dpd if keep is None else dpd * keep * rs
+    if out_stored is not None:
+        out = np.asarray(out_stored, np.float64)
     delta = (dout * out).sum(-1, keepdims=True)  # == sum_j p_ij dp_ij
     ds = p * (dp - delta)
     dq = np.einsum('bhij,bhjd->bhid', ds, k) * scale

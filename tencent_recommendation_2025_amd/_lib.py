@@ -18,7 +18,8 @@ import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 
 PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
-LIB_PATH = PKG_DIR / 'libgrk.so'
+# GRK_LIB: an alternative build of the same library (A/B experiments, scripts/)
+LIB_PATH = Path(os.environ.get('GRK_LIB', PKG_DIR / 'libgrk.so'))
 
 GRK_OK, GRK_EINVAL, GRK_EHIP, GRK_EUNSUPPORTED = 0, 1, 2, 3
 GRK_F32, GRK_BF16 = 0, 1

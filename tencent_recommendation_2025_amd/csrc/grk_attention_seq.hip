@@ -306,7 +306,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
       for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x16{};
       float m = -INFINITY, l = 0.f;
       for (int kb = kbeg; kb <= q0; kb += 32) {
-        f32x16 s = f32x16{};
+        f32x16 s = acc_zero();
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) s = mfma(lds_row8<HD>(L.img0, kb + r, 16 * ks + 8 * hh), qf[ks], s);
         // strictly below the diagonal and past the padding: nothing to mask
@@ -450,7 +450,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) acc[dt] = f32x16{};
       for (int kb = kbeg; kb <= q0; kb += 32) {
-        f32x16 s = f32x16{}, dp = f32x16{};
+        f32x16 s = acc_zero(), dp = acc_zero();
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           s = mfma(lds_row8<HD>(L.img0, kb + r, 16 * ks + 8 * hh), qf[ks], s);
@@ -617,7 +617,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
         dv[dt] = f32x16{};
       }
       for (int qb = k0; qb < Tp; qb += 32) {
-        f32x16 s = f32x16{}, dp = f32x16{};
+        f32x16 s = acc_zero(), dp = acc_zero();
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           s = mfma(lds_row8<HD>(L.img0, qb + r, 16 * ks + 8 * hh), kf[ks], s);

@@ -19,6 +19,24 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// A zero accumulator for the FIRST MFMA of a chain, opaque to the compiler.
+// With a literal zero srcC the 32x32 MFMA's destination is untied, and in the
+// VGPR form (grk_attention_seq, -amdgpu-mfma-vgpr-form) the register allocator
+// may hand it the registers of a srcA/srcB that dies at that MFMA.  A multi-pass
+// MFMA whose vdst overlaps its srcA/srcB is outside the ISA's rules; on gfx950 it
+// produced timing-dependent wrong rows whenever two workgroups shared a CU
+// (DESIGN.md §5b).  Through this value srcC is a live register tied to vdst, so
+// vdst can never alias a source.  scripts/check_mfma_overlap.py (run by `make`)
+// rejects any library whose code object still has such an MFMA.
+__device__ __forceinline__ f32x16 acc_zero() {
+  float z;
+  asm("v_mov_b32 %0, 0" : "=v"(z));
+  f32x16 r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r[i] = z;
+  return r;
+}
+
 // Swizzled LDS row image: row of HD bf16 = HD/8 16-byte chunks; chunk c of
 // row r lives at chunk position c ^ (r & MASK).
 template <int HD>

@@ -309,10 +309,11 @@ class _SoftmaxMHAFn(torch.autograd.Function):
 
 
 @_disable
-def softmax_mha(qkv, key_valid, B, T, H, hd, dropout_p=0.0, seed=0, precise=None, seq_range=None):
-    """Causal + key-padding softmax attention on a packed [B*T, 3D] (q|k|v) tensor."""
-    if precise is None:
-        precise = qkv.dtype == torch.float32
+def softmax_mha(qkv, key_valid, B, T, H, hd, dropout_p=0.0, seed=0, precise=True, seq_range=None):
+    """Causal + key-padding softmax attention on a packed [B*T, 3D] (q|k|v) tensor.
+    precise (default): probabilities / dS enter the P.V, dS.K, dS^T.Q MFMAs as
+    bf16 hi + lo pairs (fp32-accurate operands; 1-4 % slower than precise=False,
+    which rounds them to bf16 and is held only to 1e-2)."""
     return _SoftmaxMHAFn.apply(qkv, key_valid, B, T, H, hd, float(dropout_p), int(seed), bool(precise), seq_range)
 
 
@@ -362,7 +363,7 @@ class _HSTUCoreFn(torch.autograd.Function):
 
 
 @_disable
-def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, precise=False, dropout_p=0.0, seed=0,
+def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, precise=True, dropout_p=0.0, seed=0,
               seq_range=None):
     """Fused HSTU layer core on the [B*T, 4D] uvqk pre-activation (see _HSTUCoreFn)."""
     return _HSTUCoreFn.apply(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, float(inv_n), float(eps), bool(precise),

@@ -265,7 +265,7 @@ def stamp_rows(last, ids, count, capacity, t):
 
 
 def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, inv_n=1.0, dropout_p=0.0, seed=0,
-              precise=False, out_dtype=torch.bfloat16, act=None, seq_range=None):
+              precise=True, out_dtype=torch.bfloat16, act=None, seq_range=None):
     """Build grk_attn_args for bf16 [B*T, ld] column views q/k/v (head h at cols h*hd).
 
     act="silu": q/k/v are pre-activations; SiLU is applied on load and the

@@ -355,7 +355,7 @@ class BaselineModel(torch.nn.Module):
         Wc = torch.cat(cols, 1)
         return F.pad(Wc, (0, width - Wc.shape[1]))
 
-    def _embed(self, seq, feature_array, mask=None, include_user=False, with_pos=False):
+    def _embed(self, seq, feature_array, mask=None, include_user=False, with_pos=False, role='seq'):
         dev = self._device()
         seq = seq.to(dev, non_blocking=True).long()
         B, T = seq.shape
@@ -405,7 +405,7 @@ class BaselineModel(torch.nn.Module):
             splits.append((col, col + d))
             col += d
         if self._remaps is not None or self._table_refs is not None:
-            specs = self._remap_specs(specs)
+            specs = self._remap_specs(specs, role)
         blocks = list(G.feature_lookup(specs, N, col, tt, T, extras, splits))
 
         def dnn(which, width, has_proj):
@@ -429,15 +429,22 @@ class BaselineModel(torch.nn.Module):
         pos_rows = blocks.pop(0) if with_pos else None
         return x.view(B, T, d), pos_rows
 
-    def _remap_specs(self, specs):
-        """Row-sharded tables: read the rows prepare() fetched for this step."""
+    def _remap_specs(self, specs, role):
+        """Row-sharded tables: read the rows prepare() fetched for this step.
+        Remaps are keyed by (table, role, lookup mode) -- role 'seq' (log2feats),
+        'pos' / 'neg' (feat2emb) or 'pair' (the stacked pos|neg lookup) -- never by
+        tensor address: the batch's int32 ids are widened to int64 separately by
+        prepare() and by the forward, so their copies do not share storage."""
         out = []
         for s in specs:
             name = getattr(s.ref, 'name', None)
             if name is None:
                 out.append(s)
                 continue
-            hit = (self._remaps or {}).get((name, s.idx.data_ptr(), s.mode))
+            hit = (self._remaps or {}).get((name, role, s.mode))
+            if hit is not None and hit[1].numel() != s.idx.numel():
+                raise RuntimeError(f'{name}: the batch prepared ({hit[1].numel()} ids) is not the one in forward '
+                                   f'({s.idx.numel()} ids)')
             if hit is None:
                 raise RuntimeError(f'{name} is row-sharded: call the optimizer\'s prepare(batch) before forward')
             ref, inv = hit
@@ -463,11 +470,11 @@ class BaselineModel(torch.nn.Module):
         seq2 = torch.cat([pos, neg], 0)
         if self._remaps is not None:  # row-sharded tables: the stacked ids read the rows fetched for pos and neg
             for name in ('item_emb',):
-                a = self._remaps.get((name, pos.data_ptr(), L.IDX_PLAIN))
-                b = self._remaps.get((name, neg.data_ptr(), L.IDX_PLAIN))
+                a = self._remaps.get((name, 'pos', L.IDX_PLAIN))
+                b = self._remaps.get((name, 'neg', L.IDX_PLAIN))
                 if a is not None and b is not None and a[0] is b[0]:
-                    self._remaps[(name, seq2.data_ptr(), L.IDX_PLAIN)] = (a[0], torch.cat([a[1], b[1]], 0))
-        x = self._embed(seq2, feats)[0]
+                    self._remaps[(name, 'pair', L.IDX_PLAIN)] = (a[0], torch.cat([a[1], b[1]], 0))
+        x = self._embed(seq2, feats, role='pair')[0]
         return x[:B], x[B:]
 
     # -------------------------------------------------- model/BaseLine/model.py:312-350

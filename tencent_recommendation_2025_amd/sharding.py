@@ -353,20 +353,22 @@ class ShardedFusedAdamW(FusedAdamW):
     # -- input dist -------------------------------------------------------
     @staticmethod
     def _parts(batch):
-        """{table: [(index tensor the model looks up, lookup mode, ids it reads)]}."""
+        """{table: [(role of the model's lookup, index tensor, lookup mode, ids it reads)]}.
+        Roles name the model's call sites (model._remap_specs): 'seq' = log2feats,
+        'pos' / 'neg' = the two halves of feat2emb_pair."""
         seq, pos, neg, tt = batch[0], batch[1], batch[2], batch[3]
         seq, pos, neg = seq.long(), pos.long(), neg.long()
         tt = tt.to(seq.device)
         return {
-            'item_emb': [(seq, L.IDX_ITEM_MASK, lambda: seq * (tt == 1)), (pos, L.IDX_PLAIN, lambda: pos),
-                         (neg, L.IDX_PLAIN, lambda: neg)],
-            'user_emb': [(seq, L.IDX_USER_MASK, lambda: seq * (tt == 2))],
+            'item_emb': [('seq', seq, L.IDX_ITEM_MASK, lambda: seq * (tt == 1)),
+                         ('pos', pos, L.IDX_PLAIN, lambda: pos), ('neg', neg, L.IDX_PLAIN, lambda: neg)],
+            'user_emb': [('seq', seq, L.IDX_USER_MASK, lambda: seq * (tt == 2))],
         }
 
     def _route_all(self, batch, pg):
         routed = {}
         for name, plist in self._parts(batch).items():
-            ids = torch.cat([v().reshape(-1) for _, _, v in plist])
+            ids = torch.cat([v().reshape(-1) for _, _, _, v in plist])
             routed[name] = self.shards[name][1].route(ids, pg)
         counts = torch.stack([torch.stack([r['send_counts'], r['recv_counts']]) for r in routed.values()])
         return routed, counts
@@ -448,11 +450,11 @@ class ShardedFusedAdamW(FusedAdamW):
             self.sinks[name] = sink
             ref = G.TableRef(fetched, sink, 0)
             off = 0
-            for idx, mode, _ in plist:
+            for role, idx, mode, _ in plist:
                 n = idx.numel()
                 inv = inv_all[off:off + n].view(idx.shape)
                 off += n
-                remaps[(name, idx.data_ptr(), mode)] = (ref, inv)
+                remaps[(name, role, mode)] = (ref, inv)
         self.model._remaps = remaps
         self._begun = self.t
 

@@ -1,0 +1,175 @@
+"""World-size-2 row-sharded training (sharding.ShardedFusedAdamW + train.Trainer)
+against the unsharded step on the union batch.
+
+Two ranks share cuda:0 and talk over gloo (device tensors staged through the
+host; the RCCL path differs only in the transport).  Each rank trains its own
+batches; the global loss is the mean of the rank losses, so the reference is
+ONE process running the unsharded drop-in model (plain torch AdamW over every
+parameter, dense table gradients -- model/BaseLine/main.py:163-190) on
+loss = (L_rank0 + L_rank1) / 2.  After several steps the sharded tables
+(flushed, reassembled from rows rank::2), the replicated small tables and the
+dense parameters must match it, and so must the AdamW first moments.
+
+Tolerances: the two runs sum the same gradients in different orders (per rank,
+then across ranks).  After step 1 (identical inputs) the AdamW first moments
+are 0.1 x the gradients: normwise relative error < 1e-5.  The parameters go
+through Adam's m / sqrt(v), which turns rounding noise on a near-zero gradient
+into a full +-lr step; later steps then see slightly different parameters.  So
+after the last step: parameters normwise < 5e-3 with at most 0.5 % of the
+elements (or 4) outside (rtol 1e-3, atol 2e-5) and none off by more than 2 lr x steps;
+first moments normwise < 2e-2.
+
+The rank batches are int32 on odd steps (collate_fn's dtype,
+model/BaseLine/dataset.py:267-293): the sharded lookups are matched to the
+rows prepare() fetched by call-site role, never by tensor address
+(int32 ids widened twice do not share storage)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+STEPS = 4
+LR = 2e-3
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def build(seed=0):
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel, init_reference_
+    cfg = S.SyntheticConfig(batch_size=6, maxlen=40, num_items=3000, num_users=400, min_len=8)
+    stats, types = S.feature_schema(cfg)
+    torch.manual_seed(seed)
+    m = BaselineModel(cfg.num_users, cfg.num_items, stats, types,
+                      S.make_args(hidden_units=64, maxlen=40, num_blocks=2, num_heads=2)).to(DEV)
+    init_reference_(m, seed=seed, live_norms=True)
+    return m, cfg
+
+
+def rank_batches(cfg, rank):
+    from tencent_recommendation_2025_amd import synthetic as S
+    g = torch.Generator(device=DEV).manual_seed(100 + rank)
+    out = []
+    for i in range(STEPS):
+        b = S.make_batch(cfg, g, DEV)
+        if i % 2:
+            b = tuple(x.to(torch.int32) for x in b[:6]) + b[6:]
+        out.append(b)
+    return out
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from tencent_recommendation_2025_amd.sharding import ShardedFusedAdamW
+        from tencent_recommendation_2025_amd.train import Trainer
+        m, cfg = build()
+        opt = ShardedFusedAdamW(m, lr=LR, table_dtype=torch.float32, defer_period=3)
+        tr = Trainer(m, opt, loss='bce', amp_dtype=None)
+        names = {id(p): n for n, p in m.named_parameters()}
+
+        def first_moments():
+            out = {k: opt.shards[k][0].exp_avg.cpu().numpy().copy() for k in ('item_emb', 'user_emb')}
+            out.update({names[id(p)]: st['exp_avg'].float().cpu().numpy() for p, st in opt.dense.state.items()})
+            return out
+
+        losses, m1 = [], None
+        for i, b in enumerate(rank_batches(cfg, rank)):
+            losses.append(tr.step(b).item())
+            if i == 0:
+                m1 = first_moments()   # after step 1: the inputs of both runs were identical
+        # numpy, not tensors: a tensor crosses the queue as a shared-memory fd the
+        # parent could only fetch while this process is still alive
+        shards = {k: opt.shard_table(k).float().cpu().numpy() for k in ('item_emb', 'user_emb')}
+        moments = {k: (opt.shards[k][0].exp_avg.cpu().numpy(), opt.shards[k][0].exp_avg_sq.cpu().numpy())
+                   for k in shards}
+        sd = {k: v.detach().float().cpu().numpy() for k, v in m.state_dict().items()
+              if not k.startswith(('item_emb.', 'user_emb.'))}
+        q.put((rank, losses, shards, moments, sd, m1))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_world2_sharded_trainer_equals_unsharded_union_step():
+    from tencent_recommendation_2025_amd import functional as G
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+    # reference: one process, unsharded drop-in model, torch AdamW on every parameter
+    m, cfg = build()
+    batches = [rank_batches(cfg, r) for r in range(world)]
+    opt = torch.optim.AdamW(m.parameters(), lr=LR, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01)
+    names = {id(p): n for n, p in m.named_parameters()}
+    ref_m1 = None
+    for i in range(STEPS):
+        opt.zero_grad()
+        losses = []
+        for r in range(world):
+            seq, pos, neg, tt, ntt, _nat, sf, pf, nf = batches[r][i]
+            h, pe, ne = m.encode(seq, pos, neg, tt, sf, pf, nf)
+            losses.append(G.bce_loss(h, pe, ne, ntt))
+        loss = sum(losses) / world
+        loss.backward()
+        opt.step()
+        if i == 0:
+            ref_m1 = {names[id(p)]: st['exp_avg'].cpu().numpy().copy() for p, st in opt.state.items()}
+        with torch.no_grad():
+            for r in range(world):
+                assert abs(losses[r].item() - res[r][1][i]) < 1e-4 * max(1.0, abs(losses[r].item())), (i, r)
+    sd = m.state_dict()
+
+    def report(name, got, want, moment=False):
+        got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+        nrm = np.linalg.norm(want)
+        rel = np.linalg.norm(got - want) / (nrm if nrm > 0 else 1.0)
+        if moment:
+            return f'{name}: normwise {rel:.2e} >= {moment}' if rel >= moment else None
+        bad = np.abs(got - want) > 2e-5 + 1e-3 * np.abs(want)
+        worst = float(np.abs(got - want).max()) if got.size else 0.0
+        if rel >= 5e-3 or bad.sum() > max(4, 5e-3 * bad.size) or worst > 2 * LR * STEPS:
+            return f'{name}: normwise {rel:.2e}, {int(bad.sum())} of {bad.size} elements off, max abs {worst:.2e}'
+        return None
+
+    problems = []
+    for k in ('item_emb', 'user_emb'):
+        full = sd[f'{k}.weight'].cpu()
+        st = opt.state[getattr(m, k).weight]
+        for rank, _, shards, moments, _, _ in res:
+            problems.append(report(f'{k} rank {rank}', shards[k], full[rank::world].numpy()))
+            problems.append(report(f'{k} exp_avg rank {rank}', moments[k][0],
+                                   st['exp_avg'].cpu()[rank::world].numpy(), moment=2e-2))
+            problems.append(report(f'{k} exp_avg after step 1, rank {rank}', res[rank][5][k],
+                                   ref_m1[f'{k}.weight'][rank::world], moment=1e-5))
+    for n, v in res[0][5].items():
+        if n not in ('item_emb', 'user_emb'):
+            problems.append(report(f'{n} exp_avg after step 1', v, ref_m1[n], moment=1e-5))
+    for k, v in res[0][4].items():
+        problems.append(report(k, v, sd[k].cpu().float().numpy()))
+        if not np.array_equal(v, res[1][4][k]):
+            problems.append(f'replicated {k} differs between ranks')
+    problems = [p for p in problems if p]
+    assert not problems, '\n'.join(problems)
+    assert np.isfinite(res[0][1]).all()
