@@ -51,8 +51,13 @@ def parse():
     ap.add_argument('--table-mode', default='dense', choices=['dense', 'lazy'])
     ap.add_argument('--zipf', type=float, default=None)
     ap.add_argument('--cpu-baseline', type=int, default=1)
-    ap.add_argument('--cpu-batch', type=int, default=8)
-    ap.add_argument('--cpu-steps', type=int, default=6)
+    ap.add_argument('--dropout', type=float, default=0.01,
+                    help="dropout_rate (the reference default, model/BaseLine/main.py:30)")
+    ap.add_argument('--pool', type=int, default=16,
+                    help='distinct device-resident batches cycled by the timed steps (16 x ~41k item rows x 1 KiB '
+                         '~ 0.7 GB: more than the 256 MB Infinity Cache, so rows are not re-read warm)')
+    ap.add_argument('--cpu-batch', type=int, default=128)
+    ap.add_argument('--cpu-steps', type=int, default=2)
     ap.add_argument('--roofline-reps', type=int, default=20)
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='gloo: rehearse N ranks on fewer GPUs (collectives staged via host)')
@@ -279,12 +284,18 @@ def cpu_baseline(a, stats, types):
         cores = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
+    cores = max(1, min(cores, 16))   # the GPU box's CPU share is 16 threads per GPU
     torch.set_num_threads(cores)
+    model_name = 'unknown CPU'
+    try:
+        with open('/proc/cpuinfo') as f:
+            model_name = next((ln.split(':', 1)[1].strip() for ln in f if ln.startswith('model name')), model_name)
+    except OSError:  # pragma: no cover
+        pass
     cfg = S.SyntheticConfig(batch_size=a.cpu_batch, maxlen=a.maxlen, num_items=a.items, num_users=a.users,
                             zipf=a.zipf)
     margs = S.make_args(hidden_units=a.hidden, maxlen=a.maxlen, num_blocks=a.blocks, num_heads=a.heads,
-                        block=a.block, device='cpu')
+                        block=a.block, device='cpu', dropout_rate=a.dropout)
     ref = model_ref.RefBaselineModel(a.users, a.items, stats, types, margs, variant='o1', block=a.block)
     model_ref.init_params(ref, seed=0)
     opt = torch.optim.AdamW(ref.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=0.01)
@@ -310,10 +321,11 @@ def cpu_baseline(a, stats, types):
         step(b)
     dt = time.perf_counter() - t0
     n = a.cpu_batch * a.cpu_steps
-    return {'value': round(n / dt, 3), 'unit': 'seq/s', 'cores': cores, 'kind': 'port',
+    return {'value': round(n / dt, 3), 'unit': 'seq/s', 'cores': cores, 'kind': 'port', 'cpu_model': model_name,
             'sample': f'{a.cpu_steps} timed steps x B={a.cpu_batch} of the same model/config/loss '
-                      f'(fp32 CPU, full {a.items}-row item table, dense AdamW), after 1 warmup step; '
-                      f'{dt:.1f} s'}
+                      f'(fp32 CPU, full {a.items}-row item table, dense AdamW, dropout {a.dropout}), after 1 warmup step, '
+                      f'{cores} threads on {model_name}; {dt:.1f} s (BASELINE.md 3 asks 10 + 50 steps: bounded '
+                      f'here to keep the bench within minutes)'}
 
 
 def main():
@@ -342,9 +354,10 @@ def main():
     cfg = S.SyntheticConfig(batch_size=a.batch, maxlen=a.maxlen, num_items=a.items, num_users=a.users, zipf=a.zipf)
     stats, types = S.feature_schema(cfg)
     margs = S.make_args(hidden_units=a.hidden, maxlen=a.maxlen, num_blocks=a.blocks, num_heads=a.heads,
-                        block=a.block)
+                        block=a.block, dropout_rate=a.dropout)
     torch.manual_seed(0)
     model = BaselineModel(a.users, a.items, stats, types, margs).to(dev)
+    model.train()
     init_reference_(model, seed=0, live_norms=True)
     if sharded:
         from tencent_recommendation_2025_amd.sharding import ShardedFusedAdamW
@@ -353,7 +366,7 @@ def main():
         opt = FusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
     trainer = Trainer(model, opt, loss=a.loss, graph=bool(a.graph))
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    pool = [S.make_batch(cfg, gen, dev) for _ in range(4)]
+    pool = [S.make_batch(cfg, gen, dev) for _ in range(max(2, a.pool))]
 
     trace = None
     for i in range(a.warmup):
@@ -403,10 +416,12 @@ def main():
             'vs_baseline': None, 'dtype': 'bf16', 'data': 'synthetic (device-resident TencentGR-shaped batches)',
             'config': {'workload': f'BASELINE config 2: {a.block.upper()} d={a.hidden} L={a.maxlen} '
                                    f'({a.blocks} blocks x {a.heads} heads), {a.items}-item bf16 table, '
-                                   f'{a.users} users, loss={a.loss}, table AdamW={a.table_mode}',
+                                   f'{a.users} users, loss={a.loss}, table AdamW={a.table_mode}, '
+                                   f'dropout={a.dropout}',
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch, 'seq_len': a.maxlen + 1,
                        'parallelism': f'dp{world}' + ('+rowshard' if sharded else ''),
-                       'step_launch': 'hip-graph replay' if trainer.graph else 'eager'},
+                       'step_launch': 'hip-graph replay' if trainer.graph else 'eager',
+                       'batch_pool': len(pool)},
             'final_loss': round(final_loss, 5),
             'roofline': roof,
             'rooflines': more,

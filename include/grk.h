@@ -234,6 +234,10 @@ typedef struct grk_attn_args {
   const int32_t* seq_range;        /* optional [B, 2] from grk_seq_ranges (first
                                       valid key, contiguous flag); NULL = derived
                                       from key_valid inside every launch        */
+  const uint64_t* seed_dev;        /* optional: the dropout seed in device memory,
+                                      read by the kernels when they run (replaces
+                                      `seed`): a step replayed from a HIP graph
+                                      draws a fresh mask every replay           */
 } grk_attn_args;
 
 /* ranges[b] = (first j with key_valid[b, j], 1 if the valid keys are exactly
@@ -277,11 +281,12 @@ int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, int64_t ldo
  * aligned, strides multiples of 8); gamma/beta/dgamma/dbeta fp32 [dim];
  * dim multiple of 8, <= 2048.  stats fp32 [rows, 2] = (mean, rstd) saved by
  * the forward for the backward.  Dropout: counter hash of (seed, row, col),
- * identical in both directions.
+ * identical in both directions; seed_dev (optional, device memory) replaces
+ * seed with the value it holds when the kernel runs (HIP-graph replay).
  * ------------------------------------------------------------------------ */
 int grk_norm_gate_fwd(const void* o, int64_t ldo, const void* u, int64_t ldu, const float* gamma,
-                      const float* beta, float eps, int64_t rows, int dim, float dropout_p, uint64_t seed, void* y,
-                      int64_t ldy, float* stats, void* stream);
+                      const float* beta, float eps, int64_t rows, int dim, float dropout_p, uint64_t seed,
+                      const uint64_t* seed_dev, void* y, int64_t ldy, float* stats, void* stream);
 
 size_t grk_norm_gate_bwd_workspace(int64_t rows, int dim);
 
@@ -289,7 +294,8 @@ size_t grk_norm_gate_bwd_workspace(int64_t rows, int dim);
  * written (not accumulated); fixed-order, deterministic reductions. */
 int grk_norm_gate_bwd(const void* gy, int64_t ldgy, const void* o, int64_t ldo, const void* u, int64_t ldu,
                       const float* gamma, const float* beta, const float* stats, int64_t rows, int dim,
-                      float dropout_p, uint64_t seed, void* dout, int64_t lddo, void* du, int64_t lddu,
+                      float dropout_p, uint64_t seed, const uint64_t* seed_dev, void* dout, int64_t lddo, void* du,
+                      int64_t lddu,
                       float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream);
 
 /* Residual add + LayerNorm of the HSTU block's residual stream (replaces the

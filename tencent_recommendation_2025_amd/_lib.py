@@ -52,7 +52,7 @@ class GrkAttnArgs(C.Structure):
                 ('v', C.c_void_p), ('ldq', C.c_int64), ('ldk', C.c_int64), ('ldv', C.c_int64),
                 ('key_valid', C.c_void_p), ('rab', C.c_void_p), ('scale', C.c_float), ('inv_n', C.c_float),
                 ('dropout_p', C.c_float), ('precise', C.c_int32), ('seed', C.c_uint64), ('out_dtype', C.c_int32),
-                ('act', C.c_int32), ('seq_range', C.c_void_p)]
+                ('act', C.c_int32), ('seq_range', C.c_void_p), ('seed_dev', C.c_void_p)]
 
 
 ATTN_SOFTMAX, ATTN_HSTU = 0, 1
@@ -88,9 +88,9 @@ SIGNATURES = {
                                _P, _P, _P]),
     'grk_attention_bwd_parts': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64,
                                      _P, _I64, _P, _P, _I, _P]),
-    'grk_norm_gate_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _F, C.c_uint64, _P, _I64, _P, _P]),
+    'grk_norm_gate_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _F, C.c_uint64, _P, _P, _I64, _P, _P]),
     'grk_norm_gate_bwd_workspace': (_SZ, [_I64, _I]),
-    'grk_norm_gate_bwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _P, _P, _I64, _I, _F, C.c_uint64, _P, _I64, _P,
+    'grk_norm_gate_bwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _P, _P, _I64, _I, _F, C.c_uint64, _P, _P, _I64, _P,
                                _I64, _P, _P, _P, _SZ, _P]),
     'grk_seq_ranges': (_I, [_P, _I, _I, _P, _P]),
     'grk_add_norm_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _P, _I64, _P, _I64, _I, _P, _P]),

@@ -18,6 +18,7 @@ struct AttnParams {
   const uint8_t* key_valid;
   float scale, inv_n, dropout_p;
   unsigned long long seed;
+  const unsigned long long* seed_dev;  // optional: seed read at kernel time (graph replay)
   const float* rab;
   int nb;
   int precise;
@@ -34,6 +35,11 @@ struct AttnParams {
   float* drab;
 };
 
+
+// The dropout seed of a launch: the device value when one is given.
+__device__ __forceinline__ unsigned long long attn_seed(const AttnParams& p) {
+  return p.seed_dev ? *p.seed_dev : p.seed;
+}
 
 // Counter-based dropout keep decision for element (b*H+h, q, k): identical
 // in forward and backward.

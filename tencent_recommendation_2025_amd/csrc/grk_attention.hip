@@ -62,6 +62,7 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
   const float sl2 = p.scale * kLog2e;
   const float rdrop = 1.0f / (1.0f - p.dropout_p);
   const bool drop = KIND == 0 && p.dropout_p > 0.f;
+  const unsigned long long seed = drop ? attn_seed(p) : 0ull;
   const int bh = b * p.H + h;
 
   const int kbeg = (start / 32) * 32;
@@ -111,7 +112,7 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
           pd[i] = pr[i];
           if (drop) {
             const int key = kc + 32 * sub + acc_row(i, hh);
-            pd[i] = drop_keep(p.seed, bh, myq, key, T, p.dropout_p) ? pr[i] * rdrop : 0.f;
+            pd[i] = drop_keep(seed, bh, myq, key, T, p.dropout_p) ? pr[i] * rdrop : 0.f;
           }
         }
       } else {
@@ -215,6 +216,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
   const float sl2 = p.scale * kLog2e;
   const float rdrop = 1.0f / (1.0f - p.dropout_p);
   const bool drop = KIND == 0 && p.dropout_p > 0.f;
+  const unsigned long long seed = drop ? attn_seed(p) : 0ull;
 
   const int kbeg = (start / 32) * 32;
   const int kend = min(T, q0 + kBlockRows);
@@ -245,7 +247,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
         if (KIND == 0) {
           const float pv = ok ? exp2f(s[i] * sl2 - lse2) : 0.f;
           float dpv = dp[i];
-          if (drop) dpv = drop_keep(p.seed, bh, myq, key, T, p.dropout_p) ? dpv * rdrop : 0.f;
+          if (drop) dpv = drop_keep(seed, bh, myq, key, T, p.dropout_p) ? dpv * rdrop : 0.f;
           ds[i] = pv * (dpv - dlt);
         } else {
           const int bk = min(myq - key, p.nb - 1);
@@ -316,6 +318,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
   const float sl2 = p.scale * kLog2e;
   const float rdrop = 1.0f / (1.0f - p.dropout_p);
   const bool drop = KIND == 0 && p.dropout_p > 0.f;
+  const unsigned long long seed = drop ? attn_seed(p) : 0ull;
 
   // queries that can see this block's keys: q >= k0 and q >= start
   const int qbeg = (max(k0, start) / 32) * 32;
@@ -355,7 +358,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
           float dpv = dp[i];
           pd[i] = pv;
           if (drop) {
-            const bool keep = drop_keep(p.seed, bh, q, myk, T, p.dropout_p);
+            const bool keep = drop_keep(seed, bh, q, myk, T, p.dropout_p);
             pd[i] = keep ? pv * rdrop : 0.f;
             dpv = keep ? dpv * rdrop : 0.f;
           }
@@ -453,7 +456,7 @@ static int fill_params(const grk_attn_args* a, AttnParams* p) {
   p->q = (const bf16_t*)a->q; p->k = (const bf16_t*)a->k; p->v = (const bf16_t*)a->v;
   p->ldq = a->ldq; p->ldk = a->ldk; p->ldv = a->ldv;
   p->key_valid = a->key_valid;
-  p->scale = a->scale; p->inv_n = a->inv_n; p->dropout_p = a->dropout_p; p->seed = a->seed;
+  p->scale = a->scale; p->inv_n = a->inv_n; p->dropout_p = a->dropout_p; p->seed = a->seed; p->seed_dev = (const unsigned long long*)a->seed_dev;
   p->rab = a->rab; p->nb = a->num_buckets;
   p->precise = a->precise; p->out_f32 = a->out_dtype == GRK_F32;
   p->act = a->act;

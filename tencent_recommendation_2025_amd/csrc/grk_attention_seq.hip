@@ -275,6 +275,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
   const float sl2 = p.scale * kLog2e;
   const float rdrop = 1.0f / (1.0f - p.dropout_p);
   const bool drop = KIND == 0 && p.dropout_p > 0.f;
+  const unsigned long long seed = drop ? attn_seed(p) : 0ull;
   const int bh = b * p.H + h;
 
   // query tiles before the first valid key: every row fully masked -> 0
@@ -342,7 +343,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
               const int key = kb + acc_row(i, hh);
-              pd[i] = drop_keep(p.seed, bh, myq, key, T, p.dropout_p) ? pd[i] * rdrop : 0.f;
+              pd[i] = drop_keep(seed, bh, myq, key, T, p.dropout_p) ? pd[i] * rdrop : 0.f;
             }
           }
         } else {
@@ -413,6 +414,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
   const float sl2 = p.scale * kLog2e;
   const float rdrop = 1.0f / (1.0f - p.dropout_p);
   const bool drop = KIND == 0 && p.dropout_p > 0.f;
+  const unsigned long long seed = drop ? attn_seed(p) : 0ull;
 
   for (int qt = wave; qt < first; qt += kSeqWaves) {  // fully masked query rows: dq = 0
     const int myq = qt * 32 + r;
@@ -464,7 +466,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
           for (int i = 0; i < 16; ++i) {
             const float pv = ((mk >> i) & 1) ? exp2f(s[i] * sl2 - lse2) : 0.f;
             float dpv = dp[i];
-            if (drop) dpv = drop_keep(p.seed, bh, myq, kb + acc_row(i, hh), T, p.dropout_p) ? dpv * rdrop : 0.f;
+            if (drop) dpv = drop_keep(seed, bh, myq, kb + acc_row(i, hh), T, p.dropout_p) ? dpv * rdrop : 0.f;
             ds[i] = pv * (dpv - dlt);
           }
         } else {
@@ -580,6 +582,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
   const float sl2 = p.scale * kLog2e;
   const float rdrop = 1.0f / (1.0f - p.dropout_p);
   const bool drop = KIND == 0 && p.dropout_p > 0.f;
+  const unsigned long long seed = drop ? attn_seed(p) : 0ull;
 
   for (int kt = wave; kt < first; kt += kSeqWaves) {  // keys before the first valid one: no gradient
     const int myk = kt * 32 + r;
@@ -637,7 +640,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
             float dpv = dp[i];
             pd[i] = pv;
             if (drop) {
-              const bool keep = drop_keep(p.seed, bh, q, myk, T, p.dropout_p);
+              const bool keep = drop_keep(seed, bh, q, myk, T, p.dropout_p);
               pd[i] = keep ? pv * rdrop : 0.f;
               dpv = keep ? dpv * rdrop : 0.f;
             }

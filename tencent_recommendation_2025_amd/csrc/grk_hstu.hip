@@ -26,6 +26,7 @@ struct NGParams {
   float eps;
   int64_t rows; int dim;
   float dropout_p; unsigned long long seed;
+  const unsigned long long* seed_dev;  // optional: seed read at kernel time (graph replay)
   bf16_t* y; int64_t ldy;
   float* stats;  // [rows, 2] = mean, rstd
   // backward
@@ -77,8 +78,9 @@ __device__ __forceinline__ void load8f(const float* p, float* f) {
 // dropout multiplier of the 8 elements starting at column c8
 __device__ __forceinline__ void keep8(const NGParams& p, int64_t row, int c8, float* m) {
   const float rk = 1.0f / (1.0f - p.dropout_p);
+  const unsigned long long seed = p.dropout_p > 0.f && p.seed_dev ? *p.seed_dev : p.seed;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) m[e] = p.dropout_p > 0.f ? (ng_keep(p.seed, row, c8 + e, p.dim, p.dropout_p) ? rk : 0.f) : 1.f;
+  for (int e = 0; e < 8; ++e) m[e] = p.dropout_p > 0.f ? (ng_keep(seed, row, c8 + e, p.dim, p.dropout_p) ? rk : 0.f) : 1.f;
 }
 
 // ------------------------------------------------------------------ forward --
@@ -421,13 +423,14 @@ using namespace grk;
 
 extern "C" int grk_norm_gate_fwd(const void* o, int64_t ldo, const void* u, int64_t ldu, const float* gamma,
                                  const float* beta, float eps, int64_t rows, int dim, float dropout_p, uint64_t seed,
+                                 const uint64_t* seed_dev,
                                  void* y, int64_t ldy, float* stats, void* stream) {
   clear_error();
   NGParams p;
   memset(&p, 0, sizeof(p));
   p.o = (const bf16_t*)o; p.ldo = ldo; p.u = (const bf16_t*)u; p.ldu = ldu;
   p.gamma = gamma; p.beta = beta; p.eps = eps; p.rows = rows; p.dim = dim;
-  p.dropout_p = dropout_p; p.seed = seed; p.y = (bf16_t*)y; p.ldy = ldy; p.stats = stats;
+  p.dropout_p = dropout_p; p.seed = seed; p.seed_dev = (const unsigned long long*)seed_dev; p.y = (bf16_t*)y; p.ldy = ldy; p.stats = stats;
   int rc = ng_check(p);
   if (rc) return rc;
   GRK_CHECK_ARG(rows == 0 || (y && ldy >= dim && ldy % 8 == 0 && (uintptr_t)y % 16 == 0), "bad y / ldy");
@@ -448,14 +451,15 @@ extern "C" size_t grk_norm_gate_bwd_workspace(int64_t rows, int dim) {
 
 extern "C" int grk_norm_gate_bwd(const void* gy, int64_t ldgy, const void* o, int64_t ldo, const void* u,
                                  int64_t ldu, const float* gamma, const float* beta, const float* stats, int64_t rows,
-                                 int dim, float dropout_p, uint64_t seed, void* dout, int64_t lddo, void* du,
+                                 int dim, float dropout_p, uint64_t seed, const uint64_t* seed_dev, void* dout,
+                                 int64_t lddo, void* du,
                                  int64_t lddu, float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream) {
   clear_error();
   NGParams p;
   memset(&p, 0, sizeof(p));
   p.o = (const bf16_t*)o; p.ldo = ldo; p.u = (const bf16_t*)u; p.ldu = ldu;
   p.gamma = gamma; p.beta = beta; p.rows = rows; p.dim = dim;
-  p.dropout_p = dropout_p; p.seed = seed; p.stats = const_cast<float*>(stats);
+  p.dropout_p = dropout_p; p.seed = seed; p.seed_dev = (const unsigned long long*)seed_dev; p.stats = const_cast<float*>(stats);
   p.gy = (const bf16_t*)gy; p.ldgy = ldgy; p.dout = (bf16_t*)dout; p.lddo = lddo; p.du = (bf16_t*)du; p.lddu = lddu;
   p.partial = (float*)ws; p.dgamma = dgamma; p.dbeta = dbeta;
   int rc = ng_check(p);

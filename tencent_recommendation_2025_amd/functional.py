@@ -274,6 +274,11 @@ def group_stack(group, offsets, rows):
 
 
 # ------------------------------------------------------------- attention ----
+def _seed(seed):
+    """A dropout seed: an int, or an int64 [1] device tensor read by the kernels at run time."""
+    return seed if isinstance(seed, torch.Tensor) else int(seed)
+
+
 class _SoftmaxMHAFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, key_valid, B, T, H, hd, dropout_p, seed, precise, seq_range):
@@ -314,7 +319,7 @@ def softmax_mha(qkv, key_valid, B, T, H, hd, dropout_p=0.0, seed=0, precise=True
     precise (default): probabilities / dS enter the P.V, dS.K, dS^T.Q MFMAs as
     bf16 hi + lo pairs (fp32-accurate operands; 1-4 % slower than precise=False,
     which rounds them to bf16 and is held only to 1e-2)."""
-    return _SoftmaxMHAFn.apply(qkv, key_valid, B, T, H, hd, float(dropout_p), int(seed), bool(precise), seq_range)
+    return _SoftmaxMHAFn.apply(qkv, key_valid, B, T, H, hd, float(dropout_p), _seed(seed), bool(precise), seq_range)
 
 
 class _HSTUCoreFn(torch.autograd.Function):
@@ -367,7 +372,7 @@ def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, pre
               seq_range=None):
     """Fused HSTU layer core on the [B*T, 4D] uvqk pre-activation (see _HSTUCoreFn)."""
     return _HSTUCoreFn.apply(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, float(inv_n), float(eps), bool(precise),
-                             float(dropout_p), int(seed), seq_range)
+                             float(dropout_p), _seed(seed), seq_range)
 
 
 # ---------------------------------------------------------------- logits ----

@@ -264,13 +264,24 @@ def stamp_rows(last, ids, count, capacity, t):
     L.check(rc, 'grk_stamp_rows')
 
 
+def _seed_parts(seed):
+    """(host seed, device seed tensor or None) of a dropout seed given as an int or an int64 [1] device tensor."""
+    if isinstance(seed, torch.Tensor):
+        if seed.dtype != torch.int64 or seed.numel() != 1 or not seed.is_cuda:
+            raise L.GrkError('a device dropout seed must be an int64 [1] tensor on the GPU')
+        return 0, seed
+    return int(seed) & (2 ** 64 - 1), None
+
+
 def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, inv_n=1.0, dropout_p=0.0, seed=0,
               precise=True, out_dtype=torch.bfloat16, act=None, seq_range=None):
     """Build grk_attn_args for bf16 [B*T, ld] column views q/k/v (head h at cols h*hd).
 
     act="silu": q/k/v are pre-activations; SiLU is applied on load and the
     backward's dq/dk/dv are gradients w.r.t. the pre-activations.
-    seq_range: optional int32 [B, 2] from seq_ranges(key_valid) (computed once per step)."""
+    seq_range: optional int32 [B, 2] from seq_ranges(key_valid) (computed once per step).
+    seed: an int, or a device int64 [1] tensor the kernels read when they run
+    (drawn on the device each step, so a graph-replayed step gets a fresh mask)."""
     for t, n in ((q, 'q'), (k, 'k'), (v, 'v')):
         _col_view_ok(t, n)
         if t.shape[0] != B * T or t.shape[1] < H * hd:
@@ -288,11 +299,12 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
         nb = rab.shape[1]
     if scale is None:
         scale = hd ** -0.5
+    seed, seed_dev = _seed_parts(seed)
     args = L.GrkAttnArgs(kind, B, H, T, hd, nb, q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0),
                          v.stride(0), _ptr(key_valid), _ptr(rab), float(scale), float(inv_n), float(dropout_p),
                          int(bool(precise)), int(seed) & (2 ** 64 - 1), L.dtype_code(out_dtype),
-                         {None: L.ACT_NONE, 'silu': L.ACT_SILU}[act], _ptr(seq_range))
-    args._keep = (q, k, v, key_valid, rab, seq_range)  # the struct holds raw pointers: keep the tensors alive
+                         {None: L.ACT_NONE, 'silu': L.ACT_SILU}[act], _ptr(seq_range), _ptr(seed_dev))
+    args._keep = (q, k, v, key_valid, rab, seq_range, seed_dev)  # the struct holds raw pointers: keep the tensors alive
     return args
 
 
@@ -490,7 +502,8 @@ def add_norm_bwd(gx, gs, s_new, gamma, stats):
 
 
 def norm_gate_fwd(o, u, gamma, beta, eps, dropout_p=0.0, seed=0, y=None):
-    """y = dropout(LayerNorm(o) * SiLU(u)) (grk_norm_gate_fwd).  Returns (y bf16 [N, D], stats fp32 [N, 2])."""
+    """y = dropout(LayerNorm(o) * SiLU(u)) (grk_norm_gate_fwd).  Returns (y bf16 [N, D], stats fp32 [N, 2]).
+    seed: int or device int64 [1] tensor (read at kernel time)."""
     _require_cuda(o, u, gamma, beta)
     N, D = o.shape[0], gamma.shape[0]
     dev = o.device
@@ -498,9 +511,9 @@ def norm_gate_fwd(o, u, gamma, beta, eps, dropout_p=0.0, seed=0, y=None):
         y = torch.empty(N, D, dtype=torch.bfloat16, device=dev)
     stats = torch.empty(N, 2, dtype=torch.float32, device=dev)
     (op, ol), (up, ul), (yp, yl) = _bf16_rows(o, 'o', D), _bf16_rows(u, 'u', D), _bf16_rows(y, 'y', D)
+    hs, ds = _seed_parts(seed)
     rc = L.lib().grk_norm_gate_fwd(op, ol, up, ul, gamma.data_ptr(), beta.data_ptr(), float(eps), N, D,
-                                   float(dropout_p), int(seed) & (2 ** 64 - 1), yp, yl, stats.data_ptr(),
-                                   L.stream_ptr(dev))
+                                   float(dropout_p), hs, _ptr(ds), yp, yl, stats.data_ptr(), L.stream_ptr(dev))
     L.check(rc, 'grk_norm_gate_fwd')
     return y, stats
 
@@ -519,8 +532,9 @@ def norm_gate_bwd(gy, o, u, gamma, beta, stats, dropout_p=0.0, seed=0, dout=None
     ws = torch.empty(max(L.lib().grk_norm_gate_bwd_workspace(N, D), 4), dtype=torch.uint8, device=dev)
     ptrs = [_bf16_rows(t, n, D) for t, n in ((gy, 'gy'), (o, 'o'), (u, 'u'), (dout, 'dout'), (du, 'du'))]
     (gp, gl), (op, ol), (up, ul), (dp, dl), (dup, dul) = ptrs
+    hs, ds = _seed_parts(seed)
     rc = L.lib().grk_norm_gate_bwd(gp, gl, op, ol, up, ul, gamma.data_ptr(), beta.data_ptr(), stats.data_ptr(), N, D,
-                                   float(dropout_p), int(seed) & (2 ** 64 - 1), dp, dl, dup, dul, dgamma.data_ptr(),
+                                   float(dropout_p), hs, _ptr(ds), dp, dl, dup, dul, dgamma.data_ptr(),
                                    dbeta.data_ptr(), ws.data_ptr(), ws.numel(), L.stream_ptr(dev))
     L.check(rc, 'grk_norm_gate_bwd')
     return dout, du, dgamma, dbeta

@@ -67,10 +67,21 @@ class FlashMultiHeadAttention(torch.nn.Module):
         else:
             qkv = torch.cat([self.q_linear(query), self.k_linear(key), self.v_linear(value)], -1)
         p = self.dropout_rate if self.training else 0.0
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+        seed = dropout_seed(qkv.device) if p > 0 else 0
         o = G.softmax_mha(qkv.reshape(B * T, 3 * D), key_valid, B, T, self.num_heads, self.head_dim, p, seed,
                           seq_range=seq_range)
         return _linear(o.view(B, T, D), self.out_linear.weight, self.out_linear.bias), None
+
+
+def dropout_seed(device):
+    """The grk dropout seed of one launch: an int64 [1] drawn on the device from
+    torch's generator and read by the kernels when they run.  No host round
+    trip, and a step replayed from a HIP graph draws a fresh one every replay
+    (torch registers its generator with the graph), exactly as the eager step
+    would draw it."""
+    if device.type != 'cuda':
+        return int(torch.randint(0, 2 ** 62, (1,)).item())
+    return torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
 
 
 def key_valid_from_mask(attn_mask, B, T):
@@ -103,8 +114,8 @@ class HSTUAttention(torch.nn.Module):
         y = out_linear(dropout(LayerNorm(HSTU-attn(q, k, v, rab)) * u))
 
     The SiLU, LayerNorm, gating and dropout run inside the grk kernels
-    (functional.hstu_core); dropout uses grk's counter-hash mask, not torch's
-    Philox stream.
+    (functional.hstu_core); dropout uses grk's counter-hash mask (seeded from
+    torch's generator on the device), not torch's Philox stream.
     """
 
     def __init__(self, hidden_units, num_heads, dropout_rate, num_buckets):
@@ -124,7 +135,7 @@ class HSTUAttention(torch.nn.Module):
             key_valid = key_valid_from_mask(attn_mask, B, T)
         pre = _linear(query, self.uvqk.weight, self.uvqk.bias).reshape(B * T, 4 * D)
         p = self.dropout_rate if self.training else 0.0
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+        seed = dropout_seed(pre.device) if p > 0 else 0
         y = G.hstu_core(pre, self.rab, self.attn_norm.weight, self.attn_norm.bias, key_valid, B, T,
                         self.num_heads, self.head_dim, 1.0 / T, self.attn_norm.eps, dropout_p=p, seed=seed,
                         seq_range=seq_range)

@@ -59,9 +59,10 @@ class Trainer:
     loss: "bce" -- the reference loss (pos/neg BCE, main.py:177-182);
           "sampled_softmax" -- north-star in-batch sampled softmax.
     graph: capture the step in a HIP graph after ``graph_warmup`` eager steps
-          and replay it (needs a fused optimizer with a device clock, no
-          attention dropout, and batches of one fixed shape; a batch of another
-          shape runs eagerly).
+          and replay it (needs a fused optimizer with a device clock and batches
+          of one fixed shape; a batch of another shape runs eagerly).  Dropout
+          seeds are drawn on the device (model.dropout_seed), so dropout runs
+          inside the replayed step.
     """
 
     def __init__(self, model, optimizer, loss='bce', amp_dtype=torch.bfloat16, temperature=0.05, graph=False,
@@ -87,9 +88,6 @@ class Trainer:
             return 'needs a GPU'
         if getattr(self.opt, 'clock', None) is None:
             return 'the optimizer must keep a device clock (optim.FusedAdamW on the GPU)'
-        for m in self.model.modules():
-            if getattr(m, 'dropout_rate', 0.0) and m.training:
-                return 'attention dropout draws a host-side seed per step'
         return None
 
     def compute_loss(self, batch):

@@ -172,3 +172,43 @@ def test_add_norm_matches_torch(with_y, x_dtype):
         torch.testing.assert_close(y.grad.float(), y2.grad, rtol=2e-2, atol=3e-2)
     torch.testing.assert_close(w.grad, w2.grad, rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(b.grad, b2.grad, rtol=1e-3, atol=1e-2)
+
+
+def test_device_seed_equals_host_seed():
+    """A dropout seed held in device memory (read by the kernels at run time,
+    model.dropout_seed) gives bitwise the masks of the same seed passed by value:
+    norm gate forward / backward and softmax attention forward / backward."""
+    from tencent_recommendation_2025_amd import _lib as L
+    g = torch.Generator(device=DEV).manual_seed(11)
+    rows, dim, p, seed = 300, 256, 0.2, 1234567890123
+    o = torch.randn(rows, dim, device=DEV, generator=g).bfloat16()
+    u = torch.randn(rows, dim, device=DEV, generator=g).bfloat16()
+    w = torch.randn(dim, device=DEV, generator=g)
+    b = torch.randn(dim, device=DEV, generator=g)
+    gy = torch.randn(rows, dim, device=DEV, generator=g).bfloat16()
+    dseed = torch.tensor([seed], dtype=torch.int64, device=DEV)
+    outs = []
+    for s in (seed, dseed):
+        y, st = K.norm_gate_fwd(o, u, w, b, 1e-8, p, s)
+        do, du, dw, db = K.norm_gate_bwd(gy, o, u, w, b, st, p, s)
+        outs.append((y, do, du, dw, db))
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+    B, T, H, hd = 3, 97, 2, 32
+    D = H * hd
+    x = torch.randn(B * T, 3 * D, device=DEV, generator=g).bfloat16()
+    kv = torch.ones(B, T, dtype=torch.uint8, device=DEV)
+    kv[1, :40] = 0
+    dout = torch.randn(B * T, D, device=DEV, generator=g).bfloat16()
+    res = []
+    for s in (seed, dseed):
+        args = K.attn_args(L.ATTN_SOFTMAX, x[:, :D], x[:, D:2 * D], x[:, 2 * D:], B, T, H, hd, key_valid=kv,
+                           dropout_p=0.2, seed=s)
+        out = torch.empty(B * T, D, dtype=torch.bfloat16, device=DEV)
+        lse = torch.empty(B, H, T, device=DEV)
+        K.attention_fwd(args, out, lse)
+        grads = [torch.empty(B * T, D, dtype=torch.bfloat16, device=DEV) for _ in range(3)]
+        K.attention_bwd(args, out, dout, lse, torch.empty(B, H, T, device=DEV), *grads)
+        res.append([out, *grads])
+    for a, c in zip(*res):
+        assert torch.equal(a, c)

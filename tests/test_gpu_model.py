@@ -399,3 +399,38 @@ def test_bench_config_step_matches_oracle_fp32():
     assert len(grads) == sum(1 for p in ref.parameters()), sorted(set(rp) - set(grads))
     for k, tol in BENCH_TOL.items():
         assert errs[k] < tol, (k, errs[k], sorted(grads.items(), key=lambda kv: -kv[1])[:8])
+
+
+@pytest.mark.parametrize('block', ['hstu', 'softmax'])
+def test_graph_replay_with_dropout_equals_eager(block):
+    """The reference's dropout_rate 0.01 (BaseLine/main.py:30) inside the
+    graph-replayed step: grk dropout seeds are drawn on the device from torch's
+    generator (model.dropout_seed), torch's own dropouts replay their Philox
+    offsets -- so replays equal the eager steps bit for bit."""
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    cfg = S.SyntheticConfig(batch_size=8, maxlen=30, num_items=5000, num_users=700, min_len=4)
+    stats, types = S.feature_schema(cfg)
+    args = S.make_args(hidden_units=64, maxlen=30, num_blocks=2, num_heads=2, dropout_rate=0.2, block=block)
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, args).to(DEV)
+        m.train()
+        opt = FusedAdamW(m, lr=2e-3, defer_period=4)
+        tr = Trainer(m, opt, loss='bce', graph=graph, graph_warmup=2)
+        g = torch.Generator(device=DEV).manual_seed(0)
+        batches = [S.make_batch(cfg, g, DEV) for _ in range(3)]
+        torch.manual_seed(123)
+        losses = [tr.step(batches[i % 3]).clone() for i in range(6)]
+        if graph:
+            assert tr._g is not None
+        sd = m.state_dict()
+        torch.cuda.synchronize()
+        runs.append((torch.stack(losses), sd))
+    assert torch.equal(runs[0][0], runs[1][0]), (runs[0][0], runs[1][0])
+    for k in runs[0][1]:
+        assert torch.equal(runs[0][1][k], runs[1][1][k]), k
+    assert len(set(runs[0][0].tolist())) > 1  # the losses move: six real steps
