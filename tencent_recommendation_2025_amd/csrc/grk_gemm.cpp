@@ -9,16 +9,17 @@
 // uvqk forward (scripts/microbench/hipblaslt_search.cpp).  This file keeps a
 // handle per device, a workspace per (device, stream) and one plan per
 // problem shape: descriptors + the fastest of hipBLASLt's heuristic
-// candidates, timed once on the shape's first call (the library's first pick
-// is up to 2x slower here: uvqk forward 111 vs 63 us).  The choice is fixed for
-// the process; grk_gemm_tuning(1) keeps the heuristic's first pick (the same
-// kernels in every run).
+// candidates that passes validation, timed once on the shape's first call (the
+// library's first pick is up to 2x slower here: uvqk forward 111 vs 63 us).
+// The choice is fixed for the process; grk_gemm_tuning(1) keeps the heuristic's
+// first usable pick (the same kernels in every run).
 //
 // Row-major interface (as torch tensors): C[m, n] = alpha op(A) op(B) + beta C_in
 // (+ bias[n]), computed as the column-major C^T = op(B)^T op(A)^T.
 #include <hipblaslt/hipblaslt-ext.hpp>
 #include <hipblaslt/hipblaslt.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <mutex>
@@ -90,6 +91,13 @@ struct Operands {  // the first call's operands, for timing candidate algorithms
   bool capturing;
 };
 
+// One launch of an algorithm into `out` (beta = 0).
+bool run_algo(hipblasLtHandle_t h, Plan* p, const hipblasLtMatmulAlgo_t* algo, const Operands& o, void* out) {
+  const float alpha = 1.f, beta = 0.f;
+  return hipblasLtMatmul(h, p->op, &alpha, o.b, p->A, o.a, p->B, &beta, out, p->C, out, p->C, algo, o.ws,
+                         kWorkspaceBytes, o.s) == HIPBLAS_STATUS_SUCCESS;
+}
+
 // Average time of `reps` launches of one algorithm into a scratch output (never the caller's C).
 float time_algo(hipblasLtHandle_t h, Plan* p, const hipblasLtMatmulAlgo_t* algo, const Operands& o, void* scratch,
                 int reps) {
@@ -149,24 +157,67 @@ int make_plan(hipblasLtHandle_t h, const Key& key, bool has_bias, Plan* p, const
                    (long long)key.n, (long long)key.k, key.ta, key.tb);
     return GRK_EHIP;
   }
-  int best = 0;
+  // Candidate order: fastest first (timed on the first call's operands), then each is
+  // VALIDATED before it is kept: run on the operands and on copies of them at other
+  // addresses, the two outputs must be bitwise equal.  hipBLASLt's
+  // "Custom_Cijk_..._UserArgs_shortname*" kernels fail exactly that on gfx950 (right
+  // on their first call, stale results once the operand pointers change:
+  // scripts/microbench/gemm_validate.hip); they are skipped outright,
+  // and the validation rejects any other candidate with the same defect.
+  std::vector<int> order;
+  std::vector<float> tms(n, -1.f);
+  for (int i = 0; i < n; ++i)
+    if (hipblaslt_ext::getKernelNameFromAlgo(h, res[i].algo).rfind("Custom_", 0) != 0) order.push_back(i);
+  if (order.empty()) {
+    grk::set_error("hipBLASLt offers only Custom_ kernels for this GEMM (m=%lld n=%lld k=%lld)", (long long)key.m,
+                   (long long)key.n, (long long)key.k);
+    return GRK_EHIP;
+  }
+  int best = order[0];
   float t0 = -1.f, tbest = -1.f;
-  if (n > 1 && !o.capturing) {  // no timing inside a HIP graph capture: the heuristic's first choice
-    void* scratch = nullptr;
+  if (!o.capturing) {  // no timing / validation inside a HIP graph capture: the heuristic's first usable pick
     const size_t cbytes = (size_t)key.ldc * key.m * (key.ct == GRK_F32 ? 4 : 2);
-    if (hipMalloc(&scratch, cbytes) == hipSuccess) {
+    const size_t abytes = (size_t)key.lda * (key.ta ? key.k : key.m) * 2;
+    const size_t bbytes = (size_t)key.ldb * (key.tb ? key.n : key.k) * 2;
+    void *scratch = nullptr, *scratch2 = nullptr, *a2 = nullptr, *b2 = nullptr;
+    if (hipMalloc(&scratch, cbytes) == hipSuccess && hipMalloc(&scratch2, cbytes) == hipSuccess &&
+        hipMalloc(&a2, abytes) == hipSuccess && hipMalloc(&b2, bbytes) == hipSuccess) {
       if (has_bias)
         hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &o.bias, sizeof(o.bias));
-      for (int i = 0; i < n; ++i) {
-        const float t = time_algo(h, p, &res[i].algo, o, scratch, 5);
-        if (i == 0) t0 = t;
-        if (t > 0 && (tbest < 0 || t < tbest)) {
-          tbest = t;
+      (void)hipMemcpyAsync(a2, o.a, abytes, hipMemcpyDeviceToDevice, o.s);
+      (void)hipMemcpyAsync(b2, o.b, bbytes, hipMemcpyDeviceToDevice, o.s);
+      if (order.size() > 1)
+        for (int i : order) tms[i] = time_algo(h, p, &res[i].algo, o, scratch, 5);
+      t0 = tms[order[0]];
+      std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+        const float tx = tms[x] > 0 ? tms[x] : 3.0e38f, ty = tms[y] > 0 ? tms[y] : 3.0e38f;
+        return tx < ty;
+      });
+      std::vector<char> h1(cbytes), h2(cbytes);
+      Operands moved = o;
+      moved.a = a2;
+      moved.b = b2;
+      best = -1;
+      for (int i : order) {
+        if (run_algo(h, p, &res[i].algo, o, scratch) && run_algo(h, p, &res[i].algo, moved, scratch2) &&
+            hipMemcpy(h1.data(), scratch, cbytes, hipMemcpyDeviceToHost) == hipSuccess &&
+            hipMemcpy(h2.data(), scratch2, cbytes, hipMemcpyDeviceToHost) == hipSuccess &&
+            memcmp(h1.data(), h2.data(), cbytes) == 0) {
           best = i;
+          tbest = tms[i];
+          break;
         }
       }
       (void)hipDeviceSynchronize();
-      (void)hipFree(scratch);
+    }
+    if (scratch) (void)hipFree(scratch);
+    if (scratch2) (void)hipFree(scratch2);
+    if (a2) (void)hipFree(a2);
+    if (b2) (void)hipFree(b2);
+    if (best < 0) {
+      grk::set_error("grk_gemm: no hipBLASLt candidate passed validation (m=%lld n=%lld k=%lld)", (long long)key.m,
+                     (long long)key.n, (long long)key.k);
+      return GRK_EHIP;
     }
   }
   p->algo = res[best].algo;

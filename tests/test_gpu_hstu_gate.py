@@ -174,7 +174,7 @@ def test_add_norm_matches_torch(with_y, x_dtype):
     torch.testing.assert_close(b.grad, b2.grad, rtol=1e-3, atol=1e-2)
 
 
-def test_device_seed_equals_host_seed():
+def test_device_seed_equals_host_seed(K):
     """A dropout seed held in device memory (read by the kernels at run time,
     model.dropout_seed) gives bitwise the masks of the same seed passed by value:
     norm gate forward / backward and softmax attention forward / backward."""

@@ -434,3 +434,25 @@ def test_graph_replay_with_dropout_equals_eager(block):
     for k in runs[0][1]:
         assert torch.equal(runs[0][1][k], runs[1][1][k]), k
     assert len(set(runs[0][0].tolist())) > 1  # the losses move: six real steps
+
+
+@pytest.mark.parametrize('shape', [(248, 512, 64), (248, 64, 256), (25728, 2048, 512), (25728, 512, 2048),
+                                   (51456, 512, 552)])
+def test_grk_gemm_repeated_calls_with_moving_operands(shape):
+    """grk_gemm's plan for a shape is reused with new operand tensors every call
+    (functional.linear casts its operands afresh).  hipBLASLt's
+    Custom_..._UserArgs kernels return stale results once the pointers change
+    (right on the first call only); grk_gemm skips them and validates its pick by
+    running it on relocated operands.  Every call must match the reference."""
+    from tencent_recommendation_2025_amd import kernels as K
+    m, n, k = shape
+    g = torch.Generator(device=DEV).manual_seed(m + n + k)
+    x = torch.randn(m, k, device=DEV, generator=g)
+    w = torch.randn(n, k, device=DEV, generator=g)
+    ref = x.bfloat16().float() @ w.bfloat16().float().t()
+    keep = []
+    for i in range(5):
+        keep.append(torch.empty(1 + 4096 * i, device=DEV))   # move the next allocations
+        y = K.gemm(x.bfloat16(), w.bfloat16(), trans_b=True)
+        err = float((y.float() - ref).norm() / ref.norm())
+        assert err < 5e-3, (i, err)
