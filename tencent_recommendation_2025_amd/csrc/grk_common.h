@@ -103,27 +103,29 @@ template <> struct Vec16<bf16_t> {
 inline size_t dtype_size(int dt) { return dt == GRK_F32 ? 4 : 2; }
 
 namespace {
-// Zero-fill as a kernel (16-byte stores, 4-byte tail): used instead of
-// hipMemsetAsync for every buffer that must be zero at a kernel's start, so a
-// step captured in a HIP graph replays the fill as an ordinary kernel node.
+// Zero-fill as a kernel (16-byte stores when aligned, 4-byte stores otherwise).
+// Used instead of hipMemsetAsync for every buffer that must be zero at a
+// kernel's start: a hipMemsetAsync captured into a HIP graph does not zero its
+// buffer on the second and later replays (ROCm 7.2; any size above 4 bytes --
+// scripts/graph_memset_check.py), so nothing in a step that may
+// be captured uses one.
 __global__ void k_zero_fill(uint32_t* __restrict__ p, size_t words, size_t vecs) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < vecs; i += stride)
-    reinterpret_cast<uint4*>(p)[i] = make_uint4(0u, 0u, 0u, 0u);
-  if (blockIdx.x == 0 && threadIdx.x < words - vecs * 4) p[vecs * 4 + threadIdx.x] = 0u;
+  const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (size_t i = t0; i < vecs; i += stride) reinterpret_cast<uint4*>(p)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (size_t i = vecs * 4 + t0; i < words; i += stride) p[i] = 0u;
 }
 }  // namespace
 
-// bytes: a multiple of 4.  16-byte aligned buffers (every torch allocation) or
-// buffers of <= 256 words take the kernel; anything else falls back to hipMemsetAsync.
+// bytes: a multiple of 4.  Never a hipMemsetAsync (see k_zero_fill).
 inline hipError_t zero_async(void* p, size_t bytes, hipStream_t s) {
   const size_t words = bytes / 4;
   if (words == 0) return hipSuccess;
   const bool aligned = (uintptr_t)p % 16 == 0;
-  if (!aligned && words > 256) return hipMemsetAsync(p, 0, bytes, s);
   const size_t vecs = aligned ? words / 4 : 0;
-  const size_t blocks = (vecs + 255) / 256;
-  k_zero_fill<<<(unsigned)(blocks == 0 ? 1 : (blocks < 4096 ? blocks : 4096)), 256, 0, s>>>((uint32_t*)p, words, vecs);
+  const size_t work = aligned ? (vecs > 0 ? vecs : 1) : words;
+  const size_t blocks = (work + 255) / 256;
+  k_zero_fill<<<(unsigned)(blocks < 4096 ? blocks : 4096), 256, 0, s>>>((uint32_t*)p, words, vecs);
   return hipGetLastError();
 }
 

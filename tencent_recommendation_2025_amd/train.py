@@ -22,7 +22,6 @@ the device to drain before its all-to-alls."""
 from __future__ import annotations
 
 import contextlib
-import time
 
 import torch
 
@@ -66,12 +65,14 @@ class Trainer:
     """
 
     def __init__(self, model, optimizer, loss='bce', amp_dtype=torch.bfloat16, temperature=0.05, graph=False,
-                 graph_warmup=3):
+                 graph_warmup=3, graph_audit=False):
         if loss not in ('bce', 'sampled_softmax'):
             raise ValueError("loss must be 'bce' or 'sampled_softmax'")
         self.model, self.opt, self.loss_kind = model, optimizer, loss
         self.amp_dtype, self.temperature = amp_dtype, temperature
         self.graph, self.graph_warmup = bool(graph), int(graph_warmup)
+        self.graph_audit = bool(graph_audit)  # keep the captured graph and census its nodes (graph_nodes)
+        self.graph_nodes = None
         if self.graph:
             why = self._graph_blocker()
             if why:
@@ -170,17 +171,15 @@ class Trainer:
         else:
             self.opt.maybe_segment()
         torch.cuda.synchronize()
-        if torch.distributed.is_available() and torch.distributed.is_initialized():
-            # let the process groups' watchdog threads reap the (complete) collectives
-            # issued so far, so none of their events is polled while we capture (seen
-            # under rocprofv3 as a watchdog abort with a collective still listed)
-            time.sleep(1.0)
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=self.graph_audit)
         cur = torch.cuda.current_stream()
         self._side.wait_stream(cur)
         # thread_local: the process group's watchdog thread polls its collectives'
-        # events while we capture; under the default global mode that poll is an
-        # illegal call during capture and aborts the process
+        # events (hipEventQuery) while we capture.  Under the default global mode a
+        # capture forbids such calls from EVERY thread: the poll fails with a
+        # capture error, which the watchdog treats as fatal and aborts the process
+        # (seen in round 1).  thread_local confines the restriction to this thread,
+        # so the watchdog's polls are legal and nothing needs to wait for it.
         with torch.cuda.graph(g, stream=self._side, capture_error_mode='thread_local'):
             if self._sharded:
                 loss = self.compute_loss(self._static)
@@ -189,6 +188,9 @@ class Trainer:
             else:
                 self._static_loss = self.eager_step(self._static)
         cur.wait_stream(self._side)
+        if self.graph_audit:
+            self.graph_nodes = graph_node_census(g)
+            g.instantiate()
         self._g = g
         g.replay()               # the captured step itself (host state already advanced)
         if self._sharded:
@@ -197,6 +199,43 @@ class Trainer:
             self.opt.capture_state()
             self.opt.step()
         return self._static_loss.clone()
+
+
+_NODE_TYPES = {0: 'kernel', 1: 'memcpy', 2: 'memset', 3: 'host', 4: 'graph', 5: 'empty', 6: 'wait_event',
+               7: 'event_record', 10: 'mem_alloc', 11: 'mem_free'}
+
+
+def graph_node_census(g):
+    """{node type: count} of a captured torch.cuda.CUDAGraph(keep_graph=True), plus
+    'memset_bytes': the byte count of every memset node.  A memset node does not
+    re-zero its buffer on the second and later replays (ROCm 7.2,
+    scripts/graph_memset_check.py), so the training step must contain none
+    larger than 4 bytes (the one size that replays correctly)."""
+    import ctypes as C
+    hip = C.CDLL('libamdhip64.so.7')
+    graph = C.c_void_p(g.raw_cuda_graph())
+    n = C.c_size_t(0)
+    if hip.hipGraphGetNodes(graph, None, C.byref(n)) != 0:
+        raise RuntimeError('hipGraphGetNodes failed')
+    nodes = (C.c_void_p * n.value)()
+    if hip.hipGraphGetNodes(graph, nodes, C.byref(n)) != 0:
+        raise RuntimeError('hipGraphGetNodes failed')
+
+    class MemsetParams(C.Structure):
+        _fields_ = [('dst', C.c_void_p), ('elementSize', C.c_uint), ('height', C.c_size_t), ('pitch', C.c_size_t),
+                    ('value', C.c_uint), ('width', C.c_size_t)]
+
+    out = {'memset_bytes': []}
+    for i in range(n.value):
+        t = C.c_int(-1)
+        hip.hipGraphNodeGetType(C.c_void_p(nodes[i]), C.byref(t))
+        name = _NODE_TYPES.get(t.value, f'type{t.value}')
+        out[name] = out.get(name, 0) + 1
+        if name == 'memset':
+            prm = MemsetParams()
+            hip.hipGraphMemsetNodeGetParams(C.c_void_p(nodes[i]), C.byref(prm))
+            out['memset_bytes'].append(prm.elementSize * prm.width * max(prm.height, 1))
+    return out
 
 
 def _copy_batch(dst, src):

@@ -456,3 +456,30 @@ def test_grk_gemm_repeated_calls_with_moving_operands(shape):
         y = K.gemm(x.bfloat16(), w.bfloat16(), trans_b=True)
         err = float((y.float() - ref).norm() / ref.norm())
         assert err < 5e-3, (i, err)
+
+
+@pytest.mark.parametrize('block', ['hstu', 'softmax'])
+def test_captured_step_has_no_memset_nodes(block):
+    """The graph-captured training step holds no memset node above 4 bytes: such
+    a node does not re-zero its buffer on the second and later replays (ROCm 7.2;
+    scripts/graph_memset_check.py) -- the cause of round 1's wrong accumulators
+    and of the rocprim onesweep sort's illegal address under replay (its
+    histogram and look-back states are cleared with hipMemsetAsync)."""
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    cfg = S.SyntheticConfig(batch_size=8, maxlen=30, num_items=5000, num_users=700, min_len=4)
+    stats, types = S.feature_schema(cfg)
+    args = S.make_args(hidden_units=64, maxlen=30, num_blocks=2, num_heads=2, dropout_rate=0.1, block=block)
+    m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, args).to(DEV)
+    tr = Trainer(m, FusedAdamW(m, lr=1e-3, defer_period=4), loss='bce', graph=True, graph_warmup=2,
+                 graph_audit=True)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    losses = [tr.step(S.make_batch(cfg, g, DEV)).item() for _ in range(4)]
+    census = tr.graph_nodes
+    print('captured step nodes:', {k: v for k, v in census.items() if k != 'memset_bytes'},
+          'memset bytes:', census['memset_bytes'])
+    assert census.get('kernel', 0) > 50
+    assert all(b <= 4 for b in census['memset_bytes']), census['memset_bytes']
+    assert np.all(np.isfinite(losses))
