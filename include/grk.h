@@ -38,7 +38,7 @@ extern "C" {
 #endif
 
 enum { GRK_OK = 0, GRK_EINVAL = 1, GRK_EHIP = 2, GRK_EUNSUPPORTED = 3 };
-enum { GRK_F32 = 0, GRK_BF16 = 1 };                 /* floating dtypes */
+enum { GRK_F32 = 0, GRK_BF16 = 1, GRK_F16 = 2 };    /* floating dtypes */
 enum { GRK_I32 = 0, GRK_I64 = 1 };                  /* index dtypes */
 
 /* How a lookup derives its row id from the index tensor value v at token
@@ -227,7 +227,12 @@ typedef struct grk_attn_args {
   float scale;                     /* softmax: 1/sqrt(hd); hstu: alpha            */
   float inv_n;                     /* hstu: 1/n                                   */
   float dropout_p;                 /* softmax training dropout                    */
-  int32_t precise;                 /* 1: P / dS fed to MFMA as bf16 hi+lo pairs   */
+  int32_t precise;                 /* 1: P / dS fed to MFMA as bf16 hi+lo pairs;
+                                      2 (fp32 fidelity): Q/K/V and dO as well, each
+                                      product as hi*hi + hi*lo + lo*hi; q/k/v then
+                                      have dtype qkv_dtype (whole-sequence kernels
+                                      only: GRK_EUNSUPPORTED where T x hd does not
+                                      fit LDS)                                   */
   uint64_t seed;                   /* dropout stream                              */
   int32_t out_dtype;               /* GRK_F32 / GRK_BF16 for out, dq, dk, dv      */
   int32_t act;                     /* GRK_ACT_*: activation applied to q/k/v      */
@@ -238,7 +243,14 @@ typedef struct grk_attn_args {
                                       read by the kernels when they run (replaces
                                       `seed`): a step replayed from a HIP graph
                                       draws a fresh mask every replay           */
+  int32_t qkv_dtype;               /* precise == 2: GRK_F32 / GRK_F16 / GRK_BF16
+                                      q/k/v (read exactly, split into bf16 hi+lo);
+                                      ignored otherwise (bf16)                  */
 } grk_attn_args;
+
+/* 1 when grk_attention_* with precise == 2 (fp32 fidelity) runs for this
+ * sequence length and head_dim (the whole-sequence kernels' LDS), else 0. */
+int grk_attention_fidelity_supported(int seq_len, int head_dim);
 
 /* ranges[b] = (first j with key_valid[b, j], 1 if the valid keys are exactly
  * [first, T) else 0); first = T for an all-padding row.  One launch per step

@@ -22,7 +22,7 @@ REPO_DIR = PKG_DIR.parent
 LIB_PATH = Path(os.environ.get('GRK_LIB', PKG_DIR / 'libgrk.so'))
 
 GRK_OK, GRK_EINVAL, GRK_EHIP, GRK_EUNSUPPORTED = 0, 1, 2, 3
-GRK_F32, GRK_BF16 = 0, 1
+GRK_F32, GRK_BF16, GRK_F16 = 0, 1, 2
 GRK_I32, GRK_I64 = 0, 1
 IDX_PLAIN, IDX_ITEM_MASK, IDX_USER_MASK, IDX_POSITION = 0, 1, 2, 3
 ADAM_DENSE, ADAM_LAZY = 0, 1
@@ -52,7 +52,7 @@ class GrkAttnArgs(C.Structure):
                 ('v', C.c_void_p), ('ldq', C.c_int64), ('ldk', C.c_int64), ('ldv', C.c_int64),
                 ('key_valid', C.c_void_p), ('rab', C.c_void_p), ('scale', C.c_float), ('inv_n', C.c_float),
                 ('dropout_p', C.c_float), ('precise', C.c_int32), ('seed', C.c_uint64), ('out_dtype', C.c_int32),
-                ('act', C.c_int32), ('seq_range', C.c_void_p), ('seed_dev', C.c_void_p)]
+                ('act', C.c_int32), ('seq_range', C.c_void_p), ('seed_dev', C.c_void_p), ('qkv_dtype', C.c_int32)]
 
 
 ATTN_SOFTMAX, ATTN_HSTU = 0, 1
@@ -84,6 +84,7 @@ SIGNATURES = {
     'grk_table_adamw_catchup_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _I64, _P, C.c_int32, _P, _P]),
     'grk_stamp_rows_dev': (_I, [_P, _P, _P, _I64, _P, _P]),
     'grk_attention_fwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _P]),
+    'grk_attention_fidelity_supported': (_I, [_I, _I]),
     'grk_attention_bwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64, _P, _I64,
                                _P, _P, _P]),
     'grk_attention_bwd_parts': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64,
@@ -155,7 +156,9 @@ def dtype_code(t: torch.dtype) -> int:
         return GRK_F32
     if t == torch.bfloat16:
         return GRK_BF16
-    raise GrkError(f'unsupported dtype {t} (float32 / bfloat16 only)')
+    if t == torch.float16:
+        return GRK_F16
+    raise GrkError(f'unsupported dtype {t} (float32 / bfloat16 / float16)')
 
 
 def itype_code(t: torch.dtype) -> int:

@@ -21,7 +21,8 @@ struct AttnParams {
   const unsigned long long* seed_dev;  // optional: seed read at kernel time (graph replay)
   const float* rab;
   int nb;
-  int precise;
+  int precise;      // 0 fast, 1 hi/lo P and dS, 2 + hi/lo Q/K/V/dO (fp32 fidelity)
+  int in_dt;        // precise == 2: dtype of q/k/v (GRK_F32 / GRK_F16 / GRK_BF16)
   int out_f32;
   int act;  // GRK_ACT_SILU: q/k/v are pre-activations
   const int* seq_range;  // optional [B, 2] (first valid key, contiguous flag)
@@ -35,6 +36,41 @@ struct AttnParams {
   float* drab;
 };
 
+
+// Eight consecutive elements of a q/k/v/dO row as exact fp32 (dtype GRK_F32 /
+// GRK_F16 / GRK_BF16), zero when !ok.
+__device__ __forceinline__ void gload8f(const void* base, int64_t off, int dt, bool ok, float* f) {
+  if (!ok) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = 0.f;
+    return;
+  }
+  if (dt == 0) {  // GRK_F32
+    const float4* fp = reinterpret_cast<const float4*>((const float*)base + off);
+    const float4 a = fp[0], b = fp[1];
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  } else if (dt == 2) {  // GRK_F16
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    const h8 v = *reinterpret_cast<const h8*>((const _Float16*)base + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
+  } else {
+    const bf16x8 v = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>((const bf16_t*)base + off));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
+  }
+}
+
+// x = hi + lo with hi = bf16(x), lo = bf16(x - hi): 16 significant bits (fp16
+// values exactly; fp32 to ~2^-17 relative).
+__device__ __forceinline__ void split8(const float* f, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = static_cast<__bf16>(f[j]);
+    hi[j] = h;
+    lo[j] = static_cast<__bf16>(f[j] - static_cast<float>(h));
+  }
+}
 
 // The dropout seed of a launch: the device value when one is given.
 __device__ __forceinline__ unsigned long long attn_seed(const AttnParams& p) {
@@ -108,8 +144,8 @@ __device__ __forceinline__ void store4<bf16_t>(bf16_t* p, const float* v) {
 // and is multiplied by dSiLU(pre) read from the same position of dsrc.
 template <int HD, int NDT>
 __device__ __forceinline__ void store_rows(void* out, int64_t ld, bool f32, int64_t tok, int h, int hh,
-                                           const f32x16* acc, float mul, bool ok, const bf16_t* dsrc = nullptr,
-                                           int64_t ldsrc = 0) {
+                                           const f32x16* acc, float mul, bool ok, const void* dsrc = nullptr,
+                                           int64_t ldsrc = 0, int dsrc_dt = 1) {
   if (!ok) return;
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
@@ -118,12 +154,17 @@ __device__ __forceinline__ void store_rows(void* out, int64_t ld, bool f32, int6
       const int d = dt * 32 + 8 * g + 4 * hh;
       if (d >= HD) continue;
       float v[4] = {acc[dt][4 * g] * mul, acc[dt][4 * g + 1] * mul, acc[dt][4 * g + 2] * mul, acc[dt][4 * g + 3] * mul};
-      if (dsrc) {
-        const uint2 pw = *reinterpret_cast<const uint2*>(dsrc + tok * ldsrc + h * HD + d);
+      if (dsrc && dsrc_dt == 1) {
+        const uint2 pw = *reinterpret_cast<const uint2*>((const bf16_t*)dsrc + tok * ldsrc + h * HD + d);
         v[0] *= dsilu(__uint_as_float(pw.x << 16));
         v[1] *= dsilu(__uint_as_float(pw.x & 0xFFFF0000u));
         v[2] *= dsilu(__uint_as_float(pw.y << 16));
         v[3] *= dsilu(__uint_as_float(pw.y & 0xFFFF0000u));
+      } else if (dsrc) {  // fp32 / fp16 pre-activations (fidelity mode)
+        const int64_t o4 = tok * ldsrc + h * HD + d;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[e] *= dsilu(dsrc_dt == 0 ? ((const float*)dsrc)[o4 + e] : (float)((const _Float16*)dsrc)[o4 + e]);
       }
       const int64_t off = tok * ld + h * HD + d;
       if (f32) store4<float>((float*)out + off, v);

@@ -424,6 +424,11 @@ static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
     GRK_LAUNCH_CHECK();
     return GRK_OK;
   }
+  if (p.precise == 2 && which != 1) {
+    set_error("fp32-fidelity attention (precise = 2) runs in the whole-sequence kernels only: T = %d x head_dim %d "
+              "does not fit their LDS", p.T, hd);
+    return GRK_EUNSUPPORTED;
+  }
   switch (hd) {
     case 16: return launch_hd<16>(p, which, s);
     case 32: return launch_hd<32>(p, which, s);
@@ -451,6 +456,9 @@ static int fill_params(const grk_attn_args* a, AttnParams* p) {
   GRK_CHECK_ARG(a->kind == GRK_ATTN_SOFTMAX || a->dropout_p == 0.f, "hstu attention has no dropout");
   GRK_CHECK_ARG(a->out_dtype == GRK_F32 || a->out_dtype == GRK_BF16, "out_dtype must be GRK_F32 / GRK_BF16");
   GRK_CHECK_ARG(a->act == GRK_ACT_NONE || a->act == GRK_ACT_SILU, "act must be GRK_ACT_NONE / GRK_ACT_SILU");
+  GRK_CHECK_ARG(a->precise >= 0 && a->precise <= 2, "precise must be 0, 1 or 2");
+  GRK_CHECK_ARG(a->precise != 2 || a->qkv_dtype == GRK_F32 || a->qkv_dtype == GRK_F16 || a->qkv_dtype == GRK_BF16,
+                "qkv_dtype must be GRK_F32 / GRK_F16 / GRK_BF16");
   memset(p, 0, sizeof(*p));
   p->kind = a->kind; p->B = a->batch; p->H = a->heads; p->T = a->seq_len;
   p->q = (const bf16_t*)a->q; p->k = (const bf16_t*)a->k; p->v = (const bf16_t*)a->v;
@@ -459,6 +467,7 @@ static int fill_params(const grk_attn_args* a, AttnParams* p) {
   p->scale = a->scale; p->inv_n = a->inv_n; p->dropout_p = a->dropout_p; p->seed = a->seed; p->seed_dev = (const unsigned long long*)a->seed_dev;
   p->rab = a->rab; p->nb = a->num_buckets;
   p->precise = a->precise; p->out_f32 = a->out_dtype == GRK_F32;
+  p->in_dt = a->precise == 2 ? a->qkv_dtype : GRK_BF16;
   p->act = a->act;
   p->seq_range = a->seq_range;
   return GRK_OK;

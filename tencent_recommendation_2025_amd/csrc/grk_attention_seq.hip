@@ -122,10 +122,14 @@ __device__ __forceinline__ void act_frag(bf16x8* f, bool act) {
 
 // LDS carve-up shared by the three kernels: two row images of Tp x HD,
 // then per-row floats (rabx / lse / delta), key-valid bytes, scratch ints.
-template <int HD>
+// NIMG = 4 (fp32-fidelity mode): img0lo / img1lo hold the bf16 residuals
+// x - bf16(x) of the two staged operands.
+template <int HD, int NIMG = 2>
 struct SeqLds {
   char* img0;
   char* img1;
+  char* img0lo;
+  char* img1lo;
   float* f0;  // Tp + kRabPad floats
   float* f1;  // F1 x (Tp + kRabPad) floats (dQ: private drab bins per (wave, half-wave); dK/dV: delta)
   uint8_t* kvs;
@@ -133,15 +137,76 @@ struct SeqLds {
   __device__ SeqLds(char* smem, int Tp, int F1 = 1) {
     img0 = smem;
     img1 = smem + Tp * HD * 2;
-    f0 = reinterpret_cast<float*>(smem + 2 * Tp * HD * 2);
+    img0lo = smem + 2 * Tp * HD * 2;
+    img1lo = smem + 3 * Tp * HD * 2;
+    f0 = reinterpret_cast<float*>(smem + NIMG * Tp * HD * 2);
     f1 = f0 + Tp + kRabPad;
     kvs = reinterpret_cast<uint8_t*>(f1 + F1 * (Tp + kRabPad));
     sh = reinterpret_cast<int*>(kvs + Tp);
   }
   static size_t bytes(int Tp, int F1 = 1) {
-    return (size_t)2 * Tp * HD * 2 + (size_t)((1 + F1) * (Tp + kRabPad)) * 4 + Tp + 16 * 4;
+    return (size_t)NIMG * Tp * HD * 2 + (size_t)((1 + F1) * (Tp + kRabPad)) * 4 + Tp + 16 * 4;
   }
 };
+
+// Fidelity mode: fragments of row `row` split into bf16 hi + lo (SiLU applied in fp32 first when act).
+template <int HD>
+__device__ __forceinline__ void load_frag_split(bf16x8* fh, bf16x8* fl, const void* base, int64_t ld, int dt,
+                                                bool act, int b, int T, int h, int row, int hh) {
+  const bool ok = row < T;
+  const int64_t off = ((int64_t)b * T + (ok ? row : 0)) * ld + h * HD + 8 * hh;
+#pragma unroll
+  for (int ks = 0; ks < HD / 16; ++ks) {
+    float f[8];
+    gload8f(base, off + 16 * ks, dt, ok, f);
+    if (act)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = silu(f[j]);
+    split8(f, fh[ks], fl[ks]);
+  }
+}
+
+// Fidelity mode staging: rows [r0, Tp) of two head slices as hi and lo images.
+template <int HD>
+__device__ __forceinline__ void stage_pair_split(char* h0, char* l0, const void* src0, int64_t ld0, int dt0, bool act0,
+                                                 char* h1, char* l1, const void* src1, int64_t ld1, int dt1,
+                                                 bool act1, int b, int T, int h, int r0, int Tp) {
+  constexpr int NCH = HD / 8, BATCH = 4;
+  const int nvec = (Tp - r0) * NCH;
+  for (int base = threadIdx.x; base < nvec; base += BATCH * blockDim.x) {
+    float v0[BATCH][8], v1[BATCH][8];
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const int u = base + k * blockDim.x;
+      const int t = r0 + u / NCH, c = u % NCH;
+      const bool ok = u < nvec && t < T;
+      const int64_t row = (int64_t)b * T + (ok ? t : 0);
+      gload8f(src0, row * ld0 + h * HD + c * 8, dt0, ok, v0[k]);
+      gload8f(src1, row * ld1 + h * HD + c * 8, dt1, ok, v1[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const int u = base + k * blockDim.x;
+      if (u < nvec) {
+        const int row = r0 + u / NCH, c = u % NCH;
+        if (act0)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v0[k][j] = silu(v0[k][j]);
+        if (act1)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v1[k][j] = silu(v1[k][j]);
+        bf16x8 a, al, bb, bl;
+        split8(v0[k], a, al);
+        split8(v1[k], bb, bl);
+        const int o = lds_off<HD>(row, c * 8);
+        *reinterpret_cast<uint4*>(h0 + o) = __builtin_bit_cast(uint4, a);
+        *reinterpret_cast<uint4*>(l0 + o) = __builtin_bit_cast(uint4, al);
+        *reinterpret_cast<uint4*>(h1 + o) = __builtin_bit_cast(uint4, bb);
+        *reinterpret_cast<uint4*>(l1 + o) = __builtin_bit_cast(uint4, bl);
+      }
+    }
+  }
+}
 
 // Stage rows [r0, Tp) of two [B*T, ld] head slices into the images at the
 // same rows: every load of a batch is in flight before the first use (a
@@ -252,7 +317,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
   const int T = p.T, nq = (T + 31) / 32, Tp = nq * 32;
-  SeqLds<HD> L(smem, Tp);
+  SeqLds<HD, PREC == 2 ? 4 : 2> L(smem, Tp);
   GRK_STAMP(0);
   const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
@@ -262,10 +327,14 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
   GRK_STAMP(1);
   // prologue: every independent load in flight before the first wait
   bf16x8 qpre[KS];
-  if (wave < npairs) load_frag<HD>(qpre, p.q, p.ldq, b, T, h, (first + wave) * 32 + r, hh);
+  if (PREC < 2 && wave < npairs) load_frag<HD>(qpre, p.q, p.ldq, b, T, h, (first + wave) * 32 + r, hh);
   RabRegs rr;
   if (KIND == 1) rr = load_rab(p, h, Tp);
-  stage_pair<HD>(L.img0, p.k, p.ldk, false, p.act, L.img1, p.v, p.ldv, false, p.act, b, T, h, kbeg, Tp);
+  if constexpr (PREC == 2)
+    stage_pair_split<HD>(L.img0, L.img0lo, p.k, p.ldk, p.in_dt, p.act, L.img1, L.img1lo, p.v, p.ldv, p.in_dt, p.act,
+                         b, T, h, kbeg, Tp);
+  else
+    stage_pair<HD>(L.img0, p.k, p.ldk, false, p.act, L.img1, p.v, p.ldv, false, p.act, b, T, h, kbeg, Tp);
   if (KIND == 1) store_rab(L.f0, rr, Tp);
   if (!si.contig) stage_kvs(L.kvs, p.key_valid, b, T, Tp);
   GRK_STAMP(2);
@@ -294,14 +363,18 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
       if (!pair_has(pu, ps, ntiles)) break;
       const int q0 = (first + pair_tile(pu, ps, ntiles)) * 32, myq = q0 + r;
       const bool qok = myq < T;
-      bf16x8 qf[KS];
-      if (pu == wave && ps == 0) {
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) qf[ks] = qpre[ks];
+      bf16x8 qf[KS], ql[KS];
+      if constexpr (PREC == 2) {
+        load_frag_split<HD>(qf, ql, p.q, p.ldq, p.in_dt, p.act, b, T, h, myq, hh);
       } else {
-        load_frag<HD>(qf, p.q, p.ldq, b, T, h, myq, hh);
+        if (pu == wave && ps == 0) {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) qf[ks] = qpre[ks];
+        } else {
+          load_frag<HD>(qf, p.q, p.ldq, b, T, h, myq, hh);
+        }
+        act_frag<HD>(qf, p.act);
       }
-      act_frag<HD>(qf, p.act);
       f32x16 o[NDT];
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x16{};
@@ -309,7 +382,14 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
       for (int kb = kbeg; kb <= q0; kb += 32) {
         f32x16 s = acc_zero();
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) s = mfma(lds_row8<HD>(L.img0, kb + r, 16 * ks + 8 * hh), qf[ks], s);
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 ka = lds_row8<HD>(L.img0, kb + r, 16 * ks + 8 * hh);
+          s = mfma(ka, qf[ks], s);
+          if constexpr (PREC == 2) {
+            s = mfma(ka, ql[ks], s);
+            s = mfma(lds_row8<HD>(L.img0lo, kb + r, 16 * ks + 8 * hh), qf[ks], s);
+          }
+        }
         // strictly below the diagonal and past the padding: nothing to mask
         const bool fast = si.contig && kb < q0 && kb >= start;
         float pd[16];
@@ -366,6 +446,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
             const bf16x8 vf = lds_tr8<HD>(L.img1, kb + 16 * s2, dt * 32, lane);
             o[dt] = mfma(vf, ph, o[dt]);
             if (PREC) o[dt] = mfma(vf, pl, o[dt]);
+            if constexpr (PREC == 2) o[dt] = mfma(lds_tr8<HD>(L.img1lo, kb + 16 * s2, dt * 32, lane), ph, o[dt]);
           }
         }
       }
@@ -386,7 +467,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
   const int T = p.T, nq = (T + 31) / 32, Tp = nq * 32;
-  SeqLds<HD> L(smem, Tp, kDqBinArrays);
+  SeqLds<HD, PREC == 2 ? 4 : 2> L(smem, Tp, kDqBinArrays);
   // drab by distance d in [-kRabPad, Tp): bins[kRabPad + d], int64 fixed point
   unsigned long long* bins = reinterpret_cast<unsigned long long*>(L.f1);
   const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
@@ -396,14 +477,18 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
   const int ntiles = nq - first, npairs = (ntiles + 1) / 2;
   const int bh = b * p.H + h;
   bf16x8 qpre[KS], dpre[KS];
-  if (wave < npairs) {
+  if (PREC < 2 && wave < npairs) {
     const int row = (first + wave) * 32 + r;
     load_frag<HD>(qpre, p.q, p.ldq, b, T, h, row, hh);
     load_frag_any<HD>(dpre, p.dout, p.lddo, p.dout_f32, b, T, h, row, hh);
   }
   RabRegs rr;
   if (KIND == 1) rr = load_rab(p, h, Tp);
-  stage_pair<HD>(L.img0, p.k, p.ldk, false, p.act, L.img1, p.v, p.ldv, false, p.act, b, T, h, kbeg, Tp);
+  if constexpr (PREC == 2)
+    stage_pair_split<HD>(L.img0, L.img0lo, p.k, p.ldk, p.in_dt, p.act, L.img1, L.img1lo, p.v, p.ldv, p.in_dt, p.act,
+                         b, T, h, kbeg, Tp);
+  else
+    stage_pair<HD>(L.img0, p.k, p.ldk, false, p.act, L.img1, p.v, p.ldv, false, p.act, b, T, h, kbeg, Tp);
   if (KIND == 1) {
     store_rab(L.f0, rr, Tp);
     for (int j = threadIdx.x; j < Tp + kRabPad; j += blockDim.x) bins[j] = 0ull;
@@ -430,18 +515,23 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
       if (!pair_has(pu, ps, ntiles)) break;
       const int q0 = (first + pair_tile(pu, ps, ntiles)) * 32, myq = q0 + r;
       const bool qok = myq < T;
-      bf16x8 qf[KS], dof[KS];
-      if (pu == wave && ps == 0) {
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          qf[ks] = qpre[ks];
-          dof[ks] = dpre[ks];
-        }
+      bf16x8 qf[KS], dof[KS], ql[KS], dol[KS];
+      if constexpr (PREC == 2) {
+        load_frag_split<HD>(qf, ql, p.q, p.ldq, p.in_dt, p.act, b, T, h, myq, hh);
+        load_frag_split<HD>(dof, dol, p.dout, p.lddo, p.dout_f32 ? 0 : 1, false, b, T, h, myq, hh);
       } else {
-        load_frag<HD>(qf, p.q, p.ldq, b, T, h, myq, hh);
-        load_frag_any<HD>(dof, p.dout, p.lddo, p.dout_f32, b, T, h, myq, hh);
+        if (pu == wave && ps == 0) {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            qf[ks] = qpre[ks];
+            dof[ks] = dpre[ks];
+          }
+        } else {
+          load_frag<HD>(qf, p.q, p.ldq, b, T, h, myq, hh);
+          load_frag_any<HD>(dof, p.dout, p.lddo, p.dout_f32, b, T, h, myq, hh);
+        }
+        act_frag<HD>(qf, p.act);
       }
-      act_frag<HD>(qf, p.act);
       float lse2 = 0.f, dlt = 0.f;
       if (KIND == 0 && qok) {
         lse2 = p.lse[(int64_t)bh * T + myq] * kLog2e;
@@ -455,8 +545,16 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
         f32x16 s = acc_zero(), dp = acc_zero();
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          s = mfma(lds_row8<HD>(L.img0, kb + r, 16 * ks + 8 * hh), qf[ks], s);
-          dp = mfma(lds_row8<HD>(L.img1, kb + r, 16 * ks + 8 * hh), dof[ks], dp);
+          const bf16x8 ka = lds_row8<HD>(L.img0, kb + r, 16 * ks + 8 * hh);
+          const bf16x8 va = lds_row8<HD>(L.img1, kb + r, 16 * ks + 8 * hh);
+          s = mfma(ka, qf[ks], s);
+          dp = mfma(va, dof[ks], dp);
+          if constexpr (PREC == 2) {
+            s = mfma(ka, ql[ks], s);
+            s = mfma(lds_row8<HD>(L.img0lo, kb + r, 16 * ks + 8 * hh), qf[ks], s);
+            dp = mfma(va, dol[ks], dp);
+            dp = mfma(lds_row8<HD>(L.img1lo, kb + r, 16 * ks + 8 * hh), dof[ks], dp);
+          }
         }
         const bool fast = si.contig && kb < q0 && kb >= start;
         float ds[16];
@@ -510,11 +608,12 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
             const bf16x8 kf = lds_tr8<HD>(L.img0, kb + 16 * s2, dt * 32, lane);
             acc[dt] = mfma(kf, dh, acc[dt]);
             if (PREC) acc[dt] = mfma(kf, dl, acc[dt]);
+            if constexpr (PREC == 2) acc[dt] = mfma(lds_tr8<HD>(L.img0lo, kb + 16 * s2, dt * 32, lane), dh, acc[dt]);
           }
         }
       }
       store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, (int64_t)b * T + myq, h, hh, acc, p.scale, qok,
-                          p.act ? p.q : nullptr, p.ldq);
+                          p.act ? p.q : nullptr, p.ldq, p.in_dt);
     }
   if (KIND == 1 && p.drab) {
     __syncthreads();
@@ -531,7 +630,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
   const int T = p.T, nq = (T + 31) / 32, Tp = nq * 32;
-  SeqLds<HD> L(smem, Tp);
+  SeqLds<HD, PREC == 2 ? 4 : 2> L(smem, Tp);
   float* lses = L.f0;  // softmax: per-query log2-domain lse, delta
   float* dlts = L.f1;
   const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
@@ -542,7 +641,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
   const int bh = b * p.H + h;
   // key tile j (absolute first + j) visits query tiles j .. ntiles-1
   bf16x8 kpre[KS], vpre[KS];
-  if (wave < npairs) {
+  if (PREC < 2 && wave < npairs) {
     const int row = (first + wave) * 32 + r;
     load_frag<HD>(kpre, p.k, p.ldk, b, T, h, row, hh);
     load_frag<HD>(vpre, p.v, p.ldv, b, T, h, row, hh);
@@ -563,7 +662,11 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
       }
     }
   }
-  stage_pair<HD>(L.img0, p.q, p.ldq, false, p.act, L.img1, p.dout, p.lddo, p.dout_f32, false, b, T, h, kbeg, Tp);
+  if constexpr (PREC == 2)
+    stage_pair_split<HD>(L.img0, L.img0lo, p.q, p.ldq, p.in_dt, p.act, L.img1, L.img1lo, p.dout, p.lddo,
+                         p.dout_f32 ? 0 : 1, false, b, T, h, kbeg, Tp);
+  else
+    stage_pair<HD>(L.img0, p.q, p.ldq, false, p.act, L.img1, p.dout, p.lddo, p.dout_f32, false, b, T, h, kbeg, Tp);
   if (KIND == 1) {
     store_rab(L.f0, rr, Tp);
   } else {
@@ -600,19 +703,24 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
       const int k0 = (first + pair_tile(pu, ps, ntiles)) * 32, myk = k0 + r;
       const bool kin = myk < T;
       const bool kok = kin && myk >= start && (si.contig || L.kvs[myk]);
-      bf16x8 kf[KS], vf[KS];
-      if (pu == wave && ps == 0) {
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          kf[ks] = kpre[ks];
-          vf[ks] = vpre[ks];
-        }
+      bf16x8 kf[KS], vf[KS], kl[KS], vl[KS];
+      if constexpr (PREC == 2) {
+        load_frag_split<HD>(kf, kl, p.k, p.ldk, p.in_dt, p.act, b, T, h, myk, hh);
+        load_frag_split<HD>(vf, vl, p.v, p.ldv, p.in_dt, p.act, b, T, h, myk, hh);
       } else {
-        load_frag<HD>(kf, p.k, p.ldk, b, T, h, myk, hh);
-        load_frag<HD>(vf, p.v, p.ldv, b, T, h, myk, hh);
+        if (pu == wave && ps == 0) {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            kf[ks] = kpre[ks];
+            vf[ks] = vpre[ks];
+          }
+        } else {
+          load_frag<HD>(kf, p.k, p.ldk, b, T, h, myk, hh);
+          load_frag<HD>(vf, p.v, p.ldv, b, T, h, myk, hh);
+        }
+        act_frag<HD>(kf, p.act);
+        act_frag<HD>(vf, p.act);
       }
-      act_frag<HD>(kf, p.act);
-      act_frag<HD>(vf, p.act);
       f32x16 dk[NDT], dv[NDT];
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
@@ -623,8 +731,16 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
         f32x16 s = acc_zero(), dp = acc_zero();
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          s = mfma(lds_row8<HD>(L.img0, qb + r, 16 * ks + 8 * hh), kf[ks], s);
-          dp = mfma(lds_row8<HD>(L.img1, qb + r, 16 * ks + 8 * hh), vf[ks], dp);
+          const bf16x8 qa = lds_row8<HD>(L.img0, qb + r, 16 * ks + 8 * hh);
+          const bf16x8 da = lds_row8<HD>(L.img1, qb + r, 16 * ks + 8 * hh);
+          s = mfma(qa, kf[ks], s);
+          dp = mfma(da, vf[ks], dp);
+          if constexpr (PREC == 2) {
+            s = mfma(qa, kl[ks], s);
+            s = mfma(lds_row8<HD>(L.img0lo, qb + r, 16 * ks + 8 * hh), kf[ks], s);
+            dp = mfma(da, vl[ks], dp);
+            dp = mfma(lds_row8<HD>(L.img1lo, qb + r, 16 * ks + 8 * hh), vf[ks], dp);
+          }
         }
         // every query after every key of the tile, all queries < T, keys valid
         const bool fast = si.contig && qb > k0 && qb + 32 <= T && k0 >= start;
@@ -674,12 +790,18 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
               dv[dt] = mfma(dof, pl, dv[dt]);
               dk[dt] = mfma(qf, dl2, dk[dt]);
             }
+            if constexpr (PREC == 2) {
+              dv[dt] = mfma(lds_tr8<HD>(L.img1lo, qb + 16 * s2, dt * 32, lane), ph, dv[dt]);
+              dk[dt] = mfma(lds_tr8<HD>(L.img0lo, qb + 16 * s2, dt * 32, lane), dh, dk[dt]);
+            }
           }
         }
       }
       const int64_t otok = (int64_t)b * T + myk;
-      store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, otok, h, hh, dk, p.scale, kin, p.act ? p.k : nullptr, p.ldk);
-      store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, 1.f, kin, p.act ? p.v : nullptr, p.ldv);
+      store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, otok, h, hh, dk, p.scale, kin, p.act ? p.k : nullptr, p.ldk,
+                          p.in_dt);
+      store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, 1.f, kin, p.act ? p.v : nullptr, p.ldv,
+                          p.in_dt);
     }
 }
 
@@ -702,17 +824,22 @@ static void launch_lds(void (*kernel)(AttnParams), dim3 grid, int threads, size_
 template <int HD>
 static bool seq_launch_hd(const AttnParams& p, int which, hipStream_t s) {
   const int Tp = (p.T + 31) / 32 * 32;
-  const size_t lds = SeqLds<HD>::bytes(Tp, which == 2 ? kDqBinArrays : 1);
-  if (lds > (size_t)kSeqLdsMax || Tp + kRabPad > 2 * 64 * kSeqWaves) return false;
+  const int f1 = which == 2 ? kDqBinArrays : 1;
+  // fidelity mode: four images, one workgroup per CU (up to 160 KiB)
+  const size_t lds = p.precise == 2 ? SeqLds<HD, 4>::bytes(Tp, f1) : SeqLds<HD, 2>::bytes(Tp, f1);
+  const size_t cap = p.precise == 2 ? (size_t)160 * 1024 : (size_t)kSeqLdsMax;
+  if (lds > cap || Tp + kRabPad > 2 * 64 * kSeqWaves) return false;
   const dim3 grid(p.B * p.H);
   const int threads = 64 * kSeqWaves;
 #define GRK_SEQ(KERNEL)                                                                                  \
   do {                                                                                                   \
     if (p.kind == GRK_ATTN_SOFTMAX) {                                                                    \
-      if (p.precise) launch_lds(KERNEL<HD, 0, 1>, grid, threads, lds, s, p);                             \
+      if (p.precise == 2) launch_lds(KERNEL<HD, 0, 2>, grid, threads, lds, s, p);                        \
+      else if (p.precise) launch_lds(KERNEL<HD, 0, 1>, grid, threads, lds, s, p);                        \
       else launch_lds(KERNEL<HD, 0, 0>, grid, threads, lds, s, p);                                       \
     } else {                                                                                             \
-      if (p.precise) launch_lds(KERNEL<HD, 1, 1>, grid, threads, lds, s, p);                             \
+      if (p.precise == 2) launch_lds(KERNEL<HD, 1, 2>, grid, threads, lds, s, p);                        \
+      else if (p.precise) launch_lds(KERNEL<HD, 1, 1>, grid, threads, lds, s, p);                        \
       else launch_lds(KERNEL<HD, 1, 0>, grid, threads, lds, s, p);                                       \
     }                                                                                                    \
   } while (0)
@@ -721,6 +848,12 @@ static bool seq_launch_hd(const AttnParams& p, int which, hipStream_t s) {
   else GRK_SEQ(k_attn_dkdv_seq);
 #undef GRK_SEQ
   return true;
+}
+
+template <int HD>
+static bool fidelity_fits(int T) {
+  const int Tp = (T + 31) / 32 * 32;
+  return SeqLds<HD, 4>::bytes(Tp, kDqBinArrays) <= (size_t)160 * 1024 && Tp + kRabPad <= 2 * 64 * kSeqWaves;
 }
 
 bool attn_seq_launch(const AttnParams& p, int hd, int which, hipStream_t s) {
@@ -738,6 +871,17 @@ bool attn_seq_launch(const AttnParams& p, int hd, int which, hipStream_t s) {
 }  // namespace grk
 
 using namespace grk;
+
+extern "C" int grk_attention_fidelity_supported(int seq_len, int head_dim) {
+  if (seq_len <= 0 || getenv("GRK_ATTN_CHUNKED")) return 0;
+  switch (head_dim) {
+    case 16: return fidelity_fits<16>(seq_len);
+    case 32: return fidelity_fits<32>(seq_len);
+    case 64: return fidelity_fits<64>(seq_len);
+    case 128: return fidelity_fits<128>(seq_len);
+  }
+  return 0;
+}
 
 extern "C" int grk_seq_ranges(const uint8_t* key_valid, int batch, int seq_len, int32_t* ranges, void* stream) {
   clear_error();

@@ -280,37 +280,46 @@ def _seed(seed):
 
 
 class _SoftmaxMHAFn(torch.autograd.Function):
+    """fp32 / fp16 inputs (the reference's fp32 step and its fp16 autocast) run the
+    fp32-fidelity kernels when the shape allows (precise=2: Q/K/V/dO read exactly
+    and split into bf16 hi + lo, fp32 outputs cast back to the input dtype); bf16
+    inputs run the product kernels (``precise``)."""
+
     @staticmethod
     def forward(ctx, qkv, key_valid, B, T, H, hd, dropout_p, seed, precise, seq_range):
         D = H * hd
-        out_dt = qkv.dtype
-        xb = qkv if qkv.dtype == torch.bfloat16 else qkv.to(torch.bfloat16)
-        xb = xb.contiguous()
+        in_dt = qkv.dtype
+        fid = in_dt in (torch.float32, torch.float16) and K.fidelity_supported(T, hd)
+        if fid:
+            xb, prec, kdt = qkv.contiguous(), 2, torch.float32
+        else:
+            xb = (qkv if in_dt == torch.bfloat16 else qkv.to(torch.bfloat16)).contiguous()
+            prec, kdt = precise, (torch.float32 if in_dt == torch.float32 else torch.bfloat16)
         args = K.attn_args(L.ATTN_SOFTMAX, xb[:, :D], xb[:, D:2 * D], xb[:, 2 * D:3 * D], B, T, H, hd,
-                           key_valid=key_valid, dropout_p=dropout_p, seed=seed, precise=precise, out_dtype=out_dt,
+                           key_valid=key_valid, dropout_p=dropout_p, seed=seed, precise=prec, out_dtype=kdt,
                            seq_range=seq_range)
-        out = torch.empty(B * T, D, dtype=out_dt, device=qkv.device)
+        out = torch.empty(B * T, D, dtype=kdt, device=qkv.device)
         lse = torch.empty(B, H, T, dtype=torch.float32, device=qkv.device)
         K.attention_fwd(args, out, lse)
         ctx.save_for_backward(xb, out, lse, key_valid, seq_range)
-        ctx.meta = (B, T, H, hd, dropout_p, seed, precise, out_dt)
-        return out
+        ctx.meta = (B, T, H, hd, dropout_p, seed, prec, kdt, in_dt)
+        return out if kdt == in_dt else out.to(in_dt)
 
     @staticmethod
     def backward(ctx, gout):
         xb, out, lse, key_valid, seq_range = ctx.saved_tensors
-        B, T, H, hd, dropout_p, seed, precise, out_dt = ctx.meta
+        B, T, H, hd, dropout_p, seed, prec, kdt, in_dt = ctx.meta
         D = H * hd
         args = K.attn_args(L.ATTN_SOFTMAX, xb[:, :D], xb[:, D:2 * D], xb[:, 2 * D:3 * D], B, T, H, hd,
-                           key_valid=key_valid, dropout_p=dropout_p, seed=seed, precise=precise, out_dtype=out_dt,
+                           key_valid=key_valid, dropout_p=dropout_p, seed=seed, precise=prec, out_dtype=kdt,
                            seq_range=seq_range)
-        dqkv = torch.empty(B * T, 3 * D, dtype=out_dt, device=xb.device)
+        dqkv = torch.empty(B * T, 3 * D, dtype=kdt, device=xb.device)
         delta = torch.empty(B, H, T, dtype=torch.float32, device=xb.device)
         gout = gout.contiguous()
-        if gout.dtype not in (torch.float32, torch.bfloat16):
+        if gout.dtype not in (torch.float32, torch.bfloat16) or (prec == 2 and gout.dtype != torch.float32):
             gout = gout.float()
         K.attention_bwd(args, out, gout, lse, delta, dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:])
-        return dqkv, None, None, None, None, None, None, None, None, None
+        return (dqkv if kdt == in_dt else dqkv.to(in_dt)), None, None, None, None, None, None, None, None, None
 
 
 @_disable

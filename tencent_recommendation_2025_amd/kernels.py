@@ -200,9 +200,9 @@ def table_adamw(param, exp_avg, exp_avg_sq, hp, ids=None, rows=None, count=None,
 
 
 # ------------------------------------------------------------------ attention
-def _col_view_ok(t, name):
-    if t.dim() != 2 or t.stride(1) != 1 or t.dtype != torch.bfloat16:
-        raise L.GrkError(f'{name} must be a bf16 [B*T, >=H*hd] row-major view')
+def _col_view_ok(t, name, dtypes=(torch.bfloat16,)):
+    if t.dim() != 2 or t.stride(1) != 1 or t.dtype not in dtypes:
+        raise L.GrkError(f'{name} must be a {"/".join(str(d)[6:] for d in dtypes)} [B*T, >=H*hd] row-major view')
     if t.stride(0) % 8 or t.data_ptr() % 16:
         raise L.GrkError(f'{name}: row stride must be a multiple of 8 and the view 16-byte aligned')
 
@@ -281,9 +281,18 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
     backward's dq/dk/dv are gradients w.r.t. the pre-activations.
     seq_range: optional int32 [B, 2] from seq_ranges(key_valid) (computed once per step).
     seed: an int, or a device int64 [1] tensor the kernels read when they run
-    (drawn on the device each step, so a graph-replayed step gets a fresh mask)."""
+    (drawn on the device each step, so a graph-replayed step gets a fresh mask).
+    precise: 0 / False (P and dS rounded to bf16), 1 / True (P, dS as bf16 hi + lo),
+    2 (fp32 fidelity: Q/K/V and dO split into hi + lo as well; q/k/v may then be
+    fp32 / fp16 / bf16 and are read exactly -- fidelity_supported(T, hd))."""
+    precise = int(precise)
+    if precise not in (0, 1, 2):
+        raise L.GrkError('precise must be 0, 1 or 2')
+    dts = (torch.bfloat16, torch.float32, torch.float16) if precise == 2 else (torch.bfloat16,)
     for t, n in ((q, 'q'), (k, 'k'), (v, 'v')):
-        _col_view_ok(t, n)
+        _col_view_ok(t, n, dts)
+    if not q.dtype == k.dtype == v.dtype:
+        raise L.GrkError('q, k and v must share a dtype')
         if t.shape[0] != B * T or t.shape[1] < H * hd:
             raise L.GrkError(f'{n}: shape {tuple(t.shape)} does not fit B*T={B * T}, H*hd={H * hd}')
     if key_valid is not None:
@@ -302,10 +311,16 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
     seed, seed_dev = _seed_parts(seed)
     args = L.GrkAttnArgs(kind, B, H, T, hd, nb, q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0),
                          v.stride(0), _ptr(key_valid), _ptr(rab), float(scale), float(inv_n), float(dropout_p),
-                         int(bool(precise)), int(seed) & (2 ** 64 - 1), L.dtype_code(out_dtype),
-                         {None: L.ACT_NONE, 'silu': L.ACT_SILU}[act], _ptr(seq_range), _ptr(seed_dev))
+                         precise, seed, L.dtype_code(out_dtype),
+                         {None: L.ACT_NONE, 'silu': L.ACT_SILU}[act], _ptr(seq_range), _ptr(seed_dev),
+                         L.dtype_code(q.dtype))
     args._keep = (q, k, v, key_valid, rab, seq_range, seed_dev)  # the struct holds raw pointers: keep the tensors alive
     return args
+
+
+def fidelity_supported(seq_len, head_dim):
+    """Whether the fp32-fidelity attention (precise=2) runs for this shape (whole-sequence kernels' LDS)."""
+    return bool(L.lib().grk_attention_fidelity_supported(int(seq_len), int(head_dim)))
 
 
 def seq_ranges(key_valid):

@@ -306,3 +306,79 @@ def test_bwd_parts_equal_full_backward(K, kind, T):
         assert torch.equal(x1, x2)
     if ra is not None:
         assert torch.equal(ra, rb)
+
+
+def run_fidelity(K, kind, B, T, H, hd, lens, in_dtype, seed=0, act=None):
+    """precise=2: q/k/v given in fp32 / fp16 (not rounded to bf16), fp32 outputs."""
+    from tencent_recommendation_2025_amd import _lib as L
+    D = H * hd
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((B * T, 3 * D)).astype(np.float32)
+    if in_dtype == torch.float16:
+        x = x.astype(np.float16).astype(np.float32)
+    valid = np.zeros((B, T), np.uint8)
+    for b, n in enumerate(lens):
+        valid[b, T - n:] = 1
+    xd = torch.from_numpy(x).to(DEV).to(in_dtype)
+    kv = torch.from_numpy(valid).to(DEV)
+    extra, rab_np = {}, None
+    if kind == L.ATTN_HSTU:
+        rab_np = (np.random.default_rng(seed + 1).standard_normal((H, T)) * 0.5).astype(np.float32)
+        extra = dict(rab=torch.from_numpy(rab_np).to(DEV), inv_n=1.0 / T, scale=hd ** -0.5)
+    args = K.attn_args(kind, xd[:, :D], xd[:, D:2 * D], xd[:, 2 * D:], B, T, H, hd, key_valid=kv, precise=2,
+                       out_dtype=torch.float32, act=act, **extra)
+    out = torch.empty(B * T, D, device=DEV)
+    lse = torch.empty(B, H, T, device=DEV)
+    K.attention_fwd(args, out, lse)
+    dout_np = np.random.default_rng(seed + 2).standard_normal((B * T, D)).astype(np.float32)
+    dout = torch.from_numpy(dout_np).to(DEV)
+    dq, dk, dv = (torch.empty(B * T, D, device=DEV) for _ in range(3))
+    drab = torch.zeros(H, T, device=DEV) if kind == L.ATTN_HSTU else None
+    K.attention_bwd(args, out, dout, lse, torch.empty(B, H, T, device=DEV), dq, dk, dv, drab)
+    torch.cuda.synchronize()
+    xa = x.astype(np.float64)
+    if act == 'silu':
+        xa = xa / (1.0 + np.exp(-xa))
+    qh, kh, vh = (heads(xa[:, i * D:(i + 1) * D], B, T, H, hd) for i in range(3))
+    doh = heads(dout_np, B, T, H, hd)
+    if kind == L.ATTN_SOFTMAX:
+        o, _, _ = oatt.forward(qh, kh, vh, valid.astype(bool))
+        gq, gk, gv = oatt.backward(qh, kh, vh, valid.astype(bool), doh)
+        want = dict(out=flat(o), dq=flat(gq), dk=flat(gk), dv=flat(gv))
+    else:
+        o, _, _ = ohstu.forward(qh, kh, vh, valid.astype(bool), rab_np, hd ** -0.5, 1.0 / T)
+        gq, gk, gv, gr = ohstu.backward(qh, kh, vh, valid.astype(bool), rab_np, hd ** -0.5, 1.0 / T, doh)
+        want = dict(out=flat(o), dq=flat(gq), dk=flat(gk), dv=flat(gv), drab=gr)
+    if act == 'silu':
+        for i, key in enumerate(('dq', 'dk', 'dv')):
+            want[key] = want[key] * ohstu.dsilu(x[:, i * D:(i + 1) * D].astype(np.float64))
+    res = dict(out=out.cpu().numpy(), dq=dq.cpu().numpy(), dk=dk.cpu().numpy(), dv=dv.cpu().numpy())
+    if drab is not None:
+        res['drab'] = drab.cpu().numpy()
+    return res, want
+
+
+FIDELITY_TOL = 2e-5   # normwise vs the fp64 oracle on the unrounded inputs (measured: see DESIGN.md §4)
+
+
+@pytest.mark.parametrize('in_dtype', [torch.float32, torch.float16], ids=['f32', 'f16'])
+@pytest.mark.parametrize('hd,T,lens', [(16, 102, [102, 60, 7, 1]), (64, 102, [102, 60, 7, 33]),
+                                       (64, 201, [201, 120, 7]), (128, 102, [102, 50])])
+@pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
+def test_fidelity_mode_matches_fp64_oracle(K, kind, hd, T, lens, in_dtype):
+    """precise=2 (fp32 fidelity, the drop-in fp32 / fp16-autocast path): Q/K/V and
+    dO enter every MFMA as bf16 hi + lo (hi*hi + hi*lo + lo*hi), P / dS likewise,
+    so out / dq / dk / dv / drab match the fp64 oracle on the unrounded inputs to
+    fp32-level error (reference BaseLine/main.py:163-190 runs fp32)."""
+    H = 2 if hd >= 64 else 4
+    res, want = run_fidelity(K, kind, len(lens), T, H, hd, lens, in_dtype, seed=hd + T,
+                             act='silu' if kind == 1 else None)
+    for key in res:
+        err = nrel(res[key], want[key])
+        print(f'fidelity {key}: {err:.2e}')
+        assert err < FIDELITY_TOL, f'{key}: normwise rel err {err:.2e}'
+
+
+def test_fidelity_supported_shapes(K):
+    assert K.fidelity_supported(201, 64) and K.fidelity_supported(102, 128)
+    assert not K.fidelity_supported(201, 128) and not K.fidelity_supported(1025, 64)

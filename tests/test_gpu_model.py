@@ -2,8 +2,8 @@
 
 * The drop-in BaselineModel (fp32 tables, torch AdamW -- the reference's own
   training-script path) against the golden step of the imported reference
-  (BaseLine and BaseLineO1).  Attention runs on bf16 MFMA inside, so the
-  comparison is to ~1e-3-level relative error, not fp32 ulps.
+  (BaseLine and BaseLineO1).  Attention runs in the fp32-fidelity mode
+  (Q/K/V/dO/P/dS as bf16 hi + lo pairs on MFMA): fp32-level agreement.
 * The HSTU variant against the oracle's fp32 CPU restatement (parity unpinned
   vs the reference: it has no HSTU).
 * The fused trainer (table groups + grk_table_adamw) against the drop-in
@@ -68,6 +68,11 @@ def ref_loss(pl, nl, ntt, model, l2):
     return loss
 
 
+# measured on MI355X (round 2, fp32-fidelity attention): logits 2.4e-6 / 2.6e-6, loss 1.3e-7,
+# gradients <= 3.5e-5 (q/k projections: the score gradient's cancellation), all others ~1e-6
+DROPIN_TOL = dict(logits=1e-5, loss=1e-5, grad=1e-4)
+
+
 @pytest.mark.parametrize('tag', ['baseline', 'o1', 'baseline_live', 'o1_live'])
 def test_dropin_step_matches_reference(golden, tag):
     m, g, batch, args, _, _ = build(golden, tag)
@@ -76,10 +81,11 @@ def test_dropin_step_matches_reference(golden, tag):
     m.load_state_dict(sd)
     m.train()
     pl, nl = m(*batch)
-    assert nrel(pl.detach().cpu(), g['pos_logits']) < 5e-3
-    assert nrel(nl.detach().cpu(), g['neg_logits']) < 5e-3
+    lerr = max(nrel(pl.detach().cpu(), g['pos_logits']), nrel(nl.detach().cpu(), g['neg_logits']))
     loss = ref_loss(pl, nl, batch[4], m, float(g['l2_emb']))
-    assert abs(loss.item() - float(g['loss'])) < 2e-3 * abs(float(g['loss']))
+    print(f'{tag}: logits {lerr:.2e}, loss {abs(loss.item() - float(g["loss"])) / abs(float(g["loss"])):.2e}')
+    assert lerr < DROPIN_TOL['logits']
+    assert abs(loss.item() - float(g['loss'])) < DROPIN_TOL['loss'] * abs(float(g['loss']))
     opt = torch.optim.AdamW(m.parameters(), lr=float(g['lr']), betas=(0.9, 0.98),
                             weight_decay=float(g['weight_decay']))
     opt.zero_grad()
@@ -92,11 +98,12 @@ def test_dropin_step_matches_reference(golden, tag):
         # the key bias gets an analytically-zero gradient (softmax is shift-invariant): rounding noise only
         if np.linalg.norm(want) > 0 and not name.endswith('k_linear.bias'):
             worst[name] = nrel(got, want)
+    if worst:
+        print(f'{tag}: worst grads', sorted(worst.items(), key=lambda kv: -kv[1])[:4])
     if live:  # reference init zeroes LayerNorm gamma: only the live fixtures have meaningful grads
-        # fp32 drop-in: attention runs on bf16 MFMA (Q/K/V rounded to bf16, probabilities hi/lo):
-        # grads agree to a few 1e-2 normwise, not fp32 ulps ("fp32 fidelity")
-        bad = {k: v for k, v in worst.items() if v > 5e-2}
-        assert not bad, f'grad normwise errors above 5e-2: {bad}'
+        # fp32 drop-in: attention in fp32-fidelity mode (Q/K/V/dO/P/dS as bf16 hi+lo pairs)
+        bad = {k: v for k, v in worst.items() if v > DROPIN_TOL['grad']}
+        assert not bad, f'grad normwise errors above {DROPIN_TOL["grad"]}: {bad}'
         assert len(worst) > 40, 'live fixture: (almost) every gradient is non-zero'
     opt.step()
     lr = float(g['lr'])
