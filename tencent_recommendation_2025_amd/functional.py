@@ -13,6 +13,7 @@ import torch.nn.functional as F
 
 from . import _lib as L
 from . import kernels as K
+from . import ops  # noqa: F401  (registers the grk:: custom ops)
 
 _disable = torch._dynamo.disable  # ctypes calls: explicit graph breaks under torch.compile
 
@@ -108,7 +109,6 @@ class _FeatureLookupFn(torch.autograd.Function):
         return (None, None, None, None, None, None, None, *grads)
 
 
-@_disable
 def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extras=(), splits=None):
     """Fused multi-table gather (+ bag sums) into one [num_tokens, out_ld] buffer.
 
@@ -118,18 +118,44 @@ def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extras
     buffer, returned as a single tensor).  Drop-in tables get dense gradients
     through autograd; grouped tables push row-sparse gradient sources into
     their group's sink."""
-    weights, seen = [], set()
-    for s in specs:
-        if s.ref.group is None and id(s.ref.weight) not in seen and s.ref.weight.requires_grad:
-            seen.add(id(s.ref.weight))
-            weights.append(s.ref.weight)
     if token_type is not None:
         token_type = token_type.to(torch.int32).contiguous()
     single = splits is None
     splits = tuple((0, out_ld) if single else ((int(a), int(b)) for a, b in splits))
     extras = tuple((int(c), x) for c, x in extras)
-    outs = _FeatureLookupFn.apply(specs, token_type, seq_len, num_tokens, out_ld, extras, splits, *weights)
+    if all(s.ref.group is None for s in specs):
+        outs = _lookup_op(specs, token_type, seq_len, num_tokens, out_ld, extras, splits)
+    else:
+        outs = _lookup_groups(specs, token_type, seq_len, num_tokens, out_ld, extras, splits)
     return outs[0] if single else outs
+
+
+def _lookup_op(specs, token_type, seq_len, num_tokens, out_ld, extras, splits):
+    """Drop-in tables (plain weights, dense gradients): custom op grk::feature_lookup."""
+    tables, where, table_of = [], {}, []
+    for s in specs:
+        w = s.ref.weight
+        if id(w) not in where:
+            where[id(w)] = len(tables)
+            tables.append(w)
+        table_of.append(where[id(w)])
+    out = torch.ops.grk.feature_lookup(tables, [s.idx for s in specs], table_of, [int(s.out_col) for s in specs],
+                                       [int(s.mode) for s in specs], [int(s.bag) for s in specs], token_type,
+                                       int(seq_len), int(num_tokens), int(out_ld))
+    for col, x in extras:  # dense inputs (features, constants): no gradient is propagated to them
+        out[:, col:col + x.shape[1]] = x.detach().to(out.dtype)
+    return tuple(out[:, a:b] for a, b in splits)
+
+
+@_disable
+def _lookup_groups(specs, token_type, seq_len, num_tokens, out_ld, extras, splits):
+    """Table-group lookups (fused optimizer: row-sparse gradients into the groups' sinks)."""
+    weights, seen = [], set()
+    for s in specs:
+        if s.ref.group is None and id(s.ref.weight) not in seen and s.ref.weight.requires_grad:
+            seen.add(id(s.ref.weight))
+            weights.append(s.ref.weight)
+    return _FeatureLookupFn.apply(specs, token_type, seq_len, num_tokens, out_ld, extras, splits, *weights)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -279,109 +305,31 @@ def _seed(seed):
     return seed if isinstance(seed, torch.Tensor) else int(seed)
 
 
-class _SoftmaxMHAFn(torch.autograd.Function):
-    """fp32 / fp16 inputs (the reference's fp32 step and its fp16 autocast) run the
-    fp32-fidelity kernels when the shape allows (precise=2: Q/K/V/dO read exactly
-    and split into bf16 hi + lo, fp32 outputs cast back to the input dtype); bf16
-    inputs run the product kernels (``precise``)."""
-
-    @staticmethod
-    def forward(ctx, qkv, key_valid, B, T, H, hd, dropout_p, seed, precise, seq_range):
-        D = H * hd
-        in_dt = qkv.dtype
-        fid = in_dt in (torch.float32, torch.float16) and K.fidelity_supported(T, hd)
-        if fid:
-            xb, prec, kdt = qkv.contiguous(), 2, torch.float32
-        else:
-            xb = (qkv if in_dt == torch.bfloat16 else qkv.to(torch.bfloat16)).contiguous()
-            prec, kdt = precise, (torch.float32 if in_dt == torch.float32 else torch.bfloat16)
-        args = K.attn_args(L.ATTN_SOFTMAX, xb[:, :D], xb[:, D:2 * D], xb[:, 2 * D:3 * D], B, T, H, hd,
-                           key_valid=key_valid, dropout_p=dropout_p, seed=seed, precise=prec, out_dtype=kdt,
-                           seq_range=seq_range)
-        out = torch.empty(B * T, D, dtype=kdt, device=qkv.device)
-        lse = torch.empty(B, H, T, dtype=torch.float32, device=qkv.device)
-        K.attention_fwd(args, out, lse)
-        ctx.save_for_backward(xb, out, lse, key_valid, seq_range)
-        ctx.meta = (B, T, H, hd, dropout_p, seed, prec, kdt, in_dt)
-        return out if kdt == in_dt else out.to(in_dt)
-
-    @staticmethod
-    def backward(ctx, gout):
-        xb, out, lse, key_valid, seq_range = ctx.saved_tensors
-        B, T, H, hd, dropout_p, seed, prec, kdt, in_dt = ctx.meta
-        D = H * hd
-        args = K.attn_args(L.ATTN_SOFTMAX, xb[:, :D], xb[:, D:2 * D], xb[:, 2 * D:3 * D], B, T, H, hd,
-                           key_valid=key_valid, dropout_p=dropout_p, seed=seed, precise=prec, out_dtype=kdt,
-                           seq_range=seq_range)
-        dqkv = torch.empty(B * T, 3 * D, dtype=kdt, device=xb.device)
-        delta = torch.empty(B, H, T, dtype=torch.float32, device=xb.device)
-        gout = gout.contiguous()
-        if gout.dtype not in (torch.float32, torch.bfloat16) or (prec == 2 and gout.dtype != torch.float32):
-            gout = gout.float()
-        K.attention_bwd(args, out, gout, lse, delta, dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:])
-        return (dqkv if kdt == in_dt else dqkv.to(in_dt)), None, None, None, None, None, None, None, None, None
-
-
-@_disable
 def softmax_mha(qkv, key_valid, B, T, H, hd, dropout_p=0.0, seed=0, precise=True, seq_range=None):
-    """Causal + key-padding softmax attention on a packed [B*T, 3D] (q|k|v) tensor.
-    precise (default): probabilities / dS enter the P.V, dS.K, dS^T.Q MFMAs as
-    bf16 hi + lo pairs (fp32-accurate operands; 1-4 % slower than precise=False,
-    which rounds them to bf16 and is held only to 1e-2)."""
-    return _SoftmaxMHAFn.apply(qkv, key_valid, B, T, H, hd, float(dropout_p), _seed(seed), bool(precise), seq_range)
+    """Causal + key-padding softmax attention on a packed [B*T, 3D] (q|k|v) tensor
+    (custom op grk::softmax_attention; returns qkv's dtype).  fp32 / fp16 inputs
+    run the fp32-fidelity kernels where the shape allows (ops.py); bf16 inputs
+    the product kernels, precise (default: P and dS as bf16 hi + lo pairs, 1-4 %
+    slower than precise=False, which rounds them and is held only to 1e-2)."""
+    if key_valid is None:
+        key_valid = torch.ones(B, T, dtype=torch.uint8, device=qkv.device)
+    sd = seed if isinstance(seed, torch.Tensor) else None
+    out, _ = torch.ops.grk.softmax_attention(qkv, key_valid, H, hd, float(dropout_p), 0 if sd is not None else int(seed),
+                                             sd, int(precise), seq_range)
+    return out if out.dtype == qkv.dtype else out.to(qkv.dtype)
 
 
-class _HSTUCoreFn(torch.autograd.Function):
-    """y = dropout(LayerNorm(HSTU-attn(q, k, v)) * u), with u|v|q|k = SiLU(pre).
-
-    Three kernels forward, two backward, no eager elementwise glue:
-      attention (SiLU applied to q/k/v on load)        -> o
-      norm gate (LayerNorm(o) * SiLU(u), dropout)       -> y, (mean, rstd)
-    backward:
-      norm gate bwd -> do, dpre[:, :D] (x dSiLU), dgamma, dbeta
-      attention bwd -> dpre[:, D:] (dq/dk/dv x dSiLU written in place), drab
-    """
-
-    @staticmethod
-    def forward(ctx, pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps, precise, dropout_p, seed, seq_range):
-        D = H * hd
-        pb = pre.to(torch.bfloat16).contiguous()
-        rab32 = rab.float().contiguous()
-        args = K.attn_args(L.ATTN_HSTU, pb[:, 2 * D:3 * D], pb[:, 3 * D:], pb[:, D:2 * D], B, T, H, hd,
-                           key_valid=key_valid, scale=hd ** -0.5, rab=rab32, inv_n=inv_n, precise=precise,
-                           out_dtype=torch.bfloat16, act='silu', seq_range=seq_range)
-        o = torch.empty(B * T, D, dtype=torch.bfloat16, device=pre.device)
-        K.attention_fwd(args, o)
-        w32, b32 = ln_w.float().contiguous(), ln_b.float().contiguous()
-        y, stats = K.norm_gate_fwd(o, pb[:, :D], w32, b32, eps, dropout_p, seed)
-        ctx.save_for_backward(pb, o, stats, rab32, w32, b32, key_valid, seq_range)
-        ctx.meta = (B, T, H, hd, inv_n, precise, dropout_p, seed, pre.dtype, rab.dtype, ln_w.dtype, ln_b.dtype)
-        return y if pre.dtype == torch.bfloat16 else y.to(pre.dtype)
-
-    @staticmethod
-    def backward(ctx, gy):
-        pb, o, stats, rab32, w32, b32, key_valid, seq_range = ctx.saved_tensors
-        B, T, H, hd, inv_n, precise, dropout_p, seed, pdt, rdt, wdt, bdt = ctx.meta
-        D = H * hd
-        gy = gy.to(torch.bfloat16)
-        gy = gy if gy.is_contiguous() else gy.contiguous()
-        dpre = torch.empty(B * T, 4 * D, dtype=torch.bfloat16, device=pb.device)
-        do, _, dw, db = K.norm_gate_bwd(gy, o, pb[:, :D], w32, b32, stats, dropout_p, seed, du=dpre[:, :D])
-        drab = torch.zeros_like(rab32)
-        args = K.attn_args(L.ATTN_HSTU, pb[:, 2 * D:3 * D], pb[:, 3 * D:], pb[:, D:2 * D], B, T, H, hd,
-                           key_valid=key_valid, scale=hd ** -0.5, rab=rab32, inv_n=inv_n, precise=precise,
-                           out_dtype=torch.bfloat16, act='silu', seq_range=seq_range)
-        K.attention_bwd(args, None, do, None, None, dpre[:, 2 * D:3 * D], dpre[:, 3 * D:], dpre[:, D:2 * D], drab)
-        return (dpre if pdt == torch.bfloat16 else dpre.to(pdt), drab.to(rdt), dw.to(wdt), db.to(bdt),
-                None, None, None, None, None, None, None, None, None, None, None)
-
-
-@_disable
 def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, precise=True, dropout_p=0.0, seed=0,
               seq_range=None):
-    """Fused HSTU layer core on the [B*T, 4D] uvqk pre-activation (see _HSTUCoreFn)."""
-    return _HSTUCoreFn.apply(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, float(inv_n), float(eps), bool(precise),
-                             float(dropout_p), _seed(seed), seq_range)
+    """Fused HSTU layer core on the [B*T, 4D] (u|v|q|k) pre-activation (custom op
+    grk::hstu_core, ops.py): three kernels forward (attention with SiLU on load,
+    LayerNorm * SiLU(u) gate with dropout), two backward; no eager glue."""
+    if key_valid is None:
+        key_valid = torch.ones(B, T, dtype=torch.uint8, device=pre.device)
+    sd = seed if isinstance(seed, torch.Tensor) else None
+    y, _, _ = torch.ops.grk.hstu_core(pre, rab, ln_w, ln_b, key_valid, H, hd, float(inv_n), float(eps), int(precise),
+                                      float(dropout_p), 0 if sd is not None else int(seed), sd, seq_range)
+    return y if pre.dtype == torch.bfloat16 else y.to(pre.dtype)
 
 
 # ---------------------------------------------------------------- logits ----
@@ -395,31 +343,12 @@ def _shape_grads(ctx, *gs):
     return (*out, None)
 
 
-class _PairLogitsFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, h, ep, en, ntt):
-        dt = torch.promote_types(torch.promote_types(h.dtype, ep.dtype), en.dtype)
-        h2, p2, n2 = (_rows2d(x.to(dt)) for x in (h, ep, en))
-        pos, neg = K.pair_logits_fwd(h2, p2, n2, ntt)
-        ctx.save_for_backward(h2, p2, n2, ntt)
-        ctx.dtypes = (h.dtype, ep.dtype, en.dtype)
-        ctx.shapes = (h.shape, ep.shape, en.shape)
-        return pos, neg
-
-    @staticmethod
-    def backward(ctx, gpos, gneg):
-        h2, p2, n2, ntt = ctx.saved_tensors
-        need = ctx.needs_input_grad[:3]
-        dh, dp, dn = K.pair_logits_bwd(h2, p2, n2, gpos=gpos.contiguous(), gneg=gneg.contiguous(),
-                                       next_token_type=ntt, need=need)
-        return _shape_grads(ctx, dh, dp, dn)
-
-
-@_disable
 def pair_logits(h, e_pos, e_neg, next_token_type):
-    """(pos, neg) logits = rowwise <h, e> masked by next_token_type == 1 (fp32, shape of h[..., 0])."""
+    """(pos, neg) logits = rowwise <h, e> masked by next_token_type == 1 (fp32, shape of h[..., 0]);
+    custom op grk::pair_logits."""
     ntt = next_token_type.reshape(-1).to(torch.int32).contiguous()
-    pos, neg = _PairLogitsFn.apply(h, e_pos, e_neg, ntt)
+    D = h.shape[-1]
+    pos, neg = torch.ops.grk.pair_logits(h.reshape(-1, D), e_pos.reshape(-1, D), e_neg.reshape(-1, D), ntt)
     shape = h.shape[:-1]
     return pos.view(shape), neg.view(shape)
 

@@ -496,7 +496,7 @@ class BaselineModel(torch.nn.Module):
         seqs = seqs * self.item_emb.embedding_dim ** 0.5 + pos_rows.view(B, T, -1)
         seqs = self.emb_dropout(seqs)
         key_valid = (mask.to(dev, non_blocking=True) != 0).to(torch.uint8).contiguous()
-        kw = dict(key_valid=key_valid, seq_range=K.seq_ranges(key_valid))  # one launch serves every layer
+        kw = dict(key_valid=key_valid, seq_range=torch.ops.grk.seq_ranges(key_valid))  # one launch serves every layer
         if self.block == 'hstu' and _grk_gemm_ok(seqs) and self.hidden_units % 8 == 0:
             # bf16 residual stream: each residual add is fused into the next LayerNorm
             # (grk_add_norm), the last one into last_layernorm (fp32 output, as autocast's)

@@ -490,3 +490,47 @@ def test_captured_step_has_no_memset_nodes(block):
     assert census.get('kernel', 0) > 50
     assert all(b <= 4 for b in census['memset_bytes']), census['memset_bytes']
     assert np.all(np.isfinite(losses))
+
+
+@pytest.mark.parametrize('tag', ['baseline_live', 'o1_live'])
+def test_reference_flags_compile_amp_fp16_step(golden, tag):
+    """The reference's launch flags (BaseLine/run.sh:7 --use_amp --use_torch_compile;
+    main.py:114-116, 139, 173-190): torch.compile(model), the step under
+    torch.amp.autocast('cuda') (fp16) with a GradScaler.  The grk::* custom ops
+    (ops.py) trace into the compiled graph through their fake impls; fp16
+    attention runs the fp32-fidelity kernels.  Compiled == eager (to fp16
+    autocast noise), and both stay close to the fp32 reference fixture."""
+    lr = 1e-3
+    res = []
+    for compiled in (False, True):
+        torch._dynamo.reset()
+        m, g, batch, *_ = build(golden, tag)
+        m.load_state_dict({k[len('before.'):]: torch.from_numpy(g[k]) for k in g.files if k.startswith('before.')})
+        m.train()
+        model = torch.compile(m) if compiled else m
+        opt = torch.optim.AdamW(m.parameters(), lr=lr, betas=(0.9, 0.98))
+        scaler = torch.amp.GradScaler('cuda')
+        opt.zero_grad()
+        with torch.amp.autocast('cuda'):
+            pl, nl = model(*batch)
+            loss = ref_loss(pl, nl, batch[4], m, float(g['l2_emb']))
+        scaler.scale(loss).backward()
+        scaler.unscale_(opt)
+        grads = {n: p.grad.detach().float().clone() for n, p in m.named_parameters() if p.grad is not None}
+        scaler.step(opt)
+        scaler.update()
+        torch.cuda.synchronize()
+        res.append((pl.detach().float().cpu(), loss.item(), grads, {k: v.clone() for k, v in m.state_dict().items()}))
+    (pe, le, ge, se), (pc, lc, gc, sc) = res
+    print(f'{tag}: compiled vs eager logits {nrel(pc, pe):.2e} loss {abs(lc - le) / abs(le):.2e}; '
+          f'eager fp16 vs fp32 golden logits {nrel(pe, g["pos_logits"]):.2e}')
+    assert nrel(pc, pe) < 2e-3 and abs(lc - le) < 2e-3 * abs(le)
+    assert nrel(pe, g['pos_logits']) < 5e-3          # fp16 autocast vs the fp32 reference step
+    assert abs(le - float(g['loss'])) < 5e-3 * abs(float(g['loss']))
+    # k_linear.bias: analytically zero gradient (softmax is shift-invariant), rounding noise only
+    errs = {n: nrel(gc[n].cpu(), ge[n].cpu()) for n in ge if float(ge[n].norm()) > 0 and not n.endswith('k_linear.bias')}
+    print(f'{tag}: worst compiled-vs-eager grads', sorted(errs.items(), key=lambda kv: -kv[1])[:4])
+    assert max(errs.values()) < 5e-2, sorted(errs.items(), key=lambda kv: -kv[1])[:4]
+    assert set(gc) == set(ge)
+    for k in se:
+        assert float((sc[k].float() - se[k].float()).abs().max()) <= 2.05 * lr, k
