@@ -252,6 +252,37 @@ def item_gather_roofline(table, batch, reps):
     return res
 
 
+def backward_roofline(trace, reps):
+    """The largest embedding-table gradient of one step (grk_embedding_backward:
+    key build, stable radix sort, segment bounds, in-order segmented
+    reduction incl. the hot-row kernel), the whole call timed alone with HIP
+    events, the step's own arguments.  Algorithmic bytes per SURVEY.md 8(d)
+    and VERDICT r1: every occurrence's gradient row read once (D x e) + its
+    index, every unique row's fp32 sum written once (D x 4 + 8 B id)."""
+    from tencent_recommendation_2025_amd import kernels as K
+    call = max(trace, key=lambda c: sum(s.idx.numel() for s in c['sources']))
+
+    def run():
+        kw = dict(call)
+        rs = kw.pop('row_slot')
+        return K.embedding_backward(row_slot=None if rs is None else rs.clone(), **kw)
+
+    res = run()
+    occ = sum(s.idx.numel() for s in call['sources'])
+    es = call['sources'][0].grad.element_size()
+    isz = call['sources'][0].idx.element_size()
+    uniq = int(res.count.item())
+    D = call['dim']
+    ms = _time(run, reps)
+    alg = occ * (D * es + isz) + uniq * (D * 4 + 8)
+    gbps = alg / (ms * 1e-3) / 1e9
+    return {'bound': 'hbm', 'kernel': 'grk_embedding_backward (largest table-group gradient of the step, all launches)',
+            'achieved': round(gbps, 1), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': round(gbps / HBM_PEAK_GBPS, 4),
+            'traffic': None, 'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2),
+            'workload': {'occurrences': int(occ), 'unique_rows': uniq, 'table_rows': int(call['num_rows']), 'D': D,
+                         'grad_dtype': str(call['sources'][0].grad.dtype), 'lookups': len(call['sources'])}}
+
+
 def wgrad_roofline(a, reps):
     """grk_wgrad on the largest weight gradient of the step: the HSTU uvqk
     projection (dW [4D, D] = dY^T X over K = B*T tokens, + bias gradient),
@@ -368,13 +399,16 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [S.make_batch(cfg, gen, dev) for _ in range(max(2, a.pool))]
 
-    trace = None
+    from tencent_recommendation_2025_amd import kernels as K
+    trace = btrace = None
     for i in range(a.warmup):
         if i == 0:
             G.GATHER_TRACE = []          # record the fused-gather launches of one real (eager) step
+            K.BACKWARD_TRACE = []        # ... and its embedding-table gradients
         trainer.step(pool[i % len(pool)], next_batch=pool[(i + 1) % len(pool)])
         if i == 0:
             trace, G.GATHER_TRACE = G.GATHER_TRACE, None
+            btrace, K.BACKWARD_TRACE = K.BACKWARD_TRACE, None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -392,9 +426,10 @@ def main():
     final_loss = float(loss.float().item())
 
     if not trace:  # --warmup 0: trace one extra, untimed eager step after the timed region
-        G.GATHER_TRACE = []
+        G.GATHER_TRACE, K.BACKWARD_TRACE = [], []
         trainer.eager_step(pool[0])
         trace, G.GATHER_TRACE = G.GATHER_TRACE, None
+        btrace, K.BACKWARD_TRACE = K.BACKWARD_TRACE, None
     kv = (pool[0][3] != 0).to(torch.uint8)        # the first bench batch's key validity (token_type != 0)
     roof, more = attention_rooflines(a, kv, a.roofline_reps)
     more.append(gather_roofline(trace, a.roofline_reps))
@@ -402,6 +437,8 @@ def main():
     if item_table is not None:
         more.append(item_gather_roofline(item_table.detach(), pool[0], a.roofline_reps))
     more.append(wgrad_roofline(a, a.roofline_reps))
+    if btrace:
+        more.append(backward_roofline(btrace, a.roofline_reps))
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline:

@@ -165,16 +165,14 @@ __global__ void k_segments(const unsigned* __restrict__ keys, const int* __restr
 // ------------------------------------------------- segmented reduction ----
 // The sorted occurrence list is cut into fixed chunks of kRedChunk entries,
 // one row group (dim/VEC lanes, VEC = one 16-byte vector of grads) per chunk,
-// so hot rows (a cardinality-10 feature table gets thousands of occurrences
-// per row) are spread over many row groups instead of serialising one.
-//   * a row whose occurrences all fall in one chunk is summed strictly in
-//     occurrence order and written directly (bit-exact with the CPU order);
-//   * a row crossing a chunk boundary with <= 2*kRedChunk occurrences is
-//     re-summed sequentially by k_seg_combine (still bit-exact);
-//   * longer rows are summed per chunk into partial slots (A: the chunk's
-//     first piece, B: its last piece when that continues past the chunk) and
-//     k_seg_combine adds the partials in chunk order -- deterministic, a
-//     fixed blocked summation order.
+// so the work per row group is bounded whatever the row lengths.  Every row is
+// summed strictly in occurrence order (bit-exact with the reference's CPU
+// embedding_dense_backward):
+//   * a row whose occurrences all fall in one chunk is summed by that chunk
+//     and written directly;
+//   * a row crossing a chunk edge with <= 2*kRedChunk occurrences is re-summed
+//     sequentially by k_seg_combine / k_seg_combine_edges;
+//   * a longer ("hot") row is summed by k_seg_hot, one wave per 64 columns.
 constexpr int kRedChunk = 256;
 constexpr int kRedPipe = 8;  // occurrence rows loaded ahead of the in-order adds
 
@@ -206,14 +204,6 @@ __device__ __forceinline__ void store_final(const A& acc, unsigned key, int64_t 
   if (row_slot && c == 0) row_slot[key] = (int32_t)u;
 }
 
-template <typename A>
-__device__ __forceinline__ void store_slot(const A& acc, float* slot, int dim, int c) {
-  constexpr int VEC = A::VEC;
-#pragma unroll
-  for (int e = 0; e < VEC; e += 4)
-    *reinterpret_cast<float4*>(slot + c + e) = make_float4(acc.v[e], acc.v[e + 1], acc.v[e + 2], acc.v[e + 3]);
-}
-
 // Sequential in-order sum of the sorted occurrences [s, e) with kRedPipe rows in flight.
 template <typename G>
 __device__ __forceinline__ void seq_sum(RowVec<G>& acc, const unsigned long long* __restrict__ gptr, int s, int e,
@@ -237,9 +227,8 @@ __global__ void __launch_bounds__(256) k_seg_chunks(const unsigned* __restrict__
                                                     const unsigned long long* __restrict__ gptr,
                                                     const int* __restrict__ pos, const int* __restrict__ seg_start,
                                                     const int* __restrict__ seg_end, int64_t n, unsigned sentinel,
-                                                    int dim, float* __restrict__ slotA, float* __restrict__ slotB,
-                                                    float* __restrict__ dense_out, float* __restrict__ uniq_rows,
-                                                    int32_t* __restrict__ row_slot) {
+                                                    int dim, float* __restrict__ dense_out,
+                                                    float* __restrict__ uniq_rows, int32_t* __restrict__ row_slot) {
   constexpr int VEC = RowVec<G>::VEC;
   const int tpr = dim / VEC;
   const int groups = blockDim.x / tpr;
@@ -256,11 +245,8 @@ __global__ void __launch_bounds__(256) k_seg_chunks(const unsigned* __restrict__
   auto flush = [&](int64_t pe) {   // piece [ps, pe) of key cur
     const int u = pos[ps] - 1;
     const int su = seg_start[u], eu = seg_end[u];
-    if (su >= p0 && eu <= p1) {
-      store_final(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
-    } else if (eu - su > 2 * kRedChunk) {
-      store_slot(acc, (ps == p0 ? slotA : slotB) + chunk * dim, dim, c);
-    }  // else: short row crossing a boundary -- k_seg_combine sums it sequentially
+    if (su >= p0 && eu <= p1) store_final(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
+    // else: a row crossing an edge -- k_seg_combine (<= 2*kRedChunk) or k_seg_hot sums it
   };
   for (int64_t p = p0; p < p1; p += kRedPipe) {
     Vec16<G> r[kRedPipe];
@@ -296,7 +282,6 @@ __global__ void __launch_bounds__(256) k_seg_combine(const unsigned long long* _
                                                      const int* __restrict__ seg_end,
                                                      const unsigned* __restrict__ seg_key,
                                                      const int32_t* __restrict__ count, int64_t max_rows, int dim,
-                                                     const float* __restrict__ slotA, const float* __restrict__ slotB,
                                                      float* __restrict__ dense_out, float* __restrict__ uniq_rows,
                                                      int32_t* __restrict__ row_slot) {
   constexpr int VEC = RowVec<G>::VEC;
@@ -306,34 +291,11 @@ __global__ void __launch_bounds__(256) k_seg_combine(const unsigned long long* _
   const int c = (threadIdx.x % tpr) * VEC;
   if ((int)(threadIdx.x / tpr) >= groups || u >= max_rows || u >= *count) return;
   const int su = seg_start[u], eu = seg_end[u];
-  const int cs = su / kRedChunk, ce = (eu - 1) / kRedChunk;
-  if (cs == ce) return;  // written by k_seg_chunks
+  if (su / kRedChunk == (eu - 1) / kRedChunk) return;  // written by k_seg_chunks
+  if (eu - su > 2 * kRedChunk) return;                  // hot row: k_seg_hot
   RowVec<G> acc;
   acc.zero();
-  if (eu - su <= 2 * kRedChunk) {
-    seq_sum<G>(acc, gptr, su, eu, c);
-  } else {
-    const float* first = ((su % kRedChunk) == 0 ? slotA : slotB) + (int64_t)cs * dim + c;
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) acc.v[e] = first[e];
-    for (int ch = cs + 1; ch <= ce; ch += kRedPipe) {
-      float4 r[kRedPipe][VEC / 4];
-#pragma unroll
-      for (int j = 0; j < kRedPipe; ++j)
-        if (ch + j <= ce)
-#pragma unroll
-          for (int e = 0; e < VEC / 4; ++e)
-            r[j][e] = *reinterpret_cast<const float4*>(slotA + (int64_t)(ch + j) * dim + c + 4 * e);
-#pragma unroll
-      for (int j = 0; j < kRedPipe; ++j)
-        if (ch + j <= ce)
-#pragma unroll
-          for (int e = 0; e < VEC / 4; ++e) {
-            acc.v[4 * e] += r[j][e].x; acc.v[4 * e + 1] += r[j][e].y;
-            acc.v[4 * e + 2] += r[j][e].z; acc.v[4 * e + 3] += r[j][e].w;
-          }
-    }
-  }
+  seq_sum<G>(acc, gptr, su, eu, c);
   store_final(acc, seg_key[u], u, dim, c, dense_out, uniq_rows, row_slot);
 }
 
@@ -395,8 +357,8 @@ __global__ void __launch_bounds__(256) k_seg_chunks_wave(const unsigned* __restr
                                                          const unsigned long long* __restrict__ gptr,
                                                          const int* __restrict__ pos, const int* __restrict__ seg_start,
                                                          const int* __restrict__ seg_end, int64_t n, unsigned sentinel,
-                                                         int dim, float* __restrict__ slotA, float* __restrict__ slotB,
-                                                         float* __restrict__ dense_out, float* __restrict__ uniq_rows,
+                                                         int dim, float* __restrict__ dense_out,
+                                                         float* __restrict__ uniq_rows,
                                                          int32_t* __restrict__ row_slot) {
   constexpr int VEC = LW;
   constexpr int KP = kRedChunk / 64;  // chunk entries per lane
@@ -428,11 +390,8 @@ __global__ void __launch_bounds__(256) k_seg_chunks_wave(const unsigned* __restr
   int u = __builtin_amdgcn_readfirstlane(pr[0]) - 1;
   auto flush = [&]() {
     const bool whole = (ps > p0 || kprev != cur) && (pe < p1 || knext != cur);
-    if (whole) {
-      store_final(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
-    } else if (seg_end[u] - seg_start[u] > 2 * kRedChunk) {
-      store_slot(acc, (ps == p0 ? slotA : slotB) + chunk * dim, dim, c);
-    }  // else: short row crossing an edge -- k_seg_combine_edges sums it sequentially
+    if (whole) store_final(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
+    // else: a row crossing an edge -- k_seg_combine_edges (<= 2*kRedChunk) or k_seg_hot sums it
   };
   bool done = false;
 #pragma unroll
@@ -492,18 +451,17 @@ __device__ __forceinline__ void seq_sum_wave(WaveAcc<LW>& acc, const unsigned lo
 }
 
 // One wave per chunk edge b (occurrence b * kRedChunk): finishes the row that
-// first crosses a chunk edge at b, i.e. crosses b and starts in chunk b - 1.
+// first crosses a chunk edge at b, i.e. crosses b and starts in chunk b - 1,
+// when it has at most 2 * kRedChunk occurrences (longer rows: k_seg_hot).
 template <typename G, int LW>
 __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __restrict__ keys,
                                                            const unsigned long long* __restrict__ gptr,
                                                            const int* __restrict__ pos,
                                                            const int* __restrict__ seg_start,
                                                            const int* __restrict__ seg_end, int64_t n,
-                                                           unsigned sentinel, int dim, const float* __restrict__ slotA,
-                                                           const float* __restrict__ slotB,
-                                                           float* __restrict__ dense_out, float* __restrict__ uniq_rows,
+                                                           unsigned sentinel, int dim, float* __restrict__ dense_out,
+                                                           float* __restrict__ uniq_rows,
                                                            int32_t* __restrict__ row_slot) {
-  constexpr int VEC = LW;
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) + 1;
   const int64_t pb = b * kRedChunk;
@@ -513,35 +471,165 @@ __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __res
   const int u = pos[pb] - 1;
   const int su = seg_start[u], eu = seg_end[u];
   if (su / kRedChunk != b - 1) return;  // also crosses an earlier edge: finished there
-  const int c = lane * VEC;
-  const int cs = (int)(b - 1), ce = (eu - 1) / kRedChunk;
+  if (eu - su > 2 * kRedChunk) return;  // hot row: k_seg_hot
+  const int c = lane * LW;
   WaveAcc<LW> acc;
   acc.zero();
-  if (eu - su <= 2 * kRedChunk) {
-    seq_sum_wave<G, LW>(acc, gptr, su, eu, lane, c);
-  } else {
-    const float* first = ((su % kRedChunk) == 0 ? slotA : slotB) + (int64_t)cs * dim + c;
+  seq_sum_wave<G, LW>(acc, gptr, su, eu, lane, c);
+  store_final(acc, key, u, dim, c, dense_out, uniq_rows, row_slot);
+}
+
+// ------------------------------------------------------------- hot rows ----
+// Rows with more than 2 * kRedChunk occurrences (the rows of cardinality-10
+// feature tables take thousands per call), summed bit-exactly in occurrence
+// order like every other row: the reference's CPU embedding_dense_backward is
+// a sequential fp32 add per row in occurrence order, so the
+// only parallelism inside one row is across its columns.  One wave per
+// (row, 64-column slice); each lane owns one column and keeps its running sum
+// in a register.
+//   * loads: 16-byte vectors, 8 (bf16) / 4 (fp32) occurrences per wave
+//     instruction, 8 instructions per tile of 64 / 32 occurrences; kHotStages
+//     tiles in flight.  A tile's row addresses are loaded right after the data
+//     loads of the tile kHotStages earlier, in the same order in the prologue
+//     as in the loop, so every wait on them is a partial vmcnt;
+//   * bf16: the tile is written to LDS as loaded ([occurrence][64 columns],
+//     16-byte writes, rows padded to 192 B) and read back with the gfx950
+//     transposing read ds_read_b64_tr_b16, which hands each lane its column
+//     for 4 consecutive occurrences (192-B rows: the four rows a 16-lane group
+//     reads fall on disjoint banks, conflict-free);
+//     fp32: written transposed ([column][occurrence], rows padded to 136 B)
+//     and read 8 bytes at a time.
+constexpr int kHotStages = 4;
+
+template <typename G>
+__global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ keys,
+                                                const unsigned long long* __restrict__ gptr,
+                                                const int* __restrict__ pos, const int* __restrict__ seg_start,
+                                                const int* __restrict__ seg_end, int64_t n, unsigned sentinel, int dim,
+                                                float* __restrict__ dense_out, float* __restrict__ uniq_rows,
+                                                int32_t* __restrict__ row_slot) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+  constexpr int ES = sizeof(G);
+  constexpr int EPV = 16 / ES;       // elements per 16-byte vector
+  constexpr int LPO = 64 / EPV;      // lanes per occurrence slice (8 bf16, 16 fp32)
+  constexpr int OPI = 64 / LPO;      // occurrences per load instruction (8, 4)
+  constexpr int IPT = 8;             // load instructions per tile
+  constexpr int TILE = OPI * IPT;    // occurrences per tile (64, 32): 128 B of one column
+  constexpr int ROWB = ES == 2 ? 192 : TILE * ES + 8;  // bf16: [occ][cols] rows; fp32: [col][occs] rows
+  constexpr int EPR = 8 / ES;        // elements per 8-byte LDS read
+  constexpr int S = kHotStages;
+  __shared__ __attribute__((aligned(16))) unsigned char img[64 * ROWB];
+  const int lane = threadIdx.x;
+  const int64_t b = (int64_t)blockIdx.x + 1;  // chunk edge: the row that first crosses it
+  const int64_t pb = b * kRedChunk;
+  if (pb >= n) return;
+  const unsigned key = keys[pb];
+  if (key == sentinel || keys[pb - 1] != key) return;
+  const int u = pos[pb] - 1;
+  const int su = seg_start[u], eu = seg_end[u];
+  if (su / kRedChunk != b - 1 || eu - su <= 2 * kRedChunk) return;
+  const int c0 = blockIdx.y * 64;
+  const int cols = min(64, dim - c0);
+  const int wv = (lane % LPO) * EPV;                     // this lane's columns [wv, wv + EPV) of the slice
+  const int vcol = c0 + wv < dim ? c0 + wv : c0;         // clamped into the row past dim
+  const int wocc = lane / LPO;
+  const int ntiles = (eu - su + TILE - 1) / TILE;
+  auto addr = [&](int t) -> unsigned long long {  // lane j < TILE: address of occurrence j of tile t
+    const int i = su + t * TILE + (lane < TILE ? lane : 0);
+    return gptr[i < eu ? i : eu - 1];
+  };
+  auto issue = [&](u32x4 (&d)[IPT], unsigned long long a) {
+    const unsigned lo = (unsigned)a, hi = (unsigned)(a >> 32);
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) acc.v[e] = first[e];
-    for (int ch = cs + 1; ch <= ce; ch += kRedPipe) {
-      float4 r[kRedPipe][VEC / 4];
+    for (int i = 0; i < IPT; ++i) {
+      const int src = i * OPI + wocc;
+      const unsigned long long p = ((unsigned long long)(unsigned)__shfl(hi, src) << 32) | (unsigned)__shfl(lo, src);
+      d[i] = *reinterpret_cast<gu32x4*>(p + (unsigned long long)vcol * ES);
+    }
+  };
+  u32x4 data[S][IPT];
+  unsigned long long next[S];
+  {  // every address of the first 2S tiles lands before any data load: in the loop a
+     // tile's addresses then always come after the data loads they must not drain
+    unsigned long long first[S];
 #pragma unroll
-      for (int j = 0; j < kRedPipe; ++j)
-        if (ch + j <= ce)
+    for (int k = 0; k < S; ++k) {
+      first[k] = addr(k);
+      next[k] = addr(S + k);
+    }
 #pragma unroll
-          for (int e = 0; e < VEC / 4; ++e)
-            r[j][e] = *reinterpret_cast<const float4*>(slotA + (int64_t)(ch + j) * dim + c + 4 * e);
+    for (int k = 0; k < S; ++k) asm volatile("" ::"v"(first[k]), "v"(next[k]));
 #pragma unroll
-      for (int j = 0; j < kRedPipe; ++j)
-        if (ch + j <= ce)
-#pragma unroll
-          for (int e = 0; e < VEC / 4; ++e) {
-            acc.v[4 * e] += r[j][e].x; acc.v[4 * e + 1] += r[j][e].y;
-            acc.v[4 * e + 2] += r[j][e].z; acc.v[4 * e + 3] += r[j][e].w;
-          }
+    for (int k = 0; k < S; ++k) {
+      issue(data[k], first[k]);
+      __builtin_amdgcn_sched_barrier(0);  // stage order as in the loop (the waits depend on it)
     }
   }
-  store_final(acc, key, u, dim, c, dense_out, uniq_rows, row_slot);
+  float acc = 0.f;
+  unsigned char* wbase = ES == 2 ? img + wocc * ROWB + (lane % LPO) * 16 : img + wv * ROWB + wocc * ES;
+  const unsigned char* rbase = ES == 2 ? img + ((lane & 15) >> 2) * ROWB + ((lane >> 4) * 16 + (lane & 3) * 4) * 2
+                                       : img + lane * ROWB;
+  for (int t0 = 0; t0 < ntiles; t0 += S) {
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const int t = t0 + k;
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) {
+        const u32x4 v = data[k][i];
+        if constexpr (ES == 2) {
+          *reinterpret_cast<u32x4*>(wbase + i * OPI * ROWB) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < EPV; ++e) *reinterpret_cast<unsigned*>(wbase + e * ROWB + i * OPI * ES) = v[e];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      issue(data[k], next[k]);          // tile t + S (clamped addresses past the row's end)
+      next[k] = addr(t + 2 * S);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_wave_barrier();
+      const int m = t < ntiles ? min(TILE, eu - su - t * TILE) : 0;
+      if constexpr (ES == 2) {
+        // every lane joins each transposing read (EXEC must be full); adds stop at m
+        typedef short s16x4 __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+        s16x4 w[TILE / 4];
+#pragma unroll
+        for (int q = 0; q < TILE / 4; ++q)
+          w[q] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(rbase + 4 * q * ROWB));
+        if (m == TILE) {
+#pragma unroll
+          for (int q = 0; q < TILE / 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc += __uint_as_float((unsigned)(unsigned short)w[q][e] << 16);
+        } else {
+#pragma unroll
+          for (int q = 0; q < TILE / 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (4 * q + e < m) acc += __uint_as_float((unsigned)(unsigned short)w[q][e] << 16);
+        }
+      } else if (m == TILE) {  // whole tile: all LDS reads in flight ahead of the in-order adds
+        uint2 w[TILE / EPR];
+#pragma unroll
+        for (int q = 0; q < TILE / EPR; ++q) w[q] = *reinterpret_cast<const uint2*>(rbase + q * 8);
+#pragma unroll
+        for (int q = 0; q < TILE / EPR; ++q) {
+          acc += __uint_as_float(w[q].x);
+          acc += __uint_as_float(w[q].y);
+        }
+      } else {
+        for (int j = 0; j < m; ++j) acc += Elem<G>::load(reinterpret_cast<const G*>(rbase) + j);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (lane < cols) {
+    if (dense_out) dense_out[(int64_t)key * dim + c0 + lane] = acc;
+    if (uniq_rows) uniq_rows[(int64_t)u * dim + c0 + lane] = acc;
+  }
+  if (row_slot && blockIdx.y == 0 && lane == 0) row_slot[key] = (int32_t)u;
 }
 
 // ------------------------------------------------------------ workspace ----
@@ -549,7 +637,6 @@ struct BwdWs {
   unsigned *keys_in, *keys_out, *seg_key;
   int *flags, *pos, *seg_start, *seg_end;
   unsigned long long *gptr_in, *gptr_out;
-  float *slotA, *slotB;
   void* sort_tmp;
   size_t sort_bytes;
   void* scan_tmp;
@@ -575,9 +662,6 @@ static int plan_ws(int64_t n, int64_t num_rows, int dim, char* base, BwdWs* ws) 
   ws->seg_end = (int*)take(n * 4);
   ws->gptr_in = (unsigned long long*)take(n * 8);
   ws->gptr_out = (unsigned long long*)take(n * 8);
-  const int64_t chunks = (n + kRedChunk - 1) / kRedChunk;
-  ws->slotA = (float*)take((size_t)chunks * dim * 4);
-  ws->slotB = (float*)take((size_t)chunks * dim * 4);
   unsigned end_bit = 1;
   while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
   size_t sb = 0, cb = 0;
@@ -748,33 +832,43 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
     const unsigned ge = (unsigned)(chunks > 1 ? (chunks - 1 + 3) / 4 : 0);
 #define GRK_SEGW(G, LW)                                                                                              \
   k_seg_chunks_wave<G, LW><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,     \
-                                              sentinel, dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot);    \
+                                              sentinel, dim, dense_out, uniq_rows, row_slot);                        \
   GRK_LAUNCH_CHECK();                                                                                                \
   if (ge)                                                                                                            \
     k_seg_combine_edges<G, LW><<<ge, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, \
-                                                  sentinel, dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot)
+                                                  sentinel, dim, dense_out, uniq_rows, row_slot)
     if (grad_dtype == GRK_BF16) { GRK_SEGW(bf16_t, 8); }
     else if (lw == 8) { GRK_SEGW(float, 8); }
     else { GRK_SEGW(float, 4); }
 #undef GRK_SEGW
     GRK_LAUNCH_CHECK();
-    return GRK_OK;
-  }
-  const unsigned gc = (unsigned)((chunks + groups - 1) / groups);
-  const unsigned gu = (unsigned)((total + groups - 1) / groups);
-  if (grad_dtype == GRK_BF16) {
-    k_seg_chunks<bf16_t><<<gc, block, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,
-                                              sentinel, dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot);
-    GRK_LAUNCH_CHECK();
-    k_seg_combine<bf16_t><<<gu, block, 0, s>>>(ws.gptr_out, ws.seg_start, ws.seg_end, ws.seg_key, uniq_count, total,
-                                               dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot);
   } else {
-    k_seg_chunks<float><<<gc, block, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,
-                                             sentinel, dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot);
+    const unsigned gc = (unsigned)((chunks + groups - 1) / groups);
+    const unsigned gu = (unsigned)((total + groups - 1) / groups);
+    if (grad_dtype == GRK_BF16) {
+      k_seg_chunks<bf16_t><<<gc, block, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,
+                                                sentinel, dim, dense_out, uniq_rows, row_slot);
+      GRK_LAUNCH_CHECK();
+      k_seg_combine<bf16_t><<<gu, block, 0, s>>>(ws.gptr_out, ws.seg_start, ws.seg_end, ws.seg_key, uniq_count, total,
+                                                 dim, dense_out, uniq_rows, row_slot);
+    } else {
+      k_seg_chunks<float><<<gc, block, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,
+                                               sentinel, dim, dense_out, uniq_rows, row_slot);
+      GRK_LAUNCH_CHECK();
+      k_seg_combine<float><<<gu, block, 0, s>>>(ws.gptr_out, ws.seg_start, ws.seg_end, ws.seg_key, uniq_count, total,
+                                                dim, dense_out, uniq_rows, row_slot);
+    }
     GRK_LAUNCH_CHECK();
-    k_seg_combine<float><<<gu, block, 0, s>>>(ws.gptr_out, ws.seg_start, ws.seg_end, ws.seg_key, uniq_count, total,
-                                              dim, ws.slotA, ws.slotB, dense_out, uniq_rows, row_slot);
   }
-  GRK_LAUNCH_CHECK();
+  if (total > 2 * kRedChunk) {  // rows longer than 2 * kRedChunk exist only then
+    const dim3 gh((unsigned)(chunks - 1), (unsigned)((dim + 63) / 64));
+    if (grad_dtype == GRK_BF16)
+      k_seg_hot<bf16_t><<<gh, 64, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel,
+                                          dim, dense_out, uniq_rows, row_slot);
+    else
+      k_seg_hot<float><<<gh, 64, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel,
+                                         dim, dense_out, uniq_rows, row_slot);
+    GRK_LAUNCH_CHECK();
+  }
   return GRK_OK;
 }

@@ -106,6 +106,9 @@ class BackwardResult:
         self.dense, self.ids, self.rows, self.count, self.capacity = dense, ids, rows, count, capacity
 
 
+BACKWARD_TRACE = None  # bench.py: a list records the embedding_backward calls of one eager step
+
+
 def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, seq_len=0, dense=True,
                        sparse=False, row_slot=None, err_flag=None):
     """Deterministic scatter-add table gradient (grk_embedding_backward).
@@ -114,6 +117,10 @@ def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, s
     ``dense`` and ``ids``/``rows``/``count`` (row-sparse form, capacity =
     number of occurrences) when ``sparse``.
     """
+    if BACKWARD_TRACE is not None:
+        BACKWARD_TRACE.append(dict(sources=list(sources), num_rows=num_rows, dim=dim, padding_idx=padding_idx,
+                                   token_type=token_type, seq_len=seq_len, dense=dense, sparse=sparse,
+                                   row_slot=None if row_slot is None else row_slot.clone()))
     dev = sources[0].grad.device
     gdt = sources[0].grad.dtype
     it = sources[0].idx.dtype

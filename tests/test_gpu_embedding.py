@@ -181,15 +181,19 @@ def test_adamw_bf16_param(K):
     assert np.mean(got == oemb.to_bf16_f32(wp)) > 0.99
 
 
-@pytest.mark.parametrize('D,dt', [(256, torch.float32), (512, torch.bfloat16), (512, torch.float32)])
+@pytest.mark.parametrize('D,dt', [(256, torch.float32), (512, torch.bfloat16), (512, torch.float32),
+                                  (64, torch.bfloat16), (40, torch.float32), (520, torch.bfloat16)])
 def test_backward_wave_path(K, D, dt):
-    """dim == 64 x 16 bytes (one wave per row: k_seg_chunks_wave +
-    k_seg_combine_edges): rows with <= 512 occurrences -- inside one chunk or
-    crossing chunk edges -- are bit-exact in occurrence order; a 3000-occurrence
-    hot row uses the fixed blocked order; padding is skipped; deterministic."""
+    """Every row bit-exact in occurrence order (the reference's CPU
+    embedding_dense_backward): rows inside one chunk, rows of <= 512
+    occurrences crossing chunk edges, and hot rows of 600-3000 occurrences
+    (k_seg_hot, one wave per 64 columns; D = 40 and 520 leave a partial
+    column slice) -- on the one-wave-per-row path (D = 64 x 16 bytes) and the
+    generic one; padding skipped; deterministic."""
     rng = np.random.default_rng(11)
     R = 3000
-    idx = np.concatenate([np.full(3000, 5), np.repeat(np.arange(10, 20), rng.integers(300, 513, 10)),
+    idx = np.concatenate([np.full(3000, 5), np.full(600, 7), np.full(1031, 8),
+                          np.repeat(np.arange(10, 20), rng.integers(300, 513, 10)),
                           rng.integers(20, R, 20000), np.zeros(2000, np.int64)])
     rng.shuffle(idx)
     g = rng.standard_normal((len(idx), D)).astype(np.float32)
@@ -200,10 +204,8 @@ def test_backward_wave_path(K, D, dt):
     want = oemb.dense_backward(g, idx, R)
     got = res.dense.cpu().numpy()
     counts = np.bincount(idx, minlength=R)
-    exact = counts <= 512
-    assert counts[10:20].min() >= 300 and counts[5] == 3000
-    assert np.array_equal(got[exact], want[exact])
-    np.testing.assert_allclose(got[~exact], want[~exact], rtol=1e-5, atol=1e-3)
+    assert counts[10:20].min() >= 300 and counts[5] == 3000 and counts[8] == 1031
+    assert np.array_equal(got, want)
     cnt = int(res.count.item())
     uniq = oemb.unique_rows(idx)
     assert cnt == len(uniq) and np.array_equal(res.ids[:cnt].cpu().numpy(), uniq)
@@ -252,19 +254,18 @@ def test_full_size_c2_properties(K):
     assert torch.all(ids[1:] > ids[:-1])
 
 
-def test_hot_rows_blocked_reduction(K):
-    """Rows with thousands of occurrences (cardinality-10 feature tables): the
-    chunked path must equal the fp64 sum to fp32 rounding and be deterministic."""
+def test_hot_rows_bit_exact(K):
+    """Rows with thousands of occurrences (cardinality-10 feature tables, two
+    lookups of one group): bit-exact in occurrence order, as the reference."""
     rng = np.random.default_rng(4)
     R, D, N = 12, 128, 40000
     idx = rng.integers(1, R, (N,))
     idx[:300] = 3                                      # a 300-occurrence row crossing chunk boundaries
-    gr = oemb.to_bf16_f32(rng.standard_normal((N, D)).astype(np.float32))
+    gr = oemb.to_bf16_f32(rng.standard_normal((N, 2 * D)).astype(np.float32))
     g = T(gr).to(torch.bfloat16)
-    a = K.embedding_backward([K.GradSource(T(idx), g, 0)], R, D, dense=True)
-    b = K.embedding_backward([K.GradSource(T(idx), g, 0)], R, D, dense=True)
+    src = [K.GradSource(T(idx), g, 0), K.GradSource(T(idx[::-1].copy()), g, D)]
+    a = K.embedding_backward(src, R, D, dense=True)
+    b = K.embedding_backward(src, R, D, dense=True)
     assert torch.equal(a.dense, b.dense)
-    want = np.zeros((R, D))
-    np.add.at(want, idx, gr.astype(np.float64))
-    want[0] = 0
-    np.testing.assert_allclose(a.dense.cpu().numpy(), want, rtol=2e-5, atol=2e-3)
+    want = oemb.dense_backward(np.concatenate([gr[:, :D], gr[:, D:]]), np.concatenate([idx, idx[::-1]]), R)
+    assert np.array_equal(a.dense.cpu().numpy(), want)
