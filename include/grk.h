@@ -449,11 +449,14 @@ int grk_mips_topk(const void* queries, int64_t ld_q, const void* items, int64_t 
  * item_feat (optional, int32 [num_items + 1, num_feat], row 0 = the default
  * feature values): neg_feat[b,t,:] = item_feat[neg[b,t],:] -- the
  * fill_missing_feat(item_feat_dict[neg]) rows of dataset.py:161-162,
- * tensorised. */
+ * tensorised.  item_ok (optional, uint8 [num_items + 1]): a draw v with
+ * item_ok[v] == 0 is redrawn like an excluded one -- the reference's
+ * `str(t) not in self.item_feat_dict` test (dataset.py:92); NULL = every id
+ * has a feature row. */
 int grk_sample_negatives(const int32_t* pos, const int32_t* next_token_type, int64_t batch, int32_t seq_len,
                          const int32_t* excl, int32_t excl_len, int64_t num_items, uint64_t seed,
-                         int32_t max_tries, const int32_t* item_feat, int32_t num_feat, int32_t* neg,
-                         int32_t* neg_feat, int32_t* err_flag, void* stream);
+                         int32_t max_tries, const int32_t* item_feat, int32_t num_feat, const uint8_t* item_ok,
+                         int32_t* neg, int32_t* neg_feat, int32_t* err_flag, void* stream);
 
 #ifdef __cplusplus
 }

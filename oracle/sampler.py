@@ -33,8 +33,12 @@ def draw(seed, b, t, a, num_items):
     return ((x * num_items) >> 64) + 1
 
 
-def sample_negatives(pos, next_token_type, excl, num_items, seed, max_tries=1000, item_feat=None):
-    """(neg int32 [B, T], neg_feat or None, all_excluded flag) -- grk_sample_negatives' contract."""
+def sample_negatives(pos, next_token_type, excl, num_items, seed, max_tries=1000, item_feat=None, item_ok=None):
+    """(neg int32 [B, T], neg_feat or None, all_excluded flag) -- grk_sample_negatives' contract.
+
+    item_ok (bool [num_items + 1], optional): ids with a feature row; a draw
+    without one is redrawn, as ``str(t) not in self.item_feat_dict`` in
+    _random_neq (model/BaseLine/dataset.py:92)."""
     pos = np.asarray(pos)
     ntt = np.asarray(next_token_type)
     B, T = pos.shape
@@ -48,7 +52,7 @@ def sample_negatives(pos, next_token_type, excl, num_items, seed, max_tries=1000
             v, hit = 0, True
             for a in range(max_tries):
                 v = draw(seed, b, t, a, num_items)
-                hit = v in ts
+                hit = v in ts or (item_ok is not None and not item_ok[v])
                 if not hit:
                     break
             flag |= hit

@@ -6,9 +6,11 @@
 //   ts   = the item ids of the user's sequence (dataset.py:136-139);
 //   for every position t whose next token is an item (next_token_type == 1)
 //   with a non-zero positive: neg[t] = uniform draw from [1, item_num] not in ts
-//   (redrawn until it is not), other positions 0 (dataset.py:156-161).
+//   and with a feature row (redrawn until both hold: `t in s or str(t) not in
+//   self.item_feat_dict`, dataset.py:92), other positions 0 (dataset.py:156-161).
 // Here ts is the caller's exclusion list excl[b, 0:excl_len] (0 entries are
 // ignored); the torch side passes the batch window's item tokens and positives.
+// "Has a feature row" is the optional byte mask item_ok[id] (NULL: every id has one).
 // The draws come from a counter-based generator (splitmix64 of seed, b, t and the
 // attempt number), so the result is a pure function of (inputs, seed): the oracle
 // (oracle/sampler.py) restates it bit-exactly.  The reference's np.random stream
@@ -49,7 +51,7 @@ __global__ void __launch_bounds__(kSampBlock)
     k_sample_negatives(const int32_t* __restrict__ pos, const int32_t* __restrict__ ntt, int32_t T,
                        const int32_t* __restrict__ excl, int32_t excl_len, int64_t num_items, uint64_t seed,
                        int32_t max_tries, const int32_t* __restrict__ item_feat, int32_t num_feat,
-                       int32_t* __restrict__ neg, int32_t* __restrict__ neg_feat, int32_t* err_flag) {
+                       const uint8_t* __restrict__ item_ok, int32_t* __restrict__ neg, int32_t* __restrict__ neg_feat, int32_t* err_flag) {
   __shared__ int32_t ex[kMaxExcl];
   const int64_t b = blockIdx.x;
   const int32_t* e = excl + b * (int64_t)excl_len;
@@ -62,7 +64,7 @@ __global__ void __launch_bounds__(kSampBlock)
       bool hit = true;
       for (int32_t a = 0; a < max_tries && hit; ++a) {
         v = draw(seed, b, t, a, num_items);
-        hit = false;
+        hit = item_ok != nullptr && item_ok[v] == 0;
         for (int i = 0; i < excl_len; ++i) hit |= (ex[i] == v);
       }
       if (hit && err_flag) atomicOr(err_flag, 2);  // every try was excluded: the last draw is kept
@@ -81,7 +83,7 @@ using namespace grk;
 extern "C" int grk_sample_negatives(const int32_t* pos, const int32_t* next_token_type, int64_t batch,
                                     int32_t seq_len, const int32_t* excl, int32_t excl_len, int64_t num_items,
                                     uint64_t seed, int32_t max_tries, const int32_t* item_feat, int32_t num_feat,
-                                    int32_t* neg, int32_t* neg_feat, int32_t* err_flag, void* stream) {
+                                    const uint8_t* item_ok, int32_t* neg, int32_t* neg_feat, int32_t* err_flag, void* stream) {
   clear_error();
   GRK_CHECK_ARG(batch >= 0 && seq_len > 0, "bad batch (%lld) / seq_len (%d)", (long long)batch, seq_len);
   GRK_CHECK_ARG(num_items >= 1 && num_items < 0x7FFFFFFFLL, "num_items must be in [1, 2^31 - 1)");
@@ -95,7 +97,7 @@ extern "C" int grk_sample_negatives(const int32_t* pos, const int32_t* next_toke
   hipStream_t s = (hipStream_t)stream;
   k_sample_negatives<<<dim3((unsigned)batch), kSampBlock, 0, s>>>(pos, next_token_type, seq_len, excl, excl_len,
                                                                    num_items, seed, max_tries, item_feat,
-                                                                   num_feat, neg, neg_feat, err_flag);
+                                                                   num_feat, item_ok, neg, neg_feat, err_flag);
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }

@@ -235,7 +235,8 @@ def tensorize(feat_list, fids, array_fids=(), emb_fids=()):
     return out
 
 
-def sample_negatives(seq, pos, token_type, next_token_type, num_items, seed, item_feat=None, max_tries=1000):
+def sample_negatives(seq, pos, token_type, next_token_type, num_items, seed, item_feat=None, max_tries=1000,
+                     item_ok=None):
     """Negatives of a tensorised batch drawn on the device (grk_sample_negatives):
     the neg / neg_feat of MyDataset.__getitem__ (model/BaseLine/dataset.py:136-162)
     for every sequence at once, so DataLoader workers need not draw them.
@@ -244,12 +245,14 @@ def sample_negatives(seq, pos, token_type, next_token_type, num_items, seed, ite
     the item tokens of its window plus its positives -- every item of the user
     the batch holds (items older than the maxlen window are not in the batch and
     are not excluded).  item_feat: int32 [num_items + 1, F] item feature ids, row
-    0 = the default values (fill_missing_feat); returns (neg [B, T], neg_feat
-    [B, T, F] or None), int32 on the batch's device."""
+    0 = the default values (fill_missing_feat); item_ok: bool [num_items + 1], the
+    ids that have a feature row (the reference redraws the others,
+    dataset.py:92); returns (neg [B, T], neg_feat [B, T, F] or None), int32 on the
+    batch's device."""
     from . import kernels as K
     excl = torch.cat([torch.where(token_type == 1, seq, 0), pos], 1)
     return K.sample_negatives(pos, next_token_type, excl, num_items, seed, max_tries=max_tries,
-                              item_feat=item_feat)
+                              item_feat=item_feat, item_ok=item_ok)
 
 
 class MyTestDataset(MyDataset):

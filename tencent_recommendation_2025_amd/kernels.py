@@ -644,13 +644,19 @@ def sampled_softmax_grad_matrix(h, e, item_ids, valid, tau, lse2, count, grad_lo
     return G[:, :M]
 
 
-def sample_negatives(pos, next_token_type, excl, num_items, seed, max_tries=1000, item_feat=None, err_flag=None):
+def sample_negatives(pos, next_token_type, excl, num_items, seed, max_tries=1000, item_feat=None, err_flag=None,
+                     item_ok=None):
     """grk_sample_negatives: neg int32 [B, T] -- for positions with next_token_type == 1
     and pos != 0, a uniform id in [1, num_items] outside excl[b] (int32 [B, L], 0 =
-    unused slot), else 0 -- and, with item_feat (int32 [num_items + 1, F]), the
-    negatives' feature rows int32 [B, T, F].  err_flag (int32 [1]) gets bit 2 when a
-    position exhausted max_tries."""
-    _require_cuda(pos, next_token_type, excl, item_feat, err_flag)
+    unused slot) and, with item_ok (bool/uint8 [num_items + 1]), with item_ok[id] set
+    (an id with a feature row), else 0 -- and, with item_feat (int32 [num_items + 1,
+    F]), the negatives' feature rows int32 [B, T, F].  err_flag (int32 [1]) gets bit 2
+    when a position exhausted max_tries."""
+    _require_cuda(pos, next_token_type, excl, item_feat, err_flag, item_ok)
+    if item_ok is not None:
+        if item_ok.dim() != 1 or item_ok.shape[0] != num_items + 1:
+            raise L.GrkError('item_ok must be [num_items + 1]')
+        item_ok = item_ok.to(torch.uint8).contiguous()
     if pos.dim() != 2 or next_token_type.shape != pos.shape or excl.dim() != 2 or excl.shape[0] != pos.shape[0]:
         raise L.GrkError('pos / next_token_type [B, T] and excl [B, L] expected')
     i32 = lambda t: t if t.dtype == torch.int32 and t.is_contiguous() else t.to(torch.int32).contiguous()
@@ -666,7 +672,7 @@ def sample_negatives(pos, next_token_type, excl, num_items, seed, max_tries=1000
         feat = torch.empty(B, T, nf, dtype=torch.int32, device=pos.device)
     rc = L.lib().grk_sample_negatives(pos.data_ptr(), ntt.data_ptr(), B, T, excl.data_ptr(), excl.shape[1],
                                       int(num_items), int(seed) & ((1 << 64) - 1), int(max_tries),
-                                      _ptr(item_feat), nf or 0, neg.data_ptr(), _ptr(feat), _ptr(err_flag),
-                                      L.stream_ptr(pos.device))
+                                      _ptr(item_feat), nf or 0, _ptr(item_ok), neg.data_ptr(), _ptr(feat),
+                                      _ptr(err_flag), L.stream_ptr(pos.device))
     L.check(rc, 'grk_sample_negatives')
     return neg, feat

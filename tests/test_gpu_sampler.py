@@ -52,6 +52,24 @@ def test_dense_exclusion_and_feature_rows():
         assert not (set(want[b][want[b] != 0].tolist()) & set(excl[b].tolist()))
 
 
+def test_ids_without_feature_rows_are_redrawn():
+    """item_ok mask (ids with a feature row, dataset.py:92) bit-exact vs the oracle."""
+    from tencent_recommendation_2025_amd import kernels as K
+    rng = np.random.default_rng(8)
+    B, Tn, N = 16, 201, 5000
+    pos = rng.integers(0, N + 1, (B, Tn)).astype(np.int32)
+    ntt = rng.integers(0, 3, (B, Tn)).astype(np.int32)
+    excl = rng.integers(0, N + 1, (B, 300)).astype(np.int32)
+    ok = rng.random(N + 1) < 0.3
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    neg, _ = K.sample_negatives(T(pos), T(ntt), T(excl), N, 5, err_flag=err, item_ok=T(ok))
+    want, _, flag = osamp.sample_negatives(pos, ntt, excl, N, 5, item_ok=ok)
+    assert not flag and err.item() == 0
+    got = neg.cpu().numpy()
+    assert np.array_equal(got, want)
+    assert ok[got[got != 0]].all()
+
+
 def test_exhaustion_sets_flag_like_oracle():
     from tencent_recommendation_2025_amd import kernels as K
     pos = np.array([[5, 0, 6]], np.int32)
