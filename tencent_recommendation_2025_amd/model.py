@@ -236,6 +236,25 @@ class BaselineModel(torch.nn.Module):
         self._proj_cache = {}
         self._proj_off_cache = {}
         self._remaps = None      # set by ShardedFusedAdamW.prepare (rows fetched from other ranks)
+        self._flushers = []      # weak refs to optimizers holding deferred table rows (FusedAdamW)
+
+    def flush_tables(self):
+        """Bring every deferred table row to the optimizer's current step (FusedAdamW
+        keeps rows outside recent batches a few steps behind): called
+        before every read of whole tables outside training -- predict,
+        save_item_emb, eval() -- and by state_dict (optimizer hook)."""
+        alive = []
+        for ref in self._flushers:
+            fn = ref()
+            if fn is not None:
+                fn()
+                alive.append(ref)
+        self._flushers = alive
+
+    def train(self, mode=True):
+        if not mode:
+            self.flush_tables()
+        return super().train(mode)
 
     def _init_feat_info(self, feat_statistics, feat_types):
         self.USER_SPARSE_FEAT = {k: feat_statistics[k] for k in feat_types['user_sparse']}
@@ -552,10 +571,12 @@ class BaselineModel(torch.nn.Module):
             self._proj_cache = {}
 
     def predict(self, log_seqs, seq_feature, mask):
+        self.flush_tables()
         return self.log2feats(log_seqs, mask, seq_feature)[:, -1, :]
 
     def save_item_emb(self, item_ids, retrieval_ids, feat_dict, save_path, batch_size=1024):
         """Candidate item embeddings -> embedding.fbin / id.u64bin (model/BaseLine/model.py:402-433)."""
+        self.flush_tables()
         embs = []
         for s in range(0, len(item_ids), batch_size):
             e = min(s + batch_size, len(item_ids))

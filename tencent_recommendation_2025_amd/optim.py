@@ -20,6 +20,8 @@ Table storage dtype defaults to bf16 (BASELINE config 2); moments are fp32.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 import ctypes as C
@@ -176,6 +178,8 @@ class FusedAdamW:
             self._uploads = 0
         if self.defer:
             model.register_state_dict_pre_hook(lambda *args, **kw: self.flush())
+            if hasattr(model, '_flushers'):  # predict / save_item_emb / eval() read fresh rows
+                model._flushers.append(weakref.WeakMethod(self.flush))
 
     @property
     def _ring(self):

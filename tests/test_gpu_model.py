@@ -242,6 +242,36 @@ def test_deferred_table_updates_are_bit_identical_to_dense(period):
             assert torch.equal(a, b), name
 
 
+def test_eval_predict_and_export_read_flushed_rows(tmp_path):
+    """Deferred rows (FusedAdamW, defer_period 16) are brought to the current
+    step before whole-table reads: eval(), predict and save_item_emb."""
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    cfg = S.SyntheticConfig(batch_size=4, maxlen=20, num_items=3000, num_users=300, min_len=4)
+    stats, types = S.feature_schema(cfg)
+    torch.manual_seed(0)
+    m = BaselineModel(cfg.num_users, cfg.num_items, stats, types,
+                      S.make_args(hidden_units=64, maxlen=20, num_blocks=1, num_heads=2)).to(DEV)
+    opt = FusedAdamW(m, lr=2e-3, defer_period=16)
+    tr = Trainer(m, opt, loss='bce')
+    g = torch.Generator(device=DEV).manual_seed(0)
+    for _ in range(3):
+        tr.step(S.make_batch(cfg, g, DEV))
+    last = opt._deferred['item'].last
+    assert (last[1:] < opt.t).any()
+    m.eval()
+    assert (last == opt.t).all()
+    m.train()
+    tr.step(S.make_batch(cfg, g, DEV))
+    assert (last[1:] < opt.t).any()
+    batch = S.make_batch(cfg, g, DEV)
+    with torch.no_grad():
+        m.predict(batch[0], batch[6], batch[3])
+    assert (last == opt.t).all()
+
+
 def test_grk_gemm_shapes_and_accumulate():
     """grk_gemm (hipBLASLt, row-major) against a torch fp32 reference of the
     same bf16 operands: every transpose combination, bias, fp32 output
