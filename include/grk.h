@@ -360,20 +360,29 @@ int grk_pair_logits_bwd(const void* h, int64_t ldh, const void* e_pos, int64_t l
  *   z_ij = <h_i, e_j> / tau over valid columns j; j != i masked when
  *   item_ids[j] == item_ids[i]; loss = mean_valid_i (logsumexp_j z_ij - z_ii)
  * h, e: bf16 [num_rows, ld] (dim in {32, 64, 128, 256, 512}); valid uint8.
+ * Only valid positions take part: the kernels list them on the device
+ * (compact index = rank among the valid positions) and size their grids for
+ * num_rows, so nothing waits on the host.  Workspace: one buffer of
+ * grk_sampled_softmax_workspace(num_rows) bytes, reusable between calls.
  * ------------------------------------------------------------------------ */
-size_t grk_sampled_softmax_workspace(int64_t num_rows);
+size_t grk_sampled_softmax_workspace(int64_t num_rows, int dim);
 
-/* Writes lse2 fp32 [num_rows] (log2-domain logsumexp, -inf on invalid rows),
- * the loss and the valid-row count (fixed-order reduction). */
+/* Writes lse2 fp32 [num_rows] (log2-domain logsumexp of the c-th valid row at
+ * index c, c < count), the loss and the valid-row count (fixed-order
+ * reduction). */
 int grk_sampled_softmax_fwd(const void* h, int64_t ldh, const void* e, int64_t lde, const int64_t* item_ids,
                             const uint8_t* valid, int64_t num_rows, int dim, float tau, float* lse2, float* loss,
                             int32_t* count, void* workspace, size_t workspace_bytes, void* stream);
 
-/* G [num_rows, ldg] bf16 = (softmax - I) * grad_loss / (count * tau) on valid
- * (row, column) pairs, 0 elsewhere; then dh = G e and de = G^T h (GEMMs). */
-int grk_sampled_softmax_grad(const void* h, int64_t ldh, const void* e, int64_t lde, const int64_t* item_ids,
-                             const uint8_t* valid, int64_t num_rows, int dim, float tau, const float* lse2,
-                             const int32_t* count, const float* grad_loss, void* G, int64_t ldg, void* stream);
+/* Fused backward (no nv x nv matrix): with G = (softmax - I) * grad_loss /
+ * (count * tau) on valid (row, column) pairs, dh = G e and de = G^T h, fp32
+ * [num_rows, ld] (16-byte aligned rows, ld >= dim, ld % 4 == 0); rows of
+ * positions that are not valid are zero.  G enters the MFMA as bf16 hi + lo:
+ * fp32-level error.  grad_loss: device scalar (NULL = 1). */
+int grk_sampled_softmax_bwd(const void* h, int64_t ldh, const void* e, int64_t lde, const int64_t* item_ids,
+                            const uint8_t* valid, int64_t num_rows, int dim, float tau, const float* lse2,
+                            const float* grad_loss, float* dh, int64_t lddh, float* de, int64_t ldde,
+                            void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Plain GEMM for the dense layers around the hot path (HSTU uvqk /

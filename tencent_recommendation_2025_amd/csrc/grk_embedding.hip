@@ -540,11 +540,17 @@ __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ key
     return gptr[i < eu ? i : eu - 1];
   };
   auto issue = [&](u32x4 (&d)[IPT], unsigned long long a) {
+    // all of the tile's address shuffles first (one LDS round trip), then its loads
     const unsigned lo = (unsigned)a, hi = (unsigned)(a >> 32);
+    unsigned plo[IPT], phi[IPT];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
-      const int src = i * OPI + wocc;
-      const unsigned long long p = ((unsigned long long)(unsigned)__shfl(hi, src) << 32) | (unsigned)__shfl(lo, src);
+      plo[i] = (unsigned)__shfl(lo, i * OPI + wocc);
+      phi[i] = (unsigned)__shfl(hi, i * OPI + wocc);
+    }
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const unsigned long long p = ((unsigned long long)phi[i] << 32) | plo[i];
       d[i] = *reinterpret_cast<gu32x4*>(p + (unsigned long long)vcol * ES);
     }
   };

@@ -5,287 +5,494 @@
 //          item_id[j] == item_id[i] (the same item is not its own negative);
 //   loss = mean over valid rows of (logsumexp_j z_ij - z_ii).
 //
-// Forward: flash-style online logsumexp, never materialising the M x M logits.
-// A workgroup = 4 waves x 32 rows; the row block's H fragments stay in
-// registers, candidate tiles of 32 rows of E are staged through LDS
-// (swizzled row image), S^T = E H^T on MFMA 32x32x16 bf16 so a lane owns one
-// row i.  The columns are split into slices over workgroups (row blocks alone
-// would leave most CUs idle); a combine kernel merges the slices' (max, sum)
-// and reduces the loss in a fixed order.
-// Backward: a second pass recomputes the tiles and writes
-//   G_ij = (softmax_ij - [i == j]) * grad_loss / (count * tau)   (bf16)
-// so that dH = G E and dE = G^T H are two plain GEMMs (hipBLASLt).
+// Only valid positions (next token an item) take part, ~half of a C2 batch, so
+// every kernel works on the COMPACT index space: k_ss_compact lists the valid
+// positions in order (vidx, count nv on the device -- no host sync: the grids
+// are sized for all positions and idle blocks leave at once) and k_ss_gather
+// copies their h / e rows and ids into contiguous compact buffers, so the
+// tile loops below stream plain rows.
+//
+// Every pass has one shape: a workgroup owns 32 compact rows of one side,
+// keeps their fragments in registers and walks 32-row tiles of the other side
+// staged through LDS (swizzled row image; the next tile is loaded into
+// registers under the current tile's MFMAs).  The D columns are split over the
+// workgroup's waves (D = 512: 4 waves x 128); each wave's partial scores over
+// its D slice are summed through LDS in a fixed order, so every wave holds the
+// full 32 x 32 score tile S^T (MFMA 32x32x16 bf16, a lane owns one row).
+//   forward: flash-style online logsumexp over column slices (never the
+//            nv x nv logits); a combine kernel merges the slices' (max, sum)
+//            and reduces the loss in a fixed order;
+//   backward, fused (no G matrix): with G_ij = (softmax_ij - [i == j]) * g /
+//            (nv * tau),  dH = G E  (workgroups owning rows of H) and
+//            dE = G^T H  (owning rows of E) in one grid, each wave
+//            accumulating its D slice; G enters the MFMA as bf16 hi + lo
+//            (G = hi + lo to ~2^-16 relative): fp32-level gradients.
+// Deterministic: no atomics, fixed reduction orders.
 #include "grk_common.h"
 #include "grk_mfma.h"
 
 namespace grk {
 
-constexpr int kSSRows = 128;  // rows per workgroup (4 waves x 32)
-
 struct SSParams {
   const bf16_t* h; int64_t ldh;
   const bf16_t* e; int64_t lde;
   const int64_t* ids;
-  const uint8_t* valid;
-  int M;
+  int* vidx;            // compact index -> position (valid positions, ascending)
+  int* nvp;             // number of valid positions (device)
+  bf16_t *hc, *ec;      // [M, D] compact copies of the valid rows of h, e
+  int64_t* idc;         // [M] their item ids
+  int M;                // positions (upper bound of nv)
   float sl2;            // log2(e) / tau
-  int slice_cols;       // columns per slice (multiple of 32)
-  float *pm, *pl;       // [nslices, M] partial max / sum (log2 domain)
-  float* diag;          // [M] z_ii in log2 units
-  float* lse2;          // [M] log2-domain logsumexp
-  float* partials;      // [nblocks * 2]
-  float* loss; int32_t* count;
+  int nslices;          // forward column slices
+  float *pm, *pl;       // [nslices, M] partial max / sum (log2 domain), compact rows
+  float* diag;          // [M] z_ii in log2 units, compact rows
+  float* lse2;          // [M] log2-domain logsumexp, compact rows
+  float* partials;      // [nblocks]
+  float* loss;
   const float* grad_loss;
-  bf16_t* G; int64_t ldg;
-  int col_tiles;        // tiles per workgroup in the gradient kernel
+  float* dh; int64_t lddh;  // fp32 gradients, by position
+  float* de; int64_t ldde;
 };
 
-template <int D>
-__device__ __forceinline__ void ss_stage(char* Es, int64_t* cid, uint8_t* cval, const SSParams& p, int jb) {
-  constexpr int NCH = D / 8;
-  for (int u = threadIdx.x; u < 32 * NCH; u += blockDim.x) {
-    const int row = u / NCH, c = u % NCH;
-    const int j = jb + row;
-    const bool ok = j < p.M;
-    uint4 v = ok ? *reinterpret_cast<const uint4*>(p.e + (int64_t)j * p.lde + c * 8) : make_uint4(0, 0, 0, 0);
-    *reinterpret_cast<uint4*>(Es + lds_off<D>(row, c * 8)) = v;
+// valid positions in order -> vidx[0 .. nv), nv -> *nv and *count (one workgroup)
+__global__ void __launch_bounds__(1024) k_ss_compact(const uint8_t* __restrict__ valid, int M, int* __restrict__ vidx,
+                                                     int* __restrict__ nv, int32_t* __restrict__ count) {
+  __shared__ int part[1024];
+  const int per = (M + 1023) / 1024;
+  const int b0 = min(M, (int)threadIdx.x * per), b1 = min(M, b0 + per);
+  int c = 0;
+  for (int i = b0; i < b1; ++i) c += valid[i] != 0;
+  part[threadIdx.x] = c;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = (int)threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
   }
-  if (threadIdx.x < 32) {
-    const int j = jb + threadIdx.x;
-    const bool ok = j < p.M;
-    cid[threadIdx.x] = ok ? p.ids[j] : -1;
-    cval[threadIdx.x] = ok ? p.valid[j] : 0;
+  int o = part[threadIdx.x] - c;
+  for (int i = b0; i < b1; ++i)
+    if (valid[i]) vidx[o++] = i;
+  if (threadIdx.x == 1023) {
+    *nv = part[1023];
+    if (count) *count = part[1023];
   }
 }
 
+// compact copies: hc[c] = h[vidx[c]], ec[c] = e[vidx[c]], idc[c] = ids[vidx[c]]
 template <int D>
-__device__ __forceinline__ f32x16 ss_tile(const char* Es, const bf16x8* hf, int r, int hh) {
-  constexpr int KS = D / 16;
-  f32x16 s = f32x16{};
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) s = mfma(lds_row8<D>(Es, r, 16 * ks + 8 * hh), hf[ks], s);
-  return s;
+__global__ void __launch_bounds__(256) k_ss_gather(SSParams p) {
+  constexpr int NCH = D / 8;
+  const int64_t units = (int64_t)(*p.nvp) * NCH;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride) {
+    const int c = (int)(u / NCH), ch = (int)(u % NCH);
+    const int i = p.vidx[c];
+    *reinterpret_cast<uint4*>(p.hc + (int64_t)c * D + ch * 8) =
+        *reinterpret_cast<const uint4*>(p.h + (int64_t)i * p.ldh + ch * 8);
+    *reinterpret_cast<uint4*>(p.ec + (int64_t)c * D + ch * 8) =
+        *reinterpret_cast<const uint4*>(p.e + (int64_t)i * p.lde + ch * 8);
+    if (ch == 0) p.idc[c] = p.ids[i];
+  }
 }
+
+// Workgroup shape: NR row groups of 32 owned rows x NW slices of the D
+// columns, one wave each.  Every staged tile serves 32 * NR owned rows (the
+// tiles stream from L2 / the Infinity Cache once per workgroup).
+template <int D>
+struct SSB {
+  static constexpr int NW = D >= 128 ? 4 : D / 32;  // D slices
+  static constexpr int NR = NW == 4 ? 2 : 4;        // row groups (<= 512 threads)
+  static constexpr int NT = 64 * NW * NR;
+  static constexpr int ROWS = 32 * NR;
+  static constexpr int DQ = D / NW;                  // columns per wave (multiple of 32)
+  static constexpr int KSQ = DQ / 16;
+  static constexpr int NDT = DQ / 32;
+};
+
+// A tile = 32 compact rows [t0, t0 + 32) of src (zero past nv) with their ids
+// (and, when lse_in, their lse2): fetch() into registers under the previous
+// tile's work, put() into the swizzled LDS image between two barriers.
+template <int D, int NT>
+struct SSTile {
+  static constexpr int NCH = D / 8;
+  static constexpr int PER = (32 * NCH + NT - 1) / NT;  // 16-byte vectors per thread
+  uint4 v[PER];
+  int64_t id;
+  float lse;
+  __device__ __forceinline__ void fetch(const bf16_t* src, const int64_t* idsrc, const float* lse_in, int t0,
+                                        int nv) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int x = threadIdx.x + u * NT, row = x / NCH, c = x % NCH;
+      const int tc = t0 + row;
+      v[u] = make_uint4(0, 0, 0, 0);
+      if (x < 32 * NCH && tc < nv) v[u] = *reinterpret_cast<const uint4*>(src + (int64_t)tc * D + c * 8);
+    }
+    if (threadIdx.x < 32) {
+      const int tc = t0 + threadIdx.x;
+      const bool ok = tc < nv;
+      id = ok ? idsrc[tc] : -1;
+      lse = (ok && lse_in) ? lse_in[tc] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void put(char* img, int64_t* tid, float* tlse) const {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int x = threadIdx.x + u * NT, row = x / NCH, c = x % NCH;
+      if (x < 32 * NCH) *reinterpret_cast<uint4*>(img + lds_off<D>(row, c * 8)) = v[u];
+    }
+    if (threadIdx.x < 32) {
+      tid[threadIdx.x] = id;
+      tlse[threadIdx.x] = lse;
+    }
+  }
+};
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations, not for its global loads.  __syncthreads() is a release fence +
+// s_barrier, and the fence waits vmcnt(0) -- it would drain the next tile's
+// prefetch at every exchange.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Forward: 4 waves x 32 compact rows of h (full-D fragments in registers, no
+// cross-wave exchange) walk a slice of e's tiles.
+constexpr int kSSFwdRows = 128;
 
 template <int D>
 __global__ void __launch_bounds__(256) k_ss_fwd(SSParams p) {
   constexpr int KS = D / 16;
-  __shared__ __attribute__((aligned(16))) char smem[32 * D * 2 + 32 * 8 + 32];
-  char* Es = smem;
-  int64_t* cid = reinterpret_cast<int64_t*>(smem + 32 * D * 2);
-  uint8_t* cval = reinterpret_cast<uint8_t*>(smem + 32 * D * 2 + 32 * 8);
+  __shared__ __attribute__((aligned(16))) char img[32 * D * 2];
+  __shared__ int64_t tid[32];
+  __shared__ float tlse[32];
+  const int nv = *p.nvp;
+  const int oc0 = blockIdx.x * kSSFwdRows;
+  if (oc0 >= nv) return;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-  const int i = blockIdx.x * kSSRows + wave * 32 + r;
-  const bool iok = i < p.M && p.valid[i];
-  const bool wave_live = __ballot(iok) != 0;
-  const int64_t myid = iok ? p.ids[i] : -2;
-  bf16x8 hf[KS];
+  const int oc = oc0 + wave * 32 + r;
+  const bool ook = oc < nv;
+  const bool wave_live = oc0 + wave * 32 < nv;
+  const int64_t oid = ook ? p.idc[oc] : -2;
+  bf16x8 of[KS];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) hf[ks] = gload8(p.h + (int64_t)(iok ? i : 0) * p.ldh + 16 * ks + 8 * hh, iok);
+  for (int ks = 0; ks < KS; ++ks) of[ks] = gload8(p.hc + (int64_t)oc * D + 16 * ks + 8 * hh, ook);
   float m = -INFINITY, l = 0.f;
-  const int c0 = blockIdx.y * p.slice_cols;
-  const int c1 = min(p.M, c0 + p.slice_cols);
+  const int tiles = (nv + 31) / 32, per = (tiles + p.nslices - 1) / p.nslices;
+  const int c0 = blockIdx.y * per * 32, c1 = min(nv, c0 + per * 32);
+  SSTile<D, 256> tile;
+  if (c0 < c1) tile.fetch(p.ec, p.idc, nullptr, c0, nv);
   for (int jb = c0; jb < c1; jb += 32) {
     __syncthreads();
-    ss_stage<D>(Es, cid, cval, p, jb);
+    tile.put(img, tid, tlse);
     __syncthreads();
+    if (jb + 32 < c1) tile.fetch(p.ec, p.idc, nullptr, jb + 32, nv);  // in flight under this tile's work
     if (!wave_live) continue;
-    f32x16 s = ss_tile<D>(Es, hf, r, hh);
+    f32x16 s = acc_zero();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) s = mfma(lds_row8<D>(img, r, 16 * ks + 8 * hh), of[ks], s);
+    const bool full = jb + 32 <= nv;
     float x[16], tmax = -INFINITY;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const int jr = acc_row(k, hh), j = jb + jr;
-      const bool ok = iok && cval[jr] && (j == i || cid[jr] != myid);
+      const int jr = acc_row(k, hh), jc = jb + jr;
+      const bool ok = (full || jc < nv) && (jc == oc || tid[jr] != oid);
       x[k] = ok ? s[k] * p.sl2 : -INFINITY;
-      if (j == i && iok) p.diag[i] = s[k] * p.sl2;
       tmax = fmaxf(tmax, x[k]);
     }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
     const float mn = fmaxf(m, tmax);
+    if (mn == -INFINITY) continue;
     float rs = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) rs += (x[k] == -INFINITY) ? 0.f : exp2f(x[k] - mn);
+    for (int k = 0; k < 16; ++k) rs += __builtin_amdgcn_exp2f(x[k] - mn);  // exp2(-inf) = 0
     rs += __shfl_xor(rs, 32);
-    l = (mn == -INFINITY) ? 0.f : l * exp2f(m - mn) + rs;
+    l = l * __builtin_amdgcn_exp2f(m - mn) + rs;
     m = mn;
   }
-  if (hh == 0 && i < p.M) {
-    p.pm[(int64_t)blockIdx.y * p.M + i] = m;
-    p.pl[(int64_t)blockIdx.y * p.M + i] = l;
+  if (hh == 0 && ook) {
+    p.pm[(int64_t)blockIdx.y * p.M + oc] = m;
+    p.pl[(int64_t)blockIdx.y * p.M + oc] = l;
   }
 }
 
-// Merge slices -> lse2[i]; per-block (loss, count) partials in fixed order.
-__global__ void __launch_bounds__(256) k_ss_combine(SSParams p, int nslices) {
-  __shared__ float red[2][256];
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  float li = 0.f, ci = 0.f;
-  if (i < p.M && p.valid[i]) {
+// z_ii (log2 units) of every compact row: one wave per row, fixed lane order.
+template <int D>
+__global__ void __launch_bounds__(256) k_ss_diag(SSParams p) {
+  const int nv = *p.nvp;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= nv) return;
+  float acc = 0.f;
+  for (int d = lane; d < D; d += 64)
+    acc += bf16_to_f32(p.hc[(int64_t)c * D + d]) * bf16_to_f32(p.ec[(int64_t)c * D + d]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) p.diag[c] = acc * p.sl2;
+}
+
+// Merge slices -> lse2[ic]; per-block loss partials in a fixed order.
+__global__ void __launch_bounds__(256) k_ss_combine(SSParams p) {
+  __shared__ float red[256];
+  const int nv = *p.nvp;
+  const int ic = blockIdx.x * blockDim.x + threadIdx.x;
+  float li = 0.f;
+  if (ic < nv) {
     float mx = -INFINITY;
-    for (int s = 0; s < nslices; ++s) mx = fmaxf(mx, p.pm[(int64_t)s * p.M + i]);
+    for (int s = 0; s < p.nslices; ++s) mx = fmaxf(mx, p.pm[(int64_t)s * p.M + ic]);
     float sum = 0.f;
-    for (int s = 0; s < nslices; ++s) {
-      const float ms = p.pm[(int64_t)s * p.M + i];
-      if (ms != -INFINITY) sum += p.pl[(int64_t)s * p.M + i] * exp2f(ms - mx);
+    for (int s = 0; s < p.nslices; ++s) {
+      const float ms = p.pm[(int64_t)s * p.M + ic];
+      if (ms != -INFINITY) sum += p.pl[(int64_t)s * p.M + ic] * exp2f(ms - mx);
     }
     const float l2 = mx + log2f(sum);
-    p.lse2[i] = l2;
-    li = (l2 - p.diag[i]) * kLn2;
-    ci = 1.f;
-  } else if (i < p.M) {
-    p.lse2[i] = -INFINITY;
+    p.lse2[ic] = l2;
+    li = (l2 - p.diag[ic]) * kLn2;
   }
-  red[0][threadIdx.x] = li;
-  red[1][threadIdx.x] = ci;
+  red[threadIdx.x] = li;
   __syncthreads();
   for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + s];
-      red[1][threadIdx.x] += red[1][threadIdx.x + s];
-    }
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    p.partials[2 * blockIdx.x] = red[0][0];
-    p.partials[2 * blockIdx.x + 1] = red[1][0];
-  }
+  if (threadIdx.x == 0) p.partials[blockIdx.x] = red[0];
 }
 
 __global__ void __launch_bounds__(1024) k_ss_finalize(SSParams p, int nblocks) {
-  __shared__ double red[2][1024];
-  double a = 0.0, c = 0.0;
-  for (int b = threadIdx.x; b < nblocks; b += blockDim.x) {
-    a += p.partials[2 * b];
-    c += p.partials[2 * b + 1];
-  }
-  red[0][threadIdx.x] = a;
-  red[1][threadIdx.x] = c;
+  __shared__ double red[1024];
+  double a = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += blockDim.x) a += p.partials[b];
+  red[threadIdx.x] = a;
   __syncthreads();
   for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + s];
-      red[1][threadIdx.x] += red[1][threadIdx.x + s];
-    }
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const double cnt = red[1][0];
-    p.loss[0] = (float)(red[0][0] / (cnt > 0 ? cnt : 1.0));
-    p.count[0] = (int32_t)cnt;
+    const int nv = *p.nvp;
+    p.loss[0] = (float)(red[0] / (nv > 0 ? nv : 1));
   }
 }
 
-// G tile writer: every (i, j) in [0, M)^2 is written (zeros where masked).
+// Backward: blockIdx.y = 0 owns compact rows of h (dH = G E, walking e's
+// tiles), 1 owns compact rows of e (dE = G^T H, walking h's tiles).  Per tile
+// and row group: each D-slice wave's 16 partial scores go to LDS; wave ws sums
+// (in slice order) and turns into G the EPW = 16 / NW elements it owns, and
+// hands them back as bf16 hi / lo words; every wave then multiplies the whole
+// G tile into its D slice of the gradient.  The softmax math runs once per
+// element, not once per wave.
 template <int D>
-__global__ void __launch_bounds__(256) k_ss_grad(SSParams p) {
-  constexpr int KS = D / 16;
-  __shared__ __attribute__((aligned(16))) char smem[32 * D * 2 + 32 * 8 + 32];
-  char* Es = smem;
-  int64_t* cid = reinterpret_cast<int64_t*>(smem + 32 * D * 2);
-  uint8_t* cval = reinterpret_cast<uint8_t*>(smem + 32 * D * 2 + 32 * 8);
+struct SSBwdLds {
+  static constexpr int NW = SSB<D>::NW, NR = SSB<D>::NR, EPW = 16 / NW;
+  char img[32 * D * 2];
+  float4 red[NW > 1 ? NR * NW * 4 * 64 : 1];  // partial scores [rg][wave][quad][lane]
+  uint32_t gx[NR * NW * 64 * EPW];             // G words [rg][wave][lane][EPW/2 hi, EPW/2 lo]
+  int64_t tid[32];
+  float tlse[32];
+};
+
+template <int D>
+__global__ void __launch_bounds__(SSB<D>::NT) k_ss_bwd(SSParams p) {
+  constexpr int NW = SSB<D>::NW, DQ = SSB<D>::DQ, KSQ = SSB<D>::KSQ, NDT = SSB<D>::NDT;
+  constexpr int EPW = 16 / NW;
+  __shared__ __attribute__((aligned(16))) SSBwdLds<D> L;
+  const int nv = *p.nvp;
+  const int oc0 = blockIdx.x * SSB<D>::ROWS;
+  if (oc0 >= nv) return;
+  const bool rows = blockIdx.y == 0;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-  const int i = blockIdx.x * kSSRows + wave * 32 + r;
-  const bool irow = i < p.M;
-  const bool iok = irow && p.valid[i];
-  const bool wave_live = __ballot(iok) != 0;
-  const int64_t myid = iok ? p.ids[i] : -2;
-  const float l2 = iok ? p.lse2[i] : 0.f;
-  const float coef = (p.grad_loss ? *p.grad_loss : 1.f) / (float)max(*p.count, 1) * (p.sl2 / kLog2e);
-  bf16x8 hf[KS];
+  const int rg = wave / NW, ws = wave % NW;
+  const int oc = oc0 + rg * 32 + r;
+  const bool ook = oc < nv;
+  const int64_t oid = ook ? p.idc[oc] : -2;
+  const float olse = (rows && ook) ? p.lse2[oc] : 0.f;
+  const bf16_t* own = rows ? p.hc : p.ec;
+  const bf16_t* tsrc = rows ? p.ec : p.hc;
+  const float* lse_in = rows ? nullptr : p.lse2;
+  const int col0 = ws * DQ;
+  bf16x8 of[KSQ];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) hf[ks] = gload8(p.h + (int64_t)(iok ? i : 0) * p.ldh + 16 * ks + 8 * hh, iok);
-  const int jb0 = blockIdx.y * p.col_tiles * 32;
-  for (int t = 0; t < p.col_tiles; ++t) {
-    const int jb = jb0 + 32 * t;
-    if (jb >= p.M) break;
+  for (int ks = 0; ks < KSQ; ++ks) of[ks] = gload8(own + (int64_t)oc * D + col0 + 16 * ks + 8 * hh, ook);
+  const float coef = (p.grad_loss ? *p.grad_loss : 1.f) / (float)max(nv, 1) * (p.sl2 / kLog2e);
+  f32x16 acc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) acc[dt] = acc_zero();
+  uint32_t* gx_mine = L.gx + ((rg * NW + ws) * 64 + lane) * EPW;
+  SSTile<D, SSB<D>::NT> tile;
+  tile.fetch(tsrc, p.idc, lse_in, 0, nv);
+  for (int tb = 0; tb < nv; tb += 32) {
     __syncthreads();
-    ss_stage<D>(Es, cid, cval, p, jb);
+    tile.put(L.img, L.tid, L.tlse);
     __syncthreads();
-    f32x16 s = f32x16{};
-    if (wave_live) s = ss_tile<D>(Es, hf, r, hh);
+    if (tb + 32 < nv) tile.fetch(tsrc, p.idc, lse_in, tb + 32, nv);  // in flight under this tile's work
+    f32x16 s = acc_zero();
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      float v[4];
+    for (int ks = 0; ks < KSQ; ++ks) s = mfma(lds_row8<D>(L.img, r, col0 + 16 * ks + 8 * hh), of[ks], s);
+    // this wave's elements k in [ws * EPW, (ws + 1) * EPW): full scores, slice order
+    float se[EPW];
+    if constexpr (NW > 1) {
+      float4* red = L.red + rg * NW * 4 * 64;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int k = 4 * g4 + q;
-        const int jr = acc_row(k, hh), j = jb + jr;
-        const bool ok = iok && j < p.M && cval[jr] && (j == i || cid[jr] != myid);
-        const float pr = ok ? exp2f(s[k] * p.sl2 - l2) : 0.f;
-        v[q] = ok ? (pr - (j == i ? 1.f : 0.f)) * coef : 0.f;
+      for (int q = 0; q < 4; ++q) red[(ws * 4 + q) * 64 + lane] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
+      lds_barrier();
+#pragma unroll
+      for (int q = 0; q < EPW / 4; ++q) {
+        float4 t = red[(0 * 4 + ws * (EPW / 4) + q) * 64 + lane];
+#pragma unroll 1
+        for (int w = 1; w < NW; ++w) {
+          const float4 u = red[(w * 4 + ws * (EPW / 4) + q) * 64 + lane];
+          t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+        }
+        se[4 * q] = t.x; se[4 * q + 1] = t.y; se[4 * q + 2] = t.z; se[4 * q + 3] = t.w;
       }
-      const int j0 = jb + 8 * g4 + 4 * hh;
-      if (!irow) continue;
-      bf16_t* dst = p.G + (int64_t)i * p.ldg + j0;
-      if (j0 + 3 < p.M) {
-        uint2 w;
-        w.x = (unsigned)f32_to_bf16(v[0]) | ((unsigned)f32_to_bf16(v[1]) << 16);
-        w.y = (unsigned)f32_to_bf16(v[2]) | ((unsigned)f32_to_bf16(v[3]) << 16);
-        *reinterpret_cast<uint2*>(dst) = w;
-      } else {
-        for (int q = 0; q < 4; ++q)
-          if (j0 + q < p.M) dst[q] = f32_to_bf16(v[q]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) se[k] = s[k];
+    }
+    const bool full = tb + 32 <= nv;
+    float g[EPW];
+#pragma unroll
+    for (int e = 0; e < EPW; ++e) {
+      const int k = ws * EPW + e;  // not a compile-time constant across waves: acc_row by formula
+      const int tr = (k & 3) + 8 * (k >> 2) + 4 * hh, tc = tb + tr;
+      const bool ok = ook && (full || tc < nv) && (tc == oc || L.tid[tr] != oid);
+      const float pr = __builtin_amdgcn_exp2f(fmaf(se[e], p.sl2, -(rows ? olse : L.tlse[tr])));
+      g[e] = ok ? (tc == oc ? pr - 1.f : pr) * coef : 0.f;
+    }
+#pragma unroll
+    for (int e2 = 0; e2 < EPW / 2; ++e2) {
+      const __bf16 h0 = static_cast<__bf16>(g[2 * e2]), h1 = static_cast<__bf16>(g[2 * e2 + 1]);
+      const __bf16 l0 = static_cast<__bf16>(g[2 * e2] - static_cast<float>(h0));
+      const __bf16 l1 = static_cast<__bf16>(g[2 * e2 + 1] - static_cast<float>(h1));
+      gx_mine[e2] = (uint32_t)__builtin_bit_cast(bf16_t, h0) | ((uint32_t)__builtin_bit_cast(bf16_t, h1) << 16);
+      gx_mine[EPW / 2 + e2] = (uint32_t)__builtin_bit_cast(bf16_t, l0) | ((uint32_t)__builtin_bit_cast(bf16_t, l1) << 16);
+    }
+    lds_barrier();
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      uint32_t hw[4], lw[4];
+#pragma unroll
+      for (int pp = 0; pp < 4; ++pp) {  // element pair 8 s2 + 2 pp .. + 1
+        const int k = 8 * s2 + 2 * pp, w = k / EPW, kk = k % EPW;
+        const uint32_t* src = L.gx + ((rg * NW + w) * 64 + lane) * EPW;
+        hw[pp] = src[kk / 2];
+        lw[pp] = src[EPW / 2 + kk / 2];
+      }
+      const bf16x8 gh = __builtin_bit_cast(bf16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
+      const bf16x8 gl = __builtin_bit_cast(bf16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const bf16x8 tf = lds_tr8<D>(L.img, 16 * s2, col0 + 32 * dt, lane);
+        acc[dt] = mfma(tf, gh, acc[dt]);
+        acc[dt] = mfma(tf, gl, acc[dt]);
       }
     }
   }
+  if (!ook) return;
+  const int pos = p.vidx[oc];
+  float* out = rows ? p.dh + (int64_t)pos * p.lddh : p.de + (int64_t)pos * p.ldde;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4)
+      *reinterpret_cast<float4*>(out + col0 + 32 * dt + 8 * g4 + 4 * hh) =
+          make_float4(acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]);
 }
 
+// which: 0 = compaction gather + forward, 1 = compaction gather + backward
 template <int D>
-static int ss_launch(const SSParams& p, int which, int nslices, hipStream_t s) {
-  const unsigned rb = (unsigned)((p.M + kSSRows - 1) / kSSRows);
+static int ss_launch(const SSParams& p, int which, hipStream_t s) {
+  k_ss_gather<D><<<grid_for((int64_t)p.M * (D / 8), 256), 256, 0, s>>>(p);
+  GRK_LAUNCH_CHECK();
   if (which == 0) {
-    k_ss_fwd<D><<<dim3(rb, nslices), 256, 0, s>>>(p);
+    k_ss_diag<D><<<(unsigned)((p.M + 3) / 4), 256, 0, s>>>(p);
+    GRK_LAUNCH_CHECK();
+    k_ss_fwd<D><<<dim3((unsigned)((p.M + kSSFwdRows - 1) / kSSFwdRows), p.nslices), 256, 0, s>>>(p);
   } else {
-    const int tiles = (p.M + 31) / 32;
-    k_ss_grad<D><<<dim3(rb, (tiles + p.col_tiles - 1) / p.col_tiles), 256, 0, s>>>(p);
+    k_ss_bwd<D><<<dim3((unsigned)((p.M + SSB<D>::ROWS - 1) / SSB<D>::ROWS), 2), SSB<D>::NT, 0, s>>>(p);
   }
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }
 
-static int ss_dispatch(const SSParams& p, int dim, int which, int nslices, hipStream_t s) {
+static int ss_dispatch(const SSParams& p, int dim, int which, hipStream_t s) {
   switch (dim) {
-    case 32: return ss_launch<32>(p, which, nslices, s);
-    case 64: return ss_launch<64>(p, which, nslices, s);
-    case 128: return ss_launch<128>(p, which, nslices, s);
-    case 256: return ss_launch<256>(p, which, nslices, s);
-    case 512: return ss_launch<512>(p, which, nslices, s);
+    case 32: return ss_launch<32>(p, which, s);
+    case 64: return ss_launch<64>(p, which, s);
+    case 128: return ss_launch<128>(p, which, s);
+    case 256: return ss_launch<256>(p, which, s);
+    case 512: return ss_launch<512>(p, which, s);
   }
   set_error("dim %d unsupported (32, 64, 128, 256, 512)", dim);
   return GRK_EUNSUPPORTED;
 }
 
 static int ss_slices(int M) {
-  // enough workgroups to cover the chip: row blocks x slices >= ~2 per CU
-  const int rb = (M + kSSRows - 1) / kSSRows;
-  int ns = (512 + rb - 1) / rb;
+  // forward column slices: ~1k workgroups when every position is valid
+  // (half of them, ~2 per CU, at C2's ~53 % valid)
+  const int rb = (M + kSSFwdRows - 1) / kSSFwdRows;
+  int ns = (1024 + rb - 1) / rb;
   const int tiles = (M + 31) / 32;
   if (ns > tiles) ns = tiles;
   return ns < 1 ? 1 : ns;
+}
+
+struct SSWs {
+  int* vidx;
+  int* nv;
+  bf16_t *hc, *ec;
+  int64_t* idc;
+  float *pm, *pl, *diag, *partials;
+  size_t bytes;
+};
+
+static SSWs ss_ws(char* base, int M, int D) {
+  SSWs w;
+  const int ns = ss_slices(M);
+  const int nb = (M + 255) / 256;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* q = base ? base + off : nullptr;
+    off += (bytes + 255) & ~(size_t)255;
+    return q;
+  };
+  w.vidx = (int*)take((size_t)M * 4);
+  w.nv = (int*)take(4);
+  w.hc = (bf16_t*)take((size_t)M * D * 2);
+  w.ec = (bf16_t*)take((size_t)M * D * 2);
+  w.idc = (int64_t*)take((size_t)M * 8);
+  w.pm = (float*)take((size_t)ns * M * 4);
+  w.pl = (float*)take((size_t)ns * M * 4);
+  w.diag = (float*)take((size_t)M * 4);
+  w.partials = (float*)take((size_t)nb * 4);
+  w.bytes = off;
+  return w;
 }
 
 }  // namespace grk
 
 using namespace grk;
 
-extern "C" size_t grk_sampled_softmax_workspace(int64_t num_rows) {
-  const int M = (int)num_rows;
-  const int ns = ss_slices(M);
-  const int nb = (M + 255) / 256;
-  return ((size_t)2 * ns * M + 2 * (size_t)M + 2 * (size_t)nb + 64) * sizeof(float);
+extern "C" size_t grk_sampled_softmax_workspace(int64_t num_rows, int dim) {
+  if (num_rows <= 0 || num_rows >= (1LL << 30) || dim <= 0 || dim > 512) return 0;
+  return ss_ws(nullptr, (int)num_rows, dim).bytes + 256;
 }
 
 static int ss_fill(const void* h, int64_t ldh, const void* e, int64_t lde, const int64_t* ids, const uint8_t* valid,
-                   int64_t num_rows, int dim, float tau, SSParams* p) {
+                   int64_t num_rows, int dim, float tau, void* workspace, size_t workspace_bytes, SSParams* p,
+                   SSWs* w) {
   GRK_CHECK_ARG(h && e && ids && valid, "h, e, item_ids and valid are required");
   GRK_CHECK_ARG(num_rows > 0 && num_rows < (1LL << 30), "num_rows out of range");
   GRK_CHECK_ARG(dim == 32 || dim == 64 || dim == 128 || dim == 256 || dim == 512, "dim %d unsupported", dim);
   GRK_CHECK_ARG(ldh >= dim && lde >= dim && ldh % 8 == 0 && lde % 8 == 0, "row strides must be >= dim, multiple of 8");
   GRK_CHECK_ARG(((uintptr_t)h | (uintptr_t)e) % 16 == 0, "h / e must be 16-byte aligned");
   GRK_CHECK_ARG(tau > 0.f, "temperature must be > 0");
+  GRK_CHECK_ARG(workspace && workspace_bytes >= grk_sampled_softmax_workspace(num_rows, dim), "workspace too small");
   memset(p, 0, sizeof(*p));
   p->h = (const bf16_t*)h; p->ldh = ldh; p->e = (const bf16_t*)e; p->lde = lde;
-  p->ids = ids; p->valid = valid; p->M = (int)num_rows; p->sl2 = kLog2e / tau;
+  p->ids = ids; p->M = (int)num_rows; p->sl2 = kLog2e / tau;
+  p->nslices = ss_slices(p->M);
+  *w = ss_ws((char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), p->M, dim);
+  p->vidx = w->vidx; p->nvp = w->nv; p->hc = w->hc; p->ec = w->ec; p->idc = w->idc;
+  p->pm = w->pm; p->pl = w->pl; p->diag = w->diag; p->partials = w->partials;
   return GRK_OK;
 }
 
@@ -295,40 +502,43 @@ extern "C" int grk_sampled_softmax_fwd(const void* h, int64_t ldh, const void* e
                                        void* stream) {
   clear_error();
   SSParams p;
-  int rc = ss_fill(h, ldh, e, lde, item_ids, valid, num_rows, dim, tau, &p);
+  SSWs w;
+  int rc = ss_fill(h, ldh, e, lde, item_ids, valid, num_rows, dim, tau, workspace, workspace_bytes, &p, &w);
   if (rc) return rc;
-  GRK_CHECK_ARG(lse2 && loss && count && workspace, "lse2, loss, count and workspace are required");
-  GRK_CHECK_ARG(workspace_bytes >= grk_sampled_softmax_workspace(num_rows), "workspace too small");
-  const int M = p.M;
-  const int ns = ss_slices(M);
-  const int nb = (M + 255) / 256;
-  float* ws = (float*)workspace;
-  p.pm = ws; p.pl = ws + (size_t)ns * M; p.diag = ws + (size_t)2 * ns * M;
-  p.partials = p.diag + M;
-  p.lse2 = lse2; p.loss = loss; p.count = count;
-  const int tiles = (M + 31) / 32;
-  p.slice_cols = ((tiles + ns - 1) / ns) * 32;
+  GRK_CHECK_ARG(lse2 && loss && count, "lse2, loss and count are required");
+  p.lse2 = lse2; p.loss = loss;
   hipStream_t s = (hipStream_t)stream;
-  rc = ss_dispatch(p, dim, 0, ns, s);
+  k_ss_compact<<<1, 1024, 0, s>>>(valid, p.M, w.vidx, w.nv, count);
+  GRK_LAUNCH_CHECK();
+  rc = ss_dispatch(p, dim, 0, s);
   if (rc) return rc;
-  k_ss_combine<<<nb, 256, 0, s>>>(p, ns);
+  const int nb = (p.M + 255) / 256;
+  k_ss_combine<<<nb, 256, 0, s>>>(p);
   GRK_LAUNCH_CHECK();
   k_ss_finalize<<<1, 1024, 0, s>>>(p, nb);
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }
 
-extern "C" int grk_sampled_softmax_grad(const void* h, int64_t ldh, const void* e, int64_t lde,
-                                        const int64_t* item_ids, const uint8_t* valid, int64_t num_rows, int dim,
-                                        float tau, const float* lse2, const int32_t* count, const float* grad_loss,
-                                        void* G, int64_t ldg, void* stream) {
+extern "C" int grk_sampled_softmax_bwd(const void* h, int64_t ldh, const void* e, int64_t lde, const int64_t* item_ids,
+                                       const uint8_t* valid, int64_t num_rows, int dim, float tau, const float* lse2,
+                                       const float* grad_loss, float* dh, int64_t lddh, float* de, int64_t ldde,
+                                       void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
   SSParams p;
-  int rc = ss_fill(h, ldh, e, lde, item_ids, valid, num_rows, dim, tau, &p);
+  SSWs w;
+  int rc = ss_fill(h, ldh, e, lde, item_ids, valid, num_rows, dim, tau, workspace, workspace_bytes, &p, &w);
   if (rc) return rc;
-  GRK_CHECK_ARG(lse2 && count && G, "lse2, count and G are required");
-  GRK_CHECK_ARG(ldg >= num_rows && ldg % 4 == 0, "ldg must be >= num_rows and a multiple of 4");
-  p.lse2 = const_cast<float*>(lse2); p.count = const_cast<int32_t*>(count); p.grad_loss = grad_loss;
-  p.G = (bf16_t*)G; p.ldg = ldg; p.col_tiles = 8;
-  return ss_dispatch(p, dim, 1, 0, (hipStream_t)stream);
+  GRK_CHECK_ARG(lse2 && dh && de, "lse2, dh and de are required");
+  GRK_CHECK_ARG(lddh >= dim && ldde >= dim && lddh % 4 == 0 && ldde % 4 == 0, "lddh / ldde must be >= dim, multiple of 4");
+  GRK_CHECK_ARG(((uintptr_t)dh | (uintptr_t)de) % 16 == 0, "dh / de must be 16-byte aligned");
+  p.lse2 = const_cast<float*>(lse2); p.grad_loss = grad_loss;
+  p.dh = dh; p.lddh = lddh; p.de = de; p.ldde = ldde;
+  hipStream_t s = (hipStream_t)stream;
+  // rows of positions that are not valid stay zero
+  GRK_CHECK_HIP(zero_async(dh, (size_t)p.M * lddh * 4, s));
+  GRK_CHECK_HIP(zero_async(de, (size_t)p.M * ldde * 4, s));
+  k_ss_compact<<<1, 1024, 0, s>>>(valid, p.M, w.vidx, w.nv, nullptr);
+  GRK_LAUNCH_CHECK();
+  return ss_dispatch(p, dim, 1, s);
 }

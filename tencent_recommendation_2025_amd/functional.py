@@ -396,9 +396,9 @@ class _SampledSoftmaxFn(torch.autograd.Function):
     def backward(ctx, gloss):
         hb, eb, ids, valid, lse2, count = ctx.saved_tensors
         tau, hs, es, hdt, edt = ctx.meta
-        G = K.sampled_softmax_grad_matrix(hb, eb, ids, valid, tau, lse2, count, gloss)
-        dh = (G @ eb).view(hs).to(hdt) if ctx.needs_input_grad[0] else None
-        de = (G.t() @ hb).view(es).to(edt) if ctx.needs_input_grad[1] else None
+        dh, de = K.sampled_softmax_bwd(hb, eb, ids, valid, tau, lse2, gloss)
+        dh = dh.view(hs).to(hdt) if ctx.needs_input_grad[0] else None
+        de = de.view(es).to(edt) if ctx.needs_input_grad[1] else None
         return dh, de, None, None, None
 
 
@@ -406,7 +406,8 @@ class _SampledSoftmaxFn(torch.autograd.Function):
 def sampled_softmax_loss(h, pos_emb, pos_ids, next_token_type, tau):
     """In-batch sampled softmax over every valid position's positive item
     (north star; oracle/loss.py::sampled_softmax): one flash-style MFMA pass
-    for the loss, a G-matrix pass + two GEMMs for the gradients."""
+    for the loss, two fused passes (dH, dE) for the gradients, all over the
+    valid positions only."""
     ids = pos_ids.reshape(-1).to(torch.int64).contiguous()
     valid = (next_token_type.reshape(-1) == 1).to(torch.uint8).contiguous()
     return _SampledSoftmaxFn.apply(h, pos_emb, ids, valid, float(tau))

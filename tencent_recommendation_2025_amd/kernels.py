@@ -618,7 +618,7 @@ def sampled_softmax_fwd(h, e, item_ids, valid, tau):
     M, D = h.shape
     dev = h.device
     (hp, hl), (ep, el) = _rows(h, 'h'), _rows(e, 'e')
-    ws = torch.empty(max(L.lib().grk_sampled_softmax_workspace(M), 4), dtype=torch.uint8, device=dev)
+    ws = torch.empty(max(L.lib().grk_sampled_softmax_workspace(M, D), 4), dtype=torch.uint8, device=dev)
     lse2 = torch.empty(M, dtype=torch.float32, device=dev)
     loss = torch.empty((), dtype=torch.float32, device=dev)
     count = torch.empty(1, dtype=torch.int32, device=dev)
@@ -629,19 +629,21 @@ def sampled_softmax_fwd(h, e, item_ids, valid, tau):
     return loss, lse2, count
 
 
-def sampled_softmax_grad_matrix(h, e, item_ids, valid, tau, lse2, count, grad_loss=None):
-    """G [M, M] bf16 (view of a row-padded buffer) with dh = G e, de = G^T h."""
-    _require_cuda(h, e, item_ids, valid, lse2, count, grad_loss)
+def sampled_softmax_bwd(h, e, item_ids, valid, tau, lse2, grad_loss=None):
+    """(dh, de) fp32 [M, D] of the in-batch sampled softmax, fused (grk_sampled_softmax_bwd)."""
+    _require_cuda(h, e, item_ids, valid, lse2, grad_loss)
     M, D = h.shape
-    ldg = (M + 7) // 8 * 8
-    G = torch.empty(M, ldg, dtype=torch.bfloat16, device=h.device)
+    dev = h.device
+    dh = torch.empty(M, D, dtype=torch.float32, device=dev)
+    de = torch.empty(M, D, dtype=torch.float32, device=dev)
     gl = None if grad_loss is None else grad_loss.float().reshape(1).contiguous()
+    ws = torch.empty(max(L.lib().grk_sampled_softmax_workspace(M, D), 4), dtype=torch.uint8, device=dev)
     (hp, hl), (ep, el) = _rows(h, 'h'), _rows(e, 'e')
-    rc = L.lib().grk_sampled_softmax_grad(hp, hl, ep, el, item_ids.data_ptr(), valid.data_ptr(), M, D, float(tau),
-                                          lse2.data_ptr(), count.data_ptr(), _ptr(gl), G.data_ptr(), ldg,
-                                          L.stream_ptr(h.device))
-    L.check(rc, 'grk_sampled_softmax_grad')
-    return G[:, :M]
+    rc = L.lib().grk_sampled_softmax_bwd(hp, hl, ep, el, item_ids.data_ptr(), valid.data_ptr(), M, D, float(tau),
+                                         lse2.data_ptr(), _ptr(gl), dh.data_ptr(), D, de.data_ptr(), D, ws.data_ptr(),
+                                         ws.numel(), L.stream_ptr(dev))
+    L.check(rc, 'grk_sampled_softmax_bwd')
+    return dh, de
 
 
 def sample_negatives(pos, next_token_type, excl, num_items, seed, max_tries=1000, item_feat=None, err_flag=None,

@@ -570,9 +570,18 @@ class BaselineModel(torch.nn.Module):
             self._fwd_id = None
             self._proj_cache = {}
 
+    def _inference_autocast(self):
+        """bf16 tables (fused mode, optim.FusedAdamW) run inference under the bf16
+        autocast they train in; fp32 tables (drop-in mode) as the reference, fp32."""
+        ref = self._ref('item_emb').weight if self._table_refs is not None else self.item_emb.weight
+        if ref.dtype == torch.bfloat16 and ref.is_cuda and not torch.is_autocast_enabled('cuda'):
+            return torch.autocast('cuda', dtype=torch.bfloat16)
+        return contextlib.nullcontext()
+
     def predict(self, log_seqs, seq_feature, mask):
         self.flush_tables()
-        return self.log2feats(log_seqs, mask, seq_feature)[:, -1, :]
+        with self._inference_autocast():
+            return self.log2feats(log_seqs, mask, seq_feature)[:, -1, :]
 
     def save_item_emb(self, item_ids, retrieval_ids, feat_dict, save_path, batch_size=1024):
         """Candidate item embeddings -> embedding.fbin / id.u64bin (model/BaseLine/model.py:402-433)."""
@@ -582,7 +591,9 @@ class BaselineModel(torch.nn.Module):
             e = min(s + batch_size, len(item_ids))
             seq = torch.tensor(item_ids[s:e], device=self._device()).unsqueeze(0)
             feats = [np.array([feat_dict[i] for i in range(s, e)], dtype=object)]
-            embs.append(self.feat2emb(seq, feats, include_user=False).squeeze(0).detach().float().cpu().numpy())
+            with self._inference_autocast():
+                emb = self.feat2emb(seq, feats, include_user=False)
+            embs.append(emb.squeeze(0).detach().float().cpu().numpy())
         save_emb(np.concatenate(embs, 0), Path(save_path, 'embedding.fbin'))
         save_emb(np.array(retrieval_ids, dtype=np.uint64).reshape(-1, 1), Path(save_path, 'id.u64bin'))
 

@@ -1,8 +1,9 @@
 """GPU parity of the loss kernels: fused pair logits + BCE (reference loss,
 model/BaseLine/main.py:177-182) and the in-batch sampled softmax (north star,
 parity unpinned vs the reference; checked against oracle/loss.py in fp64 on the
-same bf16-rounded inputs: loss within 1e-3 relative, gradients 1e-2 normwise
-because G is rounded to bf16 before the two GEMMs)."""
+same bf16-rounded inputs: loss and gradients within 1e-3 relative (normwise)
+-- the north star's bf16 loss tolerance; the fused backward feeds G to the MFMA
+as bf16 hi + lo, so the gradients are in fact fp32-accurate)."""
 import numpy as np
 import pytest
 import torch
@@ -61,20 +62,42 @@ def sampled_case(M, D, seed, frac_valid=0.6, dup_every=7):
     return h, e, ids, valid
 
 
-@pytest.mark.parametrize('M,D', [(77, 32), (600, 64), (1000, 512), (333, 128)])
+@pytest.mark.parametrize('M,D', [(77, 32), (600, 64), (1000, 512), (333, 128), (2100, 256)])
 def test_sampled_softmax_matches_oracle(K, M, D):
+    """fp32 gradients of the fused backward vs the fp64 oracle at 1e-4 (the
+    bf16-output gradients of the autograd path at 1e-3 below)."""
     from tencent_recommendation_2025_amd import functional as G
     h, e, ids, valid = sampled_case(M, D, seed=M)
     tau = 0.05
     loss, dh, de = oloss.sampled_softmax(h, e, ids, valid, tau)
     th = torch.from_numpy(h).to(DEV).to(torch.bfloat16).requires_grad_(True)
     te = torch.from_numpy(e).to(DEV).to(torch.bfloat16).requires_grad_(True)
+    ids_d = torch.from_numpy(ids).to(DEV)
     ntt = torch.from_numpy(valid.astype(np.int64)).to(DEV)
-    got = G.sampled_softmax_loss(th, te, torch.from_numpy(ids).to(DEV), ntt, tau)
+    got = G.sampled_softmax_loss(th, te, ids_d, ntt, tau)
     got.backward()
-    assert abs(got.item() - loss) < 1e-3 * abs(loss), (got.item(), loss)
-    assert nrel(th.grad.float().cpu().numpy(), dh) < 1e-2
-    assert nrel(te.grad.float().cpu().numpy(), de) < 1e-2
+    assert abs(got.item() - loss) < 1e-4 * abs(loss), (got.item(), loss)
+    # bf16 gradients (h's dtype) vs the oracle rounded the same way
+    assert nrel(th.grad.float().cpu().numpy(), to_bf16_f32(dh.astype(np.float32))) < 1e-3
+    assert nrel(te.grad.float().cpu().numpy(), to_bf16_f32(de.astype(np.float32))) < 1e-3
+    v8 = torch.from_numpy(valid.astype(np.uint8)).to(DEV)
+    l2, lse2, cnt = K.sampled_softmax_fwd(th.detach(), te.detach(), ids_d, v8, tau)
+    fdh, fde = K.sampled_softmax_bwd(th.detach(), te.detach(), ids_d, v8, tau, lse2)
+    assert int(cnt.item()) == int(valid.sum())
+    assert nrel(fdh.cpu().numpy(), dh) < 1e-4 and nrel(fde.cpu().numpy(), de) < 1e-4
+    assert torch.all(fdh[~v8.bool()] == 0) and torch.all(fde[~v8.bool()] == 0)
+    again = K.sampled_softmax_bwd(th.detach(), te.detach(), ids_d, v8, tau, lse2)
+    assert torch.equal(again[0], fdh) and torch.equal(again[1], fde)      # deterministic
+
+
+def test_sampled_softmax_no_valid_rows(K):
+    M, D = 64, 64
+    h = torch.randn(M, D, device=DEV).bfloat16()
+    ids = torch.arange(M, device=DEV)
+    v8 = torch.zeros(M, dtype=torch.uint8, device=DEV)
+    loss, lse2, cnt = K.sampled_softmax_fwd(h, h, ids, v8, 0.1)
+    dh, de = K.sampled_softmax_bwd(h, h, ids, v8, 0.1, lse2)
+    assert loss.item() == 0 and cnt.item() == 0 and torch.all(dh == 0) and torch.all(de == 0)
 
 
 def test_sampled_softmax_full_size_vs_torch_fp32(K):
@@ -94,10 +117,10 @@ def test_sampled_softmax_full_size_vs_torch_fp32(K):
     rh, re_ = h.float().requires_grad_(True), e.float().requires_grad_(True)
     ref = model_ref.sampled_softmax_loss(rh, re_, ids, ntt, 0.05)
     ref.backward()
-    assert abs(got.item() - ref.item()) < 1e-3 * abs(ref.item())
-    for a, b in ((th.grad, rh.grad), (te.grad, re_.grad)):
-        err = float((a.float() - b).norm() / b.norm())
-        assert err < 1e-2, err
+    assert abs(got.item() - ref.item()) < 1e-4 * abs(ref.item())
+    for a, b in ((th.grad, rh.grad), (te.grad, re_.grad)):   # bf16 grads vs fp32 rounded to bf16
+        err = float((a.float() - b.bfloat16().float()).norm() / b.norm())
+        assert err < 1e-3, err
 
 
 def test_trainer_sampled_softmax_learns():
