@@ -485,21 +485,25 @@ __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __res
 // order like every other row: the reference's CPU embedding_dense_backward is
 // a sequential fp32 add per row in occurrence order, so the
 // only parallelism inside one row is across its columns.  One wave per
-// (row, 64-column slice); each lane owns one column and keeps its running sum
-// in a register.
-//   * loads: 16-byte vectors, 8 (bf16) / 4 (fp32) occurrences per wave
-//     instruction, 8 instructions per tile of 64 / 32 occurrences; kHotStages
-//     tiles in flight.  A tile's row addresses are loaded right after the data
-//     loads of the tile kHotStages earlier, in the same order in the prologue
-//     as in the loop, so every wait on them is a partial vmcnt;
-//   * bf16: the tile is written to LDS as loaded ([occurrence][64 columns],
-//     16-byte writes, rows padded to 192 B) and read back with the gfx950
-//     transposing read ds_read_b64_tr_b16, which hands each lane its column
-//     for 4 consecutive occurrences (192-B rows: the four rows a 16-lane group
-//     reads fall on disjoint banks, conflict-free);
+// (row, column slice: 32 bf16 / 64 fp32 columns); each lane owns one column and
+// keeps its running sum in a register.  A wave is latency-bound (its adds are
+// one dependent chain), so narrow slices put more waves and more loads in
+// flight on each hot row.
+//   * loads: 16-byte vectors, 16 (bf16) / 4 (fp32) occurrences per wave
+//     instruction, 4 / 8 instructions per tile of 64 / 32 occurrences, 32
+//     load instructions (8 / 4 tiles) in flight.  A tile's row addresses are
+//     loaded right after the data loads of the tile that many tiles earlier,
+//     in the same order in the prologue as in the loop, so every wait on them
+//     is a partial vmcnt;
+//   * bf16: the tile is written to LDS as loaded ([occurrence][32 columns],
+//     64-B rows, 16-byte writes) and read back with the gfx950 transposing
+//     read ds_read_b64_tr_b16, which hands each lane its column for 4
+//     consecutive occurrences (the four 64-B rows a 16-lane group reads fall on
+//     disjoint banks; lanes 32-63 repeat lanes 0-31's reads);
 //     fp32: written transposed ([column][occurrence], rows padded to 136 B)
 //     and read 8 bytes at a time.
-constexpr int kHotStages = 4;
+template <typename G>
+__host__ __device__ constexpr int kHotSlice() { return sizeof(G) == 2 ? 32 : 64; }
 
 template <typename G>
 __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ keys,
@@ -511,15 +515,17 @@ __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ key
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(1))) const u32x4 gu32x4;
   constexpr int ES = sizeof(G);
+  constexpr int SLICE = kHotSlice<G>();
   constexpr int EPV = 16 / ES;       // elements per 16-byte vector
-  constexpr int LPO = 64 / EPV;      // lanes per occurrence slice (8 bf16, 16 fp32)
-  constexpr int OPI = 64 / LPO;      // occurrences per load instruction (8, 4)
-  constexpr int IPT = 8;             // load instructions per tile
-  constexpr int TILE = OPI * IPT;    // occurrences per tile (64, 32): 128 B of one column
-  constexpr int ROWB = ES == 2 ? 192 : TILE * ES + 8;  // bf16: [occ][cols] rows; fp32: [col][occs] rows
+  constexpr int LPO = SLICE / EPV;   // lanes per occurrence slice (4 bf16, 16 fp32)
+  constexpr int OPI = 64 / LPO;      // occurrences per load instruction (16, 4)
+  constexpr int TILE = ES == 2 ? 64 : 32;  // occurrences per tile: 128 B of one column
+  constexpr int IPT = TILE / OPI;    // load instructions per tile (4, 8)
+  constexpr int ROWB = ES == 2 ? SLICE * 2 : TILE * ES + 8;  // bf16: [occ][cols] rows; fp32: [col][occs] rows
+  constexpr int IMG_ROWS = ES == 2 ? TILE : SLICE;
   constexpr int EPR = 8 / ES;        // elements per 8-byte LDS read
-  constexpr int S = kHotStages;
-  __shared__ __attribute__((aligned(16))) unsigned char img[64 * ROWB];
+  constexpr int S = 32 / IPT;        // tiles in flight
+  __shared__ __attribute__((aligned(16))) unsigned char img[IMG_ROWS * ROWB];
   const int lane = threadIdx.x;
   const int64_t b = (int64_t)blockIdx.x + 1;  // chunk edge: the row that first crosses it
   const int64_t pb = b * kRedChunk;
@@ -529,8 +535,8 @@ __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ key
   const int u = pos[pb] - 1;
   const int su = seg_start[u], eu = seg_end[u];
   if (su / kRedChunk != b - 1 || eu - su <= 2 * kRedChunk) return;
-  const int c0 = blockIdx.y * 64;
-  const int cols = min(64, dim - c0);
+  const int c0 = blockIdx.y * SLICE;
+  const int cols = min(SLICE, dim - c0);
   const int wv = (lane % LPO) * EPV;                     // this lane's columns [wv, wv + EPV) of the slice
   const int vcol = c0 + wv < dim ? c0 + wv : c0;         // clamped into the row past dim
   const int wocc = lane / LPO;
@@ -574,8 +580,9 @@ __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ key
   }
   float acc = 0.f;
   unsigned char* wbase = ES == 2 ? img + wocc * ROWB + (lane % LPO) * 16 : img + wv * ROWB + wocc * ES;
-  const unsigned char* rbase = ES == 2 ? img + ((lane & 15) >> 2) * ROWB + ((lane >> 4) * 16 + (lane & 3) * 4) * 2
-                                       : img + lane * ROWB;
+  const unsigned char* rbase =
+      ES == 2 ? img + ((lane & 15) >> 2) * ROWB + (((lane >> 4) % (SLICE / 16)) * 16 + (lane & 3) * 4) * 2
+              : img + lane * ROWB;
   for (int t0 = 0; t0 < ntiles; t0 += S) {
 #pragma unroll
     for (int k = 0; k < S; ++k) {
@@ -867,12 +874,13 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
     GRK_LAUNCH_CHECK();
   }
   if (total > 2 * kRedChunk) {  // rows longer than 2 * kRedChunk exist only then
-    const dim3 gh((unsigned)(chunks - 1), (unsigned)((dim + 63) / 64));
+    const dim3 gh((unsigned)(chunks - 1), (unsigned)((dim + kHotSlice<bf16_t>() - 1) / kHotSlice<bf16_t>()));
+    const dim3 gf((unsigned)(chunks - 1), (unsigned)((dim + kHotSlice<float>() - 1) / kHotSlice<float>()));
     if (grad_dtype == GRK_BF16)
       k_seg_hot<bf16_t><<<gh, 64, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel,
                                           dim, dense_out, uniq_rows, row_slot);
     else
-      k_seg_hot<float><<<gh, 64, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel,
+      k_seg_hot<float><<<gf, 64, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel,
                                          dim, dense_out, uniq_rows, row_slot);
     GRK_LAUNCH_CHECK();
   }
