@@ -1,0 +1,106 @@
+"""Tensorised data path (SeqStore) on the CPU: the batch it
+assembles from its columnar cache equals the reference's own MyDataset +
+collate output (tests/golden/dataset.npz, written by the imported reference)
+and this package's MyDataset.collate_tensor_fn on a larger synthetic
+directory -- every field but the negatives, which the device draws
+(tests/test_gpu_seqstore.py)."""
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN_DATA_KW
+
+
+@pytest.fixture(scope='module')
+def golden_dir(tmp_path_factory):
+    from tencent_recommendation_2025_amd.dataset import write_synthetic_tencentgr
+    d = tmp_path_factory.mktemp('tgr')
+    write_synthetic_tencentgr(d, **GOLDEN_DATA_KW)
+    return d
+
+
+def test_store_batch_matches_reference_golden(golden, golden_dir):
+    from tencent_recommendation_2025_amd.seqstore import SeqStore
+    d = golden('dataset.npz')
+    st = SeqStore(golden_dir, maxlen=20)
+    assert st.itemnum == int(d['itemnum']) and st.usernum == int(d['usernum'])
+    b = st.batch(d['uids'])
+    for i, k in enumerate(('seq', 'pos', 'neg', 'token_type', 'next_token_type', 'next_action_type')):
+        if k == 'neg':
+            assert torch.all(b[i] == 0)
+            continue
+        assert b[i].dtype == torch.int32 and np.array_equal(b[i].numpy(), d[k]), k
+    for j, side in ((6, 'seq_feat'), (7, 'pos_feat')):
+        keys = sorted(k.split('.', 1)[1] for k in d.files if k.startswith(side + '.'))
+        assert sorted(b[j]) == keys
+        for k in keys:
+            want = d[f'{side}.{k}']
+            assert b[j][k].dtype == torch.from_numpy(want).dtype and np.array_equal(b[j][k].numpy(), want), (side, k)
+
+
+@pytest.mark.parametrize('maxlen', [20, 7, 60])
+def test_store_batch_matches_collate_tensor_fn(tmp_path, maxlen):
+    """Every user of a 200-user directory (histories 3..90 events: shorter and
+    longer than the window), in shuffled batches."""
+    from tencent_recommendation_2025_amd.dataset import MyDataset, write_synthetic_tencentgr
+    from tencent_recommendation_2025_amd.seqstore import SeqStore
+    write_synthetic_tencentgr(tmp_path, num_users=200, num_items=800, max_events=90, seed=3)
+    ds = MyDataset(tmp_path, SimpleNamespace(maxlen=maxlen, mm_emb_id=['81']))
+    st = SeqStore(tmp_path, maxlen=maxlen)
+    order = np.random.default_rng(0).permutation(len(ds))
+    for s in range(0, len(order), 64):
+        uids = order[s:s + 64]
+        np.random.seed(1)
+        want = ds.collate_tensor_fn([ds[int(u)] for u in uids])
+        got = st.batch(uids)
+        for i in (0, 1, 3, 4, 5):
+            assert torch.equal(got[i], want[i]), i
+        for j in (6, 7):
+            assert list(got[j]) == list(want[j])
+            for k in want[j]:
+                assert got[j][k].dtype == want[j][k].dtype and torch.equal(got[j][k], want[j][k]), (j, k)
+
+
+def test_store_cache_reused_and_history(tmp_path):
+    from tencent_recommendation_2025_amd.dataset import MyDataset, write_synthetic_tencentgr
+    from tencent_recommendation_2025_amd.seqstore import SeqStore
+    write_synthetic_tencentgr(tmp_path, num_users=30, num_items=100, max_events=50, seed=5)
+    st = SeqStore(tmp_path, maxlen=10)
+    stamp = (tmp_path / 'grk_seqstore' / 'tid.npy').stat().st_mtime_ns
+    st2 = SeqStore(tmp_path, maxlen=25)                 # another window over the same cache
+    assert (tmp_path / 'grk_seqstore' / 'tid.npy').stat().st_mtime_ns == stamp and len(st2) == 30
+    ds = MyDataset(tmp_path, SimpleNamespace(maxlen=10, mm_emb_id=['81']))
+    hist = st.history_items(np.arange(30)).numpy()
+    for u in range(30):
+        recs = ds._load_user_data(u)
+        items = {i for _, i, _, f, _, _ in recs if i and f}
+        assert set(hist[u][hist[u] != 0].tolist()) == items
+    # negatives' feature table = fill_missing_feat(item_feat_dict[str(i)])
+    for i in (1, 17, 99):
+        d = ds.item_feat_dict[str(i)]
+        from tencent_recommendation_2025_amd.dataset import ITEM_SPARSE
+        assert [int(st.item_sparse[i, c]) for c in range(len(ITEM_SPARSE))] == [d.get(k, 0) for k in ITEM_SPARSE]
+    assert st.item_ok[0] == 0 and st.item_ok[1:].all()
+
+
+def test_store_batches_dataloader(tmp_path):
+    """StoreBatches through a 2-worker DataLoader: every user once per epoch, each
+    batch equal to SeqStore.batch of its uids; set_epoch reshuffles."""
+    from tencent_recommendation_2025_amd.dataset import write_synthetic_tencentgr
+    from tencent_recommendation_2025_amd.seqstore import SeqStore, StoreBatches
+    write_synthetic_tencentgr(tmp_path, num_users=70, num_items=200, max_events=40, seed=6)
+    st = SeqStore(tmp_path, maxlen=15)
+    sb = StoreBatches(st, 16, seed=1, drop_last=False)
+    dl = torch.utils.data.DataLoader(sb, batch_size=None, num_workers=2)
+    seen = []
+    for uids, b in dl:
+        ref = st.batch(uids.numpy())
+        assert all(torch.equal(x, y) for x, y in zip(b[:6], ref[:6]))
+        assert all(torch.equal(b[6][k], ref[6][k]) for k in ref[6])
+        seen += uids.tolist()
+    assert sorted(seen) == list(range(70))
+    first = sb.perm.copy()
+    sb.set_epoch(1)
+    assert not np.array_equal(first, sb.perm)
