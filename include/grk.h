@@ -236,9 +236,10 @@ typedef struct grk_attn_args {
   uint64_t seed;                   /* dropout stream                              */
   int32_t out_dtype;               /* GRK_F32 / GRK_BF16 for out, dq, dk, dv      */
   int32_t act;                     /* GRK_ACT_*: activation applied to q/k/v      */
-  const int32_t* seq_range;        /* optional [B, 2] from grk_seq_ranges (first
-                                      valid key, contiguous flag); NULL = derived
-                                      from key_valid inside every launch        */
+  const int32_t* seq_range;        /* optional [B, 3] from grk_seq_ranges (first
+                                      valid key, contiguous flag, order); NULL =
+                                      derived from key_valid inside every launch
+                                      (workgroups then in batch order)          */
   const uint64_t* seed_dev;        /* optional: the dropout seed in device memory,
                                       read by the kernels when they run (replaces
                                       `seed`): a step replayed from a HIP graph
@@ -252,9 +253,13 @@ typedef struct grk_attn_args {
  * sequence length and head_dim (the whole-sequence kernels' LDS), else 0. */
 int grk_attention_fidelity_supported(int seq_len, int head_dim);
 
-/* ranges[b] = (first j with key_valid[b, j], 1 if the valid keys are exactly
- * [first, T) else 0); first = T for an all-padding row.  One launch per step
- * serves every attention launch of that step (all layers, fwd and bwd). */
+/* ranges int32 [batch, 3]: ranges[b][0] = first j with key_valid[b, j] (T for
+ * an all-padding row), ranges[b][1] = 1 if the valid keys are exactly
+ * [first, T) else 0, ranges[i][2] = the sequence with the i-th largest
+ * T - first (ties by index): the whole-sequence attention kernels take their
+ * workgroups in that order (longest first; results do not depend on it).  One
+ * call per step serves every attention launch of that step (all layers, fwd
+ * and bwd). */
 int grk_seq_ranges(const uint8_t* key_valid, int batch, int seq_len, int32_t* ranges, void* stream);
 
 /* out [B*T, ldo] (out_dtype); lse fp32 [B, H, T] (softmax: natural-log

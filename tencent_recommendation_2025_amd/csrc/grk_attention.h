@@ -25,7 +25,7 @@ struct AttnParams {
   int in_dt;        // precise == 2: dtype of q/k/v (GRK_F32 / GRK_F16 / GRK_BF16)
   int out_f32;
   int act;  // GRK_ACT_SILU: q/k/v are pre-activations
-  const int* seq_range;  // optional [B, 2] (first valid key, contiguous flag)
+  const int* seq_range;  // optional [B, 3] (first valid key, contiguous flag; longest-first order)
   unsigned long long* drab_fix;  // [H, nb] int64 fixed-point drab accumulator (deterministic)
   // forward
   void* out; int64_t ldo; float* lse;

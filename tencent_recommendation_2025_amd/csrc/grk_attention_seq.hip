@@ -43,7 +43,7 @@ struct SeqInfo {
 
 __device__ __forceinline__ SeqInfo seq_info(const AttnParams& p, int b, int T, int* sh) {
   if (p.seq_range)  // uniform scalar load; clamped so a bad range can never address outside [0, T)
-    return {min(max(p.seq_range[2 * b], 0), T), p.seq_range[2 * b + 1] != 0};
+    return {min(max(p.seq_range[3 * b], 0), T), p.seq_range[3 * b + 1] != 0};
   const uint8_t* kv = p.key_valid;
   if (!kv) return {0, 1};
   int first = T, cnt = 0;
@@ -72,6 +72,15 @@ __device__ __forceinline__ SeqInfo seq_info(const AttnParams& p, int b, int T, i
   return {f, c == T - f};
 }
 
+// Sequence b of workgroup row bi: with precomputed ranges the workgroups take
+// the sequences longest first (column 2: k_seq_order), so the long ones never
+// start last and run alone at the end of the grid (lengths are ragged).
+__device__ __forceinline__ int seq_of_block(const AttnParams& p, int bi) {
+  if (!p.seq_range) return bi;
+  const int b = p.seq_range[3 * bi + 2];
+  return min(max(b, 0), p.B - 1);
+}
+
 // grk_seq_ranges: one wave per sequence.
 __global__ void __launch_bounds__(256) k_seq_ranges(const uint8_t* __restrict__ kv, int B, int T,
                                                     int* __restrict__ out) {
@@ -89,8 +98,22 @@ __global__ void __launch_bounds__(256) k_seq_ranges(const uint8_t* __restrict__ 
     cnt += __shfl_xor(cnt, off);
   }
   if (lane == 0) {
-    out[2 * b] = first;
-    out[2 * b + 1] = cnt == T - first;
+    out[3 * b] = first;
+    out[3 * b + 1] = cnt == T - first;
+  }
+}
+
+// out[3 i + 2] = the sequence with the i-th most keys from its first valid one
+// (T - first descending, ties by index): a rank count, one workgroup.
+__global__ void __launch_bounds__(1024) k_seq_order(int B, int T, int* __restrict__ out) {
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const int lb = T - out[3 * b];
+    int rank = 0;
+    for (int c = 0; c < B; ++c) {
+      const int lc = T - out[3 * c];
+      rank += (lc > lb) | ((lc == lb) & (c < b));
+    }
+    out[3 * rank + 2] = b;
   }
 }
 
@@ -319,7 +342,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
   const int T = p.T, nq = (T + 31) / 32, Tp = nq * 32;
   SeqLds<HD, PREC == 2 ? 4 : 2> L(smem, Tp);
   GRK_STAMP(0);
-  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int b = seq_of_block(p, blockIdx.x / p.H), h = blockIdx.x % p.H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const SeqInfo si = seq_info(p, b, T, L.sh);
   const int start = si.start, first = start / 32, kbeg = first * 32;
@@ -470,7 +493,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
   SeqLds<HD, PREC == 2 ? 4 : 2> L(smem, Tp, kDqBinArrays);
   // drab by distance d in [-kRabPad, Tp): bins[kRabPad + d], int64 fixed point
   unsigned long long* bins = reinterpret_cast<unsigned long long*>(L.f1);
-  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int b = seq_of_block(p, blockIdx.x / p.H), h = blockIdx.x % p.H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const SeqInfo si = seq_info(p, b, T, L.sh);
   const int start = si.start, first = start / 32, kbeg = first * 32;
@@ -633,7 +656,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
   SeqLds<HD, PREC == 2 ? 4 : 2> L(smem, Tp);
   float* lses = L.f0;  // softmax: per-query log2-domain lse, delta
   float* dlts = L.f1;
-  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int b = seq_of_block(p, blockIdx.x / p.H), h = blockIdx.x % p.H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const SeqInfo si = seq_info(p, b, T, L.sh);
   const int start = si.start, first = start / 32, kbeg = first * 32;
@@ -889,6 +912,8 @@ extern "C" int grk_seq_ranges(const uint8_t* key_valid, int batch, int seq_len, 
   if (batch == 0) return GRK_OK;
   GRK_CHECK_ARG(key_valid && ranges, "key_valid and ranges required");
   k_seq_ranges<<<(batch + 3) / 4, 256, 0, (hipStream_t)stream>>>(key_valid, batch, seq_len, ranges);
+  GRK_LAUNCH_CHECK();
+  k_seq_order<<<1, 1024, 0, (hipStream_t)stream>>>(batch, seq_len, ranges);
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }

@@ -286,7 +286,7 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
 
     act="silu": q/k/v are pre-activations; SiLU is applied on load and the
     backward's dq/dk/dv are gradients w.r.t. the pre-activations.
-    seq_range: optional int32 [B, 2] from seq_ranges(key_valid) (computed once per step).
+    seq_range: optional int32 [B, 3] from seq_ranges(key_valid) (computed once per step).
     seed: an int, or a device int64 [1] tensor the kernels read when they run
     (drawn on the device each step, so a graph-replayed step gets a fresh mask).
     precise: 0 / False (P and dS rounded to bf16), 1 / True (P, dS as bf16 hi + lo),
@@ -306,9 +306,9 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
         if key_valid.dtype != torch.uint8 or key_valid.shape != (B, T) or not key_valid.is_contiguous():
             raise L.GrkError('key_valid must be a contiguous uint8 [B, T] tensor')
     nb = 0
-    if seq_range is not None and (seq_range.dtype != torch.int32 or seq_range.shape != (B, 2)
+    if seq_range is not None and (seq_range.dtype != torch.int32 or seq_range.shape != (B, 3)
                                   or not seq_range.is_contiguous()):
-        raise L.GrkError('seq_range must be a contiguous int32 [B, 2] tensor (kernels.seq_ranges)')
+        raise L.GrkError('seq_range must be a contiguous int32 [B, 3] tensor (kernels.seq_ranges)')
     if kind == L.ATTN_HSTU:
         if rab is None or rab.dtype != torch.float32 or rab.dim() != 2 or rab.shape[0] != H or not rab.is_contiguous():
             raise L.GrkError('hstu needs a contiguous fp32 rab [H, num_buckets]')
@@ -331,12 +331,13 @@ def fidelity_supported(seq_len, head_dim):
 
 
 def seq_ranges(key_valid):
-    """int32 [B, 2]: (first valid key, contiguous flag) per sequence (grk_seq_ranges)."""
+    """int32 [B, 3]: (first valid key, contiguous flag) per sequence and, in column 2,
+    the sequences longest first (grk_seq_ranges)."""
     _require_cuda(key_valid)
     if key_valid.dtype != torch.uint8 or key_valid.dim() != 2 or not key_valid.is_contiguous():
         raise L.GrkError('key_valid must be a contiguous uint8 [B, T] tensor')
     B, T = key_valid.shape
-    out = torch.empty(B, 2, dtype=torch.int32, device=key_valid.device)
+    out = torch.empty(B, 3, dtype=torch.int32, device=key_valid.device)
     rc = L.lib().grk_seq_ranges(key_valid.data_ptr() if B else None, B, T, out.data_ptr() if B else None,
                                 L.stream_ptr(key_valid.device))
     L.check(rc, 'grk_seq_ranges')

@@ -111,13 +111,13 @@ torch.library.register_autocast('grk::feature_lookup', 'cuda', torch.float32)
 # ------------------------------------------------------------- attention ----
 @torch.library.custom_op('grk::seq_ranges', mutates_args=(), device_types='cuda')
 def seq_ranges(key_valid: Tensor) -> Tensor:
-    """int32 [B, 2]: (first valid key, contiguous flag) per sequence (grk_seq_ranges)."""
+    """int32 [B, 3]: (first valid key, contiguous flag, longest-first order) (grk_seq_ranges)."""
     return K.seq_ranges(key_valid)
 
 
 @seq_ranges.register_fake
 def _(key_valid):
-    return key_valid.new_empty(key_valid.shape[0], 2, dtype=torch.int32)
+    return key_valid.new_empty(key_valid.shape[0], 3, dtype=torch.int32)
 
 
 def _attn_plan(dtype, T, hd, precise):

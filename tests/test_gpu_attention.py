@@ -246,7 +246,8 @@ def test_seq_ranges(K):
     valid[2, 5:20] = 1         # hole at the end: not contiguous to T
     valid[3, [3, 9]] = 1       # scattered
     got = K.seq_ranges(torch.from_numpy(valid).to(DEV)).cpu().numpy()  # row 4: no valid key
-    np.testing.assert_array_equal(got, [[10, 1], [0, 1], [5, 0], [3, 0], [40, 1]])
+    np.testing.assert_array_equal(got[:, :2], [[10, 1], [0, 1], [5, 0], [3, 0], [40, 1]])
+    np.testing.assert_array_equal(got[:, 2], [1, 3, 2, 0, 4])   # T - first: 30, 40, 35, 37, 0
 
 
 @pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
