@@ -196,8 +196,16 @@ class BaselineModel(torch.nn.Module):
         self.block = getattr(args, 'block', 'softmax')
         d = args.hidden_units
         self.hidden_units = d
-        self.item_emb = torch.nn.Embedding(item_num + 1, d, padding_idx=0)
-        self.user_emb = torch.nn.Embedding(user_num + 1, d, padding_idx=0)
+        if getattr(args, 'shard_tables', False):
+            # row-sharded item / user tables (BASELINE config 3, 50M rows): the full
+            # tables are never built on any rank -- ShardedFusedAdamW creates each
+            # rank's rows directly (table_init_rows), materialize_tables_ the whole
+            # table when one process trains it
+            self.item_emb = _placeholder_table(item_num + 1, d)
+            self.user_emb = _placeholder_table(user_num + 1, d)
+        else:
+            self.item_emb = torch.nn.Embedding(item_num + 1, d, padding_idx=0)
+            self.user_emb = torch.nn.Embedding(user_num + 1, d, padding_idx=0)
         self.pos_emb = torch.nn.Embedding(2 * args.maxlen + 1, d, padding_idx=0)
         self.emb_dropout = torch.nn.Dropout(p=args.dropout_rate)
         self.sparse_emb = torch.nn.ModuleDict()
@@ -639,6 +647,64 @@ def _stack_padded(a, b):
     return torch.cat([a, b], 0)
 
 
+def _placeholder_table(rows, dim):
+    """nn.Embedding(rows, dim, padding_idx=0) with no rows allocated (weight [0, dim])."""
+    emb = torch.nn.Embedding(1, dim, padding_idx=0)
+    emb.num_embeddings = rows
+    emb.weight = torch.nn.Parameter(torch.empty(0, dim), requires_grad=False)
+    return emb
+
+
+def table_init_rows(rows, dim, seed, std, dtype=torch.float32):
+    """Rows `rows` (int64, any device) of a [R, dim] table initialised
+    N(0, std^2) from a counter-based hash of (seed, row, column): the value of
+    a row does not depend on which rank builds it or which other rows are
+    built with it, so row shards (rows rank::world) built separately equal the
+    slices of the whole table.  Row 0 (padding) is zero.  The reference draws
+    the same distribution with torch's generator (xavier_normal_,
+    model/BaseLine/main.py:95-111); a sharded run cannot reproduce that stream."""
+    M32 = 0xFFFFFFFF
+
+    def mix(x):  # lowbias32 on int64 lanes holding 32-bit values
+        x = (x ^ (x >> 16)) & M32
+        x = (x * 0x7FEB352D) & M32
+        x = (x ^ (x >> 15)) & M32
+        x = (x * 0x846CA68B) & M32
+        return (x ^ (x >> 16)) & M32
+
+    rows = rows.to(torch.int64).reshape(-1, 1)
+    col = torch.arange(dim, device=rows.device, dtype=torch.int64).reshape(1, -1)
+    base = mix(mix(rows & M32) ^ mix((rows >> 32) ^ (int(seed) & M32)))
+    u1 = (mix(base ^ mix(2 * col)).double() + 1.0) / 4294967296.0           # (0, 1]
+    u2 = mix(base ^ mix(2 * col + 1)).double() / 4294967296.0              # [0, 1)
+    z = torch.sqrt(-2.0 * torch.log(u1)) * torch.cos(6.283185307179586 * u2) * std
+    z = torch.where(rows == 0, torch.zeros_like(z), z)
+    return z.to(dtype)
+
+
+def table_init_std(num_rows, dim):
+    """xavier_normal_'s std for a [num_rows, dim] table (model/BaseLine/main.py:95-111)."""
+    return (2.0 / float(num_rows + dim)) ** 0.5
+
+
+def materialize_tables_(model, seed=0, device=None, dtype=torch.float32, chunk=1 << 18):
+    """Replace placeholder item / user tables (args.shard_tables) by whole tables
+    holding table_init_rows -- what every shard of a row-sharded run holds, in one
+    process (the unsharded twin of a sharded run)."""
+    dev = torch.device(device) if device is not None else model.pos_emb.weight.device
+    for name in ('item_emb', 'user_emb'):
+        emb = getattr(model, name)
+        if emb.weight.shape[0] != 0:
+            continue
+        R, D = emb.num_embeddings, emb.embedding_dim
+        w = torch.empty(R, D, dtype=dtype, device=dev)
+        for s in range(0, R, chunk):
+            w[s:s + chunk] = table_init_rows(torch.arange(s, min(R, s + chunk), device=dev), D,
+                                             seed + (1 if name == 'user_emb' else 0), table_init_std(R, D), dtype)
+        emb.weight = torch.nn.Parameter(w)
+    return model
+
+
 def init_reference_(model, seed=None, live_norms=False):
     """Parameter init of the training script (model/BaseLine/main.py:95-111):
     xavier_normal_ for dim >= 2, zeros for 1-D, padding rows of every table zeroed.
@@ -657,7 +723,8 @@ def init_reference_(model, seed=None, live_norms=False):
             elif p.dim() == 1:
                 p.zero_()
         for t in model.table_modules().values():
-            t.weight[0].zero_()
+            if t.weight.shape[0]:      # placeholder (row-sharded) tables hold no rows here
+                t.weight[0].zero_()
         if live_norms:
             for mm in model.modules():
                 if isinstance(mm, torch.nn.LayerNorm):

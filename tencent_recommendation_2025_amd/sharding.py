@@ -296,7 +296,8 @@ class ShardedFusedAdamW(FusedAdamW):
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
                  table_dtype=torch.bfloat16, pg=None, gather_fn=kernel_gather, reduce_fn=kernel_reduce,
-                 dense_reduce_fn=kernel_dense_reduce, defer_period=16, bucket_bytes=32 << 20, lookahead=True):
+                 dense_reduce_fn=kernel_dense_reduce, defer_period=16, bucket_bytes=32 << 20, lookahead=True,
+                 init_seed=0):
         self.pg = pg
         self.world = dist.get_world_size(pg)
         self.rank = dist.get_rank(pg)
@@ -307,8 +308,22 @@ class ShardedFusedAdamW(FusedAdamW):
         sharded_refs = {}
         for name in self.SHARDED:
             emb = tables[name]
-            full = emb.weight.detach()
-            shard = full[self.rank::self.world].to(dtype=table_dtype).contiguous()
+            if emb.weight.shape[0] == 0:
+                # placeholder (model args.shard_tables): build only this rank's rows
+                # -- global rows rank::world, table_init_rows of the whole table's
+                # init (the 50M-row tables of config 3 never exist whole anywhere)
+                from .model import table_init_rows, table_init_std
+                R, D = emb.num_embeddings, emb.embedding_dim
+                n = len(range(self.rank, R, self.world))
+                shard = torch.empty(n, D, dtype=table_dtype, device=dev)
+                ch = 1 << 18
+                for s in range(0, n, ch):
+                    rows = torch.arange(s, min(n, s + ch), device=dev) * self.world + self.rank
+                    shard[s:s + ch] = table_init_rows(rows, D, init_seed + (1 if name == 'user_emb' else 0),
+                                                      table_init_std(R, D), table_dtype)
+            else:
+                full = emb.weight.detach()
+                shard = full[self.rank::self.world].to(dtype=table_dtype).contiguous()
             grp = TableGroup(f'{name}@{self.rank}', [(name, _Holder(shard))], table_dtype, dev)
             grp.global_rows = emb.num_embeddings
             self.shards[name] = (grp, ShardExchange(name, grp.flat, emb.embedding_dim, pg, gather_fn))

@@ -96,3 +96,41 @@ def test_sharded_graph_and_lookahead_equal_eager(pg):
         assert torch.equal(runs[0][1][k], runs[1][1][k]), k
     for k in runs[0][2]:
         assert torch.equal(runs[0][2][k], runs[1][2][k]), k
+
+
+def test_shards_built_directly_equal_materialized_table(pg):
+    """args.shard_tables: the sharded optimizer builds only its rows (never the
+    whole table, config 3); it trains like FusedAdamW on the materialized twin
+    (materialize_tables_, the same per-row init) -- G = 1."""
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel, init_reference_, materialize_tables_
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.sharding import ShardedFusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    cfg = S.SyntheticConfig(batch_size=8, maxlen=40, num_items=3000, num_users=400, min_len=8)
+    stats, types = S.feature_schema(cfg)
+    models = []
+    for _ in range(2):
+        args = S.make_args(hidden_units=64, maxlen=40, num_blocks=1, num_heads=2)
+        args.shard_tables = True
+        torch.manual_seed(0)
+        m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, args).to(DEV)
+        init_reference_(m, seed=0, live_norms=True)
+        models.append(m)
+    m1, m2 = models
+    materialize_tables_(m1, seed=5)
+    assert m2.item_emb.weight.numel() == 0
+    t1 = Trainer(m1, FusedAdamW(m1, lr=2e-3, table_dtype=torch.float32, defer_period=2), loss='bce', amp_dtype=None)
+    opt2 = ShardedFusedAdamW(m2, lr=2e-3, table_dtype=torch.float32, defer_period=2, init_seed=5)
+    for k in ('item_emb', 'user_emb'):
+        assert torch.equal(opt2.shard_table(k), getattr(m1, k).weight.detach()), k
+    t2 = Trainer(m2, opt2, loss='bce', amp_dtype=None)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    for _ in range(4):
+        b = S.make_batch(cfg, g, DEV)
+        l1, l2 = t1.step(b), t2.step(b)
+        assert abs(l1.item() - l2.item()) < 1e-4 * max(1.0, abs(l1.item()))
+    s1 = m1.state_dict()
+    for k in ('item_emb', 'user_emb'):
+        torch.testing.assert_close(opt2.shard_table(k).float(), s1[f'{k}.weight'].float(), rtol=1e-3, atol=2e-5,
+                                   msg=k)

@@ -86,3 +86,39 @@ def test_key_valid_from_mask_rejects_other_masks():
     bad[0, 6, 3] = False
     with pytest.raises(NotImplementedError):
         key_valid_from_mask(bad, 1, T)
+
+
+def test_table_init_rows_shards_equal_whole_table():
+    """Config-3 tables are built shard by shard (rows rank::world, ADVICE r1):
+    every shard equals the slice of the whole table, at any world size."""
+    import torch
+    from tencent_recommendation_2025_amd.model import table_init_rows, table_init_std
+    R, D = 1001, 40
+    std = table_init_std(R, D)
+    whole = table_init_rows(torch.arange(R), D, 7, std)
+    assert torch.all(whole[0] == 0)
+    for world in (2, 3, 8):
+        for rank in range(world):
+            rows = torch.arange(rank, R, world)
+            assert torch.equal(table_init_rows(rows, D, 7, std), whole[rank::world])
+    z = whole[1:] / std
+    assert abs(float(z.mean())) < 0.01 and abs(float(z.std()) - 1.0) < 0.01
+    assert not torch.equal(table_init_rows(torch.arange(R), D, 8, std), whole)
+
+
+def test_placeholder_tables_and_materialize():
+    import torch
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import (BaselineModel, init_reference_, materialize_tables_,
+                                                       table_init_rows, table_init_std)
+    cfg = S.SyntheticConfig(batch_size=2, maxlen=10, num_items=500, num_users=60)
+    stats, types = S.feature_schema(cfg)
+    args = S.make_args(hidden_units=32, maxlen=10, num_blocks=1, num_heads=2, device='cpu')
+    args.shard_tables = True
+    m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, args)
+    assert m.item_emb.weight.shape == (0, 32) and m.item_emb.num_embeddings == 501
+    init_reference_(m, seed=0)
+    materialize_tables_(m, seed=3)
+    assert m.item_emb.weight.shape == (501, 32) and m.user_emb.weight.shape == (61, 32)
+    assert torch.equal(m.item_emb.weight.detach(), table_init_rows(torch.arange(501), 32, 3, table_init_std(501, 32)))
+    assert torch.equal(m.user_emb.weight.detach(), table_init_rows(torch.arange(61), 32, 4, table_init_std(61, 32)))
