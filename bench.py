@@ -62,6 +62,8 @@ def parse():
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='gloo: rehearse N ranks on fewer GPUs (collectives staged via host)')
     ap.add_argument('--sharded', type=int, default=None, help='force the row-sharded optimizer (default: N > 1)')
+    ap.add_argument('--shard-tables', type=int, default=None,
+                    help='build only each rank\'s table rows (default: sharded and >= 10M items, BASELINE config 3)')
     ap.add_argument('--graph', type=int, default=1,
                     help='capture the training step in a HIP graph and replay it (row-sharded: forward + backward)')
     return ap.parse_args()
@@ -386,6 +388,8 @@ def main():
     stats, types = S.feature_schema(cfg)
     margs = S.make_args(hidden_units=a.hidden, maxlen=a.maxlen, num_blocks=a.blocks, num_heads=a.heads,
                         block=a.block, dropout_rate=a.dropout)
+    shard_tables = sharded and (a.shard_tables if a.shard_tables is not None else a.items >= 10_000_000)
+    margs.shard_tables = bool(shard_tables)
     torch.manual_seed(0)
     model = BaselineModel(a.users, a.items, stats, types, margs).to(dev)
     model.train()
@@ -451,12 +455,12 @@ def main():
             'value': round(value, 2), 'unit': 'seq/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
             'ms_per_step': round(elapsed / a.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'bf16', 'data': 'synthetic (device-resident TencentGR-shaped batches)',
-            'config': {'workload': f'BASELINE config 2: {a.block.upper()} d={a.hidden} L={a.maxlen} '
+            'config': {'workload': f'BASELINE config {3 if shard_tables else 2}: {a.block.upper()} d={a.hidden} L={a.maxlen} '
                                    f'({a.blocks} blocks x {a.heads} heads), {a.items}-item bf16 table, '
                                    f'{a.users} users, loss={a.loss}, table AdamW={a.table_mode}, '
                                    f'dropout={a.dropout}',
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch, 'seq_len': a.maxlen + 1,
-                       'parallelism': f'dp{world}' + ('+rowshard' if sharded else ''),
+                       'parallelism': f'dp{world}' + ('+rowshard' if sharded else '') + ('(shard-built tables)' if shard_tables else ''),
                        'step_launch': 'hip-graph replay' if trainer.graph else 'eager',
                        'batch_pool': len(pool)},
             'final_loss': round(final_loss, 5),
