@@ -218,7 +218,7 @@ enum { GRK_ACT_NONE = 0, GRK_ACT_SILU = 1 };
 
 typedef struct grk_attn_args {
   int32_t kind;                    /* GRK_ATTN_*                                  */
-  int32_t batch, heads, seq_len, head_dim;   /* head_dim in {16, 32, 64, 128}  */
+  int32_t batch, heads, seq_len, head_dim;   /* head_dim in {16, 32, 64, 128, 256, 512} */
   int32_t num_buckets;             /* hstu: rab columns                           */
   const void* q; const void* k; const void* v;   /* bf16                        */
   int64_t ldq, ldk, ldv;           /* row strides (elements), multiples of 8      */

@@ -183,9 +183,29 @@ __device__ __forceinline__ unsigned long long to_fix(float v) {
   return (unsigned long long)(long long)d;
 }
 
+// Launch with `lds` bytes of dynamic LDS; above 64 KiB the kernel's limit is
+// raised first (once per kernel and size; gfx950 allows up to 160 KiB).
+inline void launch_lds(void (*kernel)(AttnParams), dim3 grid, int threads, size_t lds, hipStream_t s,
+                       const AttnParams& p) {
+  if (lds > 64 * 1024) {
+    static thread_local const void* last_k = nullptr;
+    static thread_local size_t last_b = 0;
+    if (last_k != (const void*)kernel || last_b < lds) {
+      (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      last_k = (const void*)kernel;
+      last_b = lds;
+    }
+  }
+  kernel<<<grid, threads, lds, s>>>(p);
+}
+
 // Whole-sequence kernels (grk_attention_seq.hip): one workgroup per
 // (batch, head) with the sequence's K/V (or Q/dO) resident in LDS.
 // Returns true and launches when the shape fits; false = use the chunked path.
 bool attn_seq_launch(const AttnParams& p, int hd, int which, hipStream_t s);
+
+// Wide-head kernels (grk_attention_wide.hip): head_dim 256 / 512, the head's
+// columns split over a workgroup's waves (which: 0 forward, 2 dQ, 3 dK/dV).
+int attn_wide_launch(const AttnParams& p, int hd, int which, hipStream_t s);
 
 }  // namespace grk

@@ -424,7 +424,7 @@ static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
     GRK_LAUNCH_CHECK();
     return GRK_OK;
   }
-  if (p.precise == 2 && which != 1) {
+  if (p.precise == 2 && which != 1 && hd <= 128) {
     set_error("fp32-fidelity attention (precise = 2) runs in the whole-sequence kernels only: T = %d x head_dim %d "
               "does not fit their LDS", p.T, hd);
     return GRK_EUNSUPPORTED;
@@ -434,8 +434,18 @@ static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
     case 32: return launch_hd<32>(p, which, s);
     case 64: return launch_hd<64>(p, which, s);
     case 128: return launch_hd<128>(p, which, s);
+    case 256:
+    case 512:
+      if (which != 1) return attn_wide_launch(p, hd, which, s);
+      {
+        const int64_t waves = (int64_t)p.B * p.T * p.H;
+        if (hd == 256) k_attn_delta<256><<<(unsigned)((waves + 3) / 4), 256, 0, s>>>(p);
+        else k_attn_delta<512><<<(unsigned)((waves + 3) / 4), 256, 0, s>>>(p);
+        GRK_LAUNCH_CHECK();
+        return GRK_OK;
+      }
   }
-  set_error("head_dim %d unsupported (16, 32, 64, 128)", hd);
+  set_error("head_dim %d unsupported (16, 32, 64, 128, 256, 512)", hd);
   return GRK_EUNSUPPORTED;
 }
 
@@ -443,8 +453,9 @@ static int fill_params(const grk_attn_args* a, AttnParams* p) {
   GRK_CHECK_ARG(a != nullptr, "args is NULL");
   GRK_CHECK_ARG(a->kind == GRK_ATTN_SOFTMAX || a->kind == GRK_ATTN_HSTU, "bad kind");
   GRK_CHECK_ARG(a->batch > 0 && a->heads > 0 && a->seq_len > 0, "batch/heads/seq_len must be > 0");
-  GRK_CHECK_ARG(a->head_dim == 16 || a->head_dim == 32 || a->head_dim == 64 || a->head_dim == 128,
-                "head_dim %d unsupported (16, 32, 64, 128)", a->head_dim);
+  GRK_CHECK_ARG(a->head_dim == 16 || a->head_dim == 32 || a->head_dim == 64 || a->head_dim == 128 ||
+                    a->head_dim == 256 || a->head_dim == 512,
+                "head_dim %d unsupported (16, 32, 64, 128, 256, 512)", a->head_dim);
   GRK_CHECK_ARG(a->q && a->k && a->v, "q/k/v required");
   const int64_t need = (int64_t)a->heads * a->head_dim;
   GRK_CHECK_ARG(a->ldq >= need && a->ldk >= need && a->ldv >= need, "row strides smaller than heads*head_dim");

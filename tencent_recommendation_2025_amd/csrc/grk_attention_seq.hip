@@ -828,22 +828,6 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
     }
 }
 
-// Launch with `lds` bytes of dynamic LDS; above 64 KiB the kernel's limit is
-// raised first (once per kernel and size; gfx950 allows up to 160 KiB).
-static void launch_lds(void (*kernel)(AttnParams), dim3 grid, int threads, size_t lds, hipStream_t s,
-                       const AttnParams& p) {
-  if (lds > 64 * 1024) {
-    static thread_local const void* last_k = nullptr;
-    static thread_local size_t last_b = 0;
-    if (last_k != (const void*)kernel || last_b < lds) {
-      (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      last_k = (const void*)kernel;
-      last_b = lds;
-    }
-  }
-  kernel<<<grid, threads, lds, s>>>(p);
-}
-
 template <int HD>
 static bool seq_launch_hd(const AttnParams& p, int which, hipStream_t s) {
   const int Tp = (p.T + 31) / 32 * 32;

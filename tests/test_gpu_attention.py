@@ -383,3 +383,66 @@ def test_fidelity_mode_matches_fp64_oracle(K, kind, hd, T, lens, in_dtype):
 def test_fidelity_supported_shapes(K):
     assert K.fidelity_supported(201, 64) and K.fidelity_supported(102, 128)
     assert not K.fidelity_supported(201, 128) and not K.fidelity_supported(1025, 64)
+
+
+# ---------------------------------------------------------------- wide heads --
+# head_dim 256 / 512 (grk_attention_wide.hip): one head over the whole hidden
+# width, as the O1 baseline's num_heads=1 (model/BaseLineO1/main.py:45).
+WIDE = [(256, 2), (512, 1)]
+
+
+@pytest.mark.parametrize('hd,H', WIDE)
+@pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
+def test_wide_head_parity(K, kind, hd, H):
+    res, want, _ = run(K, kind, B=3, T=201, H=H, hd=hd, lens=[201, 120, 7], precise=True, seed=hd,
+                       act='silu' if kind == 1 else None)
+    for key in ('out', 'dq', 'dk', 'dv') + (('drab',) if kind == 1 else ()):
+        err = nrel(res[key], want[key])
+        assert err < TOL_PRECISE, f'{key}: normwise rel err {err:.2e}'
+    if kind == 0:
+        live = np.isfinite(want['lse'])
+        np.testing.assert_allclose(res['lse'][live], want['lse'][live], rtol=1e-5, atol=1e-4)
+        assert np.all(np.isneginf(res['lse'][~live]))
+
+
+@pytest.mark.parametrize('hd,H', WIDE)
+def test_wide_head_dropout_holes_bf16(K, hd, H):
+    """Dropout (the drop_keep stream of the narrow kernels), non-contiguous key
+    validity and bf16 outputs (compared with the oracle rounded to bf16)."""
+    res, want, _ = run(K, 0, B=2, T=97, H=H, hd=hd, lens=[97, 40], precise=True, dropout=0.2, holes=True,
+                       out_dtype=torch.bfloat16)
+    for key in ('out', 'dq', 'dk', 'dv'):
+        err = nrel(res[key], to_bf16_f32(np.asarray(want[key], np.float32)))
+        assert err < TOL_PRECISE, f'{key}: normwise rel err {err:.2e}'
+
+
+def test_wide_head_long_sequence_and_repeatable(K):
+    """T=600: many 32-row tiles per workgroup; clipped rab buckets; bitwise repeatable."""
+    a, want, _ = run(K, 1, B=2, T=600, H=1, hd=256, lens=[600, 333], precise=True, nb=257)
+    for key in ('out', 'dq', 'dk', 'dv', 'drab'):
+        err = nrel(a[key], want[key])
+        assert err < TOL_PRECISE, f'{key}: normwise rel err {err:.2e}'
+    b, _, _ = run(K, 1, B=2, T=600, H=1, hd=256, lens=[600, 333], precise=True, nb=257, oracle=False)
+    for key in ('out', 'dq', 'dk', 'dv', 'drab'):
+        assert np.array_equal(a[key], b[key]), key
+
+
+def test_wide_head_masked_rows_and_fast_mode(K):
+    res, want, valid = run(K, 0, B=2, T=70, H=1, hd=512, lens=[70, 5], precise=False)
+    pad_rows = np.where(valid.reshape(-1) == 0)[0]
+    for key in ('out', 'dq'):
+        assert np.all(res[key][pad_rows] == 0)
+    for key in ('out', 'dq', 'dk', 'dv'):
+        assert np.all(np.isfinite(res[key]))
+        assert nrel(res[key], want[key]) < TOL_FAST, key
+
+
+def test_wide_head_rejects_fidelity_mode(K):
+    from tencent_recommendation_2025_amd import _lib as L
+    assert not K.fidelity_supported(101, 512)
+    x = torch.zeros(64, 3 * 512, device=DEV)
+    kv = torch.ones(2, 32, dtype=torch.uint8, device=DEV)
+    args = K.attn_args(L.ATTN_SOFTMAX, x[:, :512], x[:, 512:1024], x[:, 1024:], 2, 32, 1, 512, key_valid=kv,
+                       precise=2, out_dtype=torch.float32)
+    with pytest.raises(RuntimeError, match='head_dim 512'):
+        K.attention_fwd(args, torch.empty(64, 512, device=DEV), torch.empty(2, 1, 32, device=DEV))

@@ -51,9 +51,11 @@ def build(golden, tag, block='softmax', **over):
     variant = tag.split('_')[0]
     g = golden(f'model_{tag}.npz')
     d, batch, stats = golden_batch(golden)
-    args = SimpleNamespace(hidden_units=int(g['hidden_units']), maxlen=int(g['maxlen']),
-                           num_blocks=int(g['num_blocks']), num_heads=int(g['num_heads']), dropout_rate=0.0,
-                           norm_first=False, device=DEV, variant=variant, block=block, **over)
+    kw = dict(hidden_units=int(g['hidden_units']), maxlen=int(g['maxlen']), num_blocks=int(g['num_blocks']),
+              num_heads=int(g['num_heads']), dropout_rate=0.0, norm_first=False, device=DEV, variant=variant,
+              block=block)
+    kw.update(over)
+    args = SimpleNamespace(**kw)
     m = BaselineModel(int(d['usernum']), int(d['itemnum']), stats, feat_types(), args).to(DEV)
     return m, g, batch, args, d, stats
 
@@ -162,6 +164,39 @@ def test_hstu_model_matches_oracle(golden):
         if rp.grad is None or float(rp.grad.norm()) == 0:
             continue
         assert nrel(p.grad.cpu(), rp.grad) < 2e-2, name
+
+
+@pytest.mark.parametrize('hidden', [256, 512])
+def test_o1_single_head_wide_matches_oracle(golden, hidden):
+    """O1 with one head over the whole width (BaseLineO1/main.py:45
+    num_heads=1): head_dim = hidden_units = 256 / 512 runs the wide-head
+    attention kernels.  The fp32 drop-in model against the fp32 CPU restatement
+    (oracle/model_ref.py): these widths have no fp32-fidelity kernels, so Q/K/V
+    enter as bf16 (P / dS as hi + lo) -- tolerances of the HSTU model test."""
+    torch.manual_seed(0)
+    m, g, batch, args, d, stats = build(golden, 'o1', hidden_units=hidden, num_heads=1)
+    ref = model_ref.RefBaselineModel(int(d['usernum']), int(d['itemnum']), stats, feat_types(), args, variant='o1')
+    model_ref.init_params(ref, seed=5)
+    with torch.no_grad():   # live LayerNorm gains (the reference init zeroes them)
+        for name, p in ref.named_parameters():
+            if 'layernorm' in name.lower() and name.endswith('weight'):
+                p.uniform_(0.5, 1.5)
+    m.load_state_dict(ref.state_dict())
+    cpu_batch = [x.cpu() if torch.is_tensor(x) else {k: v.cpu() for k, v in x.items()} for x in batch]
+    seq, pos, neg, tt, ntt, nat, sf, pf, nf = cpu_batch
+    rpl, rnl = ref(seq, pos, neg, tt, ntt, sf, pf, nf)
+    model_ref.bce_loss(rpl, rnl, ntt).backward()
+    pl, nl = m(*batch)
+    assert max(nrel(pl.detach().cpu(), rpl.detach()), nrel(nl.detach().cpu(), rnl.detach())) < 5e-3
+    ref_loss(pl, nl, batch[4], m, 0.0).backward()
+    checked = 0
+    for (name, p), (_, rp) in zip(m.named_parameters(), ref.named_parameters()):
+        # the key bias's gradient is analytically zero (softmax is shift-invariant): rounding noise only
+        if rp.grad is None or float(rp.grad.norm()) == 0 or name.endswith('k_linear.bias'):
+            continue
+        assert nrel(p.grad.cpu(), rp.grad) < 2e-2, name
+        checked += 1
+    assert checked > 20
 
 
 def test_fused_trainer_matches_dropin(golden):
