@@ -6,13 +6,17 @@
 // head row per lane in registers, which stops at head_dim 128.  Here a
 // workgroup owns 32 rows -- queries (forward, dQ) or keys (dK/dV) of one
 // (batch, head) -- and its HD/64 waves split the head's columns into 64-wide
-// slices (4 waves at 256, 8 at 512): every wave forms the partial 32x32
-// score (and dP) product of its slice, the partials are exchanged through LDS and summed in wave order
-// (every wave then holds bitwise the same S / dP, so the softmax state and
-// the element math agree without further traffic), and each wave multiplies
-// P / dS into its own column slice of O / dQ / dK / dV.  K/V (or Q/dO) tiles
-// of 32 rows x HD are staged through the same swizzled LDS image as the
-// chunked kernels.  Element math, masks, dropout and the HSTU pointwise form
+// slices (4 waves at 256, 8 at 512).  Per 32-row tile every wave forms the
+// partial 32x32 score (and dP) product of its slice; the partials meet in LDS
+// and wave w sums, in wave order, only the 16/NW elements per lane it owns,
+// turns them into P / dS (the softmax or pointwise math runs once per element)
+// and hands them back as bf16 hi / lo words; every wave then multiplies the
+// whole P / dS tile into its own column slice of O / dQ / dK / dV (the
+// sampled-softmax backward's scheme, grk_sampled_softmax.hip).  The forward's
+// running max is exchanged per tile, its row sums once at the end.  K/V (or
+// Q/dO) tiles of 32 rows x HD are prefetched into registers under the
+// previous tile's work and staged through the chunked kernels' swizzled LDS
+// image.  Element math, masks, dropout and the HSTU pointwise form
 // are those of grk_attention.hip (same drop_keep stream, same lse / delta
 // conventions), so the backward of either path reads the other's forward.
 // fp32-fidelity (precise = 2) is not offered for these widths.
@@ -28,46 +32,136 @@ template <int HD>
 struct Wide {
   static constexpr int NW = HD / 64, NT = 64 * NW;  // column slices = waves
   static constexpr int DQ = 64, KSQ = DQ / 16, NDT = DQ / 32;
-  static constexpr int IMG = kWRows * HD * 2;   // one 32-row bf16 image
-  static constexpr int RED = NW * 4 * 64 * 16;  // one f32x16 per lane per wave
+  static constexpr int EPW = 16 / NW;               // tile elements per lane each wave turns into P / dS
+  static constexpr int IMG = kWRows * HD * 2;       // one 32-row bf16 image
+  static constexpr int RED = NW * 8 * 64 * 8;       // partial products: [wave][element pair][lane] float2
+  static constexpr int GX = NW * 64 * EPW * 4;      // P or dS as bf16 hi / lo words: [wave][lane][EPW]
 };
 
-__device__ __forceinline__ void red_put(float4* red, int w, int lane, const f32x16& x) {
+// This wave's partial 32x32 product (over its column slice) to LDS.
+__device__ __forceinline__ void red_put(float2* red, int ws, int lane, const f32x16& x) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) red[(w * 4 + q) * 64 + lane] = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+  for (int pr = 0; pr < 8; ++pr) red[(ws * 8 + pr) * 64 + lane] = make_float2(x[2 * pr], x[2 * pr + 1]);
 }
 
-// Sum of the NW waves' partials, in wave order (identical in every wave).
+// The EPW elements k in [ws*EPW, (ws+1)*EPW) this wave owns, summed over the
+// waves' partials in wave order.
 template <int NW>
-__device__ __forceinline__ f32x16 red_sum(const float4* red, int lane) {
-  f32x16 s;
+__device__ __forceinline__ void red_own(const float2* red, int ws, int lane, float* e) {
+  constexpr int EPW = 16 / NW;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 a = red[q * 64 + lane];
-    s[4 * q] = a.x; s[4 * q + 1] = a.y; s[4 * q + 2] = a.z; s[4 * q + 3] = a.w;
-  }
-#pragma unroll 1
-  for (int w = 1; w < NW; ++w)  // streamed: 8 waves' partials at once would not fit the registers
+  for (int q = 0; q < EPW / 2; ++q) {
+    const int pr = ws * (EPW / 2) + q;
+    float2 t = red[pr * 64 + lane];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 a = red[(w * 4 + q) * 64 + lane];
-      s[4 * q] += a.x; s[4 * q + 1] += a.y; s[4 * q + 2] += a.z; s[4 * q + 3] += a.w;
+    for (int w = 1; w < NW; ++w) {
+      const float2 u = red[(w * 8 + pr) * 64 + lane];
+      t.x += u.x;
+      t.y += u.y;
     }
-  return s;
+    e[2 * q] = t.x;
+    e[2 * q + 1] = t.y;
+  }
 }
+
+// Own elements -> bf16 hi / lo words (hi = bf16(x), lo = bf16(x - hi)).
+template <int EPW>
+__device__ __forceinline__ void put_words(uint32_t* gx, int ws, int lane, const float* g) {
+  uint32_t* dst = gx + (ws * 64 + lane) * EPW;
+#pragma unroll
+  for (int e2 = 0; e2 < EPW / 2; ++e2) {
+    const __bf16 h0 = static_cast<__bf16>(g[2 * e2]), h1 = static_cast<__bf16>(g[2 * e2 + 1]);
+    const __bf16 l0 = static_cast<__bf16>(g[2 * e2] - static_cast<float>(h0));
+    const __bf16 l1 = static_cast<__bf16>(g[2 * e2 + 1] - static_cast<float>(h1));
+    dst[e2] = (uint32_t)__builtin_bit_cast(bf16_t, h0) | ((uint32_t)__builtin_bit_cast(bf16_t, h1) << 16);
+    dst[EPW / 2 + e2] = (uint32_t)__builtin_bit_cast(bf16_t, l0) | ((uint32_t)__builtin_bit_cast(bf16_t, l1) << 16);
+  }
+}
+
+// Elements 8 s2 .. 8 s2 + 7 of the whole tile (the MFMA B operand, as
+// pack_acc forms it) from the owners' words.
+template <int EPW>
+__device__ __forceinline__ void get_words(const uint32_t* gx, int lane, int s2, bf16x8& hi, bf16x8& lo) {
+  uint32_t hw[4], lw[4];
+#pragma unroll
+  for (int pp = 0; pp < 4; ++pp) {
+    const int k = 8 * s2 + 2 * pp, w = k / EPW, kk = k % EPW;
+    const uint32_t* src = gx + (w * 64 + lane) * EPW;
+    hw[pp] = src[kk / 2];
+    lw[pp] = src[EPW / 2 + kk / 2];
+  }
+  hi = __builtin_bit_cast(bf16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
+  lo = __builtin_bit_cast(bf16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
+}
+
+// Tile row of element k (acc_row with k not a compile-time constant).
+__device__ __forceinline__ int elem_row(int k, int hh) { return (k & 3) + 8 * (k >> 2) + 4 * hh; }
 
 __device__ __forceinline__ void* shift(void* p, bool f32, int n) { return (char*)p + (size_t)n * (f32 ? 4 : 2); }
+
+// Workgroup barrier for LDS hand-offs only (waits for LDS operations, not for
+// the next tile's global loads, which __syncthreads()' fence would drain).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// 32 rows x HD of a [B*T, ld] head slice (bf16, or fp32 when F32), zero past
+// T: fetch() into registers under the previous tile's work, put() into the
+// swizzled LDS image (rounded to bf16, SiLU on the way when act) between two
+// barriers.
+template <int HD, int NT, bool F32>
+struct WRows {
+  static constexpr int NCH = HD / 8, PER = kWRows * NCH / NT;  // 16-byte chunks per thread
+  uint4 v[F32 ? 2 * PER : PER];
+  __device__ __forceinline__ void fetch(const void* src, int64_t ld, int b, int T, int h, int r0) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = threadIdx.x + j * NT, row = u / NCH, c = u % NCH, t = r0 + row;
+      const int64_t off = ((int64_t)b * T + t) * ld + h * HD + c * 8;
+      if (F32) {
+        v[2 * j] = v[2 * j + 1] = make_uint4(0, 0, 0, 0);
+        if (t < T) {
+          v[2 * j] = reinterpret_cast<const uint4*>((const float*)src + off)[0];
+          v[2 * j + 1] = reinterpret_cast<const uint4*>((const float*)src + off)[1];
+        }
+      } else {
+        v[j] = make_uint4(0, 0, 0, 0);
+        if (t < T) v[j] = *reinterpret_cast<const uint4*>((const bf16_t*)src + off);
+      }
+    }
+  }
+  __device__ __forceinline__ void put(char* img, bool act) const {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = threadIdx.x + j * NT, row = u / NCH, c = u % NCH;
+      bf16x8 x;
+      if (F32) {
+        const float4 a = __builtin_bit_cast(float4, v[2 * j]), d = __builtin_bit_cast(float4, v[2 * j + 1]);
+        x[0] = (__bf16)a.x; x[1] = (__bf16)a.y; x[2] = (__bf16)a.z; x[3] = (__bf16)a.w;
+        x[4] = (__bf16)d.x; x[5] = (__bf16)d.y; x[6] = (__bf16)d.z; x[7] = (__bf16)d.w;
+      } else {
+        x = __builtin_bit_cast(bf16x8, v[j]);
+      }
+      if (act) x = silu8(x);
+      *reinterpret_cast<uint4*>(img + lds_off<HD>(row, c * 8)) = __builtin_bit_cast(uint4, x);
+    }
+  }
+};
+
+__device__ __forceinline__ uint8_t key_ok(const AttnParams& p, int b, int t) {
+  return (t < p.T) && (!p.key_valid || p.key_valid[(int64_t)b * p.T + t]);
+}
 
 // ================================================================ forward ====
 template <int HD, int KIND>
 __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
   using W = Wide<HD>;
-  constexpr int KSQ = W::KSQ, NDT = W::NDT;
+  constexpr int KSQ = W::KSQ, NDT = W::NDT, NW = W::NW, EPW = W::EPW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + W::IMG;
-  float4* red = reinterpret_cast<float4*>(smem + 2 * W::IMG);
-  char* tail = smem + 2 * W::IMG + W::RED;
+  float2* red = reinterpret_cast<float2*>(smem + 2 * W::IMG);
+  uint32_t* gxp = reinterpret_cast<uint32_t*>(smem + 2 * W::IMG + W::RED);
+  float* mx = reinterpret_cast<float*>(smem + 2 * W::IMG + W::RED + W::GX);  // [wave][lane]
+  char* tail = smem + 2 * W::IMG + W::RED + W::GX + NW * 64 * 4;
   uint8_t* kvs = reinterpret_cast<uint8_t*>(tail);
   int* s_start = reinterpret_cast<int*>(tail + 32);
   float* rabs = reinterpret_cast<float*>(tail + kWTail);
@@ -90,71 +184,85 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
   }
   f32x16 o[NDT];
 #pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x16{};
-  float m = -INFINITY, l = 0.f;
+  for (int dt = 0; dt < NDT; ++dt) o[dt] = acc_zero();
+  float m = -INFINITY, lw = 0.f;  // running max (same in every wave); this wave's share of the row sum
   const float sl2 = p.scale * kLog2e;
   const float rdrop = 1.0f / (1.0f - p.dropout_p);
   const bool drop = KIND == 0 && p.dropout_p > 0.f;
   const unsigned long long seed = drop ? attn_seed(p) : 0ull;
   const int bh = b * p.H + h;
 
-  const int kend = min(T, q0 + kWRows);
-  for (int kb = (start / 32) * 32; kb < kend; kb += 32) {
+  const int kend = min(T, q0 + kWRows), kbeg = (start / 32) * 32;
+  WRows<HD, W::NT, false> kt, vt;
+  uint8_t kvb = 0;
+  if (kbeg < kend) {
+    kt.fetch(p.k, p.ldk, b, T, h, kbeg);
+    vt.fetch(p.v, p.ldv, b, T, h, kbeg);
+    if (threadIdx.x < 32) kvb = key_ok(p, b, kbeg + threadIdx.x);
+  }
+  for (int kb = kbeg; kb < kend; kb += 32) {
     __syncthreads();
-    stage_rows_at<HD>(Ks, p.k, p.ldk, b, T, h, kb, 32, 0, false, p.act);
-    stage_rows_at<HD>(Vs, p.v, p.ldv, b, T, h, kb, 32, 0, false, p.act);
-    if (threadIdx.x < 32) {
-      const int t = kb + threadIdx.x;
-      kvs[threadIdx.x] = (t < T) && (!p.key_valid || p.key_valid[(int64_t)b * T + t]);
+    kt.put(Ks, p.act);
+    vt.put(Vs, p.act);
+    if (threadIdx.x < 32) kvs[threadIdx.x] = kvb;
+    lds_barrier();
+    if (kb + 32 < kend) {  // in flight under this tile's work
+      kt.fetch(p.k, p.ldk, b, T, h, kb + 32);
+      vt.fetch(p.v, p.ldv, b, T, h, kb + 32);
+      if (threadIdx.x < 32) kvb = key_ok(p, b, kb + 32 + threadIdx.x);
     }
-    __syncthreads();
-    f32x16 s = f32x16{};
+    f32x16 s = acc_zero();
 #pragma unroll
     for (int ks = 0; ks < KSQ; ++ks) s = mfma(lds_row8<HD>(Ks, r, c0 + 16 * ks + 8 * hh), qf[ks], s);
     red_put(red, ws, lane, s);
-    __syncthreads();
-    s = red_sum<W::NW>(red, lane);
-    float pd[16];
+    lds_barrier();
+    float se[EPW], pd[EPW];
+    red_own<NW>(red, ws, lane, se);
     if (KIND == 0) {
-      float x[16], pr[16], tmax = -INFINITY;
+      float x[EPW], tmax = -INFINITY;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int kr = acc_row(i, hh), key = kb + kr;
+      for (int e = 0; e < EPW; ++e) {
+        const int kr = elem_row(ws * EPW + e, hh), key = kb + kr;
         const bool ok = qok && key <= myq && kvs[kr];
-        x[i] = ok ? s[i] * sl2 : -INFINITY;
-        tmax = fmaxf(tmax, x[i]);
+        x[e] = ok ? se[e] * sl2 : -INFINITY;
+        tmax = fmaxf(tmax, x[e]);
       }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+      mx[ws * 64 + lane] = fmaxf(tmax, __shfl_xor(tmax, 32));
+      lds_barrier();
+#pragma unroll
+      for (int w = 0; w < NW; ++w) tmax = fmaxf(tmax, mx[w * 64 + lane]);
       const float mn = fmaxf(m, tmax);
       const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
       float rs = 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        pr[i] = (x[i] == -INFINITY) ? 0.f : exp2f(x[i] - mn);
-        rs += pr[i];
+      for (int e = 0; e < EPW; ++e) {
+        const float pr = (x[e] == -INFINITY) ? 0.f : exp2f(x[e] - mn);
+        rs += pr;
+        pd[e] = pr;
+        if (drop) {
+          const int key = kb + elem_row(ws * EPW + e, hh);
+          pd[e] = drop_keep(seed, bh, myq, key, T, p.dropout_p) ? pr * rdrop : 0.f;
+        }
       }
-      rs += __shfl_xor(rs, 32);
-      l = l * alpha + rs;
+      lw = lw * alpha + rs;
       m = mn;
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) o[dt] *= alpha;
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        pd[i] = !drop ? pr[i]
-                      : (drop_keep(seed, bh, myq, kb + acc_row(i, hh), T, p.dropout_p) ? pr[i] * rdrop : 0.f);
     } else {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int kr = acc_row(i, hh), key = kb + kr;
+      for (int e = 0; e < EPW; ++e) {
+        const int kr = elem_row(ws * EPW + e, hh), key = kb + kr;
         const bool ok = qok && key <= myq && kvs[kr];
-        const float sp = s[i] * p.scale + rabs[ok ? min(myq - key, p.nb - 1) : 0];
-        pd[i] = ok ? silu(sp) * p.inv_n : 0.f;
+        const float sp = se[e] * p.scale + rabs[ok ? min(myq - key, p.nb - 1) : 0];
+        pd[e] = ok ? silu(sp) * p.inv_n : 0.f;
       }
     }
+    put_words<EPW>(gxp, ws, lane, pd);
+    lds_barrier();
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       bf16x8 ph, pl;
-      pack_acc(pd, s2, ph, pl);
+      get_words<EPW>(gxp, lane, s2, ph, pl);
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         const bf16x8 vf = lds_tr8<HD>(Vs, 16 * s2, c0 + 32 * dt, lane);
@@ -165,6 +273,12 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
   }
   float mul = 1.f;
   if (KIND == 0) {
+    // row sum = every wave's share, both half-waves, in a fixed order
+    mx[ws * 64 + lane] = lw;
+    lds_barrier();
+    float l = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) l += mx[w * 64 + r] + mx[w * 64 + 32 + r];
     mul = l > 0.f ? 1.0f / l : 0.f;
     if (ws == 0 && hh == 0 && qok && p.lse) p.lse[(int64_t)bh * T + myq] = l > 0.f ? (m + log2f(l)) * kLn2 : -INFINITY;
   }
@@ -175,13 +289,14 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
 template <int HD, int KIND>
 __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
   using W = Wide<HD>;
-  constexpr int KSQ = W::KSQ, NDT = W::NDT;
+  constexpr int KSQ = W::KSQ, NDT = W::NDT, NW = W::NW, EPW = W::EPW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + W::IMG;
-  float4* red = reinterpret_cast<float4*>(smem + 2 * W::IMG);
-  float4* red2 = red + W::RED / 16;
-  char* tail = smem + 2 * W::IMG + 2 * W::RED;
+  float2* red = reinterpret_cast<float2*>(smem + 2 * W::IMG);
+  float2* red2 = reinterpret_cast<float2*>(smem + 2 * W::IMG + W::RED);
+  uint32_t* gxd = reinterpret_cast<uint32_t*>(smem + 2 * W::IMG + 2 * W::RED);
+  char* tail = smem + 2 * W::IMG + 2 * W::RED + W::GX;
   uint8_t* kvs = reinterpret_cast<uint8_t*>(tail);
   int* s_start = reinterpret_cast<int*>(tail + 32);
   float* rabs = reinterpret_cast<float*>(tail + kWTail);
@@ -216,23 +331,32 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
   const bool row_live = KIND == 1 || lse2 != -INFINITY;
   f32x16 acc[NDT];
 #pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) acc[dt] = f32x16{};
+  for (int dt = 0; dt < NDT; ++dt) acc[dt] = acc_zero();
   const float sl2 = p.scale * kLog2e;
   const float rdrop = 1.0f / (1.0f - p.dropout_p);
   const bool drop = KIND == 0 && p.dropout_p > 0.f;
   const unsigned long long seed = drop ? attn_seed(p) : 0ull;
 
-  const int kend = min(T, q0 + kWRows);
-  for (int kb = (start / 32) * 32; kb < kend; kb += 32) {
+  const int kend = min(T, q0 + kWRows), kbeg = (start / 32) * 32;
+  WRows<HD, W::NT, false> kt, vt;
+  uint8_t kvb = 0;
+  if (kbeg < kend) {
+    kt.fetch(p.k, p.ldk, b, T, h, kbeg);
+    vt.fetch(p.v, p.ldv, b, T, h, kbeg);
+    if (threadIdx.x < 32) kvb = key_ok(p, b, kbeg + threadIdx.x);
+  }
+  for (int kb = kbeg; kb < kend; kb += 32) {
     __syncthreads();
-    stage_rows_at<HD>(Ks, p.k, p.ldk, b, T, h, kb, 32, 0, false, p.act);
-    stage_rows_at<HD>(Vs, p.v, p.ldv, b, T, h, kb, 32, 0, false, p.act);
-    if (threadIdx.x < 32) {
-      const int t = kb + threadIdx.x;
-      kvs[threadIdx.x] = (t < T) && (!p.key_valid || p.key_valid[(int64_t)b * T + t]);
+    kt.put(Ks, p.act);
+    vt.put(Vs, p.act);
+    if (threadIdx.x < 32) kvs[threadIdx.x] = kvb;
+    lds_barrier();
+    if (kb + 32 < kend) {  // in flight under this tile's work
+      kt.fetch(p.k, p.ldk, b, T, h, kb + 32);
+      vt.fetch(p.v, p.ldv, b, T, h, kb + 32);
+      if (threadIdx.x < 32) kvb = key_ok(p, b, kb + 32 + threadIdx.x);
     }
-    __syncthreads();
-    f32x16 s = f32x16{}, dp = f32x16{};
+    f32x16 s = acc_zero(), dp = acc_zero();
 #pragma unroll
     for (int ks = 0; ks < KSQ; ++ks) {
       s = mfma(lds_row8<HD>(Ks, r, c0 + 16 * ks + 8 * hh), qf[ks], s);
@@ -240,31 +364,32 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
     }
     red_put(red, ws, lane, s);
     red_put(red2, ws, lane, dp);
-    __syncthreads();
-    s = red_sum<W::NW>(red, lane);
-    dp = red_sum<W::NW>(red2, lane);
-    float ds[16];
+    lds_barrier();
+    float se[EPW], de[EPW], ds[EPW];
+    red_own<NW>(red, ws, lane, se);
+    red_own<NW>(red2, ws, lane, de);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int kr = acc_row(i, hh), key = kb + kr;
+    for (int e = 0; e < EPW; ++e) {
+      const int kr = elem_row(ws * EPW + e, hh), key = kb + kr;
       const bool ok = qok && row_live && key <= myq && kvs[kr];
       if (KIND == 0) {
-        const float pv = ok ? exp2f(s[i] * sl2 - lse2) : 0.f;
-        float dpv = dp[i];
+        const float pv = ok ? exp2f(se[e] * sl2 - lse2) : 0.f;
+        float dpv = de[e];
         if (drop) dpv = drop_keep(seed, bh, myq, key, T, p.dropout_p) ? dpv * rdrop : 0.f;
-        ds[i] = pv * (dpv - dlt);
+        ds[e] = pv * (dpv - dlt);
       } else {
         const int bk = min(myq - key, p.nb - 1);
-        const float sp = s[i] * p.scale + rabs[ok ? bk : 0];
-        ds[i] = ok ? dp[i] * dsilu(sp) * p.inv_n : 0.f;
-        // every wave holds the same dS: wave 0 alone adds it to the bins
-        if (ws == 0 && ok && ds[i] != 0.f && p.drab) atomicAdd(&bins[bk], to_fix(ds[i]));
+        const float sp = se[e] * p.scale + rabs[ok ? bk : 0];
+        ds[e] = ok ? de[e] * dsilu(sp) * p.inv_n : 0.f;
+        if (ok && ds[e] != 0.f && p.drab) atomicAdd(&bins[bk], to_fix(ds[e]));
       }
     }
+    put_words<EPW>(gxd, ws, lane, ds);
+    lds_barrier();
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       bf16x8 dh, dl;
-      pack_acc(ds, s2, dh, dl);
+      get_words<EPW>(gxd, lane, s2, dh, dl);
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         const bf16x8 kf = lds_tr8<HD>(Ks, 16 * s2, c0 + 32 * dt, lane);
@@ -283,16 +408,18 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
 }
 
 // ============================================================== dK / dV =====
-template <int HD, int KIND>
+template <int HD, int KIND, bool DF32>
 __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
   using W = Wide<HD>;
-  constexpr int KSQ = W::KSQ, NDT = W::NDT;
+  constexpr int KSQ = W::KSQ, NDT = W::NDT, NW = W::NW, EPW = W::EPW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Qs = smem;
   char* Ds = smem + W::IMG;
-  float4* red = reinterpret_cast<float4*>(smem + 2 * W::IMG);
-  float4* red2 = red + W::RED / 16;
-  char* tail = smem + 2 * W::IMG + 2 * W::RED;
+  float2* red = reinterpret_cast<float2*>(smem + 2 * W::IMG);
+  float2* red2 = reinterpret_cast<float2*>(smem + 2 * W::IMG + W::RED);
+  uint32_t* gxp = reinterpret_cast<uint32_t*>(smem + 2 * W::IMG + 2 * W::RED);
+  uint32_t* gxd = gxp + W::GX / 4;
+  char* tail = smem + 2 * W::IMG + 2 * W::RED + 2 * W::GX;
   int* s_start = reinterpret_cast<int*>(tail + 32);
   float* lses = reinterpret_cast<float*>(tail + 48);
   float* dlts = lses + 32;
@@ -321,29 +448,40 @@ __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
   }
   f32x16 dk[NDT], dv[NDT];
 #pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) { dk[dt] = f32x16{}; dv[dt] = f32x16{}; }
+  for (int dt = 0; dt < NDT; ++dt) { dk[dt] = acc_zero(); dv[dt] = acc_zero(); }
   const float sl2 = p.scale * kLog2e;
   const float rdrop = 1.0f / (1.0f - p.dropout_p);
   const bool drop = KIND == 0 && p.dropout_p > 0.f;
   const unsigned long long seed = drop ? attn_seed(p) : 0ull;
 
   // queries that can see this block's keys: q >= k0 and q >= start
-  for (int qb = (max(k0, start) / 32) * 32; qb < T; qb += 32) {
+  const int qbeg = (max(k0, start) / 32) * 32;
+  WRows<HD, W::NT, false> qt;
+  WRows<HD, W::NT, DF32> dt_;
+  float lv = -INFINITY, dl = 0.f;
+  auto fetch = [&](int qb) {
+    qt.fetch(p.q, p.ldq, b, T, h, qb);
+    dt_.fetch(p.dout, p.lddo, b, T, h, qb);
+    const int t = qb + (int)threadIdx.x;
+    lv = -INFINITY;
+    dl = 0.f;
+    if (KIND == 0 && threadIdx.x < 32 && t < T) {
+      lv = p.lse[(int64_t)bh * T + t];
+      dl = p.delta[(int64_t)bh * T + t];
+    }
+  };
+  if (qbeg < T) fetch(qbeg);
+  for (int qb = qbeg; qb < T; qb += 32) {
     __syncthreads();
-    stage_rows_at<HD>(Qs, p.q, p.ldq, b, T, h, qb, 32, 0, false, p.act);
-    stage_rows_at<HD>(Ds, p.dout, p.lddo, b, T, h, qb, 32, 0, p.dout_f32, false);
+    qt.put(Qs, p.act);
+    dt_.put(Ds, false);
     if (threadIdx.x < 32) {
-      const int t = qb + threadIdx.x;
-      float lv = -INFINITY, dl = 0.f;
-      if (KIND == 0 && t < T) {
-        lv = p.lse[(int64_t)bh * T + t] * kLog2e;
-        dl = p.delta[(int64_t)bh * T + t];
-      }
-      lses[threadIdx.x] = lv;
+      lses[threadIdx.x] = lv * kLog2e;
       dlts[threadIdx.x] = dl;
     }
-    __syncthreads();
-    f32x16 s = f32x16{}, dp = f32x16{};
+    lds_barrier();
+    if (qb + 32 < T) fetch(qb + 32);  // in flight under this tile's work
+    f32x16 s = acc_zero(), dp = acc_zero();
 #pragma unroll
     for (int ks = 0; ks < KSQ; ++ks) {
       s = mfma(lds_row8<HD>(Qs, r, c0 + 16 * ks + 8 * hh), kf[ks], s);
@@ -351,36 +489,39 @@ __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
     }
     red_put(red, ws, lane, s);
     red_put(red2, ws, lane, dp);
-    __syncthreads();
-    s = red_sum<W::NW>(red, lane);
-    dp = red_sum<W::NW>(red2, lane);
-    float pd[16], ds[16];
+    lds_barrier();
+    float se[EPW], de[EPW], pd[EPW], ds[EPW];
+    red_own<NW>(red, ws, lane, se);
+    red_own<NW>(red2, ws, lane, de);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qr = acc_row(i, hh), q = qb + qr;
+    for (int e = 0; e < EPW; ++e) {
+      const int qr = elem_row(ws * EPW + e, hh), q = qb + qr;
       const bool ok = kok && q < T && myk <= q;
       if (KIND == 0) {
-        const float lv = lses[qr];
-        const float pv = (ok && lv != -INFINITY) ? exp2f(s[i] * sl2 - lv) : 0.f;
-        float dpv = dp[i];
-        pd[i] = pv;
+        const float lq = lses[qr];
+        const float pv = (ok && lq != -INFINITY) ? exp2f(se[e] * sl2 - lq) : 0.f;
+        float dpv = de[e];
+        pd[e] = pv;
         if (drop) {
           const bool keep = drop_keep(seed, bh, q, myk, T, p.dropout_p);
-          pd[i] = keep ? pv * rdrop : 0.f;
+          pd[e] = keep ? pv * rdrop : 0.f;
           dpv = keep ? dpv * rdrop : 0.f;
         }
-        ds[i] = pv * (dpv - dlts[qr]);
+        ds[e] = pv * (dpv - dlts[qr]);
       } else {
-        const float sp = s[i] * p.scale + rabs[ok ? min(q - myk, p.nb - 1) : 0];
-        pd[i] = ok ? silu(sp) * p.inv_n : 0.f;
-        ds[i] = ok ? dp[i] * dsilu(sp) * p.inv_n : 0.f;
+        const float sp = se[e] * p.scale + rabs[ok ? min(q - myk, p.nb - 1) : 0];
+        pd[e] = ok ? silu(sp) * p.inv_n : 0.f;
+        ds[e] = ok ? de[e] * dsilu(sp) * p.inv_n : 0.f;
       }
     }
+    put_words<EPW>(gxp, ws, lane, pd);
+    put_words<EPW>(gxd, ws, lane, ds);
+    lds_barrier();
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8 ph, pl, dh, dl;
-      pack_acc(pd, s2, ph, pl);
-      pack_acc(ds, s2, dh, dl);
+      bf16x8 ph, pl, dh, dl2;
+      get_words<EPW>(gxp, lane, s2, ph, pl);
+      get_words<EPW>(gxd, lane, s2, dh, dl2);
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         const bf16x8 dof = lds_tr8<HD>(Ds, 16 * s2, c0 + 32 * dt, lane);
@@ -389,7 +530,7 @@ __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
         dk[dt] = mfma(qf, dh, dk[dt]);
         if (p.precise) {
           dv[dt] = mfma(dof, pl, dv[dt]);
-          dk[dt] = mfma(qf, dl, dk[dt]);
+          dk[dt] = mfma(qf, dl2, dk[dt]);
         }
       }
     }
@@ -408,14 +549,15 @@ int wide_hd(const AttnParams& p, int which, hipStream_t s) {
   const bool hstu = p.kind == GRK_ATTN_HSTU;
   const size_t rab = hstu ? (size_t)(p.nb + 1) / 2 * 2 * 4 : 0;
   if (which == 0) {
-    const size_t lds = 2 * W::IMG + W::RED + kWTail + rab;
+    const size_t lds = 2 * W::IMG + W::RED + W::GX + W::NW * 64 * 4 + kWTail + rab;
     launch_lds(hstu ? k_attn_fwd_wide<HD, 1> : k_attn_fwd_wide<HD, 0>, grid, W::NT, lds, s, p);
   } else if (which == 2) {
-    const size_t lds = 2 * W::IMG + 2 * W::RED + kWTail + rab + (hstu ? (size_t)p.nb * 8 : 0);
+    const size_t lds = 2 * W::IMG + 2 * W::RED + W::GX + kWTail + rab + (hstu ? (size_t)p.nb * 8 : 0);
     launch_lds(hstu ? k_attn_dq_wide<HD, 1> : k_attn_dq_wide<HD, 0>, grid, W::NT, lds, s, p);
   } else {
-    const size_t lds = 2 * W::IMG + 2 * W::RED + kWTail + rab;
-    launch_lds(hstu ? k_attn_dkdv_wide<HD, 1> : k_attn_dkdv_wide<HD, 0>, grid, W::NT, lds, s, p);
+    const size_t lds = 2 * W::IMG + 2 * W::RED + 2 * W::GX + kWTail + rab;
+    if (p.dout_f32) launch_lds(hstu ? k_attn_dkdv_wide<HD, 1, true> : k_attn_dkdv_wide<HD, 0, true>, grid, W::NT, lds, s, p);
+    else launch_lds(hstu ? k_attn_dkdv_wide<HD, 1, false> : k_attn_dkdv_wide<HD, 0, false>, grid, W::NT, lds, s, p);
   }
   GRK_LAUNCH_CHECK();
   return GRK_OK;
