@@ -20,6 +20,10 @@ all: $(LIB)
 # which gave timing-dependent wrong HSTU rows when two workgroups shared a CU
 # (DESIGN.md §5b); the overlap check below guards the link.
 $(OBJ_DIR)/grk_attention_seq.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
+# no SLP packing of the scalar score math into v_pk_*_f32: packed f32 VALU is
+# slower than scalar beside MFMAs, and packed SiLU chains in the forward gave
+# run-to-run different outputs
+$(OBJ_DIR)/grk_attention_seq.o: HIPFLAGS += -fno-slp-vectorize
 
 $(OBJ_DIR):
 	mkdir -p $@

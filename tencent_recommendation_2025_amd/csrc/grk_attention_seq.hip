@@ -18,6 +18,8 @@
 //  * the precise (hi/lo probability) mode is a template parameter.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "grk_attention.h"
 
 namespace grk {
@@ -33,6 +35,7 @@ __device__ unsigned long long g_attn_stamps[1 << 16][8];
 #define GRK_STAMP(k)
 #endif
 constexpr int kRabPad = 32;             // rabx[kRabPad + d], d >= -31 inside a sub-tile
+constexpr float kCausalBias = -1.0e30f;
 constexpr int kDqBinArrays = 2;         // dQ kernel: drab bins as int64 fixed point (2 float slots each)
 constexpr int kSeqLdsMax = 80 * 1024;   // LDS per workgroup: 2 per CU fit gfx950's 160 KiB
 
@@ -265,7 +268,10 @@ __device__ __forceinline__ void stage_pair(char* img0, const void* src0, int64_t
   }
 }
 
-// rabx[kRabPad + d] = rab[h, min(d, nb - 1)] for d >= 0, 0 for d < 0.
+// rabx[kRabPad + d] = rab[h, min(d, nb - 1)] for d >= 0, kCausalBias for d < 0:
+// a key after its query gets x = -1e30, SiLU(x) = dSiLU(x) = 0 exactly (the
+// sigmoid underflows to 0, every product stays finite) -- the HSTU kernels'
+// causal mask without a per-score select.
 // Tp + kRabPad <= 2 * blockDim for every shape the seq kernels take.
 struct RabRegs {
   float v[2];
@@ -276,7 +282,7 @@ __device__ __forceinline__ RabRegs load_rab(const AttnParams& p, int h, int Tp) 
   for (int k = 0; k < 2; ++k) {
     const int j = threadIdx.x + k * blockDim.x;
     const int d = j - kRabPad;
-    r.v[k] = (d < 0 || j >= Tp + kRabPad) ? 0.f : p.rab[h * p.nb + min(d, p.nb - 1)];
+    r.v[k] = d < 0 ? kCausalBias : (j >= Tp + kRabPad ? 0.f : p.rab[h * p.nb + min(d, p.nb - 1)]);
   }
   return r;
 }
@@ -291,6 +297,18 @@ __device__ __forceinline__ void store_rab(float* rabx, const RabRegs& r, int Tp)
 __device__ __forceinline__ void stage_kvs(uint8_t* kvs, const uint8_t* kv, int b, int T, int Tp) {
   for (int j = threadIdx.x; j < Tp; j += blockDim.x) kvs[j] = j < T && (!kv || kv[(int64_t)b * T + j]);
 }
+
+// HSTU forward / dQ: kbias[key] = 0 for a valid key, kCausalBias for padding,
+// invalid or past-T keys -- added to the score's pre-activation, it masks the
+// key exactly like the rab window masks the future (no per-score select).
+__device__ __forceinline__ void stage_key_bias(float* kbias, const uint8_t* kv, const SeqInfo& si, int b, int T,
+                                               int Tp) {
+  for (int j = threadIdx.x; j < Tp; j += blockDim.x) {
+    const bool ok = j >= si.start && j < T && (si.contig || kv[(int64_t)b * T + j]);
+    kbias[j] = ok ? 0.f : kCausalBias;
+  }
+}
+
 
 // relative-position bias of the 16 scores of lane (r, hh) in the sub-tile of
 // keys [kb, kb+32) for query myq: rabx[kRabPad + myq - key], key = kb + acc_row(i, hh)
@@ -358,7 +376,10 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
                          b, T, h, kbeg, Tp);
   else
     stage_pair<HD>(L.img0, p.k, p.ldk, false, p.act, L.img1, p.v, p.ldv, false, p.act, b, T, h, kbeg, Tp);
-  if (KIND == 1) store_rab(L.f0, rr, Tp);
+  if (KIND == 1) {
+    store_rab(L.f0, rr, Tp);
+    stage_key_bias(L.f1, p.key_valid, si, b, T, Tp);
+  }
   if (!si.contig) stage_kvs(L.kvs, p.key_valid, b, T, Tp);
   GRK_STAMP(2);
   __syncthreads();
@@ -450,14 +471,14 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
             }
           }
         } else {
+          // causal mask in the rab window, key mask in kbias: no select
           float rb[16];
           rab16(L.f0, myq, kb, hh, rb);
+          const float* kbb = L.f1 + kb + 4 * hh;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) pd[i] = silu(fmaf(s[i], p.scale, rb[i]));
-          if (!fast) {
-            const unsigned mk = qok ? mask16(kb, hh, start, myq, si.contig, L.kvs) : 0u;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) pd[i] = ((mk >> i) & 1) ? pd[i] : 0.f;
+          for (int i = 0; i < 16; ++i) {
+            const float x = fmaf(s[i], p.scale, rb[i]) + kbb[(i & 3) + 8 * (i >> 2)];
+            pd[i] = x * sigmoid_fast(x);
           }
         }
 #pragma unroll
@@ -490,9 +511,10 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
   const int T = p.T, nq = (T + 31) / 32, Tp = nq * 32;
-  SeqLds<HD, PREC == 2 ? 4 : 2> L(smem, Tp, kDqBinArrays);
+  SeqLds<HD, PREC == 2 ? 4 : 2> L(smem, Tp, kDqBinArrays + 1);
   // drab by distance d in [-kRabPad, Tp): bins[kRabPad + d], int64 fixed point
   unsigned long long* bins = reinterpret_cast<unsigned long long*>(L.f1);
+  float* kbias = L.f1 + kDqBinArrays * (Tp + kRabPad);
   const int b = seq_of_block(p, blockIdx.x / p.H), h = blockIdx.x % p.H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const SeqInfo si = seq_info(p, b, T, L.sh);
@@ -515,6 +537,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
   if (KIND == 1) {
     store_rab(L.f0, rr, Tp);
     for (int j = threadIdx.x; j < Tp + kRabPad; j += blockDim.x) bins[j] = 0ull;
+    stage_key_bias(kbias, p.key_valid, si, b, T, Tp);
   }
   if (!si.contig) stage_kvs(L.kvs, p.key_valid, b, T, Tp);
   __syncthreads();
@@ -581,7 +604,8 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
         }
         const bool fast = si.contig && kb < q0 && kb >= start;
         float ds[16];
-        const unsigned mk = fast ? 0xFFFFu : ((qok && row_live) ? mask16(kb, hh, start, myq, si.contig, L.kvs) : 0u);
+        const unsigned mk = (KIND == 1 || fast) ? 0xFFFFu
+                                                : ((qok && row_live) ? mask16(kb, hh, start, myq, si.contig, L.kvs) : 0u);
         if (KIND == 0) {
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
@@ -591,14 +615,17 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
             ds[i] = pv * (dpv - dlt);
           }
         } else {
+          // causal mask in the rab window, key mask in kbias: no select
           float rb[16];
           rab16(L.f0, myq, kb, hh, rb);
+          const float* kbb = kbias + kb + 4 * hh;
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            const float v = dp[i] * dsilu(fmaf(s[i], p.scale, rb[i])) * p.inv_n;
-            ds[i] = ((mk >> i) & 1) ? v : 0.f;
+            const float x = fmaf(s[i], p.scale, rb[i]) + kbb[(i & 3) + 8 * (i >> 2)];
+            const float sg = sigmoid_fast(x), sgn = sg * p.inv_n;
+            ds[i] = dp[i] * fmaf(fmaf(-x, sg, x), sgn, sgn);  // dp * dSiLU(x) / n
           }
-          if (p.drab && __any(mk != 0)) {
+          if (p.drab) {
             // drab bins by distance d = query - key.  The sub-tile's 1024 scores lie on
             // 63 diagonals: lane r of each half gathers score (key k, query (r + k) & 31)
             // of each of its 16 keys (one ds_bpermute each), whose distance is
@@ -649,7 +676,8 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
 
 // ============================================================== dK / dV =====
 template <int HD, int KIND, int PREC>
-__global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) {
+__global__ void __launch_bounds__(64 * kSeqWaves) __attribute__((amdgpu_waves_per_eu(PREC < 2 && HD <= 64 ? 2 : 1)))
+k_attn_dkdv_seq(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
   const int T = p.T, nq = (T + 31) / 32, Tp = nq * 32;
@@ -676,11 +704,14 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
   } else {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
+      // fully masked query rows (lse = -inf) and rows past T are staged as 0:
+      // every (query, key) pair they form with a valid key is masked or has dO = 0
       const int j = threadIdx.x + k * blockDim.x;
-      lv[k] = -INFINITY;
+      lv[k] = 0.f;
       dl[k] = 0.f;
       if (j < T) {
-        lv[k] = p.lse[(int64_t)bh * T + j] * kLog2e;
+        const float l = p.lse[(int64_t)bh * T + j];
+        lv[k] = l == -INFINITY ? 0.f : l * kLog2e;
         dl[k] = p.delta[(int64_t)bh * T + j];
       }
     }
@@ -744,11 +775,17 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
         act_frag<HD>(kf, p.act);
         act_frag<HD>(vf, p.act);
       }
+      if (!kok) {  // padding / invalid key: S = dP = 0 keep every product finite; stored as 0
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          kf[ks] = vf[ks] = kl[ks] = vl[ks] = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+        }
+      }
       f32x16 dk[NDT], dv[NDT];
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
-        dk[dt] = f32x16{};
-        dv[dt] = f32x16{};
+        dk[dt] = acc_zero();
+        dv[dt] = acc_zero();
       }
       for (int qb = k0; qb < Tp; qb += 32) {
         f32x16 s = acc_zero(), dp = acc_zero();
@@ -765,44 +802,70 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
             dp = mfma(lds_row8<HD>(L.img1lo, qb + r, 16 * ks + 8 * hh), vf[ks], dp);
           }
         }
-        // every query after every key of the tile, all queries < T, keys valid
-        const bool fast = si.contig && qb > k0 && qb + 32 <= T && k0 >= start;
-        float pd[16], ds[16];
+        // Invalid keys have zeroed fragments and are stored as 0; queries past T
+        // have zero Q / dO rows (their terms vanish) and a finite staged lse.
+        // HSTU: the causal mask is in the rab window (kCausalBias), so no score
+        // is selected; softmax: only the diagonal tile (or a non-contiguous
+        // key set) is masked.
+        const bool fast = si.contig && qb != k0;
+        const unsigned mk = fast ? 0xFFFFu : (kok ? mask16_range(qb, hh, myk, T - 1) : 0u);
+        // Per half tile (elements 8 s2 .. 8 s2 + 7): P and dS as bf16 hi / lo words,
+        // then that half's dV / dK MFMAs (the second half's VALU overlaps the first
+        // half's MFMAs).  Instantiated unmasked and masked behind one wave-uniform branch.
+        auto half = [&](auto masked, int s2) {
+        uint32_t pw[4], plw[4], dw[4], dlw[4];
         if (KIND == 0) {
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int qr = acc_row(i, hh), q = qb + qr;
-            const bool ok = fast | (kok & (q < T) & (myk <= q));
-            const float lq = lses[q];
-            const float e = exp2f(s[i] * sl2 - (lq == -INFINITY ? 0.f : lq));
-            const float pv = (ok & (lq != -INFINITY)) ? e : 0.f;
-            float dpv = dp[i];
-            pd[i] = pv;
-            if (drop) {
-              const bool keep = drop_keep(seed, bh, q, myk, T, p.dropout_p);
-              pd[i] = keep ? pv * rdrop : 0.f;
-              dpv = keep ? dpv * rdrop : 0.f;
+          for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * s2 + jj;
+            float pd2[2], ds2[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int i = 2 * j + u, q = qb + acc_row(i, hh);
+              const float pv = __builtin_amdgcn_exp2f(fmaf(s[i], sl2, -lses[q]));
+              float dpv = dp[i];
+              pd2[u] = pv;
+              if (drop) {
+                const bool keep = drop_keep(seed, bh, q, myk, T, p.dropout_p);
+                pd2[u] = keep ? pv * rdrop : 0.f;
+                dpv = keep ? dpv * rdrop : 0.f;
+              }
+              ds2[u] = pv * (dpv - dlts[q]);
             }
-            ds[i] = pv * (dpv - dlts[q]);
+            if constexpr (decltype(masked)::value) {
+              const bool m0 = (mk >> (2 * j)) & 1, m1 = (mk >> (2 * j + 1)) & 1;
+              pd2[0] = m0 ? pd2[0] : 0.f; ds2[0] = m0 ? ds2[0] : 0.f;
+              pd2[1] = m1 ? pd2[1] : 0.f; ds2[1] = m1 ? ds2[1] : 0.f;
+            }
+            split2(f32x2{pd2[0], pd2[1]}, pw[jj], plw[jj]);
+            split2(f32x2{ds2[0], ds2[1]}, dw[jj], dlw[jj]);
           }
         } else {
           // bias of (query qb + acc_row(i, hh), key myk): rabx[kRabPad + q - myk]
           const float* rbase = L.f0 + kRabPad + (qb - myk + 4 * hh);
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int qr = acc_row(i, hh), q = qb + qr;
-            const bool ok = fast | (kok & (q < T) & (myk <= q));
-            const float x = fmaf(s[i], p.scale, rbase[(i & 3) + 8 * (i >> 2)]);
-            const float sg = sigmoid_fast(x);
-            pd[i] = ok ? x * sg * p.inv_n : 0.f;
-            ds[i] = ok ? dp[i] * (sg * (1.0f + x * (1.0f - sg))) * p.inv_n : 0.f;
+          for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * s2 + jj;
+            float pd2[2], ds2[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int i = 2 * j + u;
+              const float x = fmaf(s[i], p.scale, rbase[(i & 3) + 8 * (i >> 2)]);
+              const float sg = sigmoid_fast(x), sgn = sg * p.inv_n;
+              pd2[u] = x * sgn;                                   // SiLU(x) / n
+              ds2[u] = dp[i] * fmaf(fmaf(-x, sg, x), sgn, sgn);   // dp * dSiLU(x) / n
+            }
+            if constexpr (decltype(masked)::value) {
+              const bool m0 = (mk >> (2 * j)) & 1, m1 = (mk >> (2 * j + 1)) & 1;
+              pd2[0] = m0 ? pd2[0] : 0.f; ds2[0] = m0 ? ds2[0] : 0.f;
+              pd2[1] = m1 ? pd2[1] : 0.f; ds2[1] = m1 ? ds2[1] : 0.f;
+            }
+            split2(f32x2{pd2[0], pd2[1]}, pw[jj], plw[jj]);
+            split2(f32x2{ds2[0], ds2[1]}, dw[jj], dlw[jj]);
           }
         }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 ph, pl, dh, dl2;
-          pack_acc(pd, s2, ph, pl);
-          pack_acc(ds, s2, dh, dl2);
+          const bf16x8 ph = words8(pw), pl = words8(plw);
+          const bf16x8 dh = words8(dw), dl2 = words8(dlw);
 #pragma unroll
           for (int dt = 0; dt < NDT; ++dt) {
             const bf16x8 dof = lds_tr8<HD>(L.img1, qb + 16 * s2, dt * 32, lane);
@@ -818,12 +881,14 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
               dk[dt] = mfma(lds_tr8<HD>(L.img0lo, qb + 16 * s2, dt * 32, lane), dh, dk[dt]);
             }
           }
-        }
+        };
+        half(std::integral_constant<bool, KIND == 0>{}, 0);
+        half(std::integral_constant<bool, KIND == 0>{}, 1);
       }
       const int64_t otok = (int64_t)b * T + myk;
-      store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, otok, h, hh, dk, p.scale, kin, p.act ? p.k : nullptr, p.ldk,
-                          p.in_dt);
-      store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, 1.f, kin, p.act ? p.v : nullptr, p.ldv,
+      store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, otok, h, hh, dk, kok ? p.scale : 0.f, kin, p.act ? p.k : nullptr,
+                          p.ldk, p.in_dt);
+      store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, kok ? 1.f : 0.f, kin, p.act ? p.v : nullptr, p.ldv,
                           p.in_dt);
     }
 }
@@ -831,7 +896,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dkdv_seq(AttnParams p) 
 template <int HD>
 static bool seq_launch_hd(const AttnParams& p, int which, hipStream_t s) {
   const int Tp = (p.T + 31) / 32 * 32;
-  const int f1 = which == 2 ? kDqBinArrays : 1;
+  const int f1 = which == 2 ? kDqBinArrays + 1 : 1;
   // fidelity mode: four images, one workgroup per CU (up to 160 KiB)
   const size_t lds = p.precise == 2 ? SeqLds<HD, 4>::bytes(Tp, f1) : SeqLds<HD, 2>::bytes(Tp, f1);
   const size_t cap = p.precise == 2 ? (size_t)160 * 1024 : (size_t)kSeqLdsMax;
@@ -860,7 +925,7 @@ static bool seq_launch_hd(const AttnParams& p, int which, hipStream_t s) {
 template <int HD>
 static bool fidelity_fits(int T) {
   const int Tp = (T + 31) / 32 * 32;
-  return SeqLds<HD, 4>::bytes(Tp, kDqBinArrays) <= (size_t)160 * 1024 && Tp + kRabPad <= 2 * 64 * kSeqWaves;
+  return SeqLds<HD, 4>::bytes(Tp, kDqBinArrays + 1) <= (size_t)160 * 1024 && Tp + kRabPad <= 2 * 64 * kSeqWaves;
 }
 
 bool attn_seq_launch(const AttnParams& p, int hd, int which, hipStream_t s) {

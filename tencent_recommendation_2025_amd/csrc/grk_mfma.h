@@ -70,15 +70,33 @@ __device__ __forceinline__ bf16x8 lds_tr8(const char* base, int row0, int col0, 
   return r;
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// Two values as packed bf16 words: hi = bf16(x) (round to nearest even),
+// lo = bf16(x - hi) -- one v_cvt_pk_bf16_f32 per word.  Scalar f32 math only:
+// packed f32 VALU (v_pk_*_f32) costs more than two scalar ops between MFMAs
+// (MI355X_MICROARCH.md), and packed SiLU sequences in the forward gave
+// run-to-run different outputs.
+__device__ __forceinline__ void split2(f32x2 x, uint32_t& hi, uint32_t& lo) {
+  const uint32_t h = __builtin_bit_cast(uint32_t, __builtin_convertvector(x, bf16x2));
+  const float r0 = x.x - __uint_as_float(h << 16), r1 = x.y - __uint_as_float(h & 0xFFFF0000u);
+  hi = h;
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{r0, r1}, bf16x2));
+}
+
+__device__ __forceinline__ bf16x8 words8(const uint32_t* w) {
+  return __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3]));
+}
+
 // Accumulator registers 8s..8s+7 as a bf16 operand (hi part, and the
 // residual lo part for the precise mode).
 __device__ __forceinline__ void pack_acc(const float* x, int s, bf16x8& hi, bf16x8& lo) {
+  uint32_t h[4], l[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    __bf16 hb = static_cast<__bf16>(x[8 * s + j]);
-    hi[j] = hb;
-    lo[j] = static_cast<__bf16>(x[8 * s + j] - static_cast<float>(hb));
-  }
+  for (int j = 0; j < 4; ++j) split2(f32x2{x[8 * s + 2 * j], x[8 * s + 2 * j + 1]}, h[j], l[j]);
+  hi = words8(h);
+  lo = words8(l);
 }
 
 __device__ __forceinline__ int acc_row(int i, int hh) { return (i & 3) + 8 * (i >> 2) + 4 * hh; }
