@@ -368,7 +368,7 @@ int grk_pair_logits_bwd(const void* h, int64_t ldh, const void* e_pos, int64_t l
  * Only valid positions take part: the kernels list them on the device
  * (compact index = rank among the valid positions) and size their grids for
  * num_rows, so nothing waits on the host.  Workspace: one buffer of
- * grk_sampled_softmax_workspace(num_rows) bytes, reusable between calls.
+ * grk_sampled_softmax_workspace(num_rows, dim) bytes, reusable between calls.
  * ------------------------------------------------------------------------ */
 size_t grk_sampled_softmax_workspace(int64_t num_rows, int dim);
 
