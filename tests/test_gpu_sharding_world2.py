@@ -17,7 +17,8 @@ through Adam's m / sqrt(v), which turns rounding noise on a near-zero gradient
 into a full +-lr step; later steps then see slightly different parameters.  So
 after the last step: parameters normwise < 5e-3 with at most 0.5 % of the
 elements (or 4) outside (rtol 1e-3, atol 2e-5) and none off by more than 2 lr x steps;
-first moments normwise < 2e-2.
+first moments normwise < 2e-2; rank losses 1e-4 relative at step 1, 1e-3
+after (the parameters they are computed from already differ).
 
 The rank batches are int32 on odd steps (collate_fn's dtype,
 model/BaseLine/dataset.py:267-293): the sharded lookups are matched to the
@@ -137,8 +138,11 @@ def test_world2_sharded_trainer_equals_unsharded_union_step():
         if i == 0:
             ref_m1 = {names[id(p)]: st['exp_avg'].cpu().numpy().copy() for p, st in opt.state.items()}
         with torch.no_grad():
+            # step 1 sees identical parameters: tight; later steps see parameters that
+            # Adam's m / sqrt(v) has moved by +-lr on near-zero gradients (docstring)
+            tol = 1e-4 if i == 0 else 1e-3
             for r in range(world):
-                assert abs(losses[r].item() - res[r][1][i]) < 1e-4 * max(1.0, abs(losses[r].item())), (i, r)
+                assert abs(losses[r].item() - res[r][1][i]) < tol * max(1.0, abs(losses[r].item())), (i, r)
     sd = m.state_dict()
 
     def report(name, got, want, moment=False):
