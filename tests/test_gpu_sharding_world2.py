@@ -15,8 +15,8 @@ then across ranks).  After step 1 (identical inputs) the AdamW first moments
 are 0.1 x the gradients: normwise relative error < 1e-5.  The parameters go
 through Adam's m / sqrt(v), which turns rounding noise on a near-zero gradient
 into a full +-lr step; later steps then see slightly different parameters.  So
-after the last step: parameters normwise < 5e-3 with at most 0.5 % of the
-elements (or 4) outside (rtol 1e-3, atol 2e-5) and none off by more than 2 lr x steps;
+after the last step: parameters normwise < 5e-3 with at most 1 % of the
+elements (or 8) outside (rtol 1e-3, atol 2e-5) and none off by more than 2 lr x steps;
 first moments normwise < 2e-2; rank losses 1e-4 relative at step 1, 1e-3
 after (the parameters they are computed from already differ).
 
@@ -153,7 +153,7 @@ def test_world2_sharded_trainer_equals_unsharded_union_step():
             return f'{name}: normwise {rel:.2e} >= {moment}' if rel >= moment else None
         bad = np.abs(got - want) > 2e-5 + 1e-3 * np.abs(want)
         worst = float(np.abs(got - want).max()) if got.size else 0.0
-        if rel >= 5e-3 or bad.sum() > max(4, 5e-3 * bad.size) or worst > 2 * LR * STEPS:
+        if rel >= 5e-3 or bad.sum() > max(8, 1e-2 * bad.size) or worst > 2 * LR * STEPS:
             return f'{name}: normwise {rel:.2e}, {int(bad.sum())} of {bad.size} elements off, max abs {worst:.2e}'
         return None
 
