@@ -106,6 +106,16 @@ typedef struct grk_lookup {
  * sum over lookups of num_tokens * bag (0 = query failed). */
 size_t grk_embedding_backward_workspace(int64_t num_occurrences, int64_t num_rows, int dim);
 
+/* Stable LSD radix sort of (uint32 key, uint64 value) pairs by the low
+ * end_bit bits of the keys (8-bit digits, three launches per digit) -- the
+ * occurrence grouping inside grk_embedding_backward, exposed for tests and
+ * reuse.  keys_in / vals_in are not modified; keys_tmp / vals_tmp are n-element
+ * scratch; workspace: grk_sort_pairs_workspace(n) bytes. */
+size_t grk_sort_pairs_workspace(int64_t n);
+int grk_sort_pairs(const uint32_t* keys_in, const uint64_t* vals_in, uint32_t* keys_out, uint64_t* vals_out,
+                   uint32_t* keys_tmp, uint64_t* vals_tmp, int64_t n, int end_bit, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
 /* Deterministic scatter-add gradient of one table, replacing autograd's
  * embedding_dense_backward.  Occurrences (lookup order,
  * then token, then bag slot) are stably sorted by row id and reduced in fp32

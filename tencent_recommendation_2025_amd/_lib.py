@@ -73,6 +73,8 @@ SIGNATURES = {
     'grk_version': (C.c_char_p, []),
     'grk_embedding_gather': (_I, [C.POINTER(GrkFeature), _I, _I, _I, _I, _I64, _P, C.c_int32, _P, _I64, _P, _P]),
     'grk_embedding_backward_workspace': (_SZ, [_I64, _I64, _I]),
+    'grk_sort_pairs_workspace': (_SZ, [_I64]),
+    'grk_sort_pairs': (_I, [_P, _P, _P, _P, _P, _P, _I64, _I, _P, _SZ, _P]),
     'grk_embedding_backward': (_I, [C.POINTER(GrkLookup), _I, _I, _I, _I, _P, C.c_int32, _I64, _I64, _P, _P, _P,
                                     _P, _P, _P, _SZ, _P, _P]),
     'grk_table_adamw': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _P, _I64, _P, GrkAdamwHparams, _I, _P]),

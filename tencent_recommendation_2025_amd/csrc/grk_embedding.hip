@@ -646,6 +646,11 @@ __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ key
 }
 
 // ------------------------------------------------------------ workspace ----
+// Stable radix sort of (row key, gradient-row address) pairs (grk_sort.hip).
+size_t sort_pairs_workspace(int64_t n);
+int sort_pairs(unsigned* k0, unsigned long long* v0, unsigned* k1, unsigned long long* v1, int64_t n, int end_bit,
+               void* ws, unsigned** kres, unsigned long long** vres, hipStream_t s);
+
 struct BwdWs {
   unsigned *keys_in, *keys_out, *seg_key;
   int *flags, *pos, *seg_start, *seg_end;
@@ -679,10 +684,7 @@ static int plan_ws(int64_t n, int64_t num_rows, int dim, char* base, BwdWs* ws) 
   while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
   size_t sb = 0, cb = 0;
   if (n > 0) {
-    if (rocprim::radix_sort_pairs(nullptr, sb, (unsigned*)nullptr, (unsigned*)nullptr,
-                                  (unsigned long long*)nullptr, (unsigned long long*)nullptr, (size_t)n, 0,
-                                  end_bit) != hipSuccess)
-      return GRK_EHIP;
+    sb = sort_pairs_workspace(n);
     if (rocprim::inclusive_scan(nullptr, cb, (int*)nullptr, (int*)nullptr, (size_t)n, rocprim::plus<int>()) !=
         hipSuccess)
       return GRK_EHIP;
@@ -823,9 +825,15 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   const int g = (int)((total + B - 1) / B);
   unsigned end_bit = 1;
   while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
-  size_t sb = ws.sort_bytes;
-  GRK_CHECK_HIP(rocprim::radix_sort_pairs(ws.sort_tmp, sb, ws.keys_in, ws.keys_out, ws.gptr_in, ws.gptr_out,
-                                          (size_t)total, 0, end_bit, s));
+  unsigned* skeys;
+  unsigned long long* sgptr;
+  {
+    const int rc = sort_pairs(ws.keys_in, ws.gptr_in, ws.keys_out, ws.gptr_out, total, (int)end_bit, ws.sort_tmp, &skeys,
+                              &sgptr, s);
+    if (rc) return rc;
+  }
+  ws.keys_out = skeys;  // the sorted pairs (either buffer of the ping-pong)
+  ws.gptr_out = sgptr;
   const unsigned sentinel = (unsigned)num_rows;
   k_mark_heads<<<g, B, 0, s>>>(ws.keys_out, ws.flags, total, sentinel);
   GRK_LAUNCH_CHECK();

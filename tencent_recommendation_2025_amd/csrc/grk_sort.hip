@@ -1,0 +1,208 @@
+// Stable LSD radix sort of (uint32 key, uint64 value) pairs for the embedding
+// backward's occurrence grouping (grk_embedding.hip): keys are table rows
+// (< 2^end_bit, end_bit = bits of the group's row count), values the
+// occurrences' gradient-row addresses, and the output must keep occurrence
+// order within a row -- the reference's CPU embedding_dense_backward sums a
+// row's occurrences sequentially in that order.
+//
+// rocprim::radix_sort_pairs took ~15 launches per call at these sizes (73
+// launches, ~0.5 ms per C2 training step over five calls).  Here a pass per
+// 8-bit digit is three launches:
+//   k_sort_hist    per 4096-key tile: digit counts -> hist[digit][tile]
+//   k_sort_scan    one workgroup per digit: exclusive scan of the digit's
+//                  tile counts, and the digit's total (the scatter's prologue
+//                  prefixes the 256 totals)
+//   k_sort_scatter per tile, 16 rounds of 256 keys in index order: a key's
+//                  slot = its (digit, tile) base + the keys of its digit in
+//                  earlier rounds, earlier waves of this round, and lower
+//                  lanes of its wave (wave ballots over the 8 digit bits)
+// so the order among equal digits is the input order: stable, deterministic,
+// and (a stable sort being unique) the same output as rocprim's.
+#include "grk_common.h"
+
+namespace grk {
+namespace {
+
+constexpr int kSortBits = 8, kSortBins = 1 << kSortBits;
+constexpr int kSortThreads = 256, kSortRounds = 16, kSortTile = kSortThreads * kSortRounds;
+
+__global__ void __launch_bounds__(kSortThreads) k_sort_hist(const unsigned* __restrict__ keys, int64_t n, int shift,
+                                                            unsigned* __restrict__ hist, int ntiles) {
+  __shared__ unsigned cnt[kSortBins];
+  const int tid = threadIdx.x, tile = blockIdx.x;
+  cnt[tid] = 0;
+  __syncthreads();
+  const int64_t t0 = (int64_t)tile * kSortTile;
+#pragma unroll 4
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int64_t i = t0 + r * kSortThreads + tid;
+    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & (kSortBins - 1)], 1u);
+  }
+  __syncthreads();
+  hist[(int64_t)tid * ntiles + tile] = cnt[tid];
+}
+
+// Per digit (one workgroup each): in-place exclusive scan of the digit's tile
+// counts hist[d][0 .. ntiles) and the digit's total -> tot[d].
+__global__ void __launch_bounds__(kSortThreads) k_sort_scan(unsigned* __restrict__ hist, int ntiles,
+                                                            unsigned* __restrict__ tot) {
+  __shared__ unsigned part[kSortThreads];
+  const int t = threadIdx.x;
+  unsigned* row = hist + (int64_t)blockIdx.x * ntiles;
+  unsigned carry = 0;
+  for (int c0 = 0; c0 < ntiles; c0 += kSortThreads) {
+    const int i = c0 + t;
+    const unsigned v = i < ntiles ? row[i] : 0u;
+    part[t] = v;
+    __syncthreads();
+    for (int off = 1; off < kSortThreads; off <<= 1) {  // inclusive scan of this chunk
+      const unsigned u = t >= off ? part[t - off] : 0u;
+      __syncthreads();
+      part[t] += u;
+      __syncthreads();
+    }
+    if (i < ntiles) row[i] = carry + part[t] - v;
+    carry += part[kSortThreads - 1];
+    __syncthreads();
+  }
+  if (t == 0) tot[blockIdx.x] = carry;
+}
+
+__global__ void __launch_bounds__(kSortThreads) k_sort_scatter(const unsigned* __restrict__ kin,
+                                                               const unsigned long long* __restrict__ vin,
+                                                               unsigned* __restrict__ kout,
+                                                               unsigned long long* __restrict__ vout, int64_t n,
+                                                               int shift, const unsigned* __restrict__ hist,
+                                                               int ntiles, const unsigned* __restrict__ tot) {
+  constexpr int NW = kSortThreads / 64;
+  __shared__ unsigned base[kSortBins];
+  __shared__ unsigned wcnt[NW][kSortBins];
+  const int tid = threadIdx.x, tile = blockIdx.x, w = tid >> 6, lane = tid & 63;
+  // base[d] = keys of smaller digits (exclusive scan of the totals) + this digit in earlier tiles
+  const unsigned td = tot[tid];
+  base[tid] = td;
+  __syncthreads();
+  for (int off = 1; off < kSortBins; off <<= 1) {
+    const unsigned u = tid >= off ? base[tid - off] : 0u;
+    __syncthreads();
+    base[tid] += u;
+    __syncthreads();
+  }
+  const unsigned dpre = base[tid] - td;
+  __syncthreads();
+  base[tid] = dpre + hist[(int64_t)tid * ntiles + tile];
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const int64_t t0 = (int64_t)tile * kSortTile;
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int64_t i = t0 + r * kSortThreads + tid;
+    const bool ok = i < n;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) wcnt[q][tid] = 0;
+    unsigned key = 0;
+    unsigned long long val = 0;
+    if (ok) {
+      key = kin[i];
+      val = vin[i];
+    }
+    const unsigned d = (key >> shift) & (kSortBins - 1);
+    // lanes of this wave holding a valid key with the same digit
+    unsigned long long peers = __ballot(ok);
+#pragma unroll
+    for (int bit = 0; bit < kSortBits; ++bit) {
+      const bool set = (d >> bit) & 1u;
+      const unsigned long long m = __ballot(set);
+      peers &= set ? m : ~m;
+    }
+    __syncthreads();  // wcnt zeroed (and the previous round's base update visible)
+    if (ok && (peers & lt) == 0) wcnt[w][d] = (unsigned)__popcll(peers);  // the digit's lowest lane
+    __syncthreads();
+    if (ok) {
+      unsigned pos = base[d] + (unsigned)__popcll(peers & lt);
+#pragma unroll
+      for (int q = 0; q < NW; ++q)
+        if (q < w) pos += wcnt[q][d];
+      kout[pos] = key;
+      vout[pos] = val;
+    }
+    __syncthreads();  // every slot of this round computed from the old base
+    unsigned add = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) add += wcnt[q][tid];
+    base[tid] += add;
+  }
+}
+
+}  // namespace
+
+// Workspace of sort_pairs: the digit histograms (digit-major, one per pass, reused).
+size_t sort_pairs_workspace(int64_t n) {
+  const int64_t ntiles = (n + kSortTile - 1) / kSortTile;
+  return ((size_t)kSortBins * (size_t)(ntiles > 0 ? ntiles : 1) + kSortBins) * sizeof(unsigned);
+}
+
+// Sorts (k0, v0) by the low end_bit bits of the keys, stably, ping-ponging
+// through (k1, v1); returns in *kres / *vres which pair of buffers holds the
+// result.  end_bit <= 32.
+int sort_pairs(unsigned* k0, unsigned long long* v0, unsigned* k1, unsigned long long* v1, int64_t n, int end_bit,
+               void* ws, unsigned** kres, unsigned long long** vres, hipStream_t s) {
+  *kres = k0;
+  *vres = v0;
+  if (n <= 0) return GRK_OK;
+  GRK_CHECK_ARG(end_bit >= 1 && end_bit <= 32, "end_bit must be in [1, 32]");
+  GRK_CHECK_ARG(n < ((int64_t)1 << 31), "too many keys");
+  const int64_t ntiles64 = (n + kSortTile - 1) / kSortTile;
+  GRK_CHECK_ARG(ntiles64 < (1 << 24), "too many tiles");
+  const int ntiles = (int)ntiles64;
+  unsigned* hist = (unsigned*)ws;
+  unsigned* tot = hist + (size_t)kSortBins * ntiles;
+  unsigned* kin = k0;
+  unsigned* kout = k1;
+  unsigned long long* vin = v0;
+  unsigned long long* vout = v1;
+  for (int shift = 0; shift < end_bit; shift += kSortBits) {
+    k_sort_hist<<<ntiles, kSortThreads, 0, s>>>(kin, n, shift, hist, ntiles);
+    GRK_LAUNCH_CHECK();
+    k_sort_scan<<<kSortBins, kSortThreads, 0, s>>>(hist, ntiles, tot);
+    GRK_LAUNCH_CHECK();
+    k_sort_scatter<<<ntiles, kSortThreads, 0, s>>>(kin, vin, kout, vout, n, shift, hist, ntiles, tot);
+    GRK_LAUNCH_CHECK();
+    unsigned* tk = kin;
+    kin = kout;
+    kout = tk;
+    unsigned long long* tv = vin;
+    vin = vout;
+    vout = tv;
+  }
+  *kres = kin;
+  *vres = vin;
+  return GRK_OK;
+}
+
+}  // namespace grk
+
+using namespace grk;
+
+extern "C" size_t grk_sort_pairs_workspace(int64_t n) { return sort_pairs_workspace(n); }
+
+extern "C" int grk_sort_pairs(const uint32_t* keys_in, const uint64_t* vals_in, uint32_t* keys_out, uint64_t* vals_out,
+                              uint32_t* keys_tmp, uint64_t* vals_tmp, int64_t n, int end_bit, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(n >= 0, "n must be >= 0");
+  if (n == 0) return GRK_OK;
+  GRK_CHECK_ARG(keys_in && vals_in && keys_out && vals_out && keys_tmp && vals_tmp, "buffers are required");
+  GRK_CHECK_ARG(workspace && workspace_bytes >= sort_pairs_workspace(n), "workspace smaller than grk_sort_pairs_workspace()");
+  hipStream_t s = (hipStream_t)stream;
+  // passes alternate out <-> tmp, starting from the caller's input: the pass
+  // count's parity decides which buffer starts, so the result lands in out
+  const int passes = (end_bit + kSortBits - 1) / kSortBits;
+  unsigned* a = (unsigned*)(passes % 2 ? keys_tmp : keys_out);
+  unsigned long long* va = (unsigned long long*)(passes % 2 ? vals_tmp : vals_out);
+  unsigned* b = (unsigned*)(passes % 2 ? keys_out : keys_tmp);
+  unsigned long long* vb = (unsigned long long*)(passes % 2 ? vals_out : vals_tmp);
+  GRK_CHECK_HIP(hipMemcpyAsync(a, keys_in, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+  GRK_CHECK_HIP(hipMemcpyAsync(va, vals_in, (size_t)n * 8, hipMemcpyDeviceToDevice, s));
+  unsigned* kr;
+  unsigned long long* vr;
+  return sort_pairs(a, va, b, vb, n, end_bit, workspace, &kr, &vr, s);
+}

@@ -161,6 +161,23 @@ def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, s
     return BackwardResult(dense_out, ids, rows, count, cap)
 
 
+def sort_pairs(keys, vals, end_bit=32):
+    """grk_sort_pairs: (keys, vals) stably sorted by the low ``end_bit`` bits of
+    the keys (uint32 keys as int32, uint64 values as int64 tensors)."""
+    _require_cuda(keys, vals)
+    if keys.dtype != torch.int32 or vals.dtype != torch.int64 or keys.dim() != 1 or vals.shape != keys.shape:
+        raise L.GrkError('sort_pairs takes int32 keys and int64 values of the same length')
+    keys, vals = keys.contiguous(), vals.contiguous()
+    n = keys.numel()
+    ko, vo = torch.empty_like(keys), torch.empty_like(vals)
+    kt, vt = torch.empty_like(keys), torch.empty_like(vals)
+    wsb = L.lib().grk_sort_pairs_workspace(n)
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=keys.device)
+    L.check(L.lib().grk_sort_pairs(_ptr(keys), _ptr(vals), _ptr(ko), _ptr(vo), _ptr(kt), _ptr(vt), n, int(end_bit),
+                                   ws.data_ptr(), ws.numel(), L.stream_ptr(keys.device)), 'grk_sort_pairs')
+    return ko, vo
+
+
 def adamw_hparams(lr, beta1, beta2, eps, weight_decay, step):
     bc1 = 1.0 - beta1 ** step
     bc2 = 1.0 - beta2 ** step

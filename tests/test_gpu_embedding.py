@@ -269,3 +269,30 @@ def test_hot_rows_bit_exact(K):
     assert torch.equal(a.dense, b.dense)
     want = oemb.dense_backward(np.concatenate([gr[:, :D], gr[:, D:]]), np.concatenate([idx, idx[::-1]]), R)
     assert np.array_equal(a.dense.cpu().numpy(), want)
+
+
+# ------------------------------------------------ occurrence sort (grk_sort) --
+@pytest.mark.parametrize('n,end_bit,card', [(1, 1, 2), (4095, 8, 200), (4097, 9, 300), (70001, 16, 40000),
+                                            (200000, 21, 1000001), (150000, 21, 10), (33333, 32, 1 << 31)])
+def test_sort_pairs_is_stable_and_exact(n, end_bit, card):
+    """grk_sort_pairs (the embedding backward's occurrence grouping) against
+    numpy's stable argsort: keys and values identical, ties in input order --
+    hot keys (card 10: every key repeated ~15k times), tile-boundary sizes,
+    1- to 32-bit keys."""
+    from tencent_recommendation_2025_amd import kernels as K
+    rng = np.random.default_rng(n + end_bit)
+    keys = rng.integers(0, min(card, 1 << end_bit), n, dtype=np.int64).astype(np.uint32)
+    vals = rng.integers(0, 1 << 62, n, dtype=np.int64)
+    kd = torch.from_numpy(keys.view(np.int32)).to(DEV)
+    vd = torch.from_numpy(vals).to(DEV)
+    ko, vo = K.sort_pairs(kd, vd, end_bit)
+    order = np.argsort(keys & np.uint32((1 << end_bit) - 1) if end_bit < 32 else keys, kind='stable')
+    assert np.array_equal(ko.cpu().numpy().view(np.uint32), keys[order])
+    assert np.array_equal(vo.cpu().numpy(), vals[order])
+    assert np.array_equal(kd.cpu().numpy().view(np.uint32), keys)  # input untouched
+
+
+def test_sort_pairs_empty():
+    from tencent_recommendation_2025_amd import kernels as K
+    k, v = K.sort_pairs(torch.empty(0, dtype=torch.int32, device=DEV), torch.empty(0, dtype=torch.int64, device=DEV))
+    assert k.numel() == 0 and v.numel() == 0
