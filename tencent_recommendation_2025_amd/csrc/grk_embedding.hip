@@ -9,8 +9,7 @@
 //
 // Both directions are HBM-bound byte movers: one 16-byte vector per lane,
 // consecutive lanes on consecutive bytes of one row, no LDS, no MFMA.
-#include <string.h>  // rocprim/iterator/texture_cache_iterator.hpp uses memset without it
-#include <rocprim/rocprim.hpp>
+#include <string.h>
 
 #include "grk_common.h"
 
@@ -132,13 +131,6 @@ __global__ void k_build_keys(LookupArgs la, int esize, const int32_t* __restrict
   }
   keys[o] = key;
   gptr[o] = (unsigned long long)((const char*)L.grad + (n * L.grad_ld + L.grad_col) * esize);
-}
-
-__global__ void k_mark_heads(const unsigned* __restrict__ keys, int* __restrict__ flags, int64_t n, unsigned sentinel) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  unsigned k = keys[i];
-  flags[i] = (k != sentinel && (i == 0 || keys[i - 1] != k)) ? 1 : 0;
 }
 
 __global__ void k_segments(const unsigned* __restrict__ keys, const int* __restrict__ pos, int64_t n,
@@ -650,6 +642,9 @@ __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ key
 size_t sort_pairs_workspace(int64_t n);
 int sort_pairs(unsigned* k0, unsigned long long* v0, unsigned* k1, unsigned long long* v1, int64_t n, int end_bit,
                void* ws, unsigned** kres, unsigned long long** vres, hipStream_t s);
+// Segment index of every sorted entry (inclusive count of row heads).
+size_t head_positions_workspace(int64_t n);
+int head_positions(const unsigned* keys, int64_t n, unsigned sentinel, int* pos, void* ws, hipStream_t s);
 
 struct BwdWs {
   unsigned *keys_in, *keys_out, *seg_key;
@@ -685,9 +680,7 @@ static int plan_ws(int64_t n, int64_t num_rows, int dim, char* base, BwdWs* ws) 
   size_t sb = 0, cb = 0;
   if (n > 0) {
     sb = sort_pairs_workspace(n);
-    if (rocprim::inclusive_scan(nullptr, cb, (int*)nullptr, (int*)nullptr, (size_t)n, rocprim::plus<int>()) !=
-        hipSuccess)
-      return GRK_EHIP;
+    cb = head_positions_workspace(n);
   }
   ws->sort_bytes = sb;
   ws->sort_tmp = take(sb);
@@ -787,7 +780,7 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   GRK_CHECK_ARG(total < 0x7FFFFFFFLL, "too many occurrences");
   BwdWs ws;
   if (plan_ws(total, num_rows, dim, nullptr, &ws) != GRK_OK) {
-    set_error("rocprim workspace query failed");
+    set_error("workspace query failed");
     return GRK_EHIP;
   }
   GRK_CHECK_ARG(workspace_bytes >= ws.total + 256 && workspace, "workspace too small (%zu < %zu)", workspace_bytes,
@@ -835,10 +828,10 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   ws.keys_out = skeys;  // the sorted pairs (either buffer of the ping-pong)
   ws.gptr_out = sgptr;
   const unsigned sentinel = (unsigned)num_rows;
-  k_mark_heads<<<g, B, 0, s>>>(ws.keys_out, ws.flags, total, sentinel);
-  GRK_LAUNCH_CHECK();
-  size_t cb = ws.scan_bytes;
-  GRK_CHECK_HIP(rocprim::inclusive_scan(ws.scan_tmp, cb, ws.flags, ws.pos, (size_t)total, rocprim::plus<int>(), s));
+  {
+    const int rc = head_positions(ws.keys_out, total, sentinel, ws.pos, ws.scan_tmp, s);
+    if (rc) return rc;
+  }
   k_segments<<<g, B, 0, s>>>(ws.keys_out, ws.pos, total, sentinel, ws.seg_start, ws.seg_end, ws.seg_key, uniq_ids,
                              uniq_count);
   GRK_LAUNCH_CHECK();

@@ -8,11 +8,11 @@
 // rocprim::radix_sort_pairs took ~15 launches per call at these sizes (73
 // launches, ~0.5 ms per C2 training step over five calls).  Here a pass per
 // 8-bit digit is three launches:
-//   k_sort_hist    per 4096-key tile: digit counts -> hist[digit][tile]
+//   k_sort_hist    per 1024-key tile: digit counts -> hist[digit][tile]
 //   k_sort_scan    one workgroup per digit: exclusive scan of the digit's
 //                  tile counts, and the digit's total (the scatter's prologue
 //                  prefixes the 256 totals)
-//   k_sort_scatter per tile, 16 rounds of 256 keys in index order: a key's
+//   k_sort_scatter per tile, 4 rounds of 256 keys in index order: a key's
 //                  slot = its (digit, tile) base + the keys of its digit in
 //                  earlier rounds, earlier waves of this round, and lower
 //                  lanes of its wave (wave ballots over the 8 digit bits)
@@ -24,7 +24,7 @@ namespace grk {
 namespace {
 
 constexpr int kSortBits = 8, kSortBins = 1 << kSortBits;
-constexpr int kSortThreads = 256, kSortRounds = 16, kSortTile = kSortThreads * kSortRounds;
+constexpr int kSortThreads = 256, kSortRounds = 4, kSortTile = kSortThreads * kSortRounds;
 
 __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const unsigned* __restrict__ keys, int64_t n, int shift,
                                                             unsigned* __restrict__ hist, int ntiles) {
@@ -132,7 +132,86 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_scatter(const unsigned* _
   }
 }
 
+// Head positions of a sorted key list (the segment index of every entry):
+// pos[i] = #{j <= i : key[j] != sentinel and (j == 0 or key[j-1] != key[j])}.
+// Per 1024-entry tile (4 consecutive entries per thread): head counts, one
+// scan over the tiles (k_sort_scan with one row), then in-tile prefix sums.
+__device__ __forceinline__ void head_flags(const unsigned* __restrict__ keys, int64_t n, unsigned sentinel,
+                                           int64_t i0, int* f) {
+  unsigned prev = i0 > 0 && i0 - 1 < n ? keys[i0 - 1] : 0u;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t i = i0 + e;
+    const unsigned k = i < n ? keys[i] : sentinel;
+    f[e] = (i < n && k != sentinel && (i == 0 || prev != k)) ? 1 : 0;
+    prev = k;
+  }
+}
+
+__global__ void __launch_bounds__(kSortThreads) k_head_count(const unsigned* __restrict__ keys, int64_t n,
+                                                             unsigned sentinel, unsigned* __restrict__ cnt) {
+  __shared__ unsigned red[kSortThreads / 64];
+  const int t = threadIdx.x;
+  int f[4];
+  head_flags(keys, n, sentinel, (int64_t)blockIdx.x * kSortTile + 4 * t, f);
+  unsigned c = f[0] + f[1] + f[2] + f[3];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((t & 63) == 0) red[t >> 6] = c;
+  __syncthreads();
+  if (t == 0) {
+    unsigned sum = 0;
+#pragma unroll
+    for (int w = 0; w < kSortThreads / 64; ++w) sum += red[w];
+    cnt[blockIdx.x] = sum;
+  }
+}
+
+__global__ void __launch_bounds__(kSortThreads) k_head_pos(const unsigned* __restrict__ keys, int64_t n,
+                                                           unsigned sentinel, const unsigned* __restrict__ off,
+                                                           int* __restrict__ pos) {
+  __shared__ unsigned part[kSortThreads];
+  const int t = threadIdx.x;
+  const int64_t i0 = (int64_t)blockIdx.x * kSortTile + 4 * t;
+  int f[4];
+  head_flags(keys, n, sentinel, i0, f);
+  const unsigned c = f[0] + f[1] + f[2] + f[3];
+  part[t] = c;
+  __syncthreads();
+  for (int o = 1; o < kSortThreads; o <<= 1) {
+    const unsigned u = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += u;
+    __syncthreads();
+  }
+  unsigned run = off[blockIdx.x] + part[t] - c;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    run += f[e];
+    if (i0 + e < n) pos[i0 + e] = (int)run;
+  }
+}
+
 }  // namespace
+
+// Workspace of head_positions: one count per tile + the total.
+size_t head_positions_workspace(int64_t n) {
+  return ((size_t)((n + kSortTile - 1) / kSortTile) + 1) * sizeof(unsigned);
+}
+
+int head_positions(const unsigned* keys, int64_t n, unsigned sentinel, int* pos, void* ws, hipStream_t s) {
+  if (n <= 0) return GRK_OK;
+  GRK_CHECK_ARG(n < ((int64_t)1 << 31), "too many keys");
+  const int ntiles = (int)((n + kSortTile - 1) / kSortTile);
+  unsigned* cnt = (unsigned*)ws;
+  k_head_count<<<ntiles, kSortThreads, 0, s>>>(keys, n, sentinel, cnt);
+  GRK_LAUNCH_CHECK();
+  k_sort_scan<<<1, kSortThreads, 0, s>>>(cnt, ntiles, cnt + ntiles);
+  GRK_LAUNCH_CHECK();
+  k_head_pos<<<ntiles, kSortThreads, 0, s>>>(keys, n, sentinel, cnt, pos);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
 
 // Workspace of sort_pairs: the digit histograms (digit-major, one per pass, reused).
 size_t sort_pairs_workspace(int64_t n) {
