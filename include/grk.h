@@ -39,6 +39,7 @@ extern "C" {
 
 enum { GRK_OK = 0, GRK_EINVAL = 1, GRK_EHIP = 2, GRK_EUNSUPPORTED = 3 };
 enum { GRK_F32 = 0, GRK_BF16 = 1, GRK_F16 = 2 };    /* floating dtypes */
+enum { GRK_F32_BF16 = 3 };  /* pair logits: fp32 h, bf16 e_pos / e_neg (and their gradients) */
 enum { GRK_I32 = 0, GRK_I64 = 1 };                  /* index dtypes */
 
 /* How a lookup derives its row id from the index tensor value v at token
@@ -353,7 +354,8 @@ size_t grk_pair_logits_partials(int64_t num_rows);
  * next_token_type[n] != 1 (NULL: every row valid).  If `loss` is non-NULL it
  * also writes the reference BCE loss (mean over valid rows of
  * softplus(-pos) plus mean of softplus(neg)) and the valid-row count, reduced
- * in a fixed order.  Inputs share `dtype`. */
+ * in a fixed order.  Inputs share `dtype`, or GRK_F32_BF16: h fp32, e_pos /
+ * e_neg bf16 (the same logits as promoting e to fp32, bitwise). */
 int grk_pair_logits_fwd(const void* h, int64_t ldh, const void* e_pos, int64_t ldp, const void* e_neg, int64_t ldn,
                         const int32_t* next_token_type, int64_t num_rows, int dim, int dtype, float* pos_logits,
                         float* neg_logits, float* partials, float* loss, int32_t* count, void* stream);
@@ -363,7 +365,8 @@ int grk_pair_logits_fwd(const void* h, int64_t ldh, const void* e_pos, int64_t l
  * next_token_type != 1 get 0, as the forward masked them) are given, or -- when
  * pos_logits/neg_logits are non-NULL -- the BCE coefficients
  * gp = g*(sigmoid(pos)-1)/count, gn = g*sigmoid(neg)/count on valid rows,
- * with g = *grad_loss (device scalar; NULL = 1).  Outputs may be NULL. */
+ * with g = *grad_loss (device scalar; NULL = 1).  Outputs may be NULL; with
+ * GRK_F32_BF16, dh is fp32 and de_pos / de_neg bf16. */
 int grk_pair_logits_bwd(const void* h, int64_t ldh, const void* e_pos, int64_t ldp, const void* e_neg, int64_t ldn,
                         int64_t num_rows, int dim, int dtype, const float* gpos, const float* gneg,
                         const float* pos_logits, const float* neg_logits, const int32_t* next_token_type,

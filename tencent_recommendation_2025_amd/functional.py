@@ -356,8 +356,13 @@ def pair_logits(h, e_pos, e_neg, next_token_type):
 class _BCELossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, ep, en, ntt):
-        dt = torch.promote_types(torch.promote_types(h.dtype, ep.dtype), en.dtype)
-        h2, p2, n2 = (_rows2d(x.to(dt)) for x in (h, ep, en))
+        if h.dtype == torch.float32 and ep.dtype == en.dtype == torch.bfloat16:
+            # fp32 log_feats, bf16 item embeddings (autocast): the kernels read both as they are
+            # (the logits of promoting e to fp32, bitwise, without the casts)
+            h2, p2, n2 = _rows2d(h), _rows2d(ep), _rows2d(en)
+        else:
+            dt = torch.promote_types(torch.promote_types(h.dtype, ep.dtype), en.dtype)
+            h2, p2, n2 = (_rows2d(x.to(dt)) for x in (h, ep, en))
         pos, neg, loss, count = K.pair_logits_fwd(h2, p2, n2, ntt, with_loss=True)
         ctx.save_for_backward(h2, p2, n2, pos, neg, ntt, count)
         ctx.dtypes = (h.dtype, ep.dtype, en.dtype)

@@ -589,9 +589,21 @@ def _rows(t, name):
     return t.data_ptr(), t.stride(0)
 
 
+def _pair_dtype(h, e_pos, e_neg):
+    if e_pos.dtype != e_neg.dtype:
+        raise L.GrkError('e_pos and e_neg must share a dtype')
+    if h.dtype == torch.float32 and e_pos.dtype == torch.bfloat16:
+        return L.GRK_F32_BF16
+    if h.dtype != e_pos.dtype:
+        raise L.GrkError('pair logits take h and e of one dtype, or fp32 h with bf16 e')
+    return L.dtype_code(h.dtype)
+
+
 def pair_logits_fwd(h, e_pos, e_neg, next_token_type=None, with_loss=False):
-    """Returns (pos_logits, neg_logits[, loss, count]) -- grk_pair_logits_fwd."""
+    """Returns (pos_logits, neg_logits[, loss, count]) -- grk_pair_logits_fwd.
+    h and e share a dtype, or h is fp32 and e bf16 (read as they are)."""
     _require_cuda(h, e_pos, e_neg, next_token_type)
+    dt = _pair_dtype(h, e_pos, e_neg)
     N, D = h.shape
     dev = h.device
     pos = torch.empty(N, dtype=torch.float32, device=dev)
@@ -603,7 +615,7 @@ def pair_logits_fwd(h, e_pos, e_neg, next_token_type=None, with_loss=False):
         count = torch.empty(1, dtype=torch.int32, device=dev)
     ntt = None if next_token_type is None else next_token_type.to(torch.int32).contiguous()
     (hp, hl), (pp, pl), (np_, nl) = _rows(h, 'h'), _rows(e_pos, 'e_pos'), _rows(e_neg, 'e_neg')
-    rc = L.lib().grk_pair_logits_fwd(hp, hl, pp, pl, np_, nl, _ptr(ntt), N, D, L.dtype_code(h.dtype),
+    rc = L.lib().grk_pair_logits_fwd(hp, hl, pp, pl, np_, nl, _ptr(ntt), N, D, dt,
                                      pos.data_ptr(), neg.data_ptr(), _ptr(part), _ptr(loss), _ptr(count),
                                      L.stream_ptr(dev))
     L.check(rc, 'grk_pair_logits_fwd')
@@ -612,17 +624,19 @@ def pair_logits_fwd(h, e_pos, e_neg, next_token_type=None, with_loss=False):
 
 def pair_logits_bwd(h, e_pos, e_neg, gpos=None, gneg=None, pos_logits=None, neg_logits=None, next_token_type=None,
                     count=None, grad_loss=None, need=(True, True, True)):
-    """Returns (dh, de_pos, de_neg) -- grk_pair_logits_bwd (None where not needed)."""
+    """Returns (dh, de_pos, de_neg) -- grk_pair_logits_bwd (None where not needed);
+    each gradient in its input's dtype."""
     _require_cuda(h, e_pos, e_neg, gpos, gneg, pos_logits, neg_logits, count, grad_loss)
+    dt = _pair_dtype(h, e_pos, e_neg)
     N, D = h.shape
-    outs = [torch.empty(N, D, dtype=h.dtype, device=h.device) if n else None for n in need]
+    outs = [torch.empty(N, D, dtype=x.dtype, device=h.device) if n else None for n, x in zip(need, (h, e_pos, e_neg))]
     ntt = None if next_token_type is None else next_token_type.to(torch.int32).contiguous()
     gpos = None if gpos is None else gpos.float().contiguous()
     gneg = None if gneg is None else gneg.float().contiguous()
     gl = None if grad_loss is None else grad_loss.float().reshape(1).contiguous()
     (hp, hl), (pp, pl), (np_, nl) = _rows(h, 'h'), _rows(e_pos, 'e_pos'), _rows(e_neg, 'e_neg')
     (a, al), (b, bl), (c, cl) = _rows(outs[0], 'dh'), _rows(outs[1], 'de_pos'), _rows(outs[2], 'de_neg')
-    rc = L.lib().grk_pair_logits_bwd(hp, hl, pp, pl, np_, nl, N, D, L.dtype_code(h.dtype), _ptr(gpos), _ptr(gneg),
+    rc = L.lib().grk_pair_logits_bwd(hp, hl, pp, pl, np_, nl, N, D, dt, _ptr(gpos), _ptr(gneg),
                                      _ptr(pos_logits), _ptr(neg_logits), _ptr(ntt), _ptr(count), _ptr(gl), a, al, b,
                                      bl, c, cl, L.stream_ptr(h.device))
     L.check(rc, 'grk_pair_logits_bwd')

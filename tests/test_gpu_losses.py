@@ -52,6 +52,30 @@ def test_pair_logits_and_bce(K, dtype):
     assert nrel(th.grad.float().cpu().numpy(), want) < tol
 
 
+def test_bce_mixed_dtypes_equal_promoted(K):
+    """fp32 h with bf16 item embeddings (the bench's autocast dtypes): the kernels
+    read them as they are (GRK_F32_BF16) -- loss and dh bitwise those of promoting
+    e to fp32, de_pos / de_neg the promoted run's fp32 gradients rounded to bf16."""
+    from tencent_recommendation_2025_amd import functional as G
+    rng = np.random.default_rng(2)
+    N, D = 2050, 512
+    h = torch.from_numpy(rng.standard_normal((N, D)).astype(np.float32) * 0.3).to(DEV)
+    ep, en = (torch.from_numpy(rng.standard_normal((N, D)).astype(np.float32) * 0.3).to(DEV).bfloat16()
+              for _ in range(2))
+    ntt = torch.from_numpy((rng.random(N) < 0.7).astype(np.int64)).to(DEV)
+    runs = []
+    for mixed in (True, False):
+        th = h.clone().requires_grad_(True)
+        tp = (ep if mixed else ep.float()).clone().requires_grad_(True)
+        tn = (en if mixed else en.float()).clone().requires_grad_(True)
+        loss = G.bce_loss(th, tp, tn, ntt)
+        loss.backward()
+        runs.append((loss.detach(), th.grad, tp.grad, tn.grad))
+    (lm, hm, pm, nm), (lf, hf, pf, nf) = runs
+    assert torch.equal(lm, lf) and torch.equal(hm, hf)
+    assert pm.dtype == torch.bfloat16 and torch.equal(pm, pf.bfloat16()) and torch.equal(nm, nf.bfloat16())
+
+
 def sampled_case(M, D, seed, frac_valid=0.6, dup_every=7):
     rng = np.random.default_rng(seed)
     h = to_bf16_f32(rng.standard_normal((M, D)).astype(np.float32) * 0.2)
