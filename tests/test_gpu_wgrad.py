@@ -15,7 +15,8 @@ def nrel(a, b):
 
 
 @pytest.mark.parametrize('K,M,N', [(25728, 2048, 512), (25728, 512, 512), (51456, 512, 560), (1000, 136, 72),
-                                   (3, 8, 8), (0, 16, 24), (777, 264, 1032)])
+                                   (3, 8, 8), (0, 16, 24), (777, 264, 1032),
+                                   (5000, 1032, 1288), (25728, 1024, 1024), (300, 2048, 520)])
 def test_wgrad_matches_fp64(K, M, N):
     from tencent_recommendation_2025_amd import kernels as Kn
     g = torch.Generator(device=DEV).manual_seed(K + M + N)
