@@ -258,6 +258,19 @@ typedef struct grk_attn_args {
   int32_t qkv_dtype;               /* precise == 2: GRK_F32 / GRK_F16 / GRK_BF16
                                       q/k/v (read exactly, split into bf16 hi+lo);
                                       ignored otherwise (bf16)                  */
+  /* HSTU time bias (SURVEY §8 a9 rab_time; whole-sequence kernels only,
+   * GRK_EUNSUPPORTED elsewhere): S[i,j] += rab_t[h, tb(ts[i] - ts[j])] with
+   * tb(d) = min(2 l + h1, num_time_buckets - 1), l = floor(log2(|d| + 1)),
+   * h1 = the bit below the leading one of |d| + 1 (0 when l = 0): half-octave
+   * buckets of the time gap, integer-exact.  Gaps are taken of the times
+   * relative to the sequence's first valid event, clamped to +-(2^30 - 1). */
+  const int64_t* timestamps;       /* [batch, seq_len] event times or NULL        */
+  const float* rab_t;              /* [heads, num_time_buckets] fp32              */
+  int32_t num_time_buckets;        /* 0 = no time bias; <= 64                     */
+  float* drab_t;                   /* backward: [heads, num_time_buckets] fp32,
+                                      the time-bias gradient is ADDED into it    */
+  int64_t* drab_t_ws;              /* backward: int64 [heads, num_time_buckets]
+                                      scratch (fixed-point accumulator)          */
 } grk_attn_args;
 
 /* 1 when grk_attention_* with precise == 2 (fp32 fidelity) runs for this

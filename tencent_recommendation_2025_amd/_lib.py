@@ -53,7 +53,9 @@ class GrkAttnArgs(C.Structure):
                 ('v', C.c_void_p), ('ldq', C.c_int64), ('ldk', C.c_int64), ('ldv', C.c_int64),
                 ('key_valid', C.c_void_p), ('rab', C.c_void_p), ('scale', C.c_float), ('inv_n', C.c_float),
                 ('dropout_p', C.c_float), ('precise', C.c_int32), ('seed', C.c_uint64), ('out_dtype', C.c_int32),
-                ('act', C.c_int32), ('seq_range', C.c_void_p), ('seed_dev', C.c_void_p), ('qkv_dtype', C.c_int32)]
+                ('act', C.c_int32), ('seq_range', C.c_void_p), ('seed_dev', C.c_void_p), ('qkv_dtype', C.c_int32),
+                ('timestamps', C.c_void_p), ('rab_t', C.c_void_p), ('num_time_buckets', C.c_int32),
+                ('drab_t', C.c_void_p), ('drab_t_ws', C.c_void_p)]
 
 
 ATTN_SOFTMAX, ATTN_HSTU = 0, 1

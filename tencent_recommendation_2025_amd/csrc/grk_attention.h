@@ -27,6 +27,12 @@ struct AttnParams {
   int act;  // GRK_ACT_SILU: q/k/v are pre-activations
   const int* seq_range;  // optional [B, 3] (first valid key, contiguous flag; longest-first order)
   unsigned long long* drab_fix;  // [H, nb] int64 fixed-point drab accumulator (deterministic)
+  // HSTU time bias (whole-sequence kernels): S += rab_t[h, time_bucket(ts_q - ts_k)]
+  const int64_t* ts;
+  const float* rab_t;
+  int nbt;                           // 0 = off
+  float* drab_t;
+  unsigned long long* drab_t_fix;    // [H, nbt] fixed point
   // forward
   void* out; int64_t ldo; float* lse;
   // backward
@@ -197,6 +203,16 @@ inline void launch_lds(void (*kernel)(AttnParams), dim3 grid, int threads, size_
     }
   }
   kernel<<<grid, threads, lds, s>>>(p);
+}
+
+constexpr int kMaxTimeBuckets = 64;
+
+// Half-octave bucket of a time gap (grk.h, grk_attn_args.timestamps).
+__device__ __forceinline__ int time_bucket(int d, int nbt) {
+  const unsigned x = (unsigned)(d < 0 ? -d : d) + 1u;
+  const int l = 31 - __clz(x);
+  const int h1 = l > 0 ? (int)((x >> (l - 1)) & 1u) : 0;
+  return min(2 * l + h1, nbt - 1);
 }
 
 // Whole-sequence kernels (grk_attention_seq.hip): one workgroup per

@@ -424,6 +424,11 @@ static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
     GRK_LAUNCH_CHECK();
     return GRK_OK;
   }
+  if (p.nbt > 0 && which != 1) {
+    set_error("the HSTU time bias runs in the whole-sequence kernels only: T = %d x head_dim %d does not fit them",
+              p.T, hd);
+    return GRK_EUNSUPPORTED;
+  }
   if (p.precise == 2 && which != 1 && hd <= 128) {
     set_error("fp32-fidelity attention (precise = 2) runs in the whole-sequence kernels only: T = %d x head_dim %d "
               "does not fit their LDS", p.T, hd);
@@ -470,8 +475,15 @@ static int fill_params(const grk_attn_args* a, AttnParams* p) {
   GRK_CHECK_ARG(a->precise >= 0 && a->precise <= 2, "precise must be 0, 1 or 2");
   GRK_CHECK_ARG(a->precise != 2 || a->qkv_dtype == GRK_F32 || a->qkv_dtype == GRK_F16 || a->qkv_dtype == GRK_BF16,
                 "qkv_dtype must be GRK_F32 / GRK_F16 / GRK_BF16");
+  GRK_CHECK_ARG(a->num_time_buckets >= 0 && a->num_time_buckets <= kMaxTimeBuckets,
+                "num_time_buckets must be in [0, %d]", kMaxTimeBuckets);
+  GRK_CHECK_ARG(a->num_time_buckets == 0 || (a->kind == GRK_ATTN_HSTU && a->timestamps && a->rab_t),
+                "the time bias is an HSTU feature and needs timestamps and rab_t");
   memset(p, 0, sizeof(*p));
   p->kind = a->kind; p->B = a->batch; p->H = a->heads; p->T = a->seq_len;
+  if (a->num_time_buckets > 0) {
+    p->ts = a->timestamps; p->rab_t = a->rab_t; p->nbt = a->num_time_buckets;
+  }
   p->q = (const bf16_t*)a->q; p->k = (const bf16_t*)a->k; p->v = (const bf16_t*)a->v;
   p->ldq = a->ldq; p->ldk = a->ldk; p->ldv = a->ldv;
   p->key_valid = a->key_valid;
@@ -523,10 +535,14 @@ extern "C" int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, 
   GRK_CHECK_ARG(!do_dq || !drab || drab_ws, "drab needs drab_ws (int64 [H, nb] scratch)");
   p.drab = (a->kind == GRK_ATTN_HSTU && do_dq) ? drab : nullptr;
   p.drab_fix = reinterpret_cast<unsigned long long*>(drab_ws);
+  GRK_CHECK_ARG(!do_dq || p.nbt == 0 || !a->drab_t || a->drab_t_ws, "drab_t needs drab_t_ws (int64 [H, nbt] scratch)");
+  p.drab_t = (p.nbt > 0 && do_dq) ? a->drab_t : nullptr;
+  p.drab_t_fix = reinterpret_cast<unsigned long long*>(a->drab_t_ws);
   hipStream_t s = (hipStream_t)stream;
   if (do_dq) {
     const int nfix = a->heads * a->num_buckets;
     if (p.drab) GRK_CHECK_HIP(zero_async(drab_ws, (size_t)nfix * 8, s));
+    if (p.drab_t) GRK_CHECK_HIP(zero_async(a->drab_t_ws, (size_t)a->heads * p.nbt * 8, s));
     if (a->kind == GRK_ATTN_SOFTMAX) {
       // out dtype of the forward output equals out_dtype of these args
       rc = launch(p, a->head_dim, 1, s);
@@ -536,6 +552,11 @@ extern "C" int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, 
     if (rc) return rc;
     if (p.drab) {
       k_drab_finalize<<<(nfix + 255) / 256, 256, 0, s>>>(p.drab, p.drab_fix, nfix);
+      GRK_LAUNCH_CHECK();
+    }
+    if (p.drab_t) {
+      const int nt = a->heads * p.nbt;
+      k_drab_finalize<<<(nt + 255) / 256, 256, 0, s>>>(p.drab_t, p.drab_t_fix, nt);
       GRK_LAUNCH_CHECK();
     }
   }

@@ -160,6 +160,10 @@ struct SeqLds {
   float* f1;  // F1 x (Tp + kRabPad) floats (dQ: private drab bins per (wave, half-wave); dK/dV: delta)
   uint8_t* kvs;
   int* sh;
+  // time bias: times relative to the first valid event, the head's table, dQ's fixed-point bins
+  unsigned long long* tbins;
+  int* tss;
+  float* rtab;
   __device__ SeqLds(char* smem, int Tp, int F1 = 1) {
     img0 = smem;
     img1 = smem + Tp * HD * 2;
@@ -169,11 +173,32 @@ struct SeqLds {
     f1 = f0 + Tp + kRabPad;
     kvs = reinterpret_cast<uint8_t*>(f1 + F1 * (Tp + kRabPad));
     sh = reinterpret_cast<int*>(kvs + Tp);
+    tbins = reinterpret_cast<unsigned long long*>(sh + 16);  // 8-byte aligned: Tp % 32 == 0
+    tss = reinterpret_cast<int*>(tbins + kMaxTimeBuckets);
+    rtab = reinterpret_cast<float*>(tss + Tp);
   }
   static size_t bytes(int Tp, int F1 = 1) {
-    return (size_t)NIMG * Tp * HD * 2 + (size_t)((1 + F1) * (Tp + kRabPad)) * 4 + Tp + 16 * 4;
+    return (size_t)NIMG * Tp * HD * 2 + (size_t)((1 + F1) * (Tp + kRabPad)) * 4 + Tp + 16 * 4 +
+           kMaxTimeBuckets * 8 + (size_t)Tp * 4 + kMaxTimeBuckets * 4;
   }
 };
+
+// Time-bias staging: tss[j] = ts[b, j] - ts[b, start] clamped to +-(2^30 - 1)
+// (0 past T), the head's rab_t row, and (dQ) zeroed gradient bins.
+__device__ __forceinline__ void stage_time(const AttnParams& p, int b, int h, int T, int Tp, int start, int* tss,
+                                           float* rtab, unsigned long long* tbins) {
+  const int64_t base = start < T ? p.ts[(int64_t)b * T + start] : 0;
+  const int64_t lim = (1 << 30) - 1;
+  for (int j = threadIdx.x; j < Tp; j += blockDim.x) {
+    int64_t d = j < T ? p.ts[(int64_t)b * T + j] - base : 0;
+    d = d > lim ? lim : (d < -lim ? -lim : d);
+    tss[j] = (int)d;
+  }
+  for (int j = threadIdx.x; j < p.nbt; j += blockDim.x) {
+    rtab[j] = p.rab_t[h * p.nbt + j];
+    if (tbins) tbins[j] = 0ull;
+  }
+}
 
 // Fidelity mode: fragments of row `row` split into bf16 hi + lo (SiLU applied in fp32 first when act).
 template <int HD>
@@ -379,6 +404,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
   if (KIND == 1) {
     store_rab(L.f0, rr, Tp);
     stage_key_bias(L.f1, p.key_valid, si, b, T, Tp);
+    if (p.nbt) stage_time(p, b, h, T, Tp, start, L.tss, L.rtab, nullptr);
   }
   if (!si.contig) stage_kvs(L.kvs, p.key_valid, b, T, Tp);
   GRK_STAMP(2);
@@ -475,6 +501,11 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
           float rb[16];
           rab16(L.f0, myq, kb, hh, rb);
           const float* kbb = L.f1 + kb + 4 * hh;
+          if (p.nbt) {  // time bias: rab_t[h, bucket(t_q - t_k)]
+            const int tq = L.tss[myq < Tp ? myq : Tp - 1];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) rb[i] += L.rtab[time_bucket(tq - L.tss[kb + acc_row(i, hh)], p.nbt)];
+          }
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const float x = fmaf(s[i], p.scale, rb[i]) + kbb[(i & 3) + 8 * (i >> 2)];
@@ -538,6 +569,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
     store_rab(L.f0, rr, Tp);
     for (int j = threadIdx.x; j < Tp + kRabPad; j += blockDim.x) bins[j] = 0ull;
     stage_key_bias(kbias, p.key_valid, si, b, T, Tp);
+    if (p.nbt) stage_time(p, b, h, T, Tp, start, L.tss, L.rtab, L.tbins);
   }
   if (!si.contig) stage_kvs(L.kvs, p.key_valid, b, T, Tp);
   __syncthreads();
@@ -619,11 +651,25 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
           float rb[16];
           rab16(L.f0, myq, kb, hh, rb);
           const float* kbb = kbias + kb + 4 * hh;
+          int tb[16];
+          if (p.nbt) {  // time bias: rab_t[h, bucket(t_q - t_k)]
+            const int tq = L.tss[myq < Tp ? myq : Tp - 1];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              tb[i] = time_bucket(tq - L.tss[kb + acc_row(i, hh)], p.nbt);
+              rb[i] += L.rtab[tb[i]];
+            }
+          }
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const float x = fmaf(s[i], p.scale, rb[i]) + kbb[(i & 3) + 8 * (i >> 2)];
             const float sg = sigmoid_fast(x), sgn = sg * p.inv_n;
             ds[i] = dp[i] * fmaf(fmaf(-x, sg, x), sgn, sgn);  // dp * dSiLU(x) / n
+          }
+          if (p.drab_t) {  // fixed-point bins per bucket (masked scores have ds == 0 exactly)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (ds[i] != 0.f) atomicAdd(&L.tbins[tb[i]], to_fix(ds[i]));
           }
           if (p.drab) {
             // drab bins by distance d = query - key.  The sub-tile's 1024 scores lie on
@@ -665,12 +711,16 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
       store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, (int64_t)b * T + myq, h, hh, acc, p.scale, qok,
                           p.act ? p.q : nullptr, p.ldq, p.in_dt);
     }
-  if (KIND == 1 && p.drab) {
+  if (KIND == 1 && (p.drab || p.drab_t)) {
     __syncthreads();
-    for (int d = threadIdx.x; d < Tp; d += blockDim.x) {
-      const unsigned long long q = bins[kRabPad + d];
-      if (q != 0) atomicAdd(&p.drab_fix[h * p.nb + min(d, p.nb - 1)], q);
-    }
+    if (p.drab)
+      for (int d = threadIdx.x; d < Tp; d += blockDim.x) {
+        const unsigned long long q = bins[kRabPad + d];
+        if (q != 0) atomicAdd(&p.drab_fix[h * p.nb + min(d, p.nb - 1)], q);
+      }
+    if (p.drab_t)
+      for (int j = threadIdx.x; j < p.nbt; j += blockDim.x)
+        if (L.tbins[j] != 0ull) atomicAdd(&p.drab_t_fix[h * p.nbt + j], L.tbins[j]);
   }
 }
 
@@ -723,6 +773,7 @@ k_attn_dkdv_seq(AttnParams p) {
     stage_pair<HD>(L.img0, p.q, p.ldq, false, p.act, L.img1, p.dout, p.lddo, p.dout_f32, false, b, T, h, kbeg, Tp);
   if (KIND == 1) {
     store_rab(L.f0, rr, Tp);
+    if (p.nbt) stage_time(p, b, h, T, Tp, start, L.tss, L.rtab, nullptr);
   } else {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -850,7 +901,10 @@ k_attn_dkdv_seq(AttnParams p) {
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
               const int i = 2 * j + u;
-              const float x = fmaf(s[i], p.scale, rbase[(i & 3) + 8 * (i >> 2)]);
+              float bias = rbase[(i & 3) + 8 * (i >> 2)];
+              if (p.nbt)  // time bias of (query qb + acc_row(i, hh), key myk)
+                bias += L.rtab[time_bucket(L.tss[qb + acc_row(i, hh)] - L.tss[myk < Tp ? myk : Tp - 1], p.nbt)];
+              const float x = fmaf(s[i], p.scale, bias);
               const float sg = sigmoid_fast(x), sgn = sg * p.inv_n;
               pd2[u] = x * sgn;                                   // SiLU(x) / n
               ds2[u] = dp[i] * fmaf(fmaf(-x, sg, x), sgn, sgn);   // dp * dSiLU(x) / n

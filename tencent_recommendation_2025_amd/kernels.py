@@ -298,7 +298,7 @@ def _seed_parts(seed):
 
 
 def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, inv_n=1.0, dropout_p=0.0, seed=0,
-              precise=True, out_dtype=torch.bfloat16, act=None, seq_range=None):
+              precise=True, out_dtype=torch.bfloat16, act=None, seq_range=None, timestamps=None, rab_t=None):
     """Build grk_attn_args for bf16 [B*T, ld] column views q/k/v (head h at cols h*hd).
 
     act="silu": q/k/v are pre-activations; SiLU is applied on load and the
@@ -308,7 +308,9 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
     (drawn on the device each step, so a graph-replayed step gets a fresh mask).
     precise: 0 / False (P and dS rounded to bf16), 1 / True (P, dS as bf16 hi + lo),
     2 (fp32 fidelity: Q/K/V and dO split into hi + lo as well; q/k/v may then be
-    fp32 / fp16 / bf16 and are read exactly -- fidelity_supported(T, hd))."""
+    fp32 / fp16 / bf16 and are read exactly -- fidelity_supported(T, hd)).
+    timestamps (int64 [B, T]) + rab_t (fp32 [H, nbt], nbt <= 64): the HSTU time
+    bias rab_t[h, time_bucket(t_q - t_k)] (include/grk.h, grk_attn_args)."""
     precise = int(precise)
     if precise not in (0, 1, 2):
         raise L.GrkError('precise must be 0, 1 or 2')
@@ -330,6 +332,15 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
         if rab is None or rab.dtype != torch.float32 or rab.dim() != 2 or rab.shape[0] != H or not rab.is_contiguous():
             raise L.GrkError('hstu needs a contiguous fp32 rab [H, num_buckets]')
         nb = rab.shape[1]
+    nbt = 0
+    if timestamps is not None or rab_t is not None:
+        if kind != L.ATTN_HSTU or timestamps is None or rab_t is None:
+            raise L.GrkError('the time bias is an HSTU feature and needs both timestamps and rab_t')
+        if timestamps.dtype != torch.int64 or timestamps.shape != (B, T) or not timestamps.is_contiguous():
+            raise L.GrkError('timestamps must be a contiguous int64 [B, T] tensor')
+        if rab_t.dtype != torch.float32 or rab_t.dim() != 2 or rab_t.shape[0] != H or not rab_t.is_contiguous():
+            raise L.GrkError('rab_t must be a contiguous fp32 [H, num_time_buckets] tensor')
+        nbt = rab_t.shape[1]
     if scale is None:
         scale = hd ** -0.5
     seed, seed_dev = _seed_parts(seed)
@@ -337,8 +348,8 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
                          v.stride(0), _ptr(key_valid), _ptr(rab), float(scale), float(inv_n), float(dropout_p),
                          precise, seed, L.dtype_code(out_dtype),
                          {None: L.ACT_NONE, 'silu': L.ACT_SILU}[act], _ptr(seq_range), _ptr(seed_dev),
-                         L.dtype_code(q.dtype))
-    args._keep = (q, k, v, key_valid, rab, seq_range, seed_dev)  # the struct holds raw pointers: keep the tensors alive
+                         L.dtype_code(q.dtype), _ptr(timestamps), _ptr(rab_t), nbt, None, None)
+    args._keep = (q, k, v, key_valid, rab, seq_range, seed_dev, timestamps, rab_t)  # raw pointers: keep alive
     return args
 
 
@@ -370,11 +381,21 @@ def attention_fwd(args, out, lse=None):
     L.check(rc, 'grk_attention_fwd')
 
 
-def attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab=None, parts=L.ATTN_BWD_DQ | L.ATTN_BWD_DKDV):
+def attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab=None, parts=L.ATTN_BWD_DQ | L.ATTN_BWD_DKDV,
+                  drab_t=None):
     """grk_attention_bwd(_parts): writes dq/dk/dv (args.out_dtype) and accumulates drab
-    (deterministic).  ``parts`` selects the dq half (L.ATTN_BWD_DQ: delta, dq, drab)
-    and/or the dk/dv half (L.ATTN_BWD_DKDV); tensors of a half not run may be None."""
-    _require_cuda(dout, dq, dk, dv, drab)
+    (and, with a time bias, drab_t) deterministically.  ``parts`` selects the dq half
+    (L.ATTN_BWD_DQ: delta, dq, drab, drab_t) and/or the dk/dv half (L.ATTN_BWD_DKDV);
+    tensors of a half not run may be None."""
+    _require_cuda(dout, dq, dk, dv, drab, drab_t)
+    wst = None
+    args.drab_t, args.drab_t_ws = None, None
+    if drab_t is not None:
+        if args.num_time_buckets == 0 or drab_t.dtype != torch.float32 or not drab_t.is_contiguous() \
+                or drab_t.numel() != args.heads * args.num_time_buckets:
+            raise L.GrkError('drab_t must be a contiguous fp32 [H, num_time_buckets] tensor of a time-bias call')
+        wst = torch.empty(drab_t.numel(), dtype=torch.int64, device=drab_t.device)
+        args.drab_t, args.drab_t_ws = drab_t.data_ptr(), wst.data_ptr()
     for t, n in ((dout, 'dout'), (dq, 'dq'), (dk, 'dk'), (dv, 'dv')):
         if t is not None and (t.stride(1) != 1 or t.stride(0) % 8):
             raise L.GrkError(f'{n} must be row-major with a row stride multiple of 8')
@@ -389,6 +410,7 @@ def attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab=None, parts=L.AT
                                          dout.data_ptr(), dout.stride(0), L.dtype_code(dout.dtype), _ptr(lse),
                                          _ptr(delta), q_p, q_ld, k_p, k_ld, v_p, v_ld, _ptr(drab), _ptr(ws), parts,
                                          L.stream_ptr(dout.device))
+    args.drab_t, args.drab_t_ws = None, None
     L.check(rc, 'grk_attention_bwd')
 
 

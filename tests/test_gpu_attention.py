@@ -75,7 +75,7 @@ def drop_mask_np(seed, B, H, T, p):
 
 
 def run(K, kind, B, T, H, hd, lens, precise, seed=0, dropout=0.0, nb=None, out_dtype=torch.float32, act=None,
-        holes=False, use_ranges=False, oracle=True):
+        holes=False, use_ranges=False, oracle=True, nbt=0):
     """act='silu': x holds pre-activations; the oracle sees SiLU(x) rounded to bf16
     and its q/k/v gradients are chained through dSiLU(x)."""
     from tencent_recommendation_2025_amd import _lib as L
@@ -90,11 +90,17 @@ def run(K, kind, B, T, H, hd, lens, precise, seed=0, dropout=0.0, nb=None, out_d
     rng = np.random.default_rng(seed + 1)
     rab = None
     extra = {}
+    ts_np = rabt_np = None
     if kind == L.ATTN_HSTU:
         nb = nb or T
         rab_np = (rng.standard_normal((H, nb)) * 0.5).astype(np.float32)
         rab = torch.from_numpy(rab_np).to(DEV)
         extra = dict(rab=rab, inv_n=1.0 / T, scale=hd ** -0.5)
+        if nbt:  # time bias: unix-like seconds, heavy-tailed gaps (seconds .. months)
+            trng = np.random.default_rng(seed + 7)
+            ts_np = (1_700_000_000 + np.cumsum(np.exp(trng.uniform(0, 16, (B, T))), 1)).astype(np.int64)
+            rabt_np = (trng.standard_normal((H, nbt)) * 0.5).astype(np.float32)
+            extra.update(timestamps=torch.from_numpy(ts_np).to(DEV), rab_t=torch.from_numpy(rabt_np).to(DEV))
     args = K.attn_args(kind, q, k, v, B, T, H, hd, key_valid=kv, precise=precise, dropout_p=dropout, seed=1234,
                        out_dtype=out_dtype, act=act, seq_range=K.seq_ranges(kv) if use_ranges else None, **extra)
     if act == 'silu':
@@ -107,7 +113,8 @@ def run(K, kind, B, T, H, hd, lens, precise, seed=0, dropout=0.0, nb=None, out_d
     dq, dk, dv = (torch.empty(B * T, D, dtype=out_dtype, device=DEV) for _ in range(3))
     delta = torch.empty(B, H, T, device=DEV)
     drab = torch.zeros(H, nb, device=DEV) if kind == L.ATTN_HSTU else None
-    K.attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab)
+    drab_t = torch.zeros(H, nbt, device=DEV) if nbt else None
+    K.attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab, drab_t=drab_t)
     torch.cuda.synchronize()
     qh, kh, vh = (heads(x[:, i * D:(i + 1) * D], B, T, H, hd) for i in range(3))
     doh = heads(dout_np, B, T, H, hd)
@@ -115,6 +122,8 @@ def run(K, kind, B, T, H, hd, lens, precise, seed=0, dropout=0.0, nb=None, out_d
                dv=dv.float().cpu().numpy(), lse=lse.cpu().numpy())
     if kind == L.ATTN_HSTU:
         res['drab'] = drab.cpu().numpy()
+    if nbt:
+        res['drab_t'] = drab_t.cpu().numpy()
     if not oracle:
         return res, None, valid
     if kind == L.ATTN_SOFTMAX:
@@ -125,9 +134,11 @@ def run(K, kind, B, T, H, hd, lens, precise, seed=0, dropout=0.0, nb=None, out_d
                                    out_stored=stored)
         want = dict(out=flat(o), dq=flat(gq), dk=flat(gk), dv=flat(gv), lse=lse_ref)
     else:
-        o, _, _ = ohstu.forward(qh, kh, vh, valid.astype(bool), rab_np, hd ** -0.5, 1.0 / T)
-        gq, gk, gv, gr = ohstu.backward(qh, kh, vh, valid.astype(bool), rab_np, hd ** -0.5, 1.0 / T, doh)
-        want = dict(out=flat(o), dq=flat(gq), dk=flat(gk), dv=flat(gv), drab=gr)
+        o, _, _ = ohstu.forward(qh, kh, vh, valid.astype(bool), rab_np, hd ** -0.5, 1.0 / T, ts_np, rabt_np)
+        g = ohstu.backward(qh, kh, vh, valid.astype(bool), rab_np, hd ** -0.5, 1.0 / T, doh, ts_np, rabt_np)
+        want = dict(out=flat(o), dq=flat(g[0]), dk=flat(g[1]), dv=flat(g[2]), drab=g[3])
+        if nbt:
+            want['drab_t'] = g[4]
     if act == 'silu':
         for i, key in enumerate(('dq', 'dk', 'dv')):
             want[key] = want[key] * ohstu.dsilu(pre[:, i * D:(i + 1) * D].astype(np.float64))
@@ -446,3 +457,40 @@ def test_wide_head_rejects_fidelity_mode(K):
                        precise=2, out_dtype=torch.float32)
     with pytest.raises(RuntimeError, match='head_dim 512'):
         K.attention_fwd(args, torch.empty(64, 512, device=DEV), torch.empty(2, 1, 32, device=DEV))
+
+
+# ------------------------------------------------------------- time bias --
+# HSTU rab_time: rab_t[h, half-octave bucket of t_q - t_k]
+@pytest.mark.parametrize('hd,H,T,lens,act', [(64, 2, 201, [201, 120, 7], 'silu'), (32, 4, 97, [97, 40], None),
+                                             (64, 2, 150, [150, 90, 40], 'silu')])
+def test_time_bias_matches_oracle(K, hd, H, T, lens, act):
+    res, want, _ = run(K, 1, B=len(lens), T=T, H=H, hd=hd, lens=lens, precise=True, nbt=48, act=act, seed=T)
+    for key in ('out', 'dq', 'dk', 'dv', 'drab', 'drab_t'):
+        err = nrel(res[key], want[key])
+        assert err < TOL_PRECISE, f'{key}: normwise rel err {err:.2e}'
+    assert np.count_nonzero(want['drab_t']) > 10
+
+
+def test_time_bias_c2_shape_and_repeatable(K):
+    a, want, _ = run(K, 1, B=128, T=201, H=8, hd=64, lens=C2_LENS, precise=True, seed=13, act='silu', nbt=64,
+                     out_dtype=torch.bfloat16)
+    for key in ('out', 'dq', 'dk', 'dv'):
+        assert nrel(a[key], to_bf16_f32(np.asarray(want[key], np.float32))) < TOL_PRECISE, key
+    for key in ('drab', 'drab_t'):
+        assert nrel(a[key], want[key]) < TOL_PRECISE, key
+    b, _, _ = run(K, 1, B=128, T=201, H=8, hd=64, lens=C2_LENS, precise=True, seed=13, act='silu', nbt=64,
+                  out_dtype=torch.bfloat16, oracle=False)
+    for key in a:
+        if key != 'lse':
+            assert np.array_equal(a[key], b[key]), key
+
+
+def test_time_bias_outside_whole_sequence_kernels_is_refused(K):
+    from tencent_recommendation_2025_amd import _lib as L
+    with pytest.raises(RuntimeError, match='whole-sequence'):
+        run(K, 1, B=1, T=1025, H=1, hd=128, lens=[900], precise=True, nbt=16, oracle=False)
+    x = torch.zeros(64, 3 * 64, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(RuntimeError, match='HSTU'):
+        K.attn_args(L.ATTN_SOFTMAX, x[:, :64], x[:, 64:128], x[:, 128:], 2, 32, 1, 64,
+                    timestamps=torch.zeros(2, 32, dtype=torch.int64, device=DEV),
+                    rab_t=torch.zeros(1, 8, device=DEV))

@@ -42,6 +42,29 @@ def test_hstu_backward_finite_differences():
     fd_check(lambda x: L(rr=x), rab, drab)
 
 
+def test_hstu_time_bias_finite_differences():
+    """The optional time bias (rab_t over half-octave buckets of the time gap):
+    its gradient and the q/k gradients through it by finite differences, and the
+    buckets against an integer restatement."""
+    q, k, v, do, valid, rab = hstu_inputs(seed=4, T=11)
+    rng = np.random.default_rng(5)
+    ts = (1_700_000_000 + np.cumsum(np.exp(rng.uniform(0, 12, (2, 11))).astype(np.int64), 1)).astype(np.int64)
+    rab_t = rng.standard_normal((2, 24)) * 0.5
+    a, n = 0.7, 1.0 / 11
+    dq, dk, dv, drab, drab_t = ohstu.backward(q, k, v, valid, rab, a, n, do, ts, rab_t)
+    L = lambda qq=q, rt=rab_t: float((ohstu.forward(qq, k, v, valid, rab, a, n, ts, rt)[0] * do).sum())
+    fd_check(lambda x: L(qq=x), q, dq)
+    fd_check(lambda x: L(rt=x), rab_t, drab_t)
+    assert np.count_nonzero(drab_t) > 5   # the gaps spread over several buckets
+
+    def tb(d, nbt):
+        x = abs(int(d)) + 1
+        lg = x.bit_length() - 1
+        return min(2 * lg + (((x >> (lg - 1)) & 1) if lg > 0 else 0), nbt - 1)
+    gaps = np.array(list(range(-40, 40)) + [2 ** e + o for e in range(1, 30) for o in (-1, 0, 1)])
+    assert [int(b) for b in ohstu.time_bucket(gaps, 64)] == [tb(g, 64) for g in gaps]
+
+
 def test_hstu_numpy_equals_torch_restatement():
     q, k, v, do, valid, rab = hstu_inputs(seed=1, T=7, nb=7)
     B, H, T, hd = q.shape
