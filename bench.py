@@ -50,6 +50,8 @@ def parse():
     ap.add_argument('--loss', default='bce', choices=['bce', 'sampled_softmax'])
     ap.add_argument('--table-mode', default='dense', choices=['dense', 'lazy'])
     ap.add_argument('--zipf', type=float, default=None)
+    ap.add_argument('--time-buckets', type=int, default=0,
+                    help='HSTU time bias (rab_time) with this many buckets; batches carry event times')
     ap.add_argument('--cpu-baseline', type=int, default=1)
     ap.add_argument('--dropout', type=float, default=0.01,
                     help="dropout_rate (the reference default, model/BaseLine/main.py:30)")
@@ -384,10 +386,11 @@ def main():
     from tencent_recommendation_2025_amd.optim import FusedAdamW
     from tencent_recommendation_2025_amd.train import Trainer
 
-    cfg = S.SyntheticConfig(batch_size=a.batch, maxlen=a.maxlen, num_items=a.items, num_users=a.users, zipf=a.zipf)
+    cfg = S.SyntheticConfig(batch_size=a.batch, maxlen=a.maxlen, num_items=a.items, num_users=a.users, zipf=a.zipf,
+                            timestamps=a.time_buckets > 0)
     stats, types = S.feature_schema(cfg)
     margs = S.make_args(hidden_units=a.hidden, maxlen=a.maxlen, num_blocks=a.blocks, num_heads=a.heads,
-                        block=a.block, dropout_rate=a.dropout)
+                        block=a.block, dropout_rate=a.dropout, hstu_time_buckets=a.time_buckets)
     shard_tables = sharded and (a.shard_tables if a.shard_tables is not None else a.items >= 10_000_000)
     margs.shard_tables = bool(shard_tables)
     torch.manual_seed(0)
@@ -458,7 +461,8 @@ def main():
             'config': {'workload': f'BASELINE config {3 if shard_tables else 2}: {a.block.upper()} d={a.hidden} L={a.maxlen} '
                                    f'({a.blocks} blocks x {a.heads} heads), {a.items}-item bf16 table, '
                                    f'{a.users} users, loss={a.loss}, table AdamW={a.table_mode}, '
-                                   f'dropout={a.dropout}',
+                                   f'dropout={a.dropout}'
+                                   + (f', rab_time buckets={a.time_buckets}' if a.time_buckets else ''),
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch, 'seq_len': a.maxlen + 1,
                        'parallelism': f'dp{world}' + ('+rowshard' if sharded else '') + ('(shard-built tables)' if shard_tables else ''),
                        'step_launch': 'hip-graph replay' if trainer.graph else 'eager',

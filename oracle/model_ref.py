@@ -23,6 +23,8 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from . import hstu
+
 EMB_SHAPE = {"81": 32, "82": 1024, "83": 3584, "84": 4096, "85": 3584, "86": 3584}  # model/BaseLine/model.py:183
 
 
@@ -49,15 +51,16 @@ class RefMHA(torch.nn.Module):
 class RefHSTU(torch.nn.Module):
     """HSTU layer (parity unpinned; see oracle/hstu.py).  Same math, torch autograd."""
 
-    def __init__(self, d, h, p, num_buckets):
+    def __init__(self, d, h, p, num_buckets, num_time_buckets=0):
         super().__init__()
         self.hidden_units, self.num_heads, self.head_dim, self.dropout_rate = d, h, d // h, p
         self.uvqk = torch.nn.Linear(d, 4 * d)
         self.rab = torch.nn.Parameter(torch.zeros(h, num_buckets))
+        self.rab_t = torch.nn.Parameter(torch.zeros(h, num_time_buckets)) if num_time_buckets else None
         self.attn_norm = torch.nn.LayerNorm(d, eps=1e-8)
         self.out_linear = torch.nn.Linear(d, d)
 
-    def forward(self, query, key, value, attn_mask=None):
+    def forward(self, query, key, value, attn_mask=None, timestamps=None, key_valid=None):
         B, T, D = query.shape
         u, v, q, k = torch.split(F.silu(self.uvqk(query)), D, dim=-1)
         sh = lambda x: x.view(B, T, self.num_heads, self.head_dim).transpose(1, 2)
@@ -67,6 +70,9 @@ class RefHSTU(torch.nn.Module):
         j = torch.arange(T)[None, :]
         bucket = (i - j).clamp(0, nb - 1)
         s = torch.matmul(q, k.transpose(-1, -2)) * self.head_dim ** -0.5 + self.rab[:, bucket][None]
+        if timestamps is not None and self.rab_t is not None:   # time bias (hstu.py _time_bias)
+            _, bt = hstu._time_bias(np.asarray(timestamps), np.asarray(key_valid), np.zeros(self.rab_t.shape))
+            s = s + self.rab_t[:, torch.from_numpy(bt)].transpose(0, 1)
         a = F.silu(s) * (1.0 / T) * attn_mask.unsqueeze(1).to(s.dtype)
         o = torch.matmul(a, v).transpose(1, 2).contiguous().view(B, T, D)
         y = self.attn_norm(o) * u
@@ -150,7 +156,8 @@ class RefBaselineModel(torch.nn.Module):
         for _ in range(args.num_blocks):
             self.attention_layernorms.append(torch.nn.LayerNorm(d, eps=1e-8))
             if block == "hstu":
-                self.attention_layers.append(RefHSTU(d, args.num_heads, args.dropout_rate, T))
+                self.attention_layers.append(RefHSTU(d, args.num_heads, args.dropout_rate, T,
+                                                     getattr(args, 'hstu_time_buckets', 0) or 0))
                 continue
             self.attention_layers.append(RefMHA(d, args.num_heads, args.dropout_rate))
             self.forward_layernorms.append(torch.nn.LayerNorm(d, eps=1e-8))
@@ -184,7 +191,7 @@ class RefBaselineModel(torch.nn.Module):
         return x
 
     # --- model/BaseLine/model.py:312-350 -------------------------------------
-    def log2feats(self, log_seqs, mask, feats):
+    def log2feats(self, log_seqs, mask, feats, timestamps=None):
         B, T = log_seqs.shape
         seqs = self.feat2emb(log_seqs, feats, mask=mask, include_user=True)
         seqs = seqs * self.item_emb.embedding_dim ** 0.5
@@ -193,7 +200,8 @@ class RefBaselineModel(torch.nn.Module):
         attn_mask = torch.tril(torch.ones((T, T), dtype=torch.bool)).unsqueeze(0) & (mask != 0).unsqueeze(1)
         for i in range(len(self.attention_layers)):
             if self.block == "hstu":
-                y, _ = self.attention_layers[i](*(3 * (self.attention_layernorms[i](seqs),)), attn_mask=attn_mask)
+                y, _ = self.attention_layers[i](*(3 * (self.attention_layernorms[i](seqs),)), attn_mask=attn_mask,
+                                                timestamps=timestamps, key_valid=(mask != 0))
                 seqs = seqs + y
             elif self.norm_first:
                 x = self.attention_layernorms[i](seqs)
@@ -205,8 +213,9 @@ class RefBaselineModel(torch.nn.Module):
         return self.last_layernorm(seqs)
 
     # --- model/BaseLine/model.py:352-384 -------------------------------------
-    def forward(self, seq, pos, neg, token_type, next_token_type, seq_feat, pos_feat, neg_feat, return_embs=False):
-        h = self.log2feats(seq, token_type, seq_feat)
+    def forward(self, seq, pos, neg, token_type, next_token_type, seq_feat, pos_feat, neg_feat, return_embs=False,
+                timestamps=None):
+        h = self.log2feats(seq, token_type, seq_feat, timestamps)
         lm = (next_token_type == 1)
         pe = self.feat2emb(pos, pos_feat, include_user=False)
         ne = self.feat2emb(neg, neg_feat, include_user=False)

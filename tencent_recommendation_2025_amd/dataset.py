@@ -81,6 +81,9 @@ class MyDataset(torch.utils.data.Dataset):
         self._load_data_and_offsets()
         self.maxlen = args.maxlen
         self.mm_emb_ids = list(getattr(args, 'mm_emb_id', ['81']))
+        # args.timestamps: samples carry the records' event times as a tenth field
+        # (int64 [maxlen + 1], 0 on padding) for the HSTU time bias; off = the reference's nine
+        self.with_timestamps = bool(getattr(args, 'timestamps', False))
         with open(self.data_dir / 'item_feat_dict.json', 'r') as f:
             self.item_feat_dict = json.load(f)
         self.mm_emb_dict = load_mm_emb(self.data_dir / 'creative_emb', self.mm_emb_ids)
@@ -146,12 +149,15 @@ class MyDataset(torch.utils.data.Dataset):
 
     def __getitem__(self, uid):
         records = self._load_user_data(uid)
-        ext = []
-        for u, i, ufeat, ifeat, act, _ in records:
+        ext, ext_ts = [], []
+        for u, i, ufeat, ifeat, act, when in records:
             if u and ufeat:
                 ext.insert(0, (u, ufeat, 2, act))
+                ext_ts.insert(0, when or 0)
             if i and ifeat:
                 ext.append((i, ifeat, 1, act))
+                ext_ts.append(when or 0)
+        times = np.zeros([self.maxlen + 1], np.int64)
         n = self.maxlen + 1
         seq, pos, neg = (np.zeros([n], np.int32) for _ in range(3))
         token_type, next_token_type, next_action_type = (np.zeros([n], np.int32) for _ in range(3))
@@ -159,8 +165,9 @@ class MyDataset(torch.utils.data.Dataset):
         nxt = ext[-1]
         idx = self.maxlen
         ts = {r[0] for r in ext if r[2] == 1 and r[0]}
-        for rec in reversed(ext[:-1]):
+        for rec, when in zip(reversed(ext[:-1]), reversed(ext_ts[:-1])):
             i, feat, type_, _ = rec
+            times[idx] = when
             next_i, next_feat, next_type, next_act = nxt
             feat = self.fill_missing_feat(feat, i)
             next_feat = self.fill_missing_feat(next_feat, next_i)
@@ -184,25 +191,30 @@ class MyDataset(torch.utils.data.Dataset):
         seq_feat = np.where(seq_feat == None, dflt, seq_feat)  # noqa: E711  (object-array compare, as the reference)
         pos_feat = np.where(pos_feat == None, dflt, pos_feat)  # noqa: E711
         neg_feat = np.where(neg_feat == None, dflt, neg_feat)  # noqa: E711
-        return seq, pos, neg, token_type, next_token_type, next_action_type, seq_feat, pos_feat, neg_feat
+        out = seq, pos, neg, token_type, next_token_type, next_action_type, seq_feat, pos_feat, neg_feat
+        return out + (times,) if self.with_timestamps else out
 
     @staticmethod
     def collate_fn(batch):
-        """Reference collate (dataset.py:267-293)."""
-        seq, pos, neg, tt, ntt, nat, sf, pf, nf = zip(*batch)
+        """Reference collate (dataset.py:267-293); a tenth field (event times) is stacked too."""
+        fields = list(zip(*batch))
+        seq, pos, neg, tt, ntt, nat, sf, pf, nf = fields[:9]
         t = lambda x: torch.from_numpy(np.array(x))
-        return t(seq), t(pos), t(neg), t(tt), t(ntt), t(nat), list(sf), list(pf), list(nf)
+        return (t(seq), t(pos), t(neg), t(tt), t(ntt), t(nat), list(sf), list(pf), list(nf)) \
+            + tuple(t(x) for x in fields[9:])
 
     def collate_tensor_fn(self, batch):
-        """Tensorised collate: the six id tensors + three feature dicts of tensors."""
-        seq, pos, neg, tt, ntt, nat, sf, pf, nf = self.collate_fn(batch)
+        """Tensorised collate: the six id tensors + three feature dicts of tensors
+        (+ the event times when the dataset carries them)."""
+        seq, pos, neg, tt, ntt, nat, sf, pf, nf, *rest = self.collate_fn(batch)
         ft = self.feature_types
         item = ft['item_sparse'] + ft['item_array'] + ft['item_emb']
         user = ft['user_sparse'] + ft['user_array']
         arr = set(ft['item_array'] + ft['user_array'])
         emb = set(ft['item_emb'])
         return (seq, pos, neg, tt, ntt, nat,
-                tensorize(sf, item + user, arr, emb), tensorize(pf, item, arr, emb), tensorize(nf, item, arr, emb))
+                tensorize(sf, item + user, arr, emb), tensorize(pf, item, arr, emb),
+                tensorize(nf, item, arr, emb)) + tuple(rest)
 
 
 def tensorize(feat_list, fids, array_fids=(), emb_fids=()):

@@ -320,15 +320,22 @@ def softmax_mha(qkv, key_valid, B, T, H, hd, dropout_p=0.0, seed=0, precise=True
 
 
 def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, precise=True, dropout_p=0.0, seed=0,
-              seq_range=None):
+              seq_range=None, timestamps=None, rab_t=None):
     """Fused HSTU layer core on the [B*T, 4D] (u|v|q|k) pre-activation (custom op
     grk::hstu_core, ops.py): three kernels forward (attention with SiLU on load,
-    LayerNorm * SiLU(u) gate with dropout), two backward; no eager glue."""
+    LayerNorm * SiLU(u) gate with dropout), two backward; no eager glue.
+    timestamps (int64 [B, T]) with rab_t ([H, nbt], nbt <= 64) add the time bias
+    rab_t[h, time_bucket(t_q - t_k)] to every score (oracle/hstu.py time_bucket)."""
     if key_valid is None:
         key_valid = torch.ones(B, T, dtype=torch.uint8, device=pre.device)
+    if (timestamps is None) != (rab_t is None):
+        raise ValueError('the time bias needs both timestamps and rab_t')
+    if timestamps is not None:
+        timestamps = timestamps.to(device=pre.device, dtype=torch.int64).contiguous()
     sd = seed if isinstance(seed, torch.Tensor) else None
     y, _, _ = torch.ops.grk.hstu_core(pre, rab, ln_w, ln_b, key_valid, H, hd, float(inv_n), float(eps), int(precise),
-                                      float(dropout_p), 0 if sd is not None else int(seed), sd, seq_range)
+                                      float(dropout_p), 0 if sd is not None else int(seed), sd, seq_range,
+                                      timestamps, rab_t)
     return y if pre.dtype == torch.bfloat16 else y.to(pre.dtype)
 
 

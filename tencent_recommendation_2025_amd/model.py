@@ -118,7 +118,7 @@ class HSTUAttention(torch.nn.Module):
     torch's generator on the device), not torch's Philox stream.
     """
 
-    def __init__(self, hidden_units, num_heads, dropout_rate, num_buckets):
+    def __init__(self, hidden_units, num_heads, dropout_rate, num_buckets, num_time_buckets=0):
         super().__init__()
         assert hidden_units % num_heads == 0, 'hidden_units must be divisible by num_heads'
         self.hidden_units, self.num_heads = hidden_units, num_heads
@@ -126,19 +126,24 @@ class HSTUAttention(torch.nn.Module):
         self.dropout_rate = dropout_rate
         self.uvqk = torch.nn.Linear(hidden_units, 4 * hidden_units)
         self.rab = torch.nn.Parameter(torch.zeros(num_heads, num_buckets))
+        # time bias rab_t[h, half-octave bucket of |t_q - t_k| + 1] (only with timestamps)
+        self.rab_t = torch.nn.Parameter(torch.zeros(num_heads, num_time_buckets)) if num_time_buckets else None
         self.attn_norm = torch.nn.LayerNorm(hidden_units, eps=1e-8)
         self.out_linear = torch.nn.Linear(hidden_units, hidden_units)
 
-    def forward(self, query, key=None, value=None, attn_mask=None, key_valid=None, seq_range=None):
+    def forward(self, query, key=None, value=None, attn_mask=None, key_valid=None, seq_range=None, timestamps=None):
         B, T, D = query.shape
         if key_valid is None:
             key_valid = key_valid_from_mask(attn_mask, B, T)
+        rab_t = self.rab_t if timestamps is not None else None
+        if rab_t is None:
+            timestamps = None
         pre = _linear(query, self.uvqk.weight, self.uvqk.bias).reshape(B * T, 4 * D)
         p = self.dropout_rate if self.training else 0.0
         seed = dropout_seed(pre.device) if p > 0 else 0
         y = G.hstu_core(pre, self.rab, self.attn_norm.weight, self.attn_norm.bias, key_valid, B, T,
                         self.num_heads, self.head_dim, 1.0 / T, self.attn_norm.eps, dropout_p=p, seed=seed,
-                        seq_range=seq_range)
+                        seq_range=seq_range, timestamps=timestamps, rab_t=rab_t)
         return _linear(y.view(B, T, D), self.out_linear.weight, self.out_linear.bias), None
 
 
@@ -226,7 +231,8 @@ class BaselineModel(torch.nn.Module):
         for _ in range(args.num_blocks):
             self.attention_layernorms.append(torch.nn.LayerNorm(d, eps=1e-8))
             if self.block == 'hstu':
-                self.attention_layers.append(HSTUAttention(d, args.num_heads, args.dropout_rate, nb))
+                self.attention_layers.append(HSTUAttention(d, args.num_heads, args.dropout_rate, nb,
+                                                           getattr(args, 'hstu_time_buckets', 0) or 0))
                 continue
             self.attention_layers.append(FlashMultiHeadAttention(d, args.num_heads, args.dropout_rate))
             self.forward_layernorms.append(torch.nn.LayerNorm(d, eps=1e-8))
@@ -516,7 +522,9 @@ class BaselineModel(torch.nn.Module):
         return x[:B], x[B:]
 
     # -------------------------------------------------- model/BaseLine/model.py:312-350
-    def log2feats(self, log_seqs, mask, seq_feature):
+    def log2feats(self, log_seqs, mask, seq_feature, timestamps=None):
+        """timestamps (int [B, T] event times, HSTU blocks with hstu_time_buckets > 0
+        only): the time bias of every HSTU layer; None = positions only."""
         dev = self._device()
         B, T = log_seqs.shape
         seqs, pos_rows = self._embed(log_seqs, seq_feature, mask=mask, include_user=True, with_pos=True)
@@ -524,6 +532,8 @@ class BaselineModel(torch.nn.Module):
         seqs = self.emb_dropout(seqs)
         key_valid = (mask.to(dev, non_blocking=True) != 0).to(torch.uint8).contiguous()
         kw = dict(key_valid=key_valid, seq_range=torch.ops.grk.seq_ranges(key_valid))  # one launch serves every layer
+        if timestamps is not None and self.block == 'hstu':
+            kw['timestamps'] = timestamps.to(dev, torch.int64, non_blocking=True).contiguous()
         if self.block == 'hstu' and _grk_gemm_ok(seqs) and self.hidden_units % 8 == 0:
             # bf16 residual stream: each residual add is fused into the next LayerNorm
             # (grk_add_norm), the last one into last_layernorm (fp32 output, as autocast's)
@@ -555,16 +565,16 @@ class BaselineModel(torch.nn.Module):
 
     # -------------------------------------------------- model/BaseLine/model.py:352-384
     def forward(self, user_item, pos_seqs, neg_seqs, mask, next_mask, next_action_type, seq_feature, pos_feature,
-                neg_feature):
+                neg_feature, timestamps=None):
         with self._shared_projections():
-            log_feats = self.log2feats(user_item, mask, seq_feature)
+            log_feats = self.log2feats(user_item, mask, seq_feature, timestamps)
             pos_embs, neg_embs = self.feat2emb_pair(pos_seqs, pos_feature, neg_seqs, neg_feature)
         return G.pair_logits(log_feats, pos_embs, neg_embs, next_mask.to(self._device(), non_blocking=True))
 
-    def encode(self, user_item, pos_seqs, neg_seqs, mask, seq_feature, pos_feature, neg_feature):
+    def encode(self, user_item, pos_seqs, neg_seqs, mask, seq_feature, pos_feature, neg_feature, timestamps=None):
         """(log_feats, pos_embs, neg_embs) -- the operands of the loss."""
         with self._shared_projections():
-            return (self.log2feats(user_item, mask, seq_feature),
+            return (self.log2feats(user_item, mask, seq_feature, timestamps),
                     *self.feat2emb_pair(pos_seqs, pos_feature, neg_seqs, neg_feature))
 
     @contextlib.contextmanager
@@ -586,10 +596,10 @@ class BaselineModel(torch.nn.Module):
             return torch.autocast('cuda', dtype=torch.bfloat16)
         return contextlib.nullcontext()
 
-    def predict(self, log_seqs, seq_feature, mask):
+    def predict(self, log_seqs, seq_feature, mask, timestamps=None):
         self.flush_tables()
         with self._inference_autocast():
-            return self.log2feats(log_seqs, mask, seq_feature)[:, -1, :]
+            return self.log2feats(log_seqs, mask, seq_feature, timestamps)[:, -1, :]
 
     def save_item_emb(self, item_ids, retrieval_ids, feat_dict, save_path, batch_size=1024):
         """Candidate item embeddings -> embedding.fbin / id.u64bin (model/BaseLine/model.py:402-433)."""

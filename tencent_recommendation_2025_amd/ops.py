@@ -204,24 +204,32 @@ def _softmax_backward(ctx, gout, glse):
 torch.library.register_autograd('grk::softmax_attention', _softmax_backward, setup_context=_softmax_setup)
 
 
-def _hstu_args(pb, rab32, key_valid, heads, head_dim, inv_n, precise, seq_range):
+def _hstu_args(pb, rab32, key_valid, heads, head_dim, inv_n, precise, seq_range, timestamps=None, rab_t32=None):
     B, T = key_valid.shape
     D = heads * head_dim
     return K.attn_args(L.ATTN_HSTU, pb[:, 2 * D:3 * D], pb[:, 3 * D:], pb[:, D:2 * D], B, T, heads, head_dim,
                        key_valid=key_valid, scale=head_dim ** -0.5, rab=rab32, inv_n=inv_n, precise=precise,
-                       out_dtype=torch.bfloat16, act='silu', seq_range=seq_range)
+                       out_dtype=torch.bfloat16, act='silu', seq_range=seq_range, timestamps=timestamps,
+                       rab_t=rab_t32)
+
+
+def _f32(t):
+    return None if t is None else t.float().contiguous()
 
 
 @torch.library.custom_op('grk::hstu_core', mutates_args=(), device_types='cuda')
 def hstu_core(pre: Tensor, rab: Tensor, ln_w: Tensor, ln_b: Tensor, key_valid: Tensor, heads: int, head_dim: int,
               inv_n: float, eps: float, precise: int, dropout_p: float, seed: int, seed_dev: Optional[Tensor],
-              seq_range: Optional[Tensor]) -> Tuple[Tensor, Tensor, Tensor]:
+              seq_range: Optional[Tensor], timestamps: Optional[Tensor] = None,
+              rab_t: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
     """y = dropout(LayerNorm(HSTU-attn(SiLU(q), SiLU(k), SiLU(v))) * SiLU(u)) on the
     [B*T, 4D] (u|v|q|k) pre-activation; bf16 math.  Returns (y bf16, o bf16,
-    LayerNorm stats fp32 [B*T, 2])."""
+    LayerNorm stats fp32 [B*T, 2]).  timestamps (int64 [B, T]) + rab_t ([H, nbt]):
+    the time bias rab_t[h, time_bucket(t_q - t_k)]."""
     D = heads * head_dim
     pb = pre.to(torch.bfloat16).contiguous()
-    args = _hstu_args(pb, rab.float().contiguous(), key_valid, heads, head_dim, inv_n, precise, seq_range)
+    args = _hstu_args(pb, rab.float().contiguous(), key_valid, heads, head_dim, inv_n, precise, seq_range,
+                      timestamps, _f32(rab_t))
     o = torch.empty(pre.shape[0], D, dtype=torch.bfloat16, device=pre.device)
     K.attention_fwd(args, o)
     y, stats = K.norm_gate_fwd(o, pb[:, :D], ln_w.float().contiguous(), ln_b.float().contiguous(), eps, dropout_p,
@@ -230,7 +238,8 @@ def hstu_core(pre: Tensor, rab: Tensor, ln_w: Tensor, ln_b: Tensor, key_valid: T
 
 
 @hstu_core.register_fake
-def _(pre, rab, ln_w, ln_b, key_valid, heads, head_dim, inv_n, eps, precise, dropout_p, seed, seed_dev, seq_range):
+def _(pre, rab, ln_w, ln_b, key_valid, heads, head_dim, inv_n, eps, precise, dropout_p, seed, seed_dev, seq_range,
+      timestamps=None, rab_t=None):
     N, D = pre.shape[0], heads * head_dim
     return (pre.new_empty(N, D, dtype=torch.bfloat16), pre.new_empty(N, D, dtype=torch.bfloat16),
             pre.new_empty(N, 2, dtype=torch.float32))
@@ -239,9 +248,11 @@ def _(pre, rab, ln_w, ln_b, key_valid, heads, head_dim, inv_n, eps, precise, dro
 @torch.library.custom_op('grk::hstu_core_backward', mutates_args=(), device_types='cuda')
 def hstu_core_backward(gy: Tensor, pre: Tensor, o: Tensor, stats: Tensor, rab: Tensor, ln_w: Tensor, ln_b: Tensor,
                        key_valid: Tensor, heads: int, head_dim: int, inv_n: float, precise: int, dropout_p: float,
-                       seed: int, seed_dev: Optional[Tensor],
-                       seq_range: Optional[Tensor]) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
-    """(dpre in pre's dtype, drab, dln_w, dln_b in their parameters' dtypes)."""
+                       seed: int, seed_dev: Optional[Tensor], seq_range: Optional[Tensor],
+                       timestamps: Optional[Tensor] = None,
+                       rab_t: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """(dpre in pre's dtype, drab, dln_w, dln_b, drab_t in their parameters' dtypes;
+    drab_t is empty without a time bias)."""
     D = heads * head_dim
     pb = pre.to(torch.bfloat16).contiguous()
     rab32 = rab.float().contiguous()
@@ -250,31 +261,38 @@ def hstu_core_backward(gy: Tensor, pre: Tensor, o: Tensor, stats: Tensor, rab: T
     do, _, dw, db = K.norm_gate_bwd(g, o, pb[:, :D], ln_w.float().contiguous(), ln_b.float().contiguous(), stats,
                                     dropout_p, _seed_arg(seed, seed_dev), du=dpre[:, :D])
     drab = torch.zeros_like(rab32)
-    args = _hstu_args(pb, rab32, key_valid, heads, head_dim, inv_n, precise, seq_range)
-    K.attention_bwd(args, None, do, None, None, dpre[:, 2 * D:3 * D], dpre[:, 3 * D:], dpre[:, D:2 * D], drab)
-    return dpre.to(pre.dtype), drab.to(rab.dtype), dw.to(ln_w.dtype), db.to(ln_b.dtype)
+    rab_t32 = _f32(rab_t)
+    drab_t = torch.zeros_like(rab_t32) if rab_t is not None else None
+    args = _hstu_args(pb, rab32, key_valid, heads, head_dim, inv_n, precise, seq_range, timestamps, rab_t32)
+    K.attention_bwd(args, None, do, None, None, dpre[:, 2 * D:3 * D], dpre[:, 3 * D:], dpre[:, D:2 * D], drab,
+                    drab_t=drab_t)
+    drab_t = drab_t.to(rab_t.dtype) if rab_t is not None else rab.new_empty(0)
+    return dpre.to(pre.dtype), drab.to(rab.dtype), dw.to(ln_w.dtype), db.to(ln_b.dtype), drab_t
 
 
 @hstu_core_backward.register_fake
 def _(gy, pre, o, stats, rab, ln_w, ln_b, key_valid, heads, head_dim, inv_n, precise, dropout_p, seed, seed_dev,
-      seq_range):
-    return torch.empty_like(pre), torch.empty_like(rab), torch.empty_like(ln_w), torch.empty_like(ln_b)
+      seq_range, timestamps=None, rab_t=None):
+    return (torch.empty_like(pre), torch.empty_like(rab), torch.empty_like(ln_w), torch.empty_like(ln_b),
+            torch.empty_like(rab_t) if rab_t is not None else rab.new_empty(0))
 
 
 def _hstu_setup(ctx, inputs, output):
-    pre, rab, ln_w, ln_b, key_valid, heads, head_dim, inv_n, eps, precise, dropout_p, seed, seed_dev, seq_range = inputs
+    (pre, rab, ln_w, ln_b, key_valid, heads, head_dim, inv_n, eps, precise, dropout_p, seed, seed_dev, seq_range,
+     timestamps, rab_t) = inputs
     _, o, stats = output
-    ctx.save_for_backward(pre, o, stats, rab, ln_w, ln_b, key_valid, seed_dev, seq_range)
+    ctx.save_for_backward(pre, o, stats, rab, ln_w, ln_b, key_valid, seed_dev, seq_range, timestamps, rab_t)
     ctx.meta = (heads, head_dim, inv_n, precise, dropout_p, seed)
 
 
 def _hstu_backward(ctx, gy, go, gstats):
-    pre, o, stats, rab, ln_w, ln_b, key_valid, seed_dev, seq_range = ctx.saved_tensors
+    pre, o, stats, rab, ln_w, ln_b, key_valid, seed_dev, seq_range, timestamps, rab_t = ctx.saved_tensors
     heads, head_dim, inv_n, precise, dropout_p, seed = ctx.meta
-    dpre, drab, dw, db = torch.ops.grk.hstu_core_backward(gy, pre, o, stats, rab, ln_w, ln_b, key_valid, heads,
-                                                          head_dim, inv_n, precise, dropout_p, seed, seed_dev,
-                                                          seq_range)
-    return dpre, drab, dw, db, None, None, None, None, None, None, None, None, None, None
+    dpre, drab, dw, db, drab_t = torch.ops.grk.hstu_core_backward(gy, pre, o, stats, rab, ln_w, ln_b, key_valid,
+                                                                  heads, head_dim, inv_n, precise, dropout_p, seed,
+                                                                  seed_dev, seq_range, timestamps, rab_t)
+    return (dpre, drab, dw, db, None, None, None, None, None, None, None, None, None, None, None,
+            drab_t if rab_t is not None else None)
 
 
 torch.library.register_autograd('grk::hstu_core', _hstu_backward, setup_context=_hstu_setup)

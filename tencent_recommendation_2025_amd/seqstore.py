@@ -33,7 +33,7 @@ import torch
 
 from .dataset import ITEM_ARRAY, ITEM_SPARSE, MM_SHAPE, USER_ARRAY, USER_SPARSE, load_mm_emb
 
-CACHE_VERSION = 1
+CACHE_VERSION = 2   # 2: per-token event times (ts)
 
 
 class SeqStore:
@@ -43,7 +43,9 @@ class SeqStore:
     ``MyDataset.__getitem__`` lays out its ``ext`` list (user tokens first,
     most recent user record first, then the item tokens in record order).
     Per token: ``tid`` (item or user id), ``ttype`` (1 item, 2 user), ``act``
-    (action type, 0 when absent), ``sparse`` int32 [F_sparse] (user then item
+    (action type, 0 when absent), ``ts`` (the record's timestamp, int64, 0 when
+    absent -- the HSTU time-bias input; the reference drops it,
+    model/BaseLine/dataset.py:117), ``sparse`` int32 [F_sparse] (user then item
     sparse fids, default 0), ``arr`` int32 [F_array, A_cap] + ``arr_len``
     (default ``[0]``), ``mm`` int32 per mm fid (row of that fid's embedding
     table, 0 = the zero row)."""
@@ -84,7 +86,7 @@ class SeqStore:
             offsets = pickle.load(f)
         sp_col = {f: c for c, f in enumerate(self.sparse_fids)}
         ar_col = {f: c for c, f in enumerate(self.array_fids)}
-        tid, ttype, act, sparse, arrs, mmi, off = [], [], [], [], [], [], [0]
+        tid, ttype, act, tss, sparse, arrs, mmi, off = [], [], [], [], [], [], [], [0]
         a_cap = 1
 
         def mm_row(token_id, fid):
@@ -98,15 +100,16 @@ class SeqStore:
             for o in offsets:
                 f.seek(o)
                 ext = []
-                for u, i, ufeat, ifeat, a, _ in json.loads(f.readline()):
+                for u, i, ufeat, ifeat, a, ts in json.loads(f.readline()):
                     if u and ufeat:
-                        ext.insert(0, (u, ufeat, 2, a))
+                        ext.insert(0, (u, ufeat, 2, a, ts))
                     if i and ifeat:
-                        ext.append((i, ifeat, 1, a))
-                for t_id, feat, t_type, a in ext:
+                        ext.append((i, ifeat, 1, a, ts))
+                for t_id, feat, t_type, a, ts in ext:
                     tid.append(t_id)
                     ttype.append(t_type)
                     act.append(0 if a is None else a)
+                    tss.append(0 if ts is None else int(ts))
                     row = np.zeros(len(self.sparse_fids), np.int32)
                     ar = [[0] for _ in self.array_fids]
                     for k, v in feat.items():
@@ -144,7 +147,7 @@ class SeqStore:
             imm[i] = [mm_row(i, fid) for fid in self.mm_ids]
         self.cache_dir.mkdir(parents=True, exist_ok=True)
         arrays = dict(off=np.asarray(off, np.int64), tid=np.asarray(tid, np.int32), ttype=np.asarray(ttype, np.int8),
-                      act=np.asarray(act, np.int32), sparse=np.asarray(sparse, np.int32).reshape(n, -1), arr=arr,
+                      act=np.asarray(act, np.int32), ts=np.asarray(tss, np.int64), sparse=np.asarray(sparse, np.int32).reshape(n, -1), arr=arr,
                       arr_len=arr_len, mm=np.asarray(mmi, np.int32).reshape(n, -1), item_sparse=isp, item_ok=iok,
                       item_mm=imm)
         for fid in self.mm_ids:
@@ -156,7 +159,7 @@ class SeqStore:
 
     def _load(self):
         ld = lambda k: np.load(self.cache_dir / f'{k}.npy', mmap_mode='r')
-        self.off, self.tid, self.ttype, self.act = ld('off'), ld('tid'), ld('ttype'), ld('act')
+        self.off, self.tid, self.ttype, self.act, self.ts = ld('off'), ld('tid'), ld('ttype'), ld('act'), ld('ts')
         self.sparse, self.arr, self.arr_len, self.mm = ld('sparse'), ld('arr'), ld('arr_len'), ld('mm')
         self.item_sparse, self.item_ok, self.item_mm = ld('item_sparse'), ld('item_ok'), ld('item_mm')
         self.mm_tables = {fid: np.load(self.cache_dir / f'mm_table_{fid}.npy') for fid in self.mm_ids}
@@ -165,10 +168,12 @@ class SeqStore:
         return len(self.off) - 1
 
     # ------------------------------------------------------------ batch ----
-    def batch(self, uids):
+    def batch(self, uids, timestamps=False):
         """The tensorised batch of users ``uids`` (= MyDataset.collate_tensor_fn of
         ``[ds[u] for u in uids]``), with ``neg`` all zero and ``neg_feat`` None:
-        the negatives are drawn on the device (DeviceNegatives)."""
+        the negatives are drawn on the device (DeviceNegatives).  timestamps=True
+        appends int64 [B, T] event times (0 on padding) as a tenth field -- the
+        input of the HSTU time bias (Trainer / model ``timestamps``)."""
         uids = np.asarray(uids, np.int64)
         B, T = len(uids), self.maxlen + 1
         start, end = self.off[uids], self.off[uids + 1]
@@ -188,7 +193,10 @@ class SeqStore:
         seq_feat = self._features(g, valid, self.item_fids + self.user_fids)
         pos_feat = self._features(gn, has_pos, self.item_fids)
         t = torch.from_numpy
-        return (t(seq), t(pos), torch.zeros(B, T, dtype=torch.int32), t(tt), t(ntt), t(nat), seq_feat, pos_feat, None)
+        out = (t(seq), t(pos), torch.zeros(B, T, dtype=torch.int32), t(tt), t(ntt), t(nat), seq_feat, pos_feat, None)
+        if timestamps:
+            out += (t(np.where(valid, self.ts[g], 0).astype(np.int64)),)
+        return out
 
     def _features(self, g, sel, fids):
         """{fid: tensor} of the tokens g where sel, the defaults elsewhere (tensorize's layout).
@@ -246,7 +254,7 @@ class DeviceNegatives:
     def attach(self, batch, uids, seed):
         """The batch (on the device) with neg and neg_feat filled."""
         from . import kernels as K
-        seq, pos, _neg, tt, ntt, nat, sf, pf, _nf = batch
+        seq, pos, _neg, tt, ntt, nat, sf, pf, _nf = batch[:9]
         excl = torch.cat([self.store.history_items(uids).to(self.device), pos.to(torch.int32)], 1)
         neg, nfeat = K.sample_negatives(pos, ntt, excl, self.store.itemnum, seed, item_feat=self.item_sparse,
                                         item_ok=self.item_ok)
@@ -256,7 +264,7 @@ class DeviceNegatives:
                 neg_feat[k] = nfeat[..., ITEM_SPARSE.index(k)].long()
             elif k in self.mm_tables:
                 neg_feat[k] = self.mm_tables[k][self.item_mm[neg.long(), self.store.mm_ids.index(k)]]
-        return seq, pos, neg, tt, ntt, nat, sf, pf, neg_feat
+        return (seq, pos, neg, tt, ntt, nat, sf, pf, neg_feat) + tuple(batch[9:])
 
 
 def to_device(batch, device):
@@ -272,8 +280,9 @@ class StoreBatches(torch.utils.data.Dataset):
     each yields ``(uids, batch)`` (the reference shuffles users every epoch,
     model/BaseLine/main.py:58-70; ``set_epoch`` reshuffles)."""
 
-    def __init__(self, store: SeqStore, batch_size, seed=0, drop_last=True):
+    def __init__(self, store: SeqStore, batch_size, seed=0, drop_last=True, timestamps=False):
         self.store, self.batch_size, self.seed, self.drop_last = store, int(batch_size), int(seed), drop_last
+        self.timestamps = bool(timestamps)
         self.set_epoch(0)
 
     def set_epoch(self, epoch):
@@ -285,4 +294,4 @@ class StoreBatches(torch.utils.data.Dataset):
 
     def __getitem__(self, i):
         uids = self.perm[i * self.batch_size:(i + 1) * self.batch_size]
-        return torch.from_numpy(uids), self.store.batch(uids)
+        return torch.from_numpy(uids), self.store.batch(uids, self.timestamps)

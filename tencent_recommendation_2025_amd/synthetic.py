@@ -35,6 +35,7 @@ class SyntheticConfig:
     min_len: int = 32
     zipf: float | None = None
     mm_ids: list = field(default_factory=lambda: ['81'])
+    timestamps: bool = False   # append int64 [B, T] event times (the HSTU time bias input)
 
 
 def feature_schema(cfg: SyntheticConfig):
@@ -108,12 +109,19 @@ def make_batch(cfg: SyntheticConfig, generator: torch.Generator, device='cuda'):
         seq_feat[f] = torch.where(is_user.unsqueeze(-1) & (slot < alen), vals, 0)
     pos_feat = item_feats(pos, pos > 0)
     neg_feat = item_feats(neg, neg > 0)
-    return seq, pos, neg, token_type, next_token_type, next_action_type, seq_feat, pos_feat, neg_feat
+    batch = (seq, pos, neg, token_type, next_token_type, next_action_type, seq_feat, pos_feat, neg_feat)
+    if cfg.timestamps:
+        # unix seconds, log-uniform gaps of 1 s .. ~1 month; 0 on padding slots (the
+        # kernels take times relative to each sequence's first valid event)
+        gaps = torch.exp(torch.rand(B, T, generator=g, device=dev) * 15.0).to(torch.int64)
+        ts = 1_720_000_000 + torch.cumsum(torch.where(valid, gaps, 0), 1)
+        batch += (torch.where(valid, ts, 0),)
+    return batch
 
 
 def make_args(hidden_units=512, maxlen=200, num_blocks=4, num_heads=8, dropout_rate=0.0, block='hstu',
-              variant='o1', norm_first=False, device='cuda'):
+              variant='o1', norm_first=False, device='cuda', hstu_time_buckets=0):
     from types import SimpleNamespace
     return SimpleNamespace(hidden_units=hidden_units, maxlen=maxlen, num_blocks=num_blocks, num_heads=num_heads,
                            dropout_rate=dropout_rate, block=block, variant=variant, norm_first=norm_first,
-                           device=device, mm_emb_id=['81'])
+                           device=device, mm_emb_id=['81'], hstu_time_buckets=hstu_time_buckets)

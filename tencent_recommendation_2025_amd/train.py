@@ -92,11 +92,14 @@ class Trainer:
         return None
 
     def compute_loss(self, batch):
-        seq, pos, neg, tt, ntt, _nat, sf, pf, nf = batch
+        """batch: the nine collate_fn fields (dataset.py), optionally a tenth --
+        int64 [B, T] event times for the HSTU time bias (model.hstu_time_buckets)."""
+        seq, pos, neg, tt, ntt, _nat, sf, pf, nf = batch[:9]
+        ts = batch[9] if len(batch) > 9 else None
         amp = (torch.autocast('cuda', dtype=self.amp_dtype) if self.amp_dtype is not None
                else contextlib.nullcontext())
         with amp:
-            h, pe, ne = self.model.encode(seq, pos, neg, tt, sf, pf, nf)
+            h, pe, ne = self.model.encode(seq, pos, neg, tt, sf, pf, nf, timestamps=ts)
             if self.loss_kind == 'bce':
                 return G.bce_loss(h, pe, ne, ntt)
             return G.sampled_softmax_loss(h, pe, pos, ntt, self.temperature)

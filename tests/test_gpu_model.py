@@ -166,6 +166,56 @@ def test_hstu_model_matches_oracle(golden):
         assert nrel(p.grad.cpu(), rp.grad) < 2e-2, name
 
 
+def _event_times(batch, seed=0):
+    """Synthetic unix-second event times for the golden batch's sequences: gaps of
+    seconds to months, as the TencentGR logs' timestamp field (dataset.py:72)."""
+    B, T = batch[0].shape
+    gaps = np.exp(np.random.default_rng(seed).uniform(0, 15, (B, T)))
+    return torch.from_numpy((1_720_000_000 + np.cumsum(gaps, 1)).astype(np.int64))
+
+
+def test_hstu_time_bias_model_matches_oracle(golden):
+    """HSTU blocks with the time bias (hstu_time_buckets, SURVEY.md §8 a9
+    +rab_time): logits and every gradient, rab_t's included, against the fp32
+    restatement (oracle/model_ref.RefHSTU) -- tolerances of the HSTU model test."""
+    torch.manual_seed(0)
+    m, g, batch, args, d, stats = build(golden, 'o1', block='hstu', hstu_time_buckets=40)
+    ref = model_ref.RefBaselineModel(int(d['usernum']), int(d['itemnum']), stats, feat_types(), args, variant='o1',
+                                     block='hstu')
+    model_ref.init_params(ref, seed=3)
+    with torch.no_grad():
+        for blk in ref.attention_layers:
+            blk.rab.normal_(0, 0.3)
+            blk.rab_t.normal_(0, 0.5)
+        for name, p in ref.named_parameters():   # live LayerNorm gains (the reference init zeroes them)
+            if 'norm' in name.lower() and name.endswith('weight'):
+                p.uniform_(0.5, 1.5)
+    assert set(ref.state_dict()) == set(m.state_dict())
+    m.load_state_dict(ref.state_dict())
+    ts = _event_times(batch)
+    cpu_batch = [x.cpu() if torch.is_tensor(x) else {k: v.cpu() for k, v in x.items()} for x in batch]
+    seq, pos, neg, tt, ntt, nat, sf, pf, nf = cpu_batch
+    rpl, rnl = ref(seq, pos, neg, tt, ntt, sf, pf, nf, timestamps=ts)
+    model_ref.bce_loss(rpl, rnl, ntt).backward()
+    pl, nl = m(*batch, timestamps=ts)
+    assert max(nrel(pl.detach().cpu(), rpl.detach()), nrel(nl.detach().cpu(), rnl.detach())) < 5e-3
+    ref_loss(pl, nl, batch[4], m, 0.0).backward()
+    checked = []
+    for (name, p), (_, rp) in zip(m.named_parameters(), ref.named_parameters()):
+        if rp.grad is None or float(rp.grad.norm()) == 0:
+            continue
+        assert nrel(p.grad.cpu(), rp.grad) < 2e-2, name
+        checked.append(name)
+    assert sum(n.endswith('rab_t') for n in checked) == len(m.attention_layers)
+    # a zero time bias adds exact zeros: bitwise the positions-only model
+    with torch.no_grad():
+        for blk in m.attention_layers:
+            blk.rab_t.zero_()
+        a = m(*batch, timestamps=ts)
+        b = m(*batch)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
 @pytest.mark.parametrize('hidden', [256, 512])
 def test_o1_single_head_wide_matches_oracle(golden, hidden):
     """O1 with one head over the whole width (BaseLineO1/main.py:45
@@ -360,19 +410,20 @@ def test_grk_linear_matches_torch_linear():
     torch.testing.assert_close(b.grad, b2.grad, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize('period', [2, 16])
-def test_graph_replayed_steps_equal_eager_steps(period):
+@pytest.mark.parametrize('period,nbt', [(2, 0), (16, 0), (2, 24)], ids=['p2', 'p16', 'p2-rab_time'])
+def test_graph_replayed_steps_equal_eager_steps(period, nbt):
     """Trainer(graph=True): the step captured once in a HIP graph and replayed
     with new batches (device clock for the table AdamW, capturable dense AdamW,
     segment work between replays) == the eager step, bit for bit: losses,
-    parameters (deferred rows flushed) and table moments."""
+    parameters (deferred rows flushed) and table moments.  nbt > 0: batches carry
+    event times and the HSTU blocks train a time bias (rab_t)."""
     from tencent_recommendation_2025_amd import synthetic as S
     from tencent_recommendation_2025_amd.model import BaselineModel
     from tencent_recommendation_2025_amd.optim import FusedAdamW
     from tencent_recommendation_2025_amd.train import Trainer
-    cfg = S.SyntheticConfig(batch_size=8, maxlen=30, num_items=5000, num_users=700, min_len=4)
+    cfg = S.SyntheticConfig(batch_size=8, maxlen=30, num_items=5000, num_users=700, min_len=4, timestamps=nbt > 0)
     stats, types = S.feature_schema(cfg)
-    args = S.make_args(hidden_units=64, maxlen=30, num_blocks=2, num_heads=2)
+    args = S.make_args(hidden_units=64, maxlen=30, num_blocks=2, num_heads=2, hstu_time_buckets=nbt)
     runs = []
     for graph in (False, True):
         torch.manual_seed(0)
@@ -390,6 +441,8 @@ def test_graph_replayed_steps_equal_eager_steps(period):
                                                 for grp in opt.groups}, opt.t, int(opt.clock.t.item())))
     assert runs[0][3] == runs[1][3] == runs[1][4] == 9
     assert torch.equal(runs[0][0], runs[1][0]), (runs[0][0], runs[1][0])
+    if nbt:
+        assert all(float(runs[1][1][f'attention_layers.{i}.rab_t'].abs().max()) > 0 for i in range(2))
     for k in runs[0][1]:
         assert torch.equal(runs[0][1][k], runs[1][1][k]), k
     for name in runs[0][2]:

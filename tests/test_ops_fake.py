@@ -64,3 +64,18 @@ def test_pair_logits_and_lookup_trace():
                                          torch.randint(0, 11, (N,)), torch.randint(0, 5, (N, 3)))
     assert _grk_nodes(gm) == ['grk.feature_lookup.default', 'grk.feature_lookup_backward.default',
                               'grk.pair_logits.default', 'grk.pair_logits_backward.default']
+
+
+def test_hstu_core_time_bias_traces_forward_and_backward():
+    def f(pre, rab, w, b, kv, ts, rab_t):
+        y, _, _ = torch.ops.grk.hstu_core(pre, rab, w, b, kv, H, hd, 1.0 / T, 1e-8, 1, 0.0, 0, None, None, ts, rab_t)
+        return torch.autograd.grad(y.float().sum(), (pre, rab, w, b, rab_t))
+
+    pre = torch.randn(B * T, 4 * D, dtype=torch.bfloat16, requires_grad=True)
+    rab, rab_t = torch.zeros(H, T, requires_grad=True), torch.zeros(H, 16, requires_grad=True)
+    w, b = torch.ones(D, requires_grad=True), torch.zeros(D, requires_grad=True)
+    ts = torch.arange(B * T, dtype=torch.int64).view(B, T)
+    gm = make_fx(f, tracing_mode='fake')(pre, rab, w, b, torch.ones(B, T, dtype=torch.uint8), ts, rab_t)
+    assert _grk_nodes(gm) == ['grk.hstu_core.default', 'grk.hstu_core_backward.default']
+    outs = [n for n in gm.graph.nodes if n.op == 'output'][0].args[0]
+    assert outs[4].meta['val'].shape == (H, 16)   # drab_t

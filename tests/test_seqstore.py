@@ -104,3 +104,43 @@ def test_store_batches_dataloader(tmp_path):
     first = sb.perm.copy()
     sb.set_epoch(1)
     assert not np.array_equal(first, sb.perm)
+
+
+@pytest.mark.parametrize('maxlen', [20, 60])
+def test_store_timestamps_match_dataset(tmp_path, maxlen):
+    """Event times (the HSTU time-bias input; the reference loader reads and drops
+    them, model/BaseLine/dataset.py:117): SeqStore.batch(timestamps=True)'s tenth
+    field == MyDataset(args.timestamps)'s, and each position carries its own
+    record's time (user token: the user record's; padding: 0)."""
+    import json
+    from tencent_recommendation_2025_amd.dataset import MyDataset, write_synthetic_tencentgr
+    from tencent_recommendation_2025_amd.seqstore import SeqStore
+    write_synthetic_tencentgr(tmp_path, num_users=80, num_items=300, max_events=90, seed=4)
+    ds = MyDataset(tmp_path, SimpleNamespace(maxlen=maxlen, mm_emb_id=['81'], timestamps=True))
+    st = SeqStore(tmp_path, maxlen=maxlen)
+    uids = np.arange(80)
+    np.random.seed(1)
+    want = ds.collate_tensor_fn([ds[int(u)] for u in uids])
+    got = st.batch(uids, timestamps=True)
+    assert len(got) == len(want) == 10
+    assert got[9].dtype == want[9].dtype == torch.int64 and torch.equal(got[9], want[9])
+    for i in (0, 1, 3, 4, 5):
+        assert torch.equal(got[i], want[i]), i
+    # direct: rebuild each user's token order from seq.jsonl
+    T = maxlen + 1
+    with open(tmp_path / 'seq.jsonl') as f:
+        lines = [json.loads(x) for x in f]
+    for u in uids:
+        toks = []
+        for uu, i, uf, itf, _a, when in lines[u]:
+            if uu and uf:
+                toks.insert(0, (uu, when))
+            if i and itf:
+                toks.append((i, when))
+        body = toks[:-1][-T:]
+        exp = np.zeros(T, np.int64)
+        exp[T - len(body):] = [w for _, w in body]
+        assert np.array_equal(got[9][u].numpy(), exp), u
+        assert np.array_equal(got[0][u].numpy()[T - len(body):], [t for t, _ in body])
+    # the default batch keeps the reference's nine fields
+    assert len(st.batch(uids[:4])) == 9 and len(MyDataset(tmp_path, SimpleNamespace(maxlen=maxlen))[0]) == 9
