@@ -40,6 +40,7 @@ extern "C" {
 enum { GRK_OK = 0, GRK_EINVAL = 1, GRK_EHIP = 2, GRK_EUNSUPPORTED = 3 };
 enum { GRK_F32 = 0, GRK_BF16 = 1, GRK_F16 = 2 };    /* floating dtypes */
 enum { GRK_F32_BF16 = 3 };  /* pair logits: fp32 h, bf16 e_pos / e_neg (and their gradients) */
+enum { GRK_FP8_E4M3 = 4 };  /* attention q/k/v: OCP fp8 e4m3 (gfx950's fp8 format) */
 enum { GRK_I32 = 0, GRK_I64 = 1 };                  /* index dtypes */
 
 /* How a lookup derives its row id from the index tensor value v at token
@@ -256,8 +257,14 @@ typedef struct grk_attn_args {
                                       `seed`): a step replayed from a HIP graph
                                       draws a fresh mask every replay           */
   int32_t qkv_dtype;               /* precise == 2: GRK_F32 / GRK_F16 / GRK_BF16
-                                      q/k/v (read exactly, split into bf16 hi+lo);
-                                      ignored otherwise (bf16)                  */
+                                      q/k/v (read exactly, split into bf16 hi+lo).
+                                      precise 0 / 1: GRK_BF16, or GRK_FP8_E4M3 --
+                                      q/k/v are fp8 ACTIVATIONS (act NONE; long-
+                                      sequence config C5): QK^T on the fp8 MFMA
+                                      (forward, dK/dV), every other product on
+                                      bf16 MFMA over the exactly widened values;
+                                      head_dim 64 / 128, no time bias; 8-byte
+                                      aligned, ld in elements (= bytes)         */
   /* HSTU time bias (SURVEY §8 a9 rab_time; whole-sequence kernels only,
    * GRK_EUNSUPPORTED elsewhere): S[i,j] += rab_t[h, tb(ts[i] - ts[j])] with
    * tb(d) = min(2 l + h1, num_time_buckets - 1), l = floor(log2(|d| + 1)),

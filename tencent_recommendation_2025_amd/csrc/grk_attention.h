@@ -25,6 +25,7 @@ struct AttnParams {
   int in_dt;        // precise == 2: dtype of q/k/v (GRK_F32 / GRK_F16 / GRK_BF16)
   int out_f32;
   int act;  // GRK_ACT_SILU: q/k/v are pre-activations
+  int qkv_f8;  // q/k/v are OCP fp8 e4m3 (chunked kernels, head_dim 64 / 128)
   const int* seq_range;  // optional [B, 3] (first valid key, contiguous flag; longest-first order)
   unsigned long long* drab_fix;  // [H, nb] int64 fixed-point drab accumulator (deterministic)
   // HSTU time bias (whole-sequence kernels): S += rab_t[h, time_bucket(ts_q - ts_k)]
@@ -100,15 +101,16 @@ __device__ __forceinline__ bool drop_keep(unsigned long long seed, int bh, int q
 // Stage rows [r0, r0 + nrows) of a [B*T, ld] head slice into image rows
 // [dst0, dst0 + nrows) of a swizzled LDS image (zeros outside [0, T));
 // act: apply SiLU on the way (pre-activation inputs).
+// src: 0 bf16, 1 fp32, 2 fp8 e4m3 (gload8_src).
 template <int HD>
 __device__ __forceinline__ void stage_rows_at(char* dst, const void* src, int64_t ld, int b, int T, int h, int r0,
-                                              int nrows, int dst0, bool f32, bool act) {
+                                              int nrows, int dst0, int src_dt, bool act) {
   constexpr int NCH = HD / 8;
   for (int u = threadIdx.x; u < nrows * NCH; u += blockDim.x) {
     const int row = u / NCH, c = u % NCH;
     const int t = r0 + row;
     const bool ok = t >= 0 && t < T;
-    bf16x8 v = gload8_any(src, ((int64_t)b * T + (ok ? t : 0)) * ld + h * HD + c * 8, f32, ok);
+    bf16x8 v = gload8_src(src, ((int64_t)b * T + (ok ? t : 0)) * ld + h * HD + c * 8, src_dt, ok);
     if (act) v = silu8(v);
     *reinterpret_cast<uint4*>(dst + lds_off<HD>(dst0 + row, c * 8)) = __builtin_bit_cast(uint4, v);
   }
@@ -116,8 +118,37 @@ __device__ __forceinline__ void stage_rows_at(char* dst, const void* src, int64_
 
 template <int HD>
 __device__ __forceinline__ void stage_rows(char* dst, const void* src, int64_t ld, int b, int T, int h, int r0,
-                                           bool f32, bool act = false) {
-  stage_rows_at<HD>(dst, src, ld, b, T, h, r0, kChunk, 0, f32, act);
+                                           int src_dt, bool act = false) {
+  stage_rows_at<HD>(dst, src, ld, b, T, h, r0, kChunk, 0, src_dt, act);
+}
+
+// fp8 row image (the A operand rows of the fp8 QK^T MFMA): row of HD bytes =
+// HD/8 8-byte granules; granule g of row r at position g ^ (r & MASK), so the
+// 32 rows a wave reads at one column spread over the banks.
+template <int HD>
+__device__ __forceinline__ int lds8_off(int row, int col) {
+  constexpr int NG = HD / 8;
+  constexpr int MASK = NG >= 16 ? 15 : NG - 1;
+  return row * HD + (((col >> 3) ^ (row & MASK)) << 3);
+}
+
+template <int HD>
+__device__ __forceinline__ f8x8 lds_row8_f8(const char* base, int row, int col) {
+  return *reinterpret_cast<const f8x8*>(base + lds8_off<HD>(row, col));
+}
+
+// Rows [r0, r0 + kChunk) of an fp8 [B*T, ld] head slice into an fp8 row image.
+template <int HD>
+__device__ __forceinline__ void stage_rows_f8(char* dst, const void* src, int64_t ld, int b, int T, int h, int r0) {
+  constexpr int NG = HD / 8;
+  for (int u = threadIdx.x; u < kChunk * NG; u += blockDim.x) {
+    const int row = u / NG, g = u % NG;
+    const int t = r0 + row;
+    const bool ok = t >= 0 && t < T;
+    const uint2 w = ok ? *reinterpret_cast<const uint2*>((const uint8_t*)src + ((int64_t)b * T + t) * ld + h * HD + g * 8)
+                       : make_uint2(0, 0);
+    *reinterpret_cast<uint2*>(dst + lds8_off<HD>(row, g * 8)) = w;
+  }
 }
 
 __device__ __forceinline__ int seq_start(const uint8_t* kv, int b, int T, int* s_start) {

@@ -27,7 +27,9 @@
 namespace grk {
 
 // ================================================================ forward ====
-template <int HD, int KIND>
+// F8: q/k/v are fp8 e4m3 (post-activation): S^T = K Q^T on the fp8 MFMA from
+// an fp8 K image and fp8 Q fragments; V staged as (exact) bf16 for P V.
+template <int HD, int KIND, bool F8>
 __global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
   constexpr int IMG = kChunk * HD * 2;
@@ -47,12 +49,17 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
   if (KIND == 1)
     for (int j = threadIdx.x; j < p.nb; j += blockDim.x) rabs[j] = p.rab[h * p.nb + j];
 
-  bf16x8 qf[KS];
-  const bf16_t* qrow = p.q + ((int64_t)b * T + (qok ? myq : 0)) * p.ldq + h * HD;
+  bf16x8 qf[F8 ? 1 : KS];
+  f8x8 qf8[F8 ? KS : 1];
+  const int64_t qoff = ((int64_t)b * T + (qok ? myq : 0)) * p.ldq + h * HD;
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    qf[ks] = gload8(qrow + 16 * ks + 8 * hh, qok);
-    if (p.act) qf[ks] = silu8(qf[ks]);
+    if constexpr (F8) {
+      qf8[ks] = qok ? *reinterpret_cast<const f8x8*>((const uint8_t*)p.q + qoff + 16 * ks + 8 * hh) : 0;
+    } else {
+      qf[ks] = gload8(p.q + qoff + 16 * ks + 8 * hh, qok);
+      if (p.act) qf[ks] = silu8(qf[ks]);
+    }
   }
 
   f32x16 o[NDT];
@@ -69,8 +76,13 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
   const int kend = min(T, q0 + kBlockRows);
   for (int kc = kbeg; kc < kend; kc += kChunk) {
     __syncthreads();
-    stage_rows<HD>(Ks, p.k, p.ldk, b, T, h, kc, false, p.act);
-    stage_rows<HD>(Vs, p.v, p.ldv, b, T, h, kc, false, p.act);
+    if constexpr (F8) {
+      stage_rows_f8<HD>(Ks, p.k, p.ldk, b, T, h, kc);
+      stage_rows<HD>(Vs, p.v, p.ldv, b, T, h, kc, 2);
+    } else {
+      stage_rows<HD>(Ks, p.k, p.ldk, b, T, h, kc, 0, p.act);
+      stage_rows<HD>(Vs, p.v, p.ldv, b, T, h, kc, 0, p.act);
+    }
     if (threadIdx.x < kChunk) {
       const int t = kc + threadIdx.x;
       kvs[threadIdx.x] = (t < T) && (!p.key_valid || p.key_valid[(int64_t)b * T + t]);
@@ -80,9 +92,12 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
     for (int sub = 0; sub < 2; ++sub) {
       const int kb = kc + 32 * sub;
       if (kb > qw + 31 || kb >= kend || kb + 32 <= start) continue;  // wave-uniform causal/padding skip
-      f32x16 s = f32x16{};
+      f32x16 s = acc_zero();
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s = mfma(lds_row8<HD>(Ks, 32 * sub + r, 16 * ks + 8 * hh), qf[ks], s);
+      for (int ks = 0; ks < KS; ++ks) {
+        if constexpr (F8) s = mfma8(lds_row8_f8<HD>(Ks, 32 * sub + r, 16 * ks + 8 * hh), qf8[ks], s);
+        else s = mfma(lds_row8<HD>(Ks, 32 * sub + r, 16 * ks + 8 * hh), qf[ks], s);
+      }
       float pr[16], pd[16];
       if (KIND == 0) {
         float x[16], tmax = -INFINITY;
@@ -171,7 +186,8 @@ __global__ void __launch_bounds__(256) k_attn_delta(AttnParams p) {
 }
 
 // ================================================================ dQ =========
-template <int HD, int KIND>
+// F8: fp8 q/k/v read as (exact) bf16; all products on the bf16 MFMA.
+template <int HD, int KIND, bool F8>
 __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
   constexpr int IMG = kChunk * HD * 2;
@@ -200,7 +216,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
   bf16x8 qf[KS], dof[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    qf[ks] = gload8(p.q + tok * p.ldq + h * HD + 16 * ks + 8 * hh, qok);
+    qf[ks] = gload8_src(p.q, tok * p.ldq + h * HD + 16 * ks + 8 * hh, F8 ? 2 : 0, qok);
     if (p.act) qf[ks] = silu8(qf[ks]);
     dof[ks] = gload8_any(p.dout, tok * p.lddo + h * HD + 16 * ks + 8 * hh, p.dout_f32, qok);
   }
@@ -222,8 +238,8 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
   const int kend = min(T, q0 + kBlockRows);
   for (int kc = kbeg; kc < kend; kc += kChunk) {
     __syncthreads();
-    stage_rows<HD>(Ks, p.k, p.ldk, b, T, h, kc, false, p.act);
-    stage_rows<HD>(Vs, p.v, p.ldv, b, T, h, kc, false, p.act);
+    stage_rows<HD>(Ks, p.k, p.ldk, b, T, h, kc, F8 ? 2 : 0, p.act);
+    stage_rows<HD>(Vs, p.v, p.ldv, b, T, h, kc, F8 ? 2 : 0, p.act);
     if (threadIdx.x < kChunk) {
       const int t = kc + threadIdx.x;
       kvs[threadIdx.x] = (t < T) && (!p.key_valid || p.key_valid[(int64_t)b * T + t]);
@@ -233,7 +249,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
     for (int sub = 0; sub < 2; ++sub) {
       const int kb = kc + 32 * sub;
       if (kb > qw + 31 || kb >= kend || kb + 32 <= start) continue;
-      f32x16 s = f32x16{}, dp = f32x16{};
+      f32x16 s = acc_zero(), dp = acc_zero();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         s = mfma(lds_row8<HD>(Ks, 32 * sub + r, 16 * ks + 8 * hh), qf[ks], s);
@@ -279,14 +295,18 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
 }
 
 // ============================================================== dK / dV =====
-template <int HD, int KIND>
+// F8: S = Q K^T on the fp8 MFMA (fp8 Q image + fp8 K fragments); Q also
+// staged as (exact) bf16 for dK = dS^T Q, V fragments as bf16 for dP.
+template <int HD, int KIND, bool F8>
 __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
   constexpr int IMG = kChunk * HD * 2;
+  constexpr int IMG8 = F8 ? kChunk * HD : 0;
   constexpr int RAB = KIND == 1 ? kRabMax : 4;
-  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 2 * kChunk * 4 + RAB * 4 + 16];
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + IMG8 + 2 * kChunk * 4 + RAB * 4 + 16];
   char* Qs = smem;
   char* Ds = smem + IMG;
+  char* Q8s = smem + 2 * IMG + 2 * kChunk * 4 + RAB * 4 + 16;
   float* lses = reinterpret_cast<float*>(smem + 2 * IMG);
   float* dlts = lses + kChunk;
   float* rabs = dlts + kChunk;
@@ -302,14 +322,21 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
   const int bh = b * p.H + h;
   const int64_t tok = (int64_t)b * T + (myk < T ? myk : 0);
 
-  bf16x8 kf[KS], vf[KS];
+  bf16x8 kf[F8 ? 1 : KS], vf[KS];
+  f8x8 kf8[F8 ? KS : 1];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    kf[ks] = gload8(p.k + tok * p.ldk + h * HD + 16 * ks + 8 * hh, myk < T);
-    vf[ks] = gload8(p.v + tok * p.ldv + h * HD + 16 * ks + 8 * hh, myk < T);
-    if (p.act) {
-      kf[ks] = silu8(kf[ks]);
-      vf[ks] = silu8(vf[ks]);
+    const int64_t ko = tok * p.ldk + h * HD + 16 * ks + 8 * hh;
+    if constexpr (F8) {
+      kf8[ks] = myk < T ? *reinterpret_cast<const f8x8*>((const uint8_t*)p.k + ko) : 0;
+      vf[ks] = gload8_src(p.v, tok * p.ldv + h * HD + 16 * ks + 8 * hh, 2, myk < T);
+    } else {
+      kf[ks] = gload8(p.k + ko, myk < T);
+      vf[ks] = gload8(p.v + tok * p.ldv + h * HD + 16 * ks + 8 * hh, myk < T);
+      if (p.act) {
+        kf[ks] = silu8(kf[ks]);
+        vf[ks] = silu8(vf[ks]);
+      }
     }
   }
   f32x16 dk[NDT], dv[NDT];
@@ -324,8 +351,9 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
   const int qbeg = (max(k0, start) / 32) * 32;
   for (int qc = qbeg; qc < T; qc += kChunk) {
     __syncthreads();
-    stage_rows<HD>(Qs, p.q, p.ldq, b, T, h, qc, false, p.act);
-    stage_rows<HD>(Ds, p.dout, p.lddo, b, T, h, qc, p.dout_f32);
+    stage_rows<HD>(Qs, p.q, p.ldq, b, T, h, qc, F8 ? 2 : 0, p.act);
+    if constexpr (F8) stage_rows_f8<HD>(Q8s, p.q, p.ldq, b, T, h, qc);
+    stage_rows<HD>(Ds, p.dout, p.lddo, b, T, h, qc, p.dout_f32 ? 1 : 0);
     if (threadIdx.x < kChunk) {
       const int t = qc + threadIdx.x;
       float lv = -INFINITY, dl = 0.f;
@@ -341,10 +369,11 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
     for (int sub = 0; sub < 2; ++sub) {
       const int qb = qc + 32 * sub;
       if (qb + 31 < kw || qb >= T) continue;  // wave-uniform: every query precedes this wave's keys
-      f32x16 s = f32x16{}, dp = f32x16{};
+      f32x16 s = acc_zero(), dp = acc_zero();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        s = mfma(lds_row8<HD>(Qs, 32 * sub + r, 16 * ks + 8 * hh), kf[ks], s);
+        if constexpr (F8) s = mfma8(lds_row8_f8<HD>(Q8s, 32 * sub + r, 16 * ks + 8 * hh), kf8[ks], s);
+        else s = mfma(lds_row8<HD>(Qs, 32 * sub + r, 16 * ks + 8 * hh), kf[ks], s);
         dp = mfma(lds_row8<HD>(Ds, 32 * sub + r, 16 * ks + 8 * hh), vf[ks], dp);
       }
       float pd[16], ds[16];
@@ -393,21 +422,21 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
   store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, 1.f, myk < T, p.act ? p.v : nullptr, p.ldv);
 }
 
-template <int HD>
+template <int HD, bool F8 = false>
 static int launch_hd(const AttnParams& p, int which, hipStream_t s) {
   dim3 grid((p.T + kBlockRows - 1) / kBlockRows, p.H, p.B);
   if (which == 0) {
-    if (p.kind == GRK_ATTN_SOFTMAX) k_attn_fwd<HD, 0><<<grid, 256, 0, s>>>(p);
-    else k_attn_fwd<HD, 1><<<grid, 256, 0, s>>>(p);
+    if (p.kind == GRK_ATTN_SOFTMAX) k_attn_fwd<HD, 0, F8><<<grid, 256, 0, s>>>(p);
+    else k_attn_fwd<HD, 1, F8><<<grid, 256, 0, s>>>(p);
   } else if (which == 1) {
     const int64_t waves = (int64_t)p.B * p.T * p.H;
     k_attn_delta<HD><<<(unsigned)((waves + 3) / 4), 256, 0, s>>>(p);
   } else if (which == 2) {
-    if (p.kind == GRK_ATTN_SOFTMAX) k_attn_bwd_dq<HD, 0><<<grid, 256, 0, s>>>(p);
-    else k_attn_bwd_dq<HD, 1><<<grid, 256, 0, s>>>(p);
+    if (p.kind == GRK_ATTN_SOFTMAX) k_attn_bwd_dq<HD, 0, F8><<<grid, 256, 0, s>>>(p);
+    else k_attn_bwd_dq<HD, 1, F8><<<grid, 256, 0, s>>>(p);
   } else {
-    if (p.kind == GRK_ATTN_SOFTMAX) k_attn_bwd_dkdv<HD, 0><<<grid, 256, 0, s>>>(p);
-    else k_attn_bwd_dkdv<HD, 1><<<grid, 256, 0, s>>>(p);
+    if (p.kind == GRK_ATTN_SOFTMAX) k_attn_bwd_dkdv<HD, 0, F8><<<grid, 256, 0, s>>>(p);
+    else k_attn_bwd_dkdv<HD, 1, F8><<<grid, 256, 0, s>>>(p);
   }
   GRK_LAUNCH_CHECK();
   return GRK_OK;
@@ -420,6 +449,12 @@ __global__ void k_drab_finalize(float* __restrict__ drab, const unsigned long lo
 }
 
 static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
+  if (p.qkv_f8) {  // fp8 q/k/v: the chunked kernels (C5: T = 1025), head_dim 64 / 128
+    if (hd == 64) return launch_hd<64, true>(p, which, s);
+    if (hd == 128) return launch_hd<128, true>(p, which, s);
+    set_error("fp8 q/k/v attention supports head_dim 64 / 128, not %d", hd);
+    return GRK_EUNSUPPORTED;
+  }
   if (which != 1 && attn_seq_launch(p, hd, which, s)) {
     GRK_LAUNCH_CHECK();
     return GRK_OK;
@@ -475,6 +510,10 @@ static int fill_params(const grk_attn_args* a, AttnParams* p) {
   GRK_CHECK_ARG(a->precise >= 0 && a->precise <= 2, "precise must be 0, 1 or 2");
   GRK_CHECK_ARG(a->precise != 2 || a->qkv_dtype == GRK_F32 || a->qkv_dtype == GRK_F16 || a->qkv_dtype == GRK_BF16,
                 "qkv_dtype must be GRK_F32 / GRK_F16 / GRK_BF16");
+  const bool f8 = a->precise != 2 && a->qkv_dtype == GRK_FP8_E4M3;
+  GRK_CHECK_ARG(!f8 || a->act == GRK_ACT_NONE, "fp8 q/k/v hold activations: act must be GRK_ACT_NONE");
+  GRK_CHECK_ARG(!f8 || a->num_time_buckets == 0, "fp8 q/k/v: no time bias (whole-sequence kernels only)");
+  GRK_CHECK_ARG(!f8 || ((uintptr_t)a->q | (uintptr_t)a->k | (uintptr_t)a->v) % 8 == 0, "fp8 q/k/v: 8-byte aligned");
   GRK_CHECK_ARG(a->num_time_buckets >= 0 && a->num_time_buckets <= kMaxTimeBuckets,
                 "num_time_buckets must be in [0, %d]", kMaxTimeBuckets);
   GRK_CHECK_ARG(a->num_time_buckets == 0 || (a->kind == GRK_ATTN_HSTU && a->timestamps && a->rab_t),
@@ -492,6 +531,7 @@ static int fill_params(const grk_attn_args* a, AttnParams* p) {
   p->precise = a->precise; p->out_f32 = a->out_dtype == GRK_F32;
   p->in_dt = a->precise == 2 ? a->qkv_dtype : GRK_BF16;
   p->act = a->act;
+  p->qkv_f8 = f8;
   p->seq_range = a->seq_range;
   return GRK_OK;
 }

@@ -118,6 +118,40 @@ __device__ __forceinline__ bf16x8 gload8_any(const void* base, int64_t off, bool
   return r;
 }
 
+// ---- OCP fp8 e4m3 (gfx950's fp8 format) ----
+// Eight e4m3 values in one 64-bit fragment: the A / B operand of the fp8
+// 32x32x16 MFMA, same lane map as the bf16 form (element j of lane (r, hh) is
+// k = 8hh + j) and the bf16 form's rate; products of fp8 values are exact in
+// its fp32 accumulation.
+typedef long f8x8;
+
+__device__ __forceinline__ f32x16 mfma8(f8x8 a, f8x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c, 0, 0, 0);
+}
+
+// Eight e4m3 values (bytes of w, element 0 in the lowest byte) as bf16.  Exact:
+// every e4m3 value is a bf16 value (3 mantissa bits, exponents 2^-9 .. 2^8),
+// so the fp32 result of v_cvt_pk_f32_fp8 truncates to bf16 without rounding.
+__device__ __forceinline__ bf16x8 f8x8_to_bf16(uint2 w) {
+  const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)w.x, false), b = __builtin_amdgcn_cvt_pk_f32_fp8((int)w.x, true);
+  const f32x2 c = __builtin_amdgcn_cvt_pk_f32_fp8((int)w.y, false), d = __builtin_amdgcn_cvt_pk_f32_fp8((int)w.y, true);
+  const uint32_t words[4] = {(__float_as_uint(a.x) >> 16) | (__float_as_uint(a.y) & 0xFFFF0000u),
+                             (__float_as_uint(b.x) >> 16) | (__float_as_uint(b.y) & 0xFFFF0000u),
+                             (__float_as_uint(c.x) >> 16) | (__float_as_uint(c.y) & 0xFFFF0000u),
+                             (__float_as_uint(d.x) >> 16) | (__float_as_uint(d.y) & 0xFFFF0000u)};
+  return words8(words);
+}
+
+// Eight consecutive elements from global as bf16: src 0 = bf16, 1 = fp32
+// (rounded), 2 = fp8 e4m3 (exact); zero when !ok.
+__device__ __forceinline__ bf16x8 gload8_src(const void* base, int64_t off, int src, bool ok) {
+  if (src == 2) {
+    const uint2 w = ok ? *reinterpret_cast<const uint2*>((const uint8_t*)base + off) : make_uint2(0, 0);
+    return f8x8_to_bf16(w);
+  }
+  return gload8_any(base, off, src == 1, ok);
+}
+
 // SiLU of each element, computed in fp32 and rounded to bf16 (= F.silu on bf16).
 __device__ __forceinline__ bf16x8 silu8(bf16x8 x) {
   bf16x8 r;

@@ -310,17 +310,26 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
     2 (fp32 fidelity: Q/K/V and dO split into hi + lo as well; q/k/v may then be
     fp32 / fp16 / bf16 and are read exactly -- fidelity_supported(T, hd)).
     timestamps (int64 [B, T]) + rab_t (fp32 [H, nbt], nbt <= 64): the HSTU time
-    bias rab_t[h, time_bucket(t_q - t_k)] (include/grk.h, grk_attn_args)."""
+    bias rab_t[h, time_bucket(t_q - t_k)] (include/grk.h, grk_attn_args).
+    float8_e4m3fn q/k/v (precise 0 / 1, act None; head_dim 64 / 128): the fp8
+    attention of config C5 -- QK^T on the fp8 MFMA, the rest on bf16 MFMA over
+    the exactly widened values."""
     precise = int(precise)
     if precise not in (0, 1, 2):
         raise L.GrkError('precise must be 0, 1 or 2')
-    dts = (torch.bfloat16, torch.float32, torch.float16) if precise == 2 else (torch.bfloat16,)
+    f8 = q.dtype == torch.float8_e4m3fn
+    if precise == 2:
+        dts = (torch.bfloat16, torch.float32, torch.float16)
+    else:
+        dts = (torch.float8_e4m3fn,) if f8 else (torch.bfloat16,)
     for t, n in ((q, 'q'), (k, 'k'), (v, 'v')):
         _col_view_ok(t, n, dts)
-    if not q.dtype == k.dtype == v.dtype:
-        raise L.GrkError('q, k and v must share a dtype')
         if t.shape[0] != B * T or t.shape[1] < H * hd:
             raise L.GrkError(f'{n}: shape {tuple(t.shape)} does not fit B*T={B * T}, H*hd={H * hd}')
+    if not q.dtype == k.dtype == v.dtype:
+        raise L.GrkError('q, k and v must share a dtype')
+    if f8 and act is not None:
+        raise L.GrkError('fp8 q/k/v hold activations: act must be None')
     if key_valid is not None:
         if key_valid.dtype != torch.uint8 or key_valid.shape != (B, T) or not key_valid.is_contiguous():
             raise L.GrkError('key_valid must be a contiguous uint8 [B, T] tensor')
@@ -348,7 +357,8 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
                          v.stride(0), _ptr(key_valid), _ptr(rab), float(scale), float(inv_n), float(dropout_p),
                          precise, seed, L.dtype_code(out_dtype),
                          {None: L.ACT_NONE, 'silu': L.ACT_SILU}[act], _ptr(seq_range), _ptr(seed_dev),
-                         L.dtype_code(q.dtype), _ptr(timestamps), _ptr(rab_t), nbt, None, None)
+                         L.GRK_FP8_E4M3 if f8 else L.dtype_code(q.dtype), _ptr(timestamps), _ptr(rab_t), nbt, None,
+                         None)
     args._keep = (q, k, v, key_valid, rab, seq_range, seed_dev, timestamps, rab_t)  # raw pointers: keep alive
     return args
 

@@ -494,3 +494,80 @@ def test_time_bias_outside_whole_sequence_kernels_is_refused(K):
         K.attn_args(L.ATTN_SOFTMAX, x[:, :64], x[:, 64:128], x[:, 128:], 2, 32, 1, 64,
                     timestamps=torch.zeros(2, 32, dtype=torch.int64, device=DEV),
                     rab_t=torch.zeros(1, 8, device=DEV))
+
+
+# ----------------------------------------------------------- fp8 (C5) ----
+# Config C5 (BASELINE.json configs[4]): d=1024, T=1025, fp8 attention.  q/k/v
+# are OCP e4m3 activations; the oracle sees exactly those values (widened to
+# fp64), so the 1e-3 bar applies unchanged: QK^T products of fp8 values are
+# exact in the MFMA's fp32 accumulation and P / dS enter as bf16 hi + lo.
+def run_fp8(K, kind, B, T, H, hd, lens, seed=0, out_dtype=torch.float32):
+    from tencent_recommendation_2025_amd import _lib as L
+    D = H * hd
+    rng = np.random.default_rng(seed)
+    x8 = torch.from_numpy(rng.standard_normal((B * T, 3 * D)).astype(np.float32)).to(torch.float8_e4m3fn)
+    x = x8.float().numpy()
+    valid = np.zeros((B, T), np.uint8)
+    for b, n in enumerate(lens):
+        valid[b, T - n:] = 1
+    xd = x8.to(DEV)
+    kv = torch.from_numpy(valid).to(DEV)
+    extra, rab_np = {}, None
+    if kind == L.ATTN_HSTU:
+        rab_np = (np.random.default_rng(seed + 1).standard_normal((H, T)) * 0.5).astype(np.float32)
+        extra = dict(rab=torch.from_numpy(rab_np).to(DEV), inv_n=1.0 / T, scale=hd ** -0.5)
+    args = K.attn_args(kind, xd[:, :D], xd[:, D:2 * D], xd[:, 2 * D:], B, T, H, hd, key_valid=kv, precise=1,
+                       out_dtype=out_dtype, **extra)
+    out = torch.empty(B * T, D, device=DEV, dtype=out_dtype)
+    lse = torch.empty(B, H, T, device=DEV)
+    K.attention_fwd(args, out, lse)
+    dout_np = to_bf16_f32(np.random.default_rng(seed + 2).standard_normal((B * T, D)).astype(np.float32))
+    dout = torch.from_numpy(dout_np).to(DEV).to(out_dtype)
+    dq, dk, dv = (torch.empty(B * T, D, device=DEV, dtype=out_dtype) for _ in range(3))
+    drab = torch.zeros(H, T, device=DEV) if kind == L.ATTN_HSTU else None
+    K.attention_bwd(args, out, dout, lse, torch.empty(B, H, T, device=DEV), dq, dk, dv, drab)
+    torch.cuda.synchronize()
+    qh, kh, vh = (heads(x[:, i * D:(i + 1) * D].astype(np.float64), B, T, H, hd) for i in range(3))
+    doh = heads(dout_np, B, T, H, hd)
+    if kind == L.ATTN_SOFTMAX:
+        o, _, _ = oatt.forward(qh, kh, vh, valid.astype(bool))
+        gq, gk, gv = oatt.backward(qh, kh, vh, valid.astype(bool), doh)
+        want = dict(out=flat(o), dq=flat(gq), dk=flat(gk), dv=flat(gv))
+    else:
+        o, _, _ = ohstu.forward(qh, kh, vh, valid.astype(bool), rab_np, hd ** -0.5, 1.0 / T)
+        gq, gk, gv, gr = ohstu.backward(qh, kh, vh, valid.astype(bool), rab_np, hd ** -0.5, 1.0 / T, doh)
+        want = dict(out=flat(o), dq=flat(gq), dk=flat(gk), dv=flat(gv), drab=gr)
+    res = {k_: t.float().cpu().numpy() for k_, t in (('out', out), ('dq', dq), ('dk', dk), ('dv', dv))}
+    if drab is not None:
+        res['drab'] = drab.cpu().numpy()
+    return res, want
+
+
+@pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
+@pytest.mark.parametrize('hd,H,T,lens', [(128, 2, 1025, [1025, 700]), (64, 2, 300, [300, 129, 1]),
+                                         (128, 1, 77, [77, 40])])
+def test_fp8_attention_matches_oracle(K, kind, hd, H, T, lens):
+    res, want = run_fp8(K, kind, B=len(lens), T=T, H=H, hd=hd, lens=lens, seed=T + hd)
+    for key in want:
+        err = nrel(res[key], want[key])
+        assert err < TOL_PRECISE, f'{key}: normwise rel err {err:.2e}'
+
+
+def test_fp8_attention_bf16_out_repeatable(K):
+    a, want = run_fp8(K, 1, B=2, T=1025, H=2, hd=128, lens=[1025, 513], seed=5, out_dtype=torch.bfloat16)
+    for key in ('out', 'dq', 'dk', 'dv'):
+        assert nrel(a[key], to_bf16_f32(np.asarray(want[key], np.float32))) < TOL_PRECISE, key
+    assert nrel(a['drab'], want['drab']) < TOL_PRECISE
+    b, _ = run_fp8(K, 1, B=2, T=1025, H=2, hd=128, lens=[1025, 513], seed=5, out_dtype=torch.bfloat16)
+    for key in a:
+        assert np.array_equal(a[key], b[key]), key
+
+
+def test_fp8_attention_refusals(K):
+    from tencent_recommendation_2025_amd import _lib as L
+    x = torch.zeros(64, 3 * 32, device=DEV).to(torch.float8_e4m3fn)
+    a = K.attn_args(L.ATTN_SOFTMAX, x[:, :32], x[:, 32:64], x[:, 64:], 2, 32, 1, 32, precise=1)
+    with pytest.raises(RuntimeError, match='head_dim 64 / 128'):
+        K.attention_fwd(a, torch.empty(64, 32, device=DEV), torch.empty(2, 1, 32, device=DEV))
+    with pytest.raises(RuntimeError, match='act'):
+        K.attn_args(L.ATTN_SOFTMAX, x[:, :32], x[:, 32:64], x[:, 64:], 2, 32, 1, 32, act='silu')
