@@ -25,6 +25,10 @@ $(OBJ_DIR)/grk_attention_seq.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
 # run-to-run different outputs
 $(OBJ_DIR)/grk_attention_seq.o: HIPFLAGS += -fno-slp-vectorize
 
+# residual quantisation: codes must be a pure function of fp32 inputs (no FMA
+# contraction of the squared differences; oracle/rqvae.py restates the order)
+$(OBJ_DIR)/grk_rqvae.o: HIPFLAGS += -ffp-contract=off
+
 $(OBJ_DIR):
 	mkdir -p $@
 

@@ -68,6 +68,9 @@ def parse():
                     help='build only each rank\'s table rows (default: sharded and >= 10M items, BASELINE config 3)')
     ap.add_argument('--graph', type=int, default=1,
                     help='capture the training step in a HIP graph and replay it (row-sharded: forward + backward)')
+    ap.add_argument('--semantic-ids', type=int, default=0,
+                    help='config 4: RQ-VAE semantic-id levels added as O1 item_sparse features (0 = off)')
+    ap.add_argument('--sid-codes', type=int, default=256, help='config 4: codes per RQ-VAE level')
     return ap.parse_args()
 
 
@@ -363,6 +366,47 @@ def cpu_baseline(a, stats, types):
                       f'here to keep the bench within minutes)'}
 
 
+FP32_VALU_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector (packed FMA)
+
+
+def semantic_id_setup(a, dev, reps):
+    """Config 4: tokenise the whole item table with an RQ-VAE (mm feature 81,
+    [items, 32] -> latent 64 -> levels x sid_codes codes) and return the
+    per-item semantic-id rows plus the code search's roofline entry.
+
+    grk_rq_assign is VALU-bound: per row levels * codes * latent * 3 FLOP (one
+    difference, square and add per element; no FMA so the codes are exact).  A
+    packed v_pk_add/v_pk_mul issue does 2 FLOP per lane, half a packed FMA's
+    4, so the FMA-free ceiling is 0.5 of the 157.3 TFLOP/s vector peak."""
+    from tencent_recommendation_2025_amd.rqvae import RQVAE, rq_assign, semantic_id_table
+    g = torch.Generator(device=dev).manual_seed(81)
+    mm = torch.randn(a.items, 32, device=dev, generator=g)
+    torch.manual_seed(4)
+    tok = RQVAE(32, hidden=(256, 128), latent_dim=64, levels=a.semantic_ids, codebook_size=a.sid_codes).to(dev)
+    tok.init_codebooks(mm[:65536], iters=5)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    codes = tok.tokenize(mm)
+    torch.cuda.synchronize()
+    tok_s = time.perf_counter() - t0
+    with torch.no_grad():
+        z = tok.encode(mm)
+    cb = tok.codebooks.detach().contiguous()
+    ms = _time(lambda: rq_assign(z, cb, want_quant=False), reps)
+    flops = 3.0 * a.items * a.semantic_ids * a.sid_codes * 64
+    tfs = flops / (ms * 1e-3) / 1e12
+    roof = {'bound': 'valu', 'kernel': 'grk::k_rq_assign<64> (RQ-VAE code search, whole item table)',
+            'achieved': round(tfs, 1), 'peak': FP32_VALU_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': round(tfs / FP32_VALU_PEAK_TFLOPS, 4), 'fma_free_ceiling_frac': 0.5, 'traffic': None,
+            'avg_launch_us': round(ms * 1e3, 1), 'flops_per_launch': int(flops),
+            'alg_bytes_per_launch': int(a.items * (64 * 4 + a.semantic_ids * 4)),
+            'tokenize_items_per_s': round(a.items / tok_s, 1),
+            'workload': {'rows': a.items, 'latent': 64, 'levels': a.semantic_ids, 'codes': a.sid_codes}}
+    sid = semantic_id_table(codes, a.items)
+    del mm, z, tok
+    return sid, roof
+
+
 def main():
     a = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -386,8 +430,9 @@ def main():
     from tencent_recommendation_2025_amd.optim import FusedAdamW
     from tencent_recommendation_2025_amd.train import Trainer
 
+    sid, sid_roof = (semantic_id_setup(a, dev, a.roofline_reps) if a.semantic_ids else (None, None))
     cfg = S.SyntheticConfig(batch_size=a.batch, maxlen=a.maxlen, num_items=a.items, num_users=a.users, zipf=a.zipf,
-                            timestamps=a.time_buckets > 0)
+                            timestamps=a.time_buckets > 0, sid_table=sid, sid_codes=a.sid_codes)
     stats, types = S.feature_schema(cfg)
     margs = S.make_args(hidden_units=a.hidden, maxlen=a.maxlen, num_blocks=a.blocks, num_heads=a.heads,
                         block=a.block, dropout_rate=a.dropout, hstu_time_buckets=a.time_buckets)
@@ -446,9 +491,11 @@ def main():
     more.append(wgrad_roofline(a, a.roofline_reps))
     if btrace:
         more.append(backward_roofline(btrace, a.roofline_reps))
+    if sid_roof is not None:
+        more.append(sid_roof)
 
     cpu = None
-    if rank == 0 and world == 1 and a.cpu_baseline:
+    if rank == 0 and world == 1 and a.cpu_baseline and not a.semantic_ids:   # config 2's CPU model only
         cpu = cpu_baseline(a, stats, types)
 
     if rank == 0:
@@ -458,7 +505,10 @@ def main():
             'value': round(value, 2), 'unit': 'seq/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
             'ms_per_step': round(elapsed / a.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'bf16', 'data': 'synthetic (device-resident TencentGR-shaped batches)',
-            'config': {'workload': f'BASELINE config {3 if shard_tables else 2}: {a.block.upper()} d={a.hidden} L={a.maxlen} '
+            'config': {'workload': f'BASELINE config {4 if a.semantic_ids else 3 if shard_tables else 2}: '
+                                   + (f'O1 + RQ-VAE semantic ids ({a.semantic_ids} levels x {a.sid_codes} codes '
+                                      f'as item_sparse features), ' if a.semantic_ids else '')
+                                   + f'{a.block.upper()} d={a.hidden} L={a.maxlen} '
                                    f'({a.blocks} blocks x {a.heads} heads), {a.items}-item bf16 table, '
                                    f'{a.users} users, loss={a.loss}, table AdamW={a.table_mode}, '
                                    f'dropout={a.dropout}'

@@ -505,6 +505,21 @@ int grk_sample_negatives(const int32_t* pos, const int32_t* next_token_type, int
                          int32_t max_tries, const int32_t* item_feat, int32_t num_feat, const uint8_t* item_ok,
                          int32_t* neg, int32_t* neg_feat, int32_t* err_flag, void* stream);
 
+/* Residual quantisation -- the code search of config 4's RQ-VAE semantic-ID
+ * tokenizer (BASELINE.json configs[3]; the reference has no tokenizer: the
+ * semantic ids it produces enter the O1 model as item_sparse features,
+ * model/BaseLineO1/model.py:271-280, 355).  z [n, dim] fp32 row-major (row
+ * stride ld_z, 16-byte aligned), codebooks [levels, codes, dim] fp32
+ * contiguous; dim in {16, 32, 64, 128}, 1 <= levels <= 8.  Per row:
+ * r_0 = z; code_l = argmin_k sum_j (r_l[j] - C_l[k][j])^2 in fp32 (difference,
+ * square and running sum each rounded, j ascending; lowest k on ties);
+ * r_{l+1} = r_l - C_l[code_l].  out_codes int32 [n, levels]; optional (NULL =
+ * skipped): out_quant [n, dim] = C_0[code_0] + C_1[code_1] + ... (level
+ * order), out_dist [n, levels] = the minimum distances, out_resid [n, dim] =
+ * r_levels.  Bit-exact vs oracle/rqvae.py. */
+int grk_rq_assign(const float* z, int64_t ld_z, const float* codebooks, int64_t n, int dim, int codes, int levels,
+                  int32_t* out_codes, float* out_quant, float* out_dist, float* out_resid, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

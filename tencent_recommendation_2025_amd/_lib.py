@@ -109,6 +109,7 @@ SIGNATURES = {
     'grk_mips_topk_workspace': (_SZ, [_I64, _I64]),
     'grk_mips_topk': (_I, [_P, _I64, _P, _I64, _I, _I64, _I64, _I, _I, _P, _P, _P, _P, _SZ, _P]),
     'grk_sample_negatives': (_I, [_P, _P, _I64, _I, _P, _I, _I64, C.c_uint64, _I, _P, _I, _P, _P, _P, _P, _P]),
+    'grk_rq_assign': (_I, [_P, _I64, _P, _I64, _I, _I, _I, _P, _P, _P, _P, _P]),
     'grk_gemm': (_I, [_I, _I, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _I, _P, _F, _F, _P, _I, _P]),
     'grk_pair_logits_partials': (_SZ, [_I64]),
     'grk_sampled_softmax_workspace': (_SZ, [_I64, _I]),

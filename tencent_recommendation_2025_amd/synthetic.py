@@ -36,6 +36,10 @@ class SyntheticConfig:
     zipf: float | None = None
     mm_ids: list = field(default_factory=lambda: ['81'])
     timestamps: bool = False   # append int64 [B, T] event times (the HSTU time bias input)
+    # config 4: RQ-VAE semantic ids as extra item_sparse features 'sid0'..;
+    # sid_table int64 [num_items + 1, levels] (rqvae.semantic_id_table), values 1..sid_codes
+    sid_table: object = None
+    sid_codes: int = 256
 
 
 def feature_schema(cfg: SyntheticConfig):
@@ -47,7 +51,13 @@ def feature_schema(cfg: SyntheticConfig):
         stats[f] = cfg.user_sparse_card
     for f in USER_ARRAY:
         stats[f] = cfg.user_array_card
-    types = {'user_sparse': list(USER_SPARSE), 'item_sparse': list(ITEM_SPARSE), 'item_array': [],
+    item_sparse = list(ITEM_SPARSE)
+    if cfg.sid_table is not None:
+        from .rqvae import semantic_id_schema
+        names, sid_stats = semantic_id_schema(cfg.sid_table.shape[1], cfg.sid_codes)
+        item_sparse += names
+        stats.update(sid_stats)
+    types = {'user_sparse': list(USER_SPARSE), 'item_sparse': item_sparse, 'item_array': [],
              'user_array': list(USER_ARRAY), 'item_emb': list(cfg.mm_ids), 'user_continual': [],
              'item_continual': []}
     return stats, types
@@ -93,6 +103,10 @@ def make_batch(cfg: SyntheticConfig, generator: torch.Generator, device='cuda'):
         for k, f in enumerate(ITEM_SPARSE):
             card = cfg.item_sparse_card[k % len(cfg.item_sparse_card)]
             out[f] = torch.where(mask, _hash_feat(ids, k, card), torch.zeros_like(ids))
+        if cfg.sid_table is not None:
+            rows = cfg.sid_table[ids]
+            for lvl in range(rows.shape[-1]):
+                out[f'sid{lvl}'] = torch.where(mask, rows[..., lvl], torch.zeros_like(ids))
         for f in cfg.mm_ids:
             mm = torch.randn(B, T, 32 if f == '81' else 1024, generator=g, device=dev)
             out[f] = mm * mask.unsqueeze(-1)
