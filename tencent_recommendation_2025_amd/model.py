@@ -201,6 +201,10 @@ class BaselineModel(torch.nn.Module):
         self.block = getattr(args, 'block', 'softmax')
         d = args.hidden_units
         self.hidden_units = d
+        # feature tables with more rows than this are looked up directly into the
+        # dnn operand instead of projected (see _projection): projecting costs
+        # ~6 rows d^2 FLOP per forward + backward, a direct block ~6 tokens d^2
+        self.proj_max_rows = int(getattr(args, 'proj_max_rows', 100_000))
         if getattr(args, 'shard_tables', False):
             # row-sharded item / user tables (BASELINE config 3, 50M rows): the full
             # tables are never built on any rank -- ShardedFusedAdamW creates each
@@ -320,6 +324,20 @@ class BaselineModel(torch.nn.Module):
     # GFLOP at d=512) and their lookups become ONE bag-sum gather of projected
     # rows, so the dnn GEMMs run with K = d + 40 instead of 16d / 9d.  The
     # projections are plain torch ops, so autograd produces dE_f and dW_f.
+    # The projection costs rows x d^2 however few rows a batch touches, so tables
+    # with more than proj_max_rows rows (real vocabularies) are instead gathered
+    # as their own d-column blocks of the GEMM operand (_direct_feats), right
+    # after the item / user rows, with their W_f blocks in the composed weight.
+    def _dnn_feats(self, which):
+        if which == 'item':
+            return list(self.ITEM_SPARSE_FEAT) + list(self.ITEM_ARRAY_FEAT)
+        return list(self.USER_SPARSE_FEAT) + list(self.USER_ARRAY_FEAT)
+
+    def _direct_feats(self, which):
+        """[(feature, dnn block index)] of the tables looked up unprojected."""
+        return [(k, j + 1) for j, k in enumerate(self._dnn_feats(which))
+                if self.sparse_emb[k].num_embeddings > self.proj_max_rows]
+
     def _projection(self, which):
         """(P [rows, d], {feature: P row of its table's row 0}) for the item or user dnn.
 
@@ -331,14 +349,13 @@ class BaselineModel(torch.nn.Module):
         if self._fwd_id is not None and key in self._proj_cache:
             return self._proj_cache[key]
         d = self.hidden_units
-        if which == 'item':
-            feats, dnn = list(self.ITEM_SPARSE_FEAT) + list(self.ITEM_ARRAY_FEAT), self.itemdnn
-        else:
-            feats, dnn = list(self.USER_SPARSE_FEAT) + list(self.USER_ARRAY_FEAT), self.userdnn
+        feats, dnn = self._dnn_feats(which), (self.itemdnn if which == 'item' else self.userdnn)
+        direct = {k for k, _ in self._direct_feats(which)}
         Wv = dnn.weight.view(d, -1, d)  # [d_out, block, d_in]
         by_rows = {}
         for j, k in enumerate(feats):  # block 0 is item_emb / user_emb
-            by_rows.setdefault(self.sparse_emb[k].num_embeddings, []).append((k, j + 1))
+            if k not in direct:
+                by_rows.setdefault(self.sparse_emb[k].num_embeddings, []).append((k, j + 1))
         parts, offs, row = [], {}, 0
         for rows, group in by_rows.items():
             refs = {k: self._ref(f'sparse_emb.{k}') for k, _ in group}
@@ -381,10 +398,12 @@ class BaselineModel(torch.nn.Module):
         return torch.where(x > 0, x + off, 0)
 
     def _dnn_weight(self, which, width):
-        """[d, width] = [W_0 | W_mm Wt | b' | 0] matching the operand [rows | mm | 1 | pad]."""
+        """[d, width] = [W_0 | W_f (direct features) | W_mm Wt | b' | 0] matching the
+        operand [rows | direct feature rows | mm | 1 | pad]."""
         d = self.hidden_units
         dnn = self.itemdnn if which == 'item' else self.userdnn
         W, cols, bias = dnn.weight, [dnn.weight[:, :d]], dnn.bias[:, None]
+        cols += [W[:, j * d:(j + 1) * d] for _, j in self._direct_feats(which)]
         if which == 'item':
             base = (1 + len(self.ITEM_SPARSE_FEAT) + len(self.ITEM_ARRAY_FEAT)) * d
             for j, k in enumerate(self.ITEM_EMB_FEAT):
@@ -413,12 +432,19 @@ class BaselineModel(torch.nn.Module):
         col = 0
         ones = None
 
-        def operand(ref, mode, dense):
-            """gather block [rows | dense | 1 | pad] feeding one dnn GEMM; returns its split."""
+        def operand(ref, mode, dense, which):
+            """gather block [rows | direct feature rows | dense | 1 | pad] feeding one
+            dnn GEMM; returns its split."""
             nonlocal col, ones
             start = col
             specs.append(G.LookupSpec(ref, seq, col, mode))
             col += d
+            for k, _ in self._direct_feats(which):
+                idx = feats[k].reshape(N, -1)
+                bag = idx.shape[1]
+                specs.append(G.LookupSpec(self._ref(f'sparse_emb.{k}'), idx if bag > 1 else idx.reshape(N), col,
+                                          L.IDX_PLAIN, bag))
+                col += d
             if ones is None:
                 ones = torch.ones(N, 1, device=dev)
             x = torch.cat(dense + [ones], 1) if dense else ones
@@ -437,13 +463,17 @@ class BaselineModel(torch.nn.Module):
             col += d
 
         mm = [feats[k].reshape(N, -1).float() for k in self.ITEM_EMB_FEAT]
-        wi = operand(self._ref('item_emb'), L.IDX_ITEM_MASK if include_user else L.IDX_PLAIN, mm)
-        if item_f:
-            projected('item', item_f)
+        direct_i = {k for k, _ in self._direct_feats('item')}
+        direct_u = {k for k, _ in self._direct_feats('user')} if include_user else set()
+        item_p = [k for k in item_f if k not in direct_i]
+        user_p = [k for k in user_f if k not in direct_u]
+        wi = operand(self._ref('item_emb'), L.IDX_ITEM_MASK if include_user else L.IDX_PLAIN, mm, 'item')
+        if item_p:
+            projected('item', item_p)
         if include_user:
-            wu = operand(self._ref('user_emb'), L.IDX_USER_MASK, [])
-            if user_f:
-                projected('user', user_f)
+            wu = operand(self._ref('user_emb'), L.IDX_USER_MASK, [], 'user')
+            if user_p:
+                projected('user', user_p)
         if with_pos:
             specs.append(G.LookupSpec(self._ref('pos_emb'), seq, col, L.IDX_POSITION))
             splits.append((col, col + d))
@@ -467,9 +497,9 @@ class BaselineModel(torch.nn.Module):
                 return torch.relu(G.linear(a, w, addend=p))
             return torch.relu(torch.addmm(p, a, w.t()) if p is not None else a @ w.t())
 
-        x = dnn('item', wi, bool(item_f))
+        x = dnn('item', wi, bool(item_p))
         if include_user:
-            x = x + dnn('user', wu, bool(user_f))
+            x = x + dnn('user', wu, bool(user_p))
         pos_rows = blocks.pop(0) if with_pos else None
         return x.view(B, T, d), pos_rows
 
