@@ -17,15 +17,15 @@
 //
 // Work is 3 * levels * codes * dim flops per row (~1.5e5 at 3 x 256 x 64) and
 // reads each row once.  A workgroup of 256 threads owns 32 row slots; 8 threads
-// per slot split the codes and keep the residual in registers.  A level's
+// per slot split the codes and keep the residuals in registers.  A level's
 // codebook is staged into LDS in chunks (rows padded by 4 floats: the code
 // rows one ds_read_b128 of a wave touches land in disjoint banks) and the 8
 // partial minima meet in LDS in a fixed order.  Packed fp32 (v_pk_add /
 // v_pk_mul: element-wise IEEE, per-code order unchanged) does two distances
-// per op: latent <= 64 (k_rq_assign2) packs two ROWS per thread against one
-// code, so every LDS read serves two rows (the one-row form is bound by LDS
-// read bandwidth: a ds_read_b128 delivers 16 B to every lane, broadcast or
-// not); latent 128 (k_rq_assign, registers) packs two codes against one row.
+// per op: two ROWS per thread against one code, so every LDS read serves two
+// rows (a one-row form packing two codes was bound by LDS read bandwidth: a
+// ds_read_b128 delivers 16 B to every lane, broadcast or not; 4.83 vs 3.46 ms
+// at latent 64, 17.8 vs 11.2 ms at 128).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -51,125 +51,14 @@ int rq_chunk(int d, int codes) {
   return codes < c ? codes : c;
 }
 
-template <int D>
-__global__ __launch_bounds__(kRqBlock) void k_rq_assign(const float* __restrict__ z, int64_t ld_z,
-                                                        const float* __restrict__ cb, int64_t n, int K,
-                                                        int levels, int chunk, int32_t* __restrict__ codes_out,
-                                                        float* __restrict__ quant, float* __restrict__ dist_out,
-                                                        float* __restrict__ resid) {
-  extern __shared__ float4 rq_smem[];
-  float* sc = reinterpret_cast<float*>(rq_smem);
-  __shared__ float red_d[kRqGroups][kRqRows];
-  __shared__ int red_k[kRqGroups][kRqRows];
-  __shared__ int code_sh[kRqMaxLevels][kRqRows];
-  constexpr int S = rq_stride(D);
-
-  const int tid = threadIdx.x;
-  const int row = tid % kRqRows;
-  const int g = tid / kRqRows;
-  const int64_t gr = (int64_t)blockIdx.x * kRqRows + row;
-  const bool valid = gr < n;
-
-  float r[D];
-  if (valid) {
-    const float4* zp = reinterpret_cast<const float4*>(z + gr * ld_z);
-#pragma unroll
-    for (int j = 0; j < D / 4; ++j) {
-      const float4 v = zp[j];
-      r[4 * j] = v.x; r[4 * j + 1] = v.y; r[4 * j + 2] = v.z; r[4 * j + 3] = v.w;
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < D; ++j) r[j] = 0.f;
-  }
-
-  for (int l = 0; l < levels; ++l) {
-    const float* C = cb + (int64_t)l * K * D;
-    float bd = INFINITY;
-    int bk = 0x7fffffff;
-    for (int c0 = 0; c0 < K; c0 += chunk) {
-      const int cn = min(chunk, K - c0);
-      __syncthreads();  // previous chunk / level fully read
-      for (int i = tid; i < cn * (D / 4); i += kRqBlock) {
-        const int k = i / (D / 4), q = i % (D / 4);
-        *reinterpret_cast<float4*>(sc + k * S + 4 * q) =
-            *reinterpret_cast<const float4*>(C + (int64_t)(c0 + k) * D + 4 * q);
-      }
-      __syncthreads();
-      // this thread scores local codes k, k+1 for k = 2g, 2g + 16, ...: its
-      // codes ascend, so strict < keeps the lowest k of equal distances
-      for (int k = 2 * g; k < cn; k += 2 * kRqGroups) {
-        const bool two = k + 1 < cn;
-        const float* a = sc + k * S;
-        const float* b = sc + (two ? k + 1 : k) * S;
-        f2 acc = {0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < D; j += 4) {
-          const float4 ca = *reinterpret_cast<const float4*>(a + j);
-          const float4 cv = *reinterpret_cast<const float4*>(b + j);
-          f2 d;
-          d = f2{r[j], r[j]} - f2{ca.x, cv.x};         acc = acc + d * d;
-          d = f2{r[j + 1], r[j + 1]} - f2{ca.y, cv.y}; acc = acc + d * d;
-          d = f2{r[j + 2], r[j + 2]} - f2{ca.z, cv.z}; acc = acc + d * d;
-          d = f2{r[j + 3], r[j + 3]} - f2{ca.w, cv.w}; acc = acc + d * d;
-        }
-        if (acc.x < bd) { bd = acc.x; bk = c0 + k; }
-        if (two && acc.y < bd) { bd = acc.y; bk = c0 + k + 1; }
-      }
-    }
-    red_d[g][row] = bd;
-    red_k[g][row] = bk;
-    __syncthreads();
-    // every thread of the row reduces the 8 partial minima in the same order
-    float md = red_d[0][row];
-    int mk = red_k[0][row];
-#pragma unroll
-    for (int q = 1; q < kRqGroups; ++q) {
-      const float d = red_d[q][row];
-      const int kk = red_k[q][row];
-      if (d < md || (d == md && kk < mk)) { md = d; mk = kk; }
-    }
-    if (mk >= K) mk = 0;  // every distance NaN
-    const float4* cw = reinterpret_cast<const float4*>(C + (int64_t)mk * D);
-#pragma unroll
-    for (int j = 0; j < D / 4; ++j) {
-      const float4 v = cw[j];
-      r[4 * j] = r[4 * j] - v.x; r[4 * j + 1] = r[4 * j + 1] - v.y;
-      r[4 * j + 2] = r[4 * j + 2] - v.z; r[4 * j + 3] = r[4 * j + 3] - v.w;
-    }
-    if (g == 0) {
-      code_sh[l][row] = mk;
-      if (valid) {
-        codes_out[gr * levels + l] = mk;
-        if (dist_out) dist_out[gr * levels + l] = md;
-      }
-    }
-  }
-  __syncthreads();
-  if (!valid) return;
-  // group g writes columns [g*D/8, (g+1)*D/8) of quant / resid (compile-time
-  // column loop with a predicate: no dynamic register indexing)
-  constexpr int W = D / kRqGroups;
-#pragma unroll
-  for (int j = 0; j < D; ++j) {
-    if (j / W != g) continue;
-    if (quant) {
-      float q = cb[(int64_t)code_sh[0][row] * D + j];
-      for (int l = 1; l < levels; ++l) q = q + cb[((int64_t)l * K + code_sh[l][row]) * D + j];
-      quant[gr * D + j] = q;
-    }
-    if (resid) resid[gr * D + j] = r[j];
-  }
-}
-
 // Two rows per thread, packed over the rows: lane pair (row a, row b) of one
 // register pair meets one code per packed op, so every codebook element read
 // from LDS serves two rows -- the one-row form is bound by the LDS read
 // bandwidth (each ds_read_b128 delivers 16 B to every lane, broadcast or not).
 // Threads take codes g, g + 8, ... in ascending order (strict < keeps the
-// lowest code of equal distances).  Latent widths up to 64.
+// lowest code of equal distances).
 template <int D>
-__global__ __launch_bounds__(kRqBlock) void k_rq_assign2(const float* __restrict__ z, int64_t ld_z,
+__global__ __launch_bounds__(kRqBlock) void k_rq_assign(const float* __restrict__ z, int64_t ld_z,
                                                          const float* __restrict__ cb, int64_t n, int K,
                                                          int levels, int chunk, int32_t* __restrict__ codes_out,
                                                          float* __restrict__ quant, float* __restrict__ dist_out,
@@ -312,25 +201,14 @@ int launch_rq(const float* z, int64_t ld_z, const float* cb, int64_t n, int K, i
   const int chunk = rq_chunk(D, K);
   const size_t lds = (size_t)chunk * rq_stride(D) * sizeof(float);
   static bool attr_set = false;
-  if constexpr (D <= 64) {  // two rows per thread
-    if (!attr_set) {
-      GRK_CHECK_HIP(hipFuncSetAttribute((const void*)k_rq_assign2<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        kRqLdsBytes));
-      attr_set = true;
-    }
-    const int64_t blocks = (n + 2 * kRqRows - 1) / (2 * kRqRows);
-    k_rq_assign2<D><<<dim3((unsigned)blocks), kRqBlock, lds, s>>>(z, ld_z, cb, n, K, levels, chunk, codes, quant,
-                                                                   dist, resid);
-  } else {
-    if (!attr_set) {
-      GRK_CHECK_HIP(hipFuncSetAttribute((const void*)k_rq_assign<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        kRqLdsBytes));
-      attr_set = true;
-    }
-    const int64_t blocks = (n + kRqRows - 1) / kRqRows;
-    k_rq_assign<D><<<dim3((unsigned)blocks), kRqBlock, lds, s>>>(z, ld_z, cb, n, K, levels, chunk, codes, quant,
-                                                                  dist, resid);
+  if (!attr_set) {
+    GRK_CHECK_HIP(hipFuncSetAttribute((const void*)k_rq_assign<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      kRqLdsBytes));
+    attr_set = true;
   }
+  const int64_t blocks = (n + 2 * kRqRows - 1) / (2 * kRqRows);
+  k_rq_assign<D><<<dim3((unsigned)blocks), kRqBlock, lds, s>>>(z, ld_z, cb, n, K, levels, chunk, codes, quant,
+                                                                 dist, resid);
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }
@@ -349,7 +227,7 @@ extern "C" int grk_rq_assign(const float* z, int64_t ld_z, const float* codebook
   GRK_CHECK_ARG(codes >= 1 && codes <= 65536, "codes (%d) must be in [1, 65536]", codes);
   GRK_CHECK_ARG(levels >= 1 && levels <= kRqMaxLevels, "levels (%d) must be in [1, %d]", levels, kRqMaxLevels);
   GRK_CHECK_ARG(ld_z >= dim && ld_z % 4 == 0, "ld_z (%lld) must be >= dim and a multiple of 4", (long long)ld_z);
-  GRK_CHECK_ARG(n < (int64_t)0x7FFFFFFF * kRqRows, "n too large");  // grid.x of the one-row kernel
+  GRK_CHECK_ARG(n < (int64_t)0x7FFFFFFF * kRqRows, "n too large");  // grid.x
   if (n == 0) return GRK_OK;
   GRK_CHECK_ARG(z && codebooks && out_codes, "NULL z / codebooks / out_codes");
   GRK_CHECK_ARG(((uintptr_t)z & 15) == 0 && ((uintptr_t)codebooks & 15) == 0, "z / codebooks must be 16-byte aligned");
