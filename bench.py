@@ -370,8 +370,9 @@ FP32_VALU_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector (packed FMA)
 
 
 def semantic_id_setup(a, dev, reps):
-    """Config 4: tokenise the whole item table with an RQ-VAE (mm feature 81,
-    [items, 32] -> latent 64 -> levels x sid_codes codes) and return the
+    """Config 4: train an RQ-VAE briefly on the items' mm rows (feature 81,
+    [items, 32] -> latent 64 -> levels x sid_codes codes; k-means init, 30 Adam
+    steps of 16384 rows, timed), tokenise the whole item table and return the
     per-item semantic-id rows plus the code search's roofline entry.
 
     grk_rq_assign is VALU-bound: per row levels * codes * latent * 3 FLOP (one
@@ -384,7 +385,21 @@ def semantic_id_setup(a, dev, reps):
     torch.manual_seed(4)
     tok = RQVAE(32, hidden=(256, 128), latent_dim=64, levels=a.semantic_ids, codebook_size=a.sid_codes).to(dev)
     tok.init_codebooks(mm[:65536], iters=5)
+    # a short tokenizer training run (MSE + codebook + commitment, Adam), timed
+    opt = torch.optim.Adam(tok.parameters(), lr=1e-3)
+    tb = 16384
+    train_steps = 30
+    for i in range(train_steps + 3):
+        if i == 3:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        x = mm[(i * tb) % (a.items - tb):][:tb]
+        opt.zero_grad(set_to_none=True)
+        loss = tok(x)[2]['loss']
+        loss.backward()
+        opt.step()
     torch.cuda.synchronize()
+    train_rows_s = train_steps * tb / (time.perf_counter() - t0)
     t0 = time.perf_counter()
     codes = tok.tokenize(mm)
     torch.cuda.synchronize()
@@ -401,6 +416,8 @@ def semantic_id_setup(a, dev, reps):
             'avg_launch_us': round(ms * 1e3, 1), 'flops_per_launch': int(flops),
             'alg_bytes_per_launch': int(a.items * (64 * 4 + a.semantic_ids * 4)),
             'tokenize_items_per_s': round(a.items / tok_s, 1),
+            'tokenizer_train_rows_per_s': round(train_rows_s, 1), 'tokenizer_train_batch': tb,
+            'tokenizer_final_loss': round(float(loss.item()), 5),
             'workload': {'rows': a.items, 'latent': 64, 'levels': a.semantic_ids, 'codes': a.sid_codes}}
     sid = semantic_id_table(codes, a.items)
     del mm, z, tok
