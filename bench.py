@@ -419,6 +419,11 @@ def semantic_id_setup(a, dev, reps):
             'tokenizer_train_rows_per_s': round(train_rows_s, 1), 'tokenizer_train_batch': tb,
             'tokenizer_final_loss': round(float(loss.item()), 5),
             'workload': {'rows': a.items, 'latent': 64, 'levels': a.semantic_ids, 'codes': a.sid_codes}}
+    p = _pmc('r2s7_pmc_rq_assign.json', roof['workload'])
+    if p is not None:
+        roof['traffic'] = int(p['traffic_bytes_per_launch'])
+        roof['traffic_note'] = ('rocprofv3 PMC (profiles/r2s7_pmc_rq_assign.json): FETCH_SIZE x2 + WRITE_SIZE '
+                                '(MI355X_MICROARCH.md gfx950 corrections)')
     sid = semantic_id_table(codes, a.items)
     del mm, z, tok
     return sid, roof

@@ -12,7 +12,10 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 def main():
     from tencent_recommendation_2025_amd.rqvae import rq_assign
-    for d, lv, k in ((64, 3, 256), (32, 3, 256), (128, 3, 256), (64, 4, 1024)):
+    shapes = ((64, 3, 256), (32, 3, 256), (128, 3, 256), (64, 4, 1024))
+    if '--first' in sys.argv:   # config 4's shape only (PMC passes)
+        shapes = shapes[:1]
+    for d, lv, k in shapes:
         n = 1_000_000
         g = torch.Generator(device='cuda').manual_seed(0)
         z = torch.randn(n, d, device='cuda', generator=g)
