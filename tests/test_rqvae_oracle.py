@@ -92,3 +92,25 @@ def test_kmeans_init_recovers_clusters():
     d = ((cent[:, None] - centres[None]) ** 2).sum(-1)
     assert d.min(1).max() < 0.1 or len(set(d.argmin(1))) < 8   # converged or a seeded local optimum
     assert orq.semantic_feature_ids(np.array([[0, 255]]), 256).tolist() == [[1, 256]]
+
+
+def test_semantic_id_features_in_synthetic_batches():
+    """Host logic of config 4's data path (CPU tensors): 1-based id table, the
+    schema entries and the per-token sid features of seq / pos / neg."""
+    import torch
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.rqvae import semantic_id_schema, semantic_id_table
+    codes = torch.randint(0, 16, (50, 2), dtype=torch.int32, generator=torch.Generator().manual_seed(0))
+    sid = semantic_id_table(codes, 50)
+    assert sid.shape == (51, 2) and int(sid[0].abs().sum()) == 0 and torch.equal(sid[1:], codes.long() + 1)
+    names, stats = semantic_id_schema(2, 16)
+    assert names == ['sid0', 'sid1'] and stats == {'sid0': 16, 'sid1': 16}
+    cfg = S.SyntheticConfig(batch_size=3, maxlen=10, num_items=50, num_users=7, min_len=3, sid_table=sid, sid_codes=16)
+    st, types = S.feature_schema(cfg)
+    assert types['item_sparse'][-2:] == names and st['sid1'] == 16
+    seq, pos, neg, tt, _, _, sf, pf, nf = S.make_batch(cfg, torch.Generator().manual_seed(1), 'cpu')
+    item = torch.where(tt == 1, seq, 0)
+    for lvl in range(2):
+        assert torch.equal(sf[f'sid{lvl}'], torch.where(item > 0, sid[item, lvl], 0))
+        assert torch.equal(pf[f'sid{lvl}'], torch.where(pos > 0, sid[pos, lvl], 0))
+        assert torch.equal(nf[f'sid{lvl}'], torch.where(neg > 0, sid[neg, lvl], 0))
