@@ -108,6 +108,18 @@ def semantic_feature_ids(codes, codebook_size):
     return np.asarray(codes, np.int64) + 1
 
 
+def dedup_level(codes):
+    """TIGER's collision level (restated with a dict walk in item order): the
+    extra code of item i = how many earlier items share its code tuple."""
+    codes = np.asarray(codes, np.int64)
+    seen = {}
+    extra = np.zeros(len(codes), np.int64)
+    for i, row in enumerate(map(tuple, codes)):
+        extra[i] = seen.get(row, 0)
+        seen[row] = extra[i] + 1
+    return np.concatenate([codes, extra[:, None]], 1)
+
+
 def kmeans_init(z, codebook_size, iters, seed=0):
     """Lloyd k-means on float32 rows (codebook initialisation, level by level
     on the residuals).  Assignment uses ``rq_assign`` with one level; the

@@ -21,7 +21,8 @@ MI355X path:
   (``grk_embedding_backward``, bit-exact sequential fp32 per code), so a
   training step is run-to-run reproducible;
 * encoder / decoder are plain ``nn.Linear`` (hipBLASLt GEMMs through torch).
-There is no CPU path: every op raises without the HIP library.
+There is no CPU path for the kernels: they raise without the HIP library
+(`dedup_level` and the id-table helpers are integer torch glue, any device).
 """
 from __future__ import annotations
 
@@ -161,6 +162,30 @@ class RQVAE(torch.nn.Module):
             z = self.encode(x[i:i + batch])
             out.append(rq_assign(z, self.codebooks, want_quant=False)[0])
         return torch.cat(out) if out else torch.empty(0, self.levels, dtype=torch.int32, device=x.device)
+
+
+def dedup_level(codes):
+    """TIGER's collision level: an extra code per item that makes every
+    item's code tuple unique -- the item's rank (in item order) among the
+    items sharing its tuple.  codes int [n, L] -> int64 [n, L + 1]; the extra
+    level's cardinality is the largest collision group (``int(out[:, -1].max()) + 1``).
+    Integer work on n x L codes: a stable sort of the packed tuples and a
+    rank-in-run (torch ops on the codes' device, deterministic)."""
+    n, lv = codes.shape
+    c = codes.long()
+    if n == 0:
+        return torch.empty(0, lv + 1, dtype=torch.int64, device=codes.device)
+    # dense tuple ids: lexicographic rank of each row's tuple (no overflow for any K, L)
+    _, tid = torch.unique(c, dim=0, return_inverse=True)
+    order = torch.sort(tid, stable=True).indices          # items grouped by tuple, item order inside
+    st = tid[order]
+    pos = torch.arange(n, device=codes.device)
+    head = torch.ones(n, dtype=torch.bool, device=codes.device)
+    head[1:] = st[1:] != st[:-1]
+    first = torch.cummax(torch.where(head, pos, torch.zeros_like(pos)), 0).values
+    rank = torch.empty(n, dtype=torch.int64, device=codes.device)
+    rank[order] = pos - first
+    return torch.cat([c, rank[:, None]], 1)
 
 
 def semantic_id_table(codes, num_items):

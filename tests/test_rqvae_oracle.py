@@ -114,3 +114,18 @@ def test_semantic_id_features_in_synthetic_batches():
         assert torch.equal(sf[f'sid{lvl}'], torch.where(item > 0, sid[item, lvl], 0))
         assert torch.equal(pf[f'sid{lvl}'], torch.where(pos > 0, sid[pos, lvl], 0))
         assert torch.equal(nf[f'sid{lvl}'], torch.where(neg > 0, sid[neg, lvl], 0))
+
+
+def test_dedup_level_matches_oracle():
+    """The collision level (rqvae.dedup_level, torch ops -- here on CPU tensors)
+    equals the oracle's item-order walk; every extended tuple is unique."""
+    import torch
+    from tencent_recommendation_2025_amd.rqvae import dedup_level
+    rng = np.random.default_rng(5)
+    for n, lv, k in ((1, 3, 4), (200, 2, 3), (1000, 3, 4), (500, 1, 2)):
+        codes = rng.integers(0, k, (n, lv)).astype(np.int32)
+        got = dedup_level(torch.from_numpy(codes)).numpy()
+        want = orq.dedup_level(codes)
+        assert np.array_equal(got, want)
+        assert len({tuple(r) for r in got}) == n
+    assert dedup_level(torch.zeros(0, 3, dtype=torch.int32)).shape == (0, 4)
