@@ -59,6 +59,15 @@ const char* grk_last_error(void);
 /* Library version string. */
 const char* grk_version(void);
 
+/* A non-blocking HIP stream of the caller's own on the current device, outside
+ * any framework's stream pool (torch hands out pooled streams round-robin, so
+ * a "new" torch stream can be the very stream a process group's collectives
+ * record their events on; capturing a HIP graph on that stream makes the
+ * process group's watchdog query of those events fail).  Trainer captures its
+ * step on one of these. */
+int grk_stream_create(void** stream);
+int grk_stream_destroy(void* stream);
+
 /* ------------------------------------------------------------------------
  * Embedding tables
  * ------------------------------------------------------------------------ */

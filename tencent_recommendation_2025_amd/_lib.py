@@ -75,6 +75,8 @@ _P, _I, _I64, _SZ, _F = C.c_void_p, C.c_int, C.c_int64, C.c_size_t, C.c_float
 SIGNATURES = {
     'grk_last_error': (C.c_char_p, []),
     'grk_version': (C.c_char_p, []),
+    'grk_stream_create': (_I, [C.POINTER(C.c_void_p)]),
+    'grk_stream_destroy': (_I, [_P]),
     'grk_embedding_gather': (_I, [C.POINTER(GrkFeature), _I, _I, _I, _I, _I64, _P, C.c_int32, _P, _I64, _P, _P]),
     'grk_embedding_backward_workspace': (_SZ, [_I64, _I64, _I]),
     'grk_sort_pairs_workspace': (_SZ, [_I64]),

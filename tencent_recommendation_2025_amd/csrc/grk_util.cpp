@@ -1,4 +1,5 @@
 // Error reporting and version for the grk C ABI (host code).
+#include <hip/hip_runtime_api.h>
 #include <stdarg.h>
 #include <stdio.h>
 
@@ -22,3 +23,28 @@ void clear_error() { g_err[0] = 0; }
 extern "C" const char* grk_last_error(void) { return grk::g_err; }
 
 extern "C" const char* grk_version(void) { return "grk 0.1 (gfx950)"; }
+
+extern "C" int grk_stream_create(void** stream) {
+  grk::clear_error();
+  if (!stream) {
+    grk::set_error("stream is NULL");
+    return GRK_EINVAL;
+  }
+  const hipError_t e = hipStreamCreateWithFlags((hipStream_t*)stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    grk::set_error("hipStreamCreateWithFlags failed: %s", hipGetErrorString(e));
+    return GRK_EHIP;
+  }
+  return GRK_OK;
+}
+
+extern "C" int grk_stream_destroy(void* stream) {
+  grk::clear_error();
+  if (!stream) return GRK_OK;
+  const hipError_t e = hipStreamDestroy((hipStream_t)stream);
+  if (e != hipSuccess) {
+    grk::set_error("hipStreamDestroy failed: %s", hipGetErrorString(e));
+    return GRK_EHIP;
+  }
+  return GRK_OK;
+}

@@ -28,6 +28,30 @@ import torch
 from . import functional as G
 
 
+_PRIVATE_STREAMS = {}
+
+
+def private_stream(device):
+    """The process's own side stream for ``device`` (grk_stream_create), wrapped
+    as a torch stream.  torch.cuda.Stream() hands out pooled streams round-robin,
+    so it can return the very stream a process group records its collectives'
+    events on; a HIP graph captured on that stream makes the NCCL watchdog's
+    query of those events fail (hipErrorCapturedEvent: "event last recorded in a
+    capturing stream"), which it treats as fatal.  Created
+    once per device, never destroyed (lives as long as the process)."""
+    import ctypes
+    from . import _lib as L
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _PRIVATE_STREAMS.get(idx)
+    if s is None:
+        with torch.cuda.device(idx):
+            raw = ctypes.c_void_p()
+            L.check(L.lib().grk_stream_create(ctypes.byref(raw)), 'grk_stream_create')
+            s = _PRIVATE_STREAMS[idx] = torch.cuda.ExternalStream(raw.value, device=torch.device('cuda', idx))
+    return s
+
+
 def _tensors(batch):
     """Flat list of the batch's tensors (tuple items and dict values, in order)."""
     out = []
@@ -153,7 +177,7 @@ class Trainer:
     def _on_side(self, fn):
         cur = torch.cuda.current_stream()
         if self._side is None:
-            self._side = torch.cuda.Stream(device=cur.device)
+            self._side = private_stream(cur.device)
         self._side.wait_stream(cur)
         with torch.cuda.stream(self._side):
             out = fn()
