@@ -345,17 +345,15 @@ struct WaveAcc {
 };
 
 template <typename G, int LW>
-__global__ void __launch_bounds__(256) k_seg_chunks_wave(const unsigned* __restrict__ keys,
-                                                         const unsigned long long* __restrict__ gptr,
-                                                         const int* __restrict__ pos, const int* __restrict__ seg_start,
-                                                         const int* __restrict__ seg_end, int64_t n, unsigned sentinel,
-                                                         int dim, float* __restrict__ dense_out,
-                                                         float* __restrict__ uniq_rows,
-                                                         int32_t* __restrict__ row_slot) {
+__device__ __forceinline__ void seg_chunks_wave_body(int64_t chunk, int lane, const unsigned* __restrict__ keys,
+                                                     const unsigned long long* __restrict__ gptr,
+                                                     const int* __restrict__ pos, const int* __restrict__ seg_start,
+                                                     const int* __restrict__ seg_end, int64_t n, unsigned sentinel,
+                                                     int dim, float* __restrict__ dense_out,
+                                                     float* __restrict__ uniq_rows,
+                                                     int32_t* __restrict__ row_slot) {
   constexpr int VEC = LW;
   constexpr int KP = kRedChunk / 64;  // chunk entries per lane
-  const int lane = threadIdx.x & 63;
-  const int64_t chunk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t p0 = chunk * kRedChunk;
   if (p0 >= n) return;
   const int64_t p1 = min(n, p0 + kRedChunk);
@@ -442,6 +440,18 @@ __device__ __forceinline__ void seq_sum_wave(WaveAcc<LW>& acc, const unsigned lo
   }
 }
 
+template <typename G, int LW>
+__global__ void __launch_bounds__(256) k_seg_chunks_wave(const unsigned* __restrict__ keys,
+                                                         const unsigned long long* __restrict__ gptr,
+                                                         const int* __restrict__ pos, const int* __restrict__ seg_start,
+                                                         const int* __restrict__ seg_end, int64_t n, unsigned sentinel,
+                                                         int dim, float* __restrict__ dense_out,
+                                                         float* __restrict__ uniq_rows,
+                                                         int32_t* __restrict__ row_slot) {
+  seg_chunks_wave_body<G, LW>((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, keys, gptr, pos,
+                              seg_start, seg_end, n, sentinel, dim, dense_out, uniq_rows, row_slot);
+}
+
 // One wave per chunk edge b (occurrence b * kRedChunk): finishes the row that
 // first crosses a chunk edge at b, i.e. crosses b and starts in chunk b - 1,
 // when it has at most 2 * kRedChunk occurrences (longer rows: k_seg_hot).
@@ -498,12 +508,19 @@ template <typename G>
 __host__ __device__ constexpr int kHotSlice() { return sizeof(G) == 2 ? 32 : 64; }
 
 template <typename G>
-__global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ keys,
-                                                const unsigned long long* __restrict__ gptr,
-                                                const int* __restrict__ pos, const int* __restrict__ seg_start,
-                                                const int* __restrict__ seg_end, int64_t n, unsigned sentinel, int dim,
-                                                float* __restrict__ dense_out, float* __restrict__ uniq_rows,
-                                                int32_t* __restrict__ row_slot) {
+__host__ __device__ constexpr int kHotImgBytes() {
+  return sizeof(G) == 2 ? 64 * (kHotSlice<G>() * 2) : kHotSlice<G>() * (32 * 4 + 8);
+}
+
+// bx = chunk edge - 1 (the wave's former blockIdx.x), by = column slice
+template <typename G>
+__device__ __forceinline__ void seg_hot_body(int64_t bx, int by, int lane, unsigned char* __restrict__ img,
+                                             const unsigned* __restrict__ keys,
+                                             const unsigned long long* __restrict__ gptr,
+                                             const int* __restrict__ pos, const int* __restrict__ seg_start,
+                                             const int* __restrict__ seg_end, int64_t n, unsigned sentinel, int dim,
+                                             float* __restrict__ dense_out, float* __restrict__ uniq_rows,
+                                             int32_t* __restrict__ row_slot) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(1))) const u32x4 gu32x4;
   constexpr int ES = sizeof(G);
@@ -517,9 +534,8 @@ __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ key
   constexpr int IMG_ROWS = ES == 2 ? TILE : SLICE;
   constexpr int EPR = 8 / ES;        // elements per 8-byte LDS read
   constexpr int S = 32 / IPT;        // tiles in flight
-  __shared__ __attribute__((aligned(16))) unsigned char img[IMG_ROWS * ROWB];
-  const int lane = threadIdx.x;
-  const int64_t b = (int64_t)blockIdx.x + 1;  // chunk edge: the row that first crosses it
+  static_assert(IMG_ROWS * ROWB == kHotImgBytes<G>(), "hot-row image size");
+  const int64_t b = bx + 1;  // chunk edge: the row that first crosses it
   const int64_t pb = b * kRedChunk;
   if (pb >= n) return;
   const unsigned key = keys[pb];
@@ -527,7 +543,7 @@ __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ key
   const int u = pos[pb] - 1;
   const int su = seg_start[u], eu = seg_end[u];
   if (su / kRedChunk != b - 1 || eu - su <= 2 * kRedChunk) return;
-  const int c0 = blockIdx.y * SLICE;
+  const int c0 = by * SLICE;
   const int cols = min(SLICE, dim - c0);
   const int wv = (lane % LPO) * EPV;                     // this lane's columns [wv, wv + EPV) of the slice
   const int vcol = c0 + wv < dim ? c0 + wv : c0;         // clamped into the row past dim
@@ -634,7 +650,43 @@ __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ key
     if (dense_out) dense_out[(int64_t)key * dim + c0 + lane] = acc;
     if (uniq_rows) uniq_rows[(int64_t)u * dim + c0 + lane] = acc;
   }
-  if (row_slot && blockIdx.y == 0 && lane == 0) row_slot[key] = (int32_t)u;
+  if (row_slot && by == 0 && lane == 0) row_slot[key] = (int32_t)u;
+}
+
+template <typename G>
+__global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ keys,
+                                                const unsigned long long* __restrict__ gptr,
+                                                const int* __restrict__ pos, const int* __restrict__ seg_start,
+                                                const int* __restrict__ seg_end, int64_t n, unsigned sentinel, int dim,
+                                                float* __restrict__ dense_out, float* __restrict__ uniq_rows,
+                                                int32_t* __restrict__ row_slot) {
+  __shared__ __attribute__((aligned(16))) unsigned char img[kHotImgBytes<G>()];
+  seg_hot_body<G>(blockIdx.x, blockIdx.y, threadIdx.x, img, keys, gptr, pos, seg_start, seg_end, n, sentinel, dim,
+                  dense_out, uniq_rows, row_slot);
+}
+
+// One launch for the bf16 wave path: waves [0, nhot) are the hot-row items
+// (edge, slice) of k_seg_hot, the rest the chunks of k_seg_chunks_wave.  The
+// hot rows' sequential chains (tens of us, a few waves) then run beside the
+// chunk waves instead of after them; the two write disjoint rows.
+template <typename G, int LW>
+__global__ void __launch_bounds__(256) k_seg_wave_fused(int64_t nhot, int nslices, const unsigned* __restrict__ keys,
+                                                        const unsigned long long* __restrict__ gptr,
+                                                        const int* __restrict__ pos,
+                                                        const int* __restrict__ seg_start,
+                                                        const int* __restrict__ seg_end, int64_t n,
+                                                        unsigned sentinel, int dim, float* __restrict__ dense_out,
+                                                        float* __restrict__ uniq_rows,
+                                                        int32_t* __restrict__ row_slot) {
+  __shared__ __attribute__((aligned(16))) unsigned char img[4][kHotImgBytes<G>()];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t item = (int64_t)blockIdx.x * 4 + wave;
+  if (item < nhot)
+    seg_hot_body<G>(item / nslices, (int)(item % nslices), lane, img[wave], keys, gptr, pos, seg_start, seg_end, n,
+                    sentinel, dim, dense_out, uniq_rows, row_slot);
+  else
+    seg_chunks_wave_body<G, LW>(item - nhot, lane, keys, gptr, pos, seg_start, seg_end, n, sentinel, dim, dense_out,
+                                uniq_rows, row_slot);
 }
 
 // ------------------------------------------------------------ workspace ----
@@ -851,6 +903,20 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   if (ge)                                                                                                            \
     k_seg_combine_edges<G, LW><<<ge, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, \
                                                   sentinel, dim, dense_out, uniq_rows, row_slot)
+    if (grad_dtype == GRK_BF16 && total > 2 * kRedChunk) {
+      // hot-row items and chunks in one launch (k_seg_wave_fused), then the edges
+      const int nsl = (dim + kHotSlice<bf16_t>() - 1) / kHotSlice<bf16_t>();
+      const int64_t nhot = (chunks - 1) * nsl;
+      const unsigned gf = (unsigned)((nhot + chunks + 3) / 4);
+      k_seg_wave_fused<bf16_t, 8><<<gf, 256, 0, s>>>(nhot, nsl, ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start,
+                                                     ws.seg_end, total, sentinel, dim, dense_out, uniq_rows, row_slot);
+      GRK_LAUNCH_CHECK();
+      if (ge)
+        k_seg_combine_edges<bf16_t, 8><<<ge, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end,
+                                                          total, sentinel, dim, dense_out, uniq_rows, row_slot);
+      GRK_LAUNCH_CHECK();
+      return GRK_OK;
+    }
     if (grad_dtype == GRK_BF16) { GRK_SEGW(bf16_t, 8); }
     else if (lw == 8) { GRK_SEGW(float, 8); }
     else { GRK_SEGW(float, 4); }
