@@ -456,16 +456,13 @@ __global__ void __launch_bounds__(256) k_seg_chunks_wave(const unsigned* __restr
 // first crosses a chunk edge at b, i.e. crosses b and starts in chunk b - 1,
 // when it has at most 2 * kRedChunk occurrences (longer rows: k_seg_hot).
 template <typename G, int LW>
-__global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __restrict__ keys,
-                                                           const unsigned long long* __restrict__ gptr,
-                                                           const int* __restrict__ pos,
-                                                           const int* __restrict__ seg_start,
-                                                           const int* __restrict__ seg_end, int64_t n,
-                                                           unsigned sentinel, int dim, float* __restrict__ dense_out,
-                                                           float* __restrict__ uniq_rows,
-                                                           int32_t* __restrict__ row_slot) {
-  const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) + 1;
+__device__ __forceinline__ void seg_edge_body(int64_t edge, int lane, const unsigned* __restrict__ keys,
+                                              const unsigned long long* __restrict__ gptr,
+                                              const int* __restrict__ pos, const int* __restrict__ seg_start,
+                                              const int* __restrict__ seg_end, int64_t n, unsigned sentinel, int dim,
+                                              float* __restrict__ dense_out, float* __restrict__ uniq_rows,
+                                              int32_t* __restrict__ row_slot) {
+  const int64_t b = edge + 1;
   const int64_t pb = b * kRedChunk;
   if (pb >= n) return;
   const unsigned key = keys[pb];
@@ -479,6 +476,19 @@ __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __res
   acc.zero();
   seq_sum_wave<G, LW>(acc, gptr, su, eu, lane, c);
   store_final(acc, key, u, dim, c, dense_out, uniq_rows, row_slot);
+}
+
+template <typename G, int LW>
+__global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __restrict__ keys,
+                                                           const unsigned long long* __restrict__ gptr,
+                                                           const int* __restrict__ pos,
+                                                           const int* __restrict__ seg_start,
+                                                           const int* __restrict__ seg_end, int64_t n,
+                                                           unsigned sentinel, int dim, float* __restrict__ dense_out,
+                                                           float* __restrict__ uniq_rows,
+                                                           int32_t* __restrict__ row_slot) {
+  seg_edge_body<G, LW>((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, keys, gptr, pos, seg_start,
+                       seg_end, n, sentinel, dim, dense_out, uniq_rows, row_slot);
 }
 
 // ------------------------------------------------------------- hot rows ----
@@ -666,11 +676,14 @@ __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ key
 }
 
 // One launch for the bf16 wave path: waves [0, nhot) are the hot-row items
-// (edge, slice) of k_seg_hot, the rest the chunks of k_seg_chunks_wave.  The
-// hot rows' sequential chains (tens of us, a few waves) then run beside the
-// chunk waves instead of after them; the two write disjoint rows.
+// (edge, slice) of k_seg_hot, the next nchunks the chunks of
+// k_seg_chunks_wave, the rest the edges of k_seg_combine_edges.  The hot
+// rows' sequential chains (tens of us, a few waves) then run beside the other
+// waves instead of after them; the three write disjoint rows (a row is
+// finished by exactly one of them).
 template <typename G, int LW>
-__global__ void __launch_bounds__(256) k_seg_wave_fused(int64_t nhot, int nslices, const unsigned* __restrict__ keys,
+__global__ void __launch_bounds__(256) k_seg_wave_fused(int64_t nhot, int nslices, int64_t nchunks,
+                                                        const unsigned* __restrict__ keys,
                                                         const unsigned long long* __restrict__ gptr,
                                                         const int* __restrict__ pos,
                                                         const int* __restrict__ seg_start,
@@ -684,9 +697,12 @@ __global__ void __launch_bounds__(256) k_seg_wave_fused(int64_t nhot, int nslice
   if (item < nhot)
     seg_hot_body<G>(item / nslices, (int)(item % nslices), lane, img[wave], keys, gptr, pos, seg_start, seg_end, n,
                     sentinel, dim, dense_out, uniq_rows, row_slot);
-  else
+  else if (item < nhot + nchunks)
     seg_chunks_wave_body<G, LW>(item - nhot, lane, keys, gptr, pos, seg_start, seg_end, n, sentinel, dim, dense_out,
                                 uniq_rows, row_slot);
+  else
+    seg_edge_body<G, LW>(item - nhot - nchunks, lane, keys, gptr, pos, seg_start, seg_end, n, sentinel, dim,
+                         dense_out, uniq_rows, row_slot);
 }
 
 // ------------------------------------------------------------ workspace ----
@@ -904,16 +920,14 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
     k_seg_combine_edges<G, LW><<<ge, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, \
                                                   sentinel, dim, dense_out, uniq_rows, row_slot)
     if (grad_dtype == GRK_BF16 && total > 2 * kRedChunk) {
-      // hot-row items and chunks in one launch (k_seg_wave_fused), then the edges
+      // hot-row items, chunks and edges in one launch (k_seg_wave_fused)
       const int nsl = (dim + kHotSlice<bf16_t>() - 1) / kHotSlice<bf16_t>();
       const int64_t nhot = (chunks - 1) * nsl;
-      const unsigned gf = (unsigned)((nhot + chunks + 3) / 4);
-      k_seg_wave_fused<bf16_t, 8><<<gf, 256, 0, s>>>(nhot, nsl, ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start,
-                                                     ws.seg_end, total, sentinel, dim, dense_out, uniq_rows, row_slot);
-      GRK_LAUNCH_CHECK();
-      if (ge)
-        k_seg_combine_edges<bf16_t, 8><<<ge, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end,
-                                                          total, sentinel, dim, dense_out, uniq_rows, row_slot);
+      const int64_t nedges = chunks - 1;
+      const unsigned gf = (unsigned)((nhot + chunks + nedges + 3) / 4);
+      k_seg_wave_fused<bf16_t, 8><<<gf, 256, 0, s>>>(nhot, nsl, chunks, ws.keys_out, ws.gptr_out, ws.pos,
+                                                     ws.seg_start, ws.seg_end, total, sentinel, dim, dense_out,
+                                                     uniq_rows, row_slot);
       GRK_LAUNCH_CHECK();
       return GRK_OK;
     }
