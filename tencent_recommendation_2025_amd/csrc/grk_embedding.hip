@@ -675,7 +675,7 @@ __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ key
                   dense_out, uniq_rows, row_slot);
 }
 
-// One launch for the bf16 wave path: waves [0, nhot) are the hot-row items
+// One launch for the wave path: waves [0, nhot) are the hot-row items
 // (edge, slice) of k_seg_hot, the next nchunks the chunks of
 // k_seg_chunks_wave, the rest the edges of k_seg_combine_edges.  The hot
 // rows' sequential chains (tens of us, a few waves) then run beside the other
@@ -919,15 +919,21 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   if (ge)                                                                                                            \
     k_seg_combine_edges<G, LW><<<ge, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, \
                                                   sentinel, dim, dense_out, uniq_rows, row_slot)
-    if (grad_dtype == GRK_BF16 && total > 2 * kRedChunk) {
+    if (total > 2 * kRedChunk) {
       // hot-row items, chunks and edges in one launch (k_seg_wave_fused)
-      const int nsl = (dim + kHotSlice<bf16_t>() - 1) / kHotSlice<bf16_t>();
-      const int64_t nhot = (chunks - 1) * nsl;
       const int64_t nedges = chunks - 1;
-      const unsigned gf = (unsigned)((nhot + chunks + nedges + 3) / 4);
-      k_seg_wave_fused<bf16_t, 8><<<gf, 256, 0, s>>>(nhot, nsl, chunks, ws.keys_out, ws.gptr_out, ws.pos,
-                                                     ws.seg_start, ws.seg_end, total, sentinel, dim, dense_out,
-                                                     uniq_rows, row_slot);
+#define GRK_SEGF(G, LW)                                                                                           \
+  do {                                                                                                            \
+    const int nsl = (dim + kHotSlice<G>() - 1) / kHotSlice<G>();                                                  \
+    const int64_t nhot = (chunks - 1) * nsl;                                                                      \
+    const unsigned gf = (unsigned)((nhot + chunks + nedges + 3) / 4);                                             \
+    k_seg_wave_fused<G, LW><<<gf, 256, 0, s>>>(nhot, nsl, chunks, ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, \
+                                               ws.seg_end, total, sentinel, dim, dense_out, uniq_rows, row_slot); \
+  } while (0)
+      if (grad_dtype == GRK_BF16) GRK_SEGF(bf16_t, 8);
+      else if (lw == 8) GRK_SEGF(float, 8);
+      else GRK_SEGF(float, 4);
+#undef GRK_SEGF
       GRK_LAUNCH_CHECK();
       return GRK_OK;
     }
