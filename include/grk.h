@@ -220,6 +220,22 @@ int grk_table_adamw_catchup_dev(void* param, int param_dtype, float* exp_avg, fl
 int grk_stamp_rows_dev(int32_t* last, const int64_t* uniq_ids, const int32_t* uniq_count, int64_t max_uniq,
                        const int32_t* t_dev, void* stream);
 
+/* l2_emb term of the BaseLine training script (model/BaseLine/main.py:184-185:
+ * loss += l2_emb * torch.norm(item_emb.weight)) for the fused optimizer.
+ * grk_table_l2_norm: *norm = ||param||_F (fp64 partial sums over a fixed grid,
+ * deterministic), *l2_coef = l2 / ||param|| (0 for a zero table) -- the scale of
+ * the term's gradient l2 * W / ||W||.  param 16-byte aligned; workspace of
+ * grk_table_l2_norm_workspace() bytes.
+ * grk_table_adamw_l2_dev: grk_table_adamw_dev in dense mode with every row's
+ * gradient g + (*l2_coef) * p (p = the parameters before this step's update). */
+size_t grk_table_l2_norm_workspace(void);
+int grk_table_l2_norm(const void* param, int param_dtype, int64_t num_rows, int dim, float l2, float* norm,
+                      float* l2_coef, void* workspace, size_t workspace_bytes, void* stream);
+int grk_table_adamw_l2_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows, int dim,
+                           const int64_t* uniq_ids, const float* uniq_rows, const int32_t* uniq_count,
+                           int64_t max_uniq, int32_t* row_slot, const grk_adamw_hparams* hp_ring, int32_t ring_len,
+                           const int32_t* t_dev, const float* l2_coef, void* stream);
+
 /* ------------------------------------------------------------------------
  * Causal attention (MFMA 32x32x16 bf16)
  *   GRK_ATTN_SOFTMAX: softmax(scale * QK^T + mask) V with dropout -- the
@@ -404,8 +420,11 @@ int grk_pair_logits_bwd(const void* h, int64_t ldh, const void* e_pos, int64_t l
 
 /* ------------------------------------------------------------------------
  * In-batch sampled softmax (north star; no reference -- oracle/loss.py)
- *   z_ij = <h_i, e_j> / tau over valid columns j; j != i masked when
+ *   z_ij = <h_i, e_j> / tau - log_q[j] over valid columns j; j != i masked when
  *   item_ids[j] == item_ids[i]; loss = mean_valid_i (logsumexp_j z_ij - z_ii)
+ * log_q (optional fp32 [num_rows], natural log, NULL = 0): the logQ correction
+ * -- log of the sampling probability of position j's item, subtracted from
+ * every logit of column j (Yi et al., RecSys 2019).
  * h, e: bf16 [num_rows, ld] (dim in {32, 64, 128, 256, 512}); valid uint8.
  * Only valid positions take part: the kernels list them on the device
  * (compact index = rank among the valid positions) and size their grids for
@@ -418,8 +437,9 @@ size_t grk_sampled_softmax_workspace(int64_t num_rows, int dim);
  * index c, c < count), the loss and the valid-row count (fixed-order
  * reduction). */
 int grk_sampled_softmax_fwd(const void* h, int64_t ldh, const void* e, int64_t lde, const int64_t* item_ids,
-                            const uint8_t* valid, int64_t num_rows, int dim, float tau, float* lse2, float* loss,
-                            int32_t* count, void* workspace, size_t workspace_bytes, void* stream);
+                            const uint8_t* valid, int64_t num_rows, int dim, float tau, const float* log_q,
+                            float* lse2, float* loss, int32_t* count, void* workspace, size_t workspace_bytes,
+                            void* stream);
 
 /* Fused backward (no nv x nv matrix): with G = (softmax - I) * grad_loss /
  * (count * tau) on valid (row, column) pairs, dh = G e and de = G^T h, fp32
@@ -427,8 +447,8 @@ int grk_sampled_softmax_fwd(const void* h, int64_t ldh, const void* e, int64_t l
  * positions that are not valid are zero.  G enters the MFMA as bf16 hi + lo:
  * fp32-level error.  grad_loss: device scalar (NULL = 1). */
 int grk_sampled_softmax_bwd(const void* h, int64_t ldh, const void* e, int64_t lde, const int64_t* item_ids,
-                            const uint8_t* valid, int64_t num_rows, int dim, float tau, const float* lse2,
-                            const float* grad_loss, float* dh, int64_t lddh, float* de, int64_t ldde,
+                            const uint8_t* valid, int64_t num_rows, int dim, float tau, const float* log_q,
+                            const float* lse2, const float* grad_loss, float* dh, int64_t lddh, float* de, int64_t ldde,
                             void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
@@ -501,7 +521,9 @@ int grk_mips_topk(const void* queries, int64_t ld_q, const void* items, int64_t 
  * positions 0.  Draws are splitmix64(seed, b, t, attempt): deterministic, so
  * oracle/sampler.py restates them bit-exactly (the reference's np.random
  * stream is not reproducible on a GPU).  pos / next_token_type / neg int32
- * [batch, seq_len], seq_len <= 65535; excl int32 [batch, excl_len], excl_len <= 4096.
+ * [batch, seq_len], seq_len <= 65535; excl int32 [batch, excl_len], any length, any order,
+ * duplicates allowed (set semantics; lists of <= 8192 entries are sorted in LDS and
+ * binary-searched, longer ones scanned in global memory).
  * item_feat (optional, int32 [num_items + 1, num_feat], row 0 = the default
  * feature values): neg_feat[b,t,:] = item_feat[neg[b,t],:] -- the
  * fill_missing_feat(item_feat_dict[neg]) rows of dataset.py:161-162,

@@ -45,10 +45,13 @@ def bce(h, e_pos, e_neg, next_token_type):
     return loss, pos, neg, dh, dep, den
 
 
-def sampled_softmax(h, e, item_ids, valid, tau):
+def sampled_softmax(h, e, item_ids, valid, tau, log_q=None):
     """In-batch sampled softmax.  Returns ``(loss, dh, de)`` (fp64).
 
-    Row i (valid) scores every valid column j: ``z_ij = <h_i, e_j> / tau``;
+    Row i (valid) scores every valid column j: ``z_ij = <h_i, e_j> / tau - log_q[j]``
+    (``log_q`` optional: the logQ correction, Yi et al. RecSys 2019 -- the log
+    sampling probability of column j's item; a constant, so the gradient
+    formulas are unchanged);
     columns j != i with ``item_ids[j] == item_ids[i]`` are masked (the same
     item is not a negative of itself); the target is column i.
     ``loss = mean_i (logsumexp_j z_ij - z_ii)`` over valid rows.
@@ -58,6 +61,8 @@ def sampled_softmax(h, e, item_ids, valid, tau):
     valid = np.asarray(valid, bool).reshape(-1)
     n = h.shape[0]
     z = h @ e.T / tau
+    if log_q is not None:
+        z = z - np.asarray(log_q, np.float64).reshape(1, -1)
     colmask = valid[None, :] & ~((ids[:, None] == ids[None, :]) & ~np.eye(n, dtype=bool))
     z = np.where(colmask, z, -np.inf)
     m = z.max(axis=1, keepdims=True)

@@ -255,13 +255,16 @@ def bce_loss(pos_logits, neg_logits, next_token_type, model=None, l2_emb=0.0):
     return loss
 
 
-def sampled_softmax_loss(h, pos_emb, pos_ids, next_token_type, tau):
-    """In-batch sampled softmax (parity unpinned; oracle/loss.py)."""
+def sampled_softmax_loss(h, pos_emb, pos_ids, next_token_type, tau, log_q=None):
+    """In-batch sampled softmax (parity unpinned; oracle/loss.py); log_q: the logQ
+    correction subtracted from every logit of a column."""
     D = h.shape[-1]
     hv = h.reshape(-1, D); ev = pos_emb.reshape(-1, D)
     ids = pos_ids.reshape(-1); valid = (next_token_type.reshape(-1) == 1)
     n = hv.shape[0]
     z = hv @ ev.t() / tau
+    if log_q is not None:
+        z = z - log_q.reshape(1, -1).to(z.dtype)
     same = (ids[:, None] == ids[None, :]) & ~torch.eye(n, dtype=torch.bool, device=hv.device)
     z = z.masked_fill(~valid[None, :] | same, float('-inf'))
     lse = torch.logsumexp(z, dim=1)

@@ -91,6 +91,9 @@ SIGNATURES = {
     'grk_table_adamw_dense_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _I, _I64, _P, C.c_int32, _P, _P]),
     'grk_table_adamw_catchup_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _I64, _P, C.c_int32, _P, _P]),
     'grk_stamp_rows_dev': (_I, [_P, _P, _P, _I64, _P, _P]),
+    'grk_table_l2_norm_workspace': (_SZ, []),
+    'grk_table_l2_norm': (_I, [_P, _I, _I64, _I, _F, _P, _P, _P, _SZ, _P]),
+    'grk_table_adamw_l2_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _P, _I64, _P, _P, C.c_int32, _P, _P, _P]),
     'grk_attention_fwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _P]),
     'grk_attention_fidelity_supported': (_I, [_I, _I]),
     'grk_attention_bwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _I64, _I, _P, _P, _P, _I64, _P, _I64, _P, _I64,
@@ -115,9 +118,9 @@ SIGNATURES = {
     'grk_gemm': (_I, [_I, _I, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _I, _P, _F, _F, _P, _I, _P]),
     'grk_pair_logits_partials': (_SZ, [_I64]),
     'grk_sampled_softmax_workspace': (_SZ, [_I64, _I]),
-    'grk_sampled_softmax_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _I, _F, _P, _P, _P, _P, _SZ, _P]),
-    'grk_sampled_softmax_bwd': (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _I, _F, _P, _P, _P, _I64, _P, _I64, _P, _SZ,
-                                     _P]),
+    'grk_sampled_softmax_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _I, _F, _P, _P, _P, _P, _P, _SZ, _P]),
+    'grk_sampled_softmax_bwd': (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _I, _F, _P, _P, _P, _P, _I64, _P, _I64, _P,
+                                     _SZ, _P]),
     'grk_pair_logits_fwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _P]),
     'grk_pair_logits_bwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _I64, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
                                  _P, _I64, _P, _I64, _P]),

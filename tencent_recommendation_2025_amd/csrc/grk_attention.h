@@ -221,18 +221,10 @@ __device__ __forceinline__ unsigned long long to_fix(float v) {
 }
 
 // Launch with `lds` bytes of dynamic LDS; above 64 KiB the kernel's limit is
-// raised first (once per kernel and size; gfx950 allows up to 160 KiB).
+// raised first (once per device, kernel and size; gfx950 allows up to 160 KiB).
 inline void launch_lds(void (*kernel)(AttnParams), dim3 grid, int threads, size_t lds, hipStream_t s,
                        const AttnParams& p) {
-  if (lds > 64 * 1024) {
-    static thread_local const void* last_k = nullptr;
-    static thread_local size_t last_b = 0;
-    if (last_k != (const void*)kernel || last_b < lds) {
-      (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      last_k = (const void*)kernel;
-      last_b = lds;
-    }
-  }
+  if (lds > 64 * 1024) (void)ensure_dynamic_lds((const void*)kernel, lds);
   kernel<<<grid, threads, lds, s>>>(p);
 }
 

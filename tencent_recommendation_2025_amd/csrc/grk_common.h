@@ -14,6 +14,8 @@ namespace grk {
 // returns 0 on success or a non-zero GRK_E* code after calling set_error().
 void set_error(const char* fmt, ...);
 void clear_error();
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) per (device, kernel), thread-safe (grk_util.cpp).
+hipError_t ensure_dynamic_lds(const void* kernel, size_t bytes);
 
 #define GRK_CHECK_ARG(cond, ...)                   \
   do {                                             \

@@ -199,7 +199,14 @@ int make_plan(hipblasLtHandle_t h, const Key& key, bool has_bias, Plan* p, const
       moved.b = b2;
       best = -1;
       for (int i : order) {
-        if (run_algo(h, p, &res[i].algo, o, scratch) && run_algo(h, p, &res[i].algo, moved, scratch2) &&
+        // different byte patterns in the two outputs before each candidate: a kernel that
+        // leaves (part of) its output unwritten cannot compare equal on stale bytes; the
+        // stream is drained before the reads (hipMemcpy does not order against the
+        // non-blocking streams the GEMMs run on)
+        if (hipMemsetAsync(scratch, 0x5A, cbytes, o.s) == hipSuccess &&
+            hipMemsetAsync(scratch2, 0xA5, cbytes, o.s) == hipSuccess &&
+            run_algo(h, p, &res[i].algo, o, scratch) && run_algo(h, p, &res[i].algo, moved, scratch2) &&
+            hipStreamSynchronize(o.s) == hipSuccess &&
             hipMemcpy(h1.data(), scratch, cbytes, hipMemcpyDeviceToHost) == hipSuccess &&
             hipMemcpy(h2.data(), scratch2, cbytes, hipMemcpyDeviceToHost) == hipSuccess &&
             memcmp(h1.data(), h2.data(), cbytes) == 0) {

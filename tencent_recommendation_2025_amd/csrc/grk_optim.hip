@@ -40,6 +40,9 @@ struct HpArg {
   const grk_adamw_hparams* ring;
   const int32_t* t;
   int ring_len;
+  // optional (dense mode): g += (*l2coef) * p -- the gradient of l2 * ||W||_F
+  // (model/BaseLine/main.py:184-185) with *l2coef = l2 / ||W|| from grk_table_l2_norm
+  const float* l2coef;
 };
 __device__ __forceinline__ grk_adamw_hparams resolve(const HpArg& a) {
   if (a.ring) return a.ring[*a.t % a.ring_len];
@@ -159,7 +162,66 @@ __global__ void __launch_bounds__(256) k_adamw_dense(P* __restrict__ param, floa
   for (int e = 0; e < NV; ++e) g[e] = 0.f;
   if (slot >= 0) load_grad<NV>(uniq_rows + (int64_t)slot * dim + c, g);
   const int64_t off = row * dim + c;
-  adam_vec<P, NV>(param + off, m + off, v + off, g, adam_step(resolve(hpa)));
+  const AdamStep st = adam_step(resolve(hpa));
+  float pv[NV], mv[NV], vv[NV];
+  load_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
+  if (hpa.l2coef) {  // + d(l2 ||W||)/dp at the parameters the loss saw (before this step's decay)
+    const float k = *hpa.l2coef;
+#pragma unroll
+    for (int e = 0; e < NV; ++e) g[e] += k * pv[e];
+  }
+#pragma unroll
+  for (int e = 0; e < NV; ++e) adam1(pv[e], mv[e], vv[e], g[e], st);
+  store_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
+}
+
+// ||W||_F of a table (l2_emb term, model/BaseLine/main.py:184-185): per-block
+// fp64 partial sums of squares over a fixed grid, then one block sums the
+// partials in block order -- deterministic, independent of scheduling.
+constexpr int kNormBlocks = 1024;
+template <typename P>
+__global__ void __launch_bounds__(256) k_table_sumsq(const P* __restrict__ p, int64_t n, double* __restrict__ part) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  constexpr int NV = Vec16<P>::N;                  // 16-byte loads (the table is 16-byte aligned)
+  const int64_t nv = n / NV;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (int64_t)kNormBlocks * 256) {
+    Vec16<P> x;
+    x.load(p + i * NV);
+    float sq = 0.f;                                  // 8 squares in fp32 (exact for bf16 inputs), then fp64
+#pragma unroll
+    for (int e = 0; e < NV; ++e) sq = fmaf(x.get(e), x.get(e), sq);
+    acc += (double)sq;
+  }
+  for (int64_t i = nv * NV + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)kNormBlocks * 256) {
+    const double x = (double)Elem<P>::load(p + i);
+    acc += x * x;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256) k_table_norm_final(const double* __restrict__ part, float l2,
+                                                          float* __restrict__ norm, float* __restrict__ coef) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < kNormBlocks; i += 256) acc += part[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float nr = (float)sqrt(red[0]);
+    norm[0] = nr;
+    if (coef) coef[0] = nr > 0.f ? l2 / nr : 0.f;   // torch's norm backward at 0 gives 0 too
+  }
 }
 
 // Dense gradient of any dtype ([rows, grad_ld], GT = float or bf16): every
@@ -378,7 +440,7 @@ static int stamp_rows(int32_t* last, const int64_t* uniq_ids, const int32_t* uni
   return GRK_OK;
 }
 
-static HpArg by_value(grk_adamw_hparams hp) { return HpArg{hp, nullptr, nullptr, 0}; }
+static HpArg by_value(grk_adamw_hparams hp) { return HpArg{hp, nullptr, nullptr, 0, nullptr}; }
 static HpArg on_device(const grk_adamw_hparams* ring, int32_t ring_len, const int32_t* t) {
   HpArg a{};
   a.ring = ring;
@@ -444,4 +506,39 @@ extern "C" int grk_stamp_rows_dev(int32_t* last, const int64_t* uniq_ids, const 
                                   const int32_t* t_dev, void* stream) {
   if (!t_dev) { set_error("t_dev required"); return GRK_EINVAL; }
   return stamp_rows(last, uniq_ids, uniq_count, max_uniq, 0, t_dev, stream);
+}
+
+extern "C" int grk_table_adamw_l2_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
+                                      int64_t num_rows, int dim, const int64_t* uniq_ids, const float* uniq_rows,
+                                      const int32_t* uniq_count, int64_t max_uniq, int32_t* row_slot,
+                                      const grk_adamw_hparams* hp_ring, int32_t ring_len, const int32_t* t_dev,
+                                      const float* l2_coef, void* stream) {
+  if (!hp_ring || !t_dev || ring_len <= 0) { set_error("hp_ring / t_dev / ring_len required"); return GRK_EINVAL; }
+  if (!l2_coef) { set_error("l2_coef required"); return GRK_EINVAL; }
+  HpArg hp = on_device(hp_ring, ring_len, t_dev);
+  hp.l2coef = l2_coef;
+  return table_adamw(param, param_dtype, exp_avg, exp_avg_sq, num_rows, dim, uniq_ids, uniq_rows, uniq_count,
+                     max_uniq, row_slot, hp, GRK_ADAM_DENSE, stream);
+}
+
+extern "C" size_t grk_table_l2_norm_workspace(void) { return (size_t)kNormBlocks * sizeof(double); }
+
+extern "C" int grk_table_l2_norm(const void* param, int param_dtype, int64_t num_rows, int dim, float l2, float* norm,
+                                 float* l2_coef, void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(num_rows >= 0 && dim > 0, "bad table shape");
+  GRK_CHECK_ARG(param_dtype == GRK_F32 || param_dtype == GRK_BF16, "bad param dtype");
+  GRK_CHECK_ARG(norm && workspace, "norm / workspace required");
+  GRK_CHECK_ARG(workspace_bytes >= grk_table_l2_norm_workspace(), "workspace too small");
+  GRK_CHECK_ARG(num_rows == 0 || param, "param required");
+  GRK_CHECK_ARG((uintptr_t)param % 16 == 0, "param must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = num_rows * (int64_t)dim;
+  double* part = (double*)workspace;
+  if (param_dtype == GRK_BF16) k_table_sumsq<bf16_t><<<kNormBlocks, 256, 0, s>>>((const bf16_t*)param, n, part);
+  else k_table_sumsq<float><<<kNormBlocks, 256, 0, s>>>((const float*)param, n, part);
+  GRK_LAUNCH_CHECK();
+  k_table_norm_final<<<1, 256, 0, s>>>(part, l2, norm, l2_coef);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
 }

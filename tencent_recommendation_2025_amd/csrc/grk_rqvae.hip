@@ -200,12 +200,7 @@ int launch_rq(const float* z, int64_t ld_z, const float* cb, int64_t n, int K, i
               float* quant, float* dist, float* resid, hipStream_t s) {
   const int chunk = rq_chunk(D, K);
   const size_t lds = (size_t)chunk * rq_stride(D) * sizeof(float);
-  static bool attr_set = false;
-  if (!attr_set) {
-    GRK_CHECK_HIP(hipFuncSetAttribute((const void*)k_rq_assign<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      kRqLdsBytes));
-    attr_set = true;
-  }
+  GRK_CHECK_HIP(ensure_dynamic_lds((const void*)k_rq_assign<D>, kRqLdsBytes));
   const int64_t blocks = (n + 2 * kRqRows - 1) / (2 * kRqRows);
   k_rq_assign<D><<<dim3((unsigned)blocks), kRqBlock, lds, s>>>(z, ld_z, cb, n, K, levels, chunk, codes, quant,
                                                                  dist, resid);

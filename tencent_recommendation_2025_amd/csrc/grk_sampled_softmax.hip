@@ -1,9 +1,13 @@
 // In-batch sampled softmax for gfx950 (north star, no
 // reference implementation -- oracle/loss.py::sampled_softmax).
 //
-//   z_ij = <h_i, e_j> / tau over valid columns j, with j != i masked when
-//          item_id[j] == item_id[i] (the same item is not its own negative);
+//   z_ij = <h_i, e_j> / tau - log q_j over valid columns j, with j != i masked
+//          when item_id[j] == item_id[i] (the same item is not its own negative);
 //   loss = mean over valid rows of (logsumexp_j z_ij - z_ii).
+// log q_j (optional, per position): the logQ correction of sampled softmax
+// (Yi et al., RecSys 2019) -- the log sampling probability of column j's item,
+// subtracted from every logit of that column (positive and negatives alike);
+// without it log q = 0.
 //
 // Only valid positions (next token an item) take part, ~half of a C2 batch, so
 // every kernel works on the COMPACT index space: k_ss_compact lists the valid
@@ -37,6 +41,8 @@ struct SSParams {
   const bf16_t* h; int64_t ldh;
   const bf16_t* e; int64_t lde;
   const int64_t* ids;
+  const float* logq;    // optional [M] log q per position (natural log)
+  float* lqc;           // [M] log2(e) * log q of the compact rows (0 without logq)
   int* vidx;            // compact index -> position (valid positions, ascending)
   int* nvp;             // number of valid positions (device)
   bf16_t *hc, *ec;      // [M, D] compact copies of the valid rows of h, e
@@ -92,7 +98,10 @@ __global__ void __launch_bounds__(256) k_ss_gather(SSParams p) {
         *reinterpret_cast<const uint4*>(p.h + (int64_t)i * p.ldh + ch * 8);
     *reinterpret_cast<uint4*>(p.ec + (int64_t)c * D + ch * 8) =
         *reinterpret_cast<const uint4*>(p.e + (int64_t)i * p.lde + ch * 8);
-    if (ch == 0) p.idc[c] = p.ids[i];
+    if (ch == 0) {
+      p.idc[c] = p.ids[i];
+      p.lqc[c] = p.logq ? p.logq[i] * kLog2e : 0.f;
+    }
   }
 }
 
@@ -159,7 +168,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // cross-wave exchange) walk a slice of e's tiles.
 constexpr int kSSFwdRows = 128;
 
-template <int D>
+template <int D, bool LQ>
 __global__ void __launch_bounds__(256) k_ss_fwd(SSParams p) {
   constexpr int KS = D / 16;
   __shared__ __attribute__((aligned(16))) char img[32 * D * 2];
@@ -180,12 +189,13 @@ __global__ void __launch_bounds__(256) k_ss_fwd(SSParams p) {
   const int tiles = (nv + 31) / 32, per = (tiles + p.nslices - 1) / p.nslices;
   const int c0 = blockIdx.y * per * 32, c1 = min(nv, c0 + per * 32);
   SSTile<D, 256> tile;
-  if (c0 < c1) tile.fetch(p.ec, p.idc, nullptr, c0, nv);
+  const float* lq_in = LQ ? p.lqc : nullptr;  // the tile's per-column log2 q rides in its lse slot
+  if (c0 < c1) tile.fetch(p.ec, p.idc, lq_in, c0, nv);
   for (int jb = c0; jb < c1; jb += 32) {
     __syncthreads();
     tile.put(img, tid, tlse);
     __syncthreads();
-    if (jb + 32 < c1) tile.fetch(p.ec, p.idc, nullptr, jb + 32, nv);  // in flight under this tile's work
+    if (jb + 32 < c1) tile.fetch(p.ec, p.idc, lq_in, jb + 32, nv);  // in flight under this tile's work
     if (!wave_live) continue;
     f32x16 s = acc_zero();
 #pragma unroll
@@ -196,7 +206,7 @@ __global__ void __launch_bounds__(256) k_ss_fwd(SSParams p) {
     for (int k = 0; k < 16; ++k) {
       const int jr = acc_row(k, hh), jc = jb + jr;
       const bool ok = (full || jc < nv) && (jc == oc || tid[jr] != oid);
-      x[k] = ok ? s[k] * p.sl2 : -INFINITY;
+      x[k] = ok ? (LQ ? s[k] * p.sl2 - tlse[jr] : s[k] * p.sl2) : -INFINITY;
       tmax = fmaxf(tmax, x[k]);
     }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
@@ -226,7 +236,7 @@ __global__ void __launch_bounds__(256) k_ss_diag(SSParams p) {
     acc += bf16_to_f32(p.hc[(int64_t)c * D + d]) * bf16_to_f32(p.ec[(int64_t)c * D + d]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-  if (lane == 0) p.diag[c] = acc * p.sl2;
+  if (lane == 0) p.diag[c] = acc * p.sl2 - p.lqc[c];
 }
 
 // Merge slices -> lse2[ic]; per-block loss partials in a fixed order.
@@ -303,10 +313,12 @@ __global__ void __launch_bounds__(SSB<D>::NT) k_ss_bwd(SSParams p) {
   const int oc = oc0 + rg * 32 + r;
   const bool ook = oc < nv;
   const int64_t oid = ook ? p.idc[oc] : -2;
-  const float olse = (rows && ook) ? p.lse2[oc] : 0.f;
+  // exponent offset of element (row i, column j) = lse2_i + log2 q_j: the own row's part
+  // here, the tile row's part staged with the tile (lse2 of h rows, or log2 q of e rows)
+  const float olse = ook ? (rows ? p.lse2[oc] : (p.logq ? p.lqc[oc] : 0.f)) : 0.f;
   const bf16_t* own = rows ? p.hc : p.ec;
   const bf16_t* tsrc = rows ? p.ec : p.hc;
-  const float* lse_in = rows ? nullptr : p.lse2;
+  const float* lse_in = rows ? (p.logq ? p.lqc : nullptr) : p.lse2;
   const int col0 = ws * DQ;
   bf16x8 of[KSQ];
 #pragma unroll
@@ -354,7 +366,7 @@ __global__ void __launch_bounds__(SSB<D>::NT) k_ss_bwd(SSParams p) {
       const int k = ws * EPW + e;  // not a compile-time constant across waves: acc_row by formula
       const int tr = (k & 3) + 8 * (k >> 2) + 4 * hh, tc = tb + tr;
       const bool ok = ook && (full || tc < nv) && (tc == oc || L.tid[tr] != oid);
-      const float pr = __builtin_amdgcn_exp2f(fmaf(se[e], p.sl2, -(rows ? olse : L.tlse[tr])));
+      const float pr = __builtin_amdgcn_exp2f(fmaf(se[e], p.sl2, -(olse + L.tlse[tr])));
       g[e] = ok ? (tc == oc ? pr - 1.f : pr) * coef : 0.f;
     }
 #pragma unroll
@@ -405,7 +417,9 @@ static int ss_launch(const SSParams& p, int which, hipStream_t s) {
   if (which == 0) {
     k_ss_diag<D><<<(unsigned)((p.M + 3) / 4), 256, 0, s>>>(p);
     GRK_LAUNCH_CHECK();
-    k_ss_fwd<D><<<dim3((unsigned)((p.M + kSSFwdRows - 1) / kSSFwdRows), p.nslices), 256, 0, s>>>(p);
+    const dim3 grid((unsigned)((p.M + kSSFwdRows - 1) / kSSFwdRows), p.nslices);
+    if (p.logq) k_ss_fwd<D, true><<<grid, 256, 0, s>>>(p);
+    else k_ss_fwd<D, false><<<grid, 256, 0, s>>>(p);
   } else {
     k_ss_bwd<D><<<dim3((unsigned)((p.M + SSB<D>::ROWS - 1) / SSB<D>::ROWS), 2), SSB<D>::NT, 0, s>>>(p);
   }
@@ -440,7 +454,7 @@ struct SSWs {
   int* nv;
   bf16_t *hc, *ec;
   int64_t* idc;
-  float *pm, *pl, *diag, *partials;
+  float *lqc, *pm, *pl, *diag, *partials;
   size_t bytes;
 };
 
@@ -459,6 +473,7 @@ static SSWs ss_ws(char* base, int M, int D) {
   w.hc = (bf16_t*)take((size_t)M * D * 2);
   w.ec = (bf16_t*)take((size_t)M * D * 2);
   w.idc = (int64_t*)take((size_t)M * 8);
+  w.lqc = (float*)take((size_t)M * 4);
   w.pm = (float*)take((size_t)ns * M * 4);
   w.pl = (float*)take((size_t)ns * M * 4);
   w.diag = (float*)take((size_t)M * 4);
@@ -477,8 +492,8 @@ extern "C" size_t grk_sampled_softmax_workspace(int64_t num_rows, int dim) {
 }
 
 static int ss_fill(const void* h, int64_t ldh, const void* e, int64_t lde, const int64_t* ids, const uint8_t* valid,
-                   int64_t num_rows, int dim, float tau, void* workspace, size_t workspace_bytes, SSParams* p,
-                   SSWs* w) {
+                   int64_t num_rows, int dim, float tau, const float* log_q, void* workspace, size_t workspace_bytes,
+                   SSParams* p, SSWs* w) {
   GRK_CHECK_ARG(h && e && ids && valid, "h, e, item_ids and valid are required");
   GRK_CHECK_ARG(num_rows > 0 && num_rows < (1LL << 30), "num_rows out of range");
   GRK_CHECK_ARG(dim == 32 || dim == 64 || dim == 128 || dim == 256 || dim == 512, "dim %d unsupported", dim);
@@ -488,22 +503,23 @@ static int ss_fill(const void* h, int64_t ldh, const void* e, int64_t lde, const
   GRK_CHECK_ARG(workspace && workspace_bytes >= grk_sampled_softmax_workspace(num_rows, dim), "workspace too small");
   memset(p, 0, sizeof(*p));
   p->h = (const bf16_t*)h; p->ldh = ldh; p->e = (const bf16_t*)e; p->lde = lde;
-  p->ids = ids; p->M = (int)num_rows; p->sl2 = kLog2e / tau;
+  p->ids = ids; p->logq = log_q; p->M = (int)num_rows; p->sl2 = kLog2e / tau;
   p->nslices = ss_slices(p->M);
   *w = ss_ws((char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), p->M, dim);
-  p->vidx = w->vidx; p->nvp = w->nv; p->hc = w->hc; p->ec = w->ec; p->idc = w->idc;
+  p->vidx = w->vidx; p->nvp = w->nv; p->hc = w->hc; p->ec = w->ec; p->idc = w->idc; p->lqc = w->lqc;
   p->pm = w->pm; p->pl = w->pl; p->diag = w->diag; p->partials = w->partials;
   return GRK_OK;
 }
 
 extern "C" int grk_sampled_softmax_fwd(const void* h, int64_t ldh, const void* e, int64_t lde, const int64_t* item_ids,
-                                       const uint8_t* valid, int64_t num_rows, int dim, float tau, float* lse2,
+                                       const uint8_t* valid, int64_t num_rows, int dim, float tau, const float* log_q,
+                                       float* lse2,
                                        float* loss, int32_t* count, void* workspace, size_t workspace_bytes,
                                        void* stream) {
   clear_error();
   SSParams p;
   SSWs w;
-  int rc = ss_fill(h, ldh, e, lde, item_ids, valid, num_rows, dim, tau, workspace, workspace_bytes, &p, &w);
+  int rc = ss_fill(h, ldh, e, lde, item_ids, valid, num_rows, dim, tau, log_q, workspace, workspace_bytes, &p, &w);
   if (rc) return rc;
   GRK_CHECK_ARG(lse2 && loss && count, "lse2, loss and count are required");
   p.lse2 = lse2; p.loss = loss;
@@ -521,13 +537,14 @@ extern "C" int grk_sampled_softmax_fwd(const void* h, int64_t ldh, const void* e
 }
 
 extern "C" int grk_sampled_softmax_bwd(const void* h, int64_t ldh, const void* e, int64_t lde, const int64_t* item_ids,
-                                       const uint8_t* valid, int64_t num_rows, int dim, float tau, const float* lse2,
+                                       const uint8_t* valid, int64_t num_rows, int dim, float tau, const float* log_q,
+                                       const float* lse2,
                                        const float* grad_loss, float* dh, int64_t lddh, float* de, int64_t ldde,
                                        void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
   SSParams p;
   SSWs w;
-  int rc = ss_fill(h, ldh, e, lde, item_ids, valid, num_rows, dim, tau, workspace, workspace_bytes, &p, &w);
+  int rc = ss_fill(h, ldh, e, lde, item_ids, valid, num_rows, dim, tau, log_q, workspace, workspace_bytes, &p, &w);
   if (rc) return rc;
   GRK_CHECK_ARG(lse2 && dh && de, "lse2, dh and de are required");
   GRK_CHECK_ARG(lddh >= dim && ldde >= dim && lddh % 4 == 0 && ldde % 4 == 0, "lddh / ldde must be >= dim, multiple of 4");

@@ -17,10 +17,14 @@
 // cannot be reproduced on a GPU; the distribution is the same (uniform over the
 // allowed ids).
 //
-// One workgroup per sequence: the exclusion list is staged once in LDS and every
-// membership test is a scan of it with all lanes reading the same word (LDS
-// broadcast, no bank conflicts); one lane per position.  Integer work on a few KB
-// per sequence: launch-bound, never HBM- or MFMA-bound.
+// One workgroup per sequence, one lane per position.  Exclusion lists of up to
+// kLdsExcl entries are staged once in LDS and bitonic-sorted there (padding
+// 0x7FFFFFFF: never drawn), so every membership test is a 13-step binary search
+// over LDS; longer lists (users with very long histories) are scanned in global
+// memory (L2-served: one workgroup rereads its own row).  The list's order and
+// duplicates do not matter (set semantics, as the reference's `ts`), so no
+// length cap and no truncation.  Integer work on a few KB per sequence:
+// launch-bound, never HBM- or MFMA-bound.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -31,7 +35,8 @@ namespace grk {
 namespace {
 
 constexpr int kSampBlock = 256;
-constexpr int kMaxExcl = 4096;  // LDS: 16 KiB of int32
+constexpr int kLdsExcl = 8192;  // LDS: 32 KiB of int32
+constexpr int32_t kPadId = 0x7FFFFFFF;
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -52,11 +57,27 @@ __global__ void __launch_bounds__(kSampBlock)
                        const int32_t* __restrict__ excl, int32_t excl_len, int64_t num_items, uint64_t seed,
                        int32_t max_tries, const int32_t* __restrict__ item_feat, int32_t num_feat,
                        const uint8_t* __restrict__ item_ok, int32_t* __restrict__ neg, int32_t* __restrict__ neg_feat, int32_t* err_flag) {
-  __shared__ int32_t ex[kMaxExcl];
+  __shared__ int32_t ex[kLdsExcl];
   const int64_t b = blockIdx.x;
   const int32_t* e = excl + b * (int64_t)excl_len;
-  for (int i = threadIdx.x; i < excl_len; i += kSampBlock) ex[i] = e[i];
-  __syncthreads();
+  const bool in_lds = excl_len <= kLdsExcl;
+  int n2 = 1;  // sorted image size: a power of two >= excl_len
+  if (in_lds) {
+    while (n2 < excl_len) n2 <<= 1;
+    for (int i = threadIdx.x; i < n2; i += kSampBlock) ex[i] = i < excl_len ? e[i] : kPadId;
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1)          // bitonic sort, ascending
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = threadIdx.x; i < n2; i += kSampBlock) {
+          const int l = i ^ j;
+          if (l > i) {
+            const int32_t x = ex[i], y = ex[l];
+            if (((i & k) == 0) ? (x > y) : (x < y)) { ex[i] = y; ex[l] = x; }
+          }
+        }
+        __syncthreads();
+      }
+  }
   for (int32_t t = threadIdx.x; t < T; t += kSampBlock) {
     const int64_t o = b * (int64_t)T + t;
     int32_t v = 0;
@@ -65,7 +86,14 @@ __global__ void __launch_bounds__(kSampBlock)
       for (int32_t a = 0; a < max_tries && hit; ++a) {
         v = draw(seed, b, t, a, num_items);
         hit = item_ok != nullptr && item_ok[v] == 0;
-        for (int i = 0; i < excl_len; ++i) hit |= (ex[i] == v);
+        if (in_lds) {
+          int base = 0;  // number of entries < v (binary search over the sorted image)
+          for (int half = n2 >> 1; half >= 1; half >>= 1)
+            if (ex[base + half - 1] < v) base += half;
+          hit |= ex[base] == v;
+        } else {
+          for (int i = 0; i < excl_len && !hit; ++i) hit = e[i] == v;
+        }
       }
       if (hit && err_flag) atomicOr(err_flag, 2);  // every try was excluded: the last draw is kept
     }
@@ -87,7 +115,7 @@ extern "C" int grk_sample_negatives(const int32_t* pos, const int32_t* next_toke
   clear_error();
   GRK_CHECK_ARG(batch >= 0 && seq_len > 0, "bad batch (%lld) / seq_len (%d)", (long long)batch, seq_len);
   GRK_CHECK_ARG(num_items >= 1 && num_items < 0x7FFFFFFFLL, "num_items must be in [1, 2^31 - 1)");
-  GRK_CHECK_ARG(excl_len >= 0 && excl_len <= kMaxExcl, "excl_len (%d) must be in [0, %d]", excl_len, kMaxExcl);
+  GRK_CHECK_ARG(excl_len >= 0, "excl_len (%d) must be >= 0", excl_len);
   GRK_CHECK_ARG(excl_len == 0 || excl, "excl is NULL");
   GRK_CHECK_ARG(max_tries >= 1 && max_tries <= 65535, "max_tries must be in [1, 65535]");
   GRK_CHECK_ARG(seq_len <= 65535, "seq_len must be <= 65535");

@@ -3,6 +3,10 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "../../include/grk.h"
 
 namespace grk {
@@ -17,6 +21,24 @@ void set_error(const char* fmt, ...) {
 }
 
 void clear_error() { g_err[0] = 0; }
+
+// Raise a kernel's dynamic-LDS limit to at least `bytes` on the CURRENT device,
+// once per (device, kernel) and size: the attribute is per device, so a process
+// that launches on a second GPU sets it there too; the map is shared by every
+// thread (mutex).
+hipError_t ensure_dynamic_lds(const void* kernel, size_t bytes) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, size_t> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lock(mu);
+  size_t& have = done[{dev, kernel}];
+  if (have >= bytes) return hipSuccess;
+  e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess) have = bytes;
+  return e;
+}
 
 }  // namespace grk
 

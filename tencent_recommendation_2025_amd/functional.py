@@ -395,31 +395,53 @@ def bce_loss(h, e_pos, e_neg, next_token_type):
 # -------------------------------------------------------- sampled softmax ----
 class _SampledSoftmaxFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, e, item_ids, valid, tau):
-        D = h.shape[-1]
+    def forward(ctx, h, e, item_ids, valid, tau, log_q):
         hb = _rows2d(h.to(torch.bfloat16))
         eb = _rows2d(e.to(torch.bfloat16))
-        loss, lse2, count = K.sampled_softmax_fwd(hb, eb, item_ids, valid, tau)
-        ctx.save_for_backward(hb, eb, item_ids, valid, lse2, count)
+        loss, lse2, count = K.sampled_softmax_fwd(hb, eb, item_ids, valid, tau, log_q)
+        ctx.save_for_backward(hb, eb, item_ids, valid, lse2, count, log_q)
         ctx.meta = (tau, h.shape, e.shape, h.dtype, e.dtype)
         return loss
 
     @staticmethod
     def backward(ctx, gloss):
-        hb, eb, ids, valid, lse2, count = ctx.saved_tensors
+        hb, eb, ids, valid, lse2, count, log_q = ctx.saved_tensors
         tau, hs, es, hdt, edt = ctx.meta
-        dh, de = K.sampled_softmax_bwd(hb, eb, ids, valid, tau, lse2, gloss)
+        dh, de = K.sampled_softmax_bwd(hb, eb, ids, valid, tau, lse2, gloss, log_q)
         dh = dh.view(hs).to(hdt) if ctx.needs_input_grad[0] else None
         de = de.view(es).to(edt) if ctx.needs_input_grad[1] else None
-        return dh, de, None, None, None
+        return dh, de, None, None, None, None
 
 
 @_disable
-def sampled_softmax_loss(h, pos_emb, pos_ids, next_token_type, tau):
+def sampled_softmax_loss(h, pos_emb, pos_ids, next_token_type, tau, log_q=None):
     """In-batch sampled softmax over every valid position's positive item
     (north star; oracle/loss.py::sampled_softmax): one flash-style MFMA pass
     for the loss, two fused passes (dH, dE) for the gradients, all over the
-    valid positions only."""
+    valid positions only.  log_q (optional, [B, T] or [N], natural log): the
+    logQ correction -- the log sampling probability of each position's item,
+    subtracted from its column's logits (no gradient flows into it)."""
     ids = pos_ids.reshape(-1).to(torch.int64).contiguous()
     valid = (next_token_type.reshape(-1) == 1).to(torch.uint8).contiguous()
-    return _SampledSoftmaxFn.apply(h, pos_emb, ids, valid, float(tau))
+    if log_q is not None:
+        log_q = log_q.detach().reshape(-1).to(torch.float32).contiguous()
+    return _SampledSoftmaxFn.apply(h, pos_emb, ids, valid, float(tau), log_q)
+
+
+def batch_log_q(pos_ids, next_token_type):
+    """log q of each position's item estimated from the batch itself: log(count of
+    the item among the valid positions / number of valid positions) -- the
+    in-batch sampling probability of that item (the logQ correction when no
+    corpus frequency table is given).  Device ops, no host sync."""
+    ids = pos_ids.reshape(-1).to(torch.int64)
+    valid = next_token_type.reshape(-1) == 1
+    key = torch.where(valid, ids, torch.full_like(ids, -1))
+    srt, inv = torch.sort(key)
+    head = torch.ones_like(srt, dtype=torch.bool)
+    head[1:] = srt[1:] != srt[:-1]
+    run = torch.cumsum(head.to(torch.int64), 0) - 1                 # run index of each sorted entry
+    counts = torch.zeros_like(srt).scatter_add_(0, run, torch.ones_like(srt))
+    cnt = torch.empty_like(srt)
+    cnt[inv] = counts[run]
+    nv = valid.sum().clamp(min=1).to(torch.float32)
+    return torch.where(valid, torch.log(cnt.to(torch.float32) / nv), torch.zeros_like(nv.expand_as(cnt)))

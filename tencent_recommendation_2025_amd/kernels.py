@@ -223,6 +223,36 @@ def table_adamw(param, exp_avg, exp_avg_sq, hp, ids=None, rows=None, count=None,
     L.check(rc, 'grk_table_adamw')
 
 
+def table_l2_norm(param, l2, norm=None, coef=None):
+    """(norm fp32 [1], l2 / norm fp32 [1]) of a whole table (grk_table_l2_norm):
+    the l2_emb term's value and gradient scale, on the device."""
+    _require_cuda(param, norm, coef)
+    if not param.is_contiguous() or param.data_ptr() % 16:
+        raise L.GrkError('param must be contiguous and 16-byte aligned')
+    dev = param.device
+    norm = torch.empty(1, dtype=torch.float32, device=dev) if norm is None else norm
+    coef = torch.empty(1, dtype=torch.float32, device=dev) if coef is None else coef
+    ws = torch.empty(L.lib().grk_table_l2_norm_workspace(), dtype=torch.uint8, device=dev)
+    rc = L.lib().grk_table_l2_norm(param.data_ptr(), L.dtype_code(param.dtype), param.shape[0], param.shape[1],
+                                   float(l2), norm.data_ptr(), coef.data_ptr(), ws.data_ptr(), ws.numel(),
+                                   L.stream_ptr(dev))
+    L.check(rc, 'grk_table_l2_norm')
+    return norm, coef
+
+
+def table_adamw_l2(param, exp_avg, exp_avg_sq, clock, l2_coef, ids=None, rows=None, count=None, capacity=0,
+                   row_slot=None):
+    """Dense-mode table AdamW with every row's gradient + l2_coef * p (grk_table_adamw_l2_dev)."""
+    _require_cuda(param, exp_avg, exp_avg_sq, ids, rows, count, row_slot, l2_coef)
+    if not (param.is_contiguous() and exp_avg.is_contiguous() and exp_avg_sq.is_contiguous()):
+        raise L.GrkError('param and moments must be contiguous')
+    rc = L.lib().grk_table_adamw_l2_dev(param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(),
+                                        exp_avg_sq.data_ptr(), param.shape[0], param.shape[1], _ptr(ids), _ptr(rows),
+                                        _ptr(count), capacity, _ptr(row_slot), clock.ring.data_ptr(), clock.ring_len,
+                                        clock.t.data_ptr(), l2_coef.data_ptr(), L.stream_ptr(param.device))
+    L.check(rc, 'grk_table_adamw_l2_dev')
+
+
 # ------------------------------------------------------------------ attention
 def _col_view_ok(t, name, dtypes=(torch.bfloat16,)):
     if t.dim() != 2 or t.stride(1) != 1 or t.dtype not in dtypes:
@@ -676,9 +706,18 @@ def pair_logits_bwd(h, e_pos, e_neg, gpos=None, gneg=None, pos_logits=None, neg_
 
 
 # --------------------------------------------------------- sampled softmax
-def sampled_softmax_fwd(h, e, item_ids, valid, tau):
-    """(loss, lse2, count) of the in-batch sampled softmax (grk_sampled_softmax_fwd)."""
-    _require_cuda(h, e, item_ids, valid)
+def _logq(log_q, M):
+    if log_q is None:
+        return None
+    if log_q.dtype != torch.float32 or log_q.numel() != M or not log_q.is_contiguous():
+        raise L.GrkError(f'log_q must be a contiguous fp32 tensor of {M} positions')
+    return log_q
+
+
+def sampled_softmax_fwd(h, e, item_ids, valid, tau, log_q=None):
+    """(loss, lse2, count) of the in-batch sampled softmax (grk_sampled_softmax_fwd);
+    log_q (fp32 [M], natural log): the logQ correction subtracted from column j's logits."""
+    _require_cuda(h, e, item_ids, valid, log_q)
     M, D = h.shape
     dev = h.device
     (hp, hl), (ep, el) = _rows(h, 'h'), _rows(e, 'e')
@@ -687,15 +726,15 @@ def sampled_softmax_fwd(h, e, item_ids, valid, tau):
     loss = torch.empty((), dtype=torch.float32, device=dev)
     count = torch.empty(1, dtype=torch.int32, device=dev)
     rc = L.lib().grk_sampled_softmax_fwd(hp, hl, ep, el, item_ids.data_ptr(), valid.data_ptr(), M, D, float(tau),
-                                         lse2.data_ptr(), loss.data_ptr(), count.data_ptr(), ws.data_ptr(),
-                                         ws.numel(), L.stream_ptr(dev))
+                                         _ptr(_logq(log_q, M)), lse2.data_ptr(), loss.data_ptr(), count.data_ptr(),
+                                         ws.data_ptr(), ws.numel(), L.stream_ptr(dev))
     L.check(rc, 'grk_sampled_softmax_fwd')
     return loss, lse2, count
 
 
-def sampled_softmax_bwd(h, e, item_ids, valid, tau, lse2, grad_loss=None):
+def sampled_softmax_bwd(h, e, item_ids, valid, tau, lse2, grad_loss=None, log_q=None):
     """(dh, de) fp32 [M, D] of the in-batch sampled softmax, fused (grk_sampled_softmax_bwd)."""
-    _require_cuda(h, e, item_ids, valid, lse2, grad_loss)
+    _require_cuda(h, e, item_ids, valid, lse2, grad_loss, log_q)
     M, D = h.shape
     dev = h.device
     dh = torch.empty(M, D, dtype=torch.float32, device=dev)
@@ -704,8 +743,8 @@ def sampled_softmax_bwd(h, e, item_ids, valid, tau, lse2, grad_loss=None):
     ws = torch.empty(max(L.lib().grk_sampled_softmax_workspace(M, D), 4), dtype=torch.uint8, device=dev)
     (hp, hl), (ep, el) = _rows(h, 'h'), _rows(e, 'e')
     rc = L.lib().grk_sampled_softmax_bwd(hp, hl, ep, el, item_ids.data_ptr(), valid.data_ptr(), M, D, float(tau),
-                                         lse2.data_ptr(), _ptr(gl), dh.data_ptr(), D, de.data_ptr(), D, ws.data_ptr(),
-                                         ws.numel(), L.stream_ptr(dev))
+                                         _ptr(_logq(log_q, M)), lse2.data_ptr(), _ptr(gl), dh.data_ptr(), D,
+                                         de.data_ptr(), D, ws.data_ptr(), ws.numel(), L.stream_ptr(dev))
     L.check(rc, 'grk_sampled_softmax_bwd')
     return dh, de
 

@@ -131,9 +131,16 @@ class FusedAdamW:
     """AdamW over a BaselineModel: table groups on grk kernels, dense params on torch fused AdamW."""
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
-                 table_dtype=torch.bfloat16, groups=DEFAULT_GROUPS, defer_period=16):
+                 table_dtype=torch.bfloat16, groups=DEFAULT_GROUPS, defer_period=16, l2_emb=0.0):
+        """l2_emb > 0: the BaseLine script's ``loss += l2_emb * ||item_emb.weight||_F``
+        (model/BaseLine/main.py:184-185) -- ``l2_term()`` gives the loss term (Trainer
+        adds it), ``step()`` adds its gradient l2 * W / ||W|| to every item row.  Every
+        row then moves every step, so the item table is updated densely (not deferred)."""
         if table_mode not in ('dense', 'lazy'):
             raise ValueError("table_mode must be 'dense' or 'lazy'")
+        self.l2_emb = float(l2_emb)
+        if self.l2_emb and table_mode == 'lazy':
+            raise ValueError('l2_emb moves every item row each step: it needs table_mode="dense"')
         self.model = model
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.lazy = table_mode == 'lazy'
@@ -164,7 +171,8 @@ class FusedAdamW:
         # bit-identical to moving every row every step, without streaming the
         # whole table through HBM each step.  Needs Trainer.step (begin_step).
         self.defer = int(defer_period) if (defer_period and not self.lazy and cuda) else 0
-        self._deferred = {g.name: g for g in self.groups if g.name in ('item', 'user')} if self.defer else {}
+        deferrable = ('user',) if self.l2_emb else ('item', 'user')
+        self._deferred = {g.name: g for g in self.groups if g.name in deferrable} if self.defer else {}
         self._seg = None     # step every deferred row was last brought up to (segment start)
         self._begun = None   # step for which begin_step caught the batch rows up
         for g in self._deferred.values():
@@ -176,6 +184,13 @@ class FusedAdamW:
         if self.clock is not None:
             self._pinned = [torch.zeros_like(self.clock.ring, device='cpu').pin_memory() for _ in range(2)]
             self._uploads = 0
+        self._l2_group = next((g for g in self.groups if g.name == 'item'), None) if self.l2_emb else None
+        if self.l2_emb and (self._l2_group is None or self.clock is None):
+            raise ValueError('l2_emb needs the item table in a table group on the GPU')
+        if self._l2_group is not None:
+            self._l2_norm = torch.zeros(1, dtype=torch.float32, device=dev)
+            self._l2_coef = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._l2_ready = None  # step whose norm / gradient scale l2_term computed
         if self.defer:
             model.register_state_dict_pre_hook(lambda *args, **kw: self.flush())
             if hasattr(model, '_flushers'):  # predict / save_item_emb / eval() read fresh rows
@@ -249,6 +264,18 @@ class FusedAdamW:
         self._begun = self.t
 
     @torch.no_grad()
+    def l2_term(self):
+        """l2_emb * ||item_emb.weight||_F at the current parameters (a device scalar, no
+        host sync) -- the BaseLine loss term; its gradient goes straight into the
+        item table's AdamW in step()."""
+        if not self.l2_emb:
+            return None
+        g = self._l2_group
+        K.table_l2_norm(g.flat, self.l2_emb, self._l2_norm, self._l2_coef)
+        self._l2_ready = self.t
+        return (self.l2_emb * self._l2_norm).reshape(())
+
+    @torch.no_grad()
     def flush(self):
         """Bring every row of the deferred tables to the current step (before reading them)."""
         if self._deferred and self._seg is not None:
@@ -266,6 +293,9 @@ class FusedAdamW:
         if self._deferred and self._begun != self.t:  # no begin_step: every row to step t, then dense
             self.flush()
         begun, self._begun = self._begun == self.t, None
+        if self.l2_emb and self._l2_ready != self.t:   # no l2_term this step: its gradient scale now
+            self.l2_term()
+        self._l2_ready = None
         self.t += 1
         if self.clock is not None:
             self.clock.advance()
@@ -283,6 +313,20 @@ class FusedAdamW:
                     g.clear()
                     continue
                 g.last.fill_(self.t)  # dense update below moves every row
+            if g is self._l2_group:  # every row: its sparse gradient + l2 * p / ||W||
+                res = None
+                if g.pending:
+                    res = K.embedding_backward(g.pending, g.rows, g.dim, padding_idx=0, token_type=g.token_type,
+                                               seq_len=g.seq_len, dense=False, sparse=True, row_slot=g.row_slot)
+                if g.dense_grads:
+                    raise RuntimeError('l2_emb: the item table takes row-sparse gradients only')
+                if res is None:
+                    K.table_adamw_l2(g.flat, g.exp_avg, g.exp_avg_sq, self.clock, self._l2_coef)
+                else:
+                    K.table_adamw_l2(g.flat, g.exp_avg, g.exp_avg_sq, self.clock, self._l2_coef, res.ids, res.rows,
+                                     res.count, res.capacity, g.row_slot)
+                g.clear()
+                continue
             if g.dense_grads and not g.pending:  # dense gradients only: per-range updates
                 g.step_dense_ranges(hp)
             elif g.dense_grads:  # mixed: one dense fp32 gradient

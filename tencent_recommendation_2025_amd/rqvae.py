@@ -199,9 +199,24 @@ def semantic_id_table(codes, num_items):
     return t
 
 
-def semantic_id_schema(levels, codebook_size, prefix='sid'):
+def semantic_id_schema(levels, codebook_size=None, prefix='sid', codes=None):
     """Feature names and statistics the semantic ids add to the O1 model's
-    ``item_sparse`` features (feat_statistics[k] = codebook_size; the model
-    sizes each table feat_statistics[k] + 1, BaseLineO1/model.py:271-280)."""
+    ``item_sparse`` features (the model sizes each table feat_statistics[k] + 1,
+    BaseLineO1/model.py:271-280).
+
+    ``codes`` (int [n, levels], 0-based -- e.g. ``dedup_level`` output, whose
+    collision level can exceed the codebook size): per-level cardinalities
+    ``codes[:, l].max() + 1``, so every 1-based id of semantic_id_table(codes)
+    has its table row.  Without codes every level gets ``codebook_size``."""
+    if codes is not None:
+        c = torch.as_tensor(codes)
+        levels = c.shape[1]
+        card = [int(c[:, lvl].max()) + 1 if c.shape[0] else 1 for lvl in range(levels)]
+        if codebook_size is not None:
+            card = [max(k, int(codebook_size)) for k in card]
+    elif codebook_size is None:
+        raise ValueError('semantic_id_schema needs codebook_size or codes')
+    else:
+        card = [int(codebook_size)] * levels
     names = [f'{prefix}{lvl}' for lvl in range(levels)]
-    return names, {n: codebook_size for n in names}
+    return names, dict(zip(names, card))

@@ -224,15 +224,18 @@ class SeqStore:
                 out[k] = torch.from_numpy(np.ascontiguousarray(sparse[..., sp_col[k]]))
         return out
 
-    def history_items(self, uids, max_len=4096):
-        """int32 [B, L]: the item ids of each user's whole history (0-padded) --
-        _random_neq's exclusion set ts (model/BaseLine/dataset.py:136-139)."""
+    def history_items(self, uids):
+        """int32 [B, L]: each user's distinct item ids over the whole history,
+        ascending, 0-padded (L = the largest distinct count in the batch) --
+        _random_neq's exclusion set ts (model/BaseLine/dataset.py:136-139).  No
+        truncation: grk_sample_negatives takes exclusion lists of any length."""
         uids = np.asarray(uids, np.int64)
         start, end = self.off[uids], self.off[uids + 1]
-        L = int(min(max_len, max(1, int((end - start).max()))))
+        sets = [np.unique(self.tid[s:e][self.ttype[s:e] == 1]) for s, e in zip(start, end)]
+        sets = [u[u != 0] for u in sets]
+        L = max(1, max((len(u) for u in sets), default=1))
         out = np.zeros((len(uids), L), np.int32)
-        for b, (s, e) in enumerate(zip(start, end)):
-            ids = self.tid[s:e][self.ttype[s:e] == 1][-L:]
+        for b, ids in enumerate(sets):
             out[b, :len(ids)] = ids
         return torch.from_numpy(out)
 
@@ -255,7 +258,8 @@ class DeviceNegatives:
         """The batch (on the device) with neg and neg_feat filled."""
         from . import kernels as K
         seq, pos, _neg, tt, ntt, nat, sf, pf, _nf = batch[:9]
-        excl = torch.cat([self.store.history_items(uids).to(self.device), pos.to(torch.int32)], 1)
+        # the whole history holds every positive of the window (pos are the users' own next items)
+        excl = self.store.history_items(uids).to(self.device)
         neg, nfeat = K.sample_negatives(pos, ntt, excl, self.store.itemnum, seed, item_feat=self.item_sparse,
                                         item_ok=self.item_ok)
         neg_feat = {}

@@ -81,6 +81,9 @@ class Trainer:
 
     loss: "bce" -- the reference loss (pos/neg BCE, main.py:177-182);
           "sampled_softmax" -- north-star in-batch sampled softmax.
+    log_q (sampled softmax): the logQ correction -- None (off), "batch" (each
+          item's in-batch frequency, functional.batch_log_q) or a tensor of
+          per-item log sampling probabilities [num_items + 1] indexed by item id.
     graph: capture the step in a HIP graph after ``graph_warmup`` eager steps
           and replay it (needs a fused optimizer with a device clock and batches
           of one fixed shape; a batch of another shape runs eagerly).  Dropout
@@ -89,9 +92,12 @@ class Trainer:
     """
 
     def __init__(self, model, optimizer, loss='bce', amp_dtype=torch.bfloat16, temperature=0.05, graph=False,
-                 graph_warmup=3, graph_audit=False):
+                 graph_warmup=3, graph_audit=False, log_q=None):
         if loss not in ('bce', 'sampled_softmax'):
             raise ValueError("loss must be 'bce' or 'sampled_softmax'")
+        if log_q is not None and (loss != 'sampled_softmax' or not (isinstance(log_q, torch.Tensor) or log_q == 'batch')):
+            raise ValueError("log_q: None, 'batch' or a per-item tensor, with loss='sampled_softmax'")
+        self.log_q = log_q
         self.model, self.opt, self.loss_kind = model, optimizer, loss
         self.amp_dtype, self.temperature = amp_dtype, temperature
         self.graph, self.graph_warmup = bool(graph), int(graph_warmup)
@@ -125,8 +131,17 @@ class Trainer:
         with amp:
             h, pe, ne = self.model.encode(seq, pos, neg, tt, sf, pf, nf, timestamps=ts)
             if self.loss_kind == 'bce':
-                return G.bce_loss(h, pe, ne, ntt)
-            return G.sampled_softmax_loss(h, pe, pos, ntt, self.temperature)
+                loss = G.bce_loss(h, pe, ne, ntt)
+            else:
+                lq = None
+                if isinstance(self.log_q, torch.Tensor):
+                    lq = self.log_q.to(pos.device)[pos.long()]
+                elif self.log_q == 'batch':
+                    lq = G.batch_log_q(pos, ntt)
+                loss = G.sampled_softmax_loss(h, pe, pos, ntt, self.temperature, log_q=lq)
+        # BaseLine's l2_emb * ||item_emb.weight|| (main.py:184-185): value here, gradient in the optimizer
+        l2 = self.opt.l2_term() if getattr(self.opt, 'l2_emb', 0.0) else None
+        return loss if l2 is None else loss + l2
 
     def eager_step(self, batch, next_batch=None):
         self.opt.zero_grad()

@@ -29,6 +29,10 @@ Fixtures:
                       the exact top-10 (float64) the HNSW search approximates.
                       ``python tests/golden/make_golden.py retrieval`` writes
                       only this fixture.
+  model_baseline_nf_live.npz, model_o1_nf_live.npz
+                   -- the same training step with ``norm_first=True`` (pre-LN
+                      blocks, model/BaseLine/model.py:338-342); written by
+                      ``python tests/golden/make_golden.py norm_first``.
 """
 from __future__ import annotations
 
@@ -87,6 +91,64 @@ def flat_feats(prefix, feats):
     return {f'{prefix}.{k}': v.numpy() for k, v in feats.items()}
 
 
+def model_step_fixture(tag, mod, wd, l2, live, args, dset, ft, batch):
+    """One full training step of the reference BaselineModel -> model_<tag>.npz."""
+    seq, pos, neg, tt, ntt, nat, sf, pf, nf = batch
+    torch.manual_seed(0)
+    m = mod.BaselineModel(dset.usernum, dset.itemnum, dset.feat_statistics, ft, args)
+    ref_init(m)
+    if live:
+        gl = torch.Generator().manual_seed(7)
+        with torch.no_grad():
+            for mm in m.modules():
+                if isinstance(mm, torch.nn.LayerNorm):
+                    mm.weight.fill_(1.0)
+            for _, p in m.named_parameters():
+                if p.dim() == 1 and not torch.all(p == 1.0):
+                    p.copy_(torch.randn(p.shape, generator=gl) * 0.05)
+    before = {k: v.detach().clone().numpy() for k, v in m.state_dict().items()}
+    opt = torch.optim.AdamW(m.parameters(), lr=args.lr, betas=(0.9, 0.98), weight_decay=wd)
+    m.train()
+    pl, nl = m(seq, pos, neg, tt, ntt, nat, sf, pf, nf)
+    # loss: model/BaseLine/main.py:177-185 (O1 main.py:233-245 has no l2 term)
+    crit = torch.nn.BCEWithLogitsLoss(reduction='mean')
+    idx = np.where(ntt == 1)
+    loss = crit(pl[idx], torch.ones_like(pl)[idx]) + crit(nl[idx], torch.zeros_like(nl)[idx])
+    if l2:
+        for p in m.item_emb.parameters():
+            loss = loss + l2 * torch.norm(p)
+    opt.zero_grad()
+    loss.backward()
+    grads = {f'grad.{k}': p.grad.detach().clone().numpy() for k, p in m.named_parameters() if p.grad is not None}
+    opt.step()
+    after = {f'after.{k}': v.detach().clone().numpy() for k, v in m.state_dict().items()}
+    save(f'model_{tag}.npz', loss=loss.detach().numpy(), pos_logits=pl.detach().numpy(),
+         neg_logits=nl.detach().numpy(), weight_decay=wd, l2_emb=l2, lr=args.lr,
+         hidden_units=args.hidden_units, num_blocks=args.num_blocks, num_heads=args.num_heads,
+         maxlen=args.maxlen, norm_first=bool(getattr(args, 'norm_first', False)),
+         **{f'before.{k}': v for k, v in before.items()}, **grads, **after)
+
+
+def norm_first_golden():
+    """model_baseline_nf_live.npz, model_o1_nf_live.npz: the pre-LN blocks
+    (``--norm_first``, model/BaseLine/model.py:338-342, BaseLineO1/model.py:451),
+    same dataset batch and live init as the other model fixtures."""
+    torch.set_num_threads(1)
+    ds_mod, base_mod, o1_mod = ref_modules()
+    from tencent_recommendation_2025_amd.dataset import write_synthetic_tencentgr
+    tmp = Path(tempfile.mkdtemp(prefix='grk_golden_'))
+    write_synthetic_tencentgr(tmp, num_users=24, num_items=300, max_events=40, seed=0,
+                              sparse_card=(10, 50, 100), user_card=100)
+    args = SimpleNamespace(maxlen=20, mm_emb_id=['81'], hidden_units=32, num_blocks=2, num_heads=2,
+                           dropout_rate=0.0, norm_first=True, device='cpu', l2_emb=0.001, lr=0.001)
+    np.random.seed(0)
+    dset = ds_mod.MyDataset(tmp, args)
+    batch = ds_mod.MyDataset.collate_fn([dset[u] for u in range(8)])
+    ft = dset.feature_types
+    for tag, mod, wd, l2 in (('baseline_nf_live', base_mod, 0.01, args.l2_emb), ('o1_nf_live', o1_mod, args.l2_emb, 0.0)):
+        model_step_fixture(tag, mod, wd, l2, True, args, dset, ft, batch)
+
+
 def main():
     torch.set_num_threads(1)
     ds_mod, base_mod, o1_mod = ref_modules()
@@ -137,38 +199,7 @@ def main():
     for tag, mod, wd, l2 in (('baseline', base_mod, 0.01, args.l2_emb), ('o1', o1_mod, args.l2_emb, 0.0)):
         runs += [(tag, mod, wd, l2, False), (tag + '_live', mod, wd, l2, True)]
     for tag, mod, wd, l2, live in runs:
-        torch.manual_seed(0)
-        m = mod.BaselineModel(dset.usernum, dset.itemnum, dset.feat_statistics, ft, args)
-        ref_init(m)
-        if live:
-            gl = torch.Generator().manual_seed(7)
-            with torch.no_grad():
-                for mm in m.modules():
-                    if isinstance(mm, torch.nn.LayerNorm):
-                        mm.weight.fill_(1.0)
-                for _, p in m.named_parameters():
-                    if p.dim() == 1 and not torch.all(p == 1.0):
-                        p.copy_(torch.randn(p.shape, generator=gl) * 0.05)
-        before = {k: v.detach().clone().numpy() for k, v in m.state_dict().items()}
-        opt = torch.optim.AdamW(m.parameters(), lr=args.lr, betas=(0.9, 0.98), weight_decay=wd)
-        m.train()
-        pl, nl = m(seq, pos, neg, tt, ntt, nat, sf, pf, nf)
-        # loss: model/BaseLine/main.py:177-185 (O1 main.py:233-245 has no l2 term)
-        crit = torch.nn.BCEWithLogitsLoss(reduction='mean')
-        idx = np.where(ntt == 1)
-        loss = crit(pl[idx], torch.ones_like(pl)[idx]) + crit(nl[idx], torch.zeros_like(nl)[idx])
-        if l2:
-            for p in m.item_emb.parameters():
-                loss = loss + l2 * torch.norm(p)
-        opt.zero_grad()
-        loss.backward()
-        grads = {f'grad.{k}': p.grad.detach().clone().numpy() for k, p in m.named_parameters() if p.grad is not None}
-        opt.step()
-        after = {f'after.{k}': v.detach().clone().numpy() for k, v in m.state_dict().items()}
-        save(f'model_{tag}.npz', loss=loss.detach().numpy(), pos_logits=pl.detach().numpy(),
-             neg_logits=nl.detach().numpy(), weight_decay=wd, l2_emb=l2, lr=args.lr,
-             hidden_units=args.hidden_units, num_blocks=args.num_blocks, num_heads=args.num_heads,
-             maxlen=args.maxlen, **{f'before.{k}': v for k, v in before.items()}, **grads, **after)
+        model_step_fixture(tag, mod, wd, l2, live, args, dset, ft, batch)
 
     # ---------------- embedding ops on the reference's own modules -------------
     torch.manual_seed(1)
@@ -262,5 +293,7 @@ def retrieval_golden():
 if __name__ == '__main__':
     if sys.argv[1:] == ['retrieval']:
         retrieval_golden()
+    elif sys.argv[1:] == ['norm_first']:
+        norm_first_golden()
     else:
         main()

@@ -52,7 +52,8 @@ def build(golden, tag, block='softmax', **over):
     g = golden(f'model_{tag}.npz')
     d, batch, stats = golden_batch(golden)
     kw = dict(hidden_units=int(g['hidden_units']), maxlen=int(g['maxlen']), num_blocks=int(g['num_blocks']),
-              num_heads=int(g['num_heads']), dropout_rate=0.0, norm_first=False, device=DEV, variant=variant,
+              num_heads=int(g['num_heads']), dropout_rate=0.0,
+              norm_first=bool(g['norm_first']) if 'norm_first' in g.files else False, device=DEV, variant=variant,
               block=block)
     kw.update(over)
     args = SimpleNamespace(**kw)
@@ -79,7 +80,9 @@ DROPIN_TOL = dict(logits=1e-5, loss=1e-5, grad=1e-4)
 # instead of projected (model._direct_feats); the golden tables have 11-101 rows,
 # so 20 mixes both paths and 0 sends every feature table through the direct one
 @pytest.mark.parametrize('tag,proj', [('baseline', None), ('o1', None), ('baseline_live', None), ('o1_live', None),
-                                      ('o1_live', 20), ('baseline_live', 0)])
+                                      ('o1_live', 20), ('baseline_live', 0),
+                                      # --norm_first (pre-LN blocks, BaseLine/model.py:338-342)
+                                      ('baseline_nf_live', None), ('o1_nf_live', None)])
 def test_dropin_step_matches_reference(golden, tag, proj):
     m, g, batch, args, _, _ = build(golden, tag, **({} if proj is None else {'proj_max_rows': proj}))
     if proj is not None:
@@ -99,6 +102,7 @@ def test_dropin_step_matches_reference(golden, tag, proj):
     opt.zero_grad()
     loss.backward()
     live = tag.endswith('_live')
+    assert m.norm_first == ('_nf' in tag)
     worst = {}
     for name, p in m.named_parameters():
         want = g[f'grad.{name}']
@@ -288,6 +292,70 @@ def test_fused_trainer_matches_dropin(golden, proj):
             assert float((diff < 1e-6).float().mean()) > 0.97, k
 
 
+def test_fused_trainer_l2_emb_matches_dropin(golden):
+    """BaseLine's loss term l2_emb * ||item_emb.weight||_F (model/BaseLine/main.py:
+    184-185) in the fused trainer (FusedAdamW(l2_emb): value from grk_table_l2_norm,
+    gradient l2 * W / ||W|| added inside the item table's AdamW) against the drop-in
+    model with the term through autograd + torch AdamW: loss to 1e-5 and every
+    parameter after the step, as test_fused_trainer_matches_dropin."""
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    m1, g, batch, *_ = build(golden, 'baseline_live')
+    l2 = 0.05   # larger than the script's 1e-3 default so the term moves every row visibly
+    sd = {k[len('before.'):]: torch.from_numpy(g[k]) for k in g.files if k.startswith('before.')}
+    m1.load_state_dict(sd)
+    m2, *_ = build(golden, 'baseline_live')
+    m2.load_state_dict(sd)
+    lr, wd = 1e-3, 0.01
+    pl, nl = m1(*batch)
+    loss1 = ref_loss(pl, nl, batch[4], m1, l2)
+    opt = torch.optim.AdamW(m1.parameters(), lr=lr, betas=(0.9, 0.98), weight_decay=wd)
+    loss1.backward()
+    opt.step()
+    fo = FusedAdamW(m2, lr=lr, weight_decay=wd, table_mode='dense', table_dtype=torch.float32, l2_emb=l2)
+    tr = Trainer(m2, fo, loss='bce', amp_dtype=None)
+    loss2 = tr.step(batch)
+    assert abs(loss1.item() - loss2.item()) < 1e-5 * max(1.0, abs(loss1.item()))
+    s1, s2 = m1.state_dict(), m2.state_dict()
+    for k in s1:
+        diff = (s1[k].float() - s2[k].float()).abs()
+        assert float(diff.max()) <= 2.05 * lr, k
+        if not k.endswith('k_linear.bias'):
+            assert float((diff < 1e-6).float().mean()) > 0.97, k
+    # the term really acted: rows no lookup touched moved by more than weight decay alone
+    w0 = torch.from_numpy(g['before.item_emb.weight']).to(DEV)
+    untouched = torch.ones(w0.shape[0], dtype=torch.bool, device=DEV)
+    for t in (torch.where(batch[3] == 1, batch[0], 0), batch[1], batch[2]):
+        untouched[t.reshape(-1)] = False
+    untouched[0] = False
+    moved = (s2['item_emb.weight'] - w0)[untouched].abs()
+    assert float(moved.max()) > 0.5 * lr
+
+
+def test_fused_l2_emb_graph_replay_equals_eager():
+    """bf16 tables, l2_emb term: the HIP-graph-replayed steps equal the eager steps bitwise."""
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    cfg = S.SyntheticConfig(batch_size=8, maxlen=30, num_items=5000, num_users=700, min_len=4)
+    stats, types = S.feature_schema(cfg)
+    args = S.make_args(hidden_units=64, maxlen=30, num_blocks=2, num_heads=2, block='softmax')
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, args).to(DEV)
+        opt = FusedAdamW(m, lr=2e-3, defer_period=4, l2_emb=1e-3)
+        tr = Trainer(m, opt, loss='bce', graph=graph, graph_warmup=2)
+        g = torch.Generator(device=DEV).manual_seed(0)
+        batches = [S.make_batch(cfg, g, DEV) for _ in range(3)]
+        losses = [tr.step(batches[i % 3]).clone() for i in range(6)]
+        runs.append((torch.stack(losses), m.state_dict()))
+    assert torch.equal(runs[0][0], runs[1][0]), (runs[0][0], runs[1][0])
+    for k in runs[0][1]:
+        assert torch.equal(runs[0][1][k], runs[1][1][k]), k
+
+
 def test_fused_trainer_bf16_hstu_learns():
     from tencent_recommendation_2025_amd import synthetic as S
     from tencent_recommendation_2025_amd.model import BaselineModel
@@ -464,7 +532,7 @@ def test_graph_replayed_steps_equal_eager_steps(period, nbt):
 # LayerNorms), 1.6e-2 (user side), up to 4.4e-2 (item tables / itemdnn: their row sums
 # mix positive- and negative-logit terms of opposite sign, which amplifies the bf16
 # rounding of the per-token gradients)
-BENCH_TOL = dict(loss=2e-3, logits=2e-2, grad=7.5e-2)
+BENCH_TOL = dict(loss=1e-3, logits=1e-2, grad=7.5e-2)   # loss: the north star's 1e-3 for bf16 loss
 
 
 def test_bench_config_step_matches_oracle_fp32():

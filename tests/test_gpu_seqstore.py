@@ -24,7 +24,10 @@ def test_device_negatives_contract_and_features(tmp_path):
     seq, pos, neg, tt, ntt, nat, sf, pf, nf = dn.attach(b, uids, seed=77)
     neg_c = neg.cpu().numpy()
     hist = st.history_items(uids).numpy()
-    excl = np.concatenate([hist, pos.cpu().numpy()], 1)
+    excl = hist
+    pos_c = pos.cpu().numpy()
+    for r in range(len(uids)):   # the history holds every positive of the window
+        assert set(pos_c[r][pos_c[r] != 0].tolist()) <= set(hist[r].tolist())
     want, _, flag = osamp.sample_negatives(pos.cpu().numpy(), ntt.cpu().numpy(), excl, st.itemnum, 77,
                                            item_ok=np.asarray(st.item_ok).astype(bool))
     assert not flag and np.array_equal(neg_c, want)
@@ -63,3 +66,26 @@ def test_model_step_on_store_batches(tmp_path):
         batch = dn.attach(to_device(st.batch(uids), DEV), uids, seed=step)
         losses.append(tr.step(batch).item())
     assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
+
+
+def test_long_history_exclusion_lists():
+    """Exclusion lists longer than the LDS image (8192 entries: scanned in
+    global memory) and between 4096 and 8192 (sorted in LDS), unsorted and with
+    duplicates: negatives bit-exact vs the set-based oracle, never excluded."""
+    from tencent_recommendation_2025_amd import kernels as K
+    rng = np.random.default_rng(3)
+    B, T, N = 6, 50, 30000
+    pos = rng.integers(1, N + 1, (B, T)).astype(np.int32)
+    ntt = (rng.random((B, T)) < 0.9).astype(np.int32)
+    for L in (5000, 12000):
+        excl = rng.integers(0, N + 1, (B, L)).astype(np.int32)      # unsorted, duplicates, zeros
+        excl[:, :T] = pos                                          # positives inside the set
+        ok = rng.random(N + 1) < 0.95
+        ok[0] = False
+        neg, _ = K.sample_negatives(torch.from_numpy(pos).to(DEV), torch.from_numpy(ntt).to(DEV),
+                                    torch.from_numpy(excl).to(DEV), N, 11, item_ok=torch.from_numpy(ok).to(DEV))
+        want, _, flag = osamp.sample_negatives(pos, ntt, excl, N, 11, item_ok=ok)
+        got = neg.cpu().numpy()
+        assert not flag and np.array_equal(got, want), L
+        for b in range(B):
+            assert not (set(got[b][got[b] != 0].tolist()) & set(excl[b].tolist()))

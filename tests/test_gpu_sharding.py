@@ -134,3 +134,35 @@ def test_shards_built_directly_equal_materialized_table(pg):
     for k in ('item_emb', 'user_emb'):
         torch.testing.assert_close(opt2.shard_table(k).float(), s1[f'{k}.weight'].float(), rtol=1e-3, atol=2e-5,
                                    msg=k)
+
+
+def test_capture_stream_is_private_never_a_pool_stream(pg):
+    """Deterministic check of the r2s7 capture abort's mechanism (DESIGN.md §5b
+    item 4): a collective's end event is recorded on a torch pool stream (the
+    process group takes its streams from torch's round-robin pool, and so would
+    the Trainer if it called torch.cuda.Stream()).  Capturing the step on such a
+    stream makes the watchdog's query of that event illegal.  The Trainer must
+    capture (and warm up) on the process's own grk_stream_create stream, which is
+    none of the pool's streams however many the process has handed out."""
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer, private_stream
+    pool = [torch.cuda.Stream() for _ in range(96)]      # every stream of torch's pool, several times over
+    pool_handles = {s.cuda_stream for s in pool}
+    x = torch.ones(4, device=DEV)
+    with torch.cuda.stream(pool[0]):                     # a collective's event on a pool stream
+        dist.all_reduce(x)
+        ev = torch.cuda.Event()
+        ev.record(pool[0])
+    m, cfg = build()
+    tr = Trainer(m, FusedAdamW(m, lr=1e-3, defer_period=4), loss='bce', graph=True, graph_warmup=1)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    for _ in range(3):
+        tr.step(S.make_batch(cfg, g, DEV))
+        ev.query()                                       # the watchdog's poll: legal outside our capture
+    assert tr._g is not None
+    side = tr._side.cuda_stream
+    assert side == private_stream(torch.device(DEV)).cuda_stream
+    assert side not in pool_handles and side != torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    assert float(x[0]) == 1.0

@@ -106,6 +106,44 @@ def test_sampled_softmax_numpy_equals_torch_autograd():
     np.testing.assert_allclose(te.grad.numpy(), de, rtol=1e-9, atol=1e-12)
 
 
+def test_sampled_softmax_logq_numpy_equals_torch_and_fd():
+    """logQ correction (z_ij -= log q_j): numpy oracle == torch autograd, and the
+    oracle's gradient == finite differences of its loss."""
+    rng = np.random.default_rng(9)
+    M, D = 36, 6
+    h, e = rng.standard_normal((M, D)), rng.standard_normal((M, D))
+    ids = rng.integers(0, 10, M)
+    valid = rng.random(M) < 0.75
+    lq = np.log(rng.uniform(0.01, 0.5, M))
+    loss, dh, de = oloss.sampled_softmax(h, e, ids, valid, 0.4, log_q=lq)
+    assert abs(loss - oloss.sampled_softmax(h, e, ids, valid, 0.4)[0]) > 1e-3   # the correction acts
+    th, te = torch.from_numpy(h).requires_grad_(True), torch.from_numpy(e).requires_grad_(True)
+    tl = model_ref.sampled_softmax_loss(th, te, torch.from_numpy(ids), torch.from_numpy(valid.astype(np.int64)), 0.4,
+                                        log_q=torch.from_numpy(lq))
+    tl.backward()
+    np.testing.assert_allclose(tl.item(), loss, rtol=1e-12)
+    np.testing.assert_allclose(th.grad.numpy(), dh, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(te.grad.numpy(), de, rtol=1e-9, atol=1e-12)
+    fd_check(lambda x: oloss.sampled_softmax(x, e, ids, valid, 0.4, log_q=lq)[0], h, dh)
+    fd_check(lambda x: oloss.sampled_softmax(h, x, ids, valid, 0.4, log_q=lq)[0], e, de)
+
+
+def test_batch_log_q_is_in_batch_item_frequency():
+    from tencent_recommendation_2025_amd.functional import batch_log_q
+    rng = np.random.default_rng(1)
+    ids = rng.integers(1, 8, (4, 30))
+    ntt = (rng.random((4, 30)) < 0.6).astype(np.int64)
+    got = batch_log_q(torch.from_numpy(ids), torch.from_numpy(ntt)).numpy().reshape(4, 30)
+    v = ntt == 1
+    nv = v.sum()
+    for b in range(4):
+        for t in range(30):
+            if v[b, t]:
+                assert abs(got[b, t] - np.log(np.sum(v & (ids == ids[b, t])) / nv)) < 1e-6
+            else:
+                assert got[b, t] == 0
+
+
 def test_bce_oracle_equals_torch():
     rng = np.random.default_rng(5)
     N, D = 30, 6

@@ -129,3 +129,22 @@ def test_dedup_level_matches_oracle():
         assert np.array_equal(got, want)
         assert len({tuple(r) for r in got}) == n
     assert dedup_level(torch.zeros(0, 3, dtype=torch.int32)).shape == (0, 4)
+
+
+def test_semantic_id_schema_covers_collision_level():
+    """dedup_level's extra level can exceed the codebook size (a collision group
+    larger than K): the schema built from the codes sizes every level's table so
+    each 1-based id of semantic_id_table has a row."""
+    import torch
+    from tencent_recommendation_2025_amd.rqvae import dedup_level, semantic_id_schema, semantic_id_table
+    codes = torch.zeros(40, 2, dtype=torch.int32)      # every item shares one tuple: collision group of 40
+    codes[::2, 1] = 1
+    ext = dedup_level(codes)
+    names, stats = semantic_id_schema(ext.shape[1], 4, codes=ext)
+    assert names == ['sid0', 'sid1', 'sid2']
+    assert stats['sid0'] == 4 and stats['sid1'] == 4 and stats['sid2'] == int(ext[:, 2].max()) + 1 == 20
+    tab = semantic_id_table(ext, 40)
+    for lvl, k in enumerate(names):
+        emb = torch.nn.Embedding(stats[k] + 1, 8, padding_idx=0)   # the O1 table of that feature
+        assert int(tab[:, lvl].max()) < emb.num_embeddings
+        emb(tab[:, lvl])                                           # every id has a row

@@ -87,8 +87,10 @@ def test_oracle_exhaustion_keeps_last_draw_and_flags():
 def test_capi_rejects_bad_arguments():
     from tencent_recommendation_2025_amd import _lib as L
     h = L.lib()
-    rc = h.grk_sample_negatives(None, None, 4, 10, None, 5000, 100, 0, 10, None, 0, None, None, None, None, None)
+    rc = h.grk_sample_negatives(None, None, 4, 10, None, -1, 100, 0, 10, None, 0, None, None, None, None, None)
     assert rc == L.GRK_EINVAL and b'excl_len' in h.grk_last_error()
+    rc = h.grk_sample_negatives(None, None, 4, 10, None, 5000, 100, 0, 10, None, 0, None, None, None, None, None)
+    assert rc == L.GRK_EINVAL and b'excl is NULL' in h.grk_last_error()   # any length, but a list is required
     rc = h.grk_sample_negatives(None, None, 4, 10, None, 0, 0, 0, 10, None, 0, None, None, None, None, None)
     assert rc == L.GRK_EINVAL and b'num_items' in h.grk_last_error()
     rc = h.grk_sample_negatives(None, None, 4, 10, None, 0, 100, 0, 0, None, 0, None, None, None, None, None)
