@@ -71,6 +71,11 @@ def parse():
     ap.add_argument('--semantic-ids', type=int, default=0,
                     help='config 4: RQ-VAE semantic-id levels added as O1 item_sparse features (0 = off)')
     ap.add_argument('--sid-codes', type=int, default=256, help='config 4: codes per RQ-VAE level')
+    ap.add_argument('--jagged', type=int, default=1,
+                    help='token-wise step over each sequence\'s span only (jagged.py; padding rows are dead in the '
+                         'reference); 0 = the padded [B, T] step')
+    ap.add_argument('--jagged-quantum', type=int, default=512,
+                    help='jagged capacity granularity (rows): one GEMM plan set and one HIP graph per capacity')
     return ap.parse_args()
 
 
@@ -102,7 +107,7 @@ def _pmc(name, match):
     return p
 
 
-def attention_rooflines(a, key_valid, reps):
+def attention_rooflines(a, key_valid, reps, jagged=False):
     """The attention kernels of one layer at the bench shape and the batch's own
     ragged lengths, timed alone (HIP events on their stream).
 
@@ -123,15 +128,23 @@ def attention_rooflines(a, key_valid, reps):
     g = torch.Generator(device=dev).manual_seed(7)
     pre = torch.randn(B * T, 4 * D, device=dev, generator=g).bfloat16()    # [u | v | q | k] as HSTUAttention
     kv = key_valid.to(torch.uint8).contiguous()
+    row_base, seq_range = None, K.seq_ranges(kv)
+    if jagged:   # the rows the jagged step holds: each sequence's span only (jagged.py)
+        from tencent_recommendation_2025_amd import jagged as J
+        jag = J.layout(kv, J.capacity_for(J.span_rows(kv), a.jagged_quantum))
+        jpre = torch.empty(jag.capacity, 4 * D, dtype=torch.bfloat16, device=dev)
+        K.gather_rows([(pre, jpre)], jag.row_map)
+        pre, row_base, seq_range = jpre, jag.row_base, jag.seq_range
+    N = pre.shape[0]
     hstu = a.block == 'hstu'
     kind = L.ATTN_HSTU if hstu else L.ATTN_SOFTMAX
     extra = dict(rab=0.1 * torch.randn(H, T, device=dev, generator=g), inv_n=1.0 / T, act='silu') if hstu else {}
     args = K.attn_args(kind, pre[:, 2 * D:3 * D], pre[:, 3 * D:], pre[:, D:2 * D], B, T, H, hd, key_valid=kv,
-                       scale=hd ** -0.5, out_dtype=torch.bfloat16, seq_range=K.seq_ranges(kv), **extra)
-    o = torch.empty(B * T, D, dtype=torch.bfloat16, device=dev)
+                       scale=hd ** -0.5, out_dtype=torch.bfloat16, seq_range=seq_range, row_base=row_base, **extra)
+    o = torch.empty(N, D, dtype=torch.bfloat16, device=dev)
     lse = torch.empty(B, H, T, device=dev)
-    do = torch.randn(B * T, D, device=dev, generator=g).bfloat16()
-    dpre = torch.empty(B * T, 4 * D, dtype=torch.bfloat16, device=dev)
+    do = torch.randn(N, D, device=dev, generator=g).bfloat16()
+    dpre = torch.empty(N, 4 * D, dtype=torch.bfloat16, device=dev)
     delta = torch.empty(B, H, T, device=dev)
     drab = torch.zeros(H, T, device=dev) if hstu else None
     K.attention_fwd(args, o, lse)
@@ -148,7 +161,8 @@ def attention_rooflines(a, key_valid, reps):
     side = H * T * 4 if hstu else n_valid * H * 4            # rab row / lse (+ delta) per kernel
     ridge = BF16_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBPS * 1e9)
     name = 'hstu' if hstu else 'softmax'
-    workload = {'B': B, 'T': T, 'D': D, 'H': H, 'kind': name, 'valid_tokens': n_valid}
+    workload = {'B': B, 'T': T, 'D': D, 'H': H, 'kind': name, 'valid_tokens': n_valid,
+                'layout': 'jagged' if jagged else 'padded'}
 
     def entry(kernel, ms, nbytes, flops, pmc_name):
         gbps = nbytes / (ms * 1e-3) / 1e9
@@ -469,26 +483,43 @@ def main():
         opt = ShardedFusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
     else:
         opt = FusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
-    trainer = Trainer(model, opt, loss=a.loss, graph=bool(a.graph))
+    jagged = bool(a.jagged) and not sharded
+    trainer = Trainer(model, opt, loss=a.loss, graph=bool(a.graph), jagged=jagged, jagged_quantum=a.jagged_quantum)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [S.make_batch(cfg, gen, dev) for _ in range(max(2, a.pool))]
+    from tencent_recommendation_2025_amd import jagged as J
+    # the data loader knows its batches' lengths: the span-row counts are host
+    # metadata of the pool, computed once here (not inside the timed steps)
+    rows = [J.span_rows(b[3]) if jagged else None for b in pool]
+    caps = sorted({J.capacity_for(r, a.jagged_quantum) for r in rows}) if jagged else []
 
     from tencent_recommendation_2025_amd import kernels as K
     trace = btrace = None
+    def step(i):
+        return trainer.step(pool[i % len(pool)], next_batch=pool[(i + 1) % len(pool)], rows=rows[i % len(pool)])
+
     for i in range(a.warmup):
         if i == 0:
             G.GATHER_TRACE = []          # record the fused-gather launches of one real (eager) step
             K.BACKWARD_TRACE = []        # ... and its embedding-table gradients
-        trainer.step(pool[i % len(pool)], next_batch=pool[(i + 1) % len(pool)])
+        step(i)
         if i == 0:
             trace, G.GATHER_TRACE = G.GATHER_TRACE, None
             btrace, K.BACKWARD_TRACE = K.BACKWARD_TRACE, None
+    # jagged + graph: one captured graph per capacity of the pool, captured before the
+    # timed region (extra untimed steps on the batches of a capacity not captured yet)
+    prewarm = 0
+    if jagged and trainer.graph:
+        for i in range(len(pool)):
+            while J.capacity_for(rows[i], a.jagged_quantum) not in trainer._graphs:
+                trainer.step(pool[i], next_batch=pool[(i + 1) % len(pool)], rows=rows[i])
+                prewarm += 1
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        loss = trainer.step(pool[i % len(pool)], next_batch=pool[(i + 1) % len(pool)])
+        loss = step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -505,7 +536,7 @@ def main():
         trace, G.GATHER_TRACE = G.GATHER_TRACE, None
         btrace, K.BACKWARD_TRACE = K.BACKWARD_TRACE, None
     kv = (pool[0][3] != 0).to(torch.uint8)        # the first bench batch's key validity (token_type != 0)
-    roof, more = attention_rooflines(a, kv, a.roofline_reps)
+    roof, more = attention_rooflines(a, kv, a.roofline_reps, jagged=jagged)
     more.append(gather_roofline(trace, a.roofline_reps))
     item_table = model.item_emb.weight if model.item_emb.weight.numel() else None
     if item_table is not None:
@@ -538,7 +569,11 @@ def main():
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch, 'seq_len': a.maxlen + 1,
                        'parallelism': f'dp{world}' + ('+rowshard' if sharded else '') + ('(shard-built tables)' if shard_tables else ''),
                        'step_launch': 'hip-graph replay' if trainer.graph else 'eager',
-                       'batch_pool': len(pool)},
+                       'batch_pool': len(pool),
+                       'layout': (f'jagged (span rows only, capacity quantum {a.jagged_quantum}: '
+                                  f'{len(caps)} capacities {caps}, span rows {min(rows)}-{max(rows)} of '
+                                  f'{a.batch * (a.maxlen + 1)})') if jagged else 'padded [B, T]',
+                       'prewarm_steps': prewarm},
             'final_loss': round(final_loss, 5),
             'roofline': roof,
             'rooflines': more,

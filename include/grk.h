@@ -303,6 +303,14 @@ typedef struct grk_attn_args {
                                       the time-bias gradient is ADDED into it    */
   int64_t* drab_t_ws;              /* backward: int64 [heads, num_time_buckets]
                                       scratch (fixed-point accumulator)          */
+  /* Jagged (valid-token) layout, optional: the rows of q/k/v, out, dout, dq,
+   * dk, dv hold only each sequence's span [start_b, seq_len) (start_b =
+   * seq_range[3 b], REQUIRED with it), packed back to back: token (b, t) is row
+   * row_base[b] + t (int64 [batch]; grk_jagged_layout builds both).  Padding
+   * rows before start_b are neither read nor written.  NULL = the padded
+   * [batch * seq_len] layout.  Whole-sequence kernels (T * head_dim within
+   * their LDS budget) only: other shapes return GRK_EUNSUPPORTED. */
+  const int64_t* row_base;
 } grk_attn_args;
 
 /* 1 when grk_attention_* with precise == 2 (fp32 fidelity) runs for this
@@ -317,6 +325,30 @@ int grk_attention_fidelity_supported(int seq_len, int head_dim);
  * call per step serves every attention launch of that step (all layers, fwd
  * and bwd). */
 int grk_seq_ranges(const uint8_t* key_valid, int batch, int seq_len, int32_t* ranges, void* stream);
+
+/* Jagged (valid-token) layout of a left-padded batch (the reference runs every
+ * token-wise op over all B*T rows, model/BaseLine/model.py:331-350, 379-384;
+ * the rows before a sequence's first valid key are dead).  Writes
+ * ranges [batch, 3] (= grk_seq_ranges), row_base int64 [batch] (token (b, t) of
+ * the span [start_b, seq_len) is row row_base[b] + t), row_map int32 [capacity]
+ * (row r <- token index b * seq_len + t; -1 for the dead rows r >= n) and
+ * *num_rows = n (int64, device).  next_token_type (optional, int32 [batch,
+ * seq_len]): err_flag bit 1 if a token before its span has next_token_type == 1;
+ * bit 2 if n > capacity (rows past capacity are not mapped). */
+int grk_jagged_layout(const uint8_t* key_valid, int batch, int seq_len, int64_t capacity,
+                      const int32_t* next_token_type, int32_t* ranges, int64_t* row_base, int32_t* row_map,
+                      int64_t* num_rows, int32_t* err_flag, void* stream);
+
+/* Multi-tensor row gather for the jagged layout: for each copy,
+ * dst + r * dst_ld <- src + row_map[r] * src_ld (row_bytes bytes; zeros where
+ * row_map[r] < 0), r in [0, rows), all copies in one launch.  row_bytes,
+ * strides and pointers multiples of 4; at most 48 copies. */
+typedef struct grk_row_copy {
+  const void* src;
+  void* dst;
+  int64_t row_bytes, src_ld, dst_ld;
+} grk_row_copy;
+int grk_gather_rows(const grk_row_copy* copies, int num_copies, const int32_t* row_map, int64_t rows, void* stream);
 
 /* out [B*T, ldo] (out_dtype); lse fp32 [B, H, T] (softmax: natural-log
  * logsumexp of the masked scaled scores, -inf for fully-masked rows). */

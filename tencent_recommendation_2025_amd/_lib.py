@@ -56,7 +56,12 @@ class GrkAttnArgs(C.Structure):
                 ('dropout_p', C.c_float), ('precise', C.c_int32), ('seed', C.c_uint64), ('out_dtype', C.c_int32),
                 ('act', C.c_int32), ('seq_range', C.c_void_p), ('seed_dev', C.c_void_p), ('qkv_dtype', C.c_int32),
                 ('timestamps', C.c_void_p), ('rab_t', C.c_void_p), ('num_time_buckets', C.c_int32),
-                ('drab_t', C.c_void_p), ('drab_t_ws', C.c_void_p)]
+                ('drab_t', C.c_void_p), ('drab_t_ws', C.c_void_p), ('row_base', C.c_void_p)]
+
+
+class GrkRowCopy(C.Structure):
+    _fields_ = [('src', C.c_void_p), ('dst', C.c_void_p), ('row_bytes', C.c_int64), ('src_ld', C.c_int64),
+                ('dst_ld', C.c_int64)]
 
 
 ATTN_SOFTMAX, ATTN_HSTU = 0, 1
@@ -105,6 +110,8 @@ SIGNATURES = {
     'grk_norm_gate_bwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _P, _P, _I64, _I, _F, C.c_uint64, _P, _P, _I64, _P,
                                _I64, _P, _P, _P, _SZ, _P]),
     'grk_seq_ranges': (_I, [_P, _I, _I, _P, _P]),
+    'grk_jagged_layout': (_I, [_P, _I, _I, _I64, _P, _P, _P, _P, _P, _P, _P]),
+    'grk_gather_rows': (_I, [C.POINTER(GrkRowCopy), _I, _P, _I64, _P]),
     'grk_add_norm_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _P, _I64, _P, _I64, _I, _P, _P]),
     'grk_add_norm_bwd_workspace': (_SZ, [_I64, _I]),
     'grk_add_norm_bwd': (_I, [_P, _I64, _I, _P, _I64, _P, _I64, _P, _P, _I64, _I, _P, _I64, _P, _P, _P, _SZ, _P]),

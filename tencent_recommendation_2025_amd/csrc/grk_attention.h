@@ -27,6 +27,9 @@ struct AttnParams {
   int act;  // GRK_ACT_SILU: q/k/v are pre-activations
   int qkv_f8;  // q/k/v are OCP fp8 e4m3 (chunked kernels, head_dim 64 / 128)
   const int* seq_range;  // optional [B, 3] (first valid key, contiguous flag; longest-first order)
+  // optional jagged layout (whole-sequence kernels + delta): token (b, t) of q/k/v/out/dO/dq/dk/dv
+  // is row row_base[b] + t and only t in [seq_range[3 b], T) exist; NULL = padded rows b * T + t
+  const int64_t* row_base;
   unsigned long long* drab_fix;  // [H, nb] int64 fixed-point drab accumulator (deterministic)
   // HSTU time bias (whole-sequence kernels): S += rab_t[h, time_bucket(ts_q - ts_k)]
   const int64_t* ts;

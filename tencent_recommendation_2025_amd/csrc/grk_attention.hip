@@ -169,7 +169,15 @@ __global__ void __launch_bounds__(256) k_attn_delta(AttnParams p) {
   const int64_t total = (int64_t)p.B * p.T * p.H;
   if (wid >= total) return;
   const int h = (int)(wid % p.H);
-  const int64_t tok = wid / p.H;
+  int64_t tok = wid / p.H;
+  const int b = (int)(tok / p.T), t = (int)(tok % p.T);
+  if (p.row_base) {  // jagged rows: only [start_b, T) exist; earlier (fully masked) queries get delta 0
+    if (t < p.seq_range[3 * b]) {
+      if ((threadIdx.x & 63) == 0) const_cast<float*>(p.delta)[((int64_t)b * p.H + h) * p.T + t] = 0.f;
+      return;
+    }
+    tok = p.row_base[b] + t;
+  }
   float acc = 0.f;
   for (int d = lane; d < HD; d += 64) {
     const int64_t oo = tok * p.ldo + h * HD + d, od = tok * p.lddo + h * HD + d;
@@ -179,10 +187,7 @@ __global__ void __launch_bounds__(256) k_attn_delta(AttnParams p) {
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-  if (lane == 0) {
-    const int b = (int)(tok / p.T), t = (int)(tok % p.T);
-    const_cast<float*>(p.delta)[((int64_t)b * p.H + h) * p.T + t] = acc;
-  }
+  if (lane == 0) const_cast<float*>(p.delta)[((int64_t)b * p.H + h) * p.T + t] = acc;
 }
 
 // ================================================================ dQ =========
@@ -449,6 +454,10 @@ __global__ void k_drab_finalize(float* __restrict__ drab, const unsigned long lo
 }
 
 static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
+  if (p.qkv_f8 && p.row_base) {
+    set_error("fp8 q/k/v run the chunked kernels, which take the padded layout only (row_base must be NULL)");
+    return GRK_EUNSUPPORTED;
+  }
   if (p.qkv_f8) {  // fp8 q/k/v: the chunked kernels (C5: T = 1025), head_dim 64 / 128
     if (hd == 64) return launch_hd<64, true>(p, which, s);
     if (hd == 128) return launch_hd<128, true>(p, which, s);
@@ -458,6 +467,11 @@ static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
   if (which != 1 && attn_seq_launch(p, hd, which, s)) {
     GRK_LAUNCH_CHECK();
     return GRK_OK;
+  }
+  if (p.row_base && (which != 1 || hd > 128)) {
+    set_error("the jagged layout (row_base) runs in the whole-sequence kernels only: T = %d x head_dim %d does not "
+              "fit them", p.T, hd);
+    return GRK_EUNSUPPORTED;
   }
   if (p.nbt > 0 && which != 1) {
     set_error("the HSTU time bias runs in the whole-sequence kernels only: T = %d x head_dim %d does not fit them",
@@ -533,6 +547,8 @@ static int fill_params(const grk_attn_args* a, AttnParams* p) {
   p->act = a->act;
   p->qkv_f8 = f8;
   p->seq_range = a->seq_range;
+  GRK_CHECK_ARG(!a->row_base || a->seq_range, "the jagged layout (row_base) needs seq_range");
+  p->row_base = a->row_base;
   return GRK_OK;
 }
 

@@ -121,20 +121,24 @@ __global__ void __launch_bounds__(1024) k_seq_order(int B, int T, int* __restric
 }
 
 // KS 8-wide fragments of row `row` of a head slice (lane hh picks 8hh..8hh+7 of each 16)
+// Row addressing: token (b, t) of a head slice is row rbase + t, rbase = b * T
+// (padded [B*T] layout) or row_base[b] (jagged layout: only the rows
+// [start_b, T) of each sequence exist, packed back to back -- AttnParams).
+// Rows outside [lo, T) are never read (zero fragments) nor written.
 template <int HD>
-__device__ __forceinline__ void load_frag(bf16x8* f, const bf16_t* base, int64_t ld, int b, int T, int h, int row,
-                                          int hh) {
-  const bool ok = row < T;
-  const bf16_t* src = base + ((int64_t)b * T + (ok ? row : 0)) * ld + h * HD + 8 * hh;
+__device__ __forceinline__ void load_frag(bf16x8* f, const bf16_t* base, int64_t ld, int64_t rbase, int lo, int T,
+                                          int h, int row, int hh) {
+  const bool ok = row >= lo && row < T;
+  const bf16_t* src = base + (ok ? rbase + row : 0) * ld + h * HD + 8 * hh;
 #pragma unroll
   for (int ks = 0; ks < HD / 16; ++ks) f[ks] = gload8(src + 16 * ks, ok);
 }
 
 template <int HD>
-__device__ __forceinline__ void load_frag_any(bf16x8* f, const void* base, int64_t ld, bool f32, int b, int T, int h,
-                                              int row, int hh) {
-  const bool ok = row < T;
-  const int64_t off = ((int64_t)b * T + (ok ? row : 0)) * ld + h * HD + 8 * hh;
+__device__ __forceinline__ void load_frag_any(bf16x8* f, const void* base, int64_t ld, bool f32, int64_t rbase, int lo,
+                                              int T, int h, int row, int hh) {
+  const bool ok = row >= lo && row < T;
+  const int64_t off = (ok ? rbase + row : 0) * ld + h * HD + 8 * hh;
 #pragma unroll
   for (int ks = 0; ks < HD / 16; ++ks) f[ks] = gload8_any(base, off + 16 * ks, f32, ok);
 }
@@ -203,9 +207,9 @@ __device__ __forceinline__ void stage_time(const AttnParams& p, int b, int h, in
 // Fidelity mode: fragments of row `row` split into bf16 hi + lo (SiLU applied in fp32 first when act).
 template <int HD>
 __device__ __forceinline__ void load_frag_split(bf16x8* fh, bf16x8* fl, const void* base, int64_t ld, int dt,
-                                                bool act, int b, int T, int h, int row, int hh) {
-  const bool ok = row < T;
-  const int64_t off = ((int64_t)b * T + (ok ? row : 0)) * ld + h * HD + 8 * hh;
+                                                bool act, int64_t rbase, int lo, int T, int h, int row, int hh) {
+  const bool ok = row >= lo && row < T;
+  const int64_t off = (ok ? rbase + row : 0) * ld + h * HD + 8 * hh;
 #pragma unroll
   for (int ks = 0; ks < HD / 16; ++ks) {
     float f[8];
@@ -221,7 +225,7 @@ __device__ __forceinline__ void load_frag_split(bf16x8* fh, bf16x8* fl, const vo
 template <int HD>
 __device__ __forceinline__ void stage_pair_split(char* h0, char* l0, const void* src0, int64_t ld0, int dt0, bool act0,
                                                  char* h1, char* l1, const void* src1, int64_t ld1, int dt1,
-                                                 bool act1, int b, int T, int h, int r0, int Tp) {
+                                                 bool act1, int64_t rbase, int lo, int T, int h, int r0, int Tp) {
   constexpr int NCH = HD / 8, BATCH = 4;
   const int nvec = (Tp - r0) * NCH;
   for (int base = threadIdx.x; base < nvec; base += BATCH * blockDim.x) {
@@ -230,8 +234,8 @@ __device__ __forceinline__ void stage_pair_split(char* h0, char* l0, const void*
     for (int k = 0; k < BATCH; ++k) {
       const int u = base + k * blockDim.x;
       const int t = r0 + u / NCH, c = u % NCH;
-      const bool ok = u < nvec && t < T;
-      const int64_t row = (int64_t)b * T + (ok ? t : 0);
+      const bool ok = u < nvec && t < T && t >= lo;
+      const int64_t row = ok ? rbase + t : 0;
       gload8f(src0, row * ld0 + h * HD + c * 8, dt0, ok, v0[k]);
       gload8f(src1, row * ld1 + h * HD + c * 8, dt1, ok, v1[k]);
     }
@@ -265,7 +269,7 @@ __device__ __forceinline__ void stage_pair_split(char* h0, char* l0, const void*
 template <int HD>
 __device__ __forceinline__ void stage_pair(char* img0, const void* src0, int64_t ld0, bool f32_0, bool act0,
                                            char* img1, const void* src1, int64_t ld1, bool f32_1, bool act1,
-                                           int b, int T, int h, int r0, int Tp) {
+                                           int64_t rbase, int lo, int T, int h, int r0, int Tp) {
   constexpr int NCH = HD / 8, BATCH = 8;
   const int nvec = (Tp - r0) * NCH;
   for (int base = threadIdx.x; base < nvec; base += BATCH * blockDim.x) {
@@ -274,8 +278,8 @@ __device__ __forceinline__ void stage_pair(char* img0, const void* src0, int64_t
     for (int k = 0; k < BATCH; ++k) {
       const int u = base + k * blockDim.x;
       const int t = r0 + u / NCH, c = u % NCH;
-      const bool ok = u < nvec && t < T;
-      const int64_t row = (int64_t)b * T + (ok ? t : 0);
+      const bool ok = u < nvec && t < T && t >= lo;
+      const int64_t row = ok ? rbase + t : 0;
       v0[k] = gload8_any(src0, row * ld0 + h * HD + c * 8, f32_0, ok);
       v1[k] = gload8_any(src1, row * ld1 + h * HD + c * 8, f32_1, ok);
     }
@@ -390,17 +394,19 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
   const SeqInfo si = seq_info(p, b, T, L.sh);
   const int start = si.start, first = start / 32, kbeg = first * 32;
   const int ntiles = nq - first, npairs = (ntiles + 1) / 2;
+  const int64_t rbase = p.row_base ? p.row_base[b] : (int64_t)b * T;
+  const int lo = p.row_base ? start : 0;  // jagged rows: only [start, T) exist
   GRK_STAMP(1);
   // prologue: every independent load in flight before the first wait
   bf16x8 qpre[KS];
-  if (PREC < 2 && wave < npairs) load_frag<HD>(qpre, p.q, p.ldq, b, T, h, (first + wave) * 32 + r, hh);
+  if (PREC < 2 && wave < npairs) load_frag<HD>(qpre, p.q, p.ldq, rbase, lo, T, h, (first + wave) * 32 + r, hh);
   RabRegs rr;
   if (KIND == 1) rr = load_rab(p, h, Tp);
   if constexpr (PREC == 2)
     stage_pair_split<HD>(L.img0, L.img0lo, p.k, p.ldk, p.in_dt, p.act, L.img1, L.img1lo, p.v, p.ldv, p.in_dt, p.act,
-                         b, T, h, kbeg, Tp);
+                         rbase, lo, T, h, kbeg, Tp);
   else
-    stage_pair<HD>(L.img0, p.k, p.ldk, false, p.act, L.img1, p.v, p.ldv, false, p.act, b, T, h, kbeg, Tp);
+    stage_pair<HD>(L.img0, p.k, p.ldk, false, p.act, L.img1, p.v, p.ldv, false, p.act, rbase, lo, T, h, kbeg, Tp);
   if (KIND == 1) {
     store_rab(L.f0, rr, Tp);
     stage_key_bias(L.f1, p.key_valid, si, b, T, Tp);
@@ -424,7 +430,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) z[dt] = f32x16{};
     if (KIND == 0 && hh == 0 && myq < T && p.lse) p.lse[(int64_t)bh * T + myq] = -INFINITY;
-    store_rows<HD, NDT>(p.out, p.ldo, p.out_f32, (int64_t)b * T + myq, h, hh, z, 0.f, myq < T);
+    store_rows<HD, NDT>(p.out, p.ldo, p.out_f32, rbase + myq, h, hh, z, 0.f, myq < T && myq >= lo);
   }
 
   for (int pu = wave; pu < npairs; pu += kSeqWaves)
@@ -435,13 +441,13 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
       const bool qok = myq < T;
       bf16x8 qf[KS], ql[KS];
       if constexpr (PREC == 2) {
-        load_frag_split<HD>(qf, ql, p.q, p.ldq, p.in_dt, p.act, b, T, h, myq, hh);
+        load_frag_split<HD>(qf, ql, p.q, p.ldq, p.in_dt, p.act, rbase, lo, T, h, myq, hh);
       } else {
         if (pu == wave && ps == 0) {
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) qf[ks] = qpre[ks];
         } else {
-          load_frag<HD>(qf, p.q, p.ldq, b, T, h, myq, hh);
+          load_frag<HD>(qf, p.q, p.ldq, rbase, lo, T, h, myq, hh);
         }
         act_frag<HD>(qf, p.act);
       }
@@ -530,7 +536,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
         mul = l > 0.f ? 1.0f / l : 0.f;
         if (hh == 0 && qok && p.lse) p.lse[(int64_t)bh * T + myq] = l > 0.f ? (m + log2f(l)) * kLn2 : -INFINITY;
       }
-      store_rows<HD, NDT>(p.out, p.ldo, p.out_f32, (int64_t)b * T + myq, h, hh, o, mul, qok);
+      store_rows<HD, NDT>(p.out, p.ldo, p.out_f32, rbase + myq, h, hh, o, mul, qok && myq >= lo);
       GRK_STAMP(4 + ps);
     }
   GRK_STAMP(6);
@@ -552,19 +558,21 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
   const int start = si.start, first = start / 32, kbeg = first * 32;
   const int ntiles = nq - first, npairs = (ntiles + 1) / 2;
   const int bh = b * p.H + h;
+  const int64_t rbase = p.row_base ? p.row_base[b] : (int64_t)b * T;
+  const int lo = p.row_base ? start : 0;  // jagged rows: only [start, T) exist
   bf16x8 qpre[KS], dpre[KS];
   if (PREC < 2 && wave < npairs) {
     const int row = (first + wave) * 32 + r;
-    load_frag<HD>(qpre, p.q, p.ldq, b, T, h, row, hh);
-    load_frag_any<HD>(dpre, p.dout, p.lddo, p.dout_f32, b, T, h, row, hh);
+    load_frag<HD>(qpre, p.q, p.ldq, rbase, lo, T, h, row, hh);
+    load_frag_any<HD>(dpre, p.dout, p.lddo, p.dout_f32, rbase, lo, T, h, row, hh);
   }
   RabRegs rr;
   if (KIND == 1) rr = load_rab(p, h, Tp);
   if constexpr (PREC == 2)
     stage_pair_split<HD>(L.img0, L.img0lo, p.k, p.ldk, p.in_dt, p.act, L.img1, L.img1lo, p.v, p.ldv, p.in_dt, p.act,
-                         b, T, h, kbeg, Tp);
+                         rbase, lo, T, h, kbeg, Tp);
   else
-    stage_pair<HD>(L.img0, p.k, p.ldk, false, p.act, L.img1, p.v, p.ldv, false, p.act, b, T, h, kbeg, Tp);
+    stage_pair<HD>(L.img0, p.k, p.ldk, false, p.act, L.img1, p.v, p.ldv, false, p.act, rbase, lo, T, h, kbeg, Tp);
   if (KIND == 1) {
     store_rab(L.f0, rr, Tp);
     for (int j = threadIdx.x; j < Tp + kRabPad; j += blockDim.x) bins[j] = 0ull;
@@ -584,7 +592,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
     f32x16 z[NDT];
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) z[dt] = f32x16{};
-    store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, (int64_t)b * T + myq, h, hh, z, 0.f, myq < T);
+    store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, rbase + myq, h, hh, z, 0.f, myq < T && myq >= lo);
   }
 
   for (int pu = wave; pu < npairs; pu += kSeqWaves)
@@ -595,8 +603,8 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
       const bool qok = myq < T;
       bf16x8 qf[KS], dof[KS], ql[KS], dol[KS];
       if constexpr (PREC == 2) {
-        load_frag_split<HD>(qf, ql, p.q, p.ldq, p.in_dt, p.act, b, T, h, myq, hh);
-        load_frag_split<HD>(dof, dol, p.dout, p.lddo, p.dout_f32 ? 0 : 1, false, b, T, h, myq, hh);
+        load_frag_split<HD>(qf, ql, p.q, p.ldq, p.in_dt, p.act, rbase, lo, T, h, myq, hh);
+        load_frag_split<HD>(dof, dol, p.dout, p.lddo, p.dout_f32 ? 0 : 1, false, rbase, lo, T, h, myq, hh);
       } else {
         if (pu == wave && ps == 0) {
 #pragma unroll
@@ -605,8 +613,8 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
             dof[ks] = dpre[ks];
           }
         } else {
-          load_frag<HD>(qf, p.q, p.ldq, b, T, h, myq, hh);
-          load_frag_any<HD>(dof, p.dout, p.lddo, p.dout_f32, b, T, h, myq, hh);
+          load_frag<HD>(qf, p.q, p.ldq, rbase, lo, T, h, myq, hh);
+          load_frag_any<HD>(dof, p.dout, p.lddo, p.dout_f32, rbase, lo, T, h, myq, hh);
         }
         act_frag<HD>(qf, p.act);
       }
@@ -708,7 +716,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
           }
         }
       }
-      store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, (int64_t)b * T + myq, h, hh, acc, p.scale, qok,
+      store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, rbase + myq, h, hh, acc, p.scale, qok && myq >= lo,
                           p.act ? p.q : nullptr, p.ldq, p.in_dt);
     }
   if (KIND == 1 && (p.drab || p.drab_t)) {
@@ -740,12 +748,14 @@ k_attn_dkdv_seq(AttnParams p) {
   const int start = si.start, first = start / 32, kbeg = first * 32;
   const int ntiles = nq - first, npairs = (ntiles + 1) / 2;
   const int bh = b * p.H + h;
+  const int64_t rbase = p.row_base ? p.row_base[b] : (int64_t)b * T;
+  const int lo = p.row_base ? start : 0;  // jagged rows: only [start, T) exist
   // key tile j (absolute first + j) visits query tiles j .. ntiles-1
   bf16x8 kpre[KS], vpre[KS];
   if (PREC < 2 && wave < npairs) {
     const int row = (first + wave) * 32 + r;
-    load_frag<HD>(kpre, p.k, p.ldk, b, T, h, row, hh);
-    load_frag<HD>(vpre, p.v, p.ldv, b, T, h, row, hh);
+    load_frag<HD>(kpre, p.k, p.ldk, rbase, lo, T, h, row, hh);
+    load_frag<HD>(vpre, p.v, p.ldv, rbase, lo, T, h, row, hh);
   }
   RabRegs rr;
   float lv[2], dl[2];
@@ -768,9 +778,9 @@ k_attn_dkdv_seq(AttnParams p) {
   }
   if constexpr (PREC == 2)
     stage_pair_split<HD>(L.img0, L.img0lo, p.q, p.ldq, p.in_dt, p.act, L.img1, L.img1lo, p.dout, p.lddo,
-                         p.dout_f32 ? 0 : 1, false, b, T, h, kbeg, Tp);
+                         p.dout_f32 ? 0 : 1, false, rbase, lo, T, h, kbeg, Tp);
   else
-    stage_pair<HD>(L.img0, p.q, p.ldq, false, p.act, L.img1, p.dout, p.lddo, p.dout_f32, false, b, T, h, kbeg, Tp);
+    stage_pair<HD>(L.img0, p.q, p.ldq, false, p.act, L.img1, p.dout, p.lddo, p.dout_f32, false, rbase, lo, T, h, kbeg, Tp);
   if (KIND == 1) {
     store_rab(L.f0, rr, Tp);
     if (p.nbt) stage_time(p, b, h, T, Tp, start, L.tss, L.rtab, nullptr);
@@ -797,8 +807,8 @@ k_attn_dkdv_seq(AttnParams p) {
     f32x16 z[NDT];
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) z[dt] = f32x16{};
-    store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, (int64_t)b * T + myk, h, hh, z, 0.f, myk < T);
-    store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, (int64_t)b * T + myk, h, hh, z, 0.f, myk < T);
+    store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, rbase + myk, h, hh, z, 0.f, myk < T && myk >= lo);
+    store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, rbase + myk, h, hh, z, 0.f, myk < T && myk >= lo);
   }
 
   for (int pu = wave; pu < npairs; pu += kSeqWaves)
@@ -810,8 +820,8 @@ k_attn_dkdv_seq(AttnParams p) {
       const bool kok = kin && myk >= start && (si.contig || L.kvs[myk]);
       bf16x8 kf[KS], vf[KS], kl[KS], vl[KS];
       if constexpr (PREC == 2) {
-        load_frag_split<HD>(kf, kl, p.k, p.ldk, p.in_dt, p.act, b, T, h, myk, hh);
-        load_frag_split<HD>(vf, vl, p.v, p.ldv, p.in_dt, p.act, b, T, h, myk, hh);
+        load_frag_split<HD>(kf, kl, p.k, p.ldk, p.in_dt, p.act, rbase, lo, T, h, myk, hh);
+        load_frag_split<HD>(vf, vl, p.v, p.ldv, p.in_dt, p.act, rbase, lo, T, h, myk, hh);
       } else {
         if (pu == wave && ps == 0) {
 #pragma unroll
@@ -820,8 +830,8 @@ k_attn_dkdv_seq(AttnParams p) {
             vf[ks] = vpre[ks];
           }
         } else {
-          load_frag<HD>(kf, p.k, p.ldk, b, T, h, myk, hh);
-          load_frag<HD>(vf, p.v, p.ldv, b, T, h, myk, hh);
+          load_frag<HD>(kf, p.k, p.ldk, rbase, lo, T, h, myk, hh);
+          load_frag<HD>(vf, p.v, p.ldv, rbase, lo, T, h, myk, hh);
         }
         act_frag<HD>(kf, p.act);
         act_frag<HD>(vf, p.act);
@@ -939,10 +949,11 @@ k_attn_dkdv_seq(AttnParams p) {
         half(std::integral_constant<bool, KIND == 0>{}, 0);
         half(std::integral_constant<bool, KIND == 0>{}, 1);
       }
-      const int64_t otok = (int64_t)b * T + myk;
-      store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, otok, h, hh, dk, kok ? p.scale : 0.f, kin, p.act ? p.k : nullptr,
+      const int64_t otok = rbase + myk;
+      const bool kst = kin && myk >= lo;
+      store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, otok, h, hh, dk, kok ? p.scale : 0.f, kst, p.act ? p.k : nullptr,
                           p.ldk, p.in_dt);
-      store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, kok ? 1.f : 0.f, kin, p.act ? p.v : nullptr, p.ldv,
+      store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, kok ? 1.f : 0.f, kst, p.act ? p.v : nullptr, p.ldv,
                           p.in_dt);
     }
 }

@@ -1,0 +1,144 @@
+// Jagged (valid-token) layout of a training batch.
+//
+// The reference left-pads every sequence to T = maxlen + 1 and runs every
+// token-wise op over all B*T rows (model/BaseLine/model.py:331-350,379-384);
+// rows before a sequence's first valid token are dead: they are no key of any
+// query (key padding mask), their logits are masked (next_token_type != 1), so
+// nothing reaches the loss from them and their gradients are exact zeros.  At
+// BASELINE config 2 they are ~47 % of the rows.  The fused trainer therefore
+// runs the token-wise part of the step over each sequence's span
+// [start_b, T) only, packed back to back:
+//
+//   row_map[r]  = b * T + t  for the r-th span token (b ascending, t ascending),
+//                 -1 for the dead capacity rows r in [n, cap);
+//   row_base[b] = (rows of the spans before b) - start_b, so token (b, t) is
+//                 row row_base[b] + t (the attention kernels' jagged addressing);
+//   seq_range   = grk_seq_ranges' [B, 3] (start, contiguous flag, longest-first).
+//
+// grk_gather_rows then copies the batch's per-token tensors (ids, features,
+// token types) into that order in one launch.  Integer / byte work of a few MB:
+// launch-bound.
+#include "grk_common.h"
+
+namespace grk {
+namespace {
+
+// exclusive scan of the spans (T - start_b) over b -> row_base, total -> *n_rows;
+// one workgroup, chunks of 1024 sequences
+__global__ void __launch_bounds__(1024) k_jagged_base(const int32_t* __restrict__ ranges, int B, int T,
+                                                      int64_t* __restrict__ row_base, int64_t* __restrict__ n_rows) {
+  __shared__ int64_t part[1024];
+  int64_t carry = 0;
+  for (int b0 = 0; b0 < B; b0 += 1024) {
+    const int b = b0 + (int)threadIdx.x;
+    const int st = b < B ? min(max(ranges[3 * b], 0), T) : T;
+    const int64_t span = b < B ? (int64_t)(T - st) : 0;
+    part[threadIdx.x] = span;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
+      const int64_t v = (int)threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+    }
+    if (b < B) row_base[b] = carry + part[threadIdx.x] - span - st;
+    carry += part[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *n_rows = carry;
+}
+
+// row_map over max(B*T, cap) indices: span tokens at their rows, -1 past n.
+// err bit 1: a token before its sequence's span has next_token_type == 1 (its
+// logit would be dropped); bit 2: the spans hold more rows than cap.
+__global__ void __launch_bounds__(256) k_jagged_map(const int32_t* __restrict__ ranges, const int64_t* __restrict__ row_base,
+                                                    const int64_t* __restrict__ n_rows, int B, int T, int64_t cap,
+                                                    const int32_t* __restrict__ ntt, int32_t* __restrict__ row_map,
+                                                    int32_t* __restrict__ err) {
+  const int64_t total = (int64_t)B * T > cap ? (int64_t)B * T : cap;
+  const int64_t n = *n_rows;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < (int64_t)B * T) {
+      const int b = (int)(i / T), t = (int)(i % T);
+      const int st = min(max(ranges[3 * b], 0), T);
+      if (t >= st) {
+        const int64_t r = row_base[b] + t;
+        if (r < cap) row_map[r] = (int32_t)i;
+        else if (err) atomicOr(err, 2);
+      } else if (ntt && err && ntt[i] == 1) {
+        atomicOr(err, 1);
+      }
+    }
+    if (i >= n && i < cap) row_map[i] = -1;
+  }
+}
+
+constexpr int kMaxRowCopies = 48;
+struct RowCopies {
+  grk_row_copy c[kMaxRowCopies];
+};
+
+// dst row r <- src row row_map[r] (zeros for -1), every copy at once: 4-byte
+// words, blockIdx.y = copy
+__global__ void __launch_bounds__(256) k_gather_rows(RowCopies rc, const int32_t* __restrict__ row_map, int64_t rows) {
+  const grk_row_copy& c = rc.c[blockIdx.y];
+  const int64_t wpr = c.row_bytes / 4;
+  const int64_t words = rows * wpr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / wpr, w = i - r * wpr;
+    const int32_t src_row = row_map[r];
+    const uint32_t v = src_row >= 0 ? reinterpret_cast<const uint32_t*>((const char*)c.src + src_row * c.src_ld)[w] : 0u;
+    reinterpret_cast<uint32_t*>((char*)c.dst + r * c.dst_ld)[w] = v;
+  }
+}
+
+}  // namespace
+}  // namespace grk
+
+using namespace grk;
+
+extern "C" int grk_jagged_layout(const uint8_t* key_valid, int batch, int seq_len, int64_t capacity,
+                                 const int32_t* next_token_type, int32_t* ranges, int64_t* row_base, int32_t* row_map,
+                                 int64_t* num_rows, int32_t* err_flag, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(batch > 0 && seq_len > 0 && capacity > 0, "batch, seq_len and capacity must be > 0");
+  GRK_CHECK_ARG(capacity < ((int64_t)1 << 31) && (int64_t)batch * seq_len < ((int64_t)1 << 31),
+                "rows must fit int32");
+  GRK_CHECK_ARG(key_valid && ranges && row_base && row_map && num_rows, "key_valid, ranges, row_base, row_map, num_rows required");
+  hipStream_t s = (hipStream_t)stream;
+  const int rc = grk_seq_ranges(key_valid, batch, seq_len, ranges, stream);
+  if (rc) return rc;
+  k_jagged_base<<<1, 1024, 0, s>>>(ranges, batch, seq_len, row_base, num_rows);
+  GRK_LAUNCH_CHECK();
+  const int64_t total = (int64_t)batch * seq_len > capacity ? (int64_t)batch * seq_len : capacity;
+  k_jagged_map<<<grid_for(total, 256), 256, 0, s>>>(ranges, row_base, num_rows, batch, seq_len, capacity,
+                                                    next_token_type, row_map, err_flag);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+extern "C" int grk_gather_rows(const grk_row_copy* copies, int num_copies, const int32_t* row_map, int64_t rows,
+                               void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(num_copies >= 0 && num_copies <= kMaxRowCopies, "num_copies must be in [0, %d]", kMaxRowCopies);
+  GRK_CHECK_ARG(rows >= 0, "rows must be >= 0");
+  if (num_copies == 0 || rows == 0) return GRK_OK;
+  GRK_CHECK_ARG(copies && row_map, "copies and row_map required");
+  RowCopies rc;
+  memset(&rc, 0, sizeof(rc));
+  int64_t maxw = 0;
+  for (int i = 0; i < num_copies; ++i) {
+    const grk_row_copy& c = copies[i];
+    GRK_CHECK_ARG(c.src && c.dst, "copy %d: src / dst required", i);
+    GRK_CHECK_ARG(c.row_bytes > 0 && c.row_bytes % 4 == 0 && c.src_ld >= c.row_bytes && c.dst_ld >= c.row_bytes &&
+                      c.src_ld % 4 == 0 && c.dst_ld % 4 == 0,
+                  "copy %d: row_bytes must be a positive multiple of 4, strides >= row_bytes and multiples of 4", i);
+    GRK_CHECK_ARG(((uintptr_t)c.src | (uintptr_t)c.dst) % 4 == 0, "copy %d: 4-byte aligned buffers required", i);
+    rc.c[i] = c;
+    maxw = c.row_bytes / 4 > maxw ? c.row_bytes / 4 : maxw;
+  }
+  const dim3 grid((unsigned)grid_for(rows * maxw, 256, 1024), (unsigned)num_copies);
+  k_gather_rows<<<grid, 256, 0, (hipStream_t)stream>>>(rc, row_map, rows);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}

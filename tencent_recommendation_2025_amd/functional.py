@@ -305,7 +305,7 @@ def _seed(seed):
     return seed if isinstance(seed, torch.Tensor) else int(seed)
 
 
-def softmax_mha(qkv, key_valid, B, T, H, hd, dropout_p=0.0, seed=0, precise=True, seq_range=None):
+def softmax_mha(qkv, key_valid, B, T, H, hd, dropout_p=0.0, seed=0, precise=True, seq_range=None, row_base=None):
     """Causal + key-padding softmax attention on a packed [B*T, 3D] (q|k|v) tensor
     (custom op grk::softmax_attention; returns qkv's dtype).  fp32 / fp16 inputs
     run the fp32-fidelity kernels where the shape allows (ops.py); bf16 inputs
@@ -315,12 +315,12 @@ def softmax_mha(qkv, key_valid, B, T, H, hd, dropout_p=0.0, seed=0, precise=True
         key_valid = torch.ones(B, T, dtype=torch.uint8, device=qkv.device)
     sd = seed if isinstance(seed, torch.Tensor) else None
     out, _ = torch.ops.grk.softmax_attention(qkv, key_valid, H, hd, float(dropout_p), 0 if sd is not None else int(seed),
-                                             sd, int(precise), seq_range)
+                                             sd, int(precise), seq_range, row_base)
     return out if out.dtype == qkv.dtype else out.to(qkv.dtype)
 
 
 def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, precise=True, dropout_p=0.0, seed=0,
-              seq_range=None, timestamps=None, rab_t=None):
+              seq_range=None, timestamps=None, rab_t=None, row_base=None):
     """Fused HSTU layer core on the [B*T, 4D] (u|v|q|k) pre-activation (custom op
     grk::hstu_core, ops.py): three kernels forward (attention with SiLU on load,
     LayerNorm * SiLU(u) gate with dropout), two backward; no eager glue.
@@ -335,7 +335,7 @@ def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, pre
     sd = seed if isinstance(seed, torch.Tensor) else None
     y, _, _ = torch.ops.grk.hstu_core(pre, rab, ln_w, ln_b, key_valid, H, hd, float(inv_n), float(eps), int(precise),
                                       float(dropout_p), 0 if sd is not None else int(seed), sd, seq_range,
-                                      timestamps, rab_t)
+                                      timestamps, rab_t, row_base)
     return y if pre.dtype == torch.bfloat16 else y.to(pre.dtype)
 
 

@@ -328,7 +328,8 @@ def _seed_parts(seed):
 
 
 def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, inv_n=1.0, dropout_p=0.0, seed=0,
-              precise=True, out_dtype=torch.bfloat16, act=None, seq_range=None, timestamps=None, rab_t=None):
+              precise=True, out_dtype=torch.bfloat16, act=None, seq_range=None, timestamps=None, rab_t=None,
+              row_base=None):
     """Build grk_attn_args for bf16 [B*T, ld] column views q/k/v (head h at cols h*hd).
 
     act="silu": q/k/v are pre-activations; SiLU is applied on load and the
@@ -341,6 +342,9 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
     fp32 / fp16 / bf16 and are read exactly -- fidelity_supported(T, hd)).
     timestamps (int64 [B, T]) + rab_t (fp32 [H, nbt], nbt <= 64): the HSTU time
     bias rab_t[h, time_bucket(t_q - t_k)] (include/grk.h, grk_attn_args).
+    row_base (int64 [B], with seq_range; jagged_layout): the jagged layout -- q/k/v
+    (and every output / gradient) hold only each sequence's span [start_b, T),
+    token (b, t) at row row_base[b] + t; key_valid / timestamps stay [B, T].
     float8_e4m3fn q/k/v (precise 0 / 1, act None; head_dim 64 / 128): the fp8
     attention of config C5 -- QK^T on the fp8 MFMA, the rest on bf16 MFMA over
     the exactly widened values."""
@@ -354,8 +358,11 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
         dts = (torch.float8_e4m3fn,) if f8 else (torch.bfloat16,)
     for t, n in ((q, 'q'), (k, 'k'), (v, 'v')):
         _col_view_ok(t, n, dts)
-        if t.shape[0] != B * T or t.shape[1] < H * hd:
+        if (row_base is None and t.shape[0] != B * T) or t.shape[1] < H * hd:
             raise L.GrkError(f'{n}: shape {tuple(t.shape)} does not fit B*T={B * T}, H*hd={H * hd}')
+    if row_base is not None:
+        if seq_range is None or row_base.dtype != torch.int64 or row_base.shape != (B,) or not row_base.is_contiguous():
+            raise L.GrkError('row_base must be a contiguous int64 [B] tensor, with seq_range (jagged_layout)')
     if not q.dtype == k.dtype == v.dtype:
         raise L.GrkError('q, k and v must share a dtype')
     if f8 and act is not None:
@@ -388,8 +395,8 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
                          precise, seed, L.dtype_code(out_dtype),
                          {None: L.ACT_NONE, 'silu': L.ACT_SILU}[act], _ptr(seq_range), _ptr(seed_dev),
                          L.GRK_FP8_E4M3 if f8 else L.dtype_code(q.dtype), _ptr(timestamps), _ptr(rab_t), nbt, None,
-                         None)
-    args._keep = (q, k, v, key_valid, rab, seq_range, seed_dev, timestamps, rab_t)  # raw pointers: keep alive
+                         None, _ptr(row_base))
+    args._keep = (q, k, v, key_valid, rab, seq_range, seed_dev, timestamps, rab_t, row_base)  # raw pointers: keep alive
     return args
 
 
@@ -410,6 +417,55 @@ def seq_ranges(key_valid):
                                 L.stream_ptr(key_valid.device))
     L.check(rc, 'grk_seq_ranges')
     return out
+
+
+def jagged_layout(key_valid, capacity, next_token_type=None, err_flag=None):
+    """The jagged (valid-token) layout of a left-padded batch (grk_jagged_layout):
+    (seq_range int32 [B, 3], row_base int64 [B], row_map int32 [capacity], n int64 [1])
+    -- device tensors, no host sync.  Row r of the layout holds token row_map[r]
+    (= b * T + t, t in the span [start_b, T)), -1 past the n span rows."""
+    _require_cuda(key_valid, next_token_type, err_flag)
+    if key_valid.dtype != torch.uint8 or key_valid.dim() != 2 or not key_valid.is_contiguous():
+        raise L.GrkError('key_valid must be a contiguous uint8 [B, T] tensor')
+    B, T = key_valid.shape
+    dev = key_valid.device
+    ranges = torch.empty(B, 3, dtype=torch.int32, device=dev)
+    row_base = torch.empty(B, dtype=torch.int64, device=dev)
+    row_map = torch.empty(int(capacity), dtype=torch.int32, device=dev)
+    n = torch.empty(1, dtype=torch.int64, device=dev)
+    ntt = None if next_token_type is None else next_token_type.to(torch.int32).contiguous()
+    rc = L.lib().grk_jagged_layout(key_valid.data_ptr(), B, T, int(capacity), _ptr(ntt), ranges.data_ptr(),
+                                   row_base.data_ptr(), row_map.data_ptr(), n.data_ptr(), _ptr(err_flag),
+                                   L.stream_ptr(dev))
+    L.check(rc, 'grk_jagged_layout')
+    return ranges, row_base, row_map, n
+
+
+def gather_rows(pairs, row_map):
+    """dst[r] = src[row_map[r]] (zeros where row_map[r] < 0) for every (src, dst) pair
+    in ONE launch (grk_gather_rows): src [N, ...] and dst [rows, ...] of one dtype with
+    contiguous rows of the same width (any trailing shape)."""
+    if not pairs:
+        return
+    rows = row_map.numel()
+    _require_cuda(row_map, *[t for pr in pairs for t in pr])
+    if row_map.dtype != torch.int32 or not row_map.is_contiguous():
+        raise L.GrkError('row_map must be a contiguous int32 tensor')
+    for i in range(0, len(pairs), 48):
+        chunk = pairs[i:i + 48]
+        cps = (L.GrkRowCopy * len(chunk))()
+        for j, (src, dst) in enumerate(chunk):
+            if src.dtype != dst.dtype or dst.shape[0] != rows or src.shape[1:] != dst.shape[1:]:
+                raise L.GrkError(f'gather_rows pair {i + j}: src {tuple(src.shape)} {src.dtype} vs dst '
+                                 f'{tuple(dst.shape)} {dst.dtype} ({rows} rows)')
+            if not (src.is_contiguous() and dst.is_contiguous()):
+                raise L.GrkError(f'gather_rows pair {i + j}: tensors must be contiguous')
+            rb = src[0].numel() * src.element_size() if src.dim() > 1 else src.element_size()
+            if rb % 4:
+                raise L.GrkError(f'gather_rows pair {i + j}: a row of {rb} bytes (multiple of 4 required)')
+            cps[j] = L.GrkRowCopy(src.data_ptr(), dst.data_ptr(), rb, rb, rb)
+        L.check(L.lib().grk_gather_rows(cps, len(chunk), row_map.data_ptr(), rows, L.stream_ptr(row_map.device)),
+                'grk_gather_rows')
 
 
 def attention_fwd(args, out, lse=None):

@@ -56,10 +56,15 @@ class FlashMultiHeadAttention(torch.nn.Module):
         self.v_linear = torch.nn.Linear(hidden_units, hidden_units)
         self.out_linear = torch.nn.Linear(hidden_units, hidden_units)
 
-    def forward(self, query, key, value, attn_mask=None, key_valid=None, seq_range=None):
+    def forward(self, query, key, value, attn_mask=None, key_valid=None, seq_range=None, row_base=None):
+        """row_base (with key_valid [B, T] and seq_range): query / key / value hold the
+        jagged rows of the batch (jagged.py) as [1, rows, D]."""
         B, T, D = query.shape
-        if key_valid is None:
+        if row_base is not None:
+            B, T = key_valid.shape
+        elif key_valid is None:
             key_valid = key_valid_from_mask(attn_mask, B, T)
+        N = query.shape[0] * query.shape[1]
         if query is key and key is value:
             w = torch.cat([self.q_linear.weight, self.k_linear.weight, self.v_linear.weight], 0)
             b = torch.cat([self.q_linear.bias, self.k_linear.bias, self.v_linear.bias], 0)
@@ -68,9 +73,9 @@ class FlashMultiHeadAttention(torch.nn.Module):
             qkv = torch.cat([self.q_linear(query), self.k_linear(key), self.v_linear(value)], -1)
         p = self.dropout_rate if self.training else 0.0
         seed = dropout_seed(qkv.device) if p > 0 else 0
-        o = G.softmax_mha(qkv.reshape(B * T, 3 * D), key_valid, B, T, self.num_heads, self.head_dim, p, seed,
-                          seq_range=seq_range)
-        return _linear(o.view(B, T, D), self.out_linear.weight, self.out_linear.bias), None
+        o = G.softmax_mha(qkv.reshape(N, 3 * D), key_valid, B, T, self.num_heads, self.head_dim, p, seed,
+                          seq_range=seq_range, row_base=row_base)
+        return _linear(o.view(query.shape), self.out_linear.weight, self.out_linear.bias), None
 
 
 def dropout_seed(device):
@@ -131,20 +136,26 @@ class HSTUAttention(torch.nn.Module):
         self.attn_norm = torch.nn.LayerNorm(hidden_units, eps=1e-8)
         self.out_linear = torch.nn.Linear(hidden_units, hidden_units)
 
-    def forward(self, query, key=None, value=None, attn_mask=None, key_valid=None, seq_range=None, timestamps=None):
+    def forward(self, query, key=None, value=None, attn_mask=None, key_valid=None, seq_range=None, timestamps=None,
+                row_base=None):
+        """row_base (with key_valid [B, T] and seq_range): query holds the jagged rows
+        of the batch (jagged.py) as [1, rows, D]; timestamps stay [B, T]."""
         B, T, D = query.shape
-        if key_valid is None:
+        if row_base is not None:
+            B, T = key_valid.shape
+        elif key_valid is None:
             key_valid = key_valid_from_mask(attn_mask, B, T)
+        N = query.shape[0] * query.shape[1]
         rab_t = self.rab_t if timestamps is not None else None
         if rab_t is None:
             timestamps = None
-        pre = _linear(query, self.uvqk.weight, self.uvqk.bias).reshape(B * T, 4 * D)
+        pre = _linear(query, self.uvqk.weight, self.uvqk.bias).reshape(N, 4 * D)
         p = self.dropout_rate if self.training else 0.0
         seed = dropout_seed(pre.device) if p > 0 else 0
         y = G.hstu_core(pre, self.rab, self.attn_norm.weight, self.attn_norm.bias, key_valid, B, T,
                         self.num_heads, self.head_dim, 1.0 / T, self.attn_norm.eps, dropout_p=p, seed=seed,
-                        seq_range=seq_range, timestamps=timestamps, rab_t=rab_t)
-        return _linear(y.view(B, T, D), self.out_linear.weight, self.out_linear.bias), None
+                        seq_range=seq_range, timestamps=timestamps, rab_t=rab_t, row_base=row_base)
+        return _linear(y.view(query.shape), self.out_linear.weight, self.out_linear.bias), None
 
 
 class PointWiseFeedForward(torch.nn.Module):
@@ -418,7 +429,10 @@ class BaselineModel(torch.nn.Module):
         Wc = torch.cat(cols, 1)
         return F.pad(Wc, (0, width - Wc.shape[1]))
 
-    def _embed(self, seq, feature_array, mask=None, include_user=False, with_pos=False, role='seq'):
+    def _embed(self, seq, feature_array, mask=None, include_user=False, with_pos=False, role='seq', pos_idx=None):
+        """pos_idx (jagged rows): the position-embedding index of each row (t + 1 where
+        the token is not padding) instead of the positional mode, which derives it from
+        the row's place in a [B, T] batch."""
         dev = self._device()
         seq = seq.to(dev, non_blocking=True).long()
         B, T = seq.shape
@@ -474,7 +488,11 @@ class BaselineModel(torch.nn.Module):
             wu = operand(self._ref('user_emb'), L.IDX_USER_MASK, [], 'user')
             if user_p:
                 projected('user', user_p)
-        if with_pos:
+        if with_pos and pos_idx is not None:
+            specs.append(G.LookupSpec(self._ref('pos_emb'), pos_idx.to(dev).reshape(N), col, L.IDX_PLAIN))
+            splits.append((col, col + d))
+            col += d
+        elif with_pos:
             specs.append(G.LookupSpec(self._ref('pos_emb'), seq, col, L.IDX_POSITION))
             splits.append((col, col + d))
             col += d
@@ -552,16 +570,22 @@ class BaselineModel(torch.nn.Module):
         return x[:B], x[B:]
 
     # -------------------------------------------------- model/BaseLine/model.py:312-350
-    def log2feats(self, log_seqs, mask, seq_feature, timestamps=None):
+    def log2feats(self, log_seqs, mask, seq_feature, timestamps=None, jagged=None, pos_idx=None):
         """timestamps (int [B, T] event times, HSTU blocks with hstu_time_buckets > 0
-        only): the time bias of every HSTU layer; None = positions only."""
+        only): the time bias of every HSTU layer; None = positions only.
+        jagged (jagged.Jagged) + pos_idx: log_seqs / mask / seq_feature / pos_idx hold
+        the batch's jagged rows as [1, rows] (jagged.compact); the result is [1, rows, D]."""
         dev = self._device()
         B, T = log_seqs.shape
-        seqs, pos_rows = self._embed(log_seqs, seq_feature, mask=mask, include_user=True, with_pos=True)
+        seqs, pos_rows = self._embed(log_seqs, seq_feature, mask=mask, include_user=True, with_pos=True,
+                                     pos_idx=pos_idx if jagged is not None else None)
         seqs = seqs * self.item_emb.embedding_dim ** 0.5 + pos_rows.view(B, T, -1)
         seqs = self.emb_dropout(seqs)
-        key_valid = (mask.to(dev, non_blocking=True) != 0).to(torch.uint8).contiguous()
-        kw = dict(key_valid=key_valid, seq_range=torch.ops.grk.seq_ranges(key_valid))  # one launch serves every layer
+        if jagged is not None:
+            kw = dict(key_valid=jagged.key_valid, seq_range=jagged.seq_range, row_base=jagged.row_base)
+        else:
+            key_valid = (mask.to(dev, non_blocking=True) != 0).to(torch.uint8).contiguous()
+            kw = dict(key_valid=key_valid, seq_range=torch.ops.grk.seq_ranges(key_valid))  # one launch serves every layer
         if timestamps is not None and self.block == 'hstu':
             kw['timestamps'] = timestamps.to(dev, torch.int64, non_blocking=True).contiguous()
         if self.block == 'hstu' and _grk_gemm_ok(seqs) and self.hidden_units % 8 == 0:
@@ -601,10 +625,12 @@ class BaselineModel(torch.nn.Module):
             pos_embs, neg_embs = self.feat2emb_pair(pos_seqs, pos_feature, neg_seqs, neg_feature)
         return G.pair_logits(log_feats, pos_embs, neg_embs, next_mask.to(self._device(), non_blocking=True))
 
-    def encode(self, user_item, pos_seqs, neg_seqs, mask, seq_feature, pos_feature, neg_feature, timestamps=None):
-        """(log_feats, pos_embs, neg_embs) -- the operands of the loss."""
+    def encode(self, user_item, pos_seqs, neg_seqs, mask, seq_feature, pos_feature, neg_feature, timestamps=None,
+               jagged=None, pos_idx=None):
+        """(log_feats, pos_embs, neg_embs) -- the operands of the loss.  jagged / pos_idx:
+        the batch fields hold its jagged rows (jagged.compact), so do the three outputs."""
         with self._shared_projections():
-            return (self.log2feats(user_item, mask, seq_feature, timestamps),
+            return (self.log2feats(user_item, mask, seq_feature, timestamps, jagged=jagged, pos_idx=pos_idx),
                     *self.feat2emb_pair(pos_seqs, pos_feature, neg_seqs, neg_feature))
 
     @contextlib.contextmanager

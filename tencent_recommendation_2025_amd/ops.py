@@ -131,48 +131,50 @@ def _seed_arg(seed, seed_dev):
     return seed_dev if seed_dev is not None else seed
 
 
-def _softmax_args(qkv, key_valid, heads, head_dim, dropout_p, seed, seed_dev, precise, seq_range):
+def _softmax_args(qkv, key_valid, heads, head_dim, dropout_p, seed, seed_dev, precise, seq_range, row_base=None):
     B, T = key_valid.shape
     D = heads * head_dim
     fid, prec, kdt = _attn_plan(qkv.dtype, T, head_dim, precise)
     xb = qkv.contiguous() if fid else qkv.to(torch.bfloat16).contiguous()
     args = K.attn_args(L.ATTN_SOFTMAX, xb[:, :D], xb[:, D:2 * D], xb[:, 2 * D:3 * D], B, T, heads, head_dim,
                        key_valid=key_valid, dropout_p=dropout_p, seed=_seed_arg(seed, seed_dev), precise=prec,
-                       out_dtype=kdt, seq_range=seq_range)
+                       out_dtype=kdt, seq_range=seq_range, row_base=row_base)
     return args, xb, prec, kdt
 
 
 @torch.library.custom_op('grk::softmax_attention', mutates_args=(), device_types='cuda')
 def softmax_attention(qkv: Tensor, key_valid: Tensor, heads: int, head_dim: int, dropout_p: float, seed: int,
-                      seed_dev: Optional[Tensor], precise: int, seq_range: Optional[Tensor]) -> Tuple[Tensor, Tensor]:
-    """Causal + key-padding softmax attention of a packed [B*T, 3D] (q|k|v).
-    Returns (out [B*T, D] in the kernel dtype: fp32 for fp32/fp16 inputs, bf16
-    for bf16; lse fp32 [B, H, T])."""
+                      seed_dev: Optional[Tensor], precise: int, seq_range: Optional[Tensor],
+                      row_base: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+    """Causal + key-padding softmax attention of a packed [B*T, 3D] (q|k|v) -- or of
+    the batch's jagged rows with row_base (jagged.py).  Returns (out [rows, D] in the
+    kernel dtype: fp32 for fp32/fp16 inputs, bf16 for bf16; lse fp32 [B, H, T])."""
     B, T = key_valid.shape
-    args, _, _, kdt = _softmax_args(qkv, key_valid, heads, head_dim, dropout_p, seed, seed_dev, precise, seq_range)
-    out = torch.empty(B * T, heads * head_dim, dtype=kdt, device=qkv.device)
+    args, _, _, kdt = _softmax_args(qkv, key_valid, heads, head_dim, dropout_p, seed, seed_dev, precise, seq_range,
+                                    row_base)
+    out = torch.empty(qkv.shape[0], heads * head_dim, dtype=kdt, device=qkv.device)
     lse = torch.empty(B, heads, T, dtype=torch.float32, device=qkv.device)
     K.attention_fwd(args, out, lse)
     return out, lse
 
 
 @softmax_attention.register_fake
-def _(qkv, key_valid, heads, head_dim, dropout_p, seed, seed_dev, precise, seq_range):
+def _(qkv, key_valid, heads, head_dim, dropout_p, seed, seed_dev, precise, seq_range, row_base=None):
     B, T = key_valid.shape
     kdt = _attn_plan(qkv.dtype, T, head_dim, precise)[2]
-    return (qkv.new_empty(B * T, heads * head_dim, dtype=kdt), qkv.new_empty(B, heads, T, dtype=torch.float32))
+    return (qkv.new_empty(qkv.shape[0], heads * head_dim, dtype=kdt), qkv.new_empty(B, heads, T, dtype=torch.float32))
 
 
 @torch.library.custom_op('grk::softmax_attention_backward', mutates_args=(), device_types='cuda')
 def softmax_attention_backward(gout: Tensor, qkv: Tensor, out: Tensor, lse: Tensor, key_valid: Tensor, heads: int,
                                head_dim: int, dropout_p: float, seed: int, seed_dev: Optional[Tensor], precise: int,
-                               seq_range: Optional[Tensor]) -> Tensor:
-    """d(q|k|v) [B*T, 3D] in qkv's dtype."""
+                               seq_range: Optional[Tensor], row_base: Optional[Tensor] = None) -> Tensor:
+    """d(q|k|v) [rows, 3D] in qkv's dtype."""
     B, T = key_valid.shape
     D = heads * head_dim
     args, xb, prec, kdt = _softmax_args(qkv, key_valid, heads, head_dim, dropout_p, seed, seed_dev, precise,
-                                        seq_range)
-    dqkv = torch.empty(B * T, 3 * D, dtype=kdt, device=qkv.device)
+                                        seq_range, row_base)
+    dqkv = torch.empty(qkv.shape[0], 3 * D, dtype=kdt, device=qkv.device)
     delta = torch.empty(B, heads, T, dtype=torch.float32, device=qkv.device)
     g = gout.contiguous()
     if g.dtype not in (torch.float32, torch.bfloat16) or (prec == 2 and g.dtype != torch.float32):
@@ -182,35 +184,36 @@ def softmax_attention_backward(gout: Tensor, qkv: Tensor, out: Tensor, lse: Tens
 
 
 @softmax_attention_backward.register_fake
-def _(gout, qkv, out, lse, key_valid, heads, head_dim, dropout_p, seed, seed_dev, precise, seq_range):
+def _(gout, qkv, out, lse, key_valid, heads, head_dim, dropout_p, seed, seed_dev, precise, seq_range, row_base=None):
     return torch.empty_like(qkv, memory_format=torch.contiguous_format)
 
 
 def _softmax_setup(ctx, inputs, output):
-    qkv, key_valid, heads, head_dim, dropout_p, seed, seed_dev, precise, seq_range = inputs
+    qkv, key_valid, heads, head_dim, dropout_p, seed, seed_dev, precise, seq_range, row_base = inputs
     out, lse = output
-    ctx.save_for_backward(qkv, out, lse, key_valid, seed_dev, seq_range)
+    ctx.save_for_backward(qkv, out, lse, key_valid, seed_dev, seq_range, row_base)
     ctx.meta = (heads, head_dim, dropout_p, seed, precise)
 
 
 def _softmax_backward(ctx, gout, glse):
-    qkv, out, lse, key_valid, seed_dev, seq_range = ctx.saved_tensors
+    qkv, out, lse, key_valid, seed_dev, seq_range, row_base = ctx.saved_tensors
     heads, head_dim, dropout_p, seed, precise = ctx.meta
     dqkv = torch.ops.grk.softmax_attention_backward(gout, qkv, out, lse, key_valid, heads, head_dim, dropout_p, seed,
-                                                    seed_dev, precise, seq_range)
-    return dqkv, None, None, None, None, None, None, None, None
+                                                    seed_dev, precise, seq_range, row_base)
+    return dqkv, None, None, None, None, None, None, None, None, None
 
 
 torch.library.register_autograd('grk::softmax_attention', _softmax_backward, setup_context=_softmax_setup)
 
 
-def _hstu_args(pb, rab32, key_valid, heads, head_dim, inv_n, precise, seq_range, timestamps=None, rab_t32=None):
+def _hstu_args(pb, rab32, key_valid, heads, head_dim, inv_n, precise, seq_range, timestamps=None, rab_t32=None,
+               row_base=None):
     B, T = key_valid.shape
     D = heads * head_dim
     return K.attn_args(L.ATTN_HSTU, pb[:, 2 * D:3 * D], pb[:, 3 * D:], pb[:, D:2 * D], B, T, heads, head_dim,
                        key_valid=key_valid, scale=head_dim ** -0.5, rab=rab32, inv_n=inv_n, precise=precise,
                        out_dtype=torch.bfloat16, act='silu', seq_range=seq_range, timestamps=timestamps,
-                       rab_t=rab_t32)
+                       rab_t=rab_t32, row_base=row_base)
 
 
 def _f32(t):
@@ -221,7 +224,7 @@ def _f32(t):
 def hstu_core(pre: Tensor, rab: Tensor, ln_w: Tensor, ln_b: Tensor, key_valid: Tensor, heads: int, head_dim: int,
               inv_n: float, eps: float, precise: int, dropout_p: float, seed: int, seed_dev: Optional[Tensor],
               seq_range: Optional[Tensor], timestamps: Optional[Tensor] = None,
-              rab_t: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
+              rab_t: Optional[Tensor] = None, row_base: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
     """y = dropout(LayerNorm(HSTU-attn(SiLU(q), SiLU(k), SiLU(v))) * SiLU(u)) on the
     [B*T, 4D] (u|v|q|k) pre-activation; bf16 math.  Returns (y bf16, o bf16,
     LayerNorm stats fp32 [B*T, 2]).  timestamps (int64 [B, T]) + rab_t ([H, nbt]):
@@ -229,7 +232,7 @@ def hstu_core(pre: Tensor, rab: Tensor, ln_w: Tensor, ln_b: Tensor, key_valid: T
     D = heads * head_dim
     pb = pre.to(torch.bfloat16).contiguous()
     args = _hstu_args(pb, rab.float().contiguous(), key_valid, heads, head_dim, inv_n, precise, seq_range,
-                      timestamps, _f32(rab_t))
+                      timestamps, _f32(rab_t), row_base)
     o = torch.empty(pre.shape[0], D, dtype=torch.bfloat16, device=pre.device)
     K.attention_fwd(args, o)
     y, stats = K.norm_gate_fwd(o, pb[:, :D], ln_w.float().contiguous(), ln_b.float().contiguous(), eps, dropout_p,
@@ -239,7 +242,7 @@ def hstu_core(pre: Tensor, rab: Tensor, ln_w: Tensor, ln_b: Tensor, key_valid: T
 
 @hstu_core.register_fake
 def _(pre, rab, ln_w, ln_b, key_valid, heads, head_dim, inv_n, eps, precise, dropout_p, seed, seed_dev, seq_range,
-      timestamps=None, rab_t=None):
+      timestamps=None, rab_t=None, row_base=None):
     N, D = pre.shape[0], heads * head_dim
     return (pre.new_empty(N, D, dtype=torch.bfloat16), pre.new_empty(N, D, dtype=torch.bfloat16),
             pre.new_empty(N, 2, dtype=torch.float32))
@@ -250,7 +253,8 @@ def hstu_core_backward(gy: Tensor, pre: Tensor, o: Tensor, stats: Tensor, rab: T
                        key_valid: Tensor, heads: int, head_dim: int, inv_n: float, precise: int, dropout_p: float,
                        seed: int, seed_dev: Optional[Tensor], seq_range: Optional[Tensor],
                        timestamps: Optional[Tensor] = None,
-                       rab_t: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+                       rab_t: Optional[Tensor] = None,
+                       row_base: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
     """(dpre in pre's dtype, drab, dln_w, dln_b, drab_t in their parameters' dtypes;
     drab_t is empty without a time bias)."""
     D = heads * head_dim
@@ -263,7 +267,7 @@ def hstu_core_backward(gy: Tensor, pre: Tensor, o: Tensor, stats: Tensor, rab: T
     drab = torch.zeros_like(rab32)
     rab_t32 = _f32(rab_t)
     drab_t = torch.zeros_like(rab_t32) if rab_t is not None else None
-    args = _hstu_args(pb, rab32, key_valid, heads, head_dim, inv_n, precise, seq_range, timestamps, rab_t32)
+    args = _hstu_args(pb, rab32, key_valid, heads, head_dim, inv_n, precise, seq_range, timestamps, rab_t32, row_base)
     K.attention_bwd(args, None, do, None, None, dpre[:, 2 * D:3 * D], dpre[:, 3 * D:], dpre[:, D:2 * D], drab,
                     drab_t=drab_t)
     drab_t = drab_t.to(rab_t.dtype) if rab_t is not None else rab.new_empty(0)
@@ -272,27 +276,27 @@ def hstu_core_backward(gy: Tensor, pre: Tensor, o: Tensor, stats: Tensor, rab: T
 
 @hstu_core_backward.register_fake
 def _(gy, pre, o, stats, rab, ln_w, ln_b, key_valid, heads, head_dim, inv_n, precise, dropout_p, seed, seed_dev,
-      seq_range, timestamps=None, rab_t=None):
+      seq_range, timestamps=None, rab_t=None, row_base=None):
     return (torch.empty_like(pre), torch.empty_like(rab), torch.empty_like(ln_w), torch.empty_like(ln_b),
             torch.empty_like(rab_t) if rab_t is not None else rab.new_empty(0))
 
 
 def _hstu_setup(ctx, inputs, output):
     (pre, rab, ln_w, ln_b, key_valid, heads, head_dim, inv_n, eps, precise, dropout_p, seed, seed_dev, seq_range,
-     timestamps, rab_t) = inputs
+     timestamps, rab_t, row_base) = inputs
     _, o, stats = output
-    ctx.save_for_backward(pre, o, stats, rab, ln_w, ln_b, key_valid, seed_dev, seq_range, timestamps, rab_t)
+    ctx.save_for_backward(pre, o, stats, rab, ln_w, ln_b, key_valid, seed_dev, seq_range, timestamps, rab_t, row_base)
     ctx.meta = (heads, head_dim, inv_n, precise, dropout_p, seed)
 
 
 def _hstu_backward(ctx, gy, go, gstats):
-    pre, o, stats, rab, ln_w, ln_b, key_valid, seed_dev, seq_range, timestamps, rab_t = ctx.saved_tensors
+    pre, o, stats, rab, ln_w, ln_b, key_valid, seed_dev, seq_range, timestamps, rab_t, row_base = ctx.saved_tensors
     heads, head_dim, inv_n, precise, dropout_p, seed = ctx.meta
     dpre, drab, dw, db, drab_t = torch.ops.grk.hstu_core_backward(gy, pre, o, stats, rab, ln_w, ln_b, key_valid,
                                                                   heads, head_dim, inv_n, precise, dropout_p, seed,
-                                                                  seed_dev, seq_range, timestamps, rab_t)
+                                                                  seed_dev, seq_range, timestamps, rab_t, row_base)
     return (dpre, drab, dw, db, None, None, None, None, None, None, None, None, None, None, None,
-            drab_t if rab_t is not None else None)
+            drab_t if rab_t is not None else None, None)
 
 
 torch.library.register_autograd('grk::hstu_core', _hstu_backward, setup_context=_hstu_setup)

@@ -26,6 +26,7 @@ import contextlib
 import torch
 
 from . import functional as G
+from . import jagged as J
 
 
 _PRIVATE_STREAMS = {}
@@ -89,10 +90,16 @@ class Trainer:
           of one fixed shape; a batch of another shape runs eagerly).  Dropout
           seeds are drawn on the device (model.dropout_seed), so dropout runs
           inside the replayed step.
+    jagged: run the token-wise step on each sequence's span [first valid token,
+          T) only, packed back to back (jagged.py; the padding rows before it are
+          dead in the reference), in ``capacity_for(span rows, jagged_quantum)``
+          rows.  ``step(batch, rows=n)`` takes the batch's span-row count from the
+          caller (jagged.span_rows; computed with one host sync otherwise).  With
+          graph=True one HIP graph is captured per capacity (sharing one memory pool).
     """
 
     def __init__(self, model, optimizer, loss='bce', amp_dtype=torch.bfloat16, temperature=0.05, graph=False,
-                 graph_warmup=3, graph_audit=False, log_q=None):
+                 graph_warmup=3, graph_audit=False, log_q=None, jagged=False, jagged_quantum=1024):
         if loss not in ('bce', 'sampled_softmax'):
             raise ValueError("loss must be 'bce' or 'sampled_softmax'")
         if log_q is not None and (loss != 'sampled_softmax' or not (isinstance(log_q, torch.Tensor) or log_q == 'batch')):
@@ -110,9 +117,15 @@ class Trainer:
         self._g = None
         self._static = None
         self._static_loss = None
-        self._warm = 0
+        self._graphs = {}        # capacity (jagged) or None -> (graph, static batch, static loss)
+        self._warm = {}
+        self._pool = None
         self._side = None
         self._sharded = hasattr(optimizer, 'prepare')
+        self.jagged, self.jagged_quantum = bool(jagged), int(jagged_quantum)
+        if self.jagged and self._sharded:
+            raise ValueError('jagged=True: the row-sharded optimizer routes padded batches (use jagged=False)')
+        self._cap = None         # jagged capacity of the current step
 
     def _graph_blocker(self):
         if not torch.cuda.is_available():
@@ -128,8 +141,13 @@ class Trainer:
         ts = batch[9] if len(batch) > 9 else None
         amp = (torch.autocast('cuda', dtype=self.amp_dtype) if self.amp_dtype is not None
                else contextlib.nullcontext())
+        jag = pidx = None
+        if self.jagged:
+            cap = self._cap if self._cap is not None else J.capacity_for(J.span_rows(tt), self.jagged_quantum)
+            jag = J.layout(tt, cap, ntt)
+            seq, pos, neg, tt, ntt, _nat, sf, pf, nf, ts, pidx = J.compact(batch, jag)
         with amp:
-            h, pe, ne = self.model.encode(seq, pos, neg, tt, sf, pf, nf, timestamps=ts)
+            h, pe, ne = self.model.encode(seq, pos, neg, tt, sf, pf, nf, timestamps=ts, jagged=jag, pos_idx=pidx)
             if self.loss_kind == 'bce':
                 loss = G.bce_loss(h, pe, ne, ntt)
             else:
@@ -156,18 +174,28 @@ class Trainer:
         self.opt.step()
         return loss.detach()
 
-    def step(self, batch, next_batch=None):
+    def step(self, batch, next_batch=None, rows=None):
         """One training step; ``next_batch`` (optional) is the batch of the following
-        step, routed ahead when the tables are row-sharded."""
+        step, routed ahead when the tables are row-sharded.  ``rows`` (jagged): the
+        batch's span-row count (jagged.span_rows), known to the host."""
+        key = None
+        if self.jagged:
+            n = int(rows) if rows is not None else J.span_rows(batch[3])
+            self._cap = key = J.capacity_for(n, self.jagged_quantum)
         if not self.graph:
             return self.eager_step(batch, next_batch)
-        if self._g is None:
-            if self._warm < self.graph_warmup:
+        entry = self._graphs.get(key)
+        if entry is None:
+            warm = self._warm.get(key, 0)
+            # the first graph: graph_warmup eager steps; a later capacity only needs its
+            # GEMM plans tuned (one eager step of that shape)
+            if warm < (self.graph_warmup if not self._graphs else 1):
                 # warm-up on the stream the capture will use: GEMM plans tuned,
                 # per-stream workspaces and the caching allocator's blocks in place
-                self._warm += 1
+                self._warm[key] = warm + 1
                 return self._on_side(lambda: self.eager_step(batch, next_batch))
-            return self._capture(batch, next_batch)
+            return self._capture(batch, next_batch, key)
+        self._g, self._static, self._static_loss = entry
         src = _tensors(batch)
         dst = _tensors(self._static)
         if len(src) != len(dst) or any(a.shape != b.shape or a.dtype != b.dtype for a, b in zip(src, dst)):
@@ -199,7 +227,7 @@ class Trainer:
         cur.wait_stream(self._side)
         return out
 
-    def _capture(self, batch, next_batch=None):
+    def _capture(self, batch, next_batch=None, key=None):
         """Record one step (host state advances once here), then replay it for this batch."""
         self._static = _clone_batch(batch)
         self.opt.zero_grad(set_to_none=True)
@@ -214,6 +242,12 @@ class Trainer:
             self.opt.maybe_segment()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph(keep_graph=self.graph_audit)
+        if self._pool is None:
+            # one memory pool for every captured capacity: the graphs never run at once,
+            # and nothing a replay leaves behind is read after another graph ran (the
+            # loss is cloned right after its replay; parameters and optimizer state
+            # live outside the pool)
+            self._pool = torch.cuda.graph_pool_handle()
         cur = torch.cuda.current_stream()
         self._side.wait_stream(cur)
         # thread_local: the process group's watchdog thread polls its collectives'
@@ -222,7 +256,7 @@ class Trainer:
         # capture error, which the watchdog treats as fatal and aborts the process
         # (seen in round 1).  thread_local confines the restriction to this thread,
         # so the watchdog's polls are legal and nothing needs to wait for it.
-        with torch.cuda.graph(g, stream=self._side, capture_error_mode='thread_local'):
+        with torch.cuda.graph(g, pool=self._pool, stream=self._side, capture_error_mode='thread_local'):
             if self._sharded:
                 loss = self.compute_loss(self._static)
                 loss.backward()
@@ -234,6 +268,7 @@ class Trainer:
             self.graph_nodes = graph_node_census(g)
             g.instantiate()
         self._g = g
+        self._graphs[key] = (g, self._static, self._static_loss)
         g.replay()               # the captured step itself (host state already advanced)
         if self._sharded:
             if buckets is not None:

@@ -1,0 +1,233 @@
+"""The jagged (valid-token) layout of the fused trainer (jagged.py, grk_jagged.hip).
+
+* layout / row gather bit-exact vs the numpy oracle (oracle/jagged.py), incl.
+  holes, empty sequences, dead capacity rows and the error flags;
+* the attention kernels on jagged rows == the padded kernels, bit for bit, on
+  every span row (HSTU with rab and time bias, softmax with dropout: forward,
+  dQ + drab (+ drab_t), dK/dV; delta) -- and no write outside the spans;
+* the jagged training step against the padded one: log_feats / item
+  embeddings equal on the span rows, loss and every gradient equal up to the
+  summation order of the GEMMs over fewer rows (fp32: 1e-5; bf16: the bench
+  tolerances), graph replay == eager bitwise across two capacities.
+The padded step is pinned to the reference (test_gpu_model.py), so the jagged
+one is pinned through it."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import jagged as ojag
+from oracle.embedding import to_bf16_f32
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def nrel(a, b):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    d = np.linalg.norm(b)
+    return float(np.linalg.norm(a - b) / (d if d > 0 else 1.0))
+
+
+def test_layout_and_gather_match_oracle():
+    from tencent_recommendation_2025_amd import jagged as J
+    from tencent_recommendation_2025_amd import kernels as K
+    rng = np.random.default_rng(0)
+    B, T = 37, 51
+    tt = np.zeros((B, T), np.int64)
+    for b in range(B):
+        n = rng.integers(0, T + 1)
+        tt[b, T - n:] = rng.integers(1, 3, n)
+    tt[3, 40:45] = 0            # a hole inside a span
+    tt[5] = 0                   # an empty sequence
+    n_rows = int(ojag.layout(tt, 1)[3])
+    assert J.span_rows(torch.from_numpy(tt)) == n_rows == J.span_rows(torch.from_numpy(tt).to(DEV))
+    for cap in (n_rows, J.capacity_for(n_rows, 256)):
+        jag = J.layout(torch.from_numpy(tt).to(DEV), cap)
+        rng_w, base_w, map_w, n_w = ojag.layout(tt, cap)
+        assert int(jag.n.item()) == n_w and int(jag.err.item()) == 0
+        assert np.array_equal(jag.seq_range.cpu().numpy()[:, :2], rng_w)
+        assert np.array_equal(jag.row_base.cpu().numpy(), base_w)
+        assert np.array_equal(jag.row_map.cpu().numpy(), map_w)
+        feats = {'a': rng.integers(0, 100, (B, T)), 'arr': rng.integers(0, 9, (B, T, 3)),
+                 'mm': rng.standard_normal((B, T, 32)).astype(np.float32)}
+        srcs = {k: torch.from_numpy(v).to(DEV) for k, v in feats.items()}
+        dsts = {k: torch.full((cap,) + v.shape[2:], 7, dtype=v.dtype, device=DEV) for k, v in srcs.items()}
+        K.gather_rows([(srcs[k].reshape(B * T, *srcs[k].shape[2:]), dsts[k]) for k in srcs], jag.row_map)
+        for k in feats:
+            assert np.array_equal(dsts[k].cpu().numpy(), ojag.gather_rows(feats[k], map_w)), k
+    # error flags: a next-item label before the span (bit 1), more span rows than capacity (bit 2)
+    ntt = (tt != 0).astype(np.int64)
+    ntt[0, 0] = 1 if tt[0, 0] == 0 else ntt[0, 0]
+    jag = J.layout(torch.from_numpy(tt).to(DEV), n_rows - 1, torch.from_numpy(ntt).to(DEV))
+    err = int(jag.err.item())
+    assert err & 2 and (err & 1) == (tt[0, 0] == 0)
+
+
+def _hstu_case(B, T, H, hd, seed, holes=False):
+    rng = np.random.default_rng(seed)
+    D = H * hd
+    pre = to_bf16_f32(rng.standard_normal((B * T, 4 * D)).astype(np.float32))
+    kv = np.zeros((B, T), np.uint8)
+    lens = rng.integers(1, T + 1, B)
+    lens[0] = T
+    for b in range(B):
+        kv[b, T - lens[b]:] = 1
+    if holes:
+        kv[1, T - 3] = 0
+    return pre, kv
+
+
+@pytest.mark.parametrize('kind,T,hd,nbt,holes', [('hstu', 201, 64, 0, False), ('hstu', 77, 64, 24, True),
+                                                  ('hstu', 130, 128, 0, False), ('softmax', 201, 64, 0, False),
+                                                  ('softmax', 60, 32, 0, True)])
+def test_attention_jagged_equals_padded_bitwise(kind, T, hd, nbt, holes):
+    from tencent_recommendation_2025_amd import _lib as L
+    from tencent_recommendation_2025_amd import jagged as J
+    from tencent_recommendation_2025_amd import kernels as K
+    B, H = 24, 4 if hd <= 64 else 2
+    D = H * hd
+    pre_np, kv_np = _hstu_case(B, T, H, hd, seed=T + hd, holes=holes)
+    pre = torch.from_numpy(pre_np).to(DEV).to(torch.bfloat16)
+    kv = torch.from_numpy(kv_np).to(DEV)
+    n = J.span_rows(kv)
+    cap = J.capacity_for(n, 128)
+    jag = J.layout(kv.to(torch.int64), cap)
+    jpre = torch.empty(cap, 4 * D, dtype=torch.bfloat16, device=DEV)
+    K.gather_rows([(pre, jpre)], jag.row_map)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    hstu = kind == 'hstu'
+    extra = {}
+    if hstu:
+        extra = dict(rab=0.2 * torch.randn(H, T, device=DEV, generator=g), inv_n=1.0 / T, act='silu')
+        if nbt:
+            ts = torch.cumsum(torch.randint(1, 10 ** 5, (B, T), device=DEV, generator=g), 1)
+            extra.update(timestamps=ts, rab_t=0.3 * torch.randn(H, nbt, device=DEV, generator=g))
+    else:
+        extra = dict(dropout_p=0.1, seed=1234)
+    ktype = L.ATTN_HSTU if hstu else L.ATTN_SOFTMAX
+    do = torch.randn(B * T, D, device=DEV, generator=g).bfloat16()
+    jdo = torch.empty(cap, D, dtype=torch.bfloat16, device=DEV)
+    K.gather_rows([(do, jdo)], jag.row_map)
+    outs = []
+    for jagged in (False, True):
+        x = jpre if jagged else pre
+        N = x.shape[0]
+        a = K.attn_args(ktype, x[:, 2 * D:3 * D], x[:, 3 * D:], x[:, D:2 * D], B, T, H, hd, key_valid=kv,
+                        scale=hd ** -0.5, out_dtype=torch.bfloat16, seq_range=jag.seq_range,
+                        row_base=jag.row_base if jagged else None, **extra)
+        sentinel = -7.0
+        o = torch.full((N, D), sentinel, dtype=torch.bfloat16, device=DEV)
+        lse = torch.empty(B, H, T, device=DEV) if not hstu else None
+        K.attention_fwd(a, o, lse)
+        dx = torch.full((N, 4 * D), sentinel, dtype=torch.bfloat16, device=DEV)
+        delta = torch.empty(B, H, T, device=DEV) if not hstu else None
+        drab = torch.zeros(H, T, device=DEV) if hstu else None
+        drab_t = torch.zeros(H, nbt, device=DEV) if nbt else None
+        K.attention_bwd(a, o if not hstu else None, jdo if jagged else do, lse, delta, dx[:, 2 * D:3 * D],
+                        dx[:, 3 * D:], dx[:, D:2 * D], drab, drab_t=drab_t)
+        outs.append((o, dx, drab, drab_t, lse, delta))
+    rm = jag.row_map.cpu().numpy()
+    live = rm >= 0
+    (o0, dx0, dr0, dt0, l0, d0), (o1, dx1, dr1, dt1, l1, d1) = outs
+    assert torch.equal(o1[torch.from_numpy(np.flatnonzero(live)).to(DEV)], o0[torch.from_numpy(rm[live]).to(DEV).long()])
+    sel = torch.from_numpy(rm[live]).to(DEV).long()
+    rows = torch.from_numpy(np.flatnonzero(live)).to(DEV)
+    assert torch.equal(dx1[rows][:, D:], dx0[sel][:, D:])             # dv | dq | dk of every span row
+    assert bool((o1[~torch.from_numpy(live).to(DEV)] == -7.0).all())  # dead rows untouched
+    assert bool((dx1[~torch.from_numpy(live).to(DEV)][:, D:] == -7.0).all())
+    if hstu:
+        assert torch.equal(dr0, dr1)
+        if nbt:
+            assert torch.equal(dt0, dt1)
+    else:
+        assert torch.equal(l0, l1)
+        assert torch.equal(d0[kv.bool().unsqueeze(1).expand_as(d0)], d1[kv.bool().unsqueeze(1).expand_as(d1)])
+
+
+def _model(cfg_kw, args_kw, seed=0):
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel, init_reference_
+    cfg = S.SyntheticConfig(**cfg_kw)
+    stats, types = S.feature_schema(cfg)
+    torch.manual_seed(seed)
+    m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, S.make_args(**args_kw)).to(DEV)
+    init_reference_(m, seed=seed, live_norms=True)
+    return m, cfg
+
+
+@pytest.mark.parametrize('block', ['hstu', 'softmax'])
+def test_jagged_encode_equals_padded_fp32(block):
+    """fp32 (no autocast): the jagged encode's log_feats / pos / neg embeddings equal
+    the padded ones on every span row (1e-6), the BCE loss to 1e-6, and the table and
+    dense gradients to 1e-5 normwise (GEMM summation order over fewer rows)."""
+    from tencent_recommendation_2025_amd import functional as G
+    from tencent_recommendation_2025_amd import jagged as J
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    res = []
+    for jagged in (False, True):
+        m, cfg = _model(dict(batch_size=12, maxlen=40, num_items=3000, num_users=300, min_len=3),
+                        dict(hidden_units=64, maxlen=40, num_blocks=2, num_heads=2, block=block))
+        opt = FusedAdamW(m, lr=1e-3, table_dtype=torch.float32)
+        batch = S.make_batch(cfg, torch.Generator(device=DEV).manual_seed(5), DEV)
+        seq, pos, neg, tt, ntt, _nat, sf, pf, nf = batch
+        opt.zero_grad()
+        opt.begin_step(batch)
+        if jagged:
+            jag = J.layout(tt, J.capacity_for(J.span_rows(tt), 64), ntt)
+            jb = J.compact(batch, jag)
+            h, pe, ne = m.encode(jb[0], jb[1], jb[2], jb[3], jb[6], jb[7], jb[8], jagged=jag, pos_idx=jb[10])
+            loss = G.bce_loss(h, pe, ne, jb[4])
+            rows = jag.row_map
+        else:
+            h, pe, ne = m.encode(seq, pos, neg, tt, sf, pf, nf)
+            loss = G.bce_loss(h, pe, ne, ntt)
+            rows = None
+        loss.backward()
+        grads = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+        for grp in opt.groups:
+            grads['group.' + grp.name] = grp.dense_gradient().clone()
+        res.append((h.detach(), pe.detach(), ne.detach(), loss.detach(), grads, rows))
+    (h0, p0, n0, l0, g0, _), (h1, p1, n1, l1, g1, rm) = res
+    live = rm >= 0
+    sel = rm[live].long()
+    D = h0.shape[-1]
+    for a, b in ((h0, h1), (p0, p1), (n0, n1)):
+        assert nrel(b.reshape(-1, D)[live].cpu(), a.reshape(-1, D)[sel].cpu()) < 1e-6
+    assert abs(l0.item() - l1.item()) < 1e-6 * abs(l0.item())
+    assert set(g0) == set(g1)
+    bad = {k: nrel(g1[k].cpu(), g0[k].cpu()) for k in g0 if nrel(g1[k].cpu(), g0[k].cpu()) > 1e-5}
+    assert not bad, bad
+
+
+def test_jagged_trainer_bf16_matches_padded_and_graph_replay_is_bitwise():
+    """bf16 autocast HSTU (the bench's regime), dropout 0: jagged losses within the
+    bench tolerance (1e-3) of the padded trainer over 4 steps; the jagged step
+    replayed from HIP graphs of two capacities == the eager jagged step, bitwise."""
+    from tencent_recommendation_2025_amd import jagged as J
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    runs = {}
+    for name, jagged, graph in (('padded', False, False), ('jagged', True, False), ('jagged_graph', True, True)):
+        m, cfg = _model(dict(batch_size=16, maxlen=60, num_items=4000, num_users=500, min_len=4),
+                        dict(hidden_units=128, maxlen=60, num_blocks=2, num_heads=2))
+        tr = Trainer(m, FusedAdamW(m, lr=1e-3, defer_period=4), loss='bce', graph=graph, graph_warmup=1,
+                     jagged=jagged, jagged_quantum=128)
+        g = torch.Generator(device=DEV).manual_seed(3)
+        cfg_short = S.SyntheticConfig(**{**cfg.__dict__, 'min_len': 4})
+        batches = [S.make_batch(cfg_short, g, DEV) for _ in range(3)]
+        # two capacity buckets: one batch of short sequences
+        short = S.SyntheticConfig(**{**cfg.__dict__, 'min_len': 2, 'maxlen': 60})
+        batches.append(S.make_batch(short, g, DEV))
+        rows = [J.span_rows(b[3]) for b in batches]
+        losses = [tr.step(batches[i % 4], rows=rows[i % 4] if jagged else None).clone() for i in range(8)]
+        if graph:
+            assert len(tr._graphs) >= 2, tr._graphs.keys()
+        runs[name] = (torch.stack(losses), m.state_dict())
+    lp, lj, lg = runs['padded'][0], runs['jagged'][0], runs['jagged_graph'][0]
+    assert torch.equal(lj, lg), (lj, lg)
+    for k in runs['jagged'][1]:
+        assert torch.equal(runs['jagged'][1][k], runs['jagged_graph'][1][k]), k
+    rel = ((lj - lp).abs() / lp.abs()).max().item()
+    assert rel < 1e-3, (lp, lj)
