@@ -309,8 +309,13 @@ typedef struct grk_attn_args {
    * row_base[b] + t (int64 [batch]; grk_jagged_layout builds both).  Padding
    * rows before start_b are neither read nor written.  NULL = the padded
    * [batch * seq_len] layout.  Whole-sequence kernels (T * head_dim within
-   * their LDS budget) only: other shapes return GRK_EUNSUPPORTED. */
+   * their LDS budget) only: other shapes return GRK_EUNSUPPORTED.  The rows
+   * [*num_rows, capacity) past the spans (dead capacity rows of the step) of
+   * every output written (out; dq / dk / dv) are set to zero, so no stale
+   * value reaches the row-wise ops and weight gradients around. */
   const int64_t* row_base;
+  const int64_t* num_rows;         /* jagged: span rows (device), with row_base */
+  int64_t capacity;                /* jagged: rows of the q/k/v / output buffers */
 } grk_attn_args;
 
 /* 1 when grk_attention_* with precise == 2 (fp32 fidelity) runs for this

@@ -56,7 +56,8 @@ class GrkAttnArgs(C.Structure):
                 ('dropout_p', C.c_float), ('precise', C.c_int32), ('seed', C.c_uint64), ('out_dtype', C.c_int32),
                 ('act', C.c_int32), ('seq_range', C.c_void_p), ('seed_dev', C.c_void_p), ('qkv_dtype', C.c_int32),
                 ('timestamps', C.c_void_p), ('rab_t', C.c_void_p), ('num_time_buckets', C.c_int32),
-                ('drab_t', C.c_void_p), ('drab_t_ws', C.c_void_p), ('row_base', C.c_void_p)]
+                ('drab_t', C.c_void_p), ('drab_t_ws', C.c_void_p), ('row_base', C.c_void_p),
+                ('num_rows', C.c_void_p), ('capacity', C.c_int64)]
 
 
 class GrkRowCopy(C.Structure):

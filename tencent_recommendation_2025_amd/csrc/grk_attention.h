@@ -30,6 +30,8 @@ struct AttnParams {
   // optional jagged layout (whole-sequence kernels + delta): token (b, t) of q/k/v/out/dO/dq/dk/dv
   // is row row_base[b] + t and only t in [seq_range[3 b], T) exist; NULL = padded rows b * T + t
   const int64_t* row_base;
+  const int64_t* jag_n;  // jagged: span rows (device); rows [*jag_n, jag_cap) of every output are zeroed
+  int64_t jag_cap;
   unsigned long long* drab_fix;  // [H, nb] int64 fixed-point drab accumulator (deterministic)
   // HSTU time bias (whole-sequence kernels): S += rab_t[h, time_bucket(ts_q - ts_k)]
   const int64_t* ts;

@@ -342,9 +342,10 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
     fp32 / fp16 / bf16 and are read exactly -- fidelity_supported(T, hd)).
     timestamps (int64 [B, T]) + rab_t (fp32 [H, nbt], nbt <= 64): the HSTU time
     bias rab_t[h, time_bucket(t_q - t_k)] (include/grk.h, grk_attn_args).
-    row_base (int64 [B], with seq_range; jagged_layout): the jagged layout -- q/k/v
-    (and every output / gradient) hold only each sequence's span [start_b, T),
-    token (b, t) at row row_base[b] + t; key_valid / timestamps stay [B, T].
+    row_base (int64 [B + 1], with seq_range -- jagged_layout): the jagged layout --
+    q/k/v (and every output / gradient) hold only each sequence's span [start_b, T),
+    token (b, t) at row row_base[b] + t; row_base[B] = n, the span rows: output rows
+    [n, q.shape[0]) are zeroed.  key_valid / timestamps stay [B, T].
     float8_e4m3fn q/k/v (precise 0 / 1, act None; head_dim 64 / 128): the fp8
     attention of config C5 -- QK^T on the fp8 MFMA, the rest on bf16 MFMA over
     the exactly widened values."""
@@ -361,8 +362,9 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
         if (row_base is None and t.shape[0] != B * T) or t.shape[1] < H * hd:
             raise L.GrkError(f'{n}: shape {tuple(t.shape)} does not fit B*T={B * T}, H*hd={H * hd}')
     if row_base is not None:
-        if seq_range is None or row_base.dtype != torch.int64 or row_base.shape != (B,) or not row_base.is_contiguous():
-            raise L.GrkError('row_base must be a contiguous int64 [B] tensor, with seq_range (jagged_layout)')
+        if seq_range is None or row_base.dtype != torch.int64 or row_base.shape != (B + 1,) \
+                or not row_base.is_contiguous():
+            raise L.GrkError('row_base must be a contiguous int64 [B + 1] tensor, with seq_range (jagged_layout)')
     if not q.dtype == k.dtype == v.dtype:
         raise L.GrkError('q, k and v must share a dtype')
     if f8 and act is not None:
@@ -395,7 +397,8 @@ def attn_args(kind, q, k, v, B, T, H, hd, key_valid=None, scale=None, rab=None, 
                          precise, seed, L.dtype_code(out_dtype),
                          {None: L.ACT_NONE, 'silu': L.ACT_SILU}[act], _ptr(seq_range), _ptr(seed_dev),
                          L.GRK_FP8_E4M3 if f8 else L.dtype_code(q.dtype), _ptr(timestamps), _ptr(rab_t), nbt, None,
-                         None, _ptr(row_base))
+                         None, _ptr(row_base), None if row_base is None else row_base.data_ptr() + 8 * B,
+                         q.shape[0] if row_base is not None else 0)
     args._keep = (q, k, v, key_valid, rab, seq_range, seed_dev, timestamps, rab_t, row_base)  # raw pointers: keep alive
     return args
 
@@ -421,18 +424,19 @@ def seq_ranges(key_valid):
 
 def jagged_layout(key_valid, capacity, next_token_type=None, err_flag=None):
     """The jagged (valid-token) layout of a left-padded batch (grk_jagged_layout):
-    (seq_range int32 [B, 3], row_base int64 [B], row_map int32 [capacity], n int64 [1])
-    -- device tensors, no host sync.  Row r of the layout holds token row_map[r]
-    (= b * T + t, t in the span [start_b, T)), -1 past the n span rows."""
+    (seq_range int32 [B, 3], row_base int64 [B + 1], row_map int32 [capacity], n int64 [1]
+    = a view of row_base[B]) -- device tensors, no host sync.  Row r of the layout
+    holds token row_map[r] (= b * T + t, t in the span [start_b, T)), -1 past the n
+    span rows; token (b, t) is row row_base[b] + t."""
     _require_cuda(key_valid, next_token_type, err_flag)
     if key_valid.dtype != torch.uint8 or key_valid.dim() != 2 or not key_valid.is_contiguous():
         raise L.GrkError('key_valid must be a contiguous uint8 [B, T] tensor')
     B, T = key_valid.shape
     dev = key_valid.device
     ranges = torch.empty(B, 3, dtype=torch.int32, device=dev)
-    row_base = torch.empty(B, dtype=torch.int64, device=dev)
+    row_base = torch.empty(B + 1, dtype=torch.int64, device=dev)
     row_map = torch.empty(int(capacity), dtype=torch.int32, device=dev)
-    n = torch.empty(1, dtype=torch.int64, device=dev)
+    n = row_base[B:]
     ntt = None if next_token_type is None else next_token_type.to(torch.int32).contiguous()
     rc = L.lib().grk_jagged_layout(key_valid.data_ptr(), B, T, int(capacity), _ptr(ntt), ranges.data_ptr(),
                                    row_base.data_ptr(), row_map.data_ptr(), n.data_ptr(), _ptr(err_flag),

@@ -4,7 +4,8 @@
   holes, empty sequences, dead capacity rows and the error flags;
 * the attention kernels on jagged rows == the padded kernels, bit for bit, on
   every span row (HSTU with rab and time bias, softmax with dropout: forward,
-  dQ + drab (+ drab_t), dK/dV; delta) -- and no write outside the spans;
+  dQ + drab (+ drab_t), dK/dV; delta) -- and the dead capacity rows of every
+  output zeroed;
 * the jagged training step against the padded one: log_feats / item
   embeddings equal on the span rows, loss and every gradient equal up to the
   summation order of the GEMMs over fewer rows (fp32: 1e-5; bf16: the bench
@@ -46,7 +47,7 @@ def test_layout_and_gather_match_oracle():
         rng_w, base_w, map_w, n_w = ojag.layout(tt, cap)
         assert int(jag.n.item()) == n_w and int(jag.err.item()) == 0
         assert np.array_equal(jag.seq_range.cpu().numpy()[:, :2], rng_w)
-        assert np.array_equal(jag.row_base.cpu().numpy(), base_w)
+        assert np.array_equal(jag.row_base.cpu().numpy()[:B], base_w) and int(jag.row_base[B]) == n_w
         assert np.array_equal(jag.row_map.cpu().numpy(), map_w)
         feats = {'a': rng.integers(0, 100, (B, T)), 'arr': rng.integers(0, 9, (B, T, 3)),
                  'mm': rng.standard_normal((B, T, 32)).astype(np.float32)}
@@ -78,7 +79,7 @@ def _hstu_case(B, T, H, hd, seed, holes=False):
 
 
 @pytest.mark.parametrize('kind,T,hd,nbt,holes', [('hstu', 201, 64, 0, False), ('hstu', 77, 64, 24, True),
-                                                  ('hstu', 130, 128, 0, False), ('softmax', 201, 64, 0, False),
+                                                  ('hstu', 100, 128, 0, False), ('softmax', 201, 64, 0, False),
                                                   ('softmax', 60, 32, 0, True)])
 def test_attention_jagged_equals_padded_bitwise(kind, T, hd, nbt, holes):
     from tencent_recommendation_2025_amd import _lib as L
@@ -133,8 +134,9 @@ def test_attention_jagged_equals_padded_bitwise(kind, T, hd, nbt, holes):
     sel = torch.from_numpy(rm[live]).to(DEV).long()
     rows = torch.from_numpy(np.flatnonzero(live)).to(DEV)
     assert torch.equal(dx1[rows][:, D:], dx0[sel][:, D:])             # dv | dq | dk of every span row
-    assert bool((o1[~torch.from_numpy(live).to(DEV)] == -7.0).all())  # dead rows untouched
-    assert bool((dx1[~torch.from_numpy(live).to(DEV)][:, D:] == -7.0).all())
+    dead = ~torch.from_numpy(live).to(DEV)
+    assert bool((o1[dead] == 0).all())                                # dead capacity rows: zeroed outputs
+    assert bool((dx1[dead][:, D:] == 0).all()) and bool((dx1[dead][:, :D] == -7.0).all())   # u block untouched
     if hstu:
         assert torch.equal(dr0, dr1)
         if nbt:
@@ -196,7 +198,9 @@ def test_jagged_encode_equals_padded_fp32(block):
         assert nrel(b.reshape(-1, D)[live].cpu(), a.reshape(-1, D)[sel].cpu()) < 1e-6
     assert abs(l0.item() - l1.item()) < 1e-6 * abs(l0.item())
     assert set(g0) == set(g1)
-    bad = {k: nrel(g1[k].cpu(), g0[k].cpu()) for k in g0 if nrel(g1[k].cpu(), g0[k].cpu()) > 1e-5}
+    # k_linear.bias: analytically zero gradient (softmax is shift-invariant), rounding noise only
+    bad = {k: nrel(g1[k].cpu(), g0[k].cpu()) for k in g0
+           if not k.endswith('k_linear.bias') and nrel(g1[k].cpu(), g0[k].cpu()) > 1e-5}
     assert not bad, bad
 
 

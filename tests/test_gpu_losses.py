@@ -144,7 +144,8 @@ def test_sampled_softmax_logq_matches_oracle(K, M, D):
     zero = torch.zeros(M, device=DEV)
     a = K.sampled_softmax_fwd(th.detach(), te.detach(), ids_d, v8, tau, log_q=zero)
     b = K.sampled_softmax_fwd(th.detach(), te.detach(), ids_d, v8, tau)
-    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    nv = int(valid.sum())                 # lse2 holds the nv valid rows (compact index)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1][:nv], b[1][:nv])
     ga = K.sampled_softmax_bwd(th.detach(), te.detach(), ids_d, v8, tau, a[1], log_q=zero)
     gb = K.sampled_softmax_bwd(th.detach(), te.detach(), ids_d, v8, tau, b[1])
     assert torch.equal(ga[0], gb[0]) and torch.equal(ga[1], gb[1])
