@@ -58,12 +58,17 @@ __device__ __forceinline__ int resolve_t(int t, const int32_t* t_dev) { return t
 // (scaling, refinement FMAs, denorm-mode switches), which made replayed steps
 // VALU-bound; the difference from torch's rounding is a few ulp of the
 // ~lr-sized update term, far inside the parity tolerances (tests/).
+// Every rounding is spelled out (explicit fmaf, contraction off): the
+// compiler's own contraction choices depend on the calling context (a gradient
+// loaded from memory vs a literal 0 in the catch-up replay), and deferred ==
+// dense bit-identity needs the same operation sequence in every kernel.
 __device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, const AdamStep& s) {
+#pragma clang fp contract(off)
   const float pe = p * s.decay;
-  const float me = m + s.w1 * (g - m);
-  const float ve = v * s.beta2 + s.w2 * g * g;
-  const float denom = __builtin_amdgcn_sqrtf(ve) * s.inv_bc2 + s.eps;
-  p = pe - s.step_size * (me * __builtin_amdgcn_rcpf(denom));
+  const float me = __builtin_fmaf(s.w1, g - m, m);
+  const float ve = __builtin_fmaf(s.w2 * g, g, v * s.beta2);
+  const float denom = __builtin_fmaf(__builtin_amdgcn_sqrtf(ve), s.inv_bc2, s.eps);
+  p = __builtin_fmaf(-s.step_size, me * __builtin_amdgcn_rcpf(denom), pe);
   m = me;
   v = ve;
 }
