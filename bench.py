@@ -74,7 +74,9 @@ def parse():
     ap.add_argument('--jagged', type=int, default=1,
                     help='token-wise step over each sequence\'s span only (jagged.py; padding rows are dead in the '
                          'reference); 0 = the padded [B, T] step')
-    ap.add_argument('--jagged-quantum', type=int, default=512,
+    ap.add_argument('--step-times', type=int, default=0,
+                    help='diagnostic: per-step device intervals (events) and host issue times to stderr')
+    ap.add_argument('--jagged-quantum', type=int, default=1024,
                     help='jagged capacity granularity (rows): one GEMM plan set and one HIP graph per capacity')
     return ap.parse_args()
 
@@ -518,8 +520,15 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
+    evs, host = [], []
     for i in range(a.steps):
+        th = time.perf_counter()
         loss = step(i)
+        if a.step_times:
+            host.append(time.perf_counter() - th)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            evs.append(e)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -529,6 +538,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     final_loss = float(loss.float().item())
+    if a.step_times and rank == 0:
+        dev_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(len(evs) - 1)]
+        caps_i = [J.capacity_for(rows[i % len(pool)], a.jagged_quantum) if jagged else 0 for i in range(a.steps)]
+        print('# step device intervals (ms) / host issue (ms) / capacity:', file=sys.stderr)
+        for i, d in enumerate(dev_ms):
+            print(f'  {i + 1:3d} {d:7.3f} {1e3 * host[i + 1]:7.3f} {caps_i[i + 1]}', file=sys.stderr)
 
     if not trace:  # --warmup 0: trace one extra, untimed eager step after the timed region
         G.GATHER_TRACE, K.BACKWARD_TRACE = [], []

@@ -40,6 +40,7 @@ class Sites(TorchDispatchMode):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=128)
+    ap.add_argument('--jagged', type=int, default=1)
     a = ap.parse_args()
     from tencent_recommendation_2025_amd import synthetic as S
     from tencent_recommendation_2025_amd.model import BaselineModel, init_reference_
@@ -50,7 +51,7 @@ def main():
     torch.manual_seed(0)
     m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, S.make_args()).cuda()
     init_reference_(m, seed=0, live_norms=True)
-    tr = Trainer(m, FusedAdamW(m, lr=1e-3), loss='bce')
+    tr = Trainer(m, FusedAdamW(m, lr=1e-3), loss='bce', jagged=bool(a.jagged))
     g = torch.Generator(device='cuda').manual_seed(0)
     batches = [S.make_batch(cfg, g, 'cuda') for _ in range(3)]
     for i in range(3):

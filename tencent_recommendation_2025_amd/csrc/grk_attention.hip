@@ -447,28 +447,6 @@ static int launch_hd(const AttnParams& p, int which, hipStream_t s) {
   return GRK_OK;
 }
 
-// Jagged layout: zero the columns [0, cols) of the dead rows [*n, cap) of an
-// output (bf16 or fp32): they hold no token, but the row-wise ops and weight
-// gradients around the attention read every row of the buffer.
-__global__ void __launch_bounds__(256) k_zero_tail(void* __restrict__ out, int64_t ld, int cols, bool f32,
-                                                   const int64_t* __restrict__ n, int64_t cap) {
-  const int64_t r0 = *n;
-  const int64_t units = (cap - r0) * cols;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < units; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = r0 + i / cols, c = i % cols;
-    if (f32) ((float*)out)[r * ld + c] = 0.f;
-    else ((bf16_t*)out)[r * ld + c] = 0;
-  }
-}
-
-static int zero_tail(const AttnParams& p, void* out, int64_t ld, int hd, hipStream_t s) {
-  if (!p.row_base || !out) return GRK_OK;
-  k_zero_tail<<<grid_for(p.jag_cap * p.H * hd, 256, 1024), 256, 0, s>>>(out, ld, p.H * hd, p.out_f32 != 0, p.jag_n,
-                                                                         p.jag_cap);
-  GRK_LAUNCH_CHECK();
-  return GRK_OK;
-}
-
 // drab[i] += fixed-point accumulator (after the dQ kernels)
 __global__ void k_drab_finalize(float* __restrict__ drab, const unsigned long long* __restrict__ fix, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -589,8 +567,7 @@ extern "C" int grk_attention_fwd(const grk_attn_args* a, void* out, int64_t ldo,
   GRK_CHECK_ARG(out && ldo >= (int64_t)a->heads * a->head_dim, "bad out / ldo");
   GRK_CHECK_ARG(a->kind == GRK_ATTN_HSTU || lse, "softmax forward needs lse [B, H, T]");
   p.out = out; p.ldo = ldo; p.lse = lse;
-  rc = launch(p, a->head_dim, 0, (hipStream_t)stream);
-  return rc ? rc : zero_tail(p, out, ldo, a->head_dim, (hipStream_t)stream);
+  return launch(p, a->head_dim, 0, (hipStream_t)stream);
 }
 
 extern "C" int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout,
@@ -632,8 +609,6 @@ extern "C" int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, 
     }
     rc = launch(p, a->head_dim, 2, s);
     if (rc) return rc;
-    rc = zero_tail(p, dq, lddq, a->head_dim, s);
-    if (rc) return rc;
     if (p.drab) {
       k_drab_finalize<<<(nfix + 255) / 256, 256, 0, s>>>(p.drab, p.drab_fix, nfix);
       GRK_LAUNCH_CHECK();
@@ -644,11 +619,7 @@ extern "C" int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, 
       GRK_LAUNCH_CHECK();
     }
   }
-  if (!do_dkdv) return GRK_OK;
-  rc = launch(p, a->head_dim, 3, s);
-  if (rc) return rc;
-  rc = zero_tail(p, dk, lddk, a->head_dim, s);
-  return rc ? rc : zero_tail(p, dv, lddv, a->head_dim, s);
+  return do_dkdv ? launch(p, a->head_dim, 3, s) : GRK_OK;
 }
 
 extern "C" int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout,

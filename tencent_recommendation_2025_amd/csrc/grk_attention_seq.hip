@@ -381,6 +381,26 @@ __device__ __forceinline__ unsigned mask16(int kb, int hh, int lo, int hi, bool 
 __device__ __forceinline__ int pair_tile(int u, int ps, int n) { return ps == 0 ? u : n - 1 - u; }
 __device__ __forceinline__ bool pair_has(int u, int ps, int n) { return ps == 0 || n - 1 - u != u; }
 
+// Jagged layout: the dead capacity rows [n, cap) past the spans hold no token,
+// but the row-wise ops and weight gradients around the attention read every
+// row of its outputs, so each launch zeroes them there: workgroup w clears its
+// share of the tail (8-byte stores), beside its real work.
+__device__ __forceinline__ void zero_tail_rows(const AttnParams& p, void* out, int64_t ld, int hd) {
+  if (!p.row_base || !out) return;
+  const int64_t n = p.jag_n[0];
+  const int per = p.out_f32 ? 2 : 4;            // elements per 8-byte store
+  const int64_t upr = (int64_t)p.H * hd / per;  // stores per row
+  const int64_t units = (p.jag_cap - n) * upr;
+  if (units <= 0) return;
+  const int64_t chunk = (units + gridDim.x - 1) / gridDim.x;
+  const int64_t u0 = (int64_t)blockIdx.x * chunk, u1 = min(units, u0 + chunk);
+  for (int64_t u = u0 + threadIdx.x; u < u1; u += blockDim.x) {
+    const int64_t r = n + u / upr, c = (u % upr) * per;
+    void* dst = p.out_f32 ? (void*)((float*)out + r * ld + c) : (void*)((bf16_t*)out + r * ld + c);
+    *reinterpret_cast<uint2*>(dst) = make_uint2(0u, 0u);
+  }
+}
+
 // ================================================================ forward ====
 template <int HD, int KIND, int PREC>
 __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
@@ -396,6 +416,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_fwd_seq(AttnParams p) {
   const int ntiles = nq - first, npairs = (ntiles + 1) / 2;
   const int64_t rbase = p.row_base ? p.row_base[b] : (int64_t)b * T;
   const int lo = p.row_base ? start : 0;  // jagged rows: only [start, T) exist
+  zero_tail_rows(p, p.out, p.ldo, HD);
   GRK_STAMP(1);
   // prologue: every independent load in flight before the first wait
   bf16x8 qpre[KS];
@@ -560,6 +581,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
   const int bh = b * p.H + h;
   const int64_t rbase = p.row_base ? p.row_base[b] : (int64_t)b * T;
   const int lo = p.row_base ? start : 0;  // jagged rows: only [start, T) exist
+  zero_tail_rows(p, p.dq, p.lddq, HD);
   bf16x8 qpre[KS], dpre[KS];
   if (PREC < 2 && wave < npairs) {
     const int row = (first + wave) * 32 + r;
@@ -750,6 +772,8 @@ k_attn_dkdv_seq(AttnParams p) {
   const int bh = b * p.H + h;
   const int64_t rbase = p.row_base ? p.row_base[b] : (int64_t)b * T;
   const int lo = p.row_base ? start : 0;  // jagged rows: only [start, T) exist
+  zero_tail_rows(p, p.dk, p.lddk, HD);
+  zero_tail_rows(p, p.dv, p.lddv, HD);
   // key tile j (absolute first + j) visits query tiles j .. ntiles-1
   bf16x8 kpre[KS], vpre[KS];
   if (PREC < 2 && wave < npairs) {
