@@ -60,6 +60,11 @@ class GrkAttnArgs(C.Structure):
                 ('num_rows', C.c_void_p), ('capacity', C.c_int64)]
 
 
+class GrkGradRange(C.Structure):
+    _fields_ = [('row_start', C.c_int64), ('row_end', C.c_int64), ('grad', C.c_void_p), ('grad_ld', C.c_int64),
+                ('grad_dtype', C.c_int32), ('pad_', C.c_int32)]
+
+
 class GrkRowCopy(C.Structure):
     _fields_ = [('src', C.c_void_p), ('dst', C.c_void_p), ('row_bytes', C.c_int64), ('src_ld', C.c_int64),
                 ('dst_ld', C.c_int64)]
@@ -98,6 +103,7 @@ SIGNATURES = {
     'grk_table_adamw_catchup_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _I64, _P, C.c_int32, _P, _P]),
     'grk_stamp_rows_dev': (_I, [_P, _P, _P, _I64, _P, _P]),
     'grk_table_l2_norm_workspace': (_SZ, []),
+    'grk_table_adamw_ranges_dev': (_I, [_P, _I, _P, _P, _I64, _I, C.POINTER(GrkGradRange), _I, _P, C.c_int32, _P, _P]),
     'grk_table_l2_norm': (_I, [_P, _I, _I64, _I, _F, _P, _P, _P, _SZ, _P]),
     'grk_table_adamw_l2_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _P, _I64, _P, _P, C.c_int32, _P, _P, _P]),
     'grk_attention_fwd': (_I, [C.POINTER(GrkAttnArgs), _P, _I64, _P, _P]),

@@ -253,6 +253,50 @@ __global__ void __launch_bounds__(256) k_adamw_dense_grad(P* __restrict__ param,
   adam_vec<P, NV>(param + off, m + off, v + off, g, adam_step(resolve(hpa)));
 }
 
+// Several dense gradients over row ranges of one table in ONE launch (the
+// feature tables of the `small` group get their gradients as dense [rows, D]
+// blocks through the dnn projections): rows covered by a range take its
+// gradient (bf16 or fp32, own row stride), rows between ranges g = 0 -- the
+// update of k_adamw_dense_grad / k_adamw_dense per row, one launch instead of
+// one per range (each ~5 us of launch in a captured step).
+constexpr int kMaxGradRanges = 64;
+struct GradRanges {
+  grk_grad_range r[kMaxGradRanges];
+  int n;
+};
+
+template <typename P, int NV>
+__global__ void __launch_bounds__(256) k_adamw_ranges(P* __restrict__ param, float* __restrict__ m,
+                                                      float* __restrict__ v, int64_t num_rows, int dim, GradRanges gr,
+                                                      HpArg hpa) {
+  const int q = dim / NV;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= num_rows * q) return;
+  const int64_t row = i / q;
+  const int c = (int)(i - row * q) * NV;
+  int lo = 0, hi = gr.n;  // first range whose end is past row (ranges sorted, disjoint)
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (gr.r[mid].row_end <= row) lo = mid + 1;
+    else hi = mid;
+  }
+  float g[NV];
+#pragma unroll
+  for (int e = 0; e < NV; ++e) g[e] = 0.f;
+  if (lo < gr.n && gr.r[lo].row_start <= row) {
+    const grk_grad_range& rr = gr.r[lo];
+    const int64_t off = (row - rr.row_start) * rr.grad_ld + c;
+    if (rr.grad_dtype == GRK_F32) {
+      load_grad<NV>(reinterpret_cast<const float*>(rr.grad) + off, g);
+    } else {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) g[e] = bf16_to_f32(reinterpret_cast<const bf16_t*>(rr.grad)[off + e]);
+    }
+  }
+  const int64_t off = row * dim + c;
+  adam_vec<P, NV>(param + off, m + off, v + off, g, adam_step(resolve(hpa)));
+}
+
 // Catch-up (deferred dense-parity updates): one wave per row; lane 0 claims
 // the row (last[row] <- t) so duplicate ids replay it once; the skipped g = 0
 // steps (last, t] are replayed in registers with each step's hyper-parameters,
@@ -544,6 +588,47 @@ extern "C" int grk_table_l2_norm(const void* param, int param_dtype, int64_t num
   else k_table_sumsq<float><<<kNormBlocks, 256, 0, s>>>((const float*)param, n, part);
   GRK_LAUNCH_CHECK();
   k_table_norm_final<<<1, 256, 0, s>>>(part, l2, norm, l2_coef);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+extern "C" int grk_table_adamw_ranges_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
+                                          int64_t num_rows, int dim, const grk_grad_range* ranges, int num_ranges,
+                                          const grk_adamw_hparams* hp_ring, int32_t ring_len, const int32_t* t_dev,
+                                          void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(num_rows >= 0, "num_rows must be >= 0");
+  if (num_rows == 0) return GRK_OK;
+  GRK_CHECK_ARG(param && exp_avg && exp_avg_sq, "param / exp_avg / exp_avg_sq required");
+  GRK_CHECK_ARG(param_dtype == GRK_F32 || param_dtype == GRK_BF16, "bad param dtype");
+  GRK_CHECK_ARG(dim > 0 && dim % 4 == 0, "dim must be a multiple of 4");
+  GRK_CHECK_ARG(hp_ring && t_dev && ring_len > 0, "hp_ring / t_dev / ring_len required");
+  GRK_CHECK_ARG(num_ranges >= 0 && num_ranges <= kMaxGradRanges, "num_ranges must be in [0, %d]", kMaxGradRanges);
+  GradRanges gr;
+  memset(&gr, 0, sizeof(gr));
+  gr.n = num_ranges;
+  bool v8 = dim % 8 == 0;
+  int64_t prev_end = 0;
+  for (int i = 0; i < num_ranges; ++i) {
+    const grk_grad_range& r = ranges[i];
+    GRK_CHECK_ARG(r.grad && r.row_start >= prev_end && r.row_end > r.row_start && r.row_end <= num_rows,
+                  "range %d: rows [%lld, %lld) must be sorted, disjoint, non-empty and inside the table", i,
+                  (long long)r.row_start, (long long)r.row_end);
+    GRK_CHECK_ARG(r.grad_dtype == GRK_F32 || r.grad_dtype == GRK_BF16, "range %d: bad grad dtype", i);
+    GRK_CHECK_ARG(r.grad_ld >= dim && r.grad_ld % 4 == 0, "range %d: grad_ld must be >= dim, multiple of 4", i);
+    v8 = v8 && r.grad_ld % 8 == 0;
+    prev_end = r.row_end;
+    gr.r[i] = r;
+  }
+  const int64_t work = num_rows * (dim / (v8 ? 8 : 4));
+  GRK_CHECK_ARG((work + 255) / 256 < (int64_t)1 << 31, "table too large for one launch");
+  const unsigned g = (unsigned)((work + 255) / 256);
+  hipStream_t s = (hipStream_t)stream;
+  const HpArg hp = on_device(hp_ring, ring_len, t_dev);
+#define GRK_RG(P, NV) k_adamw_ranges<P, NV><<<g, 256, 0, s>>>((P*)param, exp_avg, exp_avg_sq, num_rows, dim, gr, hp)
+  if (param_dtype == GRK_BF16) { if (v8) GRK_RG(bf16_t, 8); else GRK_RG(bf16_t, 4); }
+  else { if (v8) GRK_RG(float, 8); else GRK_RG(float, 4); }
+#undef GRK_RG
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }

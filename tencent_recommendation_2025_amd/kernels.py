@@ -223,6 +223,24 @@ def table_adamw(param, exp_avg, exp_avg_sq, hp, ids=None, rows=None, count=None,
     L.check(rc, 'grk_table_adamw')
 
 
+def table_adamw_ranges(param, exp_avg, exp_avg_sq, clock, ranges):
+    """Dense-parity AdamW of a whole table from dense gradient blocks in ONE launch
+    (grk_table_adamw_ranges_dev): ranges = [(row_offset, grad [rows, >= D] bf16/fp32)],
+    other rows g = 0."""
+    _require_cuda(param, exp_avg, exp_avg_sq, *[g for _, g in ranges])
+    rows, D = param.shape
+    rs = sorted(ranges, key=lambda r: r[0])
+    arr = (L.GrkGradRange * max(1, len(rs)))()
+    for i, (off, g) in enumerate(rs):
+        if g.dim() != 2 or g.stride(1) != 1 or g.shape[1] < D:
+            raise L.GrkError(f'range {i}: grad must be a row-major [n, >= {D}] matrix')
+        arr[i] = L.GrkGradRange(int(off), int(off) + g.shape[0], g.data_ptr(), g.stride(0), L.dtype_code(g.dtype), 0)
+    rc = L.lib().grk_table_adamw_ranges_dev(param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(),
+                                            exp_avg_sq.data_ptr(), rows, D, arr, len(rs), clock.ring.data_ptr(),
+                                            clock.ring_len, clock.t.data_ptr(), L.stream_ptr(param.device))
+    L.check(rc, 'grk_table_adamw_ranges_dev')
+
+
 def table_l2_norm(param, l2, norm=None, coef=None):
     """(norm fp32 [1], l2 / norm fp32 [1]) of a whole table (grk_table_l2_norm):
     the l2_emb term's value and gradient scale, on the device."""

@@ -29,6 +29,7 @@ import ctypes as C
 from . import _lib as L
 from . import functional as G
 from . import kernels as K
+from .streams import run_branches
 
 
 class TableGroup:
@@ -131,7 +132,7 @@ class FusedAdamW:
     """AdamW over a BaselineModel: table groups on grk kernels, dense params on torch fused AdamW."""
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
-                 table_dtype=torch.bfloat16, groups=DEFAULT_GROUPS, defer_period=16, l2_emb=0.0):
+                 table_dtype=torch.bfloat16, groups=DEFAULT_GROUPS, defer_period=16, l2_emb=0.0, parallel=True):
         """l2_emb > 0: the BaseLine script's ``loss += l2_emb * ||item_emb.weight||_F``
         (model/BaseLine/main.py:184-185) -- ``l2_term()`` gives the loss term (Trainer
         adds it), ``step()`` adds its gradient l2 * W / ||W|| to every item row.  Every
@@ -139,6 +140,7 @@ class FusedAdamW:
         if table_mode not in ('dense', 'lazy'):
             raise ValueError("table_mode must be 'dense' or 'lazy'")
         self.l2_emb = float(l2_emb)
+        self.parallel = bool(parallel)  # step(): independent updates as parallel stream branches
         if self.l2_emb and table_mode == 'lazy':
             raise ValueError('l2_emb moves every item row each step: it needs table_mode="dense"')
         self.model = model
@@ -299,43 +301,62 @@ class FusedAdamW:
         self.t += 1
         if self.clock is not None:
             self.clock.advance()
-        self.dense.step()
         hp = self.clock if self.clock is not None else self._hp(self.t)
-        for g in self.groups:
-            if g.name in self._deferred:
-                if begun:  # rows outside the batch stay deferred; the batch rows move now
-                    if g.pending:
-                        res = K.embedding_backward(g.pending, g.rows, g.dim, padding_idx=0, token_type=g.token_type,
-                                                   seq_len=g.seq_len, dense=False, sparse=True, row_slot=g.row_slot)
-                        K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, res.ids, res.rows, res.count,
-                                      res.capacity, g.row_slot, lazy=True)
-                        K.stamp_rows(g.last, res.ids, res.count, res.capacity, self.clock)
-                    g.clear()
-                    continue
-                g.last.fill_(self.t)  # dense update below moves every row
-            if g is self._l2_group:  # every row: its sparse gradient + l2 * p / ||W||
-                res = None
+        # the dense AdamW and every table group's reduction + update are independent
+        # chains of (mostly small) kernels: on the GPU they run as parallel branches
+        # (private streams forked from and joined into the step's stream)
+        work = [self.dense.step] + [self._group_work(g, hp, begun) for g in self.groups]
+        dev = self.groups[0].flat.device if self.groups else torch.device('cpu')
+        if self.parallel and self.clock is not None:
+            run_branches(work, dev)
+        else:
+            for f in work:
+                f()
+
+    def _group_work(self, g, hp, begun):
+        """The update of one table group this step, as a closure (run_branches)."""
+        def work():
+            self._group_step(g, hp, begun)
+        return work
+
+    def _group_step(self, g, hp, begun):
+        if g.name in self._deferred:
+            if begun:  # rows outside the batch stay deferred; the batch rows move now
                 if g.pending:
                     res = K.embedding_backward(g.pending, g.rows, g.dim, padding_idx=0, token_type=g.token_type,
                                                seq_len=g.seq_len, dense=False, sparse=True, row_slot=g.row_slot)
-                if g.dense_grads:
-                    raise RuntimeError('l2_emb: the item table takes row-sparse gradients only')
-                if res is None:
-                    K.table_adamw_l2(g.flat, g.exp_avg, g.exp_avg_sq, self.clock, self._l2_coef)
-                else:
-                    K.table_adamw_l2(g.flat, g.exp_avg, g.exp_avg_sq, self.clock, self._l2_coef, res.ids, res.rows,
-                                     res.count, res.capacity, g.row_slot)
+                    K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, res.ids, res.rows, res.count,
+                                  res.capacity, g.row_slot, lazy=True)
+                    K.stamp_rows(g.last, res.ids, res.count, res.capacity, self.clock)
                 g.clear()
-                continue
-            if g.dense_grads and not g.pending:  # dense gradients only: per-range updates
-                g.step_dense_ranges(hp)
-            elif g.dense_grads:  # mixed: one dense fp32 gradient
-                K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, None, g.dense_gradient(), None, 0, g.identity())
-            elif g.pending:
+                return
+            g.last.fill_(self.t)  # dense update below moves every row
+        if g is self._l2_group:  # every row: its sparse gradient + l2 * p / ||W||
+            res = None
+            if g.pending:
                 res = K.embedding_backward(g.pending, g.rows, g.dim, padding_idx=0, token_type=g.token_type,
                                            seq_len=g.seq_len, dense=False, sparse=True, row_slot=g.row_slot)
-                K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, res.ids, res.rows, res.count, res.capacity,
-                              None if self.lazy else g.row_slot, lazy=self.lazy)
-            elif not self.lazy:
-                K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp)
+            if g.dense_grads:
+                raise RuntimeError('l2_emb: the item table takes row-sparse gradients only')
+            if res is None:
+                K.table_adamw_l2(g.flat, g.exp_avg, g.exp_avg_sq, self.clock, self._l2_coef)
+            else:
+                K.table_adamw_l2(g.flat, g.exp_avg, g.exp_avg_sq, self.clock, self._l2_coef, res.ids, res.rows,
+                                 res.count, res.capacity, g.row_slot)
             g.clear()
+            return
+        if g.dense_grads and not g.pending and isinstance(hp, K.DeviceClock) \
+                and len(g.dense_grads) <= 64:  # dense gradient blocks only: one multi-range launch
+            K.table_adamw_ranges(g.flat, g.exp_avg, g.exp_avg_sq, hp, list(g.dense_grads.items()))
+        elif g.dense_grads and not g.pending:  # dense gradients only: per-range updates
+            g.step_dense_ranges(hp)
+        elif g.dense_grads:  # mixed: one dense fp32 gradient
+            K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, None, g.dense_gradient(), None, 0, g.identity())
+        elif g.pending:
+            res = K.embedding_backward(g.pending, g.rows, g.dim, padding_idx=0, token_type=g.token_type,
+                                       seq_len=g.seq_len, dense=False, sparse=True, row_slot=g.row_slot)
+            K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp, res.ids, res.rows, res.count, res.capacity,
+                          None if self.lazy else g.row_slot, lazy=self.lazy)
+        elif not self.lazy:
+            K.table_adamw(g.flat, g.exp_avg, g.exp_avg_sq, hp)
+        g.clear()

@@ -27,30 +27,14 @@ import torch
 
 from . import functional as G
 from . import jagged as J
-
-
-_PRIVATE_STREAMS = {}
+from . import streams as S
 
 
 def private_stream(device):
-    """The process's own side stream for ``device`` (grk_stream_create), wrapped
-    as a torch stream.  torch.cuda.Stream() hands out pooled streams round-robin,
-    so it can return the very stream a process group records its collectives'
-    events on; a HIP graph captured on that stream makes the NCCL watchdog's
-    query of those events fail (hipErrorCapturedEvent: "event last recorded in a
-    capturing stream"), which it treats as fatal.  Created
-    once per device, never destroyed (lives as long as the process)."""
-    import ctypes
-    from . import _lib as L
-    dev = torch.device(device)
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    s = _PRIVATE_STREAMS.get(idx)
-    if s is None:
-        with torch.cuda.device(idx):
-            raw = ctypes.c_void_p()
-            L.check(L.lib().grk_stream_create(ctypes.byref(raw)), 'grk_stream_create')
-            s = _PRIVATE_STREAMS[idx] = torch.cuda.ExternalStream(raw.value, device=torch.device('cuda', idx))
-    return s
+    """The process's own capture stream for ``device`` (streams.private_stream):
+    never one of torch's pooled streams, which a process group may record its
+    collectives' events on."""
+    return S.private_stream(device, 0)
 
 
 def _tensors(batch):
