@@ -132,7 +132,7 @@ class FusedAdamW:
     """AdamW over a BaselineModel: table groups on grk kernels, dense params on torch fused AdamW."""
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
-                 table_dtype=torch.bfloat16, groups=DEFAULT_GROUPS, defer_period=16, l2_emb=0.0, parallel=True):
+                 table_dtype=torch.bfloat16, groups=DEFAULT_GROUPS, defer_period=16, l2_emb=0.0, parallel=False):
         """l2_emb > 0: the BaseLine script's ``loss += l2_emb * ||item_emb.weight||_F``
         (model/BaseLine/main.py:184-185) -- ``l2_term()`` gives the loss term (Trainer
         adds it), ``step()`` adds its gradient l2 * W / ||W|| to every item row.  Every
@@ -140,7 +140,11 @@ class FusedAdamW:
         if table_mode not in ('dense', 'lazy'):
             raise ValueError("table_mode must be 'dense' or 'lazy'")
         self.l2_emb = float(l2_emb)
-        self.parallel = bool(parallel)  # step(): independent updates as parallel stream branches
+        # parallel=True: step()'s independent updates as parallel stream branches.  Off by
+        # default: measured on MI355X / ROCm 7.2, a captured step with these branches
+        # replays SLOWER (6.6 vs 5.0 ms per step, host issue spikes of 10 ms) -- the
+        # multi-stream graph costs more than the overlap of the small kernels saves
+        self.parallel = bool(parallel)
         if self.l2_emb and table_mode == 'lazy':
             raise ValueError('l2_emb moves every item row each step: it needs table_mode="dense"')
         self.model = model
