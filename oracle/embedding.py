@@ -70,6 +70,35 @@ def dense_backward(grad: np.ndarray, idx: np.ndarray, num_rows: int,
     return out
 
 
+def chunked_backward(grad: np.ndarray, idx: np.ndarray, num_rows: int, padding_idx: int | None = 0,
+                     chunk: int = 256) -> np.ndarray:
+    """The fixed chunk order of grk_embedding_backward(GRK_BWD_CHUNKED) -- no
+    reference counterpart (used only for intermediates such as the fused
+    trainer's projected feature rows, whose reference gradient is dE = sum dY W).
+
+    Occurrences are stably sorted by row (padding dropped) and cut into
+    ``chunk``-entry chunks; each (row, chunk) piece is summed in occurrence
+    order from zero, and a row's pieces are added in chunk order.
+    """
+    idx = np.asarray(idx, dtype=np.int64).reshape(-1)
+    g = np.asarray(grad, dtype=np.float32).reshape(idx.shape[0], -1)
+    keep = idx != padding_idx if padding_idx is not None else np.ones_like(idx, bool)
+    idx, g = idx[keep], g[keep]
+    order = np.argsort(idx, kind='stable')
+    keys, rows = idx[order], g[order]
+    n = len(keys)
+    out = np.zeros((num_rows, g.shape[1]), dtype=np.float32)
+    if n == 0:
+        return out
+    piece_key = keys * ((n + chunk - 1) // chunk) + np.arange(n) // chunk
+    heads = np.concatenate([[True], piece_key[1:] != piece_key[:-1]])
+    pid = np.cumsum(heads) - 1
+    pieces = np.zeros((int(pid[-1]) + 1, g.shape[1]), dtype=np.float32)
+    np.add.at(pieces, pid, rows)
+    np.add.at(out, keys[heads], pieces)
+    return out
+
+
 def multi_source_backward(sources, num_rows: int, padding_idx: int | None = 0) -> np.ndarray:
     """Sum of several lookups of ONE table (item table: seq, pos, neg calls).
 

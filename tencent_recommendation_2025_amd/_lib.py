@@ -26,6 +26,7 @@ GRK_F32, GRK_BF16, GRK_F16 = 0, 1, 2
 GRK_F32_BF16 = 3  # pair logits: fp32 h, bf16 item embeddings
 GRK_FP8_E4M3 = 4  # attention q/k/v: OCP fp8 e4m3
 GRK_I32, GRK_I64 = 0, 1
+BWD_ORDERED, BWD_CHUNKED = 0, 1  # grk_embedding_backward flags
 IDX_PLAIN, IDX_ITEM_MASK, IDX_USER_MASK, IDX_POSITION = 0, 1, 2, 3
 ADAM_DENSE, ADAM_LAZY = 0, 1
 MAX_FEATURES = 48
@@ -93,7 +94,7 @@ SIGNATURES = {
     'grk_sort_pairs_workspace': (_SZ, [_I64]),
     'grk_sort_pairs': (_I, [_P, _P, _P, _P, _P, _P, _I64, _I, _P, _SZ, _P]),
     'grk_embedding_backward': (_I, [C.POINTER(GrkLookup), _I, _I, _I, _I, _P, C.c_int32, _I64, _I64, _P, _P, _P,
-                                    _P, _P, _P, _SZ, _P, _P]),
+                                    _P, _P, _I, _P, _SZ, _P, _P]),
     'grk_table_adamw': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _P, _I64, _P, GrkAdamwHparams, _I, _P]),
     'grk_table_adamw_dense': (_I, [_P, _I, _P, _P, _I64, _I, _P, _I, _I64, GrkAdamwHparams, _P]),
     'grk_table_adamw_catchup': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _I64, _P, C.c_int32, C.c_int32, _P]),

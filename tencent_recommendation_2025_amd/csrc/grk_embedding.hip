@@ -350,8 +350,8 @@ __device__ __forceinline__ void seg_chunks_wave_body(int64_t chunk, int lane, co
                                                      const int* __restrict__ pos, const int* __restrict__ seg_start,
                                                      const int* __restrict__ seg_end, int64_t n, unsigned sentinel,
                                                      int dim, float* __restrict__ dense_out,
-                                                     float* __restrict__ uniq_rows,
-                                                     int32_t* __restrict__ row_slot) {
+                                                     float* __restrict__ uniq_rows, int32_t* __restrict__ row_slot,
+                                                     float* __restrict__ partials = nullptr) {
   constexpr int VEC = LW;
   constexpr int KP = kRedChunk / 64;  // chunk entries per lane
   const int64_t p0 = chunk * kRedChunk;
@@ -380,7 +380,15 @@ __device__ __forceinline__ void seg_chunks_wave_body(int64_t chunk, int lane, co
   int u = __builtin_amdgcn_readfirstlane(pr[0]) - 1;
   auto flush = [&]() {
     const bool whole = (ps > p0 || kprev != cur) && (pe < p1 || knext != cur);
-    if (whole) store_final(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
+    if (whole) {
+      store_final(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
+    } else if (partials) {  // chunked mode: the piece's sum goes to the chunk's head (0) or tail (1) slot
+      const int slot = (ps == p0 && kprev == cur) ? 0 : 1;
+      float* dst = partials + (chunk * 2 + slot) * dim + c;
+#pragma unroll
+      for (int e = 0; e < LW; e += 4)
+        *reinterpret_cast<float4*>(dst + e) = make_float4(acc.v[e], acc.v[e + 1], acc.v[e + 2], acc.v[e + 3]);
+    }
     // else: a row crossing an edge -- k_seg_combine_edges (<= 2*kRedChunk) or k_seg_hot sums it
   };
   bool done = false;
@@ -489,6 +497,81 @@ __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __res
                                                            int32_t* __restrict__ row_slot) {
   seg_edge_body<G, LW>((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, keys, gptr, pos, seg_start,
                        seg_end, n, sentinel, dim, dense_out, uniq_rows, row_slot);
+}
+
+// ------------------------------------------- chunked (fixed-order) mode ----
+// GRK_BWD_CHUNKED: for tables whose rows are an intermediate with no reference
+// counterpart (the projected feature rows P = E W of the fused trainer: the
+// reference's gradient is dE = sum dY W, accumulated in a different order
+// anyway), rows crossing chunk edges are not re-summed in occurrence order:
+// every chunk stores the sums of its edge-crossing pieces (head piece: the
+// row continuing from the previous chunk -> slot 0, tail piece: the row
+// continuing into the next -> slot 1), and one wave per such row adds its
+// pieces in chunk order.  Deterministic (fixed order), and a hot row of k
+// occurrences costs k / kRedChunk dependent adds instead of k.
+template <typename G, int LW>
+__global__ void __launch_bounds__(256) k_seg_chunks_partial(const unsigned* __restrict__ keys,
+                                                            const unsigned long long* __restrict__ gptr,
+                                                            const int* __restrict__ pos,
+                                                            const int* __restrict__ seg_start,
+                                                            const int* __restrict__ seg_end, int64_t n,
+                                                            unsigned sentinel, int dim, float* __restrict__ dense_out,
+                                                            float* __restrict__ uniq_rows,
+                                                            int32_t* __restrict__ row_slot,
+                                                            float* __restrict__ partials) {
+  seg_chunks_wave_body<G, LW>((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, keys, gptr, pos,
+                              seg_start, seg_end, n, sentinel, dim, dense_out, uniq_rows, row_slot, partials);
+}
+
+// One wave per chunk edge b: the row first crossing b (it starts in chunk
+// b - 1, whose tail slot holds its first piece) = tail(b - 1) + head(b) + ...
+// + head(last chunk of the row), added in that order.
+template <int LW>
+__global__ void __launch_bounds__(256) k_seg_partials_combine(const unsigned* __restrict__ keys,
+                                                              const int* __restrict__ pos,
+                                                              const int* __restrict__ seg_start,
+                                                              const int* __restrict__ seg_end, int64_t n,
+                                                              unsigned sentinel, int dim,
+                                                              const float* __restrict__ partials,
+                                                              float* __restrict__ dense_out,
+                                                              float* __restrict__ uniq_rows,
+                                                              int32_t* __restrict__ row_slot) {
+  constexpr int PIPE = 8;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) + 1;
+  const int64_t pb = b * kRedChunk;
+  if (pb >= n) return;
+  const unsigned key = keys[pb];
+  if (key == sentinel || keys[pb - 1] != key) return;
+  const int u = pos[pb] - 1;
+  const int su = seg_start[u], eu = seg_end[u];
+  if (su / kRedChunk != b - 1) return;  // crosses an earlier edge: combined there
+  const int64_t last = (eu - 1) / kRedChunk;
+  const int c = lane * LW;
+  WaveAcc<LW> acc;
+  const float* t = partials + ((b - 1) * 2 + 1) * dim + c;
+#pragma unroll
+  for (int e = 0; e < LW; ++e) acc.v[e] = t[e];
+  for (int64_t k0 = b; k0 <= last; k0 += PIPE) {
+    float4 r[PIPE][LW / 4];
+#pragma unroll
+    for (int j = 0; j < PIPE; ++j)
+      if (k0 + j <= last)
+#pragma unroll
+        for (int e = 0; e < LW / 4; ++e)
+          r[j][e] = *reinterpret_cast<const float4*>(partials + (k0 + j) * 2 * dim + c + 4 * e);
+#pragma unroll
+    for (int j = 0; j < PIPE; ++j)
+      if (k0 + j <= last)
+#pragma unroll
+        for (int e = 0; e < LW / 4; ++e) {
+          acc.v[4 * e] += r[j][e].x;
+          acc.v[4 * e + 1] += r[j][e].y;
+          acc.v[4 * e + 2] += r[j][e].z;
+          acc.v[4 * e + 3] += r[j][e].w;
+        }
+  }
+  store_final(acc, key, u, dim, c, dense_out, uniq_rows, row_slot);
 }
 
 // ------------------------------------------------------------- hot rows ----
@@ -718,6 +801,7 @@ struct BwdWs {
   unsigned *keys_in, *keys_out, *seg_key;
   int *flags, *pos, *seg_start, *seg_end;
   unsigned long long *gptr_in, *gptr_out;
+  float* partials;  // chunked mode: [chunks][2][dim] piece sums
   void* sort_tmp;
   size_t sort_bytes;
   void* scan_tmp;
@@ -743,6 +827,7 @@ static int plan_ws(int64_t n, int64_t num_rows, int dim, char* base, BwdWs* ws) 
   ws->seg_end = (int*)take(n * 4);
   ws->gptr_in = (unsigned long long*)take(n * 8);
   ws->gptr_out = (unsigned long long*)take(n * 8);
+  ws->partials = (float*)take((size_t)((n + kRedChunk - 1) / kRedChunk) * 2 * dim * sizeof(float));
   unsigned end_bit = 1;
   while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
   size_t sb = 0, cb = 0;
@@ -820,9 +905,10 @@ extern "C" size_t grk_embedding_backward_workspace(int64_t num_occurrences, int6
 extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups, int dim, int grad_dtype,
                                       int itype, const int32_t* token_type, int32_t seq_len, int64_t num_rows,
                                       int64_t padding_idx, float* dense_out, int64_t* uniq_ids, float* uniq_rows,
-                                      int32_t* uniq_count, int32_t* row_slot, void* workspace,
+                                      int32_t* uniq_count, int32_t* row_slot, int flags, void* workspace,
                                       size_t workspace_bytes, int32_t* err_flag, void* stream) {
   clear_error();
+  GRK_CHECK_ARG(flags == GRK_BWD_ORDERED || flags == GRK_BWD_CHUNKED, "bad flags %d", flags);
   GRK_CHECK_ARG(lookups && num_lookups > 0, "need at least one lookup");
   GRK_CHECK_ARG(grad_dtype == GRK_F32 || grad_dtype == GRK_BF16, "grad_dtype must be GRK_F32 or GRK_BF16");
   GRK_CHECK_ARG(itype == GRK_I32 || itype == GRK_I64, "bad itype");
@@ -912,6 +998,22 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   if ((grad_dtype == GRK_BF16 && lw == 8) || (grad_dtype != GRK_BF16 && (lw == 4 || lw == 8))) {
     const unsigned gw = (unsigned)((chunks + 3) / 4);
     const unsigned ge = (unsigned)(chunks > 1 ? (chunks - 1 + 3) / 4 : 0);
+    if (flags == GRK_BWD_CHUNKED) {
+#define GRK_SEGP(G, LW)                                                                                         \
+  k_seg_chunks_partial<G, LW><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end,    \
+                                                 total, sentinel, dim, dense_out, uniq_rows, row_slot,         \
+                                                 ws.partials);                                                 \
+  GRK_LAUNCH_CHECK();                                                                                           \
+  if (ge)                                                                                                       \
+    k_seg_partials_combine<LW><<<ge, 256, 0, s>>>(ws.keys_out, ws.pos, ws.seg_start, ws.seg_end, total,         \
+                                                  sentinel, dim, ws.partials, dense_out, uniq_rows, row_slot)
+      if (grad_dtype == GRK_BF16) { GRK_SEGP(bf16_t, 8); }
+      else if (lw == 8) { GRK_SEGP(float, 8); }
+      else { GRK_SEGP(float, 4); }
+#undef GRK_SEGP
+      GRK_LAUNCH_CHECK();
+      return GRK_OK;
+    }
 #define GRK_SEGW(G, LW)                                                                                              \
   k_seg_chunks_wave<G, LW><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,     \
                                               sentinel, dim, dense_out, uniq_rows, row_slot);                        \

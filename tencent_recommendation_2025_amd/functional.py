@@ -25,11 +25,14 @@ GATHER_TRACE = None
 class TableRef:
     """Where a lookup's rows live: a plain table weight (drop-in: dense
     autograd gradient) or a row range of a TableGroup (fused optimizer:
-    row-sparse gradient collected by the group's sink)."""
-    __slots__ = ('weight', 'group', 'row_offset')
+    row-sparse gradient collected by the group's sink).  ``chunked``: the
+    weight is an intermediate whose row gradients may be summed in the
+    chunked fixed order (K.embedding_backward); honoured when every
+    drop-in table of a fused lookup allows it."""
+    __slots__ = ('weight', 'group', 'row_offset', 'chunked')
 
-    def __init__(self, weight, group=None, row_offset=0):
-        self.weight, self.group, self.row_offset = weight, group, row_offset
+    def __init__(self, weight, group=None, row_offset=0, chunked=False):
+        self.weight, self.group, self.row_offset, self.chunked = weight, group, row_offset, chunked
 
 
 class LookupSpec:
@@ -96,7 +99,8 @@ class _FeatureLookupFn(torch.autograd.Function):
                 src = [K.GradSource(s.idx, g, c, s.mode, s.bag, offs[id(s.ref.weight)], s.ref.weight.shape[0])
                        for s, g, c in dense]
                 res = K.embedding_backward(src, total, D, padding_idx=0, token_type=ctx.token_type,
-                                           seq_len=ctx.seq_len, dense=True)
+                                           seq_len=ctx.seq_len, dense=True,
+                                           chunked=all(s.ref.chunked for s, _, _ in dense))
                 by_id = {k: res.dense[offs[k]:offs[k] + w.shape[0]].to(w.dtype) for k, w in tables.items()}
             else:
                 by_id = {k: None for k in tables}

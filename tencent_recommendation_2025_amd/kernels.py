@@ -110,17 +110,19 @@ BACKWARD_TRACE = None  # bench.py: a list records the embedding_backward calls o
 
 
 def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, seq_len=0, dense=True,
-                       sparse=False, row_slot=None, err_flag=None):
+                       sparse=False, row_slot=None, err_flag=None, chunked=False):
     """Deterministic scatter-add table gradient (grk_embedding_backward).
 
     Returns a ``BackwardResult`` with ``dense`` ([num_rows, dim] fp32) when
     ``dense`` and ``ids``/``rows``/``count`` (row-sparse form, capacity =
-    number of occurrences) when ``sparse``.
+    number of occurrences) when ``sparse``.  ``chunked``: rows spanning several
+    chunks of the sorted occurrences are added chunk-sum by chunk-sum
+    (GRK_BWD_CHUNKED; fixed order, not the occurrence order).
     """
     if BACKWARD_TRACE is not None:
         BACKWARD_TRACE.append(dict(sources=list(sources), num_rows=num_rows, dim=dim, padding_idx=padding_idx,
                                    token_type=token_type, seq_len=seq_len, dense=dense, sparse=sparse,
-                                   row_slot=None if row_slot is None else row_slot.clone()))
+                                   row_slot=None if row_slot is None else row_slot.clone(), chunked=chunked))
     dev = sources[0].grad.device
     gdt = sources[0].grad.dtype
     it = sources[0].idx.dtype
@@ -156,7 +158,8 @@ def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, s
     rc = L.lib().grk_embedding_backward(lk, len(sources), dim, L.dtype_code(gdt), L.itype_code(it),
                                         _ptr(token_type), seq_len, num_rows, -1 if padding_idx is None else padding_idx,
                                         _ptr(dense_out), _ptr(ids), _ptr(rows), count.data_ptr(), _ptr(row_slot),
-                                        ws.data_ptr(), ws.numel(), _ptr(err_flag), L.stream_ptr(dev))
+                                        L.BWD_CHUNKED if chunked else L.BWD_ORDERED, ws.data_ptr(), ws.numel(),
+                                        _ptr(err_flag), L.stream_ptr(dev))
     L.check(rc, 'grk_embedding_backward')
     return BackwardResult(dense_out, ids, rows, count, cap)
 

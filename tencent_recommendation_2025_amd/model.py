@@ -472,7 +472,9 @@ class BaselineModel(torch.nn.Module):
             nonlocal col
             P, offs = self._projection(which)
             idx = self._proj_index(feats, names, offs, N)
-            specs.append(G.LookupSpec(G.TableRef(P), idx, col, L.IDX_PLAIN, idx.shape[1]))
+            # P = E W is an intermediate: its row sums may use the chunked order (the
+            # reference accumulates dE = sum dY W, in no order P's sums could match)
+            specs.append(G.LookupSpec(G.TableRef(P, chunked=True), idx, col, L.IDX_PLAIN, idx.shape[1]))
             splits.append((col, col + d))
             col += d
 

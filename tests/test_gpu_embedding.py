@@ -272,6 +272,50 @@ def test_hot_rows_bit_exact(K):
     assert np.array_equal(a.dense.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize('D,dt', [(512, torch.bfloat16), (256, torch.float32), (512, torch.float32)])
+def test_backward_chunked_mode(K, D, dt):
+    """GRK_BWD_CHUNKED (projected feature rows of the fused trainer): rows
+    inside one chunk bit-exact in occurrence order as before, rows spanning
+    chunks equal to the oracle's chunk-order restatement bit for bit (hot rows
+    of 600-30000 occurrences, rows of <= 512 crossing one edge, a row filling
+    whole chunks); within fp32 rounding of the occurrence-order sums;
+    deterministic; row-sparse outputs and row_slot consistent."""
+    rng = np.random.default_rng(5)
+    R = 3000
+    idx = np.concatenate([np.full(30000, 5), np.full(600, 7), np.full(1031, 8), np.full(256, 9),
+                          np.repeat(np.arange(10, 20), rng.integers(300, 513, 10)),
+                          rng.integers(20, R, 20000), np.zeros(2000, np.int64)])
+    rng.shuffle(idx)
+    g = rng.standard_normal((len(idx), 2 * D)).astype(np.float32)
+    if dt == torch.bfloat16:
+        g = oemb.to_bf16_f32(g)
+    gt = T(g).to(dt)
+    rev = idx[::-1].copy()
+    src = [K.GradSource(T(idx), gt, 0), K.GradSource(T(rev), gt, D)]
+    slot = torch.full((R,), -1, dtype=torch.int32, device=DEV)
+    res = K.embedding_backward(src, R, D, dense=True, sparse=True, chunked=True, row_slot=slot)
+    gg = np.concatenate([g[:, :D], g[:, D:]])
+    ii = np.concatenate([idx, rev])
+    got = res.dense.cpu().numpy()
+    assert np.array_equal(got, oemb.chunked_backward(gg, ii, R))
+    exact = oemb.dense_backward(gg, ii, R)
+    np.testing.assert_allclose(got, exact, rtol=1e-4, atol=1e-3)
+    counts = np.bincount(ii, minlength=R)
+    small = (counts > 0) & (counts <= 20)
+    small[0] = False
+    assert small.sum() > 1000
+    # rows of a handful of occurrences sit in one chunk unless they straddle an edge
+    assert np.mean(np.all(got[small] == exact[small], axis=1)) > 0.9
+    cnt = int(res.count.item())
+    uniq = oemb.unique_rows(ii)
+    assert cnt == len(uniq) and np.array_equal(res.ids[:cnt].cpu().numpy(), uniq)
+    assert np.array_equal(res.rows[:cnt].cpu().numpy(), got[uniq])
+    s = slot.cpu().numpy()
+    assert np.array_equal(s[uniq], np.arange(cnt)) and np.all(np.delete(s, uniq) == -1)
+    again = K.embedding_backward(src, R, D, dense=True, chunked=True).dense
+    assert torch.equal(again, res.dense)
+
+
 # ------------------------------------------------ occurrence sort (grk_sort) --
 @pytest.mark.parametrize('n,end_bit,card', [(1, 1, 2), (4095, 8, 200), (4097, 9, 300), (70001, 16, 40000),
                                             (200000, 21, 1000001), (150000, 21, 10), (33333, 32, 1 << 31)])

@@ -158,3 +158,36 @@ def test_bce_oracle_equals_torch():
     tl.backward()
     np.testing.assert_allclose(tl.item(), loss, rtol=1e-12)
     np.testing.assert_allclose(th.grad.numpy(), dh, rtol=1e-9, atol=1e-12)
+
+
+def test_chunked_backward_restatement():
+    """oracle.embedding.chunked_backward: equals the occurrence-order backward
+    when every row sits inside one 256-entry chunk, and a piecewise sum of
+    the same occurrences (checked in float64) otherwise."""
+    from oracle import embedding as oemb
+    rng = np.random.default_rng(0)
+    idx = np.sort(rng.integers(1, 40, 200))            # 200 sorted occurrences: one chunk
+    rng.shuffle(idx)
+    g = rng.standard_normal((200, 8)).astype(np.float32)
+    assert np.array_equal(oemb.chunked_backward(g, idx, 40), oemb.dense_backward(g, idx, 40))
+    idx = np.concatenate([np.full(1000, 3), rng.integers(0, 50, 3000)])
+    rng.shuffle(idx)
+    g = rng.standard_normal((len(idx), 8)).astype(np.float32)
+    got = oemb.chunked_backward(g, idx, 50)
+    want = np.zeros((50, 8))
+    np.add.at(want, idx, g.astype(np.float64))
+    want[0] = 0
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-4)
+    # row 3 (1000 occurrences after the rows 0-2 ahead of it) = its chunk pieces added in order
+    keys = np.sort(idx[idx != 0], kind='stable')
+    order = np.argsort(idx[idx != 0], kind='stable')
+    rows3 = g[idx != 0][order][keys == 3]
+    first = int(np.searchsorted(keys, 3))
+    cuts = [c * 256 - first for c in range(first // 256 + 1, (first + 1000) // 256 + 1)]
+    acc = np.float32(0)
+    for part in np.split(rows3, cuts):
+        s = np.zeros(8, np.float32)
+        for r in part:
+            s = s + r
+        acc = acc + s
+    assert np.array_equal(got[3], acc)
