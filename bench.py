@@ -11,9 +11,10 @@ rank per GPU over RCCL); tables are row-sharded, dense grads all-reduced;
 every rank processes its own 128 sequences (weak scaling).
 
 Prints ONE JSON line (rank 0) with the metric, the live roofline of the
-dominant hand-written kernel (attention dK/dV; HBM-bound at this shape), the
-other attention kernels and the fused gather under `rooflines`, and the CPU
-baseline (oracle/model_ref.py, the fp32 torch-CPU restatement of
+dominant hand-written kernel (the one with the most device time per step:
+average launch x launches per step), every other measured kernel under
+`rooflines` (attention, gathers, wgrad, sampled softmax, embedding backward;
+each with PMC `traffic` from profiles/), and the CPU baseline (oracle/model_ref.py, the fp32 torch-CPU restatement of
 the same model and step, on a bounded sample).
 """
 from __future__ import annotations
@@ -59,7 +60,7 @@ def parse():
                     help='distinct device-resident batches cycled by the timed steps (16 x ~41k item rows x 1 KiB '
                          '~ 0.7 GB: more than the 256 MB Infinity Cache, so rows are not re-read warm)')
     ap.add_argument('--cpu-batch', type=int, default=128)
-    ap.add_argument('--cpu-steps', type=int, default=2)
+    ap.add_argument('--cpu-steps', type=int, default=10)
     ap.add_argument('--roofline-reps', type=int, default=20)
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='gloo: rehearse N ranks on fewer GPUs (collectives staged via host)')
@@ -94,7 +95,7 @@ def _time(fn, reps):
     return e0.elapsed_time(e1) / reps
 
 
-PMC_TAG = 'r2s4'  # round tag of the committed PMC summaries (scripts/pmc_rooflines.py)
+PMC_TAG = 'r3'  # round tag of the committed PMC summaries (scripts/pmc_rooflines.py)
 
 
 def _pmc(name, match):
@@ -179,7 +180,7 @@ def attention_rooflines(a, key_valid, reps, jagged=False):
                'traffic': None, 'alg_bytes_per_launch': int(nbytes), 'flops_per_launch': int(flops),
                'tflops': round(tfs, 1), 'mfma_frac': round(tfs / BF16_PEAK_TFLOPS, 4),
                'arith_intensity': round(ai, 1), 'ridge': round(ridge, 1), 'avg_launch_us': round(ms * 1e3, 2),
-               'workload': workload}
+               'calls_per_step': a.blocks, 'ms_per_step': round(ms * a.blocks, 4), 'workload': workload}
         p = _pmc(pmc_name, workload)
         if p is not None:
             res['traffic'] = int(p['traffic_bytes_per_launch'])
@@ -218,6 +219,7 @@ def gather_roofline(trace, reps):
     res = {'bound': 'l2/infinity-cache', 'kernel': 'grk::k_gather (seq-side fused lookup)',
            'achieved': round(alg / (ms * 1e-3) / 1e9, 1), 'peak': None, 'unit': 'GB/s', 'frac': None,
            'traffic': None, 'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2),
+           'calls_per_step': 1, 'ms_per_step': round(ms, 4),
            'rows_per_launch': int(rows), 'features': len(lookups),
            'workload': {'tokens': int(n), 'rows': int(rows), 'features': len(lookups)}}
     p = _pmc(f'{PMC_TAG}_pmc_gather.json', res['workload'])
@@ -275,44 +277,133 @@ def item_gather_roofline(table, batch, reps):
     return res
 
 
-def backward_roofline(trace, reps):
-    """The largest embedding-table gradient of one step (grk_embedding_backward:
-    key build, stable radix sort, segment bounds, in-order segmented
-    reduction incl. the hot-row kernel), the whole call timed alone with HIP
-    events, the step's own arguments.  Algorithmic bytes per SURVEY.md 8(d)
-    and VERDICT r1: every occurrence's gradient row read once (D x e) + its
-    index, every unique row's fp32 sum written once (D x 4 + 8 B id)."""
+def _source_rows_read(s, token_type):
+    """Distinct upstream gradient rows one lookup reads: its tokens with at least
+    one non-padding row in the bag (a bag's slots share one gradient row)."""
+    idx = s.idx.reshape(s.grad.shape[0], -1)
+    live = (idx != 0).any(1)
+    if s.mode in (1, 2) and token_type is not None:          # IDX_ITEM_MASK / IDX_USER_MASK
+        live &= token_type.reshape(-1)[:live.numel()] == s.mode
+    return int(live.sum().item())
+
+
+def backward_rooflines(trace, reps):
+    """grk_embedding_backward (key build, stable radix sort, segment bounds,
+    segmented reduction: every launch of the call), timed alone with HIP
+    events on the step's own arguments, for two calls of one step:
+
+    * the item-table group (1M rows, row-sparse output): seq / pos / neg item
+      rows -- the HBM-bound one;
+    * the projected feature rows P (dense output, GRK_BWD_CHUNKED), the call
+      with the most occurrences.
+
+    Algorithmic bytes count DISTINCT data: each distinct upstream
+    gradient row read once (a bag's slots and a row's repeated lookups re-read
+    the same row, from cache), 8-B / 4-B indices per occurrence, and the output
+    written once (dense: the whole [rows, D] fp32 gradient; sparse: unique
+    rows x (D x 4 + 8 B id)).  The replays run last in bench.py, item call
+    first (scripts/pmc_rooflines.py attributes the PMC windows by that order)."""
     from tencent_recommendation_2025_amd import kernels as K
-    call = max(trace, key=lambda c: sum(s.idx.numel() for s in c['sources']))
+    out = []
+    item = [c for c in trace if c['sparse'] and not c.get('chunked')]
+    proj = [c for c in trace if c.get('chunked')]
+    picks = []
+    if item:
+        picks.append(('item', max(item, key=lambda c: c['num_rows']), 1))
+    if proj:
+        picks.append(('projected', max(proj, key=lambda c: sum(s.idx.numel() for s in c['sources'])), len(proj)))
+    for kind, call, per_step in picks:
+        def run(call=call):
+            kw = dict(call)
+            rs = kw.pop('row_slot')
+            return K.embedding_backward(row_slot=None if rs is None else rs.clone(), **kw)
 
-    def run():
-        kw = dict(call)
-        rs = kw.pop('row_slot')
-        return K.embedding_backward(row_slot=None if rs is None else rs.clone(), **kw)
+        res = run()
+        srcs = call['sources']
+        occ = sum(s.idx.numel() for s in srcs)
+        D = call['dim']
+        es = srcs[0].grad.element_size()
+        isz = srcs[0].idx.element_size()
+        uniq = int(res.count.item())
+        seen, rows_read = set(), 0
+        for s in srcs:
+            key = (s.grad.data_ptr(), s.grad_col, s.grad.shape[0])
+            if key not in seen:
+                seen.add(key)
+                rows_read += _source_rows_read(s, call['token_type'])
+        written = call['num_rows'] * D * 4 if call['dense'] else uniq * (D * 4 + 8)
+        alg = rows_read * D * es + occ * isz + written
+        ms = _time(run, reps)
+        gbps = alg / (ms * 1e-3) / 1e9
+        res = {'bound': 'hbm',
+               'kernel': f'grk_embedding_backward ({kind} '
+                         + ('item-table group, row-sparse' if kind == 'item' else 'feature rows P, dense, chunked')
+                         + ' gradient: all launches of the call)',
+               'achieved': round(gbps, 1), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
+               'frac': round(gbps / HBM_PEAK_GBPS, 4), 'traffic': None, 'alg_bytes_per_launch': int(alg),
+               'avg_launch_us': round(ms * 1e3, 2), 'calls_per_step': per_step,
+               'ms_per_step': round(ms * per_step, 4), 'pmc_calls': reps + 2,   # run() + _time's 1 + reps
+               'alg_bytes_note': 'distinct upstream gradient rows read once + indices + output written once',
+               'workload': {'table': kind, 'occurrences': int(occ), 'distinct_grad_rows': int(rows_read),
+                            'unique_rows': uniq, 'table_rows': int(call['num_rows']), 'D': D,
+                            'grad_dtype': str(srcs[0].grad.dtype), 'lookups': len(srcs)}}
+        p = _pmc(f'{PMC_TAG}_pmc_emb_bwd_{kind}.json', res['workload'])
+        if p is not None:
+            res['traffic'] = int(p['traffic_bytes_per_launch'])
+            res['traffic_note'] = (f'rocprofv3 PMC (profiles/{PMC_TAG}_pmc_emb_bwd_{kind}.json): FETCH_SIZE x2 + '
+                                   'WRITE_SIZE summed over the launches of one call')
+        out.append(res)
+    return out
 
-    res = run()
-    occ = sum(s.idx.numel() for s in call['sources'])
-    es = call['sources'][0].grad.element_size()
-    isz = call['sources'][0].idx.element_size()
-    uniq = int(res.count.item())
-    D = call['dim']
-    ms = _time(run, reps)
-    alg = occ * (D * es + isz) + uniq * (D * 4 + 8)
-    gbps = alg / (ms * 1e-3) / 1e9
-    return {'bound': 'hbm', 'kernel': 'grk_embedding_backward (largest table-group gradient of the step, all launches)',
-            'achieved': round(gbps, 1), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': round(gbps / HBM_PEAK_GBPS, 4),
-            'traffic': None, 'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2),
-            'workload': {'occurrences': int(occ), 'unique_rows': uniq, 'table_rows': int(call['num_rows']), 'D': D,
-                         'grad_dtype': str(call['sources'][0].grad.dtype), 'lookups': len(call['sources'])}}
+
+def ss_rooflines(batch, a, reps):
+    """The in-batch sampled softmax of the bench batch (north star; grk_sampled_
+    softmax_fwd / _bwd, every launch of each call), bf16 h / e of the valid
+    positions, timed alone with HIP events.  MFMA-bound: nv valid positions,
+    algorithmic FLOPs fwd 2 nv^2 D (the logits; the LSE is fused), bwd 6 nv^2 D
+    (logits recomputed + dH = P E + dE = P^T H).  calls_per_step: 1 with
+    --loss sampled_softmax, else 0 (the BCE step does not run it)."""
+    from tencent_recommendation_2025_amd import kernels as K
+    seq, pos, ntt = batch[0], batch[1], batch[4]
+    B, T = seq.shape
+    D = a.hidden
+    dev = seq.device
+    g = torch.Generator(device=dev).manual_seed(11)
+    h = (0.1 * torch.randn(B * T, D, device=dev, generator=g)).bfloat16()
+    e = (0.1 * torch.randn(B * T, D, device=dev, generator=g)).bfloat16()
+    ids = pos.reshape(-1).long().contiguous()
+    valid = (ntt.reshape(-1) == 1).to(torch.uint8).contiguous()
+    nv = int(valid.sum().item())
+    loss, lse2, _ = K.sampled_softmax_fwd(h, e, ids, valid, 0.05)
+    t_f = _time(lambda: K.sampled_softmax_fwd(h, e, ids, valid, 0.05), reps)
+    t_b = _time(lambda: K.sampled_softmax_bwd(h, e, ids, valid, 0.05, lse2), reps)
+    per_step = 1 if a.loss == 'sampled_softmax' else 0
+    out = []
+    for name, ms, flops, alg, calls in (('fwd', t_f, 2.0 * nv * nv * D, 2 * nv * D * 2 + 8 * nv, reps + 2),
+                                        ('bwd', t_b, 6.0 * nv * nv * D, 2 * nv * D * 2 + 2 * nv * D * 4 + 12 * nv,
+                                         reps + 1)):
+        tfs = flops / (ms * 1e-3) / 1e12
+        res = {'bound': 'mfma', 'kernel': f'grk::k_ss_{name} (in-batch sampled softmax {name}, all launches)',
+               'achieved': round(tfs, 1), 'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+               'frac': round(tfs / BF16_PEAK_TFLOPS, 4), 'traffic': None, 'flops_per_launch': int(flops),
+               'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2), 'calls_per_step': per_step,
+               'ms_per_step': round(ms * per_step, 4), 'pmc_calls': calls,
+               'workload': {'valid_positions': nv, 'D': D, 'pass': name}}
+        p = _pmc(f'{PMC_TAG}_pmc_ss_{name}.json', res['workload'])
+        if p is not None:
+            res['traffic'] = int(p['traffic_bytes_per_launch'])
+        out.append(res)
+    return out
 
 
-def wgrad_roofline(a, reps):
+def wgrad_roofline(a, reps, k):
     """grk_wgrad on the largest weight gradient of the step: the HSTU uvqk
-    projection (dW [4D, D] = dY^T X over K = B*T tokens, + bias gradient),
-    timed alone (HIP events; k_wgrad + its in-order slice reduction).  MFMA
-    bound: algorithmic FLOPs 2*K*M*N."""
+    projection (dW [4D, D] = dY^T X over the K token rows the step holds --
+    B*T padded, the jagged capacity otherwise -- + bias gradient), timed alone
+    (HIP events; k_wgrad + its in-order slice reduction).  MFMA bound:
+    algorithmic FLOPs 2*K*M*N."""
     from tencent_recommendation_2025_amd import kernels as K
-    k, m, n = a.batch * (a.maxlen + 1), 4 * a.hidden, a.hidden
+    m, n = 4 * a.hidden, a.hidden
     g = torch.Generator(device='cuda').manual_seed(0)
     dy = torch.randn(k, m, device='cuda', generator=g).bfloat16()
     x = torch.randn(k, n, device='cuda', generator=g).bfloat16()
@@ -323,6 +414,7 @@ def wgrad_roofline(a, reps):
            'achieved': round(tf, 1), 'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
            'frac': round(tf / BF16_PEAK_TFLOPS, 4), 'traffic': None, 'flops_per_launch': int(flops),
            'alg_bytes_per_launch': int(2 * k * (m + n) + 4 * m * (n + 1)), 'avg_launch_us': round(ms * 1e3, 2),
+           'calls_per_step': a.blocks, 'ms_per_step': round(ms * a.blocks, 4),
            'workload': {'K': int(k), 'M': int(m), 'N': int(n)}}
     p = _pmc(f'{PMC_TAG}_pmc_wgrad.json', res['workload'])
     if p is not None:
@@ -370,16 +462,23 @@ def cpu_baseline(a, stats, types):
         opt.step()
 
     step(batches[0])
-    t0 = time.perf_counter()
+    times = []
     for b in batches[1:]:
+        t0 = time.perf_counter()
         step(b)
-    dt = time.perf_counter() - t0
+        times.append(time.perf_counter() - t0)
+    dt = sum(times)
     n = a.cpu_batch * a.cpu_steps
-    return {'value': round(n / dt, 3), 'unit': 'seq/s', 'cores': cores, 'kind': 'port', 'cpu_model': model_name,
+    rates = sorted(a.cpu_batch / t for t in times)
+    mean = n / dt
+    sd = (sum((r - mean) ** 2 for r in rates) / max(len(rates) - 1, 1)) ** 0.5
+    return {'value': round(mean, 3), 'unit': 'seq/s', 'cores': cores, 'kind': 'port', 'cpu_model': model_name,
+            'per_step_seq_s': {'min': round(rates[0], 3), 'median': round(rates[len(rates) // 2], 3),
+                               'max': round(rates[-1], 3), 'stdev': round(sd, 3), 'steps': len(rates)},
             'sample': f'{a.cpu_steps} timed steps x B={a.cpu_batch} of the same model/config/loss '
                       f'(fp32 CPU, full {a.items}-row item table, dense AdamW, dropout {a.dropout}), after 1 warmup step, '
-                      f'{cores} threads on {model_name}; {dt:.1f} s (BASELINE.md 3 asks 10 + 50 steps: bounded '
-                      f'here to keep the bench within minutes)'}
+                      f'{cores} threads on {model_name}; {dt:.1f} s (BASELINE.md 3 asks 10 warmup + 50 timed steps: '
+                      f'bounded to keep the bench within minutes)'}
 
 
 FP32_VALU_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector (packed FMA)
@@ -551,16 +650,24 @@ def main():
         trace, G.GATHER_TRACE = G.GATHER_TRACE, None
         btrace, K.BACKWARD_TRACE = K.BACKWARD_TRACE, None
     kv = (pool[0][3] != 0).to(torch.uint8)        # the first bench batch's key validity (token_type != 0)
-    roof, more = attention_rooflines(a, kv, a.roofline_reps, jagged=jagged)
+    dkdv, more = attention_rooflines(a, kv, a.roofline_reps, jagged=jagged)
+    more.insert(0, dkdv)
     more.append(gather_roofline(trace, a.roofline_reps))
     item_table = model.item_emb.weight if model.item_emb.weight.numel() else None
     if item_table is not None:
         more.append(item_gather_roofline(item_table.detach(), pool[0], a.roofline_reps))
-    more.append(wgrad_roofline(a, a.roofline_reps))
-    if btrace:
-        more.append(backward_roofline(btrace, a.roofline_reps))
+    wk = J.capacity_for(rows[0], a.jagged_quantum) if jagged else a.batch * (a.maxlen + 1)
+    more.append(wgrad_roofline(a, a.roofline_reps, wk))
+    more.extend(ss_rooflines(pool[0], a, a.roofline_reps))
+    if btrace:   # last: scripts/pmc_rooflines.py finds these calls' PMC windows at the end of the run
+        more.extend(backward_rooflines(btrace, a.roofline_reps))
     if sid_roof is not None:
         more.append(sid_roof)
+    # headline: the hand-written hot-path kernel with the most device time per step
+    # (average launch x launches per step), with an HBM or MFMA roof
+    ranked = [r for r in more if r.get('peak') and r.get('ms_per_step')]
+    roof = max(ranked, key=lambda r: r['ms_per_step'])
+    more.remove(roof)
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline and not a.semantic_ids:   # config 2's CPU model only

@@ -55,16 +55,70 @@ def traffic(needle, pick_largest_grid=False):
     return 2 * f * 1024, w * 1024, min(nf, nw)
 
 
+def dispatches(rows):
+    """[(dispatch id, kernel name, value)] in dispatch order (per-instance rows summed)."""
+    key = next(k for k in ('Dispatch_Id', 'Correlation_Id', 'Kernel_Id') if k in rows[0])
+    by, names = {}, {}
+    for r in rows:
+        by[r[key]] = by.get(r[key], 0.0) + float(r['Counter_Value'])
+        names[r[key]] = r['Kernel_Name']
+    return [(int(k), names[k], by[k]) for k in sorted(by, key=int)]
+
+
+def call_windows(rows, start, members, lead=()):
+    """Counter totals of each multi-launch call: a call opens at a `start`
+    kernel (with the `lead` kernels right before it, e.g. its zero fills) and
+    takes every following `members` kernel until the next call."""
+    calls, pending = [], 0.0
+    for _, name, v in dispatches(rows):
+        if any(m in name for m in lead):
+            pending += v
+        elif start in name:
+            calls.append(pending + v)
+            pending = 0.0
+        elif any(m in name for m in members) and calls:
+            calls[-1] += v
+        else:
+            pending = 0.0
+    return calls
+
+
+BWD = dict(start='k_build_keys', lead=('k_zero_fill',),
+           members=('k_sort_', 'k_head_', 'k_segments', 'k_seg_'))
+SS = dict(start='k_ss_compact', members=('k_ss_',))
+
+
+def window_traffic(family, group, calls):
+    """Traffic of entry `group` of a family whose entries made calls[i] calls
+    each, in order, at the very end of the run (bench.py's `pmc_calls`): the
+    last `reps` calls of the entry are averaged."""
+    out = []
+    for rows in (fetch, write):
+        w = call_windows(rows, **family)
+        end = len(w) - sum(calls[group + 1:])
+        mine = w[end - calls[group]:end][-reps:]
+        out.append(sum(mine) / len(mine))
+    return 2 * out[0] * 1024, out[1] * 1024, reps
+
+
+bwd_entries = [e for e in entries if e['kernel'].startswith('grk_embedding_backward')]
+ss_entries = [e for e in entries if e['kernel'].startswith('grk::k_ss_')]
 for e in entries:
     k = e['kernel'].split()[0].replace('grk::', '')
-    if k.startswith('k_attn'):
+    if k == 'grk_embedding_backward':
+        fb, wb, n = window_traffic(BWD, bwd_entries.index(e), [x['pmc_calls'] for x in bwd_entries])
+        name = f"{tag}_pmc_emb_bwd_{e['workload']['table']}.json"
+    elif k.startswith('k_ss_'):
+        fb, wb, n = window_traffic(SS, ss_entries.index(e), [x['pmc_calls'] for x in ss_entries])
+        name = f"{tag}_pmc_ss_{e['workload']['pass']}.json"
+    elif k.startswith('k_attn'):
         fb, wb, n = traffic(k + '<')
         name = f"{tag}_pmc_attn_{k[len('k_attn_'):-len('_seq')]}_{e['workload']['kind']}.json"
     elif k == 'k_gather' and 'item-table' in e['kernel']:
-        fb, wb, n = traffic('k_gather')  # the last launches of the run: the item-table roofline's
+        fb, wb, n = traffic('k_gather<')  # the last launches of the run: the item-table roofline's
         name = f'{tag}_pmc_gather_item.json'
     elif k == 'k_gather':
-        fb, wb, n = traffic('k_gather', True)  # widest launch: the seq-side fused lookup
+        fb, wb, n = traffic('k_gather<', True)  # widest launch: the seq-side fused lookup
         name = f'{tag}_pmc_gather.json'
     elif k == 'k_wgrad':
         # one grk_wgrad call = k_wgrad + k_wgrad_reduce; the last launches are the roofline's
