@@ -344,7 +344,7 @@ struct WaveAcc {
   }
 };
 
-template <typename G, int LW>
+template <typename G, int LW, int CH = kRedChunk>
 __device__ __forceinline__ void seg_chunks_wave_body(int64_t chunk, int lane, const unsigned* __restrict__ keys,
                                                      const unsigned long long* __restrict__ gptr,
                                                      const int* __restrict__ pos, const int* __restrict__ seg_start,
@@ -353,10 +353,10 @@ __device__ __forceinline__ void seg_chunks_wave_body(int64_t chunk, int lane, co
                                                      float* __restrict__ uniq_rows, int32_t* __restrict__ row_slot,
                                                      float* __restrict__ partials = nullptr) {
   constexpr int VEC = LW;
-  constexpr int KP = kRedChunk / 64;  // chunk entries per lane
-  const int64_t p0 = chunk * kRedChunk;
+  constexpr int KP = CH / 64;  // chunk entries per lane
+  const int64_t p0 = chunk * CH;
   if (p0 >= n) return;
-  const int64_t p1 = min(n, p0 + kRedChunk);
+  const int64_t p1 = min(n, p0 + CH);
   const int c = lane * VEC;
   unsigned kr[KP], glo[KP], ghi[KP];
   int pr[KP];
@@ -389,7 +389,7 @@ __device__ __forceinline__ void seg_chunks_wave_body(int64_t chunk, int lane, co
       for (int e = 0; e < LW; e += 4)
         *reinterpret_cast<float4*>(dst + e) = make_float4(acc.v[e], acc.v[e + 1], acc.v[e + 2], acc.v[e + 3]);
     }
-    // else: a row crossing an edge -- k_seg_combine_edges (<= 2*kRedChunk) or k_seg_hot sums it
+    // else: a row crossing an edge -- k_seg_combine_edges (<= 2*CH) or k_seg_hot sums it
   };
   bool done = false;
 #pragma unroll
@@ -448,7 +448,7 @@ __device__ __forceinline__ void seq_sum_wave(WaveAcc<LW>& acc, const unsigned lo
   }
 }
 
-template <typename G, int LW>
+template <typename G, int LW, int CH>
 __global__ void __launch_bounds__(256) k_seg_chunks_wave(const unsigned* __restrict__ keys,
                                                          const unsigned long long* __restrict__ gptr,
                                                          const int* __restrict__ pos, const int* __restrict__ seg_start,
@@ -456,14 +456,14 @@ __global__ void __launch_bounds__(256) k_seg_chunks_wave(const unsigned* __restr
                                                          int dim, float* __restrict__ dense_out,
                                                          float* __restrict__ uniq_rows,
                                                          int32_t* __restrict__ row_slot) {
-  seg_chunks_wave_body<G, LW>((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, keys, gptr, pos,
+  seg_chunks_wave_body<G, LW, CH>((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, keys, gptr, pos,
                               seg_start, seg_end, n, sentinel, dim, dense_out, uniq_rows, row_slot);
 }
 
 // One wave per chunk edge b (occurrence b * kRedChunk): finishes the row that
 // first crosses a chunk edge at b, i.e. crosses b and starts in chunk b - 1,
 // when it has at most 2 * kRedChunk occurrences (longer rows: k_seg_hot).
-template <typename G, int LW>
+template <typename G, int LW, int CH = kRedChunk>
 __device__ __forceinline__ void seg_edge_body(int64_t edge, int lane, const unsigned* __restrict__ keys,
                                               const unsigned long long* __restrict__ gptr,
                                               const int* __restrict__ pos, const int* __restrict__ seg_start,
@@ -471,14 +471,14 @@ __device__ __forceinline__ void seg_edge_body(int64_t edge, int lane, const unsi
                                               float* __restrict__ dense_out, float* __restrict__ uniq_rows,
                                               int32_t* __restrict__ row_slot) {
   const int64_t b = edge + 1;
-  const int64_t pb = b * kRedChunk;
+  const int64_t pb = b * CH;
   if (pb >= n) return;
   const unsigned key = keys[pb];
   if (key == sentinel || keys[pb - 1] != key) return;
   const int u = pos[pb] - 1;
   const int su = seg_start[u], eu = seg_end[u];
-  if (su / kRedChunk != b - 1) return;  // also crosses an earlier edge: finished there
-  if (eu - su > 2 * kRedChunk) return;  // hot row: k_seg_hot
+  if (su / CH != b - 1) return;  // also crosses an earlier edge: finished there
+  if (eu - su > 2 * CH) return;  // hot row: k_seg_hot
   const int c = lane * LW;
   WaveAcc<LW> acc;
   acc.zero();
@@ -486,7 +486,7 @@ __device__ __forceinline__ void seg_edge_body(int64_t edge, int lane, const unsi
   store_final(acc, key, u, dim, c, dense_out, uniq_rows, row_slot);
 }
 
-template <typename G, int LW>
+template <typename G, int LW, int CH>
 __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __restrict__ keys,
                                                            const unsigned long long* __restrict__ gptr,
                                                            const int* __restrict__ pos,
@@ -495,7 +495,7 @@ __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __res
                                                            unsigned sentinel, int dim, float* __restrict__ dense_out,
                                                            float* __restrict__ uniq_rows,
                                                            int32_t* __restrict__ row_slot) {
-  seg_edge_body<G, LW>((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, keys, gptr, pos, seg_start,
+  seg_edge_body<G, LW, CH>((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, keys, gptr, pos, seg_start,
                        seg_end, n, sentinel, dim, dense_out, uniq_rows, row_slot);
 }
 
@@ -606,7 +606,7 @@ __host__ __device__ constexpr int kHotImgBytes() {
 }
 
 // bx = chunk edge - 1 (the wave's former blockIdx.x), by = column slice
-template <typename G>
+template <typename G, int CH = kRedChunk>
 __device__ __forceinline__ void seg_hot_body(int64_t bx, int by, int lane, unsigned char* __restrict__ img,
                                              const unsigned* __restrict__ keys,
                                              const unsigned long long* __restrict__ gptr,
@@ -629,13 +629,13 @@ __device__ __forceinline__ void seg_hot_body(int64_t bx, int by, int lane, unsig
   constexpr int S = 32 / IPT;        // tiles in flight
   static_assert(IMG_ROWS * ROWB == kHotImgBytes<G>(), "hot-row image size");
   const int64_t b = bx + 1;  // chunk edge: the row that first crosses it
-  const int64_t pb = b * kRedChunk;
+  const int64_t pb = b * CH;
   if (pb >= n) return;
   const unsigned key = keys[pb];
   if (key == sentinel || keys[pb - 1] != key) return;
   const int u = pos[pb] - 1;
   const int su = seg_start[u], eu = seg_end[u];
-  if (su / kRedChunk != b - 1 || eu - su <= 2 * kRedChunk) return;
+  if (su / CH != b - 1 || eu - su <= 2 * CH) return;
   const int c0 = by * SLICE;
   const int cols = min(SLICE, dim - c0);
   const int wv = (lane % LPO) * EPV;                     // this lane's columns [wv, wv + EPV) of the slice
@@ -764,7 +764,7 @@ __global__ void __launch_bounds__(64) k_seg_hot(const unsigned* __restrict__ key
 // rows' sequential chains (tens of us, a few waves) then run beside the other
 // waves instead of after them; the three write disjoint rows (a row is
 // finished by exactly one of them).
-template <typename G, int LW>
+template <typename G, int LW, int CH>
 __global__ void __launch_bounds__(256) k_seg_wave_fused(int64_t nhot, int nslices, int64_t nchunks,
                                                         const unsigned* __restrict__ keys,
                                                         const unsigned long long* __restrict__ gptr,
@@ -778,13 +778,13 @@ __global__ void __launch_bounds__(256) k_seg_wave_fused(int64_t nhot, int nslice
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t item = (int64_t)blockIdx.x * 4 + wave;
   if (item < nhot)
-    seg_hot_body<G>(item / nslices, (int)(item % nslices), lane, img[wave], keys, gptr, pos, seg_start, seg_end, n,
+    seg_hot_body<G, CH>(item / nslices, (int)(item % nslices), lane, img[wave], keys, gptr, pos, seg_start, seg_end, n,
                     sentinel, dim, dense_out, uniq_rows, row_slot);
   else if (item < nhot + nchunks)
-    seg_chunks_wave_body<G, LW>(item - nhot, lane, keys, gptr, pos, seg_start, seg_end, n, sentinel, dim, dense_out,
+    seg_chunks_wave_body<G, LW, CH>(item - nhot, lane, keys, gptr, pos, seg_start, seg_end, n, sentinel, dim, dense_out,
                                 uniq_rows, row_slot);
   else
-    seg_edge_body<G, LW>(item - nhot - nchunks, lane, keys, gptr, pos, seg_start, seg_end, n, sentinel, dim,
+    seg_edge_body<G, LW, CH>(item - nhot - nchunks, lane, keys, gptr, pos, seg_start, seg_end, n, sentinel, dim,
                          dense_out, uniq_rows, row_slot);
 }
 
@@ -840,6 +840,35 @@ static int plan_ws(int64_t n, int64_t num_rows, int dim, char* base, BwdWs* ws) 
   ws->scan_bytes = cb;
   ws->scan_tmp = take(cb);
   ws->total = off;
+  return GRK_OK;
+}
+
+// Ordered-mode wave path with CH-entry chunks: hot-row items, chunks and edges
+// in one launch (k_seg_wave_fused) when rows longer than 2 CH can exist.
+constexpr int64_t kSmallChunkLimit = 1 << 17;
+
+template <typename G, int LW, int CH>
+static int wave_ordered(const BwdWs& ws, int64_t total, unsigned sentinel, int dim, float* dense_out,
+                        float* uniq_rows, int32_t* row_slot, hipStream_t s) {
+  const int64_t chunks = (total + CH - 1) / CH;
+  if (total > 2 * CH) {
+    const int nsl = (dim + kHotSlice<G>() - 1) / kHotSlice<G>();
+    const int64_t nhot = (chunks - 1) * nsl;
+    const unsigned gf = (unsigned)((nhot + chunks + (chunks - 1) + 3) / 4);
+    k_seg_wave_fused<G, LW, CH><<<gf, 256, 0, s>>>(nhot, nsl, chunks, ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start,
+                                                   ws.seg_end, total, sentinel, dim, dense_out, uniq_rows, row_slot);
+    GRK_LAUNCH_CHECK();
+    return GRK_OK;
+  }
+  k_seg_chunks_wave<G, LW, CH><<<(unsigned)((chunks + 3) / 4), 256, 0, s>>>(
+      ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel, dim, dense_out, uniq_rows, row_slot);
+  GRK_LAUNCH_CHECK();
+  if (chunks > 1) {
+    k_seg_combine_edges<G, LW, CH><<<(unsigned)((chunks - 1 + 3) / 4), 256, 0, s>>>(
+        ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel, dim, dense_out, uniq_rows,
+        row_slot);
+    GRK_LAUNCH_CHECK();
+  }
   return GRK_OK;
 }
 
@@ -1014,36 +1043,20 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
       GRK_LAUNCH_CHECK();
       return GRK_OK;
     }
-#define GRK_SEGW(G, LW)                                                                                              \
-  k_seg_chunks_wave<G, LW><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total,     \
-                                              sentinel, dim, dense_out, uniq_rows, row_slot);                        \
-  GRK_LAUNCH_CHECK();                                                                                                \
-  if (ge)                                                                                                            \
-    k_seg_combine_edges<G, LW><<<ge, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, \
-                                                  sentinel, dim, dense_out, uniq_rows, row_slot)
-    if (total > 2 * kRedChunk) {
-      // hot-row items, chunks and edges in one launch (k_seg_wave_fused)
-      const int64_t nedges = chunks - 1;
-#define GRK_SEGF(G, LW)                                                                                           \
-  do {                                                                                                            \
-    const int nsl = (dim + kHotSlice<G>() - 1) / kHotSlice<G>();                                                  \
-    const int64_t nhot = (chunks - 1) * nsl;                                                                      \
-    const unsigned gf = (unsigned)((nhot + chunks + nedges + 3) / 4);                                             \
-    k_seg_wave_fused<G, LW><<<gf, 256, 0, s>>>(nhot, nsl, chunks, ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, \
-                                               ws.seg_end, total, sentinel, dim, dense_out, uniq_rows, row_slot); \
-  } while (0)
-      if (grad_dtype == GRK_BF16) GRK_SEGF(bf16_t, 8);
-      else if (lw == 8) GRK_SEGF(float, 8);
-      else GRK_SEGF(float, 4);
-#undef GRK_SEGF
-      GRK_LAUNCH_CHECK();
-      return GRK_OK;
+    // occurrence-order mode: chunks of 64 for short lists (more waves in flight
+    // on calls of a few 10k mostly-distinct rows: the item / user tables),
+    // 256 otherwise
+    int rc;
+    if (total <= kSmallChunkLimit) {
+      if (grad_dtype == GRK_BF16) rc = wave_ordered<bf16_t, 8, 64>(ws, total, sentinel, dim, dense_out, uniq_rows, row_slot, s);
+      else if (lw == 8) rc = wave_ordered<float, 8, 64>(ws, total, sentinel, dim, dense_out, uniq_rows, row_slot, s);
+      else rc = wave_ordered<float, 4, 64>(ws, total, sentinel, dim, dense_out, uniq_rows, row_slot, s);
+    } else {
+      if (grad_dtype == GRK_BF16) rc = wave_ordered<bf16_t, 8, kRedChunk>(ws, total, sentinel, dim, dense_out, uniq_rows, row_slot, s);
+      else if (lw == 8) rc = wave_ordered<float, 8, kRedChunk>(ws, total, sentinel, dim, dense_out, uniq_rows, row_slot, s);
+      else rc = wave_ordered<float, 4, kRedChunk>(ws, total, sentinel, dim, dense_out, uniq_rows, row_slot, s);
     }
-    if (grad_dtype == GRK_BF16) { GRK_SEGW(bf16_t, 8); }
-    else if (lw == 8) { GRK_SEGW(float, 8); }
-    else { GRK_SEGW(float, 4); }
-#undef GRK_SEGW
-    GRK_LAUNCH_CHECK();
+    return rc;
   } else {
     const unsigned gc = (unsigned)((chunks + groups - 1) / groups);
     const unsigned gu = (unsigned)((total + groups - 1) / groups);

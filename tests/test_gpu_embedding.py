@@ -182,20 +182,24 @@ def test_adamw_bf16_param(K):
     assert np.mean(got == oemb.to_bf16_f32(wp)) > 0.99
 
 
-@pytest.mark.parametrize('D,dt', [(256, torch.float32), (512, torch.bfloat16), (512, torch.float32),
-                                  (64, torch.bfloat16), (40, torch.float32), (520, torch.bfloat16)])
-def test_backward_wave_path(K, D, dt):
+@pytest.mark.parametrize('D,dt,bulk', [(256, torch.float32, 20000), (512, torch.bfloat16, 20000),
+                                       (512, torch.float32, 20000), (64, torch.bfloat16, 20000),
+                                       (40, torch.float32, 20000), (520, torch.bfloat16, 20000),
+                                       (512, torch.bfloat16, 160000), (256, torch.float32, 160000)])
+def test_backward_wave_path(K, D, dt, bulk):
     """Every row bit-exact in occurrence order (the reference's CPU
-    embedding_dense_backward): rows inside one chunk, rows of <= 512
-    occurrences crossing chunk edges, and hot rows of 600-3000 occurrences
-    (k_seg_hot, one wave per 64 columns; D = 40 and 520 leave a partial
-    column slice) -- on the one-wave-per-row path (D = 64 x 16 bytes) and the
-    generic one; padding skipped; deterministic."""
+    embedding_dense_backward): rows inside one chunk, rows crossing chunk
+    edges (re-summed up to 2 chunks), and hot rows of 600-3000 occurrences
+    (k_seg_hot, one wave per column slice; D = 40 and 520 leave a partial
+    column slice) -- on the one-wave-per-row path (D = 64 x 16 bytes; 64-entry
+    chunks below 2^17 occurrences, 256 above: `bulk`) and the generic one;
+    padding skipped; deterministic."""
     rng = np.random.default_rng(11)
     R = 3000
     idx = np.concatenate([np.full(3000, 5), np.full(600, 7), np.full(1031, 8),
                           np.repeat(np.arange(10, 20), rng.integers(300, 513, 10)),
-                          rng.integers(20, R, 20000), np.zeros(2000, np.int64)])
+                          np.repeat(np.arange(20, 30), rng.integers(60, 129, 10)),
+                          rng.integers(30, R, bulk), np.zeros(2000, np.int64)])
     rng.shuffle(idx)
     g = rng.standard_normal((len(idx), D)).astype(np.float32)
     if dt == torch.bfloat16:
