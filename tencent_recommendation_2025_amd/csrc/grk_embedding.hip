@@ -105,6 +105,76 @@ __global__ void __launch_bounds__(256) k_gather(FeatArgs args, int dim, int64_t 
   }
 }
 
+// One wave per (token, feature) row when a row is 64 x 16 bytes (bf16 d=512,
+// fp32 d=256): lane = 16-byte column chunk, so a unit needs no index
+// arithmetic; the token's index (and bag) words are wave-uniform scalar loads,
+// and kGatherRows tokens per wave keep that many rows in flight.  Same values
+// as k_gather (bag sums in fp32 from slot 0, one rounding).
+constexpr int kGatherRows = 1;
+
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) k_gather_wave(FeatArgs args, int64_t num_tokens,
+                                                     const int32_t* __restrict__ token_type, int32_t T_len,
+                                                     T* __restrict__ out, int64_t out_ld, int32_t* err_flag) {
+  constexpr int VEC = Vec16<T>::N;
+  constexpr int dim = 64 * VEC;
+  const grk_feature& f = args.f[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n0 = ((int64_t)blockIdx.x * 4 + wave) * kGatherRows;
+  const T* table = reinterpret_cast<const T*>(f.table);
+  const I* idx = reinterpret_cast<const I*>(f.idx);
+  if (f.bag == 1) {
+    int64_t row[kGatherRows];
+#pragma unroll
+    for (int r = 0; r < kGatherRows; ++r) {
+      const int64_t n = n0 + r;
+      row[r] = n < num_tokens ? resolve_row(idx, n, 0, f.idx_ld, f.idx_mode, token_type, T_len) : 0;
+    }
+    Vec16<T> v[kGatherRows];
+#pragma unroll
+    for (int r = 0; r < kGatherRows; ++r) {
+      if (row[r] < 0 || row[r] >= f.num_rows) {
+        if (n0 + r < num_tokens && err_flag) *err_flag = 1;
+        v[r].v = {};
+      } else {
+        v[r].load(table + row[r] * dim + lane * VEC);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kGatherRows; ++r)
+      if (n0 + r < num_tokens) v[r].store(out + (n0 + r) * out_ld + f.out_col + lane * VEC);
+    return;
+  }
+  for (int r = 0; r < kGatherRows; ++r) {
+    const int64_t n = n0 + r;
+    if (n >= num_tokens) return;
+    float s[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) s[e] = 0.f;
+    for (int a = 0; a < f.bag; ++a) {
+      const int64_t row = resolve_row(idx, n, a, f.idx_ld, f.idx_mode, token_type, T_len);
+      if (row < 0 || row >= f.num_rows) {
+        if (err_flag) *err_flag = 1;
+        continue;
+      }
+      Vec16<T> x;
+      x.load(table + row * dim + lane * VEC);
+      if (a == 0) {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) s[e] = x.get(e);
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) s[e] = s[e] + x.get(e);
+      }
+    }
+    Vec16<T> acc;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc.set(e, s[e]);
+    acc.store(out + n * out_ld + f.out_col + lane * VEC);
+  }
+}
+
 // -------------------------------------------------------------- backward ----
 // Occurrences [occ_off[0], occ_off[num]) of one launch batch: sort key =
 // group row (sentinel for padding / out-of-range), payload = address of the
@@ -905,6 +975,21 @@ extern "C" int grk_embedding_gather(const grk_feature* features, int num_feature
   }
   if (num_tokens == 0) return GRK_OK;
   hipStream_t s = (hipStream_t)stream;
+  if (dim / vec == 64) {
+    const dim3 gw((unsigned)((num_tokens + 4 * kGatherRows - 1) / (4 * kGatherRows)), num_features);
+#define GRK_GATHERW(T, I) \
+  k_gather_wave<T, I><<<gw, 256, 0, s>>>(fa, num_tokens, token_type, seq_len, (T*)out, out_ld, err_flag)
+    if (dtype == GRK_BF16) {
+      if (itype == GRK_I64) GRK_GATHERW(bf16_t, int64_t);
+      else GRK_GATHERW(bf16_t, int32_t);
+    } else {
+      if (itype == GRK_I64) GRK_GATHERW(float, int64_t);
+      else GRK_GATHERW(float, int32_t);
+    }
+#undef GRK_GATHERW
+    GRK_LAUNCH_CHECK();
+    return GRK_OK;
+  }
   const int64_t units = num_tokens * (dim / vec);
   // One (row, chunk) unit per lane over a wide grid: measured faster than 4 units
   // per lane both for cold random rows (scripts/microbench/gather.hip: 19 vs 32 us

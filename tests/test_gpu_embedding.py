@@ -69,9 +69,10 @@ def test_backward_multi_source(K, golden):
     np.testing.assert_allclose(res.dense.cpu().numpy(), g['item_dgrad'], rtol=1e-6, atol=1e-6)
 
 
-def test_bf16_gather_bagsum_backward(K):
+@pytest.mark.parametrize('D', [128, 512])   # 512: the wave-per-row gather (64 x 16-byte chunks)
+def test_bf16_gather_bagsum_backward(K, D):
     rng = np.random.default_rng(0)
-    R, D, N, A = 5000, 128, 777, 3
+    R, N, A = 5000, 777, 3
     tab = oemb.to_bf16_f32(rng.standard_normal((R, D)).astype(np.float32))
     idx = rng.integers(0, R, (N,))
     idx[:50] = 0
@@ -87,9 +88,10 @@ def test_bf16_gather_bagsum_backward(K):
     assert np.array_equal(res.dense.cpu().numpy(), want)
 
 
-def test_index_modes_and_fused_features(K):
+@pytest.mark.parametrize('D', [64, 256])    # fp32 256: the wave-per-row gather
+def test_index_modes_and_fused_features(K, D):
     rng = np.random.default_rng(1)
-    B, Tn, D = 6, 17, 64
+    B, Tn = 6, 17
     item = rng.standard_normal((300, D)).astype(np.float32)
     user = rng.standard_normal((50, D)).astype(np.float32)
     pos = rng.standard_normal((2 * 16 + 1, D)).astype(np.float32)
@@ -219,17 +221,18 @@ def test_backward_wave_path(K, D, dt, bulk):
     assert torch.equal(again, res.dense)
 
 
-def test_out_of_range_flag_and_empty(K):
-    table = torch.randn(10, 16, device=DEV)
+@pytest.mark.parametrize('D', [16, 256])
+def test_out_of_range_flag_and_empty(K, D):
+    table = torch.randn(10, D, device=DEV)
     idx = torch.tensor([1, 2, 10, -1], device=DEV)
     err = torch.zeros(1, dtype=torch.int32, device=DEV)
-    out = torch.full((4, 16), 5.0, device=DEV)
+    out = torch.full((4, D), 5.0, device=DEV)
     K.embedding_gather([K.Lookup(table, idx, 0)], out, 4, err_flag=err)
     assert err.item() == 1
     assert torch.all(out[2:] == 0) and torch.equal(out[:2], table[1:3])
-    empty = torch.empty(0, 16, device=DEV)
+    empty = torch.empty(0, D, device=DEV)
     K.embedding_gather([K.Lookup(table, idx[:0], 0)], empty, 0)
-    res = K.embedding_backward([K.GradSource(idx[:0], empty, 0)], 10, 16)
+    res = K.embedding_backward([K.GradSource(idx[:0], empty, 0)], 10, D)
     assert res.count.item() == 0 and torch.all(res.dense == 0)
 
 
