@@ -418,6 +418,14 @@ int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, int64_t ldo
  * identical in both directions; seed_dev (optional, device memory) replaces
  * seed with the value it holds when the kernel runs (HIP-graph replay).
  * ------------------------------------------------------------------------ */
+/* fp8 HSTU layer (config C5): out[n, c] = e4m3(SiLU(pre[n, c])) for the
+ * layer's v|q|k pre-activation columns (bf16 in, OCP e4m3 out: fp32 SiLU,
+ * round to nearest even, clamped to +-448); and the straight-through backward
+ * g[n, c] *= dSiLU(pre[n, c]) in place (bf16).  cols multiple of 8; pre / g
+ * rows 16-byte aligned, out rows 8-byte aligned. */
+int grk_silu_fp8(const void* pre, int64_t ldpre, int64_t rows, int cols, void* out, int64_t ldout, void* stream);
+int grk_dsilu_mul(void* g, int64_t ldg, const void* pre, int64_t ldpre, int64_t rows, int cols, void* stream);
+
 int grk_norm_gate_fwd(const void* o, int64_t ldo, const void* u, int64_t ldu, const float* gamma,
                       const float* beta, float eps, int64_t rows, int dim, float dropout_p, uint64_t seed,
                       const uint64_t* seed_dev, void* y, int64_t ldy, float* stats, void* stream);

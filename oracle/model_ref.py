@@ -51,9 +51,10 @@ class RefMHA(torch.nn.Module):
 class RefHSTU(torch.nn.Module):
     """HSTU layer (parity unpinned; see oracle/hstu.py).  Same math, torch autograd."""
 
-    def __init__(self, d, h, p, num_buckets, num_time_buckets=0):
+    def __init__(self, d, h, p, num_buckets, num_time_buckets=0, fp8=False):
         super().__init__()
         self.hidden_units, self.num_heads, self.head_dim, self.dropout_rate = d, h, d // h, p
+        self.fp8 = fp8  # config C5: SiLU'd q/k/v rounded to OCP e4m3, straight-through gradient
         self.uvqk = torch.nn.Linear(d, 4 * d)
         self.rab = torch.nn.Parameter(torch.zeros(h, num_buckets))
         self.rab_t = torch.nn.Parameter(torch.zeros(h, num_time_buckets)) if num_time_buckets else None
@@ -63,7 +64,10 @@ class RefHSTU(torch.nn.Module):
     def forward(self, query, key, value, attn_mask=None, timestamps=None, key_valid=None):
         B, T, D = query.shape
         u, v, q, k = torch.split(F.silu(self.uvqk(query)), D, dim=-1)
-        sh = lambda x: x.view(B, T, self.num_heads, self.head_dim).transpose(1, 2)
+        if self.fp8:
+            r8 = lambda x: x + (x.clamp(-448, 448).to(torch.float8_e4m3fn).to(x.dtype) - x).detach()
+            v, q, k = r8(v), r8(q), r8(k)
+        sh = lambda x: x.reshape(B, T, self.num_heads, self.head_dim).transpose(1, 2)
         q, k, v = sh(q), sh(k), sh(v)
         nb = self.rab.shape[1]
         i = torch.arange(T)[:, None]
@@ -157,7 +161,8 @@ class RefBaselineModel(torch.nn.Module):
             self.attention_layernorms.append(torch.nn.LayerNorm(d, eps=1e-8))
             if block == "hstu":
                 self.attention_layers.append(RefHSTU(d, args.num_heads, args.dropout_rate, T,
-                                                     getattr(args, 'hstu_time_buckets', 0) or 0))
+                                                     getattr(args, 'hstu_time_buckets', 0) or 0,
+                                                     fp8=bool(getattr(args, 'hstu_fp8', False))))
                 continue
             self.attention_layers.append(RefMHA(d, args.num_heads, args.dropout_rate))
             self.forward_layernorms.append(torch.nn.LayerNorm(d, eps=1e-8))

@@ -90,6 +90,8 @@ SIGNATURES = {
     'grk_stream_create': (_I, [C.POINTER(C.c_void_p)]),
     'grk_stream_destroy': (_I, [_P]),
     'grk_embedding_gather': (_I, [C.POINTER(GrkFeature), _I, _I, _I, _I, _I64, _P, C.c_int32, _P, _I64, _P, _P]),
+    'grk_silu_fp8': (_I, [_P, _I64, _I64, _I, _P, _I64, _P]),
+    'grk_dsilu_mul': (_I, [_P, _I64, _P, _I64, _I64, _I, _P]),
     'grk_embedding_backward_workspace': (_SZ, [_I64, _I64, _I]),
     'grk_sort_pairs_workspace': (_SZ, [_I64]),
     'grk_sort_pairs': (_I, [_P, _P, _P, _P, _P, _P, _I64, _I, _P, _SZ, _P]),

@@ -34,6 +34,14 @@ __device__ unsigned long long g_attn_stamps[1 << 16][8];
 #else
 #define GRK_STAMP(k)
 #endif
+// dK/dV phase timestamps (100 MHz s_memrealtime) for scripts/microbench/attn_dkdv_stamps.hip.
+#ifdef GRK_DKDV_STAMPS
+__device__ unsigned long long g_dkdv_rt[1 << 16][8];
+#define GRK_RT(k) \
+  if ((threadIdx.x & 63) == 0) g_dkdv_rt[(blockIdx.x * kSeqWaves + (threadIdx.x >> 6)) & 0xFFFF][k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define GRK_RT(k)
+#endif
 constexpr int kRabPad = 32;             // rabx[kRabPad + d], d >= -31 inside a sub-tile
 constexpr float kCausalBias = -1.0e30f;
 constexpr int kDqBinArrays = 2;         // dQ kernel: drab bins as int64 fixed point (2 float slots each)
@@ -772,6 +780,7 @@ k_attn_dkdv_seq(AttnParams p) {
   const int bh = b * p.H + h;
   const int64_t rbase = p.row_base ? p.row_base[b] : (int64_t)b * T;
   const int lo = p.row_base ? start : 0;  // jagged rows: only [start, T) exist
+  GRK_RT(0);
   zero_tail_rows(p, p.dk, p.lddk, HD);
   zero_tail_rows(p, p.dv, p.lddv, HD);
   // key tile j (absolute first + j) visits query tiles j .. ntiles-1
@@ -819,12 +828,17 @@ k_attn_dkdv_seq(AttnParams p) {
     }
   }
   if (!si.contig) stage_kvs(L.kvs, p.key_valid, b, T, Tp);
+  GRK_RT(1);
   __syncthreads();
+  GRK_RT(2);
 
   const float sl2 = p.scale * kLog2e;
   const float rdrop = 1.0f / (1.0f - p.dropout_p);
   const bool drop = KIND == 0 && p.dropout_p > 0.f;
   const unsigned long long seed = drop ? attn_seed(p) : 0ull;
+#ifdef GRK_DKDV_STAMPS
+  int ntile_done = 0;
+#endif
 
   for (int kt = wave; kt < first; kt += kSeqWaves) {  // keys before the first valid one: no gradient
     const int myk = kt * 32 + r;
@@ -928,6 +942,18 @@ k_attn_dkdv_seq(AttnParams p) {
         } else {
           // bias of (query qb + acc_row(i, hh), key myk): rabx[kRabPad + q - myk]
           const float* rbase = L.f0 + kRabPad + (qb - myk + 4 * hh);
+          // time bias of this half's 8 scores, behind ONE wave-uniform branch (a
+          // branch per score split the loop body into 16 blocks the scheduler
+          // could not interleave: MFMA and VALU work then ran back to back)
+          float tbv[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) tbv[e] = 0.f;
+          if (p.nbt) {
+            const int tk = L.tss[myk < Tp ? myk : Tp - 1];
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              tbv[e] = L.rtab[time_bucket(L.tss[qb + acc_row(8 * s2 + e, hh)] - tk, p.nbt)];
+          }
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) {
             const int j = 4 * s2 + jj;
@@ -935,9 +961,7 @@ k_attn_dkdv_seq(AttnParams p) {
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
               const int i = 2 * j + u;
-              float bias = rbase[(i & 3) + 8 * (i >> 2)];
-              if (p.nbt)  // time bias of (query qb + acc_row(i, hh), key myk)
-                bias += L.rtab[time_bucket(L.tss[qb + acc_row(i, hh)] - L.tss[myk < Tp ? myk : Tp - 1], p.nbt)];
+              const float bias = rbase[(i & 3) + 8 * (i >> 2)] + tbv[2 * jj + u];
               const float x = fmaf(s[i], p.scale, bias);
               const float sg = sigmoid_fast(x), sgn = sg * p.inv_n;
               pd2[u] = x * sgn;                                   // SiLU(x) / n
@@ -979,7 +1003,12 @@ k_attn_dkdv_seq(AttnParams p) {
                           p.ldk, p.in_dt);
       store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, kok ? 1.f : 0.f, kst, p.act ? p.v : nullptr, p.ldv,
                           p.in_dt);
+#ifdef GRK_DKDV_STAMPS
+      if (ntile_done < 3) GRK_RT(3 + ntile_done);
+      ++ntile_done;
+#endif
     }
+  GRK_RT(6);
 }
 
 template <int HD>

@@ -417,6 +417,58 @@ static int ng_check(const NGParams& p) {
   return GRK_OK;
 }
 
+// ----------------------------------------------- fp8 q/k/v (config C5) ----
+// The fp8 HSTU layer quantises its SiLU'd v|q|k once per step: out[n, c] =
+// e4m3(SiLU(pre[n, c])) (fp32 SiLU, round to nearest even, clamped to the
+// e4m3 range +-448), 8 elements per lane; the backward is straight-through:
+// the attention's gradients w.r.t. those fp8 values times dSiLU(pre), in place.
+__global__ void __launch_bounds__(256) k_silu_fp8(const bf16_t* __restrict__ pre, int64_t ldp, int64_t rows,
+                                                  int cols, unsigned char* __restrict__ out, int64_t ldo) {
+  const int per_row = cols / 8;
+  const int64_t units = rows * per_row;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = u / per_row;
+    const int c = (int)(u - r * per_row) * 8;
+    const uint4 w = *reinterpret_cast<const uint4*>(pre + r * ldp + c);
+    const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+    float f[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[2 * k] = silu(__uint_as_float(ws[k] << 16));
+      f[2 * k + 1] = silu(__uint_as_float(ws[k] & 0xFFFF0000u));
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = fminf(fmaxf(f[k], -448.f), 448.f);
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+    *reinterpret_cast<uint2*>(out + r * ldo + c) = make_uint2((unsigned)lo, (unsigned)hi);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_dsilu_mul(bf16_t* __restrict__ g, int64_t ldg,
+                                                   const bf16_t* __restrict__ pre, int64_t ldp, int64_t rows,
+                                                   int cols) {
+  const int per_row = cols / 8;
+  const int64_t units = rows * per_row;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = u / per_row;
+    const int c = (int)(u - r * per_row) * 8;
+    uint4* gp = reinterpret_cast<uint4*>(g + r * ldg + c);
+    const uint4 gw = *gp, pw = *reinterpret_cast<const uint4*>(pre + r * ldp + c);
+    const unsigned gs[4] = {gw.x, gw.y, gw.z, gw.w}, ps[4] = {pw.x, pw.y, pw.z, pw.w};
+    unsigned o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float a = __uint_as_float(gs[k] << 16) * dsilu(__uint_as_float(ps[k] << 16));
+      const float b = __uint_as_float(gs[k] & 0xFFFF0000u) * dsilu(__uint_as_float(ps[k] & 0xFFFF0000u));
+      o[k] = (unsigned)f32_to_bf16(a) | ((unsigned)f32_to_bf16(b) << 16);
+    }
+    *gp = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 }  // namespace grk
 
 using namespace grk;
@@ -551,6 +603,36 @@ extern "C" int grk_add_norm_bwd(const void* gx, int64_t ldgx, int gx_dtype, cons
   memset(&q, 0, sizeof(q));
   q.dim = dim; q.partial = (float*)ws; q.dgamma = dgamma; q.dbeta = dbeta;
   k_ng_colsum<<<(2 * dim + 63) / 64, 64 * kColGroups, 0, st>>>(q, nb);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+extern "C" int grk_silu_fp8(const void* pre, int64_t ldpre, int64_t rows, int cols, void* out, int64_t ldout,
+                            void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(rows >= 0 && cols > 0 && cols % 8 == 0, "rows >= 0 and cols a positive multiple of 8");
+  GRK_CHECK_ARG(rows == 0 || (pre && out), "pre / out are required");
+  GRK_CHECK_ARG(ldpre >= cols && ldpre % 8 == 0 && (uintptr_t)pre % 16 == 0, "pre: 16-byte aligned rows");
+  GRK_CHECK_ARG(ldout >= cols && ldout % 8 == 0 && (uintptr_t)out % 8 == 0, "out: 8-byte aligned rows");
+  if (rows == 0) return GRK_OK;
+  const int64_t units = rows * (cols / 8);
+  k_silu_fp8<<<grid_for(units, 256, 8192), 256, 0, (hipStream_t)stream>>>((const bf16_t*)pre, ldpre, rows, cols,
+                                                                          (unsigned char*)out, ldout);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+extern "C" int grk_dsilu_mul(void* g, int64_t ldg, const void* pre, int64_t ldpre, int64_t rows, int cols,
+                             void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(rows >= 0 && cols > 0 && cols % 8 == 0, "rows >= 0 and cols a positive multiple of 8");
+  GRK_CHECK_ARG(rows == 0 || (g && pre), "g / pre are required");
+  GRK_CHECK_ARG(ldg >= cols && ldg % 8 == 0 && (uintptr_t)g % 16 == 0, "g: 16-byte aligned rows");
+  GRK_CHECK_ARG(ldpre >= cols && ldpre % 8 == 0 && (uintptr_t)pre % 16 == 0, "pre: 16-byte aligned rows");
+  if (rows == 0) return GRK_OK;
+  const int64_t units = rows * (cols / 8);
+  k_dsilu_mul<<<grid_for(units, 256, 8192), 256, 0, (hipStream_t)stream>>>((bf16_t*)g, ldg, (const bf16_t*)pre,
+                                                                           ldpre, rows, cols);
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }

@@ -343,6 +343,64 @@ def hstu_core(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, pre
     return y if pre.dtype == torch.bfloat16 else y.to(pre.dtype)
 
 
+class _HSTUFp8Fn(torch.autograd.Function):
+    """HSTU layer core with fp8 q/k/v (config C5, BASELINE.json configs[4]):
+    SiLU'd v|q|k quantised once to e4m3 (grk_silu_fp8), attention on the fp8
+    kernels (QK^T on the fp8 MFMA, P V on bf16 over the exactly widened values),
+    then the same LayerNorm * SiLU(u) gate as the bf16 layer.  Backward is
+    straight-through at the quantiser: the attention's gradients w.r.t. the fp8
+    values times dSiLU(pre) (grk_dsilu_mul)."""
+
+    @staticmethod
+    def forward(ctx, pre, rab, ln_w, ln_b, key_valid, H, hd, inv_n, eps, dropout_p, seed, seq_range):
+        D = H * hd
+        B, T = key_valid.shape
+        pb = pre.to(torch.bfloat16).contiguous()
+        x8 = K.silu_fp8(pb[:, D:])                       # v | q | k
+        rab32 = rab.float().contiguous()
+        args = K.attn_args(L.ATTN_HSTU, x8[:, D:2 * D], x8[:, 2 * D:], x8[:, :D], B, T, H, hd, key_valid=key_valid,
+                           scale=hd ** -0.5, rab=rab32, inv_n=inv_n, precise=1, out_dtype=torch.bfloat16,
+                           seq_range=seq_range)
+        o = torch.empty(pb.shape[0], D, dtype=torch.bfloat16, device=pb.device)
+        K.attention_fwd(args, o)
+        lw, lb = ln_w.float().contiguous(), ln_b.float().contiguous()
+        y, stats = K.norm_gate_fwd(o, pb[:, :D], lw, lb, eps, dropout_p, seed)
+        ctx.save_for_backward(pb, x8, o, stats, rab32, lw, lb, key_valid, seq_range,
+                              seed if isinstance(seed, torch.Tensor) else None)
+        ctx.meta = (H, hd, inv_n, dropout_p, seed if not isinstance(seed, torch.Tensor) else None, pre.dtype,
+                    rab.dtype, ln_w.dtype)
+        return y if pre.dtype == torch.bfloat16 else y.to(pre.dtype)
+
+    @staticmethod
+    def backward(ctx, gy):
+        pb, x8, o, stats, rab32, lw, lb, key_valid, seq_range, seed_dev = ctx.saved_tensors
+        H, hd, inv_n, dropout_p, seed, pdt, rdt, ldt = ctx.meta
+        D = H * hd
+        B, T = key_valid.shape
+        seed = seed_dev if seed_dev is not None else seed
+        dpre = torch.empty(pb.shape[0], 4 * D, dtype=torch.bfloat16, device=pb.device)
+        do, _, dw, db = K.norm_gate_bwd(gy.to(torch.bfloat16).contiguous(), o, pb[:, :D], lw, lb, stats, dropout_p,
+                                        seed, du=dpre[:, :D])
+        drab = torch.zeros_like(rab32)
+        args = K.attn_args(L.ATTN_HSTU, x8[:, D:2 * D], x8[:, 2 * D:], x8[:, :D], B, T, H, hd, key_valid=key_valid,
+                           scale=hd ** -0.5, rab=rab32, inv_n=inv_n, precise=1, out_dtype=torch.bfloat16,
+                           seq_range=seq_range)
+        K.attention_bwd(args, None, do, None, None, dpre[:, 2 * D:3 * D], dpre[:, 3 * D:], dpre[:, D:2 * D], drab)
+        K.dsilu_mul_(dpre[:, D:], pb[:, D:])
+        return (dpre.to(pdt), drab.to(rdt), dw.to(ldt), db.to(ldt), None, None, None, None, None, None, None, None)
+
+
+@_disable
+def hstu_core_fp8(pre, rab, ln_w, ln_b, key_valid, B, T, H, hd, inv_n, eps=1e-8, dropout_p=0.0, seed=0,
+                  seq_range=None):
+    """hstu_core with fp8 q/k/v (config C5): padded [B*T, 4D] layout, no time bias
+    (the fp8 kernels are the chunked ones)."""
+    if key_valid is None:
+        key_valid = torch.ones(B, T, dtype=torch.uint8, device=pre.device)
+    return _HSTUFp8Fn.apply(pre, rab, ln_w, ln_b, key_valid, H, hd, float(inv_n), float(eps), float(dropout_p), seed,
+                            seq_range)
+
+
 # ---------------------------------------------------------------- logits ----
 def _rows2d(x):
     x = x.reshape(-1, x.shape[-1])

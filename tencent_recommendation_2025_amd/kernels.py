@@ -684,6 +684,32 @@ def add_norm_bwd(gx, gs, s_new, gamma, stats):
     return ds, dgamma, dbeta
 
 
+def silu_fp8(pre, out=None):
+    """e4m3(SiLU(pre)) of bf16 [N, C] (column view allowed): grk_silu_fp8 (fp32 SiLU,
+    round to nearest even, clamped to +-448) -> float8_e4m3fn [N, C]."""
+    _require_cuda(pre, out)
+    if pre.dtype != torch.bfloat16 or pre.dim() != 2 or pre.stride(1) != 1:
+        raise L.GrkError('silu_fp8 takes a row-major bf16 [N, C] (column view)')
+    N, C = pre.shape
+    if out is None:
+        out = torch.empty(N, C, dtype=torch.float8_e4m3fn, device=pre.device)
+    L.check(L.lib().grk_silu_fp8(pre.data_ptr(), pre.stride(0), N, C, out.data_ptr(), out.stride(0),
+                                 L.stream_ptr(pre.device)), 'grk_silu_fp8')
+    return out
+
+
+def dsilu_mul_(g, pre):
+    """g *= dSiLU(pre) in place (bf16 [N, C] column views): grk_dsilu_mul."""
+    _require_cuda(g, pre)
+    if g.dtype != torch.bfloat16 or pre.dtype != torch.bfloat16 or g.shape != pre.shape or g.stride(1) != 1 \
+            or pre.stride(1) != 1:
+        raise L.GrkError('dsilu_mul_ takes two row-major bf16 [N, C] views of one shape')
+    N, C = g.shape
+    L.check(L.lib().grk_dsilu_mul(g.data_ptr(), g.stride(0), pre.data_ptr(), pre.stride(0), N, C,
+                                  L.stream_ptr(g.device)), 'grk_dsilu_mul')
+    return g
+
+
 def norm_gate_fwd(o, u, gamma, beta, eps, dropout_p=0.0, seed=0, y=None):
     """y = dropout(LayerNorm(o) * SiLU(u)) (grk_norm_gate_fwd).  Returns (y bf16 [N, D], stats fp32 [N, 2]).
     seed: int or device int64 [1] tensor (read at kernel time)."""

@@ -123,9 +123,12 @@ class HSTUAttention(torch.nn.Module):
     torch's generator on the device), not torch's Philox stream.
     """
 
-    def __init__(self, hidden_units, num_heads, dropout_rate, num_buckets, num_time_buckets=0):
+    def __init__(self, hidden_units, num_heads, dropout_rate, num_buckets, num_time_buckets=0, fp8=False):
         super().__init__()
         assert hidden_units % num_heads == 0, 'hidden_units must be divisible by num_heads'
+        if fp8 and num_time_buckets:
+            raise NotImplementedError('fp8 q/k/v (config C5) run without the time bias')
+        self.fp8 = fp8  # config C5: q/k/v quantised to e4m3 after the SiLU (functional.hstu_core_fp8)
         self.hidden_units, self.num_heads = hidden_units, num_heads
         self.head_dim = hidden_units // num_heads
         self.dropout_rate = dropout_rate
@@ -152,6 +155,13 @@ class HSTUAttention(torch.nn.Module):
         pre = _linear(query, self.uvqk.weight, self.uvqk.bias).reshape(N, 4 * D)
         p = self.dropout_rate if self.training else 0.0
         seed = dropout_seed(pre.device) if p > 0 else 0
+        if self.fp8:
+            if row_base is not None:
+                raise NotImplementedError('fp8 q/k/v take the padded [B, T] layout (chunked kernels)')
+            y = G.hstu_core_fp8(pre, self.rab, self.attn_norm.weight, self.attn_norm.bias, key_valid, B, T,
+                                self.num_heads, self.head_dim, 1.0 / T, self.attn_norm.eps, dropout_p=p, seed=seed,
+                                seq_range=seq_range)
+            return _linear(y.view(query.shape), self.out_linear.weight, self.out_linear.bias), None
         y = G.hstu_core(pre, self.rab, self.attn_norm.weight, self.attn_norm.bias, key_valid, B, T,
                         self.num_heads, self.head_dim, 1.0 / T, self.attn_norm.eps, dropout_p=p, seed=seed,
                         seq_range=seq_range, timestamps=timestamps, rab_t=rab_t, row_base=row_base)
@@ -247,7 +257,8 @@ class BaselineModel(torch.nn.Module):
             self.attention_layernorms.append(torch.nn.LayerNorm(d, eps=1e-8))
             if self.block == 'hstu':
                 self.attention_layers.append(HSTUAttention(d, args.num_heads, args.dropout_rate, nb,
-                                                           getattr(args, 'hstu_time_buckets', 0) or 0))
+                                                           getattr(args, 'hstu_time_buckets', 0) or 0,
+                                                           fp8=bool(getattr(args, 'hstu_fp8', False))))
                 continue
             self.attention_layers.append(FlashMultiHeadAttention(d, args.num_heads, args.dropout_rate))
             self.forward_layernorms.append(torch.nn.LayerNorm(d, eps=1e-8))
@@ -380,8 +391,15 @@ class BaselineModel(torch.nn.Module):
             js = self._const_index(tuple(j for _, j in group), Wv.device) if len(group) > 1 else group[0][1]
             if Wv.dtype != E.dtype:  # cast the whole weight once, not each group's blocks (bit-identical)
                 Wv = Wv.to(E.dtype)
-            Wb = Wv[:, js, :].permute(1, 0, 2) if len(group) > 1 else Wv[:, js, :][None]
-            parts.append(torch.bmm(E, Wb.transpose(1, 2)).to(E.dtype).reshape(-1, d))
+            if d >= 1024 and _grk_gemm_ok(E):
+                # torch's batched bf16 GEMM faults at this width (d = 1024, C5): hipBLASLt
+                # returned HIPBLAS_STATUS_INTERNAL_ERROR for [3 x 10001 x 1024] x [1024 x 1024]
+                # and its rocBLAS fallback made an illegal access.  One
+                # grk_gemm per block instead (plans validated at first use).
+                parts.append(torch.cat([G.linear(E[i], Wv[:, j, :]).to(E.dtype) for i, (_, j) in enumerate(group)]))
+            else:
+                Wb = Wv[:, js, :].permute(1, 0, 2) if len(group) > 1 else Wv[:, js, :][None]
+                parts.append(torch.bmm(E, Wb.transpose(1, 2)).to(E.dtype).reshape(-1, d))
             for k, _ in group:
                 offs[k] = row
                 row += rows

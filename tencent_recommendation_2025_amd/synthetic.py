@@ -134,8 +134,8 @@ def make_batch(cfg: SyntheticConfig, generator: torch.Generator, device='cuda'):
 
 
 def make_args(hidden_units=512, maxlen=200, num_blocks=4, num_heads=8, dropout_rate=0.0, block='hstu',
-              variant='o1', norm_first=False, device='cuda', hstu_time_buckets=0):
+              variant='o1', norm_first=False, device='cuda', hstu_time_buckets=0, hstu_fp8=False):
     from types import SimpleNamespace
     return SimpleNamespace(hidden_units=hidden_units, maxlen=maxlen, num_blocks=num_blocks, num_heads=num_heads,
                            dropout_rate=dropout_rate, block=block, variant=variant, norm_first=norm_first,
-                           device=device, mm_emb_id=['81'], hstu_time_buckets=hstu_time_buckets)
+                           device=device, mm_emb_id=['81'], hstu_time_buckets=hstu_time_buckets, hstu_fp8=hstu_fp8)
