@@ -27,3 +27,32 @@ def test_overlap_detector_flags_a_bad_mfma():
             '  v_mfma_f32_32x32x16_bf16 v[32:47], v[36:39], v[82:85], 0 // 000000001000\n'
             '  v_mfma_f32_32x32x16_bf16 v[0:15], v[16:19], v[20:23], v[0:15]\n')
     assert overlapping_mfmas(text) == [('k', 'v_mfma_f32_32x32x16_bf16 v[32:47], v[36:39], v[82:85], 0')]
+
+
+def test_mfma_wait_states_in_attention_objects():
+    """The attention objects keep the documented MFMA wait states
+    (scripts/isa_hazards.py: an MFMA's D untouched for 12 / 8 states except by
+    the accumulate chain, 2 states between a write and the MFMA reading it)."""
+    sys.path.insert(0, os.path.join(REPO, 'scripts'))
+    from check_mfma_overlap import disassemble
+    from isa_hazards import parse, scan
+    objs = [p for p in glob.glob(os.path.join(REPO, 'build', 'obj', 'grk_attention*.o'))]
+    if not objs:
+        pytest.skip('no build/obj (run make first)')
+    for obj in objs:
+        found = [f for f in scan(parse(disassemble(obj))) if f[0] in ('D-RAW/WAW', 'D-RAW/WAW(mfma)', 'OPERAND')]
+        assert not found, (obj, found[:5])
+
+
+def test_hazard_scanner_flags_short_gaps():
+    sys.path.insert(0, os.path.join(REPO, 'scripts'))
+    from isa_hazards import parse, scan
+    text = ('0000000000001000 <k>:\n'
+            '  v_mov_b32 v40, 0\n'
+            '  v_mfma_f32_32x32x16_bf16 v[0:15], v[40:43], v[20:23], v[0:15]\n'
+            '  s_nop 3\n'
+            '  v_add_f32 v50, v3, v4\n'
+            '  v_exp_f32 v60, v61\n'
+            '  v_pk_mul_f32 v[62:63], v[60:61], v[64:65]\n')
+    kinds = sorted({f[0] for f in scan(parse(text))})
+    assert kinds == ['D-RAW/WAW', 'OPERAND', 'TRANS-USE(packed)'], kinds
