@@ -77,6 +77,9 @@ def parse():
                          'reference); 0 = the padded [B, T] step')
     ap.add_argument('--step-times', type=int, default=0,
                     help='diagnostic: per-step device intervals (events) and host issue times to stderr')
+    ap.add_argument('--fp8', type=int, default=0,
+                    help='config C5: HSTU layers with fp8 (e4m3) q/k/v on the chunked attention kernels '
+                         '(padded layout; e.g. --fp8 1 --hidden 1024 --maxlen 1024 --batch 16)')
     ap.add_argument('--jagged-quantum', type=int, default=1024,
                     help='jagged capacity granularity (rows): one GEMM plan set and one HIP graph per capacity')
     return ap.parse_args()
@@ -140,10 +143,18 @@ def attention_rooflines(a, key_valid, reps, jagged=False):
         pre, row_base, seq_range = jpre, jag.row_base, jag.seq_range
     N = pre.shape[0]
     hstu = a.block == 'hstu'
+    fp8 = bool(getattr(a, 'fp8', 0))
     kind = L.ATTN_HSTU if hstu else L.ATTN_SOFTMAX
     extra = dict(rab=0.1 * torch.randn(H, T, device=dev, generator=g), inv_n=1.0 / T, act='silu') if hstu else {}
-    args = K.attn_args(kind, pre[:, 2 * D:3 * D], pre[:, 3 * D:], pre[:, D:2 * D], B, T, H, hd, key_valid=kv,
-                       scale=hd ** -0.5, out_dtype=torch.bfloat16, seq_range=seq_range, row_base=row_base, **extra)
+    if fp8:   # config C5: the layer's e4m3(SiLU(v|q|k)) as HSTUAttention(fp8=True) feeds the chunked kernels
+        x8 = K.silu_fp8(pre[:, D:])
+        extra.pop('act', None)
+        args = K.attn_args(kind, x8[:, D:2 * D], x8[:, 2 * D:], x8[:, :D], B, T, H, hd, key_valid=kv,
+                           scale=hd ** -0.5, out_dtype=torch.bfloat16, seq_range=seq_range, precise=1, **extra)
+    else:
+        args = K.attn_args(kind, pre[:, 2 * D:3 * D], pre[:, 3 * D:], pre[:, D:2 * D], B, T, H, hd, key_valid=kv,
+                           scale=hd ** -0.5, out_dtype=torch.bfloat16, seq_range=seq_range, row_base=row_base,
+                           **extra)
     o = torch.empty(N, D, dtype=torch.bfloat16, device=dev)
     lse = torch.empty(B, H, T, device=dev)
     do = torch.randn(N, D, device=dev, generator=g).bfloat16()
@@ -161,11 +172,16 @@ def attention_rooflines(a, key_valid, reps, jagged=False):
     n_valid = int(lens.sum().item())
     pairs = float((lens * (lens + 1) / 2).sum().item()) * H
     row = D * 2
+    qkv_row = D if fp8 else D * 2                              # bytes of one token's q (k, v) row
     side = H * T * 4 if hstu else n_valid * H * 4            # rab row / lse (+ delta) per kernel
     ridge = BF16_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBPS * 1e9)
-    name = 'hstu' if hstu else 'softmax'
+    name = ('hstu' if hstu else 'softmax') + ('_fp8' if fp8 else '')
     workload = {'B': B, 'T': T, 'D': D, 'H': H, 'kind': name, 'valid_tokens': n_valid,
                 'layout': 'jagged' if jagged else 'padded'}
+    # whole-sequence kernels at the C2 shape; the chunked ones for fp8 q/k/v or long sequences
+    seq = not fp8 and (T + 31) // 32 * 32 + 32 <= 512 and hd <= 128
+    kn = {'fwd': 'k_attn_fwd_seq', 'dq': 'k_attn_dq_seq', 'dkdv': 'k_attn_dkdv_seq'} if seq else \
+        {'fwd': 'k_attn_fwd', 'dq': 'k_attn_bwd_dq', 'dkdv': 'k_attn_bwd_dkdv'}
 
     def entry(kernel, ms, nbytes, flops, pmc_name):
         gbps = nbytes / (ms * 1e-3) / 1e9
@@ -188,12 +204,21 @@ def attention_rooflines(a, key_valid, reps, jagged=False):
                                    '(MI355X_MICROARCH.md gfx950 corrections)')
         return res
 
-    dkdv = entry(f'grk::k_attn_dkdv_seq ({name} attention dK/dV, one layer)', t_dkdv,
-                 6 * n_valid * row + side, 8 * hd * pairs, f'{PMC_TAG}_pmc_attn_dkdv_{name}.json')
-    fwd = entry(f'grk::k_attn_fwd_seq ({name} attention forward, one layer)', t_fwd,
-                4 * n_valid * row + side, 4 * hd * pairs, f'{PMC_TAG}_pmc_attn_fwd_{name}.json')
-    dq = entry(f'grk::k_attn_dq_seq ({name} attention dQ{" + drab" if hstu else ""}, one layer)', t_dq,
-               5 * n_valid * row + side, 6 * hd * pairs, f'{PMC_TAG}_pmc_attn_dq_{name}.json')
+    dkdv = entry(f'grk::{kn["dkdv"]} ({name} attention dK/dV, one layer)', t_dkdv,
+                 3 * n_valid * qkv_row + 3 * n_valid * row + side, 8 * hd * pairs,
+                 f'{PMC_TAG}_pmc_attn_dkdv_{name}.json')
+    fwd = entry(f'grk::{kn["fwd"]} ({name} attention forward, one layer)', t_fwd,
+                3 * n_valid * qkv_row + n_valid * row + side, 4 * hd * pairs, f'{PMC_TAG}_pmc_attn_fwd_{name}.json')
+    dq = entry(f'grk::{kn["dq"]} ({name} attention dQ{" + drab" if hstu else ""}, one layer)', t_dq,
+               3 * n_valid * qkv_row + 2 * n_valid * row + side, 6 * hd * pairs,
+               f'{PMC_TAG}_pmc_attn_dq_{name}.json')
+    for e, k in ((fwd, 'fwd'), (dq, 'dq'), (dkdv, 'dkdv')):
+        e['pmc_kernel'] = kn[k] + '<'
+        e['pmc_name'] = f'{PMC_TAG}_pmc_attn_{k}_{name}.json'
+    if fp8:
+        for e in (fwd, dq, dkdv):
+            e['peak_note'] = 'bf16 MFMA peak (QK^T runs on the fp8 MFMA, the other products on bf16)'
+
     fwd['survey_formula_flops'] = int(2 * B * D * T * (T + 1))  # 2*B*D*T(T+1) per layer fwd
     return dkdv, [fwd, dq]
 
@@ -571,8 +596,11 @@ def main():
     cfg = S.SyntheticConfig(batch_size=a.batch, maxlen=a.maxlen, num_items=a.items, num_users=a.users, zipf=a.zipf,
                             timestamps=a.time_buckets > 0, sid_table=sid, sid_codes=a.sid_codes)
     stats, types = S.feature_schema(cfg)
+    if a.fp8 and (a.block != 'hstu' or a.time_buckets):
+        raise SystemExit('--fp8 takes HSTU blocks without the time bias (chunked fp8 kernels)')
     margs = S.make_args(hidden_units=a.hidden, maxlen=a.maxlen, num_blocks=a.blocks, num_heads=a.heads,
-                        block=a.block, dropout_rate=a.dropout, hstu_time_buckets=a.time_buckets)
+                        block=a.block, dropout_rate=a.dropout, hstu_time_buckets=a.time_buckets,
+                        hstu_fp8=bool(a.fp8))
     shard_tables = sharded and (a.shard_tables if a.shard_tables is not None else a.items >= 10_000_000)
     margs.shard_tables = bool(shard_tables)
     torch.manual_seed(0)
@@ -584,7 +612,8 @@ def main():
         opt = ShardedFusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
     else:
         opt = FusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
-    jagged = bool(a.jagged) and not sharded
+    # the jagged layout runs on the whole-sequence attention kernels (T <= 256 at hd <= 128, not fp8)
+    jagged = bool(a.jagged) and not sharded and not a.fp8 and a.maxlen + 1 <= 256 and a.hidden // a.heads <= 128
     trainer = Trainer(model, opt, loss=a.loss, graph=bool(a.graph), jagged=jagged, jagged_quantum=a.jagged_quantum)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [S.make_batch(cfg, gen, dev) for _ in range(max(2, a.pool))]
@@ -670,7 +699,7 @@ def main():
     more.remove(roof)
 
     cpu = None
-    if rank == 0 and world == 1 and a.cpu_baseline and not a.semantic_ids:   # config 2's CPU model only
+    if rank == 0 and world == 1 and a.cpu_baseline and not a.semantic_ids and not a.fp8:   # config 2's CPU model only
         cpu = cpu_baseline(a, stats, types)
 
     if rank == 0:
@@ -679,15 +708,16 @@ def main():
             'metric': 'seq/sec training throughput, TencentGR HSTU d=512 L=200, at 1/2/4/8 MI355X',
             'value': round(value, 2), 'unit': 'seq/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
             'ms_per_step': round(elapsed / a.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': 'bf16', 'data': 'synthetic (device-resident TencentGR-shaped batches)',
-            'config': {'workload': f'BASELINE config {4 if a.semantic_ids else 3 if shard_tables else 2}: '
+            'vs_baseline': None, 'dtype': 'bf16+fp8' if a.fp8 else 'bf16', 'data': 'synthetic (device-resident TencentGR-shaped batches)',
+            'config': {'workload': f'BASELINE config {5 if a.fp8 else 4 if a.semantic_ids else 3 if shard_tables else 2}: '
                                    + (f'O1 + RQ-VAE semantic ids ({a.semantic_ids} levels x {a.sid_codes} codes '
                                       f'as item_sparse features), ' if a.semantic_ids else '')
                                    + f'{a.block.upper()} d={a.hidden} L={a.maxlen} '
                                    f'({a.blocks} blocks x {a.heads} heads), {a.items}-item bf16 table, '
                                    f'{a.users} users, loss={a.loss}, table AdamW={a.table_mode}, '
                                    f'dropout={a.dropout}'
-                                   + (f', rab_time buckets={a.time_buckets}' if a.time_buckets else ''),
+                                   + (f', rab_time buckets={a.time_buckets}' if a.time_buckets else '')
+                                   + (', fp8 (e4m3) q/k/v attention' if a.fp8 else ''),
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch, 'seq_len': a.maxlen + 1,
                        'parallelism': f'dp{world}' + ('+rowshard' if sharded else '') + ('(shard-built tables)' if shard_tables else ''),
                        'step_launch': 'hip-graph replay' if trainer.graph else 'eager',

@@ -111,6 +111,9 @@ for e in entries:
     elif k.startswith('k_ss_'):
         fb, wb, n = window_traffic(SS, ss_entries.index(e), [x['pmc_calls'] for x in ss_entries])
         name = f"{tag}_pmc_ss_{e['workload']['pass']}.json"
+    elif k.startswith('k_attn') and 'pmc_name' in e:
+        fb, wb, n = traffic(e['pmc_kernel'])
+        name = e['pmc_name']
     elif k.startswith('k_attn'):
         fb, wb, n = traffic(k + '<')
         name = f"{tag}_pmc_attn_{k[len('k_attn_'):-len('_seq')]}_{e['workload']['kind']}.json"
