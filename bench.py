@@ -62,6 +62,9 @@ def parse():
     ap.add_argument('--cpu-batch', type=int, default=128)
     ap.add_argument('--cpu-steps', type=int, default=10)
     ap.add_argument('--roofline-reps', type=int, default=20)
+    ap.add_argument('--rooflines', type=int, default=1,
+                    help='0: skip the per-kernel roofline replays (profiling runs: the trace then ends with the '
+                         'timed steps)')
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='gloo: rehearse N ranks on fewer GPUs (collectives staged via host)')
     ap.add_argument('--sharded', type=int, default=None, help='force the row-sharded optimizer (default: N > 1)')
@@ -569,6 +572,31 @@ def semantic_id_setup(a, dev, reps):
     return sid, roof
 
 
+def _rooflines(a, kv, jagged, rows, trace, btrace, model, pool, sid_roof):
+    """Every measured kernel (after the timed region): (headline roofline, the others)."""
+    from tencent_recommendation_2025_amd import jagged as J
+    dkdv, more = attention_rooflines(a, kv, a.roofline_reps, jagged=jagged)
+    more.insert(0, dkdv)
+    more.append(gather_roofline(trace, a.roofline_reps))
+    item_table = model.item_emb.weight if model.item_emb.weight.numel() else None
+    if item_table is not None:
+        more.append(item_gather_roofline(item_table.detach(), pool[0], a.roofline_reps))
+    wk = J.capacity_for(rows[0], a.jagged_quantum) if jagged else a.batch * (a.maxlen + 1)
+    more.append(wgrad_roofline(a, a.roofline_reps, wk))
+    more.extend(ss_rooflines(pool[0], a, a.roofline_reps))
+    if btrace:   # last: scripts/pmc_rooflines.py finds these calls' PMC windows at the end of the run
+        more.extend(backward_rooflines(btrace, a.roofline_reps))
+    if sid_roof is not None:
+        more.append(sid_roof)
+    # headline: the hand-written hot-path kernel with the most device time per step
+    # (average launch x launches per step), with an HBM or MFMA roof
+    ranked = [r for r in more if r.get('peak') and r.get('ms_per_step')]
+    roof = max(ranked, key=lambda r: r['ms_per_step'])
+    more.remove(roof)
+
+    return roof, more
+
+
 def main():
     a = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -679,24 +707,9 @@ def main():
         trace, G.GATHER_TRACE = G.GATHER_TRACE, None
         btrace, K.BACKWARD_TRACE = K.BACKWARD_TRACE, None
     kv = (pool[0][3] != 0).to(torch.uint8)        # the first bench batch's key validity (token_type != 0)
-    dkdv, more = attention_rooflines(a, kv, a.roofline_reps, jagged=jagged)
-    more.insert(0, dkdv)
-    more.append(gather_roofline(trace, a.roofline_reps))
-    item_table = model.item_emb.weight if model.item_emb.weight.numel() else None
-    if item_table is not None:
-        more.append(item_gather_roofline(item_table.detach(), pool[0], a.roofline_reps))
-    wk = J.capacity_for(rows[0], a.jagged_quantum) if jagged else a.batch * (a.maxlen + 1)
-    more.append(wgrad_roofline(a, a.roofline_reps, wk))
-    more.extend(ss_rooflines(pool[0], a, a.roofline_reps))
-    if btrace:   # last: scripts/pmc_rooflines.py finds these calls' PMC windows at the end of the run
-        more.extend(backward_rooflines(btrace, a.roofline_reps))
-    if sid_roof is not None:
-        more.append(sid_roof)
-    # headline: the hand-written hot-path kernel with the most device time per step
-    # (average launch x launches per step), with an HBM or MFMA roof
-    ranked = [r for r in more if r.get('peak') and r.get('ms_per_step')]
-    roof = max(ranked, key=lambda r: r['ms_per_step'])
-    more.remove(roof)
+    roof, more = None, []
+    if a.rooflines:
+        roof, more = _rooflines(a, kv, jagged, rows, trace, btrace, model, pool, sid_roof)
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline and not a.semantic_ids and not a.fp8:   # config 2's CPU model only

@@ -86,8 +86,9 @@ def bce(pl, nl, ntt):
     return crit(pl[idx], torch.ones_like(pl[idx])) + crit(nl[idx], torch.zeros_like(nl[idx]))
 
 
-def run(cfg_name, variant, d, maxlen, items, users, heads, B, steps, mods):
-    cfg = S.SyntheticConfig(batch_size=B, maxlen=maxlen, num_items=items, num_users=users)
+def run(cfg_name, variant, d, maxlen, items, users, heads, B, steps, mods, mm=True):
+    cfg = S.SyntheticConfig(batch_size=B, maxlen=maxlen, num_items=items, num_users=users,
+                            mm_ids=['81'] if mm else [])
     stats, types = S.feature_schema(cfg)
     g = torch.Generator().manual_seed(0)
     batches = [S.make_batch(cfg, g, 'cpu') for _ in range(steps + 1)]
@@ -95,7 +96,7 @@ def run(cfg_name, variant, d, maxlen, items, users, heads, B, steps, mods):
     item_f = types['item_sparse'] + types['item_array'] + types['item_emb']
     user_f = types['user_sparse'] + types['user_array']
     res = {'config': cfg_name, 'variant': variant, 'd': d, 'maxlen': maxlen, 'items': items, 'heads': heads, 'B': B,
-           'steps': steps}
+           'steps': steps, 'mm_feature_81': mm}
 
     # ---- reference ----
     args = SimpleNamespace(hidden_units=d, maxlen=maxlen, num_blocks=4, num_heads=heads, dropout_rate=0.0,
@@ -175,13 +176,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--threads', type=int, default=8)
     ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--c1-steps', type=int, default=20)
+    ap.add_argument('--c1-only', action='store_true')
     ap.add_argument('--out', default=str(REPO / 'profiles' / 'r3_cpu_speed_parity.json'))
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
     mods = ref_modules()
-    rows = [run('C1', 'baseline', 64, 50, 10_000, 10_000, 4, 128, a.steps, mods),
-            run('C1', 'o1', 64, 50, 10_000, 10_000, 4, 128, a.steps, mods),
-            run('C2', 'o1', 512, 200, 1_000_000, 1_000_000, 8, 32, a.steps, mods)]
+    # C1 also without the mm feature: the reference gathers it per token in a Python
+    # loop inside its step (model.py:281-296), which its feat2tensor timing misses
+    rows = [run('C1', 'baseline', 64, 50, 10_000, 10_000, 4, 128, a.c1_steps, mods),
+            run('C1', 'o1', 64, 50, 10_000, 10_000, 4, 128, a.c1_steps, mods),
+            run('C1', 'baseline', 64, 50, 10_000, 10_000, 4, 128, a.c1_steps, mods, mm=False),
+            run('C1', 'o1', 64, 50, 10_000, 10_000, 4, 128, a.c1_steps, mods, mm=False)]
+    if not a.c1_only:
+        rows.append(run('C2', 'o1', 512, 200, 1_000_000, 1_000_000, 8, 32, a.steps, mods))
     out = {'threads': a.threads, 'torch': torch.__version__,
            'note': 'reference imported from /root/reference in the build container; softmax-attention models '
                    '(the reference has no HSTU block); oracle inputs are tensors, the reference marshals its '

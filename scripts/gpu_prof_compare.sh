@@ -11,7 +11,7 @@ i=0
 for args in "$@"; do
   d=/tmp/kt_${TAG}_$i
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o run -- \
-    python bench.py --steps 10 --warmup 5 --cpu-baseline 0 --roofline-reps 5 $args > gpurun_out/kt_${TAG}_$i.log 2>&1
+    python bench.py --steps 10 --warmup 5 --cpu-baseline 0 --rooflines 0 $args > gpurun_out/kt_${TAG}_$i.log 2>&1
   kt=$(find $d -name "*kernel_trace.csv" | head -n 1)
   st=$(find $d -name "*kernel_stats.csv" | head -n 1)
   cp "$st" gpurun_out/${TAG}_kernel_stats_$i.csv

@@ -10,7 +10,7 @@ for mode in ${MODES:-fused sharded1}; do
   [ $mode = sharded1 ] && extra="--sharded 1"
   d=/tmp/kt_$mode
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o run -- \
-    python bench.py --steps 10 --warmup 5 --cpu-baseline 0 --roofline-reps 5 $extra > gpurun_out/kt_$mode.log 2>&1
+    python bench.py --steps 10 --warmup 5 --cpu-baseline 0 --rooflines 0 $extra > gpurun_out/kt_$mode.log 2>&1
   kt=$(find $d -name "*kernel_trace.csv" | head -n 1)
   st=$(find $d -name "*kernel_stats.csv" | head -n 1)
   cp "$st" gpurun_out/kernel_stats_$mode.csv

@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 d=/tmp/kt_$TAG
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $d -o run -- \
-  python bench.py --steps 20 --warmup 5 --cpu-baseline 0 --roofline-reps 1 "$@" > gpurun_out/kt_$TAG.log 2>&1
+  python bench.py --steps 20 --warmup 5 --cpu-baseline 0 --rooflines 0 "$@" > gpurun_out/kt_$TAG.log 2>&1
 kt=$(find $d -name "*kernel_trace.csv" | head -n 1)
 python - "$kt" > gpurun_out/${TAG}_markers.txt <<'PY'
 import csv, sys
