@@ -56,3 +56,17 @@ def test_hazard_scanner_flags_short_gaps():
             '  v_pk_mul_f32 v[62:63], v[60:61], v[64:65]\n')
     kinds = sorted({f[0] for f in scan(parse(text))})
     assert kinds == ['D-RAW/WAW', 'OPERAND', 'TRANS-USE(packed)'], kinds
+
+
+def test_python_sources_bind_every_global_they_read():
+    """Every global a function in the shipped Python (package, bench.py, the
+    graft entry, oracle, tests) reads is bound somewhere in its module
+    (scripts/undefined_names.py): a typo there would surface only when the line
+    runs on the GPU box."""
+    sys.path.insert(0, os.path.join(REPO, 'scripts'))
+    from undefined_names import undefined
+    paths = [os.path.join(REPO, p) for p in ('bench.py', '__graft_entry__.py')]
+    for d in ('tencent_recommendation_2025_amd', 'oracle', 'tests', 'scripts'):
+        paths += sorted(glob.glob(os.path.join(REPO, d, '*.py')))
+    bad = [(os.path.relpath(p, REPO), scope, n) for p in paths for scope, n in undefined(p)]
+    assert not bad, bad
