@@ -70,7 +70,7 @@ def rank_batches(cfg, rank):
     return out
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, lr=LR):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     import torch.distributed as dist
     dist.init_process_group('gloo', rank=rank, world_size=world)
@@ -78,7 +78,7 @@ def _worker(rank, world, port, q):
         from tencent_recommendation_2025_amd.sharding import ShardedFusedAdamW
         from tencent_recommendation_2025_amd.train import Trainer
         m, cfg = build()
-        opt = ShardedFusedAdamW(m, lr=LR, table_dtype=torch.float32, defer_period=3)
+        opt = ShardedFusedAdamW(m, lr=lr, table_dtype=torch.float32, defer_period=3)
         tr = Trainer(m, opt, loss='bce', amp_dtype=None)
         names = {id(p): n for n, p in m.named_parameters()}
 
@@ -99,32 +99,36 @@ def _worker(rank, world, port, q):
                    for k in shards}
         sd = {k: v.detach().float().cpu().numpy() for k, v in m.state_dict().items()
               if not k.startswith(('item_emb.', 'user_emb.'))}
-        q.put((rank, losses, shards, moments, sd, m1))
+        q.put((rank, losses, shards, moments, sd, m1, first_moments()))
     finally:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def test_world2_sharded_trainer_equals_unsharded_union_step():
-    from tencent_recommendation_2025_amd import functional as G
-    world = 2
+def run_ranks(world, lr):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, lr)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return res
 
-    # reference: one process, unsharded drop-in model, torch AdamW on every parameter
+
+def reference_run(world, lr):
+    """One process, unsharded drop-in model, torch AdamW on every parameter, on
+    loss = mean of the rank losses: (model, optimizer, per-step rank losses,
+    first moments after step 1)."""
+    from tencent_recommendation_2025_amd import functional as G
     m, cfg = build()
     batches = [rank_batches(cfg, r) for r in range(world)]
-    opt = torch.optim.AdamW(m.parameters(), lr=LR, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01)
+    opt = torch.optim.AdamW(m.parameters(), lr=lr, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01)
     names = {id(p): n for n, p in m.named_parameters()}
-    ref_m1 = None
+    ref_m1, step_losses = None, []
     for i in range(STEPS):
         opt.zero_grad()
         losses = []
@@ -137,12 +141,21 @@ def test_world2_sharded_trainer_equals_unsharded_union_step():
         opt.step()
         if i == 0:
             ref_m1 = {names[id(p)]: st['exp_avg'].cpu().numpy().copy() for p, st in opt.state.items()}
-        with torch.no_grad():
-            # step 1 sees identical parameters: tight; later steps see parameters that
-            # Adam's m / sqrt(v) has moved by +-lr on near-zero gradients (docstring)
-            tol = 1e-4 if i == 0 else 1e-3
-            for r in range(world):
-                assert abs(losses[r].item() - res[r][1][i]) < tol * max(1.0, abs(losses[r].item())), (i, r)
+        step_losses.append([x.item() for x in losses])
+    return m, opt, step_losses, ref_m1
+
+
+def test_world2_sharded_trainer_equals_unsharded_union_step():
+    world = 2
+    res = run_ranks(world, LR)
+    m, opt, step_losses, ref_m1 = reference_run(world, LR)
+    for i in range(STEPS):
+        # step 1 sees identical parameters: tight; later steps see parameters that
+        # Adam's m / sqrt(v) has moved by +-lr on near-zero gradients (docstring)
+        tol = 1e-4 if i == 0 else 1e-3
+        for r in range(world):
+            want = step_losses[i][r]
+            assert abs(want - res[r][1][i]) < tol * max(1.0, abs(want)), (i, r)
     sd = m.state_dict()
 
     def report(name, got, want, moment=False):
@@ -161,7 +174,7 @@ def test_world2_sharded_trainer_equals_unsharded_union_step():
     for k in ('item_emb', 'user_emb'):
         full = sd[f'{k}.weight'].cpu()
         st = opt.state[getattr(m, k).weight]
-        for rank, _, shards, moments, _, _ in res:
+        for rank, _, shards, moments, _, _, _ in res:
             problems.append(report(f'{k} rank {rank}', shards[k], full[rank::world].numpy()))
             problems.append(report(f'{k} exp_avg rank {rank}', moments[k][0],
                                    st['exp_avg'].cpu()[rank::world].numpy(), moment=2e-2))
@@ -175,5 +188,54 @@ def test_world2_sharded_trainer_equals_unsharded_union_step():
         if not np.array_equal(v, res[1][4][k]):
             problems.append(f'replicated {k} differs between ranks')
     problems = [p for p in problems if p]
+    assert not problems, '\n'.join(problems)
+    assert np.isfinite(res[0][1]).all()
+
+
+def test_world2_sharded_exchange_tight_at_lr0():
+    """The same two-rank run at lr = 0 (pin the exchange with tight
+    bounds).  Parameters never move, so every step of both runs sees identical
+    parameters and only the summation order of the gradients differs: rank
+    losses 1e-4 relative at EVERY step, the AdamW first moments of every
+    parameter (sharded tables reassembled from rows rank::2) normwise < 1e-5 and
+    second moments < 1e-4 after all steps, and every parameter bit-identical to
+    the reference's (p * (1 - 0 * wd) - 0 * update).  A row fetched from or
+    pushed to the wrong owner, or a remap keyed to the wrong call site, moves
+    the moments by O(1)."""
+    world = 2
+    res = run_ranks(world, 0.0)
+    m, opt, step_losses, _ = reference_run(world, 0.0)
+    for i in range(STEPS):
+        for r in range(world):
+            want = step_losses[i][r]
+            assert abs(want - res[r][1][i]) < 1e-4 * max(1.0, abs(want)), (i, r, want, res[r][1][i])
+    sd = m.state_dict()
+
+    def nrel(got, want):
+        got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+        nrm = np.linalg.norm(want)
+        return float(np.linalg.norm(got - want) / (nrm if nrm > 0 else 1.0))
+
+    problems = []
+    for k in ('item_emb', 'user_emb'):
+        full = sd[f'{k}.weight'].cpu().numpy()
+        st = opt.state[getattr(m, k).weight]
+        for rank, _, shards, moments, _, _, _ in res:
+            if not np.array_equal(shards[k], full[rank::world]):
+                problems.append(f'{k} rank {rank}: table rows moved at lr 0')
+            e1 = nrel(moments[k][0], st['exp_avg'].cpu()[rank::world].numpy())
+            e2 = nrel(moments[k][1], st['exp_avg_sq'].cpu()[rank::world].numpy())
+            if e1 >= 1e-5 or e2 >= 1e-4:
+                problems.append(f'{k} rank {rank}: moments normwise {e1:.2e} / {e2:.2e}')
+    params = dict(m.named_parameters())
+    for n, v in res[0][6].items():        # the dense / replicated parameters' first moments
+        if n in ('item_emb', 'user_emb'):
+            continue
+        e1 = nrel(v, opt.state[params[n]]['exp_avg'].cpu().numpy())
+        if e1 >= 1e-5:
+            problems.append(f'{n}: exp_avg normwise {e1:.2e}')
+    for k, v in res[0][4].items():
+        if not np.array_equal(v, sd[k].cpu().float().numpy()):
+            problems.append(f'{k} moved at lr 0')
     assert not problems, '\n'.join(problems)
     assert np.isfinite(res[0][1]).all()
