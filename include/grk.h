@@ -146,13 +146,16 @@ int grk_sort_pairs(const uint32_t* keys_in, const uint64_t* vals_in, uint32_t* k
  *              entries of untouched rows are left as they were (-1 by
  *              contract; grk_table_adamw restores them).
  * flags: GRK_BWD_ORDERED (every row in occurrence order, as above) or
- *   GRK_BWD_CHUNKED: a row spanning several 256-occurrence chunks of the
- *   sorted list is summed per chunk (occurrence order) and the chunk sums are
- *   added in chunk order -- deterministic, not the sequential order.  For
- *   tables that are intermediates with no reference counterpart (the fused
- *   trainer's projected feature rows); honoured when dim is 64 x (8 bf16 /
- *   4 or 8 fp32 elements), otherwise the call runs ordered. */
+ *   GRK_BWD_CHUNKED: a row spanning several chunks of the sorted list
+ *   (grk_embedding_chunked_size() occurrences each: 256 unless the library
+ *   was built with -DGRK_CHUNKED_CH=64 / 128) is summed per chunk (occurrence
+ *   order) and the chunk sums are added in chunk order -- deterministic, not
+ *   the sequential order.  For tables that are intermediates with no
+ *   reference counterpart (the fused trainer's projected feature rows);
+ *   honoured when dim is 64 x (8 bf16 / 4 or 8 fp32 elements), otherwise the
+ *   call runs ordered. */
 enum { GRK_BWD_ORDERED = 0, GRK_BWD_CHUNKED = 1 };
+int grk_embedding_chunked_size(void);
 int grk_embedding_backward(const grk_lookup* lookups, int num_lookups, int dim, int grad_dtype, int itype,
                            const int32_t* token_type, int32_t seq_len, int64_t num_rows, int64_t padding_idx,
                            float* dense_out, int64_t* uniq_ids, float* uniq_rows, int32_t* uniq_count,

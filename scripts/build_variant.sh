@@ -1,0 +1,28 @@
+#!/bin/bash
+# An A/B build of libgrk.so: the in-tree objects (make first) with ONE source
+# recompiled under extra flags, linked to abtest/libgrk_<name>.so (git-ignored,
+# travels with gpurun; bench / tests pick it with GRK_LIB=...).
+#   bash scripts/build_variant.sh ch64 grk_embedding "-DGRK_CHUNKED_CH=64"
+#   then on the box: bash scripts/gpu_ab.sh 3 "tencent_recommendation_2025_amd/libgrk.so abtest/libgrk_ch64.so"
+set -e -o pipefail
+NAME=$1; SRC=$2; FLAGS=$3
+cd "$(dirname "$0")/.."
+HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
+make -s
+mkdir -p abtest/obj
+# the per-object flags of the Makefile for this source (attention: VGPR-form MFMA, no SLP)
+EXTRA=""
+case $SRC in
+  grk_attention_seq) EXTRA="-mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize" ;;
+  grk_rqvae) EXTRA="-ffp-contract=off" ;;
+esac
+$HIPCC --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Iinclude -Wall -Wno-unused-function -Wno-unused-variable \
+  -Wno-unused-but-set-variable $EXTRA $FLAGS -x hip -c tencent_recommendation_2025_amd/csrc/$SRC.hip \
+  -o abtest/obj/$SRC.$NAME.o
+OBJS=$(ls build/obj/*.o | grep -v "/$SRC.o$")
+if ! out=$(python3 scripts/check_mfma_overlap.py abtest/obj/$SRC.$NAME.o 2>&1); then
+  echo "$out" | grep -q "no gfx950 MFMA code" || { echo "$out"; exit 1; }
+fi
+$HIPCC --offload-arch=gfx950 -shared -fPIC -o abtest/libgrk_$NAME.so $OBJS abtest/obj/$SRC.$NAME.o \
+  -L/opt/rocm/lib -lhipblaslt
+echo abtest/libgrk_$NAME.so

@@ -93,6 +93,7 @@ SIGNATURES = {
     'grk_silu_fp8': (_I, [_P, _I64, _I64, _I, _P, _I64, _P]),
     'grk_dsilu_mul': (_I, [_P, _I64, _P, _I64, _I64, _I, _P]),
     'grk_embedding_backward_workspace': (_SZ, [_I64, _I64, _I]),
+    'grk_embedding_chunked_size': (_I, []),
     'grk_sort_pairs_workspace': (_SZ, [_I64]),
     'grk_sort_pairs': (_I, [_P, _P, _P, _P, _P, _P, _I64, _I, _P, _SZ, _P]),
     'grk_embedding_backward': (_I, [C.POINTER(GrkLookup), _I, _I, _I, _I, _P, C.c_int32, _I64, _I64, _P, _P, _P,

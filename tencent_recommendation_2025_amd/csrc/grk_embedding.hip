@@ -579,7 +579,18 @@ __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __res
 // continuing into the next -> slot 1), and one wave per such row adds its
 // pieces in chunk order.  Deterministic (fixed order), and a hot row of k
 // occurrences costs k / kRedChunk dependent adds instead of k.
-template <typename G, int LW>
+//
+// The chunk length is a build constant (GRK_CHUNKED_CH, 256 by default; 64 /
+// 128 for A/B builds: more waves in flight on a call of ~0.5M occurrences, more
+// pieces per hot row); grk_embedding_chunked_size() reports it, so callers
+// that restate the order (oracle/embedding.chunked_backward) take it from there.
+#ifndef GRK_CHUNKED_CH
+#define GRK_CHUNKED_CH 256
+#endif
+constexpr int kPartialChunk = GRK_CHUNKED_CH;
+static_assert(kPartialChunk == 64 || kPartialChunk == 128 || kPartialChunk == 256, "GRK_CHUNKED_CH: 64, 128 or 256");
+
+template <typename G, int LW, int CH>
 __global__ void __launch_bounds__(256) k_seg_chunks_partial(const unsigned* __restrict__ keys,
                                                             const unsigned long long* __restrict__ gptr,
                                                             const int* __restrict__ pos,
@@ -589,14 +600,14 @@ __global__ void __launch_bounds__(256) k_seg_chunks_partial(const unsigned* __re
                                                             float* __restrict__ uniq_rows,
                                                             int32_t* __restrict__ row_slot,
                                                             float* __restrict__ partials) {
-  seg_chunks_wave_body<G, LW>((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, keys, gptr, pos,
-                              seg_start, seg_end, n, sentinel, dim, dense_out, uniq_rows, row_slot, partials);
+  seg_chunks_wave_body<G, LW, CH>((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, keys, gptr, pos,
+                                  seg_start, seg_end, n, sentinel, dim, dense_out, uniq_rows, row_slot, partials);
 }
 
 // One wave per chunk edge b: the row first crossing b (it starts in chunk
 // b - 1, whose tail slot holds its first piece) = tail(b - 1) + head(b) + ...
 // + head(last chunk of the row), added in that order.
-template <int LW>
+template <int LW, int CH>
 __global__ void __launch_bounds__(256) k_seg_partials_combine(const unsigned* __restrict__ keys,
                                                               const int* __restrict__ pos,
                                                               const int* __restrict__ seg_start,
@@ -609,14 +620,14 @@ __global__ void __launch_bounds__(256) k_seg_partials_combine(const unsigned* __
   constexpr int PIPE = 8;
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) + 1;
-  const int64_t pb = b * kRedChunk;
+  const int64_t pb = b * CH;
   if (pb >= n) return;
   const unsigned key = keys[pb];
   if (key == sentinel || keys[pb - 1] != key) return;
   const int u = pos[pb] - 1;
   const int su = seg_start[u], eu = seg_end[u];
-  if (su / kRedChunk != b - 1) return;  // crosses an earlier edge: combined there
-  const int64_t last = (eu - 1) / kRedChunk;
+  if (su / CH != b - 1) return;  // crosses an earlier edge: combined there
+  const int64_t last = (eu - 1) / CH;
   const int c = lane * LW;
   WaveAcc<LW> acc;
   const float* t = partials + ((b - 1) * 2 + 1) * dim + c;
@@ -897,7 +908,7 @@ static int plan_ws(int64_t n, int64_t num_rows, int dim, char* base, BwdWs* ws) 
   ws->seg_end = (int*)take(n * 4);
   ws->gptr_in = (unsigned long long*)take(n * 8);
   ws->gptr_out = (unsigned long long*)take(n * 8);
-  ws->partials = (float*)take((size_t)((n + kRedChunk - 1) / kRedChunk) * 2 * dim * sizeof(float));
+  ws->partials = (float*)take((size_t)((n + kPartialChunk - 1) / kPartialChunk) * 2 * dim * sizeof(float));
   unsigned end_bit = 1;
   while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
   size_t sb = 0, cb = 0;
@@ -1010,6 +1021,8 @@ extern "C" int grk_embedding_gather(const grk_feature* features, int num_feature
   return GRK_OK;
 }
 
+extern "C" int grk_embedding_chunked_size(void) { return kPartialChunk; }
+
 extern "C" size_t grk_embedding_backward_workspace(int64_t num_occurrences, int64_t num_rows, int dim) {
   BwdWs ws;
   if (plan_ws(num_occurrences, num_rows, dim, nullptr, &ws) != GRK_OK) return 0;
@@ -1110,17 +1123,19 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   const int64_t chunks = (total + kRedChunk - 1) / kRedChunk;
   const int lw = dim % 64 == 0 ? dim / 64 : 0;  // elements per lane with one wave per row
   if ((grad_dtype == GRK_BF16 && lw == 8) || (grad_dtype != GRK_BF16 && (lw == 4 || lw == 8))) {
-    const unsigned gw = (unsigned)((chunks + 3) / 4);
-    const unsigned ge = (unsigned)(chunks > 1 ? (chunks - 1 + 3) / 4 : 0);
     if (flags == GRK_BWD_CHUNKED) {
-#define GRK_SEGP(G, LW)                                                                                         \
-  k_seg_chunks_partial<G, LW><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end,    \
-                                                 total, sentinel, dim, dense_out, uniq_rows, row_slot,         \
-                                                 ws.partials);                                                 \
-  GRK_LAUNCH_CHECK();                                                                                           \
-  if (ge)                                                                                                       \
-    k_seg_partials_combine<LW><<<ge, 256, 0, s>>>(ws.keys_out, ws.pos, ws.seg_start, ws.seg_end, total,         \
-                                                  sentinel, dim, ws.partials, dense_out, uniq_rows, row_slot)
+      const int64_t pchunks = (total + kPartialChunk - 1) / kPartialChunk;
+      const unsigned gw = (unsigned)((pchunks + 3) / 4);
+      const unsigned ge = (unsigned)(pchunks > 1 ? (pchunks - 1 + 3) / 4 : 0);
+#define GRK_SEGP(G, LW)                                                                                          \
+  k_seg_chunks_partial<G, LW, kPartialChunk><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start,  \
+                                                                ws.seg_end, total, sentinel, dim, dense_out,     \
+                                                                uniq_rows, row_slot, ws.partials);               \
+  GRK_LAUNCH_CHECK();                                                                                            \
+  if (ge)                                                                                                        \
+    k_seg_partials_combine<LW, kPartialChunk><<<ge, 256, 0, s>>>(ws.keys_out, ws.pos, ws.seg_start, ws.seg_end,  \
+                                                                 total, sentinel, dim, ws.partials, dense_out,    \
+                                                                 uniq_rows, row_slot)
       if (grad_dtype == GRK_BF16) { GRK_SEGP(bf16_t, 8); }
       else if (lw == 8) { GRK_SEGP(float, 8); }
       else { GRK_SEGP(float, 4); }

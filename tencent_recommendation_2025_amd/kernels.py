@@ -164,6 +164,12 @@ def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, s
     return BackwardResult(dense_out, ids, rows, count, cap)
 
 
+def chunked_size():
+    """Chunk length of the GRK_BWD_CHUNKED order (a build constant of the
+    library: oracle/embedding.chunked_backward restates the order with it)."""
+    return int(L.lib().grk_embedding_chunked_size())
+
+
 def sort_pairs(keys, vals, end_bit=32):
     """grk_sort_pairs: (keys, vals) stably sorted by the low ``end_bit`` bits of
     the keys (uint32 keys as int32, uint64 values as int64 tensors)."""

@@ -69,6 +69,8 @@ def test_workspace_query_needs_no_device(lib):
     n = 77184
     got = lib.lib().grk_embedding_backward_workspace(n, 1_000_001, 512)
     per_occ = 7 * 4 + 2 * 8                      # keys in / out / seg, flags, pos, seg start / end; 2 addresses
-    partials = -(-n // 256) * 2 * 512 * 4          # chunked mode: two piece sums per 256-entry chunk
+    ch = lib.lib().grk_embedding_chunked_size()
+    assert ch in (64, 128, 256)
+    partials = -(-n // ch) * 2 * 512 * 4           # chunked mode: two piece sums per chunk
     assert got >= n * per_occ + partials and got < n * per_occ + partials + (1 << 20)
     assert lib.lib().grk_sort_pairs_workspace(n) > 0

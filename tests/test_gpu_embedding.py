@@ -304,7 +304,7 @@ def test_backward_chunked_mode(K, D, dt):
     gg = np.concatenate([g[:, :D], g[:, D:]])
     ii = np.concatenate([idx, rev])
     got = res.dense.cpu().numpy()
-    assert np.array_equal(got, oemb.chunked_backward(gg, ii, R))
+    assert np.array_equal(got, oemb.chunked_backward(gg, ii, R, chunk=K.chunked_size()))
     exact = oemb.dense_backward(gg, ii, R)
     np.testing.assert_allclose(got, exact, rtol=1e-4, atol=1e-3)
     counts = np.bincount(ii, minlength=R)
@@ -312,7 +312,7 @@ def test_backward_chunked_mode(K, D, dt):
     small[0] = False
     assert small.sum() > 1000
     # rows of a handful of occurrences sit in one chunk unless they straddle an edge
-    assert np.mean(np.all(got[small] == exact[small], axis=1)) > 0.9
+    assert np.mean(np.all(got[small] == exact[small], axis=1)) > min(0.9, 1 - 12 / K.chunked_size())
     cnt = int(res.count.item())
     uniq = oemb.unique_rows(ii)
     assert cnt == len(uniq) and np.array_equal(res.ids[:cnt].cpu().numpy(), uniq)
