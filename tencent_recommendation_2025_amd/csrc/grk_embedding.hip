@@ -371,7 +371,12 @@ __global__ void __launch_bounds__(256) k_seg_combine(const unsigned long long* _
 // step; whether a piece is a whole segment follows from the neighbouring keys
 // (keys[p0-1], keys[p1]), so seg_start / seg_end are read only for the (at
 // most two) pieces that cross the chunk's edges.
-constexpr int kWavePipe = 16;
+// (GRK_WAVE_PIPE: a build constant for A/B builds, scripts/build_variant.sh)
+#ifndef GRK_WAVE_PIPE
+#define GRK_WAVE_PIPE 16
+#endif
+constexpr int kWavePipe = GRK_WAVE_PIPE;
+static_assert(kWavePipe == 8 || kWavePipe == 16 || kWavePipe == 32, "GRK_WAVE_PIPE: 8, 16 or 32");
 
 // (readlane returns int: both halves go through unsigned, or the low word
 // would sign-extend into the high one)
