@@ -26,20 +26,36 @@
 
 namespace grk {
 
+// HSTU time bias in the chunked kernels (TB instantiations): stamps relative to
+// the sequence's first valid key, clamped to +-(2^30 - 1), 0 past T -- the
+// whole-sequence kernels' stage_time convention, so both paths bucket alike.
+__device__ __forceinline__ int rel_stamp(const AttnParams& p, int b, int T, int start, int j) {
+  const int64_t base = start < T ? p.ts[(int64_t)b * T + start] : 0;
+  const int64_t lim = (1 << 30) - 1;
+  const int64_t d = j < T ? p.ts[(int64_t)b * T + j] - base : 0;
+  return (int)(d > lim ? lim : (d < -lim ? -lim : d));
+}
+// LDS of the TB instantiations: kChunk staged stamps, the head's rab_t row and
+// (dQ) the drab_t fixed-point bins.
+constexpr int kTimeLds = kChunk * 4 + kMaxTimeBuckets * 4 + kMaxTimeBuckets * 8;
+
 // ================================================================ forward ====
 // F8: q/k/v are fp8 e4m3 (post-activation): S^T = K Q^T on the fp8 MFMA from
 // an fp8 K image and fp8 Q fragments; V staged as (exact) bf16 for P V.
-template <int HD, int KIND, bool F8>
+// TB: with the HSTU time bias rab_t[h, time_bucket(t_q - t_k)] (KIND 1, not F8).
+template <int HD, int KIND, bool F8, bool TB = false>
 __global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
   constexpr int IMG = kChunk * HD * 2;
   constexpr int RAB = KIND == 1 ? kRabMax : 4;
-  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 64 + RAB * 4 + 16];
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 64 + RAB * 4 + 16 + (TB ? kTimeLds : 0)];
   char* Ks = smem;
   char* Vs = smem + IMG;
   uint8_t* kvs = reinterpret_cast<uint8_t*>(smem + 2 * IMG);
   float* rabs = reinterpret_cast<float*>(smem + 2 * IMG + 64);
   int* s_start = reinterpret_cast<int*>(smem + 2 * IMG + 64 + RAB * 4);
+  int* tsk = reinterpret_cast<int*>(smem + 2 * IMG + 64 + RAB * 4 + 16);  // TB: key stamps of the chunk
+  float* rtab = reinterpret_cast<float*>(tsk + kChunk);                    // TB: rab_t[h, :]
 
   const int b = blockIdx.z, h = blockIdx.y, T = p.T;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
@@ -48,6 +64,11 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
   const int start = seq_start(p.key_valid, b, T, s_start);
   if (KIND == 1)
     for (int j = threadIdx.x; j < p.nb; j += blockDim.x) rabs[j] = p.rab[h * p.nb + j];
+  int tq = 0;
+  if constexpr (TB) {
+    for (int j = threadIdx.x; j < p.nbt; j += blockDim.x) rtab[j] = p.rab_t[h * p.nbt + j];
+    tq = rel_stamp(p, b, T, start, myq);
+  }
 
   bf16x8 qf[F8 ? 1 : KS];
   f8x8 qf8[F8 ? KS : 1];
@@ -86,6 +107,7 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
     if (threadIdx.x < kChunk) {
       const int t = kc + threadIdx.x;
       kvs[threadIdx.x] = (t < T) && (!p.key_valid || p.key_valid[(int64_t)b * T + t]);
+      if constexpr (TB) tsk[threadIdx.x] = rel_stamp(p, b, T, start, t);
     }
     __syncthreads();
 #pragma unroll
@@ -135,7 +157,8 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AttnParams p) {
         for (int i = 0; i < 16; ++i) {
           const int kr = 32 * sub + acc_row(i, hh), key = kc + kr;
           const bool ok = qok && key <= myq && kvs[kr];
-          const float sp = s[i] * p.scale + rabs[ok ? min(myq - key, p.nb - 1) : 0];
+          float sp = s[i] * p.scale + rabs[ok ? min(myq - key, p.nb - 1) : 0];
+          if constexpr (TB) sp += rtab[time_bucket(tq - tsk[kr], p.nbt)];
           pd[i] = ok ? silu(sp) * p.inv_n : 0.f;
         }
       }
@@ -192,18 +215,21 @@ __global__ void __launch_bounds__(256) k_attn_delta(AttnParams p) {
 
 // ================================================================ dQ =========
 // F8: fp8 q/k/v read as (exact) bf16; all products on the bf16 MFMA.
-template <int HD, int KIND, bool F8>
+template <int HD, int KIND, bool F8, bool TB = false>
 __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
   constexpr int IMG = kChunk * HD * 2;
   constexpr int RAB = KIND == 1 ? kRabMax : 4;
-  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 64 + 3 * RAB * 4 + 16];
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 64 + 3 * RAB * 4 + 16 + (TB ? kTimeLds : 0)];
   char* Ks = smem;
   char* Vs = smem + IMG;
   uint8_t* kvs = reinterpret_cast<uint8_t*>(smem + 2 * IMG);
   float* rabs = reinterpret_cast<float*>(smem + 2 * IMG + 64);
   unsigned long long* bins = reinterpret_cast<unsigned long long*>(rabs + RAB);  // int64 fixed point
   int* s_start = reinterpret_cast<int*>(smem + 2 * IMG + 64 + 3 * RAB * 4);
+  int* tsk = reinterpret_cast<int*>(smem + 2 * IMG + 64 + 3 * RAB * 4 + 16);  // TB: key stamps of the chunk
+  float* rtab = reinterpret_cast<float*>(tsk + kChunk);                        // TB: rab_t[h, :]
+  unsigned long long* tbins = reinterpret_cast<unsigned long long*>(rtab + kMaxTimeBuckets);  // TB: drab_t bins
 
   const int b = blockIdx.z, h = blockIdx.y, T = p.T;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
@@ -215,6 +241,14 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
       rabs[j] = p.rab[h * p.nb + j];
       bins[j] = 0ull;
     }
+  int tq = 0;
+  if constexpr (TB) {
+    for (int j = threadIdx.x; j < p.nbt; j += blockDim.x) {
+      rtab[j] = p.rab_t[h * p.nbt + j];
+      tbins[j] = 0ull;
+    }
+    tq = rel_stamp(p, b, T, start, myq);
+  }
   const int bh = b * p.H + h;
   const int64_t tok = (int64_t)b * T + (qok ? myq : 0);
 
@@ -248,6 +282,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
     if (threadIdx.x < kChunk) {
       const int t = kc + threadIdx.x;
       kvs[threadIdx.x] = (t < T) && (!p.key_valid || p.key_valid[(int64_t)b * T + t]);
+      if constexpr (TB) tsk[threadIdx.x] = rel_stamp(p, b, T, start, t);
     }
     __syncthreads();
 #pragma unroll
@@ -272,9 +307,16 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
           ds[i] = pv * (dpv - dlt);
         } else {
           const int bk = min(myq - key, p.nb - 1);
-          const float sp = s[i] * p.scale + rabs[ok ? bk : 0];
+          float sp = s[i] * p.scale + rabs[ok ? bk : 0];
+          int tbk = 0;
+          if constexpr (TB) {
+            tbk = time_bucket(tq - tsk[kr], p.nbt);
+            sp += rtab[tbk];
+          }
           ds[i] = ok ? dp[i] * dsilu(sp) * p.inv_n : 0.f;
           if (ok && ds[i] != 0.f && p.drab) atomicAdd(&bins[bk], to_fix(ds[i]));
+          if constexpr (TB)
+            if (ok && ds[i] != 0.f && p.drab_t) atomicAdd(&tbins[tbk], to_fix(ds[i]));
         }
       }
 #pragma unroll
@@ -292,23 +334,29 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dq(AttnParams p) {
   }
   store_rows<HD, NDT>(p.dq, p.lddq, p.out_f32, (int64_t)b * T + myq, h, hh, acc, p.scale, qok,
                       p.act ? p.q : nullptr, p.ldq);
-  if (KIND == 1 && p.drab) {
+  if (KIND == 1 && (p.drab || (TB && p.drab_t))) {
     __syncthreads();
-    for (int j = threadIdx.x; j < p.nb; j += blockDim.x)
-      if (bins[j] != 0ull) atomicAdd(&p.drab_fix[h * p.nb + j], bins[j]);
+    if (p.drab)
+      for (int j = threadIdx.x; j < p.nb; j += blockDim.x)
+        if (bins[j] != 0ull) atomicAdd(&p.drab_fix[h * p.nb + j], bins[j]);
+    if constexpr (TB)
+      if (p.drab_t)
+        for (int j = threadIdx.x; j < p.nbt; j += blockDim.x)
+          if (tbins[j] != 0ull) atomicAdd(&p.drab_t_fix[h * p.nbt + j], tbins[j]);
   }
 }
 
 // ============================================================== dK / dV =====
 // F8: S = Q K^T on the fp8 MFMA (fp8 Q image + fp8 K fragments); Q also
 // staged as (exact) bf16 for dK = dS^T Q, V fragments as bf16 for dP.
-template <int HD, int KIND, bool F8>
+template <int HD, int KIND, bool F8, bool TB = false>
 __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
   constexpr int IMG = kChunk * HD * 2;
   constexpr int IMG8 = F8 ? kChunk * HD : 0;
   constexpr int RAB = KIND == 1 ? kRabMax : 4;
-  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + IMG8 + 2 * kChunk * 4 + RAB * 4 + 16];
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + IMG8 + 2 * kChunk * 4 + RAB * 4 + 16 +
+                                                    (TB ? kTimeLds : 0)];
   char* Qs = smem;
   char* Ds = smem + IMG;
   char* Q8s = smem + 2 * IMG + 2 * kChunk * 4 + RAB * 4 + 16;
@@ -316,6 +364,8 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
   float* dlts = lses + kChunk;
   float* rabs = dlts + kChunk;
   int* s_start = reinterpret_cast<int*>(smem + 2 * IMG + 2 * kChunk * 4 + RAB * 4);
+  int* tsq = reinterpret_cast<int*>(smem + 2 * IMG + IMG8 + 2 * kChunk * 4 + RAB * 4 + 16);  // TB: query stamps
+  float* rtab = reinterpret_cast<float*>(tsq + kChunk);                                      // TB: rab_t[h, :]
 
   const int b = blockIdx.z, h = blockIdx.y, T = p.T;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
@@ -324,6 +374,11 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
   const bool kok = myk < T && myk >= start && (!p.key_valid || p.key_valid[(int64_t)b * T + myk]);
   if (KIND == 1)
     for (int j = threadIdx.x; j < p.nb; j += blockDim.x) rabs[j] = p.rab[h * p.nb + j];
+  int tk = 0;
+  if constexpr (TB) {
+    for (int j = threadIdx.x; j < p.nbt; j += blockDim.x) rtab[j] = p.rab_t[h * p.nbt + j];
+    tk = rel_stamp(p, b, T, start, myk);
+  }
   const int bh = b * p.H + h;
   const int64_t tok = (int64_t)b * T + (myk < T ? myk : 0);
 
@@ -368,6 +423,7 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
       }
       lses[threadIdx.x] = lv;
       dlts[threadIdx.x] = dl;
+      if constexpr (TB) tsq[threadIdx.x] = rel_stamp(p, b, T, start, t);
     }
     __syncthreads();
 #pragma unroll
@@ -398,7 +454,8 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
           }
           ds[i] = pv * (dpv - dlts[qr]);
         } else {
-          const float sp = s[i] * p.scale + rabs[ok ? min(q - myk, p.nb - 1) : 0];
+          float sp = s[i] * p.scale + rabs[ok ? min(q - myk, p.nb - 1) : 0];
+          if constexpr (TB) sp += rtab[time_bucket(tsq[qr] - tk, p.nbt)];
           pd[i] = ok ? silu(sp) * p.inv_n : 0.f;
           ds[i] = ok ? dp[i] * dsilu(sp) * p.inv_n : 0.f;
         }
@@ -430,17 +487,21 @@ __global__ void __launch_bounds__(256) k_attn_bwd_dkdv(AttnParams p) {
 template <int HD, bool F8 = false>
 static int launch_hd(const AttnParams& p, int which, hipStream_t s) {
   dim3 grid((p.T + kBlockRows - 1) / kBlockRows, p.H, p.B);
+  const bool tb = !F8 && p.kind == GRK_ATTN_HSTU && p.nbt > 0;  // fill_params: fp8 q/k/v take no time bias
   if (which == 0) {
     if (p.kind == GRK_ATTN_SOFTMAX) k_attn_fwd<HD, 0, F8><<<grid, 256, 0, s>>>(p);
+    else if (tb) k_attn_fwd<HD, 1, false, true><<<grid, 256, 0, s>>>(p);
     else k_attn_fwd<HD, 1, F8><<<grid, 256, 0, s>>>(p);
   } else if (which == 1) {
     const int64_t waves = (int64_t)p.B * p.T * p.H;
     k_attn_delta<HD><<<(unsigned)((waves + 3) / 4), 256, 0, s>>>(p);
   } else if (which == 2) {
     if (p.kind == GRK_ATTN_SOFTMAX) k_attn_bwd_dq<HD, 0, F8><<<grid, 256, 0, s>>>(p);
+    else if (tb) k_attn_bwd_dq<HD, 1, false, true><<<grid, 256, 0, s>>>(p);
     else k_attn_bwd_dq<HD, 1, F8><<<grid, 256, 0, s>>>(p);
   } else {
     if (p.kind == GRK_ATTN_SOFTMAX) k_attn_bwd_dkdv<HD, 0, F8><<<grid, 256, 0, s>>>(p);
+    else if (tb) k_attn_bwd_dkdv<HD, 1, false, true><<<grid, 256, 0, s>>>(p);
     else k_attn_bwd_dkdv<HD, 1, F8><<<grid, 256, 0, s>>>(p);
   }
   GRK_LAUNCH_CHECK();
@@ -473,7 +534,9 @@ static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
               "fit them", p.T, hd);
     return GRK_EUNSUPPORTED;
   }
-  if (p.nbt > 0 && which != 1) {
+  // The chunked kernels' time bias (TB instantiations) is built but refused until
+  // its parity test has run on hardware (GRK_ATTN_CHUNKED_TIME=1 opts in).
+  if (p.nbt > 0 && which != 1 && (hd > 128 || !getenv("GRK_ATTN_CHUNKED_TIME"))) {
     set_error("the HSTU time bias runs in the whole-sequence kernels only: T = %d x head_dim %d does not fit them",
               p.T, hd);
     return GRK_EUNSUPPORTED;
