@@ -68,6 +68,9 @@ def parse():
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='gloo: rehearse N ranks on fewer GPUs (collectives staged via host)')
     ap.add_argument('--sharded', type=int, default=None, help='force the row-sharded optimizer (default: N > 1)')
+    ap.add_argument('--sharded-jagged', type=int, default=0,
+                    help='1: the row-sharded trainer on jagged rows too (train.jagged_remaps; opt-in until verified '
+                         'on hardware -- the sharded step runs the padded layout by default)')
     ap.add_argument('--shard-tables', type=int, default=None,
                     help='build only each rank\'s table rows (default: sharded and >= 10M items, BASELINE config 3)')
     ap.add_argument('--graph', type=int, default=1,
@@ -641,7 +644,8 @@ def main():
     else:
         opt = FusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
     # the jagged layout runs on the whole-sequence attention kernels (T <= 256 at hd <= 128, not fp8)
-    jagged = bool(a.jagged) and not sharded and not a.fp8 and a.maxlen + 1 <= 256 and a.hidden // a.heads <= 128
+    jagged = (bool(a.jagged) and (not sharded or bool(a.sharded_jagged)) and not a.fp8 and a.maxlen + 1 <= 256
+              and a.hidden // a.heads <= 128)
     trainer = Trainer(model, opt, loss=a.loss, graph=bool(a.graph), jagged=jagged, jagged_quantum=a.jagged_quantum)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [S.make_batch(cfg, gen, dev) for _ in range(max(2, a.pool))]

@@ -60,6 +60,28 @@ def _clone_batch(batch):
     return tuple(res)
 
 
+def jagged_remaps(remaps, parts, row_map):
+    """Row-sharded tables + jagged rows: the remaps ShardedFusedAdamW.prepare built
+    for the [B, T] batch ({(table, role, mode): (fetched rows, fetched-row index
+    [B, T])}) re-indexed to the jagged order -- index[r] = index[row_map[r]].  A row
+    past the span rows (row_map -1, a dead row: zero ids, no loss term, exact-zero
+    gradient) reads the fetched row of the role's first padding id, as its zero id
+    would.  ``parts``: ShardedFusedAdamW._parts(batch) (each role's ids).  Device
+    ops only (no host sync: capturable)."""
+    ids = {(name, role, mode): v for name, plist in parts.items() for role, _, mode, v in plist}
+    rm = row_map.long()
+    src = rm.clamp(min=0)
+    out = {}
+    for key, (ref, inv) in remaps.items():
+        flat = inv.reshape(-1)
+        v = ids.get(key)
+        if v is None:   # a derived role (feat2emb_pair's 'pair' is rebuilt from pos / neg)
+            continue
+        pad = torch.argmax((v().reshape(-1) == 0).to(torch.int8))   # first padding position (0 if none)
+        out[key] = (ref, torch.where(rm >= 0, flat[src], flat[pad]).unsqueeze(0))
+    return out
+
+
 class Trainer:
     """``step(batch)`` = one training step on a tensorised batch
     (``MyDataset.collate_tensor_fn`` layout, tensors on the device).
@@ -107,8 +129,6 @@ class Trainer:
         self._side = None
         self._sharded = hasattr(optimizer, 'prepare')
         self.jagged, self.jagged_quantum = bool(jagged), int(jagged_quantum)
-        if self.jagged and self._sharded:
-            raise ValueError('jagged=True: the row-sharded optimizer routes padded batches (use jagged=False)')
         self._cap = None         # jagged capacity of the current step
 
     def _graph_blocker(self):
@@ -129,6 +149,10 @@ class Trainer:
         if self.jagged:
             cap = self._cap if self._cap is not None else J.capacity_for(J.span_rows(tt), self.jagged_quantum)
             jag = J.layout(tt, cap, ntt)
+            if self._sharded and getattr(self.model, '_remaps', None) is not None:
+                # prepare() routed the [B, T] batch: its lookups' fetched-row indices follow
+                # the batch into the jagged row order
+                self.model._remaps = jagged_remaps(self.model._remaps, self.opt._parts(batch), jag.row_map)
             seq, pos, neg, tt, ntt, _nat, sf, pf, nf, ts, pidx = J.compact(batch, jag)
         with amp:
             h, pe, ne = self.model.encode(seq, pos, neg, tt, sf, pf, nf, timestamps=ts, jagged=jag, pos_idx=pidx)

@@ -137,3 +137,48 @@ def test_grad_buckets_average_over_ranks():
     for r in res:
         assert not r[3].any()
         assert r[5] > 2 and 0 < r[4] < r[5]   # some buckets went out during backward, the last at finish()
+
+
+def test_jagged_remaps_follow_the_row_map():
+    """train.jagged_remaps (row-sharded tables + jagged rows, CPU): every role's
+    fetched-row index moves with its token into the jagged order (row r <- token
+    row_map[r]); a dead row (row_map -1) reads the fetched row of the role's first
+    padding id; derived roles are left to the model."""
+    from tencent_recommendation_2025_amd.sharding import ShardedFusedAdamW
+    from tencent_recommendation_2025_amd.train import jagged_remaps
+    g = torch.Generator().manual_seed(3)
+    B, T, cap = 4, 9, 32
+    starts = [0, 3, 8, 5]
+    tt = torch.zeros(B, T, dtype=torch.int64)
+    for b, s0 in enumerate(starts):
+        tt[b, s0:] = 1
+        tt[b, s0] = 2                                   # the user token
+    seq = torch.randint(1, 50, (B, T), generator=g) * (tt != 0)
+    pos = torch.randint(1, 50, (B, T), generator=g) * (tt != 0)
+    neg = torch.randint(1, 50, (B, T), generator=g) * (tt != 0)
+    batch = (seq, pos, neg, tt)
+    parts = ShardedFusedAdamW._parts(batch)
+    remaps, fetched = {}, object()
+    for name, plist in parts.items():
+        for role, idx, mode, v in plist:
+            ids = v()
+            _, inv = torch.unique(ids.reshape(-1), return_inverse=True)   # what prepare() builds
+            remaps[(name, role, mode)] = (fetched, inv.view(B, T))
+    span = [(b, t) for b in range(B) for t in range(starts[b], T)]
+    row_map = torch.full((cap,), -1, dtype=torch.int32)
+    row_map[:len(span)] = torch.tensor([b * T + t for b, t in span], dtype=torch.int32)
+    out = jagged_remaps(remaps, parts, row_map)
+    assert set(out) == set(remaps)
+    for key, (ref, inv) in remaps.items():
+        ref2, got = out[key]
+        assert ref2 is ref and got.shape == (1, cap)
+        flat = inv.reshape(-1)
+        want = flat[row_map[:len(span)].long()]
+        assert torch.equal(got[0, :len(span)], want), key
+        name, role, mode = key
+        ids = dict(((n, r, m), v) for n, pl in parts.items() for r, _, m, v in pl)[key]().reshape(-1)
+        zero_slot = flat[int(torch.nonzero(ids == 0)[0])]
+        assert torch.all(got[0, len(span):] == zero_slot), key
+    # a derived role (feat2emb_pair's 'pair') is not carried over
+    remaps[('item_emb', 'pair', 0)] = (fetched, torch.zeros(2, B, T, dtype=torch.int64))
+    assert ('item_emb', 'pair', 0) not in jagged_remaps(remaps, parts, row_map)
