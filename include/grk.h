@@ -318,9 +318,10 @@ typedef struct grk_attn_args {
                                       head_dim 64 / 128, no time bias; 8-byte
                                       aligned, ld in elements (= bytes)         */
   /* HSTU time bias (SURVEY §8 a9 rab_time; whole-sequence kernels, and the
-   * chunked kernels (head_dim <= 128) when the environment sets
-   * GRK_ATTN_CHUNKED_TIME -- opt-in until their parity has run on hardware;
-   * GRK_EUNSUPPORTED elsewhere): S[i,j] += rab_t[h, tb(ts[i] - ts[j])] with
+   * chunked and wide-head kernels when the environment sets
+   * GRK_ATTN_CHUNKED_TIME -- opt-in until their parity has run on hardware,
+   * GRK_EUNSUPPORTED otherwise; not with fp8 q/k/v):
+   * S[i,j] += rab_t[h, tb(ts[i] - ts[j])] with
    * tb(d) = min(2 l + h1, num_time_buckets - 1), l = floor(log2(|d| + 1)),
    * h1 = the bit below the leading one of |d| + 1 (0 when l = 0): half-octave
    * buckets of the time gap, integer-exact.  Gaps are taken of the times

@@ -243,6 +243,16 @@ __device__ __forceinline__ int time_bucket(int d, int nbt) {
   return min(2 * l + h1, nbt - 1);
 }
 
+// Time bias of the chunked / wide kernels (TB instantiations): a stamp relative
+// to the sequence's first valid key, clamped to +-(2^30 - 1), 0 past T -- the
+// whole-sequence kernels' stage_time convention, so every path buckets alike.
+__device__ __forceinline__ int rel_stamp(const AttnParams& p, int b, int T, int start, int j) {
+  const int64_t base = start < T ? p.ts[(int64_t)b * T + start] : 0;
+  const int64_t lim = (1 << 30) - 1;
+  const int64_t d = j < T ? p.ts[(int64_t)b * T + j] - base : 0;
+  return (int)(d > lim ? lim : (d < -lim ? -lim : d));
+}
+
 // Whole-sequence kernels (grk_attention_seq.hip): one workgroup per
 // (batch, head) with the sequence's K/V (or Q/dO) resident in LDS.
 // Returns true and launches when the shape fits; false = use the chunked path.

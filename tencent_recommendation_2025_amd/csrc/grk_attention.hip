@@ -26,15 +26,6 @@
 
 namespace grk {
 
-// HSTU time bias in the chunked kernels (TB instantiations): stamps relative to
-// the sequence's first valid key, clamped to +-(2^30 - 1), 0 past T -- the
-// whole-sequence kernels' stage_time convention, so both paths bucket alike.
-__device__ __forceinline__ int rel_stamp(const AttnParams& p, int b, int T, int start, int j) {
-  const int64_t base = start < T ? p.ts[(int64_t)b * T + start] : 0;
-  const int64_t lim = (1 << 30) - 1;
-  const int64_t d = j < T ? p.ts[(int64_t)b * T + j] - base : 0;
-  return (int)(d > lim ? lim : (d < -lim ? -lim : d));
-}
 // LDS of the TB instantiations: kChunk staged stamps, the head's rab_t row and
 // (dQ) the drab_t fixed-point bins.
 constexpr int kTimeLds = kChunk * 4 + kMaxTimeBuckets * 4 + kMaxTimeBuckets * 8;
@@ -534,9 +525,9 @@ static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
               "fit them", p.T, hd);
     return GRK_EUNSUPPORTED;
   }
-  // The chunked kernels' time bias (TB instantiations) is built but refused until
-  // its parity test has run on hardware (GRK_ATTN_CHUNKED_TIME=1 opts in).
-  if (p.nbt > 0 && which != 1 && (hd > 128 || !getenv("GRK_ATTN_CHUNKED_TIME"))) {
+  // The chunked and wide kernels' time bias (TB instantiations) is built but refused
+  // until its parity test has run on hardware (GRK_ATTN_CHUNKED_TIME=1 opts in).
+  if (p.nbt > 0 && which != 1 && !getenv("GRK_ATTN_CHUNKED_TIME")) {
     set_error("the HSTU time bias runs in the whole-sequence kernels only: T = %d x head_dim %d does not fit them",
               p.T, hd);
     return GRK_EUNSUPPORTED;

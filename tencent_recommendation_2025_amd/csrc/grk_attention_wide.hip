@@ -27,6 +27,8 @@ namespace {
 
 constexpr int kWRows = 32;   // queries (fwd, dQ) or keys (dK/dV) per workgroup
 constexpr int kWTail = 304;  // kvs[32] | s_start | lses[32] | dlts[32], then rab (+ drab bins)
+// TB (time bias) instantiations, after those: stamps[32] | rab_t[64] | drab_t bins[64] (dQ)
+constexpr int kWTime = kWRows * 4 + kMaxTimeBuckets * 4 + kMaxTimeBuckets * 8;
 
 template <int HD>
 struct Wide {
@@ -151,7 +153,8 @@ __device__ __forceinline__ uint8_t key_ok(const AttnParams& p, int b, int t) {
 }
 
 // ================================================================ forward ====
-template <int HD, int KIND>
+// TB: with the HSTU time bias rab_t[h, time_bucket(t_q - t_k)] (KIND 1).
+template <int HD, int KIND, bool TB = false>
 __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
   using W = Wide<HD>;
   constexpr int KSQ = W::KSQ, NDT = W::NDT, NW = W::NW, EPW = W::EPW;
@@ -165,6 +168,8 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
   uint8_t* kvs = reinterpret_cast<uint8_t*>(tail);
   int* s_start = reinterpret_cast<int*>(tail + 32);
   float* rabs = reinterpret_cast<float*>(tail + kWTail);
+  int* tsk = reinterpret_cast<int*>(rabs + (p.nb + 1) / 2 * 2);  // TB: the key tile's stamps
+  float* rtab = reinterpret_cast<float*>(tsk + kWRows);          // TB: rab_t[h, :]
 
   const int b = blockIdx.z, h = blockIdx.y, T = p.T;
   const int ws = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
@@ -173,6 +178,11 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
   const int start = seq_start(p.key_valid, b, T, s_start);
   if (KIND == 1)
     for (int j = threadIdx.x; j < p.nb; j += blockDim.x) rabs[j] = p.rab[h * p.nb + j];
+  int tq = 0;
+  if constexpr (TB) {
+    for (int j = threadIdx.x; j < p.nbt; j += blockDim.x) rtab[j] = p.rab_t[h * p.nbt + j];
+    tq = rel_stamp(p, b, T, start, myq);
+  }
   const int c0 = ws * W::DQ;  // this wave's columns within the head
 
   bf16x8 qf[KSQ];
@@ -204,7 +214,10 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
     __syncthreads();
     kt.put(Ks, p.act);
     vt.put(Vs, p.act);
-    if (threadIdx.x < 32) kvs[threadIdx.x] = kvb;
+    if (threadIdx.x < 32) {
+      kvs[threadIdx.x] = kvb;
+      if constexpr (TB) tsk[threadIdx.x] = rel_stamp(p, b, T, start, kb + threadIdx.x);
+    }
     lds_barrier();
     if (kb + 32 < kend) {  // in flight under this tile's work
       kt.fetch(p.k, p.ldk, b, T, h, kb + 32);
@@ -253,7 +266,8 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
       for (int e = 0; e < EPW; ++e) {
         const int kr = elem_row(ws * EPW + e, hh), key = kb + kr;
         const bool ok = qok && key <= myq && kvs[kr];
-        const float sp = se[e] * p.scale + rabs[ok ? min(myq - key, p.nb - 1) : 0];
+        float sp = se[e] * p.scale + rabs[ok ? min(myq - key, p.nb - 1) : 0];
+        if constexpr (TB) sp += rtab[time_bucket(tq - tsk[kr], p.nbt)];
         pd[e] = ok ? silu(sp) * p.inv_n : 0.f;
       }
     }
@@ -286,7 +300,7 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
 }
 
 // ================================================================ dQ =========
-template <int HD, int KIND>
+template <int HD, int KIND, bool TB = false>
 __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
   using W = Wide<HD>;
   constexpr int KSQ = W::KSQ, NDT = W::NDT, NW = W::NW, EPW = W::EPW;
@@ -301,6 +315,9 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
   int* s_start = reinterpret_cast<int*>(tail + 32);
   float* rabs = reinterpret_cast<float*>(tail + kWTail);
   unsigned long long* bins = reinterpret_cast<unsigned long long*>(rabs + (p.nb + 1) / 2 * 2);
+  int* tsk = reinterpret_cast<int*>(bins + p.nb);                                   // TB: key tile stamps
+  float* rtab = reinterpret_cast<float*>(tsk + kWRows);                             // TB: rab_t[h, :]
+  unsigned long long* tbins = reinterpret_cast<unsigned long long*>(rtab + kMaxTimeBuckets);  // TB: drab_t
 
   const int b = blockIdx.z, h = blockIdx.y, T = p.T;
   const int ws = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
@@ -312,6 +329,14 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
       rabs[j] = p.rab[h * p.nb + j];
       bins[j] = 0ull;
     }
+  int tq = 0;
+  if constexpr (TB) {
+    for (int j = threadIdx.x; j < p.nbt; j += blockDim.x) {
+      rtab[j] = p.rab_t[h * p.nbt + j];
+      tbins[j] = 0ull;
+    }
+    tq = rel_stamp(p, b, T, start, myq);
+  }
   const int bh = b * p.H + h;
   const int c0 = ws * W::DQ;
   const int64_t tok = (int64_t)b * T + (qok ? myq : 0);
@@ -349,7 +374,10 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
     __syncthreads();
     kt.put(Ks, p.act);
     vt.put(Vs, p.act);
-    if (threadIdx.x < 32) kvs[threadIdx.x] = kvb;
+    if (threadIdx.x < 32) {
+      kvs[threadIdx.x] = kvb;
+      if constexpr (TB) tsk[threadIdx.x] = rel_stamp(p, b, T, start, kb + threadIdx.x);
+    }
     lds_barrier();
     if (kb + 32 < kend) {  // in flight under this tile's work
       kt.fetch(p.k, p.ldk, b, T, h, kb + 32);
@@ -379,9 +407,16 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
         ds[e] = pv * (dpv - dlt);
       } else {
         const int bk = min(myq - key, p.nb - 1);
-        const float sp = se[e] * p.scale + rabs[ok ? bk : 0];
+        float sp = se[e] * p.scale + rabs[ok ? bk : 0];
+        int tbk = 0;
+        if constexpr (TB) {
+          tbk = time_bucket(tq - tsk[kr], p.nbt);
+          sp += rtab[tbk];
+        }
         ds[e] = ok ? de[e] * dsilu(sp) * p.inv_n : 0.f;
         if (ok && ds[e] != 0.f && p.drab) atomicAdd(&bins[bk], to_fix(ds[e]));
+        if constexpr (TB)
+          if (ok && ds[e] != 0.f && p.drab_t) atomicAdd(&tbins[tbk], to_fix(ds[e]));
       }
     }
     put_words<EPW>(gxd, ws, lane, ds);
@@ -400,15 +435,20 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
   }
   store_rows<HD, NDT>(shift(p.dq, p.out_f32, c0), p.lddq, p.out_f32, (int64_t)b * T + myq, h, hh, acc, p.scale, qok,
                       p.act ? (const void*)(p.q + c0) : nullptr, p.ldq);
-  if (KIND == 1 && p.drab) {
+  if (KIND == 1 && (p.drab || (TB && p.drab_t))) {
     __syncthreads();
-    for (int j = threadIdx.x; j < p.nb; j += blockDim.x)
-      if (bins[j] != 0ull) atomicAdd(&p.drab_fix[h * p.nb + j], bins[j]);
+    if (p.drab)
+      for (int j = threadIdx.x; j < p.nb; j += blockDim.x)
+        if (bins[j] != 0ull) atomicAdd(&p.drab_fix[h * p.nb + j], bins[j]);
+    if constexpr (TB)
+      if (p.drab_t)
+        for (int j = threadIdx.x; j < p.nbt; j += blockDim.x)
+          if (tbins[j] != 0ull) atomicAdd(&p.drab_t_fix[h * p.nbt + j], tbins[j]);
   }
 }
 
 // ============================================================== dK / dV =====
-template <int HD, int KIND, bool DF32>
+template <int HD, int KIND, bool DF32, bool TB = false>
 __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
   using W = Wide<HD>;
   constexpr int KSQ = W::KSQ, NDT = W::NDT, NW = W::NW, EPW = W::EPW;
@@ -424,6 +464,8 @@ __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
   float* lses = reinterpret_cast<float*>(tail + 48);
   float* dlts = lses + 32;
   float* rabs = reinterpret_cast<float*>(tail + kWTail);
+  int* tsq = reinterpret_cast<int*>(rabs + (p.nb + 1) / 2 * 2);  // TB: the query tile's stamps
+  float* rtab = reinterpret_cast<float*>(tsq + kWRows);          // TB: rab_t[h, :]
 
   const int b = blockIdx.z, h = blockIdx.y, T = p.T;
   const int ws = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
@@ -432,6 +474,11 @@ __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
   const bool kok = myk < T && myk >= start && (!p.key_valid || p.key_valid[(int64_t)b * T + myk]);
   if (KIND == 1)
     for (int j = threadIdx.x; j < p.nb; j += blockDim.x) rabs[j] = p.rab[h * p.nb + j];
+  int tk = 0;
+  if constexpr (TB) {
+    for (int j = threadIdx.x; j < p.nbt; j += blockDim.x) rtab[j] = p.rab_t[h * p.nbt + j];
+    tk = rel_stamp(p, b, T, start, myk);
+  }
   const int bh = b * p.H + h;
   const int c0 = ws * W::DQ;
   const int64_t tok = (int64_t)b * T + (myk < T ? myk : 0);
@@ -478,6 +525,7 @@ __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
     if (threadIdx.x < 32) {
       lses[threadIdx.x] = lv * kLog2e;
       dlts[threadIdx.x] = dl;
+      if constexpr (TB) tsq[threadIdx.x] = rel_stamp(p, b, T, start, qb + threadIdx.x);
     }
     lds_barrier();
     if (qb + 32 < T) fetch(qb + 32);  // in flight under this tile's work
@@ -509,7 +557,8 @@ __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
         }
         ds[e] = pv * (dpv - dlts[qr]);
       } else {
-        const float sp = se[e] * p.scale + rabs[ok ? min(q - myk, p.nb - 1) : 0];
+        float sp = se[e] * p.scale + rabs[ok ? min(q - myk, p.nb - 1) : 0];
+        if constexpr (TB) sp += rtab[time_bucket(tsq[qr] - tk, p.nbt)];
         pd[e] = ok ? silu(sp) * p.inv_n : 0.f;
         ds[e] = ok ? de[e] * dsilu(sp) * p.inv_n : 0.f;
       }
@@ -547,17 +596,25 @@ int wide_hd(const AttnParams& p, int which, hipStream_t s) {
   using W = Wide<HD>;
   const dim3 grid((p.T + kWRows - 1) / kWRows, p.H, p.B);
   const bool hstu = p.kind == GRK_ATTN_HSTU;
+  const bool tb = hstu && p.nbt > 0;
   const size_t rab = hstu ? (size_t)(p.nb + 1) / 2 * 2 * 4 : 0;
+  const size_t tlds = tb ? (size_t)kWTime : 0;
   if (which == 0) {
-    const size_t lds = 2 * W::IMG + W::RED + W::GX + W::NW * 64 * 4 + kWTail + rab;
-    launch_lds(hstu ? k_attn_fwd_wide<HD, 1> : k_attn_fwd_wide<HD, 0>, grid, W::NT, lds, s, p);
+    const size_t lds = 2 * W::IMG + W::RED + W::GX + W::NW * 64 * 4 + kWTail + rab + tlds;
+    launch_lds(tb ? k_attn_fwd_wide<HD, 1, true> : hstu ? k_attn_fwd_wide<HD, 1> : k_attn_fwd_wide<HD, 0>, grid, W::NT,
+               lds, s, p);
   } else if (which == 2) {
-    const size_t lds = 2 * W::IMG + 2 * W::RED + W::GX + kWTail + rab + (hstu ? (size_t)p.nb * 8 : 0);
-    launch_lds(hstu ? k_attn_dq_wide<HD, 1> : k_attn_dq_wide<HD, 0>, grid, W::NT, lds, s, p);
+    const size_t lds = 2 * W::IMG + 2 * W::RED + W::GX + kWTail + rab + (hstu ? (size_t)p.nb * 8 : 0) + tlds;
+    launch_lds(tb ? k_attn_dq_wide<HD, 1, true> : hstu ? k_attn_dq_wide<HD, 1> : k_attn_dq_wide<HD, 0>, grid, W::NT,
+               lds, s, p);
   } else {
-    const size_t lds = 2 * W::IMG + 2 * W::RED + 2 * W::GX + kWTail + rab;
-    if (p.dout_f32) launch_lds(hstu ? k_attn_dkdv_wide<HD, 1, true> : k_attn_dkdv_wide<HD, 0, true>, grid, W::NT, lds, s, p);
-    else launch_lds(hstu ? k_attn_dkdv_wide<HD, 1, false> : k_attn_dkdv_wide<HD, 0, false>, grid, W::NT, lds, s, p);
+    const size_t lds = 2 * W::IMG + 2 * W::RED + 2 * W::GX + kWTail + rab + tlds;
+    if (p.dout_f32)
+      launch_lds(tb ? k_attn_dkdv_wide<HD, 1, true, true> : hstu ? k_attn_dkdv_wide<HD, 1, true> : k_attn_dkdv_wide<HD, 0, true>,
+                 grid, W::NT, lds, s, p);
+    else
+      launch_lds(tb ? k_attn_dkdv_wide<HD, 1, false, true> : hstu ? k_attn_dkdv_wide<HD, 1, false> : k_attn_dkdv_wide<HD, 0, false>,
+                 grid, W::NT, lds, s, p);
   }
   GRK_LAUNCH_CHECK();
   return GRK_OK;

@@ -498,10 +498,11 @@ def test_time_bias_outside_whole_sequence_kernels_is_refused(K):
                     rab_t=torch.zeros(1, 8, device=DEV))
 
 
-# The chunked kernels (T beyond the whole-sequence kernels' LDS) carry the time
-# bias in their TB instantiations.  Built in round 3 without hardware: the
-# library refuses it unless GRK_ATTN_CHUNKED_TIME is set, and this parity test
-# is opt-in (GRK_CHUNKED_TIME_TESTS=1) until it has run on an MI355X.
+# The chunked kernels (T beyond the whole-sequence kernels' LDS) and the wide-head
+# kernels (head_dim 256 / 512) carry the time bias in their TB instantiations.
+# Built in round 3 without hardware: the library refuses it unless
+# GRK_ATTN_CHUNKED_TIME is set, and this parity test is opt-in
+# (GRK_CHUNKED_TIME_TESTS=1) until it has run on an MI355X.
 CHUNKED_TIME = pytest.mark.skipif(os.environ.get('GRK_CHUNKED_TIME_TESTS') != '1',
                                   reason='chunked-kernel time bias: opt-in until verified on hardware')
 
@@ -509,8 +510,10 @@ CHUNKED_TIME = pytest.mark.skipif(os.environ.get('GRK_CHUNKED_TIME_TESTS') != '1
 @CHUNKED_TIME
 @pytest.mark.parametrize('hd,H,T,lens,act,nbt', [(64, 2, 300, [300, 170, 20], 'silu', 48),
                                                  (128, 1, 1025, [1025, 600], None, 64),
-                                                 (32, 4, 260, [260, 3], None, 16)])
-def test_time_bias_chunked_kernels_match_oracle(K, monkeypatch, hd, H, T, lens, act, nbt):
+                                                 (32, 4, 260, [260, 3], None, 16),
+                                                 (256, 1, 150, [150, 90, 7], 'silu', 32),
+                                                 (512, 2, 70, [70, 33], None, 16)])
+def test_time_bias_chunked_and_wide_kernels_match_oracle(K, monkeypatch, hd, H, T, lens, act, nbt):
     monkeypatch.setenv('GRK_ATTN_CHUNKED_TIME', '1')
     res, want, _ = run(K, 1, B=len(lens), T=T, H=H, hd=hd, lens=lens, precise=True, nbt=nbt, act=act, seed=T)
     for key in ('out', 'dq', 'dk', 'dv', 'drab', 'drab_t'):
@@ -524,9 +527,9 @@ def test_time_bias_chunked_kernels_match_oracle(K, monkeypatch, hd, H, T, lens, 
             assert np.array_equal(res[key], again[key]), key
 
 
-def test_time_bias_wide_heads_refused(K, monkeypatch):
-    """head_dim 256 / 512 (the wide-head kernels) take no time bias, opted in or not."""
-    monkeypatch.setenv('GRK_ATTN_CHUNKED_TIME', '1')
+def test_time_bias_wide_heads_refused_unless_opted_in(K):
+    """head_dim 256 / 512 (the wide-head kernels): refused like the chunked kernels'
+    time bias until GRK_ATTN_CHUNKED_TIME opts in."""
     with pytest.raises(RuntimeError, match='whole-sequence'):
         run(K, 1, B=1, T=64, H=1, hd=256, lens=[50], precise=True, nbt=16, oracle=False)
 
