@@ -763,7 +763,19 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
 }
 
 // ============================================================== dK / dV =====
-template <int HD, int KIND, int PREC>
+// A/B build constants (scripts/build_variant.sh; both 0 in the product build):
+//   GRK_ATTN_FOLD_INVN  HSTU dK/dV: P and dS without the 1/n factor, folded into
+//                       the dK / dV store scales instead (one VALU per score);
+//   GRK_ATTN_TB_SPLIT   HSTU dK/dV without the time bias instantiated apart
+//                       (TBK = false: no per-score add of a zero bias).
+#ifndef GRK_ATTN_FOLD_INVN
+#define GRK_ATTN_FOLD_INVN 0
+#endif
+#ifndef GRK_ATTN_TB_SPLIT
+#define GRK_ATTN_TB_SPLIT 0
+#endif
+
+template <int HD, int KIND, int PREC, bool TBK = true>
 __global__ void __launch_bounds__(64 * kSeqWaves) __attribute__((amdgpu_waves_per_eu(PREC < 2 && HD <= 64 ? 2 : 1)))
 k_attn_dkdv_seq(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -836,6 +848,9 @@ k_attn_dkdv_seq(AttnParams p) {
   const float rdrop = 1.0f / (1.0f - p.dropout_p);
   const bool drop = KIND == 0 && p.dropout_p > 0.f;
   const unsigned long long seed = drop ? attn_seed(p) : 0ull;
+  constexpr bool fold = GRK_ATTN_FOLD_INVN && KIND == 1;
+  const float pscale = fold ? p.inv_n : 1.f;  // the 1/n factor of P and dS (HSTU)
+  const float sn = fold ? 1.f : p.inv_n;
 #ifdef GRK_DKDV_STAMPS
   int ntile_done = 0;
 #endif
@@ -948,7 +963,7 @@ k_attn_dkdv_seq(AttnParams p) {
           float tbv[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) tbv[e] = 0.f;
-          if (p.nbt) {
+          if (TBK && p.nbt) {
             const int tk = L.tss[myk < Tp ? myk : Tp - 1];
 #pragma unroll
             for (int e = 0; e < 8; ++e)
@@ -961,9 +976,9 @@ k_attn_dkdv_seq(AttnParams p) {
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
               const int i = 2 * j + u;
-              const float bias = rbase[(i & 3) + 8 * (i >> 2)] + tbv[2 * jj + u];
+              const float bias = TBK ? rbase[(i & 3) + 8 * (i >> 2)] + tbv[2 * jj + u] : rbase[(i & 3) + 8 * (i >> 2)];
               const float x = fmaf(s[i], p.scale, bias);
-              const float sg = sigmoid_fast(x), sgn = sg * p.inv_n;
+              const float sg = sigmoid_fast(x), sgn = fold ? sg : sg * sn;
               pd2[u] = x * sgn;                                   // SiLU(x) / n
               ds2[u] = dp[i] * fmaf(fmaf(-x, sg, x), sgn, sgn);   // dp * dSiLU(x) / n
             }
@@ -999,10 +1014,10 @@ k_attn_dkdv_seq(AttnParams p) {
       }
       const int64_t otok = rbase + myk;
       const bool kst = kin && myk >= lo;
-      store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, otok, h, hh, dk, kok ? p.scale : 0.f, kst, p.act ? p.k : nullptr,
-                          p.ldk, p.in_dt);
-      store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, kok ? 1.f : 0.f, kst, p.act ? p.v : nullptr, p.ldv,
-                          p.in_dt);
+      store_rows<HD, NDT>(p.dk, p.lddk, p.out_f32, otok, h, hh, dk, kok ? (fold ? p.scale * pscale : p.scale) : 0.f,
+                          kst, p.act ? p.k : nullptr, p.ldk, p.in_dt);
+      store_rows<HD, NDT>(p.dv, p.lddv, p.out_f32, otok, h, hh, dv, kok ? pscale : 0.f, kst, p.act ? p.v : nullptr,
+                          p.ldv, p.in_dt);
 #ifdef GRK_DKDV_STAMPS
       if (ntile_done < 3) GRK_RT(3 + ntile_done);
       ++ntile_done;
@@ -1035,6 +1050,13 @@ static bool seq_launch_hd(const AttnParams& p, int which, hipStream_t s) {
   } while (0)
   if (which == 0) GRK_SEQ(k_attn_fwd_seq);
   else if (which == 2) GRK_SEQ(k_attn_dq_seq);
+#if GRK_ATTN_TB_SPLIT
+  else if (p.kind != GRK_ATTN_SOFTMAX && p.nbt == 0) {
+    if (p.precise == 2) launch_lds(k_attn_dkdv_seq<HD, 1, 2, false>, grid, threads, lds, s, p);
+    else if (p.precise) launch_lds(k_attn_dkdv_seq<HD, 1, 1, false>, grid, threads, lds, s, p);
+    else launch_lds(k_attn_dkdv_seq<HD, 1, 0, false>, grid, threads, lds, s, p);
+  }
+#endif
   else GRK_SEQ(k_attn_dkdv_seq);
 #undef GRK_SEQ
   return true;
