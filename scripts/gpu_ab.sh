@@ -14,9 +14,11 @@ for i in $(seq 1 $N); do
     python - "$v" "gpurun_out/ab_$v$i.json" >> gpurun_out/ab.txt <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read())
-rl = {r['kernel'][:40]: r.get('avg_launch_us') for r in [d['roofline']] + d['rooflines']}
-g = [v for k, v in rl.items() if 'k_gather' in k]
-print(sys.argv[1], d['value'], d['ms_per_step'], 'gathers(us)', g)
+ents = [d['roofline']] + d['rooflines']
+def us(*needles):
+    return [r.get('avg_launch_us') for r in ents if all(n in r.get('kernel', '') for n in needles)]
+print(sys.argv[1], d['value'], d['ms_per_step'], 'gathers(us)', us('k_gather'), 'dkdv(us)', us('dkdv'),
+      'emb_bwd(us)', us('grk_embedding_backward'))
 PY
   done
 done
