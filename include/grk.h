@@ -294,9 +294,11 @@ typedef struct grk_attn_args {
   int32_t precise;                 /* 1: P / dS fed to MFMA as bf16 hi+lo pairs;
                                       2 (fp32 fidelity): Q/K/V and dO as well, each
                                       product as hi*hi + hi*lo + lo*hi; q/k/v then
-                                      have dtype qkv_dtype (whole-sequence kernels
-                                      only: GRK_EUNSUPPORTED where T x hd does not
-                                      fit LDS)                                   */
+                                      have dtype qkv_dtype (whole-sequence kernels,
+                                      and head_dim 256 in the wide-head kernels
+                                      when GRK_ATTN_WIDE_FIDELITY is set -- opt-in
+                                      until hardware-tested; GRK_EUNSUPPORTED
+                                      elsewhere)                                 */
   uint64_t seed;                   /* dropout stream                              */
   int32_t out_dtype;               /* GRK_F32 / GRK_BF16 for out, dq, dk, dv      */
   int32_t act;                     /* GRK_ACT_*: activation applied to q/k/v      */
@@ -349,7 +351,8 @@ typedef struct grk_attn_args {
 } grk_attn_args;
 
 /* 1 when grk_attention_* with precise == 2 (fp32 fidelity) runs for this
- * sequence length and head_dim (the whole-sequence kernels' LDS), else 0. */
+ * sequence length and head_dim (the whole-sequence kernels' LDS; head_dim 256
+ * at any length with GRK_ATTN_WIDE_FIDELITY set), else 0. */
 int grk_attention_fidelity_supported(int seq_len, int head_dim);
 
 /* ranges int32 [batch, 3]: ranges[b][0] = first j with key_valid[b, j] (T for

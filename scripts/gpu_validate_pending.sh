@@ -23,6 +23,8 @@ PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 GRK_CHUNKED_TIME_TESTS=1 timeout -k 10 400 $PYT tests/test_gpu_attention.py -k "time_bias" > $O/time_bias.log 2>&1
 GRK_SHARDED_JAGGED_TESTS=1 timeout -k 10 300 $PYT tests/test_gpu_sharding.py -k "sharded_jagged" > $O/sharded_jagged.log 2>&1
 GRK_C5_MODEL_TESTS=1 timeout -k 10 400 $PYT tests/test_gpu_fp8.py > $O/c5.log 2>&1
+GRK_WIDE_FIDELITY_TESTS=1 timeout -k 10 400 $PYT tests/test_gpu_attention.py tests/test_gpu_model.py \
+  -k "wide_fidelity or 256_fidelity" > $O/wide_fidelity.log 2>&1
 
 # 2) the variants' parity (the tests restate the chunk order from the library)
 for v in ch64 ch128 pipe32; do

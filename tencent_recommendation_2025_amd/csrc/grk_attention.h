@@ -261,5 +261,7 @@ bool attn_seq_launch(const AttnParams& p, int hd, int which, hipStream_t s);
 // Wide-head kernels (grk_attention_wide.hip): head_dim 256 / 512, the head's
 // columns split over a workgroup's waves (which: 0 forward, 2 dQ, 3 dK/dV).
 int attn_wide_launch(const AttnParams& p, int hd, int which, hipStream_t s);
+// Whether the wide-head kernels take precise = 2 at this head_dim (256, opt-in).
+bool wide_fidelity_enabled(int hd);
 
 }  // namespace grk
