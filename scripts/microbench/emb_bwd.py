@@ -1,7 +1,9 @@
 """Microbench of grk_embedding_backward (run under rocprofv3 --kernel-trace --stats
 for the per-kernel split): D=512 bf16 gradients, C2-sized occurrence counts,
 (a) uniform ids over 1M rows (item-table shape), (b) a feature-table mix with
-cardinality-10 hot rows (thousands of occurrences each, k_seg_hot).
+cardinality-10 hot rows (thousands of occurrences each, k_seg_hot), (c) the
+projected-feature-row call of the bench step (its headline roofline entry).
+GRK_LIB=abtest/libgrk_<variant>.so times a build variant (scripts/build_variant.sh).
 
     python scripts/microbench/emb_bwd.py
 """
@@ -45,6 +47,28 @@ def main():
     us = time_call(lambda: K.embedding_backward(srcs, offs, D, dense=False, sparse=True))
     res = K.embedding_backward(srcs, offs, D, dense=False, sparse=True)
     print(f'feature tables {cards}, {len(cards) * N} occurrences ({int(res.count.item())} unique): {us:.1f} us')
+    # (c) the headline call: the seq side's projected feature rows P (bench.py's first
+    # roofline entry) -- 14,336 jagged rows, 14 item features (cardinalities 10 / 100 /
+    # 1k / 10k cycled) as one bag of 14 and 20 user slots (4 sparse + 4 arrays x 4) as a
+    # bag of 20 that only the user token of each sequence fills, stacked P rows,
+    # GRK_BWD_CHUNKED with a dense fp32 output
+    n, B = 14336, 128
+    card_i = [(10, 100, 1000, 10000)[f % 4] for f in range(14)]
+    card_u = [1000] * 20
+    offs, col = [], 1
+    for c in card_i + card_u:
+        offs.append(col)
+        col += c
+    rows = col
+    gi = torch.randn(n, 2 * D, device=dev, generator=g).bfloat16()
+    ii = torch.stack([offs[f] + torch.randint(0, card_i[f], (n,), device=dev, generator=g) for f in range(14)], 1)
+    iu = torch.zeros(n, 20, dtype=torch.int64, device=dev)
+    users = torch.arange(0, n, n // B, device=dev)[:B]
+    iu[users] = torch.stack([offs[14 + f] + torch.randint(0, 1000, (B,), device=dev, generator=g)
+                             for f in range(20)], 1)
+    srcs = [K.GradSource(ii, gi, 0, bag=14), K.GradSource(iu, gi, D, bag=20)]
+    us = time_call(lambda: K.embedding_backward(srcs, rows, D, dense=True, chunked=True))
+    print(f'projected P rows ({rows} rows, {34 * n} occurrences, chunk {K.chunked_size()}): {us:.1f} us')
 
 
 if __name__ == '__main__':
