@@ -37,7 +37,14 @@ for v in tbsplit foldtb; do
     > $O/attn_$v.log 2>&1
 done
 
-# 3) bench A/B, round-robin (scripts/gpu_ab.sh writes gpurun_out/ab.txt)
+# 3) the headline call standalone under each embedding variant
+for lib in tencent_recommendation_2025_amd/libgrk.so abtest/libgrk_ch64.so abtest/libgrk_ch128.so abtest/libgrk_pipe32.so; do
+  [ -f $lib ] || continue
+  echo "== $lib" >> $O/emb_bwd_micro.txt
+  GRK_LIB=$PWD/$lib timeout -k 10 120 python -u scripts/microbench/emb_bwd.py >> $O/emb_bwd_micro.txt 2>&1
+done
+
+# 4) bench A/B, round-robin (scripts/gpu_ab.sh writes gpurun_out/ab.txt)
 LIBS="tencent_recommendation_2025_amd/libgrk.so"
 for v in ch64 ch128 pipe32 tbsplit foldtb; do
   [ -f abtest/libgrk_$v.so ] && LIBS="$LIBS abtest/libgrk_$v.so"
