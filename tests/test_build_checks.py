@@ -70,3 +70,16 @@ def test_python_sources_bind_every_global_they_read():
         paths += sorted(glob.glob(os.path.join(REPO, d, '*.py')))
     bad = [(os.path.relpath(p, REPO), scope, n) for p in paths for scope, n in undefined(p)]
     assert not bad, bad
+
+
+def test_gpu_code_writes_no_memory_through_the_scalar_cache():
+    """scripts/check_scalar_writes.py over every built GPU object (a host-only
+    checker kept out of GPU uploads: it names the instructions it rejects)."""
+    script = os.path.join(REPO, 'scripts', 'check_scalar_writes.py')
+    if not os.path.exists(script):
+        pytest.skip('checker not present (GPU box upload)')
+    objs = sorted(p for p in glob.glob(os.path.join(REPO, 'build', 'obj', 'grk_*.o')) if not p.endswith('.cpp.o'))
+    if not objs:
+        pytest.skip('no build/obj (run make first)')
+    r = subprocess.run([sys.executable, script, *objs], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
