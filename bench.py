@@ -68,6 +68,9 @@ def parse():
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='gloo: rehearse N ranks on fewer GPUs (collectives staged via host)')
     ap.add_argument('--sharded', type=int, default=None, help='force the row-sharded optimizer (default: N > 1)')
+    ap.add_argument('--merge-proj', type=int, default=0,
+                    help='1: the projected feature tables\' row gradients of the seq-side and pair lookups in one '
+                         'grk_embedding_backward call (functional.DenseMerge; opt-in until verified on hardware)')
     ap.add_argument('--sharded-jagged', type=int, default=0,
                     help='1: the row-sharded trainer on jagged rows too (train.jagged_remaps; opt-in until verified '
                          'on hardware -- the sharded step runs the padded layout by default)')
@@ -634,6 +637,7 @@ def main():
                         hstu_fp8=bool(a.fp8))
     shard_tables = sharded and (a.shard_tables if a.shard_tables is not None else a.items >= 10_000_000)
     margs.shard_tables = bool(shard_tables)
+    margs.merge_proj_backward = bool(a.merge_proj)
     torch.manual_seed(0)
     model = BaselineModel(a.users, a.items, stats, types, margs).to(dev)
     model.train()
@@ -734,7 +738,8 @@ def main():
                                    f'{a.users} users, loss={a.loss}, table AdamW={a.table_mode}, '
                                    f'dropout={a.dropout}'
                                    + (f', rab_time buckets={a.time_buckets}' if a.time_buckets else '')
-                                   + (', fp8 (e4m3) q/k/v attention' if a.fp8 else ''),
+                                   + (', fp8 (e4m3) q/k/v attention' if a.fp8 else '')
+                                   + (', merged projected-row backward' if a.merge_proj else ''),
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch, 'seq_len': a.maxlen + 1,
                        'parallelism': f'dp{world}' + ('+rowshard' if sharded else '') + ('(shard-built tables)' if shard_tables else ''),
                        'step_launch': 'hip-graph replay' if trainer.graph else 'eager',

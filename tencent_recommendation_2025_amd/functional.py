@@ -28,11 +28,61 @@ class TableRef:
     row-sparse gradient collected by the group's sink).  ``chunked``: the
     weight is an intermediate whose row gradients may be summed in the
     chunked fixed order (K.embedding_backward); honoured when every
-    drop-in table of a fused lookup allows it."""
-    __slots__ = ('weight', 'group', 'row_offset', 'chunked')
+    drop-in table of a fused lookup allows it.  ``merge``: a DenseMerge
+    shared by the fused lookups of one forward that read this weight."""
+    __slots__ = ('weight', 'group', 'row_offset', 'chunked', 'merge')
 
-    def __init__(self, weight, group=None, row_offset=0, chunked=False):
+    def __init__(self, weight, group=None, row_offset=0, chunked=False, merge=None):
         self.weight, self.group, self.row_offset, self.chunked = weight, group, row_offset, chunked
+        self.merge = merge
+
+
+class DenseMerge:
+    """Dense row gradients of intermediate tables read by several fused lookups
+    of one forward -- the projected feature tables P, read by the seq-side
+    feat2emb and by feat2emb_pair: instead of one grk_embedding_backward per
+    lookup (each a sort, a zero-filled dense output and a cast) plus autograd's
+    add of the two results, every lookup's backward deposits its gradient
+    sources here and the LAST one to run reduces them all in one chunked call.
+    Every lookup takes all the merged weights as inputs (so whichever runs last
+    can return their gradients); the earlier ones return None for them.  The
+    sources are added in deposit order (the backward's fixed call order):
+    deterministic.  Opt-in (model args.merge_proj_backward)."""
+
+    def __init__(self):
+        self.weights = []
+        self.pending = 0
+        self.sources = []
+
+    def add(self, w):
+        if all(x is not w for x in self.weights):
+            self.weights.append(w)
+
+    def deposit(self, live):
+        for s, g, c in live:
+            if s.mode != L.IDX_PLAIN:
+                raise RuntimeError('merged dense lookups must be plain (no token-type mask)')
+            self.sources.append((s, g, c))
+
+    def resolve(self):
+        """{id(weight): gradient or None} after one consumer's backward."""
+        self.pending -= 1
+        if self.pending > 0:
+            return {id(w): None for w in self.weights}
+        offs, total = {}, 0
+        for w in self.weights:
+            offs[id(w)] = total
+            total += w.shape[0]
+        out = {id(w): None for w in self.weights}
+        if self.sources:
+            D = self.weights[0].shape[1]
+            src = [K.GradSource(sp.idx, g, c, sp.mode, sp.bag, offs[id(sp.ref.weight)], sp.ref.weight.shape[0])
+                   for sp, g, c in self.sources]
+            res = K.embedding_backward(src, total, D, padding_idx=0, dense=True,
+                                       chunked=all(sp.ref.chunked for sp, _, _ in self.sources))
+            out = {id(w): res.dense[offs[id(w)]:offs[id(w)] + w.shape[0]].to(w.dtype) for w in self.weights}
+        self.sources = []
+        return out
 
 
 class LookupSpec:
@@ -63,6 +113,7 @@ class _FeatureLookupFn(torch.autograd.Function):
         ctx.specs, ctx.token_type, ctx.seq_len, ctx.splits = specs, token_type, seq_len, splits
         ctx.n_weights = len(weights)
         ctx.weight_ids = [id(w) for w in weights]
+        ctx.merges = _merges_of(specs)
         return tuple(out[:, a:b] for a, b in splits)
 
     @staticmethod
@@ -87,7 +138,9 @@ class _FeatureLookupFn(torch.autograd.Function):
         grads = []
         # drop-in: one deterministic reduction over every distinct table of the call
         dense = [(s, g, c) for s, g, c in live if s.ref.group is None]
-        if ctx.n_weights:
+        if ctx.n_weights and ctx.merges:
+            grads = _merged_grads(ctx, dense)
+        elif ctx.n_weights:
             tables, offs, total = {}, {}, 0
             for s in specs:
                 w = s.ref.weight
@@ -111,6 +164,44 @@ class _FeatureLookupFn(torch.autograd.Function):
                                                  s.ref.weight.shape[0]), ctx.token_type, ctx.seq_len)
         # extras are dense inputs (features, constants): no gradient is propagated to them
         return (None, None, None, None, None, None, None, *grads)
+
+
+def _merges_of(specs):
+    out = []
+    for s in specs:
+        m = s.ref.merge
+        if s.ref.group is None and m is not None and all(x is not m for x in out):
+            out.append(m)
+    return out
+
+
+def _merged_grads(ctx, dense):
+    """Gradients of the call's drop-in weights when some are DenseMerge members:
+    the members' sources go to their merge (resolved by its last consumer), the
+    other drop-in tables are reduced here as usual."""
+    D = ctx.specs[0].ref.weight.shape[1]
+    by_id = {}
+    for m in ctx.merges:
+        m.deposit([(s, g, c) for s, g, c in dense if s.ref.merge is m])
+    plain = [(s, g, c) for s, g, c in dense if s.ref.merge is None]
+    tables, offs, total = {}, {}, 0
+    for s in ctx.specs:
+        w = s.ref.weight
+        if s.ref.group is None and s.ref.merge is None and id(w) not in tables:
+            tables[id(w)] = w
+            offs[id(w)] = total
+            total += w.shape[0]
+    if plain:
+        src = [K.GradSource(s.idx, g, c, s.mode, s.bag, offs[id(s.ref.weight)], s.ref.weight.shape[0])
+               for s, g, c in plain]
+        res = K.embedding_backward(src, total, D, padding_idx=0, token_type=ctx.token_type, seq_len=ctx.seq_len,
+                                   dense=True, chunked=all(s.ref.chunked for s, _, _ in plain))
+        by_id.update({k: res.dense[offs[k]:offs[k] + w.shape[0]].to(w.dtype) for k, w in tables.items()})
+    else:
+        by_id.update({k: None for k in tables})
+    for m in ctx.merges:
+        by_id.update(m.resolve())
+    return [by_id.get(wid) for wid in ctx.weight_ids]
 
 
 def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extras=(), splits=None):
@@ -159,6 +250,13 @@ def _lookup_groups(specs, token_type, seq_len, num_tokens, out_ld, extras, split
         if s.ref.group is None and id(s.ref.weight) not in seen and s.ref.weight.requires_grad:
             seen.add(id(s.ref.weight))
             weights.append(s.ref.weight)
+    merges = _merges_of(specs) if torch.is_grad_enabled() else []
+    for m in merges:   # every merged weight is an input of every consumer (the last one returns the gradients)
+        m.pending += 1
+        for w in m.weights:
+            if id(w) not in seen and w.requires_grad:
+                seen.add(id(w))
+                weights.append(w)
     return _FeatureLookupFn.apply(specs, token_type, seq_len, num_tokens, out_ld, extras, splits, *weights)
 
 

@@ -226,6 +226,9 @@ class BaselineModel(torch.nn.Module):
         # dnn operand instead of projected (see _projection): projecting costs
         # ~6 rows d^2 FLOP per forward + backward, a direct block ~6 tokens d^2
         self.proj_max_rows = int(getattr(args, 'proj_max_rows', 100_000))
+        # fused path: the projected tables' row gradients of the seq-side and pair
+        # lookups reduced in one call (functional.DenseMerge); opt-in until run on hardware
+        self.merge_proj = bool(getattr(args, 'merge_proj_backward', False))
         if getattr(args, 'shard_tables', False):
             # row-sharded item / user tables (BASELINE config 3, 50M rows): the full
             # tables are never built on any rank -- ShardedFusedAdamW creates each
@@ -408,6 +411,17 @@ class BaselineModel(torch.nn.Module):
             self._proj_cache[key] = res
         return res
 
+    def _proj_merge(self, P):
+        """The forward's DenseMerge of the projected tables (args.merge_proj_backward, fused
+        lookups only: table groups present), with P registered; None otherwise."""
+        if not self.merge_proj or self._fwd_id is None or self._table_refs is None or not P.requires_grad:
+            return None
+        m = self._proj_cache.get(('merge', self._fwd_id))
+        if m is None:
+            m = self._proj_cache[('merge', self._fwd_id)] = G.DenseMerge()
+        m.add(P)
+        return m
+
     def _const_index(self, values, device):
         """Cached device int64 tensor (built once: no host->device copy per forward)."""
         t = self._proj_off_cache.get(('idx', values))
@@ -492,7 +506,8 @@ class BaselineModel(torch.nn.Module):
             idx = self._proj_index(feats, names, offs, N)
             # P = E W is an intermediate: its row sums may use the chunked order (the
             # reference accumulates dE = sum dY W, in no order P's sums could match)
-            specs.append(G.LookupSpec(G.TableRef(P, chunked=True), idx, col, L.IDX_PLAIN, idx.shape[1]))
+            specs.append(G.LookupSpec(G.TableRef(P, chunked=True, merge=self._proj_merge(P)), idx, col, L.IDX_PLAIN,
+                                      idx.shape[1]))
             splits.append((col, col + d))
             col += d
 
