@@ -1,0 +1,73 @@
+"""Host-side helpers of the fused step (CPU, no kernel launched).
+
+* kernels.adamw_hparams -- the per-step constants every table AdamW kernel
+  consumes (grk_optim.hip adam1: p *= 1 - lr wd; m += (1 - b1)(g - m);
+  v = b2 v + (1 - b2) g^2; p -= step_size m / (sqrt(v) / bias_corr2_sqrt + eps)):
+  restated here in fp32 numpy with those constants over several steps, it
+  tracks torch.optim.AdamW (model/BaseLine/main.py:131,189, betas (0.9, 0.98)).
+* jagged.span_rows / capacity_for -- the host metadata that picks the jagged
+  step's capacity (and with it the GEMM plans and the captured graph)."""
+import numpy as np
+import pytest
+import torch
+
+from tencent_recommendation_2025_amd import jagged as J
+from tencent_recommendation_2025_amd import kernels as K
+
+
+def adam1(p, m, v, g, hp):
+    """grk_optim.hip adam1 in fp32 (IEEE sqrt / division where the kernel uses the
+    1-ulp hardware forms)."""
+    f = np.float32
+    pe = p * f(1.0 - f(hp.lr) * f(hp.weight_decay))
+    me = m + f(1.0 - f(hp.beta1)) * (g - m)
+    ve = v * f(hp.beta2) + f(1.0 - f(hp.beta2)) * g * g
+    denom = np.sqrt(ve) * f(1.0 / f(hp.bias_corr2_sqrt)) + f(hp.eps)
+    return pe - f(hp.step_size) * (me / denom), me, ve
+
+
+@pytest.mark.parametrize('wd', [0.0, 0.01])
+def test_adamw_hparams_track_torch_adamw(wd):
+    rng = np.random.default_rng(0)
+    p0 = rng.standard_normal(4096).astype(np.float32)
+    grads = [rng.standard_normal(4096).astype(np.float32) * s for s in (1.0, 1e-3, 0.0, 3.0, 1e-6)]
+    lr, b1, b2, eps = 1e-3, 0.9, 0.98, 1e-8
+    tp = torch.nn.Parameter(torch.from_numpy(p0.copy()))
+    opt = torch.optim.AdamW([tp], lr=lr, betas=(b1, b2), eps=eps, weight_decay=wd)
+    p, m, v = p0.copy(), np.zeros_like(p0), np.zeros_like(p0)
+    for t, g in enumerate(grads, start=1):
+        hp = K.adamw_hparams(lr, b1, b2, eps, wd, t)
+        assert hp.step_size == pytest.approx(lr / (1 - b1 ** t), rel=1e-6)
+        assert hp.bias_corr2_sqrt == pytest.approx((1 - b2 ** t) ** 0.5, rel=1e-6)
+        p, m, v = adam1(p, m, v, g, hp)
+        tp.grad = torch.from_numpy(g.copy())
+        opt.step()
+        st = opt.state[tp]
+        # torch forms m with lerp (its own rounding of m + w (g - m)): ulps of max |m|
+        np.testing.assert_allclose(m, st['exp_avg'].numpy(), rtol=1e-6, atol=1e-6 * np.abs(m).max())
+        np.testing.assert_allclose(v, st['exp_avg_sq'].numpy(), rtol=1e-5, atol=1e-6 * np.abs(v).max())
+        # the update term is ~lr: a few fp32 ulp of it on top of p's own rounding
+        np.testing.assert_allclose(p, tp.detach().numpy(), rtol=0, atol=4e-8 + 2e-7 * np.abs(p).max())
+
+
+def test_span_rows_and_capacity():
+    T = 9
+    tt = torch.zeros(4, T, dtype=torch.int64)
+    starts = [0, 4, 9, 8]                        # full, partial, empty, one token
+    for b, s0 in enumerate(starts):
+        tt[b, s0:] = 1
+    assert J.span_rows(tt) == sum(T - s0 for s0 in starts)
+    tt[1, 6] = 0                                 # a hole inside a span still counts (span = [first, T))
+    assert J.span_rows(tt) == sum(T - s0 for s0 in starts)
+    assert J.capacity_for(0) == 1024 and J.capacity_for(1) == 1024 and J.capacity_for(1024) == 1024
+    assert J.capacity_for(1025) == 2048 and J.capacity_for(13670) == 14336
+    assert J.capacity_for(5000, 1024, limit=4096) == 4096
+    assert J.capacity_for(100, 128) == 128
+
+
+def test_device_clock_advances_on_its_device():
+    clk = K.DeviceClock(16, torch.device('cpu'))
+    assert clk.ring.shape[0] == 16 and int(clk.t.item()) == 0
+    clk.advance()
+    clk.advance()
+    assert int(clk.t.item()) == 2
