@@ -365,7 +365,8 @@ def backward_rooflines(trace, reps):
             if key not in seen:
                 seen.add(key)
                 rows_read += _source_rows_read(s, call['token_type'])
-        written = call['num_rows'] * D * 4 if call['dense'] else uniq * (D * 4 + 8)
+        dsz = 2 if call.get('dense_dtype') == torch.bfloat16 else 4
+        written = call['num_rows'] * D * dsz if call['dense'] else uniq * (D * 4 + 8)
         alg = rows_read * D * es + occ * isz + written
         ms = _time(run, reps)
         gbps = alg / (ms * 1e-3) / 1e9

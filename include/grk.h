@@ -136,7 +136,7 @@ int grk_sort_pairs(const uint32_t* keys_in, const uint64_t* vals_in, uint32_t* k
  * (deterministic).  Rows == padding_idx are skipped (padding_idx < 0: none).
  *
  * Outputs (any may be NULL):
- *   dense_out  [num_rows, dim] fp32: zero-filled then written (drop-in mode)
+ *   dense_out  [num_rows, dim] fp32 (bf16 with GRK_BWD_DENSE_BF16): zero-filled then written
  *   uniq_ids   int64 [num_occurrences]: sorted unique row ids
  *   uniq_rows  fp32  [num_occurrences, dim]: their gradient rows
  *   uniq_count int32 [1]: number of unique rows
@@ -154,11 +154,14 @@ int grk_sort_pairs(const uint32_t* keys_in, const uint64_t* vals_in, uint32_t* k
  *   reference counterpart (the fused trainer's projected feature rows);
  *   honoured when dim is 64 x (8 bf16 / 4 or 8 fp32 elements), otherwise the
  *   call runs ordered. */
-enum { GRK_BWD_ORDERED = 0, GRK_BWD_CHUNKED = 1 };
+/* | GRK_BWD_DENSE_BF16 (with GRK_BWD_CHUNKED, bf16 gradients of 512 columns):
+ *   dense_out is bf16 [num_rows, dim], each row rounded once from its fp32 sum
+ *   (the intermediate tables are bf16: no fp32 buffer, no cast afterwards). */
+enum { GRK_BWD_ORDERED = 0, GRK_BWD_CHUNKED = 1, GRK_BWD_DENSE_BF16 = 2 };
 int grk_embedding_chunked_size(void);
 int grk_embedding_backward(const grk_lookup* lookups, int num_lookups, int dim, int grad_dtype, int itype,
                            const int32_t* token_type, int32_t seq_len, int64_t num_rows, int64_t padding_idx,
-                           float* dense_out, int64_t* uniq_ids, float* uniq_rows, int32_t* uniq_count,
+                           void* dense_out, int64_t* uniq_ids, float* uniq_rows, int32_t* uniq_count,
                            int32_t* row_slot, int flags, void* workspace, size_t workspace_bytes,
                            int32_t* err_flag, void* stream);
 

@@ -25,7 +25,8 @@ GRK_SHARDED_JAGGED_TESTS=1 timeout -k 10 300 $PYT tests/test_gpu_sharding.py -k 
 GRK_C5_MODEL_TESTS=1 timeout -k 10 400 $PYT tests/test_gpu_fp8.py > $O/c5.log 2>&1
 GRK_WIDE_FIDELITY_TESTS=1 timeout -k 10 400 $PYT tests/test_gpu_attention.py tests/test_gpu_model.py \
   -k "wide_fidelity or 256_fidelity" > $O/wide_fidelity.log 2>&1
-GRK_MERGE_PROJ_TESTS=1 timeout -k 10 300 $PYT tests/test_gpu_jagged.py -k merged_projection > $O/merge_proj.log 2>&1
+GRK_MERGE_PROJ_TESTS=1 timeout -k 10 300 $PYT tests/test_gpu_embedding.py tests/test_gpu_jagged.py \
+  -k "bf16_dense or merged_projection" > $O/merge_proj.log 2>&1
 timeout -k 10 200 python -u bench.py --steps 30 --warmup 10 --cpu-baseline 0 --roofline-reps 5 --merge-proj 1 \
   > $O/bench_merge_proj.json 2> $O/bench_merge_proj.err
 

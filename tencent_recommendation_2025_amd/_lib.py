@@ -26,7 +26,7 @@ GRK_F32, GRK_BF16, GRK_F16 = 0, 1, 2
 GRK_F32_BF16 = 3  # pair logits: fp32 h, bf16 item embeddings
 GRK_FP8_E4M3 = 4  # attention q/k/v: OCP fp8 e4m3
 GRK_I32, GRK_I64 = 0, 1
-BWD_ORDERED, BWD_CHUNKED = 0, 1  # grk_embedding_backward flags
+BWD_ORDERED, BWD_CHUNKED, BWD_DENSE_BF16 = 0, 1, 2  # grk_embedding_backward flags (bf16 dense: | with CHUNKED)
 IDX_PLAIN, IDX_ITEM_MASK, IDX_USER_MASK, IDX_POSITION = 0, 1, 2, 3
 ADAM_DENSE, ADAM_LAZY = 0, 1
 MAX_FEATURES = 48

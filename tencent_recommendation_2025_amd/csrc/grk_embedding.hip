@@ -266,6 +266,27 @@ __device__ __forceinline__ void store_final(const A& acc, unsigned key, int64_t 
   if (row_slot && c == 0) row_slot[key] = (int32_t)u;
 }
 
+// GRK_BWD_DENSE_BF16: the dense row rounded to bf16 once (the intermediate
+// tables' own dtype: no fp32 buffer and no cast kernel after the call).
+template <typename A>
+__device__ __forceinline__ void store_final(const A& acc, unsigned key, int64_t u, int dim, int c,
+                                            bf16_t* dense_out, float* uniq_rows, int32_t* row_slot) {
+  constexpr int VEC = A::VEC;
+#pragma unroll
+  for (int e = 0; e < VEC; e += 4) {
+    if (dense_out) {
+      uint2 t;
+      t.x = (unsigned)f32_to_bf16(acc.v[e]) | ((unsigned)f32_to_bf16(acc.v[e + 1]) << 16);
+      t.y = (unsigned)f32_to_bf16(acc.v[e + 2]) | ((unsigned)f32_to_bf16(acc.v[e + 3]) << 16);
+      *reinterpret_cast<uint2*>(dense_out + (int64_t)key * dim + c + e) = t;
+    }
+    if (uniq_rows)
+      *reinterpret_cast<float4*>(uniq_rows + u * dim + c + e) =
+          make_float4(acc.v[e], acc.v[e + 1], acc.v[e + 2], acc.v[e + 3]);
+  }
+  if (row_slot && c == 0) row_slot[key] = (int32_t)u;
+}
+
 // Sequential in-order sum of the sorted occurrences [s, e) with kRedPipe rows in flight.
 template <typename G>
 __device__ __forceinline__ void seq_sum(RowVec<G>& acc, const unsigned long long* __restrict__ gptr, int s, int e,
@@ -419,12 +440,12 @@ struct WaveAcc {
   }
 };
 
-template <typename G, int LW, int CH = kRedChunk>
+template <typename G, int LW, int CH = kRedChunk, typename OT = float>
 __device__ __forceinline__ void seg_chunks_wave_body(int64_t chunk, int lane, const unsigned* __restrict__ keys,
                                                      const unsigned long long* __restrict__ gptr,
                                                      const int* __restrict__ pos, const int* __restrict__ seg_start,
                                                      const int* __restrict__ seg_end, int64_t n, unsigned sentinel,
-                                                     int dim, float* __restrict__ dense_out,
+                                                     int dim, OT* __restrict__ dense_out,
                                                      float* __restrict__ uniq_rows, int32_t* __restrict__ row_slot,
                                                      float* __restrict__ partials = nullptr) {
   constexpr int VEC = LW;
@@ -595,31 +616,32 @@ __global__ void __launch_bounds__(256) k_seg_combine_edges(const unsigned* __res
 constexpr int kPartialChunk = GRK_CHUNKED_CH;
 static_assert(kPartialChunk == 64 || kPartialChunk == 128 || kPartialChunk == 256, "GRK_CHUNKED_CH: 64, 128 or 256");
 
-template <typename G, int LW, int CH>
+template <typename G, int LW, int CH, typename OT = float>
 __global__ void __launch_bounds__(256) k_seg_chunks_partial(const unsigned* __restrict__ keys,
                                                             const unsigned long long* __restrict__ gptr,
                                                             const int* __restrict__ pos,
                                                             const int* __restrict__ seg_start,
                                                             const int* __restrict__ seg_end, int64_t n,
-                                                            unsigned sentinel, int dim, float* __restrict__ dense_out,
+                                                            unsigned sentinel, int dim, OT* __restrict__ dense_out,
                                                             float* __restrict__ uniq_rows,
                                                             int32_t* __restrict__ row_slot,
                                                             float* __restrict__ partials) {
-  seg_chunks_wave_body<G, LW, CH>((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, keys, gptr, pos,
-                                  seg_start, seg_end, n, sentinel, dim, dense_out, uniq_rows, row_slot, partials);
+  seg_chunks_wave_body<G, LW, CH, OT>((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, keys, gptr,
+                                      pos, seg_start, seg_end, n, sentinel, dim, dense_out, uniq_rows, row_slot,
+                                      partials);
 }
 
 // One wave per chunk edge b: the row first crossing b (it starts in chunk
 // b - 1, whose tail slot holds its first piece) = tail(b - 1) + head(b) + ...
 // + head(last chunk of the row), added in that order.
-template <int LW, int CH>
+template <int LW, int CH, typename OT = float>
 __global__ void __launch_bounds__(256) k_seg_partials_combine(const unsigned* __restrict__ keys,
                                                               const int* __restrict__ pos,
                                                               const int* __restrict__ seg_start,
                                                               const int* __restrict__ seg_end, int64_t n,
                                                               unsigned sentinel, int dim,
                                                               const float* __restrict__ partials,
-                                                              float* __restrict__ dense_out,
+                                                              OT* __restrict__ dense_out,
                                                               float* __restrict__ uniq_rows,
                                                               int32_t* __restrict__ row_slot) {
   constexpr int PIPE = 8;
@@ -1036,11 +1058,17 @@ extern "C" size_t grk_embedding_backward_workspace(int64_t num_occurrences, int6
 
 extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups, int dim, int grad_dtype,
                                       int itype, const int32_t* token_type, int32_t seq_len, int64_t num_rows,
-                                      int64_t padding_idx, float* dense_out, int64_t* uniq_ids, float* uniq_rows,
+                                      int64_t padding_idx, void* dense_out_, int64_t* uniq_ids, float* uniq_rows,
                                       int32_t* uniq_count, int32_t* row_slot, int flags, void* workspace,
                                       size_t workspace_bytes, int32_t* err_flag, void* stream) {
   clear_error();
+  const bool dense_bf16 = (flags & GRK_BWD_DENSE_BF16) != 0;
+  flags &= ~GRK_BWD_DENSE_BF16;
   GRK_CHECK_ARG(flags == GRK_BWD_ORDERED || flags == GRK_BWD_CHUNKED, "bad flags %d", flags);
+  GRK_CHECK_ARG(!dense_bf16 || (flags == GRK_BWD_CHUNKED && grad_dtype == GRK_BF16 && dim == 512),
+                "GRK_BWD_DENSE_BF16 needs GRK_BWD_CHUNKED with bf16 gradients of 512 columns");
+  float* dense_out = dense_bf16 ? nullptr : (float*)dense_out_;
+  bf16_t* dense_out16 = dense_bf16 ? (bf16_t*)dense_out_ : nullptr;
   GRK_CHECK_ARG(lookups && num_lookups > 0, "need at least one lookup");
   GRK_CHECK_ARG(grad_dtype == GRK_F32 || grad_dtype == GRK_BF16, "grad_dtype must be GRK_F32 or GRK_BF16");
   GRK_CHECK_ARG(itype == GRK_I32 || itype == GRK_I64, "bad itype");
@@ -1076,6 +1104,7 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   hipStream_t s = (hipStream_t)stream;
   GRK_CHECK_HIP(zero_async(uniq_count, sizeof(int32_t), s));
   if (dense_out) GRK_CHECK_HIP(zero_async(dense_out, (size_t)num_rows * dim * sizeof(float), s));
+  if (dense_out16) GRK_CHECK_HIP(zero_async(dense_out16, (size_t)num_rows * dim * sizeof(bf16_t), s));
   if (total == 0) return GRK_OK;
   const int B = 256;
   const int esize = grad_dtype == GRK_F32 ? 4 : 2;
@@ -1141,7 +1170,16 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
     k_seg_partials_combine<LW, kPartialChunk><<<ge, 256, 0, s>>>(ws.keys_out, ws.pos, ws.seg_start, ws.seg_end,  \
                                                                  total, sentinel, dim, ws.partials, dense_out,    \
                                                                  uniq_rows, row_slot)
-      if (grad_dtype == GRK_BF16) { GRK_SEGP(bf16_t, 8); }
+      if (dense_out16) {
+        k_seg_chunks_partial<bf16_t, 8, kPartialChunk, bf16_t><<<gw, 256, 0, s>>>(
+            ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel, dim, dense_out16, uniq_rows,
+            row_slot, ws.partials);
+        GRK_LAUNCH_CHECK();
+        if (ge)
+          k_seg_partials_combine<8, kPartialChunk, bf16_t><<<ge, 256, 0, s>>>(
+              ws.keys_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel, dim, ws.partials, dense_out16, uniq_rows,
+              row_slot);
+      } else if (grad_dtype == GRK_BF16) { GRK_SEGP(bf16_t, 8); }
       else if (lw == 8) { GRK_SEGP(float, 8); }
       else { GRK_SEGP(float, 4); }
 #undef GRK_SEGP

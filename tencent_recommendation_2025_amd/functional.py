@@ -78,8 +78,13 @@ class DenseMerge:
             D = self.weights[0].shape[1]
             src = [K.GradSource(sp.idx, g, c, sp.mode, sp.bag, offs[id(sp.ref.weight)], sp.ref.weight.shape[0])
                    for sp, g, c in self.sources]
-            res = K.embedding_backward(src, total, D, padding_idx=0, dense=True,
-                                       chunked=all(sp.ref.chunked for sp, _, _ in self.sources))
+            chunked = all(sp.ref.chunked for sp, _, _ in self.sources)
+            # bf16 tables (the fused trainer's projections): the kernel rounds each dense row to
+            # bf16 itself (GRK_BWD_DENSE_BF16) -- no fp32 buffer and no cast kernel
+            bf16 = (chunked and D == 512 and all(w.dtype == torch.bfloat16 for w in self.weights)
+                    and all(g.dtype == torch.bfloat16 for _, g, _ in self.sources))
+            res = K.embedding_backward(src, total, D, padding_idx=0, dense=True, chunked=chunked,
+                                       dense_dtype=torch.bfloat16 if bf16 else torch.float32)
             out = {id(w): res.dense[offs[id(w)]:offs[id(w)] + w.shape[0]].to(w.dtype) for w in self.weights}
         self.sources = []
         return out

@@ -110,19 +110,22 @@ BACKWARD_TRACE = None  # bench.py: a list records the embedding_backward calls o
 
 
 def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, seq_len=0, dense=True,
-                       sparse=False, row_slot=None, err_flag=None, chunked=False):
+                       sparse=False, row_slot=None, err_flag=None, chunked=False, dense_dtype=torch.float32):
     """Deterministic scatter-add table gradient (grk_embedding_backward).
 
     Returns a ``BackwardResult`` with ``dense`` ([num_rows, dim] fp32) when
     ``dense`` and ``ids``/``rows``/``count`` (row-sparse form, capacity =
     number of occurrences) when ``sparse``.  ``chunked``: rows spanning several
     chunks of the sorted occurrences are added chunk-sum by chunk-sum
-    (GRK_BWD_CHUNKED; fixed order, not the occurrence order).
+    (GRK_BWD_CHUNKED; fixed order, not the occurrence order).  ``dense_dtype``
+    bfloat16 (chunked, bf16 gradients, dim 512): the dense rows rounded to bf16
+    once in the kernel (GRK_BWD_DENSE_BF16).
     """
     if BACKWARD_TRACE is not None:
         BACKWARD_TRACE.append(dict(sources=list(sources), num_rows=num_rows, dim=dim, padding_idx=padding_idx,
                                    token_type=token_type, seq_len=seq_len, dense=dense, sparse=sparse,
-                                   row_slot=None if row_slot is None else row_slot.clone(), chunked=chunked))
+                                   row_slot=None if row_slot is None else row_slot.clone(), chunked=chunked,
+                                   dense_dtype=dense_dtype))
     dev = sources[0].grad.device
     gdt = sources[0].grad.dtype
     it = sources[0].idx.dtype
@@ -150,7 +153,13 @@ def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, s
         keep.append(token_type)
     ws_bytes = L.lib().grk_embedding_backward_workspace(total, num_rows, dim)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    dense_out = torch.empty((num_rows, dim), dtype=torch.float32, device=dev) if dense else None
+    if dense_dtype not in (torch.float32, torch.bfloat16):
+        raise L.GrkError(f'dense gradient dtype {dense_dtype} is neither fp32 nor bf16')
+    bf16_out = dense and dense_dtype == torch.bfloat16
+    if bf16_out and not (chunked and gdt == torch.bfloat16 and dim == 512):
+        raise L.GrkError('a bf16 dense gradient needs chunked=True with bf16 gradients of 512 columns')
+    dense_out = torch.empty((num_rows, dim), dtype=torch.bfloat16 if bf16_out else torch.float32,
+                            device=dev) if dense else None
     cap = max(total, 1)
     ids = torch.empty(cap, dtype=torch.int64, device=dev) if sparse else None
     rows = torch.empty((cap, dim), dtype=torch.float32, device=dev) if sparse else None
@@ -158,7 +167,8 @@ def embedding_backward(sources, num_rows, dim, padding_idx=0, token_type=None, s
     rc = L.lib().grk_embedding_backward(lk, len(sources), dim, L.dtype_code(gdt), L.itype_code(it),
                                         _ptr(token_type), seq_len, num_rows, -1 if padding_idx is None else padding_idx,
                                         _ptr(dense_out), _ptr(ids), _ptr(rows), count.data_ptr(), _ptr(row_slot),
-                                        L.BWD_CHUNKED if chunked else L.BWD_ORDERED, ws.data_ptr(), ws.numel(),
+                                        (L.BWD_CHUNKED if chunked else L.BWD_ORDERED) | (L.BWD_DENSE_BF16 if bf16_out else 0),
+                                        ws.data_ptr(), ws.numel(),
                                         _ptr(err_flag), L.stream_ptr(dev))
     L.check(rc, 'grk_embedding_backward')
     return BackwardResult(dense_out, ids, rows, count, cap)

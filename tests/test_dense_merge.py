@@ -28,7 +28,7 @@ CALLS = []
 
 
 def fake_backward(sources, num_rows, dim, padding_idx=0, token_type=None, seq_len=0, dense=True, sparse=False,
-                  row_slot=None, err_flag=None, chunked=False):
+                  row_slot=None, err_flag=None, chunked=False, dense_dtype=torch.float32):
     CALLS.append(len(sources))
     out = torch.zeros(num_rows, dim, dtype=torch.float64)
     for s in sources:
@@ -39,7 +39,7 @@ def fake_backward(sources, num_rows, dim, padding_idx=0, token_type=None, seq_le
             rows = idx[:, a]
             keep = rows != padding_idx
             out.index_add_(0, (rows + s.row_offset)[keep], g[keep])
-    return _Res(out.float())
+    return _Res(out.to(dense_dtype))
 
 
 @pytest.fixture

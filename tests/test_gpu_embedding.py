@@ -2,6 +2,8 @@
 grk_table_adamw) against the oracle, which is itself pinned to the reference's
 golden vectors (tests/test_oracle_golden.py).  Integer/byte work is checked
 bit-exact; the fp32 order-defined sums too."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -321,6 +323,29 @@ def test_backward_chunked_mode(K, D, dt):
     assert np.array_equal(s[uniq], np.arange(cnt)) and np.all(np.delete(s, uniq) == -1)
     again = K.embedding_backward(src, R, D, dense=True, chunked=True).dense
     assert torch.equal(again, res.dense)
+
+
+@pytest.mark.skipif(os.environ.get('GRK_MERGE_PROJ_TESTS') != '1',
+                    reason='bf16 dense output not yet run on the GPU (set GRK_MERGE_PROJ_TESTS=1)')
+def test_backward_chunked_bf16_dense_is_the_rounded_fp32_result(K):
+    """GRK_BWD_DENSE_BF16: the dense rows are the chunked fp32 result rounded
+    to bf16 once (round to nearest even, as torch's cast) -- bit-exact against
+    the fp32 call; untouched rows zero; row-sparse outputs stay fp32 and equal."""
+    rng = np.random.default_rng(6)
+    R, D = 3000, 512
+    idx = np.concatenate([np.full(9000, 5), np.repeat(np.arange(10, 20), rng.integers(300, 513, 10)),
+                          rng.integers(20, R, 12000), np.zeros(500, np.int64)])
+    rng.shuffle(idx)
+    gt = T(oemb.to_bf16_f32(rng.standard_normal((len(idx), D)).astype(np.float32))).to(torch.bfloat16)
+    src = [K.GradSource(T(idx), gt, 0)]
+    ref = K.embedding_backward(src, R, D, dense=True, sparse=True, chunked=True)
+    got = K.embedding_backward(src, R, D, dense=True, sparse=True, chunked=True, dense_dtype=torch.bfloat16)
+    assert got.dense.dtype == torch.bfloat16 and got.dense.shape == (R, D)
+    assert torch.equal(got.dense, ref.dense.to(torch.bfloat16))
+    cnt = int(ref.count.item())
+    assert int(got.count.item()) == cnt and torch.equal(got.rows[:cnt], ref.rows[:cnt])
+    with pytest.raises(RuntimeError):
+        K.embedding_backward(src, R, D, dense=True, chunked=False, dense_dtype=torch.bfloat16)
 
 
 # ------------------------------------------------ occurrence sort (grk_sort) --
