@@ -298,8 +298,8 @@ typedef struct grk_attn_args {
                                       2 (fp32 fidelity): Q/K/V and dO as well, each
                                       product as hi*hi + hi*lo + lo*hi; q/k/v then
                                       have dtype qkv_dtype (whole-sequence kernels,
-                                      and head_dim 256 in the wide-head kernels
-                                      when GRK_ATTN_WIDE_FIDELITY is set -- opt-in
+                                      and head_dim 256 / 512 in the wide-head
+                                      kernels when GRK_ATTN_WIDE_FIDELITY is set -- opt-in
                                       until hardware-tested; GRK_EUNSUPPORTED
                                       elsewhere)                                 */
   uint64_t seed;                   /* dropout stream                              */
@@ -355,7 +355,7 @@ typedef struct grk_attn_args {
 
 /* 1 when grk_attention_* with precise == 2 (fp32 fidelity) runs for this
  * sequence length and head_dim (the whole-sequence kernels' LDS; head_dim 256
- * at any length with GRK_ATTN_WIDE_FIDELITY set), else 0. */
+ * and 512 at any length with GRK_ATTN_WIDE_FIDELITY set), else 0. */
 int grk_attention_fidelity_supported(int seq_len, int head_dim);
 
 /* ranges int32 [batch, 3]: ranges[b][0] = first j with key_valid[b, j] (T for

@@ -52,7 +52,7 @@ case "${1:-tests}" in
     step sharded_jagged 300 env GRK_SHARDED_JAGGED_TESTS=1 $PYT tests/test_gpu_sharding.py -k sharded_jagged
     step time_bias 400 env GRK_CHUNKED_TIME_TESTS=1 $PYT tests/test_gpu_attention.py -k time_bias
     step wide_fidelity 400 env GRK_WIDE_FIDELITY_TESTS=1 $PYT tests/test_gpu_attention.py tests/test_gpu_model.py \
-      -k "wide_fidelity or 256_fidelity"
+      -k wide_fidelity
     timeout -k 10 200 python -u bench.py --steps 30 --warmup 10 --cpu-baseline 0 --roofline-reps 5 --merge-proj 1 \
       > $O/bench_merge_proj.json 2> $O/bench_merge_proj.err
     echo "bench_merge_proj rc=$?" >> $O/summary.txt

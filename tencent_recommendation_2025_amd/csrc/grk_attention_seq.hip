@@ -1091,7 +1091,8 @@ extern "C" int grk_attention_fidelity_supported(int seq_len, int head_dim) {
     case 32: return fidelity_fits<32>(seq_len);
     case 64: return fidelity_fits<64>(seq_len);
     case 128: return fidelity_fits<128>(seq_len);
-    case 256: return wide_fidelity_enabled(256) ? 1 : 0;  // the wide-head kernels (any T)
+    case 256:
+    case 512: return wide_fidelity_enabled(head_dim) ? 1 : 0;  // the wide-head kernels (any T)
   }
   return 0;
 }

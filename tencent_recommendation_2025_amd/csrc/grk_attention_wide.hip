@@ -19,25 +19,25 @@
 // image.  Element math, masks, dropout and the HSTU pointwise form
 // are those of grk_attention.hip (same drop_keep stream, same lse / delta
 // conventions), so the backward of either path reads the other's forward.
-// fp32-fidelity (precise = 2): head_dim 256 only, opt-in (grk_attention_wide_fid.hip).
+// fp32-fidelity (precise = 2): head_dim 256 / 512, opt-in (grk_attention_wide_fid.hip).
 // The kernels: grk_attention_wide_kernels.h.
 #include "grk_attention_wide_kernels.h"
 
 namespace grk {
 
 bool wide_fidelity_enabled(int hd) {
-  // head_dim 256 only (512's hi + lo images do not fit LDS beside the partial
-  // products); written in round 3 without hardware: opt-in until its parity
-  // test has run on an MI355X
-  return hd == 256 && getenv("GRK_ATTN_WIDE_FIDELITY") != nullptr;
+  // head_dim 256 and 512 (512: the partial products meet in rounds, WideF);
+  // written in round 3 without hardware: opt-in until its parity test has
+  // run on an MI355X
+  return (hd == 256 || hd == 512) && getenv("GRK_ATTN_WIDE_FIDELITY") != nullptr;
 }
 
 // grk_attention_wide_fid.hip
-int attn_wide_fid_launch(const AttnParams& p, int which, hipStream_t s);
+int attn_wide_fid_launch(const AttnParams& p, int hd, int which, hipStream_t s);
 
 int attn_wide_launch(const AttnParams& p, int hd, int which, hipStream_t s) {
   if (p.precise == 2) {
-    if (wide_fidelity_enabled(hd)) return attn_wide_fid_launch(p, which, s);
+    if (wide_fidelity_enabled(hd)) return attn_wide_fid_launch(p, hd, which, s);
     set_error("fp32-fidelity attention (precise = 2) is not offered for head_dim %d", hd);
     return GRK_EUNSUPPORTED;
   }

@@ -26,6 +26,19 @@ struct Wide {
   static constexpr int GX = NW * 64 * EPW * 4;      // P or dS as bf16 hi / lo words: [wave][lane][EPW]
 };
 
+// fp32 fidelity at head_dim 512: the hi + lo images (4 x 32 KiB) leave no room
+// for whole-tile partial products, so the partials meet in RR rounds of 8 / RR
+// element pairs (red_rounds) -- the same additions in the same order, 1 / RR of
+// the LDS -- and the next tile is fetched at the top of the loop instead of
+// under the current tile's products (its registers would spill).
+template <int HD, bool FID>
+struct WideF {
+  static constexpr int RR = (FID && HD == 512) ? 4 : 1;
+  static constexpr int RED = Wide<HD>::RED / RR;    // one partial-product buffer
+  static constexpr bool PREFETCH = RR == 1;
+};
+constexpr size_t kMaxWideLds = 160 * 1024;
+
 // This wave's partial 32x32 product (over its column slice) to LDS.
 __device__ __forceinline__ void red_put(float2* red, int ws, int lane, const f32x16& x) {
 #pragma unroll
@@ -90,6 +103,49 @@ __device__ __forceinline__ void* shift(void* p, bool f32, int n) { return (char*
 // Workgroup barrier for LDS hand-offs only (waits for LDS operations, not for
 // the next tile's global loads, which __syncthreads()' fence would drain).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// red_put + barrier + red_own (of one or, TWO, two products) in RR rounds: in
+// round rd every wave writes pairs [rd PR, (rd + 1) PR) of its partials and the
+// waves owning one of those pairs sum them, wave 0 first, as red_own does.
+template <int NW, int RR, bool TWO>
+__device__ __forceinline__ void red_rounds(float2* red, float2* red2, int ws, int lane, const f32x16& x,
+                                           const f32x16& x2, float* e, float* e2) {
+  constexpr int PR = 8 / RR, OWN = 16 / NW / 2;  // pairs per round; pairs a wave owns
+#pragma unroll
+  for (int rd = 0; rd < RR; ++rd) {
+    if (rd > 0) lds_barrier();  // the previous round's partials have been read
+#pragma unroll
+    for (int q = 0; q < PR; ++q) {
+      const int pr = rd * PR + q;
+      red[(ws * PR + q) * 64 + lane] = make_float2(x[2 * pr], x[2 * pr + 1]);
+      if (TWO) red2[(ws * PR + q) * 64 + lane] = make_float2(x2[2 * pr], x2[2 * pr + 1]);
+    }
+    lds_barrier();
+#pragma unroll
+    for (int q = 0; q < OWN; ++q) {
+      const int lp = ws * OWN + q - rd * PR;  // the owned pair's slot in this round (wave-uniform)
+      if (lp < 0 || lp >= PR) continue;
+      float2 t = red[lp * 64 + lane], t2 = TWO ? red2[lp * 64 + lane] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int w = 1; w < NW; ++w) {
+        const float2 u = red[(w * PR + lp) * 64 + lane];
+        t.x += u.x;
+        t.y += u.y;
+        if (TWO) {
+          const float2 u2 = red2[(w * PR + lp) * 64 + lane];
+          t2.x += u2.x;
+          t2.y += u2.y;
+        }
+      }
+      e[2 * q] = t.x;
+      e[2 * q + 1] = t.y;
+      if (TWO) {
+        e2[2 * q] = t2.x;
+        e2[2 * q + 1] = t2.y;
+      }
+    }
+  }
+}
 
 // 32 rows x HD of a [B*T, ld] head slice (bf16, or fp32 when F32), zero past
 // T: fetch() into registers under the previous tile's work, put() into the
@@ -195,6 +251,7 @@ __device__ __forceinline__ uint8_t key_ok(const AttnParams& p, int b, int t) {
 template <int HD, int KIND, bool TB = false, bool FID = false>
 __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
   using W = Wide<HD>;
+  using WF = WideF<HD, FID>;
   constexpr int KSQ = W::KSQ, NDT = W::NDT, NW = W::NW, EPW = W::EPW;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   char* smem = smem_raw + (FID ? 2 * W::IMG : 0);
@@ -203,9 +260,9 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
   char* Ks = smem;
   char* Vs = smem + W::IMG;
   float2* red = reinterpret_cast<float2*>(smem + 2 * W::IMG);
-  uint32_t* gxp = reinterpret_cast<uint32_t*>(smem + 2 * W::IMG + W::RED);
-  float* mx = reinterpret_cast<float*>(smem + 2 * W::IMG + W::RED + W::GX);  // [wave][lane]
-  char* tail = smem + 2 * W::IMG + W::RED + W::GX + NW * 64 * 4;
+  uint32_t* gxp = reinterpret_cast<uint32_t*>(smem + 2 * W::IMG + WF::RED);
+  float* mx = reinterpret_cast<float*>(smem + 2 * W::IMG + WF::RED + W::GX);  // [wave][lane]
+  char* tail = smem + 2 * W::IMG + WF::RED + W::GX + NW * 64 * 4;
   uint8_t* kvs = reinterpret_cast<uint8_t*>(tail);
   int* s_start = reinterpret_cast<int*>(tail + 32);
   float* rabs = reinterpret_cast<float*>(tail + kWTail);
@@ -254,8 +311,10 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
   uint8_t kvb = 0;
   if (kbeg < kend) {
     if constexpr (FID) {
-      ktf.fetch(p.k, p.ldk, p.in_dt, b, T, h, kbeg);
-      vtf.fetch(p.v, p.ldv, p.in_dt, b, T, h, kbeg);
+      if (WF::PREFETCH) {
+        ktf.fetch(p.k, p.ldk, p.in_dt, b, T, h, kbeg);
+        vtf.fetch(p.v, p.ldv, p.in_dt, b, T, h, kbeg);
+      }
     } else {
       kt.fetch(p.k, p.ldk, b, T, h, kbeg);
       vt.fetch(p.v, p.ldv, b, T, h, kbeg);
@@ -263,6 +322,10 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
     if (threadIdx.x < 32) kvb = key_ok(p, b, kbeg + threadIdx.x);
   }
   for (int kb = kbeg; kb < kend; kb += 32) {
+    if (!WF::PREFETCH) {  // FID at 512: this tile fetched here, not under the previous one
+      ktf.fetch(p.k, p.ldk, p.in_dt, b, T, h, kb);
+      vtf.fetch(p.v, p.ldv, p.in_dt, b, T, h, kb);
+    }
     __syncthreads();
     if constexpr (FID) {
       ktf.put(Ks, Kl, p.act);
@@ -278,8 +341,10 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
     lds_barrier();
     if (kb + 32 < kend) {  // in flight under this tile's work
       if constexpr (FID) {
-        ktf.fetch(p.k, p.ldk, p.in_dt, b, T, h, kb + 32);
-        vtf.fetch(p.v, p.ldv, p.in_dt, b, T, h, kb + 32);
+        if (WF::PREFETCH) {
+          ktf.fetch(p.k, p.ldk, p.in_dt, b, T, h, kb + 32);
+          vtf.fetch(p.v, p.ldv, p.in_dt, b, T, h, kb + 32);
+        }
       } else {
         kt.fetch(p.k, p.ldk, b, T, h, kb + 32);
         vt.fetch(p.v, p.ldv, b, T, h, kb + 32);
@@ -299,10 +364,14 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
 #pragma unroll
       for (int ks = 0; ks < KSQ; ++ks) s = mfma(lds_row8<HD>(Ks, r, c0 + 16 * ks + 8 * hh), qf[ks], s);
     }
-    red_put(red, ws, lane, s);
-    lds_barrier();
     float se[EPW], pd[EPW];
-    red_own<NW>(red, ws, lane, se);
+    if constexpr (WF::RR > 1) {
+      red_rounds<NW, WF::RR, false>(red, red, ws, lane, s, s, se, se);
+    } else {
+      red_put(red, ws, lane, s);
+      lds_barrier();
+      red_own<NW>(red, ws, lane, se);
+    }
     if (KIND == 0) {
       float x[EPW], tmax = -INFINITY;
 #pragma unroll
@@ -376,6 +445,7 @@ __global__ void __launch_bounds__(HD) k_attn_fwd_wide(AttnParams p) {
 template <int HD, int KIND, bool TB = false, bool FID = false>
 __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
   using W = Wide<HD>;
+  using WF = WideF<HD, FID>;
   constexpr int KSQ = W::KSQ, NDT = W::NDT, NW = W::NW, EPW = W::EPW;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   char* smem = smem_raw + (FID ? 2 * W::IMG : 0);
@@ -384,9 +454,9 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
   char* Ks = smem;
   char* Vs = smem + W::IMG;
   float2* red = reinterpret_cast<float2*>(smem + 2 * W::IMG);
-  float2* red2 = reinterpret_cast<float2*>(smem + 2 * W::IMG + W::RED);
-  uint32_t* gxd = reinterpret_cast<uint32_t*>(smem + 2 * W::IMG + 2 * W::RED);
-  char* tail = smem + 2 * W::IMG + 2 * W::RED + W::GX;
+  float2* red2 = reinterpret_cast<float2*>(smem + 2 * W::IMG + WF::RED);
+  uint32_t* gxd = reinterpret_cast<uint32_t*>(smem + 2 * W::IMG + 2 * WF::RED);
+  char* tail = smem + 2 * W::IMG + 2 * WF::RED + W::GX;
   uint8_t* kvs = reinterpret_cast<uint8_t*>(tail);
   int* s_start = reinterpret_cast<int*>(tail + 32);
   float* rabs = reinterpret_cast<float*>(tail + kWTail);
@@ -449,8 +519,10 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
   uint8_t kvb = 0;
   if (kbeg < kend) {
     if constexpr (FID) {
-      ktf.fetch(p.k, p.ldk, p.in_dt, b, T, h, kbeg);
-      vtf.fetch(p.v, p.ldv, p.in_dt, b, T, h, kbeg);
+      if (WF::PREFETCH) {
+        ktf.fetch(p.k, p.ldk, p.in_dt, b, T, h, kbeg);
+        vtf.fetch(p.v, p.ldv, p.in_dt, b, T, h, kbeg);
+      }
     } else {
       kt.fetch(p.k, p.ldk, b, T, h, kbeg);
       vt.fetch(p.v, p.ldv, b, T, h, kbeg);
@@ -458,6 +530,10 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
     if (threadIdx.x < 32) kvb = key_ok(p, b, kbeg + threadIdx.x);
   }
   for (int kb = kbeg; kb < kend; kb += 32) {
+    if (!WF::PREFETCH) {  // FID at 512: this tile fetched here, not under the previous one
+      ktf.fetch(p.k, p.ldk, p.in_dt, b, T, h, kb);
+      vtf.fetch(p.v, p.ldv, p.in_dt, b, T, h, kb);
+    }
     __syncthreads();
     if constexpr (FID) {
       ktf.put(Ks, Kl, p.act);
@@ -473,8 +549,10 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
     lds_barrier();
     if (kb + 32 < kend) {  // in flight under this tile's work
       if constexpr (FID) {
-        ktf.fetch(p.k, p.ldk, p.in_dt, b, T, h, kb + 32);
-        vtf.fetch(p.v, p.ldv, p.in_dt, b, T, h, kb + 32);
+        if (WF::PREFETCH) {
+          ktf.fetch(p.k, p.ldk, p.in_dt, b, T, h, kb + 32);
+          vtf.fetch(p.v, p.ldv, p.in_dt, b, T, h, kb + 32);
+        }
       } else {
         kt.fetch(p.k, p.ldk, b, T, h, kb + 32);
         vt.fetch(p.v, p.ldv, b, T, h, kb + 32);
@@ -501,12 +579,16 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
         dp = mfma(lds_row8<HD>(Vs, r, c0 + 16 * ks + 8 * hh), dof[ks], dp);
       }
     }
-    red_put(red, ws, lane, s);
-    red_put(red2, ws, lane, dp);
-    lds_barrier();
     float se[EPW], de[EPW], ds[EPW];
-    red_own<NW>(red, ws, lane, se);
-    red_own<NW>(red2, ws, lane, de);
+    if constexpr (WF::RR > 1) {
+      red_rounds<NW, WF::RR, true>(red, red2, ws, lane, s, dp, se, de);
+    } else {
+      red_put(red, ws, lane, s);
+      red_put(red2, ws, lane, dp);
+      lds_barrier();
+      red_own<NW>(red, ws, lane, se);
+      red_own<NW>(red2, ws, lane, de);
+    }
 #pragma unroll
     for (int e = 0; e < EPW; ++e) {
       const int kr = elem_row(ws * EPW + e, hh), key = kb + kr;
@@ -567,6 +649,7 @@ __global__ void __launch_bounds__(HD) k_attn_dq_wide(AttnParams p) {
 template <int HD, int KIND, bool DF32, bool TB = false, bool FID = false>
 __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
   using W = Wide<HD>;
+  using WF = WideF<HD, FID>;
   constexpr int KSQ = W::KSQ, NDT = W::NDT, NW = W::NW, EPW = W::EPW;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   char* smem = smem_raw + (FID ? 2 * W::IMG : 0);
@@ -575,10 +658,10 @@ __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
   char* Qs = smem;
   char* Ds = smem + W::IMG;
   float2* red = reinterpret_cast<float2*>(smem + 2 * W::IMG);
-  float2* red2 = reinterpret_cast<float2*>(smem + 2 * W::IMG + W::RED);
-  uint32_t* gxp = reinterpret_cast<uint32_t*>(smem + 2 * W::IMG + 2 * W::RED);
+  float2* red2 = reinterpret_cast<float2*>(smem + 2 * W::IMG + WF::RED);
+  uint32_t* gxp = reinterpret_cast<uint32_t*>(smem + 2 * W::IMG + 2 * WF::RED);
   uint32_t* gxd = gxp + W::GX / 4;
-  char* tail = smem + 2 * W::IMG + 2 * W::RED + 2 * W::GX;
+  char* tail = smem + 2 * W::IMG + 2 * WF::RED + 2 * W::GX;
   int* s_start = reinterpret_cast<int*>(tail + 32);
   float* lses = reinterpret_cast<float*>(tail + 48);
   float* dlts = lses + 32;
@@ -647,8 +730,9 @@ __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
       dl = p.delta[(int64_t)bh * T + t];
     }
   };
-  if (qbeg < T) fetch(qbeg);
+  if (WF::PREFETCH && qbeg < T) fetch(qbeg);
   for (int qb = qbeg; qb < T; qb += 32) {
+    if (!WF::PREFETCH) fetch(qb);  // FID at 512: this tile fetched here, not under the previous one
     __syncthreads();
     if constexpr (FID) {
       qtf.put(Qs, Ql, p.act);
@@ -663,7 +747,7 @@ __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
       if constexpr (TB) tsq[threadIdx.x] = rel_stamp(p, b, T, start, qb + threadIdx.x);
     }
     lds_barrier();
-    if (qb + 32 < T) fetch(qb + 32);  // in flight under this tile's work
+    if (WF::PREFETCH && qb + 32 < T) fetch(qb + 32);  // in flight under this tile's work
     f32x16 s = acc_zero(), dp = acc_zero();
     if constexpr (FID) {
 #pragma unroll
@@ -684,12 +768,16 @@ __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
         dp = mfma(lds_row8<HD>(Ds, r, c0 + 16 * ks + 8 * hh), vf[ks], dp);
       }
     }
-    red_put(red, ws, lane, s);
-    red_put(red2, ws, lane, dp);
-    lds_barrier();
     float se[EPW], de[EPW], pd[EPW], ds[EPW];
-    red_own<NW>(red, ws, lane, se);
-    red_own<NW>(red2, ws, lane, de);
+    if constexpr (WF::RR > 1) {
+      red_rounds<NW, WF::RR, true>(red, red2, ws, lane, s, dp, se, de);
+    } else {
+      red_put(red, ws, lane, s);
+      red_put(red2, ws, lane, dp);
+      lds_barrier();
+      red_own<NW>(red, ws, lane, se);
+      red_own<NW>(red2, ws, lane, de);
+    }
 #pragma unroll
     for (int e = 0; e < EPW; ++e) {
       const int qr = elem_row(ws * EPW + e, hh), q = qb + qr;
@@ -751,28 +839,38 @@ __global__ void __launch_bounds__(HD) k_attn_dkdv_wide(AttnParams p) {
   }
 }
 
+inline int wide_lds_refused(size_t lds) {
+  set_error("wide-head attention needs %zu bytes of LDS (at most %zu: fewer relative-position buckets)", lds,
+            kMaxWideLds);
+  return GRK_EUNSUPPORTED;
+}
+
 template <int HD, bool FID = false>
 int wide_hd(const AttnParams& p, int which, hipStream_t s) {
   using W = Wide<HD>;
+  constexpr size_t RED = WideF<HD, FID>::RED;
   const dim3 grid((p.T + kWRows - 1) / kWRows, p.H, p.B);
   const bool hstu = p.kind == GRK_ATTN_HSTU;
   const bool tb = hstu && p.nbt > 0;
   const size_t rab = hstu ? (size_t)(p.nb + 1) / 2 * 2 * 4 : 0;
   const size_t tlds = (tb ? (size_t)kWTime : 0) + (FID ? (size_t)2 * W::IMG : 0);  // + FID's lo images
   if (which == 0) {
-    const size_t lds = 2 * W::IMG + W::RED + W::GX + W::NW * 64 * 4 + kWTail + rab + tlds;
+    const size_t lds = 2 * W::IMG + RED + W::GX + W::NW * 64 * 4 + kWTail + rab + tlds;
+    if (lds > kMaxWideLds) return wide_lds_refused(lds);
     launch_lds(tb     ? k_attn_fwd_wide<HD, 1, true, FID>
                : hstu ? k_attn_fwd_wide<HD, 1, false, FID>
                       : k_attn_fwd_wide<HD, 0, false, FID>,
                grid, W::NT, lds, s, p);
   } else if (which == 2) {
-    const size_t lds = 2 * W::IMG + 2 * W::RED + W::GX + kWTail + rab + (hstu ? (size_t)p.nb * 8 : 0) + tlds;
+    const size_t lds = 2 * W::IMG + 2 * RED + W::GX + kWTail + rab + (hstu ? (size_t)p.nb * 8 : 0) + tlds;
+    if (lds > kMaxWideLds) return wide_lds_refused(lds);
     launch_lds(tb     ? k_attn_dq_wide<HD, 1, true, FID>
                : hstu ? k_attn_dq_wide<HD, 1, false, FID>
                       : k_attn_dq_wide<HD, 0, false, FID>,
                grid, W::NT, lds, s, p);
   } else {
-    const size_t lds = 2 * W::IMG + 2 * W::RED + 2 * W::GX + kWTail + rab + tlds;
+    const size_t lds = 2 * W::IMG + 2 * RED + 2 * W::GX + kWTail + rab + tlds;
+    if (lds > kMaxWideLds) return wide_lds_refused(lds);
     if (p.dout_f32)
       launch_lds(tb     ? k_attn_dkdv_wide<HD, 1, true, true, FID>
                  : hstu ? k_attn_dkdv_wide<HD, 1, true, false, FID>

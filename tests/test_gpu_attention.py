@@ -462,7 +462,7 @@ def test_wide_head_rejects_fidelity_mode(K):
         K.attention_fwd(args, torch.empty(64, 512, device=DEV), torch.empty(2, 1, 32, device=DEV))
 
 
-# fp32 fidelity at head_dim 256 (grk_attention_wide_fid.hip): written in round 3
+# fp32 fidelity at head_dim 256 / 512 (grk_attention_wide_fid.hip): written in round 3
 # without hardware; the library takes it only with GRK_ATTN_WIDE_FIDELITY set,
 # and this parity test is opt-in (GRK_WIDE_FIDELITY_TESTS=1) until it has run.
 WIDE_FIDELITY = pytest.mark.skipif(os.environ.get('GRK_WIDE_FIDELITY_TESTS') != '1',
@@ -473,13 +473,15 @@ WIDE_FIDELITY = pytest.mark.skipif(os.environ.get('GRK_WIDE_FIDELITY_TESTS') != 
 @pytest.mark.parametrize('in_dtype', [torch.float32, torch.float16], ids=['f32', 'f16'])
 @pytest.mark.parametrize('H,T,lens', [(1, 102, [102, 60, 7]), (2, 201, [201, 33])])
 @pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
-def test_wide_fidelity_matches_fp64_oracle(K, monkeypatch, kind, H, T, lens, in_dtype):
-    """precise=2 at head_dim 256 (O1's num_heads=1 at hidden 256): Q/K/V / dO read
-    exactly and split into bf16 hi + lo, every product hi*hi + hi*lo + lo*hi,
-    against the fp64 oracle on the unrounded inputs (the narrow kernels' bound)."""
+@pytest.mark.parametrize('hd', [256, 512])
+def test_wide_fidelity_matches_fp64_oracle(K, monkeypatch, hd, kind, H, T, lens, in_dtype):
+    """precise=2 at head_dim 256 / 512 (O1's num_heads=1 at hidden 256 / 512): Q/K/V /
+    dO read exactly and split into bf16 hi + lo, every product hi*hi + hi*lo + lo*hi,
+    against the fp64 oracle on the unrounded inputs (the narrow kernels' bound).  At
+    512 the waves' partial products meet in four rounds (WideF)."""
     monkeypatch.setenv('GRK_ATTN_WIDE_FIDELITY', '1')
-    assert K.fidelity_supported(T, 256)
-    res, want = run_fidelity(K, kind, len(lens), T, H, 256, lens, in_dtype, seed=T + H,
+    assert K.fidelity_supported(T, hd)
+    res, want = run_fidelity(K, kind, len(lens), T, H, hd, lens, in_dtype, seed=T + H,
                              act='silu' if kind == 1 else None)
     for key in res:
         err = nrel(res[key], want[key])
