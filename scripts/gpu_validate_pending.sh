@@ -14,6 +14,7 @@
 #   gpurun --timeout 900 -- bash scripts/gpu_validate_pending.sh variants
 #   gpurun --timeout 900 -- bash scripts/gpu_validate_pending.sh ab
 #   gpurun --timeout 600 -- bash scripts/gpu_validate_pending.sh c5
+#   (c5lib: the torch GEMM forms at the C5 projection shape, diagnostic only)
 # Every step has its own time limit.  A step whose tests merely fail (pytest
 # exit 1) lets the independent steps after it run; a GPU fault (its message in
 # the log -- torch reports an illegal access as an ordinary exception), an
@@ -83,11 +84,23 @@ case "${1:-tests}" in
     bash scripts/gpu_ab.sh 2 "$LIBS" --steps 30 --warmup 10 && cp gpurun_out/ab.txt $O/ab.txt
     ;;
   c5)
-    # last: the d = 1024 model step faulted inside torch's batched GEMM in round 3
+    # last: the d = 1024 model step faulted inside torch's batched GEMM in round 3.
+    # First the projection shape alone on the path the model now takes (grk_gemm per
+    # block), in its own process; the model tests only if it is right.
+    step c5_grk_gemm 120 python -u scripts/diag/c5_gemm_isolate.py grk
+    grep -q "grk: normwise .* ok" $O/c5_grk_gemm.log || { echo "c5: projection GEMM not ok -- stopping" >> $O/summary.txt; exit 4; }
     step c5 400 env GRK_C5_MODEL_TESTS=1 $PYT tests/test_gpu_fp8.py
     ;;
+  c5lib)
+    # which torch GEMM form faults at the C5 projection shape (library behaviour, not the
+    # product path): non-batched, batched contiguous, then the round-3 strided call.
+    # Expect the call to end at the first fault (one gpurun strike).
+    for s in torch_mm torch_bmm torch_bmm_strided; do
+      step c5_$s 120 python -u scripts/diag/c5_gemm_isolate.py $s
+    done
+    ;;
   *)
-    echo "usage: $0 tests|variants|ab|c5" >&2
+    echo "usage: $0 tests|variants|ab|c5|c5lib" >&2
     exit 2
     ;;
 esac
