@@ -632,6 +632,53 @@ int grk_sample_negatives(const int32_t* pos, const int32_t* next_token_type, int
 int grk_rq_assign(const float* z, int64_t ld_z, const float* codebooks, int64_t n, int dim, int codes, int levels,
                   int32_t* out_codes, float* out_quant, float* out_dist, float* out_resid, void* stream);
 
+/* Host-side batch assembly of the columnar token store (seqstore.SeqStore,
+ * SURVEY.md §8(f) #1).  Replaces the per-token feature dicts of
+ * MyDataset.__getitem__ + fill_missing_feat (model/BaseLine/dataset.py:
+ * 136-169, 254-262) and feat2tensor (model/BaseLine/model.py:186-224) for a
+ * whole batch: no GPU, no allocation, plain loads and stores on host memory
+ * (DataLoader workers call it).
+ *
+ * The store holds, per token t: sparse[t, f_sparse] int32 feature ids,
+ * arr[t, f_array, a_cap] int32 array values (zero past each length) with
+ * arr_len[t, f_array], mm[t, f_mm] int32 rows of the multimodal tables. */
+typedef struct grk_store_view {
+  const int32_t* sparse; /* [tokens, f_sparse] */
+  const int32_t* arr;    /* [tokens, f_array, a_cap] */
+  const int32_t* arr_len;/* [tokens, f_array] */
+  const int32_t* mm;     /* [tokens, f_mm] */
+  int64_t tokens;
+  int32_t f_sparse, f_array, a_cap, f_mm;
+} grk_store_view;
+
+enum { GRK_STORE_SPARSE = 0, GRK_STORE_ARRAY = 1, GRK_STORE_MM = 2 };
+
+/* One output column: kind, its column in the store block, width (ARRAY: the
+ * output row width A, 1 <= A <= a_cap; MM: the table's row length; SPARSE: 1),
+ * mm_table (MM only: fp32 [mm_rows, width], row 0 = the zero row, mm_rows
+ * bounds the stored row ids), out (SPARSE: int64 [n]; ARRAY: int64 [n, A];
+ * MM: fp32 [n, width]). */
+typedef struct grk_store_col {
+  int32_t kind, src_col, width, pad_;
+  int64_t mm_rows;
+  const float* mm_table;
+  void* out;
+} grk_store_col;
+
+/* Output position i (0 <= i < n) is token tok[i] where sel[i] != 0 and the
+ * default (feature id 0 / array [0] padded with 0 / mm table row 0) where
+ * sel[i] == 0: out SPARSE[i] = sparse[tok, c]; ARRAY[i, j] = arr[tok, c, j]
+ * for j < arr_len[tok, c], else 0; MM[i, :] = mm_table[mm[tok, c], :].
+ * Fails (GRK_EINVAL, nothing written) when a selected tok[i] or a stored mm row
+ * is out of range. */
+int grk_store_features(const grk_store_view* store, const int64_t* tok, const uint8_t* sel, int64_t n,
+                       const grk_store_col* cols, int num_cols);
+
+/* widths[c] = max(1, max over selected i of arr_len[tok[i], c]) for c < f_array:
+ * the batch's longest array per array feature (feat2tensor pads to it). */
+int grk_store_array_widths(const grk_store_view* store, const int64_t* tok, const uint8_t* sel, int64_t n,
+                           int32_t* widths);
+
 #ifdef __cplusplus
 }
 #endif

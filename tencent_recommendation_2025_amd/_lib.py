@@ -71,6 +71,18 @@ class GrkRowCopy(C.Structure):
                 ('dst_ld', C.c_int64)]
 
 
+class GrkStoreView(C.Structure):
+    _fields_ = [('sparse', C.c_void_p), ('arr', C.c_void_p), ('arr_len', C.c_void_p), ('mm', C.c_void_p),
+                ('tokens', C.c_int64), ('f_sparse', C.c_int32), ('f_array', C.c_int32), ('a_cap', C.c_int32),
+                ('f_mm', C.c_int32)]
+
+
+class GrkStoreCol(C.Structure):
+    _fields_ = [('kind', C.c_int32), ('src_col', C.c_int32), ('width', C.c_int32), ('pad_', C.c_int32),
+                ('mm_rows', C.c_int64), ('mm_table', C.c_void_p), ('out', C.c_void_p)]
+
+
+STORE_SPARSE, STORE_ARRAY, STORE_MM = 0, 1, 2
 ATTN_SOFTMAX, ATTN_HSTU = 0, 1
 ATTN_BWD_DQ, ATTN_BWD_DKDV = 1, 2
 ACT_NONE, ACT_SILU = 0, 1
@@ -132,6 +144,8 @@ SIGNATURES = {
     'grk_mips_topk_workspace': (_SZ, [_I64, _I64]),
     'grk_mips_topk': (_I, [_P, _I64, _P, _I64, _I, _I64, _I64, _I, _I, _P, _P, _P, _P, _SZ, _P]),
     'grk_sample_negatives': (_I, [_P, _P, _I64, _I, _P, _I, _I64, C.c_uint64, _I, _P, _I, _P, _P, _P, _P, _P]),
+    'grk_store_features': (_I, [C.POINTER(GrkStoreView), _P, _P, _I64, C.POINTER(GrkStoreCol), _I]),
+    'grk_store_array_widths': (_I, [C.POINTER(GrkStoreView), _P, _P, _I64, _P]),
     'grk_rq_assign': (_I, [_P, _I64, _P, _I64, _I, _I, _I, _P, _P, _P, _P, _P]),
     'grk_gemm': (_I, [_I, _I, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _I, _P, _F, _F, _P, _I, _P]),
     'grk_pair_logits_partials': (_SZ, [_I64]),

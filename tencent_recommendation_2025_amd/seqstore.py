@@ -24,6 +24,7 @@ their values are parity-unpinned (the contract they satisfy is tested).
 """
 from __future__ import annotations
 
+import ctypes as C
 import json
 import pickle
 from pathlib import Path
@@ -201,28 +202,53 @@ class SeqStore:
     def _features(self, g, sel, fids):
         """{fid: tensor} of the tokens g where sel, the defaults elsewhere (tensorize's layout).
         One gather per feature kind (sparse block, array block, mm rows), then per-fid columns."""
-        out = {}
+        # grk_store_features (host code in libgrk, no GPU): one pass per output
+        # column, straight into the int64 / fp32 tensors feat2tensor would build
+        from . import _lib as L
+        B, T = g.shape
+        N = B * T
         sp_col = {f: c for c, f in enumerate(self.sparse_fids)}
         ar_col = {f: c for c, f in enumerate(self.array_fids)}
-        sparse = np.where(sel[..., None], self.sparse[g], 0).astype(np.int64) \
-            if any(k in sp_col for k in fids) else None
-        arrays = None
+        tok = np.ascontiguousarray(g.reshape(-1), dtype=np.int64)
+        sl = np.ascontiguousarray(sel.reshape(-1), dtype=np.uint8)
+        view = self._view()
+        widths = np.ones(max(1, len(self.array_fids)), np.int32)
         if any(k in ar_col for k in fids):
-            ln = np.where(sel[..., None], self.arr_len[g], 1)                  # [B, T, F_array]
-            vals = self.arr[g]                                                 # [B, T, F_array, A_cap]
-            keep = sel[..., None, None] & (np.arange(vals.shape[-1]) < ln[..., None])
-            arrays = (np.where(keep, vals, 0).astype(np.int64), ln)
+            L.check(L.lib().grk_store_array_widths(C.byref(view), tok.ctypes.data, sl.ctypes.data, N,
+                                                   widths.ctypes.data), 'grk_store_array_widths')
+        out, cols = {}, []
         for k in fids:
             if k in ar_col:
-                c = ar_col[k]
-                A = int(arrays[1][..., c].max()) if arrays[1].size else 1       # the batch's longest array
-                out[k] = torch.from_numpy(np.ascontiguousarray(arrays[0][:, :, c, :A]))
+                c, A = ar_col[k], int(widths[ar_col[k]])       # the batch's longest array
+                t = torch.empty((B, T, A), dtype=torch.int64)
+                cols.append(L.GrkStoreCol(L.STORE_ARRAY, c, A, 0, 0, None, t.data_ptr()))
             elif k in self.mm_ids:
-                rows = np.where(sel, self.mm[g, self.mm_ids.index(k)], 0)
-                out[k] = torch.from_numpy(self.mm_tables[k][rows])
+                tab = self.mm_tables[k]
+                if tab.dtype != np.float32 or not tab.flags['C_CONTIGUOUS']:
+                    raise L.GrkError(f'mm table {k} must be C-contiguous float32')
+                t = torch.empty((B, T, tab.shape[1]), dtype=torch.float32)
+                cols.append(L.GrkStoreCol(L.STORE_MM, self.mm_ids.index(k), tab.shape[1], 0, tab.shape[0],
+                                          tab.ctypes.data, t.data_ptr()))
             else:
-                out[k] = torch.from_numpy(np.ascontiguousarray(sparse[..., sp_col[k]]))
+                t = torch.empty((B, T), dtype=torch.int64)
+                cols.append(L.GrkStoreCol(L.STORE_SPARSE, sp_col[k], 1, 0, 0, None, t.data_ptr()))
+            out[k] = t
+        arr = (L.GrkStoreCol * max(1, len(cols)))(*cols)
+        L.check(L.lib().grk_store_features(C.byref(view), tok.ctypes.data, sl.ctypes.data, N, arr, len(cols)),
+                'grk_store_features')
         return out
+
+    def _view(self):
+        """grk_store_view over the memory-mapped token blocks.  Built per call, never
+        cached on the store: a cached struct's raw pointers would travel with a
+        pickled store into a spawned DataLoader worker and point into the parent."""
+        from . import _lib as L
+        for a in (self.sparse, self.arr, self.arr_len, self.mm):
+            if not a.flags['C_CONTIGUOUS'] or a.dtype != np.int32:
+                raise L.GrkError('SeqStore blocks must be C-contiguous int32')
+        return L.GrkStoreView(self.sparse.ctypes.data, self.arr.ctypes.data, self.arr_len.ctypes.data,
+                              self.mm.ctypes.data, len(self.tid), self.sparse.shape[1], self.arr.shape[1],
+                              self.arr.shape[2], self.mm.shape[1])
 
     def history_items(self, uids):
         """int32 [B, L]: each user's distinct item ids over the whole history,

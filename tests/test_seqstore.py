@@ -144,3 +144,60 @@ def test_store_timestamps_match_dataset(tmp_path, maxlen):
         assert np.array_equal(got[0][u].numpy()[T - len(body):], [t for t, _ in body])
     # the default batch keeps the reference's nine fields
     assert len(st.batch(uids[:4])) == 9 and len(MyDataset(tmp_path, SimpleNamespace(maxlen=maxlen))[0]) == 9
+
+
+def _store_view(sparse, arr, arr_len, mm):
+    from tencent_recommendation_2025_amd import _lib as L
+    return L.GrkStoreView(sparse.ctypes.data, arr.ctypes.data, arr_len.ctypes.data, mm.ctypes.data, len(sparse),
+                          sparse.shape[1], arr.shape[1], arr.shape[2], mm.shape[1])
+
+
+def test_store_features_entry_points_restated():
+    """grk_store_features / grk_store_array_widths (host code, include/grk.h) on a random
+    store against a numpy restatement: unselected positions take the defaults (id 0,
+    array [0] padded with 0, mm row 0), arrays are cut at each length and padded to the
+    requested width, widths are the selected tokens' longest arrays (>= 1); a selected
+    token or a stored mm row out of range is refused before anything is written."""
+    import ctypes as C
+    from tencent_recommendation_2025_amd import _lib as L
+    rng = np.random.default_rng(3)
+    n_tok, Fs, Fa, cap, Fm, mm_rows, W = 500, 5, 3, 6, 2, 40, 8
+    sparse = rng.integers(0, 1000, (n_tok, Fs)).astype(np.int32)
+    arr_len = rng.integers(1, cap + 1, (n_tok, Fa)).astype(np.int32)
+    arr = rng.integers(1, 99, (n_tok, Fa, cap)).astype(np.int32)     # values past each length must not leak
+    mm = rng.integers(0, mm_rows, (n_tok, Fm)).astype(np.int32)
+    tab = rng.standard_normal((mm_rows, W)).astype(np.float32)
+    tab[0] = 0
+    view = _store_view(sparse, arr, arr_len, mm)
+    n = 300
+    tok = rng.integers(0, n_tok, n).astype(np.int64)
+    sel = (rng.random(n) < 0.7).astype(np.uint8)
+    tok[sel == 0] = -5                                               # ignored where unselected
+    widths = np.zeros(Fa, np.int32)
+    lib = L.lib()
+    L.check(lib.grk_store_array_widths(C.byref(view), tok.ctypes.data, sel.ctypes.data, n, widths.ctypes.data), 'w')
+    on = sel.astype(bool)
+    assert widths.tolist() == [max(1, int(arr_len[tok[on], c].max())) for c in range(Fa)]
+    outs = [np.full(n, -1, np.int64), np.full((n, 4), -1, np.int64), np.full((n, W), -1, np.float32)]
+    cols = (L.GrkStoreCol * 3)(L.GrkStoreCol(L.STORE_SPARSE, 3, 1, 0, 0, None, outs[0].ctypes.data),
+                               L.GrkStoreCol(L.STORE_ARRAY, 1, 4, 0, 0, None, outs[1].ctypes.data),
+                               L.GrkStoreCol(L.STORE_MM, 1, W, 0, mm_rows, tab.ctypes.data, outs[2].ctypes.data))
+    L.check(lib.grk_store_features(C.byref(view), tok.ctypes.data, sel.ctypes.data, n, cols, 3), 'f')
+    t = np.where(on, tok, 0)
+    assert np.array_equal(outs[0], np.where(on, sparse[t, 3], 0))
+    keep = on[:, None] & (np.arange(4)[None, :] < arr_len[t, 1][:, None])
+    assert np.array_equal(outs[1], np.where(keep, arr[t, 1, :4], 0))
+    assert np.array_equal(outs[2], tab[np.where(on, mm[t, 1], 0)])
+    # refused inputs leave the outputs untouched
+    before = [o.copy() for o in outs]
+    bad = tok.copy()
+    bad[np.flatnonzero(on)[0]] = n_tok
+    assert lib.grk_store_features(C.byref(view), bad.ctypes.data, sel.ctypes.data, n, cols, 3) == L.GRK_EINVAL
+    assert b'outside the store' in lib.grk_last_error()
+    mm_bad = mm.copy()
+    mm_bad[tok[on][0], 1] = mm_rows
+    view_bad = _store_view(sparse, arr, arr_len, mm_bad)
+    assert lib.grk_store_features(C.byref(view_bad), tok.ctypes.data, sel.ctypes.data, n, cols, 3) == L.GRK_EINVAL
+    cols[1].width = cap + 1
+    assert lib.grk_store_features(C.byref(view), tok.ctypes.data, sel.ctypes.data, n, cols, 3) == L.GRK_EINVAL
+    assert all(np.array_equal(a, b) for a, b in zip(outs, before))
