@@ -401,6 +401,100 @@ class _GroupStackFn(torch.autograd.Function):
 _ANCHOR = torch.zeros((), requires_grad=True)  # makes _GroupStackFn's output part of the graph
 
 
+class _WeightBlocksFn(torch.autograd.Function):
+    """Column blocks of an itemdnn / userdnn weight ``W [d_out, nb * d]`` for the
+    projection restatement (model._projection / model._dnn_weight): ``singles``
+    are single blocks as views of W (W_0, direct-feature and mm blocks of the
+    composed dnn weight), ``stacks`` are [len(js), d_out, d] stacks of blocks
+    cast to the tables' dtype (the projections P_f = E_f W_f^T, one per
+    equal-row-count table group).
+
+    The backward writes every block's gradient into ONE buffer of W's shape --
+    zeros only for blocks no output reached.  Autograd of the slice / index
+    ops it replaces zero-fills a full-size tensor per slice and per group,
+    index_puts into it, adds those full-size tensors and casts the bf16 sum
+    back to fp32 (~18 launches and ~300 MB per step for C2's itemdnn).  Every
+    block gets its gradient from exactly one output, so the values are the
+    same bits (a sum with zeros is exact; bf16 -> fp32 is exact)."""
+
+    @staticmethod
+    def forward(ctx, W, d, singles, stacks):
+        ctx.set_materialize_grads(False)
+        ctx.d, ctx.singles, ctx.stacks = d, singles, stacks
+        ctx.shape, ctx.dtype, ctx.device = W.shape, W.dtype, W.device
+        Wv = W.detach().view(W.shape[0], -1, d)
+        outs = [Wv[:, j, :] for j in singles]
+        cast = {W.dtype: Wv}
+        for js, dt in stacks:
+            if dt not in cast:
+                cast[dt] = Wv.to(dt)           # the whole weight once per dtype, as before
+            src = cast[dt]
+            outs.append(src[:, js[0], :][None] if len(js) == 1 else
+                        src.index_select(1, _block_index(js, W.device)).permute(1, 0, 2))
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        d, (rows, cols) = ctx.d, ctx.shape
+        nb = cols // d
+        if all(g is None for g in grads):
+            return None, None, None, None
+        dW = torch.empty(ctx.shape, dtype=ctx.dtype, device=ctx.device)
+        dWv = dW.view(rows, nb, d)
+        covered = [False] * nb
+        for j, g in zip(ctx.singles, grads):
+            if g is not None:
+                dWv[:, j, :].copy_(g)
+                covered[j] = True
+        for (js, _), g in zip(ctx.stacks, grads[len(ctx.singles):]):
+            if g is None:
+                continue
+            if len(js) == 1:
+                dWv[:, js[0], :].copy_(g[0])
+            else:
+                dWv.index_copy_(1, _block_index(js, ctx.device), g.permute(1, 0, 2).to(ctx.dtype))
+            for j in js:
+                covered[j] = True
+        j = 0
+        while j < nb:                           # runs of blocks no output reached
+            if covered[j]:
+                j += 1
+                continue
+            e = j
+            while e < nb and not covered[e]:
+                e += 1
+            dWv[:, j:e, :].zero_()
+            j = e
+        return dW, None, None, None
+
+
+_BLOCK_INDEX = {}
+
+
+def _block_index(js, device):
+    """Cached device int64 index of block numbers (no host -> device copy per step)."""
+    key = (tuple(js), str(device))
+    t = _BLOCK_INDEX.get(key)
+    if t is None:
+        t = _BLOCK_INDEX[key] = torch.tensor(js, dtype=torch.int64).to(device)
+    return t
+
+
+def weight_blocks(W, d, singles=(), stacks=()):
+    """Views of single column blocks and dtype-cast stacks of blocks of ``W`` (see
+    _WeightBlocksFn): returns ``(singles..., stacks...)``; ``stacks`` is a sequence
+    of (block numbers, dtype)."""
+    singles = tuple(int(j) for j in singles)
+    stacks = tuple((tuple(int(j) for j in js), dt) for js, dt in stacks)
+    nb = W.shape[1] // d
+    if W.shape[1] != nb * d or any(not 0 <= j < nb for j in singles + sum((js for js, _ in stacks), ())):
+        raise ValueError(f'weight blocks: W {tuple(W.shape)} is not [.., nb * {d}] or a block is outside [0, {nb})')
+    seen = list(singles) + [j for js, _ in stacks for j in js]
+    if len(seen) != len(set(seen)):
+        raise ValueError('weight blocks: every block may appear in one output only')
+    return _WeightBlocksFn.apply(W, d, singles, stacks)
+
+
 @_disable
 def group_stack(group, offsets, rows):
     return _GroupStackFn.apply(_ANCHOR, group, tuple(offsets), rows)

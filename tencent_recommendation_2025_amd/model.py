@@ -374,39 +374,70 @@ class BaselineModel(torch.nn.Module):
         if self._fwd_id is not None and key in self._proj_cache:
             return self._proj_cache[key]
         d = self.hidden_units
-        feats, dnn = self._dnn_feats(which), (self.itemdnn if which == 'item' else self.userdnn)
-        direct = {k for k, _ in self._direct_feats(which)}
-        Wv = dnn.weight.view(d, -1, d)  # [d_out, block, d_in]
-        by_rows = {}
-        for j, k in enumerate(feats):  # block 0 is item_emb / user_emb
-            if k not in direct:
-                by_rows.setdefault(self.sparse_emb[k].num_embeddings, []).append((k, j + 1))
+        stacks = self._weight_pieces(which)[1]
         parts, offs, row = [], {}, 0
-        for rows, group in by_rows.items():
-            refs = {k: self._ref(f'sparse_emb.{k}') for k, _ in group}
+        for rows, group, refs in self._proj_groups(which):
             grp = next(iter(refs.values())).group
             if grp is not None and all(r.group is grp for r in refs.values()):
-                group = sorted(group, key=lambda kj: refs[kj[0]].row_offset)
                 E = G.group_stack(grp, [refs[k].row_offset for k, _ in group], rows)
             else:
                 E = torch.stack([refs[k].weight for k, _ in group])
-            # one indexing op for all blocks: its backward is one scatter into the weight gradient
-            js = self._const_index(tuple(j for _, j in group), Wv.device) if len(group) > 1 else group[0][1]
-            if Wv.dtype != E.dtype:  # cast the whole weight once, not each group's blocks (bit-identical)
-                Wv = Wv.to(E.dtype)
+            # the group's itemdnn / userdnn blocks [len(group), d_out, d_in] in E's dtype
+            # (functional.weight_blocks: one gradient buffer for the whole dnn weight)
+            Wb = stacks[tuple(j for _, j in group)]
             if d >= 1024 and _grk_gemm_ok(E):
                 # torch's batched bf16 GEMM faults at this width (d = 1024, C5): hipBLASLt
                 # returned HIPBLAS_STATUS_INTERNAL_ERROR for [3 x 10001 x 1024] x [1024 x 1024]
                 # and its rocBLAS fallback made an illegal access (DESIGN.md §5b).  One
                 # grk_gemm per block instead (plans validated at first use).
-                parts.append(torch.cat([G.linear(E[i], Wv[:, j, :]).to(E.dtype) for i, (_, j) in enumerate(group)]))
+                parts.append(torch.cat([G.linear(E[i], Wb[i]).to(E.dtype) for i in range(len(group))]))
             else:
-                Wb = Wv[:, js, :].permute(1, 0, 2) if len(group) > 1 else Wv[:, js, :][None]
                 parts.append(torch.bmm(E, Wb.transpose(1, 2)).to(E.dtype).reshape(-1, d))
             for k, _ in group:
                 offs[k] = row
                 row += rows
         res = (torch.cat(parts) if len(parts) > 1 else parts[0]), offs
+        if self._fwd_id is not None:
+            self._proj_cache[key] = res
+        return res
+
+    def _proj_groups(self, which):
+        """[(rows, [(feature, dnn block)], {feature: TableRef})] of the projected tables,
+        grouped by row count; a group's tables in group-buffer order when they share
+        a table group (so group_stack can view them without a copy)."""
+        direct = {k for k, _ in self._direct_feats(which)}
+        by_rows = {}
+        for j, k in enumerate(self._dnn_feats(which)):  # block 0 is item_emb / user_emb
+            if k not in direct:
+                by_rows.setdefault(self.sparse_emb[k].num_embeddings, []).append((k, j + 1))
+        out = []
+        for rows, group in by_rows.items():
+            refs = {k: self._ref(f'sparse_emb.{k}') for k, _ in group}
+            grp = next(iter(refs.values())).group
+            if grp is not None and all(r.group is grp for r in refs.values()):
+                group = sorted(group, key=lambda kj: refs[kj[0]].row_offset)
+            out.append((rows, group, refs))
+        return out
+
+    def _weight_pieces(self, which):
+        """The itemdnn / userdnn weight's column blocks this forward reads, from ONE
+        functional.weight_blocks call per forward and side: ({block: fp32 view} for
+        W_0, the direct-feature and the mm blocks, {block tuple: [G, d, d] stack in the
+        tables' dtype} for the projected groups)."""
+        key = ('wb', which, self._fwd_id)
+        if self._fwd_id is not None and key in self._proj_cache:
+            return self._proj_cache[key]
+        d = self.hidden_units
+        dnn = self.itemdnn if which == 'item' else self.userdnn
+        singles = [0] + [j for _, j in self._direct_feats(which)]
+        if which == 'item':
+            base = 1 + len(self.ITEM_SPARSE_FEAT) + len(self.ITEM_ARRAY_FEAT)
+            singles += [base + j for j in range(len(self.ITEM_EMB_FEAT))]
+        stacks = [(tuple(j for _, j in group), next(iter(refs.values())).weight.dtype)
+                  for _, group, refs in self._proj_groups(which)]
+        outs = G.weight_blocks(dnn.weight, d, singles, stacks)
+        res = ({j: o for j, o in zip(singles, outs)},
+               {js: o for (js, _), o in zip(stacks, outs[len(singles):])})
         if self._fwd_id is not None:
             self._proj_cache[key] = res
         return res
@@ -445,12 +476,13 @@ class BaselineModel(torch.nn.Module):
         operand [rows | direct feature rows | mm | 1 | pad]."""
         d = self.hidden_units
         dnn = self.itemdnn if which == 'item' else self.userdnn
-        W, cols, bias = dnn.weight, [dnn.weight[:, :d]], dnn.bias[:, None]
-        cols += [W[:, j * d:(j + 1) * d] for _, j in self._direct_feats(which)]
+        blk = self._weight_pieces(which)[0]
+        cols, bias = [blk[0]], dnn.bias[:, None]
+        cols += [blk[j] for _, j in self._direct_feats(which)]
         if which == 'item':
-            base = (1 + len(self.ITEM_SPARSE_FEAT) + len(self.ITEM_ARRAY_FEAT)) * d
+            base = 1 + len(self.ITEM_SPARSE_FEAT) + len(self.ITEM_ARRAY_FEAT)
             for j, k in enumerate(self.ITEM_EMB_FEAT):
-                Wk = W[:, base + j * d:base + (j + 1) * d]
+                Wk = blk[base + j]
                 et = self.emb_transform[k]
                 # one matrix-matrix product for [Wk Wt | Wk bt] (a matrix-vector product
                 # for Wk bt costs milliseconds of host time in its backward on ROCm)
