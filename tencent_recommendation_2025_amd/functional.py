@@ -480,6 +480,7 @@ def _block_index(js, device):
     return t
 
 
+@_disable
 def weight_blocks(W, d, singles=(), stacks=()):
     """Views of single column blocks and dtype-cast stacks of blocks of ``W`` (see
     _WeightBlocksFn): returns ``(singles..., stacks...)``; ``stacks`` is a sequence
