@@ -165,6 +165,19 @@ class SeqStore:
         self.item_sparse, self.item_ok, self.item_mm = ld('item_sparse'), ld('item_ok'), ld('item_mm')
         self.mm_tables = {fid: np.load(self.cache_dir / f'mm_table_{fid}.npy') for fid in self.mm_ids}
 
+    _MAPPED = ('off', 'tid', 'ttype', 'act', 'ts', 'sparse', 'arr', 'arr_len', 'mm', 'item_sparse', 'item_ok',
+               'item_mm', 'mm_tables')
+
+    def __getstate__(self):
+        """Pickled (DataLoader workers under spawn / forkserver) as the cache's path
+        only: np.memmap pickles its whole contents, which would copy the token
+        store into every worker; the worker maps the same files again."""
+        return {k: v for k, v in self.__dict__.items() if k not in self._MAPPED}
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        self._load()
+
     def __len__(self):
         return len(self.off) - 1
 

@@ -106,6 +106,29 @@ def test_store_batches_dataloader(tmp_path):
     assert not np.array_equal(first, sb.perm)
 
 
+def test_store_pickles_as_its_path(tmp_path):
+    """A SeqStore crosses into spawned DataLoader workers as its cache path (the
+    memory-mapped blocks are mapped again there, not copied into the pickle), and
+    the unpickled store assembles the same batches; a spawn-context loader too."""
+    import pickle
+    from tencent_recommendation_2025_amd.dataset import write_synthetic_tencentgr
+    from tencent_recommendation_2025_amd.seqstore import SeqStore, StoreBatches
+    write_synthetic_tencentgr(tmp_path, num_users=60, num_items=200, max_events=40, seed=8)
+    st = SeqStore(tmp_path, maxlen=15)
+    blob = pickle.dumps(st)
+    assert len(blob) < 4096 < st.sparse.nbytes + st.arr.nbytes
+    st2 = pickle.loads(blob)
+    uids = np.arange(0, 60, 3)
+    a, b = st.batch(uids), st2.batch(uids)
+    assert all(torch.equal(x, y) for x, y in zip(a[:6], b[:6]))
+    assert all(torch.equal(a[j][k], b[j][k]) for j in (6, 7) for k in a[j])
+    dl = torch.utils.data.DataLoader(StoreBatches(st, 20, seed=2), batch_size=None, num_workers=1,
+                                     multiprocessing_context='spawn')
+    for u, bb in dl:
+        ref = st.batch(u.numpy())
+        assert all(torch.equal(x, y) for x, y in zip(bb[:6], ref[:6]))
+
+
 @pytest.mark.parametrize('maxlen', [20, 60])
 def test_store_timestamps_match_dataset(tmp_path, maxlen):
     """Event times (the HSTU time-bias input; the reference loader reads and drops
