@@ -34,7 +34,7 @@ import torch
 
 from .dataset import ITEM_ARRAY, ITEM_SPARSE, MM_SHAPE, USER_ARRAY, USER_SPARSE, load_mm_emb
 
-CACHE_VERSION = 2   # 2: per-token event times (ts)
+CACHE_VERSION = 3   # 2: per-token event times (ts); 3: per-user distinct item histories
 
 
 class SeqStore:
@@ -146,8 +146,19 @@ class SeqStore:
                 if k in icol:
                     isp[i, icol[k]] = v
             imm[i] = [mm_row(i, fid) for fid in self.mm_ids]
+        # per-user distinct item ids, ascending (the exclusion sets of the negatives,
+        # DeviceNegatives / history_items), CSR over the users
+        tid_a, tt_a, off_a = np.asarray(tid, np.int32), np.asarray(ttype, np.int8), np.asarray(off, np.int64)
+        hist, hist_off = [], [0]
+        for u in range(len(off_a) - 1):
+            s_, e_ = off_a[u], off_a[u + 1]
+            h = np.unique(tid_a[s_:e_][tt_a[s_:e_] == 1])
+            h = h[h != 0]
+            hist.append(h)
+            hist_off.append(hist_off[-1] + len(h))
+        hist_items = np.concatenate(hist).astype(np.int32) if hist else np.zeros(0, np.int32)
         self.cache_dir.mkdir(parents=True, exist_ok=True)
-        arrays = dict(off=np.asarray(off, np.int64), tid=np.asarray(tid, np.int32), ttype=np.asarray(ttype, np.int8),
+        arrays = dict(hist_items=hist_items, hist_off=np.asarray(hist_off, np.int64),off=np.asarray(off, np.int64), tid=np.asarray(tid, np.int32), ttype=np.asarray(ttype, np.int8),
                       act=np.asarray(act, np.int32), ts=np.asarray(tss, np.int64), sparse=np.asarray(sparse, np.int32).reshape(n, -1), arr=arr,
                       arr_len=arr_len, mm=np.asarray(mmi, np.int32).reshape(n, -1), item_sparse=isp, item_ok=iok,
                       item_mm=imm)
@@ -163,10 +174,11 @@ class SeqStore:
         self.off, self.tid, self.ttype, self.act, self.ts = ld('off'), ld('tid'), ld('ttype'), ld('act'), ld('ts')
         self.sparse, self.arr, self.arr_len, self.mm = ld('sparse'), ld('arr'), ld('arr_len'), ld('mm')
         self.item_sparse, self.item_ok, self.item_mm = ld('item_sparse'), ld('item_ok'), ld('item_mm')
+        self.hist_items, self.hist_off = ld('hist_items'), ld('hist_off')
         self.mm_tables = {fid: np.load(self.cache_dir / f'mm_table_{fid}.npy') for fid in self.mm_ids}
 
     _MAPPED = ('off', 'tid', 'ttype', 'act', 'ts', 'sparse', 'arr', 'arr_len', 'mm', 'item_sparse', 'item_ok',
-               'item_mm', 'mm_tables')
+               'item_mm', 'mm_tables', 'hist_items', 'hist_off')
 
     def __getstate__(self):
         """Pickled (DataLoader workers under spawn / forkserver) as the cache's path
@@ -267,16 +279,16 @@ class SeqStore:
         """int32 [B, L]: each user's distinct item ids over the whole history,
         ascending, 0-padded (L = the largest distinct count in the batch) --
         _random_neq's exclusion set ts (model/BaseLine/dataset.py:136-139).  No
-        truncation: grk_sample_negatives takes exclusion lists of any length."""
+        truncation: grk_sample_negatives takes exclusion lists of any length.
+        One gather from the per-user lists the cache holds (no per-user work)."""
         uids = np.asarray(uids, np.int64)
-        start, end = self.off[uids], self.off[uids + 1]
-        sets = [np.unique(self.tid[s:e][self.ttype[s:e] == 1]) for s, e in zip(start, end)]
-        sets = [u[u != 0] for u in sets]
-        L = max(1, max((len(u) for u in sets), default=1))
-        out = np.zeros((len(uids), L), np.int32)
-        for b, ids in enumerate(sets):
-            out[b, :len(ids)] = ids
-        return torch.from_numpy(out)
+        start, n = self.hist_off[uids], self.hist_off[uids + 1] - self.hist_off[uids]
+        L = max(1, int(n.max()) if len(n) else 1)
+        col = np.arange(L)[None, :]
+        keep = col < n[:, None]
+        src = np.where(keep, start[:, None] + col, 0)
+        out = np.where(keep, self.hist_items[src] if len(self.hist_items) else 0, 0).astype(np.int32)
+        return torch.from_numpy(np.ascontiguousarray(out))
 
 
 class DeviceNegatives:

@@ -72,11 +72,16 @@ def test_store_cache_reused_and_history(tmp_path):
     st2 = SeqStore(tmp_path, maxlen=25)                 # another window over the same cache
     assert (tmp_path / 'grk_seqstore' / 'tid.npy').stat().st_mtime_ns == stamp and len(st2) == 30
     ds = MyDataset(tmp_path, SimpleNamespace(maxlen=10, mm_emb_id=['81']))
-    hist = st.history_items(np.arange(30)).numpy()
-    for u in range(30):
-        recs = ds._load_user_data(u)
-        items = {i for _, i, _, f, _, _ in recs if i and f}
-        assert set(hist[u][hist[u] != 0].tolist()) == items
+    uids = np.r_[np.arange(30), [7, 7, 0]]               # repeated users are fine
+    hist = st.history_items(uids).numpy()
+    width = 0
+    for r, u in enumerate(uids):
+        recs = ds._load_user_data(int(u))
+        items = sorted({i for _, i, _, f, _, _ in recs if i and f})
+        width = max(width, len(items))
+        # ascending distinct ids, then zero padding
+        assert hist[r][:len(items)].tolist() == items and not hist[r][len(items):].any()
+    assert hist.shape == (len(uids), max(1, width)) and hist.dtype == np.int32
     # negatives' feature table = fill_missing_feat(item_feat_dict[str(i)])
     for i in (1, 17, 99):
         d = ds.item_feat_dict[str(i)]
