@@ -71,6 +71,9 @@ def parse():
     ap.add_argument('--merge-proj', type=int, default=0,
                     help='1: the projected feature tables\' row gradients of the seq-side and pair lookups in one '
                          'grk_embedding_backward call (functional.DenseMerge; opt-in until verified on hardware)')
+    ap.add_argument('--dense-flat', type=int, default=0,
+                    help='1: the dense parameters as one flat buffer on grk\'s multi-range AdamW instead of torch\'s '
+                         'fused AdamW (optim.DenseFlat; opt-in until verified on hardware)')
     ap.add_argument('--sharded-jagged', type=int, default=0,
                     help='1: the row-sharded trainer on jagged rows too (train.jagged_remaps; opt-in until verified '
                          'on hardware -- the sharded step runs the padded layout by default)')
@@ -647,7 +650,7 @@ def main():
         from tencent_recommendation_2025_amd.sharding import ShardedFusedAdamW
         opt = ShardedFusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
     else:
-        opt = FusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode)
+        opt = FusedAdamW(model, lr=1e-3, weight_decay=0.01, table_mode=a.table_mode, dense_flat=bool(a.dense_flat))
     # the jagged layout runs on the whole-sequence attention kernels (T <= 256 at hd <= 128, not fp8)
     jagged = (bool(a.jagged) and (not sharded or bool(a.sharded_jagged)) and not a.fp8 and a.maxlen + 1 <= 256
               and a.hidden // a.heads <= 128)
@@ -740,7 +743,8 @@ def main():
                                    f'dropout={a.dropout}'
                                    + (f', rab_time buckets={a.time_buckets}' if a.time_buckets else '')
                                    + (', fp8 (e4m3) q/k/v attention' if a.fp8 else '')
-                                   + (', merged projected-row backward' if a.merge_proj else ''),
+                                   + (', merged projected-row backward' if a.merge_proj else '')
+                                   + (', flat dense AdamW' if a.dense_flat else ''),
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch, 'seq_len': a.maxlen + 1,
                        'parallelism': f'dp{world}' + ('+rowshard' if sharded else '') + ('(shard-built tables)' if shard_tables else ''),
                        'step_launch': 'hip-graph replay' if trainer.graph else 'eager',

@@ -54,9 +54,16 @@ case "${1:-tests}" in
     step time_bias 400 env GRK_CHUNKED_TIME_TESTS=1 $PYT tests/test_gpu_attention.py -k time_bias
     step wide_fidelity 400 env GRK_WIDE_FIDELITY_TESTS=1 $PYT tests/test_gpu_attention.py tests/test_gpu_model.py \
       -k wide_fidelity
+    step dense_flat 300 env GRK_DENSE_FLAT_TESTS=1 $PYT tests/test_gpu_dense_flat.py
     timeout -k 10 200 python -u bench.py --steps 30 --warmup 10 --cpu-baseline 0 --roofline-reps 5 --merge-proj 1 \
       > $O/bench_merge_proj.json 2> $O/bench_merge_proj.err
     echo "bench_merge_proj rc=$?" >> $O/summary.txt
+    timeout -k 10 200 python -u bench.py --steps 30 --warmup 10 --cpu-baseline 0 --roofline-reps 5 --dense-flat 1 \
+      > $O/bench_dense_flat.json 2> $O/bench_dense_flat.err
+    echo "bench_dense_flat rc=$?" >> $O/summary.txt
+    timeout -k 10 200 python -u bench.py --steps 30 --warmup 10 --cpu-baseline 0 --roofline-reps 5 \
+      > $O/bench_default.json 2> $O/bench_default.err
+    echo "bench_default rc=$?" >> $O/summary.txt
     ;;
   variants)
     # the variants' parity (the tests restate the chunk order from the library), then

@@ -128,11 +128,86 @@ class TableGroup:
 DEFAULT_GROUPS = (('item', ('item_emb',)), ('user', ('user_emb',)), ('pos', ('pos_emb',)), ('small', None))
 
 
+DENSE_FLAT_DIM = 8   # the flat buffer as [rows, 8] for k_adamw_ranges (16-byte fp32 pairs per lane)
+
+
+def flat_layout(numels, dim=DENSE_FLAT_DIM):
+    """Row offsets of tensors of the given sizes (each a multiple of dim) packed back
+    to back in a [rows, dim] buffer: ([row_start...], total rows)."""
+    starts, row = [], 0
+    for n in numels:
+        if n % dim:
+            raise ValueError(f'a flat tensor holds a multiple of {dim} elements, not {n}')
+        starts.append(row)
+        row += n // dim
+    return starts, row
+
+
+def grad_runs(starts, ends, has_grad):
+    """Maximal runs [(row_lo, row_hi, [indices])] of consecutive tensors that all have a
+    gradient: torch's AdamW skips a parameter without one, so the multi-range update
+    (which moves every row of its buffer) is launched per run, never over a gap."""
+    runs, cur = [], None
+    for i, ok in enumerate(has_grad):
+        if not ok:
+            cur = None
+            continue
+        if cur is None or cur[1] != starts[i]:
+            cur = [starts[i], ends[i], []]
+            runs.append(cur)
+        cur[1] = ends[i]
+        cur[2].append(i)
+    return [tuple(r) for r in runs]
+
+
+class DenseFlat:
+    """fp32 dense parameters as views of one [rows, 8] buffer with flat AdamW moments,
+    stepped by grk_table_adamw_ranges_dev (each parameter's gradient one range)."""
+
+    def __init__(self, params, device):
+        self.params = list(params)
+        self.starts, rows = flat_layout([p.numel() for p in self.params])
+        self.ends = [s + p.numel() // DENSE_FLAT_DIM for s, p in zip(self.starts, self.params)]
+        self.buf = torch.empty(rows, DENSE_FLAT_DIM, dtype=torch.float32, device=device)
+        for p, s, e in zip(self.params, self.starts, self.ends):
+            view = self.buf[s:e].view(p.shape)
+            with torch.no_grad():
+                view.copy_(p.detach())
+            p.data = view            # the Parameter object (and the model's references) stays
+        self.exp_avg = torch.zeros_like(self.buf)
+        self.exp_avg_sq = torch.zeros_like(self.buf)
+
+    def zero_grad(self, set_to_none=True):
+        for p in self.params:
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                p.grad.zero_()
+
+    def step(self, clock):
+        grads = [p.grad for p in self.params]
+        for lo, hi, idx in grad_runs(self.starts, self.ends, [g is not None for g in grads]):
+            ranges = []
+            for i in idx:
+                g = grads[i]
+                if g.dtype not in (torch.float32, torch.bfloat16):
+                    g = g.float()
+                ranges.append((self.starts[i] - lo, g.contiguous().view(-1, DENSE_FLAT_DIM)))
+            K.table_adamw_ranges(self.buf[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi], clock, ranges)
+
+    def state(self, p):
+        """{'exp_avg', 'exp_avg_sq'} views of parameter p (torch AdamW's state names)."""
+        i = next(i for i, q in enumerate(self.params) if q is p)
+        s, e = self.starts[i], self.ends[i]
+        return {'exp_avg': self.exp_avg[s:e].view(p.shape), 'exp_avg_sq': self.exp_avg_sq[s:e].view(p.shape)}
+
+
 class FusedAdamW:
     """AdamW over a BaselineModel: table groups on grk kernels, dense params on torch fused AdamW."""
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
-                 table_dtype=torch.bfloat16, groups=DEFAULT_GROUPS, defer_period=16, l2_emb=0.0, parallel=False):
+                 table_dtype=torch.bfloat16, groups=DEFAULT_GROUPS, defer_period=16, l2_emb=0.0, parallel=False,
+                 dense_flat=False):
         """l2_emb > 0: the BaseLine script's ``loss += l2_emb * ||item_emb.weight||_F``
         (model/BaseLine/main.py:184-185) -- ``l2_term()`` gives the loss term (Trainer
         adds it), ``step()`` adds its gradient l2 * W / ||W|| to every item row.  Every
@@ -164,10 +239,16 @@ class FusedAdamW:
         model._table_refs = refs
         dense = [p for p in model.parameters() if p.requires_grad]
         cuda = dev.type == 'cuda'
+        self._flat = None
+        if dense_flat and cuda:
+            flat_ps = [p for p in dense if p.dtype == torch.float32 and p.numel() % DENSE_FLAT_DIM == 0]
+            if flat_ps:
+                self._flat = DenseFlat(flat_ps, dev)
+                dense = [p for p in dense if all(p is not q for q in flat_ps)]
         # capturable: the dense AdamW keeps its step count on the device, so the
         # whole training step can be captured in a HIP graph (train.Trainer)
         self.dense = torch.optim.AdamW(dense, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
-                                       fused=cuda, capturable=cuda)
+                                       fused=cuda, capturable=cuda) if dense else None
         self.t = 0
         # Deferred dense parity for the big item/user tables: a row outside the
         # step's batch takes a g = 0 update that depends on nothing but (p, m, v)
@@ -289,7 +370,10 @@ class FusedAdamW:
                 K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock)
 
     def zero_grad(self, set_to_none=True):
-        self.dense.zero_grad(set_to_none=set_to_none)
+        if self.dense is not None:
+            self.dense.zero_grad(set_to_none=set_to_none)
+        if self._flat is not None:
+            self._flat.zero_grad(set_to_none)
         for g in self.groups:
             g.clear()
 
@@ -309,13 +393,22 @@ class FusedAdamW:
         # the dense AdamW and every table group's reduction + update are independent
         # chains of (mostly small) kernels: on the GPU they run as parallel branches
         # (private streams forked from and joined into the step's stream)
-        work = [self.dense.step] + [self._group_work(g, hp, begun) for g in self.groups]
+        work = [self._dense_step(hp)] + [self._group_work(g, hp, begun) for g in self.groups]
         dev = self.groups[0].flat.device if self.groups else torch.device('cpu')
         if self.parallel and self.clock is not None:
             run_branches(work, dev)
         else:
             for f in work:
                 f()
+
+    def _dense_step(self, hp):
+        """The dense parameters' update this step, as a closure (run_branches)."""
+        def work():
+            if self.dense is not None:
+                self.dense.step()
+            if self._flat is not None:
+                self._flat.step(hp)
+        return work
 
     def _group_work(self, g, hp, begun):
         """The update of one table group this step, as a closure (run_branches)."""

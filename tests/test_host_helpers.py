@@ -71,3 +71,20 @@ def test_device_clock_advances_on_its_device():
     clk.advance()
     clk.advance()
     assert int(clk.t.item()) == 2
+
+
+def test_dense_flat_layout_and_grad_runs():
+    """optim.DenseFlat's host logic: parameters packed back to back as [rows, 8]
+    (sizes multiples of 8, refused otherwise), and the multi-range update launched
+    per maximal run of consecutive parameters that all have a gradient (torch's
+    AdamW skips a parameter without one; k_adamw_ranges moves every row it covers)."""
+    from tencent_recommendation_2025_amd.optim import flat_layout, grad_runs
+    starts, rows = flat_layout([16, 8, 64, 24])
+    assert starts == [0, 2, 3, 11] and rows == 14
+    with pytest.raises(ValueError):
+        flat_layout([16, 12])
+    ends = [2, 3, 11, 14]
+    assert grad_runs(starts, ends, [True] * 4) == [(0, 14, [0, 1, 2, 3])]
+    assert grad_runs(starts, ends, [True, False, True, True]) == [(0, 2, [0]), (3, 14, [2, 3])]
+    assert grad_runs(starts, ends, [False, False, False, False]) == []
+    assert grad_runs(starts, ends, [False, True, True, False]) == [(2, 11, [1, 2])]
