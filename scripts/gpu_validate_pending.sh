@@ -9,6 +9,7 @@
 #   bash scripts/build_variant.sh pipe32 grk_embedding "-DGRK_WAVE_PIPE=32"
 #   bash scripts/build_variant.sh tbsplit grk_attention_seq "-DGRK_ATTN_TB_SPLIT=1"
 #   bash scripts/build_variant.sh foldtb grk_attention_seq "-DGRK_ATTN_FOLD_INVN=1 -DGRK_ATTN_TB_SPLIT=1"
+#   mkdir -p mbbin && hipcc --offload-arch=gfx950 -O3 -o mbbin/mfma_scale_probe scripts/microbench/mfma_scale_probe.hip
 # then one gpurun call per stage, least risky first:
 #   gpurun --timeout 900 -- bash scripts/gpu_validate_pending.sh tests
 #   gpurun --timeout 900 -- bash scripts/gpu_validate_pending.sh variants
@@ -94,6 +95,8 @@ case "${1:-tests}" in
     # last: the d = 1024 model step faulted inside torch's batched GEMM in round 3.
     # First the projection shape alone on the path the model now takes (grk_gemm per
     # block), in its own process; the model tests only if it is right.
+    # the block-scaled fp8 MFMA's operand and scale maps (one wave), for the C5 kernels
+    [ -x mbbin/mfma_scale_probe ] && step mfma_scale_probe 60 mbbin/mfma_scale_probe
     step c5_grk_gemm 120 python -u scripts/diag/c5_gemm_isolate.py grk
     grep -q "grk: normwise .* ok" $O/c5_grk_gemm.log || { echo "c5: projection GEMM not ok -- stopping" >> $O/summary.txt; exit 4; }
     step c5 400 env GRK_C5_MODEL_TESTS=1 $PYT tests/test_gpu_fp8.py
