@@ -113,8 +113,7 @@ class _FeatureLookupFn(torch.autograd.Function):
             K.embedding_gather(lookups[i:i + L.MAX_FEATURES], out, num_tokens, token_type, seq_len)
         if GATHER_TRACE is not None:
             GATHER_TRACE.append((lookups, out, num_tokens, token_type, seq_len))
-        for col, x in extras:
-            out[:, col:col + x.shape[1]] = x.to(dt)
+        write_extras(out, extras)
         ctx.specs, ctx.token_type, ctx.seq_len, ctx.splits = specs, token_type, seq_len, splits
         ctx.n_weights = len(weights)
         ctx.weight_ids = [id(w) for w in weights]
@@ -212,8 +211,8 @@ def _merged_grads(ctx, dense):
 def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extras=(), splits=None):
     """Fused multi-table gather (+ bag sums) into one [num_tokens, out_ld] buffer.
 
-    ``extras``: (column, [num_tokens, w] tensor) blocks copied into the buffer
-    (dense features, constants; treated as non-differentiable).  Returns the
+    ``extras``: (column, [num_tokens, w] or broadcast [1, w] tensor) blocks copied
+    into the buffer (dense features, constants; treated as non-differentiable).  Returns the
     buffer's column blocks ``splits`` (list of (start, end); default: the whole
     buffer, returned as a single tensor).  Drop-in tables get dense gradients
     through autograd; grouped tables push row-sparse gradient sources into
@@ -242,9 +241,17 @@ def _lookup_op(specs, token_type, seq_len, num_tokens, out_ld, extras, splits):
     out = torch.ops.grk.feature_lookup(tables, [s.idx for s in specs], table_of, [int(s.out_col) for s in specs],
                                        [int(s.mode) for s in specs], [int(s.bag) for s in specs], token_type,
                                        int(seq_len), int(num_tokens), int(out_ld))
-    for col, x in extras:  # dense inputs (features, constants): no gradient is propagated to them
-        out[:, col:col + x.shape[1]] = x.detach().to(out.dtype)
+    write_extras(out, extras)
     return tuple(out[:, a:b] for a, b in splits)
+
+
+def write_extras(out, extras):
+    """Dense blocks into the gather buffer: (column, [num_tokens, w] tensor, or a [1, w]
+    row broadcast over every token -- e.g. the dnn operand's constant [1, 0, ...] bias /
+    padding columns).  One copy kernel per block, the dtype converted inside it (the
+    same rounding as a .to() before the copy).  Dense inputs: no gradient propagates."""
+    for col, x in extras:
+        out[:, col:col + x.shape[1]].copy_(x.detach())
 
 
 @_disable

@@ -58,7 +58,7 @@ def capacity_for(n, quantum=1024, limit=None):
 
 def layout(token_type, capacity, next_token_type=None):
     """The jagged layout of a batch with token_type [B, T] (0 = padding) in `capacity` rows."""
-    kv = (token_type != 0).to(torch.uint8).contiguous()
+    kv = (token_type != 0).contiguous().view(torch.uint8)   # bool bytes are 0 / 1: no cast kernel
     B, T = kv.shape
     err = torch.zeros(1, dtype=torch.int32, device=kv.device)
     ranges, row_base, row_map, n = K.jagged_layout(kv, capacity, next_token_type, err)
@@ -69,6 +69,18 @@ def _as_rows(t, N):
     """A [B, T, ...] tensor viewed as [B*T, ...] contiguous rows."""
     t = t if t.is_contiguous() else t.contiguous()
     return t.reshape(N, *t.shape[2:])
+
+
+_POSITIONS = {}
+
+
+def _positions(T, device):
+    """Cached int64 [1, T] = 1 .. T on the device."""
+    key = (int(T), str(device))
+    t = _POSITIONS.get(key)
+    if t is None:
+        t = _POSITIONS[key] = torch.arange(1, T + 1, dtype=torch.int64).unsqueeze(0).to(device)
+    return t
 
 
 def compact(batch, jag, with_positions=True):
@@ -98,7 +110,7 @@ def compact(batch, jag, with_positions=True):
     out.append(batch[9] if len(batch) > 9 else None)
     if with_positions:
         seq = batch[0]
-        pidx = (torch.arange(1, T + 1, device=seq.device).unsqueeze(0) * (seq != 0)).to(torch.int64)
+        pidx = torch.where(seq != 0, _positions(T, seq.device), 0)
         out.append(take(pidx))
     K.gather_rows(pairs, jag.row_map)
     return tuple(out)

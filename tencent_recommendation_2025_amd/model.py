@@ -101,6 +101,21 @@ def key_valid_from_mask(attn_mask, B, T):
     return kv.to(torch.uint8).contiguous()
 
 
+_UNIT_ROWS = {}
+
+
+def _unit_row(w, device):
+    """Cached fp32 [1, w] = [1, 0, ..., 0] on the device: the dnn operand's bias column and
+    its padding, broadcast over the tokens by functional.write_extras."""
+    key = (int(w), str(device))
+    t = _UNIT_ROWS.get(key)
+    if t is None:
+        t = torch.zeros(1, w)
+        t[0, 0] = 1.0
+        t = _UNIT_ROWS[key] = t.to(device)
+    return t
+
+
 def _grk_gemm_ok(x):
     """Dense layers run on grk_gemm (hipBLASLt, stream-K eligible) under bf16
     autocast on the GPU -- the training regime of the reference and the
@@ -508,12 +523,13 @@ class BaselineModel(torch.nn.Module):
         tt = mask.to(dev, non_blocking=True) if mask is not None else None
         specs, extras, splits = [], [], []
         col = 0
-        ones = None
 
         def operand(ref, mode, dense, which):
             """gather block [rows | direct feature rows | dense | 1 | pad] feeding one
-            dnn GEMM; returns its split."""
-            nonlocal col, ones
+            dnn GEMM; returns its split.  The dense features are copied into the gather
+            buffer as they are, the constant [1 | 0 ...] columns as one broadcast row
+            (no ones / cat / pad tensors per step)."""
+            nonlocal col
             start = col
             specs.append(G.LookupSpec(ref, seq, col, mode))
             col += d
@@ -523,12 +539,12 @@ class BaselineModel(torch.nn.Module):
                 specs.append(G.LookupSpec(self._ref(f'sparse_emb.{k}'), idx if bag > 1 else idx.reshape(N), col,
                                           L.IDX_PLAIN, bag))
                 col += d
-            if ones is None:
-                ones = torch.ones(N, 1, device=dev)
-            x = torch.cat(dense + [ones], 1) if dense else ones
-            pad = (-x.shape[1]) % 8
-            extras.append((col, F.pad(x, (0, pad)) if pad else x))
-            col += x.shape[1] + pad
+            for x in dense:
+                extras.append((col, x))
+                col += x.shape[1]
+            w = 1 + (-(sum(x.shape[1] for x in dense) + 1)) % 8     # the 1 column + padding to a multiple of 8
+            extras.append((col, _unit_row(w, dev)))
+            col += w
             splits.append((start, col))
             return col - start
 
@@ -651,7 +667,7 @@ class BaselineModel(torch.nn.Module):
         if jagged is not None:
             kw = dict(key_valid=jagged.key_valid, seq_range=jagged.seq_range, row_base=jagged.row_base)
         else:
-            key_valid = (mask.to(dev, non_blocking=True) != 0).to(torch.uint8).contiguous()
+            key_valid = (mask.to(dev, non_blocking=True) != 0).contiguous().view(torch.uint8)   # bool bytes are 0 / 1
             kw = dict(key_valid=key_valid, seq_range=torch.ops.grk.seq_ranges(key_valid))  # one launch serves every layer
         if timestamps is not None and self.block == 'hstu':
             kw['timestamps'] = timestamps.to(dev, torch.int64, non_blocking=True).contiguous()

@@ -88,3 +88,48 @@ def test_dense_flat_layout_and_grad_runs():
     assert grad_runs(starts, ends, [True, False, True, True]) == [(0, 2, [0]), (3, 14, [2, 3])]
     assert grad_runs(starts, ends, [False, False, False, False]) == []
     assert grad_runs(starts, ends, [False, True, True, False]) == [(2, 11, [1, 2])]
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('m', [0, 32, 7])
+def test_operand_extras_equal_the_cat_pad_form(dt, m):
+    """The dnn operand's dense columns (model._embed.operand): the mm features copied as
+    they are plus one broadcast [1, 0, ...] row (functional.write_extras) write the same
+    bytes as the round-3 form -- cat(mm, ones), zero-padded to a multiple of 8, cast,
+    copied -- for fp32 and bf16 gather buffers."""
+    import torch.nn.functional as F
+    from tencent_recommendation_2025_amd import functional as G
+    from tencent_recommendation_2025_amd.model import _unit_row
+    N, col = 37, 16
+    g = torch.Generator().manual_seed(m)
+    dense = [torch.randn(N, m, generator=g) * 3] if m else []
+    old = torch.full((N, 64), 7.0, dtype=dt)
+    x = torch.cat(dense + [torch.ones(N, 1)], 1)
+    pad = (-x.shape[1]) % 8
+    x = F.pad(x, (0, pad)) if pad else x
+    old[:, col:col + x.shape[1]] = x.to(dt)
+    new = torch.full((N, 64), 7.0, dtype=dt)
+    extras, c = [], col
+    for t in dense:
+        extras.append((c, t))
+        c += t.shape[1]
+    w = 1 + (-(sum(t.shape[1] for t in dense) + 1)) % 8
+    extras.append((c, _unit_row(w, 'cpu')))
+    c += w
+    G.write_extras(new, extras)
+    assert c - col == x.shape[1]
+    assert torch.equal(old.view(torch.int16 if dt == torch.bfloat16 else torch.int32),
+                       new.view(torch.int16 if dt == torch.bfloat16 else torch.int32))
+
+
+def test_key_valid_bytes_and_jagged_positions():
+    """bool -> uint8 by view (no cast kernel) and the cached position index equal the
+    casting forms: key_valid bytes 0 / 1, pidx = (t + 1) where the token is valid."""
+    from tencent_recommendation_2025_amd.jagged import _positions
+    g = torch.Generator().manual_seed(1)
+    tt = torch.randint(0, 3, (5, 11), generator=g, dtype=torch.int32)
+    assert torch.equal((tt != 0).contiguous().view(torch.uint8), (tt != 0).to(torch.uint8))
+    seq = torch.randint(0, 4, (5, 11), generator=g)
+    want = (torch.arange(1, 12).unsqueeze(0) * (seq != 0)).to(torch.int64)
+    got = torch.where(seq != 0, _positions(11, 'cpu'), 0)
+    assert got.dtype == torch.int64 and torch.equal(got, want)
