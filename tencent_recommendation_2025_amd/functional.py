@@ -487,6 +487,23 @@ def _block_index(js, device):
     return t
 
 
+def weight_blocks_sliced(W, d, singles, stacks):
+    """weight_blocks' outputs as plain slice / index ops (autograd zero-fills a full-size
+    gradient per slice and per stack): the form torch.compile traces, so a compiled
+    model keeps one graph through the projections (weight_blocks itself is an explicit
+    graph break)."""
+    Wv = W.view(W.shape[0], -1, d)
+    outs = [Wv[:, j, :] for j in singles]
+    cast = {W.dtype: Wv}
+    for js, dt in stacks:
+        if dt not in cast:
+            cast[dt] = Wv.to(dt)
+        src = cast[dt]
+        outs.append(src[:, js[0], :][None] if len(js) == 1 else
+                    src.index_select(1, _block_index(js, W.device)).permute(1, 0, 2))
+    return tuple(outs)
+
+
 @_disable
 def weight_blocks(W, d, singles=(), stacks=()):
     """Views of single column blocks and dtype-cast stacks of blocks of ``W`` (see

@@ -450,7 +450,10 @@ class BaselineModel(torch.nn.Module):
             singles += [base + j for j in range(len(self.ITEM_EMB_FEAT))]
         stacks = [(tuple(j for _, j in group), next(iter(refs.values())).weight.dtype)
                   for _, group, refs in self._proj_groups(which)]
-        outs = G.weight_blocks(dnn.weight, d, singles, stacks)
+        if torch.compiler.is_compiling():      # traced: the slice form (weight_blocks is a graph break)
+            outs = G.weight_blocks_sliced(dnn.weight, d, singles, stacks)
+        else:
+            outs = G.weight_blocks(dnn.weight, d, singles, stacks)
         res = ({j: o for j, o in zip(singles, outs)},
                {js: o for (js, _), o in zip(stacks, outs[len(singles):])})
         if self._fwd_id is not None:

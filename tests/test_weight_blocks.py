@@ -71,7 +71,8 @@ def test_weight_blocks_bitwise_equal_to_the_slice_chain(case):
     for o in old_chain(W0, d, singles, stacks):
         outs_g.append(torch.randn(o.shape, generator=g).to(o.dtype))
     grads = {}
-    for name, fn in (('old', old_chain), ('new', lambda *a: G.weight_blocks(*a))):
+    for name, fn in (('old', old_chain), ('new', lambda *a: G.weight_blocks(*a)),
+                     ('sliced', lambda *a: G.weight_blocks_sliced(*a))):
         W = W0.clone().requires_grad_(True)
         outs = fn(W, d, singles, stacks)
         ref = old_chain(W0, d, singles, stacks)
@@ -85,6 +86,7 @@ def test_weight_blocks_bitwise_equal_to_the_slice_chain(case):
             torch.autograd.backward([o for o, _ in used], [gr for _, gr in used])
         grads[name] = (W.grad.clone(), counter.ops)
     assert torch.equal(grads['old'][0], grads['new'][0])
+    assert torch.equal(grads['old'][0], grads['sliced'][0])       # the form torch.compile traces
     old_k, new_k = kernels(grads['old'][1]), kernels(grads['new'][1])
     # the replaced chain zero-fills one full-size tensor per slice / group and adds them
     assert new_k < old_k, (grads['old'][1], grads['new'][1])
