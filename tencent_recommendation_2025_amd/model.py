@@ -653,7 +653,10 @@ class BaselineModel(torch.nn.Module):
                 if a is not None and b is not None and a[0] is b[0]:
                     self._remaps[(name, 'pair', L.IDX_PLAIN)] = (a[0], torch.cat([a[1], b[1]], 0))
         x = self._embed(seq2, feats, role='pair')[0]
-        return x[:B], x[B:]
+        # split, not x[:B] / x[B:]: its backward is one cat of the two gradients, where two
+        # slices' backwards zero-fill a full-size gradient each and add them (same values)
+        pe, ne = x.split(B, 0)
+        return pe, ne
 
     # -------------------------------------------------- model/BaseLine/model.py:312-350
     def log2feats(self, log_seqs, mask, seq_feature, timestamps=None, jagged=None, pos_idx=None):

@@ -133,3 +133,35 @@ def test_key_valid_bytes_and_jagged_positions():
     want = (torch.arange(1, 12).unsqueeze(0) * (seq != 0)).to(torch.int64)
     got = torch.where(seq != 0, _positions(11, 'cpu'), 0)
     assert got.dtype == torch.int64 and torch.equal(got, want)
+
+
+def test_pair_split_backward_equals_slices():
+    """feat2emb_pair returns x.split(B) (backward: one cat of the two gradients) where it
+    returned x[:B], x[B:] (backward: a zero-filled full-size gradient per slice, added):
+    same views forward, same gradient bits, fewer kernels."""
+    import collections
+    from torch.utils._python_dispatch import TorchDispatchMode
+
+    class Ops(TorchDispatchMode):
+        def __init__(self):
+            super().__init__()
+            self.n = collections.Counter()
+
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            self.n[str(func.overloadpacket)] += 1
+            return func(*args, **(kwargs or {}))
+
+    g = torch.Generator().manual_seed(2)
+    x0 = torch.randn(2, 7, 16, generator=g).bfloat16()
+    ga, gb = torch.randn(1, 7, 16, generator=g).bfloat16(), torch.randn(1, 7, 16, generator=g).bfloat16()
+    res = []
+    for form in ('slices', 'split'):
+        x = x0.clone().requires_grad_(True)
+        y = x * 1                                     # a non-leaf, as the dnn output is
+        a, b = (y[:1], y[1:]) if form == 'slices' else y.split(1, 0)
+        ops = Ops()
+        with ops:
+            torch.autograd.backward([a, b], [ga, gb])
+        res.append((x.grad.clone(), ops.n))
+    assert torch.equal(res[0][0], res[1][0])
+    assert 'aten.slice_backward' in res[0][1] and 'aten.slice_backward' not in res[1][1]
