@@ -192,7 +192,10 @@ class DenseFlat:
                 g = grads[i]
                 if g.dtype not in (torch.float32, torch.bfloat16):
                     g = g.float()
-                ranges.append((self.starts[i] - lo, g.contiguous().view(-1, DENSE_FLAT_DIM)))
+                g = g.contiguous()
+                if g.data_ptr() % 16:          # the kernel reads fp32 gradients as 16-byte vectors
+                    g = g.clone()
+                ranges.append((self.starts[i] - lo, g.view(-1, DENSE_FLAT_DIM)))
             K.table_adamw_ranges(self.buf[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi], clock, ranges)
 
     def state(self, p):
