@@ -460,6 +460,16 @@ def wgrad_roofline(a, reps, k):
     return res
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """One stderr line per phase (stdout keeps the single JSON line): a run whose
+    phases take minutes in total -- model build, capture, rooflines, the CPU
+    baseline -- always shows it is alive."""
+    print(f'# bench {time.perf_counter() - _T0:7.1f} s: {msg}', file=sys.stderr, flush=True)
+
+
 def cpu_baseline(a, stats, types):
     """fp32 torch-CPU restatement (oracle/model_ref.py) of the same model + step, bounded sample."""
     from oracle import model_ref
@@ -500,11 +510,13 @@ def cpu_baseline(a, stats, types):
         opt.step()
 
     step(batches[0])
+    progress(f'cpu baseline: warm-up step done ({cores} threads)')
     times = []
-    for b in batches[1:]:
+    for i, b in enumerate(batches[1:]):
         t0 = time.perf_counter()
         step(b)
         times.append(time.perf_counter() - t0)
+        progress(f'cpu baseline: step {i + 1}/{len(batches) - 1} {times[-1]:.1f} s')
     dt = sum(times)
     n = a.cpu_batch * a.cpu_steps
     rates = sorted(a.cpu_batch / t for t in times)
@@ -642,6 +654,7 @@ def main():
     shard_tables = sharded and (a.shard_tables if a.shard_tables is not None else a.items >= 10_000_000)
     margs.shard_tables = bool(shard_tables)
     margs.merge_proj_backward = bool(a.merge_proj)
+    progress(f'rank {rank}/{world}: building the model')
     torch.manual_seed(0)
     model = BaselineModel(a.users, a.items, stats, types, margs).to(dev)
     model.train()
@@ -668,6 +681,7 @@ def main():
     def step(i):
         return trainer.step(pool[i % len(pool)], next_batch=pool[(i + 1) % len(pool)], rows=rows[i % len(pool)])
 
+    progress('warm-up steps')
     for i in range(a.warmup):
         if i == 0:
             G.GATHER_TRACE = []          # record the fused-gather launches of one real (eager) step
@@ -685,6 +699,7 @@ def main():
                 trainer.step(pool[i], next_batch=pool[(i + 1) % len(pool)], rows=rows[i])
                 prewarm += 1
     torch.cuda.synchronize()
+    progress(f'timed region: {a.steps} steps ({prewarm} prewarm steps captured the remaining capacities)')
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -720,8 +735,10 @@ def main():
         btrace, K.BACKWARD_TRACE = K.BACKWARD_TRACE, None
     kv = (pool[0][3] != 0).to(torch.uint8)        # the first bench batch's key validity (token_type != 0)
     roof, more = None, []
+    progress(f'timed region done: {elapsed / a.steps * 1e3:.3f} ms/step')
     if a.rooflines:
         roof, more = _rooflines(a, kv, jagged, rows, trace, btrace, model, pool, sid_roof)
+        progress('rooflines done')
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline and not a.semantic_ids and not a.fp8:   # config 2's CPU model only
