@@ -176,6 +176,7 @@ class DenseFlat:
             p.data = view            # the Parameter object (and the model's references) stays
         self.exp_avg = torch.zeros_like(self.buf)
         self.exp_avg_sq = torch.zeros_like(self.buf)
+        self._ptrs = [p.data_ptr() for p in self.params]
 
     def zero_grad(self, set_to_none=True):
         for p in self.params:
@@ -185,6 +186,10 @@ class DenseFlat:
                 p.grad.zero_()
 
     def step(self, clock):
+        if any(p.data_ptr() != q for p, q in zip(self.params, self._ptrs)):
+            # e.g. model.to() / load_state_dict(assign=True) after the optimizer was built:
+            # the update would land in the old buffer
+            raise RuntimeError('dense_flat: a parameter no longer lives in the flat buffer')
         grads = [p.grad for p in self.params]
         for lo, hi, idx in grad_runs(self.starts, self.ends, [g is not None for g in grads]):
             ranges = []
