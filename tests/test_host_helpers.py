@@ -165,3 +165,66 @@ def test_pair_split_backward_equals_slices():
         res.append((x.grad.clone(), ops.n))
     assert torch.equal(res[0][0], res[1][0])
     assert 'aten.slice_backward' in res[0][1] and 'aten.slice_backward' not in res[1][1]
+
+
+def test_dense_flat_step_plumbing_tracks_torch_adamw(monkeypatch):
+    """optim.DenseFlat on the CPU with grk_table_adamw_ranges_dev emulated by the element
+    update restated above (adam1): parameters become views of the flat buffer (the
+    Parameter objects stay), each gradient lands on its own rows, a parameter without a
+    gradient is skipped for that step (torch's rule; the kernel would move every row it
+    covers), and several steps track torch.optim.AdamW parameter by parameter."""
+    from tencent_recommendation_2025_amd import optim as O
+    lr, b1, b2, eps, wd = 1e-3, 0.9, 0.98, 1e-8, 0.01
+    calls = []
+
+    class Clock:
+        t = 0
+
+    def emulated(param, exp_avg, exp_avg_sq, clock, ranges):
+        hp = K.adamw_hparams(lr, b1, b2, eps, wd, clock.t)
+        calls.append(param.shape[0])
+        g = np.zeros(param.shape, np.float32)
+        for off, gr in ranges:
+            g[off:off + gr.shape[0]] = gr.float().numpy()
+        p, m, v = adam1(param.numpy(), exp_avg.numpy(), exp_avg_sq.numpy(), g, hp)
+        param.copy_(torch.from_numpy(p))
+        exp_avg.copy_(torch.from_numpy(m))
+        exp_avg_sq.copy_(torch.from_numpy(v))
+
+    monkeypatch.setattr(O.K, 'table_adamw_ranges', emulated)
+    gen = torch.Generator().manual_seed(5)
+    shapes = [(16, 8), (24,), (4, 6, 2), (8,), (40, 16)]
+    ps = [torch.nn.Parameter(torch.randn(s, generator=gen)) for s in shapes]
+    twins = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    flat = O.DenseFlat(ps, 'cpu')
+    assert all(flat.buf.data_ptr() <= p.data_ptr() < flat.buf.data_ptr() + flat.buf.numel() * 4 for p in ps)
+    assert all(torch.equal(p.detach(), q.detach()) for p, q in zip(ps, twins))
+    ref = torch.optim.AdamW(twins, lr=lr, betas=(b1, b2), eps=eps, weight_decay=wd)
+    clock = Clock()
+    skip = {2: {2}, 4: {0, 4}}                      # step -> parameters without a gradient
+    skipped = set()
+    for step in range(1, 6):
+        clock.t = step
+        before = [p.detach().clone() for p in ps]
+        for i, (p, q) in enumerate(zip(ps, twins)):
+            if i in skip.get(step, ()):
+                p.grad = q.grad = None
+            else:
+                g = torch.randn(p.shape, generator=gen) * (1e-3 if i == 1 else 1.0)
+                p.grad, q.grad = g.clone(), g.clone()
+        calls.clear()
+        flat.step(clock)
+        ref.step()
+        assert len(calls) == len(O.grad_runs(flat.starts, flat.ends, [p.grad is not None for p in ps]))
+        for i, (p, q) in enumerate(zip(ps, twins)):
+            if i in skip.get(step, ()):
+                assert torch.equal(p.detach(), before[i])   # no gradient: not moved this step
+                skipped.add(i)
+            elif i not in skipped:
+                # (after a skipped step torch counts that parameter's steps apart -- its own bias
+                # correction -- where the clock's step is global: DESIGN.md §3c, dense_flat)
+                np.testing.assert_allclose(p.detach().numpy(), q.detach().numpy(), rtol=0,
+                                           atol=4e-8 + 2e-7 * float(q.detach().abs().max()))
+    assert skipped == {0, 2, 4}
+    st = flat.state(ps[1])
+    np.testing.assert_allclose(st['exp_avg'].numpy(), ref.state[twins[1]]['exp_avg'].numpy(), rtol=1e-5, atol=1e-9)
