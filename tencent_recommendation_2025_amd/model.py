@@ -471,14 +471,6 @@ class BaselineModel(torch.nn.Module):
         m.add(P)
         return m
 
-    def _const_index(self, values, device):
-        """Cached device int64 tensor (built once: no host->device copy per forward)."""
-        t = self._proj_off_cache.get(('idx', values))
-        if t is None:
-            t = torch.tensor(values, dtype=torch.int64).to(device)
-            self._proj_off_cache[('idx', values)] = t
-        return t
-
     def _proj_index(self, feats, names, offs, N):
         """[N, sum of bags] rows of P: feature value v of table k -> offs[k] + v, 0 -> 0."""
         x = torch.cat([feats[k].reshape(N, -1) for k in names], 1)
