@@ -375,7 +375,11 @@ int grk_seq_ranges(const uint8_t* key_valid, int batch, int seq_len, int32_t* ra
  * (row r <- token index b * seq_len + t; -1 for the dead rows r >= n) and
  * *num_rows = n (int64, device).  next_token_type (optional, int32 [batch,
  * seq_len]): err_flag bit 1 if a token before its span has next_token_type == 1;
- * bit 2 if n > capacity (rows past capacity are not mapped). */
+ * bit 2 if the spans hold more than capacity rows: then the trailing spans that
+ * do not fit are dropped (ranges start = seq_len: an empty sequence to every
+ * kernel, row_base -seq_len, *num_rows = the kept rows <= capacity), so no
+ * kernel of the step addresses a row past capacity.  err_flag is OR-ed into,
+ * never cleared. */
 int grk_jagged_layout(const uint8_t* key_valid, int batch, int seq_len, int64_t capacity,
                       const int32_t* next_token_type, int32_t* ranges, int64_t* row_base, int32_t* row_map,
                       int64_t* num_rows, int32_t* err_flag, void* stream);

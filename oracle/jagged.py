@@ -15,21 +15,27 @@ import numpy as np
 def layout(key_valid, capacity):
     """(ranges int32 [B, 3] cols 0-1, row_base int64 [B], row_map int32 [capacity], n)
     of a [B, T] key-validity array: span of b = [start_b, T), start_b = first valid
-    position (T if none); spans packed in b order."""
+    position (T if none); spans packed in b order.  A capacity below the span rows
+    drops the trailing spans that do not fit (grk_jagged_layout, err bit 2)."""
     kv = np.asarray(key_valid) != 0
     B, T = kv.shape
     start = np.where(kv.any(1), kv.argmax(1), T)
     contig = np.array([kv[b, start[b]:].all() for b in range(B)], np.int32)
     span = T - start
+    incl = np.cumsum(span)
+    # spans ending past the capacity are dropped (start T, row_base -T; err bit 2)
+    drop = incl > capacity
+    start = np.where(drop, T, start)
+    contig = np.where(drop, 1, contig).astype(np.int32)
+    span = np.where(drop, 0, span)
     base = np.concatenate([[0], np.cumsum(span)[:-1]]).astype(np.int64)
     n = int(span.sum())
     row_map = np.full(capacity, -1, np.int32)
     for b in range(B):
         for t in range(start[b], T):
-            r = base[b] + t - start[b]
-            if r < capacity:
-                row_map[r] = b * T + t
-    return np.stack([start, contig], 1).astype(np.int32), (base - start).astype(np.int64), row_map, n
+            row_map[base[b] + t - start[b]] = b * T + t
+    row_base = np.where(drop, -T, base - start).astype(np.int64)
+    return np.stack([start, contig], 1).astype(np.int32), row_base, row_map, n
 
 
 def gather_rows(src, row_map):

@@ -24,10 +24,21 @@ namespace grk {
 namespace {
 
 // exclusive scan of the spans (T - start_b) over b -> row_base, total -> *n_rows;
-// one workgroup, chunks of 1024 sequences
-__global__ void __launch_bounds__(1024) k_jagged_base(const int32_t* __restrict__ ranges, int B, int T,
-                                                      int64_t* __restrict__ row_base, int64_t* __restrict__ n_rows) {
+// one workgroup, chunks of 1024 sequences.  Spans that would end past `cap`
+// (the caller under-stated the batch's rows) are dropped, never addressed out of
+// bounds: their start becomes T (an empty sequence for every kernel that reads
+// the ranges: no rows read or written), row_base -T, and err bit 2 is raised.
+// The kept spans are a prefix (the inclusive scan is monotone), so *n_rows <= cap.
+__global__ void __launch_bounds__(1024) k_jagged_base(int32_t* __restrict__ ranges, int B, int T, int64_t cap,
+                                                      int64_t* __restrict__ row_base, int64_t* __restrict__ n_rows,
+                                                      int32_t* __restrict__ err) {
   __shared__ int64_t part[1024];
+  __shared__ int dropped;
+  __shared__ unsigned long long kept;   // largest inclusive span sum <= cap
+  if (threadIdx.x == 0) {
+    dropped = 0;
+    kept = 0;
+  }
   int64_t carry = 0;
   for (int b0 = 0; b0 < B; b0 += 1024) {
     const int b = b0 + (int)threadIdx.x;
@@ -41,16 +52,32 @@ __global__ void __launch_bounds__(1024) k_jagged_base(const int32_t* __restrict_
       part[threadIdx.x] += v;
       __syncthreads();
     }
-    if (b < B) row_base[b] = carry + part[threadIdx.x] - span - st;
+    const int64_t incl = carry + part[threadIdx.x];
+    if (b < B) {
+      if (incl <= cap) {
+        row_base[b] = incl - span - st;
+        atomicMax(&kept, (unsigned long long)incl);
+      } else {
+        row_base[b] = -(int64_t)T;
+        ranges[3 * b] = T;
+        ranges[3 * b + 1] = 1;
+        dropped = 1;
+      }
+    }
     carry += part[1023];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *n_rows = carry;
+  if (threadIdx.x == 0) {
+    *n_rows = (int64_t)kept;
+    if (dropped && err) atomicOr(err, 2);
+  }
 }
 
 // row_map over max(B*T, cap) indices: span tokens at their rows, -1 past n.
 // err bit 1: a token before its sequence's span has next_token_type == 1 (its
-// logit would be dropped); bit 2: the spans hold more rows than cap.
+// logit would be dropped; this includes every labelled token of a span that
+// k_jagged_base dropped); bit 2 (k_jagged_base): the spans hold more rows than
+// cap -- the trailing spans were dropped.
 __global__ void __launch_bounds__(256) k_jagged_map(const int32_t* __restrict__ ranges, const int64_t* __restrict__ row_base,
                                                     const int64_t* __restrict__ n_rows, int B, int T, int64_t cap,
                                                     const int32_t* __restrict__ ntt, int32_t* __restrict__ row_map,
@@ -108,7 +135,7 @@ extern "C" int grk_jagged_layout(const uint8_t* key_valid, int batch, int seq_le
   hipStream_t s = (hipStream_t)stream;
   const int rc = grk_seq_ranges(key_valid, batch, seq_len, ranges, stream);
   if (rc) return rc;
-  k_jagged_base<<<1, 1024, 0, s>>>(ranges, batch, seq_len, row_base, num_rows);
+  k_jagged_base<<<1, 1024, 0, s>>>(ranges, batch, seq_len, capacity, row_base, num_rows, err_flag);
   GRK_LAUNCH_CHECK();
   const int64_t total = (int64_t)batch * seq_len > capacity ? (int64_t)batch * seq_len : capacity;
   k_jagged_map<<<grid_for(total, 256), 256, 0, s>>>(ranges, row_base, num_rows, batch, seq_len, capacity,

@@ -49,6 +49,19 @@ def span_rows(token_type):
     return int((T - first).sum().item())
 
 
+JAGGED_ERRORS = {1: 'a labelled token (next_token_type == 1) lies before its sequence\'s first valid token '
+                    'or in a dropped span',
+                 2: 'the batch holds more span rows than the jagged capacity (rows under-stated): '
+                    'trailing sequences were dropped'}
+
+
+def check_error(err):
+    """Raise ValueError when a layout error flag (int32 [1], host sync) is set."""
+    v = int(err.item())
+    if v:
+        raise ValueError('jagged layout: ' + '; '.join(m for bit, m in JAGGED_ERRORS.items() if v & bit))
+
+
 def capacity_for(n, quantum=1024, limit=None):
     """Rows of the jagged step for n span rows: n rounded up to a multiple of quantum
     (a few distinct shapes = a few GEMM plans and captured graphs), at most ``limit``."""
@@ -56,11 +69,17 @@ def capacity_for(n, quantum=1024, limit=None):
     return min(cap, limit) if limit is not None else cap
 
 
-def layout(token_type, capacity, next_token_type=None):
-    """The jagged layout of a batch with token_type [B, T] (0 = padding) in `capacity` rows."""
+def layout(token_type, capacity, next_token_type=None, err=None):
+    """The jagged layout of a batch with token_type [B, T] (0 = padding) in `capacity` rows.
+
+    ``err`` (optional int32 [1] device tensor, OR-ed into, never cleared; a fresh
+    zero flag otherwise): bit 1 -- a labelled token (next_token_type == 1) outside
+    the kept spans; bit 2 -- the spans hold more than ``capacity`` rows, so the
+    trailing spans were dropped (never addressed past the capacity)."""
     kv = (token_type != 0).contiguous().view(torch.uint8)   # bool bytes are 0 / 1: no cast kernel
     B, T = kv.shape
-    err = torch.zeros(1, dtype=torch.int32, device=kv.device)
+    if err is None:
+        err = torch.zeros(1, dtype=torch.int32, device=kv.device)
     ranges, row_base, row_map, n = K.jagged_layout(kv, capacity, next_token_type, err)
     return Jagged(B, T, int(capacity), kv, ranges, row_base, row_map, n, err)
 

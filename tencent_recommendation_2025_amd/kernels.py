@@ -242,17 +242,27 @@ def table_adamw(param, exp_avg, exp_avg_sq, hp, ids=None, rows=None, count=None,
     L.check(rc, 'grk_table_adamw')
 
 
+MAX_GRAD_RANGES = 64   # kMaxGradRanges (csrc/grk_optim.hip)
+
+
 def table_adamw_ranges(param, exp_avg, exp_avg_sq, clock, ranges):
     """Dense-parity AdamW of a whole table from dense gradient blocks in ONE launch
     (grk_table_adamw_ranges_dev): ranges = [(row_offset, grad [rows, >= D] bf16/fp32)],
     other rows g = 0."""
     _require_cuda(param, exp_avg, exp_avg_sq, *[g for _, g in ranges])
     rows, D = param.shape
+    if len(ranges) > MAX_GRAD_RANGES:
+        raise L.GrkError(f'at most {MAX_GRAD_RANGES} gradient ranges per launch, got {len(ranges)}')
+    if not (param.is_contiguous() and exp_avg.is_contiguous() and exp_avg_sq.is_contiguous()):
+        raise L.GrkError('param and moments must be contiguous')
     rs = sorted(ranges, key=lambda r: r[0])
     arr = (L.GrkGradRange * max(1, len(rs)))()
     for i, (off, g) in enumerate(rs):
         if g.dim() != 2 or g.stride(1) != 1 or g.shape[1] < D:
             raise L.GrkError(f'range {i}: grad must be a row-major [n, >= {D}] matrix')
+        if g.dtype == torch.float32 and (g.data_ptr() % 16 or g.stride(0) % 4):
+            # k_adamw_ranges reads fp32 gradient rows as 16-byte vectors
+            raise L.GrkError(f'range {i}: fp32 grad rows must be 16-byte aligned')
         arr[i] = L.GrkGradRange(int(off), int(off) + g.shape[0], g.data_ptr(), g.stride(0), L.dtype_code(g.dtype), 0)
     rc = L.lib().grk_table_adamw_ranges_dev(param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(),
                                             exp_avg_sq.data_ptr(), rows, D, arr, len(rs), clock.ring.data_ptr(),

@@ -160,6 +160,25 @@ def grad_runs(starts, ends, has_grad):
     return [tuple(r) for r in runs]
 
 
+def aligned_rows(g):
+    """g itself, or a copy when its fp32 rows are not 16-byte aligned (the multi-range
+    kernel reads fp32 gradient rows as 16-byte vectors)."""
+    if g.stride(-1) != 1 or (g.dtype == torch.float32 and (g.data_ptr() % 16 or g.stride(0) % 4)):
+        return g.contiguous().clone()
+    return g
+
+
+def split_runs(runs, starts, ends, limit):
+    """Runs of grad_runs cut into pieces of at most ``limit`` tensors (the multi-range
+    kernel's cap); each piece's rows stay contiguous."""
+    out = []
+    for _lo, _hi, idx in runs:
+        for k in range(0, len(idx), limit):
+            part = idx[k:k + limit]
+            out.append((starts[part[0]], ends[part[-1]], part))
+    return out
+
+
 class DenseFlat:
     """fp32 dense parameters as views of one [rows, 8] buffer with flat AdamW moments,
     stepped by grk_table_adamw_ranges_dev (each parameter's gradient one range)."""
@@ -191,7 +210,8 @@ class DenseFlat:
             # the update would land in the old buffer
             raise RuntimeError('dense_flat: a parameter no longer lives in the flat buffer')
         grads = [p.grad for p in self.params]
-        for lo, hi, idx in grad_runs(self.starts, self.ends, [g is not None for g in grads]):
+        for lo, hi, idx in split_runs(grad_runs(self.starts, self.ends, [g is not None for g in grads]),
+                                      self.starts, self.ends, K.MAX_GRAD_RANGES):
             ranges = []
             for i in idx:
                 g = grads[i]
@@ -462,8 +482,9 @@ class FusedAdamW:
             g.clear()
             return
         if g.dense_grads and not g.pending and isinstance(hp, K.DeviceClock) \
-                and len(g.dense_grads) <= 64:  # dense gradient blocks only: one multi-range launch
-            K.table_adamw_ranges(g.flat, g.exp_avg, g.exp_avg_sq, hp, list(g.dense_grads.items()))
+                and len(g.dense_grads) <= K.MAX_GRAD_RANGES:  # dense gradient blocks only: one multi-range launch
+            K.table_adamw_ranges(g.flat, g.exp_avg, g.exp_avg_sq, hp,
+                                 [(off, aligned_rows(x)) for off, x in g.dense_grads.items()])
         elif g.dense_grads and not g.pending:  # dense gradients only: per-range updates
             g.step_dense_ranges(hp)
         elif g.dense_grads:  # mixed: one dense fp32 gradient

@@ -129,7 +129,10 @@ class Trainer:
         self._side = None
         self._sharded = hasattr(optimizer, 'prepare')
         self.jagged, self.jagged_quantum = bool(jagged), int(jagged_quantum)
-        self._cap = None         # jagged capacity of the current step
+        self._cap = None         # jagged capacity of the current step (set by step(), cleared after it)
+        self._jag_err = None     # jagged layout error flags, OR-ed over steps (int32 [1], device)
+        self._err_host = None    # pinned copy of the flags, polled every ERR_POLL graph replays
+        self._replays = 0
 
     def _graph_blocker(self):
         if not torch.cuda.is_available():
@@ -147,8 +150,13 @@ class Trainer:
                else contextlib.nullcontext())
         jag = pidx = None
         if self.jagged:
+            # a direct compute_loss / eager_step call (no step()) counts the batch's rows itself
             cap = self._cap if self._cap is not None else J.capacity_for(J.span_rows(tt), self.jagged_quantum)
-            jag = J.layout(tt, cap, ntt)
+            if self._jag_err is None:
+                self._jag_err = torch.zeros(1, dtype=torch.int32, device=tt.device)
+            # rows under-stated by the caller: the layout drops the spans past cap (no kernel
+            # addresses a row beyond it) and raises err bit 2, checked by check_jagged()
+            jag = J.layout(tt, cap, ntt, err=self._jag_err)
             if self._sharded and getattr(self.model, '_remaps', None) is not None:
                 # prepare() routed the [B, T] batch: its lookups' fetched-row indices follow
                 # the batch into the jagged row order
@@ -180,7 +188,30 @@ class Trainer:
         loss = self.compute_loss(batch)
         loss.backward()
         self.opt.step()
+        if self.jagged and not torch.cuda.is_current_stream_capturing():
+            self.check_jagged()   # eager: one host sync per step
         return loss.detach()
+
+    ERR_POLL = 16
+
+    def check_jagged(self):
+        """Raise ValueError if any jagged layout so far flagged an error (host sync)."""
+        if self._jag_err is not None:
+            J.check_error(self._jag_err)
+
+    def _poll_jagged(self):
+        """Graph replays: copy the flags to pinned memory every ERR_POLL replays and
+        check the copy made ERR_POLL replays earlier (no host wait)."""
+        if self._jag_err is None:
+            return
+        self._replays += 1
+        if self._replays % self.ERR_POLL:
+            return
+        if self._err_host is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        elif int(self._err_host[0]):
+            J.check_error(self._err_host)
+        self._err_host.copy_(self._jag_err, non_blocking=True)
 
     def step(self, batch, next_batch=None, rows=None):
         """One training step; ``next_batch`` (optional) is the batch of the following
@@ -190,6 +221,12 @@ class Trainer:
         if self.jagged:
             n = int(rows) if rows is not None else J.span_rows(batch[3])
             self._cap = key = J.capacity_for(n, self.jagged_quantum)
+        try:
+            return self._step(batch, next_batch, key)
+        finally:
+            self._cap = None
+
+    def _step(self, batch, next_batch, key):
         if not self.graph:
             return self.eager_step(batch, next_batch)
         entry = self._graphs.get(key)
@@ -223,6 +260,8 @@ class Trainer:
             self.opt.maybe_segment()
             self._g.replay()
             self.opt.graph_replayed()
+        if self.jagged:
+            self._poll_jagged()
         return self._static_loss.clone()
 
     def _on_side(self, fn):

@@ -42,7 +42,7 @@ def test_layout_and_gather_match_oracle():
         tt[b, T - n:] = rng.integers(1, 3, n)
     tt[3, 40:45] = 0            # a hole inside a span
     tt[5] = 0                   # an empty sequence
-    n_rows = int(ojag.layout(tt, 1)[3])
+    n_rows = int(ojag.layout(tt, B * T)[3])
     assert J.span_rows(torch.from_numpy(tt)) == n_rows == J.span_rows(torch.from_numpy(tt).to(DEV))
     for cap in (n_rows, J.capacity_for(n_rows, 256)):
         jag = J.layout(torch.from_numpy(tt).to(DEV), cap)
@@ -58,12 +58,25 @@ def test_layout_and_gather_match_oracle():
         K.gather_rows([(srcs[k].reshape(B * T, *srcs[k].shape[2:]), dsts[k]) for k in srcs], jag.row_map)
         for k in feats:
             assert np.array_equal(dsts[k].cpu().numpy(), ojag.gather_rows(feats[k], map_w)), k
-    # error flags: a next-item label before the span (bit 1), more span rows than capacity (bit 2)
+    # error flags: a next-item label before the span (bit 1)
     ntt = (tt != 0).astype(np.int64)
-    ntt[0, 0] = 1 if tt[0, 0] == 0 else ntt[0, 0]
-    jag = J.layout(torch.from_numpy(tt).to(DEV), n_rows - 1, torch.from_numpy(ntt).to(DEV))
-    err = int(jag.err.item())
-    assert err & 2 and (err & 1) == (tt[0, 0] == 0)
+    b0 = int(np.flatnonzero(tt[:, 0] == 0)[0])
+    ntt[b0, 0] = 1
+    jag = J.layout(torch.from_numpy(tt).to(DEV), n_rows, torch.from_numpy(ntt).to(DEV))
+    assert int(jag.err.item()) == 1
+    # more span rows than capacity (bit 2): the trailing spans are dropped, exactly as
+    # the oracle restates, and nothing is mapped past the capacity
+    for cap in (n_rows - 1, n_rows // 2, 1):
+        ntt = (tt != 0).astype(np.int64)
+        jag = J.layout(torch.from_numpy(tt).to(DEV), cap, torch.from_numpy(ntt).to(DEV))
+        rng_w, base_w, map_w, n_w = ojag.layout(tt, cap)
+        assert int(jag.err.item()) & 2
+        assert int(jag.n.item()) == n_w <= cap
+        assert np.array_equal(jag.seq_range.cpu().numpy()[:, :2], rng_w)
+        assert np.array_equal(jag.row_base.cpu().numpy()[:B], base_w)
+        assert np.array_equal(jag.row_map.cpu().numpy(), map_w)
+        with pytest.raises(ValueError, match='more span rows'):
+            J.check_error(jag.err)
 
 
 def _hstu_case(B, T, H, hd, seed, holes=False):
@@ -206,37 +219,136 @@ def test_jagged_encode_equals_padded_fp32(block):
     assert not bad, bad
 
 
-def test_jagged_trainer_bf16_matches_padded_and_graph_replay_is_bitwise():
-    """bf16 autocast HSTU (the bench's regime), dropout 0: jagged losses within the
-    bench tolerance (1e-3) of the padded trainer over 4 steps; the jagged step
-    replayed from HIP graphs of two capacities == the eager jagged step, bitwise."""
-    from tencent_recommendation_2025_amd import jagged as J
+_TRAINER_CFG = (dict(batch_size=16, maxlen=60, num_items=4000, num_users=500, min_len=4),
+                dict(hidden_units=128, maxlen=60, num_blocks=2, num_heads=2))
+
+
+def _trainer_batches(cfg):
+    """Three batches of the config plus one of short sequences (a second capacity bucket)."""
     from tencent_recommendation_2025_amd import synthetic as S
+    g = torch.Generator(device=DEV).manual_seed(3)
+    batches = [S.make_batch(cfg, g, DEV) for _ in range(3)]
+    batches.append(S.make_batch(S.SyntheticConfig(**{**cfg.__dict__, 'min_len': 2}), g, DEV))
+    return batches
+
+
+def _one_step_grads(state, jagged, batch):
+    """Loss and every gradient (dense parameters; each table group's dense row
+    gradient) of ONE bf16-autocast trainer step from the parameters ``state``."""
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    m, _ = _model(*_TRAINER_CFG)
+    m.load_state_dict(state)
+    opt = FusedAdamW(m, lr=1e-3, defer_period=4)
+    tr = Trainer(m, opt, loss='bce', jagged=jagged, jagged_quantum=128)
+    opt.zero_grad()
+    opt.begin_step(batch)
+    loss = tr.compute_loss(batch)
+    loss.backward()
+    if jagged:
+        tr.check_jagged()
+    grads = {n: p.grad.detach().float().clone() for n, p in m.named_parameters() if p.grad is not None}
+    for grp in opt.groups:
+        grads['group.' + grp.name] = grp.dense_gradient().float().clone()
+    return float(loss), grads
+
+
+# Per-step bound of the bf16 jagged step against the padded one from identical
+# parameters.  The dead rows contribute exact zeros, so what differs is only the
+# fp32 summation order of the GEMMs / grk_wgrad over K = capacity vs B*T rows (and
+# the bf16 rounding that order can flip in autocast outputs).  Measured on MI355X
+# (round 4): see the test's printout.
+JAGGED_STEP_TOL = dict(loss=1e-5, grad=1e-3)
+
+
+def test_jagged_step_matches_padded_from_identical_parameters():
+    """bf16 autocast HSTU (the bench's regime), dropout 0: from the SAME parameters,
+    one jagged step's loss and every gradient against the padded step's, at the
+    initial parameters and after 2 and 5 padded training steps, on batches of two
+    capacity buckets (reference loop: model/BaseLine/main.py:177-185)."""
+    from tencent_recommendation_2025_amd import jagged as J
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    m, cfg = _model(*_TRAINER_CFG)
+    batches = _trainer_batches(cfg)
+    tr = Trainer(m, FusedAdamW(m, lr=1e-3, defer_period=4), loss='bce')
+    worst = {}
+    done = 0
+    for trained, probe in ((0, 0), (2, 3), (5, 1)):
+        while done < trained:
+            tr.step(batches[done % 4])
+            done += 1
+        state = {k: v.detach().clone() for k, v in m.state_dict().items()}   # flushes deferred rows
+        lp, gp = _one_step_grads(state, False, batches[probe])
+        lj, gj = _one_step_grads(state, True, batches[probe])
+        assert set(gp) == set(gj)
+        errs = {k: nrel(gj[k].cpu(), gp[k].cpu()) for k in gp}
+        errs['loss'] = abs(lj - lp) / abs(lp)
+        print(f'after {trained} steps, batch {probe} (capacity {J.capacity_for(J.span_rows(batches[probe][3]), 128)}):',
+              f"loss {errs['loss']:.2e}", sorted(((k, f'{v:.2e}') for k, v in errs.items() if k != 'loss'),
+                                                 key=lambda kv: -float(kv[1]))[:6])
+        for k, v in errs.items():
+            worst[k] = max(worst.get(k, 0.0), v)
+    assert worst.pop('loss') < JAGGED_STEP_TOL['loss'], worst
+    bad = {k: v for k, v in worst.items() if v > JAGGED_STEP_TOL['grad']}
+    assert not bad, bad
+
+
+def test_jagged_trainer_graph_replay_is_bitwise_and_tracks_padded():
+    """The jagged step replayed from HIP graphs of two capacities == the eager jagged
+    step, bitwise (losses and every parameter over 8 steps).  The padded trainer's
+    8-step loss trajectory is reported beside it, held only to 5e-3: AdamW's first
+    steps move every parameter by ~lr * sign(g), so a gradient element that is
+    rounding noise in either run (e.g. an analytically zero one) moves by +-lr and
+    the trajectories separate by design; per-step parity is the test above."""
+    from tencent_recommendation_2025_amd import jagged as J
     from tencent_recommendation_2025_amd.optim import FusedAdamW
     from tencent_recommendation_2025_amd.train import Trainer
     runs = {}
     for name, jagged, graph in (('padded', False, False), ('jagged', True, False), ('jagged_graph', True, True)):
-        m, cfg = _model(dict(batch_size=16, maxlen=60, num_items=4000, num_users=500, min_len=4),
-                        dict(hidden_units=128, maxlen=60, num_blocks=2, num_heads=2))
+        m, cfg = _model(*_TRAINER_CFG)
         tr = Trainer(m, FusedAdamW(m, lr=1e-3, defer_period=4), loss='bce', graph=graph, graph_warmup=1,
                      jagged=jagged, jagged_quantum=128)
-        g = torch.Generator(device=DEV).manual_seed(3)
-        cfg_short = S.SyntheticConfig(**{**cfg.__dict__, 'min_len': 4})
-        batches = [S.make_batch(cfg_short, g, DEV) for _ in range(3)]
-        # two capacity buckets: one batch of short sequences
-        short = S.SyntheticConfig(**{**cfg.__dict__, 'min_len': 2, 'maxlen': 60})
-        batches.append(S.make_batch(short, g, DEV))
+        batches = _trainer_batches(cfg)
         rows = [J.span_rows(b[3]) for b in batches]
         losses = [tr.step(batches[i % 4], rows=rows[i % 4] if jagged else None).clone() for i in range(8)]
         if graph:
             assert len(tr._graphs) >= 2, tr._graphs.keys()
+        if jagged:
+            tr.check_jagged()
         runs[name] = (torch.stack(losses), m.state_dict())
     lp, lj, lg = runs['padded'][0], runs['jagged'][0], runs['jagged_graph'][0]
     assert torch.equal(lj, lg), (lj, lg)
     for k in runs['jagged'][1]:
         assert torch.equal(runs['jagged'][1][k], runs['jagged_graph'][1][k]), k
-    rel = ((lj - lp).abs() / lp.abs()).max().item()
-    assert rel < 1e-3, (lp, lj)
+    rel = ((lj - lp).abs() / lp.abs())
+    print('8-step loss trajectory, jagged vs padded (rel):', [f'{x:.1e}' for x in rel.tolist()])
+    assert rel.max().item() < 5e-3, (lp, lj)
+
+
+def test_understated_rows_raise_instead_of_addressing_past_capacity():
+    """a caller that under-states the batch's span rows gets a ValueError
+    (err bit 2 checked after the eager step), and no kernel touches a row past the
+    capacity (the layout drops the trailing spans)."""
+    from tencent_recommendation_2025_amd import jagged as J
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    m, cfg = _model(*_TRAINER_CFG)
+    batch = _trainer_batches(cfg)[0]
+    n = J.span_rows(batch[3])
+    assert n > 256
+    tr = Trainer(m, FusedAdamW(m, lr=1e-3), loss='bce', jagged=True, jagged_quantum=128)
+    with pytest.raises(ValueError, match='more span rows'):
+        tr.step(batch, rows=n // 2)
+    assert tr._cap is None
+    torch.cuda.synchronize()
+    # a direct compute_loss call after a step recomputes the capacity (no stale _cap)
+    tr2 = Trainer(m, FusedAdamW(m, lr=1e-3), loss='bce', jagged=True, jagged_quantum=128)
+    tr2.step(batch, rows=n)
+    small = _trainer_batches(cfg)[3]
+    loss = tr2.compute_loss(small)
+    assert torch.isfinite(loss).all()
+    tr2.check_jagged()
 
 
 @pytest.mark.skipif(os.environ.get('GRK_MERGE_PROJ_TESTS') != '1',

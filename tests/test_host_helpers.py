@@ -182,6 +182,7 @@ def test_dense_flat_step_plumbing_tracks_torch_adamw(monkeypatch):
 
     def emulated(param, exp_avg, exp_avg_sq, clock, ranges):
         hp = K.adamw_hparams(lr, b1, b2, eps, wd, clock.t)
+        assert len(ranges) <= K.MAX_GRAD_RANGES          # the kernel refuses more (kMaxGradRanges)
         calls.append(param.shape[0])
         g = np.zeros(param.shape, np.float32)
         for off, gr in ranges:
@@ -215,7 +216,8 @@ def test_dense_flat_step_plumbing_tracks_torch_adamw(monkeypatch):
         calls.clear()
         flat.step(clock)
         ref.step()
-        assert len(calls) == len(O.grad_runs(flat.starts, flat.ends, [p.grad is not None for p in ps]))
+        assert len(calls) == len(O.split_runs(O.grad_runs(flat.starts, flat.ends, [p.grad is not None for p in ps]),
+                                              flat.starts, flat.ends, K.MAX_GRAD_RANGES))
         for i, (p, q) in enumerate(zip(ps, twins)):
             if i in skip.get(step, ()):
                 assert torch.equal(p.detach(), before[i])   # no gradient: not moved this step
@@ -228,3 +230,45 @@ def test_dense_flat_step_plumbing_tracks_torch_adamw(monkeypatch):
     assert skipped == {0, 2, 4}
     st = flat.state(ps[1])
     np.testing.assert_allclose(st['exp_avg'].numpy(), ref.state[twins[1]]['exp_avg'].numpy(), rtol=1e-5, atol=1e-9)
+
+
+def test_dense_flat_splits_runs_beyond_the_kernel_range_cap(monkeypatch):
+    """a run of more than kMaxGradRanges (64) parameters with gradients -- the
+    softmax-block model's ~70 dense parameters -- is cut into launches of at most 64
+    ranges, each over contiguous rows, and every parameter still takes exactly its
+    torch AdamW update."""
+    from tencent_recommendation_2025_amd import optim as O
+    lr, b1, b2, eps, wd = 1e-3, 0.9, 0.98, 1e-8, 0.01
+    calls = []
+
+    class Clock:
+        t = 1
+
+    def emulated(param, exp_avg, exp_avg_sq, clock, ranges):
+        assert len(ranges) <= K.MAX_GRAD_RANGES
+        calls.append(len(ranges))
+        hp = K.adamw_hparams(lr, b1, b2, eps, wd, clock.t)
+        g = np.zeros(param.shape, np.float32)
+        for off, gr in ranges:
+            assert 0 <= off and off + gr.shape[0] <= param.shape[0]
+            g[off:off + gr.shape[0]] = gr.float().numpy()
+        p, m, v = adam1(param.numpy(), exp_avg.numpy(), exp_avg_sq.numpy(), g, hp)
+        param.copy_(torch.from_numpy(p))
+        exp_avg.copy_(torch.from_numpy(m))
+        exp_avg_sq.copy_(torch.from_numpy(v))
+
+    monkeypatch.setattr(O.K, 'table_adamw_ranges', emulated)
+    gen = torch.Generator().manual_seed(9)
+    ps = [torch.nn.Parameter(torch.randn((8 * (1 + i % 3),), generator=gen)) for i in range(150)]
+    twins = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    flat = O.DenseFlat(ps, 'cpu')
+    ref = torch.optim.AdamW(twins, lr=lr, betas=(b1, b2), eps=eps, weight_decay=wd)
+    for p, q in zip(ps, twins):
+        g = torch.randn(p.shape, generator=gen)
+        p.grad, q.grad = g.clone(), g.clone()
+    flat.step(Clock())
+    ref.step()
+    assert calls == [64, 64, 22]
+    for p, q in zip(ps, twins):
+        np.testing.assert_allclose(p.detach().numpy(), q.detach().numpy(), rtol=0,
+                                   atol=4e-8 + 2e-7 * float(q.detach().abs().max()))
