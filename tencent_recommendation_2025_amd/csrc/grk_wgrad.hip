@@ -169,6 +169,152 @@ __global__ void __launch_bounds__(256) k_wgrad(const bf16_t* __restrict__ A, int
   }
 }
 
+// ---------------------------------------------------------------------------
+// The same tile and K split with the operands staged by LDS-DMA
+// (global_load_lds_dwordx4) in a 4-deep ring: the 32-row steps t+1..t+3 are in
+// flight while step t is multiplied.  Measured on the register-staged kernel
+// above (round 3): each step waited ~1.5k cycles for its loads behind 256
+// cycles of MFMA per wave (one step of prefetch), ~10x the MFMA time per
+// launch.  Here nothing is staged through VGPRs:
+//   * a wave-instruction writes 1 KiB = 4 rows of the [32][128] image at
+//     wave-uniform base + lane * 16, so the XOR swizzle of wg_off is applied
+//     to the SOURCE: lane l of row group g loads global chunk (l & 15) ^ f(row)
+//     into LDS slot l & 15 (wg_frag reads slot ch ^ f(row) for chunk ch);
+//   * per step each wave issues 2 + 2 instructions (dY, X); step t is retired
+//     by `s_waitcnt vmcnt(8)` (steps t+1, t+2 stay in flight) and a raw
+//     s_barrier (a __syncthreads() would drain every DMA: vmcnt(0));
+//   * the slot refilled with step t+3 is the one step t-1 read: every wave
+//     has passed this step's barrier, so its reads of it are done;
+//   * db from the dY fragments the wn = 0 waves hold anyway: each lane sums
+//     its 8 k values per fragment (column m = c0 + (lane & 31)), the two
+//     k halves (lanes l, l + 32) are added once at the end.
+//   * columns past M / N read a valid column instead (their outputs are
+//     never stored); K must be a multiple of 32 (no partial steps: the
+//     slices are whole steps) -- else the register-staged kernel runs.
+constexpr int kWgStages = 4;
+constexpr int kWgStage = 2 * kWgImg;            // dY + X images of one step: 16 KiB
+
+__device__ __forceinline__ int wg_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+// One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4) to the wave-uniform LDS
+// address lds.  In asm, so hipcc does not count it: its alias tracking of
+// LDS-DMA stores otherwise puts s_waitcnt vmcnt(0) before the step's first
+// ds_read (seen in the ISA), draining the ring; the counted waits below are
+// the only ones (cdna_hip_programming.md §5.7: M0 set and restored inside).
+__device__ __forceinline__ void wg_dma16(const bf16_t* src, unsigned lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wg_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <bool DB>
+__global__ void __launch_bounds__(256) k_wgrad_lds(const bf16_t* __restrict__ A, int64_t lda,
+                                                   const bf16_t* __restrict__ B, int64_t ldb, int K, int M, int N,
+                                                   int kchunk, float* __restrict__ part, float* __restrict__ dbpart) {
+  __shared__ __attribute__((aligned(16))) char smem[kWgStages * kWgStage];  // 64 KiB
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 1, wn = w >> 1, r = lane & 31, hh = lane >> 5;
+  const unsigned nx = gridDim.x, my = gridDim.y;
+  const unsigned total = nx * my * gridDim.z;
+  const unsigned phys = blockIdx.x + nx * (blockIdx.y + my * blockIdx.z);
+  const unsigned logical = total % 8 == 0 ? (phys % 8) * (total / 8) + phys / 8 : phys;
+  const int bx = (int)(logical % nx), by = (int)((logical / nx) % my), s = (int)(logical / (nx * my));
+  const int n0 = bx * kWgTile, m0 = by * kWgTile;
+  const int kb = s * kchunk, ke = min(K, kb + kchunk);
+  const int nsteps = ke > kb ? (ke - kb) / kWgK : 0;
+  const bool do_db = DB && bx == 0 && wn == 0;
+  // this lane's two staged rows per image and step: row group 2w + i, row 4 (2w + i) + (lane >> 4)
+  const int slot = lane & 15;
+  const bf16_t* pa[2];
+  const bf16_t* pb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 4 * (2 * w + i) + (lane >> 4);
+    const int chunk = slot ^ wg_swz(row);
+    const int ma = m0 + 8 * chunk, nb = n0 + 8 * chunk;
+    pa[i] = A + (int64_t)(kb + row) * lda + (ma < M ? ma : 0);
+    pb[i] = B + (int64_t)(kb + row) * ldb + (nb < N ? nb : 0);
+  }
+  // wave-uniform LDS byte address of this wave's first row group in stage 0
+  const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane(
+      (int)((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem + 2 * w * 1024));
+  auto issue = [&](int step, int buf) {
+    const unsigned base = lds0 + buf * kWgStage;
+    const int64_t ka = (int64_t)step * kWgK * lda, kbb = (int64_t)step * kWgK * ldb;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      wg_dma16(pa[i] + ka, base + i * 1024);
+      wg_dma16(pb[i] + kbb, base + kWgImg + i * 1024);
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  float cs[2] = {0.f, 0.f};
+
+  for (int t = 0; t < kWgStages - 1 && t < nsteps; ++t) issue(t, t);
+  for (int t = 0; t < nsteps; ++t) {
+    const int ahead = nsteps - 1 - t;   // steps issued after t that may stay in flight (<= 2)
+    if (ahead >= 2) wg_wait_barrier<8>();
+    else if (ahead == 1) wg_wait_barrier<4>();
+    else wg_wait_barrier<0>();
+    if (t + kWgStages - 1 < nsteps) issue(t + kWgStages - 1, (t + kWgStages - 1) & (kWgStages - 1));
+    const char* ia = smem + (t & (kWgStages - 1)) * kWgStage;
+    const char* ib = ia + kWgImg;
+#pragma unroll
+    for (int ks = 0; ks < kWgK / 16; ++ks) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = wg_frag(ia, 16 * ks, 64 * wm + 32 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = wg_frag(ib, 16 * ks, 64 * wn + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
+      if (do_db) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          float q = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) q += static_cast<float>(fa[i][e]);
+          cs[i] += q;
+        }
+      }
+    }
+  }
+  float* out = part + (int64_t)s * M * N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + 64 * wn + 32 * j + r;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + 64 * wm + 32 * i + acc_row(e, hh);
+        if (m < M && n < N) out[(int64_t)m * N + n] = acc[i][j][e];
+      }
+    }
+  if (do_db) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float other = __shfl_xor(cs[i], 32);   // the other k half of column r
+      const int m = m0 + 64 * wm + 32 * i + r;
+      if (hh == 0 && m < M) dbpart[(int64_t)s * M + m] = cs[i] + other;
+    }
+  }
+}
+
 __device__ __forceinline__ void wg_store4(float* p, const float4& v) { *reinterpret_cast<float4*>(p) = v; }
 __device__ __forceinline__ void wg_store4(bf16_t* p, const float4& v) {
   uint2 t;
@@ -283,7 +429,16 @@ extern "C" int grk_wgrad(const void* dy, int64_t ld_dy, const void* x, int64_t l
   float* dbp = part + (size_t)S * m * n;
   const int kchunk = (int)(((k + S - 1) / S + kWgK - 1) / kWgK * kWgK);
   const dim3 grid((unsigned)((n + kWgTile - 1) / kWgTile), (unsigned)((m + kWgTile - 1) / kWgTile), (unsigned)S);
-  if (db)
+  // LDS-DMA ring for whole 32-row steps (GRK_WGRAD_REG=1: the register-staged kernel, A/B)
+  static const bool force_reg = getenv("GRK_WGRAD_REG") != nullptr;
+  if (k % kWgK == 0 && !force_reg) {
+    if (db)
+      k_wgrad_lds<true><<<grid, 256, 0, s>>>((const bf16_t*)dy, ld_dy, (const bf16_t*)x, ld_x, (int)k, (int)m, (int)n,
+                                             kchunk, part, dbp);
+    else
+      k_wgrad_lds<false><<<grid, 256, 0, s>>>((const bf16_t*)dy, ld_dy, (const bf16_t*)x, ld_x, (int)k, (int)m,
+                                              (int)n, kchunk, part, nullptr);
+  } else if (db)
     k_wgrad<true><<<grid, 256, 0, s>>>((const bf16_t*)dy, ld_dy, (const bf16_t*)x, ld_x, (int)k, (int)m, (int)n,
                                        kchunk, part, dbp);
   else

@@ -1,7 +1,8 @@
 """grk_wgrad (split-K MFMA weight gradient + bias gradient) against a torch
 fp64 reference of the same bf16 operands, on the bench's shapes (K = B*T
 tokens, the HSTU projections) and on ragged edges; run-to-run bitwise
-determinism (in-order slice reduction, no atomics)."""
+determinism (in-order slice reduction, no atomics).  K a multiple of 32 takes
+the LDS-DMA ring kernel (k_wgrad_lds), other K the register-staged one."""
 import pytest
 import torch
 
@@ -16,7 +17,9 @@ def nrel(a, b):
 
 @pytest.mark.parametrize('K,M,N', [(25728, 2048, 512), (25728, 512, 512), (51456, 512, 560), (1000, 136, 72),
                                    (3, 8, 8), (0, 16, 24), (777, 264, 1032),
-                                   (5000, 1032, 1288), (25728, 1024, 1024), (300, 2048, 520)])
+                                   (5000, 1032, 1288), (25728, 1024, 1024), (300, 2048, 520),
+                                   # K % 32 == 0: the LDS-DMA ring kernel, ragged M / N tiles, short slices
+                                   (14336, 2048, 512), (1024, 136, 72), (3200, 264, 1032), (32, 8, 8), (96, 520, 2048)])
 def test_wgrad_matches_fp64(K, M, N):
     from tencent_recommendation_2025_amd import kernels as Kn
     g = torch.Generator(device=DEV).manual_seed(K + M + N)

@@ -182,3 +182,98 @@ def test_jagged_remaps_follow_the_row_map():
     # a derived role (feat2emb_pair's 'pair') is not carried over
     remaps[('item_emb', 'pair', 0)] = (fetched, torch.zeros(2, B, T, dtype=torch.int64))
     assert ('item_emb', 'pair', 0) not in jagged_remaps(remaps, parts, row_map)
+
+
+def _jagged_worker(rank, world, port, out_q):
+    """One rank of the jagged sharded exchange: a left-padded [B, T] batch routed as
+    ShardedFusedAdamW does (every role's ids of a table in one route), the fetched-row
+    indices carried into the jagged row order (train.jagged_remaps, row map from the
+    jagged oracle), rows read through them, per-row gradients pushed back to owners."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from oracle import jagged as ojag
+        from tencent_recommendation_2025_amd.sharding import ShardExchange, ShardedFusedAdamW
+        from tencent_recommendation_2025_amd.train import jagged_remaps
+        torch.manual_seed(0)
+        R, D, B, T = 97, 8, 5, 11
+        full = torch.randn(R, D)
+        full[0] = 0
+        g = torch.Generator().manual_seed(200 + rank)
+        tt = torch.zeros(B, T, dtype=torch.int64)
+        for b in range(B):
+            s0 = int(torch.randint(0, T, (1,), generator=g))
+            tt[b, s0:] = 1
+            tt[b, s0] = 2                                   # the user token
+        seq = torch.randint(1, R, (B, T), generator=g) * (tt != 0)
+        pos = torch.randint(1, R, (B, T), generator=g) * (tt != 0)
+        neg = torch.randint(1, R, (B, T), generator=g) * (tt != 0)
+        seq[0, -1] = pos[1, -1] = 7                         # a row shared across roles
+        parts = ShardedFusedAdamW._parts((seq, pos, neg, tt))
+        shard = full[rank::world].contiguous()
+        ex = ShardExchange('item_emb', shard, D, gather_fn=torch_gather)
+        plist = parts['item_emb']
+        r = ex.route(torch.cat([v().reshape(-1) for _, _, _, v in plist]))
+        counts = torch.stack([r['send_counts'], r['recv_counts']]).tolist()
+        fetched = ex.fetch(r, counts[0], counts[1])
+        remaps, off = {}, 0
+        for role, idx, mode, _ in plist:
+            remaps[('item_emb', role, mode)] = (fetched, r['inverse'][off:off + idx.numel()].view(B, T))
+            off += idx.numel()
+        _, _, row_map, n = ojag.layout(tt.numpy(), 64)
+        row_map = torch.from_numpy(row_map)
+        jr = jagged_remaps(remaps, parts, row_map)
+        ok = True
+        grads = {}
+        for (name, role, mode), (ref, jinv) in jr.items():
+            ids = dict(((n_, r_, m_), v) for n_, pl in parts.items() for r_, _, m_, v in pl)[(name, role, mode)]()
+            flat = ids.reshape(-1)
+            live = row_map >= 0
+            want = full[flat[row_map.clamp(min=0).long()]]
+            want[~live] = 0                                 # dead rows read the padding row (zeros)
+            ok &= torch.equal(ref[jinv[0]], want)
+            # per-row gradients of the jagged step: dead rows carry exact zeros
+            gj = torch.randn(len(row_map), D, generator=g) * live.unsqueeze(1)
+            grads[role] = (gj, jinv[0], flat, row_map)
+        ug = torch.zeros(len(r['uniq']), D)
+        for gj, jinv, _, _ in grads.values():
+            ug.index_add_(0, jinv, gj)
+        local, rows = ex.push_grads(ug)
+        shard_grad = torch.zeros_like(shard).index_add_(0, local, rows)
+        if rank == 0:
+            shard_grad[0] = 0
+        # the padded form of the same gradients: token row_map[r] of role ids gets gj[r]
+        want_full = torch.zeros(R, D, dtype=torch.float64)
+        for gj, _, flat, rm in grads.values():
+            live = rm >= 0
+            want_full.index_add_(0, flat[rm[live].long()], gj[live].double())
+        out_q.put((rank, bool(ok), shard_grad.numpy(), want_full.numpy(), int(n)))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_jagged_sharded_exchange_equals_unsharded():
+    """World 2 (gloo): the row-sharded tables on jagged rows (train.jagged_remaps over
+    ShardExchange's routing) read the same rows as an unsharded table at every span
+    row (padding rows for the dead capacity rows), and the owners receive the same
+    gradient sums as an unsharded dense backward of the padded batch."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_jagged_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] for r in res), 'jagged fetched rows differ from the unsharded table'
+    R, D = 97, 8
+    want = sum(r[3] for r in res)
+    want[0] = 0
+    got = np.zeros((R, D))
+    for rank, _, sg, _, _ in res:
+        got[rank::world] = sg
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5)
