@@ -101,6 +101,14 @@ def key_valid_from_mask(attn_mask, B, T):
     return kv.to(torch.uint8).contiguous()
 
 
+def _valid_bytes(token_type):
+    """uint8 [B, T] = token_type != 0: the bool bytes viewed as uint8 (0 / 1, no cast
+    kernel) in eager mode; a cast when traced (inductor cannot lower a bool -> uint8
+    dtype view)."""
+    kv = (token_type != 0).contiguous()
+    return kv.to(torch.uint8) if torch.compiler.is_compiling() else kv.view(torch.uint8)
+
+
 _UNIT_ROWS = {}
 
 
@@ -665,7 +673,7 @@ class BaselineModel(torch.nn.Module):
         if jagged is not None:
             kw = dict(key_valid=jagged.key_valid, seq_range=jagged.seq_range, row_base=jagged.row_base)
         else:
-            key_valid = (mask.to(dev, non_blocking=True) != 0).contiguous().view(torch.uint8)   # bool bytes are 0 / 1
+            key_valid = _valid_bytes(mask.to(dev, non_blocking=True))
             kw = dict(key_valid=key_valid, seq_range=torch.ops.grk.seq_ranges(key_valid))  # one launch serves every layer
         if timestamps is not None and self.block == 'hstu':
             kw['timestamps'] = timestamps.to(dev, torch.int64, non_blocking=True).contiguous()

@@ -232,6 +232,19 @@ def _trainer_batches(cfg):
     return batches
 
 
+def _permuted(batch, perm):
+    """The batch with its sequences in another order (every field along dim 0)."""
+    out = []
+    for x in batch:
+        if isinstance(x, torch.Tensor):
+            out.append(x[perm].contiguous())
+        elif isinstance(x, dict):
+            out.append({k: v[perm].contiguous() for k, v in x.items()})
+        else:
+            out.append(x)
+    return tuple(out)
+
+
 def _one_step_grads(state, jagged, batch):
     """Loss and every gradient (dense parameters; each table group's dense row
     gradient) of ONE bf16-autocast trainer step from the parameters ``state``."""
@@ -255,42 +268,59 @@ def _one_step_grads(state, jagged, batch):
 
 # Per-step bound of the bf16 jagged step against the padded one from identical
 # parameters.  The dead rows contribute exact zeros, so what differs is only the
-# fp32 summation order of the GEMMs / grk_wgrad over K = capacity vs B*T rows (and
-# the bf16 rounding that order can flip in autocast outputs).  Measured on MI355X
-# (round 4): see the test's printout.
-JAGGED_STEP_TOL = dict(loss=1e-5, grad=1e-3)
+# order of the sums over tokens (GEMM / grk_wgrad reductions over K = capacity vs
+# B*T rows, the chunked order of the projected-row backward) and the bf16 roundings
+# that order can flip in autocast outputs.  Measured on MI355X (round 4, the r4a
+# run): loss 6e-6; attention / LayerNorm / uvqk grads <= 3e-6, but itemdnn,
+# userdnn, emb_transform and the small tables 1e-3 .. 2.7e-3 -- the dnn weights'
+# gradients sum pos-item and neg-item terms of opposite sign (BCE at logits near 0),
+# so the sum is far smaller than its terms and any reordering is amplified.  The
+# bound is therefore set against the SAME padded step with the batch's sequences
+# permuted (mathematically identical, only the summation order differs): jagged
+# vs padded may not differ by more than REORDER_FACTOR x that reorder sensitivity
+# (or GRAD_FLOOR, whichever is larger), parameter by parameter.
+JAGGED_STEP_TOL = dict(loss=1e-5)
+REORDER_FACTOR, GRAD_FLOOR = 4.0, 1e-5
 
 
 def test_jagged_step_matches_padded_from_identical_parameters():
     """bf16 autocast HSTU (the bench's regime), dropout 0: from the SAME parameters,
     one jagged step's loss and every gradient against the padded step's, at the
     initial parameters and after 2 and 5 padded training steps, on batches of two
-    capacity buckets (reference loop: model/BaseLine/main.py:177-185)."""
+    capacity buckets (reference loop: model/BaseLine/main.py:177-185).  Each
+    gradient's bound is the padded step's own sensitivity to the order of the
+    batch's sequences (see JAGGED_STEP_TOL)."""
     from tencent_recommendation_2025_amd import jagged as J
     from tencent_recommendation_2025_amd.optim import FusedAdamW
     from tencent_recommendation_2025_amd.train import Trainer
     m, cfg = _model(*_TRAINER_CFG)
     batches = _trainer_batches(cfg)
     tr = Trainer(m, FusedAdamW(m, lr=1e-3, defer_period=4), loss='bce')
-    worst = {}
     done = 0
+    bad, worst_loss = {}, 0.0
     for trained, probe in ((0, 0), (2, 3), (5, 1)):
         while done < trained:
             tr.step(batches[done % 4])
             done += 1
         state = {k: v.detach().clone() for k, v in m.state_dict().items()}   # flushes deferred rows
-        lp, gp = _one_step_grads(state, False, batches[probe])
-        lj, gj = _one_step_grads(state, True, batches[probe])
-        assert set(gp) == set(gj)
+        batch = batches[probe]
+        perm = torch.arange(batch[0].shape[0] - 1, -1, -1, device=DEV)
+        lp, gp = _one_step_grads(state, False, batch)
+        lr_, gr = _one_step_grads(state, False, _permuted(batch, perm))
+        lj, gj = _one_step_grads(state, True, batch)
+        assert set(gp) == set(gj) == set(gr)
         errs = {k: nrel(gj[k].cpu(), gp[k].cpu()) for k in gp}
-        errs['loss'] = abs(lj - lp) / abs(lp)
-        print(f'after {trained} steps, batch {probe} (capacity {J.capacity_for(J.span_rows(batches[probe][3]), 128)}):',
-              f"loss {errs['loss']:.2e}", sorted(((k, f'{v:.2e}') for k, v in errs.items() if k != 'loss'),
-                                                 key=lambda kv: -float(kv[1]))[:6])
+        reorder = {k: nrel(gr[k].cpu(), gp[k].cpu()) for k in gp}
+        loss_err = abs(lj - lp) / abs(lp)
+        worst_loss = max(worst_loss, loss_err)
+        top = sorted(errs, key=lambda k: -errs[k])[:6]
+        print(f'after {trained} steps, batch {probe} (capacity {J.capacity_for(J.span_rows(batch[3]), 128)}):',
+              f'loss {loss_err:.2e} (reordered {abs(lr_ - lp) / abs(lp):.2e})',
+              [(k, f'{errs[k]:.2e}', f'reorder {reorder[k]:.2e}') for k in top])
         for k, v in errs.items():
-            worst[k] = max(worst.get(k, 0.0), v)
-    assert worst.pop('loss') < JAGGED_STEP_TOL['loss'], worst
-    bad = {k: v for k, v in worst.items() if v > JAGGED_STEP_TOL['grad']}
+            if v > max(REORDER_FACTOR * reorder[k], GRAD_FLOOR):
+                bad[(trained, k)] = (v, reorder[k])
+    assert worst_loss < JAGGED_STEP_TOL['loss'], worst_loss
     assert not bad, bad
 
 

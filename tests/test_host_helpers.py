@@ -272,3 +272,15 @@ def test_dense_flat_splits_runs_beyond_the_kernel_range_cap(monkeypatch):
     for p, q in zip(ps, twins):
         np.testing.assert_allclose(p.detach().numpy(), q.detach().numpy(), rtol=0,
                                    atol=4e-8 + 2e-7 * float(q.detach().abs().max()))
+
+
+def test_valid_bytes_eager_and_compiled():
+    """model._valid_bytes: the key-valid bytes of a token_type batch -- a bool -> uint8
+    view in eager mode, a cast when traced (round 4: inductor cannot lower the dtype view
+    of a bool tensor, which broke the reference's --use_torch_compile path)."""
+    from tencent_recommendation_2025_amd import model as M
+    tt = torch.tensor([[0, 0, 2, 1, 1], [0, 1, 1, 0, 1]], dtype=torch.int64)
+    want = (tt != 0).to(torch.uint8)
+    assert torch.equal(M._valid_bytes(tt), want)
+    got = torch.compile(lambda t: M._valid_bytes(t) + 0, backend='inductor', fullgraph=True)(tt)
+    assert got.dtype == torch.uint8 and torch.equal(got, want)
