@@ -180,10 +180,21 @@ __global__ void __launch_bounds__(256) k_gather_wave(FeatArgs args, int64_t num_
 // group row (sentinel for padding / out-of-range), payload = address of the
 // occurrence's gradient row.  The radix sort is stable, so after sorting the
 // payloads of one key are in occurrence order.
+// Blocks past key_blocks (first launch of a call only) zero the dense output
+// (16-byte words, grid-stride) and the unique-row count instead: the fill then
+// overlaps the key build instead of taking a launch of its own.
 template <typename I>
 __global__ void k_build_keys(LookupArgs la, int esize, const int32_t* __restrict__ token_type, int32_t T_len,
                              int64_t num_rows, int64_t padding_idx, unsigned* __restrict__ keys,
-                             unsigned long long* __restrict__ gptr, int32_t* err_flag) {
+                             unsigned long long* __restrict__ gptr, int32_t* err_flag, unsigned key_blocks,
+                             uint4* __restrict__ zero_dst, int64_t zero_vecs, int32_t* __restrict__ zero_count) {
+  if (blockIdx.x >= key_blocks) {
+    const int64_t stride = (int64_t)(gridDim.x - key_blocks) * blockDim.x;
+    for (int64_t v = (int64_t)(blockIdx.x - key_blocks) * blockDim.x + threadIdx.x; v < zero_vecs; v += stride)
+      zero_dst[v] = make_uint4(0, 0, 0, 0);
+    if (zero_count && blockIdx.x == key_blocks && threadIdx.x == 0) *zero_count = 0;
+    return;
+  }
   const int64_t o = la.occ_off[0] + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= la.occ_off[la.num]) return;
   int l = 0;
@@ -222,6 +233,22 @@ __global__ void k_segments(const unsigned* __restrict__ keys, const int* __restr
     seg_end[u] = (int)(i + 1);
     if (i == n - 1 || keys[i + 1] == sentinel) *count = u + 1;
   }
+}
+
+// Chunked dense mode with num_rows <= n: segment bounds indexed by the ROW
+// (seg_start[key], seg_end[key]) -- no segment numbering (head positions: three
+// launches) is needed when nothing is written per unique row.
+__global__ void k_segments_key(const unsigned* __restrict__ keys, int64_t n, unsigned sentinel,
+                               int* __restrict__ seg_start, int* __restrict__ seg_end, int32_t* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const unsigned k = keys[i];
+  if (k == sentinel) return;
+  if (i == 0 || keys[i - 1] != k) {
+    seg_start[k] = (int)i;
+    atomicAdd(count, 1);
+  }
+  if (i == n - 1 || keys[i + 1] != k) seg_end[k] = (int)(i + 1);
 }
 
 // ------------------------------------------------- segmented reduction ----
@@ -461,7 +488,7 @@ __device__ __forceinline__ void seg_chunks_wave_body(int64_t chunk, int lane, co
   for (int k = 0; k < KP; ++k) {
     const int64_t i = p0 + k * 64 + lane;
     kr[k] = i < p1 ? keys[i] : sentinel;
-    pr[k] = i < p1 ? pos[i] : 0;
+    pr[k] = i < p1 && pos ? pos[i] : 0;   // null pos: key-indexed segments, nothing stored per unique row
     const unsigned long long g = i < p1 ? gptr[i] : g0;
     glo[k] = (unsigned)g;
     ghi[k] = (unsigned)(g >> 32);
@@ -651,8 +678,9 @@ __global__ void __launch_bounds__(256) k_seg_partials_combine(const unsigned* __
   if (pb >= n) return;
   const unsigned key = keys[pb];
   if (key == sentinel || keys[pb - 1] != key) return;
-  const int u = pos[pb] - 1;
-  const int su = seg_start[u], eu = seg_end[u];
+  const int u = pos ? pos[pb] - 1 : 0;
+  const int seg = pos ? u : (int)key;   // null pos: segment bounds indexed by row
+  const int su = seg_start[seg], eu = seg_end[seg];
   if (su / CH != b - 1) return;  // crosses an earlier edge: combined there
   const int64_t last = (eu - 1) / CH;
   const int c = lane * LW;
@@ -1102,13 +1130,19 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
   plan_ws(total, num_rows, dim, base, &ws);
   hipStream_t s = (hipStream_t)stream;
-  GRK_CHECK_HIP(zero_async(uniq_count, sizeof(int32_t), s));
-  if (dense_out) GRK_CHECK_HIP(zero_async(dense_out, (size_t)num_rows * dim * sizeof(float), s));
-  if (dense_out16) GRK_CHECK_HIP(zero_async(dense_out16, (size_t)num_rows * dim * sizeof(bf16_t), s));
+  void* dense_any = dense_out ? (void*)dense_out : (void*)dense_out16;
+  const size_t dense_bytes = (size_t)num_rows * dim * (dense_out ? sizeof(float) : sizeof(bf16_t));
+  // the zero fill rides on the first key-build launch (16-byte aligned outputs; else a fill kernel)
+  const bool fused_zero = total > 0 && (!dense_any || ((uintptr_t)dense_any % 16 == 0 && dense_bytes % 16 == 0));
+  if (!fused_zero) {
+    GRK_CHECK_HIP(zero_async(uniq_count, sizeof(int32_t), s));
+    if (dense_any) GRK_CHECK_HIP(zero_async(dense_any, dense_bytes, s));
+  }
   if (total == 0) return GRK_OK;
   const int B = 256;
   const int esize = grad_dtype == GRK_F32 ? 4 : 2;
   int64_t occ = 0;
+  bool first_launch = true;
   for (int first = 0; first < num_lookups; first += kLookupsPerLaunch) {
     LookupArgs la;
     memset(&la, 0, sizeof(la));
@@ -1122,13 +1156,19 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
     const int64_t cnt = occ - la.occ_off[0];
     if (cnt == 0) continue;
     const unsigned g = (unsigned)((cnt + B - 1) / B);
+    const bool zero_here = fused_zero && first_launch;
+    const int64_t zvecs = zero_here && dense_any ? (int64_t)(dense_bytes / 16) : 0;
+    const unsigned gz = zero_here ? (unsigned)grid_for(zvecs > 0 ? zvecs : 1, B, 2048) : 0;
+    uint4* zdst = zvecs ? (uint4*)dense_any : nullptr;
+    int32_t* zcnt = zero_here ? uniq_count : nullptr;
     if (itype == GRK_I64)
-      k_build_keys<int64_t><<<g, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
-                                            ws.gptr_in, err_flag);
+      k_build_keys<int64_t><<<g + gz, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
+                                                 ws.gptr_in, err_flag, g, zdst, zvecs, zcnt);
     else
-      k_build_keys<int32_t><<<g, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
-                                            ws.gptr_in, err_flag);
+      k_build_keys<int32_t><<<g + gz, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
+                                                 ws.gptr_in, err_flag, g, zdst, zvecs, zcnt);
     GRK_LAUNCH_CHECK();
+    first_launch = false;
   }
   const int g = (int)((total + B - 1) / B);
   unsigned end_bit = 1;
@@ -1143,13 +1183,21 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   ws.keys_out = skeys;  // the sorted pairs (either buffer of the ping-pong)
   ws.gptr_out = sgptr;
   const unsigned sentinel = (unsigned)num_rows;
-  {
+  // chunked mode writing only the dense rows: segment bounds by row, no numbering
+  const bool by_key = flags == GRK_BWD_CHUNKED && !uniq_ids && !uniq_rows && !row_slot && num_rows <= total;
+  const int lw0 = dim % 64 == 0 ? dim / 64 : 0;
+  const bool wave_path = (grad_dtype == GRK_BF16 && lw0 == 8) || (grad_dtype != GRK_BF16 && (lw0 == 4 || lw0 == 8));
+  if (by_key && wave_path) {
+    k_segments_key<<<g, B, 0, s>>>(ws.keys_out, total, sentinel, ws.seg_start, ws.seg_end, uniq_count);
+    GRK_LAUNCH_CHECK();
+    ws.pos = nullptr;
+  } else {
     const int rc = head_positions(ws.keys_out, total, sentinel, ws.pos, ws.scan_tmp, s);
     if (rc) return rc;
+    k_segments<<<g, B, 0, s>>>(ws.keys_out, ws.pos, total, sentinel, ws.seg_start, ws.seg_end, ws.seg_key, uniq_ids,
+                               uniq_count);
+    GRK_LAUNCH_CHECK();
   }
-  k_segments<<<g, B, 0, s>>>(ws.keys_out, ws.pos, total, sentinel, ws.seg_start, ws.seg_end, ws.seg_key, uniq_ids,
-                             uniq_count);
-  GRK_LAUNCH_CHECK();
   const int vec = grad_dtype == GRK_BF16 ? 8 : 4;
   const int tpr = dim / vec;
   const int groups = tpr >= 256 ? 1 : 256 / tpr;

@@ -78,7 +78,9 @@ def jagged_remaps(remaps, parts, row_map):
         if v is None:   # a derived role (feat2emb_pair's 'pair' is rebuilt from pos / neg)
             continue
         pad = torch.argmax((v().reshape(-1) == 0).to(torch.int8))   # first padding position (0 if none)
-        out[key] = (ref, torch.where(rm >= 0, flat[src], flat[pad]).unsqueeze(0))
+        # index_select with a 1-element index: flat[pad] with a 0-d tensor would read it on
+        # the host (a sync, illegal while the step is being captured)
+        out[key] = (ref, torch.where(rm >= 0, flat[src], flat.index_select(0, pad.reshape(1))).unsqueeze(0))
     return out
 
 

@@ -3,13 +3,9 @@ flat buffer, updated by grk's multi-range AdamW (k_adamw_ranges) instead of
 torch's fused AdamW.  Opt-in until it has run on hardware (written in round 3
 after gpurun closed; GRK_DENSE_FLAT_TESTS=1).
 
-Against the default optimizer on the same batches: step 1 sees the same
-parameters, so its loss is the same bits; the element updates differ by the
-hardware sqrt / reciprocal (a few ulp of the lr-sized update), so
-after three steps the dense parameters agree to 1e-5 normwise with at most 0.1 %
-of the elements (or 8) more than 1e-6 apart (a near-zero gradient's m / sqrt(v)
-can flip), none by more than 2 lr x steps; first moments 1e-4 normwise; losses 1e-5.  Graph replay == eager,
-bit for bit, as for the default optimizer."""
+Against torch's fused AdamW driven by the same gradients (the element updates
+differ by the hardware sqrt / reciprocal only); graph replay ==
+eager, bit for bit, as for the default optimizer."""
 import os
 
 import pytest
@@ -48,22 +44,56 @@ def _run(dense_flat, graph, steps=3):
 
 
 def test_dense_flat_tracks_torch_fused_adamw():
-    la, pa, ma = _run(False, False)
-    lb, pb, mb = _run(True, False)
-    assert torch.equal(la[0], lb[0])
-    assert float(((la - lb).abs() / la.abs()).max()) < 1e-5, (la, lb)
-    assert pa.keys() == pb.keys()
+    """Driven by IDENTICAL gradients (model A's backward each step, copied into model
+    B's dense parameters), the flat multi-range AdamW (B) and torch's fused AdamW (A)
+    differ only by the element update's rounding (hardware sqrt / reciprocal,
+    DESIGN.md §7): after 3 steps every dense parameter within steps * lr * 2^-12 of
+    A's, element by element, and 1e-6 normwise; both moments 1e-6 normwise.  (Comparing two free-running trajectories instead,
+    as round 3 did, measures Adam's sign flips on near-zero gradients, not the kernel.)"""
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    cfg = S.SyntheticConfig(batch_size=8, maxlen=30, num_items=5000, num_users=700, min_len=4)
+    stats, types = S.feature_schema(cfg)
+    args = S.make_args(hidden_units=64, maxlen=30, num_blocks=2, num_heads=2)
     lr, steps = 2e-3, 3
-    for n in pa:
-        d = (pa[n] - pb[n]).abs()
-        # Adam's m / sqrt(v) turns the later steps' rounding noise on a near-zero gradient
-        # into up to a full +-lr step (as in the world-2 test): a few elements may move
-        assert float(d.norm() / max(float(pa[n].norm()), 1e-30)) < 1e-5, n
-        assert int((d > 1e-6).sum()) <= max(8, d.numel() // 1000) and float(d.max()) <= 2 * lr * steps, n
-    assert mb and set(mb) <= set(ma)
-    for n in mb:
-        ref = ma[n].float()
-        assert float((mb[n] - ref).norm() / max(float(ref.norm()), 1e-30)) < 1e-4, n
+    models, opts = [], []
+    for flat in (False, True):
+        torch.manual_seed(0)
+        m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, args).to(DEV)
+        models.append(m)
+        opts.append(FusedAdamW(m, lr=lr, dense_flat=flat))
+    (ma, mb), (oa, ob) = models, opts
+    assert ob._flat is not None and len(ob._flat.params) > 0
+    tr = Trainer(ma, oa, loss='bce')
+    g = torch.Generator(device=DEV).manual_seed(0)
+    for _ in range(steps):
+        batch = S.make_batch(cfg, g, DEV)
+        oa.zero_grad()
+        ob.zero_grad()
+        oa.begin_step(batch)
+        tr.compute_loss(batch).backward()
+        for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+            if pa.requires_grad and pa.grad is not None:
+                pb.grad = pa.grad.detach().clone()
+        oa.step()
+        ob.step()
+    torch.cuda.synchronize()
+    flat_ids = {id(p) for p in ob._flat.params}
+    checked = 0
+    for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+        if id(pb) not in flat_ids:
+            continue
+        checked += 1
+        d = (pa.detach() - pb.detach()).abs()
+        assert float(d.max()) <= steps * lr * 2 ** -12, (n, float(d.max()))
+        assert float(d.norm() / max(float(pa.norm()), 1e-30)) < 1e-6, n
+        sa, sb = oa.dense.state[pa], ob._flat.state(pb)
+        for key in ('exp_avg', 'exp_avg_sq'):
+            ref = sa[key]
+            assert float((ref - sb[key]).norm() / max(float(ref.norm()), 1e-30)) < 1e-6, (n, key)
+    assert checked == len(ob._flat.params)
 
 
 def test_dense_flat_graph_replay_equals_eager():
