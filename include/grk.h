@@ -299,9 +299,7 @@ typedef struct grk_attn_args {
                                       product as hi*hi + hi*lo + lo*hi; q/k/v then
                                       have dtype qkv_dtype (whole-sequence kernels,
                                       and head_dim 256 / 512 in the wide-head
-                                      kernels when GRK_ATTN_WIDE_FIDELITY is set -- opt-in
-                                      until hardware-tested; GRK_EUNSUPPORTED
-                                      elsewhere)                                 */
+                                      kernels; GRK_EUNSUPPORTED elsewhere)       */
   uint64_t seed;                   /* dropout stream                              */
   int32_t out_dtype;               /* GRK_F32 / GRK_BF16 for out, dq, dk, dv      */
   int32_t act;                     /* GRK_ACT_*: activation applied to q/k/v      */
@@ -322,10 +320,8 @@ typedef struct grk_attn_args {
                                       bf16 MFMA over the exactly widened values;
                                       head_dim 64 / 128, no time bias; 8-byte
                                       aligned, ld in elements (= bytes)         */
-  /* HSTU time bias (SURVEY §8 a9 rab_time; whole-sequence kernels, and the
-   * chunked and wide-head kernels when the environment sets
-   * GRK_ATTN_CHUNKED_TIME -- opt-in until their parity has run on hardware,
-   * GRK_EUNSUPPORTED otherwise; not with fp8 q/k/v):
+  /* HSTU time bias (SURVEY §8 a9 rab_time; whole-sequence, chunked and
+   * wide-head kernels; not with fp8 q/k/v):
    * S[i,j] += rab_t[h, tb(ts[i] - ts[j])] with
    * tb(d) = min(2 l + h1, num_time_buckets - 1), l = floor(log2(|d| + 1)),
    * h1 = the bit below the leading one of |d| + 1 (0 when l = 0): half-octave
@@ -355,7 +351,7 @@ typedef struct grk_attn_args {
 
 /* 1 when grk_attention_* with precise == 2 (fp32 fidelity) runs for this
  * sequence length and head_dim (the whole-sequence kernels' LDS; head_dim 256
- * and 512 at any length with GRK_ATTN_WIDE_FIDELITY set), else 0. */
+ * and 512 at any length), else 0. */
 int grk_attention_fidelity_supported(int seq_len, int head_dim);
 
 /* ranges int32 [batch, 3]: ranges[b][0] = first j with key_valid[b, j] (T for

@@ -9,9 +9,9 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 FAULT='illegal memory access|memory access fault|HSA_STATUS_ERROR|hipErrorIllegalAddress|HW Exception|GPU Hang|page not present'
 PYT="python -u -m pytest -v -rs --timeout 200 --timeout-method thread"
-env GRK_MERGE_PROJ_TESTS=1 GRK_DENSE_FLAT_TESTS=1 GRK_SHARDED_JAGGED_TESTS=1 timeout -k 10 400 $PYT \
-  tests/test_gpu_embedding.py tests/test_gpu_wgrad.py tests/test_gpu_dense_flat.py tests/test_gpu_sharding.py \
-  tests/test_gpu_jagged.py > gpurun_out/r4c_tests.log 2>&1
+env GRK_MERGE_PROJ_TESTS=1 GRK_DENSE_FLAT_TESTS=1 GRK_SHARDED_JAGGED_TESTS=1 timeout -k 10 600 $PYT \
+  tests/test_gpu_embedding.py tests/test_gpu_wgrad.py tests/test_gpu_dense_flat.py tests/test_gpu_jagged.py \
+  tests/test_gpu_attention.py tests/test_gpu_model.py tests/test_gpu_sharding.py > gpurun_out/r4c_tests.log 2>&1
 rc=$?; echo "tests rc=$rc" | tee -a gpurun_out/r4c_tests.log
 grep -Eqi "$FAULT" gpurun_out/r4c_tests.log && { echo "GPU fault -- stopping"; exit 3; }
 case $rc in 0|1) ;; *) exit $rc ;; esac

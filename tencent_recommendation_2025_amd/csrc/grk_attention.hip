@@ -525,13 +525,6 @@ static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
               "fit them", p.T, hd);
     return GRK_EUNSUPPORTED;
   }
-  // The chunked and wide kernels' time bias (TB instantiations) is built but refused
-  // until its parity test has run on hardware (GRK_ATTN_CHUNKED_TIME=1 opts in).
-  if (p.nbt > 0 && which != 1 && !getenv("GRK_ATTN_CHUNKED_TIME")) {
-    set_error("the HSTU time bias runs in the whole-sequence kernels only: T = %d x head_dim %d does not fit them",
-              p.T, hd);
-    return GRK_EUNSUPPORTED;
-  }
   if (p.precise == 2 && which != 1 && hd <= 128) {
     set_error("fp32-fidelity attention (precise = 2) runs in the whole-sequence kernels only: T = %d x head_dim %d "
               "does not fit their LDS", p.T, hd);

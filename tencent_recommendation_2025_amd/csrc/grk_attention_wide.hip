@@ -27,9 +27,8 @@ namespace grk {
 
 bool wide_fidelity_enabled(int hd) {
   // head_dim 256 and 512 (512: the partial products meet in rounds, WideF);
-  // written in round 3 without hardware: opt-in until its parity test has
-  // run on an MI355X
-  return (hd == 256 || hd == 512) && getenv("GRK_ATTN_WIDE_FIDELITY") != nullptr;
+  // parity vs the fp64 oracle verified on MI355X in round 4
+  return hd == 256 || hd == 512;
 }
 
 // grk_attention_wide_fid.hip

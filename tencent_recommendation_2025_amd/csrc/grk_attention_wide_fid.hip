@@ -1,6 +1,6 @@
 // fp32-fidelity (precise = 2) wide-head attention, head_dim 256 / 512: the FID
 // instantiations of grk_attention_wide_kernels.h in a translation unit of
-// their own (see there).  Opt-in (wide_fidelity_enabled, GRK_ATTN_WIDE_FIDELITY)
+// their own (see there).  Selected by wide_fidelity_enabled (head_dim 256 / 512)
 // until the parity test has run on hardware.
 #include "grk_attention_wide_kernels.h"
 

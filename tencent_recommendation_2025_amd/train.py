@@ -238,8 +238,15 @@ class Trainer:
             # GEMM plans tuned (one eager step of that shape)
             if warm < (self.graph_warmup if not self._graphs else 1):
                 # warm-up on the stream the capture will use: GEMM plans tuned,
-                # per-stream workspaces and the caching allocator's blocks in place
+                # per-stream workspaces and the caching allocator's blocks in place.
+                # Row-sharded: on the current stream -- its collectives must never run
+                # on the capture stream (the process group's watchdog polls their
+                # events; polling one recorded on a stream that is now capturing is
+                # fatal, seen when a second capacity was warmed up and captured at
+                # once); the capture stream gets its GEMM workspace in _capture.
                 self._warm[key] = warm + 1
+                if self._sharded:
+                    return self.eager_step(batch, next_batch)
                 return self._on_side(lambda: self.eager_step(batch, next_batch))
             return self._capture(batch, next_batch, key)
         self._g, self._static, self._static_loss = entry
@@ -278,6 +285,10 @@ class Trainer:
 
     def _capture(self, batch, next_batch=None, key=None):
         """Record one step (host state advances once here), then replay it for this batch."""
+        if self._side is None:
+            self._side = private_stream(torch.cuda.current_stream().device)
+        if self._sharded:
+            _gemm_stream_ready(self._side)
         self._static = _clone_batch(batch)
         self.opt.zero_grad(set_to_none=True)
         if self._sharded:  # exchange eagerly, capture forward + backward only
@@ -325,6 +336,18 @@ class Trainer:
             self.opt.capture_state()
             self.opt.step()
         return self._static_loss.clone()
+
+
+def _gemm_stream_ready(stream):
+    """grk_gemm allocates its per-stream hipBLASLt workspace on a stream's first GEMM,
+    which must not happen inside a capture: one tiny GEMM on ``stream`` first."""
+    from . import kernels as K
+    cur = torch.cuda.current_stream()
+    stream.wait_stream(cur)
+    with torch.cuda.stream(stream):
+        a = torch.zeros(16, 16, dtype=torch.bfloat16, device=cur.device)
+        K.gemm(a, a, trans_b=True)
+    cur.wait_stream(stream)
 
 
 _NODE_TYPES = {0: 'kernel', 1: 'memcpy', 2: 'memset', 3: 'host', 4: 'graph', 5: 'empty', 6: 'wait_event',

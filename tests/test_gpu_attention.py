@@ -450,36 +450,26 @@ def test_wide_head_masked_rows_and_fast_mode(K):
         assert nrel(res[key], want[key]) < TOL_FAST, key
 
 
-def test_wide_head_rejects_fidelity_mode(K):
-    from tencent_recommendation_2025_amd import _lib as L
-    assert not K.fidelity_supported(101, 512)
-    assert not K.fidelity_supported(101, 256)   # opt-in (GRK_ATTN_WIDE_FIDELITY) until hardware-tested
-    x = torch.zeros(64, 3 * 512, device=DEV)
-    kv = torch.ones(2, 32, dtype=torch.uint8, device=DEV)
-    args = K.attn_args(L.ATTN_SOFTMAX, x[:, :512], x[:, 512:1024], x[:, 1024:], 2, 32, 1, 512, key_valid=kv,
-                       precise=2, out_dtype=torch.float32)
-    with pytest.raises(RuntimeError, match='head_dim 512'):
-        K.attention_fwd(args, torch.empty(64, 512, device=DEV), torch.empty(2, 1, 32, device=DEV))
+def test_wide_head_fidelity_mode_supported():
+    """fp32 fidelity at head_dim 256 / 512 (the wide kernels' FID instantiations,
+    hardware-verified in round 4): supported at any length; other widths beyond the
+    whole-sequence LDS are refused."""
+    from tencent_recommendation_2025_amd import kernels as K
+    assert K.fidelity_supported(101, 512) and K.fidelity_supported(3000, 256)
+    assert not K.fidelity_supported(3000, 64)
 
 
 # fp32 fidelity at head_dim 256 / 512 (grk_attention_wide_fid.hip): written in round 3
-# without hardware; the library takes it only with GRK_ATTN_WIDE_FIDELITY set,
-# and this parity test is opt-in (GRK_WIDE_FIDELITY_TESTS=1) until it has run.
-WIDE_FIDELITY = pytest.mark.skipif(os.environ.get('GRK_WIDE_FIDELITY_TESTS') != '1',
-                                   reason='wide-head fp32 fidelity: opt-in until verified on hardware')
-
-
-@WIDE_FIDELITY
+# without hardware, verified on MI355X in round 4 (this test, then default).
 @pytest.mark.parametrize('in_dtype', [torch.float32, torch.float16], ids=['f32', 'f16'])
 @pytest.mark.parametrize('H,T,lens', [(1, 102, [102, 60, 7]), (2, 201, [201, 33])])
 @pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
 @pytest.mark.parametrize('hd', [256, 512])
-def test_wide_fidelity_matches_fp64_oracle(K, monkeypatch, hd, kind, H, T, lens, in_dtype):
+def test_wide_fidelity_matches_fp64_oracle(K, hd, kind, H, T, lens, in_dtype):
     """precise=2 at head_dim 256 / 512 (O1's num_heads=1 at hidden 256 / 512): Q/K/V /
     dO read exactly and split into bf16 hi + lo, every product hi*hi + hi*lo + lo*hi,
     against the fp64 oracle on the unrounded inputs (the narrow kernels' bound).  At
     512 the waves' partial products meet in four rounds (WideF)."""
-    monkeypatch.setenv('GRK_ATTN_WIDE_FIDELITY', '1')
     assert K.fidelity_supported(T, hd)
     res, want = run_fidelity(K, kind, len(lens), T, H, hd, lens, in_dtype, seed=T + H,
                              act='silu' if kind == 1 else None)
@@ -527,22 +517,14 @@ def test_time_bias_outside_whole_sequence_kernels_is_refused(K):
 
 
 # The chunked kernels (T beyond the whole-sequence kernels' LDS) and the wide-head
-# kernels (head_dim 256 / 512) carry the time bias in their TB instantiations.
-# Built in round 3 without hardware: the library refuses it unless
-# GRK_ATTN_CHUNKED_TIME is set, and this parity test is opt-in
-# (GRK_CHUNKED_TIME_TESTS=1) until it has run on an MI355X.
-CHUNKED_TIME = pytest.mark.skipif(os.environ.get('GRK_CHUNKED_TIME_TESTS') != '1',
-                                  reason='chunked-kernel time bias: opt-in until verified on hardware')
-
-
-@CHUNKED_TIME
+# kernels (head_dim 256 / 512) carry the time bias in their TB instantiations
+# (written in round 3 without hardware, verified on MI355X in round 4).
 @pytest.mark.parametrize('hd,H,T,lens,act,nbt', [(64, 2, 300, [300, 170, 20], 'silu', 48),
                                                  (128, 1, 1025, [1025, 600], None, 64),
                                                  (32, 4, 260, [260, 3], None, 16),
                                                  (256, 1, 150, [150, 90, 7], 'silu', 32),
                                                  (512, 2, 70, [70, 33], None, 16)])
-def test_time_bias_chunked_and_wide_kernels_match_oracle(K, monkeypatch, hd, H, T, lens, act, nbt):
-    monkeypatch.setenv('GRK_ATTN_CHUNKED_TIME', '1')
+def test_time_bias_chunked_and_wide_kernels_match_oracle(K, hd, H, T, lens, act, nbt):
     res, want, _ = run(K, 1, B=len(lens), T=T, H=H, hd=hd, lens=lens, precise=True, nbt=nbt, act=act, seed=T)
     for key in ('out', 'dq', 'dk', 'dv', 'drab', 'drab_t'):
         err = nrel(res[key], want[key])
@@ -553,13 +535,6 @@ def test_time_bias_chunked_and_wide_kernels_match_oracle(K, monkeypatch, hd, H, 
     for key in res:
         if key != 'lse':
             assert np.array_equal(res[key], again[key]), key
-
-
-def test_time_bias_wide_heads_refused_unless_opted_in(K):
-    """head_dim 256 / 512 (the wide-head kernels): refused like the chunked kernels'
-    time bias until GRK_ATTN_CHUNKED_TIME opts in."""
-    with pytest.raises(RuntimeError, match='whole-sequence'):
-        run(K, 1, B=1, T=64, H=1, hd=256, lens=[50], precise=True, nbt=16, oracle=False)
 
 
 # ----------------------------------------------------------- fp8 (C5) ----

@@ -260,14 +260,11 @@ def test_o1_single_head_wide_matches_oracle(golden, hidden):
     assert checked > 20
 
 
-@pytest.mark.skipif(os.environ.get('GRK_WIDE_FIDELITY_TESTS') != '1',
-                    reason='wide-head fp32 fidelity: opt-in until verified on hardware')
 @pytest.mark.parametrize('hidden', [256, 512])
-def test_o1_single_head_wide_fidelity_matches_oracle(golden, monkeypatch, hidden):
-    """hidden 256 / 512, num_heads 1 with the wide-head fp32-fidelity kernels
-    (GRK_ATTN_WIDE_FIDELITY): the drop-in fp32 step at the narrow heads' bounds,
-    logits 1e-5 and gradients 1e-4 vs the fp32 CPU restatement."""
-    monkeypatch.setenv('GRK_ATTN_WIDE_FIDELITY', '1')
+def test_o1_single_head_wide_fidelity_matches_oracle(golden, hidden):
+    """hidden 256 / 512, num_heads 1 (O1's default, model/BaseLineO1/main.py:45) on
+    the wide-head fp32-fidelity kernels: the drop-in fp32 step at the narrow heads'
+    bounds, logits 1e-5 and gradients 1e-4 vs the fp32 CPU restatement."""
     torch.manual_seed(0)
     m, g, batch, args, d, stats = build(golden, 'o1', hidden_units=hidden, num_heads=1)
     ref = model_ref.RefBaselineModel(int(d['usernum']), int(d['itemnum']), stats, feat_types(), args, variant='o1')
