@@ -180,38 +180,71 @@ __global__ void __launch_bounds__(256) k_gather_wave(FeatArgs args, int64_t num_
 // group row (sentinel for padding / out-of-range), payload = address of the
 // occurrence's gradient row.  The radix sort is stable, so after sorting the
 // payloads of one key are in occurrence order.
-// Blocks past key_blocks (first launch of a call only) zero the dense output
-// (16-byte words, grid-stride) and the unique-row count instead: the fill then
-// overlaps the key build instead of taking a launch of its own.
+// Keys are built in tiles of kKeyTile occurrences per 256-thread block (4 per
+// thread), the radix sort's tile: with hist0 the block also counts the first
+// digit (bits 0-7) of its keys into hist0[digit][tile], the sort's first
+// histogram (grk_sort.hip), so that pass needs no launch of its own.
+// Blocks past key_blocks (first launch of a call only) instead zero the dense
+// output (16-byte words, grid-stride) and the unique-row count, and fill the
+// row-indexed segment bounds (INT_MAX / 0): those fills then overlap the key
+// build instead of taking launches of their own.
+constexpr int kKeyTile = 1024;
+struct KeyFill {
+  uint4* zero_dst;
+  int64_t zero_vecs;
+  int32_t* zero_count;
+  int* seg_start;   // filled with INT_MAX
+  int* seg_end;     // filled with 0
+  int64_t seg_n;
+};
 template <typename I>
-__global__ void k_build_keys(LookupArgs la, int esize, const int32_t* __restrict__ token_type, int32_t T_len,
-                             int64_t num_rows, int64_t padding_idx, unsigned* __restrict__ keys,
-                             unsigned long long* __restrict__ gptr, int32_t* err_flag, unsigned key_blocks,
-                             uint4* __restrict__ zero_dst, int64_t zero_vecs, int32_t* __restrict__ zero_count) {
+__global__ void __launch_bounds__(256) k_build_keys(LookupArgs la, int esize, const int32_t* __restrict__ token_type,
+                                                    int32_t T_len, int64_t num_rows, int64_t padding_idx,
+                                                    unsigned* __restrict__ keys, unsigned long long* __restrict__ gptr,
+                                                    int32_t* err_flag, unsigned key_blocks,
+                                                    unsigned* __restrict__ hist0, int ntiles, KeyFill fill) {
   if (blockIdx.x >= key_blocks) {
-    const int64_t stride = (int64_t)(gridDim.x - key_blocks) * blockDim.x;
-    for (int64_t v = (int64_t)(blockIdx.x - key_blocks) * blockDim.x + threadIdx.x; v < zero_vecs; v += stride)
-      zero_dst[v] = make_uint4(0, 0, 0, 0);
-    if (zero_count && blockIdx.x == key_blocks && threadIdx.x == 0) *zero_count = 0;
+    const int64_t nb = gridDim.x - key_blocks, t = (int64_t)(blockIdx.x - key_blocks) * blockDim.x + threadIdx.x;
+    const int64_t stride = nb * blockDim.x;
+    for (int64_t v = t; v < fill.zero_vecs; v += stride) fill.zero_dst[v] = make_uint4(0, 0, 0, 0);
+    for (int64_t v = t; v < fill.seg_n; v += stride) {
+      fill.seg_start[v] = 0x7FFFFFFF;
+      fill.seg_end[v] = 0;
+    }
+    if (fill.zero_count && t == 0) *fill.zero_count = 0;
     return;
   }
-  const int64_t o = la.occ_off[0] + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= la.occ_off[la.num]) return;
-  int l = 0;
-  while (l + 1 < la.num && o >= la.occ_off[l + 1]) ++l;
-  const grk_lookup& L = la.l[l];
-  const int64_t rel = o - la.occ_off[l];
-  const int64_t n = rel / L.bag;
-  const int a = (int)(rel - n * L.bag);
-  const int64_t row = resolve_row(reinterpret_cast<const I*>(L.idx), n, a, L.idx_ld, L.idx_mode, token_type, T_len);
-  unsigned key = (unsigned)num_rows;  // sentinel: sorts after every real row
-  if (row < 0 || row >= L.table_rows || L.row_offset + row >= num_rows) {
-    if (err_flag) *err_flag = 1;
-  } else if (row != padding_idx) {
-    key = (unsigned)(L.row_offset + row);
+  __shared__ unsigned cnt[256];
+  if (hist0) {
+    cnt[threadIdx.x] = 0;
+    __syncthreads();
   }
-  keys[o] = key;
-  gptr[o] = (unsigned long long)((const char*)L.grad + (n * L.grad_ld + L.grad_col) * esize);
+  const int64_t end = la.occ_off[la.num];
+#pragma unroll
+  for (int rd = 0; rd < kKeyTile / 256; ++rd) {
+    const int64_t o = la.occ_off[0] + (int64_t)blockIdx.x * kKeyTile + rd * 256 + threadIdx.x;
+    if (o >= end) break;
+    int l = 0;
+    while (l + 1 < la.num && o >= la.occ_off[l + 1]) ++l;
+    const grk_lookup& L = la.l[l];
+    const int64_t rel = o - la.occ_off[l];
+    const int64_t n = rel / L.bag;
+    const int a = (int)(rel - n * L.bag);
+    const int64_t row = resolve_row(reinterpret_cast<const I*>(L.idx), n, a, L.idx_ld, L.idx_mode, token_type, T_len);
+    unsigned key = (unsigned)num_rows;  // sentinel: sorts after every real row
+    if (row < 0 || row >= L.table_rows || L.row_offset + row >= num_rows) {
+      if (err_flag) *err_flag = 1;
+    } else if (row != padding_idx) {
+      key = (unsigned)(L.row_offset + row);
+    }
+    keys[o] = key;
+    gptr[o] = (unsigned long long)((const char*)L.grad + (n * L.grad_ld + L.grad_col) * esize);
+    if (hist0) atomicAdd(&cnt[key & 255u], 1u);
+  }
+  if (hist0) {
+    __syncthreads();
+    hist0[(int64_t)threadIdx.x * ntiles + blockIdx.x] = cnt[threadIdx.x];
+  }
 }
 
 __global__ void k_segments(const unsigned* __restrict__ keys, const int* __restrict__ pos, int64_t n,
@@ -233,22 +266,6 @@ __global__ void k_segments(const unsigned* __restrict__ keys, const int* __restr
     seg_end[u] = (int)(i + 1);
     if (i == n - 1 || keys[i + 1] == sentinel) *count = u + 1;
   }
-}
-
-// Chunked dense mode with num_rows <= n: segment bounds indexed by the ROW
-// (seg_start[key], seg_end[key]) -- no segment numbering (head positions: three
-// launches) is needed when nothing is written per unique row.
-__global__ void k_segments_key(const unsigned* __restrict__ keys, int64_t n, unsigned sentinel,
-                               int* __restrict__ seg_start, int* __restrict__ seg_end, int32_t* __restrict__ count) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const unsigned k = keys[i];
-  if (k == sentinel) return;
-  if (i == 0 || keys[i - 1] != k) {
-    seg_start[k] = (int)i;
-    atomicAdd(count, 1);
-  }
-  if (i == n - 1 || keys[i + 1] != k) seg_end[k] = (int)(i + 1);
 }
 
 // ------------------------------------------------- segmented reduction ----
@@ -927,8 +944,10 @@ __global__ void __launch_bounds__(256) k_seg_wave_fused(int64_t nhot, int nslice
 // ------------------------------------------------------------ workspace ----
 // Stable radix sort of (row key, gradient-row address) pairs (grk_sort.hip).
 size_t sort_pairs_workspace(int64_t n);
+unsigned* sort_pairs_hist0(void* ws);
 int sort_pairs(unsigned* k0, unsigned long long* v0, unsigned* k1, unsigned long long* v1, int64_t n, int end_bit,
-               void* ws, unsigned** kres, unsigned long long** vres, hipStream_t s);
+               void* ws, unsigned** kres, unsigned long long** vres, hipStream_t s, bool hist0_ready,
+               const SortSegments* seg);
 // Segment index of every sorted entry (inclusive count of row heads).
 size_t head_positions_workspace(int64_t n);
 int head_positions(const unsigned* keys, int64_t n, unsigned sentinel, int* pos, void* ws, hipStream_t s);
@@ -1141,6 +1160,16 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   if (total == 0) return GRK_OK;
   const int B = 256;
   const int esize = grad_dtype == GRK_F32 ? 4 : 2;
+  const unsigned sentinel = (unsigned)num_rows;
+  // chunked mode writing only the dense rows: segment bounds by row (recorded by the
+  // sort's last pass), no segment numbering (head positions) at all
+  const int lw0 = dim % 64 == 0 ? dim / 64 : 0;
+  const bool wave_path = (grad_dtype == GRK_BF16 && lw0 == 8) || (grad_dtype != GRK_BF16 && (lw0 == 4 || lw0 == 8));
+  const bool by_key = wave_path && flags == GRK_BWD_CHUNKED && !uniq_ids && !uniq_rows && !row_slot &&
+                      num_rows <= total;
+  // one key-build launch (<= kLookupsPerLaunch lookups): it also counts the sort's first digit
+  const bool one_launch = num_lookups <= kLookupsPerLaunch;
+  const int ntiles = (int)((total + kKeyTile - 1) / kKeyTile);
   int64_t occ = 0;
   bool first_launch = true;
   for (int first = 0; first < num_lookups; first += kLookupsPerLaunch) {
@@ -1155,18 +1184,29 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
     la.occ_off[la.num] = occ;
     const int64_t cnt = occ - la.occ_off[0];
     if (cnt == 0) continue;
-    const unsigned g = (unsigned)((cnt + B - 1) / B);
-    const bool zero_here = fused_zero && first_launch;
-    const int64_t zvecs = zero_here && dense_any ? (int64_t)(dense_bytes / 16) : 0;
-    const unsigned gz = zero_here ? (unsigned)grid_for(zvecs > 0 ? zvecs : 1, B, 2048) : 0;
-    uint4* zdst = zvecs ? (uint4*)dense_any : nullptr;
-    int32_t* zcnt = zero_here ? uniq_count : nullptr;
+    const unsigned g = (unsigned)((cnt + kKeyTile - 1) / kKeyTile);
+    const bool fill_here = first_launch;
+    KeyFill fill;
+    memset(&fill, 0, sizeof(fill));
+    if (fill_here) {
+      fill.zero_vecs = fused_zero && dense_any ? (int64_t)(dense_bytes / 16) : 0;
+      fill.zero_dst = fill.zero_vecs ? (uint4*)dense_any : nullptr;
+      fill.zero_count = fused_zero ? uniq_count : nullptr;
+      if (by_key) {
+        fill.seg_start = ws.seg_start;
+        fill.seg_end = ws.seg_end;
+        fill.seg_n = num_rows;
+      }
+    }
+    const int64_t fill_work = fill.zero_vecs > fill.seg_n ? fill.zero_vecs : fill.seg_n;
+    const unsigned gz = fill_here ? (unsigned)grid_for(fill_work > 0 ? fill_work : 1, B, 2048) : 0;
+    unsigned* h0 = one_launch ? sort_pairs_hist0(ws.sort_tmp) : nullptr;
     if (itype == GRK_I64)
       k_build_keys<int64_t><<<g + gz, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
-                                                 ws.gptr_in, err_flag, g, zdst, zvecs, zcnt);
+                                                 ws.gptr_in, err_flag, g, h0, ntiles, fill);
     else
       k_build_keys<int32_t><<<g + gz, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
-                                                 ws.gptr_in, err_flag, g, zdst, zvecs, zcnt);
+                                                 ws.gptr_in, err_flag, g, h0, ntiles, fill);
     GRK_LAUNCH_CHECK();
     first_launch = false;
   }
@@ -1176,20 +1216,14 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   unsigned* skeys;
   unsigned long long* sgptr;
   {
+    SortSegments seg{ws.seg_start, ws.seg_end, sentinel, uniq_count};
     const int rc = sort_pairs(ws.keys_in, ws.gptr_in, ws.keys_out, ws.gptr_out, total, (int)end_bit, ws.sort_tmp, &skeys,
-                              &sgptr, s);
+                              &sgptr, s, one_launch, by_key ? &seg : nullptr);
     if (rc) return rc;
   }
   ws.keys_out = skeys;  // the sorted pairs (either buffer of the ping-pong)
   ws.gptr_out = sgptr;
-  const unsigned sentinel = (unsigned)num_rows;
-  // chunked mode writing only the dense rows: segment bounds by row, no numbering
-  const bool by_key = flags == GRK_BWD_CHUNKED && !uniq_ids && !uniq_rows && !row_slot && num_rows <= total;
-  const int lw0 = dim % 64 == 0 ? dim / 64 : 0;
-  const bool wave_path = (grad_dtype == GRK_BF16 && lw0 == 8) || (grad_dtype != GRK_BF16 && (lw0 == 4 || lw0 == 8));
-  if (by_key && wave_path) {
-    k_segments_key<<<g, B, 0, s>>>(ws.keys_out, total, sentinel, ws.seg_start, ws.seg_end, uniq_count);
-    GRK_LAUNCH_CHECK();
+  if (by_key) {
     ws.pos = nullptr;
   } else {
     const int rc = head_positions(ws.keys_out, total, sentinel, ws.pos, ws.scan_tmp, s);

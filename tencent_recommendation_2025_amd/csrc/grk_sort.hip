@@ -18,6 +18,15 @@
 //                  lanes of its wave (wave ballots over the 8 digit bits)
 // so the order among equal digits is the input order: stable, deterministic,
 // and (a stable sort being unique) the same output as rocprim's.
+//
+// Round 4, fewer launches per pass: the digit histograms live in two buffers
+// used in turn; each pass's scatter counts the NEXT digit of every key it
+// places into the other buffer (integer atomics on [digit][output tile]:
+// exact counts, so the result is unchanged), which that pass's scan zeroed
+// beforehand -- so only the first pass has a histogram launch, and the
+// embedding backward builds even that one inside its key-build kernel.  The
+// last pass can also record each row's segment bounds (first / last sorted
+// position, integer atomicMin / atomicMax) for the chunked backward.
 #include "grk_common.h"
 
 namespace grk {
@@ -43,12 +52,15 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const unsigned* __re
 }
 
 // Per digit (one workgroup each): in-place exclusive scan of the digit's tile
-// counts hist[d][0 .. ntiles) and the digit's total -> tot[d].
+// counts hist[d][0 .. ntiles) and the digit's total -> tot[d]; zeroes row d of
+// the next pass's histogram (hzero, may be null) for the scatter's counts.
 __global__ void __launch_bounds__(kSortThreads) k_sort_scan(unsigned* __restrict__ hist, int ntiles,
-                                                            unsigned* __restrict__ tot) {
+                                                            unsigned* __restrict__ tot, unsigned* __restrict__ hzero) {
   __shared__ unsigned part[kSortThreads];
   const int t = threadIdx.x;
   unsigned* row = hist + (int64_t)blockIdx.x * ntiles;
+  if (hzero)
+    for (int i = t; i < ntiles; i += kSortThreads) hzero[(int64_t)blockIdx.x * ntiles + i] = 0u;
   unsigned carry = 0;
   for (int c0 = 0; c0 < ntiles; c0 += kSortThreads) {
     const int i = c0 + t;
@@ -68,12 +80,20 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_scan(unsigned* __restrict
   if (t == 0) tot[blockIdx.x] = carry;
 }
 
+// hnext (may be null): this key's NEXT digit (shift_next) counted into
+// hnext[digit][pos / kSortTile] -- the next pass's histogram.  seg_start /
+// seg_end (may be null; last pass): per key below `sentinel`, the first and
+// one-past-last sorted position (atomicMin / atomicMax on buffers holding
+// INT_MAX / 0), and *seg_count = distinct keys.
 __global__ void __launch_bounds__(kSortThreads) k_sort_scatter(const unsigned* __restrict__ kin,
                                                                const unsigned long long* __restrict__ vin,
                                                                unsigned* __restrict__ kout,
                                                                unsigned long long* __restrict__ vout, int64_t n,
                                                                int shift, const unsigned* __restrict__ hist,
-                                                               int ntiles, const unsigned* __restrict__ tot) {
+                                                               int ntiles, const unsigned* __restrict__ tot,
+                                                               unsigned* __restrict__ hnext, int shift_next,
+                                                               int* __restrict__ seg_start, int* __restrict__ seg_end,
+                                                               unsigned sentinel, int32_t* __restrict__ seg_count) {
   constexpr int NW = kSortThreads / 64;
   __shared__ unsigned base[kSortBins];
   __shared__ unsigned wcnt[NW][kSortBins];
@@ -123,6 +143,11 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_scatter(const unsigned* _
         if (q < w) pos += wcnt[q][d];
       kout[pos] = key;
       vout[pos] = val;
+      if (hnext) atomicAdd(&hnext[(int64_t)((key >> shift_next) & (kSortBins - 1)) * ntiles + pos / kSortTile], 1u);
+      if (seg_start && key < sentinel) {
+        if (atomicMin(&seg_start[key], (int)pos) == 0x7FFFFFFF) atomicAdd(seg_count, 1);
+        atomicMax(&seg_end[key], (int)pos + 1);
+      }
     }
     __syncthreads();  // every slot of this round computed from the old base
     unsigned add = 0;
@@ -206,24 +231,33 @@ int head_positions(const unsigned* keys, int64_t n, unsigned sentinel, int* pos,
   unsigned* cnt = (unsigned*)ws;
   k_head_count<<<ntiles, kSortThreads, 0, s>>>(keys, n, sentinel, cnt);
   GRK_LAUNCH_CHECK();
-  k_sort_scan<<<1, kSortThreads, 0, s>>>(cnt, ntiles, cnt + ntiles);
+  k_sort_scan<<<1, kSortThreads, 0, s>>>(cnt, ntiles, cnt + ntiles, nullptr);
   GRK_LAUNCH_CHECK();
   k_head_pos<<<ntiles, kSortThreads, 0, s>>>(keys, n, sentinel, cnt, pos);
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }
 
-// Workspace of sort_pairs: the digit histograms (digit-major, one per pass, reused).
+// Workspace of sort_pairs: two digit-histogram buffers (digit-major, used in
+// turn by the passes) and the digit totals.
 size_t sort_pairs_workspace(int64_t n) {
   const int64_t ntiles = (n + kSortTile - 1) / kSortTile;
-  return ((size_t)kSortBins * (size_t)(ntiles > 0 ? ntiles : 1) + kSortBins) * sizeof(unsigned);
+  return (2 * (size_t)kSortBins * (size_t)(ntiles > 0 ? ntiles : 1) + kSortBins) * sizeof(unsigned);
 }
+
+// The first pass's histogram buffer inside a sort_pairs workspace (a caller
+// that counts digit 0 itself writes hist[digit][tile] there, kSortTile keys per tile).
+unsigned* sort_pairs_hist0(void* ws) { return (unsigned*)ws; }
 
 // Sorts (k0, v0) by the low end_bit bits of the keys, stably, ping-ponging
 // through (k1, v1); returns in *kres / *vres which pair of buffers holds the
-// result.  end_bit <= 32.
+// result.  end_bit <= 32.  hist0_ready: sort_pairs_hist0(ws) already holds the
+// first digit's tile counts.  seg (optional, keys < sentinel): the last pass
+// records per-key segment bounds (see k_sort_scatter; seg_start / seg_end
+// pre-filled with INT_MAX / 0, *seg_count with 0).
 int sort_pairs(unsigned* k0, unsigned long long* v0, unsigned* k1, unsigned long long* v1, int64_t n, int end_bit,
-               void* ws, unsigned** kres, unsigned long long** vres, hipStream_t s) {
+               void* ws, unsigned** kres, unsigned long long** vres, hipStream_t s, bool hist0_ready,
+               const SortSegments* seg) {
   *kres = k0;
   *vres = v0;
   if (n <= 0) return GRK_OK;
@@ -232,18 +266,28 @@ int sort_pairs(unsigned* k0, unsigned long long* v0, unsigned* k1, unsigned long
   const int64_t ntiles64 = (n + kSortTile - 1) / kSortTile;
   GRK_CHECK_ARG(ntiles64 < (1 << 24), "too many tiles");
   const int ntiles = (int)ntiles64;
-  unsigned* hist = (unsigned*)ws;
-  unsigned* tot = hist + (size_t)kSortBins * ntiles;
+  unsigned* hbuf[2] = {(unsigned*)ws, (unsigned*)ws + (size_t)kSortBins * ntiles};
+  unsigned* tot = hbuf[1] + (size_t)kSortBins * ntiles;
   unsigned* kin = k0;
   unsigned* kout = k1;
   unsigned long long* vin = v0;
   unsigned long long* vout = v1;
-  for (int shift = 0; shift < end_bit; shift += kSortBits) {
-    k_sort_hist<<<ntiles, kSortThreads, 0, s>>>(kin, n, shift, hist, ntiles);
+  int pass = 0;
+  for (int shift = 0; shift < end_bit; shift += kSortBits, ++pass) {
+    unsigned* hist = hbuf[pass & 1];
+    const bool last = shift + kSortBits >= end_bit;
+    unsigned* hnext = last ? nullptr : hbuf[(pass + 1) & 1];
+    if (pass == 0 && !hist0_ready) {
+      k_sort_hist<<<ntiles, kSortThreads, 0, s>>>(kin, n, shift, hist, ntiles);
+      GRK_LAUNCH_CHECK();
+    }
+    k_sort_scan<<<kSortBins, kSortThreads, 0, s>>>(hist, ntiles, tot, hnext);
     GRK_LAUNCH_CHECK();
-    k_sort_scan<<<kSortBins, kSortThreads, 0, s>>>(hist, ntiles, tot);
-    GRK_LAUNCH_CHECK();
-    k_sort_scatter<<<ntiles, kSortThreads, 0, s>>>(kin, vin, kout, vout, n, shift, hist, ntiles, tot);
+    const SortSegments* sg = last ? seg : nullptr;
+    k_sort_scatter<<<ntiles, kSortThreads, 0, s>>>(kin, vin, kout, vout, n, shift, hist, ntiles, tot, hnext,
+                                                   shift + kSortBits, sg ? sg->start : nullptr,
+                                                   sg ? sg->end : nullptr, sg ? sg->sentinel : 0u,
+                                                   sg ? sg->count : nullptr);
     GRK_LAUNCH_CHECK();
     unsigned* tk = kin;
     kin = kout;
@@ -283,5 +327,5 @@ extern "C" int grk_sort_pairs(const uint32_t* keys_in, const uint64_t* vals_in, 
   GRK_CHECK_HIP(hipMemcpyAsync(va, vals_in, (size_t)n * 8, hipMemcpyDeviceToDevice, s));
   unsigned* kr;
   unsigned long long* vr;
-  return sort_pairs(a, va, b, vb, n, end_bit, workspace, &kr, &vr, s);
+  return sort_pairs(a, va, b, vb, n, end_bit, workspace, &kr, &vr, s, false, nullptr);
 }
