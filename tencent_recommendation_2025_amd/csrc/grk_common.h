@@ -66,16 +66,6 @@ __device__ __forceinline__ float dsilu(float x) {
   return sg * (1.0f + x * (1.0f - sg));
 }
 
-// Segment bounds recorded by the last pass of the embedding backward's radix
-// sort (grk_sort.hip): start[key] / end[key] = first / one-past-last sorted
-// position of each key < sentinel; *count = distinct keys.
-struct SortSegments {
-  int* start;
-  int* end;
-  unsigned sentinel;
-  int32_t* count;
-};
-
 template <typename T> struct Elem;
 template <> struct Elem<float> {
   static __device__ __forceinline__ float load(const float* p) { return *p; }

@@ -185,17 +185,13 @@ __global__ void __launch_bounds__(256) k_gather_wave(FeatArgs args, int64_t num_
 // digit (bits 0-7) of its keys into hist0[digit][tile], the sort's first
 // histogram (grk_sort.hip), so that pass needs no launch of its own.
 // Blocks past key_blocks (first launch of a call only) instead zero the dense
-// output (16-byte words, grid-stride) and the unique-row count, and fill the
-// row-indexed segment bounds (INT_MAX / 0): those fills then overlap the key
-// build instead of taking launches of their own.
+// output (16-byte words, grid-stride) and the unique-row count: the fill then
+// overlaps the key build instead of taking a launch of its own.
 constexpr int kKeyTile = 1024;
 struct KeyFill {
   uint4* zero_dst;
   int64_t zero_vecs;
   int32_t* zero_count;
-  int* seg_start;   // filled with INT_MAX
-  int* seg_end;     // filled with 0
-  int64_t seg_n;
 };
 template <typename I>
 __global__ void __launch_bounds__(256) k_build_keys(LookupArgs la, int esize, const int32_t* __restrict__ token_type,
@@ -207,10 +203,6 @@ __global__ void __launch_bounds__(256) k_build_keys(LookupArgs la, int esize, co
     const int64_t nb = gridDim.x - key_blocks, t = (int64_t)(blockIdx.x - key_blocks) * blockDim.x + threadIdx.x;
     const int64_t stride = nb * blockDim.x;
     for (int64_t v = t; v < fill.zero_vecs; v += stride) fill.zero_dst[v] = make_uint4(0, 0, 0, 0);
-    for (int64_t v = t; v < fill.seg_n; v += stride) {
-      fill.seg_start[v] = 0x7FFFFFFF;
-      fill.seg_end[v] = 0;
-    }
     if (fill.zero_count && t == 0) *fill.zero_count = 0;
     return;
   }
@@ -266,6 +258,24 @@ __global__ void k_segments(const unsigned* __restrict__ keys, const int* __restr
     seg_end[u] = (int)(i + 1);
     if (i == n - 1 || keys[i + 1] == sentinel) *count = u + 1;
   }
+}
+
+// Chunked dense mode with num_rows <= n: segment bounds indexed by the ROW
+// (seg_start[key], seg_end[key]) -- no segment numbering (head positions: three
+// launches) is needed when nothing is written per unique row.  The distinct-row
+// count is added once per wave (one add per head contended on a single word:
+// 29 us per call on MI355X, round 4).
+__global__ void __launch_bounds__(256) k_segments_key(const unsigned* __restrict__ keys, int64_t n, unsigned sentinel,
+                                                      int* __restrict__ seg_start, int* __restrict__ seg_end,
+                                                      int32_t* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned k = i < n ? keys[i] : sentinel;
+  const bool live = k != sentinel;
+  const bool head = live && (i == 0 || keys[i - 1] != k);
+  if (head) seg_start[k] = (int)i;
+  if (live && (i == n - 1 || keys[i + 1] != k)) seg_end[k] = (int)(i + 1);
+  const unsigned long long heads = __ballot(head);
+  if ((threadIdx.x & 63) == 0 && heads) atomicAdd(count, (int)__popcll(heads));
 }
 
 // ------------------------------------------------- segmented reduction ----
@@ -946,8 +956,7 @@ __global__ void __launch_bounds__(256) k_seg_wave_fused(int64_t nhot, int nslice
 size_t sort_pairs_workspace(int64_t n);
 unsigned* sort_pairs_hist0(void* ws);
 int sort_pairs(unsigned* k0, unsigned long long* v0, unsigned* k1, unsigned long long* v1, int64_t n, int end_bit,
-               void* ws, unsigned** kres, unsigned long long** vres, hipStream_t s, bool hist0_ready,
-               const SortSegments* seg);
+               void* ws, unsigned** kres, unsigned long long** vres, hipStream_t s, bool hist0_ready);
 // Segment index of every sorted entry (inclusive count of row heads).
 size_t head_positions_workspace(int64_t n);
 int head_positions(const unsigned* keys, int64_t n, unsigned sentinel, int* pos, void* ws, hipStream_t s);
@@ -1161,8 +1170,8 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   const int B = 256;
   const int esize = grad_dtype == GRK_F32 ? 4 : 2;
   const unsigned sentinel = (unsigned)num_rows;
-  // chunked mode writing only the dense rows: segment bounds by row (recorded by the
-  // sort's last pass), no segment numbering (head positions) at all
+  // chunked mode writing only the dense rows: segment bounds by row (k_segments_key),
+  // no segment numbering (head positions) at all
   const int lw0 = dim % 64 == 0 ? dim / 64 : 0;
   const bool wave_path = (grad_dtype == GRK_BF16 && lw0 == 8) || (grad_dtype != GRK_BF16 && (lw0 == 4 || lw0 == 8));
   const bool by_key = wave_path && flags == GRK_BWD_CHUNKED && !uniq_ids && !uniq_rows && !row_slot &&
@@ -1192,14 +1201,8 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
       fill.zero_vecs = fused_zero && dense_any ? (int64_t)(dense_bytes / 16) : 0;
       fill.zero_dst = fill.zero_vecs ? (uint4*)dense_any : nullptr;
       fill.zero_count = fused_zero ? uniq_count : nullptr;
-      if (by_key) {
-        fill.seg_start = ws.seg_start;
-        fill.seg_end = ws.seg_end;
-        fill.seg_n = num_rows;
-      }
     }
-    const int64_t fill_work = fill.zero_vecs > fill.seg_n ? fill.zero_vecs : fill.seg_n;
-    const unsigned gz = fill_here ? (unsigned)grid_for(fill_work > 0 ? fill_work : 1, B, 2048) : 0;
+    const unsigned gz = fill_here ? (unsigned)grid_for(fill.zero_vecs > 0 ? fill.zero_vecs : 1, B, 2048) : 0;
     unsigned* h0 = one_launch ? sort_pairs_hist0(ws.sort_tmp) : nullptr;
     if (itype == GRK_I64)
       k_build_keys<int64_t><<<g + gz, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
@@ -1216,14 +1219,15 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   unsigned* skeys;
   unsigned long long* sgptr;
   {
-    SortSegments seg{ws.seg_start, ws.seg_end, sentinel, uniq_count};
     const int rc = sort_pairs(ws.keys_in, ws.gptr_in, ws.keys_out, ws.gptr_out, total, (int)end_bit, ws.sort_tmp, &skeys,
-                              &sgptr, s, one_launch, by_key ? &seg : nullptr);
+                              &sgptr, s, one_launch);
     if (rc) return rc;
   }
   ws.keys_out = skeys;  // the sorted pairs (either buffer of the ping-pong)
   ws.gptr_out = sgptr;
   if (by_key) {
+    k_segments_key<<<g, B, 0, s>>>(ws.keys_out, total, sentinel, ws.seg_start, ws.seg_end, uniq_count);
+    GRK_LAUNCH_CHECK();
     ws.pos = nullptr;
   } else {
     const int rc = head_positions(ws.keys_out, total, sentinel, ws.pos, ws.scan_tmp, s);

@@ -24,9 +24,7 @@
 // places into the other buffer (integer atomics on [digit][output tile]:
 // exact counts, so the result is unchanged), which that pass's scan zeroed
 // beforehand -- so only the first pass has a histogram launch, and the
-// embedding backward builds even that one inside its key-build kernel.  The
-// last pass can also record each row's segment bounds (first / last sorted
-// position, integer atomicMin / atomicMax) for the chunked backward.
+// embedding backward builds even that one inside its key-build kernel.
 #include "grk_common.h"
 
 namespace grk {
@@ -81,19 +79,14 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_scan(unsigned* __restrict
 }
 
 // hnext (may be null): this key's NEXT digit (shift_next) counted into
-// hnext[digit][pos / kSortTile] -- the next pass's histogram.  seg_start /
-// seg_end (may be null; last pass): per key below `sentinel`, the first and
-// one-past-last sorted position (atomicMin / atomicMax on buffers holding
-// INT_MAX / 0), and *seg_count = distinct keys.
+// hnext[digit][pos / kSortTile] -- the next pass's histogram.
 __global__ void __launch_bounds__(kSortThreads) k_sort_scatter(const unsigned* __restrict__ kin,
                                                                const unsigned long long* __restrict__ vin,
                                                                unsigned* __restrict__ kout,
                                                                unsigned long long* __restrict__ vout, int64_t n,
                                                                int shift, const unsigned* __restrict__ hist,
                                                                int ntiles, const unsigned* __restrict__ tot,
-                                                               unsigned* __restrict__ hnext, int shift_next,
-                                                               int* __restrict__ seg_start, int* __restrict__ seg_end,
-                                                               unsigned sentinel, int32_t* __restrict__ seg_count) {
+                                                               unsigned* __restrict__ hnext, int shift_next) {
   constexpr int NW = kSortThreads / 64;
   __shared__ unsigned base[kSortBins];
   __shared__ unsigned wcnt[NW][kSortBins];
@@ -144,10 +137,6 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_scatter(const unsigned* _
       kout[pos] = key;
       vout[pos] = val;
       if (hnext) atomicAdd(&hnext[(int64_t)((key >> shift_next) & (kSortBins - 1)) * ntiles + pos / kSortTile], 1u);
-      if (seg_start && key < sentinel) {
-        if (atomicMin(&seg_start[key], (int)pos) == 0x7FFFFFFF) atomicAdd(seg_count, 1);
-        atomicMax(&seg_end[key], (int)pos + 1);
-      }
     }
     __syncthreads();  // every slot of this round computed from the old base
     unsigned add = 0;
@@ -252,12 +241,9 @@ unsigned* sort_pairs_hist0(void* ws) { return (unsigned*)ws; }
 // Sorts (k0, v0) by the low end_bit bits of the keys, stably, ping-ponging
 // through (k1, v1); returns in *kres / *vres which pair of buffers holds the
 // result.  end_bit <= 32.  hist0_ready: sort_pairs_hist0(ws) already holds the
-// first digit's tile counts.  seg (optional, keys < sentinel): the last pass
-// records per-key segment bounds (see k_sort_scatter; seg_start / seg_end
-// pre-filled with INT_MAX / 0, *seg_count with 0).
+// first digit's tile counts.
 int sort_pairs(unsigned* k0, unsigned long long* v0, unsigned* k1, unsigned long long* v1, int64_t n, int end_bit,
-               void* ws, unsigned** kres, unsigned long long** vres, hipStream_t s, bool hist0_ready,
-               const SortSegments* seg) {
+               void* ws, unsigned** kres, unsigned long long** vres, hipStream_t s, bool hist0_ready) {
   *kres = k0;
   *vres = v0;
   if (n <= 0) return GRK_OK;
@@ -283,11 +269,8 @@ int sort_pairs(unsigned* k0, unsigned long long* v0, unsigned* k1, unsigned long
     }
     k_sort_scan<<<kSortBins, kSortThreads, 0, s>>>(hist, ntiles, tot, hnext);
     GRK_LAUNCH_CHECK();
-    const SortSegments* sg = last ? seg : nullptr;
     k_sort_scatter<<<ntiles, kSortThreads, 0, s>>>(kin, vin, kout, vout, n, shift, hist, ntiles, tot, hnext,
-                                                   shift + kSortBits, sg ? sg->start : nullptr,
-                                                   sg ? sg->end : nullptr, sg ? sg->sentinel : 0u,
-                                                   sg ? sg->count : nullptr);
+                                                   shift + kSortBits);
     GRK_LAUNCH_CHECK();
     unsigned* tk = kin;
     kin = kout;
@@ -327,5 +310,5 @@ extern "C" int grk_sort_pairs(const uint32_t* keys_in, const uint64_t* vals_in, 
   GRK_CHECK_HIP(hipMemcpyAsync(va, vals_in, (size_t)n * 8, hipMemcpyDeviceToDevice, s));
   unsigned* kr;
   unsigned long long* vr;
-  return sort_pairs(a, va, b, vb, n, end_bit, workspace, &kr, &vr, s, false, nullptr);
+  return sort_pairs(a, va, b, vb, n, end_bit, workspace, &kr, &vr, s, false);
 }

@@ -232,20 +232,7 @@ def _trainer_batches(cfg):
     return batches
 
 
-def _permuted(batch, perm):
-    """The batch with its sequences in another order (every field along dim 0)."""
-    out = []
-    for x in batch:
-        if isinstance(x, torch.Tensor):
-            out.append(x[perm].contiguous())
-        elif isinstance(x, dict):
-            out.append({k: v[perm].contiguous() for k, v in x.items()})
-        else:
-            out.append(x)
-    return tuple(out)
-
-
-def _one_step_grads(state, jagged, batch):
+def _one_step_grads(state, jagged, batch, quantum=128):
     """Loss and every gradient (dense parameters; each table group's dense row
     gradient) of ONE bf16-autocast trainer step from the parameters ``state``."""
     from tencent_recommendation_2025_amd.optim import FusedAdamW
@@ -253,7 +240,7 @@ def _one_step_grads(state, jagged, batch):
     m, _ = _model(*_TRAINER_CFG)
     m.load_state_dict(state)
     opt = FusedAdamW(m, lr=1e-3, defer_period=4)
-    tr = Trainer(m, opt, loss='bce', jagged=jagged, jagged_quantum=128)
+    tr = Trainer(m, opt, loss='bce', jagged=jagged, jagged_quantum=quantum)
     opt.zero_grad()
     opt.begin_step(batch)
     loss = tr.compute_loss(batch)
@@ -266,30 +253,33 @@ def _one_step_grads(state, jagged, batch):
     return float(loss), grads
 
 
-# Per-step bound of the bf16 jagged step against the padded one from identical
-# parameters.  The dead rows contribute exact zeros, so what differs is only the
-# order of the sums over tokens (GEMM / grk_wgrad reductions over K = capacity vs
-# B*T rows, the chunked order of the projected-row backward) and the bf16 roundings
-# that order can flip in autocast outputs.  Measured on MI355X (round 4, the r4a
-# run): loss 6e-6; attention / LayerNorm / uvqk grads <= 3e-6, but itemdnn,
-# userdnn, emb_transform and the small tables 1e-3 .. 2.7e-3 -- the dnn weights'
-# gradients sum pos-item and neg-item terms of opposite sign (BCE at logits near 0),
-# so the sum is far smaller than its terms and any reordering is amplified.  The
-# bound is therefore set against the SAME padded step with the batch's sequences
-# permuted (mathematically identical, only the summation order differs): jagged
-# vs padded may not differ by more than REORDER_FACTOR x that reorder sensitivity
-# (or GRAD_FLOOR, whichever is larger), parameter by parameter.
-JAGGED_STEP_TOL = dict(loss=1e-5)
-REORDER_FACTOR, GRAD_FLOOR = 4.0, 1e-5
+# Per-step bounds of the bf16 jagged step against the padded one from identical
+# parameters.  The dead rows contribute exact zeros and every span row sees the
+# same inputs, so what can differ is (a) the order of the sums over rows (dW = dY^T X,
+# LayerNorm gamma / beta, the row reductions of the tables) and (b), when the
+# jagged capacity differs from B*T, which hipBLASLt kernel grk_gemm picks for the
+# other row count -- each GEMM output is rounded to bf16, so another kernel's fp32
+# summation order can move an output by one bf16 ulp.  Measured on MI355X
+# (round 4; scripts/diag/jagged_vs_padded.py): with the capacity rounded to 128
+# rows, loss bitwise, every gradient of every span row bitwise, parameters 1e-7
+# .. 4e-4 -- in another process (other GEMM kernels picked) up to 2.7e-3.  The
+# largest are the dnn weights whose sums over tokens mix pos-item and neg-item
+# terms of opposite sign (BCE at logits near 0): the sum is far smaller than its
+# terms, so any reordering is amplified.  fp32 (no bf16 rounding at all) pins
+# every gradient at 1e-5: test_jagged_encode_equals_padded_fp32.
+#   capacity == B*T (same GEMM shapes, so the same kernels): every parameter 1e-5
+#     normwise except the cancellation-dominated dnn / feature-table sums (1e-3);
+#   the bench's capacity rounding (128 rows here): every parameter 5e-3.
+JAGGED_STEP_TOL = dict(loss=1e-5, grad_same=1e-5, grad_sums=1e-3, grad_capacity=5e-3)
+DNN_SUMS = ('itemdnn.', 'userdnn.', 'emb_transform.', 'group.small', 'group.item', 'group.user')
 
 
 def test_jagged_step_matches_padded_from_identical_parameters():
     """bf16 autocast HSTU (the bench's regime), dropout 0: from the SAME parameters,
     one jagged step's loss and every gradient against the padded step's, at the
     initial parameters and after 2 and 5 padded training steps, on batches of two
-    capacity buckets (reference loop: model/BaseLine/main.py:177-185).  Each
-    gradient's bound is the padded step's own sensitivity to the order of the
-    batch's sequences (see JAGGED_STEP_TOL)."""
+    capacity buckets (reference loop: model/BaseLine/main.py:177-185); once with
+    capacity B*T (same GEMM shapes) and once with the bench's capacity rounding."""
     from tencent_recommendation_2025_amd import jagged as J
     from tencent_recommendation_2025_amd.optim import FusedAdamW
     from tencent_recommendation_2025_amd.train import Trainer
@@ -297,30 +287,31 @@ def test_jagged_step_matches_padded_from_identical_parameters():
     batches = _trainer_batches(cfg)
     tr = Trainer(m, FusedAdamW(m, lr=1e-3, defer_period=4), loss='bce')
     done = 0
-    bad, worst_loss = {}, 0.0
+    bad = {}
     for trained, probe in ((0, 0), (2, 3), (5, 1)):
         while done < trained:
             tr.step(batches[done % 4])
             done += 1
         state = {k: v.detach().clone() for k, v in m.state_dict().items()}   # flushes deferred rows
         batch = batches[probe]
-        perm = torch.arange(batch[0].shape[0] - 1, -1, -1, device=DEV)
+        B, T = batch[0].shape
         lp, gp = _one_step_grads(state, False, batch)
-        lr_, gr = _one_step_grads(state, False, _permuted(batch, perm))
-        lj, gj = _one_step_grads(state, True, batch)
-        assert set(gp) == set(gj) == set(gr)
-        errs = {k: nrel(gj[k].cpu(), gp[k].cpu()) for k in gp}
-        reorder = {k: nrel(gr[k].cpu(), gp[k].cpu()) for k in gp}
-        loss_err = abs(lj - lp) / abs(lp)
-        worst_loss = max(worst_loss, loss_err)
-        top = sorted(errs, key=lambda k: -errs[k])[:6]
-        print(f'after {trained} steps, batch {probe} (capacity {J.capacity_for(J.span_rows(batch[3]), 128)}):',
-              f'loss {loss_err:.2e} (reordered {abs(lr_ - lp) / abs(lp):.2e})',
-              [(k, f'{errs[k]:.2e}', f'reorder {reorder[k]:.2e}') for k in top])
-        for k, v in errs.items():
-            if v > max(REORDER_FACTOR * reorder[k], GRAD_FLOOR):
-                bad[(trained, k)] = (v, reorder[k])
-    assert worst_loss < JAGGED_STEP_TOL['loss'], worst_loss
+        for name, quantum in (('same', B * T), ('capacity', 128)):
+            lj, gj = _one_step_grads(state, True, batch, quantum=quantum)
+            assert set(gp) == set(gj)
+            errs = {k: nrel(gj[k].cpu(), gp[k].cpu()) for k in gp}
+            loss_err = abs(lj - lp) / abs(lp)
+            top = sorted(errs, key=lambda k: -errs[k])[:5]
+            print(f'after {trained} steps, batch {probe}, {name} (capacity '
+                  f'{J.capacity_for(J.span_rows(batch[3]), quantum)}): loss {loss_err:.2e}',
+                  [(k, f'{errs[k]:.2e}') for k in top])
+            if loss_err > JAGGED_STEP_TOL['loss']:
+                bad[(trained, name, 'loss')] = loss_err
+            for k, v in errs.items():
+                tol = (JAGGED_STEP_TOL['grad_capacity'] if name == 'capacity' else
+                       JAGGED_STEP_TOL['grad_sums'] if k.startswith(DNN_SUMS) else JAGGED_STEP_TOL['grad_same'])
+                if v > tol:
+                    bad[(trained, name, k)] = v
     assert not bad, bad
 
 

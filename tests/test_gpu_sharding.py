@@ -205,8 +205,18 @@ def test_sharded_jagged_equals_sharded_padded_and_graph_replay(pg):
         tabs = {k: opt.shard_table(k).clone() for k in ('item_emb', 'user_emb')}
         torch.cuda.synchronize()
         runs[name] = (torch.stack(losses), sd, tabs)
+    assert torch.equal(runs['jagged_bf16'][0], runs['jagged_graph'][0])
+    for i in (1, 2):
+        for k in runs['jagged_bf16'][i]:
+            assert torch.equal(runs['jagged_bf16'][i][k], runs['jagged_graph'][i][k]), k
     lp, lj = runs['padded'][0], runs['jagged'][0]
-    assert ((lj - lp).abs() / lp.abs()).max().item() < 1e-4, (lp, lj)
+    rel = (lj - lp).abs() / lp.abs()
+    # step 1 sees identical parameters: the same loss up to the order of the sums over
+    # rows; the later steps follow two trajectories, and Adam turns the fp32 rounding
+    # noise of a near-zero gradient element into a +-lr move (measured on MI355X,
+    # round 4: 0, 2e-5, 1e-5, 1.6e-4, 4e-6, 3e-5, 1e-4, 3e-5 over the 8 steps)
+    assert rel[0].item() < 1e-6, (lp, lj)
+    assert rel.max().item() < 5e-4, (lp, lj)
     for k in runs['padded'][1]:
         if k in ('item_emb.weight', 'user_emb.weight'):
             continue
@@ -215,7 +225,3 @@ def test_sharded_jagged_equals_sharded_padded_and_graph_replay(pg):
     for k in runs['padded'][2]:
         torch.testing.assert_close(runs['jagged'][2][k].float(), runs['padded'][2][k].float(), rtol=1e-3, atol=2e-5,
                                    msg=k)
-    assert torch.equal(runs['jagged_bf16'][0], runs['jagged_graph'][0])
-    for i in (1, 2):
-        for k in runs['jagged_bf16'][i]:
-            assert torch.equal(runs['jagged_bf16'][i][k], runs['jagged_graph'][i][k]), k
