@@ -68,12 +68,12 @@ def parse():
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='gloo: rehearse N ranks on fewer GPUs (collectives staged via host)')
     ap.add_argument('--sharded', type=int, default=None, help='force the row-sharded optimizer (default: N > 1)')
-    ap.add_argument('--merge-proj', type=int, default=0,
+    ap.add_argument('--merge-proj', type=int, default=1,
                     help='1: the projected feature tables\' row gradients of the seq-side and pair lookups in one '
-                         'grk_embedding_backward call (functional.DenseMerge; opt-in until verified on hardware)')
-    ap.add_argument('--dense-flat', type=int, default=0,
-                    help='1: the dense parameters as one flat buffer on grk\'s multi-range AdamW instead of torch\'s '
-                         'fused AdamW (optim.DenseFlat; opt-in until verified on hardware)')
+                         'grk_embedding_backward call (functional.DenseMerge); 0: one call per lookup')
+    ap.add_argument('--dense-flat', type=int, default=1,
+                    help='1: the dense parameters as one flat buffer on grk\'s multi-range AdamW (optim.DenseFlat); '
+                         '0: torch\'s fused AdamW')
     ap.add_argument('--sharded-jagged', type=int, default=0,
                     help='1: the row-sharded trainer on jagged rows too (train.jagged_remaps; opt-in until verified '
                          'on hardware -- the sharded step runs the padded layout by default)')

@@ -14,7 +14,7 @@
 #   gpurun --timeout 900 -- bash scripts/gpu_validate_pending.sh tests
 #   gpurun --timeout 900 -- bash scripts/gpu_validate_pending.sh variants
 #   gpurun --timeout 900 -- bash scripts/gpu_validate_pending.sh ab
-#   gpurun --timeout 600 -- bash scripts/gpu_validate_pending.sh c5
+#   gpurun --timeout 600 -- bash scripts/gpu_c5.sh
 #   (c5lib: the torch GEMM forms at the C5 projection shape, diagnostic only)
 # Every step has its own time limit.  A step whose tests merely fail (pytest
 # exit 1) lets the independent steps after it run; a GPU fault (its message in

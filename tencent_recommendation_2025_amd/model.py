@@ -251,7 +251,7 @@ class BaselineModel(torch.nn.Module):
         self.proj_max_rows = int(getattr(args, 'proj_max_rows', 100_000))
         # fused path: the projected tables' row gradients of the seq-side and pair
         # lookups reduced in one call (functional.DenseMerge); opt-in until run on hardware
-        self.merge_proj = bool(getattr(args, 'merge_proj_backward', False))
+        self.merge_proj = bool(getattr(args, 'merge_proj_backward', True))
         if getattr(args, 'shard_tables', False):
             # row-sharded item / user tables (BASELINE config 3, 50M rows): the full
             # tables are never built on any rank -- ShardedFusedAdamW creates each

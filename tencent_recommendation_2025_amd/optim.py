@@ -235,17 +235,17 @@ class FusedAdamW:
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
                  table_dtype=torch.bfloat16, groups=DEFAULT_GROUPS, defer_period=16, l2_emb=0.0, parallel=False,
-                 dense_flat=False):
+                 dense_flat=True):
         """l2_emb > 0: the BaseLine script's ``loss += l2_emb * ||item_emb.weight||_F``
         (model/BaseLine/main.py:184-185) -- ``l2_term()`` gives the loss term (Trainer
         adds it), ``step()`` adds its gradient l2 * W / ||W|| to every item row.  Every
         row then moves every step, so the item table is updated densely (not deferred).
 
-        dense_flat=True (GPU; opt-in until measured): the fp32 dense
-        parameters whose sizes are multiples of 8 become views of ONE flat buffer
-        (DenseFlat) updated by grk's multi-range AdamW (one k_adamw_ranges launch, each
-        parameter's gradient a range) instead of torch's fused AdamW (~0.14 ms per C2
-        step at 2.4 TB/s).  The element update is the tables' (hardware sqrt /
+        dense_flat=True (GPU; the default since round 4, measured -0.06 ms per C2 step):
+        the fp32 dense parameters whose sizes are multiples of 8 become views of ONE flat
+        buffer (DenseFlat) updated by grk's multi-range AdamW (one k_adamw_ranges launch
+        per run of <= 64 parameters with a gradient) instead of torch's fused AdamW
+        (~0.14-0.19 ms per C2 step).  The element update is the tables' (hardware sqrt /
         reciprocal): within a few ulp of torch's.  A parameter without a
         gradient in a step is not moved (torch's rule); its bias correction afterwards
         follows the global step (the device clock) where torch counts each parameter's

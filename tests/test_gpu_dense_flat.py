@@ -1,19 +1,16 @@
 """optim.FusedAdamW(dense_flat=True): the fp32 dense parameters as views of one
 flat buffer, updated by grk's multi-range AdamW (k_adamw_ranges) instead of
-torch's fused AdamW.  Opt-in until it has run on hardware (written in round 3
-after gpurun closed; GRK_DENSE_FLAT_TESTS=1).
+torch's fused AdamW (written in round 3, hardware-verified and the default since
+round 4).
 
 Against torch's fused AdamW driven by the same gradients (the element updates
 differ by the hardware sqrt / reciprocal only); graph replay ==
 eager, bit for bit, as for the default optimizer."""
-import os
 
 import pytest
 import torch
 
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(os.environ.get('GRK_DENSE_FLAT_TESTS') != '1',
-                                 reason='dense_flat is opt-in until run on hardware (GRK_DENSE_FLAT_TESTS=1)')]
+pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
 

@@ -2,7 +2,6 @@
 grk_table_adamw) against the oracle, which is itself pinned to the reference's
 golden vectors (tests/test_oracle_golden.py).  Integer/byte work is checked
 bit-exact; the fp32 order-defined sums too."""
-import os
 
 import numpy as np
 import pytest
@@ -325,8 +324,6 @@ def test_backward_chunked_mode(K, D, dt):
     assert torch.equal(again, res.dense)
 
 
-@pytest.mark.skipif(os.environ.get('GRK_MERGE_PROJ_TESTS') != '1',
-                    reason='bf16 dense output not yet run on the GPU (set GRK_MERGE_PROJ_TESTS=1)')
 def test_backward_chunked_bf16_dense_is_the_rounded_fp32_result(K):
     """GRK_BWD_DENSE_BF16: the dense rows are the chunked fp32 result rounded
     to bf16 once (round to nearest even, as torch's cast) -- bit-exact against

@@ -12,7 +12,6 @@
   tolerances), graph replay == eager bitwise across two capacities.
 The padded step is pinned to the reference (test_gpu_model.py), so the jagged
 one is pinned through it."""
-import os
 
 import numpy as np
 import pytest
@@ -372,8 +371,6 @@ def test_understated_rows_raise_instead_of_addressing_past_capacity():
     tr2.check_jagged()
 
 
-@pytest.mark.skipif(os.environ.get('GRK_MERGE_PROJ_TESTS') != '1',
-                    reason='merged projected-row backward: opt-in until verified on hardware')
 def test_merged_projection_backward_matches_and_replays_bitwise():
     """args.merge_proj_backward (functional.DenseMerge): the projected tables' row
     gradients of the seq-side and pair lookups in ONE chunked call -- bf16 trainer
