@@ -380,6 +380,31 @@ int grk_jagged_layout(const uint8_t* key_valid, int batch, int seq_len, int64_t 
                       const int32_t* next_token_type, int32_t* ranges, int64_t* row_base, int32_t* row_map,
                       int64_t* num_rows, int32_t* err_flag, void* stream);
 
+/* Projected-table index of the fused model (model._projection; the reference's
+ * per-feature lookups model/BaseLine/model.py:254-277 restated over the stacked
+ * projected tables P): out[r, out_col_k + j] = src_k[r, j] > 0 ? src_k[r, j] +
+ * offset_k : 0 for every block k (its feature's index columns; offset_k = its
+ * table's first P row), int64 out [rows, >= sum of widths]; the blocks tile the
+ * columns in order (out_col_0 = 0).  src int32 or int64 (itype), at most 64
+ * blocks.  One launch. */
+typedef struct grk_index_block {
+  const void* src;       /* [rows, src_ld] index values, itype              */
+  int64_t src_ld;        /* elements between consecutive rows              */
+  int64_t width;         /* index columns of this block                    */
+  int64_t out_col;       /* first output column                            */
+  int64_t offset;        /* added to every non-zero value                  */
+} grk_index_block;
+int grk_proj_index(const grk_index_block* blocks, int num_blocks, int itype, int64_t rows, int64_t* out,
+                   int64_t out_ld, void* stream);
+
+/* Rows of the item / user tables a training batch reads (model/BaseLine/
+ * model.py:331-350, 376-377), -1 for padding: item_ids [3n] = (item ids of item
+ * tokens | pos | neg), user_ids [n] = user ids of user tokens (NULL: skipped).
+ * seq / pos / neg / token_type: n elements each of itype.  The ids the deferred
+ * dense-parity table AdamW catches up before the forward. */
+int grk_batch_row_ids(const void* seq, const void* pos, const void* neg, const void* token_type, int itype,
+                      int64_t n, int64_t* item_ids, int64_t* user_ids, void* stream);
+
 /* Multi-tensor row gather for the jagged layout: for each copy,
  * dst + r * dst_ld <- src + row_map[r] * src_ld (row_bytes bytes; zeros where
  * row_map[r] < 0), r in [0, rows), all copies in one launch.  row_bytes,

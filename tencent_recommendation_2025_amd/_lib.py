@@ -71,6 +71,11 @@ class GrkRowCopy(C.Structure):
                 ('dst_ld', C.c_int64)]
 
 
+class GrkIndexBlock(C.Structure):
+    _fields_ = [('src', C.c_void_p), ('src_ld', C.c_int64), ('width', C.c_int64), ('out_col', C.c_int64),
+                ('offset', C.c_int64)]
+
+
 class GrkStoreView(C.Structure):
     _fields_ = [('sparse', C.c_void_p), ('arr', C.c_void_p), ('arr_len', C.c_void_p), ('mm', C.c_void_p),
                 ('tokens', C.c_int64), ('f_sparse', C.c_int32), ('f_array', C.c_int32), ('a_cap', C.c_int32),
@@ -135,6 +140,8 @@ SIGNATURES = {
     'grk_seq_ranges': (_I, [_P, _I, _I, _P, _P]),
     'grk_jagged_layout': (_I, [_P, _I, _I, _I64, _P, _P, _P, _P, _P, _P, _P]),
     'grk_gather_rows': (_I, [C.POINTER(GrkRowCopy), _I, _P, _I64, _P]),
+    'grk_proj_index': (_I, [C.POINTER(GrkIndexBlock), _I, _I, _I64, _P, _I64, _P]),
+    'grk_batch_row_ids': (_I, [_P, _P, _P, _P, _I, _I64, _P, _P, _P]),
     'grk_add_norm_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _P, _I64, _P, _I64, _I, _P, _P]),
     'grk_add_norm_bwd_workspace': (_SZ, [_I64, _I]),
     'grk_add_norm_bwd': (_I, [_P, _I64, _I, _P, _I64, _P, _I64, _P, _P, _I64, _I, _P, _I64, _P, _P, _P, _SZ, _P]),

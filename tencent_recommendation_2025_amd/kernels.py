@@ -492,6 +492,52 @@ def jagged_layout(key_valid, capacity, next_token_type=None, err_flag=None):
     return ranges, row_base, row_map, n
 
 
+def proj_index(blocks, rows, out=None):
+    """int64 [rows, sum of widths]: column block k = blocks[k] = (src [rows, w] int, offset)
+    with every non-zero value shifted by offset, 0 kept (grk_proj_index, one launch):
+    the projected tables' bag index of the fused model (model._proj_index)."""
+    if not blocks:
+        raise L.GrkError('proj_index needs at least one block')
+    _require_cuda(*[b for b, _ in blocks], out)
+    itype = blocks[0][0].dtype
+    if itype not in (torch.int32, torch.int64) or any(b.dtype != itype for b, _ in blocks):
+        raise L.GrkError('proj_index blocks must share one int32 / int64 dtype')
+    arr = (L.GrkIndexBlock * len(blocks))()
+    col = 0
+    for k, (b, off) in enumerate(blocks):
+        b2 = b.reshape(rows, -1)
+        if b2.stride(-1) != 1:
+            raise L.GrkError(f'proj_index block {k}: rows must be contiguous')
+        arr[k] = L.GrkIndexBlock(b2.data_ptr(), b2.stride(0), b2.shape[1], col, int(off))
+        col += b2.shape[1]
+    if out is None:
+        out = torch.empty(rows, col, dtype=torch.int64, device=blocks[0][0].device)
+    if out.dtype != torch.int64 or out.dim() != 2 or out.shape[0] != rows or out.shape[1] < col or out.stride(1) != 1:
+        raise L.GrkError('proj_index out must be an int64 [rows, >= columns] row-major tensor')
+    L.check(L.lib().grk_proj_index(arr, len(blocks), 1 if itype == torch.int64 else 0, rows, out.data_ptr(),
+                                   out.stride(0), L.stream_ptr(out.device)), 'grk_proj_index')
+    return out
+
+
+def batch_row_ids(seq, pos, neg, token_type, with_user=True):
+    """(item ids int64 [3n] = item tokens' ids | pos | neg, user ids int64 [n] or None), -1 for
+    padding (grk_batch_row_ids, one launch): the table rows a batch reads."""
+    _require_cuda(seq, pos, neg, token_type)
+    ts = [t.contiguous() for t in (seq, pos, neg, token_type)]
+    dt = ts[0].dtype
+    if dt not in (torch.int32, torch.int64):
+        raise L.GrkError('batch_row_ids: int32 / int64 ids')
+    ts = [t if t.dtype == dt else t.to(dt) for t in ts]
+    n = ts[0].numel()
+    if any(t.numel() != n for t in ts):
+        raise L.GrkError('batch_row_ids: seq, pos, neg and token_type must have one shape')
+    item = torch.empty(3 * n, dtype=torch.int64, device=seq.device)
+    user = torch.empty(n, dtype=torch.int64, device=seq.device) if with_user else None
+    L.check(L.lib().grk_batch_row_ids(*[t.data_ptr() for t in ts], 1 if dt == torch.int64 else 0, n,
+                                      item.data_ptr(), _ptr(user), L.stream_ptr(seq.device)), 'grk_batch_row_ids')
+    return item, user
+
+
 def gather_rows(pairs, row_map):
     """dst[r] = src[row_map[r]] (zeros where row_map[r] < 0) for every (src, dst) pair
     in ONE launch (grk_gather_rows): src [N, ...] and dst [rows, ...] of one dtype with

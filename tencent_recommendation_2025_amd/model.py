@@ -480,7 +480,12 @@ class BaselineModel(torch.nn.Module):
         return m
 
     def _proj_index(self, feats, names, offs, N):
-        """[N, sum of bags] rows of P: feature value v of table k -> offs[k] + v, 0 -> 0."""
+        """[N, sum of bags] rows of P: feature value v of table k -> offs[k] + v, 0 -> 0
+        (grk_proj_index: one launch on the GPU)."""
+        blocks = [(feats[k].reshape(N, -1), offs[k]) for k in names]
+        if blocks[0][0].is_cuda and not torch.compiler.is_compiling() \
+                and len({b.dtype for b, _ in blocks}) == 1 and blocks[0][0].dtype in (torch.int32, torch.int64):
+            return K.proj_index(blocks, N)
         x = torch.cat([feats[k].reshape(N, -1) for k in names], 1)
         key = tuple((offs[k], feats[k].reshape(N, -1).shape[1]) for k in names)
         off = self._proj_off_cache.get(key)

@@ -375,16 +375,13 @@ class FusedAdamW:
         self.maybe_segment()
         if not self._deferred:
             return
-        seq, pos, neg, tt = (x.long() for x in batch[:4])
         # Padding (id 0, and tokens of the other type) -> -1, skipped by the kernel:
         # thousands of duplicate claims on row 0 would serialise on one atomic.
         # The padding row is brought up at the segment flush; it is zero and gets
         # no gradient (nn.Embedding padding_idx), and a g = 0 step maps a zero
         # (p, m, v) row to exactly zero, so reading it early changes nothing.
-        skip = torch.full((), -1, dtype=torch.long, device=seq.device)
-        item = torch.cat([torch.where(tt == 1, seq, 0).reshape(-1), pos.reshape(-1), neg.reshape(-1)])
-        ids = {'item': torch.where(item > 0, item, skip),
-               'user': torch.where((tt == 2) & (seq > 0), seq, skip).reshape(-1)}
+        item, user = K.batch_row_ids(*batch[:4], with_user='user' in self._deferred)
+        ids = {'item': item, 'user': user}
         for name, g in self._deferred.items():
             K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock, ids[name])
         self._begun = self.t

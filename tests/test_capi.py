@@ -74,3 +74,17 @@ def test_workspace_query_needs_no_device(lib):
     partials = -(-n // ch) * 2 * 512 * 4           # chunked mode: two piece sums per chunk
     assert got >= n * per_occ + partials and got < n * per_occ + partials + (1 << 20)
     assert lib.lib().grk_sort_pairs_workspace(n) > 0
+
+
+def test_index_entry_points_refuse_bad_blocks(lib):
+    """grk_proj_index / grk_batch_row_ids (round 4) check their blocks on the host."""
+    h = lib.lib()
+    blocks = (lib.GrkIndexBlock * 2)()
+    blocks[0] = lib.GrkIndexBlock(16, 4, 4, 0, 1)
+    blocks[1] = lib.GrkIndexBlock(16, 3, 3, 5, 1)          # out_col 5 != 4: blocks must tile the columns
+    assert h.grk_proj_index(blocks, 2, lib.GRK_I64, 10, 16, 16, None) == lib.GRK_EINVAL
+    assert b'out_col' in h.grk_last_error()
+    blocks[1] = lib.GrkIndexBlock(16, 3, 3, 4, 1)
+    assert h.grk_proj_index(blocks, 2, lib.GRK_I64, 10, 16, 6, None) == lib.GRK_EINVAL   # out_ld < 7 columns
+    assert h.grk_proj_index(blocks, 0, lib.GRK_I64, 10, 16, 16, None) == lib.GRK_EINVAL
+    assert h.grk_batch_row_ids(None, None, None, None, 7, 4, None, None, None) == lib.GRK_EINVAL
