@@ -191,9 +191,6 @@ __global__ void __launch_bounds__(256) k_wgrad(const bf16_t* __restrict__ A, int
 //   * columns past M / N read a valid column instead (their outputs are
 //     never stored); K must be a multiple of 32 (no partial steps: the
 //     slices are whole steps) -- else the register-staged kernel runs.
-constexpr int kWgStages = 4;
-constexpr int kWgStage = 2 * kWgImg;            // dY + X images of one step: 16 KiB
-
 __device__ __forceinline__ int wg_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
 // One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4) to the wave-uniform LDS
@@ -215,45 +212,107 @@ __device__ __forceinline__ void wg_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <bool DB>
-__global__ void __launch_bounds__(256) k_wgrad_lds(const bf16_t* __restrict__ A, int64_t lda,
-                                                   const bf16_t* __restrict__ B, int64_t ldb, int K, int M, int N,
-                                                   int kchunk, float* __restrict__ part, float* __restrict__ dbpart) {
-  __shared__ __attribute__((aligned(16))) char smem[kWgStages * kWgStage];  // 64 KiB
+// Ring geometry: WM x WN waves, each owning a 64 x 64 quarter-tile of the output
+// (2 x 2 MFMA 32x32x16 tiles), so a workgroup owns a (64 WM) x (64 WN) tile; NST
+// LDS stages of one 32-row step each (dY image [32][64 WM], X image [32][64 WN]),
+// NST - 1 steps issued ahead.  <2, 2, 4>: 128 x 128 tiles, 64 KiB, two
+// workgroups per CU; <4, 2, 6>: 256 x 128 tiles, 144 KiB, one workgroup of 8
+// waves per CU -- a third fewer operand bytes per FLOP and 4 steps in flight
+// (an LDS-DMA lands ~1.1 us after issue, MI355X_MICROARCH.md).
+template <int WM, int WN, int NST>
+struct WgRing {
+  static constexpr int TM = 64 * WM, TN = 64 * WN;   // output tile rows (M) / columns (N)
+  static constexpr int RBA = 2 * TM, RBB = 2 * TN;   // image row bytes
+  static constexpr int IMGA = kWgK * RBA, IMGB = kWgK * RBB;
+  static constexpr int STAGE = IMGA + IMGB;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int PWA = IMGA / 1024 / NW, PWB = IMGB / 1024 / NW;   // DMA instructions per wave and stage
+  static constexpr int P = PWA + PWB;
+  static_assert(IMGA % (1024 * NW) == 0 && IMGB % (1024 * NW) == 0, "images must split evenly over the waves");
+  static_assert(NST >= 3 && NST * STAGE <= 160 * 1024, "ring too large for the LDS");
+};
+
+// Fragment over k rows [k0, k0+16) of an image with RB-byte rows (wg_frag's map).
+template <int RB>
+__device__ __forceinline__ bf16x8 ring_frag(const char* img, int k0, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
+  const int row = k0 + 4 * (g >> 1) + (i >> 2);
+  const int sub = 2 * (col & 7);
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(img + row * RB + 16 * ((col >> 3) ^ wg_swz(row)) + sub));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(img + (row + 8) * RB + 16 * ((col >> 3) ^ wg_swz(row + 8)) + sub));
+  const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
+  bf16x8 f;
+  f[0] = l4[0]; f[1] = l4[1]; f[2] = l4[2]; f[3] = l4[3];
+  f[4] = h4[0]; f[5] = h4[1]; f[6] = h4[2]; f[7] = h4[3];
+  return f;
+}
+
+// Retire the oldest step in flight: at most `ahead` later stages (P DMA instructions
+// each) may stay outstanding.
+template <int P, int NST>
+__device__ __forceinline__ void ring_wait(int ahead) {
+  static_assert(NST - 2 <= 5, "ring_wait covers at most 5 stages ahead");
+  if (ahead >= NST - 2) ahead = NST - 2;
+  switch (ahead) {
+    case 5: wg_wait_barrier<5 * P>(); break;
+    case 4: wg_wait_barrier<4 * P>(); break;
+    case 3: wg_wait_barrier<3 * P>(); break;
+    case 2: wg_wait_barrier<2 * P>(); break;
+    case 1: wg_wait_barrier<1 * P>(); break;
+    default: wg_wait_barrier<0>(); break;
+  }
+}
+
+template <bool DB, int WM, int WN, int NST>
+__global__ void __launch_bounds__(64 * WM * WN) k_wgrad_lds(const bf16_t* __restrict__ A, int64_t lda,
+                                                            const bf16_t* __restrict__ B, int64_t ldb, int K, int M,
+                                                            int N, int kchunk, float* __restrict__ part,
+                                                            float* __restrict__ dbpart) {
+  using G = WgRing<WM, WN, NST>;
+  __shared__ __attribute__((aligned(16))) char smem[NST * G::STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w & 1, wn = w >> 1, r = lane & 31, hh = lane >> 5;
+  const int wm = w % WM, wn = w / WM, r = lane & 31, hh = lane >> 5;
   const unsigned nx = gridDim.x, my = gridDim.y;
   const unsigned total = nx * my * gridDim.z;
   const unsigned phys = blockIdx.x + nx * (blockIdx.y + my * blockIdx.z);
   const unsigned logical = total % 8 == 0 ? (phys % 8) * (total / 8) + phys / 8 : phys;
   const int bx = (int)(logical % nx), by = (int)((logical / nx) % my), s = (int)(logical / (nx * my));
-  const int n0 = bx * kWgTile, m0 = by * kWgTile;
+  const int n0 = bx * G::TN, m0 = by * G::TM;
   const int kb = s * kchunk, ke = min(K, kb + kchunk);
   const int nsteps = ke > kb ? (ke - kb) / kWgK : 0;
   const bool do_db = DB && bx == 0 && wn == 0;
-  // this lane's two staged rows per image and step: row group 2w + i, row 4 (2w + i) + (lane >> 4)
-  const int slot = lane & 15;
-  const bf16_t* pa[2];
-  const bf16_t* pb[2];
+  // this lane's source rows: DMA instruction q of an image covers rows [q * 1024 / RB, ...)
+  const bf16_t* pa[G::PWA];
+  const bf16_t* pb[G::PWB];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 4 * (2 * w + i) + (lane >> 4);
-    const int chunk = slot ^ wg_swz(row);
-    const int ma = m0 + 8 * chunk, nb = n0 + 8 * chunk;
+  for (int i = 0; i < G::PWA; ++i) {
+    constexpr int CPR = G::RBA / 16;   // 16-byte chunks per row
+    const int q = w * G::PWA + i, row = q * (1024 / G::RBA) + lane / CPR;
+    const int ma = m0 + 8 * ((lane % CPR) ^ wg_swz(row));
     pa[i] = A + (int64_t)(kb + row) * lda + (ma < M ? ma : 0);
+  }
+#pragma unroll
+  for (int i = 0; i < G::PWB; ++i) {
+    constexpr int CPR = G::RBB / 16;
+    const int q = w * G::PWB + i, row = q * (1024 / G::RBB) + lane / CPR;
+    const int nb = n0 + 8 * ((lane % CPR) ^ wg_swz(row));
     pb[i] = B + (int64_t)(kb + row) * ldb + (nb < N ? nb : 0);
   }
-  // wave-uniform LDS byte address of this wave's first row group in stage 0
+  // wave-uniform LDS byte address of stage 0
   const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane(
-      (int)((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem + 2 * w * 1024));
+      (int)((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem));
+  const unsigned wu = (unsigned)__builtin_amdgcn_readfirstlane(w);   // wave-uniform: the DMA base is an SGPR
   auto issue = [&](int step, int buf) {
-    const unsigned base = lds0 + buf * kWgStage;
+    const unsigned base = lds0 + buf * G::STAGE;
     const int64_t ka = (int64_t)step * kWgK * lda, kbb = (int64_t)step * kWgK * ldb;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      wg_dma16(pa[i] + ka, base + i * 1024);
-      wg_dma16(pb[i] + kbb, base + kWgImg + i * 1024);
-    }
+    for (int i = 0; i < G::PWA; ++i) wg_dma16(pa[i] + ka, base + (wu * G::PWA + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < G::PWB; ++i) wg_dma16(pb[i] + kbb, base + G::IMGA + (wu * G::PWB + i) * 1024);
   };
   f32x16 acc[2][2];
 #pragma unroll
@@ -262,22 +321,19 @@ __global__ void __launch_bounds__(256) k_wgrad_lds(const bf16_t* __restrict__ A,
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
   float cs[2] = {0.f, 0.f};
 
-  for (int t = 0; t < kWgStages - 1 && t < nsteps; ++t) issue(t, t);
+  for (int t = 0; t < NST - 1 && t < nsteps; ++t) issue(t, t);
   for (int t = 0; t < nsteps; ++t) {
-    const int ahead = nsteps - 1 - t;   // steps issued after t that may stay in flight (<= 2)
-    if (ahead >= 2) wg_wait_barrier<8>();
-    else if (ahead == 1) wg_wait_barrier<4>();
-    else wg_wait_barrier<0>();
-    if (t + kWgStages - 1 < nsteps) issue(t + kWgStages - 1, (t + kWgStages - 1) & (kWgStages - 1));
-    const char* ia = smem + (t & (kWgStages - 1)) * kWgStage;
-    const char* ib = ia + kWgImg;
+    ring_wait<G::P, NST>(nsteps - 1 - t);
+    if (t + NST - 1 < nsteps) issue(t + NST - 1, (t + NST - 1) % NST);
+    const char* ia = smem + (t % NST) * G::STAGE;
+    const char* ib = ia + G::IMGA;
 #pragma unroll
     for (int ks = 0; ks < kWgK / 16; ++ks) {
       bf16x8 fa[2], fb[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = wg_frag(ia, 16 * ks, 64 * wm + 32 * i, lane);
+      for (int i = 0; i < 2; ++i) fa[i] = ring_frag<G::RBA>(ia, 16 * ks, 64 * wm + 32 * i, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) fb[j] = wg_frag(ib, 16 * ks, 64 * wn + 32 * j, lane);
+      for (int j = 0; j < 2; ++j) fb[j] = ring_frag<G::RBB>(ib, 16 * ks, 64 * wn + 32 * j, lane);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -397,6 +453,32 @@ int wgrad_splits(int64_t K, int64_t M, int64_t N) {
   return S;
 }
 
+// Kernel plan of a shape: which ring (kind 0: the register-staged kernel, K not a
+// multiple of 32; 1: 128 x 128 tiles, two workgroups per CU; 2: 256 x 128 tiles, one
+// 8-wave workgroup per CU, for M >= 1024 -- the uvqk weight gradients), the tile and
+// the K split.  GRK_WGRAD_RING=1 / 2 forces a ring where it applies (A/B builds).
+struct WgPlan {
+  int kind, tm, tn, S;
+};
+WgPlan wgrad_plan(int64_t K, int64_t M, int64_t N) {
+  static const int force = [] {
+    const char* e = getenv("GRK_WGRAD_RING");
+    return e ? atoi(e) : -1;
+  }();
+  static const bool force_reg = getenv("GRK_WGRAD_REG") != nullptr;
+  WgPlan p{0, kWgTile, kWgTile, wgrad_splits(K, M, N)};
+  if (K % kWgK || force_reg) return p;
+  const bool big = force == 2 || (force != 1 && M >= 1024);
+  if (!big) {
+    p.kind = 1;
+    return p;
+  }
+  p = WgPlan{2, 256, 128, 1};
+  const int64_t tiles = ((M + 255) / 256) * ((N + 127) / 128);
+  while (p.S < 64 && tiles * p.S < 256 && K >= (int64_t)p.S * 2 * 512) p.S *= 2;   // one workgroup per CU
+  return p;
+}
+
 }  // namespace
 }  // namespace grk
 
@@ -404,7 +486,7 @@ using namespace grk;
 
 extern "C" size_t grk_wgrad_workspace(int64_t k, int64_t m, int64_t n) {
   if (k < 0 || m <= 0 || n <= 0) return 0;
-  const int S = wgrad_splits(k, m, n);
+  const int S = wgrad_plan(k, m, n).S;
   return ((size_t)S * m * n + (size_t)S * m) * sizeof(float);
 }
 
@@ -423,27 +505,31 @@ extern "C" int grk_wgrad(const void* dy, int64_t ld_dy, const void* x, int64_t l
   GRK_CHECK_ARG(dw_dtype == GRK_F32 || dw_dtype == GRK_BF16, "dw must be fp32 or bf16");
   GRK_CHECK_ARG(ld_dw >= n && ld_dw % 4 == 0, "ld_dw must be >= n and a multiple of 4");
   GRK_CHECK_ARG(workspace_bytes >= grk_wgrad_workspace(k, m, n), "workspace smaller than grk_wgrad_workspace()");
-  const int S = wgrad_splits(k, m, n);
+  const WgPlan pl = wgrad_plan(k, m, n);
+  const int S = pl.S;
   hipStream_t s = (hipStream_t)stream;
   float* part = (float*)workspace;
   float* dbp = part + (size_t)S * m * n;
   const int kchunk = (int)(((k + S - 1) / S + kWgK - 1) / kWgK * kWgK);
-  const dim3 grid((unsigned)((n + kWgTile - 1) / kWgTile), (unsigned)((m + kWgTile - 1) / kWgTile), (unsigned)S);
-  // LDS-DMA ring for whole 32-row steps (GRK_WGRAD_REG=1: the register-staged kernel, A/B)
-  static const bool force_reg = getenv("GRK_WGRAD_REG") != nullptr;
-  if (k % kWgK == 0 && !force_reg) {
-    if (db)
-      k_wgrad_lds<true><<<grid, 256, 0, s>>>((const bf16_t*)dy, ld_dy, (const bf16_t*)x, ld_x, (int)k, (int)m, (int)n,
-                                             kchunk, part, dbp);
-    else
-      k_wgrad_lds<false><<<grid, 256, 0, s>>>((const bf16_t*)dy, ld_dy, (const bf16_t*)x, ld_x, (int)k, (int)m,
-                                              (int)n, kchunk, part, nullptr);
-  } else if (db)
-    k_wgrad<true><<<grid, 256, 0, s>>>((const bf16_t*)dy, ld_dy, (const bf16_t*)x, ld_x, (int)k, (int)m, (int)n,
-                                       kchunk, part, dbp);
-  else
-    k_wgrad<false><<<grid, 256, 0, s>>>((const bf16_t*)dy, ld_dy, (const bf16_t*)x, ld_x, (int)k, (int)m, (int)n,
-                                        kchunk, part, nullptr);
+  const dim3 grid((unsigned)((n + pl.tn - 1) / pl.tn), (unsigned)((m + pl.tm - 1) / pl.tm), (unsigned)S);
+  const bf16_t *A = (const bf16_t*)dy, *Bx = (const bf16_t*)x;
+#define GRK_WG(KERN, THREADS)                                                                               \
+  do {                                                                                                     \
+    if (db) KERN<true><<<grid, THREADS, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, dbp); \
+    else KERN<false><<<grid, THREADS, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, nullptr); \
+  } while (0)
+  if (pl.kind == 2) {
+    if (db) k_wgrad_lds<true, 4, 2, 6><<<grid, 512, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, dbp);
+    else k_wgrad_lds<false, 4, 2, 6><<<grid, 512, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part,
+                                                          nullptr);
+  } else if (pl.kind == 1) {
+    if (db) k_wgrad_lds<true, 2, 2, 4><<<grid, 256, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, dbp);
+    else k_wgrad_lds<false, 2, 2, 4><<<grid, 256, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part,
+                                                          nullptr);
+  } else {
+    GRK_WG(k_wgrad, 256);
+  }
+#undef GRK_WG
   GRK_LAUNCH_CHECK();
   const int64_t work = m * n / 4;
   const unsigned g = (unsigned)std::min<int64_t>((work + 255) / 256, 4096);

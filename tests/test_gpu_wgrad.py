@@ -2,7 +2,8 @@
 fp64 reference of the same bf16 operands, on the bench's shapes (K = B*T
 tokens, the HSTU projections) and on ragged edges; run-to-run bitwise
 determinism (in-order slice reduction, no atomics).  K a multiple of 32 takes
-the LDS-DMA ring kernel (k_wgrad_lds), other K the register-staged one."""
+the LDS-DMA ring kernels (k_wgrad_lds: 128 x 128 tiles, or 256 x 128 tiles at
+M >= 1024), other K the register-staged one."""
 import pytest
 import torch
 
@@ -19,7 +20,9 @@ def nrel(a, b):
                                    (3, 8, 8), (0, 16, 24), (777, 264, 1032),
                                    (5000, 1032, 1288), (25728, 1024, 1024), (300, 2048, 520),
                                    # K % 32 == 0: the LDS-DMA ring kernel, ragged M / N tiles, short slices
-                                   (14336, 2048, 512), (1024, 136, 72), (3200, 264, 1032), (32, 8, 8), (96, 520, 2048)])
+                                   (14336, 2048, 512), (1024, 136, 72), (3200, 264, 1032), (32, 8, 8), (96, 520, 2048),
+                                   # M >= 1024: the 256 x 128-tile ring (ragged M / N tiles, short slices)
+                                   (3200, 1032, 1288), (64, 1024, 8), (28672, 4096, 512)])
 def test_wgrad_matches_fp64(K, M, N):
     from tencent_recommendation_2025_amd import kernels as Kn
     g = torch.Generator(device=DEV).manual_seed(K + M + N)
