@@ -332,8 +332,11 @@ class ShardedFusedAdamW(FusedAdamW):
                                             requires_grad=False)
             sharded_refs[name] = ShardedRef(name, emb.weight)
         small_keys = tuple(k for k in tables if k not in self.SHARDED and k != 'pos_emb')
+        # dense parameters stay on torch's AdamW here: their gradients are all-reduced in
+        # buckets (GradBuckets over self.dense's parameters) before step() updates them
         super().__init__(model, lr, betas, eps, weight_decay, table_mode, table_dtype,
-                         groups=(('pos', ('pos_emb',)), ('small', small_keys)), defer_period=defer_period)
+                         groups=(('pos', ('pos_emb',)), ('small', small_keys)), defer_period=defer_period,
+                         dense_flat=False)
         model._table_refs.update(sharded_refs)
         # replicated groups: their fp32 gradients share one buffer (one all-reduce)
         self.replicated = list(self.groups)
