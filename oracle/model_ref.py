@@ -48,13 +48,31 @@ class RefMHA(torch.nn.Module):
         return self.out_linear(o.transpose(1, 2).contiguous().view(B, T, self.hidden_units)), None
 
 
+class _RoundBF16(torch.autograd.Function):
+    """x rounded to bf16 (kept in x's dtype); the gradient rounded to bf16 as well."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
 class RefHSTU(torch.nn.Module):
-    """HSTU layer (parity unpinned; see oracle/hstu.py).  Same math, torch autograd."""
+    """HSTU layer (parity unpinned; see oracle/hstu.py).  Same math, torch autograd.
+
+    bf16_core=True: the fp32 math fed the grk HSTU core's bf16 storage points
+    (ops.hstu_core: the u|v|q|k pre-activation, the attention output o and the
+    gated output y are bf16 tensors, and so are their gradients dpre, do, dy) --
+    the checker that separates that storage rounding from the kernels' math."""
 
     def __init__(self, d, h, p, num_buckets, num_time_buckets=0, fp8=False):
         super().__init__()
         self.hidden_units, self.num_heads, self.head_dim, self.dropout_rate = d, h, d // h, p
         self.fp8 = fp8  # config C5: SiLU'd q/k/v rounded to OCP e4m3, straight-through gradient
+        self.bf16_core = False
         self.uvqk = torch.nn.Linear(d, 4 * d)
         self.rab = torch.nn.Parameter(torch.zeros(h, num_buckets))
         self.rab_t = torch.nn.Parameter(torch.zeros(h, num_time_buckets)) if num_time_buckets else None
@@ -63,7 +81,8 @@ class RefHSTU(torch.nn.Module):
 
     def forward(self, query, key, value, attn_mask=None, timestamps=None, key_valid=None):
         B, T, D = query.shape
-        u, v, q, k = torch.split(F.silu(self.uvqk(query)), D, dim=-1)
+        rb = _RoundBF16.apply if self.bf16_core else (lambda x: x)
+        u, v, q, k = torch.split(F.silu(rb(self.uvqk(query))), D, dim=-1)
         if self.fp8:
             r8 = lambda x: x + (x.clamp(-448, 448).to(torch.float8_e4m3fn).to(x.dtype) - x).detach()
             v, q, k = r8(v), r8(q), r8(k)
@@ -78,8 +97,8 @@ class RefHSTU(torch.nn.Module):
             _, bt = hstu._time_bias(np.asarray(timestamps), np.asarray(key_valid), np.zeros(self.rab_t.shape))
             s = s + self.rab_t[:, torch.from_numpy(bt)].transpose(0, 1)
         a = F.silu(s) * (1.0 / T) * attn_mask.unsqueeze(1).to(s.dtype)
-        o = torch.matmul(a, v).transpose(1, 2).contiguous().view(B, T, D)
-        y = self.attn_norm(o) * u
+        o = rb(torch.matmul(a, v).transpose(1, 2).contiguous().view(B, T, D))
+        y = rb(self.attn_norm(o) * u)
         y = F.dropout(y, self.dropout_rate, self.training)
         return self.out_linear(y), None
 

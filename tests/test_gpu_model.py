@@ -9,6 +9,7 @@
 * The fused trainer (table groups + grk_table_adamw) against the drop-in
   path + torch AdamW on the same batch.
 """
+import contextlib
 import os
 from types import SimpleNamespace
 
@@ -151,30 +152,57 @@ def test_list_of_dicts_input_equals_tensor_input(golden, tmp_path):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
 
 
+# The fp32 HSTU model's attention core (ops.hstu_core) stores its pre-activation,
+# attention output and gated output -- and their gradients -- as bf16 tensors.  Against
+# the plain fp32 oracle that storage alone costs ~5e-3 on the logits (HSTU_FP32_TOL).
+# Against the oracle fed the same bf16 storage points (RefHSTU.bf16_core) the kernels'
+# own math is held to HSTU_CORE_TOL: the north star's 1e-3 on the logits.
+HSTU_FP32_TOL = dict(logits=5e-3, grad=2e-2)
+HSTU_CORE_TOL = dict(logits=1e-3, grad=5e-3)
+
+
 def test_hstu_model_matches_oracle(golden):
     torch.manual_seed(0)
     m, g, batch, args, d, stats = build(golden, 'o1', block='hstu')
-    ref = model_ref.RefBaselineModel(int(d['usernum']), int(d['itemnum']), stats, feat_types(), args, variant='o1',
-                                     block='hstu')
-    model_ref.init_params(ref, seed=3)
-    with torch.no_grad():
-        for blk in ref.attention_layers:
-            blk.rab.normal_(0, 0.3)
-    assert set(ref.state_dict()) == set(m.state_dict())
-    m.load_state_dict(ref.state_dict())
     cpu_batch = [x.cpu() if torch.is_tensor(x) else {k: v.cpu() for k, v in x.items()} for x in batch]
     seq, pos, neg, tt, ntt, nat, sf, pf, nf = cpu_batch
-    rpl, rnl = ref(seq, pos, neg, tt, ntt, sf, pf, nf)
-    rloss = model_ref.bce_loss(rpl, rnl, ntt)
-    rloss.backward()
+    refs = {}
+    for core in (False, True):
+        ref = model_ref.RefBaselineModel(int(d['usernum']), int(d['itemnum']), stats, feat_types(), args,
+                                         variant='o1', block='hstu')
+        model_ref.init_params(ref, seed=3)
+        with torch.no_grad():
+            gen = torch.Generator().manual_seed(4)
+            for n, p in ref.named_parameters():   # live: the reference init zeroes LayerNorm gains
+                if p.dim() == 1 and 'norm' in n and n.endswith('weight'):
+                    p.copy_(1.0 + 0.1 * torch.randn(p.shape, generator=gen))
+                elif p.dim() == 1:
+                    p.copy_(0.02 * torch.randn(p.shape, generator=gen))
+            for blk in ref.attention_layers:
+                blk.rab.normal_(0, 0.3, generator=gen)
+                blk.bf16_core = core
+        rpl, rnl = ref(seq, pos, neg, tt, ntt, sf, pf, nf)
+        model_ref.bce_loss(rpl, rnl, ntt).backward()
+        refs[core] = (ref, rpl.detach(), rnl.detach())
+    ref = refs[False][0]
+    assert float(refs[False][1].norm()) > 0, 'live parameters: non-zero logits'
+    assert set(ref.state_dict()) == set(m.state_dict())
+    m.load_state_dict(ref.state_dict())
     pl, nl = m(*batch)
-    assert nrel(pl.detach().cpu(), rpl.detach()) < 5e-3
     loss = ref_loss(pl, nl, batch[4], m, 0.0)
     loss.backward()
-    for (name, p), (_, rp) in zip(m.named_parameters(), ref.named_parameters()):
-        if rp.grad is None or float(rp.grad.norm()) == 0:
-            continue
-        assert nrel(p.grad.cpu(), rp.grad) < 2e-2, name
+    for core, tol in ((False, HSTU_FP32_TOL), (True, HSTU_CORE_TOL)):
+        ref, rpl, rnl = refs[core]
+        lerr = max(nrel(pl.detach().cpu(), rpl), nrel(nl.detach().cpu(), rnl))
+        gerr = {}
+        for (name, p), (_, rp) in zip(m.named_parameters(), ref.named_parameters()):
+            if rp.grad is not None and float(rp.grad.norm()) > 0:
+                gerr[name] = nrel(p.grad.cpu(), rp.grad)
+        print(f'hstu model vs {"bf16-core" if core else "fp32"} oracle: logits {lerr:.2e}; worst grads',
+              sorted(gerr.items(), key=lambda kv: -kv[1])[:4])
+        assert lerr < tol['logits'], (core, lerr)
+        bad = {k: v for k, v in gerr.items() if v >= tol['grad']}
+        assert not bad, (core, bad)
 
 
 def _event_times(batch, seed=0):
@@ -209,13 +237,13 @@ def test_hstu_time_bias_model_matches_oracle(golden):
     rpl, rnl = ref(seq, pos, neg, tt, ntt, sf, pf, nf, timestamps=ts)
     model_ref.bce_loss(rpl, rnl, ntt).backward()
     pl, nl = m(*batch, timestamps=ts)
-    assert max(nrel(pl.detach().cpu(), rpl.detach()), nrel(nl.detach().cpu(), rnl.detach())) < 5e-3
+    assert max(nrel(pl.detach().cpu(), rpl.detach()), nrel(nl.detach().cpu(), rnl.detach())) < HSTU_FP32_TOL['logits']
     ref_loss(pl, nl, batch[4], m, 0.0).backward()
     checked = []
     for (name, p), (_, rp) in zip(m.named_parameters(), ref.named_parameters()):
         if rp.grad is None or float(rp.grad.norm()) == 0:
             continue
-        assert nrel(p.grad.cpu(), rp.grad) < 2e-2, name
+        assert nrel(p.grad.cpu(), rp.grad) < HSTU_FP32_TOL['grad'], name
         checked.append(name)
     assert sum(n.endswith('rab_t') for n in checked) == len(m.attention_layers)
     # a zero time bias adds exact zeros: bitwise the positions-only model
@@ -248,7 +276,7 @@ def test_o1_single_head_wide_matches_oracle(golden, hidden):
     rpl, rnl = ref(seq, pos, neg, tt, ntt, sf, pf, nf)
     model_ref.bce_loss(rpl, rnl, ntt).backward()
     pl, nl = m(*batch)
-    assert max(nrel(pl.detach().cpu(), rpl.detach()), nrel(nl.detach().cpu(), rnl.detach())) < 5e-3
+    assert max(nrel(pl.detach().cpu(), rpl.detach()), nrel(nl.detach().cpu(), rnl.detach())) < HSTU_FP32_TOL['logits']
     ref_loss(pl, nl, batch[4], m, 0.0).backward()
     checked = 0
     for (name, p), (_, rp) in zip(m.named_parameters(), ref.named_parameters()):
@@ -559,27 +587,52 @@ def test_graph_replayed_steps_equal_eager_steps(period, nbt):
             assert torch.equal(a, b), name
 
 
-# measured on MI355X (round 2): loss 1.2e-4, logits 5.5e-3; gradients 1.3e-2 (attention,
-# LayerNorms), 1.6e-2 (user side), up to 4.4e-2 (item tables / itemdnn: their row sums
-# mix positive- and negative-logit terms of opposite sign, which amplifies the bf16
-# rounding of the per-token gradients)
-BENCH_TOL = dict(loss=1e-3, logits=1e-2, grad=7.5e-2)   # loss: the north star's 1e-3 for bf16 loss
+# The bf16 bound is calibrated, not guessed: the reference trains under
+# torch.amp.autocast (--use_amp, model/BaseLine/main.py:139-141,173), so the oracle
+# model is also run under CPU bf16 autocast on the same parameters and batch -- the
+# reference's own mixed-precision step -- and its distance from the fp32 oracle is the
+# measured cost of bf16 (CPU, this configuration: loss 2.3e-4, logits 5.0e-3, gradients
+# 2.2e-3 .. 5.7e-2, the item / feature tables ~4e-2: their row sums mix positive- and
+# negative-logit terms of opposite sign).  The grk step is held to the north star's
+# 1e-3 on the loss and, everywhere else, to the AMP reference's own error:
+#   logits    <= BENCH_AMP_FACTOR * amp(logits)
+#   every gradient tensor <= max(BENCH_AMP_FACTOR * amp(tensor), BENCH_GRAD_FLOOR)
+# plus BENCH_TOL as absolute ceilings.  (MI355X round 2, padded: loss 1.2e-4, logits
+# 5.5e-3, gradients 1.3e-2 .. 4.4e-2.)
+BENCH_TOL = dict(loss=1e-3, logits=1e-2, grad=7.5e-2)
+BENCH_AMP_FACTOR = 1.5
+BENCH_GRAD_FLOOR = 1e-2   # tensors whose AMP error is tiny (LayerNorm / last biases): bf16 GEMM outputs feed them
 
 
-def test_bench_config_step_matches_oracle_fp32():
+def _amp_reference(ref, cpu, bf16):
+    """The oracle's step (fp32, or under CPU bf16 autocast = the reference's --use_amp at
+    the config's bf16): loss, logits and every parameter gradient."""
+    ref.zero_grad()
+    ctx = torch.autocast('cpu', dtype=torch.bfloat16) if bf16 else contextlib.nullcontext()
+    with ctx:
+        rpl, rnl = ref(cpu[0], cpu[1], cpu[2], cpu[3], cpu[4], cpu[6], cpu[7], cpu[8])
+        rloss = model_ref.bce_loss(rpl.float(), rnl.float(), cpu[4])
+    rloss.backward()
+    grads = {n: p.grad.detach().clone() for n, p in ref.named_parameters() if p.grad is not None}
+    return rloss.detach(), rpl.detach().float(), rnl.detach().float(), grads
+
+
+@pytest.mark.parametrize('layout', ['padded', 'jagged'])
+def test_bench_config_step_matches_oracle_fp32(layout):
     """The configuration bench.py times -- fused trainer with bf16 table groups,
     bf16 autocast GEMMs (grk_gemm / grk_wgrad), HSTU blocks on the precise
-    attention kernels, fused BCE -- at reduced size (d=128 as 2 heads of hd=64
-    like the bench's heads, 2 blocks, T=61, B=16) against the oracle's fp32 CPU
-    model (oracle/model_ref.py) on the same parameters (tables rounded to bf16,
-    as the fused optimizer stores them).  The gap is bf16 autocast itself (every
-    GEMM operand rounded to bf16): loss, logits and EVERY gradient (dense
-    parameters and each table, padding rows excluded) are held to BENCH_TOL."""
+    attention kernels, fused BCE, and (layout='jagged', the bench default) the
+    span-row layout -- at reduced size (d=128 as 2 heads of hd=64 like the bench's
+    heads, 2 blocks, T=61, B=16) against the oracle's fp32 CPU model
+    (oracle/model_ref.py) on the same parameters (tables rounded to bf16, as the
+    fused optimizer stores them).  Loss, logits and EVERY gradient (dense
+    parameters and each table, padding rows excluded) are held to the bounds
+    above, calibrated by the oracle's own bf16-autocast step."""
     from tencent_recommendation_2025_amd import functional as G
+    from tencent_recommendation_2025_amd import jagged as J
     from tencent_recommendation_2025_amd import synthetic as S
     from tencent_recommendation_2025_amd.model import BaselineModel
     from tencent_recommendation_2025_amd.optim import FusedAdamW
-    from tencent_recommendation_2025_amd.train import Trainer
     cfg = S.SyntheticConfig(batch_size=16, maxlen=60, num_items=4000, num_users=500, min_len=8)
     stats, types = S.feature_schema(cfg)
     args = S.make_args(hidden_units=128, maxlen=60, num_blocks=2, num_heads=2)
@@ -601,38 +654,58 @@ def test_bench_config_step_matches_oracle_fp32():
     assert set(m.state_dict()) == set(ref.state_dict())
     m.load_state_dict(ref.state_dict())
     opt = FusedAdamW(m, lr=1e-3)
-    tr = Trainer(m, opt, loss='bce')
     batch = S.make_batch(cfg, torch.Generator(device=DEV).manual_seed(7), DEV)
     seq, pos, neg, tt, ntt, _nat, sf, pf, nf = batch
     opt.zero_grad()
     opt.begin_step(batch)
+    jag = pidx = None
+    if layout == 'jagged':
+        jag = J.layout(tt, J.capacity_for(J.span_rows(tt), 128), ntt)
+        seq, pos, neg, tt, ntt, _nat, sf, pf, nf, _ts, pidx = J.compact(batch, jag)
     with torch.autocast('cuda', dtype=torch.bfloat16):
-        h, pe, ne = m.encode(seq, pos, neg, tt, sf, pf, nf)
+        h, pe, ne = m.encode(seq, pos, neg, tt, sf, pf, nf, jagged=jag, pos_idx=pidx)
         loss = G.bce_loss(h, pe, ne, ntt)
     pl, nl = G.pair_logits(h.detach().float(), pe.detach().float(), ne.detach().float(), ntt)
     loss.backward()
+    if jag is not None:
+        J.check_error(jag.err)
     cpu = [x.cpu() if torch.is_tensor(x) else {k: v.cpu() for k, v in x.items()} for x in batch]
-    rpl, rnl = ref(cpu[0], cpu[1], cpu[2], cpu[3], cpu[4], cpu[6], cpu[7], cpu[8])
-    rloss = model_ref.bce_loss(rpl, rnl, cpu[4])
-    rloss.backward()
+    rloss, rpl, rnl, rgrad = _amp_reference(ref, cpu, bf16=False)
+    aloss, apl, anl, agrad = _amp_reference(ref, cpu, bf16=True)
+    pl, nl = pl.cpu().reshape(-1), nl.cpu().reshape(-1)
+    sel = slice(None)
+    if jag is not None:   # jagged row r holds token row_map[r] of the [B, T] batch (-1: dead)
+        rm = jag.row_map.cpu().long()
+        live = rm >= 0
+        assert int(live.sum()) == J.span_rows(batch[3])
+        pl, nl, sel = pl[live], nl[live], rm[live]
+    rpl, rnl, apl, anl = (x.reshape(-1)[sel] for x in (rpl, rnl, apl, anl))
     errs = {'loss': abs(loss.item() - rloss.item()) / abs(rloss.item()),
-            'logits': max(nrel(pl.cpu(), rpl.detach()), nrel(nl.cpu(), rnl.detach()))}
-    grads = {}
-    rp = dict(ref.named_parameters())
+            'logits': max(nrel(pl, rpl), nrel(nl, rnl))}
+    amp = {'loss': abs(aloss.item() - rloss.item()) / abs(rloss.item()),
+           'logits': max(nrel(apl, rpl), nrel(anl, rnl))}
+    grads, amp_grads = {}, {}
     for n, p in m.named_parameters():
         if p.grad is not None:
-            grads[n] = nrel(p.grad.float().cpu(), rp[n].grad)
+            grads[n] = nrel(p.grad.float().cpu(), rgrad[n])
+            amp_grads[n] = nrel(agrad[n], rgrad[n])
     for grp in opt.groups:
         dg = grp.dense_gradient().cpu()
         for key, off in grp.offsets.items():
-            want = rp[f'{key}.weight'].grad
+            want = rgrad[f'{key}.weight']
             if float(want[1:].norm()) > 0:
                 grads[f'{key}.weight'] = nrel(dg[off + 1:off + want.shape[0]], want[1:])
+                amp_grads[f'{key}.weight'] = nrel(agrad[f'{key}.weight'][1:], want[1:])
     errs['grad'] = max(grads.values())
-    print('bench-config errors:', errs, 'worst grads:', sorted(grads.items(), key=lambda kv: -kv[1])[:6])
-    assert len(grads) == sum(1 for p in ref.parameters()), sorted(set(rp) - set(grads))
-    for k, tol in BENCH_TOL.items():
-        assert errs[k] < tol, (k, errs[k], sorted(grads.items(), key=lambda kv: -kv[1])[:8])
+    amp['grad'] = max(amp_grads.values())
+    worst = sorted(((e, amp_grads[k], k) for k, e in grads.items()), reverse=True)[:8]
+    print(f'bench-config [{layout}] grk errors: {errs}; AMP reference errors: {amp}; worst grads (grk, amp):', worst)
+    assert len(grads) == sum(1 for p in ref.parameters()), sorted(set(rgrad) - set(grads))
+    assert errs['loss'] < BENCH_TOL['loss'], (errs, amp)
+    assert errs['logits'] <= min(BENCH_TOL['logits'], BENCH_AMP_FACTOR * amp['logits']), (errs, amp)
+    over = [(k, e, amp_grads[k]) for k, e in grads.items()
+            if e > min(BENCH_TOL['grad'], max(BENCH_AMP_FACTOR * amp_grads[k], BENCH_GRAD_FLOOR))]
+    assert not over, over
 
 
 @pytest.mark.parametrize('block', ['hstu', 'softmax'])
