@@ -136,7 +136,38 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_scatter(const unsigned* _
         if (q < w) pos += wcnt[q][d];
       kout[pos] = key;
       vout[pos] = val;
-      if (hnext) atomicAdd(&hnext[(int64_t)((key >> shift_next) & (kSortBins - 1)) * ntiles + pos / kSortTile], 1u);
+    }
+    if (hnext) {
+      // The next digit counted once per (next digit, output tile) group of the wave:
+      // the lanes sharing this digit AND the next one hold consecutive slots (at most
+      // two output tiles); a per-lane atomic serialises on one word for runs of equal
+      // keys (a hot row's thousands of occurrences), measured 0.9 ms per C2 step.
+      const unsigned nd = (key >> shift_next) & (kSortBins - 1);
+      unsigned long long grp = peers;
+#pragma unroll
+      for (int bit = 0; bit < kSortBits; ++bit) {
+        const bool set = (nd >> bit) & 1u;
+        const unsigned long long m = __ballot(set);
+        grp &= set ? m : ~m;
+      }
+      unsigned pos = 0;
+      if (ok) {
+        pos = base[d] + (unsigned)__popcll(peers & lt);
+#pragma unroll
+        for (int q = 0; q < NW; ++q)
+          if (q < w) pos += wcnt[q][d];
+      }
+      const int otile = (int)(pos / kSortTile);
+      const int leader = ok ? __ffsll((long long)grp) - 1 : lane;
+      const int lead_tile = __shfl(otile, leader);
+      const unsigned long long hi = __ballot(ok && otile != lead_tile) & grp;
+      if (ok) {
+        const bool first_lo = lane == leader;
+        const bool first_hi = hi != 0ull && lane == __ffsll((long long)hi) - 1;
+        if (first_lo)
+          atomicAdd(&hnext[(int64_t)nd * ntiles + lead_tile], (unsigned)__popcll(grp & ~hi));
+        if (first_hi) atomicAdd(&hnext[(int64_t)nd * ntiles + otile], (unsigned)__popcll(hi));
+      }
     }
     __syncthreads();  // every slot of this round computed from the old base
     unsigned add = 0;

@@ -479,15 +479,22 @@ class ShardedFusedAdamW(FusedAdamW):
     # -- HIP graph capture of forward + backward (train.Trainer) ------------
     def capture_state(self):
         """After the forward + backward of a captured step: what its replays rewrite
-        in place (gradient sources of every group and sink, dense gradients)."""
+        in place (gradient sources of every group and sink, dense gradients).
+        Returned to the caller, which keeps it with ITS graph: a trainer holding one
+        graph per jagged capacity restores the state of the graph it replays (the
+        buffers of another capacity's graph hold that graph's last gradients)."""
         self._captured = dict(
             groups=[(g, list(g.pending), dict(g.dense_grads), g.token_type, g.seq_len) for g in self.replicated],
             sinks={k: list(sk.sources) for k, sk in self.sinks.items()},
             grads=[(p, p.grad) for grp in self.dense.param_groups for p in grp['params']])
+        return self._captured
 
-    def restore_captured(self):
-        """Before step() after a replay: point the groups, sinks and .grad back at the graph's buffers."""
-        c = self._captured
+    def restore_captured(self, state=None):
+        """Before step() after a replay: point the groups, sinks and .grad back at the
+        buffers of the replayed graph (``state`` from its capture_state(); default the
+        last one captured)."""
+        c = self._captured if state is None else state
+        self._captured = c
         for g, pend, dg, tt, sl in c['groups']:
             g.pending, g.dense_grads, g.token_type, g.seq_len = list(pend), dict(dg), tt, sl
         self.sinks = {}

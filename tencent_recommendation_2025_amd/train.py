@@ -126,6 +126,7 @@ class Trainer:
         self._static = None
         self._static_loss = None
         self._graphs = {}        # capacity (jagged) or None -> (graph, static batch, static loss)
+        self._cap_states = {}    # row-sharded: capacity -> the optimizer's capture_state() of that graph
         self._warm = {}
         self._pool = None
         self._side = None
@@ -263,7 +264,7 @@ class Trainer:
         if self._sharded:
             self.opt.prepare(self._static, key=batch[0])
             self._g.replay()
-            self.opt.restore_captured()
+            self.opt.restore_captured(self._cap_states.get(key))
             self.opt.step()
         else:
             self.opt.maybe_segment()
@@ -306,7 +307,8 @@ class Trainer:
             # one memory pool for every captured capacity: the graphs never run at once,
             # and nothing a replay leaves behind is read after another graph ran (the
             # loss is cloned right after its replay; parameters and optimizer state
-            # live outside the pool)
+            # live outside the pool; row-sharded, the eager step() reads the replayed
+            # graph's own gradient buffers, kept alive by its _cap_states entry)
             self._pool = torch.cuda.graph_pool_handle()
         cur = torch.cuda.current_stream()
         self._side.wait_stream(cur)
@@ -333,7 +335,7 @@ class Trainer:
         if self._sharded:
             if buckets is not None:
                 buckets.enabled = True
-            self.opt.capture_state()
+            self._cap_states[key] = self.opt.capture_state()
             self.opt.step()
         return self._static_loss.clone()
 

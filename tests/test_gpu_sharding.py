@@ -45,7 +45,10 @@ def test_sharded_optimizer_world1_equals_fused(pg):
     from tencent_recommendation_2025_amd.train import Trainer
     m1, cfg = build()
     m2, _ = build()
-    t1 = Trainer(m1, FusedAdamW(m1, lr=2e-3, table_dtype=torch.float32, defer_period=2), loss='bce', amp_dtype=None)
+    # dense_flat=False: the sharded optimizer keeps the dense parameters on torch's AdamW
+    # (their gradients are all-reduced in buckets), so its twin does too
+    t1 = Trainer(m1, FusedAdamW(m1, lr=2e-3, table_dtype=torch.float32, defer_period=2, dense_flat=False), loss='bce',
+                 amp_dtype=None)
     t2 = Trainer(m2, ShardedFusedAdamW(m2, lr=2e-3, table_dtype=torch.float32, defer_period=2), loss='bce', amp_dtype=None)
     g = torch.Generator(device=DEV).manual_seed(0)
     batches = [S.make_batch(cfg, g, DEV) for _ in range(5)]
@@ -120,7 +123,8 @@ def test_shards_built_directly_equal_materialized_table(pg):
     m1, m2 = models
     materialize_tables_(m1, seed=5)
     assert m2.item_emb.weight.numel() == 0
-    t1 = Trainer(m1, FusedAdamW(m1, lr=2e-3, table_dtype=torch.float32, defer_period=2), loss='bce', amp_dtype=None)
+    t1 = Trainer(m1, FusedAdamW(m1, lr=2e-3, table_dtype=torch.float32, defer_period=2, dense_flat=False), loss='bce',
+                 amp_dtype=None)
     opt2 = ShardedFusedAdamW(m2, lr=2e-3, table_dtype=torch.float32, defer_period=2, init_seed=5)
     for k in ('item_emb', 'user_emb'):
         assert torch.equal(opt2.shard_table(k), getattr(m1, k).weight.detach()), k
@@ -168,13 +172,10 @@ def test_capture_stream_is_private_never_a_pool_stream(pg):
     assert float(x[0]) == 1.0
 
 
-# Jagged rows under the row-sharded optimizer (train.jagged_remaps): written in
-# round 3 after the GPU budget closed, opt-in until it has run on hardware.
-SHARDED_JAGGED = pytest.mark.skipif(os.environ.get('GRK_SHARDED_JAGGED_TESTS') != '1',
-                                    reason='sharded + jagged: opt-in until verified on hardware')
-
-
-@SHARDED_JAGGED
+# Jagged rows under the row-sharded optimizer (train.jagged_remaps).  Its first
+# hardware run (round 4) found the graph replays of the first capacity stepping
+# with the gradient buffers of the second capacity's graph (one capture state per
+# optimizer): the states are now kept per graph (Trainer._cap_states).
 def test_sharded_jagged_equals_sharded_padded_and_graph_replay(pg):
     """World 1, fp32: the row-sharded trainer on jagged rows == on the padded batch
     (losses 1e-4, parameters and shards within the world-1 bounds); the jagged
