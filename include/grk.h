@@ -245,7 +245,10 @@ int grk_stamp_rows_dev(int32_t* last, const int64_t* uniq_ids, const int32_t* un
 /* grk_table_adamw_dev over a whole table whose gradient comes as dense blocks:
  * ranges (sorted by row_start, disjoint, at most 64) give rows [row_start,
  * row_end) the gradient rows grad + (row - row_start) * grad_ld (bf16 or
- * fp32); every other row takes g = 0 (dense parity).  One launch. */
+ * fp32); every other row takes g = 0 (dense parity).  One launch.
+ * shadow (may be NULL; fp32 params only, 16-byte aligned): the updated
+ * parameters rounded to bf16, same [num_rows, dim] layout -- the bf16 GEMM
+ * operands of the dense layers (optim.DenseFlat), kept in step by the update. */
 typedef struct grk_grad_range {
   int64_t row_start, row_end;
   const void* grad;
@@ -256,7 +259,7 @@ typedef struct grk_grad_range {
 int grk_table_adamw_ranges_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows,
                                int dim, const grk_grad_range* ranges, int num_ranges,
                                const grk_adamw_hparams* hp_ring, int32_t ring_len, const int32_t* t_dev,
-                               void* stream);
+                               void* shadow, void* stream);
 
 size_t grk_table_l2_norm_workspace(void);
 int grk_table_l2_norm(const void* param, int param_dtype, int64_t num_rows, int dim, float l2, float* norm,

@@ -265,17 +265,33 @@ __global__ void k_segments(const unsigned* __restrict__ keys, const int* __restr
 // launches) is needed when nothing is written per unique row.  The distinct-row
 // count is added once per wave (one add per head contended on a single word:
 // 29 us per call on MI355X, round 4).
+// Grid-stride (kSegKeyBlocks workgroups at most): the distinct-row count is summed
+// per workgroup and added once per workgroup -- one atomic per wave on the single
+// counter serialised (~14k waves at C2: 29-46 us per call).
+constexpr int kSegKeyBlocks = 512;
 __global__ void __launch_bounds__(256) k_segments_key(const unsigned* __restrict__ keys, int64_t n, unsigned sentinel,
                                                       int* __restrict__ seg_start, int* __restrict__ seg_end,
                                                       int32_t* __restrict__ count) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned k = i < n ? keys[i] : sentinel;
-  const bool live = k != sentinel;
-  const bool head = live && (i == 0 || keys[i - 1] != k);
-  if (head) seg_start[k] = (int)i;
-  if (live && (i == n - 1 || keys[i + 1] != k)) seg_end[k] = (int)(i + 1);
-  const unsigned long long heads = __ballot(head);
-  if ((threadIdx.x & 63) == 0 && heads) atomicAdd(count, (int)__popcll(heads));
+  __shared__ int wsum[4];
+  int heads = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned k = keys[i];
+    if (k == sentinel) continue;
+    const bool head = i == 0 || keys[i - 1] != k;
+    if (head) {
+      seg_start[k] = (int)i;
+      ++heads;
+    }
+    if (i == n - 1 || keys[i + 1] != k) seg_end[k] = (int)(i + 1);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) heads += __shfl_xor(heads, off);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = heads;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (t) atomicAdd(count, t);
+  }
 }
 
 // ------------------------------------------------- segmented reduction ----
@@ -1226,7 +1242,8 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   ws.keys_out = skeys;  // the sorted pairs (either buffer of the ping-pong)
   ws.gptr_out = sgptr;
   if (by_key) {
-    k_segments_key<<<g, B, 0, s>>>(ws.keys_out, total, sentinel, ws.seg_start, ws.seg_end, uniq_count);
+    k_segments_key<<<g < kSegKeyBlocks ? g : kSegKeyBlocks, B, 0, s>>>(ws.keys_out, total, sentinel, ws.seg_start,
+                                                                       ws.seg_end, uniq_count);
     GRK_LAUNCH_CHECK();
     ws.pos = nullptr;
   } else {

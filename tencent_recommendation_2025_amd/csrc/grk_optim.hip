@@ -265,10 +265,13 @@ struct GradRanges {
   int n;
 };
 
+// shadow (fp32 params only, may be null): the updated parameters also written
+// as bf16 in the same [num_rows, dim] layout -- the bf16 GEMM operand of the
+// dense layers, so the forward reads it instead of casting every weight per step.
 template <typename P, int NV>
 __global__ void __launch_bounds__(256) k_adamw_ranges(P* __restrict__ param, float* __restrict__ m,
                                                       float* __restrict__ v, int64_t num_rows, int dim, GradRanges gr,
-                                                      HpArg hpa) {
+                                                      HpArg hpa, bf16_t* __restrict__ shadow) {
   const int q = dim / NV;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= num_rows * q) return;
@@ -294,7 +297,20 @@ __global__ void __launch_bounds__(256) k_adamw_ranges(P* __restrict__ param, flo
     }
   }
   const int64_t off = row * dim + c;
-  adam_vec<P, NV>(param + off, m + off, v + off, g, adam_step(resolve(hpa)));
+  float pv[NV], mv[NV], vv[NV];
+  load_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
+  const AdamStep st = adam_step(resolve(hpa));
+#pragma unroll
+  for (int e = 0; e < NV; ++e) adam1(pv[e], mv[e], vv[e], g[e], st);
+  store_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
+  if (shadow) {
+    unsigned w[NV / 2];
+#pragma unroll
+    for (int k = 0; k < NV / 2; ++k)
+      w[k] = (unsigned)f32_to_bf16(pv[2 * k]) | ((unsigned)f32_to_bf16(pv[2 * k + 1]) << 16);
+    if constexpr (NV == 8) *reinterpret_cast<uint4*>(shadow + off) = make_uint4(w[0], w[1], w[2], w[3]);
+    else *reinterpret_cast<uint2*>(shadow + off) = make_uint2(w[0], w[1]);
+  }
 }
 
 // Catch-up (deferred dense-parity updates): one wave per row; lane 0 claims
@@ -595,12 +611,14 @@ extern "C" int grk_table_l2_norm(const void* param, int param_dtype, int64_t num
 extern "C" int grk_table_adamw_ranges_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
                                           int64_t num_rows, int dim, const grk_grad_range* ranges, int num_ranges,
                                           const grk_adamw_hparams* hp_ring, int32_t ring_len, const int32_t* t_dev,
-                                          void* stream) {
+                                          void* shadow, void* stream) {
   clear_error();
   GRK_CHECK_ARG(num_rows >= 0, "num_rows must be >= 0");
   if (num_rows == 0) return GRK_OK;
   GRK_CHECK_ARG(param && exp_avg && exp_avg_sq, "param / exp_avg / exp_avg_sq required");
   GRK_CHECK_ARG(param_dtype == GRK_F32 || param_dtype == GRK_BF16, "bad param dtype");
+  GRK_CHECK_ARG(!shadow || (param_dtype == GRK_F32 && (uintptr_t)shadow % 16 == 0),
+                "shadow: fp32 params only, 16-byte aligned");
   GRK_CHECK_ARG(dim > 0 && dim % 4 == 0, "dim must be a multiple of 4");
   GRK_CHECK_ARG(hp_ring && t_dev && ring_len > 0, "hp_ring / t_dev / ring_len required");
   GRK_CHECK_ARG(num_ranges >= 0 && num_ranges <= kMaxGradRanges, "num_ranges must be in [0, %d]", kMaxGradRanges);
@@ -625,7 +643,8 @@ extern "C" int grk_table_adamw_ranges_dev(void* param, int param_dtype, float* e
   const unsigned g = (unsigned)((work + 255) / 256);
   hipStream_t s = (hipStream_t)stream;
   const HpArg hp = on_device(hp_ring, ring_len, t_dev);
-#define GRK_RG(P, NV) k_adamw_ranges<P, NV><<<g, 256, 0, s>>>((P*)param, exp_avg, exp_avg_sq, num_rows, dim, gr, hp)
+#define GRK_RG(P, NV) \
+  k_adamw_ranges<P, NV><<<g, 256, 0, s>>>((P*)param, exp_avg, exp_avg_sq, num_rows, dim, gr, hp, (bf16_t*)shadow)
   if (param_dtype == GRK_BF16) { if (v8) GRK_RG(bf16_t, 8); else GRK_RG(bf16_t, 4); }
   else { if (v8) GRK_RG(float, 8); else GRK_RG(float, 4); }
 #undef GRK_RG

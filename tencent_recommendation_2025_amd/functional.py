@@ -8,6 +8,8 @@ kernels require device tensors.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 import torch.nn.functional as F
 
@@ -16,6 +18,18 @@ from . import kernels as K
 from . import ops  # noqa: F401  (registers the grk:: custom ops)
 
 _disable = torch._dynamo.disable  # ctypes calls: explicit graph breaks under torch.compile
+
+# bf16 shadows of fp32 dense weights (optim.DenseFlat registers them): the bf16 copy
+# its AdamW launch writes with every update, read by the GEMMs here instead of a
+# per-step cast of each weight.  Parameter -> the DenseFlat holding it.
+_SHADOWS = weakref.WeakKeyDictionary()
+
+
+def bf16_shadow(weight):
+    """weight's bf16 shadow (a view of its DenseFlat's shadow buffer, equal to
+    weight.to(bf16) bit for bit), or None when the weight has none."""
+    flat = _SHADOWS.get(weight)
+    return None if flat is None else flat.shadow_of(weight)
 
 # Debug hook (bench.py): when a list, every fused gather appends its launch arguments.
 GATHER_TRACE = None
@@ -286,8 +300,9 @@ class _LinearFn(torch.autograd.Function):
             x2 = x2.to(torch.bfloat16)
         if x2.stride(-1) != 1 or (x2.shape[0] > 1 and x2.stride(0) < x2.shape[1]):
             x2 = x2.contiguous()
-        wb = weight if weight.dtype == torch.bfloat16 and weight.is_contiguous() else \
-            weight.detach().to(torch.bfloat16).contiguous()
+        wb = weight if weight.dtype == torch.bfloat16 and weight.is_contiguous() else bf16_shadow(weight)
+        if wb is None:
+            wb = weight.detach().to(torch.bfloat16).contiguous()
         if addend is not None:
             addend = addend.reshape(-1, wb.shape[0])
             if addend.dtype != torch.bfloat16 or addend.stride(1) != 1 or addend.stride(0) != wb.shape[0]:
@@ -432,6 +447,9 @@ class _WeightBlocksFn(torch.autograd.Function):
         Wv = W.detach().view(W.shape[0], -1, d)
         outs = [Wv[:, j, :] for j in singles]
         cast = {W.dtype: Wv}
+        sh = bf16_shadow(W) if any(dt == torch.bfloat16 for _, dt in stacks) else None
+        if sh is not None:
+            cast[torch.bfloat16] = sh.view(W.shape[0], -1, d)
         for js, dt in stacks:
             if dt not in cast:
                 cast[dt] = Wv.to(dt)           # the whole weight once per dtype, as before

@@ -245,11 +245,15 @@ def table_adamw(param, exp_avg, exp_avg_sq, hp, ids=None, rows=None, count=None,
 MAX_GRAD_RANGES = 64   # kMaxGradRanges (csrc/grk_optim.hip)
 
 
-def table_adamw_ranges(param, exp_avg, exp_avg_sq, clock, ranges):
+def table_adamw_ranges(param, exp_avg, exp_avg_sq, clock, ranges, shadow=None):
     """Dense-parity AdamW of a whole table from dense gradient blocks in ONE launch
     (grk_table_adamw_ranges_dev): ranges = [(row_offset, grad [rows, >= D] bf16/fp32)],
-    other rows g = 0."""
+    other rows g = 0.  shadow (bf16, param's shape, fp32 param only): also receives
+    the updated parameters rounded to bf16."""
     _require_cuda(param, exp_avg, exp_avg_sq, *[g for _, g in ranges])
+    if shadow is not None and (shadow.dtype != torch.bfloat16 or shadow.shape != param.shape
+                               or not shadow.is_contiguous() or param.dtype != torch.float32):
+        raise L.GrkError('shadow: a contiguous bf16 tensor of an fp32 param\'s shape')
     rows, D = param.shape
     if len(ranges) > MAX_GRAD_RANGES:
         raise L.GrkError(f'at most {MAX_GRAD_RANGES} gradient ranges per launch, got {len(ranges)}')
@@ -266,7 +270,8 @@ def table_adamw_ranges(param, exp_avg, exp_avg_sq, clock, ranges):
         arr[i] = L.GrkGradRange(int(off), int(off) + g.shape[0], g.data_ptr(), g.stride(0), L.dtype_code(g.dtype), 0)
     rc = L.lib().grk_table_adamw_ranges_dev(param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(),
                                             exp_avg_sq.data_ptr(), rows, D, arr, len(rs), clock.ring.data_ptr(),
-                                            clock.ring_len, clock.t.data_ptr(), L.stream_ptr(param.device))
+                                            clock.ring_len, clock.t.data_ptr(),
+                                            None if shadow is None else shadow.data_ptr(), L.stream_ptr(param.device))
     L.check(rc, 'grk_table_adamw_ranges_dev')
 
 

@@ -181,9 +181,14 @@ def split_runs(runs, starts, ends, limit):
 
 class DenseFlat:
     """fp32 dense parameters as views of one [rows, 8] buffer with flat AdamW moments,
-    stepped by grk_table_adamw_ranges_dev (each parameter's gradient one range)."""
+    stepped by grk_table_adamw_ranges_dev (each parameter's gradient one range).
 
-    def __init__(self, params, device):
+    shadow=True: a bf16 copy of the buffer, written by the same AdamW launch, serves
+    the GEMMs' bf16 weight operands (functional.bf16_shadow) instead of a cast kernel
+    per weight and step.  A parameter changed outside the optimizer (load_state_dict,
+    in-place ops: its version counter moves) has its shadow refreshed on next use."""
+
+    def __init__(self, params, device, shadow=False):
         self.params = list(params)
         self.starts, rows = flat_layout([p.numel() for p in self.params])
         self.ends = [s + p.numel() // DENSE_FLAT_DIM for s, p in zip(self.starts, self.params)]
@@ -196,6 +201,35 @@ class DenseFlat:
         self.exp_avg = torch.zeros_like(self.buf)
         self.exp_avg_sq = torch.zeros_like(self.buf)
         self._ptrs = [p.data_ptr() for p in self.params]
+        self.shadow = None
+        if shadow:
+            self.shadow = self.buf.to(torch.bfloat16)
+            self._index = {id(p): i for i, p in enumerate(self.params)}
+            self._versions = [p._version for p in self.params]
+            for p in self.params:
+                G._SHADOWS[p] = self
+
+    def sync_shadow(self):
+        """Refresh the shadow of every parameter changed outside the optimizer (a
+        graph replay reads the shadow without running the Python forward)."""
+        if self.shadow is not None:
+            for p, ver in zip(self.params, self._versions):
+                if p._version != ver:
+                    self.shadow_of(p)
+
+    def shadow_of(self, p):
+        """bf16 view of p's rows in the shadow buffer, refreshed first if p changed
+        outside the optimizer since the shadow last matched it."""
+        i = self._index[id(p)]
+        s, e = self.starts[i], self.ends[i]
+        view = self.shadow[s:e].view(p.shape)
+        if p._version != self._versions[i] or p.data_ptr() != self._ptrs[i]:
+            if p.data_ptr() != self._ptrs[i]:
+                return None        # no longer lives in the flat buffer (DenseFlat.step refuses too)
+            with torch.no_grad():
+                view.copy_(p.detach())
+            self._versions[i] = p._version
+        return view
 
     def zero_grad(self, set_to_none=True):
         for p in self.params:
@@ -221,7 +255,8 @@ class DenseFlat:
                 if g.data_ptr() % 16:          # the kernel reads fp32 gradients as 16-byte vectors
                     g = g.clone()
                 ranges.append((self.starts[i] - lo, g.view(-1, DENSE_FLAT_DIM)))
-            K.table_adamw_ranges(self.buf[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi], clock, ranges)
+            K.table_adamw_ranges(self.buf[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi], clock, ranges,
+                                 shadow=None if self.shadow is None else self.shadow[lo:hi])
 
     def state(self, p):
         """{'exp_avg', 'exp_avg_sq'} views of parameter p (torch AdamW's state names)."""
@@ -282,7 +317,7 @@ class FusedAdamW:
         if dense_flat and cuda:
             flat_ps = [p for p in dense if p.dtype == torch.float32 and p.numel() % DENSE_FLAT_DIM == 0]
             if flat_ps:
-                self._flat = DenseFlat(flat_ps, dev)
+                self._flat = DenseFlat(flat_ps, dev, shadow=True)
                 dense = [p for p in dense if all(p is not q for q in flat_ps)]
         # capturable: the dense AdamW keeps its step count on the device, so the
         # whole training step can be captured in a HIP graph (train.Trainer)
@@ -356,7 +391,11 @@ class FusedAdamW:
         self._seg = t
 
     def maybe_segment(self):
-        """Host-side segment bookkeeping due before step self.t + 1 (eager; never inside a captured step)."""
+        """Host-side segment bookkeeping due before step self.t + 1 (eager; never inside a captured step).
+        Also brings the dense weights' bf16 shadows up to date with writes made outside
+        the optimizer (load_state_dict between graph replays)."""
+        if self._flat is not None:
+            self._flat.sync_shadow()
         if self.clock is not None and (self._seg is None or self.t - self._seg >= self.clock.ring_len):
             self._segment(self.t)
 

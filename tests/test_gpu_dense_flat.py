@@ -101,3 +101,39 @@ def test_dense_flat_graph_replay_equals_eager():
         assert torch.equal(pe[n], pg[n]), n
     for n in me:
         assert torch.equal(me[n], mg[n]), n
+
+
+def test_bf16_shadow_follows_every_update_and_outside_writes():
+    """DenseFlat's bf16 shadow (the dense GEMMs' weight operands): after eager and
+    graph-replayed steps it equals the fp32 parameters rounded to bf16, bit for bit;
+    a parameter changed outside the optimizer (load_state_dict) is re-shadowed on its
+    next use; and the GEMM path reads the shadow (functional.bf16_shadow)."""
+    from tencent_recommendation_2025_amd import functional as G
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    cfg = S.SyntheticConfig(batch_size=8, maxlen=30, num_items=5000, num_users=700, min_len=4)
+    stats, types = S.feature_schema(cfg)
+    args = S.make_args(hidden_units=64, maxlen=30, num_blocks=2, num_heads=2)
+    torch.manual_seed(0)
+    m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, args).to(DEV)
+    opt = FusedAdamW(m, lr=2e-3)
+    flat = opt._flat
+    assert flat is not None and flat.shadow is not None
+    w = m.attention_layers[0].uvqk.weight
+    assert G.bf16_shadow(w) is not None
+    tr = Trainer(m, opt, loss='bce', graph=True, graph_warmup=1)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    for _ in range(4):
+        tr.step(S.make_batch(cfg, g, DEV))
+        torch.cuda.synchronize()
+        assert torch.equal(flat.shadow, flat.buf.to(torch.bfloat16))
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    with torch.no_grad():
+        sd['attention_layers.0.uvqk.weight'].mul_(0.5)
+    m.load_state_dict(sd)
+    tr.step(S.make_batch(cfg, g, DEV))           # a graph replay right after the outside write
+    torch.cuda.synchronize()
+    assert torch.equal(flat.shadow, flat.buf.to(torch.bfloat16))
+    assert torch.equal(G.bf16_shadow(w), w.detach().to(torch.bfloat16))

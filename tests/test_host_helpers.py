@@ -180,7 +180,7 @@ def test_dense_flat_step_plumbing_tracks_torch_adamw(monkeypatch):
     class Clock:
         t = 0
 
-    def emulated(param, exp_avg, exp_avg_sq, clock, ranges):
+    def emulated(param, exp_avg, exp_avg_sq, clock, ranges, shadow=None):
         hp = K.adamw_hparams(lr, b1, b2, eps, wd, clock.t)
         assert len(ranges) <= K.MAX_GRAD_RANGES          # the kernel refuses more (kMaxGradRanges)
         calls.append(param.shape[0])
@@ -244,7 +244,7 @@ def test_dense_flat_splits_runs_beyond_the_kernel_range_cap(monkeypatch):
     class Clock:
         t = 1
 
-    def emulated(param, exp_avg, exp_avg_sq, clock, ranges):
+    def emulated(param, exp_avg, exp_avg_sq, clock, ranges, shadow=None):
         assert len(ranges) <= K.MAX_GRAD_RANGES
         calls.append(len(ranges))
         hp = K.adamw_hparams(lr, b1, b2, eps, wd, clock.t)
