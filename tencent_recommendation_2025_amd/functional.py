@@ -21,15 +21,22 @@ _disable = torch._dynamo.disable  # ctypes calls: explicit graph breaks under to
 
 # bf16 shadows of fp32 dense weights (optim.DenseFlat registers them): the bf16 copy
 # its AdamW launch writes with every update, read by the GEMMs here instead of a
-# per-step cast of each weight.  Parameter -> the DenseFlat holding it.
-_SHADOWS = weakref.WeakKeyDictionary()
+# per-step cast of each weight.  id(Parameter) -> (weakref to it, its DenseFlat):
+# keyed by identity (a tensor's == is elementwise, so it cannot key a mapping).
+_SHADOWS = {}
+
+
+def register_shadow(p, flat):
+    _SHADOWS[id(p)] = (weakref.ref(p), flat)
 
 
 def bf16_shadow(weight):
     """weight's bf16 shadow (a view of its DenseFlat's shadow buffer, equal to
     weight.to(bf16) bit for bit), or None when the weight has none."""
-    flat = _SHADOWS.get(weight)
-    return None if flat is None else flat.shadow_of(weight)
+    hit = _SHADOWS.get(id(weight))
+    if hit is None or hit[0]() is not weight:
+        return None
+    return hit[1].shadow_of(weight)
 
 # Debug hook (bench.py): when a list, every fused gather appends its launch arguments.
 GATHER_TRACE = None

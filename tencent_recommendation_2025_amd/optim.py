@@ -207,7 +207,7 @@ class DenseFlat:
             self._index = {id(p): i for i, p in enumerate(self.params)}
             self._versions = [p._version for p in self.params]
             for p in self.params:
-                G._SHADOWS[p] = self
+                G.register_shadow(p, self)
 
     def sync_shadow(self):
         """Refresh the shadow of every parameter changed outside the optimizer (a
