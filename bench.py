@@ -71,6 +71,9 @@ def parse():
     ap.add_argument('--merge-proj', type=int, default=1,
                     help='1: the projected feature tables\' row gradients of the seq-side and pair lookups in one '
                          'grk_embedding_backward call (functional.DenseMerge); 0: one call per lookup')
+    ap.add_argument('--grouped-proj', type=int, default=1,
+                    help='1 (default): the projected feature tables on the grouped MFMA GEMMs '
+                         '(grk_grouped_gemm / grk_grouped_wgrad); 0: torch.bmm per equal-row-count stack')
     ap.add_argument('--dense-flat', type=int, default=1,
                     help='1: the dense parameters as one flat buffer on grk\'s multi-range AdamW (optim.DenseFlat); '
                          '0: torch\'s fused AdamW')
@@ -654,6 +657,7 @@ def main():
     shard_tables = sharded and (a.shard_tables if a.shard_tables is not None else a.items >= 10_000_000)
     margs.shard_tables = bool(shard_tables)
     margs.merge_proj_backward = bool(a.merge_proj)
+    margs.grouped_proj = bool(a.grouped_proj)
     progress(f'rank {rank}/{world}: building the model')
     torch.manual_seed(0)
     model = BaselineModel(a.users, a.items, stats, types, margs).to(dev)
@@ -761,6 +765,7 @@ def main():
                                    + (f', rab_time buckets={a.time_buckets}' if a.time_buckets else '')
                                    + (', fp8 (e4m3) q/k/v attention' if a.fp8 else '')
                                    + (', merged projected-row backward' if a.merge_proj else '')
+                                   + (', grouped MFMA projections' if a.grouped_proj else '')
                                    + (', flat dense AdamW' if a.dense_flat else ''),
                        'global_batch': a.batch * world, 'per_gpu_batch': a.batch, 'seq_len': a.maxlen + 1,
                        'parallelism': f'dp{world}' + ('+rowshard' if sharded else '') + ('(shard-built tables)' if shard_tables else ''),

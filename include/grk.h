@@ -597,6 +597,37 @@ size_t grk_wgrad_workspace(int64_t k, int64_t m, int64_t n);
 int grk_wgrad(const void* dy, int64_t ld_dy, const void* x, int64_t ld_x, int64_t k, int64_t m, int64_t n, void* dw,
               int64_t ld_dw, int dw_dtype, float* db, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Grouped GEMMs of the projected feature tables (model._projection; replaces the
+ * torch.bmm stacks over the per-feature tables of model/BaseLine/model.py:254-310
+ * as restated by the projection P_f = E_f W_f^T).  One group per table, at most
+ * 32 per launch; operands bf16, fp32 accumulation, every pointer 16-byte aligned
+ * and every row stride of a / b a multiple of 8 elements.
+ *
+ * grk_grouped_gemm: C_g [rows_g, n] = A_g [rows_g, k] . op(B_g), A K-contiguous
+ * (row stride lda); b_layout 0: B_g [n, k] (C = A B^T), 1: B_g [k, n] (C = A B);
+ * C fp32 or bf16 (c_dtype), row stride ldc; k a multiple of 32.  (b_rows unused.)
+ *
+ * grk_grouped_wgrad: C_g [m, n] fp32 (row stride ldc, a multiple of 4) =
+ * A_g^T B_g with A_g [rows_g, m], B_g [rows_g, n] row-major, rows_g a multiple
+ * of 32; B's rows past b_rows are read as its row b_rows - 1 (A's rows there
+ * must be zero: they then add exact zeros).  Split-K slices summed in slice
+ * order (deterministic); workspace of grk_grouped_wgrad_workspace() bytes. */
+typedef struct grk_gemm_group {
+  const void* a;
+  int64_t lda;
+  const void* b;
+  int64_t ldb;
+  void* c;
+  int64_t ldc;
+  int64_t rows;
+  int64_t b_rows;
+} grk_gemm_group;
+int grk_grouped_gemm(const grk_gemm_group* groups, int num_groups, int b_layout, int64_t n, int64_t k, int c_dtype,
+                     void* stream);
+size_t grk_grouped_wgrad_workspace(const grk_gemm_group* groups, int num_groups, int64_t m, int64_t n);
+int grk_grouped_wgrad(const grk_gemm_group* groups, int num_groups, int64_t m, int64_t n, void* workspace,
+                      size_t workspace_bytes, void* stream);
+
 /* Exact maximum-inner-product top-k retrieval: the ANN step of inference
  * (model/BaseLine/infer.py:213-225 runs an external faiss HNSW binary with
  * --faiss_metric_type=0 (inner product) --query_ann_top_k=10 over the

@@ -66,8 +66,9 @@ class RefHSTU(torch.nn.Module):
     bf16_core=True: the fp32 math fed the grk HSTU core's bf16 storage points
     (ops.hstu_core: the u|v|q|k pre-activation, the attention output o and the
     gated output y are bf16 tensors, and so are their gradients dpre, do, dy;
-    the MFMA operands SiLU(q), SiLU(k), SiLU(v) are bf16 values) -- the checker
-    that separates that rounding from the kernels' math."""
+    the MFMA operands SiLU(q), SiLU(k), SiLU(v) and the gate SiLU(u) are bf16
+    values, csrc/grk_hstu.hip k_ng_fwd) -- the checker that separates that
+    rounding from the kernels' math."""
 
     def __init__(self, d, h, p, num_buckets, num_time_buckets=0, fp8=False):
         super().__init__()
@@ -84,8 +85,8 @@ class RefHSTU(torch.nn.Module):
         B, T, D = query.shape
         rb = _RoundBF16.apply if self.bf16_core else (lambda x: x)
         u, v, q, k = torch.split(F.silu(rb(self.uvqk(query))), D, dim=-1)
-        if self.bf16_core:   # the MFMA operands SiLU(v), SiLU(q), SiLU(k) are bf16 (forward value only)
-            v, q, k = (x + (x.to(torch.bfloat16).to(x.dtype) - x).detach() for x in (v, q, k))
+        if self.bf16_core:   # SiLU(v), SiLU(q), SiLU(k) (MFMA operands) and the gate SiLU(u) are bf16 values
+            u, v, q, k = (x + (x.to(torch.bfloat16).to(x.dtype) - x).detach() for x in (u, v, q, k))
         if self.fp8:
             r8 = lambda x: x + (x.clamp(-448, 448).to(torch.float8_e4m3fn).to(x.dtype) - x).detach()
             v, q, k = r8(v), r8(q), r8(k)

@@ -2,7 +2,8 @@
 
 The fp32 HSTU model test (tests/test_gpu_model.py) measured logits 1.6e-3 from
 the fp32 oracle and 1.3e-3 from the oracle with the core's bf16 storage points
-(RefHSTU.bf16_core).  Here one layer core (functional.hstu_core: y from a bf16-
+(RefHSTU.bf16_core) -- before the gate's bf16 SiLU(u) (k_ng_fwd) was added to
+them; round 4 run (gpurun_out/r4h_hstu_rounding.txt) found the remaining 2.4e-3.  Here one layer core (functional.hstu_core: y from a bf16-
 exact pre-activation) against a float64 restatement with each candidate rounding
 switched on or off, normwise errors printed per variant.
 
@@ -27,7 +28,7 @@ def core(pre, rab, ln_w, ln_b, B, T, H, hd, round_qkv, round_p, round_o, round_y
     x = pre.double().view(B, T, 4 * D)
     u, v, q, k = torch.split(F.silu(x), D, dim=-1)
     if round_qkv:
-        v, q, k = rb(v), rb(q), rb(k)
+        u, v, q, k = rb(u), rb(v), rb(q), rb(k)
     sh = lambda t: t.reshape(B, T, H, hd).transpose(1, 2)
     q, k, v = sh(q), sh(k), sh(v)
     if scale_q:

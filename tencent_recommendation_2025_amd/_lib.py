@@ -76,6 +76,11 @@ class GrkIndexBlock(C.Structure):
                 ('offset', C.c_int64)]
 
 
+class GrkGemmGroup(C.Structure):
+    _fields_ = [('a', C.c_void_p), ('lda', C.c_int64), ('b', C.c_void_p), ('ldb', C.c_int64), ('c', C.c_void_p),
+                ('ldc', C.c_int64), ('rows', C.c_int64), ('b_rows', C.c_int64)]
+
+
 class GrkStoreView(C.Structure):
     _fields_ = [('sparse', C.c_void_p), ('arr', C.c_void_p), ('arr_len', C.c_void_p), ('mm', C.c_void_p),
                 ('tokens', C.c_int64), ('f_sparse', C.c_int32), ('f_array', C.c_int32), ('a_cap', C.c_int32),
@@ -149,6 +154,9 @@ SIGNATURES = {
     'grk_gemm_tuning': (_I, [_I]),
     'grk_wgrad_workspace': (_SZ, [_I64, _I64, _I64]),
     'grk_wgrad': (_I, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _I, _P, _P, _SZ, _P]),
+    'grk_grouped_gemm': (_I, [C.POINTER(GrkGemmGroup), _I, _I, _I64, _I64, _I, _P]),
+    'grk_grouped_wgrad_workspace': (_SZ, [C.POINTER(GrkGemmGroup), _I, _I64, _I64]),
+    'grk_grouped_wgrad': (_I, [C.POINTER(GrkGemmGroup), _I, _I64, _I64, _P, _SZ, _P]),
     'grk_mips_topk_workspace': (_SZ, [_I64, _I64]),
     'grk_mips_topk': (_I, [_P, _I64, _P, _I64, _I, _I64, _I64, _I, _I, _P, _P, _P, _P, _SZ, _P]),
     'grk_sample_negatives': (_I, [_P, _P, _I64, _I, _P, _I, _I64, C.c_uint64, _I, _P, _I, _P, _P, _P, _P, _P]),

@@ -19,12 +19,11 @@
 // so the order among equal digits is the input order: stable, deterministic,
 // and (a stable sort being unique) the same output as rocprim's.
 //
-// Round 4, fewer launches per pass: the digit histograms live in two buffers
-// used in turn; each pass's scatter counts the NEXT digit of every key it
-// places into the other buffer (integer atomics on [digit][output tile]:
-// exact counts, so the result is unchanged), which that pass's scan zeroed
-// beforehand -- so only the first pass has a histogram launch, and the
-// embedding backward builds even that one inside its key-build kernel.
+// The first pass's histogram can come from the caller (the embedding
+// backward counts digit 0 inside its key-build kernel: hist0_ready).  Round 4
+// also tried counting each next digit inside the scatter (global atomics per
+// (digit, output tile), wave-aggregated): 0.34 ms per C2 step against 0.06 for
+// these histogram launches -- runs of equal keys contend on one counter.
 #include "grk_common.h"
 
 namespace grk {
@@ -50,15 +49,12 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const unsigned* __re
 }
 
 // Per digit (one workgroup each): in-place exclusive scan of the digit's tile
-// counts hist[d][0 .. ntiles) and the digit's total -> tot[d]; zeroes row d of
-// the next pass's histogram (hzero, may be null) for the scatter's counts.
+// counts hist[d][0 .. ntiles) and the digit's total -> tot[d].
 __global__ void __launch_bounds__(kSortThreads) k_sort_scan(unsigned* __restrict__ hist, int ntiles,
-                                                            unsigned* __restrict__ tot, unsigned* __restrict__ hzero) {
+                                                            unsigned* __restrict__ tot) {
   __shared__ unsigned part[kSortThreads];
   const int t = threadIdx.x;
   unsigned* row = hist + (int64_t)blockIdx.x * ntiles;
-  if (hzero)
-    for (int i = t; i < ntiles; i += kSortThreads) hzero[(int64_t)blockIdx.x * ntiles + i] = 0u;
   unsigned carry = 0;
   for (int c0 = 0; c0 < ntiles; c0 += kSortThreads) {
     const int i = c0 + t;
@@ -78,15 +74,12 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_scan(unsigned* __restrict
   if (t == 0) tot[blockIdx.x] = carry;
 }
 
-// hnext (may be null): this key's NEXT digit (shift_next) counted into
-// hnext[digit][pos / kSortTile] -- the next pass's histogram.
 __global__ void __launch_bounds__(kSortThreads) k_sort_scatter(const unsigned* __restrict__ kin,
                                                                const unsigned long long* __restrict__ vin,
                                                                unsigned* __restrict__ kout,
                                                                unsigned long long* __restrict__ vout, int64_t n,
                                                                int shift, const unsigned* __restrict__ hist,
-                                                               int ntiles, const unsigned* __restrict__ tot,
-                                                               unsigned* __restrict__ hnext, int shift_next) {
+                                                               int ntiles, const unsigned* __restrict__ tot) {
   constexpr int NW = kSortThreads / 64;
   __shared__ unsigned base[kSortBins];
   __shared__ unsigned wcnt[NW][kSortBins];
@@ -136,38 +129,6 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_scatter(const unsigned* _
         if (q < w) pos += wcnt[q][d];
       kout[pos] = key;
       vout[pos] = val;
-    }
-    if (hnext) {
-      // The next digit counted once per (next digit, output tile) group of the wave:
-      // the lanes sharing this digit AND the next one hold consecutive slots (at most
-      // two output tiles); a per-lane atomic serialises on one word for runs of equal
-      // keys (a hot row's thousands of occurrences), measured 0.9 ms per C2 step.
-      const unsigned nd = (key >> shift_next) & (kSortBins - 1);
-      unsigned long long grp = peers;
-#pragma unroll
-      for (int bit = 0; bit < kSortBits; ++bit) {
-        const bool set = (nd >> bit) & 1u;
-        const unsigned long long m = __ballot(set);
-        grp &= set ? m : ~m;
-      }
-      unsigned pos = 0;
-      if (ok) {
-        pos = base[d] + (unsigned)__popcll(peers & lt);
-#pragma unroll
-        for (int q = 0; q < NW; ++q)
-          if (q < w) pos += wcnt[q][d];
-      }
-      const int otile = (int)(pos / kSortTile);
-      const int leader = ok ? __ffsll((long long)grp) - 1 : lane;
-      const int lead_tile = __shfl(otile, leader);
-      const unsigned long long hi = __ballot(ok && otile != lead_tile) & grp;
-      if (ok) {
-        const bool first_lo = lane == leader;
-        const bool first_hi = hi != 0ull && lane == __ffsll((long long)hi) - 1;
-        if (first_lo)
-          atomicAdd(&hnext[(int64_t)nd * ntiles + lead_tile], (unsigned)__popcll(grp & ~hi));
-        if (first_hi) atomicAdd(&hnext[(int64_t)nd * ntiles + otile], (unsigned)__popcll(hi));
-      }
     }
     __syncthreads();  // every slot of this round computed from the old base
     unsigned add = 0;
@@ -251,18 +212,17 @@ int head_positions(const unsigned* keys, int64_t n, unsigned sentinel, int* pos,
   unsigned* cnt = (unsigned*)ws;
   k_head_count<<<ntiles, kSortThreads, 0, s>>>(keys, n, sentinel, cnt);
   GRK_LAUNCH_CHECK();
-  k_sort_scan<<<1, kSortThreads, 0, s>>>(cnt, ntiles, cnt + ntiles, nullptr);
+  k_sort_scan<<<1, kSortThreads, 0, s>>>(cnt, ntiles, cnt + ntiles);
   GRK_LAUNCH_CHECK();
   k_head_pos<<<ntiles, kSortThreads, 0, s>>>(keys, n, sentinel, cnt, pos);
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }
 
-// Workspace of sort_pairs: two digit-histogram buffers (digit-major, used in
-// turn by the passes) and the digit totals.
+// Workspace of sort_pairs: the digit histogram (digit-major) and the digit totals.
 size_t sort_pairs_workspace(int64_t n) {
   const int64_t ntiles = (n + kSortTile - 1) / kSortTile;
-  return (2 * (size_t)kSortBins * (size_t)(ntiles > 0 ? ntiles : 1) + kSortBins) * sizeof(unsigned);
+  return ((size_t)kSortBins * (size_t)(ntiles > 0 ? ntiles : 1) + kSortBins) * sizeof(unsigned);
 }
 
 // The first pass's histogram buffer inside a sort_pairs workspace (a caller
@@ -283,25 +243,21 @@ int sort_pairs(unsigned* k0, unsigned long long* v0, unsigned* k1, unsigned long
   const int64_t ntiles64 = (n + kSortTile - 1) / kSortTile;
   GRK_CHECK_ARG(ntiles64 < (1 << 24), "too many tiles");
   const int ntiles = (int)ntiles64;
-  unsigned* hbuf[2] = {(unsigned*)ws, (unsigned*)ws + (size_t)kSortBins * ntiles};
-  unsigned* tot = hbuf[1] + (size_t)kSortBins * ntiles;
+  unsigned* hist = (unsigned*)ws;
+  unsigned* tot = hist + (size_t)kSortBins * ntiles;
   unsigned* kin = k0;
   unsigned* kout = k1;
   unsigned long long* vin = v0;
   unsigned long long* vout = v1;
   int pass = 0;
   for (int shift = 0; shift < end_bit; shift += kSortBits, ++pass) {
-    unsigned* hist = hbuf[pass & 1];
-    const bool last = shift + kSortBits >= end_bit;
-    unsigned* hnext = last ? nullptr : hbuf[(pass + 1) & 1];
-    if (pass == 0 && !hist0_ready) {
+    if (pass > 0 || !hist0_ready) {
       k_sort_hist<<<ntiles, kSortThreads, 0, s>>>(kin, n, shift, hist, ntiles);
       GRK_LAUNCH_CHECK();
     }
-    k_sort_scan<<<kSortBins, kSortThreads, 0, s>>>(hist, ntiles, tot, hnext);
+    k_sort_scan<<<kSortBins, kSortThreads, 0, s>>>(hist, ntiles, tot);
     GRK_LAUNCH_CHECK();
-    k_sort_scatter<<<ntiles, kSortThreads, 0, s>>>(kin, vin, kout, vout, n, shift, hist, ntiles, tot, hnext,
-                                                   shift + kSortBits);
+    k_sort_scatter<<<ntiles, kSortThreads, 0, s>>>(kin, vin, kout, vout, n, shift, hist, ntiles, tot);
     GRK_LAUNCH_CHECK();
     unsigned* tk = kin;
     kin = kout;

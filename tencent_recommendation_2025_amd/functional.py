@@ -550,6 +550,114 @@ def group_stack(group, offsets, rows):
     return _GroupStackFn.apply(_ANCHOR, group, tuple(offsets), rows)
 
 
+PROJ_ROW_ALIGN = 32   # grouped projection: each table's P rows start at a multiple of 32
+
+
+class _ProjectFn(torch.autograd.Function):
+    """The projected feature tables of one dnn on the grouped MFMA GEMMs
+    (grk_grouped_gemm / grk_grouped_wgrad; model._projection restates the
+    reference's per-feature lookups feeding itemdnn / userdnn,
+    model/BaseLine/model.py:254-310, as lookups of P_f = E_f W_f^T).
+
+    Inputs: the dnn weight W [d_out, nb * d] and its column blocks ``singles``
+    (returned as views, as weight_blocks does); ``tables`` = [(block j, row offset
+    in ``group``, rows, P row offset)] of tables held by one bf16 TableGroup.
+    Returns (singles..., P [P rows, d_out] bf16): table f's P rows at its P offset
+    (a multiple of 32; the rows between tables are never read).
+
+    Backward: dE_f = dP_f W_f (one launch, bf16) into the group's dense gradient
+    sink (group.collect_dense), dW_f = dP_f^T E_f (one launch + the split-K
+    reduction) straight into the blocks of ONE fp32 gradient of W's shape, the
+    singles' gradients copied into theirs, zeros for blocks no output reached.
+    dP's rows between tables are zero (the embedding backward writes only rows
+    that are looked up), so the weight gradient sums each table's padded rows
+    exactly (B rows past the table read its last row, times zero)."""
+
+    @staticmethod
+    def forward(ctx, W, d, singles, tables, group, p_rows):
+        ctx.set_materialize_grads(False)
+        d_out, cols = W.shape
+        nb = cols // d
+        Wb = W.detach() if W.dtype == torch.bfloat16 else bf16_shadow(W)
+        if Wb is None:
+            Wb = W.detach().to(torch.bfloat16)
+        E = group.flat
+        P = torch.empty(p_rows, d_out, dtype=torch.bfloat16, device=E.device)
+        K.grouped_gemm([(E[off:off + rows], Wb[:, j * d:(j + 1) * d], P[poff:poff + rows])
+                        for j, off, rows, poff in tables], n=d_out, k=d, b_layout=0)
+        ctx.save_for_backward(Wb)
+        ctx.meta = (d, nb, tuple(singles), tuple(tables), group, W.dtype, W.shape)
+        Wv = W.detach().view(d_out, nb, d)
+        return (*[Wv[:, j, :] for j in singles], P)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        (Wb,) = ctx.saved_tensors
+        d, nb, singles, tables, group, wdt, wshape = ctx.meta
+        d_out = wshape[0]
+        gs, dP = grads[:len(singles)], grads[len(singles)]
+        if all(g is None for g in gs) and dP is None:
+            return None, None, None, None, None, None
+        dW = torch.empty(wshape, dtype=torch.float32, device=Wb.device)
+        dWv = dW.view(d_out, nb, d)
+        covered = [False] * nb
+        for j, g in zip(singles, gs):
+            if g is not None:
+                dWv[:, j, :].copy_(g)
+                covered[j] = True
+        if dP is not None:
+            if dP.dtype != torch.bfloat16:
+                dP = dP.to(torch.bfloat16)
+            dP = dP if dP.is_contiguous() else dP.contiguous()
+            E = group.flat
+            dE = torch.empty(sum(rows for _, _, rows, _ in tables), d, dtype=torch.bfloat16, device=dP.device)
+            gg, r = [], 0
+            for j, off, rows, poff in tables:
+                gg.append((dP[poff:poff + rows], Wb[:, j * d:(j + 1) * d], dE[r:r + rows]))
+                r += rows
+            K.grouped_gemm(gg, n=d, k=d_out, b_layout=1)
+            r = 0
+            for j, off, rows, poff in tables:
+                group.collect_dense(off, dE[r:r + rows])
+                r += rows
+            K.grouped_wgrad([(dP[poff:], E[off:], dW[:, j * d:(j + 1) * d], _pad_rows(rows), rows)
+                             for j, off, rows, poff in tables], m=d_out, n=d)
+            for j, _, _, _ in tables:
+                covered[j] = True
+        j = 0
+        while j < nb:                           # runs of blocks no output reached
+            if covered[j]:
+                j += 1
+                continue
+            e = j
+            while e < nb and not covered[e]:
+                e += 1
+            dWv[:, j:e, :].zero_()
+            j = e
+        return (dW if wdt == torch.float32 else dW.to(wdt)), None, None, None, None, None
+
+
+def _pad_rows(rows):
+    return -(-int(rows) // PROJ_ROW_ALIGN) * PROJ_ROW_ALIGN
+
+
+def proj_layout(rows_list):
+    """P row offsets of tables with the given row counts (each a multiple of
+    PROJ_ROW_ALIGN) and the padded total."""
+    offs, r = [], 0
+    for rows in rows_list:
+        offs.append(r)
+        r += _pad_rows(rows)
+    return offs, r
+
+
+def project_blocks(W, d, singles, tables, group, p_rows):
+    """(singles..., P): see _ProjectFn.  tables: [(block j, group row offset, rows, P row offset)]."""
+    singles = tuple(int(j) for j in singles)
+    tables = tuple((int(j), int(o), int(r), int(p)) for j, o, r, p in tables)
+    return _ProjectFn.apply(W, int(d), singles, tables, group, int(p_rows))
+
+
 # ------------------------------------------------------------- attention ----
 def _seed(seed):
     """A dropout seed: an int, or an int64 [1] device tensor read by the kernels at run time."""

@@ -669,6 +669,60 @@ def wgrad(dy, x, out_dtype=torch.float32, want_db=False):
     return dw, db
 
 
+def _gemm_group_array(groups):
+    arr = (L.GrkGemmGroup * len(groups))()
+    for i, (a, b, c, rows, b_rows) in enumerate(groups):
+        for t, nm in ((a, 'A'), (b, 'B'), (c, 'C')):
+            if t.dim() != 2 or t.stride(1) != 1:
+                raise L.GrkError(f'group {i}: {nm} must be a 2-D view with unit column stride')
+        if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+            raise L.GrkError(f'group {i}: A and B must be bf16')
+        arr[i] = L.GrkGemmGroup(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
+                                int(rows), int(b_rows))
+    return arr
+
+
+def grouped_gemm(groups, n, k, b_layout):
+    """grk_grouped_gemm: for each (A [rows, >= k] bf16, B bf16, C [rows, >= n] fp32 / bf16)
+    C = A . B^T (b_layout 0, B [n, k]) or A . B (b_layout 1, B [k, n]); views with unit
+    column strides (row strides taken from the views).  One launch for every group."""
+    if not groups:
+        return
+    _require_cuda(*[t for g in groups for t in g])
+    cdt = {g[2].dtype for g in groups}
+    if len(cdt) != 1 or next(iter(cdt)) not in (torch.float32, torch.bfloat16):
+        raise L.GrkError('every C must be fp32, or every C bf16')
+    for i, (a, b, c) in enumerate(groups):
+        kb, nb = (b.shape[1], b.shape[0]) if b_layout == 0 else (b.shape[0], b.shape[1])
+        if a.shape[1] < k or kb < k or nb < n or c.shape[1] < n or c.shape[0] != a.shape[0]:
+            raise L.GrkError(f'group {i}: shapes do not match n = {n}, k = {k}')
+    arr = _gemm_group_array([(a, b, c, a.shape[0], 0) for a, b, c in groups])
+    rc = L.lib().grk_grouped_gemm(arr, len(groups), int(b_layout), int(n), int(k),
+                                  L.dtype_code(next(iter(cdt))), L.stream_ptr(groups[0][0].device))
+    L.check(rc, 'grk_grouped_gemm')
+
+
+def grouped_wgrad(groups, m, n):
+    """grk_grouped_wgrad: for each (A [rows, >= m] bf16, B [>= b_rows, >= n] bf16, C [m, >= n]
+    fp32, rows, b_rows) C = A[:rows]^T . B[:rows] with B's rows past b_rows read as its row
+    b_rows - 1 (A must be zero there); rows a multiple of 32.  One launch (+ one
+    reduction of the split-K slices)."""
+    if not groups:
+        return
+    _require_cuda(*[t for g in groups for t in g[:3]])
+    for i, (a, b, c, rows, b_rows) in enumerate(groups):
+        if c.dtype != torch.float32 or a.shape[0] < rows or b.shape[0] < b_rows or c.shape[0] != m:
+            raise L.GrkError(f'group {i}: C must be fp32 [m, n], A hold rows, B hold b_rows rows')
+    arr = _gemm_group_array(groups)
+    dev = groups[0][0].device
+    nbytes = L.lib().grk_grouped_wgrad_workspace(arr, len(groups), int(m), int(n))
+    if nbytes == 0:
+        raise L.GrkError('grouped_wgrad: rows must be positive multiples of 32')
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    rc = L.lib().grk_grouped_wgrad(arr, len(groups), int(m), int(n), ws.data_ptr(), ws.numel(), L.stream_ptr(dev))
+    L.check(rc, 'grk_grouped_wgrad')
+
+
 def wgrad_ok(dy, x):
     """Shapes / strides / alignment grk_wgrad takes (else the hipBLASLt GEMM path)."""
     return (dy.dim() == 2 and x.dim() == 2 and dy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0

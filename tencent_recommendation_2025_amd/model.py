@@ -250,8 +250,11 @@ class BaselineModel(torch.nn.Module):
         # ~6 rows d^2 FLOP per forward + backward, a direct block ~6 tokens d^2
         self.proj_max_rows = int(getattr(args, 'proj_max_rows', 100_000))
         # fused path: the projected tables' row gradients of the seq-side and pair
-        # lookups reduced in one call (functional.DenseMerge); opt-in until run on hardware
+        # lookups reduced in one call (functional.DenseMerge; the default since round 4)
         self.merge_proj = bool(getattr(args, 'merge_proj_backward', True))
+        # fused path: the projections on the grouped MFMA GEMMs (functional.project_blocks)
+        # instead of torch.bmm over equal-row-count stacks (_grouped_proj)
+        self.grouped_proj = bool(getattr(args, 'grouped_proj', True))
         if getattr(args, 'shard_tables', False):
             # row-sharded item / user tables (BASELINE config 3, 50M rows): the full
             # tables are never built on any rank -- ShardedFusedAdamW creates each
@@ -397,7 +400,13 @@ class BaselineModel(torch.nn.Module):
         if self._fwd_id is not None and key in self._proj_cache:
             return self._proj_cache[key]
         d = self.hidden_units
-        stacks = self._weight_pieces(which)[1]
+        pieces = self._weight_pieces(which)
+        if len(pieces) > 2:                     # grouped MFMA projection (_grouped_proj)
+            res = pieces[2]
+            if self._fwd_id is not None:
+                self._proj_cache[key] = res
+            return res
+        stacks = pieces[1]
         parts, offs, row = [], {}, 0
         for rows, group, refs in self._proj_groups(which):
             grp = next(iter(refs.values())).group
@@ -442,11 +451,39 @@ class BaselineModel(torch.nn.Module):
             out.append((rows, group, refs))
         return out
 
+    def _grouped_proj(self, which):
+        """(tables [(block, group row offset, rows, P row offset)], group, {feature: P
+        offset}, P rows) when the projection runs on the grouped MFMA GEMMs
+        (functional.project_blocks: every projected table in one bf16 table group, on
+        the GPU, d a multiple of 32, at most 32 tables), else None."""
+        if torch.compiler.is_compiling():
+            return None
+        d = self.hidden_units
+        grp, entries = None, []
+        for rows, group, refs in self._proj_groups(which):
+            for k, j in group:
+                r = refs[k]
+                if r.group is None or (grp is not None and r.group is not grp):
+                    return None
+                grp = r.group
+                entries.append((k, j, r.row_offset, rows))
+        if (grp is None or not grp.flat.is_cuda or grp.flat.dtype != torch.bfloat16 or d % 32
+                or len(entries) > 32):
+            return None
+        dnn = self.itemdnn if which == 'item' else self.userdnn
+        if dnn.weight.dtype not in (torch.float32, torch.bfloat16) or dnn.weight.shape[0] % 8:
+            return None
+        entries.sort(key=lambda e: e[2])        # P in group-buffer order; the first table's row 0 is P[0]
+        poffs, p_rows = G.proj_layout([e[3] for e in entries])
+        tables = [(j, off, rows, po) for (_, j, off, rows), po in zip(entries, poffs)]
+        return tables, grp, {k: po for (k, _, _, _), po in zip(entries, poffs)}, p_rows
+
     def _weight_pieces(self, which):
         """The itemdnn / userdnn weight's column blocks this forward reads, from ONE
         functional.weight_blocks call per forward and side: ({block: fp32 view} for
         W_0, the direct-feature and the mm blocks, {block tuple: [G, d, d] stack in the
-        tables' dtype} for the projected groups)."""
+        tables' dtype} for the projected groups) -- or, on the grouped MFMA projection
+        (functional.project_blocks), ({block: view}, {}, (P, {feature: P offset}))."""
         key = ('wb', which, self._fwd_id)
         if self._fwd_id is not None and key in self._proj_cache:
             return self._proj_cache[key]
@@ -456,6 +493,14 @@ class BaselineModel(torch.nn.Module):
         if which == 'item':
             base = 1 + len(self.ITEM_SPARSE_FEAT) + len(self.ITEM_ARRAY_FEAT)
             singles += [base + j for j in range(len(self.ITEM_EMB_FEAT))]
+        gp = self._grouped_proj(which) if self.grouped_proj else None
+        if gp is not None:
+            tables, grp, offs, p_rows = gp
+            outs = G.project_blocks(dnn.weight, d, singles, tables, grp, p_rows)
+            res = ({j: o for j, o in zip(singles, outs)}, {}, (outs[-1], offs))
+            if self._fwd_id is not None:
+                self._proj_cache[key] = res
+            return res
         stacks = [(tuple(j for _, j in group), next(iter(refs.values())).weight.dtype)
                   for _, group, refs in self._proj_groups(which)]
         if torch.compiler.is_compiling():      # traced: the slice form (weight_blocks is a graph break)

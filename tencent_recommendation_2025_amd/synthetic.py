@@ -135,9 +135,9 @@ def make_batch(cfg: SyntheticConfig, generator: torch.Generator, device='cuda'):
 
 def make_args(hidden_units=512, maxlen=200, num_blocks=4, num_heads=8, dropout_rate=0.0, block='hstu',
               variant='o1', norm_first=False, device='cuda', hstu_time_buckets=0, hstu_fp8=False,
-              merge_proj_backward=True):
+              merge_proj_backward=True, grouped_proj=True):
     from types import SimpleNamespace
     return SimpleNamespace(hidden_units=hidden_units, maxlen=maxlen, num_blocks=num_blocks, num_heads=num_heads,
                            dropout_rate=dropout_rate, block=block, variant=variant, norm_first=norm_first,
                            device=device, mm_emb_id=['81'], hstu_time_buckets=hstu_time_buckets, hstu_fp8=hstu_fp8,
-                           merge_proj_backward=merge_proj_backward)
+                           merge_proj_backward=merge_proj_backward, grouped_proj=grouped_proj)
