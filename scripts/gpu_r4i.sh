@@ -13,6 +13,8 @@ rc=$?
 echo "pytest rc=$rc" >> gpurun_out/r4i_ggemm.log
 grep -Eqi "$FAULT" gpurun_out/r4i_ggemm.log && { echo "GPU fault in the grouped GEMM tests -- stopping"; exit 3; }
 case $rc in 0|1) ;; *) echo "pytest exit $rc -- stopping"; exit $rc ;; esac
+timeout -k 10 180 python -u scripts/microbench/ggemm_shapes.py > gpurun_out/r4i_ggemm_shapes.txt 2>&1 || exit $?
+timeout -k 10 300 python -u scripts/op_sites.py > gpurun_out/r4i_op_sites.txt 2>&1 || exit $?
 bash scripts/gpu_suite.sh r4i 1 || exit $?
 timeout -k 10 300 python -u bench.py --grouped-proj 0 > gpurun_out/r4i_bench_bmmproj.json 2> gpurun_out/r4i_bench_bmmproj.err || exit $?
 MODES=fused bash scripts/gpu_step_profiles.sh || exit $?
