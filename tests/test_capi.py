@@ -88,3 +88,23 @@ def test_index_entry_points_refuse_bad_blocks(lib):
     assert h.grk_proj_index(blocks, 2, lib.GRK_I64, 10, 16, 6, None) == lib.GRK_EINVAL   # out_ld < 7 columns
     assert h.grk_proj_index(blocks, 0, lib.GRK_I64, 10, 16, 16, None) == lib.GRK_EINVAL
     assert h.grk_batch_row_ids(None, None, None, None, 7, 4, None, None, None) == lib.GRK_EINVAL
+
+
+def test_grouped_gemm_entry_points_refuse_bad_groups(lib):
+    """grk_grouped_gemm / grk_grouped_wgrad (round 4) check groups, alignment and
+    sizes on the host, before any launch."""
+    h = lib.lib()
+    g = (lib.GrkGemmGroup * 2)()
+    g[0] = lib.GrkGemmGroup(256, 512, 4096, 512, 8192, 512, 100, 100)
+    g[1] = lib.GrkGemmGroup(258, 512, 4096, 512, 8192, 512, 100, 100)      # A not 16-byte aligned
+    assert h.grk_grouped_gemm(g, 2, 0, 512, 512, lib.GRK_BF16, None) == lib.GRK_EINVAL
+    assert b'aligned' in h.grk_last_error()
+    assert h.grk_grouped_gemm(g, 0, 0, 512, 512, lib.GRK_BF16, None) == lib.GRK_EINVAL        # no groups
+    assert h.grk_grouped_gemm(g, 1, 0, 512, 500, lib.GRK_BF16, None) == lib.GRK_EINVAL        # k % 32
+    assert h.grk_grouped_gemm(g, 1, 2, 512, 512, lib.GRK_BF16, None) == lib.GRK_EINVAL        # b_layout
+    assert h.grk_grouped_gemm(g, 1, 0, 1024, 512, lib.GRK_BF16, None) == lib.GRK_EINVAL       # ldc < n
+    assert h.grk_grouped_wgrad_workspace(g, 1, 512, 512) == 0                                  # rows % 32
+    g[0] = lib.GrkGemmGroup(256, 512, 4096, 512, 8192, 512, 128, 200)                         # b_rows > rows
+    assert h.grk_grouped_wgrad_workspace(g, 1, 512, 512) > 0
+    assert h.grk_grouped_wgrad(g, 1, 512, 512, 16, 1 << 30, None) == lib.GRK_EINVAL
+    assert b'b_rows' in h.grk_last_error()
