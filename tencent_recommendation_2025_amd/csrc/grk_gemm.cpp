@@ -177,15 +177,30 @@ int make_plan(hipblasLtHandle_t h, const Key& key, bool has_bias, Plan* p, const
   float t0 = -1.f, tbest = -1.f;
   if (!o.capturing) {  // no timing / validation inside a HIP graph capture: the heuristic's first usable pick
     const size_t cbytes = (size_t)key.ldc * key.m * (key.ct == GRK_F32 ? 4 : 2);
-    const size_t abytes = (size_t)key.lda * (key.ta ? key.k : key.m) * 2;
-    const size_t bbytes = (size_t)key.ldb * (key.tb ? key.n : key.k) * 2;
+    // the operands' exact spans: (rows - 1) strides + one row.  rows x stride reads past
+    // the end of a strided view that ends its allocation (a column block of the gather
+    // buffer): hipMemcpyAsync then fails with hipErrorInvalidValue, the copy is missing,
+    // every candidate "fails" validation and the sticky error surfaces in the next call
+    const int64_t arows = key.ta ? key.k : key.m, acols = key.ta ? key.m : key.k;
+    const int64_t brows = key.tb ? key.n : key.k, bcols = key.tb ? key.k : key.n;
+    const size_t abytes = (size_t)((arows - 1) * key.lda + acols) * 2;
+    const size_t bbytes = (size_t)((brows - 1) * key.ldb + bcols) * 2;
     void *scratch = nullptr, *scratch2 = nullptr, *a2 = nullptr, *b2 = nullptr;
     if (hipMalloc(&scratch, cbytes) == hipSuccess && hipMalloc(&scratch2, cbytes) == hipSuccess &&
         hipMalloc(&a2, abytes) == hipSuccess && hipMalloc(&b2, bbytes) == hipSuccess) {
       if (has_bias)
         hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &o.bias, sizeof(o.bias));
-      (void)hipMemcpyAsync(a2, o.a, abytes, hipMemcpyDeviceToDevice, o.s);
-      (void)hipMemcpyAsync(b2, o.b, bbytes, hipMemcpyDeviceToDevice, o.s);
+      if (hipMemcpyAsync(a2, o.a, abytes, hipMemcpyDeviceToDevice, o.s) != hipSuccess ||
+          hipMemcpyAsync(b2, o.b, bbytes, hipMemcpyDeviceToDevice, o.s) != hipSuccess) {
+        (void)hipGetLastError();   // not left behind for the next caller's launch check
+        (void)hipFree(scratch);
+        (void)hipFree(scratch2);
+        (void)hipFree(a2);
+        (void)hipFree(b2);
+        grk::set_error("grk_gemm: copying the operands for plan validation failed (m=%lld n=%lld k=%lld)",
+                       (long long)key.m, (long long)key.n, (long long)key.k);
+        return GRK_EHIP;
+      }
       if (order.size() > 1)
         for (int i : order) tms[i] = time_algo(h, p, &res[i].algo, o, scratch, 5);
       t0 = tms[order[0]];
