@@ -579,6 +579,15 @@ int grk_gemm(int trans_a, int trans_b, int64_t m, int64_t n, int64_t k, const vo
              int64_t ldb, int ab_dtype, void* c, int64_t ldc, int c_dtype, const void* c_in, float alpha, float beta,
              const void* bias, int bias_dtype, void* stream);
 
+/* grk_gemm with an epilogue: GRK_GEMM_EP_RELU stores max(alpha op(A) op(B) + beta C
+ * (+ bias), 0) -- the itemdnn / userdnn ReLU (model/BaseLine/model.py:302-309) in the
+ * GEMM's store instead of a separate pass. */
+#define GRK_GEMM_EP_NONE 0
+#define GRK_GEMM_EP_RELU 1
+int grk_gemm_ex(int trans_a, int trans_b, int64_t m, int64_t n, int64_t k, const void* a, int64_t lda, const void* b,
+                int64_t ldb, int ab_dtype, void* c, int64_t ldc, int c_dtype, const void* c_in, float alpha,
+                float beta, const void* bias, int bias_dtype, int epilogue, void* stream);
+
 /* Number of hipBLASLt candidates grk_gemm times for each NEW shape (1..256,
  * default 256; env GRK_GEMM_TUNE at load).  1 = the heuristic's first pick,
  * with no timing: the same kernel in every process. */

@@ -26,6 +26,7 @@ GRK_F32, GRK_BF16, GRK_F16 = 0, 1, 2
 GRK_F32_BF16 = 3  # pair logits: fp32 h, bf16 item embeddings
 GRK_FP8_E4M3 = 4  # attention q/k/v: OCP fp8 e4m3
 GRK_I32, GRK_I64 = 0, 1
+GRK_GEMM_EP_NONE, GRK_GEMM_EP_RELU = 0, 1
 BWD_ORDERED, BWD_CHUNKED, BWD_DENSE_BF16 = 0, 1, 2  # grk_embedding_backward flags (bf16 dense: | with CHUNKED)
 IDX_PLAIN, IDX_ITEM_MASK, IDX_USER_MASK, IDX_POSITION = 0, 1, 2, 3
 ADAM_DENSE, ADAM_LAZY = 0, 1
@@ -164,6 +165,7 @@ SIGNATURES = {
     'grk_store_array_widths': (_I, [C.POINTER(GrkStoreView), _P, _P, _I64, _P]),
     'grk_rq_assign': (_I, [_P, _I64, _P, _I64, _I, _I, _I, _P, _P, _P, _P, _P]),
     'grk_gemm': (_I, [_I, _I, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _I, _P, _F, _F, _P, _I, _P]),
+    'grk_gemm_ex': (_I, [_I, _I, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _I, _P, _F, _F, _P, _I, _I, _P]),
     'grk_pair_logits_partials': (_SZ, [_I64]),
     'grk_sampled_softmax_workspace': (_SZ, [_I64, _I]),
     'grk_sampled_softmax_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _I, _F, _P, _P, _P, _P, _P, _SZ, _P]),

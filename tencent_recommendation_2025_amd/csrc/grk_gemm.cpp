@@ -35,15 +35,16 @@ constexpr size_t kWorkspaceBytes = 256ull << 20;  // stream-K partials of the 2,
 struct Key {
   int ta, tb, abt, ct, bt, dev;
   int64_t m, n, k, lda, ldb, ldc;
+  int ep;   // GRK_GEMM_EP_*
   bool operator==(const Key& o) const {
     return ta == o.ta && tb == o.tb && abt == o.abt && ct == o.ct && bt == o.bt && dev == o.dev && m == o.m &&
-           n == o.n && k == o.k && lda == o.lda && ldb == o.ldb && ldc == o.ldc;
+           n == o.n && k == o.k && lda == o.lda && ldb == o.ldb && ldc == o.ldc && ep == o.ep;
   }
 };
 struct KeyHash {
   size_t operator()(const Key& x) const {
     size_t h = 1469598103934665603ull;
-    const int64_t v[] = {x.ta, x.tb, x.abt, x.ct, x.bt, x.dev, x.m, x.n, x.k, x.lda, x.ldb, x.ldc};
+    const int64_t v[] = {x.ta, x.tb, x.abt, x.ct, x.bt, x.dev, x.m, x.n, x.k, x.lda, x.ldb, x.ldc, x.ep};
     for (int64_t e : v) h = (h ^ (size_t)e) * 1099511628211ull;
     return h;
   }
@@ -128,10 +129,15 @@ int make_plan(hipblasLtHandle_t h, const Key& key, bool has_bias, Plan* p, const
   GRK_CHECK_BLAS(hipblasLtMatmulDescCreate(&p->op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
   GRK_CHECK_BLAS(hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)));
   GRK_CHECK_BLAS(hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)));
-  if (has_bias) {
-    const hipblasLtEpilogue_t ep = HIPBLASLT_EPILOGUE_BIAS;
-    const hipDataType bt = hip_type(key.bt);
+  if (has_bias || key.ep == GRK_GEMM_EP_RELU) {
+    // RELU: max(alpha A B + beta C (+ bias), 0) -- the dnn layers' relu in the GEMM's store
+    const hipblasLtEpilogue_t ep = key.ep == GRK_GEMM_EP_RELU
+                                       ? (has_bias ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_RELU)
+                                       : HIPBLASLT_EPILOGUE_BIAS;
     GRK_CHECK_BLAS(hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &ep, sizeof(ep)));
+  }
+  if (has_bias) {
+    const hipDataType bt = hip_type(key.bt);
     GRK_CHECK_BLAS(hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
   }
   const hipDataType ab = hip_type(key.abt);
@@ -259,7 +265,16 @@ using namespace grk;
 extern "C" int grk_gemm(int trans_a, int trans_b, int64_t m, int64_t n, int64_t k, const void* a, int64_t lda,
                         const void* b, int64_t ldb, int ab_dtype, void* c, int64_t ldc, int c_dtype, const void* c_in,
                         float alpha, float beta, const void* bias, int bias_dtype, void* stream) {
+  return grk_gemm_ex(trans_a, trans_b, m, n, k, a, lda, b, ldb, ab_dtype, c, ldc, c_dtype, c_in, alpha, beta, bias,
+                     bias_dtype, GRK_GEMM_EP_NONE, stream);
+}
+
+extern "C" int grk_gemm_ex(int trans_a, int trans_b, int64_t m, int64_t n, int64_t k, const void* a, int64_t lda,
+                           const void* b, int64_t ldb, int ab_dtype, void* c, int64_t ldc, int c_dtype,
+                           const void* c_in, float alpha, float beta, const void* bias, int bias_dtype, int epilogue,
+                           void* stream) {
   clear_error();
+  GRK_CHECK_ARG(epilogue == GRK_GEMM_EP_NONE || epilogue == GRK_GEMM_EP_RELU, "bad epilogue %d", epilogue);
   GRK_CHECK_ARG(m >= 0 && n >= 0 && k >= 0, "negative GEMM size");
   if (m == 0 || n == 0) return GRK_OK;
   GRK_CHECK_ARG(a && b && c, "a, b and c are required");
@@ -293,7 +308,7 @@ extern "C" int grk_gemm(int trans_a, int trans_b, int64_t m, int64_t n, int64_t 
     ws = wi->second;
   }
   const Key key{trans_a ? 1 : 0, trans_b ? 1 : 0, ab_dtype, c_dtype, bias ? bias_dtype : -1, dev,
-                m, n, k, lda, ldb, ldc};
+                m, n, k, lda, ldb, ldc, epilogue};
   auto pi = g_plans.find(key);
   if (pi == g_plans.end()) {
     Plan p;

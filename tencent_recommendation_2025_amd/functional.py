@@ -294,13 +294,20 @@ def _lookup_groups(specs, token_type, seq_len, num_tokens, out_ld, extras, split
 
 
 class _LinearFn(torch.autograd.Function):
-    """y = x W^T + b on grk_gemm (hipBLASLt with stream-K eligible).  bf16
-    operands (the autocast dtype of the reference's training), fp32
-    accumulation; the weight gradient is written by the GEMM in the weight's
-    own dtype (fp32 master weights: no bf16 round trip and no cast kernel)."""
+    """y = x W^T + b (+ addend) (then ReLU) on grk_gemm (hipBLASLt with stream-K
+    eligible).  bf16 operands (the autocast dtype of the reference's training),
+    fp32 accumulation; the weight gradient is written by the GEMM in the weight's
+    own dtype (fp32 master weights: no bf16 round trip and no cast kernel).
+
+    relu: the dnn layers' ReLU in the GEMM's store (grk_gemm_ex epilogue); the
+    backward masks the gradient by the saved output (threshold_backward).
+    in_place: a bf16 row-major addend whose only use is this sum (the projected
+    rows' bag sum, a column block of the gather buffer) is accumulated into where
+    it lies -- the output is that view -- instead of being copied to a contiguous
+    C first."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, addend):
+    def forward(ctx, x, weight, bias, addend, relu, in_place):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         if x2.dtype != torch.bfloat16:
@@ -310,21 +317,28 @@ class _LinearFn(torch.autograd.Function):
         wb = weight if weight.dtype == torch.bfloat16 and weight.is_contiguous() else bf16_shadow(weight)
         if wb is None:
             wb = weight.detach().to(torch.bfloat16).contiguous()
+        b = None if bias is None else bias.detach().contiguous()
+        out = None
         if addend is not None:
             addend = addend.reshape(-1, wb.shape[0])
-            if addend.dtype != torch.bfloat16 or addend.stride(1) != 1 or addend.stride(0) != wb.shape[0]:
+            if in_place and addend.dtype == torch.bfloat16 and addend.stride(1) == 1 and addend.stride(0) % 8 == 0 \
+                    and addend.data_ptr() % 16 == 0:
+                out, addend = addend, None
+            elif addend.dtype != torch.bfloat16 or addend.stride(1) != 1 or addend.stride(0) != wb.shape[0]:
                 addend = addend.to(torch.bfloat16).contiguous()
-        y = K.gemm(x2, wb, trans_b=True, bias=None if bias is None else bias.detach().contiguous(),
-                   addend=addend, beta=0.0 if addend is None else 1.0)
-        ctx.save_for_backward(x2, wb)
+        y = K.gemm(x2, wb, trans_b=True, bias=b, addend=addend, out=out,
+                   beta=0.0 if addend is None and out is None else 1.0, relu=relu)
+        ctx.save_for_backward(x2, wb, y if relu else None)
         ctx.meta = (shp, weight.dtype, None if bias is None else bias.dtype, ctx.needs_input_grad[3])
         return y.view(*shp[:-1], wb.shape[0])
 
     @staticmethod
     def backward(ctx, gy):
-        x2, wb = ctx.saved_tensors
+        x2, wb, y = ctx.saved_tensors
         shp, wdt, bdt, want_addend = ctx.meta
         g2 = gy.reshape(-1, gy.shape[-1])
+        if y is not None:            # ReLU in the forward's store: the gradient through its mask
+            g2 = torch.ops.aten.threshold_backward(g2, y, 0)
         if g2.dtype != torch.bfloat16:
             g2 = g2.to(torch.bfloat16)
         if not g2.is_contiguous():
@@ -340,14 +354,18 @@ class _LinearFn(torch.autograd.Function):
             dw = K.gemm(g2, x2, trans_a=True, out_dtype=dw_dt)
         if ctx.needs_input_grad[2] and db is None:
             db = g2.sum(0, dtype=torch.float32).to(bdt)
-        return dx, dw, db, (gy if want_addend else None)
+        ga = None
+        if want_addend:
+            ga = g2.view(gy.shape) if y is not None else gy
+        return dx, dw, db, ga, None, None
 
 
 @_disable
-def linear(x, weight, bias=None, addend=None):
-    """torch.nn.functional.linear (+ addend, as torch.addmm) on grk_gemm:
-    bf16 operands, fp32 accumulation, bf16 output."""
-    return _LinearFn.apply(x, weight, bias, addend)
+def linear(x, weight, bias=None, addend=None, relu=False, in_place=False):
+    """torch.nn.functional.linear (+ addend, as torch.addmm; then ReLU with relu) on
+    grk_gemm: bf16 operands, fp32 accumulation, bf16 output.  in_place: accumulate
+    into the addend where it lies (see _LinearFn; the addend's values are consumed)."""
+    return _LinearFn.apply(x, weight, bias, addend, bool(relu), bool(in_place))
 
 
 class _AddNormFn(torch.autograd.Function):

@@ -614,8 +614,9 @@ def attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab=None, parts=L.AT
 
 # ------------------------------------------------------------------ GEMM
 def gemm(a, b, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat16, alpha=1.0, beta=0.0, bias=None,
-         addend=None):
-    """grk_gemm (hipBLASLt): out[m, n] = alpha op(a) @ op(b) + beta C (+ bias[n]).
+         addend=None, relu=False):
+    """grk_gemm (hipBLASLt): out[m, n] = alpha op(a) @ op(b) + beta C (+ bias[n]),
+    then max(., 0) with relu (grk_gemm_ex's epilogue).
 
     a, b bf16 row-major 2-D (op = transpose when trans_*); out bf16 or fp32.
     C = ``addend`` (out's dtype and row stride) when given, else ``out``
@@ -640,11 +641,12 @@ def gemm(a, b, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat16,
         raise L.GrkError("addend must match the output's shape, dtype and row stride")
     if bias is not None and (bias.numel() != n or not bias.is_contiguous()):
         raise L.GrkError(f'bias must be a contiguous vector of {n}')
-    rc = L.lib().grk_gemm(int(trans_a), int(trans_b), m, n, k, a.data_ptr(), max(a.stride(0), 1), b.data_ptr(),
-                          max(b.stride(0), 1), L.dtype_code(a.dtype), out.data_ptr(), max(out.stride(0), 1),
-                          L.dtype_code(out.dtype), _ptr(addend), float(alpha), float(beta), _ptr(bias),
-                          L.dtype_code(bias.dtype) if bias is not None else 0, L.stream_ptr(a.device))
-    L.check(rc, 'grk_gemm')
+    rc = L.lib().grk_gemm_ex(int(trans_a), int(trans_b), m, n, k, a.data_ptr(), max(a.stride(0), 1), b.data_ptr(),
+                             max(b.stride(0), 1), L.dtype_code(a.dtype), out.data_ptr(), max(out.stride(0), 1),
+                             L.dtype_code(out.dtype), _ptr(addend), float(alpha), float(beta), _ptr(bias),
+                             L.dtype_code(bias.dtype) if bias is not None else 0,
+                             L.GRK_GEMM_EP_RELU if relu else L.GRK_GEMM_EP_NONE, L.stream_ptr(a.device))
+    L.check(rc, 'grk_gemm_ex')
     return out
 
 

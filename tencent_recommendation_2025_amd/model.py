@@ -648,7 +648,9 @@ class BaselineModel(torch.nn.Module):
                 if self._fwd_id is not None:
                     self._proj_cache[key] = w
             if _grk_gemm_ok(a):
-                return torch.relu(G.linear(a, w, addend=p))
+                # ReLU in the GEMM's store; the projected rows' sum p (a column block of the
+                # gather buffer, read by nothing else) accumulated into where it lies
+                return G.linear(a, w, addend=p, relu=True, in_place=True)
             return torch.relu(torch.addmm(p, a, w.t()) if p is not None else a @ w.t())
 
         x = dnn('item', wi, bool(item_p))

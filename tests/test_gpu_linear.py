@@ -1,0 +1,50 @@
+"""functional.linear's fused forms (round 4): the ReLU in hipBLASLt's store
+(grk_gemm_ex, GRK_GEMM_EP_RELU) and the addend accumulated where it lies
+(in_place) -- the itemdnn / userdnn layers of the fused model
+(model/BaseLine/model.py:302-309: relu(linear(cat(...)))) -- against the same
+math in fp32 from the same bf16 operands."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+@pytest.mark.parametrize('in_place', [False, True])
+@pytest.mark.parametrize('bias', [False, True])
+def test_linear_relu_addend_matches_fp32(in_place, bias):
+    from tencent_recommendation_2025_amd import functional as G
+    g = torch.Generator(device=DEV).manual_seed(0)
+    M, K, N = 1000, 552, 512
+    # the addend as a column block of a wider buffer, as the gather writes it
+    buf = torch.randn(M, K + N + 64, generator=g, device=DEV).bfloat16()
+    x = buf[:, :K].detach().requires_grad_(True)
+    p = buf[:, K:K + N].clone().detach()
+    holder = torch.zeros(M, K + N + 64, dtype=torch.bfloat16, device=DEV)
+    holder[:, K:K + N] = p
+    pv = holder[:, K:K + N].requires_grad_(False)
+    pv_ref = p.float()
+    w = (0.05 * torch.randn(N, K, generator=g, device=DEV)).requires_grad_(True)
+    b = (0.1 * torch.randn(N, generator=g, device=DEV)).requires_grad_(True) if bias else None
+    pa = pv.detach().requires_grad_(True) if not in_place else holder[:, K:K + N]
+    if in_place:
+        pa.requires_grad_(False)
+    y = G.linear(x, w, b, addend=pa, relu=True, in_place=in_place)
+    ref = torch.relu(x.detach().float() @ w.detach().bfloat16().float().t()
+                     + (b.detach().float() if bias else 0) + pv_ref)
+    got = y.float()
+    assert ((got - ref).abs() <= ref.abs() * 2 ** -7 + 1e-2).all()
+    assert (got[ref == 0] == 0).all()
+    gy = torch.randn(M, N, generator=g, device=DEV).bfloat16()
+    y.backward(gy)
+    # the reference gradients through the fp32 graph
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    yr = torch.relu(xr @ wr.t() + (b.detach().float() if bias else 0) + p.float())
+    yr.backward(gy.float())
+    for name, a, r in (('dx', x.grad.float(), xr.grad), ('dw', w.grad.float(), wr.grad)):
+        assert float((a - r).norm() / r.norm()) < 1e-2, name
+    if bias:
+        assert float((b.grad - (gy.float() * (yr > 0)).sum(0)).norm() / b.grad.norm()) < 1e-2
+    if not in_place:
+        assert float((pa.grad.float() - gy.float() * (yr > 0)).norm() / pa.grad.float().norm()) < 1e-2
