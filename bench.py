@@ -77,9 +77,9 @@ def parse():
     ap.add_argument('--dense-flat', type=int, default=1,
                     help='1: the dense parameters as one flat buffer on grk\'s multi-range AdamW (optim.DenseFlat); '
                          '0: torch\'s fused AdamW')
-    ap.add_argument('--sharded-jagged', type=int, default=0,
-                    help='1: the row-sharded trainer on jagged rows too (train.jagged_remaps; opt-in until verified '
-                         'on hardware -- the sharded step runs the padded layout by default)')
+    ap.add_argument('--sharded-jagged', type=int, default=1,
+                    help='1 (default since round 4, hardware-verified): the row-sharded trainer on jagged rows too '
+                         '(train.jagged_remaps), so N > 1 trains on the same rows as N = 1; 0: the padded layout')
     ap.add_argument('--shard-tables', type=int, default=None,
                     help='build only each rank\'s table rows (default: sharded and >= 10M items, BASELINE config 3)')
     ap.add_argument('--graph', type=int, default=1,
