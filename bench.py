@@ -696,12 +696,25 @@ def main():
             btrace, K.BACKWARD_TRACE = K.BACKWARD_TRACE, None
     # jagged + graph: one captured graph per capacity of the pool, captured before the
     # timed region (extra untimed steps on the batches of a capacity not captured yet)
+    # Every rank takes the same number of steps (each one's collectives: the row
+    # exchange and the all-reduces); a rank whose pool has its capacities captured
+    # keeps stepping until every rank's are.  The batch sequence continues from the
+    # warm-up, so every prefetch is the batch of the step after it.
     prewarm = 0
     if jagged and trainer.graph:
-        for i in range(len(pool)):
-            while J.capacity_for(rows[i], a.jagged_quantum) not in trainer._graphs:
-                trainer.step(pool[i], next_batch=pool[(i + 1) % len(pool)], rows=rows[i])
-                prewarm += 1
+        k = a.warmup
+        while True:
+            done = all(c in trainer._graphs for c in caps)
+            if world > 1:
+                flag = torch.tensor([0 if done else 1], dtype=torch.int32, device=dev)
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+                done = int(flag.item()) == 0
+            if done:
+                break
+            step(k)
+            k += 1
+            prewarm += 1
+    first = a.warmup + prewarm
     torch.cuda.synchronize()
     progress(f'timed region: {a.steps} steps ({prewarm} prewarm steps captured the remaining capacities)')
     if world > 1:
@@ -710,7 +723,7 @@ def main():
     evs, host = [], []
     for i in range(a.steps):
         th = time.perf_counter()
-        loss = step(i)
+        loss = step(first + i)
         if a.step_times:
             host.append(time.perf_counter() - th)
             e = torch.cuda.Event(enable_timing=True)
@@ -727,7 +740,8 @@ def main():
     final_loss = float(loss.float().item())
     if a.step_times and rank == 0:
         dev_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(len(evs) - 1)]
-        caps_i = [J.capacity_for(rows[i % len(pool)], a.jagged_quantum) if jagged else 0 for i in range(a.steps)]
+        caps_i = [J.capacity_for(rows[(first + i) % len(pool)], a.jagged_quantum) if jagged else 0
+                  for i in range(a.steps)]
         print('# step device intervals (ms) / host issue (ms) / capacity:', file=sys.stderr)
         for i, d in enumerate(dev_ms):
             print(f'  {i + 1:3d} {d:7.3f} {1e3 * host[i + 1]:7.3f} {caps_i[i + 1]}', file=sys.stderr)

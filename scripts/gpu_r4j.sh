@@ -24,6 +24,10 @@ GRK_C5_MODEL_TESTS=1 timeout -k 10 400 python -u -m pytest -v -rs --timeout 300 
 timeout -k 10 300 python -u bench.py --fp8 1 --hidden 1024 --maxlen 1024 --batch 16 --steps 10 --warmup 3 \
   --cpu-baseline 0 --roofline-reps 3 > $O/bench_c5.json 2> $O/bench_c5.log; check bench_c5 $?
 timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.log; check bench $?
+# the N = 2 path (row-sharded, jagged rows, lockstep prewarm) rehearsed with two gloo ranks on this one GPU
+timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29611 bench.py --gpus 2 --steps 6 --warmup 2 --backend gloo --cpu-baseline 0 --roofline-reps 1 \
+  > $O/bench_world2.json 2> $O/bench_world2.log; check bench_world2 $?
 MODES=fused bash scripts/gpu_step_profiles.sh || exit $?
 cp gpurun_out/step_breakdown_fused.txt $O/step_breakdown.txt
 cp gpurun_out/step_timeline_fused.txt $O/step_timeline.txt
