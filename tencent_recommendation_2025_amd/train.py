@@ -48,7 +48,75 @@ def _tensors(batch):
     return out
 
 
+class PackedBatch(tuple):
+    """A batch whose tensors are views of ONE byte arena (pack_batch): a graph
+    replay's input copy is then a single copy of the arena instead of a
+    multi-tensor copy per dtype over ~70 tensors (~83 us per C2 step measured)."""
+    arena: torch.Tensor
+    layout: tuple
+
+
+_ARENA_ALIGN = 256
+
+
+def _arena_layout(tensors):
+    offs, off = [], 0
+    for t in tensors:
+        offs.append(off)
+        off += -(-t.numel() * t.element_size() // _ARENA_ALIGN) * _ARENA_ALIGN
+    return offs, off
+
+
+def _rebuild(batch, views):
+    """batch's structure with its tensors (in _tensors order) replaced by views."""
+    it = iter(views)
+    res = []
+    for x in batch:
+        if isinstance(x, torch.Tensor):
+            res.append(next(it))
+        elif isinstance(x, dict):
+            d = dict(x)
+            for k, v in sorted(x.items()):
+                if isinstance(v, torch.Tensor):
+                    d[k] = next(it)
+            res.append(d)
+        else:
+            res.append(x)
+    return res
+
+
+def _views(arena, tensors, offs):
+    out = []
+    for t, o in zip(tensors, offs):
+        nb = t.numel() * t.element_size()
+        out.append(arena[o:o + nb].view(t.dtype).view(t.shape))
+    return out
+
+
+def pack_batch(batch):
+    """The batch with every tensor moved into one arena on its device (same values,
+    dtypes and shapes; contiguous views).  All tensors must share one device."""
+    ts = _tensors(batch)
+    if not ts or len({t.device for t in ts}) != 1:
+        raise ValueError('pack_batch: a batch with tensors on one device')
+    offs, total = _arena_layout(ts)
+    arena = torch.empty(total, dtype=torch.uint8, device=ts[0].device)
+    views = _views(arena, ts, offs)
+    for v, t in zip(views, ts):
+        v.copy_(t)
+    out = PackedBatch(_rebuild(batch, views))
+    out.arena = arena
+    out.layout = tuple((o, t.dtype, tuple(t.shape)) for o, t in zip(offs, ts))
+    return out
+
+
 def _clone_batch(batch):
+    if isinstance(batch, PackedBatch):
+        ts = _tensors(batch)
+        arena = batch.arena.clone()
+        out = PackedBatch(_rebuild(batch, _views(arena, ts, [o for o, _, _ in batch.layout])))
+        out.arena, out.layout = arena, batch.layout
+        return out
     res = []
     for x in batch:
         if isinstance(x, torch.Tensor):
@@ -260,7 +328,11 @@ class Trainer:
             # stream then waits only for the previous step, and prepare(next) finds
             # the split sizes on the host a whole step early
             self.opt.prefetch(next_batch)
-        _copy_batch(dst, src)
+        if isinstance(batch, PackedBatch) and isinstance(self._static, PackedBatch) \
+                and batch.layout == self._static.layout:
+            self._static.arena.copy_(batch.arena, non_blocking=True)   # one copy for the whole batch
+        else:
+            _copy_batch(dst, src)
         if self._sharded:
             self.opt.prepare(self._static, key=batch[0])
             self._g.replay()

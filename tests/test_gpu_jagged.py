@@ -403,3 +403,35 @@ def test_merged_projection_backward_matches_and_replays_bitwise():
     assert torch.equal(lm, lg), (lm, lg)
     for k in runs['merged'][1]:
         assert torch.equal(runs['merged'][1][k], runs['merged_graph'][1][k]), k
+
+
+def test_packed_batches_replay_equals_unpacked():
+    """Graph replays fed arena-packed batches (train.pack_batch: the input copy is one
+    launch) give the same losses and parameters, bit for bit, as replays fed the
+    plain batches (a multi-tensor copy per dtype) -- jagged rows, two capacities."""
+    from tencent_recommendation_2025_amd import jagged as J
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer, pack_batch
+    cfg = S.SyntheticConfig(batch_size=8, maxlen=40, num_items=2000, num_users=300, min_len=4)
+    short = S.SyntheticConfig(**{**cfg.__dict__, 'min_len': 2})
+    stats, types = S.feature_schema(cfg)
+    args = S.make_args(hidden_units=64, maxlen=40, num_blocks=1, num_heads=2)
+    runs = []
+    for packed in (False, True):
+        torch.manual_seed(0)
+        m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, args).to(DEV)
+        tr = Trainer(m, FusedAdamW(m, lr=1e-3), loss='bce', graph=True, graph_warmup=1, jagged=True,
+                     jagged_quantum=64)
+        g = torch.Generator(device=DEV).manual_seed(5)
+        pool = [S.make_batch(cfg, g, DEV), S.make_batch(short, g, DEV), S.make_batch(cfg, g, DEV)]
+        if packed:
+            pool = [pack_batch(b) for b in pool]
+        rows = [J.span_rows(b[3]) for b in pool]
+        losses = torch.stack([tr.step(pool[i % 3], rows=rows[i % 3]).clone() for i in range(9)])
+        torch.cuda.synchronize()
+        runs.append((losses, {k: v.clone() for k, v in m.state_dict().items()}))
+    assert torch.equal(runs[0][0], runs[1][0])
+    for k in runs[0][1]:
+        assert torch.equal(runs[0][1][k], runs[1][1][k]), k

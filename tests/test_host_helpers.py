@@ -284,3 +284,26 @@ def test_valid_bytes_eager_and_compiled():
     assert torch.equal(M._valid_bytes(tt), want)
     got = torch.compile(lambda t: M._valid_bytes(t) + 0, backend='inductor', fullgraph=True)(tt)
     assert got.dtype == torch.uint8 and torch.equal(got, want)
+
+
+def test_pack_batch_one_arena_same_values():
+    """train.pack_batch: every tensor of a collate-shaped batch (tuple fields, feature
+    dicts, mixed dtypes) becomes a view of one byte arena with the same values,
+    dtypes and shapes; a clone has the same layout, and copying one arena into the
+    other's is the whole batch copy a graph replay does (one launch)."""
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd import train as T
+    cfg = S.SyntheticConfig(batch_size=4, maxlen=12, num_items=300, num_users=40, min_len=3)
+    b1 = S.make_batch(cfg, torch.Generator().manual_seed(1), 'cpu')
+    b2 = S.make_batch(cfg, torch.Generator().manual_seed(2), 'cpu')
+    p1, p2 = T.pack_batch(b1), T.pack_batch(b2)
+    assert isinstance(p1, T.PackedBatch) and p1.layout == p2.layout
+    for a, b in zip(T._tensors(p1), T._tensors(b1)):
+        assert a.dtype == b.dtype and a.shape == b.shape and torch.equal(a, b)
+        assert a.untyped_storage().data_ptr() == p1.arena.untyped_storage().data_ptr()
+    st = T._clone_batch(p1)
+    assert isinstance(st, T.PackedBatch) and st.layout == p1.layout and st.arena.data_ptr() != p1.arena.data_ptr()
+    st.arena.copy_(p2.arena)
+    for a, b in zip(T._tensors(st), T._tensors(b2)):
+        assert torch.equal(a, b)
+    assert isinstance(st[6], dict) and set(st[6]) == set(b2[6])
