@@ -967,6 +967,124 @@ __global__ void __launch_bounds__(256) k_seg_wave_fused(int64_t nhot, int nslice
                          dense_out, uniq_rows, row_slot);
 }
 
+// ----------------------------------------------------- one-workgroup calls ----
+// A call of at most kTinyN occurrences (the user table at BASELINE config 2: one
+// user token per sequence, 128 occurrences) in ONE launch instead of ~14: keys
+// built into LDS, stable ranks by counting (rank = smaller keys + equal keys
+// earlier in occurrence order: the stable sort's permutation), segment heads by
+// wave ballots, then one wave per unique row summing its occurrences in
+// occurrence order -- the ordered mode's arithmetic (fp32 adds from 0, row by
+// row in occurrence order), so the outputs equal the general path's bit for bit.
+// Sparse outputs only (uniq_ids / uniq_rows / uniq_count / row_slot).
+constexpr int kTinyN = 2048;
+constexpr int kTinyThreads = 1024;
+
+template <typename G, typename I, int LW>
+__global__ void __launch_bounds__(kTinyThreads) k_bwd_tiny(LookupArgs la, int esize, const int32_t* __restrict__ token_type,
+                                                          int32_t T_len, int64_t num_rows, int64_t padding_idx, int dim,
+                                                          int64_t* __restrict__ uniq_ids, float* __restrict__ uniq_rows,
+                                                          int32_t* __restrict__ uniq_count,
+                                                          int32_t* __restrict__ row_slot, int32_t* err_flag) {
+  __shared__ unsigned key[kTinyN];
+  __shared__ unsigned long long ptr[kTinyN];
+  __shared__ unsigned short ord[kTinyN];
+  __shared__ int seg[kTinyN + 1];
+  __shared__ int wtot[kTinyThreads / 64 + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = kTinyThreads / 64;
+  const int64_t base = la.occ_off[0];
+  const int n = (int)(la.occ_off[la.num] - base);
+  const unsigned sentinel = (unsigned)num_rows;
+  for (int o = tid; o < n; o += kTinyThreads) {
+    const int64_t oa = base + o;
+    int l = 0;
+    while (l + 1 < la.num && oa >= la.occ_off[l + 1]) ++l;
+    const grk_lookup& L = la.l[l];
+    const int64_t rel = oa - la.occ_off[l];
+    const int64_t t = rel / L.bag;
+    const int a = (int)(rel - t * L.bag);
+    const int64_t row = resolve_row(reinterpret_cast<const I*>(L.idx), t, a, L.idx_ld, L.idx_mode, token_type, T_len);
+    unsigned k = sentinel;
+    if (row < 0 || row >= L.table_rows || L.row_offset + row >= num_rows) {
+      if (err_flag) *err_flag = 1;
+    } else if (row != padding_idx) {
+      k = (unsigned)(L.row_offset + row);
+    }
+    key[o] = k;
+    ptr[o] = (unsigned long long)((const char*)L.grad + (t * L.grad_ld + L.grad_col) * esize);
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += kTinyThreads) {
+    const unsigned ki = key[i];
+    int r = 0;
+    for (int j = 0; j < n; ++j) {
+      const unsigned kj = key[j];
+      r += (kj < ki) | ((kj == ki) & (j < i));
+    }
+    ord[r] = (unsigned short)i;
+  }
+  __syncthreads();
+  // segment heads in sorted order: each wave takes 2 x 64 consecutive positions
+  constexpr int PER = kTinyN / kTinyThreads;   // positions per thread (2)
+  int cnt = 0;
+  bool hd[PER];
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int pidx = (wave * PER + e) * 64 + lane;
+    bool h = false;
+    if (pidx < n) {
+      const unsigned k = key[ord[pidx]];
+      h = k != sentinel && (pidx == 0 || key[ord[pidx - 1]] != k);
+    }
+    hd[e] = h;
+    cnt += __popcll(__ballot(h));
+  }
+  if (lane == 0) wtot[wave] = cnt;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int w = 0; w < NW; ++w) {
+      const int c = wtot[w];
+      wtot[w] = acc;
+      acc += c;
+    }
+    wtot[NW] = acc;
+  }
+  __syncthreads();
+  int u0 = wtot[wave];
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const unsigned long long m = __ballot(hd[e]);
+    if (hd[e]) seg[u0 + __popcll(m & below)] = (wave * PER + e) * 64 + lane;
+    u0 += __popcll(m);
+  }
+  const int nseg = wtot[NW];
+  if (tid == 0) {
+    // one past the last real occurrence: the first sentinel position (sentinels sort last)
+    int end = n;
+    while (end > 0 && key[ord[end - 1]] == sentinel) --end;
+    seg[nseg] = end;
+    *uniq_count = nseg;
+  }
+  __syncthreads();
+  const int c = lane * LW;
+  for (int u = wave; u < nseg; u += NW) {
+    const int s0 = seg[u], s1 = seg[u + 1];
+    const unsigned k = key[ord[s0]];
+    WaveAcc<LW> acc;
+    acc.zero();
+    for (int p = s0; p < s1; ++p) {
+      WaveVec<G, LW> r;
+      r.load(ptr[ord[p]], c);
+#pragma unroll
+      for (int x = 0; x < LW; ++x) acc.v[x] += r.get(x);
+    }
+    store_final(acc, k, u, dim, c, (float*)nullptr, uniq_rows, row_slot);
+    if (uniq_ids && lane == 0) uniq_ids[u] = (int64_t)k;
+  }
+}
+
 // ------------------------------------------------------------ workspace ----
 // Stable radix sort of (row key, gradient-row address) pairs (grk_sort.hip).
 size_t sort_pairs_workspace(int64_t n);
@@ -1186,6 +1304,40 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   const int B = 256;
   const int esize = grad_dtype == GRK_F32 ? 4 : 2;
   const unsigned sentinel = (unsigned)num_rows;
+  {
+    // a small sparse call in one launch (k_bwd_tiny): ordered mode, sparse outputs only
+    const int lwt = dim % 64 == 0 ? dim / 64 : 0;
+    const bool tiny_ok = total <= kTinyN && num_lookups <= kLookupsPerLaunch && flags == GRK_BWD_ORDERED &&
+                         !dense_any && (uniq_rows || row_slot || uniq_ids) &&
+                         ((grad_dtype == GRK_BF16 && lwt == 8) || (grad_dtype != GRK_BF16 && (lwt == 4 || lwt == 8)));
+    if (tiny_ok) {
+      LookupArgs la;
+      memset(&la, 0, sizeof(la));
+      la.num = num_lookups;
+      int64_t occ = 0;
+      for (int i = 0; i < num_lookups; ++i) {
+        la.l[i] = lookups[i];
+        la.occ_off[i] = occ;
+        occ += lookups[i].num_tokens * lookups[i].bag;
+      }
+      la.occ_off[num_lookups] = occ;
+#define GRK_TINY(G, I, LW)                                                                                          \
+  k_bwd_tiny<G, I, LW><<<1, kTinyThreads, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, dim,    \
+                                                  uniq_ids, uniq_rows, uniq_count, row_slot, err_flag)
+      if (itype == GRK_I64) {
+        if (grad_dtype == GRK_BF16) GRK_TINY(bf16_t, int64_t, 8);
+        else if (lwt == 8) GRK_TINY(float, int64_t, 8);
+        else GRK_TINY(float, int64_t, 4);
+      } else {
+        if (grad_dtype == GRK_BF16) GRK_TINY(bf16_t, int32_t, 8);
+        else if (lwt == 8) GRK_TINY(float, int32_t, 8);
+        else GRK_TINY(float, int32_t, 4);
+      }
+#undef GRK_TINY
+      GRK_LAUNCH_CHECK();
+      return GRK_OK;
+    }
+  }
   // chunked mode writing only the dense rows: segment bounds by row (k_segments_key),
   // no segment numbering (head positions) at all
   const int lw0 = dim % 64 == 0 ? dim / 64 : 0;
