@@ -15,7 +15,7 @@ check() {  # name rc
   if grep -Eqi "$FAULT" $O/$1.log; then echo "$1: GPU fault -- stopping" >> $O/summary.txt; exit 3; fi
   case $2 in 0|1) return 0 ;; *) echo "$1: exit $2 -- stopping" >> $O/summary.txt; exit $2 ;; esac
 }
-timeout -k 10 600 python -u -m pytest -v -rs --timeout 200 --timeout-method thread tests/test_gpu_linear.py \
+timeout -k 10 600 python -u -m pytest -v -rs --timeout 200 --timeout-method thread tests/test_gpu_embedding.py tests/test_gpu_linear.py \
   tests/test_gpu_seqstore.py tests/test_gpu_model.py tests/test_gpu_jagged.py tests/test_gpu_ggemm.py \
   > $O/tests.log 2>&1; check tests $?
 timeout -k 10 120 python -u scripts/diag/c5_gemm_isolate.py grk > $O/c5_gemm.log 2>&1; check c5_gemm $?
