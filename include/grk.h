@@ -466,6 +466,23 @@ int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, int64_t ldo
 int grk_silu_fp8(const void* pre, int64_t ldpre, int64_t rows, int cols, void* out, int64_t ldout, void* stream);
 int grk_dsilu_mul(void* g, int64_t ldg, const void* pre, int64_t ldpre, int64_t rows, int cols, void* stream);
 
+/* Embedding combine (round 4), the first block's input in log2feats
+ * (replaces model/BaseLine/model.py:313-321, the seqs = item + user features,
+ * *= sqrt(d), += pos_emb, emb_dropout chain; the ReLUs of itemdnn / userdnn,
+ * model.py:302-309, folded in with relu != 0):
+ *   y = dropout((act(a) + act(b)) * scale + pos),  act = ReLU if relu else identity
+ * bf16 rows (strides multiples of 8, 16-byte aligned); b and pos optional.
+ * Backward: g = gy * keep / (1 - p); gpos = g; ga = g * scale * [a > 0 if relu],
+ * gb likewise (each output optional).  The dropout decisions are the
+ * norm-gate's counter hash of (seed, row, col); seed_dev as there. */
+int grk_emb_combine_fwd(const void* a, int64_t lda, const void* b, int64_t ldb, const void* pos, int64_t ldp,
+                        float scale, int relu, int64_t rows, int dim, float dropout_p, uint64_t seed,
+                        const uint64_t* seed_dev, void* y, int64_t ldy, void* stream);
+int grk_emb_combine_bwd(const void* gy, int64_t ldgy, const void* a, int64_t lda, const void* b, int64_t ldb,
+                        float scale, int relu, int64_t rows, int dim, float dropout_p, uint64_t seed,
+                        const uint64_t* seed_dev, void* ga, int64_t ldga, void* gb, int64_t ldgb, void* gpos,
+                        int64_t ldgp, void* stream);
+
 int grk_norm_gate_fwd(const void* o, int64_t ldo, const void* u, int64_t ldu, const float* gamma,
                       const float* beta, float eps, int64_t rows, int dim, float dropout_p, uint64_t seed,
                       const uint64_t* seed_dev, void* y, int64_t ldy, float* stats, void* stream);

@@ -16,7 +16,7 @@ check() {  # name rc
   case $2 in 0|1) return 0 ;; *) echo "$1: exit $2 -- stopping" >> $O/summary.txt; exit $2 ;; esac
 }
 timeout -k 10 600 python -u -m pytest -v -rs --timeout 200 --timeout-method thread tests/test_gpu_embedding.py tests/test_gpu_linear.py \
-  tests/test_gpu_seqstore.py tests/test_gpu_model.py tests/test_gpu_jagged.py tests/test_gpu_ggemm.py \
+  tests/test_gpu_seqstore.py tests/test_gpu_model.py tests/test_gpu_jagged.py tests/test_gpu_ggemm.py tests/test_gpu_emb_combine.py \
   > $O/tests.log 2>&1; check tests $?
 timeout -k 10 120 python -u scripts/diag/c5_gemm_isolate.py grk > $O/c5_gemm.log 2>&1; check c5_gemm $?
 GRK_C5_MODEL_TESTS=1 timeout -k 10 400 python -u -m pytest -v -rs --timeout 300 --timeout-method thread \

@@ -115,6 +115,9 @@ SIGNATURES = {
     'grk_embedding_gather': (_I, [C.POINTER(GrkFeature), _I, _I, _I, _I, _I64, _P, C.c_int32, _P, _I64, _P, _P]),
     'grk_silu_fp8': (_I, [_P, _I64, _I64, _I, _P, _I64, _P]),
     'grk_dsilu_mul': (_I, [_P, _I64, _P, _I64, _I64, _I, _P]),
+    'grk_emb_combine_fwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _F, _I, _I64, _I, _F, C.c_uint64, _P, _P, _I64, _P]),
+    'grk_emb_combine_bwd': (_I, [_P, _I64, _P, _I64, _P, _I64, _F, _I, _I64, _I, _F, C.c_uint64, _P, _P, _I64, _P,
+                                 _I64, _P, _I64, _P]),
     'grk_embedding_backward_workspace': (_SZ, [_I64, _I64, _I]),
     'grk_embedding_chunked_size': (_I, []),
     'grk_sort_pairs_workspace': (_SZ, [_I64]),

@@ -469,9 +469,159 @@ __global__ void __launch_bounds__(256) k_dsilu_mul(bf16_t* __restrict__ g, int64
   }
 }
 
+// ----------------------------------------- embedding combine (log2feats) ----
+// The input of the first block (model/BaseLine/model.py:313-321):
+//   seqs = dropout((act(a) + act(b)) * scale + pos),  act = ReLU or identity
+// where a / b are the itemdnn / userdnn GEMM outputs (pre-activation with
+// relu) and pos the position-embedding rows.  Eager: two ReLUs, an add, a
+// mul, an add and a dropout forward; masking, scaling and two ReLU masks
+// backward.  Here one pass each way, 8 elements per lane, rounded to bf16
+// once.  Backward: g = gy m, gpos = g, ga = g scale [a > 0], gb likewise.
+struct ECParams {
+  const bf16_t* a; int64_t lda;
+  const bf16_t* b; int64_t ldb;  // optional
+  const bf16_t* pos; int64_t ldp;  // optional
+  float scale; int relu;
+  int64_t rows; int dim;
+  float dropout_p; unsigned long long seed;
+  const unsigned long long* seed_dev;
+  bf16_t* y; int64_t ldy;
+  const bf16_t* gy; int64_t ldgy;
+  bf16_t* ga; int64_t ldga;
+  bf16_t* gb; int64_t ldgb;
+  bf16_t* gpos; int64_t ldgp;
+};
+
+__device__ __forceinline__ void ec_keep8(const ECParams& p, int64_t row, int c8, float* m) {
+  if (p.dropout_p <= 0.f) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = 1.f;
+    return;
+  }
+  const float rk = 1.0f / (1.0f - p.dropout_p);
+  const unsigned long long seed = p.seed_dev ? *p.seed_dev : p.seed;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) m[e] = ng_keep(seed, row, c8 + e, p.dim, p.dropout_p) ? rk : 0.f;
+}
+
+__global__ void __launch_bounds__(256) k_emb_combine(ECParams p) {
+  const int per_row = p.dim >> 3;
+  const int64_t units = p.rows * per_row;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = u / per_row;
+    const int c = (int)(u - r * per_row) * 8;
+    float a[8], b[8], q[8], m[8], y[8];
+    load8(p.a + r * p.lda + c, a);
+    if (p.b) load8(p.b + r * p.ldb + c, b);
+    if (p.pos) load8(p.pos + r * p.ldp + c, q);
+    ec_keep8(p, r, c, m);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float s = p.relu ? fmaxf(a[e], 0.f) : a[e];
+      if (p.b) s += p.relu ? fmaxf(b[e], 0.f) : b[e];
+      s *= p.scale;
+      if (p.pos) s += q[e];
+      y[e] = s * m[e];
+    }
+    store8(p.y + r * p.ldy + c, y);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_emb_combine_bwd(ECParams p) {
+  const int per_row = p.dim >> 3;
+  const int64_t units = p.rows * per_row;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = u / per_row;
+    const int c = (int)(u - r * per_row) * 8;
+    float g[8], m[8], t[8];
+    load8(p.gy + r * p.ldgy + c, g);
+    ec_keep8(p, r, c, m);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] *= m[e];
+    if (p.gpos) store8(p.gpos + r * p.ldgp + c, g);
+    if (p.ga) {
+      if (p.relu) load8(p.a + r * p.lda + c, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = (!p.relu || t[e] > 0.f) ? g[e] * p.scale : 0.f;
+      store8(p.ga + r * p.ldga + c, t);
+    }
+    if (p.gb) {
+      if (p.relu) load8(p.b + r * p.ldb + c, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = (!p.relu || t[e] > 0.f) ? g[e] * p.scale : 0.f;
+      store8(p.gb + r * p.ldgb + c, t);
+    }
+  }
+}
+
+static unsigned ec_grid(int64_t rows, int dim) {
+  const int64_t units = rows * (dim / 8);
+  const int64_t want = (units + 255) / 256;
+  return (unsigned)(want < 4096 ? (want < 1 ? 1 : want) : 4096);
+}
+
+static int ec_check_rows(const void* t, int64_t ld, int dim, const char* name) {
+  if (!t) return GRK_OK;
+  if (ld < dim || ld % 8 != 0 || (uintptr_t)t % 16 != 0) {
+    set_error("%s: row stride must be >= dim and a multiple of 8, 16-byte aligned", name);
+    return GRK_EINVAL;
+  }
+  return GRK_OK;
+}
+
 }  // namespace grk
 
 using namespace grk;
+
+extern "C" int grk_emb_combine_fwd(const void* a, int64_t lda, const void* b, int64_t ldb, const void* pos,
+                                   int64_t ldp, float scale, int relu, int64_t rows, int dim, float dropout_p,
+                                   uint64_t seed, const uint64_t* seed_dev, void* y, int64_t ldy, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(rows >= 0 && dim > 0 && dim % 8 == 0, "dim must be a positive multiple of 8");
+  GRK_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f, "dropout_p must be in [0, 1)");
+  if (rows == 0) return GRK_OK;
+  GRK_CHECK_ARG(a && y, "a and y required");
+  int rc;
+  if ((rc = ec_check_rows(a, lda, dim, "a")) || (rc = ec_check_rows(b, ldb, dim, "b")) ||
+      (rc = ec_check_rows(pos, ldp, dim, "pos")) || (rc = ec_check_rows(y, ldy, dim, "y")))
+    return rc;
+  ECParams p;
+  memset(&p, 0, sizeof(p));
+  p.a = (const bf16_t*)a; p.lda = lda; p.b = (const bf16_t*)b; p.ldb = ldb; p.pos = (const bf16_t*)pos; p.ldp = ldp;
+  p.scale = scale; p.relu = relu != 0; p.rows = rows; p.dim = dim;
+  p.dropout_p = dropout_p; p.seed = seed; p.seed_dev = (const unsigned long long*)seed_dev;
+  p.y = (bf16_t*)y; p.ldy = ldy;
+  k_emb_combine<<<ec_grid(rows, dim), 256, 0, (hipStream_t)stream>>>(p);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+extern "C" int grk_emb_combine_bwd(const void* gy, int64_t ldgy, const void* a, int64_t lda, const void* b,
+                                   int64_t ldb, float scale, int relu, int64_t rows, int dim, float dropout_p,
+                                   uint64_t seed, const uint64_t* seed_dev, void* ga, int64_t ldga, void* gb,
+                                   int64_t ldgb, void* gpos, int64_t ldgp, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(rows >= 0 && dim > 0 && dim % 8 == 0, "dim must be a positive multiple of 8");
+  GRK_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f, "dropout_p must be in [0, 1)");
+  if (rows == 0) return GRK_OK;
+  GRK_CHECK_ARG(gy, "gy required");
+  GRK_CHECK_ARG(!relu || ((!ga || a) && (!gb || b)), "relu: ga / gb need the forward's a / b");
+  int rc;
+  if ((rc = ec_check_rows(gy, ldgy, dim, "gy")) || (rc = ec_check_rows(a, lda, dim, "a")) ||
+      (rc = ec_check_rows(b, ldb, dim, "b")) || (rc = ec_check_rows(ga, ldga, dim, "ga")) ||
+      (rc = ec_check_rows(gb, ldgb, dim, "gb")) || (rc = ec_check_rows(gpos, ldgp, dim, "gpos")))
+    return rc;
+  ECParams p;
+  memset(&p, 0, sizeof(p));
+  p.a = (const bf16_t*)a; p.lda = lda; p.b = (const bf16_t*)b; p.ldb = ldb;
+  p.scale = scale; p.relu = relu != 0; p.rows = rows; p.dim = dim;
+  p.dropout_p = dropout_p; p.seed = seed; p.seed_dev = (const unsigned long long*)seed_dev;
+  p.gy = (const bf16_t*)gy; p.ldgy = ldgy; p.ga = (bf16_t*)ga; p.ldga = ldga; p.gb = (bf16_t*)gb; p.ldgb = ldgb;
+  p.gpos = (bf16_t*)gpos; p.ldgp = ldgp;
+  k_emb_combine_bwd<<<ec_grid(rows, dim), 256, 0, (hipStream_t)stream>>>(p);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
 
 extern "C" int grk_norm_gate_fwd(const void* o, int64_t ldo, const void* u, int64_t ldu, const float* gamma,
                                  const float* beta, float eps, int64_t rows, int dim, float dropout_p, uint64_t seed,

@@ -368,6 +368,51 @@ def linear(x, weight, bias=None, addend=None, relu=False, in_place=False):
     return _LinearFn.apply(x, weight, bias, addend, bool(relu), bool(in_place))
 
 
+class _EmbCombineFn(torch.autograd.Function):
+    """seqs = dropout((act(a) + act(b)) * scale + pos) on grk_emb_combine (one pass
+    each way); a / b the itemdnn / userdnn outputs before their ReLU when relu."""
+
+    @staticmethod
+    def forward(ctx, a, b, pos, scale, relu, dropout_p, seed):
+        D = a.shape[-1]
+
+        def rows(t):
+            if t is None:
+                return None
+            t = t.reshape(-1, D)
+            return t if t.dtype == torch.bfloat16 and t.stride(-1) == 1 and t.stride(0) % 8 == 0 \
+                and t.data_ptr() % 16 == 0 else t.to(torch.bfloat16).contiguous()
+
+        a2, b2, p2 = rows(a), rows(b), rows(pos)
+        y = K.emb_combine_fwd(a2, b2, p2, scale, relu, dropout_p, seed)
+        ctx.save_for_backward(a2 if relu else None, b2 if relu else None,
+                              seed if isinstance(seed, torch.Tensor) else None)
+        ctx.meta = (a.shape, scale, relu, dropout_p, None if isinstance(seed, torch.Tensor) else seed,
+                    a.dtype, None if b is None else b.dtype, None if pos is None else pos.dtype)
+        return y.view(a.shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        a2, b2, seed_t = ctx.saved_tensors
+        shp, scale, relu, p, seed_i, adt, bdt, pdt = ctx.meta
+        g2 = gy.reshape(-1, shp[-1])
+        if g2.dtype != torch.bfloat16 or g2.stride(-1) != 1 or g2.stride(0) % 8 or g2.data_ptr() % 16:
+            g2 = g2.to(torch.bfloat16).contiguous()
+        want = (ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        ga, gb, gp = K.emb_combine_bwd(g2, a2, b2, scale, relu, p, seed_t if seed_t is not None else seed_i, want)
+        ga = ga.view(shp).to(adt) if ga is not None else None
+        gb = gb.view(shp).to(bdt) if gb is not None else None
+        gp = gp.view(shp).to(pdt) if gp is not None else None
+        return ga, gb, gp, None, None, None, None
+
+
+@_disable
+def emb_combine(a, b, pos, scale, relu=True, dropout_p=0.0, seed=0):
+    """The first block's input: dropout((act(a) + act(b)) * scale + pos) (bf16 out).
+    b / pos may be None; seed an int or a device int64 [1] tensor (model.dropout_seed)."""
+    return _EmbCombineFn.apply(a, b, pos, float(scale), bool(relu), float(dropout_p), seed)
+
+
 class _AddNormFn(torch.autograd.Function):
     """HSTU residual stream step on grk_add_norm: s_new = bf16(s + y),
     x = LayerNorm(s_new) (x_dtype).  Returns (s_new, x), or x alone when y is

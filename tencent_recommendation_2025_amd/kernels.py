@@ -882,6 +882,39 @@ def norm_gate_bwd(gy, o, u, gamma, beta, stats, dropout_p=0.0, seed=0, dout=None
     return dout, du, dgamma, dbeta
 
 
+def emb_combine_fwd(a, b, pos, scale, relu=True, dropout_p=0.0, seed=0):
+    """y = dropout((act(a) + act(b)) * scale + pos) (grk_emb_combine_fwd): bf16 [N, D]
+    rows in, a contiguous bf16 [N, D] out.  b / pos may be None."""
+    _require_cuda(a, b, pos)
+    N, D = a.shape
+    y = torch.empty(N, D, dtype=torch.bfloat16, device=a.device)
+    (ap, al), (bp, bl), (pp, pl), (yp, yl) = [_bf16_rows(t, n, D) if t is not None else (None, 0)
+                                              for t, n in ((a, 'a'), (b, 'b'), (pos, 'pos'), (y, 'y'))]
+    hs, ds = _seed_parts(seed)
+    L.check(L.lib().grk_emb_combine_fwd(ap, al, bp, bl, pp, pl, float(scale), int(bool(relu)), N, D,
+                                        float(dropout_p), hs, _ptr(ds), yp, yl, L.stream_ptr(a.device)),
+            'grk_emb_combine_fwd')
+    return y
+
+
+def emb_combine_bwd(gy, a, b, scale, relu=True, dropout_p=0.0, seed=0, want=(True, True, True)):
+    """Gradients of emb_combine_fwd w.r.t. (a, b, pos) (grk_emb_combine_bwd); None where
+    not wanted (or b absent)."""
+    _require_cuda(gy, a, b)
+    N, D = gy.shape
+    dev = gy.device
+    outs = [torch.empty(N, D, dtype=torch.bfloat16, device=dev) if w and (i != 1 or b is not None) else None
+            for i, w in enumerate(want)]
+    rows = [_bf16_rows(t, n, D) if t is not None else (None, 0)
+            for t, n in ((gy, 'gy'), (a, 'a'), (b, 'b'), (outs[0], 'ga'), (outs[1], 'gb'), (outs[2], 'gpos'))]
+    (gp, gl), (ap, al), (bp, bl), (p0, l0), (p1, l1), (p2, l2) = rows
+    hs, ds = _seed_parts(seed)
+    L.check(L.lib().grk_emb_combine_bwd(gp, gl, ap, al, bp, bl, float(scale), int(bool(relu)), N, D,
+                                        float(dropout_p), hs, _ptr(ds), p0, l0, p1, l1, p2, l2, L.stream_ptr(dev)),
+            'grk_emb_combine_bwd')
+    return tuple(outs)
+
+
 # -------------------------------------------------------------- pair logits
 def _rows(t, name):
     if t is None:

@@ -561,10 +561,13 @@ class BaselineModel(torch.nn.Module):
         Wc = torch.cat(cols, 1)
         return F.pad(Wc, (0, width - Wc.shape[1]))
 
-    def _embed(self, seq, feature_array, mask=None, include_user=False, with_pos=False, role='seq', pos_idx=None):
+    def _embed(self, seq, feature_array, mask=None, include_user=False, with_pos=False, role='seq', pos_idx=None,
+               combine=None):
         """pos_idx (jagged rows): the position-embedding index of each row (t + 1 where
         the token is not padding) instead of the positional mode, which derives it from
-        the row's place in a [B, T] batch."""
+        the row's place in a [B, T] batch.  combine = (scale, dropout_p): return the
+        first block's input dropout((item + user) * scale + pos) itself (and None for
+        the position rows) where the grk path runs."""
         dev = self._device()
         seq = seq.to(dev, non_blocking=True).long()
         B, T = seq.shape
@@ -636,7 +639,7 @@ class BaselineModel(torch.nn.Module):
             specs = self._remap_specs(specs, role)
         blocks = list(G.feature_lookup(specs, N, col, tt, T, extras, splits))
 
-        def dnn(which, width, has_proj):
+        def dnn(which, width, has_proj, relu=True):
             a = blocks.pop(0)
             p = blocks.pop(0) if has_proj else None
             # one composed (and cast) dnn weight per forward: the seq-side and the
@@ -650,9 +653,18 @@ class BaselineModel(torch.nn.Module):
             if _grk_gemm_ok(a):
                 # ReLU in the GEMM's store; the projected rows' sum p (a column block of the
                 # gather buffer, read by nothing else) accumulated into where it lies
-                return G.linear(a, w, addend=p, relu=True, in_place=True)
-            return torch.relu(torch.addmm(p, a, w.t()) if p is not None else a @ w.t())
+                return G.linear(a, w, addend=p, relu=relu, in_place=True)
+            y = torch.addmm(p, a, w.t()) if p is not None else a @ w.t()
+            return torch.relu(y) if relu else y
 
+        if combine is not None and include_user and with_pos and _grk_gemm_ok(blocks[0]):
+            # log2feats' first-block input in one pass: the dnn ReLUs, the sum, the
+            # sqrt(d) scale, the position rows and the dropout (grk_emb_combine)
+            scale, p = combine
+            xi = dnn('item', wi, bool(item_p), relu=False)
+            xu = dnn('user', wu, bool(user_p), relu=False)
+            seed = dropout_seed(dev) if p > 0 else 0
+            return G.emb_combine(xi, xu, blocks.pop(0), scale, True, p, seed).view(B, T, d), None
         x = dnn('item', wi, bool(item_p))
         if include_user:
             x = x + dnn('user', wu, bool(user_p))
@@ -718,10 +730,13 @@ class BaselineModel(torch.nn.Module):
         the batch's jagged rows as [1, rows] (jagged.compact); the result is [1, rows, D]."""
         dev = self._device()
         B, T = log_seqs.shape
+        scale = self.item_emb.embedding_dim ** 0.5
+        p = self.emb_dropout.p if self.training else 0.0
         seqs, pos_rows = self._embed(log_seqs, seq_feature, mask=mask, include_user=True, with_pos=True,
-                                     pos_idx=pos_idx if jagged is not None else None)
-        seqs = seqs * self.item_emb.embedding_dim ** 0.5 + pos_rows.view(B, T, -1)
-        seqs = self.emb_dropout(seqs)
+                                     pos_idx=pos_idx if jagged is not None else None, combine=(scale, p))
+        if pos_rows is not None:
+            seqs = seqs * scale + pos_rows.view(B, T, -1)
+            seqs = self.emb_dropout(seqs)
         if jagged is not None:
             kw = dict(key_valid=jagged.key_valid, seq_range=jagged.seq_range, row_base=jagged.row_base)
         else:
