@@ -317,35 +317,54 @@ __global__ void __launch_bounds__(256) k_adamw_ranges(P* __restrict__ param, flo
 // the row (last[row] <- t) so duplicate ids replay it once; the skipped g = 0
 // steps (last, t] are replayed in registers with each step's hyper-parameters,
 // rounding bf16 parameters after every step exactly as a store/load would.
-// The replayed step range is wave-uniform, so the ring is read with scalar
-// loads and the slot advances without a per-step modulo.
+// The replayed step range is wave-uniform; the per-step constants of the whole
+// ring are computed once per workgroup into LDS (the replay loop then waits on
+// no scalar load per step) and the slot advances without a per-step modulo.
+// Full flush (ids == null): every row once, so the claim is a plain read and
+// store (no atomic) and the row's first vector is loaded before it.
+constexpr int kCatchupLds = 64;
 template <typename P, int NV>
 __global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, float* __restrict__ m,
                                                        float* __restrict__ v, int64_t num_rows, int dim,
                                                        int32_t* __restrict__ last, const int64_t* __restrict__ ids,
                                                        int64_t num_ids, const grk_adamw_hparams* __restrict__ ring,
                                                        int ring_len, int t_host, const int32_t* __restrict__ t_dev) {
+  __shared__ AdamStep steps[kCatchupLds];
+  const bool staged = ring_len <= kCatchupLds;
+  if (staged) {
+    for (int i = threadIdx.x; i < ring_len; i += blockDim.x) steps[i] = adam_step(ring[i]);
+    __syncthreads();
+  }
   const int t = resolve_t(t_host, t_dev);
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (w >= (ids ? num_ids : num_rows)) return;
   const int64_t row = ids ? ids[w] : w;
   if (row < 0 || row >= num_rows) return;
-  // A plain read first: later duplicates of a hot row see the claim without
-  // queueing on the atomic; the exchange still decides who replays.
-  if (__builtin_nontemporal_load(&last[row]) >= t) return;
+  float pv[NV], mv[NV], vv[NV];
+  int c = lane * NV;
   int from = 0;
-  if (lane == 0) from = atomicExch(&last[row], t);
-  from = __builtin_amdgcn_readfirstlane(__shfl(from, 0));
-  if (from >= t) return;
+  if (ids) {
+    // A plain read first: later duplicates of a hot row see the claim without
+    // queueing on the atomic; the exchange still decides who replays.
+    if (__builtin_nontemporal_load(&last[row]) >= t) return;
+    if (lane == 0) from = atomicExch(&last[row], t);
+    from = __builtin_amdgcn_readfirstlane(__shfl(from, 0));
+    if (from >= t) return;
+    if (c < dim) load_pmv<P, NV>(param + row * dim + c, m + row * dim + c, v + row * dim + c, pv, mv, vv);
+  } else {
+    if (c < dim) load_pmv<P, NV>(param + row * dim + c, m + row * dim + c, v + row * dim + c, pv, mv, vv);
+    from = __builtin_amdgcn_readfirstlane(last[row]);
+    if (from >= t) return;
+    if (lane == 0) last[row] = t;
+  }
   const int slot0 = (from + 1) % ring_len;
-  for (int c = lane * NV; c < dim; c += 64 * NV) {
-    float pv[NV], mv[NV], vv[NV];
+  for (bool first = true; c < dim; c += 64 * NV, first = false) {
     const int64_t off = row * dim + c;
-    load_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
+    if (!first) load_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
     int slot = slot0;
     for (int st = from + 1; st <= t; ++st) {
-      const AdamStep s = adam_step(ring[slot]);
+      const AdamStep s = staged ? steps[slot] : adam_step(ring[slot]);
       slot = slot + 1 == ring_len ? 0 : slot + 1;
 #pragma unroll
       for (int e = 0; e < NV; ++e) {
