@@ -368,6 +368,77 @@ def linear(x, weight, bias=None, addend=None, relu=False, in_place=False):
     return _LinearFn.apply(x, weight, bias, addend, bool(relu), bool(in_place))
 
 
+class _DnnWeightFn(torch.autograd.Function):
+    """The composed itemdnn / userdnn weight of the projection restatement
+    (model._dnn_weight): [d, width] = [blocks... | W_k [W_t | b_t] (mm features,
+    the emb_transform folded in) | b + sum_k W_k b_t | 0], cast once to `dtype`.
+
+    Forward: one cat + one mm per mm feature, one cat of every column block and
+    one cast; backward: one cast of the gradient, then views, plus one cat and
+    two mm per mm feature -- where autograd of the eager composition (cats,
+    pads, slices, their zero-filled backwards, autocast casts) ran ~25 kernels
+    for C2's two dnn weights.  fp32 arithmetic throughout (the eager form ran
+    the W_k [W_t | b_t] product under bf16 autocast)."""
+
+    @staticmethod
+    def forward(ctx, nblocks, nmm, width, dtype, *ts):
+        blocks, bias = ts[:nblocks], ts[nblocks]
+        mms = [ts[nblocks + 1 + 3 * i: nblocks + 4 + 3 * i] for i in range(nmm)]
+        d = bias.shape[0]
+        cols = [b.detach() for b in blocks]
+        bcol = bias.detach()[:, None]
+        ets = []
+        with torch.autocast(bias.device.type, enabled=False):
+            for Wk, Wt, bt in mms:
+                et = torch.cat([Wt.detach(), bt.detach()[:, None]], 1)
+                Mk = Wk.detach() @ et
+                cols.append(Mk[:, :-1])
+                bcol = bcol + Mk[:, -1:]
+                ets.append(et)
+            cols.append(bcol)
+            used = sum(c.shape[1] for c in cols)
+            if width > used:
+                cols.append(bias.new_zeros(d, width - used))
+            Wc = torch.cat(cols, 1)
+        out = Wc.to(dtype) if dtype != Wc.dtype else Wc
+        ctx.save_for_backward(*[m[0] for m in mms], *ets)
+        ctx.meta = (nblocks, nmm, [b.shape[1] for b in blocks], [m[1].shape[1] for m in mms],
+                    [b.dtype for b in blocks], bias.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        nblocks, nmm, bw, mmw, bdt, biasdt = ctx.meta
+        saved = ctx.saved_tensors
+        Wks, ets = saved[:nmm], saved[nmm:]
+        g32 = g.float()
+        grads, c = [], 0
+        for w, dt in zip(bw, bdt):
+            grads.append(g32[:, c:c + w].to(dt))
+            c += w
+        mm_cols = []
+        for w in mmw:
+            mm_cols.append((c, c + w))
+            c += w
+        gb = g32[:, c]
+        mm_grads = []
+        with torch.autocast(g.device.type, enabled=False):
+            for (c0, c1), Wk, et in zip(mm_cols, Wks, ets):
+                dM = torch.cat([g32[:, c0:c1], g32[:, c:c + 1]], 1)
+                dWk = dM @ et.t()
+                det = Wk.t() @ dM
+                mm_grads += [dWk, det[:, :-1], det[:, -1]]
+        return (None, None, None, None, *grads, gb.to(biasdt), *mm_grads)
+
+
+@_disable
+def dnn_weight(blocks, bias, mms, width, dtype):
+    """model._dnn_weight as one autograd node (_DnnWeightFn): blocks = the weight's
+    column blocks taken as they are, mms = [(W_k, emb_transform weight, bias)]."""
+    flat = [t for m in mms for t in m]
+    return _DnnWeightFn.apply(len(blocks), len(mms), int(width), dtype, *blocks, bias, *flat)
+
+
 class _EmbCombineFn(torch.autograd.Function):
     """seqs = dropout((act(a) + act(b)) * scale + pos) on grk_emb_combine (one pass
     each way); a / b the itemdnn / userdnn outputs before their ReLU when relu."""

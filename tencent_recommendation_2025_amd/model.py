@@ -539,12 +539,23 @@ class BaselineModel(torch.nn.Module):
             self._proj_off_cache[key] = off
         return torch.where(x > 0, x + off, 0)
 
-    def _dnn_weight(self, which, width):
+    def _dnn_weight(self, which, width, dtype=None):
         """[d, width] = [W_0 | W_f (direct features) | W_mm Wt | b' | 0] matching the
-        operand [rows | direct feature rows | mm | 1 | pad]."""
+        operand [rows | direct feature rows | mm | 1 | pad], in `dtype` (None: fp32)."""
         d = self.hidden_units
         dnn = self.itemdnn if which == 'item' else self.userdnn
         blk = self._weight_pieces(which)[0]
+        if dnn.bias.is_cuda and dtype is not None:
+            # one autograd node (functional.dnn_weight): the eager composition below
+            # costs ~25 small kernels per forward + backward
+            blocks = [blk[0]] + [blk[j] for _, j in self._direct_feats(which)]
+            mms = []
+            if which == 'item':
+                base = 1 + len(self.ITEM_SPARSE_FEAT) + len(self.ITEM_ARRAY_FEAT)
+                for j, k in enumerate(self.ITEM_EMB_FEAT):
+                    et = self.emb_transform[k]
+                    mms.append((blk[base + j], et.weight, et.bias))
+            return G.dnn_weight(blocks, dnn.bias, mms, width, dtype)
         cols, bias = [blk[0]], dnn.bias[:, None]
         cols += [blk[j] for _, j in self._direct_feats(which)]
         if which == 'item':
@@ -647,7 +658,8 @@ class BaselineModel(torch.nn.Module):
             key = ('w', which, width, a.dtype, self._fwd_id)
             w = self._proj_cache.get(key) if self._fwd_id is not None else None
             if w is None:
-                w = self._dnn_weight(which, width).to(a.dtype)
+                w = self._dnn_weight(which, width, a.dtype) if _grk_gemm_ok(a) else \
+                    self._dnn_weight(which, width).to(a.dtype)
                 if self._fwd_id is not None:
                     self._proj_cache[key] = w
             if _grk_gemm_ok(a):
