@@ -182,7 +182,7 @@ __global__ void __launch_bounds__(256) k_gather_wave(FeatArgs args, int64_t num_
 // payloads of one key are in occurrence order.
 // Keys are built in tiles of kKeyTile occurrences per 256-thread block (4 per
 // thread), the radix sort's tile: with hist0 the block also counts the first
-// digit (bits 0-7) of its keys into hist0[digit][tile], the sort's first
+// digit (the low bits0 bits) of its keys into hist0[digit][tile], the sort's first
 // histogram (grk_sort.hip), so that pass needs no launch of its own.
 // Blocks past key_blocks (first launch of a call only) instead zero the dense
 // output (16-byte words, grid-stride) and the unique-row count: the fill then
@@ -198,7 +198,8 @@ __global__ void __launch_bounds__(256) k_build_keys(LookupArgs la, int esize, co
                                                     int32_t T_len, int64_t num_rows, int64_t padding_idx,
                                                     unsigned* __restrict__ keys, unsigned long long* __restrict__ gptr,
                                                     int32_t* err_flag, unsigned key_blocks,
-                                                    unsigned* __restrict__ hist0, int ntiles, KeyFill fill) {
+                                                    unsigned* __restrict__ hist0, int ntiles, int bits0,
+                                                    KeyFill fill) {
   if (blockIdx.x >= key_blocks) {
     const int64_t nb = gridDim.x - key_blocks, t = (int64_t)(blockIdx.x - key_blocks) * blockDim.x + threadIdx.x;
     const int64_t stride = nb * blockDim.x;
@@ -206,9 +207,10 @@ __global__ void __launch_bounds__(256) k_build_keys(LookupArgs la, int esize, co
     if (fill.zero_count && t == 0) *fill.zero_count = 0;
     return;
   }
-  __shared__ unsigned cnt[256];
+  __shared__ unsigned cnt[2048];
+  const int nb0 = 1 << bits0;
   if (hist0) {
-    cnt[threadIdx.x] = 0;
+    for (int d = threadIdx.x; d < nb0; d += blockDim.x) cnt[d] = 0;
     __syncthreads();
   }
   const int64_t end = la.occ_off[la.num];
@@ -231,11 +233,11 @@ __global__ void __launch_bounds__(256) k_build_keys(LookupArgs la, int esize, co
     }
     keys[o] = key;
     gptr[o] = (unsigned long long)((const char*)L.grad + (n * L.grad_ld + L.grad_col) * esize);
-    if (hist0) atomicAdd(&cnt[key & 255u], 1u);
+    if (hist0) atomicAdd(&cnt[key & (unsigned)(nb0 - 1)], 1u);
   }
   if (hist0) {
     __syncthreads();
-    hist0[(int64_t)threadIdx.x * ntiles + blockIdx.x] = cnt[threadIdx.x];
+    for (int d = threadIdx.x; d < nb0; d += blockDim.x) hist0[(int64_t)d * ntiles + blockIdx.x] = cnt[d];
   }
 }
 
@@ -1089,6 +1091,7 @@ __global__ void __launch_bounds__(kTinyThreads) k_bwd_tiny(LookupArgs la, int es
 // Stable radix sort of (row key, gradient-row address) pairs (grk_sort.hip).
 size_t sort_pairs_workspace(int64_t n);
 unsigned* sort_pairs_hist0(void* ws);
+int sort_digit_bits(int end_bit);
 int sort_pairs(unsigned* k0, unsigned long long* v0, unsigned* k1, unsigned long long* v1, int64_t n, int end_bit,
                void* ws, unsigned** kres, unsigned long long** vres, hipStream_t s, bool hist0_ready);
 // Segment index of every sorted entry (inclusive count of row heads).
@@ -1347,6 +1350,9 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   // one key-build launch (<= kLookupsPerLaunch lookups): it also counts the sort's first digit
   const bool one_launch = num_lookups <= kLookupsPerLaunch;
   const int ntiles = (int)((total + kKeyTile - 1) / kKeyTile);
+  unsigned end_bit = 1;
+  while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
+  const int bits0 = sort_digit_bits((int)end_bit);
   int64_t occ = 0;
   bool first_launch = true;
   for (int first = 0; first < num_lookups; first += kLookupsPerLaunch) {
@@ -1374,16 +1380,14 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
     unsigned* h0 = one_launch ? sort_pairs_hist0(ws.sort_tmp) : nullptr;
     if (itype == GRK_I64)
       k_build_keys<int64_t><<<g + gz, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
-                                                 ws.gptr_in, err_flag, g, h0, ntiles, fill);
+                                                 ws.gptr_in, err_flag, g, h0, ntiles, bits0, fill);
     else
       k_build_keys<int32_t><<<g + gz, B, 0, s>>>(la, esize, token_type, seq_len, num_rows, padding_idx, ws.keys_in,
-                                                 ws.gptr_in, err_flag, g, h0, ntiles, fill);
+                                                 ws.gptr_in, err_flag, g, h0, ntiles, bits0, fill);
     GRK_LAUNCH_CHECK();
     first_launch = false;
   }
   const int g = (int)((total + B - 1) / B);
-  unsigned end_bit = 1;
-  while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
   unsigned* skeys;
   unsigned long long* sgptr;
   {

@@ -7,17 +7,23 @@
 //
 // rocprim::radix_sort_pairs took ~15 launches per call at these sizes (73
 // launches, ~0.5 ms per C2 training step over five calls).  Here a pass per
-// 8-bit digit is three launches:
+// digit is three launches:
 //   k_sort_hist    per 1024-key tile: digit counts -> hist[digit][tile]
 //   k_sort_scan    one workgroup per digit: exclusive scan of the digit's
 //                  tile counts, and the digit's total (the scatter's prologue
-//                  prefixes the 256 totals)
+//                  prefixes the totals)
 //   k_sort_scatter per tile, 4 rounds of 256 keys in index order: a key's
 //                  slot = its (digit, tile) base + the keys of its digit in
 //                  earlier rounds, earlier waves of this round, and lower
-//                  lanes of its wave (wave ballots over the 8 digit bits)
+//                  lanes of its wave (wave ballots over the digit bits)
 // so the order among equal digits is the input order: stable, deterministic,
 // and (a stable sort being unique) the same output as rocprim's.
+//
+// Digits are up to 11 bits wide, as few passes as the key width allows
+// (sort_digit_bits): the 1M-row tables' 20-bit keys take two passes of 10
+// bits where 8-bit digits took three (round 4: one pass = 3 launches less
+// per call).  Per-wave digit counts of a round live in LDS tagged with the
+// round, so no per-round clearing of 4 x 2048 counters.
 //
 // The first pass's histogram can come from the caller (the embedding
 // backward counts digit 0 inside its key-build kernel: hist0_ready).  Round 4
@@ -27,25 +33,35 @@
 #include "grk_common.h"
 
 namespace grk {
+
+// Width of every digit of a sort of end_bit-bit keys: as few passes of <= 11
+// bits as cover them, split evenly.
+int sort_digit_bits(int end_bit) {
+  if (end_bit <= 8) return end_bit < 1 ? 1 : end_bit;
+  const int passes = (end_bit + 10) / 11;
+  return (end_bit + passes - 1) / passes;
+}
+
 namespace {
 
-constexpr int kSortBits = 8, kSortBins = 1 << kSortBits;
+constexpr int kSortMaxBits = 11, kSortMaxBins = 1 << kSortMaxBits;
 constexpr int kSortThreads = 256, kSortRounds = 4, kSortTile = kSortThreads * kSortRounds;
 
 __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const unsigned* __restrict__ keys, int64_t n, int shift,
-                                                            unsigned* __restrict__ hist, int ntiles) {
-  __shared__ unsigned cnt[kSortBins];
-  const int tid = threadIdx.x, tile = blockIdx.x;
-  cnt[tid] = 0;
+                                                            int bits, unsigned* __restrict__ hist, int ntiles) {
+  __shared__ unsigned cnt[kSortMaxBins];
+  const int tid = threadIdx.x, tile = blockIdx.x, nbins = 1 << bits;
+  const unsigned mask = (unsigned)nbins - 1u;
+  for (int d = tid; d < nbins; d += kSortThreads) cnt[d] = 0;
   __syncthreads();
   const int64_t t0 = (int64_t)tile * kSortTile;
 #pragma unroll 4
   for (int r = 0; r < kSortRounds; ++r) {
     const int64_t i = t0 + r * kSortThreads + tid;
-    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & (kSortBins - 1)], 1u);
+    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & mask], 1u);
   }
   __syncthreads();
-  hist[(int64_t)tid * ntiles + tile] = cnt[tid];
+  for (int d = tid; d < nbins; d += kSortThreads) hist[(int64_t)d * ntiles + tile] = cnt[d];
 }
 
 // Per digit (one workgroup each): in-place exclusive scan of the digit's tile
@@ -74,67 +90,91 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_scan(unsigned* __restrict
   if (t == 0) tot[blockIdx.x] = carry;
 }
 
+// Exclusive scan of v[0 .. nbins) in LDS in place (nbins a power of two
+// <= kSortMaxBins; each thread owns nbins / 256 consecutive entries, or one).
+__device__ __forceinline__ void block_exclusive_scan(unsigned* v, int nbins, unsigned* part) {
+  const int tid = threadIdx.x;
+  const int per = nbins > kSortThreads ? nbins / kSortThreads : 1;
+  const int b0 = tid * per;
+  unsigned s = 0;
+  if (b0 < nbins)
+    for (int j = 0; j < per; ++j) s += v[b0 + j];
+  part[tid] = s;
+  __syncthreads();
+  for (int off = 1; off < kSortThreads; off <<= 1) {
+    const unsigned u = tid >= off ? part[tid - off] : 0u;
+    __syncthreads();
+    part[tid] += u;
+    __syncthreads();
+  }
+  unsigned run = part[tid] - s;
+  if (b0 < nbins)
+    for (int j = 0; j < per; ++j) {
+      const unsigned x = v[b0 + j];
+      v[b0 + j] = run;
+      run += x;
+    }
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(kSortThreads) k_sort_scatter(const unsigned* __restrict__ kin,
                                                                const unsigned long long* __restrict__ vin,
                                                                unsigned* __restrict__ kout,
                                                                unsigned long long* __restrict__ vout, int64_t n,
-                                                               int shift, const unsigned* __restrict__ hist,
+                                                               int shift, int bits, const unsigned* __restrict__ hist,
                                                                int ntiles, const unsigned* __restrict__ tot) {
   constexpr int NW = kSortThreads / 64;
-  __shared__ unsigned base[kSortBins];
-  __shared__ unsigned wcnt[NW][kSortBins];
-  const int tid = threadIdx.x, tile = blockIdx.x, w = tid >> 6, lane = tid & 63;
+  __shared__ unsigned base[kSortMaxBins];
+  __shared__ unsigned part[kSortThreads];
+  // wcnt[q][d] = (round + 1) << 24 | keys of digit d in wave q this round; other tags read as 0
+  __shared__ unsigned wcnt[NW][kSortMaxBins];
+  const int tid = threadIdx.x, tile = blockIdx.x, w = tid >> 6, lane = tid & 63, nbins = 1 << bits;
+  const unsigned mask = (unsigned)nbins - 1u;
   // base[d] = keys of smaller digits (exclusive scan of the totals) + this digit in earlier tiles
-  const unsigned td = tot[tid];
-  base[tid] = td;
-  __syncthreads();
-  for (int off = 1; off < kSortBins; off <<= 1) {
-    const unsigned u = tid >= off ? base[tid - off] : 0u;
-    __syncthreads();
-    base[tid] += u;
-    __syncthreads();
+  for (int d = tid; d < nbins; d += kSortThreads) {
+    base[d] = tot[d];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) wcnt[q][d] = 0;
   }
-  const unsigned dpre = base[tid] - td;
   __syncthreads();
-  base[tid] = dpre + hist[(int64_t)tid * ntiles + tile];
+  block_exclusive_scan(base, nbins, part);
+  for (int d = tid; d < nbins; d += kSortThreads) base[d] += hist[(int64_t)d * ntiles + tile];
   const unsigned long long lt = (1ull << lane) - 1ull;
   const int64_t t0 = (int64_t)tile * kSortTile;
   for (int r = 0; r < kSortRounds; ++r) {
     const int64_t i = t0 + r * kSortThreads + tid;
     const bool ok = i < n;
-#pragma unroll
-    for (int q = 0; q < NW; ++q) wcnt[q][tid] = 0;
     unsigned key = 0;
     unsigned long long val = 0;
     if (ok) {
       key = kin[i];
       val = vin[i];
     }
-    const unsigned d = (key >> shift) & (kSortBins - 1);
+    const unsigned d = (key >> shift) & mask;
     // lanes of this wave holding a valid key with the same digit
     unsigned long long peers = __ballot(ok);
-#pragma unroll
-    for (int bit = 0; bit < kSortBits; ++bit) {
+    for (int bit = 0; bit < bits; ++bit) {
       const bool set = (d >> bit) & 1u;
       const unsigned long long m = __ballot(set);
       peers &= set ? m : ~m;
     }
-    __syncthreads();  // wcnt zeroed (and the previous round's base update visible)
-    if (ok && (peers & lt) == 0) wcnt[w][d] = (unsigned)__popcll(peers);  // the digit's lowest lane
-    __syncthreads();
+    const unsigned tag = (unsigned)(r + 1) << 24;
+    const bool leader = ok && (peers & lt) == 0;  // the digit's lowest lane in this wave
+    const unsigned cnt = (unsigned)__popcll(peers);
+    if (leader) wcnt[w][d] = tag | cnt;
+    __syncthreads();  // this round's counts (and the previous round's base update) visible
     if (ok) {
       unsigned pos = base[d] + (unsigned)__popcll(peers & lt);
 #pragma unroll
-      for (int q = 0; q < NW; ++q)
-        if (q < w) pos += wcnt[q][d];
+      for (int q = 0; q < NW; ++q) {
+        const unsigned c = wcnt[q][d];
+        if (q < w && (c & 0xFF000000u) == tag) pos += c & 0x00FFFFFFu;
+      }
       kout[pos] = key;
       vout[pos] = val;
     }
     __syncthreads();  // every slot of this round computed from the old base
-    unsigned add = 0;
-#pragma unroll
-    for (int q = 0; q < NW; ++q) add += wcnt[q][tid];
-    base[tid] += add;
+    if (leader) atomicAdd(&base[d], cnt);
   }
 }
 
@@ -222,11 +262,12 @@ int head_positions(const unsigned* keys, int64_t n, unsigned sentinel, int* pos,
 // Workspace of sort_pairs: the digit histogram (digit-major) and the digit totals.
 size_t sort_pairs_workspace(int64_t n) {
   const int64_t ntiles = (n + kSortTile - 1) / kSortTile;
-  return ((size_t)kSortBins * (size_t)(ntiles > 0 ? ntiles : 1) + kSortBins) * sizeof(unsigned);
+  return ((size_t)kSortMaxBins * (size_t)(ntiles > 0 ? ntiles : 1) + kSortMaxBins) * sizeof(unsigned);
 }
 
 // The first pass's histogram buffer inside a sort_pairs workspace (a caller
-// that counts digit 0 itself writes hist[digit][tile] there, kSortTile keys per tile).
+// that counts digit 0 itself -- the low sort_digit_bits(end_bit) bits --
+// writes hist[digit][tile] there, kSortTile keys per tile).
 unsigned* sort_pairs_hist0(void* ws) { return (unsigned*)ws; }
 
 // Sorts (k0, v0) by the low end_bit bits of the keys, stably, ping-ponging
@@ -243,21 +284,22 @@ int sort_pairs(unsigned* k0, unsigned long long* v0, unsigned* k1, unsigned long
   const int64_t ntiles64 = (n + kSortTile - 1) / kSortTile;
   GRK_CHECK_ARG(ntiles64 < (1 << 24), "too many tiles");
   const int ntiles = (int)ntiles64;
+  const int bits = sort_digit_bits(end_bit), nbins = 1 << bits;
   unsigned* hist = (unsigned*)ws;
-  unsigned* tot = hist + (size_t)kSortBins * ntiles;
+  unsigned* tot = hist + (size_t)kSortMaxBins * ntiles;
   unsigned* kin = k0;
   unsigned* kout = k1;
   unsigned long long* vin = v0;
   unsigned long long* vout = v1;
   int pass = 0;
-  for (int shift = 0; shift < end_bit; shift += kSortBits, ++pass) {
+  for (int shift = 0; shift < end_bit; shift += bits, ++pass) {
     if (pass > 0 || !hist0_ready) {
-      k_sort_hist<<<ntiles, kSortThreads, 0, s>>>(kin, n, shift, hist, ntiles);
+      k_sort_hist<<<ntiles, kSortThreads, 0, s>>>(kin, n, shift, bits, hist, ntiles);
       GRK_LAUNCH_CHECK();
     }
-    k_sort_scan<<<kSortBins, kSortThreads, 0, s>>>(hist, ntiles, tot);
+    k_sort_scan<<<nbins, kSortThreads, 0, s>>>(hist, ntiles, tot);
     GRK_LAUNCH_CHECK();
-    k_sort_scatter<<<ntiles, kSortThreads, 0, s>>>(kin, vin, kout, vout, n, shift, hist, ntiles, tot);
+    k_sort_scatter<<<ntiles, kSortThreads, 0, s>>>(kin, vin, kout, vout, n, shift, bits, hist, ntiles, tot);
     GRK_LAUNCH_CHECK();
     unsigned* tk = kin;
     kin = kout;
@@ -288,7 +330,9 @@ extern "C" int grk_sort_pairs(const uint32_t* keys_in, const uint64_t* vals_in, 
   hipStream_t s = (hipStream_t)stream;
   // passes alternate out <-> tmp, starting from the caller's input: the pass
   // count's parity decides which buffer starts, so the result lands in out
-  const int passes = (end_bit + kSortBits - 1) / kSortBits;
+  GRK_CHECK_ARG(end_bit >= 1 && end_bit <= 32, "end_bit must be in [1, 32]");
+  const int bits = sort_digit_bits(end_bit);
+  const int passes = (end_bit + bits - 1) / bits;
   unsigned* a = (unsigned*)(passes % 2 ? keys_tmp : keys_out);
   unsigned long long* va = (unsigned long long*)(passes % 2 ? vals_tmp : vals_out);
   unsigned* b = (unsigned*)(passes % 2 ? keys_out : keys_tmp);

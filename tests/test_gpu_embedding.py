@@ -347,12 +347,13 @@ def test_backward_chunked_bf16_dense_is_the_rounded_fp32_result(K):
 
 # ------------------------------------------------ occurrence sort (grk_sort) --
 @pytest.mark.parametrize('n,end_bit,card', [(1, 1, 2), (4095, 8, 200), (4097, 9, 300), (70001, 16, 40000),
-                                            (200000, 21, 1000001), (150000, 21, 10), (33333, 32, 1 << 31)])
+                                            (200000, 21, 1000001), (150000, 21, 10), (33333, 32, 1 << 31),
+                                            (5000, 11, 2048), (100000, 20, 1000001), (43008, 20, 30000)])
 def test_sort_pairs_is_stable_and_exact(n, end_bit, card):
     """grk_sort_pairs (the embedding backward's occurrence grouping) against
     numpy's stable argsort: keys and values identical, ties in input order --
     hot keys (card 10: every key repeated ~15k times), tile-boundary sizes,
-    1- to 32-bit keys."""
+    1- to 32-bit keys: one digit of 1-11 bits, two of 8 / 10 / 11, three of 11."""
     from tencent_recommendation_2025_amd import kernels as K
     rng = np.random.default_rng(n + end_bit)
     keys = rng.integers(0, min(card, 1 << end_bit), n, dtype=np.int64).astype(np.uint32)
