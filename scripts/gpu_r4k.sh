@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 4, call k: PMC traffic of every bench roofline (profiles/r4_pmc_*), then an
+# A/B of prepared builds (abtest/: chunked-backward chunk 128, wave pipe 32, attention
+# 1/n folded into the dK/dV store scales, + time-bias-free instantiation; norm-gate /
+# add-norm backward on 1024 workgroups instead of 512) against the
+# product build, two rounds each, round-robin.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r4k
+mkdir -p $O
+timeout -k 10 900 bash scripts/gpu_pmc_round.sh r4 > $O/pmc.log 2>&1 || { echo "pmc rc=$?" >> $O/summary.txt; exit 1; }
+echo "pmc ok" >> $O/summary.txt
+timeout -k 10 900 bash scripts/gpu_ab.sh 2 "tencent_recommendation_2025_amd/libgrk.so abtest/libgrk_ch128.so abtest/libgrk_pipe32.so abtest/libgrk_fold.so abtest/libgrk_foldtb.so abtest/libgrk_ngb1024.so" > $O/ab.log 2>&1
+echo "ab rc=$?" >> $O/summary.txt
+cp gpurun_out/ab.txt $O/ab.txt 2>/dev/null
+cat $O/ab.txt

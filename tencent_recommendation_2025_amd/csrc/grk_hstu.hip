@@ -17,7 +17,11 @@
 namespace grk {
 
 constexpr int kNgWaves = 4;        // waves per workgroup
-constexpr int kNgBwdBlocks = 512;  // fixed backward grid -> fixed reduction order
+// fixed backward grid -> fixed reduction order (GRK_NG_BWD_BLOCKS: A/B builds)
+#ifndef GRK_NG_BWD_BLOCKS
+#define GRK_NG_BWD_BLOCKS 512
+#endif
+constexpr int kNgBwdBlocks = GRK_NG_BWD_BLOCKS;
 
 struct NGParams {
   const bf16_t* o; int64_t ldo;
