@@ -107,25 +107,59 @@ def compact(batch, jag, with_positions=True):
     tensors (one grk_gather_rows launch for all of them): (seq, pos, neg, tt, ntt, nat,
     seq_feat, pos_feat, neg_feat) and, with_positions, the position-embedding index
     (t + 1 where seq != 0, model/BaseLine/model.py:326-328) as an 11th field.  A
-    10th field (event times) stays [B, T]: the attention kernels read it per (b, t)."""
+    10th field (event times) stays [B, T]: the attention kernels read it per (b, t).
+    pos / neg ids and each pos / neg feature of one shape land in the two halves of
+    one buffer (model.feat2emb_pair stacks them without a copy)."""
     B, T, cap = jag.B, jag.T, jag.capacity
     N = B * T
     pairs, out = [], []
 
-    def take(t):
-        if t is None:
-            return None
+    def source(t):
         src = _as_rows(t, N)
         if src.dtype == torch.bool or src.element_size() * (src[0].numel() if src.dim() > 1 else 1) % 4:
             src = src.to(torch.int32)
-        dst = torch.empty((cap,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        return src
+
+    def take(t, dst=None):
+        if t is None:
+            return None
+        src = source(t)
+        if dst is None:
+            dst = torch.empty((cap,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
         pairs.append((src, dst))
         return dst.unsqueeze(0)
 
-    for x in batch[:6]:
-        out.append(take(x))
-    for f in batch[6:9]:
-        out.append(None if f is None else {k: take(v) for k, v in f.items()})
+    def take_pair(a, b):
+        """Two tensors of one shape and dtype into the halves of ONE [2 cap, ...] buffer:
+        the model's pos / neg stacking (feat2emb_pair) is then a view, not a copy."""
+        if a is None or b is None:
+            return take(a), take(b)
+        sa, sb = source(a), source(b)
+        if sa.dtype != sb.dtype or sa.shape[1:] != sb.shape[1:]:
+            return take(a), take(b)
+        buf = torch.empty((2 * cap,) + tuple(sa.shape[1:]), dtype=sa.dtype, device=sa.device)
+        pairs.append((sa, buf[:cap]))
+        pairs.append((sb, buf[cap:]))
+        return buf[:cap].unsqueeze(0), buf[cap:].unsqueeze(0)
+
+    seq_o = take(batch[0])
+    pos_o, neg_o = take_pair(batch[1], batch[2])
+    out += [seq_o, pos_o, neg_o] + [take(x) for x in batch[3:6]]
+    sf, pf, nf = batch[6:9]
+    out.append(None if sf is None else {k: take(v) for k, v in sf.items()})
+    if pf is not None and nf is not None:
+        po, no = {}, {}
+        for k, v in pf.items():
+            if k in nf:
+                po[k], no[k] = take_pair(v, nf[k])
+            else:
+                po[k] = take(v)
+        for k, v in nf.items():
+            if k not in no:
+                no[k] = take(v)
+        out += [po, no]
+    else:
+        out += [None if f is None else {k: take(v) for k, v in f.items()} for f in (pf, nf)]
     out.append(batch[9] if len(batch) > 9 else None)
     if with_positions:
         seq = batch[0]

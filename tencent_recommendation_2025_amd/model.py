@@ -721,7 +721,7 @@ class BaselineModel(torch.nn.Module):
         fp = self._feats(pos_feature, fids, B, T)
         fn = self._feats(neg_feature, fids, B, T)
         feats = _stack_pairs(fp, fn, fids)
-        seq2 = torch.cat([pos, neg], 0)
+        seq2 = _cat0(pos, neg)
         if self._remaps is not None:  # row-sharded tables: the stacked ids read the rows fetched for pos and neg
             for name in ('item_emb',):
                 a = self._remaps.get((name, 'pos', L.IDX_PLAIN))
@@ -840,13 +840,32 @@ class BaselineModel(torch.nn.Module):
         save_emb(np.array(retrieval_ids, dtype=np.uint64).reshape(-1, 1), Path(save_path, 'id.u64bin'))
 
 
+def _adjacent(a, b):
+    """torch.cat([a, b], 0) as a view when b starts where a ends in one storage
+    (jagged.compact lays pos / neg out that way), else None."""
+    if a.dtype != b.dtype or a.shape[1:] != b.shape[1:] or not (a.is_contiguous() and b.is_contiguous()) \
+            or a.device != b.device or a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr() \
+            or b.data_ptr() != a.data_ptr() + a.numel() * a.element_size():
+        return None
+    return a.as_strided((a.shape[0] + b.shape[0],) + tuple(a.shape[1:]), a.stride(), a.storage_offset())
+
+
+def _cat0(a, b):
+    v = _adjacent(a, b)
+    return v if v is not None else torch.cat([a, b], 0)
+
+
 def _stack_pairs(fa, fb, fids):
     """{k: _stack_padded(fa[k], fb[k])} for every feature with (at most) one
     zero-fill and one multi-tensor copy kernel per dtype instead of a cat (and
-    pads) per feature."""
+    pads) per feature; no copy at all for pairs already adjacent in memory."""
     out, groups, pad = {}, {}, []
     for k in fids:
         a, b = fa[k], fb[k]
+        v = _adjacent(a, b)
+        if v is not None:
+            out[k] = v
+            continue
         if a.dim() != b.dim() or a.shape[0] != b.shape[0] or a.shape[1:2] != b.shape[1:2] or a.dtype != b.dtype \
                 or (a.dim() == 3 and a.is_floating_point() and a.shape[2] != b.shape[2]) or a.dim() > 3:
             out[k] = _stack_padded(a, b)

@@ -435,3 +435,29 @@ def test_packed_batches_replay_equals_unpacked():
     assert torch.equal(runs[0][0], runs[1][0])
     for k in runs[0][1]:
         assert torch.equal(runs[0][1][k], runs[1][1][k]), k
+
+
+def test_compact_lays_pos_neg_pairs_out_adjacent():
+    """jagged.compact puts pos / neg ids and each pos / neg feature of one shape into
+    the halves of one buffer (round 4), so feat2emb_pair stacks them as a view: the
+    stacked tensors share the buffer and equal the copying stack."""
+    from tencent_recommendation_2025_amd import jagged as J
+    from tencent_recommendation_2025_amd import model as Mm
+    from tencent_recommendation_2025_amd import synthetic as S
+    cfg = S.SyntheticConfig(batch_size=8, maxlen=40, num_items=500, num_users=50, min_len=4)
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    batch = S.make_batch(cfg, gen, DEV)
+    tt = batch[3]
+    jag = J.layout(tt, J.capacity_for(J.span_rows(tt), 64), batch[4])
+    jb = J.compact(batch, jag)
+    pos, neg = jb[1], jb[2]
+    v = Mm._adjacent(pos.reshape(1, -1), neg.reshape(1, -1))
+    assert v is not None and torch.equal(Mm._cat0(pos, neg), torch.cat([pos, neg], 0))
+    pf, nf = jb[7], jb[8]
+    fids = sorted(set(pf) & set(nf))
+    assert fids
+    st = Mm._stack_pairs(pf, nf, fids)
+    for k in fids:
+        assert torch.equal(st[k], torch.cat([pf[k], nf[k]], 0)), k
+        if pf[k].shape[1:] == nf[k].shape[1:] and pf[k].dtype == nf[k].dtype:
+            assert st[k].data_ptr() == pf[k].data_ptr(), k     # a view, no copy

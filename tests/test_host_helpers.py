@@ -307,3 +307,18 @@ def test_pack_batch_one_arena_same_values():
     for a, b in zip(T._tensors(st), T._tensors(b2)):
         assert torch.equal(a, b)
     assert isinstance(st[6], dict) and set(st[6]) == set(b2[6])
+
+
+def test_stack_pairs_is_a_view_for_adjacent_halves():
+    """model._stack_pairs / _cat0 (round 4): pos / neg tensors that are the two
+    halves of one buffer stack as a view of it; anything else is copied as before."""
+    from tencent_recommendation_2025_amd import model as Mm
+    buf = torch.arange(2 * 3 * 5 * 4).reshape(6, 5, 4)
+    a, b = buf[:3], buf[3:]
+    other = buf[3:].clone()
+    st = Mm._stack_pairs({'x': a, 'y': a}, {'x': b, 'y': other}, ['x', 'y'])
+    assert st['x'].data_ptr() == buf.data_ptr() and torch.equal(st['x'], buf)
+    assert st['y'].data_ptr() != buf.data_ptr() and torch.equal(st['y'], buf)
+    assert Mm._adjacent(b, a) is None                       # wrong order
+    assert Mm._adjacent(buf[:2], buf[3:]) is None           # a gap
+    assert torch.equal(Mm._cat0(buf[:2], buf[3:]), torch.cat([buf[:2], buf[3:]]))
