@@ -78,14 +78,39 @@ class FlashMultiHeadAttention(torch.nn.Module):
         return _linear(o.view(query.shape), self.out_linear.weight, self.out_linear.bias), None
 
 
+# The dropout seeds of one forward, drawn in ONE launch (seed_pool): dropout_seed
+# hands out [1] views of it in call order.
+_SEED_POOL = {'buf': None, 'next': 0}
+
+
+@contextlib.contextmanager
+def seed_pool(device, n):
+    """Within the block, dropout_seed(device) takes its seeds from n values drawn in
+    one torch.randint launch (then falls back to one launch per seed)."""
+    if device.type != 'cuda' or n <= 0:
+        yield
+        return
+    prev = dict(_SEED_POOL)
+    _SEED_POOL['buf'] = torch.randint(0, 2 ** 62, (int(n),), device=device, dtype=torch.int64)
+    _SEED_POOL['next'] = 0
+    try:
+        yield
+    finally:
+        _SEED_POOL.update(prev)
+
+
 def dropout_seed(device):
     """The grk dropout seed of one launch: an int64 [1] drawn on the device from
     torch's generator and read by the kernels when they run.  No host round
     trip, and a step replayed from a HIP graph draws a fresh one every replay
     (torch registers its generator with the graph), exactly as the eager step
-    would draw it."""
+    would draw it.  Inside seed_pool: the pool's next value."""
     if device.type != 'cuda':
         return int(torch.randint(0, 2 ** 62, (1,)).item())
+    buf, i = _SEED_POOL['buf'], _SEED_POOL['next']
+    if buf is not None and buf.device == device and i < buf.numel():
+        _SEED_POOL['next'] = i + 1
+        return buf[i:i + 1]
     return torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
 
 
@@ -803,11 +828,15 @@ class BaselineModel(torch.nn.Module):
 
     @contextlib.contextmanager
     def _shared_projections(self):
-        """One set of projected feature tables for every feat2emb of this forward."""
+        """One set of projected feature tables for every feat2emb of this forward, and
+        its dropout seeds drawn in one launch (training only: the first-block input and
+        one per attention layer)."""
         self._fwd_id = object()
         self._proj_cache = {}
+        n = len(self.attention_layers) + 1 if self.training and self.emb_dropout.p > 0 else 0
         try:
-            yield
+            with seed_pool(self._device(), n):
+                yield
         finally:
             self._fwd_id = None
             self._proj_cache = {}
