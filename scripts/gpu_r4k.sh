@@ -11,6 +11,10 @@ O=gpurun_out/r4k
 mkdir -p $O
 timeout -k 10 900 bash scripts/gpu_pmc_round.sh r4 > $O/pmc.log 2>&1 || { echo "pmc rc=$?" >> $O/summary.txt; exit 1; }
 echo "pmc ok" >> $O/summary.txt
+# the N > 1 code path at world 1 (RCCL, row-sharded tables, jagged rows) beside the fused step
+timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+  --master-port 29613 bench.py --sharded 1 --cpu-baseline 0 --roofline-reps 1 > $O/bench_sharded1.json 2> $O/bench_sharded1.err
+echo "sharded1 rc=$?" >> $O/summary.txt
 timeout -k 10 900 bash scripts/gpu_ab.sh 2 "tencent_recommendation_2025_amd/libgrk.so abtest/libgrk_ch128.so abtest/libgrk_pipe32.so abtest/libgrk_fold.so abtest/libgrk_foldtb.so abtest/libgrk_ngb1024.so" > $O/ab.log 2>&1
 echo "ab rc=$?" >> $O/summary.txt
 cp gpurun_out/ab.txt $O/ab.txt 2>/dev/null
