@@ -14,7 +14,10 @@ echo "pmc ok" >> $O/summary.txt
 # the N > 1 code path at world 1 (RCCL, row-sharded tables, jagged rows) beside the fused step
 timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
   --master-port 29613 bench.py --sharded 1 --cpu-baseline 0 --roofline-reps 1 > $O/bench_sharded1.json 2> $O/bench_sharded1.err
-echo "sharded1 rc=$?" >> $O/summary.txt
+rc=$?; echo "sharded1 rc=$rc" >> $O/summary.txt
+if grep -Eqi 'illegal memory access|memory access fault|HSA_STATUS_ERROR|GPU Hang' $O/bench_sharded1.err || [ $rc -gt 1 ]; then
+  echo "sharded1 failed -- stopping" >> $O/summary.txt; exit 3
+fi
 timeout -k 10 900 bash scripts/gpu_ab.sh 2 "tencent_recommendation_2025_amd/libgrk.so abtest/libgrk_ch128.so abtest/libgrk_pipe32.so abtest/libgrk_fold.so abtest/libgrk_foldtb.so abtest/libgrk_ngb1024.so" > $O/ab.log 2>&1
 echo "ab rc=$?" >> $O/summary.txt
 cp gpurun_out/ab.txt $O/ab.txt 2>/dev/null
