@@ -3,7 +3,7 @@
 # A/B of prepared builds (abtest/: chunked-backward chunk 128, wave pipe 32, attention
 # 1/n folded into the dK/dV store scales, + time-bias-free instantiation; norm-gate /
 # add-norm backward on 1024 workgroups instead of 512) against the
-# product build, two rounds each, round-robin.
+# product build, one run each.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -18,7 +18,7 @@ rc=$?; echo "sharded1 rc=$rc" >> $O/summary.txt
 if grep -Eqi 'illegal memory access|memory access fault|HSA_STATUS_ERROR|GPU Hang' $O/bench_sharded1.err || [ $rc -gt 1 ]; then
   echo "sharded1 failed -- stopping" >> $O/summary.txt; exit 3
 fi
-timeout -k 10 900 bash scripts/gpu_ab.sh 2 "tencent_recommendation_2025_amd/libgrk.so abtest/libgrk_ch128.so abtest/libgrk_pipe32.so abtest/libgrk_fold.so abtest/libgrk_foldtb.so abtest/libgrk_ngb1024.so" > $O/ab.log 2>&1
+timeout -k 10 900 bash scripts/gpu_ab.sh 1 "tencent_recommendation_2025_amd/libgrk.so abtest/libgrk_ch128.so abtest/libgrk_pipe32.so abtest/libgrk_fold.so abtest/libgrk_foldtb.so abtest/libgrk_ngb1024.so" > $O/ab.log 2>&1
 echo "ab rc=$?" >> $O/summary.txt
 cp gpurun_out/ab.txt $O/ab.txt 2>/dev/null
 cat $O/ab.txt
