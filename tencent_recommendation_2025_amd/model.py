@@ -87,7 +87,7 @@ _SEED_POOL = {'buf': None, 'next': 0}
 def seed_pool(device, n):
     """Within the block, dropout_seed(device) takes its seeds from n values drawn in
     one torch.randint launch (then falls back to one launch per seed)."""
-    if device.type != 'cuda' or n <= 0:
+    if device.type != 'cuda' or n <= 0 or torch.compiler.is_compiling():
         yield
         return
     prev = dict(_SEED_POOL)
@@ -108,7 +108,7 @@ def dropout_seed(device):
     if device.type != 'cuda':
         return int(torch.randint(0, 2 ** 62, (1,)).item())
     buf, i = _SEED_POOL['buf'], _SEED_POOL['next']
-    if buf is not None and buf.device == device and i < buf.numel():
+    if buf is not None and buf.device == device and i < buf.numel() and not torch.compiler.is_compiling():
         _SEED_POOL['next'] = i + 1
         return buf[i:i + 1]
     return torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
@@ -871,7 +871,9 @@ class BaselineModel(torch.nn.Module):
 
 def _adjacent(a, b):
     """torch.cat([a, b], 0) as a view when b starts where a ends in one storage
-    (jagged.compact lays pos / neg out that way), else None."""
+    (jagged.compact lays pos / neg out that way), else None (always when traced)."""
+    if torch.compiler.is_compiling():
+        return None
     if a.dtype != b.dtype or a.shape[1:] != b.shape[1:] or not (a.is_contiguous() and b.is_contiguous()) \
             or a.device != b.device or a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr() \
             or b.data_ptr() != a.data_ptr() + a.numel() * a.element_size():
