@@ -83,8 +83,13 @@ typedef struct grk_feature {
   int32_t bag;           /* index columns per token: 1 = gather, >1 = sum  */
   int32_t out_col;       /* first output column (elements)                 */
   int32_t idx_mode;      /* GRK_IDX_*                                       */
-  int32_t pad_;
+  int32_t flags;         /* GRK_FEAT_* (0: none)                            */
 } grk_feature;
+
+/* grk_feature.flags: row 0 of the table is a zero padding row, so bag slots
+ * that resolve to it add nothing and are not read (round 4: the projected
+ * feature tables, whose user-feature slots are padding on every item token). */
+#define GRK_FEAT_SKIP_ROW0 1
 
 /* out[n, f.out_col : f.out_col+dim] = sum_a table_f[row(n, a)] for every
  * feature f and token n < num_tokens.  Bag sums accumulate in fp32 from slot
@@ -118,7 +123,7 @@ typedef struct grk_lookup {
 size_t grk_embedding_backward_workspace(int64_t num_occurrences, int64_t num_rows, int dim);
 
 /* Stable LSD radix sort of (uint32 key, uint64 value) pairs by the low
- * end_bit bits of the keys (8-bit digits, three launches per digit) -- the
+ * end_bit bits of the keys (digits of up to 11 bits, three launches per digit) -- the
  * occurrence grouping inside grk_embedding_backward, exposed for tests and
  * reuse.  keys_in / vals_in are not modified; keys_tmp / vals_tmp are n-element
  * scratch; workspace: grk_sort_pairs_workspace(n) bytes. */

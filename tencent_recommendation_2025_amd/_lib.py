@@ -26,6 +26,7 @@ GRK_F32, GRK_BF16, GRK_F16 = 0, 1, 2
 GRK_F32_BF16 = 3  # pair logits: fp32 h, bf16 item embeddings
 GRK_FP8_E4M3 = 4  # attention q/k/v: OCP fp8 e4m3
 GRK_I32, GRK_I64 = 0, 1
+FEAT_SKIP_ROW0 = 1   # GRK_FEAT_SKIP_ROW0
 GRK_GEMM_EP_NONE, GRK_GEMM_EP_RELU = 0, 1
 BWD_ORDERED, BWD_CHUNKED, BWD_DENSE_BF16 = 0, 1, 2  # grk_embedding_backward flags (bf16 dense: | with CHUNKED)
 IDX_PLAIN, IDX_ITEM_MASK, IDX_USER_MASK, IDX_POSITION = 0, 1, 2, 3
@@ -35,7 +36,7 @@ MAX_FEATURES = 48
 
 class GrkFeature(C.Structure):
     _fields_ = [('table', C.c_void_p), ('idx', C.c_void_p), ('num_rows', C.c_int64), ('idx_ld', C.c_int64),
-                ('bag', C.c_int32), ('out_col', C.c_int32), ('idx_mode', C.c_int32), ('pad_', C.c_int32)]
+                ('bag', C.c_int32), ('out_col', C.c_int32), ('idx_mode', C.c_int32), ('flags', C.c_int32)]
 
 
 class GrkLookup(C.Structure):

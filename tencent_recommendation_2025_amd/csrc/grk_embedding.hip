@@ -82,6 +82,7 @@ __global__ void __launch_bounds__(256) k_gather(FeatArgs args, int dim, int64_t 
             if (err_flag) *err_flag = 1;
             continue;
           }
+          if (row == 0 && (f.flags & GRK_FEAT_SKIP_ROW0)) continue;  // a zero padding row adds nothing
           Vec16<T> r;
           r.load(table + row * dim + cc[u] * VEC);
           if (a == 0) {
@@ -109,7 +110,9 @@ __global__ void __launch_bounds__(256) k_gather(FeatArgs args, int dim, int64_t 
 // fp32 d=256): lane = 16-byte column chunk, so a unit needs no index
 // arithmetic; the token's index (and bag) words are wave-uniform scalar loads,
 // and kGatherRows tokens per wave keep that many rows in flight.  Same values
-// as k_gather (bag sums in fp32 from slot 0, one rounding).
+// as k_gather (bag sums in fp32 from slot 0, one rounding; with
+// GRK_FEAT_SKIP_ROW0 the zero padding row's slots are not read -- adding +0
+// changes no sum, up to the sign of an all-zero result).
 constexpr int kGatherRows = 1;
 
 template <typename T, typename I>
@@ -158,6 +161,7 @@ __global__ void __launch_bounds__(256) k_gather_wave(FeatArgs args, int64_t num_
         if (err_flag) *err_flag = 1;
         continue;
       }
+      if (row == 0 && (f.flags & GRK_FEAT_SKIP_ROW0)) continue;  // wave-uniform: a zero padding row
       Vec16<T> x;
       x.load(table + row * dim + lane * VEC);
       if (a == 0) {

@@ -51,11 +51,12 @@ class TableRef:
     chunked fixed order (K.embedding_backward); honoured when every
     drop-in table of a fused lookup allows it.  ``merge``: a DenseMerge
     shared by the fused lookups of one forward that read this weight."""
-    __slots__ = ('weight', 'group', 'row_offset', 'chunked', 'merge')
+    __slots__ = ('weight', 'group', 'row_offset', 'chunked', 'merge', 'zero_row0')
 
-    def __init__(self, weight, group=None, row_offset=0, chunked=False, merge=None):
+    def __init__(self, weight, group=None, row_offset=0, chunked=False, merge=None, zero_row0=False):
         self.weight, self.group, self.row_offset, self.chunked = weight, group, row_offset, chunked
         self.merge = merge
+        self.zero_row0 = zero_row0   # row 0 is a zero padding row (the gather skips bag slots on it)
 
 
 class DenseMerge:
@@ -129,7 +130,8 @@ class _FeatureLookupFn(torch.autograd.Function):
         dt = specs[0].ref.weight.dtype
         dev = specs[0].ref.weight.device
         out = torch.empty(num_tokens, out_ld, dtype=dt, device=dev)
-        lookups = [K.Lookup(s.ref.weight, s.idx, s.out_col, s.mode, s.bag) for s in specs]
+        lookups = [K.Lookup(s.ref.weight, s.idx, s.out_col, s.mode, s.bag, getattr(s.ref, 'zero_row0', False))
+                   for s in specs]
         for i in range(0, len(lookups), L.MAX_FEATURES):
             K.embedding_gather(lookups[i:i + L.MAX_FEATURES], out, num_tokens, token_type, seq_len)
         if GATHER_TRACE is not None:

@@ -38,6 +38,7 @@ class Lookup:
     out_col: int
     mode: int = L.IDX_PLAIN
     bag: int = 1
+    skip_row0: bool = False   # row 0 is a zero padding row: bag slots on it are not read
 
     def idx_ld(self):
         return self.bag
@@ -73,7 +74,7 @@ def embedding_gather(lookups, out, num_tokens, token_type=None, seq_len=0, err_f
             raise L.GrkError(f'lookup {i}: {n} tokens, expected {num_tokens}')
         keep.append(idx)
         feats[i] = L.GrkFeature(lk.table.data_ptr(), idx.data_ptr(), lk.table.shape[0], lk.bag, lk.bag,
-                                lk.out_col, lk.mode, 0)
+                                lk.out_col, lk.mode, L.FEAT_SKIP_ROW0 if lk.skip_row0 else 0)
     if token_type is not None:
         token_type = token_type.to(torch.int32).contiguous()
         keep.append(token_type)

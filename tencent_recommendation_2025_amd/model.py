@@ -646,8 +646,10 @@ class BaselineModel(torch.nn.Module):
             idx = self._proj_index(feats, names, offs, N)
             # P = E W is an intermediate: its row sums may use the chunked order (the
             # reference accumulates dE = sum dY W, in no order P's sums could match)
-            specs.append(G.LookupSpec(G.TableRef(P, chunked=True, merge=self._proj_merge(P)), idx, col, L.IDX_PLAIN,
-                                      idx.shape[1]))
+            # P's row 0 is the zero padding row every feature's padding maps to (grk_proj_index):
+            # the gather skips those slots (all user-feature slots of an item token)
+            specs.append(G.LookupSpec(G.TableRef(P, chunked=True, merge=self._proj_merge(P), zero_row0=True), idx,
+                                      col, L.IDX_PLAIN, idx.shape[1]))
             splits.append((col, col + d))
             col += d
 

@@ -410,3 +410,28 @@ def test_small_sparse_call_one_workgroup(K, n, D, dt):
     assert np.array_equal(res.rows[:cnt].cpu().numpy(), want_dense[uniq])
     s = slot.cpu().numpy()
     assert np.array_equal(s[uniq], np.arange(cnt)) and np.all(np.delete(s, uniq) == -1)
+
+
+@pytest.mark.parametrize('D,dt', [(512, torch.bfloat16), (64, torch.float32)])
+def test_skip_row0_bag_slots_change_no_sum(K, D, dt):
+    """GRK_FEAT_SKIP_ROW0 (round 4): bag slots on a zero padding row 0 are not read;
+    the bag sums equal the flag-less gather and the oracle's slot-0-upward sums
+    (values; an all-padding bag is +0 either way)."""
+    rng = np.random.default_rng(D)
+    R, N, A = 3000, 999, 6
+    tab = rng.standard_normal((R, D)).astype(np.float32)
+    tab[0] = 0.0
+    if dt == torch.bfloat16:
+        tab = oemb.to_bf16_f32(tab)
+    idx = rng.integers(1, R, (N, A))
+    idx[rng.random((N, A)) < 0.6] = 0
+    idx[:7] = 0                                    # all-padding bags
+    tb = T(tab).to(dt)
+    outs = []
+    for skip in (False, True):
+        out = torch.full((N, D), float('nan'), dtype=dt, device=DEV)
+        K.embedding_gather([K.Lookup(tb, T(idx), 0, bag=A, skip_row0=skip)], out, N)
+        outs.append(out.float().cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[1], oemb.bag_sum(tab, idx, out_bf16=dt == torch.bfloat16))
+    assert np.all(outs[1][:7] == 0)
