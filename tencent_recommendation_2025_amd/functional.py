@@ -441,6 +441,44 @@ def dnn_weight(blocks, bias, mms, width, dtype):
     return _DnnWeightFn.apply(len(blocks), len(mms), int(width), dtype, *blocks, bias, *flat)
 
 
+class _SplitPairFn(torch.autograd.Function):
+    """x[:n], x[n:] whose backward takes the two gradients back as ONE view when
+    they are the halves of one buffer (kernels.pair_logits_bwd writes them so),
+    where autograd's split backward always copies them into a new tensor (cat)."""
+
+    @staticmethod
+    def forward(ctx, x, n):
+        ctx.n, ctx.shape = n, x.shape
+        return x[:n], x[n:]
+
+    @staticmethod
+    def backward(ctx, ga, gb):
+        n, shape = ctx.n, ctx.shape
+        if ga is None and gb is None:
+            return None, None
+        if ga is None:
+            ga = gb.new_zeros((n,) + tuple(shape[1:]))
+        if gb is None:
+            gb = ga.new_zeros((shape[0] - n,) + tuple(shape[1:]))
+        v = _adjacent_rows(ga, gb)
+        return (v if v is not None else torch.cat([ga, gb], 0)), None
+
+
+def _adjacent_rows(a, b):
+    """torch.cat([a, b], 0) as a view when b starts where a ends in one storage, else None."""
+    if a.dtype != b.dtype or a.shape[1:] != b.shape[1:] or not (a.is_contiguous() and b.is_contiguous()) \
+            or a.device != b.device or a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr() \
+            or b.data_ptr() != a.data_ptr() + a.numel() * a.element_size():
+        return None
+    return a.as_strided((a.shape[0] + b.shape[0],) + tuple(a.shape[1:]), a.stride(), a.storage_offset())
+
+
+@_disable
+def split_pair(x, n):
+    """(x[:n], x[n:]) along dim 0; the backward joins adjacent gradient halves without a copy."""
+    return _SplitPairFn.apply(x, int(n))
+
+
 class _EmbCombineFn(torch.autograd.Function):
     """seqs = dropout((act(a) + act(b)) * scale + pos) on grk_emb_combine (one pass
     each way); a / b the itemdnn / userdnn outputs before their ReLU when relu."""

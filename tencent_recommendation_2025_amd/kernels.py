@@ -966,6 +966,11 @@ def pair_logits_bwd(h, e_pos, e_neg, gpos=None, gneg=None, pos_logits=None, neg_
     dt = _pair_dtype(h, e_pos, e_neg)
     N, D = h.shape
     outs = [torch.empty(N, D, dtype=x.dtype, device=h.device) if n else None for n, x in zip(need, (h, e_pos, e_neg))]
+    if need[1] and need[2] and e_pos.dtype == e_neg.dtype:
+        # de_pos and de_neg in the halves of one buffer: the model's pos / neg split of one
+        # stacked feat2emb (functional.split_pair) takes them back without a cat
+        pair = torch.empty(2 * N, D, dtype=e_pos.dtype, device=h.device)
+        outs[1], outs[2] = pair[:N], pair[N:]
     ntt = None if next_token_type is None else next_token_type.to(torch.int32).contiguous()
     gpos = None if gpos is None else gpos.float().contiguous()
     gneg = None if gneg is None else gneg.float().contiguous()

@@ -757,7 +757,10 @@ class BaselineModel(torch.nn.Module):
                     self._remaps[(name, 'pair', L.IDX_PLAIN)] = (a[0], torch.cat([a[1], b[1]], 0))
         x = self._embed(seq2, feats, role='pair')[0]
         # split, not x[:B] / x[B:]: its backward is one cat of the two gradients, where two
-        # slices' backwards zero-fill a full-size gradient each and add them (same values)
+        # slices' backwards zero-fill a full-size gradient each and add them (same values);
+        # on the GPU not even the cat: the fused loss writes the halves into one buffer
+        if x.is_cuda and not torch.compiler.is_compiling():
+            return G.split_pair(x, B)
         pe, ne = x.split(B, 0)
         return pe, ne
 
@@ -876,11 +879,7 @@ def _adjacent(a, b):
     (jagged.compact lays pos / neg out that way), else None (always when traced)."""
     if torch.compiler.is_compiling():
         return None
-    if a.dtype != b.dtype or a.shape[1:] != b.shape[1:] or not (a.is_contiguous() and b.is_contiguous()) \
-            or a.device != b.device or a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr() \
-            or b.data_ptr() != a.data_ptr() + a.numel() * a.element_size():
-        return None
-    return a.as_strided((a.shape[0] + b.shape[0],) + tuple(a.shape[1:]), a.stride(), a.storage_offset())
+    return G._adjacent_rows(a, b)
 
 
 def _cat0(a, b):

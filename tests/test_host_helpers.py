@@ -322,3 +322,22 @@ def test_stack_pairs_is_a_view_for_adjacent_halves():
     assert Mm._adjacent(b, a) is None                       # wrong order
     assert Mm._adjacent(buf[:2], buf[3:]) is None           # a gap
     assert torch.equal(Mm._cat0(buf[:2], buf[3:]), torch.cat([buf[:2], buf[3:]]))
+
+
+def test_split_pair_joins_adjacent_gradients_without_a_copy():
+    """functional.split_pair (round 4): forward = x[:n], x[n:]; backward returns the two
+    gradient halves as one view when they are adjacent, a cat otherwise -- same values
+    as torch's split either way."""
+    from tencent_recommendation_2025_amd import functional as G
+    x = torch.randn(6, 3, requires_grad=True)
+    a, b = G.split_pair(x, 2)
+    assert torch.equal(a, x[:2]) and torch.equal(b, x[2:])
+    buf = torch.randn(6, 3)
+    (a * buf[:2]).sum().backward(retain_graph=True)   # gb None: zeros for the second half
+    assert torch.equal(x.grad, torch.cat([buf[:2], torch.zeros(4, 3)]))
+    x.grad = None
+    ga, gb = buf[:2], buf[2:]
+    gx, = torch.autograd.grad((a, b), (x,), (ga, gb))
+    assert torch.equal(gx, buf) and gx.data_ptr() == buf.data_ptr()     # a view of the joint buffer
+    gx, = torch.autograd.grad((a, b), (x,), (ga.clone(), gb.clone()))
+    assert torch.equal(gx, buf)
