@@ -405,6 +405,23 @@ typedef struct grk_index_block {
 int grk_proj_index(const grk_index_block* blocks, int num_blocks, int itype, int64_t rows, int64_t* out,
                    int64_t out_ld, void* stream);
 
+/* Dense column blocks written into a row-major [rows, out_ld] buffer (bf16 or
+ * fp32) in ONE launch -- the gather buffer's mm-embedding columns (fp32
+ * [rows, 32] -> the dnn operand, model/BaseLine/model.py:290-299) and its
+ * constant [1, 0, ...] bias / padding columns (one source row broadcast:
+ * src_ld = 0).  Blocks in column order, disjoint; fp32 -> bf16 rounds to
+ * nearest even. */
+typedef struct grk_column_block {
+  const void* src;       /* [rows, src_ld] or one row (src_ld = 0)           */
+  int64_t src_ld;        /* elements; 0 = broadcast row 0                    */
+  int32_t width;         /* columns                                          */
+  int32_t out_col;       /* first output column                              */
+  int32_t src_dtype;     /* GRK_F32 / GRK_BF16                               */
+  int32_t pad_;
+} grk_column_block;
+int grk_write_columns(const grk_column_block* blocks, int num_blocks, int64_t rows, void* out, int64_t out_ld,
+                      int out_dtype, void* stream);
+
 /* Rows of the item / user tables a training batch reads (model/BaseLine/
  * model.py:331-350, 376-377), -1 for padding: item_ids [3n] = (item ids of item
  * tokens | pos | neg), user_ids [n] = user ids of user tokens (NULL: skipped).

@@ -78,6 +78,11 @@ class GrkIndexBlock(C.Structure):
                 ('offset', C.c_int64)]
 
 
+class GrkColumnBlock(C.Structure):
+    _fields_ = [('src', C.c_void_p), ('src_ld', C.c_int64), ('width', C.c_int32), ('out_col', C.c_int32),
+                ('src_dtype', C.c_int32), ('pad_', C.c_int32)]
+
+
 class GrkGemmGroup(C.Structure):
     _fields_ = [('a', C.c_void_p), ('lda', C.c_int64), ('b', C.c_void_p), ('ldb', C.c_int64), ('c', C.c_void_p),
                 ('ldc', C.c_int64), ('rows', C.c_int64), ('b_rows', C.c_int64)]
@@ -152,6 +157,7 @@ SIGNATURES = {
     'grk_jagged_layout': (_I, [_P, _I, _I, _I64, _P, _P, _P, _P, _P, _P, _P]),
     'grk_gather_rows': (_I, [C.POINTER(GrkRowCopy), _I, _P, _I64, _P]),
     'grk_proj_index': (_I, [C.POINTER(GrkIndexBlock), _I, _I, _I64, _P, _I64, _P]),
+    'grk_write_columns': (_I, [C.POINTER(GrkColumnBlock), _I, _I64, _P, _I64, _I, _P]),
     'grk_batch_row_ids': (_I, [_P, _P, _P, _P, _I, _I64, _P, _P, _P]),
     'grk_add_norm_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _P, _I64, _P, _I64, _I, _P, _P]),
     'grk_add_norm_bwd_workspace': (_SZ, [_I64, _I]),

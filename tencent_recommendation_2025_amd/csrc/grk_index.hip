@@ -8,12 +8,17 @@
 //    shifted to its table's first P row, padding (0) kept at 0 -- the
 //    reference's per-feature nn.Embedding(padding_idx=0) lookups
 //    (model/BaseLine/model.py:254-277) restated over P.
+//  * grk_write_columns: the dense column blocks of the gather buffer (mm
+//    embeddings, the dnn operands' constant bias / padding columns) in one
+//    launch (were one copy kernel per block).
 //  * grk_batch_row_ids: the rows of the item / user tables a training batch
 //    reads (model/BaseLine/model.py:331-350, 376-377: item ids of item tokens,
 //    pos, neg; user ids of user tokens), -1 for padding -- the ids the deferred
 //    dense-parity AdamW brings up to date before the forward
 //    (optim.FusedAdamW.begin_step).
 // Integer work of a few hundred KB: launch-bound; grid-stride, 256 threads.
+#include <string.h>
+
 #include "grk_common.h"
 
 namespace grk {
@@ -53,10 +58,70 @@ __global__ void __launch_bounds__(256) k_batch_row_ids(const I* __restrict__ seq
   }
 }
 
+// Dense column blocks into a row-major buffer (the gather buffer's mm-embedding
+// columns and its constant [1, 0, ...] bias / padding columns): one thread per
+// output element, blocks found by their column range, dtype converted on the
+// way (fp32 -> bf16 rounds to nearest even, as torch's copy_).
+constexpr int kMaxColumnBlocks = 16;
+struct ColumnBlocks {
+  grk_column_block b[kMaxColumnBlocks];
+};
+
+template <typename OT>
+__global__ void __launch_bounds__(256) k_write_columns(ColumnBlocks cb, int nb, int64_t rows, int width,
+                                                       OT* __restrict__ out, int64_t out_ld) {
+  const int64_t total = rows * width;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / width;
+    int c = (int)(i - r * width);
+    int k = 0;
+    while (k + 1 < nb && c >= cb.b[k].width) {
+      c -= cb.b[k].width;
+      ++k;
+    }
+    const grk_column_block& b = cb.b[k];
+    const int64_t si = (b.src_ld ? r * b.src_ld : 0) + c;
+    const float v = b.src_dtype == GRK_F32 ? reinterpret_cast<const float*>(b.src)[si]
+                                           : bf16_to_f32(reinterpret_cast<const bf16_t*>(b.src)[si]);
+    OT* dst = out + r * out_ld + b.out_col + c;
+    if constexpr (sizeof(OT) == 4) *dst = v;
+    else *dst = f32_to_bf16(v);
+  }
+}
+
 }  // namespace
 }  // namespace grk
 
 using namespace grk;
+
+extern "C" int grk_write_columns(const grk_column_block* blocks, int num_blocks, int64_t rows, void* out,
+                                 int64_t out_ld, int out_dtype, void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(num_blocks >= 1 && num_blocks <= kMaxColumnBlocks, "num_blocks must be in [1, %d]", kMaxColumnBlocks);
+  GRK_CHECK_ARG(out_dtype == GRK_F32 || out_dtype == GRK_BF16, "out_dtype must be GRK_F32 or GRK_BF16");
+  GRK_CHECK_ARG(rows >= 0 && blocks && (out || rows == 0), "bad rows / blocks / out");
+  ColumnBlocks cb;
+  memset(&cb, 0, sizeof(cb));
+  int width = 0;
+  for (int k = 0; k < num_blocks; ++k) {
+    const grk_column_block& b = blocks[k];
+    GRK_CHECK_ARG(b.src && b.width >= 1 && (b.src_ld == 0 || b.src_ld >= b.width), "block %d: src / width / src_ld", k);
+    GRK_CHECK_ARG(b.src_dtype == GRK_F32 || b.src_dtype == GRK_BF16, "block %d: src_dtype", k);
+    GRK_CHECK_ARG(b.out_col >= 0 && b.out_col + b.width <= out_ld, "block %d: columns past out_ld", k);
+    GRK_CHECK_ARG(k == 0 || b.out_col >= blocks[k - 1].out_col + blocks[k - 1].width,
+                  "block %d: blocks must be in column order and disjoint", k);
+    cb.b[k] = b;
+    width += b.width;
+  }
+  if (rows == 0) return GRK_OK;
+  const int g = grid_for(rows * width, 256);
+  if (out_dtype == GRK_F32)
+    k_write_columns<float><<<g, 256, 0, (hipStream_t)stream>>>(cb, num_blocks, rows, width, (float*)out, out_ld);
+  else
+    k_write_columns<bf16_t><<<g, 256, 0, (hipStream_t)stream>>>(cb, num_blocks, rows, width, (bf16_t*)out, out_ld);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
 
 extern "C" int grk_proj_index(const grk_index_block* blocks, int num_blocks, int itype, int64_t rows, int64_t* out,
                               int64_t out_ld, void* stream) {

@@ -271,8 +271,14 @@ def _lookup_op(specs, token_type, seq_len, num_tokens, out_ld, extras, splits):
 def write_extras(out, extras):
     """Dense blocks into the gather buffer: (column, [num_tokens, w] tensor, or a [1, w]
     row broadcast over every token -- e.g. the dnn operand's constant [1, 0, ...] bias /
-    padding columns).  One copy kernel per block, the dtype converted inside it (the
-    same rounding as a .to() before the copy).  Dense inputs: no gradient propagates."""
+    padding columns).  On the GPU one grk_write_columns launch for every block (was one
+    copy kernel per block), the dtype converted inside it (the same rounding as a .to()
+    before the copy).  Dense inputs: no gradient propagates."""
+    if not extras:
+        return
+    if out.is_cuda and len(extras) <= K.MAX_COLUMN_BLOCKS and out.dtype in (torch.float32, torch.bfloat16):
+        K.write_columns(out, extras)
+        return
     for col, x in extras:
         out[:, col:col + x.shape[1]].copy_(x.detach())
 

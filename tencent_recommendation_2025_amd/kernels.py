@@ -498,6 +498,39 @@ def jagged_layout(key_valid, capacity, next_token_type=None, err_flag=None):
     return ranges, row_base, row_map, n
 
 
+MAX_COLUMN_BLOCKS = 16   # kMaxColumnBlocks (csrc/grk_index.hip)
+
+
+def write_columns(out, blocks):
+    """out[:, col:col + w] = x for every (col, x) in blocks (grk_write_columns, one launch):
+    x fp32 / bf16 [rows, w] with unit column stride, or [1, w] broadcast to every row;
+    out bf16 / fp32 [rows, ld] row-major.  Blocks in column order, disjoint."""
+    if not blocks:
+        return out
+    if len(blocks) > MAX_COLUMN_BLOCKS:
+        raise L.GrkError(f'at most {MAX_COLUMN_BLOCKS} column blocks per launch')
+    _require_cuda(out, *[x for _, x in blocks])
+    if out.dim() != 2 or out.stride(1) != 1 or out.dtype not in (torch.float32, torch.bfloat16):
+        raise L.GrkError('out must be a row-major [rows, ld] fp32 / bf16 tensor')
+    rows = out.shape[0]
+    arr = (L.GrkColumnBlock * len(blocks))()
+    keep = []
+    for k, (col, x) in enumerate(sorted(blocks, key=lambda b: b[0])):
+        x = x.detach()
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        if x.dim() != 2 or x.stride(1) != 1:
+            x = x.reshape(x.shape[0], -1).contiguous()
+        if x.shape[0] not in (1, rows):
+            raise L.GrkError(f'column block {k}: {x.shape[0]} rows, expected 1 or {rows}')
+        keep.append(x)
+        ld = 0 if x.shape[0] == 1 and rows != 1 else x.stride(0)
+        arr[k] = L.GrkColumnBlock(x.data_ptr(), ld, x.shape[1], int(col), L.dtype_code(x.dtype), 0)
+    L.check(L.lib().grk_write_columns(arr, len(blocks), rows, out.data_ptr(), out.stride(0), L.dtype_code(out.dtype),
+                                      L.stream_ptr(out.device)), 'grk_write_columns')
+    return out
+
+
 def proj_index(blocks, rows, out=None):
     """int64 [rows, sum of widths]: column block k = blocks[k] = (src [rows, w] int, offset)
     with every non-zero value shifted by offset, 0 kept (grk_proj_index, one launch):

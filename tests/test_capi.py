@@ -108,3 +108,18 @@ def test_grouped_gemm_entry_points_refuse_bad_groups(lib):
     assert h.grk_grouped_wgrad_workspace(g, 1, 512, 512) > 0
     assert h.grk_grouped_wgrad(g, 1, 512, 512, 16, 1 << 30, None) == lib.GRK_EINVAL
     assert b'b_rows' in h.grk_last_error()
+
+
+def test_write_columns_refuses_bad_blocks(lib):
+    """grk_write_columns (round 4) checks its column blocks on the host."""
+    h = lib.lib()
+    b = (lib.GrkColumnBlock * 2)()
+    b[0] = lib.GrkColumnBlock(16, 32, 32, 0, lib.GRK_F32, 0)
+    b[1] = lib.GrkColumnBlock(16, 0, 8, 16, lib.GRK_F32, 0)            # overlaps block 0
+    assert h.grk_write_columns(b, 2, 10, 16, 64, lib.GRK_BF16, None) == lib.GRK_EINVAL
+    assert b'column order' in h.grk_last_error()
+    b[1] = lib.GrkColumnBlock(16, 0, 8, 60, lib.GRK_F32, 0)            # past out_ld
+    assert h.grk_write_columns(b, 2, 10, 16, 64, lib.GRK_BF16, None) == lib.GRK_EINVAL
+    b[1] = lib.GrkColumnBlock(16, 0, 8, 32, 7, 0)                       # bad dtype
+    assert h.grk_write_columns(b, 2, 10, 16, 64, lib.GRK_BF16, None) == lib.GRK_EINVAL
+    assert h.grk_write_columns(b, 0, 10, 16, 64, lib.GRK_BF16, None) == lib.GRK_EINVAL

@@ -435,3 +435,23 @@ def test_skip_row0_bag_slots_change_no_sum(K, D, dt):
     assert np.array_equal(outs[0], outs[1])
     assert np.array_equal(outs[1], oemb.bag_sum(tab, idx, out_bf16=dt == torch.bfloat16))
     assert np.all(outs[1][:7] == 0)
+
+
+@pytest.mark.parametrize('odt', [torch.bfloat16, torch.float32])
+def test_write_columns_equals_copies(K, odt):
+    """grk_write_columns (round 4): the gather buffer's dense blocks (an fp32 [N, 32]
+    mm block, a broadcast [1, 8] constant row, a bf16 block) in one launch == the
+    per-block copy_ it replaces, bit for bit; other columns untouched."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    N = 3001
+    mm = torch.randn(N, 40, generator=g, device=DEV)[:, 3:35]          # strided rows
+    unit = torch.zeros(1, 8, device=DEV)
+    unit[0, 0] = 1.0
+    b16 = torch.randn(N, 16, generator=g, device=DEV).bfloat16()
+    blocks = [(64, mm), (96, unit), (112, b16)]
+    got = torch.full((N, 136), -3.0, dtype=odt, device=DEV)
+    want = got.clone()
+    K.write_columns(got, blocks)
+    for col, x in blocks:
+        want[:, col:col + x.shape[1]].copy_(x)
+    assert torch.equal(got, want)
