@@ -18,6 +18,12 @@ rc=$?; echo "sharded1 rc=$rc" >> $O/summary.txt
 if grep -Eqi 'illegal memory access|memory access fault|HSA_STATUS_ERROR|GPU Hang' $O/bench_sharded1.err || [ $rc -gt 1 ]; then
   echo "sharded1 failed -- stopping" >> $O/summary.txt; exit 3
 fi
+# every variant must export what the product build exports (built from the same objects)
+want=$(nm -D --defined-only tencent_recommendation_2025_amd/libgrk.so | grep -c " T grk_")
+for v in abtest/*.so; do
+  have=$(nm -D --defined-only $v | grep -c " T grk_")
+  [ "$have" = "$want" ] || { echo "$v: $have of $want entry points -- stale variant, stopping" >> $O/summary.txt; exit 4; }
+done
 timeout -k 10 900 bash scripts/gpu_ab.sh 1 "tencent_recommendation_2025_amd/libgrk.so abtest/libgrk_ch128.so abtest/libgrk_pipe32.so abtest/libgrk_fold.so abtest/libgrk_foldtb.so abtest/libgrk_ngb1024.so" > $O/ab.log 2>&1
 echo "ab rc=$?" >> $O/summary.txt
 cp gpurun_out/ab.txt $O/ab.txt 2>/dev/null
