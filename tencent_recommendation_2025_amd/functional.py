@@ -376,6 +376,18 @@ def linear(x, weight, bias=None, addend=None, relu=False, in_place=False):
     return _LinearFn.apply(x, weight, bias, addend, bool(relu), bool(in_place))
 
 
+_ZERO_BLOCKS = {}
+
+
+def _zero_block(rows, cols, dtype, device):
+    """A cached all-zero [rows, cols] tensor (read only): no fill kernel per use."""
+    key = (int(rows), int(cols), dtype, str(device))
+    t = _ZERO_BLOCKS.get(key)
+    if t is None:
+        t = _ZERO_BLOCKS[key] = torch.zeros(rows, cols, dtype=dtype, device=device)
+    return t
+
+
 class _DnnWeightFn(torch.autograd.Function):
     """The composed itemdnn / userdnn weight of the projection restatement
     (model._dnn_weight): [d, width] = [blocks... | W_k [W_t | b_t] (mm features,
@@ -406,7 +418,7 @@ class _DnnWeightFn(torch.autograd.Function):
             cols.append(bcol)
             used = sum(c.shape[1] for c in cols)
             if width > used:
-                cols.append(bias.new_zeros(d, width - used))
+                cols.append(_zero_block(d, width - used, bias.dtype, bias.device))
             Wc = torch.cat(cols, 1)
         out = Wc.to(dtype) if dtype != Wc.dtype else Wc
         ctx.save_for_backward(*[m[0] for m in mms], *ets)
