@@ -528,7 +528,8 @@ class _EmbCombineFn(torch.autograd.Function):
         if g2.dtype != torch.bfloat16 or g2.stride(-1) != 1 or g2.stride(0) % 8 or g2.data_ptr() % 16:
             g2 = g2.to(torch.bfloat16).contiguous()
         want = (ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2])
-        ga, gb, gp = K.emb_combine_bwd(g2, a2, b2, scale, relu, p, seed_t if seed_t is not None else seed_i, want)
+        ga, gb, gp = K.emb_combine_bwd(g2, a2, b2, scale, relu, p, seed_t if seed_t is not None else seed_i, want,
+                                       has_b=bdt is not None)
         ga = ga.view(shp).to(adt) if ga is not None else None
         gb = gb.view(shp).to(bdt) if gb is not None else None
         gp = gp.view(shp).to(pdt) if gp is not None else None
@@ -990,7 +991,7 @@ class _BCELossFn(torch.autograd.Function):
         h2, p2, n2, pos, neg, ntt, count = ctx.saved_tensors
         need = ctx.needs_input_grad[:3]
         dh, dp, dn = K.pair_logits_bwd(h2, p2, n2, pos_logits=pos, neg_logits=neg, next_token_type=ntt, count=count,
-                                       grad_loss=gloss, need=need)
+                                       grad_loss=gloss, need=need, stacked=True)
         return _shape_grads(ctx, dh, dp, dn)
 
 

@@ -931,13 +931,16 @@ def emb_combine_fwd(a, b, pos, scale, relu=True, dropout_p=0.0, seed=0):
     return y
 
 
-def emb_combine_bwd(gy, a, b, scale, relu=True, dropout_p=0.0, seed=0, want=(True, True, True)):
+def emb_combine_bwd(gy, a, b, scale, relu=True, dropout_p=0.0, seed=0, want=(True, True, True), has_b=None):
     """Gradients of emb_combine_fwd w.r.t. (a, b, pos) (grk_emb_combine_bwd); None where
-    not wanted (or b absent)."""
+    not wanted (or the forward had no b).  a / b: the forward's operands, needed with
+    relu only (their signs mask the gradient); has_b: whether the forward had a b
+    (default: b is not None)."""
     _require_cuda(gy, a, b)
     N, D = gy.shape
     dev = gy.device
-    outs = [torch.empty(N, D, dtype=torch.bfloat16, device=dev) if w and (i != 1 or b is not None) else None
+    has_b = b is not None if has_b is None else bool(has_b)
+    outs = [torch.empty(N, D, dtype=torch.bfloat16, device=dev) if w and (i != 1 or has_b) else None
             for i, w in enumerate(want)]
     rows = [_bf16_rows(t, n, D) if t is not None else (None, 0)
             for t, n in ((gy, 'gy'), (a, 'a'), (b, 'b'), (outs[0], 'ga'), (outs[1], 'gb'), (outs[2], 'gpos'))]
@@ -992,14 +995,15 @@ def pair_logits_fwd(h, e_pos, e_neg, next_token_type=None, with_loss=False):
 
 
 def pair_logits_bwd(h, e_pos, e_neg, gpos=None, gneg=None, pos_logits=None, neg_logits=None, next_token_type=None,
-                    count=None, grad_loss=None, need=(True, True, True)):
+                    count=None, grad_loss=None, need=(True, True, True), stacked=False):
     """Returns (dh, de_pos, de_neg) -- grk_pair_logits_bwd (None where not needed);
-    each gradient in its input's dtype."""
+    each gradient in its input's dtype.  stacked: de_pos and de_neg as the two halves
+    of one buffer (not for custom-op returns, which may not alias each other)."""
     _require_cuda(h, e_pos, e_neg, gpos, gneg, pos_logits, neg_logits, count, grad_loss)
     dt = _pair_dtype(h, e_pos, e_neg)
     N, D = h.shape
     outs = [torch.empty(N, D, dtype=x.dtype, device=h.device) if n else None for n, x in zip(need, (h, e_pos, e_neg))]
-    if need[1] and need[2] and e_pos.dtype == e_neg.dtype:
+    if stacked and need[1] and need[2] and e_pos.dtype == e_neg.dtype:
         # de_pos and de_neg in the halves of one buffer: the model's pos / neg split of one
         # stacked feat2emb (functional.split_pair) takes them back without a cat
         pair = torch.empty(2 * N, D, dtype=e_pos.dtype, device=h.device)

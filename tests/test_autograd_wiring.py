@@ -5,6 +5,7 @@ tests/test_gpu_emb_combine.py).  What is checked here is the Python side:
 which tensors the Functions save, which gradients they return in which slot,
 and that the in-place linear's output lives in its addend's storage while
 autograd still routes the addend's gradient to its producer."""
+import pytest
 import torch
 
 from tencent_recommendation_2025_amd import functional as G
@@ -77,25 +78,28 @@ def _fake_combine_fwd(a, b, pos, scale, relu=True, dropout_p=0.0, seed=0):
     return s.bfloat16()
 
 
-def _fake_combine_bwd(gy, a, b, scale, relu=True, dropout_p=0.0, seed=0, want=(True, True, True)):
+def _fake_combine_bwd(gy, a, b, scale, relu=True, dropout_p=0.0, seed=0, want=(True, True, True), has_b=None):
     g = gy.float()
+    has_b = b is not None if has_b is None else has_b
     ga = (g * scale * ((a.float() > 0) if relu else 1)).bfloat16() if want[0] else None
-    gb = (g * scale * ((b.float() > 0) if relu else 1)).bfloat16() if want[1] and b is not None else None
+    gb = (g * scale * ((b.float() > 0) if relu else 1)).bfloat16() if want[1] and has_b else None
     gp = g.bfloat16() if want[2] else None
     return ga, gb, gp
 
 
-def test_emb_combine_returns_gradients_in_input_order(monkeypatch):
+@pytest.mark.parametrize('relu', [True, False])
+def test_emb_combine_returns_gradients_in_input_order(monkeypatch, relu):
     monkeypatch.setattr(K, 'emb_combine_fwd', _fake_combine_fwd)
     monkeypatch.setattr(K, 'emb_combine_bwd', _fake_combine_bwd)
     g = torch.Generator().manual_seed(1)
     N, D = 30, 16
     a, b, p = (torch.randn(N, D, generator=g).bfloat16().requires_grad_(True) for _ in range(3))
-    y = G.emb_combine(a, b, p, 3.0, relu=True)
+    y = G.emb_combine(a, b, p, 3.0, relu=relu)
     gy = torch.randn(N, D, generator=g).bfloat16()
     y.backward(gy)
     af, bf, pf = (t.detach().float().requires_grad_(True) for t in (a, b, p))
-    yr = (torch.relu(af) + torch.relu(bf)) * 3.0 + pf
+    act = torch.relu if relu else (lambda t: t)
+    yr = (act(af) + act(bf)) * 3.0 + pf
     yr.backward(gy.float())
     assert torch.allclose(y.float(), yr, rtol=1e-2, atol=1e-2)
     for name, got, want in (('a', a.grad, af.grad), ('b', b.grad, bf.grad), ('pos', p.grad, pf.grad)):
