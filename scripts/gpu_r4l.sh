@@ -14,7 +14,7 @@ check() {  # name rc
   if grep -Eqi "$FAULT" $O/$1.log; then echo "$1: GPU fault -- stopping" >> $O/summary.txt; exit 3; fi
   case $2 in 0|1) return 0 ;; *) echo "$1: exit $2 -- stopping" >> $O/summary.txt; exit $2 ;; esac
 }
-GRK_C5_MODEL_TESTS=1 timeout -k 10 780 python -u -m pytest -m gpu -v -rs --timeout 240 --timeout-method thread tests \
+timeout -k 10 780 python -u -m pytest -m gpu -v -rs --timeout 240 --timeout-method thread tests \
   > $O/tests.log 2>&1; check tests $?
 timeout -k 10 200 python -u bench.py --cpu-baseline 0 --roofline-reps 5 > $O/bench.json 2> $O/bench.log; check bench $?
 timeout -k 10 200 python -u bench.py --fp8 1 --hidden 1024 --maxlen 1024 --batch 16 --steps 10 --warmup 3 \

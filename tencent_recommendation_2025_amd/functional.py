@@ -276,7 +276,8 @@ def write_extras(out, extras):
     before the copy).  Dense inputs: no gradient propagates."""
     if not extras:
         return
-    if out.is_cuda and len(extras) <= K.MAX_COLUMN_BLOCKS and out.dtype in (torch.float32, torch.bfloat16):
+    if out.is_cuda and len(extras) <= K.MAX_COLUMN_BLOCKS and out.dtype in (torch.float32, torch.bfloat16) \
+            and not torch.compiler.is_compiling():   # traced (drop-in under torch.compile): the copies
         K.write_columns(out, extras)
         return
     for col, x in extras:

@@ -4,8 +4,6 @@ attention.  The fp8 layer quantises its SiLU'd v|q|k to OCP e4m3 once
 straight-through at the quantiser (grk_dsilu_mul).  The oracle
 (oracle/model_ref.RefHSTU(fp8=True)) rounds the same activations to e4m3 with
 the same straight-through gradient, in fp32 everywhere else."""
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -14,13 +12,12 @@ from oracle import model_ref
 
 pytestmark = pytest.mark.gpu
 DEV = 'cuda'
-# The d = 1024 model tests are opt-in until they have run on hardware: their first
-# run (r3) hit an illegal address in torch's batched bf16 GEMM of the projected
-# feature tables (hipBLASLt HIPBLAS_STATUS_INTERNAL_ERROR at m 1024 n 10001 k 1024,
-# then the rocBLAS fallback faulted), before any fp8 code ran.  model._projection
-# now takes grk_gemm per block at d >= 1024; DESIGN.md §5b item 7.
-C5_MODEL = pytest.mark.skipif(os.environ.get('GRK_C5_MODEL_TESTS') != '1',
-                              reason='d=1024 model tests are opt-in (GRK_C5_MODEL_TESTS=1) until verified on hardware')
+# The d = 1024 model tests were opt-in in round 3: their first run hit an illegal
+# address in torch's batched bf16 GEMM of the projected feature tables (hipBLASLt
+# HIPBLAS_STATUS_INTERNAL_ERROR at m 1024 n 10001 k 1024, then the rocBLAS fallback
+# faulted), before any fp8 code ran.  The projections now run on grk's grouped MFMA
+# GEMM / grk_gemm; both tests passed on MI355X in round 4
+# (gpurun_out r4l) and run by default.
 
 
 def nrel(a, b):
@@ -80,7 +77,6 @@ def _c5_models(B, blocks, seed=5):
     return cfg, m, ref
 
 
-@C5_MODEL
 def test_c5_fp8_model_step_matches_oracle():
     """C5 shape (d=1024 = 8 heads x 128, T=1025) at reduced B=2 and 2 blocks: the
     drop-in model with fp8 HSTU layers (bf16 autocast GEMMs) against the fp32
@@ -113,7 +109,6 @@ def test_c5_fp8_model_step_matches_oracle():
     assert errs['loss'] < 1e-2 and errs['logits'] < 5e-2 and errs['attn_grad'] < 0.15, errs
 
 
-@C5_MODEL
 def test_c5_fp8_trainer_graph_equals_eager():
     """The fused trainer with fp8 HSTU layers at the C5 shape (B=2, 1 block):
     the HIP-graph replayed step equals the eager step bitwise (losses and every
