@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4, call k: PMC traffic of every bench roofline (profiles/r4_pmc_*), then an
+# Round 4, call k: the world-1 row-sharded bench line, then an
 # A/B of prepared builds (abtest/: chunked-backward chunk 128, wave pipe 32, attention
 # 1/n folded into the dK/dV store scales, + time-bias-free instantiation; norm-gate /
 # add-norm backward on 1024 workgroups instead of 512) against the
@@ -9,8 +9,6 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r4k
 mkdir -p $O
-timeout -k 10 900 bash scripts/gpu_pmc_round.sh r4 > $O/pmc.log 2>&1 || { echo "pmc rc=$?" >> $O/summary.txt; exit 1; }
-echo "pmc ok" >> $O/summary.txt
 # the N > 1 code path at world 1 (RCCL, row-sharded tables, jagged rows) beside the fused step
 timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
   --master-port 29613 bench.py --sharded 1 --cpu-baseline 0 --roofline-reps 1 > $O/bench_sharded1.json 2> $O/bench_sharded1.err
