@@ -315,7 +315,7 @@ class Trainer:
                 # once); the capture stream gets its GEMM workspace in _capture.
                 self._warm[key] = warm + 1
                 if self._sharded:
-                    return self.eager_step(batch, next_batch)
+                    return self._sharded_warm_step(batch, next_batch)
                 return self._on_side(lambda: self.eager_step(batch, next_batch))
             return self._capture(batch, next_batch, key)
         self._g, self._static, self._static_loss = entry
@@ -345,6 +345,39 @@ class Trainer:
         if self.jagged:
             self._poll_jagged()
         return self._static_loss.clone()
+
+    def _sharded_warm_step(self, batch, next_batch):
+        """Row-sharded warm-up step: the exchange, the dense all-reduces and the update
+        on the current stream (never the capture stream, see _step), the forward and
+        backward on the capture stream.  The dense parameters' AccumulateGrad nodes
+        outlive a step (the bucket all-reduce hooks keep them) and stay bound to the
+        stream of the backward that created them: created here on the capture stream,
+        the captured backward accumulates on its own stream.  Created on the current
+        (default) stream instead, every capture joined the default stream inside the
+        capture (torch's AccumulateGrad stream-mismatch warning), and capturing a second
+        jagged capacity that way crashed in capture_end (round 4, bench --sharded 1)."""
+        self.opt.zero_grad()
+        self.opt.prepare(batch)
+        if next_batch is not None:
+            self.opt.prefetch(next_batch)
+        if hasattr(self.opt, 'begin_step'):
+            self.opt.begin_step(batch)
+        buckets = getattr(self.opt, 'buckets', None)
+        if buckets is not None:
+            buckets.enabled = False   # no collectives from the side stream: step() reduces the buckets
+        try:
+            def fwd_bwd():
+                loss = self.compute_loss(batch)
+                loss.backward()
+                return loss.detach()
+            loss = self._on_side(fwd_bwd)
+        finally:
+            if buckets is not None:
+                buckets.enabled = True
+        self.opt.step()
+        if self.jagged:
+            self.check_jagged()
+        return loss
 
     def _on_side(self, fn):
         cur = torch.cuda.current_stream()
