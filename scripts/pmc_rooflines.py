@@ -118,14 +118,15 @@ for e in entries:
         fb, wb, n = traffic(k + '<')
         name = f"{tag}_pmc_attn_{k[len('k_attn_'):-len('_seq')]}_{e['workload']['kind']}.json"
     elif k == 'k_gather' and 'item-table' in e['kernel']:
-        fb, wb, n = traffic('k_gather<')  # the last launches of the run: the item-table roofline's
+        # k_gather< or k_gather_wave< (rows of 64 x 16 B): the last launches of the run are the roofline's
+        fb, wb, n = traffic('k_gather')
         name = f'{tag}_pmc_gather_item.json'
     elif k == 'k_gather':
-        fb, wb, n = traffic('k_gather<', True)  # widest launch: the seq-side fused lookup
+        fb, wb, n = traffic('k_gather', True)  # widest launch: the seq-side fused lookup
         name = f'{tag}_pmc_gather.json'
     elif k == 'k_wgrad':
-        # one grk_wgrad call = k_wgrad + k_wgrad_reduce; the last launches are the roofline's
-        f1, w1, n1 = traffic('k_wgrad<')
+        # one grk_wgrad call = the ring kernel (k_wgrad_lds<, k_wgrad< before round 4) + k_wgrad_reduce
+        f1, w1, n1 = traffic('k_wgrad_lds<' if any('k_wgrad_lds<' in r['Kernel_Name'] for r in fetch) else 'k_wgrad<')
         f2, w2, n2 = traffic('k_wgrad_reduce')
         fb, wb, n = f1 + f2, w1 + w2, min(n1, n2)
         name = f'{tag}_pmc_wgrad.json'
