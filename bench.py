@@ -604,15 +604,19 @@ def _rooflines(a, kv, jagged, rows, trace, btrace, model, pool, sid_roof):
     from tencent_recommendation_2025_amd import jagged as J
     dkdv, more = attention_rooflines(a, kv, a.roofline_reps, jagged=jagged)
     more.insert(0, dkdv)
+    progress('rooflines: attention')
     more.append(gather_roofline(trace, a.roofline_reps))
     item_table = model.item_emb.weight if model.item_emb.weight.numel() else None
     if item_table is not None:
         more.append(item_gather_roofline(item_table.detach(), pool[0], a.roofline_reps))
+    progress('rooflines: gathers')
     wk = J.capacity_for(rows[0], a.jagged_quantum) if jagged else a.batch * (a.maxlen + 1)
     more.append(wgrad_roofline(a, a.roofline_reps, wk))
     more.extend(ss_rooflines(pool[0], a, a.roofline_reps))
+    progress('rooflines: wgrad, sampled softmax')
     if btrace:   # last: scripts/pmc_rooflines.py finds these calls' PMC windows at the end of the run
         more.extend(backward_rooflines(btrace, a.roofline_reps))
+        progress('rooflines: embedding backward')
     if sid_roof is not None:
         more.append(sid_roof)
     # headline: the hand-written hot-path kernel with the most device time per step
