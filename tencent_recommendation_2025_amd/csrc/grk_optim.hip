@@ -73,6 +73,21 @@ __device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, con
   v = ve;
 }
 
+// adam1 with g = 0 (the catch-up replay), the same bits with fewer operations:
+//   g - m = -m and fma(w1, -m, m) == fma(-w1, m, m) for every m (signed zeros
+//   included: both give +0 for m = +-0);  fma(w2 * 0, 0, v * b2) == v * b2
+//   (v >= 0 is never -0, so adding +0 changes nothing).
+__device__ __forceinline__ void adam1_g0(float& p, float& m, float& v, const AdamStep& s) {
+#pragma clang fp contract(off)
+  const float pe = p * s.decay;
+  const float me = __builtin_fmaf(-s.w1, m, m);
+  const float ve = v * s.beta2;
+  const float denom = __builtin_fmaf(__builtin_amdgcn_sqrtf(ve), s.inv_bc2, s.eps);
+  p = __builtin_fmaf(-s.step_size, me * __builtin_amdgcn_rcpf(denom), pe);
+  m = me;
+  v = ve;
+}
+
 // NV consecutive elements (NV = 4 or 8) of param / exp_avg / exp_avg_sq in
 // registers: param via one 8/16-byte access (bf16) or NV/4 float4s, moments
 // via NV/4 float4s each.
@@ -368,7 +383,7 @@ __global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, fl
       slot = slot + 1 == ring_len ? 0 : slot + 1;
 #pragma unroll
       for (int e = 0; e < NV; ++e) {
-        adam1(pv[e], mv[e], vv[e], 0.0f, s);
+        adam1_g0(pv[e], mv[e], vv[e], s);
         if constexpr (sizeof(P) == 2) pv[e] = bf16_to_f32(f32_to_bf16(pv[e]));
       }
     }
