@@ -38,7 +38,9 @@ BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
+    # 32 = two 16-step segments: any 32 consecutive steps hold exactly two segment flushes of the
+    # deferred dense-parity table AdamW, so the default line carries them at their true rate
+    ap.add_argument('--steps', type=int, default=32)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--batch', type=int, default=128)
     ap.add_argument('--maxlen', type=int, default=200)
