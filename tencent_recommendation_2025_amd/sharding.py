@@ -297,7 +297,7 @@ class ShardedFusedAdamW(FusedAdamW):
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
                  table_dtype=torch.bfloat16, pg=None, gather_fn=kernel_gather, reduce_fn=kernel_reduce,
                  dense_reduce_fn=kernel_dense_reduce, defer_period=16, bucket_bytes=32 << 20, lookahead=True,
-                 init_seed=0):
+                 init_seed=0, dense_flat=True):
         self.pg = pg
         self.world = dist.get_world_size(pg)
         self.rank = dist.get_rank(pg)
@@ -332,11 +332,12 @@ class ShardedFusedAdamW(FusedAdamW):
                                             requires_grad=False)
             sharded_refs[name] = ShardedRef(name, emb.weight)
         small_keys = tuple(k for k in tables if k not in self.SHARDED and k != 'pos_emb')
-        # dense parameters stay on torch's AdamW here: their gradients are all-reduced in
-        # buckets (GradBuckets over self.dense's parameters) before step() updates them
+        # dense parameters: their gradients are all-reduced in buckets (GradBuckets), then
+        # updated by the flat multi-range AdamW (dense_flat: one launch, bf16 GEMM shadows
+        # written with the update) -- parameters it cannot hold stay on torch's AdamW
         super().__init__(model, lr, betas, eps, weight_decay, table_mode, table_dtype,
                          groups=(('pos', ('pos_emb',)), ('small', small_keys)), defer_period=defer_period,
-                         dense_flat=False)
+                         dense_flat=dense_flat)
         model._table_refs.update(sharded_refs)
         # replicated groups: their fp32 gradients share one buffer (one all-reduce)
         self.replicated = list(self.groups)
@@ -348,7 +349,7 @@ class ShardedFusedAdamW(FusedAdamW):
             self._deferred = {name: grp for name, (grp, _) in self.shards.items()}
             for g in self._deferred.values():
                 g.last = torch.zeros(g.rows, dtype=torch.int32, device=dev)
-        params = [p for grp in self.dense.param_groups for p in grp['params']]
+        params = self._dense_params()
         self.buckets = GradBuckets(params, pg, bucket_bytes) if params else None
         # fixed exchange buffers (rows fetched for a step, inverse indices): a captured
         # forward reads them at the same addresses every step
@@ -477,6 +478,13 @@ class ShardedFusedAdamW(FusedAdamW):
         self._begun = self.t
 
     # -- HIP graph capture of forward + backward (train.Trainer) ------------
+    def _dense_params(self):
+        """Every dense parameter: the flat buffer's, then torch AdamW's."""
+        out = list(self._flat.params) if self._flat is not None else []
+        if self.dense is not None:
+            out += [p for grp in self.dense.param_groups for p in grp['params']]
+        return out
+
     def capture_state(self):
         """After the forward + backward of a captured step: what its replays rewrite
         in place (gradient sources of every group and sink, dense gradients).
@@ -486,7 +494,7 @@ class ShardedFusedAdamW(FusedAdamW):
         self._captured = dict(
             groups=[(g, list(g.pending), dict(g.dense_grads), g.token_type, g.seq_len) for g in self.replicated],
             sinks={k: list(sk.sources) for k, sk in self.sinks.items()},
-            grads=[(p, p.grad) for grp in self.dense.param_groups for p in grp['params']])
+            grads=[(p, p.grad) for p in self._dense_params()])
         return self._captured
 
     def restore_captured(self, state=None):
@@ -557,7 +565,10 @@ class ShardedFusedAdamW(FusedAdamW):
                 K.stamp_rows(grp.last, res.ids, res.count, res.capacity, self.clock)
         if self.buckets is not None:
             self.buckets.finish()
-        self.dense.step()
+        if self.dense is not None:
+            self.dense.step()
+        if self._flat is not None:
+            self._flat.step(hp)
         if rep_work is not None:
             rep_work.wait()
         if self.world > 1:

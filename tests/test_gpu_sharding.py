@@ -45,9 +45,9 @@ def test_sharded_optimizer_world1_equals_fused(pg):
     from tencent_recommendation_2025_amd.train import Trainer
     m1, cfg = build()
     m2, _ = build()
-    # dense_flat=False: the sharded optimizer keeps the dense parameters on torch's AdamW
-    # (their gradients are all-reduced in buckets), so its twin does too
-    t1 = Trainer(m1, FusedAdamW(m1, lr=2e-3, table_dtype=torch.float32, defer_period=2, dense_flat=False), loss='bce',
+    # both on the flat multi-range AdamW for the dense parameters (the sharded one after its
+    # bucketed all-reduce)
+    t1 = Trainer(m1, FusedAdamW(m1, lr=2e-3, table_dtype=torch.float32, defer_period=2), loss='bce',
                  amp_dtype=None)
     t2 = Trainer(m2, ShardedFusedAdamW(m2, lr=2e-3, table_dtype=torch.float32, defer_period=2), loss='bce', amp_dtype=None)
     g = torch.Generator(device=DEV).manual_seed(0)
@@ -123,7 +123,7 @@ def test_shards_built_directly_equal_materialized_table(pg):
     m1, m2 = models
     materialize_tables_(m1, seed=5)
     assert m2.item_emb.weight.numel() == 0
-    t1 = Trainer(m1, FusedAdamW(m1, lr=2e-3, table_dtype=torch.float32, defer_period=2, dense_flat=False), loss='bce',
+    t1 = Trainer(m1, FusedAdamW(m1, lr=2e-3, table_dtype=torch.float32, defer_period=2), loss='bce',
                  amp_dtype=None)
     opt2 = ShardedFusedAdamW(m2, lr=2e-3, table_dtype=torch.float32, defer_period=2, init_seed=5)
     for k in ('item_emb', 'user_emb'):
@@ -201,7 +201,7 @@ def test_sharded_jagged_equals_sharded_padded_and_graph_replay(pg):
         if sharded:
             opt = ShardedFusedAdamW(m, lr=2e-3, table_dtype=tdt, defer_period=3)
         else:
-            opt = FusedAdamW(m, lr=2e-3, table_dtype=tdt, defer_period=3, dense_flat=False)
+            opt = FusedAdamW(m, lr=2e-3, table_dtype=tdt, defer_period=3)
         tr = Trainer(m, opt, loss='bce', amp_dtype=amp, graph=graph, graph_warmup=1, jagged=jagged,
                      jagged_quantum=64)
         g = torch.Generator(device=DEV).manual_seed(0)
