@@ -114,6 +114,18 @@ class ShardExchange:
         self.gather_fn = gather_fn
         self.plan = None
 
+    @staticmethod
+    def _stable_sort(keys, bound):
+        """(sorted keys, permutation) of int64 keys in [0, bound): grk's radix sort on the
+        GPU (a few launches over ceil(log2 bound) bits; torch.sort runs ~30 rocprim
+        merge-sort launches here), torch.sort on the CPU."""
+        if not keys.is_cuda or bound >= (1 << 31):
+            return torch.sort(keys, stable=True)
+        n = keys.numel()
+        k32, perm = K.sort_pairs(keys.to(torch.int32), torch.arange(n, dtype=torch.int64, device=keys.device),
+                                 max(1, int(bound - 1).bit_length()))
+        return k32.to(keys.dtype), perm
+
     def route(self, ids, pg=None):
         """Phase 1 (before the single host sync): unique ids, owner order, counts.
         pg: communicator for the counts exchange (default: the table's).
@@ -125,7 +137,7 @@ class ShardExchange:
         the stable owner order lists every real id first.  n_uniq reaches the
         host as sum(send_counts) with the split sizes."""
         n = ids.numel()
-        srt, perm = torch.sort(ids, stable=True)
+        srt, perm = self._stable_sort(ids, self.shard.shape[0] * self.world + self.world)
         head = torch.ones_like(srt, dtype=torch.bool)
         if n > 1:
             head[1:] = srt[1:] != srt[:-1]
@@ -136,7 +148,7 @@ class ShardExchange:
         uniq.scatter_(0, upos, srt)                      # duplicates write the same value
         n_uniq = upos[-1:] + 1 if n else upos.new_zeros(1)
         owner = torch.where(torch.arange(n, device=ids.device) < n_uniq, uniq % self.world, self.world)
-        order = torch.argsort(owner, stable=True)
+        order = self._stable_sort(owner, self.world + 1)[1]
         send_ids = uniq[order]
         # fetched rows and per-unique gradients live in owner order (slot s holds
         # send_ids[s]): rows come back from the owners already in place and the
