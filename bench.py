@@ -38,8 +38,10 @@ BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    # 32 = two 16-step segments: any 32 consecutive steps hold exactly two segment flushes of the
-    # deferred dense-parity table AdamW, so the default line carries them at their true rate
+    # the deferred dense-parity table AdamW flushes rolling (one 1/16 slice of every deferred table
+    # per step, inside the step: optim.FusedAdamW rolling), so every step costs the same and the
+    # line does not depend on --steps (round 4 flushed every row once per 16 steps, a 5.7 ms spike
+    # that a 20-step window held once or twice)
     ap.add_argument('--steps', type=int, default=32)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--batch', type=int, default=128)
@@ -442,29 +444,103 @@ def ss_rooflines(batch, a, reps):
     return out
 
 
-def wgrad_roofline(a, reps, k):
-    """grk_wgrad on the largest weight gradient of the step: the HSTU uvqk
-    projection (dW [4D, D] = dY^T X over the K token rows the step holds --
-    B*T padded, the jagged capacity otherwise -- + bias gradient), timed alone
-    (HIP events; k_wgrad + its in-order slice reduction).  MFMA bound:
-    algorithmic FLOPs 2*K*M*N."""
+def _wgrad_time(k, m, n, reps, out_dtype=torch.float32, want_db=True):
     from tencent_recommendation_2025_amd import kernels as K
-    m, n = 4 * a.hidden, a.hidden
     g = torch.Generator(device='cuda').manual_seed(0)
     dy = torch.randn(k, m, device='cuda', generator=g).bfloat16()
     x = torch.randn(k, n, device='cuda', generator=g).bfloat16()
-    ms = _time(lambda: K.wgrad(dy, x, want_db=True), reps)
-    flops = 2 * k * m * n
-    tf = flops / (ms * 1e-3) / 1e12
-    res = {'bound': 'mfma', 'kernel': 'grk::k_wgrad + k_wgrad_reduce (uvqk weight + bias gradient)',
+    return _time(lambda: K.wgrad(dy, x, out_dtype=out_dtype, want_db=want_db), reps)
+
+
+def wgrad_roofline(a, reps, k, wtrace=None):
+    """grk_wgrad, the whole kernel family of one step (every k_wgrad
+    instantiation counts toward the headline ranking): every weight gradient the
+    step computes on grk_wgrad (recorded from one eager step: the HSTU uvqk and
+    output projections, the item / user dnn weights ...), each shape timed alone
+    (HIP events; k_wgrad + its in-order slice reduction).  MFMA bound: algorithmic
+    FLOPs 2*K*M*N per call.  ``shapes`` lists each distinct shape; the uvqk one
+    (dW [4D, D] over the K token rows of the step + bias gradient) carries the
+    PMC traffic."""
+    m, n = 4 * a.hidden, a.hidden
+    calls = {}
+    for kk, mm, nn, odt, db in (wtrace or [(k, m, n, torch.float32, True)] * a.blocks):
+        key = (int(kk), int(mm), int(nn), odt, bool(db))
+        calls[key] = calls.get(key, 0) + 1
+    shapes, tot_ms, tot_flops, launches = [], 0.0, 0, 0
+    for (kk, mm, nn, odt, db), cnt in sorted(calls.items(), key=lambda kv: -kv[0][0] * kv[0][1] * kv[0][2]):
+        ms = _wgrad_time(kk, mm, nn, reps, odt, db)
+        fl = 2 * kk * mm * nn
+        tot_ms += ms * cnt
+        tot_flops += fl * cnt
+        launches += cnt
+        shapes.append({'K': kk, 'M': mm, 'N': nn, 'calls_per_step': cnt, 'avg_launch_us': round(ms * 1e3, 2),
+                       'tflops': round(fl / (ms * 1e-3) / 1e12, 1),
+                       'frac': round(fl / (ms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, 4)})
+    tf = tot_flops / (tot_ms * 1e-3) / 1e12
+    uvqk = next((s for s in shapes if s['M'] == m and s['N'] == n), None)
+    res = {'bound': 'mfma', 'kernel': 'grk::k_wgrad* + k_wgrad_reduce (every weight + bias gradient of the step)',
            'achieved': round(tf, 1), 'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-           'frac': round(tf / BF16_PEAK_TFLOPS, 4), 'traffic': None, 'flops_per_launch': int(flops),
-           'alg_bytes_per_launch': int(2 * k * (m + n) + 4 * m * (n + 1)), 'avg_launch_us': round(ms * 1e3, 2),
-           'calls_per_step': a.blocks, 'ms_per_step': round(ms * a.blocks, 4),
+           'frac': round(tf / BF16_PEAK_TFLOPS, 4), 'traffic': None, 'flops_per_step': int(tot_flops),
+           'avg_launch_us': round(tot_ms / launches * 1e3, 2), 'calls_per_step': launches,
+           'ms_per_step': round(tot_ms, 4), 'shapes': shapes,
            'workload': {'K': int(k), 'M': int(m), 'N': int(n)}}
     p = _pmc(f'{PMC_TAG}_pmc_wgrad.json', res['workload'])
-    if p is not None:
-        res['traffic'] = int(p['traffic_bytes_per_launch'])
+    if p is not None and uvqk is not None:
+        uvqk['traffic'] = int(p['traffic_bytes_per_launch'])
+        uvqk['alg_bytes_per_launch'] = int(2 * k * (m + n) + 4 * m * (n + 1))
+    return res
+
+
+def catchup_roofline(opt, reps):
+    """The rolling flush of the deferred dense-parity table AdamW (FusedAdamW
+    rolling, round 5): one k_adamw_catchup launch per deferred table and step over
+    a 1/period slice of its rows, each row replaying the g = 0 steps it lags.
+    Timed on copies of the item table's state as the timed region left it (the
+    slice the clock points at, its real lags), last[] restored before every
+    launch.  Algorithmic bytes: slice rows x D x (2 + 4 + 4) B read and written
+    + 8 B of last[] per row; the kernel is VALU-heavy (~70 instructions per
+    replayed step of 8 elements), reported against HBM."""
+    from tencent_recommendation_2025_amd import kernels as K
+    if not getattr(opt, 'rolling', False):
+        return None
+    g = opt._deferred.get('item') or next(iter(opt._deferred.values()))
+    period = opt._period
+    p, m, v = g.flat.clone(), g.exp_avg.clone(), g.exp_avg_sq.clone()
+    last0 = g.last.clone()
+    last = last0.clone()
+    t = int(opt.clock.t.item())
+    rows, D = p.shape
+    per = -(-rows // period)
+    s = t % period
+    lo, hi = s * per, min(rows, (s + 1) * per)
+    lag = (t - last0[lo:hi].long()).clamp(min=0)
+    stream = torch.cuda.current_stream()
+    total = 0.0
+    for _ in range(reps):
+        last.copy_(last0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        K.table_adamw_catchup_slice(p, m, v, last, opt.clock, period)
+        e1.record(stream)
+        e1.synchronize()
+        total += e0.elapsed_time(e1)
+    ms = total / reps
+    n = hi - lo
+    moved = int((lag > 0).sum().item())
+    alg = moved * D * (p.element_size() + 8) * 2 + n * 8
+    gbps = alg / (ms * 1e-3) / 1e9
+    res = {'bound': 'hbm', 'kernel': 'grk::k_adamw_catchup (rolling flush: one 1/%d slice of a 1M-row table)' % period,
+           'achieved': round(gbps, 1), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': round(gbps / HBM_PEAK_GBPS, 4),
+           'traffic': None, 'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2),
+           'calls_per_step': len(opt._deferred), 'ms_per_step': round(ms * len(opt._deferred), 4),
+           'replayed_steps_per_launch': int(lag.sum().item()), 'rows_moved_per_launch': moved,
+           'mean_lag_steps': round(float(lag.float().mean().item()), 2),
+           'note': 'VALU-heavy: the g = 0 AdamW replay is ~70 VALU instructions per replayed step of 8 elements',
+           'workload': {'table_rows': int(rows), 'D': int(D), 'slice_rows': int(n), 'period': int(period)}}
+    p_ = _pmc(f'{PMC_TAG}_pmc_catchup.json', {k: res['workload'][k] for k in ('table_rows', 'D', 'period')})
+    if p_ is not None:
+        res['traffic'] = int(p_['traffic_bytes_per_launch'])
+    del p, m, v, last, last0
     return res
 
 
@@ -602,7 +678,7 @@ def semantic_id_setup(a, dev, reps):
     return sid, roof
 
 
-def _rooflines(a, kv, jagged, rows, trace, btrace, model, pool, sid_roof):
+def _rooflines(a, kv, jagged, rows, trace, btrace, model, pool, sid_roof, wtrace=None, opt=None):
     """Every measured kernel (after the timed region): (headline roofline, the others)."""
     from tencent_recommendation_2025_amd import jagged as J
     dkdv, more = attention_rooflines(a, kv, a.roofline_reps, jagged=jagged)
@@ -614,16 +690,21 @@ def _rooflines(a, kv, jagged, rows, trace, btrace, model, pool, sid_roof):
         more.append(item_gather_roofline(item_table.detach(), pool[0], a.roofline_reps))
     progress('rooflines: gathers')
     wk = J.capacity_for(rows[0], a.jagged_quantum) if jagged else a.batch * (a.maxlen + 1)
-    more.append(wgrad_roofline(a, a.roofline_reps, wk))
+    more.append(wgrad_roofline(a, a.roofline_reps, wk, wtrace))
     more.extend(ss_rooflines(pool[0], a, a.roofline_reps))
     progress('rooflines: wgrad, sampled softmax')
+    cu = catchup_roofline(opt, a.roofline_reps) if opt is not None else None
+    if cu is not None:
+        more.append(cu)
+        progress('rooflines: rolling flush')
     if btrace:   # last: scripts/pmc_rooflines.py finds these calls' PMC windows at the end of the run
         more.extend(backward_rooflines(btrace, a.roofline_reps))
         progress('rooflines: embedding backward')
     if sid_roof is not None:
         more.append(sid_roof)
-    # headline: the hand-written hot-path kernel with the most device time per step
-    # (average launch x launches per step), with an HBM or MFMA roof
+    # headline: the hand-written hot-path kernel family with the most device time per step
+    # (every launch of the family in one step: average launch x launches per step), with
+    # an HBM or MFMA roof
     ranked = [r for r in more if r.get('peak') and r.get('ms_per_step')]
     roof = max(ranked, key=lambda r: r['ms_per_step'])
     more.remove(roof)
@@ -692,7 +773,7 @@ def main():
     caps = sorted({J.capacity_for(r, a.jagged_quantum) for r in rows}) if jagged else []
 
     from tencent_recommendation_2025_amd import kernels as K
-    trace = btrace = None
+    trace = btrace = wtrace = None
     def step(i):
         return trainer.step(pool[i % len(pool)], next_batch=pool[(i + 1) % len(pool)], rows=rows[i % len(pool)])
 
@@ -700,11 +781,13 @@ def main():
     for i in range(a.warmup):
         if i == 0:
             G.GATHER_TRACE = []          # record the fused-gather launches of one real (eager) step
-            K.BACKWARD_TRACE = []        # ... and its embedding-table gradients
+            K.BACKWARD_TRACE = []        # ... its embedding-table gradients
+            K.WGRAD_TRACE = []           # ... and its weight gradients
         step(i)
         if i == 0:
             trace, G.GATHER_TRACE = G.GATHER_TRACE, None
             btrace, K.BACKWARD_TRACE = K.BACKWARD_TRACE, None
+            wtrace, K.WGRAD_TRACE = K.WGRAD_TRACE, None
     # jagged + graph: one captured graph per capacity of the pool, captured before the
     # timed region (extra untimed steps on the batches of a capacity not captured yet)
     # Every rank takes the same number of steps (each one's collectives: the row
@@ -758,15 +841,17 @@ def main():
             print(f'  {i + 1:3d} {d:7.3f} {1e3 * host[i + 1]:7.3f} {caps_i[i + 1]}', file=sys.stderr)
 
     if not trace:  # --warmup 0: trace one extra, untimed eager step after the timed region
-        G.GATHER_TRACE, K.BACKWARD_TRACE = [], []
+        G.GATHER_TRACE, K.BACKWARD_TRACE, K.WGRAD_TRACE = [], [], []
         trainer.eager_step(pool[0])
         trace, G.GATHER_TRACE = G.GATHER_TRACE, None
         btrace, K.BACKWARD_TRACE = K.BACKWARD_TRACE, None
+        wtrace, K.WGRAD_TRACE = K.WGRAD_TRACE, None
     kv = (pool[0][3] != 0).to(torch.uint8)        # the first bench batch's key validity (token_type != 0)
     roof, more = None, []
     progress(f'timed region done: {elapsed / a.steps * 1e3:.3f} ms/step')
     if a.rooflines:
-        roof, more = _rooflines(a, kv, jagged, rows, trace, btrace, model, pool, sid_roof)
+        roof, more = _rooflines(a, kv, jagged, rows, trace, btrace, model, pool, sid_roof, wtrace,
+                                None if sharded else opt)
         progress('rooflines done')
 
     cpu = None

@@ -239,6 +239,17 @@ int grk_table_adamw_catchup_dev(void* param, int param_dtype, float* exp_avg, fl
 int grk_stamp_rows_dev(int32_t* last, const int64_t* uniq_ids, const int32_t* uniq_count, int64_t max_uniq,
                        const int32_t* t_dev, void* stream);
 
+/* Rolling flush of a deferred table (replaces the every-num_slices-steps full
+ * flush; same reference call site as grk_table_adamw_catchup,
+ * model/BaseLine/main.py:189 optimizer.step() over every table row): brings
+ * slice s = (*t_dev mod num_slices) of the rows, [s * per, min((s + 1) * per,
+ * num_rows)) with per = ceil(num_rows / num_slices), to step *t_dev.  Called
+ * once per step, every row is replayed at least every num_slices steps, so the
+ * ring must hold the hyper-parameters of steps (t - num_slices, t]. */
+int grk_table_adamw_catchup_slice_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
+                                      int64_t num_rows, int dim, int32_t* last, const grk_adamw_hparams* hp_ring,
+                                      int32_t ring_len, const int32_t* t_dev, int32_t num_slices, void* stream);
+
 /* l2_emb term of the BaseLine training script (model/BaseLine/main.py:184-185:
  * loss += l2_emb * torch.norm(item_emb.weight)) for the fused optimizer.
  * grk_table_l2_norm: *norm = ||param||_F (fp64 partial sums over a fixed grid,

@@ -68,7 +68,9 @@ class RefHSTU(torch.nn.Module):
     gated output y are bf16 tensors, and so are their gradients dpre, do, dy;
     the MFMA operands SiLU(q), SiLU(k), SiLU(v) and the gate SiLU(u) are bf16
     values, csrc/grk_hstu.hip k_ng_fwd) -- the checker that separates that
-    rounding from the kernels' math."""
+    rounding from the kernels' math.  With fp8=True the same points as
+    functional._HSTUFp8Fn: SiLU(v|q|k) of the bf16 pre-activation rounded once
+    to e4m3, their gradients stored as bf16."""
 
     def __init__(self, d, h, p, num_buckets, num_time_buckets=0, fp8=False):
         super().__init__()
@@ -85,11 +87,19 @@ class RefHSTU(torch.nn.Module):
         B, T, D = query.shape
         rb = _RoundBF16.apply if self.bf16_core else (lambda x: x)
         u, v, q, k = torch.split(F.silu(rb(self.uvqk(query))), D, dim=-1)
-        if self.bf16_core:   # SiLU(v), SiLU(q), SiLU(k) (MFMA operands) and the gate SiLU(u) are bf16 values
-            u, v, q, k = (x + (x.to(torch.bfloat16).to(x.dtype) - x).detach() for x in (u, v, q, k))
+        r16 = lambda x: x + (x.to(torch.bfloat16).to(x.dtype) - x).detach()
         if self.fp8:
+            # e4m3(SiLU(pre)) in ONE rounding from the fp32 SiLU of the (bf16) pre-activation, as
+            # grk_silu_fp8 does; straight-through gradient.  bf16_core: the gate SiLU(u) is a bf16
+            # value (k_ng_fwd) and the attention's dq / dk / dv are stored as bf16 before
+            # grk_dsilu_mul (rb on the e4m3 values: identity forward, every e4m3 value is a bf16 one)
             r8 = lambda x: x + (x.clamp(-448, 448).to(torch.float8_e4m3fn).to(x.dtype) - x).detach()
             v, q, k = r8(v), r8(q), r8(k)
+            if self.bf16_core:
+                u = r16(u)
+                v, q, k = rb(v), rb(q), rb(k)
+        elif self.bf16_core:   # SiLU(v), SiLU(q), SiLU(k) (MFMA operands) and the gate SiLU(u) are bf16 values
+            u, v, q, k = (r16(x) for x in (u, v, q, k))
         sh = lambda x: x.reshape(B, T, self.num_heads, self.head_dim).transpose(1, 2)
         q, k, v = sh(q), sh(k), sh(v)
         nb = self.rab.shape[1]

@@ -137,6 +137,7 @@ SIGNATURES = {
     'grk_table_adamw_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _P, _I64, _P, _P, C.c_int32, _P, _I, _P]),
     'grk_table_adamw_dense_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _I, _I64, _P, C.c_int32, _P, _P]),
     'grk_table_adamw_catchup_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, _I64, _P, C.c_int32, _P, _P]),
+    'grk_table_adamw_catchup_slice_dev': (_I, [_P, _I, _P, _P, _I64, _I, _P, _P, C.c_int32, _P, C.c_int32, _P]),
     'grk_stamp_rows_dev': (_I, [_P, _P, _P, _I64, _P, _P]),
     'grk_table_l2_norm_workspace': (_SZ, []),
     'grk_table_adamw_ranges_dev': (_I, [_P, _I, _P, _P, _I64, _I, C.POINTER(GrkGradRange), _I, _P, C.c_int32, _P, _P,

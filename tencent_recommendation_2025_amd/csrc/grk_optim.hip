@@ -337,13 +337,19 @@ __global__ void __launch_bounds__(256) k_adamw_ranges(P* __restrict__ param, flo
 // no scalar load per step) and the slot advances without a per-step modulo.
 // Full flush (ids == null): every row once, so the claim is a plain read and
 // store (no atomic) and the row's first vector is loaded before it.
+// Rolling flush (ids == null, num_slices > 1): only slice (t mod num_slices) of
+// the rows, [s * per, (s + 1) * per) with per = ceil(num_rows / num_slices) --
+// one launch per step, captured once in the step's HIP graph, brings every row
+// up at least every num_slices steps at a constant per-step cost (the full
+// flush's spike of every row once per segment, spread evenly).
 constexpr int kCatchupLds = 64;
 template <typename P, int NV>
 __global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, float* __restrict__ m,
                                                        float* __restrict__ v, int64_t num_rows, int dim,
                                                        int32_t* __restrict__ last, const int64_t* __restrict__ ids,
                                                        int64_t num_ids, const grk_adamw_hparams* __restrict__ ring,
-                                                       int ring_len, int t_host, const int32_t* __restrict__ t_dev) {
+                                                       int ring_len, int t_host, const int32_t* __restrict__ t_dev,
+                                                       int num_slices) {
   __shared__ AdamStep steps[kCatchupLds];
   const bool staged = ring_len <= kCatchupLds;
   if (staged) {
@@ -353,8 +359,18 @@ __global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, fl
   const int t = resolve_t(t_host, t_dev);
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (w >= (ids ? num_ids : num_rows)) return;
-  const int64_t row = ids ? ids[w] : w;
+  int64_t row;
+  if (ids) {
+    if (w >= num_ids) return;
+    row = ids[w];
+  } else if (num_slices > 1) {
+    const int64_t per = (num_rows + num_slices - 1) / num_slices;
+    if (w >= per) return;
+    row = (int64_t)(t % num_slices) * per + w;
+  } else {
+    if (w >= num_rows) return;
+    row = w;
+  }
   if (row < 0 || row >= num_rows) return;
   float pv[NV], mv[NV], vv[NV];
   int c = lane * NV;
@@ -506,10 +522,11 @@ static int table_adamw_dense(void* param, int param_dtype, float* exp_avg, float
 static int table_adamw_catchup(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq, int64_t num_rows,
                                int dim, int32_t* last, const int64_t* ids, int64_t num_ids,
                                const grk_adamw_hparams* hp_ring, int32_t ring_len, int32_t t, const int32_t* t_dev,
-                               void* stream) {
+                               void* stream, int32_t num_slices = 1) {
   clear_error();
   GRK_CHECK_ARG(num_rows >= 0 && num_ids >= 0, "num_rows / num_ids must be >= 0");
-  const int64_t waves = ids ? num_ids : num_rows;
+  GRK_CHECK_ARG(num_slices >= 1 && (num_slices == 1 || !ids), "num_slices >= 1 (and > 1 only without ids)");
+  const int64_t waves = ids ? num_ids : (num_rows + num_slices - 1) / num_slices;
   if (waves == 0) return GRK_OK;
   GRK_CHECK_ARG(param && exp_avg && exp_avg_sq && last && hp_ring, "param / moments / last / hp_ring required");
   GRK_CHECK_ARG(param_dtype == GRK_F32 || param_dtype == GRK_BF16, "bad param dtype");
@@ -520,7 +537,8 @@ static int table_adamw_catchup(void* param, int param_dtype, float* exp_avg, flo
   hipStream_t s = (hipStream_t)stream;
   const bool v8 = dim % 8 == 0;
 #define GRK_CU(P, NV) k_adamw_catchup<P, NV><<<g, 256, 0, s>>>((P*)param, exp_avg, exp_avg_sq, num_rows, dim, last, \
-                                                               ids, num_ids, hp_ring, ring_len, t, t_dev)
+                                                               ids, num_ids, hp_ring, ring_len, t, t_dev, \
+                                                               num_slices)
   if (param_dtype == GRK_BF16) { if (v8) GRK_CU(bf16_t, 8); else GRK_CU(bf16_t, 4); }
   else { if (v8) GRK_CU(float, 8); else GRK_CU(float, 4); }
 #undef GRK_CU
@@ -594,6 +612,15 @@ extern "C" int grk_table_adamw_catchup_dev(void* param, int param_dtype, float* 
   if (!t_dev) { set_error("t_dev required"); return GRK_EINVAL; }
   return table_adamw_catchup(param, param_dtype, exp_avg, exp_avg_sq, num_rows, dim, last, ids, num_ids, hp_ring,
                              ring_len, 0, t_dev, stream);
+}
+
+extern "C" int grk_table_adamw_catchup_slice_dev(void* param, int param_dtype, float* exp_avg, float* exp_avg_sq,
+                                                 int64_t num_rows, int dim, int32_t* last,
+                                                 const grk_adamw_hparams* hp_ring, int32_t ring_len,
+                                                 const int32_t* t_dev, int32_t num_slices, void* stream) {
+  if (!t_dev) { set_error("t_dev required"); return GRK_EINVAL; }
+  return table_adamw_catchup(param, param_dtype, exp_avg, exp_avg_sq, num_rows, dim, last, nullptr, 0, hp_ring,
+                             ring_len, 0, t_dev, stream, num_slices);
 }
 
 extern "C" int grk_stamp_rows(int32_t* last, const int64_t* uniq_ids, const int32_t* uniq_count, int64_t max_uniq,

@@ -21,13 +21,30 @@ _disable = torch._dynamo.disable  # ctypes calls: explicit graph breaks under to
 
 # bf16 shadows of fp32 dense weights (optim.DenseFlat registers them): the bf16 copy
 # its AdamW launch writes with every update, read by the GEMMs here instead of a
-# per-step cast of each weight.  id(Parameter) -> (weakref to it, its DenseFlat):
-# keyed by identity (a tensor's == is elementwise, so it cannot key a mapping).
+# per-step cast of each weight.  id(Parameter) -> (weakref to it, weakref to its
+# DenseFlat): keyed by identity (a tensor's == is elementwise, so it cannot key a
+# mapping).  Both references are weak -- the DenseFlat holds its Parameters, so a
+# strong one here would keep every optimizer's parameters, moments and shadow alive
+# for the life of the process -- and a DenseFlat that dies takes its
+# entries with it (weakref.finalize).
 _SHADOWS = {}
 
 
-def register_shadow(p, flat):
-    _SHADOWS[id(p)] = (weakref.ref(p), flat)
+def _drop_shadows(keys, flat_ref):
+    for k in keys:
+        hit = _SHADOWS.get(k)
+        if hit is not None and hit[1] is flat_ref:
+            del _SHADOWS[k]
+
+
+def register_shadows(params, flat):
+    """Register ``flat`` (an optim.DenseFlat) as the bf16 shadow owner of ``params``."""
+    fref = weakref.ref(flat)
+    keys = []
+    for p in params:
+        _SHADOWS[id(p)] = (weakref.ref(p), fref)
+        keys.append(id(p))
+    weakref.finalize(flat, _drop_shadows, keys, fref)
 
 
 def bf16_shadow(weight):
@@ -36,7 +53,8 @@ def bf16_shadow(weight):
     hit = _SHADOWS.get(id(weight))
     if hit is None or hit[0]() is not weight:
         return None
-    return hit[1].shadow_of(weight)
+    flat = hit[1]()
+    return None if flat is None else flat.shadow_of(weight)
 
 # Debug hook (bench.py): when a list, every fused gather appends its launch arguments.
 GATHER_TRACE = None

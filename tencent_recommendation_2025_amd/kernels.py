@@ -359,6 +359,21 @@ def table_adamw_catchup(param, exp_avg, exp_avg_sq, last, hp_ring, t, ids=None):
     L.check(rc, 'grk_table_adamw_catchup')
 
 
+def table_adamw_catchup_slice(param, exp_avg, exp_avg_sq, last, clock, num_slices):
+    """Rolling flush (grk_table_adamw_catchup_slice_dev): bring slice (clock.t mod
+    num_slices) of the rows up to the clock's step -- one launch per step, its slice
+    read on the device, so a captured step replays the right slice every time."""
+    _require_cuda(param, exp_avg, exp_avg_sq, last)
+    rows, D = param.shape
+    if last.dtype != torch.int32 or last.shape != (rows,):
+        raise L.GrkError('last must be an int32 [rows] tensor')
+    rc = L.lib().grk_table_adamw_catchup_slice_dev(param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(),
+                                                   exp_avg_sq.data_ptr(), rows, D, last.data_ptr(), clock.ring.data_ptr(),
+                                                   clock.ring_len, clock.t.data_ptr(), int(num_slices),
+                                                   L.stream_ptr(param.device))
+    L.check(rc, 'grk_table_adamw_catchup_slice')
+
+
 def stamp_rows(last, ids, count, capacity, t):
     """last[ids[:count]] = t (grk_stamp_rows; t may be a DeviceClock)."""
     _require_cuda(last, ids, count)
@@ -684,10 +699,15 @@ def gemm(a, b, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat16,
     return out
 
 
+WGRAD_TRACE = None   # bench.py: a list records the (K, M, N, out_dtype, want_db) of every grk_wgrad call
+
+
 def wgrad(dy, x, out_dtype=torch.float32, want_db=False):
     """grk_wgrad: (dW = dy^T x [M, N] in out_dtype, db = column sums of dy [M] fp32 or None)
     for dy [K, M] and x [K, N] bf16 row-major (the weight / bias gradients of x @ W^T + b)."""
     _require_cuda(dy, x)
+    if WGRAD_TRACE is not None:
+        WGRAD_TRACE.append((dy.shape[0], dy.shape[1], x.shape[1], out_dtype, want_db))
     if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or dy.dim() != 2 or x.dim() != 2:
         raise L.GrkError('wgrad operands must be bf16 2-D matrices')
     if dy.stride(1) != 1 or x.stride(1) != 1 or dy.shape[0] != x.shape[0]:

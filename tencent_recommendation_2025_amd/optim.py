@@ -185,8 +185,14 @@ class DenseFlat:
 
     shadow=True: a bf16 copy of the buffer, written by the same AdamW launch, serves
     the GEMMs' bf16 weight operands (functional.bf16_shadow) instead of a cast kernel
-    per weight and step.  A parameter changed outside the optimizer (load_state_dict,
-    in-place ops: its version counter moves) has its shadow refreshed on next use."""
+    per weight and step.  Writes made outside the optimizer are detected by version
+    counters and the shadow is refreshed before its next use: in-place ops on a
+    parameter (load_state_dict, ``p.mul_``: p's own counter) and writes through ``buf``
+    or any view of it (the counter every view of ``buf`` shares).  One kind of write
+    cannot be seen: through ``p.data`` (a fresh counter each time) -- call
+    ``sync_shadow(force=True)`` after such writes.  Refreshes write the shadow through
+    a ``.data`` alias, so they never bump the counter the shadow views share: a view
+    an earlier GEMM saved for backward stays valid."""
 
     def __init__(self, params, device, shadow=False):
         self.params = list(params)
@@ -206,28 +212,41 @@ class DenseFlat:
             self.shadow = self.buf.to(torch.bfloat16)
             self._index = {id(p): i for i, p in enumerate(self.params)}
             self._versions = [p._version for p in self.params]
-            for p in self.params:
-                G.register_shadow(p, self)
+            self._buf_version = self.buf._version
+            G.register_shadows(self.params, self)
 
-    def sync_shadow(self):
+    def _refresh_all(self):
+        with torch.no_grad():
+            self.shadow.data.copy_(self.buf)
+        self._versions = [p._version for p in self.params]
+        self._buf_version = self.buf._version
+
+    def sync_shadow(self, force=False):
         """Refresh the shadow of every parameter changed outside the optimizer (a
-        graph replay reads the shadow without running the Python forward)."""
-        if self.shadow is not None:
-            for p, ver in zip(self.params, self._versions):
-                if p._version != ver:
-                    self.shadow_of(p)
+        graph replay reads the shadow without running the Python forward);
+        force=True recasts all of it (after writes through ``p.data``)."""
+        if self.shadow is None:
+            return
+        if force or self.buf._version != self._buf_version:
+            self._refresh_all()
+            return
+        for p, ver in zip(self.params, self._versions):
+            if p._version != ver:
+                self.shadow_of(p)
 
     def shadow_of(self, p):
         """bf16 view of p's rows in the shadow buffer, refreshed first if p changed
         outside the optimizer since the shadow last matched it."""
         i = self._index[id(p)]
+        if p.data_ptr() != self._ptrs[i]:
+            return None        # no longer lives in the flat buffer (DenseFlat.step refuses too)
+        if self.buf._version != self._buf_version:
+            self._refresh_all()
         s, e = self.starts[i], self.ends[i]
         view = self.shadow[s:e].view(p.shape)
-        if p._version != self._versions[i] or p.data_ptr() != self._ptrs[i]:
-            if p.data_ptr() != self._ptrs[i]:
-                return None        # no longer lives in the flat buffer (DenseFlat.step refuses too)
+        if p._version != self._versions[i]:
             with torch.no_grad():
-                view.copy_(p.detach())
+                view.data.copy_(p.detach())
             self._versions[i] = p._version
         return view
 
@@ -270,7 +289,7 @@ class FusedAdamW:
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
                  table_dtype=torch.bfloat16, groups=DEFAULT_GROUPS, defer_period=16, l2_emb=0.0, parallel=False,
-                 dense_flat=True):
+                 dense_flat=True, rolling=True):
         """l2_emb > 0: the BaseLine script's ``loss += l2_emb * ||item_emb.weight||_F``
         (model/BaseLine/main.py:184-185) -- ``l2_term()`` gives the loss term (Trainer
         adds it), ``step()`` adds its gradient l2 * W / ||W|| to every item row.  Every
@@ -285,7 +304,18 @@ class FusedAdamW:
         gradient in a step is not moved (torch's rule); its bias correction afterwards
         follows the global step (the device clock) where torch counts each parameter's
         steps -- the same whenever every dense parameter gets a gradient every step, as
-        in the model's training step."""
+        in the model's training step.
+
+        rolling=True (the default since round 5; deferred tables only): the deferred
+        rows are flushed ROLLING -- every step brings one 1/defer_period slice of each
+        deferred table up to date inside the step (grk_table_adamw_catchup_slice_dev,
+        captured with the step), so every row is replayed at least every defer_period
+        steps at a constant per-step cost, instead of all rows at once at every
+        defer_period-th step between graph replays (a ~5.7 ms spike at C2 that made a
+        timed window's cost depend on how many segment starts it held).  Same values
+        bit for bit: a replayed g = 0 step does not depend on when it runs.  The ring
+        then holds 2 x defer_period steps (the pending steps behind a row and the
+        steps ahead)."""
         if table_mode not in ('dense', 'lazy'):
             raise ValueError("table_mode must be 'dense' or 'lazy'")
         self.l2_emb = float(l2_emb)
@@ -341,7 +371,8 @@ class FusedAdamW:
         # The table kernels read the step and its hyper-parameters on the device
         # (K.DeviceClock): the ring holds the steps of the current segment,
         # refilled at segment starts from alternating pinned buffers.
-        self.clock = K.DeviceClock(self.defer or 16, dev) if cuda else None
+        self.rolling = bool(rolling) and bool(self._deferred)
+        self.clock = K.DeviceClock((2 if self.rolling else 1) * (self.defer or 16), dev) if cuda else None
         if self.clock is not None:
             self._pinned = [torch.zeros_like(self.clock.ring, device='cpu').pin_memory() for _ in range(2)]
             self._uploads = 0
@@ -364,8 +395,14 @@ class FusedAdamW:
     def _hp(self, step):
         return K.adamw_hparams(self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, step)
 
+    @property
+    def _period(self):
+        """Steps between segment starts (ring refills; full flushes unless rolling)."""
+        return self.clock.ring_len // 2 if self.rolling else self.clock.ring_len
+
     def _upload_ring(self, t):
-        """Hyper-parameters of steps t+1 .. t+ring_len into the device ring (slot s % ring_len)."""
+        """Hyper-parameters of steps t+1 .. t+period into the device ring (slot s % ring_len);
+        rolling: also steps t-period+1 .. t, which rows behind by up to a period replay."""
         n = self.clock.ring_len
         k = self._uploads % 2  # alternate buffers; the host may run many (graph-replayed) steps ahead
         self._uploads += 1
@@ -375,7 +412,8 @@ class FusedAdamW:
         if done[k] is not None:
             done[k].synchronize()  # the copy out of this buffer two segments ago has run
         buf = self._pinned[k]
-        for step in range(t + 1, t + n + 1):
+        lo = t - n // 2 + 1 if self.rolling else t + 1
+        for step in range(max(lo, 1), lo + n):
             hp = self._hp(step)
             buf[step % n] = torch.tensor([getattr(hp, f) for f, _ in hp._fields_], dtype=torch.float32)
         self.clock.ring.copy_(buf, non_blocking=True)
@@ -383,8 +421,9 @@ class FusedAdamW:
         done[k].record()
 
     def _segment(self, t):
-        """Start a new segment at step t: bring every deferred row to t, refill the ring."""
-        if self._seg is not None and self._seg < t:
+        """Start a new segment at step t: bring every deferred row to t (not when rolling:
+        the per-step slices do), refill the ring."""
+        if self._seg is not None and self._seg < t and not self.rolling:
             for g in self._deferred.values():
                 K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock)
         self._upload_ring(t)
@@ -396,7 +435,7 @@ class FusedAdamW:
         the optimizer (load_state_dict between graph replays)."""
         if self._flat is not None:
             self._flat.sync_shadow()
-        if self.clock is not None and (self._seg is None or self.t - self._seg >= self.clock.ring_len):
+        if self.clock is not None and (self._seg is None or self.t - self._seg >= self._period):
             self._segment(self.t)
 
     def graph_replayed(self):
@@ -422,6 +461,8 @@ class FusedAdamW:
         item, user = K.batch_row_ids(*batch[:4], with_user='user' in self._deferred)
         ids = {'item': item, 'user': user}
         for name, g in self._deferred.items():
+            if self.rolling:   # this step's slice of every row
+                K.table_adamw_catchup_slice(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self.clock, self._period)
             K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock, ids[name])
         self._begun = self.t
 

@@ -107,10 +107,12 @@ class FetchSink:
 class ShardExchange:
     """Routes ids / rows / gradients of one row-sharded table."""
 
-    def __init__(self, name, shard, dim, pg=None, gather_fn=kernel_gather):
+    def __init__(self, name, shard, dim, pg=None, gather_fn=kernel_gather, global_rows=None):
         self.name, self.shard, self.dim, self.pg = name, shard, dim, pg
         self.world = dist.get_world_size(pg)
         self.rank = dist.get_rank(pg)
+        # rows of the whole table (ids past it are refused); default: this shard's rows x world
+        self.global_rows = int(global_rows) if global_rows is not None else shard.shape[0] * self.world
         self.gather_fn = gather_fn
         self.plan = None
 
@@ -118,7 +120,9 @@ class ShardExchange:
     def _stable_sort(keys, bound):
         """(sorted keys, permutation) of int64 keys in [0, bound): grk's radix sort on the
         GPU (a few launches over ceil(log2 bound) bits; torch.sort runs ~30 rocprim
-        merge-sort launches here), torch.sort on the CPU."""
+        merge-sort launches here), torch.sort on the CPU.  Keys outside [0, bound) are
+        mis-ordered by the radix sort: route() counts out-of-range ids on the device
+        and prepare() raises on them at the step's host read of the split sizes."""
         if not keys.is_cuda or bound >= (1 << 31):
             return torch.sort(keys, stable=True)
         n = keys.numel()
@@ -137,6 +141,9 @@ class ShardExchange:
         the stable owner order lists every real id first.  n_uniq reaches the
         host as sum(send_counts) with the split sizes."""
         n = ids.numel()
+        # ids a shard cannot hold (negative, or past the last global row): counted here,
+        # raised by prepare() when the counts reach the host (no sync of its own)
+        bad = ((ids < 0) | (ids >= self.global_rows)).sum()
         srt, perm = self._stable_sort(ids, self.shard.shape[0] * self.world + self.world)
         head = torch.ones_like(srt, dtype=torch.bool)
         if n > 1:
@@ -162,7 +169,7 @@ class ShardExchange:
         recv_counts = torch.empty_like(send_counts)
         a2a(recv_counts, send_counts, pg=self.pg if pg is None else pg)
         return dict(uniq=uniq, inverse=inverse, order=order, send_ids=send_ids, send_counts=send_counts,
-                    recv_counts=recv_counts)
+                    recv_counts=recv_counts, bad=bad)
 
     def fetch(self, r, send_split, recv_split, before_gather=None, out=None):
         """Phase 2: ids to owners, owners gather, rows back; returns rows in slot (owner) order.
@@ -338,7 +345,8 @@ class ShardedFusedAdamW(FusedAdamW):
                 shard = full[self.rank::self.world].to(dtype=table_dtype).contiguous()
             grp = TableGroup(f'{name}@{self.rank}', [(name, _Holder(shard))], table_dtype, dev)
             grp.global_rows = emb.num_embeddings
-            self.shards[name] = (grp, ShardExchange(name, grp.flat, emb.embedding_dim, pg, gather_fn))
+            self.shards[name] = (grp, ShardExchange(name, grp.flat, emb.embedding_dim, pg, gather_fn,
+                                                     global_rows=emb.num_embeddings))
             # the full table is not kept: this rank holds rows rank::world only
             emb.weight = torch.nn.Parameter(torch.empty(0, emb.embedding_dim, dtype=table_dtype, device=dev),
                                             requires_grad=False)
@@ -402,7 +410,10 @@ class ShardedFusedAdamW(FusedAdamW):
             ids = torch.cat([v().reshape(-1) for _, _, _, v in plist])
             routed[name] = self.shards[name][1].route(ids, pg)
         counts = torch.stack([torch.stack([r['send_counts'], r['recv_counts']]) for r in routed.values()])
-        return routed, counts
+        # one more [2, world] block: [0][0] = ids out of every table's range (read with the counts)
+        flag = torch.zeros_like(counts[:1])
+        flag[0, 0, 0] = sum(r['bad'] for r in routed.values())
+        return routed, torch.cat([counts, flag])
 
     def prefetch(self, batch):
         """Route a coming batch ahead of its step (own communicator for the counts):
@@ -461,6 +472,9 @@ class ShardedFusedAdamW(FusedAdamW):
         else:
             routed, counts = self._route_all(batch, self.pg)
             counts = counts.cpu().tolist()  # the one host sync of the step: all-to-all split sizes
+        if counts[-1][0][0]:
+            raise ValueError(f'row-sharded lookup: {counts[-1][0][0]} ids outside [0, rows) of their table')
+        counts = counts[:-1]
         self.maybe_segment()
         remaps = {}
         self.sinks = {}

@@ -203,6 +203,7 @@ class Trainer:
         self._cap = None         # jagged capacity of the current step (set by step(), cleared after it)
         self._jag_err = None     # jagged layout error flags, OR-ed over steps (int32 [1], device)
         self._err_host = None    # pinned copy of the flags, polled every ERR_POLL graph replays
+        self._err_evt = None     # event after the copy into _err_host (None: no copy in flight)
         self._replays = 0
 
     def _graph_blocker(self):
@@ -263,7 +264,7 @@ class Trainer:
             self.check_jagged()   # eager: one host sync per step
         return loss.detach()
 
-    ERR_POLL = 16
+    ERR_POLL = 4
 
     def check_jagged(self):
         """Raise ValueError if any jagged layout so far flagged an error (host sync)."""
@@ -271,18 +272,26 @@ class Trainer:
             J.check_error(self._jag_err)
 
     def _poll_jagged(self):
-        """Graph replays: copy the flags to pinned memory every ERR_POLL replays and
-        check the copy made ERR_POLL replays earlier (no host wait)."""
+        """Graph replays: every ERR_POLL replays (one copy in flight at a time) the flags
+        are copied to pinned memory behind an event; the copy is read only once its
+        event has completed (event query: no host wait).  An error (e.g. a jagged
+        capacity overflow from under-stated ``rows``: the trailing spans were dropped)
+        therefore raises within about ERR_POLL + the host's lead in replays -- those
+        steps have trained on the truncated batch.  check_jagged() reads the flags
+        synchronously."""
         if self._jag_err is None:
             return
         self._replays += 1
-        if self._replays % self.ERR_POLL:
-            return
-        if self._err_host is None:
-            self._err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
-        elif int(self._err_host[0]):
-            J.check_error(self._err_host)
-        self._err_host.copy_(self._jag_err, non_blocking=True)
+        if self._err_evt is not None and self._err_evt.query():
+            self._err_evt = None
+            if int(self._err_host[0]):
+                J.check_error(self._err_host)
+        if self._err_evt is None and self._replays % self.ERR_POLL == 0:
+            if self._err_host is None:
+                self._err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+            self._err_host.copy_(self._jag_err, non_blocking=True)
+            self._err_evt = torch.cuda.Event()
+            self._err_evt.record()
 
     def step(self, batch, next_batch=None, rows=None):
         """One training step; ``next_batch`` (optional) is the batch of the following

@@ -1,0 +1,217 @@
+"""The benched configuration at its OWN size against the oracle.
+
+``bench.py`` times BASELINE config 2: O1 + HSTU d=512 (8 heads x hd 64), 4 blocks,
+maxlen 200 (T = 201), 1M-item and 1M-user bf16 tables, the jagged (span-row)
+layout, bf16 autocast GEMMs, the grouped MFMA projections, the merged
+projected-row backward, the flat dense AdamW and the deferred dense-parity table
+AdamW.  Here exactly that model and optimizer take ONE training step at B = 8
+(dropout 0: the oracle cannot draw grk's dropout masks) and are compared with
+``oracle/model_ref.py`` -- the fp32 torch-CPU restatement of the reference step
+(``model/BaseLine/main.py:163-190``: forward, BCE, backward, ``torch.optim.AdamW``
+with betas (0.9, 0.98), weight decay 0.01) -- on the same parameters and batch:
+
+* loss, logits, every gradient (dense parameters and each table, padding rows
+  excluded), and every parameter after the update (deferred rows flushed);
+* the error budget is the reference's own mixed precision: the oracle step run
+  under CPU bf16 autocast (the reference's ``--use_amp``, ``main.py:139-141,173``)
+  is measured against the fp32 oracle on the same inputs, and grk may not exceed
+  BENCH_AMP_FACTOR x that (or a floor, stated per quantity);
+* rows the batch does not touch take the g = 0 AdamW step (decay only): after the
+  flush they must equal the fp32 oracle's rows rounded to bf16 BIT FOR BIT.
+
+HSTU has no reference implementation: the oracle's HSTU (``oracle/hstu.py``) is
+the HSTU paper restated (parity unpinned against the reference).
+"""
+import contextlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import model_ref
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+B, MAXLEN, D, HEADS, BLOCKS = 8, 200, 512, 8, 4
+ITEMS = USERS = 1_000_000
+LR, BETAS, EPS, WD = 1e-3, (0.9, 0.98), 1e-8, 0.01
+
+# Bounds.  loss: the north star's 1e-3.  Everything else: BENCH_AMP_FACTOR x the
+# AMP reference's own error on the same quantity, or the floor when that is smaller.
+BENCH_AMP_FACTOR = 1.5
+LOSS_TOL = 1e-3
+LOGIT_FLOOR = 5e-3
+GRAD_FLOOR = 2.5e-2          # as the reduced-size test (tests/test_gpu_model.py): HSTU rab sums
+UPDATE_FLOOR = 2.5e-2        # the AdamW step-1 update is ~lr * sign(g): sign flips where |g| ~ its error
+
+
+def nrel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    d = np.linalg.norm(b)
+    return float(np.linalg.norm(a - b) / (d if d > 0 else 1.0))
+
+
+def oracle_setup(seed=5):
+    """The fp32 oracle model at the bench configuration with live parameters (reference
+    init, then LayerNorm gains 1 and small random biases / rab: the reference init
+    zeroes them, which makes the first step's logits identically zero), tables
+    rounded to bf16 (the fused optimizer stores them so)."""
+    from tencent_recommendation_2025_amd import synthetic as S
+    cfg = S.SyntheticConfig(batch_size=B, maxlen=MAXLEN, num_items=ITEMS, num_users=USERS)
+    stats, types = S.feature_schema(cfg)
+    args = S.make_args(hidden_units=D, maxlen=MAXLEN, num_blocks=BLOCKS, num_heads=HEADS, dropout_rate=0.0)
+    ref = model_ref.RefBaselineModel(USERS, ITEMS, stats, types, args, variant='o1', block='hstu')
+    model_ref.init_params(ref, seed=seed)
+    g = torch.Generator().manual_seed(seed + 1)
+    tables = ('item_emb', 'user_emb', 'pos_emb', 'sparse_emb.')
+    with torch.no_grad():
+        for n, p in ref.named_parameters():
+            if p.dim() == 1 and 'norm' in n and n.endswith('weight'):
+                p.fill_(1.0)
+            elif p.dim() == 1:
+                p.copy_(0.02 * torch.randn(p.shape, generator=g))
+            elif n.endswith('.rab'):
+                p.copy_(0.3 * torch.randn(p.shape, generator=g))
+            if n.startswith(tables):
+                p.copy_(p.bfloat16().float())
+    return cfg, stats, types, args, ref
+
+
+def oracle_step(ref, cpu, bf16):
+    """One oracle forward + BCE + backward (fp32, or under CPU bf16 autocast): loss,
+    logits and every parameter gradient."""
+    ref.zero_grad(set_to_none=True)
+    ctx = torch.autocast('cpu', dtype=torch.bfloat16) if bf16 else contextlib.nullcontext()
+    with ctx:
+        pl, nl = ref(cpu[0], cpu[1], cpu[2], cpu[3], cpu[4], cpu[6], cpu[7], cpu[8])
+        loss = model_ref.bce_loss(pl.float(), nl.float(), cpu[4])
+    loss.backward()
+    grads = {n: p.grad.detach().clone() for n, p in ref.named_parameters() if p.grad is not None}
+    return loss.detach(), pl.detach().float(), nl.detach().float(), grads
+
+
+def adamw_step1_update(p, g):
+    """The first torch AdamW step's change of p (m_hat = g, v_hat = g^2): restated
+    to price the AMP reference's gradient error in parameter space."""
+    return -LR * WD * p - LR * g / (g.abs() + EPS)
+
+
+def _table_rows(grp, key, n):
+    off = grp.offsets[key]
+    return off, off + n
+
+
+def test_bench_config_full_size_step_matches_oracle():
+    from tencent_recommendation_2025_amd import functional as G
+    from tencent_recommendation_2025_amd import jagged as J
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.model import BaselineModel
+    from tencent_recommendation_2025_amd.optim import FusedAdamW
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    cfg, stats, types, args, ref = oracle_setup()
+    before = {k: v.detach().clone() for k, v in ref.state_dict().items()}
+    m = BaselineModel(USERS, ITEMS, stats, types, args).to(DEV)
+    m.load_state_dict(ref.state_dict())
+    m.train()
+    opt = FusedAdamW(m, lr=LR, betas=BETAS, eps=EPS, weight_decay=WD)   # bench defaults: dense_flat, defer 16
+    assert opt._flat is not None and set(opt._deferred) == {'item', 'user'}
+    batch = S.make_batch(cfg, torch.Generator(device=DEV).manual_seed(7), DEV)
+
+    # the fused trainer's eager step (train.Trainer.compute_loss, jagged layout, quantum 512),
+    # opened up to keep the logits and the gradients before the update
+    opt.zero_grad()
+    opt.begin_step(batch)
+    tt = batch[3]
+    n_span = J.span_rows(tt)
+    jag = J.layout(tt, J.capacity_for(n_span, 512), batch[4])
+    seq, pos, neg, tt_j, ntt, _nat, sf, pf, nf, _ts, pidx = J.compact(batch, jag)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        h, pe, ne = m.encode(seq, pos, neg, tt_j, sf, pf, nf, jagged=jag, pos_idx=pidx)
+        loss = G.bce_loss(h, pe, ne, ntt)
+    pl, nl = G.pair_logits(h.detach().float(), pe.detach().float(), ne.detach().float(), ntt)
+    loss.backward()
+    J.check_error(jag.err)
+    grads = {n: p.grad.float().cpu() for n, p in m.named_parameters() if p.grad is not None}
+    tgrads = {}
+    for grp in opt.groups:
+        dg = grp.dense_gradient()
+        for key in grp.offsets:
+            rows = dict(m.table_modules())[key].num_embeddings
+            lo, hi = _table_rows(grp, key, rows)
+            tgrads[f'{key}.weight'] = dg[lo + 1:hi].cpu()          # padding row excluded
+        del dg
+    opt.step()
+    opt.flush()
+    after = {k: v.detach().float().cpu() for k, v in m.state_dict().items()}
+    torch.cuda.synchronize()
+
+    # the oracle: fp32 step, AMP step, then torch AdamW on the fp32 gradients
+    cpu = [x.cpu() if torch.is_tensor(x) else {k: v.cpu() for k, v in x.items()} for x in batch]
+    aloss, apl, anl, agrad = oracle_step(ref, cpu, bf16=True)
+    rloss, rpl, rnl, rgrad = oracle_step(ref, cpu, bf16=False)
+    torch.optim.AdamW(ref.parameters(), lr=LR, betas=BETAS, eps=EPS, weight_decay=WD).step()
+    rafter = {k: v.detach() for k, v in ref.state_dict().items()}
+
+    rm = jag.row_map.cpu().long()
+    live = rm >= 0
+    assert int(live.sum()) == n_span
+    pl, nl = pl.cpu().reshape(-1)[live], nl.cpu().reshape(-1)[live]
+    sel = rm[live]
+    rpl, rnl, apl, anl = (x.reshape(-1)[sel] for x in (rpl, rnl, apl, anl))
+    errs = {'loss': abs(loss.item() - rloss.item()) / abs(rloss.item()),
+            'logits': max(nrel(pl, rpl), nrel(nl, rnl))}
+    amp = {'loss': abs(aloss.item() - rloss.item()) / abs(rloss.item()),
+           'logits': max(nrel(apl, rpl), nrel(anl, rnl))}
+
+    # gradients: every dense parameter and every table (padding row excluded)
+    g_err, g_amp = {}, {}
+    for n, want in rgrad.items():
+        is_table = n.startswith(('item_emb', 'user_emb', 'pos_emb', 'sparse_emb.'))
+        got = tgrads[n] if is_table else grads[n]
+        w = want[1:] if is_table else want
+        a = agrad[n][1:] if is_table else agrad[n]
+        if float(w.norm()) == 0:
+            assert float(got.norm()) == 0, n
+            continue
+        g_err[n] = nrel(got, w)
+        g_amp[n] = nrel(a.float(), w)
+    assert set(g_err) | {n for n in rgrad if n not in g_err} == set(rgrad)
+    assert len(rgrad) == sum(1 for _ in ref.parameters())
+
+    # parameters after the update: grk (bf16 tables, fp32 dense) vs the oracle rounded
+    # alike; the change is compared (the parameters themselves are mostly unchanged)
+    u_err, u_amp, exact_rows = {}, {}, {}
+    for n, p0 in before.items():
+        is_table = n.startswith(('item_emb', 'user_emb', 'pos_emb', 'sparse_emb.'))
+        want = rafter[n].bfloat16().float() if is_table else rafter[n]
+        du_grk = after[n] - p0
+        du_ref = want - p0
+        if n in agrad:
+            du_amp = adamw_step1_update(p0, agrad[n].float())
+            du_fp = adamw_step1_update(p0, rgrad[n])
+            u_amp[n] = nrel(du_amp, du_fp)
+        else:
+            u_amp[n] = 0.0
+        u_err[n] = nrel(du_grk, du_ref)
+        if n in ('item_emb.weight', 'user_emb.weight'):
+            untouched = rgrad[n].abs().amax(1) == 0        # g = 0 rows: decay only, deferred then flushed
+            untouched[0] = False
+            exact_rows[n] = (int(untouched.sum()),
+                             int((after[n][untouched] != want[untouched]).any(1).sum()))
+    worst_g = sorted(((e, g_amp[k], k) for k, e in g_err.items()), reverse=True)[:6]
+    worst_u = sorted(((e, u_amp[k], k) for k, e in u_err.items()), reverse=True)[:6]
+    print(f'bench-size step (B={B}, {n_span} span rows): grk {errs}, AMP {amp}')
+    print('  worst grads (grk, amp, name):', worst_g)
+    print('  worst updates (grk, amp, name):', worst_u)
+    print('  untouched table rows (count, mismatching):', exact_rows)
+
+    assert errs['loss'] < LOSS_TOL, (errs, amp)
+    assert errs['logits'] <= max(BENCH_AMP_FACTOR * amp['logits'], LOGIT_FLOOR), (errs, amp)
+    over = [(k, e, g_amp[k]) for k, e in g_err.items() if e > max(BENCH_AMP_FACTOR * g_amp[k], GRAD_FLOOR)]
+    assert not over, over
+    over = [(k, e, u_amp[k]) for k, e in u_err.items() if e > max(BENCH_AMP_FACTOR * u_amp[k], UPDATE_FLOOR)]
+    assert not over, over
+    for n, (cnt, bad) in exact_rows.items():
+        assert cnt > ITEMS // 2 and bad == 0, (n, cnt, bad)

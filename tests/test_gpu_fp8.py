@@ -4,6 +4,8 @@ attention.  The fp8 layer quantises its SiLU'd v|q|k to OCP e4m3 once
 straight-through at the quantiser (grk_dsilu_mul).  The oracle
 (oracle/model_ref.RefHSTU(fp8=True)) rounds the same activations to e4m3 with
 the same straight-through gradient, in fp32 everywhere else."""
+import contextlib
+
 import numpy as np
 import pytest
 import torch
@@ -77,36 +79,89 @@ def _c5_models(B, blocks, seed=5):
     return cfg, m, ref
 
 
+# Bounds of the C5 model step (the round-4 bounds -- loss 1e-2, logits
+# 5e-2, attention gradients 0.15 -- came from comparing bf16 activations rounded to e4m3
+# with fp32 ones rounded to e4m3, where e4m3 flips dominate).  Now:
+# * the fp32 model against the oracle fed the core's own rounding points (RefHSTU
+#   bf16_core + fp8: bf16 pre-activation, e4m3(SiLU) in one rounding, bf16 gate, o, y
+#   and gradients) -- what is left is the kernels' math and the rare e4m3 flips of the
+#   hardware SiLU's last bit (tests/test_silu_fp8_and_dsilu_mul: < 1e-3 of elements);
+# * the bf16-autocast model (the bench's) against the fp32 oracle, held to the oracle's
+#   own bf16-autocast error (the reference's --use_amp), as the bench-config tests.
+C5_CORE_TOL = dict(loss=1e-3, logits=5e-3, grad=2e-2)
+C5_AMP_FACTOR = 1.5
+C5_AMP_FLOOR = dict(logits=5e-3, grad=2.5e-2)
+
+
+def _c5_oracles(ref, cpu):
+    """(fp32 oracle, bf16-core oracle, AMP oracle): loss, logits, gradients of each."""
+    out = {}
+    for mode in ('fp32', 'core', 'amp'):
+        for blk in ref.attention_layers:
+            blk.bf16_core = mode == 'core'
+        ref.zero_grad(set_to_none=True)
+        ctx = torch.autocast('cpu', dtype=torch.bfloat16) if mode == 'amp' else contextlib.nullcontext()
+        with ctx:
+            rpl, rnl = ref(cpu[0], cpu[1], cpu[2], cpu[3], cpu[4], cpu[6], cpu[7], cpu[8])
+            rloss = model_ref.bce_loss(rpl.float(), rnl.float(), cpu[4])
+        rloss.backward()
+        out[mode] = (rloss.item(), rpl.detach().float(), rnl.detach().float(),
+                     {n: p.grad.detach().float().clone() for n, p in ref.named_parameters() if p.grad is not None})
+    for blk in ref.attention_layers:
+        blk.bf16_core = False
+    return out
+
+
+def _c5_errors(loss, pl, nl, grads, want):
+    wl, wpl, wnl, wg = want
+    e = {'loss': abs(loss - wl) / abs(wl), 'logits': max(nrel(pl, wpl), nrel(nl, wnl))}
+    g = {n: nrel(grads[n], w) for n, w in wg.items() if float(w.norm()) > 0}
+    return e, g
+
+
 def test_c5_fp8_model_step_matches_oracle():
     """C5 shape (d=1024 = 8 heads x 128, T=1025) at reduced B=2 and 2 blocks: the
-    drop-in model with fp8 HSTU layers (bf16 autocast GEMMs) against the fp32
-    oracle with the same e4m3 rounding of q/k/v: loss, logits and every dense
-    gradient.  The bound is the bf16 autocast gap plus the e4m3 rounding flips
-    it causes (the oracle rounds its fp32 activations, the model its bf16 ones)."""
+    drop-in model with fp8 HSTU layers against the oracle with the same e4m3
+    rounding of q/k/v: loss, logits and EVERY gradient, twice -- the fp32 model
+    against the oracle fed the core's rounding points (C5_CORE_TOL), the bf16
+    autocast model against the fp32 oracle within its AMP reference's error."""
     from tencent_recommendation_2025_amd import functional as G
     from tencent_recommendation_2025_amd import synthetic as S
     cfg, m, ref = _c5_models(B=2, blocks=2)
     batch = S.make_batch(cfg, torch.Generator(device=DEV).manual_seed(7), DEV)
     seq, pos, neg, tt, ntt, _nat, sf, pf, nf = batch
-    m.train()
-    with torch.autocast('cuda', dtype=torch.bfloat16):
-        h, pe, ne = m.encode(seq, pos, neg, tt, sf, pf, nf)
-        loss = G.bce_loss(h, pe, ne, ntt)
-    pl, nl = G.pair_logits(h.detach().float(), pe.detach().float(), ne.detach().float(), ntt)
-    loss.backward()
     cpu = [x.cpu() if torch.is_tensor(x) else {k: v.cpu() for k, v in x.items()} for x in batch]
-    rpl, rnl = ref(cpu[0], cpu[1], cpu[2], cpu[3], cpu[4], cpu[6], cpu[7], cpu[8])
-    rloss = model_ref.bce_loss(rpl, rnl, cpu[4])
-    rloss.backward()
-    errs = {'loss': abs(loss.item() - rloss.item()) / abs(rloss.item()),
-            'logits': max(nrel(pl.cpu(), rpl.detach()), nrel(nl.cpu(), rnl.detach()))}
-    rp = dict(ref.named_parameters())
-    grads = {n: nrel(p.grad.float().cpu(), rp[n].grad) for n, p in m.named_parameters()
-             if p.grad is not None and 'attention_layers' in n}
-    errs['attn_grad'] = max(grads.values())
-    print('C5 fp8 step errors:', errs, sorted(grads.items(), key=lambda kv: -kv[1])[:6])
-    assert np.isfinite(loss.item())
-    assert errs['loss'] < 1e-2 and errs['logits'] < 5e-2 and errs['attn_grad'] < 0.15, errs
+    want = _c5_oracles(ref, cpu)
+    m.train()
+    res = {}
+    for amp in (False, True):
+        m.zero_grad(set_to_none=True)
+        ctx = torch.autocast('cuda', dtype=torch.bfloat16) if amp else contextlib.nullcontext()
+        with ctx:
+            h, pe, ne = m.encode(seq, pos, neg, tt, sf, pf, nf)
+            loss = G.bce_loss(h, pe, ne, ntt)
+        pl, nl = G.pair_logits(h.detach().float(), pe.detach().float(), ne.detach().float(), ntt)
+        loss.backward()
+        assert np.isfinite(loss.item())
+        res[amp] = (loss.item(), pl.cpu(), nl.cpu(),
+                    {n: p.grad.float().cpu() for n, p in m.named_parameters() if p.grad is not None})
+    # (1) fp32 model vs the bf16-core oracle
+    e, g = _c5_errors(*res[False], want['core'])
+    worst = sorted(g.items(), key=lambda kv: -kv[1])[:6]
+    print('C5 fp32 model vs bf16-core fp8 oracle:', e, 'worst grads', worst)
+    assert len(want['core'][3]) == sum(1 for _ in ref.parameters())   # every parameter's gradient compared
+    assert e['loss'] < C5_CORE_TOL['loss'] and e['logits'] < C5_CORE_TOL['logits'], e
+    bad = {k: v for k, v in g.items() if v >= C5_CORE_TOL['grad']}
+    assert not bad, bad
+    # (2) bf16-autocast model vs the fp32 oracle, within the AMP oracle's own error
+    e, g = _c5_errors(*res[True], want['fp32'])
+    ea, ga = _c5_errors(*want['amp'], want['fp32'])
+    print('C5 autocast model vs fp32 oracle:', e, '; AMP oracle:', ea)
+    print('   worst grads (grk, amp):', sorted(((v, ga.get(k), k) for k, v in g.items()), reverse=True)[:6])
+    assert e['loss'] < 1e-3, (e, ea)
+    assert e['logits'] <= max(C5_AMP_FACTOR * ea['logits'], C5_AMP_FLOOR['logits']), (e, ea)
+    over = [(k, v, ga[k]) for k, v in g.items() if v > max(C5_AMP_FACTOR * ga[k], C5_AMP_FLOOR['grad'])]
+    assert not over, over
 
 
 def test_c5_fp8_trainer_graph_equals_eager():

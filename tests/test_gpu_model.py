@@ -433,11 +433,13 @@ def test_fused_trainer_bf16_hstu_learns():
     assert losses[-1] < losses[0] - 0.05, losses
 
 
-@pytest.mark.parametrize('period', [1, 3])
-def test_deferred_table_updates_are_bit_identical_to_dense(period):
+@pytest.mark.parametrize('period,rolling', [(1, False), (3, False), (1, True), (3, True), (4, True)])
+def test_deferred_table_updates_are_bit_identical_to_dense(period, rolling):
     """FusedAdamW(defer_period=k): rows outside the batch replayed when next
-    read / every k steps / before state_dict == moving every row every step,
-    bit for bit (tables and moments), across several segment boundaries."""
+    read / every k steps (rolling: a 1/k slice of the rows every step) / before
+    state_dict == moving every row every step, bit for bit (tables and moments),
+    across several segment boundaries.  Rolling: no row ever lags more than k
+    steps behind."""
     from tencent_recommendation_2025_amd import synthetic as S
     from tencent_recommendation_2025_amd.model import BaselineModel
     from tencent_recommendation_2025_amd.optim import FusedAdamW
@@ -449,11 +451,16 @@ def test_deferred_table_updates_are_bit_identical_to_dense(period):
     for defer in (0, period):
         torch.manual_seed(0)
         m = BaselineModel(cfg.num_users, cfg.num_items, stats, types, args).to(DEV)
-        opt = FusedAdamW(m, lr=2e-3, defer_period=defer)
+        opt = FusedAdamW(m, lr=2e-3, defer_period=defer, rolling=rolling)
+        assert opt.rolling == (rolling and defer > 0)
         tr = Trainer(m, opt, loss='bce')
         g = torch.Generator(device=DEV).manual_seed(0)
-        for _ in range(7):
+        for _ in range(9):
             tr.step(S.make_batch(cfg, g, DEV))
+            if opt.rolling:
+                for grp in opt._deferred.values():
+                    lag = opt.t - int(grp.last[1:].min())
+                    assert lag <= period, (opt.t, lag)
         sd = m.state_dict()  # flushes deferred rows first
         torch.cuda.synchronize()
         runs.append((sd, {grp.name: (grp.exp_avg.clone(), grp.exp_avg_sq.clone()) for grp in opt.groups}))

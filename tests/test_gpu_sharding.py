@@ -241,3 +241,37 @@ def test_sharded_jagged_equals_sharded_padded_and_graph_replay(pg):
     for k in runs['fused_jagged'][2]:
         torch.testing.assert_close(runs['jagged'][2][k].float(), runs['fused_jagged'][2][k].float(), rtol=1e-3,
                                    atol=2e-5, msg=k)
+
+def test_sharded_dense_flat_equals_torch_adamw_and_shadows_match(pg):
+    """the row-sharded optimizer's dense parameters on the flat multi-range
+    AdamW (dense_flat=True, the default: gradients are views of the all-reduce
+    buckets, bf16 GEMM shadows written by the update) against dense_flat=False
+    (torch's fused AdamW) over 4 bf16 steps: losses, and the parameters after the first step, within the flat
+    update's few-ulp deviation (hardware sqrt / reciprocal), and every
+    shadow == its parameter rounded to bf16, bit for bit."""
+    from tencent_recommendation_2025_amd import functional as G
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.sharding import ShardedFusedAdamW
+    from tencent_recommendation_2025_amd.train import Trainer
+    runs = []
+    for flat in (True, False):
+        m, cfg = build()
+        opt = ShardedFusedAdamW(m, lr=2e-3, defer_period=3, dense_flat=flat)
+        assert (opt._flat is not None) == flat
+        tr = Trainer(m, opt, loss='bce')
+        g = torch.Generator(device=DEV).manual_seed(0)
+        losses, first = [], None
+        for i in range(4):
+            losses.append(tr.step(S.make_batch(cfg, g, DEV)).item())
+            if i == 0:   # parameters after step 1 (same gradients in both runs)
+                first = {k: v.float().clone() for k, v in m.state_dict().items()}
+        if flat:
+            for p in opt._flat.params:
+                assert torch.equal(G.bf16_shadow(p), p.detach().bfloat16())
+        runs.append((losses, first))
+    (l1, s1), (l2, s2) = runs
+    assert all(abs(a - b) < 1e-3 * max(1.0, abs(b)) for a, b in zip(l1, l2)), (l1, l2)
+    for k in s1:
+        if k in ('item_emb.weight', 'user_emb.weight'):
+            continue
+        torch.testing.assert_close(s1[k], s2[k], rtol=2e-3, atol=1e-4, msg=k)

@@ -341,3 +341,47 @@ def test_split_pair_joins_adjacent_gradients_without_a_copy():
     assert torch.equal(gx, buf) and gx.data_ptr() == buf.data_ptr()     # a view of the joint buffer
     gx, = torch.autograd.grad((a, b), (x,), (ga.clone(), gb.clone()))
     assert torch.equal(gx, buf)
+
+
+def test_dense_flat_shadow_registry_does_not_keep_parameters_alive():
+    """the bf16-shadow registry held each DenseFlat (and through it
+    the Parameters, the flat buffer, both moments and the shadow) for the life of the
+    process.  Dropping the parameters and the DenseFlat must free them and clear
+    their registry entries."""
+    import gc
+    import weakref
+    from tencent_recommendation_2025_amd import functional as G
+    from tencent_recommendation_2025_amd import optim as O
+    ps = [torch.nn.Parameter(torch.randn(4, 8)), torch.nn.Parameter(torch.randn(16))]
+    keys = [id(p) for p in ps]
+    flat = O.DenseFlat(ps, 'cpu', shadow=True)
+    assert all(k in G._SHADOWS for k in keys)
+    assert torch.equal(G.bf16_shadow(ps[0]), ps[0].detach().bfloat16())
+    wp, wf = weakref.ref(ps[0]), weakref.ref(flat)
+    del ps, flat
+    gc.collect()
+    assert wp() is None and wf() is None
+    assert not any(k in G._SHADOWS for k in keys)
+
+
+def test_dense_flat_shadow_follows_writes_outside_the_optimizer():
+    """the bf16 shadow tracks in-place writes to a parameter (its own version
+    counter) and writes through the flat buffer or any view of it (the counter the
+    views share); writes through ``p.data`` need sync_shadow(force=True).  A refresh
+    never bumps the counter the shadow views share, so a shadow view saved for
+    backward before the refresh stays usable."""
+    from tencent_recommendation_2025_amd import functional as G
+    from tencent_recommendation_2025_amd import optim as O
+    ps = [torch.nn.Parameter(torch.randn(4, 8)), torch.nn.Parameter(torch.randn(2, 8))]
+    flat = O.DenseFlat(ps, 'cpu', shadow=True)
+    s1 = G.bf16_shadow(ps[1])
+    saved_version = s1._version
+    with torch.no_grad():
+        ps[0].mul_(3.0)                                    # in place on the parameter
+    assert torch.equal(G.bf16_shadow(ps[0]), ps[0].detach().bfloat16())
+    flat.buf[4:6].add_(1.0)                                # through the flat buffer (= ps[1]'s rows)
+    assert torch.equal(G.bf16_shadow(ps[1]), ps[1].detach().bfloat16())
+    ps[1].data.copy_(torch.full((2, 8), 0.25))             # invisible to version counters ...
+    flat.sync_shadow(force=True)                           # ... hence the explicit refresh
+    assert torch.equal(G.bf16_shadow(ps[1]), torch.full((2, 8), 0.25, dtype=torch.bfloat16))
+    assert s1._version == saved_version                    # refreshes did not bump the shared counter

@@ -41,8 +41,11 @@ def _worker(rank, world, port, out_q):
         ids = torch.randint(0, R, (257,), generator=g)
         ids[:20] = 0                       # padding
         ids[20:60] = 7                     # hot row shared by both ranks
-        ex = ShardExchange('t', shard, D, gather_fn=torch_gather)
+        ex = ShardExchange('t', shard, D, gather_fn=torch_gather, global_rows=R)
         r = ex.route(ids)
+        assert int(r['bad']) == 0
+        # ids outside [0, R) are counted (prepare() raises on the count)
+        assert int(ex.route(torch.tensor([-1, R, 5, R - 1]))['bad']) == 2
         counts = torch.stack([r['send_counts'], r['recv_counts']]).tolist()
         fetched = ex.fetch(r, counts[0], counts[1])
         ok_fetch = torch.equal(fetched[r['inverse']], full[ids])
