@@ -638,6 +638,25 @@ int grk_gemm_ex(int trans_a, int trans_b, int64_t m, int64_t n, int64_t k, const
                 int64_t ldb, int ab_dtype, void* c, int64_t ldc, int c_dtype, const void* c_in, float alpha,
                 float beta, const void* bias, int bias_dtype, int epilogue, void* stream);
 
+/* grk's own MFMA GEMM (csrc/grk_mgemm.hip), which grk_gemm / grk_gemm_ex run for
+ * every shape grk_gemm_mfma_supported accepts (hipBLASLt for the rest; env
+ * GRK_GEMM_BACKEND=hipblaslt forces hipBLASLt).  Replaces the bf16-autocast
+ * forward and input-gradient products of the dense layers
+ * (model/BaseLine/model.py:129-139,302-309 and the HSTU uvqk / out_linear):
+ *   C[m, n] = act(A . op(B) + bias[n] + C_in[m, n]),  A [m, k] (lda) bf16,
+ *   b_layout 0: B [n, k] (ldb) -> op(B) = B^T;  1: B [k, n] (ldb) -> op(B) = B;
+ *   C bf16 or fp32 (ldc); C_in NULL or a C-shaped matrix of C's dtype and ldc
+ *   (may be C itself: accumulate); bias NULL or [n] fp32 / bf16; act by
+ *   GRK_GEMM_EP_*.  n, k, lda, ldb, ldc multiples of 8, pointers 16-byte aligned;
+ *   fp32 accumulation, one rounding at the store, deterministic.
+ * grk_gemm_mfma_supported: 1 when a grk_gemm_ex call with these arguments runs
+ * here (trans_a 0, alpha 1, beta 0 or 1). */
+int grk_gemm_mfma_supported(int trans_a, int b_layout, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb,
+                            int64_t ldc, int c_dtype, float alpha, float beta);
+int grk_gemm_mfma(int b_layout, int64_t m, int64_t n, int64_t k, const void* a, int64_t lda, const void* b,
+                  int64_t ldb, void* c, int64_t ldc, int c_dtype, const void* c_in, const void* bias, int bias_dtype,
+                  int epilogue, void* stream);
+
 /* Number of hipBLASLt candidates grk_gemm times for each NEW shape (1..256,
  * default 256; env GRK_GEMM_TUNE at load).  1 = the heuristic's first pick,
  * with no timing: the same kernel in every process. */

@@ -177,6 +177,8 @@ SIGNATURES = {
     'grk_rq_assign': (_I, [_P, _I64, _P, _I64, _I, _I, _I, _P, _P, _P, _P, _P]),
     'grk_gemm': (_I, [_I, _I, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _I, _P, _F, _F, _P, _I, _P]),
     'grk_gemm_ex': (_I, [_I, _I, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _I, _P, _F, _F, _P, _I, _I, _P]),
+    'grk_gemm_mfma_supported': (_I, [_I, _I, _I64, _I64, _I64, _I64, _I64, _I64, _I, _F, _F]),
+    'grk_gemm_mfma': (_I, [_I, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _I, _P, _P, _I, _I, _P]),
     'grk_pair_logits_partials': (_SZ, [_I64]),
     'grk_sampled_softmax_workspace': (_SZ, [_I64, _I]),
     'grk_sampled_softmax_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _I, _F, _P, _P, _P, _P, _P, _SZ, _P]),

@@ -293,6 +293,17 @@ extern "C" int grk_gemm_ex(int trans_a, int trans_b, int64_t m, int64_t n, int64
   GRK_CHECK_ARG(!bias || bias_dtype == GRK_BF16 || bias_dtype == GRK_F32, "bias must be bf16 or fp32");
   GRK_CHECK_ARG(lda >= (trans_a ? m : k) && ldb >= (trans_b ? k : n) && ldc >= n, "leading dimension too small");
   GRK_CHECK_ARG(k > 0 || beta == 1.0f || bias, "k == 0 needs beta == 1 or a bias");
+  // grk's own MFMA GEMM (grk_mgemm.hip) for every shape it takes -- the dense layers'
+  // forward and input-gradient products; hipBLASLt for the rest (transposed A, other
+  // alpha / beta).  GRK_GEMM_BACKEND=hipblaslt forces hipBLASLt (A/B runs).
+  static const bool force_blas = [] {
+    const char* e = getenv("GRK_GEMM_BACKEND");
+    return e && strcmp(e, "hipblaslt") == 0;
+  }();
+  if (!force_blas && grk_gemm_mfma_supported(trans_a, trans_b ? 0 : 1, m, n, k, lda, ldb, ldc, c_dtype, alpha, beta) &&
+      ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c | (uintptr_t)c_in | (uintptr_t)bias) % 16 == 0)
+    return grk_gemm_mfma(trans_b ? 0 : 1, m, n, k, a, lda, b, ldb, c, ldc, c_dtype,
+                         beta == 1.0f ? (c_in ? c_in : c) : nullptr, bias, bias_dtype, epilogue, stream);
   int dev = 0;
   GRK_CHECK_HIP(hipGetDevice(&dev));
   hipStream_t s = (hipStream_t)stream;
