@@ -34,6 +34,8 @@
 //    8 consecutive columns -- bias / C_in reads and the bf16 stores are 16-byte
 //    vectors over whole 128-B row segments (from registers they would be 2-byte
 //    scattered stores).
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "grk_common.h"
@@ -43,16 +45,23 @@
 namespace grk {
 namespace {
 
-constexpr int kMgK = 64;                         // K per ring stage
+// K-contiguous images: rows of BK k (RB = 2 BK bytes), 16-byte chunk c of row r at
+// slot c ^ mg_swz<RB>(r) -- conflict-free for the fragment reads (lane l reads row
+// l & 31, so each ds_read_b128 lane group, {0-3, 12-15, 20-27}-shaped, covers 16
+// rows whose (bank row, slot) pairs the swizzle makes distinct).
+template <int RB>
+__device__ __forceinline__ int mg_swz(int row) {
+  if constexpr (RB == 128) return (row >> 1) & 7;
+  else return (row >> 2) & 3;
+}
 
-__device__ __forceinline__ int mg_swz(int row) { return (row >> 1) & 7; }
-
-template <int BM, int BN, int WM, int WN, int NST, bool BNC>
+template <int BM, int BN, int WM, int WN, int NST, bool BNC, int BK>
 struct MgGeo {
   static constexpr int NW = WM * WN, NT = 64 * NW;
-  static constexpr int IMGA = BM * 128;                       // [BM][64] bf16
-  static constexpr int RBB = BNC ? 2 * BN : 128;              // B image row bytes
-  static constexpr int IMGB = BNC ? kMgK * RBB : BN * 128;    // [64][BN] or [BN][64]
+  static constexpr int RBA = 2 * BK;                          // K-contiguous image row bytes
+  static constexpr int IMGA = BM * RBA;                       // [BM][BK] bf16
+  static constexpr int RBB = BNC ? 2 * BN : RBA;              // B image row bytes
+  static constexpr int IMGB = BNC ? BK * RBB : BN * RBA;      // [BK][BN] or [BN][BK]
   static constexpr int STAGE = IMGA + IMGB;
   static constexpr int PWA = IMGA / 1024 / NW, PWB = IMGB / 1024 / NW;
   static constexpr int P = PWA + PWB;                         // DMA instructions per wave and stage
@@ -63,18 +72,21 @@ struct MgGeo {
   static_assert(NST >= 2 && NST * STAGE <= 160 * 1024, "ring too large for the LDS");
   static_assert(NW * 32 * SROW * 4 <= NST * STAGE, "epilogue stage must fit in the ring");
   static_assert(WTN % 32 == 0 && WTM % 32 == 0 && (WTN / 8) <= 64, "wave tile");
+  static_assert(BK == 32 || BK == 64, "BK: 32 or 64");
 };
 
 // Natural k order (B K-contiguous): element j of lane (r, h) = img[row][k0 + 8h + j].
+template <int RB>
 __device__ __forceinline__ uint4 mg_chunk(const char* img, int row, int c) {
-  return *reinterpret_cast<const uint4*>(img + row * 128 + 16 * (c ^ mg_swz(row)));
+  return *reinterpret_cast<const uint4*>(img + row * RB + 16 * (c ^ mg_swz<RB>(row)));
 }
 
 // ring_frag's k order (beside an N-contiguous B): element j of lane (r, h) =
 // img[row][k0 + 8(j >> 2) + 4h + (j & 3)]: two 8-byte halves of chunks c0, c0 + 1.
+template <int RB>
 __device__ __forceinline__ uint4 mg_chunk_perm(const char* img, int row, int c0, int h) {
-  const uint2 lo = *reinterpret_cast<const uint2*>(img + row * 128 + 16 * (c0 ^ mg_swz(row)) + 8 * h);
-  const uint2 hi = *reinterpret_cast<const uint2*>(img + row * 128 + 16 * ((c0 + 1) ^ mg_swz(row)) + 8 * h);
+  const uint2 lo = *reinterpret_cast<const uint2*>(img + row * RB + 16 * (c0 ^ mg_swz<RB>(row)) + 8 * h);
+  const uint2 hi = *reinterpret_cast<const uint2*>(img + row * RB + 16 * ((c0 + 1) ^ mg_swz<RB>(row)) + 8 * h);
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
 
@@ -123,9 +135,10 @@ struct MgArgs {
   int total;            // tiles of the launch
 };
 
-template <int BM, int BN, int WM, int WN, int NST, bool BNC, typename OT>
+template <int BM, int BN, int WM, int WN, int NST, bool BNC, int BK, typename OT>
 __global__ void __launch_bounds__(64 * WM * WN) k_mgemm(MgArgs g) {
-  using G = MgGeo<BM, BN, WM, WN, NST, BNC>;
+  using G = MgGeo<BM, BN, WM, WN, NST, BNC, BK>;
+  constexpr int RBA = G::RBA, CPR = RBA / 16, RPI = 1024 / RBA;   // chunks per row, rows per DMA instruction
   __shared__ __attribute__((aligned(16))) char smem[NST * G::STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % WM, wn = w / WM, r = lane & 31, hh = lane >> 5;
@@ -135,7 +148,7 @@ __global__ void __launch_bounds__(64 * WM * WN) k_mgemm(MgArgs g) {
   const unsigned logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + phys / 8;
   const int m0 = (int)(logical / g.tiles_n) * BM, n0 = (int)(logical % g.tiles_n) * BN;
   const int M = g.M, N = g.N, K = g.K;
-  const int nsteps = (K + kMgK - 1) / kMgK;
+  const int nsteps = (K + BK - 1) / BK;
   // DMA sources of this lane (rows clamped into the matrices: their outputs are not stored)
   // (K-contiguous images: row base + this lane's chunk column; a chunk past K -- the
   // last step's tail -- reads the row's last chunk instead, never past the row's end,
@@ -145,25 +158,25 @@ __global__ void __launch_bounds__(64 * WM * WN) k_mgemm(MgArgs g) {
   int acol[G::PWA], bcol[G::PWB];
 #pragma unroll
   for (int i = 0; i < G::PWA; ++i) {
-    const int q = w * G::PWA + i, row = 8 * q + (lane >> 3);     // 8 rows of 128 B per instruction
+    const int q = w * G::PWA + i, row = RPI * q + lane / CPR;     // RPI rows of RBA bytes per instruction
     const int ma = min(m0 + row, M - 1);
     pa[i] = g.a + (int64_t)ma * g.lda;
-    acol[i] = 8 * ((lane & 7) ^ mg_swz(row));
+    acol[i] = 8 * ((lane % CPR) ^ mg_swz<RBA>(row));
   }
 #pragma unroll
   for (int i = 0; i < G::PWB; ++i) {
     const int q = w * G::PWB + i;
     if constexpr (BNC) {
-      constexpr int CPR = G::RBB / 16;                            // chunks per k row
-      const int row = q * (1024 / G::RBB) + lane / CPR;
-      const int nb = n0 + 8 * ((lane % CPR) ^ wg_swz(row));
+      constexpr int CPB = G::RBB / 16;                            // chunks per k row
+      const int row = q * (1024 / G::RBB) + lane / CPB;
+      const int nb = n0 + 8 * ((lane % CPB) ^ wg_swz(row));
       bcol[i] = row;                                              // the image row (k) of this lane
       pb[i] = g.b + (nb < N ? nb : 0);
     } else {
-      const int row = 8 * q + (lane >> 3);
+      const int row = RPI * q + lane / CPR;
       const int nb = min(n0 + row, N - 1);
       pb[i] = g.b + (int64_t)nb * g.ldb;
-      bcol[i] = 8 * ((lane & 7) ^ mg_swz(row));
+      bcol[i] = 8 * ((lane % CPR) ^ mg_swz<RBA>(row));
     }
   }
   const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane(
@@ -171,7 +184,7 @@ __global__ void __launch_bounds__(64 * WM * WN) k_mgemm(MgArgs g) {
   const unsigned wu = (unsigned)__builtin_amdgcn_readfirstlane(w);
   auto issue = [&](int step, int buf) {
     const unsigned base = lds0 + buf * G::STAGE;
-    const int k0 = step * kMgK;
+    const int k0 = step * BK;
 #pragma unroll
     for (int i = 0; i < G::PWA; ++i) wg_dma16(pa[i] + min(k0 + acol[i], K - 8), base + (wu * G::PWA + i) * 1024);
 #pragma unroll
@@ -190,24 +203,24 @@ __global__ void __launch_bounds__(64 * WM * WN) k_mgemm(MgArgs g) {
 #pragma unroll
     for (int j = 0; j < G::TJ; ++j) acc[i][j] = acc_zero();
 
-  // one 64-deep step; MASK: the K tail (chunks at k >= K read as zeros)
+  // one BK-deep step; MASK: the K tail (chunks at k >= K read as zeros)
   auto compute = [&](const char* ia, const char* ib, int kvalid, auto mask_tag) {
     constexpr bool MASK = decltype(mask_tag)::value;
 #pragma unroll
-    for (int ks = 0; ks < kMgK / 16; ++ks) {
+    for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 fa[G::TI], fb[G::TJ];
 #pragma unroll
       for (int i = 0; i < G::TI; ++i) {
         const int row = wm * G::WTM + 32 * i + r;
         uint4 v;
         if constexpr (BNC) {
-          v = mg_chunk_perm(ia, row, 2 * ks, hh);
+          v = mg_chunk_perm<RBA>(ia, row, 2 * ks, hh);
           if (MASK) {
             if (8 * (2 * ks) >= kvalid) v.x = v.y = 0u;
             if (8 * (2 * ks + 1) >= kvalid) v.z = v.w = 0u;
           }
         } else {
-          v = mg_chunk(ia, row, 2 * ks + hh);
+          v = mg_chunk<RBA>(ia, row, 2 * ks + hh);
           if (MASK && 8 * (2 * ks + hh) >= kvalid) v = make_uint4(0u, 0u, 0u, 0u);
         }
         fa[i] = __builtin_bit_cast(bf16x8, v);
@@ -217,7 +230,7 @@ __global__ void __launch_bounds__(64 * WM * WN) k_mgemm(MgArgs g) {
         if constexpr (BNC) {
           fb[j] = ring_frag<G::RBB>(ib, 16 * ks, wn * G::WTN + 32 * j, lane);
         } else {
-          uint4 v = mg_chunk(ib, wn * G::WTN + 32 * j + r, 2 * ks + hh);
+          uint4 v = mg_chunk<RBA>(ib, wn * G::WTN + 32 * j + r, 2 * ks + hh);
           if (MASK && 8 * (2 * ks + hh) >= kvalid) v = make_uint4(0u, 0u, 0u, 0u);
           fb[j] = __builtin_bit_cast(bf16x8, v);
         }
@@ -230,14 +243,14 @@ __global__ void __launch_bounds__(64 * WM * WN) k_mgemm(MgArgs g) {
   };
 
   for (int t = 0; t < NST - 1 && t < nsteps; ++t) issue(t, t);
-  const bool tail = K % kMgK != 0;
+  const bool tail = K % BK != 0;
   for (int t = 0; t < nsteps; ++t) {
     ring_wait<G::P, NST>(nsteps - 1 - t);
     if (t + NST - 1 < nsteps) issue(t + NST - 1, (t + NST - 1) % NST);
     const char* ia = smem + (t % NST) * G::STAGE;
     const char* ib = ia + G::IMGA;
-    if (tail && t == nsteps - 1) compute(ia, ib, K - t * kMgK, std::true_type{});
-    else compute(ia, ib, kMgK, std::false_type{});
+    if (tail && t == nsteps - 1) compute(ia, ib, K - t * BK, std::true_type{});
+    else compute(ia, ib, BK, std::false_type{});
   }
   __syncthreads();   // every wave is done reading the ring: its LDS holds the epilogue stages
 
@@ -289,15 +302,23 @@ __global__ void __launch_bounds__(64 * WM * WN) k_mgemm(MgArgs g) {
   }
 }
 
-// Tile configuration: 256 x 128, 8 waves of 64 x 64, 3 stages (144 KiB of LDS,
-// one workgroup per CU; 170-194 VGPRs).  (256 x 256 with 128 x 64 wave tiles
-// spills at the 256-VGPR cap of two waves per SIMD.)
+// Tile configuration: 256 x 128, 8 waves of 64 x 64, one workgroup per CU (144 KiB
+// of LDS, 170-194 VGPRs): 32-deep K steps in a 6-stage ring (4 steps in flight:
+// at ~90 FLOP per staged byte a CU needs ~110 KB of loads in flight to cover an
+// LDS-DMA's ~1.1 us) -- or, GRK_MGEMM_CFG=1, 64-deep steps in 3 stages (one step
+// in flight, for A/B).  (256 x 256 with 128 x 64 wave tiles spills at the
+// 256-VGPR cap of two waves per SIMD.)
 template <bool BNC, typename OT>
 hipError_t launch(const MgArgs& a0, hipStream_t s) {
+  static const int cfg = [] {
+    const char* e = getenv("GRK_MGEMM_CFG");
+    return e ? atoi(e) : 0;
+  }();
   MgArgs a = a0;
   a.tiles_n = (a.N + 127) / 128;
   a.total = ((a.M + 255) / 256) * a.tiles_n;
-  k_mgemm<256, 128, 4, 2, 3, BNC, OT><<<(unsigned)a.total, 512, 0, s>>>(a);
+  if (cfg == 1) k_mgemm<256, 128, 4, 2, 3, BNC, 64, OT><<<(unsigned)a.total, 512, 0, s>>>(a);
+  else k_mgemm<256, 128, 4, 2, 6, BNC, 32, OT><<<(unsigned)a.total, 512, 0, s>>>(a);
   return hipGetLastError();
 }
 

@@ -88,7 +88,11 @@ def _c5_models(B, blocks, seed=5):
 #   hardware SiLU's last bit (tests/test_silu_fp8_and_dsilu_mul: < 1e-3 of elements);
 # * the bf16-autocast model (the bench's) against the fp32 oracle, held to the oracle's
 #   own bf16-autocast error (the reference's --use_amp), as the bench-config tests.
-C5_CORE_TOL = dict(loss=1e-3, logits=5e-3, grad=2e-2)
+# measured on MI355X (round 5, gpurun_out r5a): core loss 3.2e-6, logits 9.0e-5, gradients
+# <= 1.7e-3 (the rab and uvqk weight of the second block); autocast loss 1.2e-4 (AMP 1.1e-5),
+# logits 2.8e-3 (AMP 2.8e-3), gradients <= 9.5e-2 (AMP <= 9.8e-2: the user-side feature
+# tables at B = 2, one token per row)
+C5_CORE_TOL = dict(loss=1e-4, logits=1e-3, grad=5e-3)
 C5_AMP_FACTOR = 1.5
 C5_AMP_FLOOR = dict(logits=5e-3, grad=2.5e-2)
 
@@ -158,7 +162,7 @@ def test_c5_fp8_model_step_matches_oracle():
     ea, ga = _c5_errors(*want['amp'], want['fp32'])
     print('C5 autocast model vs fp32 oracle:', e, '; AMP oracle:', ea)
     print('   worst grads (grk, amp):', sorted(((v, ga.get(k), k) for k, v in g.items()), reverse=True)[:6])
-    assert e['loss'] < 1e-3, (e, ea)
+    assert e['loss'] < 1e-3, (e, ea)                                        # the north star's loss bound
     assert e['logits'] <= max(C5_AMP_FACTOR * ea['logits'], C5_AMP_FLOOR['logits']), (e, ea)
     over = [(k, v, ga[k]) for k, v in g.items() if v > max(C5_AMP_FACTOR * ga[k], C5_AMP_FLOOR['grad'])]
     assert not over, over

@@ -42,7 +42,7 @@ def test_mgemm_matches_torch(m, n, k, layout):
     from tencent_recommendation_2025_amd import kernels as K
     g = torch.Generator(device=DEV).manual_seed(m + 7 * n + 13 * k + layout)
     a, b, ref = _operands(m, n, k, layout, g, pad=24)
-    assert L.lib().grk_gemm_mfma_supported(0, layout, m, n, k, a.stride(0), b.stride(0), n, L.BF16, 1.0, 0.0)
+    assert L.lib().grk_gemm_mfma_supported(0, layout, m, n, k, a.stride(0), b.stride(0), n, L.GRK_BF16, 1.0, 0.0)
     bias = torch.randn(n, device=DEV, generator=g)
     y = K.gemm(a, b, trans_b=layout == 0)
     assert torch.isfinite(y).all()
