@@ -62,17 +62,16 @@ if __name__ == '__main__':
         run()
         sys.exit(0)
     res = {}
-    for backend in ('mfma', 'hipblaslt'):
-        env = dict(os.environ)
-        if backend == 'hipblaslt':
-            env['GRK_GEMM_BACKEND'] = 'hipblaslt'
+    variants = {'mfma': {}, 'mfma_bk64': {'GRK_MGEMM_CFG': '1'}, 'hipblaslt': {'GRK_GEMM_BACKEND': 'hipblaslt'}}
+    for name, extra in variants.items():
+        env = dict(os.environ, **extra)
         r = subprocess.run([sys.executable, __file__, 'one'], env=env, capture_output=True, text=True, timeout=600)
         if r.returncode:
             print(r.stderr[-3000:])
             sys.exit(r.returncode)
-        res[backend] = json.loads(r.stdout.strip().splitlines()[-1])
-    print(f'{"shape":18s} {"M":>6s} {"N":>5s} {"K":>5s} {"mfma us":>8s} {"TF/s":>6s} {"hipblaslt":>9s} {"TF/s":>6s}')
+        res[name] = json.loads(r.stdout.strip().splitlines()[-1])
+    print(f'{"shape":18s} {"M":>6s} {"N":>5s} {"K":>5s}' + ''.join(f' {v:>10s} {"TF/s":>5s}' for v in variants))
     for name, m, n, k, _ in SHAPES:
         f = 2.0 * m * n * k
-        a, b = res['mfma'][name], res['hipblaslt'][name]
-        print(f'{name:18s} {m:6d} {n:5d} {k:5d} {a:8.1f} {f / a / 1e6:6.0f} {b:9.1f} {f / b / 1e6:6.0f}')
+        print(f'{name:18s} {m:6d} {n:5d} {k:5d}' + ''.join(f' {res[v][name]:10.1f} {f / res[v][name] / 1e6:5.0f}'
+                                                        for v in variants))
