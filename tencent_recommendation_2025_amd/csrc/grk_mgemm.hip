@@ -135,8 +135,14 @@ struct MgArgs {
   int total;            // tiles of the launch
 };
 
+// Waves per SIMD the register budget is cut for: 2 for 8-wave (and 4-wave, two per
+// CU) workgroups, 4 for 16-wave ones; with 4 the fragment reads of the next 16-deep
+// k slice are not hoisted over the current slice's MFMAs (sched_barrier), which
+// keeps the kernel inside 128 VGPRs (the other waves of the SIMD cover the latency).
+template <int WM, int WN> constexpr int mg_waves_per_simd() { return WM * WN >= 16 ? 4 : 2; }
+
 template <int BM, int BN, int WM, int WN, int NST, bool BNC, int BK, typename OT>
-__global__ void __launch_bounds__(64 * WM * WN) k_mgemm(MgArgs g) {
+__global__ void __launch_bounds__(64 * WM * WN, (mg_waves_per_simd<WM, WN>())) k_mgemm(MgArgs g) {
   using G = MgGeo<BM, BN, WM, WN, NST, BNC, BK>;
   constexpr int RBA = G::RBA, CPR = RBA / 16, RPI = 1024 / RBA;   // chunks per row, rows per DMA instruction
   __shared__ __attribute__((aligned(16))) char smem[NST * G::STAGE];
@@ -239,6 +245,7 @@ __global__ void __launch_bounds__(64 * WM * WN) k_mgemm(MgArgs g) {
       for (int i = 0; i < G::TI; ++i)
 #pragma unroll
         for (int j = 0; j < G::TJ; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
+      if constexpr (mg_waves_per_simd<WM, WN>() >= 4 || G::TI * G::TJ >= 8) __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -302,23 +309,36 @@ __global__ void __launch_bounds__(64 * WM * WN) k_mgemm(MgArgs g) {
   }
 }
 
-// Tile configuration: 256 x 128, 8 waves of 64 x 64, one workgroup per CU (144 KiB
-// of LDS, 170-194 VGPRs): 32-deep K steps in a 6-stage ring (4 steps in flight:
-// at ~90 FLOP per staged byte a CU needs ~110 KB of loads in flight to cover an
-// LDS-DMA's ~1.1 us) -- or, GRK_MGEMM_CFG=1, 64-deep steps in 3 stages (one step
-// in flight, for A/B).  (256 x 256 with 128 x 64 wave tiles spills at the
-// 256-VGPR cap of two waves per SIMD.)
+// Tile configurations (every wave owns 64 x 64 = 2 x 2 MFMA tiles; 32-deep K steps;
+// at ~90-128 FLOP per staged byte a CU needs ~85-110 KB of LDS-DMA in flight to cover
+// a DMA's ~1.1 us, hence deep rings):
+//   cfg 2: 256 x 128, 8 waves, 6 stages (144 KiB, one workgroup per CU);
+//   cfg 3: 256 x 256, 16 waves, 5 stages (160 KiB, one workgroup per CU);
+//   cfg 4: 128 x 128, 4 waves, 4 stages (64 KiB, two workgroups per CU);
+//   cfg 1: 256 x 128 with 64-deep steps in 3 stages (one step in flight);
+//   cfg 5: 256 x 256, 8 waves of 128 x 64, 5 stages.
+// (A 256 x 256 tile of 8 waves with 128 x 64 wave tiles spills at the 256-VGPR cap of
+// two waves per SIMD.)  Default (cfg 0): chosen per shape below; GRK_MGEMM_CFG forces one.
 template <bool BNC, typename OT>
 hipError_t launch(const MgArgs& a0, hipStream_t s) {
-  static const int cfg = [] {
+  static const int force = [] {
     const char* e = getenv("GRK_MGEMM_CFG");
     return e ? atoi(e) : 0;
   }();
   MgArgs a = a0;
-  a.tiles_n = (a.N + 127) / 128;
-  a.total = ((a.M + 255) / 256) * a.tiles_n;
-  if (cfg == 1) k_mgemm<256, 128, 4, 2, 3, BNC, 64, OT><<<(unsigned)a.total, 512, 0, s>>>(a);
-  else k_mgemm<256, 128, 4, 2, 6, BNC, 32, OT><<<(unsigned)a.total, 512, 0, s>>>(a);
+  int cfg = force;
+  if (cfg < 1 || cfg > 5) cfg = 2;
+  const int bm = cfg == 4 ? 128 : 256, bn = (cfg == 3 || cfg == 5) ? 256 : 128;
+  a.tiles_n = (a.N + bn - 1) / bn;
+  a.total = ((a.M + bm - 1) / bm) * a.tiles_n;
+  const unsigned g = (unsigned)a.total;
+  switch (cfg) {
+    case 1: k_mgemm<256, 128, 4, 2, 3, BNC, 64, OT><<<g, 512, 0, s>>>(a); break;
+    case 3: k_mgemm<256, 256, 4, 4, 5, BNC, 32, OT><<<g, 1024, 0, s>>>(a); break;
+    case 5: k_mgemm<256, 256, 2, 4, 5, BNC, 32, OT><<<g, 512, 0, s>>>(a); break;
+    case 4: k_mgemm<128, 128, 2, 2, 4, BNC, 32, OT><<<g, 256, 0, s>>>(a); break;
+    default: k_mgemm<256, 128, 4, 2, 6, BNC, 32, OT><<<g, 512, 0, s>>>(a); break;
+  }
   return hipGetLastError();
 }
 
