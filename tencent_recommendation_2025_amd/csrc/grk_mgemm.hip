@@ -250,14 +250,19 @@ __global__ void __launch_bounds__(64 * WM * WN, (mg_waves_per_simd<WM, WN>())) k
   };
 
   for (int t = 0; t < NST - 1 && t < nsteps; ++t) issue(t, t);
-  const bool tail = K % BK != 0;
-  for (int t = 0; t < nsteps; ++t) {
+  // full steps in the loop, the K tail (if any) peeled after it: one compute body
+  // in the loop keeps the accumulators in fixed registers
+  const int nfull = K / BK;
+  for (int t = 0; t < nfull; ++t) {
     ring_wait<G::P, NST>(nsteps - 1 - t);
     if (t + NST - 1 < nsteps) issue(t + NST - 1, (t + NST - 1) % NST);
     const char* ia = smem + (t % NST) * G::STAGE;
-    const char* ib = ia + G::IMGA;
-    if (tail && t == nsteps - 1) compute(ia, ib, K - t * BK, std::true_type{});
-    else compute(ia, ib, BK, std::false_type{});
+    compute(ia, ia + G::IMGA, BK, std::false_type{});
+  }
+  if (nfull < nsteps) {
+    ring_wait<G::P, NST>(0);
+    const char* ia = smem + (nfull % NST) * G::STAGE;
+    compute(ia, ia + G::IMGA, K - nfull * BK, std::true_type{});
   }
   __syncthreads();   // every wave is done reading the ring: its LDS holds the epilogue stages
 
