@@ -379,8 +379,11 @@ int wgrad_splits(int64_t K, int64_t M, int64_t N) {
 
 // Kernel plan of a shape: which ring (kind 0: the register-staged kernel, K not a
 // multiple of 32; 1: 128 x 128 tiles, two workgroups per CU; 2: 256 x 128 tiles, one
-// 8-wave workgroup per CU, for M >= 1024 -- the uvqk weight gradients), the tile and
-// the K split.  GRK_WGRAD_RING=1 / 2 forces a ring where it applies (A/B builds).
+// 8-wave workgroup per CU, for M >= 1024 -- the uvqk weight gradients; 3: grk_mgemm's
+// K-major mode, the default since round 5: 256 x 128 tiles of 8 waves, a 6-stage ring,
+// the slices of one K range on one XCD), the tile and the K split.
+// GRK_WGRAD_RING=1 / 2 forces a ring where it applies (A/B builds), GRK_WGRAD_MGEMM=0
+// the round-4 kernels.
 struct WgPlan {
   int kind, tm, tn, S;
 };
@@ -390,8 +393,19 @@ WgPlan wgrad_plan(int64_t K, int64_t M, int64_t N) {
     return e ? atoi(e) : -1;
   }();
   static const bool force_reg = getenv("GRK_WGRAD_REG") != nullptr;
+  static const bool mgemm = [] {
+    const char* e = getenv("GRK_WGRAD_MGEMM");
+    return !(e && atoi(e) == 0);
+  }();
   WgPlan p{0, kWgTile, kWgTile, wgrad_splits(K, M, N)};
   if (K % kWgK || force_reg) return p;
+  if (mgemm && force < 0) {
+    // one workgroup per CU: slices until the launch has >= 256 workgroups, >= 256 rows each
+    p = WgPlan{3, 256, 128, 1};
+    const int64_t tiles = ((M + 255) / 256) * ((N + 127) / 128);
+    while (p.S < 64 && tiles * p.S < 256 && K >= (int64_t)p.S * 2 * 256) p.S *= 2;
+    return p;
+  }
   const bool big = force == 2 || (force != 1 && M >= 1024);
   if (!big) {
     p.kind = 1;
@@ -404,6 +418,10 @@ WgPlan wgrad_plan(int64_t K, int64_t M, int64_t N) {
 }
 
 }  // namespace
+
+int mgemm_wgrad(const bf16_t* dy, int64_t ld_dy, const bf16_t* x, int64_t ld_x, int K, int M, int N, int S, int kchunk,
+                float* part, float* dbpart, hipStream_t s);   // grk_mgemm.hip
+
 }  // namespace grk
 
 using namespace grk;
@@ -442,7 +460,10 @@ extern "C" int grk_wgrad(const void* dy, int64_t ld_dy, const void* x, int64_t l
     if (db) KERN<true><<<grid, THREADS, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, dbp); \
     else KERN<false><<<grid, THREADS, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, nullptr); \
   } while (0)
-  if (pl.kind == 2) {
+  if (pl.kind == 3) {
+    const int rc = mgemm_wgrad(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, S, kchunk, part, db ? dbp : nullptr, s);
+    if (rc) return rc;
+  } else if (pl.kind == 2) {
     if (db) k_wgrad_lds<true, 4, 2, 6><<<grid, 512, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, dbp);
     else k_wgrad_lds<false, 4, 2, 6><<<grid, 512, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part,
                                                           nullptr);
