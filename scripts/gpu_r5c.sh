@@ -17,4 +17,9 @@ timeout -k 10 400 python -u scripts/microbench/mgemm.py > $O/mgemm_bench.txt 2>&
 echo "mgemm bench rc=$?" >> $O/summary.txt
 timeout -k 10 300 python -u scripts/microbench/wgrad_ab.py > $O/wgrad_ab.txt 2>&1
 echo "wgrad ab rc=$?" >> $O/summary.txt
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
+  SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --kernel-include-regex "k_mgemm" --output-format csv \
+  -d /tmp/sqm -o run -- python -u scripts/microbench/mgemm.py eager > $O/sq.log 2>&1
+echo "sq rc=$?" >> $O/summary.txt
+cp $(find /tmp/sqm -name "*counter_collection.csv" | head -1) $O/sq_mgemm.csv 2>/dev/null
 cat $O/summary.txt; cat $O/mgemm_bench.txt $O/wgrad_ab.txt; grep -E "passed|failed|Error" $O/tests.log | tail -8

@@ -57,9 +57,27 @@ def run():
     print(json.dumps(out))
 
 
+def run_eager(reps=5):
+    """Each shape `reps` times, eagerly (for rocprofv3 counter passes)."""
+    from tencent_recommendation_2025_amd import kernels as K
+    for name, m, n, k, layout in SHAPES:
+        g = torch.Generator(device='cuda').manual_seed(0)
+        a = torch.randn(m, k, device='cuda', generator=g).bfloat16()
+        b = (torch.randn(n, k, device='cuda', generator=g) if layout == 0 else
+             torch.randn(k, n, device='cuda', generator=g)).bfloat16()
+        c = torch.empty(m, n, device='cuda').bfloat16()
+        for _ in range(reps):
+            K.gemm(a, b, trans_b=layout == 0, out=c)
+        torch.cuda.synchronize()
+        print(name, flush=True)
+
+
 if __name__ == '__main__':
     if len(sys.argv) > 1 and sys.argv[1] == 'one':
         run()
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == 'eager':
+        run_eager()
         sys.exit(0)
     res = {}
     variants = {'auto': {}, 'c1_bk64': {'GRK_MGEMM_CFG': '1'}, 'c2_256x128': {'GRK_MGEMM_CFG': '2'},
