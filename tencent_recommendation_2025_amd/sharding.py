@@ -308,15 +308,16 @@ class ShardedFusedAdamW(FusedAdamW):
     owner brings the rows it is asked for up to the current step inside
     ``prepare`` (catch-up replay) before gathering them, updates the rows it
     receives gradients for after backward (lazy update + step stamp), and the
-    rows nobody asked for stay deferred until the segment flush -- every
-    ``defer_period`` steps, or before ``state_dict``."""
+    rows nobody asked for stay deferred until the rolling flush reaches them
+    (one 1/defer_period slice of each shard per step, in ``prepare``; rolling=False:
+    all rows every ``defer_period`` steps), or before ``state_dict``."""
 
     SHARDED = ('item_emb', 'user_emb')
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, table_mode='dense',
                  table_dtype=torch.bfloat16, pg=None, gather_fn=kernel_gather, reduce_fn=kernel_reduce,
                  dense_reduce_fn=kernel_dense_reduce, defer_period=16, bucket_bytes=32 << 20, lookahead=True,
-                 init_seed=0, dense_flat=True):
+                 init_seed=0, dense_flat=True, rolling=True):
         self.pg = pg
         self.world = dist.get_world_size(pg)
         self.rank = dist.get_rank(pg)
@@ -369,6 +370,12 @@ class ShardedFusedAdamW(FusedAdamW):
             self._deferred = {name: grp for name, (grp, _) in self.shards.items()}
             for g in self._deferred.values():
                 g.last = torch.zeros(g.rows, dtype=torch.int32, device=dev)
+            if rolling and self.clock is not None:
+                # the rolling flush (optim.FusedAdamW rolling): prepare() brings one 1/defer_period
+                # slice of every shard up to date each step; the ring holds 2 x defer_period steps
+                self.rolling = True
+                self.clock = K.DeviceClock(2 * self.defer, dev)
+                self._pinned = [torch.zeros_like(self.clock.ring, device='cpu').pin_memory() for _ in range(2)]
         params = self._dense_params()
         self.buckets = GradBuckets(params, pg, bucket_bytes) if params else None
         # fixed exchange buffers (rows fetched for a step, inverse indices): a captured
@@ -482,6 +489,9 @@ class ShardedFusedAdamW(FusedAdamW):
             grp, ex = self.shards[name]
             r = routed[name]
             catchup = None
+            if self.rolling:   # this step's slice of the shard (rolling flush), before any row is read
+                K.table_adamw_catchup_slice(grp.flat, grp.exp_avg, grp.exp_avg_sq, grp.last, self.clock,
+                                            self._period)
             if self.defer:
                 def catchup(local, grp=grp):
                     K.table_adamw_catchup(grp.flat, grp.exp_avg, grp.exp_avg_sq, grp.last, None, self.clock,
