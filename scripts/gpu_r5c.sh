@@ -15,7 +15,7 @@ grep -Eqi "$FAULT" $O/tests.log && { echo "GPU fault -- stopping"; cat $O/summar
 case $rc in 0|1) ;; *) echo "pytest exit $rc -- stopping"; exit $rc ;; esac
 timeout -k 10 400 python -u scripts/microbench/mgemm.py > $O/mgemm_bench.txt 2>&1
 echo "mgemm bench rc=$?" >> $O/summary.txt
-timeout -k 10 300 python -u scripts/microbench/wgrad_ab.py > $O/wgrad_ab.txt 2>&1
+timeout -k 10 400 python -u scripts/microbench/wgrad_ab.py > $O/wgrad_ab.txt 2>&1
 echo "wgrad ab rc=$?" >> $O/summary.txt
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
   SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --kernel-include-regex "k_mgemm" --output-format csv \

@@ -80,9 +80,10 @@ if __name__ == '__main__':
         run_eager()
         sys.exit(0)
     res = {}
-    variants = {'auto': {}, 'c1_bk64': {'GRK_MGEMM_CFG': '1'}, 'c2_256x128': {'GRK_MGEMM_CFG': '2'},
-                'c3_256x256': {'GRK_MGEMM_CFG': '3'}, 'c4_128x128': {'GRK_MGEMM_CFG': '4'}, 'c5_256x256w8': {'GRK_MGEMM_CFG': '5'},
-                'hipblaslt': {'GRK_GEMM_BACKEND': 'hipblaslt'}}
+    mf = {'GRK_GEMM_BACKEND': 'mfma'}
+    variants = {'routed': {}, 'c1_bk64': {**mf, 'GRK_MGEMM_CFG': '1'}, 'c2_256x128': {**mf, 'GRK_MGEMM_CFG': '2'},
+                'c3_256x256': {**mf, 'GRK_MGEMM_CFG': '3'}, 'c4_128x128': {**mf, 'GRK_MGEMM_CFG': '4'},
+                'c5_256x256w8': {**mf, 'GRK_MGEMM_CFG': '5'}, 'hipblaslt': {'GRK_GEMM_BACKEND': 'hipblaslt'}}
     for name, extra in variants.items():
         env = dict(os.environ, **extra)
         r = subprocess.run([sys.executable, __file__, 'one'], env=env, capture_output=True, text=True, timeout=600)

@@ -1,6 +1,6 @@
 """grk_wgrad at the jagged C2 step's weight-gradient shapes (bench.py's recorded trace):
-grk_mgemm's K-major mode (default) against the round-4 ring kernels
-(GRK_WGRAD_MGEMM=0), each in its own process, device time per call (HIP graph of 30
+the ring kernels (default), with thinner K slices (GRK_WGRAD_SLICE) and on grk_mgemm's
+K-major mode (GRK_WGRAD_MGEMM=1), each in its own process, device time per call (HIP graph of 30
 calls between events; k_wgrad* + the slice reduction, bias gradient included).
 
     python scripts/microbench/wgrad_ab.py
@@ -60,7 +60,8 @@ if __name__ == '__main__':
         run()
         sys.exit(0)
     res = {}
-    for name, extra in (('mgemm', {}), ('round4', {'GRK_WGRAD_MGEMM': '0'})):
+    for name, extra in (('default', {}), ('slice256', {'GRK_WGRAD_SLICE': '256'}),
+                        ('slice128', {'GRK_WGRAD_SLICE': '128'}), ('mgemm', {'GRK_WGRAD_MGEMM': '1'})):
         r = subprocess.run([sys.executable, __file__, 'one'], env=dict(os.environ, **extra), capture_output=True,
                            text=True, timeout=600)
         if r.returncode:

@@ -293,14 +293,20 @@ extern "C" int grk_gemm_ex(int trans_a, int trans_b, int64_t m, int64_t n, int64
   GRK_CHECK_ARG(!bias || bias_dtype == GRK_BF16 || bias_dtype == GRK_F32, "bias must be bf16 or fp32");
   GRK_CHECK_ARG(lda >= (trans_a ? m : k) && ldb >= (trans_b ? k : n) && ldc >= n, "leading dimension too small");
   GRK_CHECK_ARG(k > 0 || beta == 1.0f || bias, "k == 0 needs beta == 1 or a bias");
-  // grk's own MFMA GEMM (grk_mgemm.hip) for every shape it takes -- the dense layers'
-  // forward and input-gradient products; hipBLASLt for the rest (transposed A, other
-  // alpha / beta).  GRK_GEMM_BACKEND=hipblaslt forces hipBLASLt (A/B runs).
-  static const bool force_blas = [] {
+  // grk's own MFMA GEMM (grk_mgemm.hip) where it measured faster than hipBLASLt's tuned
+  // plans (round 5, scripts/microbench/mgemm.py): the forward products with a K that is
+  // not a multiple of 64 -- the item / user dnn layers, K = d + 40 = 552 at C2 (itemdnn
+  // 17.3 vs 21.4 us, the pair 31.5 vs 33.6 us) -- hipBLASLt for the rest (K = 512 / 2048
+  // and every input gradient: 0.26-0.32 of the bf16 peak against grk's 0.18-0.24).
+  // GRK_GEMM_BACKEND=hipblaslt / mfma forces one side for every shape it takes.
+  static const int backend = [] {
     const char* e = getenv("GRK_GEMM_BACKEND");
-    return e && strcmp(e, "hipblaslt") == 0;
+    if (e && strcmp(e, "hipblaslt") == 0) return 0;
+    if (e && strcmp(e, "mfma") == 0) return 2;
+    return 1;
   }();
-  if (!force_blas && grk_gemm_mfma_supported(trans_a, trans_b ? 0 : 1, m, n, k, lda, ldb, ldc, c_dtype, alpha, beta) &&
+  const bool mfma_pick = backend == 2 || (backend == 1 && !trans_a && trans_b && k % 64 != 0);
+  if (mfma_pick && grk_gemm_mfma_supported(trans_a, trans_b ? 0 : 1, m, n, k, lda, ldb, ldc, c_dtype, alpha, beta) &&
       ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c | (uintptr_t)c_in | (uintptr_t)bias) % 16 == 0)
     return grk_gemm_mfma(trans_b ? 0 : 1, m, n, k, a, lda, b, ldb, c, ldc, c_dtype,
                          beta == 1.0f ? (c_in ? c_in : c) : nullptr, bias, bias_dtype, epilogue, stream);

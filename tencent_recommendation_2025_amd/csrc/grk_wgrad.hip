@@ -369,11 +369,19 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(const float* __restrict__ 
     }
 }
 
-// K slices: about two workgroups per CU (latency hiding), slices of >= 512 rows.
+// K slices: about two workgroups per CU (latency hiding), slices of >= kSliceRows rows
+// (GRK_WGRAD_SLICE; 512 by default).
+int slice_rows() {
+  static const int v = [] {
+    const char* e = getenv("GRK_WGRAD_SLICE");
+    return e ? std::max(32, atoi(e)) : 512;
+  }();
+  return v;
+}
 int wgrad_splits(int64_t K, int64_t M, int64_t N) {
   const int64_t tiles = ((M + kWgTile - 1) / kWgTile) * ((N + kWgTile - 1) / kWgTile);
   int S = 1;
-  while (S < 64 && tiles * S < 512 && K >= (int64_t)S * 2 * 512) S *= 2;
+  while (S < 64 && tiles * S < 512 && K >= (int64_t)S * 2 * slice_rows()) S *= 2;
   return S;
 }
 
@@ -381,9 +389,8 @@ int wgrad_splits(int64_t K, int64_t M, int64_t N) {
 // multiple of 32; 1: 128 x 128 tiles, two workgroups per CU; 2: 256 x 128 tiles, one
 // 8-wave workgroup per CU, for M >= 1024 -- the uvqk weight gradients; 3: grk_mgemm's
 // K-major mode, the default since round 5: 256 x 128 tiles of 8 waves, a 6-stage ring,
-// the slices of one K range on one XCD), the tile and the K split.
-// GRK_WGRAD_RING=1 / 2 forces a ring where it applies (A/B builds), GRK_WGRAD_MGEMM=0
-// the round-4 kernels.
+// the slices of one K range on one XCD -- opt-in, GRK_WGRAD_MGEMM=1), the tile and the
+// K split.  GRK_WGRAD_RING=1 / 2 forces a ring where it applies (A/B builds).
 struct WgPlan {
   int kind, tm, tn, S;
 };
@@ -393,9 +400,9 @@ WgPlan wgrad_plan(int64_t K, int64_t M, int64_t N) {
     return e ? atoi(e) : -1;
   }();
   static const bool force_reg = getenv("GRK_WGRAD_REG") != nullptr;
-  static const bool mgemm = [] {
+  static const bool mgemm = [] {   // opt-in: measured no faster (round 5)
     const char* e = getenv("GRK_WGRAD_MGEMM");
-    return !(e && atoi(e) == 0);
+    return e && atoi(e) == 1;
   }();
   WgPlan p{0, kWgTile, kWgTile, wgrad_splits(K, M, N)};
   if (K % kWgK || force_reg) return p;
@@ -413,7 +420,7 @@ WgPlan wgrad_plan(int64_t K, int64_t M, int64_t N) {
   }
   p = WgPlan{2, 256, 128, 1};
   const int64_t tiles = ((M + 255) / 256) * ((N + 127) / 128);
-  while (p.S < 64 && tiles * p.S < 256 && K >= (int64_t)p.S * 2 * 512) p.S *= 2;   // one workgroup per CU
+  while (p.S < 64 && tiles * p.S < 256 && K >= (int64_t)p.S * 2 * slice_rows()) p.S *= 2;   // one workgroup per CU
   return p;
 }
 

@@ -699,6 +699,29 @@ def gemm(a, b, trans_a=False, trans_b=False, out=None, out_dtype=torch.bfloat16,
     return out
 
 
+def gemm_mfma(a, b, trans_b=False, out=None, out_dtype=torch.bfloat16, bias=None, c_in=None, relu=False):
+    """grk_gemm_mfma directly (grk's MFMA GEMM, whatever grk_gemm would route the shape to):
+    out[m, n] = act(a @ op(b) + bias + c_in); a [m, k] bf16 row-major, b [n, k] (trans_b) or
+    [k, n] bf16, c_in None or out-shaped (may be out itself)."""
+    _require_cuda(a, b, out, bias, c_in)
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.stride(1) != 1 or b.stride(1) != 1:
+        raise L.GrkError('gemm_mfma operands must be bf16 row-major')
+    m, k = a.shape
+    n = b.shape[0] if trans_b else b.shape[1]
+    if (b.shape[1] if trans_b else b.shape[0]) != k:
+        raise L.GrkError('gemm_mfma inner dimensions differ')
+    if out is None:
+        out = torch.empty(m, n, dtype=out_dtype, device=a.device)
+    if c_in is not None and (c_in.shape != out.shape or c_in.stride() != out.stride() or c_in.dtype != out.dtype):
+        raise L.GrkError("c_in must match the output's shape, strides and dtype")
+    rc = L.lib().grk_gemm_mfma(0 if trans_b else 1, m, n, k, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+                               out.data_ptr(), out.stride(0), L.dtype_code(out.dtype), _ptr(c_in), _ptr(bias),
+                               L.dtype_code(bias.dtype) if bias is not None else 0,
+                               L.GRK_GEMM_EP_RELU if relu else L.GRK_GEMM_EP_NONE, L.stream_ptr(a.device))
+    L.check(rc, 'grk_gemm_mfma')
+    return out
+
+
 WGRAD_TRACE = None   # bench.py: a list records the (K, M, N, out_dtype, want_db) of every grk_wgrad call
 
 

@@ -44,29 +44,33 @@ def test_mgemm_matches_torch(m, n, k, layout):
     a, b, ref = _operands(m, n, k, layout, g, pad=24)
     assert L.lib().grk_gemm_mfma_supported(0, layout, m, n, k, a.stride(0), b.stride(0), n, L.GRK_BF16, 1.0, 0.0)
     bias = torch.randn(n, device=DEV, generator=g)
-    y = K.gemm(a, b, trans_b=layout == 0)
+    mm = K.gemm_mfma
+    y = mm(a, b, trans_b=layout == 0)
     assert torch.isfinite(y).all()
     assert nrel(y.float(), ref) < 4e-3
-    y2 = K.gemm(a, b, trans_b=layout == 0)
+    y2 = mm(a, b, trans_b=layout == 0)
     assert torch.equal(y, y2)                                              # deterministic
-    yr = K.gemm(a, b, trans_b=layout == 0, bias=bias, relu=True)           # bias + ReLU in the store
+    yr = mm(a, b, trans_b=layout == 0, bias=bias, relu=True)               # bias + ReLU in the store
     assert nrel(yr.float(), torch.relu(ref + bias)) < 4e-3
-    yb = K.gemm(a, b, trans_b=layout == 0, bias=bias.bfloat16())
+    yb = mm(a, b, trans_b=layout == 0, bias=bias.bfloat16())
     assert nrel(yb.float(), ref + bias.bfloat16().float()) < 4e-3
-    y32 = K.gemm(a, b, trans_b=layout == 0, out_dtype=torch.float32)       # fp32 C: only the accumulation order
+    y32 = mm(a, b, trans_b=layout == 0, out_dtype=torch.float32)           # fp32 C: only the accumulation order
     assert nrel(y32, ref) < 1e-5
     # accumulate in place into a column block of a wider bf16 buffer (functional.linear in_place)
     cbuf = torch.randn(m, n + 16, device=DEV, generator=g).bfloat16()
     c = cbuf[:, :n]
     keep = cbuf[:, n:].clone()
     want = c.float() + ref
-    K.gemm(a, b, trans_b=layout == 0, out=c, beta=1.0)
+    mm(a, b, trans_b=layout == 0, out=c, c_in=c)
     assert nrel(c.float(), want) < 4e-3
     assert torch.equal(cbuf[:, n:], keep)                                  # columns past n untouched
     # a separate addend
     add = torch.randn(m, n, device=DEV, generator=g).bfloat16()
-    ya = K.gemm(a, b, trans_b=layout == 0, addend=add, beta=1.0, relu=True)
+    ya = mm(a, b, trans_b=layout == 0, c_in=add, relu=True)
     assert nrel(ya.float(), torch.relu(ref + add.float())) < 4e-3
+    # grk_gemm's routing: the forward at K % 64 != 0 runs here (the dnn layers), bitwise the same
+    if layout == 0 and k % 64:
+        assert torch.equal(K.gemm(a, b, trans_b=True, bias=bias, relu=True), yr)
 
 
 def test_mgemm_rows_past_m_untouched():
@@ -75,6 +79,6 @@ def test_mgemm_rows_past_m_untouched():
     g = torch.Generator(device=DEV).manual_seed(3)
     a, b, ref = _operands(300, 256, 128, 0, g)
     big = torch.full((512, 256), 7.0, device=DEV).bfloat16()
-    K.gemm(a, b, trans_b=True, out=big[:300])
+    K.gemm_mfma(a, b, trans_b=True, out=big[:300])
     assert nrel(big[:300].float(), ref) < 4e-3
     assert bool((big[300:] == 7.0).all())
