@@ -11,6 +11,11 @@
 // consecutive lanes on consecutive bytes of one row, no LDS, no MFMA.
 #include <string.h>
 
+#include <stdlib.h>
+
+#include <algorithm>
+#include <utility>
+
 #include "grk_common.h"
 
 namespace grk {
@@ -707,6 +712,111 @@ __global__ void __launch_bounds__(256) k_seg_chunks_partial(const unsigned* __re
                                       partials);
 }
 
+// Column-sliced form of k_seg_chunks_partial (dim = 64 * slices, slices in {1, 2, 4, 8}):
+// the chunk sums run per 64-column slice, slice s on XCD s (mod slices), so an XCD
+// gathers only its slice of every upstream gradient row -- 128 B of bf16 per row -- and
+// the rows a call reads (~40k: ~5 MB per slice) meet in the XCD's 4 MB L2 instead of
+// every XCD fetching whole 1 KB rows from the Infinity Cache.  One wave sums 8 chunks
+// side by side, 8 lanes x 8 elements per chunk; every column is still summed in the
+// chunk's entry order and the pieces crossing chunk edges go to the same partial slots,
+// so the result is the same bits as the whole-row kernel (and the oracle's chunk-order
+// restatement).  The keys and gradient-row addresses of the next PIPE entries load
+// while the current rows are summed; keys / gptr are read up to the chunk's end past n
+// (the workspace rounds both up to whole chunks).
+template <typename G, int CH, int PIPE, typename OT = float>
+__global__ void __launch_bounds__(256) k_seg_chunks_sliced(const unsigned* __restrict__ keys,
+                                                           const unsigned long long* __restrict__ gptr,
+                                                           const int* __restrict__ pos, int64_t n, unsigned sentinel,
+                                                           int dim, int slices, int64_t groups,
+                                                           OT* __restrict__ dense_out, float* __restrict__ uniq_rows,
+                                                           int32_t* __restrict__ row_slot,
+                                                           float* __restrict__ partials) {
+  constexpr int LW = 8;
+  static_assert(CH % PIPE == 0 && PIPE % 4 == 0, "batch");
+  const int lane = threadIdx.x & 63, grp = lane >> 3, sub = lane & 7;
+  const unsigned xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+  const int slice = (int)xcd % slices;
+  const int64_t cg = (int64_t)q * (8 / slices) + (int64_t)xcd / slices;  // 32 chunks per workgroup
+  if (cg >= groups) return;
+  const int64_t chunk = cg * 32 + (threadIdx.x >> 6) * 8 + grp;
+  const int64_t p0 = chunk * CH;
+  const int c = slice * 64 + sub * LW;
+  const int64_t p1 = p0 < n ? min(n, p0 + CH) : p0;
+  unsigned cur = p0 < n ? keys[p0] : sentinel;
+  const bool act = cur != sentinel;
+  const unsigned kprev = act && p0 > 0 ? keys[p0 - 1] : sentinel;
+  const unsigned knext = act && p1 < n ? keys[p1] : sentinel;
+  int u = act && pos ? pos[p0] - 1 : 0;
+  WaveAcc<LW> acc;
+  acc.zero();
+  int64_t ps = p0, pe = p0;  // current piece [ps, pe) of key cur
+  bool live = act;
+  auto flush = [&]() {
+    const bool whole = (ps > p0 || kprev != cur) && (pe < p1 || knext != cur);
+    if (whole) {
+      store_final(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
+    } else {  // the piece's sum goes to the chunk's head (0) or tail (1) slot
+      const int slot = (ps == p0 && kprev == cur) ? 0 : 1;
+      float* dst = partials + (chunk * 2 + slot) * dim + c;
+#pragma unroll
+      for (int e = 0; e < LW; e += 4)
+        *reinterpret_cast<float4*>(dst + e) = make_float4(acc.v[e], acc.v[e + 1], acc.v[e + 2], acc.v[e + 3]);
+    }
+  };
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  unsigned kk[PIPE];
+  unsigned long long gg[PIPE];
+  auto fetch = [&](int s0) {
+#pragma unroll
+    for (int j = 0; j < PIPE; j += 4) {
+      const u32x4 t = *reinterpret_cast<const u32x4*>(keys + p0 + s0 + j);
+      kk[j] = t.x;
+      kk[j + 1] = t.y;
+      kk[j + 2] = t.z;
+      kk[j + 3] = t.w;
+    }
+#pragma unroll
+    for (int j = 0; j < PIPE; j += 2) {
+      const u64x2 t = *reinterpret_cast<const u64x2*>(gptr + p0 + s0 + j);
+      gg[j] = t.x;
+      gg[j + 1] = t.y;
+    }
+  };
+  if (live) fetch(0);
+  for (int s0 = 0; s0 < CH; s0 += PIPE) {
+    if (__ballot(live) == 0) break;
+    WaveVec<G, LW> r[PIPE];
+    bool ok[PIPE];
+    unsigned kc[PIPE];
+#pragma unroll
+    for (int j = 0; j < PIPE; ++j) {
+      ok[j] = live && p0 + s0 + j < p1 && kk[j] != sentinel;  // sorted: false from the first padding entry on
+      kc[j] = kk[j];
+      if (ok[j]) r[j].load(gg[j], c);
+    }
+    if (live && s0 + PIPE < CH && p0 + s0 + PIPE < p1) fetch(s0 + PIPE);
+#pragma unroll
+    for (int j = 0; j < PIPE; ++j) {
+      if (!ok[j]) {
+        live = false;
+      } else {
+        if (kc[j] != cur) {
+          flush();
+          acc.zero();
+          cur = kc[j];
+          ps = p0 + s0 + j;
+          if (pos) u = pos[ps] - 1;
+        }
+#pragma unroll
+        for (int x = 0; x < LW; ++x) acc.v[x] += r[j].get(x);
+        pe = p0 + s0 + j + 1;
+      }
+    }
+  }
+  if (act) flush();
+}
+
 // One wave per chunk edge b: the row first crossing b (it starts in chunk
 // b - 1, whose tail slot holds its first piece) = tail(b - 1) + head(b) + ...
 // + head(last chunk of the row), added in that order.
@@ -1124,14 +1234,15 @@ static int plan_ws(int64_t n, int64_t num_rows, int dim, char* base, BwdWs* ws) 
     return p;
   };
   ws->keys_in = (unsigned*)take(n * 4);
-  ws->keys_out = (unsigned*)take(n * 4);
+  const int64_t nr = (n + kPartialChunk - 1) / kPartialChunk * kPartialChunk;  // k_seg_chunks_sliced reads whole chunks
+  ws->keys_out = (unsigned*)take(nr * 4);
   ws->seg_key = (unsigned*)take(n * 4);
   ws->flags = (int*)take(n * 4);
   ws->pos = (int*)take(n * 4);
   ws->seg_start = (int*)take(n * 4);
   ws->seg_end = (int*)take(n * 4);
   ws->gptr_in = (unsigned long long*)take(n * 8);
-  ws->gptr_out = (unsigned long long*)take(n * 8);
+  ws->gptr_out = (unsigned long long*)take(nr * 8);
   ws->partials = (float*)take((size_t)((n + kPartialChunk - 1) / kPartialChunk) * 2 * dim * sizeof(float));
   unsigned end_bit = 1;
   while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
@@ -1424,19 +1535,40 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
       const int64_t pchunks = (total + kPartialChunk - 1) / kPartialChunk;
       const unsigned gw = (unsigned)((pchunks + 3) / 4);
       const unsigned ge = (unsigned)(pchunks > 1 ? (pchunks - 1 + 3) / 4 : 0);
+      // column-sliced chunk sums (GRK_BWD_SLICED=1; default: whole rows per wave -- the
+      // same bits either way)
+      static const bool sliced_env = [] {
+        const char* e = getenv("GRK_BWD_SLICED");
+        return e && atoi(e) != 0;
+      }();
+      const int slices = dim / 64;
+      const bool sliced = sliced_env && dim % 64 == 0 && (slices == 1 || slices == 2 || slices == 4 || slices == 8);
+      const int64_t sgroups = (pchunks + 31) / 32;
+      const int rep = sliced ? 8 / slices : 1;
+      const unsigned gs = (unsigned)(8 * ((sgroups + rep - 1) / rep));
 #define GRK_SEGP(G, LW)                                                                                          \
-  k_seg_chunks_partial<G, LW, kPartialChunk><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start,  \
-                                                                ws.seg_end, total, sentinel, dim, dense_out,     \
-                                                                uniq_rows, row_slot, ws.partials);               \
+  if (sliced)                                                                                                    \
+    k_seg_chunks_sliced<G, kPartialChunk, sizeof(G) == 2 ? 16 : 8><<<gs, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, total,        \
+                                                                 sentinel, dim, slices, sgroups, dense_out,      \
+                                                                 uniq_rows, row_slot, ws.partials);              \
+  else                                                                                                           \
+    k_seg_chunks_partial<G, LW, kPartialChunk><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start,\
+                                                                  ws.seg_end, total, sentinel, dim, dense_out,   \
+                                                                  uniq_rows, row_slot, ws.partials);             \
   GRK_LAUNCH_CHECK();                                                                                            \
   if (ge)                                                                                                        \
     k_seg_partials_combine<LW, kPartialChunk><<<ge, 256, 0, s>>>(ws.keys_out, ws.pos, ws.seg_start, ws.seg_end,  \
                                                                  total, sentinel, dim, ws.partials, dense_out,    \
                                                                  uniq_rows, row_slot)
       if (dense_out16) {
-        k_seg_chunks_partial<bf16_t, 8, kPartialChunk, bf16_t><<<gw, 256, 0, s>>>(
-            ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel, dim, dense_out16, uniq_rows,
-            row_slot, ws.partials);
+        if (sliced)
+          k_seg_chunks_sliced<bf16_t, kPartialChunk, 16, bf16_t><<<gs, 256, 0, s>>>(
+              ws.keys_out, ws.gptr_out, ws.pos, total, sentinel, dim, slices, sgroups, dense_out16, uniq_rows,
+              row_slot, ws.partials);
+        else
+          k_seg_chunks_partial<bf16_t, 8, kPartialChunk, bf16_t><<<gw, 256, 0, s>>>(
+              ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel, dim, dense_out16, uniq_rows,
+              row_slot, ws.partials);
         GRK_LAUNCH_CHECK();
         if (ge)
           k_seg_partials_combine<8, kPartialChunk, bf16_t><<<ge, 256, 0, s>>>(
