@@ -452,6 +452,30 @@ typedef struct grk_row_copy {
 } grk_row_copy;
 int grk_gather_rows(const grk_row_copy* copies, int num_copies, const int32_t* row_map, int64_t rows, void* stream);
 
+/* Row-sharded tables (sharding.ShardExchange.route; replaces the sort-based torch
+ * route): the distinct ids of ids[n] grouped by owner (id % world) and ascending
+ * inside an owner -> send_ids[0, n_uniq); send_counts[world] = distinct ids per
+ * owner (the all-to-all split sizes); inverse[i] = slot of ids[i] in send_ids (-1
+ * for ids outside [0, global_rows)); bad[0] = how many such ids; n_uniq (may be
+ * NULL).  rows_per_owner * world >= global_rows (local row = id / world).  ws:
+ * grk_route_workspace(world, rows_per_owner) bytes.  Deterministic, graph-safe. */
+size_t grk_route_workspace(int world, int64_t rows_per_owner);
+int grk_route(const int64_t* ids, int64_t n, int world, int64_t rows_per_owner, int64_t global_rows,
+              int64_t* send_ids, int64_t* inverse, int64_t* send_counts, int64_t* n_uniq, int64_t* bad, void* ws,
+              size_t ws_bytes, void* stream);
+
+/* The dense gradients of one all-reduce bucket into its fp32 flat buffer
+ * (sharding.GradBuckets): dst[dst_offset + e] = src[e] for e < count (bf16 / fp32
+ * -> fp32), zeros where src is NULL; at most 64 ranges per launch. */
+typedef struct grk_pack_range {
+  const void* src;
+  int64_t count;
+  int64_t dst_offset;
+  int32_t src_dtype;
+  int32_t pad_;
+} grk_pack_range;
+int grk_flat_pack(const grk_pack_range* ranges, int num_ranges, float* dst, void* stream);
+
 /* out [B*T, ldo] (out_dtype); lse fp32 [B, H, T] (softmax: natural-log
  * logsumexp of the masked scaled scores, -inf for fully-masked rows). */
 int grk_attention_fwd(const grk_attn_args* a, void* out, int64_t ldo, float* lse, void* stream);

@@ -83,6 +83,11 @@ class GrkColumnBlock(C.Structure):
                 ('src_dtype', C.c_int32), ('pad_', C.c_int32)]
 
 
+class GrkPackRange(C.Structure):
+    _fields_ = [('src', C.c_void_p), ('count', C.c_int64), ('dst_offset', C.c_int64), ('src_dtype', C.c_int32),
+                ('pad_', C.c_int32)]
+
+
 class GrkGemmGroup(C.Structure):
     _fields_ = [('a', C.c_void_p), ('lda', C.c_int64), ('b', C.c_void_p), ('ldb', C.c_int64), ('c', C.c_void_p),
                 ('ldc', C.c_int64), ('rows', C.c_int64), ('b_rows', C.c_int64)]
@@ -160,6 +165,9 @@ SIGNATURES = {
     'grk_proj_index': (_I, [C.POINTER(GrkIndexBlock), _I, _I, _I64, _P, _I64, _P]),
     'grk_write_columns': (_I, [C.POINTER(GrkColumnBlock), _I, _I64, _P, _I64, _I, _P]),
     'grk_batch_row_ids': (_I, [_P, _P, _P, _P, _I, _I64, _P, _P, _P]),
+    'grk_route_workspace': (_SZ, [_I, _I64]),
+    'grk_route': (_I, [_P, _I64, _I, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    'grk_flat_pack': (_I, [C.POINTER(GrkPackRange), _I, _P, _P]),
     'grk_add_norm_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _P, _I64, _P, _I64, _I, _P, _P]),
     'grk_add_norm_bwd_workspace': (_SZ, [_I64, _I]),
     'grk_add_norm_bwd': (_I, [_P, _I64, _I, _P, _I64, _P, _I64, _P, _P, _I64, _I, _P, _I64, _P, _P, _P, _SZ, _P]),

@@ -619,6 +619,69 @@ def gather_rows(pairs, row_map):
                 'grk_gather_rows')
 
 
+_ROUTE_WS = {}
+
+
+def route(ids, world, rows_per_owner, global_rows):
+    """Routing plan of one row-sharded table's ids (grk_route, five launches, no sort):
+    {'send_ids': int64 [n] (distinct ids, owner-major (owner = id % world), ascending
+    within an owner, in the first n_uniq slots), 'inverse': int64 [n] (each id's slot,
+    -1 for ids outside the table), 'send_counts': int64 [world], 'n_uniq': int64 [1],
+    'bad': int64 [1] (ids outside [0, global_rows))} -- sharding.ShardExchange.route's
+    plan; the caller's all-to-all of the counts completes it."""
+    _require_cuda(ids)
+    ids = ids.reshape(-1)
+    if ids.dtype != torch.int64:
+        ids = ids.long()
+    ids = ids.contiguous()
+    dev, n = ids.device, ids.numel()
+    key = (dev, int(world), int(rows_per_owner))
+    ws = _ROUTE_WS.get(key)
+    if ws is None:
+        ws = _ROUTE_WS[key] = torch.empty(max(L.lib().grk_route_workspace(world, rows_per_owner), 1),
+                                          dtype=torch.uint8, device=dev)
+    out = dict(send_ids=torch.empty(n, dtype=torch.int64, device=dev),
+               inverse=torch.empty(n, dtype=torch.int64, device=dev),
+               send_counts=torch.empty(world, dtype=torch.int64, device=dev),
+               n_uniq=torch.empty(1, dtype=torch.int64, device=dev),
+               bad=torch.empty(1, dtype=torch.int64, device=dev))
+    L.check(L.lib().grk_route(_ptr(ids), n, int(world), int(rows_per_owner), int(global_rows), _ptr(out['send_ids']),
+                              _ptr(out['inverse']), _ptr(out['send_counts']), _ptr(out['n_uniq']), _ptr(out['bad']),
+                              ws.data_ptr(), ws.numel(), L.stream_ptr(dev)), 'grk_route')
+    return out
+
+
+MAX_PACK_RANGES = 64   # kPackMax (csrc/grk_shard.hip)
+
+
+def flat_pack(dst, parts):
+    """dst (fp32, contiguous) [off:off + n] = src (bf16 / fp32, any shape, contiguous) or
+    zeros for src None, for every (src, off, n) in parts -- grk_flat_pack, one launch
+    per 64 parts (an all-reduce bucket's gradients into its flat buffer)."""
+    _require_cuda(dst)
+    if dst.dtype != torch.float32 or not dst.is_contiguous():
+        raise L.GrkError('flat_pack: dst must be a contiguous fp32 tensor')
+    keep = []
+    for i in range(0, len(parts), MAX_PACK_RANGES):
+        chunk = parts[i:i + MAX_PACK_RANGES]
+        arr = (L.GrkPackRange * len(chunk))()
+        for j, (src, off, n) in enumerate(chunk):
+            if off < 0 or off + n > dst.numel():
+                raise L.GrkError(f'flat_pack part {i + j}: [{off}, {off + n}) outside dst ({dst.numel()})')
+            if src is None:
+                arr[j] = L.GrkPackRange(None, n, off, L.GRK_F32, 0)
+                continue
+            if src.dtype not in (torch.float32, torch.bfloat16):
+                src = src.float()
+            src = src.contiguous()
+            if src.numel() != n:
+                raise L.GrkError(f'flat_pack part {i + j}: {src.numel()} elements, expected {n}')
+            keep.append(src)
+            arr[j] = L.GrkPackRange(src.data_ptr(), n, off, L.dtype_code(src.dtype), 0)
+        L.check(L.lib().grk_flat_pack(arr, len(chunk), dst.data_ptr(), L.stream_ptr(dst.device)), 'grk_flat_pack')
+    return dst
+
+
 def attention_fwd(args, out, lse=None):
     """grk_attention_fwd: out [B*T, >=H*hd] (args.out_dtype); lse fp32 [B, H, T] (softmax)."""
     _require_cuda(out, lse)

@@ -132,7 +132,20 @@ class ShardExchange:
 
     def route(self, ids, pg=None):
         """Phase 1 (before the single host sync): unique ids, owner order, counts.
-        pg: communicator for the counts exchange (default: the table's).
+        pg: communicator for the counts exchange (default: the table's).  Device ids:
+        grk_route (K.route: a presence bitmap, five launches); host ids: the
+        sort-based restatement below (_route_torch), the same plan."""
+        if ids.is_cuda:
+            rows_per_owner = -(-self.global_rows // self.world)
+            r = K.route(ids, self.world, max(rows_per_owner, 1), self.global_rows)
+            recv_counts = torch.empty_like(r['send_counts'])
+            a2a(recv_counts, r['send_counts'], pg=self.pg if pg is None else pg)
+            return dict(uniq=r['send_ids'], inverse=r['inverse'], send_ids=r['send_ids'],
+                        send_counts=r['send_counts'], recv_counts=recv_counts, bad=r['bad'])
+        return self._route_torch(ids, pg)
+
+    def _route_torch(self, ids, pg=None):
+        """route() on host tensors (and the reference the GPU test holds grk_route to).
 
         Every output has a fixed size (len(ids)), so nothing here waits for the
         device (torch.unique / bincount would: their output sizes are data
@@ -254,8 +267,23 @@ class GradBuckets:
             self.next += 1
 
     def _launch(self, b):
-        """Bucket b's gradients into its flat buffer (one cat kernel), then its all-reduce."""
-        flat, off, src, alias = self.flat[b], 0, [], 0
+        """Bucket b's gradients into its flat buffer (device: one grk_flat_pack launch;
+        host: one cat), then its all-reduce."""
+        flat = self.flat[b]
+        if flat.is_cuda and all(p.grad is None or p.grad.data_ptr() < flat.data_ptr()
+                                or p.grad.data_ptr() >= flat.data_ptr() + flat.numel() * 4
+                                for p in self.buckets[b]):
+            parts, off = [], 0
+            for p in self.buckets[b]:
+                parts.append((p.grad, off, p.numel()))
+                off += p.numel()
+            K.flat_pack(flat, parts)
+            if self.async_ok:
+                self.works[b] = dist.all_reduce(flat, group=self.pg, async_op=True)
+            else:
+                all_reduce(flat, self.pg)
+            return
+        off, src, alias = 0, [], 0
         for p in self.buckets[b]:
             n = p.numel()
             if p.grad is None:

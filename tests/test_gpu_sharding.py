@@ -275,3 +275,64 @@ def test_sharded_dense_flat_equals_torch_adamw_and_shadows_match(pg):
         if k in ('item_emb.weight', 'user_emb.weight'):
             continue
         torch.testing.assert_close(s1[k], s2[k], rtol=2e-3, atol=1e-4, msg=k)
+
+
+def _route_reference(ids, world, global_rows):
+    """The routing plan of ShardExchange._route_torch restated on the host: distinct
+    in-range ids ordered by (owner = id % world, id), each id's slot, per-owner counts."""
+    import numpy as np
+    ok = (ids >= 0) & (ids < global_rows)
+    uniq = sorted(set(ids[ok].tolist()), key=lambda v: (v % world, v))
+    slot = {v: i for i, v in enumerate(uniq)}
+    inverse = np.array([slot[v] if 0 <= v < global_rows else -1 for v in ids.tolist()], dtype=np.int64)
+    counts = np.bincount(np.array([v % world for v in uniq], dtype=np.int64), minlength=world)[:world]
+    return np.array(uniq, dtype=np.int64), inverse, counts, int((~ok).sum())
+
+
+@pytest.mark.parametrize('world,rows,n', [(1, 1_000_001, 41472), (2, 1_000_001, 30000), (3, 1000, 5000),
+                                          (8, 50_000_017, 20000), (5, 7, 64), (4, 100, 0)])
+def test_grk_route_equals_sort_route(world, rows, n):
+    """grk_route (the presence-bitmap route of the row-sharded tables) == the sort-based
+    plan: send order, slots, split sizes, out-of-range count -- duplicates, ids past the
+    last row and negative ids included."""
+    import numpy as np
+    from tencent_recommendation_2025_amd import kernels as K
+    rng = np.random.default_rng(world * 7 + n)
+    ids = rng.integers(0, rows, n)
+    if n:
+        ids[rng.integers(0, n, n // 3)] = ids[0]                        # duplicates
+        ids[rng.integers(0, n, max(1, n // 100))] = rng.integers(0, min(rows, 50), max(1, n // 100))
+    if n >= 64:
+        ids[5], ids[9], ids[11] = -1, rows, rows + 12                   # out of range
+    R = -(-rows // world)
+    got = K.route(torch.tensor(ids, device=DEV), world, R, rows)
+    uniq, inverse, counts, bad = _route_reference(ids, world, rows)
+    nu = len(uniq)
+    assert int(got['n_uniq'].item()) == nu and int(got['bad'].item()) == bad
+    assert np.array_equal(got['send_ids'][:nu].cpu().numpy(), uniq)
+    assert np.array_equal(got['inverse'].cpu().numpy(), inverse)
+    assert np.array_equal(got['send_counts'].cpu().numpy(), counts)
+
+
+def test_flat_pack_equals_cat():
+    """grk_flat_pack: a bucket's bf16 / fp32 gradients (and a missing one, zeros) into the
+    fp32 flat buffer == torch.cat of the fp32 casts, more than 64 parts (two launches)."""
+    from tencent_recommendation_2025_amd import kernels as K
+    g = torch.Generator(device=DEV).manual_seed(3)
+    shapes = [(512, 2048), (512,), (7,), (552, 512), (1, 33), (2049,)] * 12
+    parts, ref, off = [], [], 0
+    for i, sh in enumerate(shapes):
+        n = int(torch.tensor(sh).prod())
+        if i % 11 == 5:
+            src = None
+            ref.append(torch.zeros(n, device=DEV))
+        else:
+            src = torch.randn(sh, device=DEV, generator=g)
+            if i % 2:
+                src = src.bfloat16()
+            ref.append(src.float().reshape(-1))
+        parts.append((src, off, n))
+        off += n
+    flat = torch.full((off,), float('nan'), device=DEV)
+    K.flat_pack(flat, parts)
+    assert torch.equal(flat, torch.cat(ref))
