@@ -476,6 +476,20 @@ typedef struct grk_pack_range {
 } grk_pack_range;
 int grk_flat_pack(const grk_pack_range* ranges, int num_ranges, float* dst, void* stream);
 
+/* Row-sharded tables + jagged rows (train.jagged_remaps): for every role (at most 8)
+ * out[r] = inv[row_map[r]] for r < rows; a dead row (row_map[r] < 0) reads
+ * inv[first padding position of the role] -- the role's id at position i is ids[i],
+ * or 0 where tt is given and tt[i] != tt_want; position 0 when no id is 0.  One launch. */
+typedef struct grk_remap_role {
+  const int64_t* inv;   /* [n] fetched-row slot of every [B, T] position */
+  int64_t* out;         /* [rows] */
+  const int64_t* ids;   /* [n] the role's ids */
+  const int64_t* tt;    /* [n] token types or NULL */
+  int64_t tt_want;
+  int64_t n;
+} grk_remap_role;
+int grk_jagged_remap(const grk_remap_role* roles, int num_roles, const int32_t* row_map, int64_t rows, void* stream);
+
 /* out [B*T, ldo] (out_dtype); lse fp32 [B, H, T] (softmax: natural-log
  * logsumexp of the masked scaled scores, -inf for fully-masked rows). */
 int grk_attention_fwd(const grk_attn_args* a, void* out, int64_t ldo, float* lse, void* stream);

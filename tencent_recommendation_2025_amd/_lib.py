@@ -88,6 +88,11 @@ class GrkPackRange(C.Structure):
                 ('pad_', C.c_int32)]
 
 
+class GrkRemapRole(C.Structure):
+    _fields_ = [('inv', C.c_void_p), ('out', C.c_void_p), ('ids', C.c_void_p), ('tt', C.c_void_p),
+                ('tt_want', C.c_int64), ('n', C.c_int64)]
+
+
 class GrkGemmGroup(C.Structure):
     _fields_ = [('a', C.c_void_p), ('lda', C.c_int64), ('b', C.c_void_p), ('ldb', C.c_int64), ('c', C.c_void_p),
                 ('ldc', C.c_int64), ('rows', C.c_int64), ('b_rows', C.c_int64)]
@@ -168,6 +173,7 @@ SIGNATURES = {
     'grk_route_workspace': (_SZ, [_I, _I64]),
     'grk_route': (_I, [_P, _I64, _I, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'grk_flat_pack': (_I, [C.POINTER(GrkPackRange), _I, _P, _P]),
+    'grk_jagged_remap': (_I, [C.POINTER(GrkRemapRole), _I, _P, _I64, _P]),
     'grk_add_norm_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _P, _I64, _P, _I64, _I, _P, _P]),
     'grk_add_norm_bwd_workspace': (_SZ, [_I64, _I]),
     'grk_add_norm_bwd': (_I, [_P, _I64, _I, _P, _I64, _P, _I64, _P, _P, _I64, _I, _P, _I64, _P, _P, _P, _SZ, _P]),

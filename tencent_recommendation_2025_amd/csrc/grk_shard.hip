@@ -34,14 +34,24 @@ __global__ void __launch_bounds__(kRouteThreads) k_route_mark(const int64_t* __r
                                                               unsigned long long* __restrict__ bad) {
   __shared__ unsigned wbad[kRouteThreads / 64];
   unsigned nbad = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t id = ids[i];
+  // A batch repeats ids in runs (the padding row of every non-item token, hot items):
+  // atomics on one word serialise (one table's 41k ids took 0.4 ms), so a lane whose
+  // id equals its left neighbour's, or whose bit is already visible, adds nothing.
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t span = (n + stride - 1) / stride * stride;  // every lane runs every round (the shuffle)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < span; i += stride) {
+    const int64_t id = i < n ? ids[i] : -1;
+    const int64_t left = __shfl_up(id, 1);
+    if (i >= n) continue;
     if (id < 0 || id >= global_rows) {
       ++nbad;
       continue;
     }
+    if ((threadIdx.x & 63) != 0 && left == id) continue;
     const uint64_t key = (uint64_t)(id % world) * (uint64_t)rows_per_owner + (uint64_t)(id / world);
-    atomicOr(&bitmap[key >> 5], 1u << (key & 31));
+    const unsigned bit = 1u << (key & 31);
+    if (__builtin_nontemporal_load(&bitmap[key >> 5]) & bit) continue;
+    atomicOr(&bitmap[key >> 5], bit);
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) nbad += __shfl_xor(nbad, off);
@@ -210,6 +220,40 @@ __global__ void __launch_bounds__(256) k_flat_pack(PackRanges pr, float* __restr
   }
 }
 
+// Jagged rows under the row-sharded tables (train.jagged_remaps): each role's
+// fetched-row index carried into the jagged row order, out[r] = inv[row_map[r]]; a
+// dead row (row_map -1) reads the slot of the role's first padding id (position 0
+// when the role has none), found by the wave that needs it, 64 ids per ballot.
+constexpr int kRemapMax = 8;
+struct RemapRoles {
+  grk_remap_role r[kRemapMax];
+};
+
+__global__ void __launch_bounds__(256) k_jagged_remap(RemapRoles rr, const int32_t* __restrict__ row_map,
+                                                      int64_t rows) {
+  const grk_remap_role& R = rr.r[blockIdx.y];
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int m = r < rows ? row_map[r] : 0;
+  const bool dead = r < rows && m < 0;
+  int64_t pad = 0;
+  if (__ballot(dead)) {  // wave-uniform: the first position whose id is the padding id 0
+    const int lane = threadIdx.x & 63;
+    pad = -1;
+    for (int64_t b = 0; b < R.n && pad < 0; b += 64) {
+      const int64_t i = b + lane;
+      bool z = false;
+      if (i < R.n) {
+        const int64_t id = R.ids[i];
+        z = R.tt ? (R.tt[i] != R.tt_want || id == 0) : id == 0;
+      }
+      const unsigned long long mask = __ballot(z);
+      if (mask) pad = b + __ffsll((long long)mask) - 1;
+    }
+    if (pad < 0) pad = 0;
+  }
+  if (r < rows) R.out[r] = dead ? R.inv[pad] : R.inv[m];
+}
+
 }  // namespace
 }  // namespace grk
 
@@ -287,6 +331,24 @@ extern "C" int grk_flat_pack(const grk_pack_range* ranges, int num_ranges, float
   if (pieces == 0) return GRK_OK;
   GRK_CHECK_ARG(pieces < ((int64_t)1 << 31), "too many elements");
   k_flat_pack<<<(unsigned)pieces, 256, 0, (hipStream_t)stream>>>(pr, dst);
+  GRK_LAUNCH_CHECK();
+  return GRK_OK;
+}
+
+extern "C" int grk_jagged_remap(const grk_remap_role* roles, int num_roles, const int32_t* row_map, int64_t rows,
+                                void* stream) {
+  clear_error();
+  GRK_CHECK_ARG(num_roles >= 0 && num_roles <= kRemapMax, "num_roles must be in [0, %d]", kRemapMax);
+  GRK_CHECK_ARG(rows >= 0 && (rows == 0 || num_roles == 0 || (roles && row_map)), "bad roles / row_map");
+  if (rows == 0 || num_roles == 0) return GRK_OK;
+  RemapRoles rr;
+  memset(&rr, 0, sizeof(rr));
+  for (int k = 0; k < num_roles; ++k) {
+    GRK_CHECK_ARG(roles[k].inv && roles[k].out && roles[k].ids && roles[k].n >= 1, "role %d: inv / out / ids / n", k);
+    rr.r[k] = roles[k];
+  }
+  const dim3 grid((unsigned)((rows + 255) / 256), (unsigned)num_roles);
+  k_jagged_remap<<<grid, 256, 0, (hipStream_t)stream>>>(rr, row_map, rows);
   GRK_LAUNCH_CHECK();
   return GRK_OK;
 }

@@ -682,6 +682,39 @@ def flat_pack(dst, parts):
     return dst
 
 
+def jagged_remap(roles, row_map):
+    """[out int64 [rows] per role] with out[r] = inv[row_map[r]] and, for a dead row
+    (row_map < 0), inv at the role's first padding position (grk_jagged_remap, one
+    launch): roles = [(inv int64 [n], ids int64 [n], tt int64 [n] or None, tt_want)],
+    a role's id at i being ids[i], or 0 where tt[i] != tt_want."""
+    if not roles:
+        return []
+    if len(roles) > 8:
+        raise L.GrkError('jagged_remap: at most 8 roles per launch')
+    _require_cuda(row_map)
+    if row_map.dtype != torch.int32 or not row_map.is_contiguous():
+        raise L.GrkError('row_map must be a contiguous int32 tensor')
+    rows = row_map.numel()
+    arr = (L.GrkRemapRole * len(roles))()
+    outs, keep = [], []
+    for k, (inv, ids, tt, want) in enumerate(roles):
+        inv = inv.reshape(-1).contiguous()
+        ids = ids.reshape(-1).long().contiguous()
+        if inv.dtype != torch.int64 or ids.numel() != inv.numel() or inv.numel() == 0:
+            raise L.GrkError(f'jagged_remap role {k}: int64 inv and ids of one non-zero length')
+        if tt is not None:
+            tt = tt.reshape(-1).long().contiguous()
+            if tt.numel() != ids.numel():
+                raise L.GrkError(f'jagged_remap role {k}: tt of {tt.numel()} elements, expected {ids.numel()}')
+        out = torch.empty(rows, dtype=torch.int64, device=row_map.device)
+        keep += [inv, ids, tt]
+        outs.append(out)
+        arr[k] = L.GrkRemapRole(inv.data_ptr(), out.data_ptr(), ids.data_ptr(), _ptr(tt), int(want), inv.numel())
+    L.check(L.lib().grk_jagged_remap(arr, len(roles), row_map.data_ptr(), rows, L.stream_ptr(row_map.device)),
+            'grk_jagged_remap')
+    return outs
+
+
 def attention_fwd(args, out, lse=None):
     """grk_attention_fwd: out [B*T, >=H*hd] (args.out_dtype); lse fp32 [B, H, T] (softmax)."""
     _require_cuda(out, lse)

@@ -655,6 +655,20 @@ def _dense_grad_into(g, out, dense_reduce_fn):
         for off, dg in g.dense_grads.items():
             out[off:off + dg.shape[0]] += dg
         return
+    D = out.shape[1]
+    if out.is_cuda and out.is_contiguous():
+        # every range and the gaps between them in one grk_flat_pack launch (bf16 -> fp32)
+        parts, pos = [], 0
+        for off in sorted(g.dense_grads):
+            dg = g.dense_grads[off]
+            if off > pos:
+                parts.append((None, pos * D, (off - pos) * D))
+            parts.append((dg, off * D, dg.shape[0] * D))
+            pos = off + dg.shape[0]
+        if pos < g.rows:
+            parts.append((None, pos * D, (g.rows - pos) * D))
+        K.flat_pack(out.view(-1), parts)
+        return
     pos = 0
     for off in sorted(g.dense_grads):
         dg = g.dense_grads[off]

@@ -25,8 +25,10 @@ import contextlib
 
 import torch
 
+from . import _lib as L
 from . import functional as G
 from . import jagged as J
+from . import kernels as K
 from . import streams as S
 
 
@@ -128,7 +130,7 @@ def _clone_batch(batch):
     return tuple(res)
 
 
-def jagged_remaps(remaps, parts, row_map):
+def jagged_remaps(remaps, parts, row_map, token_type=None):
     """Row-sharded tables + jagged rows: the remaps ShardedFusedAdamW.prepare built
     for the [B, T] batch ({(table, role, mode): (fetched rows, fetched-row index
     [B, T])}) re-indexed to the jagged order -- index[r] = index[row_map[r]].  A row
@@ -137,6 +139,14 @@ def jagged_remaps(remaps, parts, row_map):
     would.  ``parts``: ShardedFusedAdamW._parts(batch) (each role's ids).  Device
     ops only (no host sync: capturable)."""
     ids = {(name, role, mode): v for name, plist in parts.items() for role, _, mode, v in plist}
+    if row_map.is_cuda and token_type is not None:
+        # every role in one grk_jagged_remap launch (was ~8 torch kernels per role)
+        raw = {(name, role, mode): idx for name, plist in parts.items() for role, idx, mode, _ in plist}
+        want = {L.IDX_ITEM_MASK: 1, L.IDX_USER_MASK: 2}
+        keys = [k for k in remaps if k in raw]
+        roles = [(remaps[k][1], raw[k], token_type if k[2] in want else None, want.get(k[2], 0)) for k in keys]
+        outs = K.jagged_remap(roles, row_map)
+        return {k: (remaps[k][0], o.unsqueeze(0)) for k, o in zip(keys, outs)}
     rm = row_map.long()
     src = rm.clamp(min=0)
     out = {}
@@ -232,7 +242,8 @@ class Trainer:
             if self._sharded and getattr(self.model, '_remaps', None) is not None:
                 # prepare() routed the [B, T] batch: its lookups' fetched-row indices follow
                 # the batch into the jagged row order
-                self.model._remaps = jagged_remaps(self.model._remaps, self.opt._parts(batch), jag.row_map)
+                self.model._remaps = jagged_remaps(self.model._remaps, self.opt._parts(batch), jag.row_map,
+                                                   batch[3])
             seq, pos, neg, tt, ntt, _nat, sf, pf, nf, ts, pidx = J.compact(batch, jag)
         with amp:
             h, pe, ne = self.model.encode(seq, pos, neg, tt, sf, pf, nf, timestamps=ts, jagged=jag, pos_idx=pidx)

@@ -336,3 +336,38 @@ def test_flat_pack_equals_cat():
     flat = torch.full((off,), float('nan'), device=DEV)
     K.flat_pack(flat, parts)
     assert torch.equal(flat, torch.cat(ref))
+
+
+def test_grk_jagged_remap_equals_torch_remap():
+    """train.jagged_remaps on the device (grk_jagged_remap, one launch for every role) ==
+    its torch form: span rows follow the row map, dead rows read the role's first
+    padding slot (position 0 when a role has no padding id)."""
+    from tencent_recommendation_2025_amd.sharding import ShardedFusedAdamW
+    from tencent_recommendation_2025_amd.train import jagged_remaps
+    g = torch.Generator().manual_seed(5)
+    B, T, cap = 16, 40, 640
+    starts = torch.randint(0, T - 3, (B,), generator=g).tolist()
+    starts[3] = 0
+    tt = torch.zeros(B, T, dtype=torch.int64)
+    for b, s0 in enumerate(starts):
+        tt[b, s0:] = 1
+        tt[b, s0] = 2
+    seq = torch.randint(1, 500, (B, T), generator=g) * (tt != 0)
+    pos = torch.randint(1, 500, (B, T), generator=g) * (tt != 0)
+    neg = torch.randint(1, 500, (B, T), generator=g)              # no padding id at all
+    batch = tuple(t.to(DEV) for t in (seq, pos, neg, tt))
+    parts = ShardedFusedAdamW._parts(batch)
+    remaps, fetched = {}, object()
+    for name, plist in parts.items():
+        for role, idx, mode, v in plist:
+            inv = torch.randint(0, 10_000, (B * T,), generator=g).to(DEV)
+            remaps[(name, role, mode)] = (fetched, inv.view(B, T))
+    span = [(b, t) for b in range(B) for t in range(starts[b], T)]
+    row_map = torch.full((cap,), -1, dtype=torch.int32)
+    row_map[:len(span)] = torch.tensor([b * T + t for b, t in span], dtype=torch.int32)
+    row_map = row_map.to(DEV)
+    want = jagged_remaps(remaps, parts, row_map)                  # torch form (no token_type)
+    got = jagged_remaps(remaps, parts, row_map, batch[3])         # grk_jagged_remap
+    assert set(got) == set(want)
+    for k in want:
+        assert got[k][0] is want[k][0] and torch.equal(got[k][1], want[k][1]), k
