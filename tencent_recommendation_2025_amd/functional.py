@@ -8,6 +8,7 @@ kernels require device tensors.
 """
 from __future__ import annotations
 
+import os
 import weakref
 
 import torch
@@ -320,6 +321,46 @@ def _lookup_groups(specs, token_type, seq_len, num_tokens, out_ld, extras, split
     return _FeatureLookupFn.apply(specs, token_type, seq_len, num_tokens, out_ld, extras, splits, *weights)
 
 
+# Weight gradients of leaf weights on a side stream (GRK_WGRAD_SIDE=0: in line).  In a
+# layer's backward the dX GEMM, the norm / attention backward and the previous layer
+# depend on each other in a chain, while dW = dY^T X of a leaf weight feeds only the
+# optimizer: issued on a private stream (a parallel branch of the captured step), the
+# split-K wgrad -- MFMA-bound -- runs under the latency-bound attention backward
+# instead of after it.  join_side_work() puts the current stream behind it; the trainer
+# calls it right after backward (inside the captured region), the optimizers before
+# they read a gradient.  Only leaf weights without a gradient yet take the side stream
+# (AccumulateGrad then stores the tensor, no kernel reads it before the join).
+WGRAD_SIDE = os.environ.get('GRK_WGRAD_SIDE', '1') != '0'
+_SIDE_STREAM_INDEX = 6
+_SIDE_PENDING = {}
+
+
+def join_side_work():
+    """The current stream waits for every weight gradient issued on the side stream."""
+    if not _SIDE_PENDING:
+        return
+    for idx, side in list(_SIDE_PENDING.items()):
+        torch.cuda.current_stream(idx).wait_stream(side)
+    _SIDE_PENDING.clear()
+
+
+def _wgrad_side(g2, x2, out_dtype, want_db):
+    from .streams import private_stream
+    dev = g2.device
+    cur = torch.cuda.current_stream(dev)
+    side = private_stream(dev, _SIDE_STREAM_INDEX)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        dw, db = K.wgrad(g2, x2, out_dtype=out_dtype, want_db=want_db)
+    g2.record_stream(side)   # read there: not reused by the current stream before it is done
+    x2.record_stream(side)
+    dw.record_stream(cur)    # allocated there, read here (after the join)
+    if db is not None:
+        db.record_stream(cur)
+    _SIDE_PENDING[dev.index if dev.index is not None else torch.cuda.current_device()] = side
+    return dw, db
+
+
 class _LinearFn(torch.autograd.Function):
     """y = x W^T + b (+ addend) (then ReLU) on grk_gemm (hipBLASLt with stream-K
     eligible).  bf16 operands (the autocast dtype of the reference's training),
@@ -357,6 +398,9 @@ class _LinearFn(torch.autograd.Function):
                    beta=0.0 if addend is None and out is None else 1.0, relu=relu)
         ctx.save_for_backward(x2, wb, y if relu else None)
         ctx.meta = (shp, weight.dtype, None if bias is None else bias.dtype, ctx.needs_input_grad[3])
+        # a leaf weight (and bias) whose gradients nothing but AccumulateGrad consumes
+        ctx.side = WGRAD_SIDE and weight.is_cuda and weight.is_leaf and (bias is None or bias.is_leaf)
+        ctx.leaves = (weight, bias) if ctx.side else None
         return y.view(*shp[:-1], wb.shape[0])
 
     @staticmethod
@@ -373,7 +417,11 @@ class _LinearFn(torch.autograd.Function):
         dx = K.gemm(g2, wb).view(shp) if ctx.needs_input_grad[0] else None
         dw_dt = torch.float32 if wdt == torch.float32 else torch.bfloat16
         dw = db = None
-        if ctx.needs_input_grad[1] and K.wgrad_ok(g2, x2):
+        side = ctx.side and all(t is None or t.grad is None for t in ctx.leaves) \
+            and (bdt is None or bdt == torch.float32 or not ctx.needs_input_grad[2])
+        if ctx.needs_input_grad[1] and K.wgrad_ok(g2, x2) and side:
+            dw, db = _wgrad_side(g2, x2, dw_dt, ctx.needs_input_grad[2])
+        elif ctx.needs_input_grad[1] and K.wgrad_ok(g2, x2):
             # split-K MFMA weight gradient, bias gradient from the same pass over gy
             dw, db = K.wgrad(g2, x2, out_dtype=dw_dt, want_db=ctx.needs_input_grad[2])
             db = db.to(bdt) if db is not None else None

@@ -495,6 +495,7 @@ class FusedAdamW:
 
     @torch.no_grad()
     def step(self):
+        G.join_side_work()   # weight gradients still being written on the side stream
         self.maybe_segment()
         if self._deferred and self._begun != self.t:  # no begin_step: every row to step t, then dense
             self.flush()

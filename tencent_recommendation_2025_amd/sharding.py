@@ -269,6 +269,7 @@ class GradBuckets:
     def _launch(self, b):
         """Bucket b's gradients into its flat buffer (device: one grk_flat_pack launch;
         host: one cat), then its all-reduce."""
+        G.join_side_work()   # weight gradients issued on the side stream (functional.WGRAD_SIDE)
         flat = self.flat[b]
         if flat.is_cuda and all(p.grad is None or p.grad.data_ptr() < flat.data_ptr()
                                 or p.grad.data_ptr() >= flat.data_ptr() + flat.numel() * 4
@@ -579,6 +580,7 @@ class ShardedFusedAdamW(FusedAdamW):
     # -- gradient sync + update -------------------------------------------
     @torch.no_grad()
     def step(self):
+        G.join_side_work()
         if self._deferred and self._begun != self.t:
             raise RuntimeError('ShardedFusedAdamW: call prepare(batch) before forward (Trainer.step does)')
         self._begun = None

@@ -270,6 +270,7 @@ class Trainer:
             self.opt.begin_step(batch)
         loss = self.compute_loss(batch)
         loss.backward()
+        G.join_side_work()   # weight gradients issued on the side stream (functional.WGRAD_SIDE)
         self.opt.step()
         if self.jagged and not torch.cuda.is_current_stream_capturing():
             self.check_jagged()   # eager: one host sync per step
@@ -389,6 +390,7 @@ class Trainer:
             def fwd_bwd():
                 loss = self.compute_loss(batch)
                 loss.backward()
+                G.join_side_work()
                 return loss.detach()
             loss = self._on_side(fwd_bwd)
         finally:
@@ -447,6 +449,7 @@ class Trainer:
             if self._sharded:
                 loss = self.compute_loss(self._static)
                 loss.backward()
+                G.join_side_work()   # every side-stream branch rejoins the capture stream
                 self._static_loss = loss.detach()
             else:
                 self._static_loss = self.eager_step(self._static)
