@@ -339,9 +339,23 @@ def join_side_work():
     """The current stream waits for every weight gradient issued on the side stream."""
     if not _SIDE_PENDING:
         return
-    for idx, side in list(_SIDE_PENDING.items()):
+    for (idx, _), side in list(_SIDE_PENDING.items()):
         torch.cuda.current_stream(idx).wait_stream(side)
     _SIDE_PENDING.clear()
+
+
+def run_on_side(fn, device, index):
+    """fn() on private stream ``index`` of ``device``, forked from the current stream;
+    joined by the next join_side_work().  fn's tensors must be kept alive by the
+    caller (or record_stream'd) until then."""
+    from .streams import private_stream
+    dev = torch.device(device)
+    cur = torch.cuda.current_stream(dev)
+    side = private_stream(dev, index)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        fn()
+    _SIDE_PENDING[(dev.index if dev.index is not None else torch.cuda.current_device(), index)] = side
 
 
 def _wgrad_side(g2, x2, out_dtype, want_db):
@@ -357,7 +371,7 @@ def _wgrad_side(g2, x2, out_dtype, want_db):
     dw.record_stream(cur)    # allocated there, read here (after the join)
     if db is not None:
         db.record_stream(cur)
-    _SIDE_PENDING[dev.index if dev.index is not None else torch.cuda.current_device()] = side
+    _SIDE_PENDING[(dev.index if dev.index is not None else torch.cuda.current_device(), _SIDE_STREAM_INDEX)] = side
     return dw, db
 
 

@@ -20,11 +20,11 @@ Table storage dtype defaults to bf16 (BASELINE config 2); moments are fp32.
 """
 from __future__ import annotations
 
+import ctypes as C
+import os
 import weakref
 
 import torch
-
-import ctypes as C
 
 from . import _lib as L
 from . import functional as G
@@ -127,6 +127,10 @@ class TableGroup:
 # are dense (they feed the dnns through projections: model._projection)
 DEFAULT_GROUPS = (('item', ('item_emb',)), ('user', ('user_emb',)), ('pos', ('pos_emb',)), ('small', None))
 
+
+# The rolling flush's per-step slice on a side stream (GRK_SLICE_SIDE=0: in line).
+SLICE_SIDE = os.environ.get('GRK_SLICE_SIDE', '1') != '0'
+SLICE_SIDE_STREAM = 7
 
 DENSE_FLAT_DIM = 8   # the flat buffer as [rows, 8] for k_adamw_ranges (16-byte fp32 pairs per lane)
 
@@ -460,10 +464,20 @@ class FusedAdamW:
         # (p, m, v) row to exactly zero, so reading it early changes nothing.
         item, user = K.batch_row_ids(*batch[:4], with_user='user' in self._deferred)
         ids = {'item': item, 'user': user}
+        side = self.rolling and SLICE_SIDE and not self.l2_emb and self.clock.ring.is_cuda
         for name, g in self._deferred.items():
-            if self.rolling:   # this step's slice of every row
+            if self.rolling and not side:   # this step's slice of every row
                 K.table_adamw_catchup_slice(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self.clock, self._period)
             K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock, ids[name])
+        if side:
+            # the slice after the batch rows (which it then skips: their step stamps are
+            # current) on a side stream: VALU-bound replay under the step's GEMMs and
+            # attention; no kernel of the step reads or writes the rows it touches (the
+            # gathers read batch rows only), joined before step() updates any row
+            def slices():
+                for g in self._deferred.values():
+                    K.table_adamw_catchup_slice(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self.clock, self._period)
+            G.run_on_side(slices, self.clock.ring.device, SLICE_SIDE_STREAM)
         self._begun = self.t
 
     @torch.no_grad()
@@ -481,6 +495,7 @@ class FusedAdamW:
     @torch.no_grad()
     def flush(self):
         """Bring every row of the deferred tables to the current step (before reading them)."""
+        G.join_side_work()
         if self._deferred and self._seg is not None:
             for g in self._deferred.values():
                 K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock)

@@ -36,7 +36,7 @@ import torch.distributed as dist
 from . import _lib as L
 from . import functional as G
 from . import kernels as K
-from .optim import FusedAdamW, TableGroup
+from .optim import SLICE_SIDE, SLICE_SIDE_STREAM, FusedAdamW, TableGroup
 
 
 # ----------------------------------------------------------- device work ----
@@ -514,11 +514,15 @@ class ShardedFusedAdamW(FusedAdamW):
         self.maybe_segment()
         remaps = {}
         self.sinks = {}
+        # the rolling slice after the fetch (the requested rows are then current and
+        # skipped) on a side stream, under the step's forward and backward; step() joins it
+        # before any shard row is updated
+        slice_side = self.rolling and SLICE_SIDE and self.clock.ring.is_cuda
         for gi, (name, plist) in enumerate(self._parts(batch).items()):
             grp, ex = self.shards[name]
             r = routed[name]
             catchup = None
-            if self.rolling:   # this step's slice of the shard (rolling flush), before any row is read
+            if self.rolling and not slice_side:   # this step's slice of the shard (rolling flush)
                 K.table_adamw_catchup_slice(grp.flat, grp.exp_avg, grp.exp_avg_sq, grp.last, self.clock,
                                             self._period)
             if self.defer:
@@ -540,6 +544,12 @@ class ShardedFusedAdamW(FusedAdamW):
                 off += n
                 remaps[(name, role, mode)] = (ref, inv)
         self.model._remaps = remaps
+        if slice_side:
+            def slices():
+                for grp, _ in self.shards.values():
+                    K.table_adamw_catchup_slice(grp.flat, grp.exp_avg, grp.exp_avg_sq, grp.last, self.clock,
+                                                self._period)
+            G.run_on_side(slices, self.clock.ring.device, SLICE_SIDE_STREAM)
         self._begun = self.t
 
     # -- HIP graph capture of forward + backward (train.Trainer) ------------
