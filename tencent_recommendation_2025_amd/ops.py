@@ -285,11 +285,16 @@ def _hstu_setup(ctx, inputs, output):
     (pre, rab, ln_w, ln_b, key_valid, heads, head_dim, inv_n, eps, precise, dropout_p, seed, seed_dev, seq_range,
      timestamps, rab_t, row_base) = inputs
     _, o, stats = output
+    # o and stats are saved for backward, never differentiated: their None gradients stay
+    # None (materialised, they were a bf16 [N, D] and an fp32 [N, 2] zero fill per layer)
+    ctx.set_materialize_grads(False)
     ctx.save_for_backward(pre, o, stats, rab, ln_w, ln_b, key_valid, seed_dev, seq_range, timestamps, rab_t, row_base)
     ctx.meta = (heads, head_dim, inv_n, precise, dropout_p, seed)
 
 
 def _hstu_backward(ctx, gy, go, gstats):
+    if gy is None:   # y unused (grads are not materialised: _hstu_setup)
+        return (None,) * 17
     pre, o, stats, rab, ln_w, ln_b, key_valid, seed_dev, seq_range, timestamps, rab_t, row_base = ctx.saved_tensors
     heads, head_dim, inv_n, precise, dropout_p, seed = ctx.meta
     dpre, drab, dw, db, drab_t = torch.ops.grk.hstu_core_backward(gy, pre, o, stats, rab, ln_w, ln_b, key_valid,
