@@ -118,7 +118,7 @@ def _time(fn, reps):
     return e0.elapsed_time(e1) / reps
 
 
-PMC_TAG = 'r4'  # round tag of the committed PMC summaries (scripts/pmc_rooflines.py)
+PMC_TAG = 'r5'  # round tag of the committed PMC summaries (scripts/pmc_rooflines.py)
 
 
 def _pmc(name, match):
@@ -498,8 +498,8 @@ def catchup_roofline(opt, reps):
     Timed on copies of the item table's state as the timed region left it (the
     slice the clock points at, its real lags), last[] restored before every
     launch.  Algorithmic bytes: slice rows x D x (2 + 4 + 4) B read and written
-    + 8 B of last[] per row; the kernel is VALU-heavy (~70 instructions per
-    replayed step of 8 elements), reported against HBM."""
+    + 8 B of last[] per row; the kernel is VALU-bound (~100 instructions, 16 of them
+    sqrt / rcp, per replayed step of 8 elements), reported against HBM."""
     from tencent_recommendation_2025_amd import kernels as K
     if not getattr(opt, 'rolling', False):
         return None
@@ -535,7 +535,8 @@ def catchup_roofline(opt, reps):
            'calls_per_step': len(opt._deferred), 'ms_per_step': round(ms * len(opt._deferred), 4),
            'replayed_steps_per_launch': int(lag.sum().item()), 'rows_moved_per_launch': moved,
            'mean_lag_steps': round(float(lag.float().mean().item()), 2),
-           'note': 'VALU-heavy: the g = 0 AdamW replay is ~70 VALU instructions per replayed step of 8 elements',
+           'note': 'VALU-bound: the g = 0 AdamW replay is ~100 VALU instructions (16 of them 8-cycle '
+                   'sqrt / rcp) per replayed step of 8 elements',
            'workload': {'table_rows': int(rows), 'D': int(D), 'slice_rows': int(n), 'period': int(period)}}
     p_ = _pmc(f'{PMC_TAG}_pmc_catchup.json', {k: res['workload'][k] for k in ('table_rows', 'D', 'period')})
     if p_ is not None:

@@ -130,6 +130,10 @@ for e in entries:
         f2, w2, n2 = traffic('k_wgrad_reduce')
         fb, wb, n = f1 + f2, w1 + w2, min(n1, n2)
         name = f'{tag}_pmc_wgrad.json'
+    elif k.startswith('k_adamw_catchup'):
+        # the rolling flush's slice launches of the roofline replays (the run's last catch-ups)
+        fb, wb, n = traffic('k_adamw_catchup')
+        name = f'{tag}_pmc_catchup.json'
     else:
         continue
     out = {'kernel': k, 'workload': e['workload'], 'launches_averaged': n,

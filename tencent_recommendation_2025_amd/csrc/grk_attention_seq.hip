@@ -774,6 +774,11 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
 #ifndef GRK_ATTN_TB_SPLIT
 #define GRK_ATTN_TB_SPLIT 0
 #endif
+//   GRK_DKDV_PREFETCH   dK/dV: the first key tile's K / V fragments loaded before the
+//                       Q / dO staging (1, product) or at the tile (0: 32 VGPRs fewer)
+#ifndef GRK_DKDV_PREFETCH
+#define GRK_DKDV_PREFETCH 1
+#endif
 
 template <int HD, int KIND, int PREC, bool TBK = true>
 __global__ void __launch_bounds__(64 * kSeqWaves) __attribute__((amdgpu_waves_per_eu(PREC < 2 && HD <= 64 ? 2 : 1)))
@@ -797,7 +802,7 @@ k_attn_dkdv_seq(AttnParams p) {
   zero_tail_rows(p, p.dv, p.lddv, HD);
   // key tile j (absolute first + j) visits query tiles j .. ntiles-1
   bf16x8 kpre[KS], vpre[KS];
-  if (PREC < 2 && wave < npairs) {
+  if (GRK_DKDV_PREFETCH && PREC < 2 && wave < npairs) {
     const int row = (first + wave) * 32 + r;
     load_frag<HD>(kpre, p.k, p.ldk, rbase, lo, T, h, row, hh);
     load_frag<HD>(vpre, p.v, p.ldv, rbase, lo, T, h, row, hh);
@@ -876,7 +881,7 @@ k_attn_dkdv_seq(AttnParams p) {
         load_frag_split<HD>(kf, kl, p.k, p.ldk, p.in_dt, p.act, rbase, lo, T, h, myk, hh);
         load_frag_split<HD>(vf, vl, p.v, p.ldv, p.in_dt, p.act, rbase, lo, T, h, myk, hh);
       } else {
-        if (pu == wave && ps == 0) {
+        if (GRK_DKDV_PREFETCH && pu == wave && ps == 0) {
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
             kf[ks] = kpre[ks];
