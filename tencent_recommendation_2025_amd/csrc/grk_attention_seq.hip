@@ -774,6 +774,7 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
 #ifndef GRK_ATTN_TB_SPLIT
 #define GRK_ATTN_TB_SPLIT 0
 #endif
+//   GRK_DKDV_WAVES      dK/dV (hd <= 64, PREC < 2): the waves-per-SIMD register target
 //   GRK_DKDV_PREFETCH   dK/dV: the first key tile's K / V fragments loaded before the
 //                       Q / dO staging (1, product) or at the tile (0: 32 VGPRs fewer)
 #ifndef GRK_DKDV_PREFETCH
@@ -781,7 +782,11 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
 #endif
 
 template <int HD, int KIND, int PREC, bool TBK = true>
-__global__ void __launch_bounds__(64 * kSeqWaves) __attribute__((amdgpu_waves_per_eu(PREC < 2 && HD <= 64 ? 2 : 1)))
+#ifndef GRK_DKDV_WAVES
+#define GRK_DKDV_WAVES 2
+#endif
+__global__ void __launch_bounds__(64 * kSeqWaves)
+__attribute__((amdgpu_waves_per_eu(PREC < 2 && HD <= 64 ? GRK_DKDV_WAVES : 1)))
 k_attn_dkdv_seq(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KS = HD / 16, NDT = (HD + 31) / 32;
