@@ -88,6 +88,28 @@ __device__ __forceinline__ void adam1_g0(float& p, float& m, float& v, const Ada
   v = ve;
 }
 
+// adam1_g0 on two elements at once, written on 2-vectors so every multiply / FMA
+// is one packed v_pk_*_f32 (the denominator's FMA included, which the compiler
+// left unpacked behind the two sqrts): per element the same IEEE operations in the
+// same order -- the same bits as adam1_g0 (the replay loop of k_adamw_catchup).
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void adam2_g0(f2v& p, f2v& m, f2v& v, const AdamStep& s) {
+#pragma clang fp contract(off)
+  const f2v pe = p * s.decay;
+  const f2v me = __builtin_elementwise_fma((f2v)(-s.w1), m, m);
+  const f2v ve = v * s.beta2;
+  f2v sq;
+  sq.x = __builtin_amdgcn_sqrtf(ve.x);
+  sq.y = __builtin_amdgcn_sqrtf(ve.y);
+  const f2v den = __builtin_elementwise_fma(sq, (f2v)(s.inv_bc2), (f2v)(s.eps));
+  f2v r;
+  r.x = __builtin_amdgcn_rcpf(den.x);
+  r.y = __builtin_amdgcn_rcpf(den.y);
+  p = __builtin_elementwise_fma((f2v)(-s.step_size), me * r, pe);
+  m = me;
+  v = ve;
+}
+
 // NV consecutive elements (NV = 4 or 8) of param / exp_avg / exp_avg_sq in
 // registers: param via one 8/16-byte access (bf16) or NV/4 float4s, moments
 // via NV/4 float4s each.
@@ -343,6 +365,9 @@ __global__ void __launch_bounds__(256) k_adamw_ranges(P* __restrict__ param, flo
 // up at least every num_slices steps at a constant per-step cost (the full
 // flush's spike of every row once per segment, spread evenly).
 constexpr int kCatchupLds = 64;
+#ifndef GRK_CATCHUP_PACKED
+#define GRK_CATCHUP_PACKED 1
+#endif
 template <typename P, int NV>
 __global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, float* __restrict__ m,
                                                        float* __restrict__ v, int64_t num_rows, int dim,
@@ -397,11 +422,26 @@ __global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, fl
     for (int st = from + 1; st <= t; ++st) {
       const AdamStep s = staged ? steps[slot] : adam_step(ring[slot]);
       slot = slot + 1 == ring_len ? 0 : slot + 1;
+#if GRK_CATCHUP_PACKED
+#pragma unroll
+      for (int e = 0; e < NV; e += 2) {
+        f2v p2 = {pv[e], pv[e + 1]}, m2 = {mv[e], mv[e + 1]}, v2 = {vv[e], vv[e + 1]};
+        adam2_g0(p2, m2, v2, s);
+        pv[e] = p2.x; pv[e + 1] = p2.y; mv[e] = m2.x; mv[e + 1] = m2.y; vv[e] = v2.x; vv[e + 1] = v2.y;
+        if constexpr (sizeof(P) == 2) {   // one v_cvt_pk_bf16_f32 per pair, then the two halves back
+          typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+          const unsigned w = __builtin_bit_cast(unsigned, __builtin_convertvector(p2, bf2v));
+          pv[e] = __uint_as_float(w << 16);
+          pv[e + 1] = __uint_as_float(w & 0xFFFF0000u);
+        }
+      }
+#else
 #pragma unroll
       for (int e = 0; e < NV; ++e) {
         adam1_g0(pv[e], mv[e], vv[e], s);
         if constexpr (sizeof(P) == 2) pv[e] = bf16_to_f32(f32_to_bf16(pv[e]));
       }
+#endif
     }
     store_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
   }
