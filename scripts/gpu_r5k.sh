@@ -9,6 +9,10 @@ O=gpurun_out/r5k
 mkdir -p $O
 FAULT='illegal memory access|memory access fault|HSA_STATUS_ERROR|hipErrorIllegalAddress|HW Exception|GPU Hang|page not present'
 PYT="python -u -m pytest -v -rs --timeout 200 --timeout-method thread -m gpu"
+timeout -k 10 500 $PYT -s tests/test_gpu_bench_size.py tests/test_gpu_model.py -k "bench_config or deferred or graph_replayed" \
+  > $O/parity.log 2>&1
+echo "parity rc=$?" >> $O/summary.txt
+grep -Eqi "$FAULT" $O/parity.log && { echo "GPU fault"; cat $O/summary.txt; exit 3; }
 GRK_BWD_SLICED=2 timeout -k 10 300 $PYT tests/test_gpu_embedding.py tests/test_gpu_jagged.py -k "chunked or merged or projected" \
   > $O/tests2.log 2>&1
 rc=$?; echo "tests sliced2 rc=$rc" >> $O/summary.txt
@@ -31,7 +35,7 @@ GRK_BWD_SLICED=2 timeout -s KILL 150 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --
   --output-format csv -d /tmp/ph2 -o run -- $B > $O/ph2.log 2>&1
 echo "hit rc=$?" >> $O/summary.txt
 cp $(find /tmp/ph2 -name "*counter_collection.csv" | head -1) $O/bench_hit_sliced2.csv 2>/dev/null
-cat $O/summary.txt; grep -E "passed|failed" $O/tests2.log | tail -3; cat $O/emb_bwd_*.txt | grep projected
+cat $O/summary.txt; grep -E "passed|failed" $O/parity.log $O/tests2.log | tail -4; grep -E "bench-size|table elements|optimizer" $O/parity.log | head -4; cat $O/emb_bwd_*.txt | grep projected
 python - <<'PY'
 import json
 for v in (2, 0):
