@@ -488,6 +488,11 @@ def wgrad_roofline(a, reps, k, wtrace=None):
     if p is not None and uvqk is not None:
         uvqk['traffic'] = int(p['traffic_bytes_per_launch'])
         uvqk['alg_bytes_per_launch'] = int(2 * k * (m + n) + 4 * m * (n + 1))
+        # the family's traffic field: its largest launch's (uvqk: ring kernel + slice reduction)
+        res['traffic'] = uvqk['traffic']
+        res['traffic_note'] = ('rocprofv3 PMC (profiles/%s_pmc_wgrad.json) of the uvqk shape (dW [4D, D] + db, '
+                               'the largest launch): FETCH_SIZE x2 + WRITE_SIZE; algorithmic %d B'
+                               % (PMC_TAG, uvqk['alg_bytes_per_launch']))
     return res
 
 

@@ -124,10 +124,17 @@ for e in entries:
     elif k == 'k_gather':
         fb, wb, n = traffic('k_gather', True)  # widest launch: the seq-side fused lookup
         name = f'{tag}_pmc_gather.json'
-    elif k == 'k_wgrad':
-        # one grk_wgrad call = the ring kernel (k_wgrad_lds<, k_wgrad< before round 4) + k_wgrad_reduce
-        f1, w1, n1 = traffic('k_wgrad_lds<' if any('k_wgrad_lds<' in r['Kernel_Name'] for r in fetch) else 'k_wgrad<')
-        f2, w2, n2 = traffic('k_wgrad_reduce')
+    elif k.startswith('k_wgrad'):
+        # one grk_wgrad call = the ring kernel (k_wgrad_lds<, k_wgrad< before round 4) + k_wgrad_reduce;
+        # round 5: the entry is the whole family, the PMC is the uvqk shape's (the 8-wave 256 x 128 ring,
+        # the largest reduce grid)
+        big = 'k_wgrad_lds<true, 4, 2, 6>'
+        if any(big in r['Kernel_Name'] for r in fetch):
+            f1, w1, n1 = traffic(big)
+            f2, w2, n2 = traffic('k_wgrad_reduce', True)
+        else:
+            f1, w1, n1 = traffic('k_wgrad_lds<' if any('k_wgrad_lds<' in r['Kernel_Name'] for r in fetch) else 'k_wgrad<')
+            f2, w2, n2 = traffic('k_wgrad_reduce')
         fb, wb, n = f1 + f2, w1 + w2, min(n1, n2)
         name = f'{tag}_pmc_wgrad.json'
     elif k.startswith('k_adamw_catchup'):
