@@ -14,7 +14,7 @@ for v in nopre fold foldtb; do
   echo "attn $v rc=$?" >> $O/summary.txt
   grep -Eqi "$FAULT" $O/attn_$v.log && { echo "GPU fault"; cat $O/summary.txt; exit 3; }
 done
-for i in 1 2; do
+for i in 1; do
   for v in default nopre fold foldtb; do
     lib=tencent_recommendation_2025_amd/libgrk.so; [ $v = default ] || lib=abvar/libgrk_$v.so
     GRK_LIB=$PWD/$lib timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --cpu-baseline 0 --roofline-reps 5 \
@@ -27,7 +27,10 @@ for q in 256 512; do
     > $O/quantum_$q.json 2>/dev/null
   echo "quantum $q rc=$?" >> $O/summary.txt
 done
-cat $O/summary.txt; grep -hE "passed|failed" $O/attn_*.log
+timeout -k 10 600 bash scripts/gpu_pmc_round.sh r5 > $O/pmc.log 2>&1
+echo "pmc rc=$?" >> $O/summary.txt
+cp gpurun_out/pmc_r5/r5_pmc_*.json $O/ 2>/dev/null
+cat $O/summary.txt; grep -hE "passed|failed" $O/attn_*.log; grep "vs algorithmic" $O/pmc.log
 python - <<'PY'
 import json, glob
 for f in sorted(glob.glob('gpurun_out/r5l/*.json')):
