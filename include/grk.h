@@ -66,6 +66,9 @@ const char* grk_version(void);
  * process group's watchdog query of those events fail).  Trainer captures its
  * step on one of these. */
 int grk_stream_create(void** stream);
+/* The same with a HIP stream priority (lower = more urgent; clamped into the device's
+ * range): the deferred tables' flush slice runs on a low-priority stream beside the step. */
+int grk_stream_create_priority(void** stream, int priority);
 int grk_stream_destroy(void* stream);
 
 /* ------------------------------------------------------------------------

@@ -127,6 +127,7 @@ SIGNATURES = {
     'grk_last_error': (C.c_char_p, []),
     'grk_version': (C.c_char_p, []),
     'grk_stream_create': (_I, [C.POINTER(C.c_void_p)]),
+    'grk_stream_create_priority': (_I, [C.POINTER(C.c_void_p), _I]),
     'grk_stream_destroy': (_I, [_P]),
     'grk_embedding_gather': (_I, [C.POINTER(GrkFeature), _I, _I, _I, _I, _I64, _P, C.c_int32, _P, _I64, _P, _P]),
     'grk_silu_fp8': (_I, [_P, _I64, _I64, _I, _P, _I64, _P]),

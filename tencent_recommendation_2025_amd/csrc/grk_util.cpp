@@ -46,6 +46,29 @@ extern "C" const char* grk_last_error(void) { return grk::g_err; }
 
 extern "C" const char* grk_version(void) { return "grk 0.1 (gfx950)"; }
 
+// priority: hipStreamCreateWithPriority's value (lower = more urgent; 0 = default,
+// hipDeviceGetStreamPriorityRange gives the range); clamped into the range.
+extern "C" int grk_stream_create_priority(void** stream, int priority) {
+  grk::clear_error();
+  if (!stream) {
+    grk::set_error("stream is NULL");
+    return GRK_EINVAL;
+  }
+  int lo = 0, hi = 0;   // least, greatest priority
+  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (e != hipSuccess) {
+    grk::set_error("hipDeviceGetStreamPriorityRange failed: %s", hipGetErrorString(e));
+    return GRK_EHIP;
+  }
+  const int pr = priority > lo ? lo : (priority < hi ? hi : priority);
+  e = hipStreamCreateWithPriority((hipStream_t*)stream, hipStreamNonBlocking, pr);
+  if (e != hipSuccess) {
+    grk::set_error("hipStreamCreateWithPriority failed: %s", hipGetErrorString(e));
+    return GRK_EHIP;
+  }
+  return GRK_OK;
+}
+
 extern "C" int grk_stream_create(void** stream) {
   grk::clear_error();
   if (!stream) {

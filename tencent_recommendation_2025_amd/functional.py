@@ -349,14 +349,14 @@ def join_side_work():
     _SIDE_PENDING.clear()
 
 
-def run_on_side(fn, device, index):
-    """fn() on private stream ``index`` of ``device``, forked from the current stream;
-    joined by the next join_side_work().  fn's tensors must be kept alive by the
-    caller (or record_stream'd) until then."""
+def run_on_side(fn, device, index, priority=None):
+    """fn() on private stream ``index`` of ``device`` (created with ``priority`` on first
+    use), forked from the current stream; joined by the next join_side_work().  fn's
+    tensors must be kept alive by the caller (or record_stream'd) until then."""
     from .streams import private_stream
     dev = torch.device(device)
     cur = torch.cuda.current_stream(dev)
-    side = private_stream(dev, index)
+    side = private_stream(dev, index, priority)
     side.wait_stream(cur)
     with torch.cuda.stream(side):
         fn()

@@ -131,6 +131,10 @@ DEFAULT_GROUPS = (('item', ('item_emb',)), ('user', ('user_emb',)), ('pos', ('po
 # The rolling flush's per-step slice on a side stream (GRK_SLICE_SIDE=0: in line).
 SLICE_SIDE = os.environ.get('GRK_SLICE_SIDE', '1') != '0'
 SLICE_SIDE_STREAM = 7
+# its stream's HIP priority (GRK_SLICE_PRIORITY; 0 = default; positive = less urgent,
+# clamped into the device's range): the main chain's kernels first, the replay in the gaps
+SLICE_SIDE_PRIORITY = int(os.environ.get('GRK_SLICE_PRIORITY', '0'))
+SLICE_AT = os.environ.get('GRK_SLICE_AT', 'forward')   # 'forward' | 'backward' (see begin_step)
 
 DENSE_FLAT_DIM = 8   # the flat buffer as [rows, 8] for k_adamw_ranges (16-byte fp32 pairs per lane)
 
@@ -473,12 +477,23 @@ class FusedAdamW:
             # the slice after the batch rows (which it then skips: their step stamps are
             # current) on a side stream: VALU-bound replay under the step's GEMMs and
             # attention; no kernel of the step reads or writes the rows it touches (the
-            # gathers read batch rows only), joined before step() updates any row
+            # gathers read batch rows only), joined before step() updates any row.
+            # GRK_SLICE_AT=backward: forked when the trainer starts the backward
+            # (side_work()), beside the latency-bound attention backward instead of the
+            # forward's gathers
             def slices():
                 for g in self._deferred.values():
                     K.table_adamw_catchup_slice(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self.clock, self._period)
-            G.run_on_side(slices, self.clock.ring.device, SLICE_SIDE_STREAM)
+            self._side_pending = slices
+            if SLICE_AT != 'backward':
+                self.side_work()
         self._begun = self.t
+
+    def side_work(self):
+        """Fork the pending flush slice onto its side stream (Trainer: before backward)."""
+        fn, self._side_pending = getattr(self, '_side_pending', None), None
+        if fn is not None:
+            G.run_on_side(fn, self.clock.ring.device, SLICE_SIDE_STREAM, SLICE_SIDE_PRIORITY)
 
     @torch.no_grad()
     def l2_term(self):
@@ -510,6 +525,7 @@ class FusedAdamW:
 
     @torch.no_grad()
     def step(self):
+        self.side_work()     # a slice no trainer forked yet: fork it now (joined right below)
         G.join_side_work()   # weight gradients still being written on the side stream
         self.maybe_segment()
         if self._deferred and self._begun != self.t:  # no begin_step: every row to step t, then dense

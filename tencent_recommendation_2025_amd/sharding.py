@@ -36,7 +36,7 @@ import torch.distributed as dist
 from . import _lib as L
 from . import functional as G
 from . import kernels as K
-from .optim import SLICE_SIDE, SLICE_SIDE_STREAM, FusedAdamW, TableGroup
+from .optim import SLICE_SIDE, SLICE_SIDE_PRIORITY, SLICE_SIDE_STREAM, FusedAdamW, TableGroup
 
 
 # ----------------------------------------------------------- device work ----
@@ -549,7 +549,7 @@ class ShardedFusedAdamW(FusedAdamW):
                 for grp, _ in self.shards.values():
                     K.table_adamw_catchup_slice(grp.flat, grp.exp_avg, grp.exp_avg_sq, grp.last, self.clock,
                                                 self._period)
-            G.run_on_side(slices, self.clock.ring.device, SLICE_SIDE_STREAM)
+            G.run_on_side(slices, self.clock.ring.device, SLICE_SIDE_STREAM, SLICE_SIDE_PRIORITY)
         self._begun = self.t
 
     # -- HIP graph capture of forward + backward (train.Trainer) ------------

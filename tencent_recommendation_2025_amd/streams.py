@@ -17,8 +17,9 @@ import torch
 _STREAMS = {}
 
 
-def private_stream(device, index=0):
-    """Private stream number ``index`` of ``device``."""
+def private_stream(device, index=0, priority=None):
+    """Private stream number ``index`` of ``device`` (``priority``: a HIP stream priority
+    for its creation, lower = more urgent; None = the default)."""
     from . import _lib as L
     dev = torch.device(device)
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
@@ -26,7 +27,11 @@ def private_stream(device, index=0):
     if s is None:
         with torch.cuda.device(idx):
             raw = ctypes.c_void_p()
-            L.check(L.lib().grk_stream_create(ctypes.byref(raw)), 'grk_stream_create')
+            if priority is None:
+                L.check(L.lib().grk_stream_create(ctypes.byref(raw)), 'grk_stream_create')
+            else:
+                L.check(L.lib().grk_stream_create_priority(ctypes.byref(raw), int(priority)),
+                        'grk_stream_create_priority')
             s = _STREAMS[(idx, index)] = torch.cuda.ExternalStream(raw.value, device=torch.device('cuda', idx))
     return s
 

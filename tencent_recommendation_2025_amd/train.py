@@ -269,6 +269,8 @@ class Trainer:
         if hasattr(self.opt, 'begin_step'):  # deferred table updates: bring this batch's rows up to date
             self.opt.begin_step(batch)
         loss = self.compute_loss(batch)
+        if hasattr(self.opt, 'side_work'):
+            self.opt.side_work()   # the deferred tables' flush slice beside the backward (GRK_SLICE_AT)
         loss.backward()
         G.join_side_work()   # weight gradients issued on the side stream (functional.WGRAD_SIDE)
         self.opt.step()
