@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5, call m: where the flush slice overlaps (GRK_SLICE_AT forward / backward) and
-# its stream priority; bitwise deferred / graph tests with the backward fork.
+# the capture stream's priority (GRK_MAIN_PRIORITY=-1); bitwise deferred / graph tests with the backward fork.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -14,9 +14,10 @@ GRK_SLICE_AT=backward timeout -k 10 500 python -u -m pytest -v -rs --timeout 300
 echo "tests rc=$?" >> $O/summary.txt
 grep -Eqi "$FAULT" $O/tests.log && { echo "GPU fault"; cat $O/summary.txt; exit 3; }
 for i in 1 2; do
-  for cfg in "forward 0" "backward 0" "forward 1" "backward 1"; do
+  for cfg in "forward 0" "backward 0" "forward -1" "backward -1"; do
     set -- $cfg
-    GRK_SLICE_AT=$1 GRK_SLICE_PRIORITY=$2 timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --cpu-baseline 0 \
+    if [ "$2" = 0 ]; then unset GRK_MAIN_PRIORITY; else export GRK_MAIN_PRIORITY=$2; fi
+    GRK_SLICE_AT=$1 timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --cpu-baseline 0 \
       --rooflines 0 > $O/bench_${1}_$2_$i.json 2>/dev/null
     echo "bench $1 $2 $i rc=$?" >> $O/summary.txt
   done

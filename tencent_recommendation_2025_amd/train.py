@@ -22,6 +22,7 @@ the device to drain before its all-to-alls."""
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 
@@ -32,11 +33,16 @@ from . import kernels as K
 from . import streams as S
 
 
+# the capture stream's HIP priority (GRK_MAIN_PRIORITY, e.g. -1 = the most urgent level):
+# side work (the flush slice) then fills the gaps the step's own chain leaves
+MAIN_PRIORITY = os.environ.get('GRK_MAIN_PRIORITY')
+
+
 def private_stream(device):
     """The process's own capture stream for ``device`` (streams.private_stream):
     never one of torch's pooled streams, which a process group may record its
     collectives' events on."""
-    return S.private_stream(device, 0)
+    return S.private_stream(device, 0, None if MAIN_PRIORITY is None else int(MAIN_PRIORITY))
 
 
 def _tensors(batch):
