@@ -137,6 +137,9 @@ for e in entries:
             f2, w2, n2 = traffic('k_wgrad_reduce')
         fb, wb, n = f1 + f2, w1 + w2, min(n1, n2)
         name = f'{tag}_pmc_wgrad.json'
+        if 'alg_bytes_per_launch' not in e:   # the family entry: the uvqk shape's operands + outputs
+            w = e['workload']
+            e = dict(e, alg_bytes_per_launch=int(2 * w['K'] * (w['M'] + w['N']) + 4 * w['M'] * (w['N'] + 1)))
     elif k.startswith('k_adamw_catchup'):
         # the rolling flush's slice launches of the roofline replays (the run's last catch-ups)
         fb, wb, n = traffic('k_adamw_catchup')
