@@ -13,7 +13,7 @@ GRK_SLICE_AT=backward timeout -k 10 500 python -u -m pytest -v -rs --timeout 300
   > $O/tests.log 2>&1
 echo "tests rc=$?" >> $O/summary.txt
 grep -Eqi "$FAULT" $O/tests.log && { echo "GPU fault"; cat $O/summary.txt; exit 3; }
-for i in 1 2; do
+for i in 1; do
   for cfg in "forward 0" "backward 0" "forward -1" "backward -1"; do
     set -- $cfg
     if [ "$2" = 0 ]; then unset GRK_MAIN_PRIORITY; else export GRK_MAIN_PRIORITY=$2; fi
@@ -22,5 +22,8 @@ for i in 1 2; do
     echo "bench $1 $2 $i rc=$?" >> $O/summary.txt
   done
 done
+timeout -k 10 600 bash scripts/gpu_pmc_round.sh r5 > $O/pmc.log 2>&1
+echo "pmc rc=$?" >> $O/summary.txt
+cp gpurun_out/pmc_r5/r5_pmc_*.json gpurun_out/pmc_r5/summary.txt $O/ 2>/dev/null
 cat $O/summary.txt $O/prio.txt; grep -E "passed|failed" $O/tests.log | tail -3
 for f in $O/bench_*.json; do echo "$(basename $f) $(grep -o '"ms_per_step": [0-9.]*' $f | head -1)"; done
