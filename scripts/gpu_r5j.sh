@@ -9,7 +9,7 @@ O=gpurun_out/r5j
 mkdir -p $O
 FAULT='illegal memory access|memory access fault|HSA_STATUS_ERROR|hipErrorIllegalAddress|HW Exception|GPU Hang|page not present'
 PYT="python -u -m pytest -v -rs -s --timeout 300 --timeout-method thread -m gpu"
-timeout -k 10 400 $PYT tests/test_gpu_bench_size.py \
+timeout -k 10 500 $PYT tests/test_gpu_bench_size.py tests/test_gpu_model.py -k "bench_config or deferred or graph_replayed" \
   > $O/parity.log 2>&1
 echo "parity rc=$?" >> $O/summary.txt
 grep -Eqi "$FAULT" $O/parity.log && { echo "GPU fault"; exit 3; }
