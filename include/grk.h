@@ -447,7 +447,7 @@ int grk_batch_row_ids(const void* seq, const void* pos, const void* neg, const v
 /* Multi-tensor row gather for the jagged layout: for each copy,
  * dst + r * dst_ld <- src + row_map[r] * src_ld (row_bytes bytes; zeros where
  * row_map[r] < 0), r in [0, rows), all copies in one launch.  row_bytes,
- * strides and pointers multiples of 4; at most 48 copies. */
+ * strides and pointers multiples of 4; at most 64 copies. */
 typedef struct grk_row_copy {
   const void* src;
   void* dst;

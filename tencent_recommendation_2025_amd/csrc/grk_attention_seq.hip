@@ -115,13 +115,77 @@ __global__ void __launch_bounds__(256) k_seq_ranges(const uint8_t* __restrict__ 
 }
 
 // out[3 i + 2] = the sequence with the i-th most keys from its first valid one
-// (T - first descending, ties by index): a rank count, one workgroup.
+// (T - first descending, ties by index): a rank count, one workgroup.  The
+// key counts are staged in LDS first when B <= kSeqOrderLds (read from memory
+// in the rank loop they cost 84 us at B = 128, nearly all load latency).
+constexpr int kSeqOrderLds = 8192;
 __global__ void __launch_bounds__(1024) k_seq_order(int B, int T, int* __restrict__ out) {
+  __shared__ int len[kSeqOrderLds];
+  const bool lds = B <= kSeqOrderLds;
+  if (lds)
+    for (int b = threadIdx.x; b < B; b += blockDim.x) len[b] = T - out[3 * b];
+  __syncthreads();
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    const int lb = T - out[3 * b];
+    const int lb = lds ? len[b] : T - out[3 * b];
     int rank = 0;
     for (int c = 0; c < B; ++c) {
-      const int lc = T - out[3 * c];
+      const int lc = lds ? len[c] : T - out[3 * c];
+      rank += (lc > lb) | ((lc == lb) & (c < b));
+    }
+    out[3 * rank + 2] = b;
+  }
+}
+
+// Both columns in ONE workgroup for B <= kSeqFused: 16 waves scan 4
+// sequences each per round (their key bytes' loads in flight together), the
+// key counts T - first go to LDS, and the rank count reads them there.  Same
+// output as k_seq_ranges + k_seq_order, one launch instead of two.
+constexpr int kSeqFused = 1024;
+__global__ void __launch_bounds__(1024) k_seq_ranges_order(const uint8_t* __restrict__ kv, int B, int T,
+                                                           int* __restrict__ out) {
+  __shared__ int len[kSeqFused];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int b0 = 4 * w; b0 < B; b0 += 64) {
+    int first[4], cnt[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      first[u] = T;
+      cnt[u] = 0;
+    }
+    for (int j = lane; j < T; j += 64) {
+      uint8_t x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = b0 + u < B ? kv[(int64_t)(b0 + u) * T + j] : 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (x[u]) {
+          first[u] = min(first[u], j);
+          ++cnt[u];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        first[u] = min(first[u], __shfl_xor(first[u], off));
+        cnt[u] += __shfl_xor(cnt[u], off);
+      }
+    if (lane == 0)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int b = b0 + u;
+        if (b >= B) break;
+        out[3 * b] = first[u];
+        out[3 * b + 1] = cnt[u] == T - first[u];
+        len[b] = T - first[u];
+      }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const int lb = len[b];
+    int rank = 0;
+    for (int c = 0; c < B; ++c) {
+      const int lc = len[c];
       rank += (lc > lb) | ((lc == lb) & (c < b));
     }
     out[3 * rank + 2] = b;
@@ -1112,6 +1176,11 @@ extern "C" int grk_seq_ranges(const uint8_t* key_valid, int batch, int seq_len, 
   GRK_CHECK_ARG(batch >= 0 && seq_len > 0, "batch must be >= 0 and seq_len > 0");
   if (batch == 0) return GRK_OK;
   GRK_CHECK_ARG(key_valid && ranges, "key_valid and ranges required");
+  if (batch <= kSeqFused) {
+    k_seq_ranges_order<<<1, 1024, 0, (hipStream_t)stream>>>(key_valid, batch, seq_len, ranges);
+    GRK_LAUNCH_CHECK();
+    return GRK_OK;
+  }
   k_seq_ranges<<<(batch + 3) / 4, 256, 0, (hipStream_t)stream>>>(key_valid, batch, seq_len, ranges);
   GRK_LAUNCH_CHECK();
   k_seq_order<<<1, 1024, 0, (hipStream_t)stream>>>(batch, seq_len, ranges);

@@ -47,13 +47,33 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// Counter-based dropout decision for element (row, col); identical in fwd/bwd.
-__device__ __forceinline__ bool ng_keep(unsigned long long seed, int64_t row, int col, int dim, float p) {
-  unsigned long long x = seed ^ ((unsigned long long)(row * dim + col) * 0x9E3779B97F4A7C15ull);
+// Dropout decisions of the norm gate and the embedding combine: element
+// (row, col) of a [rows, dim] activation is dropped iff its 16-bit uniform is
+// below thr16 = ceil(p * 65536) (the drop probability is p to within 2^-16).
+// The uniforms of the flattened elements 4j .. 4j+3 are the four 16-bit fields
+// of ONE splitmix64 finalisation of (seed, j) -- a quarter of the 64-bit
+// multiplies of one mix per element, which left the gate kernels VALU-bound
+// (k_ng_fwd 540 VALU per row-lane, 84 of them quarter-rate integer multiplies).
+// Forward and backward draw the same decisions; dim % 8 == 0, so a lane's 8
+// elements are two whole groups.
+__device__ __forceinline__ unsigned long long drop_mix(unsigned long long seed, unsigned long long j) {
+  unsigned long long x = seed ^ (j * 0x9E3779B97F4A7C15ull);
   x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
   x ^= x >> 27; x *= 0x94D049BB133111EBull;
   x ^= x >> 31;
-  return (float)(x >> 40) * (1.0f / 16777216.0f) >= p;
+  return x;
+}
+
+__device__ __forceinline__ void drop8(unsigned long long seed, float p, int64_t row, int c8, int dim, float* m) {
+  const float rk = 1.0f / (1.0f - p);
+  const unsigned thr = (unsigned)ceilf(p * 65536.0f);
+  const unsigned long long j = (unsigned long long)(row * dim + c8) >> 2;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const unsigned long long x = drop_mix(seed, j + g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[4 * g + e] = ((unsigned)(x >> (16 * e)) & 0xFFFFu) >= thr ? rk : 0.f;
+  }
 }
 
 __device__ __forceinline__ void load8(const bf16_t* p, float* f) {
@@ -81,10 +101,12 @@ __device__ __forceinline__ void load8f(const float* p, float* f) {
 
 // dropout multiplier of the 8 elements starting at column c8
 __device__ __forceinline__ void keep8(const NGParams& p, int64_t row, int c8, float* m) {
-  const float rk = 1.0f / (1.0f - p.dropout_p);
-  const unsigned long long seed = p.dropout_p > 0.f && p.seed_dev ? *p.seed_dev : p.seed;
+  if (p.dropout_p <= 0.f) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) m[e] = p.dropout_p > 0.f ? (ng_keep(seed, row, c8 + e, p.dim, p.dropout_p) ? rk : 0.f) : 1.f;
+    for (int e = 0; e < 8; ++e) m[e] = 1.f;
+    return;
+  }
+  drop8(p.seed_dev ? *p.seed_dev : p.seed, p.dropout_p, row, c8, p.dim, m);
 }
 
 // ------------------------------------------------------------------ forward --
@@ -430,8 +452,9 @@ __global__ void __launch_bounds__(256) k_silu_fp8(const bf16_t* __restrict__ pre
                                                   int cols, unsigned char* __restrict__ out, int64_t ldo) {
   const int per_row = cols / 8;
   const int64_t units = rows * per_row;
+  const bool div32 = units < ((int64_t)1 << 32);   // 32-bit division where the units allow
   for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = u / per_row;
+    const int64_t r = div32 ? (int64_t)((uint32_t)u / (uint32_t)per_row) : u / per_row;
     const int c = (int)(u - r * per_row) * 8;
     const uint4 w = *reinterpret_cast<const uint4*>(pre + r * ldp + c);
     const unsigned ws[4] = {w.x, w.y, w.z, w.w};
@@ -456,8 +479,9 @@ __global__ void __launch_bounds__(256) k_dsilu_mul(bf16_t* __restrict__ g, int64
                                                    int cols) {
   const int per_row = cols / 8;
   const int64_t units = rows * per_row;
+  const bool div32 = units < ((int64_t)1 << 32);   // 32-bit division where the units allow
   for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = u / per_row;
+    const int64_t r = div32 ? (int64_t)((uint32_t)u / (uint32_t)per_row) : u / per_row;
     const int c = (int)(u - r * per_row) * 8;
     uint4* gp = reinterpret_cast<uint4*>(g + r * ldg + c);
     const uint4 gw = *gp, pw = *reinterpret_cast<const uint4*>(pre + r * ldp + c);
@@ -502,17 +526,15 @@ __device__ __forceinline__ void ec_keep8(const ECParams& p, int64_t row, int c8,
     for (int e = 0; e < 8; ++e) m[e] = 1.f;
     return;
   }
-  const float rk = 1.0f / (1.0f - p.dropout_p);
-  const unsigned long long seed = p.seed_dev ? *p.seed_dev : p.seed;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) m[e] = ng_keep(seed, row, c8 + e, p.dim, p.dropout_p) ? rk : 0.f;
+  drop8(p.seed_dev ? *p.seed_dev : p.seed, p.dropout_p, row, c8, p.dim, m);
 }
 
 __global__ void __launch_bounds__(256) k_emb_combine(ECParams p) {
   const int per_row = p.dim >> 3;
   const int64_t units = p.rows * per_row;
+  const bool div32 = units < ((int64_t)1 << 32);   // 32-bit division where the units allow
   for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = u / per_row;
+    const int64_t r = div32 ? (int64_t)((uint32_t)u / (uint32_t)per_row) : u / per_row;
     const int c = (int)(u - r * per_row) * 8;
     float a[8], b[8], q[8], m[8], y[8];
     load8(p.a + r * p.lda + c, a);
@@ -534,8 +556,9 @@ __global__ void __launch_bounds__(256) k_emb_combine(ECParams p) {
 __global__ void __launch_bounds__(256) k_emb_combine_bwd(ECParams p) {
   const int per_row = p.dim >> 3;
   const int64_t units = p.rows * per_row;
+  const bool div32 = units < ((int64_t)1 << 32);   // 32-bit division where the units allow
   for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = u / per_row;
+    const int64_t r = div32 ? (int64_t)((uint32_t)u / (uint32_t)per_row) : u / per_row;
     const int c = (int)(u - r * per_row) * 8;
     float g[8], m[8], t[8];
     load8(p.gy + r * p.ldgy + c, g);

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -592,6 +593,9 @@ def batch_row_ids(seq, pos, neg, token_type, with_user=True):
     return item, user
 
 
+MAX_ROW_COPIES = int(os.environ.get('GRK_MAX_ROW_COPIES', '64'))   # kMaxRowCopies (csrc/grk_jagged.hip); A/B builds: 48
+
+
 def gather_rows(pairs, row_map):
     """dst[r] = src[row_map[r]] (zeros where row_map[r] < 0) for every (src, dst) pair
     in ONE launch (grk_gather_rows): src [N, ...] and dst [rows, ...] of one dtype with
@@ -602,8 +606,8 @@ def gather_rows(pairs, row_map):
     _require_cuda(row_map, *[t for pr in pairs for t in pr])
     if row_map.dtype != torch.int32 or not row_map.is_contiguous():
         raise L.GrkError('row_map must be a contiguous int32 tensor')
-    for i in range(0, len(pairs), 48):
-        chunk = pairs[i:i + 48]
+    for i in range(0, len(pairs), MAX_ROW_COPIES):
+        chunk = pairs[i:i + MAX_ROW_COPIES]
         cps = (L.GrkRowCopy * len(chunk))()
         for j, (src, dst) in enumerate(chunk):
             if src.dtype != dst.dtype or dst.shape[0] != rows or src.shape[1:] != dst.shape[1:]:

@@ -263,6 +263,23 @@ def test_seq_ranges(K):
     np.testing.assert_array_equal(got[:, 2], [1, 3, 2, 0, 4])   # T - first: 30, 40, 35, 37, 0
 
 
+@pytest.mark.parametrize('B', [1, 128, 1024, 1025, 9000])   # one-launch form (<= 1024), LDS rank, memory rank
+def test_seq_ranges_random(K, B):
+    T = 201
+    rng = np.random.default_rng(B)
+    first = rng.integers(0, T + 1, B)
+    first[rng.random(B) < 0.3] = rng.integers(0, 4)          # many ties in the length order
+    valid = (np.arange(T)[None, :] >= first[:, None]).astype(np.uint8)
+    holes = rng.random(B) < 0.2
+    valid[holes, -1] = 0                                     # not contiguous to T
+    got = K.seq_ranges(torch.from_numpy(valid).to(DEV)).cpu().numpy()
+    f = np.where(valid.any(1), valid.argmax(1), T)
+    contig = valid.sum(1) == T - f
+    np.testing.assert_array_equal(got[:, 0], f)
+    np.testing.assert_array_equal(got[:, 1], contig.astype(np.int32))
+    np.testing.assert_array_equal(got[:, 2], np.argsort(-(T - f), kind='stable'))
+
+
 @pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
 def test_precomputed_ranges_bitwise_equal(K, kind):
     a, _, _ = run(K, kind, B=3, T=201, H=2, hd=64, lens=[201, 120, 7], precise=False, act='silu' if kind else None)

@@ -27,15 +27,16 @@ def nrel(a, b):
 
 
 def keep_np(seed, rows, dim, p):
-    """numpy replica of ng_keep() in grk_hstu.hip (test infrastructure)."""
+    """numpy replica of drop8() in grk_hstu.hip (test infrastructure): one splitmix64
+    finalisation per 4 consecutive elements, 16-bit uniforms, kept iff >= ceil(p 2^16)."""
     with np.errstate(over='ignore'):
-        idx = np.arange(rows * dim, dtype=np.uint64).reshape(rows, dim)
-        x = np.uint64(seed) ^ (idx * np.uint64(0x9E3779B97F4A7C15))
+        j = np.arange(rows * dim // 4, dtype=np.uint64)
+        x = np.uint64(seed) ^ (j * np.uint64(0x9E3779B97F4A7C15))
         x ^= x >> np.uint64(30); x *= np.uint64(0xBF58476D1CE4E5B9)
         x ^= x >> np.uint64(27); x *= np.uint64(0x94D049BB133111EB)
         x ^= x >> np.uint64(31)
-    u = (x >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
-    return torch.from_numpy(u >= np.float32(p))
+    u16 = np.stack([(x >> np.uint64(16 * e)) & np.uint64(0xFFFF) for e in range(4)], 1).reshape(rows, dim)
+    return torch.from_numpy(u16 >= np.ceil(np.float32(p) * np.float32(65536)))
 
 
 def reference(o, u, w, b, eps, gy, keep, p):

@@ -78,6 +78,29 @@ def test_layout_and_gather_match_oracle():
             J.check_error(jag.err)
 
 
+def test_gather_rows_many_copies_every_unit_width():
+    """70 copies (two launches of <= 64) with rows of 4 .. 132 bytes: 16-, 8- and
+    4-byte units, and sources offset by 4 / 8 bytes from 16-byte alignment."""
+    from tencent_recommendation_2025_amd import kernels as K
+    rng = np.random.default_rng(5)
+    N, rows = 3001, 2113
+    row_map = rng.integers(-1, N, rows).astype(np.int32)
+    rmap = torch.from_numpy(row_map).to(DEV)
+    pairs, want = [], []
+    for i in range(70):
+        width = [1, 2, 3, 4, 8, 33, 6][i % 7]                       # int32 words per row
+        lead = [0, 1, 2][i % 3]                                     # misalign the source start
+        base = torch.from_numpy(rng.integers(-2**31, 2**31 - 1, N * width + lead).astype(np.int32)).to(DEV)
+        src = base[lead:].view(N, width)
+        dst = torch.full((rows, width), 9, dtype=torch.int32, device=DEV)
+        pairs.append((src, dst))
+        s = src.cpu().numpy()
+        want.append(np.where(row_map[:, None] >= 0, s[np.maximum(row_map, 0)], 0))
+    K.gather_rows(pairs, rmap)
+    for i, ((_, dst), w) in enumerate(zip(pairs, want)):
+        assert np.array_equal(dst.cpu().numpy(), w), i
+
+
 def _hstu_case(B, T, H, hd, seed, holes=False):
     rng = np.random.default_rng(seed)
     D = H * hd
