@@ -252,6 +252,14 @@ def table_adamw_ranges(param, exp_avg, exp_avg_sq, clock, ranges, shadow=None):
     (grk_table_adamw_ranges_dev): ranges = [(row_offset, grad [rows, >= D] bf16/fp32)],
     other rows g = 0.  shadow (bf16, param's shape, fp32 param only): also receives
     the updated parameters rounded to bf16."""
+    launch_prepared(prepare_table_adamw_ranges(param, exp_avg, exp_avg_sq, clock, ranges, shadow))
+
+
+def prepare_table_adamw_ranges(param, exp_avg, exp_avg_sq, clock, ranges, shadow=None):
+    """The checked arguments of one table_adamw_ranges launch (a PreparedCall):
+    launch_prepared() runs it on the current stream.  A caller whose tensors keep
+    their storage from step to step (optim.DenseFlat) builds it once -- the ctypes
+    range array is most of the host cost of a launch with dozens of ranges."""
     _require_cuda(param, exp_avg, exp_avg_sq, *[g for _, g in ranges])
     if shadow is not None and (shadow.dtype != torch.bfloat16 or shadow.shape != param.shape
                                or not shadow.is_contiguous() or param.dtype != torch.float32):
@@ -270,11 +278,26 @@ def table_adamw_ranges(param, exp_avg, exp_avg_sq, clock, ranges, shadow=None):
             # k_adamw_ranges reads fp32 gradient rows as 16-byte vectors
             raise L.GrkError(f'range {i}: fp32 grad rows must be 16-byte aligned')
         arr[i] = L.GrkGradRange(int(off), int(off) + g.shape[0], g.data_ptr(), g.stride(0), L.dtype_code(g.dtype), 0)
-    rc = L.lib().grk_table_adamw_ranges_dev(param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(),
-                                            exp_avg_sq.data_ptr(), rows, D, arr, len(rs), clock.ring.data_ptr(),
-                                            clock.ring_len, clock.t.data_ptr(),
-                                            None if shadow is None else shadow.data_ptr(), L.stream_ptr(param.device))
-    L.check(rc, 'grk_table_adamw_ranges_dev')
+    args = (param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(), exp_avg_sq.data_ptr(), rows, D, arr,
+            len(rs), clock.ring.data_ptr(), clock.ring_len, clock.t.data_ptr(),
+            None if shadow is None else shadow.data_ptr())
+    return PreparedCall('grk_table_adamw_ranges_dev', args, param.device,
+                        (param, exp_avg, exp_avg_sq, clock.ring, clock.t, shadow, [g for _, g in rs]))
+
+
+@dataclass
+class PreparedCall:
+    """A grk entry point and its arguments but the stream (appended at launch);
+    ``keep`` holds the tensors the pointers refer to."""
+    name: str
+    args: tuple
+    device: torch.device
+    keep: tuple
+
+
+def launch_prepared(call):
+    rc = getattr(L.lib(), call.name)(*call.args, L.stream_ptr(call.device))
+    L.check(rc, call.name)
 
 
 def table_l2_norm(param, l2, norm=None, coef=None):

@@ -215,6 +215,7 @@ class DenseFlat:
         self.exp_avg = torch.zeros_like(self.buf)
         self.exp_avg_sq = torch.zeros_like(self.buf)
         self._ptrs = [p.data_ptr() for p in self.params]
+        self._prep_key, self._prepared = None, []
         self.shadow = None
         if shadow:
             self.shadow = self.buf.to(torch.bfloat16)
@@ -271,19 +272,36 @@ class DenseFlat:
             # the update would land in the old buffer
             raise RuntimeError('dense_flat: a parameter no longer lives in the flat buffer')
         grads = [p.grad for p in self.params]
+        # the launches' arguments are kept while every gradient is the same storage
+        # as last step (row-sharded: views of the all-reduce buckets; graph replays):
+        # rebuilding the ctypes range arrays of ~50 parameters costs more host time
+        # than the update takes on the device
+        key = (tuple(None if g is None else (g.data_ptr(), g.dtype, g.is_contiguous()) for g in grads),
+               id(clock))
+        if key == self._prep_key:
+            for call in self._prepared:
+                K.launch_prepared(call)
+            return
+        calls, reusable = [], True
         for lo, hi, idx in split_runs(grad_runs(self.starts, self.ends, [g is not None for g in grads]),
                                       self.starts, self.ends, K.MAX_GRAD_RANGES):
             ranges = []
             for i in idx:
                 g = grads[i]
                 if g.dtype not in (torch.float32, torch.bfloat16):
-                    g = g.float()
-                g = g.contiguous()
+                    g, reusable = g.float(), False
+                if not g.is_contiguous():
+                    g, reusable = g.contiguous(), False
                 if g.data_ptr() % 16:          # the kernel reads fp32 gradients as 16-byte vectors
-                    g = g.clone()
+                    g, reusable = g.clone(), False
                 ranges.append((self.starts[i] - lo, g.view(-1, DENSE_FLAT_DIM)))
-            K.table_adamw_ranges(self.buf[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi], clock, ranges,
-                                 shadow=None if self.shadow is None else self.shadow[lo:hi])
+            calls.append(K.prepare_table_adamw_ranges(self.buf[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi],
+                                                      clock, ranges,
+                                                      shadow=None if self.shadow is None else self.shadow[lo:hi]))
+        for call in calls:
+            K.launch_prepared(call)
+        # copies made for the launch are fresh each step: only a copy-free plan is kept
+        self._prep_key, self._prepared = (key, calls) if reusable else (None, [])
 
     def state(self, p):
         """{'exp_avg', 'exp_avg_sq'} views of parameter p (torch AdamW's state names)."""

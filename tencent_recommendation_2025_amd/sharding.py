@@ -36,6 +36,8 @@ import torch.distributed as dist
 from . import _lib as L
 from . import functional as G
 from . import kernels as K
+from . import streams as S
+from .streams import host_lap
 from .optim import SLICE_SIDE, SLICE_SIDE_PRIORITY, SLICE_SIDE_STREAM, FusedAdamW, TableGroup
 
 
@@ -246,6 +248,14 @@ class GradBuckets:
         self.where = {id(p): b for b, ps in enumerate(self.buckets) for p in ps}
         dev = self.params[0].device if self.params else torch.device('cpu')
         self.flat = [torch.empty(sum(p.numel() for p in ps), dtype=torch.float32, device=dev) for ps in self.buckets]
+        # each parameter's gradient view of its bucket, made once (finish() hands them out)
+        self._views = []
+        for b, ps in enumerate(self.buckets):
+            off, vs = 0, []
+            for p in ps:
+                vs.append(self.flat[b][off:off + p.numel()].view_as(p))
+                off += p.numel()
+            self._views.append(vs)
         self.async_ok = dev.type == 'cuda' and dist.get_backend(pg) != 'gloo'
         self.enabled = True  # off while a backward is being captured into a HIP graph
         self._reset()
@@ -319,13 +329,10 @@ class GradBuckets:
         for b, ps in enumerate(self.buckets):
             if self.works[b] is not None:
                 self.works[b].wait()
-            flat, off = self.flat[b], 0
             if self.world > 1:
-                flat.mul_(inv)
-            for p in ps:
-                n = p.numel()
-                p.grad = flat[off:off + n].view_as(p)
-                off += n
+                self.flat[b].mul_(inv)
+            for p, v in zip(ps, self._views[b]):
+                p.grad = v
         self._reset()
 
 
@@ -498,7 +505,13 @@ class ShardedFusedAdamW(FusedAdamW):
             _, routed, host, done = ahead
             if self.trace is not None:
                 self.trace.append(('route done at prepare', done.query()))
+            host_lap('prepare.issue')
+            S.host_check('replay_end', 'n:prev_replay_done_before_wait')
+            S.host_check('step_end', 'n:prev_step_done_before_wait')
             done.synchronize()  # long done: the route ran during the previous step
+            host_lap('prepare.route_wait')
+            S.host_check('replay_end', 'n:prev_replay_done_after_wait')
+            S.host_check('step_end', 'n:prev_step_done_after_wait')
             counts = host.tolist()
             main = torch.cuda.current_stream()
             main.wait_event(done)
@@ -531,7 +544,9 @@ class ShardedFusedAdamW(FusedAdamW):
                                           local.contiguous())
             n_ids = r['inverse'].numel()
             fbuf = self._buffer(self._fbuf, name, (n_ids, grp.dim), grp.flat.dtype, grp.flat.device)
+            host_lap('prepare.issue')
             fetched = ex.fetch(r, counts[gi][0], counts[gi][1], before_gather=catchup, out=fbuf)
+            host_lap('prepare.fetch')
             inv_all = self._buffer(self._ibuf, name, (n_ids,), r['inverse'].dtype, grp.flat.device)
             inv_all[:n_ids].copy_(r['inverse'])
             sink = FetchSink()
@@ -551,6 +566,7 @@ class ShardedFusedAdamW(FusedAdamW):
                                                 self._period)
             G.run_on_side(slices, self.clock.ring.device, SLICE_SIDE_STREAM, SLICE_SIDE_PRIORITY)
         self._begun = self.t
+        host_lap('prepare.issue')
 
     # -- HIP graph capture of forward + backward (train.Trainer) ------------
     def _dense_params(self):
@@ -615,6 +631,7 @@ class ShardedFusedAdamW(FusedAdamW):
                 pushed.append((grp, ex.push_grads(ug)))
             elif not self.lazy and not self.defer:
                 K.table_adamw(grp.flat, grp.exp_avg, grp.exp_avg_sq, hp)
+        host_lap('step.shard_grads')
         # replicated tables (pos + feature tables): dense fp32 gradients in one buffer
         dev = self.replicated[0].flat.device
         rep = torch.empty(self.rep_rows, self.replicated[0].dim, dtype=torch.float32, device=dev)
@@ -628,8 +645,10 @@ class ShardedFusedAdamW(FusedAdamW):
                 rep_work = dist.all_reduce(rep, group=self.pg, async_op=True)
             else:
                 all_reduce(rep, self.pg)
+        host_lap('step.replicated')
         if self.buckets is not None:
             self.buckets.launch_rest()  # dense parameters (all of them when the backward was a graph replay)
+        host_lap('step.buckets_launch')
         # owners: reduce what arrived (rank order: deterministic), update the shard rows
         for grp, (local, rows) in pushed:
             src = [K.GradSource(local, rows, 0)]
@@ -639,12 +658,15 @@ class ShardedFusedAdamW(FusedAdamW):
                           None if self.lazy else grp.row_slot, lazy=self.lazy or bool(self.defer))
             if self.defer:
                 K.stamp_rows(grp.last, res.ids, res.count, res.capacity, self.clock)
+        host_lap('step.owner_updates')
         if self.buckets is not None:
             self.buckets.finish()
+        host_lap('step.buckets_finish')
         if self.dense is not None:
             self.dense.step()
         if self._flat is not None:
             self._flat.step(hp)
+        host_lap('step.dense_update')
         if rep_work is not None:
             rep_work.wait()
         if self.world > 1:
@@ -657,6 +679,7 @@ class ShardedFusedAdamW(FusedAdamW):
             g.clear()
         self.sinks = {}
         self.model._remaps = None
+        host_lap('step.replicated_update')
 
 
 def _dense_grad_into(g, out, dense_reduce_fn):

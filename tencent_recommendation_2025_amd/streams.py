@@ -9,12 +9,68 @@ forks work onto is one of these instead: created once per (device, index),
 never destroyed (they live as long as the process)."""
 from __future__ import annotations
 
+import atexit
 import contextlib
 import ctypes
+import os
+import sys
+import time
 
 import torch
 
 _STREAMS = {}
+
+# GRK_HOST_TIMES=1: host issue time of the eager phases of a row-sharded replayed
+# step (host_lap), printed per step at exit -- where the device waits on the host.
+HOST_TIMES = os.environ.get('GRK_HOST_TIMES') == '1'
+_HOST_T = {}
+_HOST_LAST = [0.0]
+_HOST_ON = [False]
+
+
+def host_lap(key=None, step=False):
+    """Add the host time since the previous lap to ``key`` (None: (re)start the clock and
+    the recording -- laps outside a recorded step, e.g. warm-up, are not counted);
+    step=True counts one step and stops the recording.  No-op unless GRK_HOST_TIMES=1."""
+    if not HOST_TIMES:
+        return
+    t = time.perf_counter()
+    if key is None:
+        _HOST_ON[0] = True
+    elif _HOST_ON[0]:
+        _HOST_T[key] = _HOST_T.get(key, 0.0) + t - _HOST_LAST[0]
+    if step and _HOST_ON[0]:
+        _HOST_T['#steps'] = _HOST_T.get('#steps', 0) + 1
+        _HOST_ON[0] = False
+    _HOST_LAST[0] = t
+
+
+_HOST_EV = {}
+
+
+def host_mark(name):
+    """Record a device event ``name`` on the current stream (GRK_HOST_TIMES=1)."""
+    if HOST_TIMES and _HOST_ON[0]:
+        e = torch.cuda.Event()
+        e.record()
+        _HOST_EV[name] = e
+
+
+def host_check(name, key):
+    """Count (under ``key``, per step) whether event ``name`` has completed: the device
+    has drained up to that point when the host gets here."""
+    if HOST_TIMES and _HOST_ON[0] and name in _HOST_EV:
+        _HOST_T[key] = _HOST_T.get(key, 0) + (1 if _HOST_EV[name].query() else 0)
+
+
+@atexit.register
+def _report_host_times():
+    n = _HOST_T.get('#steps')
+    if n:
+        print('host issue us/step: ' + ', '.join(f'{k} {1e6 * v / n:.0f}' for k, v in _HOST_T.items()
+                                                 if k != '#steps' and not k.startswith('n:')), file=sys.stderr)
+        print('fraction of steps: ' + ', '.join(f'{k[2:]} {v / n:.2f}' for k, v in _HOST_T.items()
+                                                if k.startswith('n:')), file=sys.stderr)
 
 
 def private_stream(device, index=0, priority=None):

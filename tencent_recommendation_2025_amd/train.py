@@ -352,21 +352,28 @@ class Trainer:
         dst = _tensors(self._static)
         if len(src) != len(dst) or any(a.shape != b.shape or a.dtype != b.dtype for a, b in zip(src, dst)):
             return self.eager_step(batch, next_batch)
+        S.host_lap()
         if self._sharded and next_batch is not None:
             # route the next batch before anything of this step is queued: its side
             # stream then waits only for the previous step, and prepare(next) finds
             # the split sizes on the host a whole step early
             self.opt.prefetch(next_batch)
+            S.host_lap('prefetch')
         if isinstance(batch, PackedBatch) and isinstance(self._static, PackedBatch) \
                 and batch.layout == self._static.layout:
             self._static.arena.copy_(batch.arena, non_blocking=True)   # one copy for the whole batch
         else:
             _copy_batch(dst, src)
         if self._sharded:
+            S.host_lap('batch_copy')
             self.opt.prepare(self._static, key=batch[0])
             self._g.replay()
+            S.host_mark('replay_end')
             self.opt.restore_captured(self._cap_states.get(key))
+            S.host_lap('replay')
             self.opt.step()
+            S.host_mark('step_end')
+            S.host_lap('step', step=True)
         else:
             self.opt.maybe_segment()
             self._g.replay()

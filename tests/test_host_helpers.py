@@ -167,6 +167,15 @@ def test_pair_split_backward_equals_slices():
     assert 'aten.slice_backward' in res[0][1] and 'aten.slice_backward' not in res[1][1]
 
 
+def _stub_adamw_ranges(monkeypatch, O, fn):
+    """DenseFlat plans its launches (K.prepare_table_adamw_ranges) and runs them
+    (K.launch_prepared): both stubbed so that each launch calls fn with the plan's
+    arguments at launch time, as the device would read them."""
+    monkeypatch.setattr(O.K, 'prepare_table_adamw_ranges',
+                        lambda param, m, v, clock, ranges, shadow=None: (param, m, v, clock, ranges, shadow))
+    monkeypatch.setattr(O.K, 'launch_prepared', lambda call: fn(*call))
+
+
 def test_dense_flat_step_plumbing_tracks_torch_adamw(monkeypatch):
     """optim.DenseFlat on the CPU with grk_table_adamw_ranges_dev emulated by the element
     update restated above (adam1): parameters become views of the flat buffer (the
@@ -192,7 +201,7 @@ def test_dense_flat_step_plumbing_tracks_torch_adamw(monkeypatch):
         exp_avg.copy_(torch.from_numpy(m))
         exp_avg_sq.copy_(torch.from_numpy(v))
 
-    monkeypatch.setattr(O.K, 'table_adamw_ranges', emulated)
+    _stub_adamw_ranges(monkeypatch, O, emulated)
     gen = torch.Generator().manual_seed(5)
     shapes = [(16, 8), (24,), (4, 6, 2), (8,), (40, 16)]
     ps = [torch.nn.Parameter(torch.randn(s, generator=gen)) for s in shapes]
@@ -204,7 +213,7 @@ def test_dense_flat_step_plumbing_tracks_torch_adamw(monkeypatch):
     clock = Clock()
     skip = {2: {2}, 4: {0, 4}}                      # step -> parameters without a gradient
     skipped = set()
-    for step in range(1, 6):
+    for step in range(1, 8):
         clock.t = step
         before = [p.detach().clone() for p in ps]
         for i, (p, q) in enumerate(zip(ps, twins)):
@@ -212,7 +221,11 @@ def test_dense_flat_step_plumbing_tracks_torch_adamw(monkeypatch):
                 p.grad = q.grad = None
             else:
                 g = torch.randn(p.shape, generator=gen) * (1e-3 if i == 1 else 1.0)
-                p.grad, q.grad = g.clone(), g.clone()
+                if step >= 6:   # gradients written in place: step 5's launch plan is reused
+                    p.grad.copy_(g)
+                    q.grad.copy_(g)
+                else:
+                    p.grad, q.grad = g.clone(), g.clone()
         calls.clear()
         flat.step(clock)
         ref.step()
@@ -228,6 +241,7 @@ def test_dense_flat_step_plumbing_tracks_torch_adamw(monkeypatch):
                 np.testing.assert_allclose(p.detach().numpy(), q.detach().numpy(), rtol=0,
                                            atol=4e-8 + 2e-7 * float(q.detach().abs().max()))
     assert skipped == {0, 2, 4}
+    assert flat._prep_key is not None and len(flat._prepared) == 1   # the plan kept since step 5
     st = flat.state(ps[1])
     np.testing.assert_allclose(st['exp_avg'].numpy(), ref.state[twins[1]]['exp_avg'].numpy(), rtol=1e-5, atol=1e-9)
 
@@ -257,7 +271,7 @@ def test_dense_flat_splits_runs_beyond_the_kernel_range_cap(monkeypatch):
         exp_avg.copy_(torch.from_numpy(m))
         exp_avg_sq.copy_(torch.from_numpy(v))
 
-    monkeypatch.setattr(O.K, 'table_adamw_ranges', emulated)
+    _stub_adamw_ranges(monkeypatch, O, emulated)
     gen = torch.Generator().manual_seed(9)
     ps = [torch.nn.Parameter(torch.randn((8 * (1 + i % 3),), generator=gen)) for i in range(150)]
     twins = [torch.nn.Parameter(p.detach().clone()) for p in ps]
