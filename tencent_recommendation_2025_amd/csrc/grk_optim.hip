@@ -383,67 +383,61 @@ __global__ void __launch_bounds__(256) k_adamw_catchup(P* __restrict__ param, fl
   }
   const int t = resolve_t(t_host, t_dev);
   const int lane = threadIdx.x & 63;
-  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  int64_t row;
-  if (ids) {
-    if (w >= num_ids) return;
-    row = ids[w];
-  } else if (num_slices > 1) {
-    const int64_t per = (num_rows + num_slices - 1) / num_slices;
-    if (w >= per) return;
-    row = (int64_t)(t % num_slices) * per + w;
-  } else {
-    if (w >= num_rows) return;
-    row = w;
-  }
-  if (row < 0 || row >= num_rows) return;
-  float pv[NV], mv[NV], vv[NV];
-  int c = lane * NV;
-  int from = 0;
-  if (ids) {
-    // A plain read first: later duplicates of a hot row see the claim without
-    // queueing on the atomic; the exchange still decides who replays.
-    if (__builtin_nontemporal_load(&last[row]) >= t) return;
-    if (lane == 0) from = atomicExch(&last[row], t);
-    from = __builtin_amdgcn_readfirstlane(__shfl(from, 0));
-    if (from >= t) return;
-    if (c < dim) load_pmv<P, NV>(param + row * dim + c, m + row * dim + c, v + row * dim + c, pv, mv, vv);
-  } else {
-    if (c < dim) load_pmv<P, NV>(param + row * dim + c, m + row * dim + c, v + row * dim + c, pv, mv, vv);
-    from = __builtin_amdgcn_readfirstlane(last[row]);
-    if (from >= t) return;
-    if (lane == 0) last[row] = t;
-  }
-  const int slot0 = (from + 1) % ring_len;
-  for (bool first = true; c < dim; c += 64 * NV, first = false) {
-    const int64_t off = row * dim + c;
-    if (!first) load_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
-    int slot = slot0;
-    for (int st = from + 1; st <= t; ++st) {
-      const AdamStep s = staged ? steps[slot] : adam_step(ring[slot]);
-      slot = slot + 1 == ring_len ? 0 : slot + 1;
+  // one wave per row; a grid smaller than the rows' waves (the rolling slice under
+  // GRK_SLICE_WGS) walks them grid-stride
+  const int64_t per = num_slices > 1 ? (num_rows + num_slices - 1) / num_slices : num_rows;
+  const int64_t nw = ids ? num_ids : per;
+  for (int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w < nw; w += (int64_t)gridDim.x * 4) {
+    const int64_t row = ids ? ids[w] : (num_slices > 1 ? (int64_t)(t % num_slices) * per + w : w);
+    if (row < 0 || row >= num_rows) continue;
+    float pv[NV], mv[NV], vv[NV];
+    int c = lane * NV;
+    int from = 0;
+    if (ids) {
+      // A plain read first: later duplicates of a hot row see the claim without
+      // queueing on the atomic; the exchange still decides who replays.
+      if (__builtin_nontemporal_load(&last[row]) >= t) continue;
+      if (lane == 0) from = atomicExch(&last[row], t);
+      from = __builtin_amdgcn_readfirstlane(__shfl(from, 0));
+      if (from >= t) continue;
+      if (c < dim) load_pmv<P, NV>(param + row * dim + c, m + row * dim + c, v + row * dim + c, pv, mv, vv);
+    } else {
+      if (c < dim) load_pmv<P, NV>(param + row * dim + c, m + row * dim + c, v + row * dim + c, pv, mv, vv);
+      from = __builtin_amdgcn_readfirstlane(last[row]);
+      if (from >= t) continue;
+      if (lane == 0) last[row] = t;
+    }
+    const int slot0 = (from + 1) % ring_len;
+    for (bool first = true; c < dim; c += 64 * NV, first = false) {
+      const int64_t off = row * dim + c;
+      if (!first) load_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
+      int slot = slot0;
+      for (int st = from + 1; st <= t; ++st) {
+        const AdamStep s = staged ? steps[slot] : adam_step(ring[slot]);
+        slot = slot + 1 == ring_len ? 0 : slot + 1;
 #if GRK_CATCHUP_PACKED
 #pragma unroll
-      for (int e = 0; e < NV; e += 2) {
-        f2v p2 = {pv[e], pv[e + 1]}, m2 = {mv[e], mv[e + 1]}, v2 = {vv[e], vv[e + 1]};
-        adam2_g0(p2, m2, v2, s);
-        pv[e] = p2.x; pv[e + 1] = p2.y; mv[e] = m2.x; mv[e + 1] = m2.y; vv[e] = v2.x; vv[e + 1] = v2.y;
-        if constexpr (sizeof(P) == 2) {   // one v_cvt_pk_bf16_f32 per pair, then the two halves back
-          typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
-          const unsigned w = __builtin_bit_cast(unsigned, __builtin_convertvector(p2, bf2v));
-          pv[e] = __uint_as_float(w << 16);
-          pv[e + 1] = __uint_as_float(w & 0xFFFF0000u);
+        for (int e = 0; e < NV; e += 2) {
+          f2v p2 = {pv[e], pv[e + 1]}, m2 = {mv[e], mv[e + 1]}, v2 = {vv[e], vv[e + 1]};
+          adam2_g0(p2, m2, v2, s);
+          pv[e] = p2.x; pv[e + 1] = p2.y; mv[e] = m2.x; mv[e + 1] = m2.y; vv[e] = v2.x; vv[e + 1] = v2.y;
+          if constexpr (sizeof(P) == 2) {   // one v_cvt_pk_bf16_f32 per pair, then the two halves back
+            typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+            const unsigned w2 = __builtin_bit_cast(unsigned, __builtin_convertvector(p2, bf2v));
+            pv[e] = __uint_as_float(w2 << 16);
+            pv[e + 1] = __uint_as_float(w2 & 0xFFFF0000u);
+          }
         }
-      }
 #else
 #pragma unroll
-      for (int e = 0; e < NV; ++e) {
-        adam1_g0(pv[e], mv[e], vv[e], s);
-        if constexpr (sizeof(P) == 2) pv[e] = bf16_to_f32(f32_to_bf16(pv[e]));
-      }
+        for (int e = 0; e < NV; ++e) {
+          adam1_g0(pv[e], mv[e], vv[e], s);
+          if constexpr (sizeof(P) == 2) pv[e] = bf16_to_f32(f32_to_bf16(pv[e]));
+        }
 #endif
+      }
+      store_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
     }
-    store_pmv<P, NV>(param + off, m + off, v + off, pv, mv, vv);
   }
 }
 
@@ -573,7 +567,16 @@ static int table_adamw_catchup(void* param, int param_dtype, float* exp_avg, flo
   GRK_CHECK_ARG(dim > 0 && dim % 4 == 0, "dim must be a multiple of 4");
   GRK_CHECK_ARG(ring_len > 0 && t >= 0, "ring_len must be > 0 and t >= 0");
   GRK_CHECK_ARG((waves + 3) / 4 < (int64_t)1 << 31, "too many rows for one launch");
-  const unsigned g = (unsigned)((waves + 3) / 4);
+  unsigned g = (unsigned)((waves + 3) / 4);
+  // GRK_SLICE_WGS (rolling slice only): at most that many workgroups, walking the
+  // slice's rows grid-stride -- the slice then holds a bounded share of the CUs while it
+  // runs beside the step on its side stream, instead of flooding every CU at launch
+  // (512 = two per CU, measured best: 3.99 vs 4.04 ms/step with the full grid, 4.11 at 256)
+  static const int slice_wgs = [] {
+    const char* e = getenv("GRK_SLICE_WGS");
+    return e ? atoi(e) : 512;
+  }();
+  if (!ids && num_slices > 1 && slice_wgs > 0 && g > (unsigned)slice_wgs) g = (unsigned)slice_wgs;
   hipStream_t s = (hipStream_t)stream;
   const bool v8 = dim % 8 == 0;
 #define GRK_CU(P, NV) k_adamw_catchup<P, NV><<<g, 256, 0, s>>>((P*)param, exp_avg, exp_avg_sq, num_rows, dim, last, \
