@@ -259,6 +259,7 @@ def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extras
     buffer, returned as a single tensor).  Drop-in tables get dense gradients
     through autograd; grouped tables push row-sparse gradient sources into
     their group's sink."""
+    _wait_table_barrier()   # rows a side-stream catch-up is bringing up to date
     if token_type is not None:
         token_type = token_type.to(torch.int32).contiguous()
     single = splits is None
@@ -338,10 +339,25 @@ def _lookup_groups(specs, token_type, seq_len, num_tokens, out_ld, extras, split
 WGRAD_SIDE = os.environ.get('GRK_WGRAD_SIDE', '0') == '1'
 _SIDE_STREAM_INDEX = 6
 _SIDE_PENDING = {}
+# events the next table gather (feature_lookup) makes the current stream wait for:
+# the deferred tables' batch-row catch-up runs on a side stream (optim.begin_step)
+# under the step's first kernels, and only the gathers need its rows
+_TABLE_BARRIER = []
+
+
+def table_barrier(event):
+    """The next feature_lookup (or join_side_work) waits for ``event`` first."""
+    _TABLE_BARRIER.append(event)
+
+
+def _wait_table_barrier():
+    while _TABLE_BARRIER:
+        torch.cuda.current_stream().wait_event(_TABLE_BARRIER.pop())
 
 
 def join_side_work():
     """The current stream waits for every weight gradient issued on the side stream."""
+    _wait_table_barrier()
     if not _SIDE_PENDING:
         return
     for (idx, _), side in list(_SIDE_PENDING.items()):

@@ -135,6 +135,9 @@ SLICE_SIDE_STREAM = 7
 # clamped into the device's range): the main chain's kernels first, the replay in the gaps
 SLICE_SIDE_PRIORITY = int(os.environ.get('GRK_SLICE_PRIORITY', '0'))
 SLICE_AT = os.environ.get('GRK_SLICE_AT', 'forward')   # 'forward' | 'backward' (see begin_step)
+# batch-row catch-up on the slice's stream, the first table gather waiting for it: opt-in
+# (same-box A/B 4.058 vs 4.028 ms/step on the main stream)
+CATCHUP_SIDE = os.environ.get('GRK_CATCHUP_SIDE', '0') == '1'
 
 DENSE_FLAT_DIM = 8   # the flat buffer as [rows, 8] for k_adamw_ranges (16-byte fp32 pairs per lane)
 
@@ -484,13 +487,29 @@ class FusedAdamW:
         # The padding row is brought up at the segment flush; it is zero and gets
         # no gradient (nn.Embedding padding_idx), and a g = 0 step maps a zero
         # (p, m, v) row to exactly zero, so reading it early changes nothing.
-        item, user = K.batch_row_ids(*batch[:4], with_user='user' in self._deferred)
-        ids = {'item': item, 'user': user}
         side = self.rolling and SLICE_SIDE and not self.l2_emb and self.clock.ring.is_cuda
-        for name, g in self._deferred.items():
-            if self.rolling and not side:   # this step's slice of every row
-                K.table_adamw_catchup_slice(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self.clock, self._period)
-            K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock, ids[name])
+
+        def catchups():
+            item, user = K.batch_row_ids(*batch[:4], with_user='user' in self._deferred)
+            ids = {'item': item, 'user': user}
+            for name, g in self._deferred.items():
+                if self.rolling and not side:   # this step's slice of every row
+                    K.table_adamw_catchup_slice(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self.clock, self._period)
+                K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock, ids[name])
+
+        if side and CATCHUP_SIDE:
+            # the batch rows' catch-up on the slice's side stream (the slice follows it
+            # there: both claim rows through the step stamps), under the step's first
+            # kernels (jagged layout, batch compaction, feature projections); the first
+            # table gather waits for it (functional.table_barrier)
+            def forked():
+                catchups()
+                ev = torch.cuda.Event()
+                ev.record()
+                G.table_barrier(ev)
+            G.run_on_side(forked, self.clock.ring.device, SLICE_SIDE_STREAM, SLICE_SIDE_PRIORITY)
+        else:
+            catchups()
         if side:
             # the slice after the batch rows (which it then skips: their step stamps are
             # current) on a side stream: VALU-bound replay under the step's GEMMs and
