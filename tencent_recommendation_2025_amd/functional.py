@@ -490,8 +490,65 @@ def _zero_block(rows, cols, dtype, device):
     return t
 
 
+# the dnn-weight composition on grk_dnn_weight_fwd / _bwd: opt-in -- one thread per output
+# with the K = 512 sums of the mm / bias columns as serial global-load loops ran the step
+# 4.30-4.37 ms vs 3.95-4.02 with the torch composition (hipBLASLt for the two products),
+# same box
+DNNW_KERNEL = os.environ.get('GRK_DNNW_KERNEL', '0') == '1'
+
+
 class _DnnWeightFn(torch.autograd.Function):
     """The composed itemdnn / userdnn weight of the projection restatement
+    (model._dnn_weight): [d, width] = [blocks... | W_k Wt (mm features, the
+    emb_transform folded in) | b + sum_k W_k b_t | 0], in `dtype`.
+
+    One grk_dnn_weight_fwd launch forward (every column, the K = kk products of the
+    mm columns summed in k order in fp32); backward one grk_dnn_weight_bwd call (two
+    launches): g in fp32 (the blocks' and the bias's gradients are its columns), and
+    per mm feature dW_k = dM [W_t | b_t]^T, [dW_t | db_t] = W_k^T dM with dM = [g(mm
+    columns) | g(bias column)].  The eager composition -- a cat, a GEMM and an add per
+    mm feature, a cat of every block and a cast forward, a cast, a cat and two GEMMs
+    back -- ran ~12 launches of a few microseconds each per step."""
+
+    @staticmethod
+    def forward(ctx, nblocks, nmm, width, dtype, *ts):
+        blocks, bias = ts[:nblocks], ts[nblocks]
+        mms = [ts[nblocks + 1 + 3 * i: nblocks + 4 + 3 * i] for i in range(nmm)]
+        cols, c = [], 0
+        for blk in blocks:
+            cols.append((blk.detach(), c))
+            c += blk.shape[1]
+        mm_args = []
+        for Wk, Wt, bt in mms:
+            mm_args.append((Wk.detach(), Wt.detach(), bt.detach(), c))
+            c += Wt.shape[1]
+        if c >= width:
+            raise ValueError(f'dnn_weight: {c + 1} columns do not fit width {width}')
+        out = K.dnn_weight_fwd(cols, mm_args, bias.detach().float(), width, c, dtype)
+        ctx.save_for_backward(*[t for m in mm_args for t in m[:3]])
+        ctx.meta = (nblocks, nmm, [b.shape[1] for b in blocks], [m[3] for m in mm_args], c,
+                    [b.dtype for b in blocks], bias.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        nblocks, nmm, bw, mm_cols, bias_col, bdt, biasdt = ctx.meta
+        saved = ctx.saved_tensors
+        mm_args = [(saved[3 * i], saved[3 * i + 1], saved[3 * i + 2], mm_cols[i]) for i in range(nmm)]
+        g32, dwks, dwts, dbts = K.dnn_weight_bwd(g, mm_args, bias_col)
+        grads, c = [], 0
+        for w, dt in zip(bw, bdt):
+            grads.append(g32[:, c:c + w].to(dt))
+            c += w
+        mm_grads = []
+        for dWk, dWt, dbt in zip(dwks, dwts, dbts):
+            mm_grads += [dWk, dWt, dbt]
+        return (None, None, None, None, *grads, g32[:, bias_col].to(biasdt), *mm_grads)
+
+
+class _DnnWeightTorchFn(torch.autograd.Function):
+    """(A/B, GRK_DNNW_KERNEL=0) _DnnWeightFn in torch ops (round 4): the composed
+    itemdnn / userdnn weight of the projection restatement
     (model._dnn_weight): [d, width] = [blocks... | W_k [W_t | b_t] (mm features,
     the emb_transform folded in) | b + sum_k W_k b_t | 0], cast once to `dtype`.
 
@@ -558,7 +615,8 @@ def dnn_weight(blocks, bias, mms, width, dtype):
     """model._dnn_weight as one autograd node (_DnnWeightFn): blocks = the weight's
     column blocks taken as they are, mms = [(W_k, emb_transform weight, bias)]."""
     flat = [t for m in mms for t in m]
-    return _DnnWeightFn.apply(len(blocks), len(mms), int(width), dtype, *blocks, bias, *flat)
+    fn = _DnnWeightFn if DNNW_KERNEL else _DnnWeightTorchFn
+    return fn.apply(len(blocks), len(mms), int(width), dtype, *blocks, bias, *flat)
 
 
 class _SplitPairFn(torch.autograd.Function):

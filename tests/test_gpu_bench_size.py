@@ -59,6 +59,11 @@ TABLE_FLIP_FRAC = 2e-3       # bf16 tables: robust elements whose step-1 update 
                              # BENCH_AMP_FACTOR x the AMP step's own gradient sign flips there); measured
                              # r5k / r5fin: item 1530 of 974,656 (0.16 %), user 4 of 3,768 (0.11 %)
 OPT_TOL = 1e-3               # update vs torch AdamW of grk's own gradient (fp32 dense parameters)
+DENSE_FLIPS = (2e-3, 1)      # dense parameters: robust elements whose step-1 update sign flipped, at most
+                             # max(BENCH_AMP_FACTOR x the AMP step's flips there, 0.2 % of the robust
+                             # elements, 1); the rest compared normwise (UPDATE_FLOOR).  One flipped element
+                             # of a ~1.6k-element rab alone is a normwise 0.06 (r5s: rab of layer 1 after an
+                             # ulp-level change of the forward's dnn weight)
 
 
 def nrel(a, b):
@@ -235,7 +240,14 @@ def test_bench_config_full_size_step_matches_oracle():
                 (n, far, amp_flips, int(robust.sum()))
             u_err[n] = 0.0
         else:
-            u_err[n] = nrel(du_grk[robust], du_ref[robust])
+            flip = robust & ((du_grk > 0) != (du_ref > 0)) & (du_ref != 0)
+            nflip = int(flip.sum())
+            amp_flips = int((((agrad[n].float() > 0) != (rg > 0)) & robust).sum()) if n in agrad else 0
+            assert nflip <= max(BENCH_AMP_FACTOR * amp_flips, DENSE_FLIPS[0] * int(robust.sum()), DENSE_FLIPS[1]), \
+                (n, nflip, amp_flips, int(robust.sum()))
+            ulp_off[n] = (0, nflip, int(robust.sum()), amp_flips)
+            keep = robust & ~flip
+            u_err[n] = nrel(du_grk[keep], du_ref[keep])
         if not is_table and n in grads:
             # the optimizer itself: the change grk applied == torch AdamW's step-1 change
             # computed from grk's own gradient, on every element
@@ -252,7 +264,7 @@ def test_bench_config_full_size_step_matches_oracle():
     print('  worst updates (grk, amp, name):', worst_u)
     print('  untouched table rows (count, mismatching):', exact_rows)
     print('  optimizer (update vs AdamW of grk gradients), worst:', max(u_opt.values()) if u_opt else None)
-    print('  table elements (one ulp off, sign-flipped, robust, AMP sign flips):',
+    print('  table + dense elements (one ulp off, sign-flipped, robust, AMP sign flips):',
           [sum(v[i] for v in ulp_off.values()) for i in range(4)])
 
     assert errs['loss'] < LOSS_TOL, (errs, amp)
