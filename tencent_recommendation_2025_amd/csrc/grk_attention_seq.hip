@@ -136,49 +136,50 @@ __global__ void __launch_bounds__(1024) k_seq_order(int B, int T, int* __restric
   }
 }
 
-// Both columns in ONE workgroup for B <= kSeqFused: 16 waves scan 4
-// sequences each per round (their key bytes' loads in flight together), the
-// key counts T - first go to LDS, and the rank count reads them there.  Same
-// output as k_seq_ranges + k_seq_order, one launch instead of two.
+// Both columns in ONE workgroup for B <= kSeqFused and B * T <= kSeqFusedBytes:
+// the key-valid bytes are staged into LDS with 16-byte loads by every thread
+// (the per-sequence byte scans then read LDS, not memory -- with byte loads
+// from memory the workgroup ran 38 us at B = 128, T = 201), 16 waves scan the
+// sequences, the key counts T - first go to LDS, and the rank count reads them
+// there.  Same output as k_seq_ranges + k_seq_order, one launch instead of two.
 constexpr int kSeqFused = 1024;
+constexpr int kSeqFusedBytes = 48 * 1024;
+// JAG: also the jagged layout's row bases (k_jagged_base of grk_jagged.hip, the
+// same drop rule for spans past `cap`), from the counts already in LDS.
+template <bool JAG>
 __global__ void __launch_bounds__(1024) k_seq_ranges_order(const uint8_t* __restrict__ kv, int B, int T,
-                                                           int* __restrict__ out) {
+                                                           int* __restrict__ out, int64_t cap,
+                                                           int64_t* __restrict__ row_base,
+                                                           int64_t* __restrict__ n_rows, int32_t* __restrict__ err) {
   __shared__ int len[kSeqFused];
+  __shared__ __attribute__((aligned(16))) uint8_t kvs[kSeqFusedBytes];
+  const int n = B * T;
+  if (((uintptr_t)kv & 15) == 0) {
+    for (int i = threadIdx.x; i < n / 16; i += blockDim.x)
+      reinterpret_cast<uint4*>(kvs)[i] = reinterpret_cast<const uint4*>(kv)[i];
+    for (int i = n / 16 * 16 + threadIdx.x; i < n; i += blockDim.x) kvs[i] = kv[i];
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) kvs[i] = kv[i];
+  }
+  __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int b0 = 4 * w; b0 < B; b0 += 64) {
-    int first[4], cnt[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      first[u] = T;
-      cnt[u] = 0;
-    }
-    for (int j = lane; j < T; j += 64) {
-      uint8_t x[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) x[u] = b0 + u < B ? kv[(int64_t)(b0 + u) * T + j] : 0;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (x[u]) {
-          first[u] = min(first[u], j);
-          ++cnt[u];
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        first[u] = min(first[u], __shfl_xor(first[u], off));
-        cnt[u] += __shfl_xor(cnt[u], off);
+  for (int b = w; b < B; b += 16) {
+    int first = T, cnt = 0;
+    for (int j = lane; j < T; j += 64)
+      if (kvs[b * T + j]) {
+        first = min(first, j);
+        ++cnt;
       }
-    if (lane == 0)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int b = b0 + u;
-        if (b >= B) break;
-        out[3 * b] = first[u];
-        out[3 * b + 1] = cnt[u] == T - first[u];
-        len[b] = T - first[u];
-      }
+    for (int off = 32; off > 0; off >>= 1) {
+      first = min(first, __shfl_xor(first, off));
+      cnt += __shfl_xor(cnt, off);
+    }
+    if (lane == 0) {
+      out[3 * b] = first;
+      out[3 * b + 1] = cnt == T - first;
+      len[b] = T - first;
+    }
   }
   __syncthreads();
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
@@ -189,6 +190,40 @@ __global__ void __launch_bounds__(1024) k_seq_ranges_order(const uint8_t* __rest
       rank += (lc > lb) | ((lc == lb) & (c < b));
     }
     out[3 * rank + 2] = b;
+  }
+  if constexpr (JAG) {
+    // inclusive scan of the spans (B * T <= kSeqFusedBytes: int32), then the row bases;
+    // a span ending past cap is dropped (start T, row base -T, err bit 2) -- the kept
+    // spans are a prefix, so n_rows <= cap
+    __shared__ int part[kSeqFused];
+    const int tid = threadIdx.x;
+    const int span = tid < B ? len[tid] : 0;
+    part[tid] = span;
+    __syncthreads();
+    for (int off = 1; off < kSeqFused; off <<= 1) {
+      const int v = tid >= off ? part[tid - off] : 0;
+      __syncthreads();
+      part[tid] += v;
+      __syncthreads();
+    }
+    const int incl = part[tid];
+    bool drop = false;
+    if (tid < B) {
+      const int st = T - span;
+      if (incl <= cap) {
+        row_base[tid] = (int64_t)incl - span - st;
+      } else {
+        row_base[tid] = -(int64_t)T;
+        out[3 * tid] = T;
+        out[3 * tid + 1] = 1;
+        drop = true;
+      }
+    }
+    // kept = the largest inclusive sum <= cap: the last kept sequence's (a prefix)
+    const bool last_kept = tid < B && !drop && (tid + 1 >= B || part[tid + 1] > cap);
+    if (last_kept) *n_rows = incl;
+    if (tid == 0 && (B == 0 || part[0] > cap)) *n_rows = 0;
+    if (drop && err && (tid == 0 || part[tid - 1] <= cap)) atomicOr(err, 2);   // the first dropped one
   }
 }
 
@@ -1171,13 +1206,25 @@ extern "C" int grk_attention_fidelity_supported(int seq_len, int head_dim) {
   return 0;
 }
 
+namespace grk {
+// grk_jagged_layout's ranges + row bases in one launch when the batch fits the fused
+// workgroup (false: the caller runs grk_seq_ranges and k_jagged_base)
+bool seq_ranges_jagged(const uint8_t* key_valid, int batch, int seq_len, int64_t cap, int32_t* ranges,
+                       int64_t* row_base, int64_t* n_rows, int32_t* err, hipStream_t s) {
+  if (batch <= 0 || batch > kSeqFused || (int64_t)batch * seq_len > kSeqFusedBytes) return false;
+  k_seq_ranges_order<true><<<1, 1024, 0, s>>>(key_valid, batch, seq_len, ranges, cap, row_base, n_rows, err);
+  return true;
+}
+}  // namespace grk
+
 extern "C" int grk_seq_ranges(const uint8_t* key_valid, int batch, int seq_len, int32_t* ranges, void* stream) {
   clear_error();
   GRK_CHECK_ARG(batch >= 0 && seq_len > 0, "batch must be >= 0 and seq_len > 0");
   if (batch == 0) return GRK_OK;
   GRK_CHECK_ARG(key_valid && ranges, "key_valid and ranges required");
-  if (batch <= kSeqFused) {
-    k_seq_ranges_order<<<1, 1024, 0, (hipStream_t)stream>>>(key_valid, batch, seq_len, ranges);
+  if (batch <= kSeqFused && (int64_t)batch * seq_len <= kSeqFusedBytes) {
+    k_seq_ranges_order<false><<<1, 1024, 0, (hipStream_t)stream>>>(key_valid, batch, seq_len, ranges, 0, nullptr,
+                                                                    nullptr, nullptr);
     GRK_LAUNCH_CHECK();
     return GRK_OK;
   }

@@ -168,6 +168,9 @@ __global__ void __launch_bounds__(256) k_gather_rows(RowCopies rc, const int32_t
 }
 
 }  // namespace
+
+bool seq_ranges_jagged(const uint8_t* key_valid, int batch, int seq_len, int64_t cap, int32_t* ranges,
+                       int64_t* row_base, int64_t* n_rows, int32_t* err, hipStream_t s);   // grk_attention_seq.hip
 }  // namespace grk
 
 using namespace grk;
@@ -181,10 +184,14 @@ extern "C" int grk_jagged_layout(const uint8_t* key_valid, int batch, int seq_le
                 "rows must fit int32");
   GRK_CHECK_ARG(key_valid && ranges && row_base && row_map && num_rows, "key_valid, ranges, row_base, row_map, num_rows required");
   hipStream_t s = (hipStream_t)stream;
-  const int rc = grk_seq_ranges(key_valid, batch, seq_len, ranges, stream);
-  if (rc) return rc;
-  k_jagged_base<<<1, 1024, 0, s>>>(ranges, batch, seq_len, capacity, row_base, num_rows, err_flag);
-  GRK_LAUNCH_CHECK();
+  if (seq_ranges_jagged(key_valid, batch, seq_len, capacity, ranges, row_base, num_rows, err_flag, s)) {
+    GRK_LAUNCH_CHECK();
+  } else {
+    const int rc = grk_seq_ranges(key_valid, batch, seq_len, ranges, stream);
+    if (rc) return rc;
+    k_jagged_base<<<1, 1024, 0, s>>>(ranges, batch, seq_len, capacity, row_base, num_rows, err_flag);
+    GRK_LAUNCH_CHECK();
+  }
   const int64_t total = (int64_t)batch * seq_len > capacity ? (int64_t)batch * seq_len : capacity;
   k_jagged_map<<<grid_for(total, 256), 256, 0, s>>>(ranges, row_base, num_rows, batch, seq_len, capacity,
                                                     next_token_type, row_map, err_flag);

@@ -263,7 +263,7 @@ def test_seq_ranges(K):
     np.testing.assert_array_equal(got[:, 2], [1, 3, 2, 0, 4])   # T - first: 30, 40, 35, 37, 0
 
 
-@pytest.mark.parametrize('B', [1, 128, 1024, 1025, 9000])   # one-launch form (<= 1024), LDS rank, memory rank
+@pytest.mark.parametrize('B', [1, 128, 240, 1024, 1025, 9000])   # one launch (B T <= 48 KiB), LDS rank, memory rank
 def test_seq_ranges_random(K, B):
     T = 201
     rng = np.random.default_rng(B)

@@ -78,6 +78,27 @@ def test_layout_and_gather_match_oracle():
             J.check_error(jag.err)
 
 
+@pytest.mark.parametrize('B', [200, 300])   # one-launch ranges + row bases (B T <= 48 KiB) and the two-launch form
+def test_layout_at_bench_lengths_matches_oracle(B):
+    from tencent_recommendation_2025_amd import jagged as J
+    rng = np.random.default_rng(B)
+    T = 201
+    tt = np.zeros((B, T), np.int64)
+    for b in range(B):
+        n = rng.integers(0, T + 1)
+        tt[b, T - n:] = rng.integers(1, 3, n)
+    tt[7, 100:110] = 0          # a hole inside a span
+    n_rows = int(ojag.layout(tt, B * T)[3])
+    for cap in (n_rows, J.capacity_for(n_rows, 1024), n_rows // 2):
+        jag = J.layout(torch.from_numpy(tt).to(DEV), cap)
+        rng_w, base_w, map_w, n_w = ojag.layout(tt, cap)
+        assert int(jag.n.item()) == n_w
+        assert bool(int(jag.err.item()) & 2) == (cap < n_rows)
+        assert np.array_equal(jag.seq_range.cpu().numpy()[:, :2], rng_w)
+        assert np.array_equal(jag.row_base.cpu().numpy()[:B], base_w)
+        assert np.array_equal(jag.row_map.cpu().numpy(), map_w)
+
+
 def test_gather_rows_many_copies_every_unit_width():
     """70 copies (two launches of <= 64) with rows of 4 .. 132 bytes: 16-, 8- and
     4-byte units, and sources offset by 4 / 8 bytes from 16-byte alignment."""
