@@ -875,9 +875,11 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
 #endif
 //   GRK_DKDV_WAVES      dK/dV (hd <= 64, PREC < 2): the waves-per-SIMD register target
 //   GRK_DKDV_PREFETCH   dK/dV: the first key tile's K / V fragments loaded before the
-//                       Q / dO staging (1, product) or at the tile (0: 32 VGPRs fewer)
+//                       Q / dO staging (1) or at the tile (0, product since round 5:
+//                       218 VGPRs instead of 251, dK/dV 65-67 vs 67-70 us, step 4.03
+//                       vs 4.03-4.14 ms over three same-box pairs, gpurun_out/r5v)
 #ifndef GRK_DKDV_PREFETCH
-#define GRK_DKDV_PREFETCH 1
+#define GRK_DKDV_PREFETCH 0
 #endif
 
 template <int HD, int KIND, int PREC, bool TBK = true>
