@@ -496,15 +496,17 @@ def wgrad_roofline(a, reps, k, wtrace=None):
     return res
 
 
-def catchup_roofline(opt, reps):
-    """The rolling flush of the deferred dense-parity table AdamW (FusedAdamW
-    rolling, round 5): one k_adamw_catchup launch per deferred table and step over
-    a 1/period slice of its rows, each row replaying the g = 0 steps it lags.
-    Timed on copies of the item table's state as the timed region left it (the
-    slice the clock points at, its real lags), last[] restored before every
-    launch.  Algorithmic bytes: slice rows x D x (2 + 4 + 4) B read and written
-    + 8 B of last[] per row; the kernel is VALU-bound (~100 instructions, 16 of them
-    sqrt / rcp, per replayed step of 8 elements), reported against HBM."""
+def catchup_roofline(opt, reps, batch=None):
+    """The deferred dense-parity table AdamW's replays (FusedAdamW rolling, round 5),
+    every k_adamw_catchup launch of a step: per deferred table the
+    batch rows' catch-up at the head of the step (the rows the step reads, brought to
+    the current step) and the rolling flush slice (a 1/period slice of its rows, each
+    row replaying the g = 0 steps it lags).  Timed on copies of the item table's state
+    as the timed region left it (the slice the clock points at, its real lags), last[]
+    restored before every launch; the batch-row launch on the first pool batch's ids.
+    Algorithmic bytes: moved rows x D x (2 + 4 + 4) B read and written + 8 B of last[]
+    per row; the kernel is VALU-bound (~100 instructions, 16 of them sqrt / rcp, per
+    replayed step of 8 elements), reported against HBM."""
     from tencent_recommendation_2025_amd import kernels as K
     if not getattr(opt, 'rolling', False):
         return None
@@ -520,34 +522,88 @@ def catchup_roofline(opt, reps):
     lo, hi = s * per, min(rows, (s + 1) * per)
     lag = (t - last0[lo:hi].long()).clamp(min=0)
     stream = torch.cuda.current_stream()
-    total = 0.0
-    for _ in range(reps):
-        last.copy_(last0)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        K.table_adamw_catchup_slice(p, m, v, last, opt.clock, period)
-        e1.record(stream)
-        e1.synchronize()
-        total += e0.elapsed_time(e1)
-    ms = total / reps
+
+    def timed(fn):
+        total = 0.0
+        for _ in range(reps):
+            last.copy_(last0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            e1.synchronize()
+            total += e0.elapsed_time(e1)
+        return total / reps
+
+    ms = timed(lambda: K.table_adamw_catchup_slice(p, m, v, last, opt.clock, period))
     n = hi - lo
     moved = int((lag > 0).sum().item())
     alg = moved * D * (p.element_size() + 8) * 2 + n * 8
-    gbps = alg / (ms * 1e-3) / 1e9
-    res = {'bound': 'hbm', 'kernel': 'grk::k_adamw_catchup (rolling flush: one 1/%d slice of a 1M-row table)' % period,
+    # the batch rows' catch-up: rows the batch reads, from the state the timed region left
+    # (their lag since they were last read or flushed, at most one period)
+    b_ms = b_alg = 0.0
+    if batch is not None:
+        ids = K.batch_row_ids(*batch[:4], with_user=False)[0]
+        b_ms = timed(lambda: K.table_adamw_catchup(p, m, v, last, None, opt.clock, ids))
+        u = ids[ids > 0].unique()
+        b_moved = int(((t - last0[u].long()) > 0).sum().item())
+        b_alg = b_moved * D * (p.element_size() + 8) * 2 + ids.numel() * 8 + u.numel() * 8
+    calls = len(opt._deferred)
+    launches = calls * (2 if batch is not None else 1)
+    tot_ms = calls * (ms + b_ms)
+    tot_alg = calls * (alg + b_alg)
+    gbps = tot_alg / (tot_ms * 1e-3) / 1e9
+    res = {'bound': 'hbm', 'kernel': 'grk::k_adamw_catchup (every launch of a step: per deferred table the batch '
+                                     'rows\' catch-up + the rolling flush slice, 1/%d of a 1M-row table)' % period,
            'achieved': round(gbps, 1), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': round(gbps / HBM_PEAK_GBPS, 4),
-           'traffic': None, 'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2),
-           'calls_per_step': len(opt._deferred), 'ms_per_step': round(ms * len(opt._deferred), 4),
-           'replayed_steps_per_launch': int(lag.sum().item()), 'rows_moved_per_launch': moved,
-           'mean_lag_steps': round(float(lag.float().mean().item()), 2),
+           'traffic': None, 'alg_bytes_per_launch': int(tot_alg / launches),
+           'avg_launch_us': round(tot_ms / launches * 1e3, 2), 'calls_per_step': launches,
+           'ms_per_step': round(tot_ms, 4),
+           'slice': {'avg_launch_us': round(ms * 1e3, 2), 'alg_bytes_per_launch': int(alg),
+                     'replayed_steps_per_launch': int(lag.sum().item()), 'rows_moved_per_launch': moved,
+                     'mean_lag_steps': round(float(lag.float().mean().item()), 2)},
+           'batch_rows': {'avg_launch_us': round(b_ms * 1e3, 2), 'alg_bytes_per_launch': int(b_alg)},
            'note': 'VALU-bound: the g = 0 AdamW replay is ~100 VALU instructions (16 of them 8-cycle '
                    'sqrt / rcp) per replayed step of 8 elements',
            'workload': {'table_rows': int(rows), 'D': int(D), 'slice_rows': int(n), 'period': int(period)}}
     p_ = _pmc(f'{PMC_TAG}_pmc_catchup.json', {k: res['workload'][k] for k in ('table_rows', 'D', 'period')})
     if p_ is not None:
-        res['traffic'] = int(p_['traffic_bytes_per_launch'])
+        res['slice']['traffic'] = int(p_['traffic_bytes_per_launch'])
+        res['traffic_note'] = f'PMC of the slice launch only: slice.traffic (profiles/{PMC_TAG}_pmc_catchup.json)'
     del p, m, v, last, last0
     return res
+
+
+def family_entry(name, members):
+    """One kernel family (the headline is ONE rule -- the family with
+    the most device time per step): every launch of the family in one step, i.e. its
+    members' ms_per_step summed, and its rate = the members' algorithmic bytes (HBM
+    bound) or FLOPs (MFMA bound) per step over that time.  ``traffic`` is the PMC HBM
+    bytes per launch averaged over the members that carry one (None if none does)."""
+    members = [r for r in members if r and r.get('peak') and r.get('ms_per_step')]
+    if not members:
+        return None
+    bound = members[0]['bound']
+    ms = sum(r['ms_per_step'] for r in members)
+    calls = sum(r.get('calls_per_step', 1) for r in members)
+    if bound == 'mfma':
+        work = sum(r.get('flops_per_launch', 0) * r.get('calls_per_step', 1) for r in members) \
+            or sum(r.get('flops_per_step', 0) for r in members)
+        achieved, peak, unit = work / (ms * 1e-3) / 1e12, BF16_PEAK_TFLOPS, 'TFLOP/s'
+    else:
+        work = sum(r.get('alg_bytes_per_launch', 0) * r.get('calls_per_step', 1) for r in members)
+        achieved, peak, unit = work / (ms * 1e-3) / 1e9, HBM_PEAK_GBPS, 'GB/s'
+    with_t = [r for r in members if r.get('traffic')]
+    traffic = alg = None
+    if with_t:
+        c = sum(r.get('calls_per_step', 1) for r in with_t)
+        traffic = int(sum(r['traffic'] * r.get('calls_per_step', 1) for r in with_t) / c)
+        alg = int(sum(r.get('alg_bytes_per_launch', 0) * r.get('calls_per_step', 1) for r in with_t) / c)
+    return {'family': name, 'bound': bound, 'kernel': name + ': ' + ' + '.join(r['kernel'] for r in members),
+            'achieved': round(achieved, 1), 'peak': peak, 'unit': unit, 'frac': round(achieved / peak, 4),
+            'traffic': traffic, 'traffic_alg_bytes_per_launch': alg,
+            'avg_launch_us': round(ms / calls * 1e3, 2), 'calls_per_step': calls, 'ms_per_step': round(ms, 4),
+            'members': [r['kernel'] for r in members]}
 
 
 _T0 = time.perf_counter()
@@ -685,37 +741,45 @@ def semantic_id_setup(a, dev, reps):
 
 
 def _rooflines(a, kv, jagged, rows, trace, btrace, model, pool, sid_roof, wtrace=None, opt=None):
-    """Every measured kernel (after the timed region): (headline roofline, the others)."""
+    """Every measured kernel (after the timed region): (headline roofline, the others).
+
+    The headline is the kernel FAMILY with the most device time per step (every launch
+    of the family in one step; one rule for all of them): the attention kernels of every
+    layer (forward, dQ, dK/dV), the weight gradients, the table AdamW replays, the
+    embedding backward calls, the sampled softmax (with --loss sampled_softmax).  The
+    family entries head ``rooflines``, followed by every member and the unranked
+    entries (cold item gather, seq-side gather, RQ-VAE code search)."""
     from tencent_recommendation_2025_amd import jagged as J
-    dkdv, more = attention_rooflines(a, kv, a.roofline_reps, jagged=jagged)
-    more.insert(0, dkdv)
+    dkdv, (fwd, dq) = attention_rooflines(a, kv, a.roofline_reps, jagged=jagged)
     progress('rooflines: attention')
-    more.append(gather_roofline(trace, a.roofline_reps))
+    others = [gather_roofline(trace, a.roofline_reps)]
     item_table = model.item_emb.weight if model.item_emb.weight.numel() else None
     if item_table is not None:
-        more.append(item_gather_roofline(item_table.detach(), pool[0], a.roofline_reps))
+        others.append(item_gather_roofline(item_table.detach(), pool[0], a.roofline_reps))
     progress('rooflines: gathers')
     wk = J.capacity_for(rows[0], a.jagged_quantum) if jagged else a.batch * (a.maxlen + 1)
-    more.append(wgrad_roofline(a, a.roofline_reps, wk, wtrace))
-    more.extend(ss_rooflines(pool[0], a, a.roofline_reps))
+    wg = wgrad_roofline(a, a.roofline_reps, wk, wtrace)
+    ss = ss_rooflines(pool[0], a, a.roofline_reps)
     progress('rooflines: wgrad, sampled softmax')
-    cu = catchup_roofline(opt, a.roofline_reps) if opt is not None else None
+    cu = catchup_roofline(opt, a.roofline_reps, pool[0]) if opt is not None else None
     if cu is not None:
-        more.append(cu)
-        progress('rooflines: rolling flush')
+        progress('rooflines: table AdamW replays')
+    eb = []
     if btrace:   # last: scripts/pmc_rooflines.py finds these calls' PMC windows at the end of the run
-        more.extend(backward_rooflines(btrace, a.roofline_reps))
+        eb = backward_rooflines(btrace, a.roofline_reps)
         progress('rooflines: embedding backward')
     if sid_roof is not None:
-        more.append(sid_roof)
-    # headline: the hand-written hot-path kernel family with the most device time per step
-    # (every launch of the family in one step: average launch x launches per step), with
-    # an HBM or MFMA roof
-    ranked = [r for r in more if r.get('peak') and r.get('ms_per_step')]
-    roof = max(ranked, key=lambda r: r['ms_per_step'])
-    more.remove(roof)
-
-    return roof, more
+        others.append(sid_roof)
+    fams = [family_entry('HSTU attention (fwd + dQ + dK/dV, every layer)' if a.block == 'hstu'
+                         else 'softmax attention (fwd + dQ + dK/dV, every layer)', [fwd, dq, dkdv]),
+            family_entry('weight gradients (grk_wgrad, every dense layer)', [wg]),
+            family_entry('table AdamW replays (k_adamw_catchup)', [cu]),
+            family_entry('embedding backward (grk_embedding_backward calls)', eb),
+            family_entry('in-batch sampled softmax (fwd + bwd)', ss)]
+    fams = sorted((f for f in fams if f is not None), key=lambda f: -f['ms_per_step'])
+    roof = fams[0]
+    members = [fwd, dq, dkdv, wg] + ([cu] if cu else []) + eb + ss
+    return roof, fams[1:] + members + others
 
 
 def main():

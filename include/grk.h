@@ -455,36 +455,6 @@ typedef struct grk_row_copy {
 } grk_row_copy;
 int grk_gather_rows(const grk_row_copy* copies, int num_copies, const int32_t* row_map, int64_t rows, void* stream);
 
-/* The composed itemdnn / userdnn weight of the projection restatement
- * (functional.dnn_weight; the eager composition of model._dnn_weight, reference
- * model/BaseLine/model.py:129-139 with emb_transform folded in, 242-277):
- *   out[d, width] = [ blocks at their columns | W_k Wt_k at mm columns |
- *                     bias + sum_k W_k bt_k at bias_col | 0 elsewhere ]
- * blocks: [d, width_j] fp32 / bf16 with row stride ld; mm: W_k [d, kk] (stride ldk),
- * Wt [kk, w] (stride ldt), bt [kk], all fp32; sums in k order, fp32.  out fp32 / bf16
- * contiguous.  At most 16 blocks and 4 mm features. */
-typedef struct grk_dnnw_block {
-  const void* src;
-  int64_t ld;
-  int dtype, col, width;
-} grk_dnnw_block;
-typedef struct grk_dnnw_mm {
-  const float* wk;
-  int64_t ldk;
-  const float* wt;
-  int64_t ldt;
-  const float* bt;
-  int kk, w, col;
-} grk_dnnw_mm;
-int grk_dnn_weight_fwd(const grk_dnnw_block* blocks, int nblocks, const grk_dnnw_mm* mms, int nmm, const float* bias,
-                       int d, int width, int bias_col, void* out, int out_dtype, void* stream);
-/* Its backward from g [d, width] (fp32 / bf16, row stride ldg): g32 = fp32(g) [d, width]
- * contiguous (the blocks' and the bias's gradients are its columns); per mm feature f,
- * dM = [g(mm columns) | g(bias_col)]: dW_k = dM [Wt | bt]^T ([d, kk] blocks of dwk, in
- * feature order) and [dWt | dbt] = W_k^T dM ([kk, w + 1] blocks of det). */
-int grk_dnn_weight_bwd(const void* g, int g_dtype, int64_t ldg, const grk_dnnw_mm* mms, int nmm, int d, int width,
-                       int bias_col, float* g32, float* dwk, float* det, void* stream);
-
 /* Row-sharded tables (sharding.ShardExchange.route; replaces the sort-based torch
  * route): the distinct ids of ids[n] grouped by owner (id % world) and ascending
  * inside an owner -> send_ids[0, n_uniq); send_counts[world] = distinct ids per

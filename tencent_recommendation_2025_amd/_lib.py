@@ -93,15 +93,6 @@ class GrkRemapRole(C.Structure):
                 ('tt_want', C.c_int64), ('n', C.c_int64)]
 
 
-class GrkDnnwBlock(C.Structure):
-    _fields_ = [('src', C.c_void_p), ('ld', C.c_int64), ('dtype', C.c_int), ('col', C.c_int), ('width', C.c_int)]
-
-
-class GrkDnnwMm(C.Structure):
-    _fields_ = [('wk', C.c_void_p), ('ldk', C.c_int64), ('wt', C.c_void_p), ('ldt', C.c_int64), ('bt', C.c_void_p),
-                ('kk', C.c_int), ('w', C.c_int), ('col', C.c_int)]
-
-
 class GrkGemmGroup(C.Structure):
     _fields_ = [('a', C.c_void_p), ('lda', C.c_int64), ('b', C.c_void_p), ('ldb', C.c_int64), ('c', C.c_void_p),
                 ('ldc', C.c_int64), ('rows', C.c_int64), ('b_rows', C.c_int64)]
@@ -184,8 +175,6 @@ SIGNATURES = {
     'grk_route': (_I, [_P, _I64, _I, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'grk_flat_pack': (_I, [C.POINTER(GrkPackRange), _I, _P, _P]),
     'grk_jagged_remap': (_I, [C.POINTER(GrkRemapRole), _I, _P, _I64, _P]),
-    'grk_dnn_weight_fwd': (_I, [C.POINTER(GrkDnnwBlock), _I, C.POINTER(GrkDnnwMm), _I, _P, _I, _I, _I, _P, _I, _P]),
-    'grk_dnn_weight_bwd': (_I, [_P, _I, _I64, C.POINTER(GrkDnnwMm), _I, _I, _I, _I, _P, _P, _P, _P]),
     'grk_add_norm_fwd': (_I, [_P, _I64, _P, _I64, _P, _P, _F, _I64, _I, _P, _I64, _P, _I64, _I, _P, _P]),
     'grk_add_norm_bwd_workspace': (_SZ, [_I64, _I]),
     'grk_add_norm_bwd': (_I, [_P, _I64, _I, _P, _I64, _P, _I64, _P, _P, _I64, _I, _P, _I64, _P, _P, _P, _SZ, _P]),

@@ -280,25 +280,15 @@ __global__ void k_segments(const unsigned* __restrict__ keys, const int* __restr
 // per workgroup and added once per workgroup -- one atomic per wave on the single
 // counter serialised (~14k waves at C2: 29-46 us per call).
 constexpr int kSegKeyBlocks = 512;
-// recs (may be null): the 4-byte occurrence records of the sliced chunk kernel --
-// (gradient row address - gbase) / 16 with bit 31 = segment head, kRecEnd past the
-// real keys (k_seg_chunks_sliced2).
-constexpr unsigned kRecEnd = 0xFFFFFFFFu;
 __global__ void __launch_bounds__(256) k_segments_key(const unsigned* __restrict__ keys, int64_t n, unsigned sentinel,
                                                       int* __restrict__ seg_start, int* __restrict__ seg_end,
-                                                      int32_t* __restrict__ count,
-                                                      const unsigned long long* __restrict__ gptr,
-                                                      unsigned long long gbase, unsigned* __restrict__ recs) {
+                                                      int32_t* __restrict__ count) {
   __shared__ int wsum[4];
   int heads = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const unsigned k = keys[i];
-    if (k == sentinel) {
-      if (recs) recs[i] = kRecEnd;
-      continue;
-    }
+    if (k == sentinel) continue;
     const bool head = i == 0 || keys[i - 1] != k;
-    if (recs) recs[i] = (unsigned)((gptr[i] - gbase) >> 4) | (head ? 0x80000000u : 0u);
     if (head) {
       seg_start[k] = (int)i;
       ++heads;
@@ -722,202 +712,6 @@ __global__ void __launch_bounds__(256) k_seg_chunks_partial(const unsigned* __re
                                       partials);
 }
 
-// Column-sliced form of k_seg_chunks_partial (dim = 64 * slices, slices in {1, 2, 4, 8}):
-// the chunk sums run per 64-column slice, slice s on XCD s (mod slices), so an XCD
-// gathers only its slice of every upstream gradient row -- 128 B of bf16 per row -- and
-// the rows a call reads (~40k: ~5 MB per slice) meet in the XCD's 4 MB L2 instead of
-// every XCD fetching whole 1 KB rows from the Infinity Cache.  One wave sums 8 chunks
-// side by side, 8 lanes x 8 elements per chunk; every column is still summed in the
-// chunk's entry order and the pieces crossing chunk edges go to the same partial slots,
-// so the result is the same bits as the whole-row kernel (and the oracle's chunk-order
-// restatement).  The keys and gradient-row addresses of the next PIPE entries load
-// while the current rows are summed; keys / gptr are read up to the chunk's end past n
-// (the workspace rounds both up to whole chunks).
-// k_seg_chunks_sliced with 4-byte occurrence records (k_segments_key writes them):
-// a lane group reads 64 B of records per 16 entries (was 64 B of keys + 128 B of
-// addresses, 8x over across the XCDs, and 64 VGPRs), the key itself only at a
-// segment head.  Row address = gbase + 16 * (rec & 0x7FFFFFFF).  Same bits.
-template <typename G, int CH, int PIPE, typename OT = float>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_seg_chunks_sliced2(const unsigned* __restrict__ keys,
-                                                            const unsigned* __restrict__ recs, const char* gbase,
-                                                            const int* __restrict__ pos, int64_t n,
-                                                            unsigned sentinel, int dim, int slices, int64_t groups,
-                                                            OT* __restrict__ dense_out, float* __restrict__ uniq_rows,
-                                                            int32_t* __restrict__ row_slot,
-                                                            float* __restrict__ partials) {
-  constexpr int LW = 8;
-  static_assert(CH % PIPE == 0 && PIPE % 4 == 0, "batch");
-  const int lane = threadIdx.x & 63, grp = lane >> 3, sub = lane & 7;
-  const unsigned xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
-  const int slice = (int)xcd % slices;
-  const int64_t cg = (int64_t)q * (8 / slices) + (int64_t)xcd / slices;  // 32 chunks per workgroup
-  if (cg >= groups) return;
-  const int64_t chunk = cg * 32 + (threadIdx.x >> 6) * 8 + grp;
-  const int64_t p0 = chunk * CH;
-  const int c = slice * 64 + sub * LW;
-  const int64_t p1 = p0 < n ? min(n, p0 + CH) : p0;
-  unsigned cur = p0 < n ? keys[p0] : sentinel;
-  const bool act = cur != sentinel;
-  const unsigned kprev = act && p0 > 0 ? keys[p0 - 1] : sentinel;
-  const unsigned knext = act && p1 < n ? keys[p1] : sentinel;
-  int u = act && pos ? pos[p0] - 1 : 0;
-  WaveAcc<LW> acc;
-  acc.zero();
-  int64_t ps = p0, pe = p0;  // current piece [ps, pe) of key cur
-  bool live = act;
-  auto flush = [&]() {
-    const bool whole = (ps > p0 || kprev != cur) && (pe < p1 || knext != cur);
-    if (whole) {
-      store_final(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
-    } else {
-      const int slot = (ps == p0 && kprev == cur) ? 0 : 1;
-      float* dst = partials + (chunk * 2 + slot) * dim + c;
-#pragma unroll
-      for (int e = 0; e < LW; e += 4)
-        *reinterpret_cast<float4*>(dst + e) = make_float4(acc.v[e], acc.v[e + 1], acc.v[e + 2], acc.v[e + 3]);
-    }
-  };
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  unsigned rr[PIPE];
-  auto fetch = [&](int s0) {
-#pragma unroll
-    for (int j = 0; j < PIPE; j += 4) {
-      const u32x4 t = *reinterpret_cast<const u32x4*>(recs + p0 + s0 + j);
-      rr[j] = t.x;
-      rr[j + 1] = t.y;
-      rr[j + 2] = t.z;
-      rr[j + 3] = t.w;
-    }
-  };
-  if (live) fetch(0);
-  for (int s0 = 0; s0 < CH; s0 += PIPE) {
-    if (__ballot(live) == 0) break;
-    WaveVec<G, LW> r[PIPE];
-    bool ok[PIPE], hd[PIPE];
-#pragma unroll
-    for (int j = 0; j < PIPE; ++j) {
-      ok[j] = live && p0 + s0 + j < p1 && rr[j] != kRecEnd;  // sorted: false from the first padding entry on
-      hd[j] = (rr[j] >> 31) != 0;
-      if (ok[j])
-        r[j].load((unsigned long long)(gbase + (unsigned long long)(rr[j] & 0x7FFFFFFFu) * 16), c);
-    }
-    if (live && s0 + PIPE < CH && p0 + s0 + PIPE < p1) fetch(s0 + PIPE);
-#pragma unroll
-    for (int j = 0; j < PIPE; ++j) {
-      if (!ok[j]) {
-        live = false;
-      } else {
-        const int64_t p = p0 + s0 + j;
-        if (hd[j] && p > p0) {   // a new segment starts at p
-          flush();
-          acc.zero();
-          cur = keys[p];
-          ps = p;
-          if (pos) u = pos[ps] - 1;
-        }
-#pragma unroll
-        for (int x = 0; x < LW; ++x) acc.v[x] += r[j].get(x);
-        pe = p + 1;
-      }
-    }
-  }
-  if (act) flush();
-}
-
-template <typename G, int CH, int PIPE, typename OT = float>
-__global__ void __launch_bounds__(256) k_seg_chunks_sliced(const unsigned* __restrict__ keys,
-                                                           const unsigned long long* __restrict__ gptr,
-                                                           const int* __restrict__ pos, int64_t n, unsigned sentinel,
-                                                           int dim, int slices, int64_t groups,
-                                                           OT* __restrict__ dense_out, float* __restrict__ uniq_rows,
-                                                           int32_t* __restrict__ row_slot,
-                                                           float* __restrict__ partials) {
-  constexpr int LW = 8;
-  static_assert(CH % PIPE == 0 && PIPE % 4 == 0, "batch");
-  const int lane = threadIdx.x & 63, grp = lane >> 3, sub = lane & 7;
-  const unsigned xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
-  const int slice = (int)xcd % slices;
-  const int64_t cg = (int64_t)q * (8 / slices) + (int64_t)xcd / slices;  // 32 chunks per workgroup
-  if (cg >= groups) return;
-  const int64_t chunk = cg * 32 + (threadIdx.x >> 6) * 8 + grp;
-  const int64_t p0 = chunk * CH;
-  const int c = slice * 64 + sub * LW;
-  const int64_t p1 = p0 < n ? min(n, p0 + CH) : p0;
-  unsigned cur = p0 < n ? keys[p0] : sentinel;
-  const bool act = cur != sentinel;
-  const unsigned kprev = act && p0 > 0 ? keys[p0 - 1] : sentinel;
-  const unsigned knext = act && p1 < n ? keys[p1] : sentinel;
-  int u = act && pos ? pos[p0] - 1 : 0;
-  WaveAcc<LW> acc;
-  acc.zero();
-  int64_t ps = p0, pe = p0;  // current piece [ps, pe) of key cur
-  bool live = act;
-  auto flush = [&]() {
-    const bool whole = (ps > p0 || kprev != cur) && (pe < p1 || knext != cur);
-    if (whole) {
-      store_final(acc, cur, u, dim, c, dense_out, uniq_rows, row_slot);
-    } else {  // the piece's sum goes to the chunk's head (0) or tail (1) slot
-      const int slot = (ps == p0 && kprev == cur) ? 0 : 1;
-      float* dst = partials + (chunk * 2 + slot) * dim + c;
-#pragma unroll
-      for (int e = 0; e < LW; e += 4)
-        *reinterpret_cast<float4*>(dst + e) = make_float4(acc.v[e], acc.v[e + 1], acc.v[e + 2], acc.v[e + 3]);
-    }
-  };
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-  unsigned kk[PIPE];
-  unsigned long long gg[PIPE];
-  auto fetch = [&](int s0) {
-#pragma unroll
-    for (int j = 0; j < PIPE; j += 4) {
-      const u32x4 t = *reinterpret_cast<const u32x4*>(keys + p0 + s0 + j);
-      kk[j] = t.x;
-      kk[j + 1] = t.y;
-      kk[j + 2] = t.z;
-      kk[j + 3] = t.w;
-    }
-#pragma unroll
-    for (int j = 0; j < PIPE; j += 2) {
-      const u64x2 t = *reinterpret_cast<const u64x2*>(gptr + p0 + s0 + j);
-      gg[j] = t.x;
-      gg[j + 1] = t.y;
-    }
-  };
-  if (live) fetch(0);
-  for (int s0 = 0; s0 < CH; s0 += PIPE) {
-    if (__ballot(live) == 0) break;
-    WaveVec<G, LW> r[PIPE];
-    bool ok[PIPE];
-    unsigned kc[PIPE];
-#pragma unroll
-    for (int j = 0; j < PIPE; ++j) {
-      ok[j] = live && p0 + s0 + j < p1 && kk[j] != sentinel;  // sorted: false from the first padding entry on
-      kc[j] = kk[j];
-      if (ok[j]) r[j].load(gg[j], c);
-    }
-    if (live && s0 + PIPE < CH && p0 + s0 + PIPE < p1) fetch(s0 + PIPE);
-#pragma unroll
-    for (int j = 0; j < PIPE; ++j) {
-      if (!ok[j]) {
-        live = false;
-      } else {
-        if (kc[j] != cur) {
-          flush();
-          acc.zero();
-          cur = kc[j];
-          ps = p0 + s0 + j;
-          if (pos) u = pos[ps] - 1;
-        }
-#pragma unroll
-        for (int x = 0; x < LW; ++x) acc.v[x] += r[j].get(x);
-        pe = p0 + s0 + j + 1;
-      }
-    }
-  }
-  if (act) flush();
-}
-
 // One wave per chunk edge b: the row first crossing b (it starts in chunk
 // b - 1, whose tail slot holds its first piece) = tail(b - 1) + head(b) + ...
 // + head(last chunk of the row), added in that order.
@@ -1318,7 +1112,6 @@ struct BwdWs {
   int *flags, *pos, *seg_start, *seg_end;
   unsigned long long *gptr_in, *gptr_out;
   float* partials;  // chunked mode: [chunks][2][dim] piece sums
-  unsigned* recs;   // chunked sliced mode: 4-byte occurrence records (k_segments_key)
   void* sort_tmp;
   size_t sort_bytes;
   void* scan_tmp;
@@ -1336,16 +1129,14 @@ static int plan_ws(int64_t n, int64_t num_rows, int dim, char* base, BwdWs* ws) 
     return p;
   };
   ws->keys_in = (unsigned*)take(n * 4);
-  const int64_t nr = (n + kPartialChunk - 1) / kPartialChunk * kPartialChunk;  // k_seg_chunks_sliced reads whole chunks
-  ws->keys_out = (unsigned*)take(nr * 4);
+  ws->keys_out = (unsigned*)take(n * 4);
   ws->seg_key = (unsigned*)take(n * 4);
   ws->flags = (int*)take(n * 4);
   ws->pos = (int*)take(n * 4);
   ws->seg_start = (int*)take(n * 4);
   ws->seg_end = (int*)take(n * 4);
   ws->gptr_in = (unsigned long long*)take(n * 8);
-  ws->gptr_out = (unsigned long long*)take(nr * 8);
-  ws->recs = (unsigned*)take(nr * 4);
+  ws->gptr_out = (unsigned long long*)take(n * 8);
   ws->partials = (float*)take((size_t)((n + kPartialChunk - 1) / kPartialChunk) * 2 * dim * sizeof(float));
   unsigned end_bit = 1;
   while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)num_rows) ++end_bit;
@@ -1615,31 +1406,9 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
   }
   ws.keys_out = skeys;  // the sorted pairs (either buffer of the ping-pong)
   ws.gptr_out = sgptr;
-  // chunked mode, column-sliced (GRK_BWD_SLICED: 0 / unset whole rows per wave, 1 the
-  // first sliced form, 2 the record form): the records need 16-byte gradient rows within
-  // 32 GB of the lowest gradient buffer
-  static const int sliced_mode = [] {
-    const char* e = getenv("GRK_BWD_SLICED");
-    return e ? atoi(e) : 0;
-  }();
-  unsigned long long gbase = ~0ull, gend = 0;
-  bool rec_ok = flags == GRK_BWD_CHUNKED && by_key && sliced_mode == 2 && dim % 64 == 0 &&
-                (dim / 64 == 1 || dim / 64 == 2 || dim / 64 == 4 || dim / 64 == 8);
-  for (int i = 0; i < num_lookups && rec_ok; ++i) {
-    const grk_lookup& L = lookups[i];
-    if (!L.num_tokens) continue;
-    const unsigned long long a = (unsigned long long)L.grad;
-    rec_ok = (L.grad_ld * esize) % 16 == 0 && (L.grad_col * esize) % 16 == 0;
-    gbase = std::min(gbase, a);
-    gend = std::max(gend, a + (unsigned long long)((L.num_tokens - 1) * L.grad_ld + L.grad_col + dim) * esize);
-  }
-  for (int i = 0; i < num_lookups && rec_ok; ++i)
-    if (lookups[i].num_tokens) rec_ok = ((unsigned long long)lookups[i].grad - gbase) % 16 == 0;
-  rec_ok = rec_ok && gend > gbase && gend - gbase < (1ull << 35);
   if (by_key) {
     k_segments_key<<<g < kSegKeyBlocks ? g : kSegKeyBlocks, B, 0, s>>>(ws.keys_out, total, sentinel, ws.seg_start,
-                                                                       ws.seg_end, uniq_count, ws.gptr_out, gbase,
-                                                                       rec_ok ? ws.recs : nullptr);
+                                                                       ws.seg_end, uniq_count);
     GRK_LAUNCH_CHECK();
     ws.pos = nullptr;
   } else {
@@ -1660,45 +1429,19 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
       const int64_t pchunks = (total + kPartialChunk - 1) / kPartialChunk;
       const unsigned gw = (unsigned)((pchunks + 3) / 4);
       const unsigned ge = (unsigned)(pchunks > 1 ? (pchunks - 1 + 3) / 4 : 0);
-      // column-sliced chunk sums (GRK_BWD_SLICED=1 / 2; default: whole rows per wave --
-      // the same bits either way)
-      const int slices = dim / 64;
-      const bool sliced = (sliced_mode == 1 || rec_ok) && dim % 64 == 0 &&
-                          (slices == 1 || slices == 2 || slices == 4 || slices == 8);
-      const int64_t sgroups = (pchunks + 31) / 32;
-      const int rep = sliced ? 8 / slices : 1;
-      const unsigned gs = (unsigned)(8 * ((sgroups + rep - 1) / rep));
 #define GRK_SEGP(G, LW)                                                                                          \
-  if (sliced && rec_ok)                                                                                          \
-    k_seg_chunks_sliced2<G, kPartialChunk, sizeof(G) == 2 ? 16 : 8><<<gs, 256, 0, s>>>(ws.keys_out, ws.recs, (const char*)gbase,     \
-                                                                  ws.pos, total, sentinel, dim, slices, sgroups, \
-                                                                  dense_out, uniq_rows, row_slot, ws.partials);  \
-  else if (sliced)                                                                                               \
-    k_seg_chunks_sliced<G, kPartialChunk, sizeof(G) == 2 ? 16 : 8><<<gs, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, total,        \
-                                                                 sentinel, dim, slices, sgroups, dense_out,      \
-                                                                 uniq_rows, row_slot, ws.partials);              \
-  else                                                                                                           \
-    k_seg_chunks_partial<G, LW, kPartialChunk><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start,\
-                                                                  ws.seg_end, total, sentinel, dim, dense_out,   \
-                                                                  uniq_rows, row_slot, ws.partials);             \
+  k_seg_chunks_partial<G, LW, kPartialChunk><<<gw, 256, 0, s>>>(ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start,  \
+                                                                ws.seg_end, total, sentinel, dim, dense_out,     \
+                                                                uniq_rows, row_slot, ws.partials);               \
   GRK_LAUNCH_CHECK();                                                                                            \
   if (ge)                                                                                                        \
     k_seg_partials_combine<LW, kPartialChunk><<<ge, 256, 0, s>>>(ws.keys_out, ws.pos, ws.seg_start, ws.seg_end,  \
                                                                  total, sentinel, dim, ws.partials, dense_out,    \
                                                                  uniq_rows, row_slot)
       if (dense_out16) {
-        if (sliced && rec_ok)
-          k_seg_chunks_sliced2<bf16_t, kPartialChunk, 16, bf16_t><<<gs, 256, 0, s>>>(
-              ws.keys_out, ws.recs, (const char*)gbase, ws.pos, total, sentinel, dim, slices, sgroups, dense_out16,
-              uniq_rows, row_slot, ws.partials);
-        else if (sliced)
-          k_seg_chunks_sliced<bf16_t, kPartialChunk, 16, bf16_t><<<gs, 256, 0, s>>>(
-              ws.keys_out, ws.gptr_out, ws.pos, total, sentinel, dim, slices, sgroups, dense_out16, uniq_rows,
-              row_slot, ws.partials);
-        else
-          k_seg_chunks_partial<bf16_t, 8, kPartialChunk, bf16_t><<<gw, 256, 0, s>>>(
-              ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel, dim, dense_out16, uniq_rows,
-              row_slot, ws.partials);
+        k_seg_chunks_partial<bf16_t, 8, kPartialChunk, bf16_t><<<gw, 256, 0, s>>>(
+            ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel, dim, dense_out16, uniq_rows,
+            row_slot, ws.partials);
         GRK_LAUNCH_CHECK();
         if (ge)
           k_seg_partials_combine<8, kPartialChunk, bf16_t><<<ge, 256, 0, s>>>(

@@ -260,11 +260,6 @@ int make_plan(hipblasLtHandle_t h, const Key& key, bool has_bias, Plan* p, const
   }
   p->algo = res[best].algo;
   p->ws = res[best].workspaceSize;
-  if (getenv("GRK_GEMM_LOG"))
-    fprintf(stderr, "grk_gemm plan m=%lld n=%lld k=%lld ta=%d tb=%d c=%s bias=%d ws=%zu: candidate %d of %d "
-            "(%.1f us; first %.1f us): %s\n", (long long)key.m, (long long)key.n, (long long)key.k, key.ta, key.tb,
-            key.ct == GRK_F32 ? "f32" : "bf16", key.bt, p->ws, best, n, tbest, t0,
-            hipblaslt_ext::getKernelNameFromAlgo(h, p->algo).c_str());
   return GRK_OK;
 }
 

@@ -34,8 +34,6 @@
 //    8 consecutive columns -- bias / C_in reads and the bf16 stores are 16-byte
 //    vectors over whole 128-B row segments (from registers they would be 2-byte
 //    scattered stores).
-#include <stdlib.h>
-
 #include <type_traits>
 
 #include "grk_common.h"
@@ -55,11 +53,11 @@ __device__ __forceinline__ int mg_swz(int row) {
   else return (row >> 2) & 3;
 }
 
-template <int BM, int BN, int WM, int WN, int NST, bool BNC, int BK, bool ATR = false>
+template <int BM, int BN, int WM, int WN, int NST, bool BNC, int BK>
 struct MgGeo {
   static constexpr int NW = WM * WN, NT = 64 * NW;
-  static constexpr int RBA = ATR ? 2 * BM : 2 * BK;           // A image row bytes ([BK][BM] K-major or [BM][BK])
-  static constexpr int IMGA = ATR ? BK * RBA : BM * RBA;
+  static constexpr int RBA = 2 * BK;                          // A image row bytes ([BM][BK])
+  static constexpr int IMGA = BM * RBA;
   static constexpr int RBB = BNC ? 2 * BN : 2 * BK;           // B image row bytes
   static constexpr int IMGB = BNC ? BK * RBB : BN * RBA;      // [BK][BN] or [BN][BK]
   static constexpr int STAGE = IMGA + IMGB;
@@ -73,7 +71,6 @@ struct MgGeo {
   static_assert(NW * 32 * SROW * 4 <= NST * STAGE, "epilogue stage must fit in the ring");
   static_assert(WTN % 32 == 0 && WTM % 32 == 0 && (WTN / 8) <= 64, "wave tile");
   static_assert(BK == 32 || BK == 64, "BK: 32 or 64");
-  static_assert(!ATR || BNC, "a K-major A goes with a K-major B (the weight gradient)");
 };
 
 // Natural k order (B K-contiguous): element j of lane (r, h) = img[row][k0 + 8h + j].
@@ -133,13 +130,7 @@ struct MgArgs {
   int relu;
   int M, N, K;
   int tiles_n;          // column tiles
-  int total;            // tiles of the launch (x K slices)
-  // split K (weight gradients): slices of kchunk rows (multiples of BK); slice s
-  // writes C + s * slice_stride, and with dbpart the column sums of its A rows
-  // (the bias gradient) to dbpart[s * M + m]
-  int slices, kchunk;
-  int64_t slice_stride;
-  float* dbpart;
+  int total;            // tiles of the launch
 };
 
 // Waves per SIMD the register budget is cut for: 2 for 8-wave (and 4-wave, two per
@@ -148,9 +139,9 @@ struct MgArgs {
 // keeps the kernel inside 128 VGPRs (the other waves of the SIMD cover the latency).
 template <int WM, int WN> constexpr int mg_waves_per_simd() { return WM * WN >= 16 ? 4 : 2; }
 
-template <int BM, int BN, int WM, int WN, int NST, bool BNC, int BK, typename OT, bool ATR = false>
+template <int BM, int BN, int WM, int WN, int NST, bool BNC, int BK, typename OT>
 __global__ void __launch_bounds__(64 * WM * WN, (mg_waves_per_simd<WM, WN>())) k_mgemm(MgArgs g) {
-  using G = MgGeo<BM, BN, WM, WN, NST, BNC, BK, ATR>;
+  using G = MgGeo<BM, BN, WM, WN, NST, BNC, BK>;
   constexpr int RBA = G::RBA, CPR = RBA / 16, RPI = 1024 / RBA;   // chunks per row, rows per DMA instruction
   __shared__ __attribute__((aligned(16))) char smem[NST * G::STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -159,13 +150,10 @@ __global__ void __launch_bounds__(64 * WM * WN, (mg_waves_per_simd<WM, WN>())) k
   const unsigned phys = blockIdx.x, total = (unsigned)g.total;
   const unsigned q8 = total / 8, r8 = total % 8, xcd = phys % 8;
   const unsigned logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + phys / 8;
-  // slice-major: the tiles of one K slice (reading the same operand rows) share an XCD
-  const unsigned tiles = (unsigned)(g.total / g.slices);
-  const int slice = (int)(logical / tiles), tile = (int)(logical % tiles);
+  const int tile = (int)logical;
   const int m0 = (tile / g.tiles_n) * BM, n0 = (tile % g.tiles_n) * BN;
   const int M = g.M, N = g.N;
-  const int kb = slice * g.kchunk;                       // this block's K rows: [kb, kb + K)
-  const int K = min(g.K - kb, g.kchunk);
+  const int K = g.K;
   const int nsteps = K > 0 ? (K + BK - 1) / BK : 0;
   // DMA sources of this lane (rows clamped into the matrices: their outputs are not stored)
   // (K-contiguous images: row base + this lane's chunk column; a chunk past K -- the
@@ -177,15 +165,9 @@ __global__ void __launch_bounds__(64 * WM * WN, (mg_waves_per_simd<WM, WN>())) k
 #pragma unroll
   for (int i = 0; i < G::PWA; ++i) {
     const int q = w * G::PWA + i, row = RPI * q + lane / CPR;     // RPI rows of RBA bytes per instruction
-    if constexpr (ATR) {                                          // [BK][BM] K-major image (the ring_frag layout)
-      const int ma = m0 + 8 * ((lane % CPR) ^ wg_swz(row));
-      acol[i] = row;
-      pa[i] = g.a + (int64_t)kb * g.lda + (ma < M ? ma : 0);
-    } else {
-      const int ma = min(m0 + row, M - 1);
-      pa[i] = g.a + (int64_t)ma * g.lda;
-      acol[i] = 8 * ((lane % CPR) ^ mg_swz<RBA>(row));
-    }
+    const int ma = min(m0 + row, M - 1);
+    pa[i] = g.a + (int64_t)ma * g.lda;
+    acol[i] = 8 * ((lane % CPR) ^ mg_swz<RBA>(row));
   }
 #pragma unroll
   for (int i = 0; i < G::PWB; ++i) {
@@ -195,7 +177,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (mg_waves_per_simd<WM, WN>())) k
       const int row = q * (1024 / G::RBB) + lane / CPB;
       const int nb = n0 + 8 * ((lane % CPB) ^ wg_swz(row));
       bcol[i] = row;                                              // the image row (k) of this lane
-      pb[i] = g.b + (int64_t)kb * g.ldb + (nb < N ? nb : 0);
+      pb[i] = g.b + (nb < N ? nb : 0);
     } else {
       const int row = RPI * q + lane / CPR;
       const int nb = min(n0 + row, N - 1);
@@ -210,10 +192,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (mg_waves_per_simd<WM, WN>())) k
     const unsigned base = lds0 + buf * G::STAGE;
     const int k0 = step * BK;
 #pragma unroll
-    for (int i = 0; i < G::PWA; ++i) {
-      if constexpr (ATR) wg_dma16(pa[i] + (int64_t)(k0 + acol[i]) * g.lda, base + (wu * G::PWA + i) * 1024);
-      else wg_dma16(pa[i] + min(k0 + acol[i], K - 8), base + (wu * G::PWA + i) * 1024);
-    }
+    for (int i = 0; i < G::PWA; ++i) wg_dma16(pa[i] + min(k0 + acol[i], K - 8), base + (wu * G::PWA + i) * 1024);
 #pragma unroll
     for (int i = 0; i < G::PWB; ++i) {
       if constexpr (BNC) {
@@ -230,12 +209,6 @@ __global__ void __launch_bounds__(64 * WM * WN, (mg_waves_per_simd<WM, WN>())) k
 #pragma unroll
     for (int j = 0; j < G::TJ; ++j) acc[i][j] = acc_zero();
 
-  // db (ATR): the column sums of A this lane's fragments hold (its column, its k half)
-  const bool do_db = ATR && g.dbpart != nullptr && wn == 0 && n0 == 0;
-  float cs[G::TI];
-#pragma unroll
-  for (int i = 0; i < G::TI; ++i) cs[i] = 0.f;
-
   // one BK-deep step; MASK: the K tail (chunks at k >= K read as zeros)
   auto compute = [&](const char* ia, const char* ib, int kvalid, auto mask_tag) {
     constexpr bool MASK = decltype(mask_tag)::value;
@@ -246,16 +219,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (mg_waves_per_simd<WM, WN>())) k
       for (int i = 0; i < G::TI; ++i) {
         const int row = wm * G::WTM + 32 * i + r;
         uint4 v;
-        if constexpr (ATR) {
-          fa[i] = ring_frag<RBA>(ia, 16 * ks, wm * G::WTM + 32 * i, lane);
-          if (do_db) {
-            float q = 0.f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) q += static_cast<float>(fa[i][e]);
-            cs[i] += q;
-          }
-          continue;
-        } else if constexpr (BNC) {
+        if constexpr (BNC) {
           v = mg_chunk_perm<RBA>(ia, row, 2 * ks, hh);
           if (MASK) {
             if (8 * (2 * ks) >= kvalid) v.x = v.y = 0u;
@@ -316,18 +280,8 @@ __global__ void __launch_bounds__(64 * WM * WN, (mg_waves_per_simd<WM, WN>())) k
     if (g.bias_f32) MgOut<float>::load8(reinterpret_cast<const float*>(g.bias) + ncol, bias);
     else MgOut<bf16_t>::load8(reinterpret_cast<const bf16_t*>(g.bias) + ncol, bias);
   }
-  OT* C = reinterpret_cast<OT*>(g.c) + (int64_t)slice * g.slice_stride;
+  OT* C = reinterpret_cast<OT*>(g.c);
   const OT* Cin = reinterpret_cast<const OT*>(g.c_in);
-  if constexpr (ATR) {
-    if (do_db) {
-#pragma unroll
-      for (int i = 0; i < G::TI; ++i) {
-        const float other = __shfl_xor(cs[i], 32);   // the other k half of column r
-        const int m = m0 + wm * G::WTM + 32 * i + r;
-        if (hh == 0 && m < M) g.dbpart[(int64_t)slice * M + m] = cs[i] + other;
-      }
-    }
-  }
 #pragma unroll
   for (int i = 0; i < G::TI; ++i) {
 #pragma unroll
@@ -360,71 +314,20 @@ __global__ void __launch_bounds__(64 * WM * WN, (mg_waves_per_simd<WM, WN>())) k
   }
 }
 
-// Tile configurations (every wave owns 64 x 64 = 2 x 2 MFMA tiles; 32-deep K steps;
-// at ~90-128 FLOP per staged byte a CU needs ~85-110 KB of LDS-DMA in flight to cover
-// a DMA's ~1.1 us, hence deep rings):
-//   cfg 2: 256 x 128, 8 waves, 6 stages (144 KiB, one workgroup per CU);
-//   cfg 3: 256 x 256, 16 waves, 5 stages (160 KiB, one workgroup per CU);
-//   cfg 4: 128 x 128, 4 waves, 4 stages (64 KiB, two workgroups per CU);
-//   cfg 1: 256 x 128 with 64-deep steps in 3 stages (one step in flight);
-//   cfg 5: 256 x 256, 8 waves of 128 x 64, 5 stages.
-// (A 256 x 256 tile of 8 waves with 128 x 64 wave tiles spills at the 256-VGPR cap of
-// two waves per SIMD.)  Default (cfg 0): chosen per shape below; GRK_MGEMM_CFG forces one.
+// Tile configuration: 256 x 128 tiles of 8 waves (each wave 64 x 64 = 2 x 2 MFMA
+// tiles), 64-deep K steps in a 3-stage ring -- the fastest of the round-5 sweep
+// (256 x 128 / 256 x 256 / 128 x 128 tiles, 32-deep steps in 4-6 stages) on every
+// step shape.
 template <bool BNC, typename OT>
 hipError_t launch(const MgArgs& a0, hipStream_t s) {
-  static const int force = [] {
-    const char* e = getenv("GRK_MGEMM_CFG");
-    return e ? atoi(e) : 0;
-  }();
   MgArgs a = a0;
-  a.slices = 1;
-  a.kchunk = a.K;
-  a.slice_stride = 0;
-  a.dbpart = nullptr;
-  int cfg = force;
-  if (cfg < 1 || cfg > 5) cfg = 1;   // 64-deep steps: the fastest measured on every step shape (round 5)
-  const int bm = cfg == 4 ? 128 : 256, bn = (cfg == 3 || cfg == 5) ? 256 : 128;
-  a.tiles_n = (a.N + bn - 1) / bn;
-  a.total = ((a.M + bm - 1) / bm) * a.tiles_n;
-  const unsigned g = (unsigned)a.total;
-  switch (cfg) {
-    case 1: k_mgemm<256, 128, 4, 2, 3, BNC, 64, OT><<<g, 512, 0, s>>>(a); break;
-    case 3: k_mgemm<256, 256, 4, 4, 5, BNC, 32, OT><<<g, 1024, 0, s>>>(a); break;
-    case 5: k_mgemm<256, 256, 2, 4, 5, BNC, 32, OT><<<g, 512, 0, s>>>(a); break;
-    case 4: k_mgemm<128, 128, 2, 2, 4, BNC, 32, OT><<<g, 256, 0, s>>>(a); break;
-    default: k_mgemm<256, 128, 4, 2, 6, BNC, 32, OT><<<g, 512, 0, s>>>(a); break;
-  }
+  a.tiles_n = (a.N + 127) / 128;
+  a.total = ((a.M + 255) / 256) * a.tiles_n;
+  k_mgemm<256, 128, 4, 2, 3, BNC, 64, OT><<<(unsigned)a.total, 512, 0, s>>>(a);
   return hipGetLastError();
 }
 
 }  // namespace
-
-// Weight gradient on the same kernel (grk_wgrad.hip): part[s] = dY[ks]^T X[ks] for the K
-// slices ks of kchunk rows (K and kchunk multiples of 32), db partials from the dY
-// fragments; 256 x 128 tiles of 8 waves, 6-stage ring of 32-row steps; both operands
-// K-major (the tokens' rows), read with ds_read_b64_tr_b16.
-int mgemm_wgrad(const bf16_t* dy, int64_t ld_dy, const bf16_t* x, int64_t ld_x, int K, int M, int N, int S, int kchunk,
-                float* part, float* dbpart, hipStream_t s) {
-  MgArgs a{};
-  a.a = dy;
-  a.lda = ld_dy;
-  a.b = x;
-  a.ldb = ld_x;
-  a.c = part;
-  a.ldc = N;
-  a.M = M;
-  a.N = N;
-  a.K = K;
-  a.tiles_n = (N + 127) / 128;
-  a.slices = S;
-  a.kchunk = kchunk;
-  a.slice_stride = (int64_t)M * N;
-  a.dbpart = dbpart;
-  a.total = ((M + 255) / 256) * a.tiles_n * S;
-  k_mgemm<256, 128, 4, 2, 6, true, 32, float, true><<<(unsigned)a.total, 512, 0, s>>>(a);
-  GRK_LAUNCH_CHECK();
-  return GRK_OK;
-}
 
 }  // namespace grk
 

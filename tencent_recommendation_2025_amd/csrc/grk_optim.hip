@@ -568,15 +568,12 @@ static int table_adamw_catchup(void* param, int param_dtype, float* exp_avg, flo
   GRK_CHECK_ARG(ring_len > 0 && t >= 0, "ring_len must be > 0 and t >= 0");
   GRK_CHECK_ARG((waves + 3) / 4 < (int64_t)1 << 31, "too many rows for one launch");
   unsigned g = (unsigned)((waves + 3) / 4);
-  // GRK_SLICE_WGS (rolling slice only): at most that many workgroups, walking the
-  // slice's rows grid-stride -- the slice then holds a bounded share of the CUs while it
-  // runs beside the step on its side stream, instead of flooding every CU at launch
-  // (512 = two per CU, measured best: 3.99 vs 4.04 ms/step with the full grid, 4.11 at 256)
-  static const int slice_wgs = [] {
-    const char* e = getenv("GRK_SLICE_WGS");
-    return e ? atoi(e) : 512;
-  }();
-  if (!ids && num_slices > 1 && slice_wgs > 0 && g > (unsigned)slice_wgs) g = (unsigned)slice_wgs;
+  // rolling slice: at most kSliceWgs workgroups, walking the slice's rows grid-stride --
+  // the slice then holds a bounded share of the CUs while it runs beside the step on its
+  // side stream, instead of flooding every CU at launch (512 = two per CU, measured best:
+  // 3.99 vs 4.04 ms/step with the full grid, 4.11 at 256)
+  constexpr unsigned kSliceWgs = 512;
+  if (!ids && num_slices > 1 && g > kSliceWgs) g = kSliceWgs;
   hipStream_t s = (hipStream_t)stream;
   const bool v8 = dim % 8 == 0;
 #define GRK_CU(P, NV) k_adamw_catchup<P, NV><<<g, 256, 0, s>>>((P*)param, exp_avg, exp_avg_sq, num_rows, dim, last, \

@@ -369,65 +369,37 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(const float* __restrict__ 
     }
 }
 
-// K slices: about two workgroups per CU (latency hiding), slices of >= kSliceRows rows
-// (GRK_WGRAD_SLICE; 512 by default).
-int slice_rows() {
-  static const int v = [] {
-    const char* e = getenv("GRK_WGRAD_SLICE");
-    return e ? std::max(32, atoi(e)) : 512;
-  }();
-  return v;
-}
+// K slices: about two workgroups per CU (latency hiding), slices of >= kSliceRows rows.
+// Measured (round 5): 256- and 128-row slices slower than 512.
+constexpr int kSliceRows = 512;
 int wgrad_splits(int64_t K, int64_t M, int64_t N) {
   const int64_t tiles = ((M + kWgTile - 1) / kWgTile) * ((N + kWgTile - 1) / kWgTile);
   int S = 1;
-  while (S < 64 && tiles * S < 512 && K >= (int64_t)S * 2 * slice_rows()) S *= 2;
+  while (S < 64 && tiles * S < 512 && K >= (int64_t)S * 2 * kSliceRows) S *= 2;
   return S;
 }
 
 // Kernel plan of a shape: which ring (kind 0: the register-staged kernel, K not a
 // multiple of 32; 1: 128 x 128 tiles, two workgroups per CU; 2: 256 x 128 tiles, one
-// 8-wave workgroup per CU, for M >= 1024 -- the uvqk weight gradients; 3: grk_mgemm's
-// K-major mode, the default since round 5: 256 x 128 tiles of 8 waves, a 6-stage ring,
-// the slices of one K range on one XCD -- opt-in, GRK_WGRAD_MGEMM=1), the tile and the
-// K split.  GRK_WGRAD_RING=1 / 2 forces a ring where it applies (A/B builds).
+// 8-wave workgroup per CU, for M >= 1024 -- the uvqk weight gradients), the tile and
+// the K split.  grk_mgemm's K-major split-K mode was measured slower (round 5) and removed.
 struct WgPlan {
   int kind, tm, tn, S;
 };
 WgPlan wgrad_plan(int64_t K, int64_t M, int64_t N) {
-  static const int force = [] {
-    const char* e = getenv("GRK_WGRAD_RING");
-    return e ? atoi(e) : -1;
-  }();
-  static const bool force_reg = getenv("GRK_WGRAD_REG") != nullptr;
-  static const bool mgemm = [] {   // opt-in: measured no faster (round 5)
-    const char* e = getenv("GRK_WGRAD_MGEMM");
-    return e && atoi(e) == 1;
-  }();
   WgPlan p{0, kWgTile, kWgTile, wgrad_splits(K, M, N)};
-  if (K % kWgK || force_reg) return p;
-  if (mgemm && force < 0) {
-    // one workgroup per CU: slices until the launch has >= 256 workgroups, >= 256 rows each
-    p = WgPlan{3, 256, 128, 1};
-    const int64_t tiles = ((M + 255) / 256) * ((N + 127) / 128);
-    while (p.S < 64 && tiles * p.S < 256 && K >= (int64_t)p.S * 2 * 256) p.S *= 2;
-    return p;
-  }
-  const bool big = force == 2 || (force != 1 && M >= 1024);
-  if (!big) {
+  if (K % kWgK) return p;
+  if (M < 1024) {
     p.kind = 1;
     return p;
   }
   p = WgPlan{2, 256, 128, 1};
   const int64_t tiles = ((M + 255) / 256) * ((N + 127) / 128);
-  while (p.S < 64 && tiles * p.S < 256 && K >= (int64_t)p.S * 2 * slice_rows()) p.S *= 2;   // one workgroup per CU
+  while (p.S < 64 && tiles * p.S < 256 && K >= (int64_t)p.S * 2 * kSliceRows) p.S *= 2;   // one workgroup per CU
   return p;
 }
 
 }  // namespace
-
-int mgemm_wgrad(const bf16_t* dy, int64_t ld_dy, const bf16_t* x, int64_t ld_x, int K, int M, int N, int S, int kchunk,
-                float* part, float* dbpart, hipStream_t s);   // grk_mgemm.hip
 
 }  // namespace grk
 
@@ -467,10 +439,7 @@ extern "C" int grk_wgrad(const void* dy, int64_t ld_dy, const void* x, int64_t l
     if (db) KERN<true><<<grid, THREADS, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, dbp); \
     else KERN<false><<<grid, THREADS, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, nullptr); \
   } while (0)
-  if (pl.kind == 3) {
-    const int rc = mgemm_wgrad(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, S, kchunk, part, db ? dbp : nullptr, s);
-    if (rc) return rc;
-  } else if (pl.kind == 2) {
+  if (pl.kind == 2) {
     if (db) k_wgrad_lds<true, 4, 2, 6><<<grid, 512, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, dbp);
     else k_wgrad_lds<false, 4, 2, 6><<<grid, 512, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part,
                                                           nullptr);

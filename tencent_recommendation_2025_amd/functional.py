@@ -259,7 +259,6 @@ def feature_lookup(specs, num_tokens, out_ld, token_type=None, seq_len=0, extras
     buffer, returned as a single tensor).  Drop-in tables get dense gradients
     through autograd; grouped tables push row-sparse gradient sources into
     their group's sink."""
-    _wait_table_barrier()   # rows a side-stream catch-up is bringing up to date
     if token_type is not None:
         token_type = token_type.to(torch.int32).contiguous()
     single = splits is None
@@ -322,78 +321,37 @@ def _lookup_groups(specs, token_type, seq_len, num_tokens, out_ld, extras, split
     return _FeatureLookupFn.apply(specs, token_type, seq_len, num_tokens, out_ld, extras, splits, *weights)
 
 
-# Weight gradients of leaf weights on a side stream (opt-in: GRK_WGRAD_SIDE=1).  In a
-# layer's backward the dX GEMM, the norm / attention backward and the previous layer
-# depend on each other in a chain, while dW = dY^T X of a leaf weight feeds only the
-# optimizer: issued on a private stream (a parallel branch of the captured step), the
-# split-K wgrad -- MFMA-bound -- runs under the latency-bound attention backward
-# instead of after it.  join_side_work() puts the current stream behind it; the trainer
-# calls it right after backward (inside the captured region), the optimizers before
-# they read a gradient.  Only leaf weights without a gradient yet take the side stream
-# (AccumulateGrad then stores the tensor, no kernel reads it before the join).
-# Off by default: measured ~1 % on the C2 step (the wgrad and the attention backward
-# slow each other), and at the C5 shape the graph-replayed step then differed from
-# the eager one run to run (tests/test_gpu_fp8.py graph == eager, bisected in
-# gpurun r5i) -- a cross-stream read of a gradient before the join that eager issue
-# timing hides; not root-caused.
-WGRAD_SIDE = os.environ.get('GRK_WGRAD_SIDE', '0') == '1'
-_SIDE_STREAM_INDEX = 6
+# Side-stream branches of the step (the deferred tables' rolling flush slice,
+# optim.begin_step): run_on_side forks them from the current stream, join_side_work
+# puts the current stream behind them.  Weight gradients on a side stream were tried
+# and removed (round 6): the captured C5 step then differed from the eager one
+# (DESIGN.md §3f).
 _SIDE_PENDING = {}
-# events the next table gather (feature_lookup) makes the current stream wait for:
-# the deferred tables' batch-row catch-up runs on a side stream (optim.begin_step)
-# under the step's first kernels, and only the gathers need its rows
-_TABLE_BARRIER = []
 
 
-def table_barrier(event):
-    """The next feature_lookup (or join_side_work) waits for ``event`` first."""
-    _TABLE_BARRIER.append(event)
-
-
-def _wait_table_barrier():
-    while _TABLE_BARRIER:
-        torch.cuda.current_stream().wait_event(_TABLE_BARRIER.pop())
-
-
-def join_side_work():
-    """The current stream waits for every weight gradient issued on the side stream."""
-    _wait_table_barrier()
+def join_side_work(index=None):
+    """The current stream waits for the pending side-stream work (every private
+    stream, or only private stream ``index``)."""
     if not _SIDE_PENDING:
         return
-    for (idx, _), side in list(_SIDE_PENDING.items()):
-        torch.cuda.current_stream(idx).wait_stream(side)
-    _SIDE_PENDING.clear()
+    for key, side in list(_SIDE_PENDING.items()):
+        if index is None or key[1] == index:
+            torch.cuda.current_stream(key[0]).wait_stream(side)
+            del _SIDE_PENDING[key]
 
 
-def run_on_side(fn, device, index, priority=None):
-    """fn() on private stream ``index`` of ``device`` (created with ``priority`` on first
-    use), forked from the current stream; joined by the next join_side_work().  fn's
-    tensors must be kept alive by the caller (or record_stream'd) until then."""
+def run_on_side(fn, device, index):
+    """fn() on private stream ``index`` of ``device``, forked from the current stream;
+    joined by the next join_side_work().  fn's tensors must be kept alive by the
+    caller (or record_stream'd) until then."""
     from .streams import private_stream
     dev = torch.device(device)
     cur = torch.cuda.current_stream(dev)
-    side = private_stream(dev, index, priority)
+    side = private_stream(dev, index)
     side.wait_stream(cur)
     with torch.cuda.stream(side):
         fn()
     _SIDE_PENDING[(dev.index if dev.index is not None else torch.cuda.current_device(), index)] = side
-
-
-def _wgrad_side(g2, x2, out_dtype, want_db):
-    from .streams import private_stream
-    dev = g2.device
-    cur = torch.cuda.current_stream(dev)
-    side = private_stream(dev, _SIDE_STREAM_INDEX)
-    side.wait_stream(cur)
-    with torch.cuda.stream(side):
-        dw, db = K.wgrad(g2, x2, out_dtype=out_dtype, want_db=want_db)
-    g2.record_stream(side)   # read there: not reused by the current stream before it is done
-    x2.record_stream(side)
-    dw.record_stream(cur)    # allocated there, read here (after the join)
-    if db is not None:
-        db.record_stream(cur)
-    _SIDE_PENDING[(dev.index if dev.index is not None else torch.cuda.current_device(), _SIDE_STREAM_INDEX)] = side
-    return dw, db
 
 
 class _LinearFn(torch.autograd.Function):
@@ -433,9 +391,6 @@ class _LinearFn(torch.autograd.Function):
                    beta=0.0 if addend is None and out is None else 1.0, relu=relu)
         ctx.save_for_backward(x2, wb, y if relu else None)
         ctx.meta = (shp, weight.dtype, None if bias is None else bias.dtype, ctx.needs_input_grad[3])
-        # a leaf weight (and bias) whose gradients nothing but AccumulateGrad consumes
-        ctx.side = WGRAD_SIDE and weight.is_cuda and weight.is_leaf and (bias is None or bias.is_leaf)
-        ctx.leaves = (weight, bias) if ctx.side else None
         return y.view(*shp[:-1], wb.shape[0])
 
     @staticmethod
@@ -452,11 +407,7 @@ class _LinearFn(torch.autograd.Function):
         dx = K.gemm(g2, wb).view(shp) if ctx.needs_input_grad[0] else None
         dw_dt = torch.float32 if wdt == torch.float32 else torch.bfloat16
         dw = db = None
-        side = ctx.side and all(t is None or t.grad is None for t in ctx.leaves) \
-            and (bdt is None or bdt == torch.float32 or not ctx.needs_input_grad[2])
-        if ctx.needs_input_grad[1] and K.wgrad_ok(g2, x2) and side:
-            dw, db = _wgrad_side(g2, x2, dw_dt, ctx.needs_input_grad[2])
-        elif ctx.needs_input_grad[1] and K.wgrad_ok(g2, x2):
+        if ctx.needs_input_grad[1] and K.wgrad_ok(g2, x2):
             # split-K MFMA weight gradient, bias gradient from the same pass over gy
             dw, db = K.wgrad(g2, x2, out_dtype=dw_dt, want_db=ctx.needs_input_grad[2])
             db = db.to(bdt) if db is not None else None
@@ -490,64 +441,8 @@ def _zero_block(rows, cols, dtype, device):
     return t
 
 
-# the dnn-weight composition on grk_dnn_weight_fwd / _bwd: opt-in -- one thread per output
-# with the K = 512 sums of the mm / bias columns as serial global-load loops ran the step
-# 4.30-4.37 ms vs 3.95-4.02 with the torch composition (hipBLASLt for the two products),
-# same box
-DNNW_KERNEL = os.environ.get('GRK_DNNW_KERNEL', '0') == '1'
-
-
 class _DnnWeightFn(torch.autograd.Function):
-    """The composed itemdnn / userdnn weight of the projection restatement
-    (model._dnn_weight): [d, width] = [blocks... | W_k Wt (mm features, the
-    emb_transform folded in) | b + sum_k W_k b_t | 0], in `dtype`.
-
-    One grk_dnn_weight_fwd launch forward (every column, the K = kk products of the
-    mm columns summed in k order in fp32); backward one grk_dnn_weight_bwd call (two
-    launches): g in fp32 (the blocks' and the bias's gradients are its columns), and
-    per mm feature dW_k = dM [W_t | b_t]^T, [dW_t | db_t] = W_k^T dM with dM = [g(mm
-    columns) | g(bias column)].  The eager composition -- a cat, a GEMM and an add per
-    mm feature, a cat of every block and a cast forward, a cast, a cat and two GEMMs
-    back -- ran ~12 launches of a few microseconds each per step."""
-
-    @staticmethod
-    def forward(ctx, nblocks, nmm, width, dtype, *ts):
-        blocks, bias = ts[:nblocks], ts[nblocks]
-        mms = [ts[nblocks + 1 + 3 * i: nblocks + 4 + 3 * i] for i in range(nmm)]
-        cols, c = [], 0
-        for blk in blocks:
-            cols.append((blk.detach(), c))
-            c += blk.shape[1]
-        mm_args = []
-        for Wk, Wt, bt in mms:
-            mm_args.append((Wk.detach(), Wt.detach(), bt.detach(), c))
-            c += Wt.shape[1]
-        if c >= width:
-            raise ValueError(f'dnn_weight: {c + 1} columns do not fit width {width}')
-        out = K.dnn_weight_fwd(cols, mm_args, bias.detach().float(), width, c, dtype)
-        ctx.save_for_backward(*[t for m in mm_args for t in m[:3]])
-        ctx.meta = (nblocks, nmm, [b.shape[1] for b in blocks], [m[3] for m in mm_args], c,
-                    [b.dtype for b in blocks], bias.dtype)
-        return out
-
-    @staticmethod
-    def backward(ctx, g):
-        nblocks, nmm, bw, mm_cols, bias_col, bdt, biasdt = ctx.meta
-        saved = ctx.saved_tensors
-        mm_args = [(saved[3 * i], saved[3 * i + 1], saved[3 * i + 2], mm_cols[i]) for i in range(nmm)]
-        g32, dwks, dwts, dbts = K.dnn_weight_bwd(g, mm_args, bias_col)
-        grads, c = [], 0
-        for w, dt in zip(bw, bdt):
-            grads.append(g32[:, c:c + w].to(dt))
-            c += w
-        mm_grads = []
-        for dWk, dWt, dbt in zip(dwks, dwts, dbts):
-            mm_grads += [dWk, dWt, dbt]
-        return (None, None, None, None, *grads, g32[:, bias_col].to(biasdt), *mm_grads)
-
-
-class _DnnWeightTorchFn(torch.autograd.Function):
-    """(A/B, GRK_DNNW_KERNEL=0) _DnnWeightFn in torch ops (round 4): the composed
+    """The composed
     itemdnn / userdnn weight of the projection restatement
     (model._dnn_weight): [d, width] = [blocks... | W_k [W_t | b_t] (mm features,
     the emb_transform folded in) | b + sum_k W_k b_t | 0], cast once to `dtype`.
@@ -557,7 +452,8 @@ class _DnnWeightTorchFn(torch.autograd.Function):
     two mm per mm feature -- where autograd of the eager composition (cats,
     pads, slices, their zero-filled backwards, autocast casts) ran ~25 kernels
     for C2's two dnn weights.  fp32 arithmetic throughout (the eager form ran
-    the W_k [W_t | b_t] product under bf16 autocast)."""
+    the W_k [W_t | b_t] product under bf16 autocast).  A one-launch HIP form of
+    this node was measured slower and removed."""
 
     @staticmethod
     def forward(ctx, nblocks, nmm, width, dtype, *ts):
@@ -615,8 +511,7 @@ def dnn_weight(blocks, bias, mms, width, dtype):
     """model._dnn_weight as one autograd node (_DnnWeightFn): blocks = the weight's
     column blocks taken as they are, mms = [(W_k, emb_transform weight, bias)]."""
     flat = [t for m in mms for t in m]
-    fn = _DnnWeightFn if DNNW_KERNEL else _DnnWeightTorchFn
-    return fn.apply(len(blocks), len(mms), int(width), dtype, *blocks, bias, *flat)
+    return _DnnWeightFn.apply(len(blocks), len(mms), int(width), dtype, *blocks, bias, *flat)
 
 
 class _SplitPairFn(torch.autograd.Function):

@@ -281,14 +281,17 @@ def prepare_table_adamw_ranges(param, exp_avg, exp_avg_sq, clock, ranges, shadow
     args = (param.data_ptr(), L.dtype_code(param.dtype), exp_avg.data_ptr(), exp_avg_sq.data_ptr(), rows, D, arr,
             len(rs), clock.ring.data_ptr(), clock.ring_len, clock.t.data_ptr(),
             None if shadow is None else shadow.data_ptr())
+    # the gradients are not kept: a caller reusing the call checks that its gradients
+    # still live at these addresses (optim.DenseFlat's key), and holding them would keep
+    # a whole extra set of dense gradients alive between eager steps
     return PreparedCall('grk_table_adamw_ranges_dev', args, param.device,
-                        (param, exp_avg, exp_avg_sq, clock.ring, clock.t, shadow, [g for _, g in rs]))
+                        (param, exp_avg, exp_avg_sq, clock.ring, clock.t, shadow))
 
 
 @dataclass
 class PreparedCall:
     """A grk entry point and its arguments but the stream (appended at launch);
-    ``keep`` holds the tensors the pointers refer to."""
+    ``keep`` holds the long-lived tensors the pointers refer to."""
     name: str
     args: tuple
     device: torch.device
@@ -616,64 +619,7 @@ def batch_row_ids(seq, pos, neg, token_type, with_user=True):
     return item, user
 
 
-def _dnnw_mms(mms):
-    """ctypes GrkDnnwMm array of [(W_k [d, kk] fp32 (row stride), Wt [kk, w] fp32, bt [kk] fp32, col)]."""
-    arr = (L.GrkDnnwMm * max(1, len(mms)))()
-    for f, (wk, wt, bt, col) in enumerate(mms):
-        for t in (wk, wt, bt):
-            if t.dtype != torch.float32 or t.stride(-1) != 1:
-                raise L.GrkError(f'dnn_weight mm {f}: fp32 tensors with unit column stride required')
-        if wk.shape[1] != wt.shape[0] or bt.numel() != wt.shape[0]:
-            raise L.GrkError(f'dnn_weight mm {f}: W_k {tuple(wk.shape)}, Wt {tuple(wt.shape)}, bt {tuple(bt.shape)}')
-        arr[f] = L.GrkDnnwMm(wk.data_ptr(), wk.stride(0), wt.data_ptr(), wt.stride(0), bt.data_ptr(),
-                             wt.shape[0], wt.shape[1], int(col))
-    return arr
-
-
-def dnn_weight_fwd(blocks, mms, bias, width, bias_col, out_dtype):
-    """[d, width] composed dnn weight (grk_dnn_weight_fwd): blocks = [(B [d, w] fp32 / bf16,
-    col)], mms = [(W_k, Wt, bt, col)], bias [d] fp32 at bias_col, zeros elsewhere."""
-    _require_cuda(bias, *[b for b, _ in blocks], *[t for m in mms for t in m[:3]])
-    d = bias.shape[0]
-    out = torch.empty(d, width, dtype=out_dtype, device=bias.device)
-    arr = (L.GrkDnnwBlock * max(1, len(blocks)))()
-    for j, (b, col) in enumerate(blocks):
-        if b.stride(-1) != 1 or b.shape[0] != d:
-            raise L.GrkError(f'dnn_weight block {j}: [{d}, w] with unit column stride required')
-        arr[j] = L.GrkDnnwBlock(b.data_ptr(), b.stride(0), L.dtype_code(b.dtype), int(col), b.shape[1])
-    L.check(L.lib().grk_dnn_weight_fwd(arr, len(blocks), _dnnw_mms(mms), len(mms), bias.contiguous().data_ptr(), d,
-                                       width, bias_col, out.data_ptr(), L.dtype_code(out_dtype),
-                                       L.stream_ptr(bias.device)), 'grk_dnn_weight_fwd')
-    return out
-
-
-def dnn_weight_bwd(g, mms, bias_col):
-    """(g32 [d, width] fp32, [dW_k], [dWt], [dbt]) of grk_dnn_weight_bwd for g [d, width]."""
-    _require_cuda(g, *[t for m in mms for t in m[:3]])
-    if g.stride(-1) != 1:
-        g = g.contiguous()
-    d, width = g.shape
-    g32 = torch.empty(d, width, dtype=torch.float32, device=g.device)
-    nk = sum(d * m[1].shape[0] for m in mms)
-    nt = sum(m[1].shape[0] * (m[1].shape[1] + 1) for m in mms)
-    dwk = torch.empty(max(nk, 1), dtype=torch.float32, device=g.device)
-    det = torch.empty(max(nt, 1), dtype=torch.float32, device=g.device)
-    L.check(L.lib().grk_dnn_weight_bwd(g.data_ptr(), L.dtype_code(g.dtype), g.stride(0), _dnnw_mms(mms), len(mms), d,
-                                       width, bias_col, g32.data_ptr(), dwk.data_ptr(), det.data_ptr(),
-                                       L.stream_ptr(g.device)), 'grk_dnn_weight_bwd')
-    dwks, dwts, dbts, ok, ot = [], [], [], 0, 0
-    for wk, wt, bt, _ in mms:
-        kk, w = wt.shape
-        dwks.append(dwk[ok:ok + d * kk].view(d, kk))
-        e = det[ot:ot + kk * (w + 1)].view(kk, w + 1)
-        dwts.append(e[:, :w])
-        dbts.append(e[:, w])
-        ok += d * kk
-        ot += kk * (w + 1)
-    return g32, dwks, dwts, dbts
-
-
-MAX_ROW_COPIES = int(os.environ.get('GRK_MAX_ROW_COPIES', '64'))   # kMaxRowCopies (csrc/grk_jagged.hip); A/B builds: 48
+MAX_ROW_COPIES = 64   # kMaxRowCopies (csrc/grk_jagged.hip)
 
 
 def gather_rows(pairs, row_map):

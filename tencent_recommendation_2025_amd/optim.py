@@ -129,15 +129,11 @@ DEFAULT_GROUPS = (('item', ('item_emb',)), ('user', ('user_emb',)), ('pos', ('po
 
 
 # The rolling flush's per-step slice on a side stream (GRK_SLICE_SIDE=0: in line).
+# Measured alternatives, not kept: the slice forked at the backward
+# instead of the forward, a lower stream priority for it, the batch rows' catch-up on
+# the same side stream.
 SLICE_SIDE = os.environ.get('GRK_SLICE_SIDE', '1') != '0'
 SLICE_SIDE_STREAM = 7
-# its stream's HIP priority (GRK_SLICE_PRIORITY; 0 = default; positive = less urgent,
-# clamped into the device's range): the main chain's kernels first, the replay in the gaps
-SLICE_SIDE_PRIORITY = int(os.environ.get('GRK_SLICE_PRIORITY', '0'))
-SLICE_AT = os.environ.get('GRK_SLICE_AT', 'forward')   # 'forward' | 'backward' (see begin_step)
-# batch-row catch-up on the slice's stream, the first table gather waiting for it: opt-in
-# (same-box A/B 4.058 vs 4.028 ms/step on the main stream)
-CATCHUP_SIDE = os.environ.get('GRK_CATCHUP_SIDE', '0') == '1'
 
 DENSE_FLAT_DIM = 8   # the flat buffer as [rows, 8] for k_adamw_ranges (16-byte fp32 pairs per lane)
 
@@ -488,49 +484,22 @@ class FusedAdamW:
         # no gradient (nn.Embedding padding_idx), and a g = 0 step maps a zero
         # (p, m, v) row to exactly zero, so reading it early changes nothing.
         side = self.rolling and SLICE_SIDE and not self.l2_emb and self.clock.ring.is_cuda
-
-        def catchups():
-            item, user = K.batch_row_ids(*batch[:4], with_user='user' in self._deferred)
-            ids = {'item': item, 'user': user}
-            for name, g in self._deferred.items():
-                if self.rolling and not side:   # this step's slice of every row
-                    K.table_adamw_catchup_slice(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self.clock, self._period)
-                K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock, ids[name])
-
-        if side and CATCHUP_SIDE:
-            # the batch rows' catch-up on the slice's side stream (the slice follows it
-            # there: both claim rows through the step stamps), under the step's first
-            # kernels (jagged layout, batch compaction, feature projections); the first
-            # table gather waits for it (functional.table_barrier)
-            def forked():
-                catchups()
-                ev = torch.cuda.Event()
-                ev.record()
-                G.table_barrier(ev)
-            G.run_on_side(forked, self.clock.ring.device, SLICE_SIDE_STREAM, SLICE_SIDE_PRIORITY)
-        else:
-            catchups()
+        item, user = K.batch_row_ids(*batch[:4], with_user='user' in self._deferred)
+        ids = {'item': item, 'user': user}
+        for name, g in self._deferred.items():
+            if self.rolling and not side:   # this step's slice of every row
+                K.table_adamw_catchup_slice(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self.clock, self._period)
+            K.table_adamw_catchup(g.flat, g.exp_avg, g.exp_avg_sq, g.last, None, self.clock, ids[name])
         if side:
             # the slice after the batch rows (which it then skips: their step stamps are
             # current) on a side stream: VALU-bound replay under the step's GEMMs and
             # attention; no kernel of the step reads or writes the rows it touches (the
-            # gathers read batch rows only), joined before step() updates any row.
-            # GRK_SLICE_AT=backward: forked when the trainer starts the backward
-            # (side_work()), beside the latency-bound attention backward instead of the
-            # forward's gathers
+            # gathers read batch rows only), joined before step() updates any row
             def slices():
                 for g in self._deferred.values():
                     K.table_adamw_catchup_slice(g.flat, g.exp_avg, g.exp_avg_sq, g.last, self.clock, self._period)
-            self._side_pending = slices
-            if SLICE_AT != 'backward':
-                self.side_work()
+            G.run_on_side(slices, self.clock.ring.device, SLICE_SIDE_STREAM)
         self._begun = self.t
-
-    def side_work(self):
-        """Fork the pending flush slice onto its side stream (Trainer: before backward)."""
-        fn, self._side_pending = getattr(self, '_side_pending', None), None
-        if fn is not None:
-            G.run_on_side(fn, self.clock.ring.device, SLICE_SIDE_STREAM, SLICE_SIDE_PRIORITY)
 
     @torch.no_grad()
     def l2_term(self):
@@ -562,8 +531,7 @@ class FusedAdamW:
 
     @torch.no_grad()
     def step(self):
-        self.side_work()     # a slice no trainer forked yet: fork it now (joined right below)
-        G.join_side_work()   # weight gradients still being written on the side stream
+        G.join_side_work()   # the flush slice still running on its side stream
         self.maybe_segment()
         if self._deferred and self._begun != self.t:  # no begin_step: every row to step t, then dense
             self.flush()

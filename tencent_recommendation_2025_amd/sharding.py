@@ -29,6 +29,7 @@ the gradient reductions are the grk kernels.
 from __future__ import annotations
 
 import dataclasses
+import os
 
 import torch
 import torch.distributed as dist
@@ -38,7 +39,12 @@ from . import functional as G
 from . import kernels as K
 from . import streams as S
 from .streams import host_lap
-from .optim import SLICE_SIDE, SLICE_SIDE_PRIORITY, SLICE_SIDE_STREAM, FusedAdamW, TableGroup
+from .optim import SLICE_SIDE, SLICE_SIDE_STREAM, FusedAdamW, TableGroup
+
+
+# GRK_ROUTE=torch: device ids take the sort-based torch route (_route_torch) instead of
+# grk_route, so a multi-GPU run can A/B the two (grk_route is the default since round 5)
+ROUTE_TORCH = os.environ.get('GRK_ROUTE', 'grk') == 'torch'
 
 
 # ----------------------------------------------------------- device work ----
@@ -137,7 +143,7 @@ class ShardExchange:
         pg: communicator for the counts exchange (default: the table's).  Device ids:
         grk_route (K.route: a presence bitmap, five launches); host ids: the
         sort-based restatement below (_route_torch), the same plan."""
-        if ids.is_cuda:
+        if ids.is_cuda and not ROUTE_TORCH:
             rows_per_owner = -(-self.global_rows // self.world)
             r = K.route(ids, self.world, max(rows_per_owner, 1), self.global_rows)
             recv_counts = torch.empty_like(r['send_counts'])
@@ -279,7 +285,6 @@ class GradBuckets:
     def _launch(self, b):
         """Bucket b's gradients into its flat buffer (device: one grk_flat_pack launch;
         host: one cat), then its all-reduce."""
-        G.join_side_work()   # weight gradients issued on the side stream (functional.WGRAD_SIDE)
         flat = self.flat[b]
         if flat.is_cuda and all(p.grad is None or p.grad.data_ptr() < flat.data_ptr()
                                 or p.grad.data_ptr() >= flat.data_ptr() + flat.numel() * 4
@@ -564,7 +569,7 @@ class ShardedFusedAdamW(FusedAdamW):
                 for grp, _ in self.shards.values():
                     K.table_adamw_catchup_slice(grp.flat, grp.exp_avg, grp.exp_avg_sq, grp.last, self.clock,
                                                 self._period)
-            G.run_on_side(slices, self.clock.ring.device, SLICE_SIDE_STREAM, SLICE_SIDE_PRIORITY)
+            G.run_on_side(slices, self.clock.ring.device, SLICE_SIDE_STREAM)
         self._begun = self.t
         host_lap('prepare.issue')
 

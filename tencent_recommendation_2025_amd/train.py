@@ -22,7 +22,6 @@ the device to drain before its all-to-alls."""
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 
@@ -33,16 +32,11 @@ from . import kernels as K
 from . import streams as S
 
 
-# the capture stream's HIP priority (GRK_MAIN_PRIORITY, e.g. -1 = the most urgent level):
-# side work (the flush slice) then fills the gaps the step's own chain leaves
-MAIN_PRIORITY = os.environ.get('GRK_MAIN_PRIORITY')
-
-
 def private_stream(device):
     """The process's own capture stream for ``device`` (streams.private_stream):
     never one of torch's pooled streams, which a process group may record its
     collectives' events on."""
-    return S.private_stream(device, 0, None if MAIN_PRIORITY is None else int(MAIN_PRIORITY))
+    return S.private_stream(device, 0)
 
 
 def _tensors(batch):
@@ -275,10 +269,7 @@ class Trainer:
         if hasattr(self.opt, 'begin_step'):  # deferred table updates: bring this batch's rows up to date
             self.opt.begin_step(batch)
         loss = self.compute_loss(batch)
-        if hasattr(self.opt, 'side_work'):
-            self.opt.side_work()   # the deferred tables' flush slice beside the backward (GRK_SLICE_AT)
         loss.backward()
-        G.join_side_work()   # weight gradients issued on the side stream (functional.WGRAD_SIDE)
         self.opt.step()
         if self.jagged and not torch.cuda.is_current_stream_capturing():
             self.check_jagged()   # eager: one host sync per step

@@ -371,3 +371,25 @@ def test_grk_jagged_remap_equals_torch_remap():
     assert set(got) == set(want)
     for k in want:
         assert got[k][0] is want[k][0] and torch.equal(got[k][1], want[k][1]), k
+
+
+def test_torch_route_switch_equals_grk_route(pg, monkeypatch):
+    """GRK_ROUTE=torch (sharding.ROUTE_TORCH): the sort-based torch route on device ids
+    trains bit for bit like grk_route (the same plan: owner order, ascending ids)."""
+    from tencent_recommendation_2025_amd import sharding
+    from tencent_recommendation_2025_amd import synthetic as S
+    from tencent_recommendation_2025_amd.train import Trainer
+    out = []
+    for torch_route in (False, True):
+        monkeypatch.setattr(sharding, 'ROUTE_TORCH', torch_route)
+        m, cfg = build()
+        tr = Trainer(m, sharding.ShardedFusedAdamW(m, lr=2e-3, defer_period=2), loss='bce')
+        g = torch.Generator(device=DEV).manual_seed(4)
+        losses = [float(tr.step(S.make_batch(cfg, g, DEV))) for _ in range(4)]
+        state = {k: v.detach().clone() for k, v in m.state_dict().items()
+                 if k not in ('item_emb.weight', 'user_emb.weight')}
+        state.update({k: tr.opt.shard_table(k).clone() for k in ('item_emb', 'user_emb')})
+        out.append((losses, state))
+    assert out[0][0] == out[1][0]
+    for k in out[0][1]:
+        assert torch.equal(out[0][1][k], out[1][1][k]), k
