@@ -44,6 +44,16 @@ __global__ void __launch_bounds__(256) kA(const uint4* __restrict__ table, const
   }
 }
 
+// A1: one (row, chunk) unit per lane, grid-stride, BS threads per block
+template <int BS>
+__global__ void __launch_bounds__(BS) kA1(const uint4* __restrict__ table, const int64_t* __restrict__ idx,
+                                          int64_t n, uint4* __restrict__ out) {
+  const int64_t units = n * CH;
+  const int64_t stride = (int64_t)gridDim.x * BS;
+  for (int64_t u = (int64_t)blockIdx.x * BS + threadIdx.x; u < units; u += stride)
+    out[u] = table[idx[u / CH] * CH + u % CH];
+}
+
 // B: each wave owns R consecutive output rows: one index load per lane (lane r<R
 // loads idx[r]), broadcast with readlane, then R independent 1 KiB row loads.
 template <int R, bool NT>
@@ -60,6 +70,34 @@ __global__ void __launch_bounds__(256) kB(const uint4* __restrict__ table, const
       const int64_t row = __builtin_amdgcn_readlane((int)my, r) | ((int64_t)__builtin_amdgcn_readlane((int)(my >> 32), r) << 32);
       if (r0 + r < n) v[r] = table[row * CH + lane];
     }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r0 + r >= n) continue;
+      if (NT) nt_store(v[r], out + (r0 + r) * CH + lane);
+      else out[(r0 + r) * CH + lane] = v[r];
+    }
+  }
+}
+
+// C: persistent waves (a capped grid), R rows per wave and pass; the next pass's
+// indices are loaded while the current rows are in flight
+template <int R, bool NT>
+__global__ void __launch_bounds__(256) kC(const uint4* __restrict__ table, const int64_t* __restrict__ idx,
+                                          int64_t n, uint4* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  int64_t r0 = wave * R;
+  int64_t my = lane < R && r0 + lane < n ? idx[r0 + lane] : 0;
+  for (; r0 < n; r0 += waves * R) {
+    uint4 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t row = __builtin_amdgcn_readlane((int)my, r) | ((int64_t)__builtin_amdgcn_readlane((int)(my >> 32), r) << 32);
+      if (r0 + r < n) v[r] = table[row * CH + lane];
+    }
+    const int64_t r1 = r0 + waves * R;
+    my = lane < R && r1 + lane < n ? idx[r1 + lane] : 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (r0 + r >= n) continue;
@@ -168,6 +206,37 @@ int main(int argc, char** argv) {
   run("B R=8 NT", [&] { kB<8, true><<<grid((n + 7) / 8 * 64, 1 << 20), 256>>>(table, idx, n, out); }, bytes, flush, flush_units);
   run("B R=16", [&] { kB<16, false><<<grid((n + 15) / 16 * 64, 1 << 20), 256>>>(table, idx, n, out); }, bytes, flush, flush_units);
   run("B R=4 half grid", [&] { kB<4, false><<<grid((n + 7) / 8 * 64, 1 << 20), 256>>>(table, idx, n, out); }, bytes, flush, flush_units);
+  if (argc > 3) {   // round-6 second sweep: the one-unit-per-lane form around its best grid
+    for (int cap : {2048, 4096, 6144, 8192, 12288, 16384, 1 << 20}) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "A1 256 cap %d", cap);
+      run(nm, [&] { kA1<256><<<grid(n * CH, cap), 256>>>(table, idx, n, out); }, bytes, flush, flush_units);
+    }
+    auto grid2 = [&](int64_t work, int bs, int cap) { int64_t g = (work + bs - 1) / bs; return (unsigned)(g < cap ? g : cap); };
+    for (int cap : {1024, 2048, 4096, 1 << 20}) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "A1 512 cap %d", cap);
+      run(nm, [&] { kA1<512><<<grid2(n * CH, 512, cap), 512>>>(table, idx, n, out); }, bytes, flush, flush_units);
+      snprintf(nm, sizeof nm, "A1 1024 cap %d", cap);
+      run(nm, [&] { kA1<1024><<<grid2(n * CH, 1024, cap), 1024>>>(table, idx, n, out); }, bytes, flush, flush_units);
+    }
+    run("copy (contiguous) again", [&] { kCopy<<<grid(n * CH, 8192), 256>>>(src, n * CH, out); }, bytes, flush, flush_units);
+    CK(hipDeviceSynchronize());
+    return 0;
+  }
+  for (int cap : {512, 1024, 2048, 4096}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "C R=4 grid %d", cap);
+    run(nm, [&] { kC<4, false><<<cap, 256>>>(table, idx, n, out); }, bytes, flush, flush_units);
+    snprintf(nm, sizeof nm, "C R=4 NT grid %d", cap);
+    run(nm, [&] { kC<4, true><<<cap, 256>>>(table, idx, n, out); }, bytes, flush, flush_units);
+    snprintf(nm, sizeof nm, "C R=2 grid %d", cap);
+    run(nm, [&] { kC<2, false><<<cap, 256>>>(table, idx, n, out); }, bytes, flush, flush_units);
+    snprintf(nm, sizeof nm, "C R=8 grid %d", cap);
+    run(nm, [&] { kC<8, false><<<cap, 256>>>(table, idx, n, out); }, bytes, flush, flush_units);
+  }
+  run("B R=1", [&] { kB<1, false><<<grid(n * 64, 1 << 20), 256>>>(table, idx, n, out); }, bytes, flush, flush_units);
+  run("B R=1 NT", [&] { kB<1, true><<<grid(n * 64, 1 << 20), 256>>>(table, idx, n, out); }, bytes, flush, flush_units);
   CK(hipDeviceSynchronize());
   return 0;
 }

@@ -34,6 +34,7 @@
 // Deterministic: no atomics, fixed reduction orders.
 #include "grk_common.h"
 #include "grk_mfma.h"
+#include "grk_ring.h"
 
 namespace grk {
 
@@ -53,6 +54,7 @@ struct SSParams {
   float *pm, *pl;       // [nslices, M] partial max / sum (log2 domain), compact rows
   float* diag;          // [M] z_ii in log2 units, compact rows
   float* lse2;          // [M] log2-domain logsumexp, compact rows
+  float* lsec;          // backward at D = 512: lse2 copied into the workspace ([M + kSS2Pad])
   float* partials;      // [nblocks]
   float* loss;
   const float* grad_loss;
@@ -101,6 +103,7 @@ __global__ void __launch_bounds__(256) k_ss_gather(SSParams p) {
     if (ch == 0) {
       p.idc[c] = p.ids[i];
       p.lqc[c] = p.logq ? p.logq[i] * kLog2e : 0.f;
+      if (p.lsec) p.lsec[c] = p.lse2[c];
     }
   }
 }
@@ -222,6 +225,132 @@ __global__ void __launch_bounds__(256) k_ss_fwd(SSParams p) {
   if (hh == 0 && ook) {
     p.pm[(int64_t)blockIdx.y * p.M + oc] = m;
     p.pl[(int64_t)blockIdx.y * p.M + oc] = l;
+  }
+}
+
+// Forward at D = 512 (BASELINE config 2; round 6): the E tiles stream through an
+// LDS-DMA ring instead of being staged through registers.
+//  * 8 waves x 32 compact rows of h = 256 rows per workgroup, each wave holding its
+//    rows' full-D fragments (128 VGPRs) for the whole column walk, so a staged
+//    32-row E tile serves 256 rows (the round-2 kernel: 128, behind two barriers
+//    and a register round trip per tile);
+//  * E tiles (32 rows x 1 KiB, the lds_off<512> swizzle, one global_load_lds_dwordx4
+//    per row) plus the tile's ids and log2 q (one more DMA) land in a kSS2Nst-stage
+//    ring; one barrier per tile (ring_wait);
+//  * the columns are cut into kSS2Slices slices; the slices' workgroups are dealt to
+//    the XCDs slice-major (slice s on XCD s mod 8), so an XCD streams 2/16 of E
+//    (~1.7 MB at C2) through its own 4 MiB L2 for all of its row blocks.
+// Per tile a wave runs 32 MFMAs (32 ds_read_b128 of the E image) and the online
+// logsumexp update of its 16 scores per lane -- the math of k_ss_fwd.
+// The D = 512 tile images: 32 rows of 1 KiB at a padded stride of kSS2Row = 1040 B, so
+// row r starts 4 banks after row r - 1: a fragment read (ds_read_b128, lane (r, hh)
+// reads 16 bytes of row r) spreads each group of 16 lanes over all 64 banks, and
+// every fragment of a tile is one lane base plus an immediate offset (an XOR swizzle
+// would need an address register per fragment: the backward's accumulators and own-row
+// fragments leave none).  A row lands as one contiguous 1 KiB LDS-DMA.
+constexpr int kSS2Row = 1040;
+__device__ __forceinline__ int ss_off(int row, int col) { return row * kSS2Row + col * 2; }
+__device__ __forceinline__ bf16x8 ss_row8(const char* img, int row, int col) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(img + ss_off(row, col)));
+}
+// lds_tr8's transposed fragment over the ss_off image
+__device__ __forceinline__ bf16x8 ss_tr8(const char* img, int row0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int q4 = i >> 2, pp = i & 3;
+  const int hh = g >> 1;
+  const int col = col0 + 16 * (g & 1) + 4 * pp;
+  const int ra = row0 + 4 * hh + q4;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + ss_off(ra, col)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + ss_off(ra + 8, col)));
+  bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
+  bf16x8 f;
+  f[0] = l4[0]; f[1] = l4[1]; f[2] = l4[2]; f[3] = l4[3];
+  f[4] = h4[0]; f[5] = h4[1]; f[6] = h4[2]; f[7] = h4[3];
+  return f;
+}
+
+constexpr int kSS2Rows = 256;
+constexpr int kSS2Slices = 16;
+constexpr int kSS2Nst = 4;
+constexpr int kSS2Img = 32 * kSS2Row;
+constexpr int kSS2Stage = kSS2Img + 1024;   // + the tile's ids (256 B) and log2 q (128 B)
+constexpr int kSS2Pad = 64;                 // idc / lqc rows past M the meta DMA may read
+
+template <bool LQ>
+__global__ void __launch_bounds__(512) k_ss_fwd2(SSParams p, int rblocks) {
+  constexpr int D = 512, KS = D / 16, NST = kSS2Nst, P = 5;
+  __shared__ __attribute__((aligned(16))) char smem[NST * kSS2Stage];
+  const int nv = *p.nvp;
+  const unsigned phys = blockIdx.x, xcd = phys & 7, q = phys >> 3;
+  const int slice = (int)(xcd + 8 * (q / rblocks)), rb = (int)(q % rblocks);
+  const int oc0 = rb * kSS2Rows;
+  if (oc0 >= nv) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int oc = oc0 + wave * 32 + r;
+  const bool ook = oc < nv;
+  const bool wave_live = oc0 + wave * 32 < nv;
+  const int64_t oid = ook ? p.idc[oc] : -2;
+  bf16x8 of[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) of[ks] = gload8(p.hc + (int64_t)oc * D + 16 * ks + 8 * hh, ook);
+  const int tiles = (nv + 31) / 32, per = (tiles + kSS2Slices - 1) / kSS2Slices;
+  const int tb = min(tiles, slice * per), te = min(tiles, tb + per), nt = te - tb;
+  const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane(
+      (int)((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem));
+  // this lane's DMA sources: E rows 4 wave .. 4 wave + 3 of a tile (16-byte chunk
+  // lane of each: rows land whole at the padded stride), and one 16-byte piece of the meta
+  auto issue = [&](int t, int buf) {
+    const unsigned base = lds0 + buf * kSS2Stage;
+    const int t0 = t * 32;
+    const int wu = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wu * 4 + i;
+      const int srow = min(t0 + row, nv - 1);
+      wg_dma16(p.ec + (int64_t)srow * D + 8 * lane, base + row * kSS2Row);
+    }
+    const bf16_t* meta = lane >= 16 && lane < 24 ? (const bf16_t*)(p.lqc + t0 + 4 * (lane - 16))
+                                                 : (const bf16_t*)(p.idc + t0 + 2 * (lane & 15));
+    wg_dma16(meta, base + kSS2Img);
+  };
+  for (int i = 0; i < NST - 1 && i < nt; ++i) issue(tb + i, i);
+  float m = -INFINITY, l = 0.f;
+  for (int i = 0; i < nt; ++i) {
+    ring_wait<P, NST>(nt - 1 - i);
+    if (i + NST - 1 < nt) issue(tb + i + NST - 1, (i + NST - 1) % NST);
+    if (!wave_live) continue;
+    const char* img = smem + (i % NST) * kSS2Stage;
+    const int64_t* tid = reinterpret_cast<const int64_t*>(img + kSS2Img);
+    const float* tlq = reinterpret_cast<const float*>(img + kSS2Img + 256);
+    f32x16 s = acc_zero();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) s = mfma(ss_row8(img, r, 16 * ks + 8 * hh), of[ks], s);
+    const int jb = (tb + i) * 32;
+    const bool full = jb + 32 <= nv;
+    float x[16], tmax = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int jr = acc_row(k, hh), jc = jb + jr;
+      // branch-free (the id is read whatever the other terms: no per-score branch)
+      const int64_t tj = tid[jr];
+      const bool ok = (full | (jc < nv)) & ((jc == oc) | (tj != oid));
+      x[k] = ok ? (LQ ? s[k] * p.sl2 - tlq[jr] : s[k] * p.sl2) : -INFINITY;
+      tmax = fmaxf(tmax, x[k]);
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+    const float mn = fmaxf(m, tmax);
+    if (mn == -INFINITY) continue;
+    float rs = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) rs += __builtin_amdgcn_exp2f(x[k] - mn);  // exp2(-inf) = 0
+    rs += __shfl_xor(rs, 32);
+    l = l * __builtin_amdgcn_exp2f(m - mn) + rs;
+    m = mn;
+  }
+  if (hh == 0 && ook) {
+    p.pm[(int64_t)slice * p.M + oc] = m;
+    p.pl[(int64_t)slice * p.M + oc] = l;
   }
 }
 
@@ -409,6 +538,178 @@ __global__ void __launch_bounds__(SSB<D>::NT) k_ss_bwd(SSParams p) {
           make_float4(acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]);
 }
 
+// Backward at D = 512 (round 6): k_ss_bwd's math (S recomputed per tile, G = softmax -
+// onehot as bf16 hi + lo, dH = G E / dE = G^T H) with two waves per 32 own rows, each
+// owning one half of D: a wave computes the score tile over its half (16 MFMAs), the
+// pair swaps those partial tiles through LDS (ONE hand-off per tile, double-buffered),
+// both finish the full scores and G in their own lanes (the softmax VALU twice, no G
+// hand-off), and each multiplies G into its 8 column blocks (32 MFMAs).  4 row groups x
+// 2 halves = 8 waves, 128 own rows per workgroup; the other side's 32-row tiles stream
+// through a 3-stage LDS-DMA ring (k_ss_fwd2's image + meta).  The round-2 kernel: 64
+// own rows, 4 D quarters, three hand-offs per tile, tiles staged through registers.
+// Any score of elements k0 .. k0 + 7 of lane (r, hh) whose column id matches the own
+// row's id in its low word but is not the row itself (then compared in full).
+__device__ __forceinline__ bool lo_dup(const uint32_t* tid32, uint32_t olo, uint32_t ohi, int tb, int oc, int k0,
+                                       int hh) {
+  bool any = false;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int tr = acc_row(k0 + e, hh);
+    any |= (tid32[2 * tr] == olo) & (tb + tr != oc);
+  }
+  return any;
+}
+
+constexpr int kSSBRg = 4;                       // row groups
+constexpr int kSSBRows = 32 * kSSBRg;
+constexpr int kSSBNst = 3;
+constexpr int kSSBXch = 8 * 64 * 16 * 4;        // [wave][lane][16 floats]
+
+template <int P, int NST>
+__device__ __forceinline__ void ssb_wait(int ahead) { ring_wait<P, NST>(ahead); }
+
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) k_ss_bwd2(SSParams p) {
+  constexpr int D = 512, DH = D / 2, KSQ = DH / 16, NDT = DH / 32, NST = kSSBNst;
+  __shared__ __attribute__((aligned(16))) char smem[NST * kSS2Stage + kSSBXch];
+  float4* xch = reinterpret_cast<float4*>(smem + NST * kSS2Stage);
+  const int nv = *p.nvp;
+  const int oc0 = blockIdx.x * kSSBRows;
+  if (oc0 >= nv) return;
+  const bool rows = blockIdx.y == 0;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int rg = wave >> 1, half = wave & 1;
+  const int oc = oc0 + rg * 32 + r;
+  const bool ook = oc < nv;
+  const int64_t oid = ook ? p.idc[oc] : -2;
+  const uint32_t olo = (uint32_t)oid, ohi = (uint32_t)((uint64_t)oid >> 32);
+  // exponent offset of element (row i, column j) = lse2_i + log2 q_j: the own row's part
+  // here, the tile row's part in the tile's meta (log2 q of e rows, or lse2 of h rows)
+  const float olse = ook ? (rows ? p.lsec[oc] : p.lqc[oc]) : 0.f;
+  const bf16_t* own = rows ? p.hc : p.ec;
+  const bf16_t* tsrc = rows ? p.ec : p.hc;
+  const float* tmeta = rows ? p.lqc : p.lsec;
+  const int col0 = half * DH;
+  bf16x8 of[KSQ];
+#pragma unroll
+  for (int ks = 0; ks < KSQ; ++ks) of[ks] = gload8(own + (int64_t)oc * D + col0 + 16 * ks + 8 * hh, ook);
+  const float coef = (p.grad_loss ? *p.grad_loss : 1.f) / (float)max(nv, 1) * (p.sl2 / kLog2e);
+  f32x16 acc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) acc[dt] = acc_zero();
+  const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane(
+      (int)((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem));
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
+  const int nt = (nv + 31) / 32;
+  auto issue = [&](int t, int buf) {   // 4 tile rows per wave, the meta by wave 0
+    const unsigned base = lds0 + buf * kSS2Stage;
+    const int t0 = t * 32;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wu * 4 + i;
+      const int srow = min(t0 + row, nv - 1);
+      wg_dma16(tsrc + (int64_t)srow * D + 8 * lane, base + row * kSS2Row);
+    }
+    if (wu == 0) {
+      const bf16_t* meta = lane >= 16 && lane < 24 ? (const bf16_t*)(tmeta + t0 + 4 * (lane - 16))
+                                                   : (const bf16_t*)(p.idc + t0 + 2 * (lane & 15));
+      wg_dma16(meta, base + kSS2Img);
+    }
+  };
+  for (int i = 0; i < NST - 1 && i < nt; ++i) issue(i, i);
+  for (int i = 0; i < nt; ++i) {
+    if (wu == 0) ssb_wait<5, NST>(nt - 1 - i);
+    else ssb_wait<4, NST>(nt - 1 - i);
+    if (i + NST - 1 < nt) issue(i + NST - 1, (i + NST - 1) % NST);
+    const char* img = smem + (i % NST) * kSS2Stage;
+    const int64_t* tid = reinterpret_cast<const int64_t*>(img + kSS2Img);
+    const uint32_t* tid32 = reinterpret_cast<const uint32_t*>(img + kSS2Img);
+    const float* tlse = reinterpret_cast<const float*>(img + kSS2Img + 256);
+    const int tb = i * 32;
+    f32x16 s = acc_zero();
+#pragma unroll
+    for (int ks = 0; ks < KSQ; ++ks) {
+      s = mfma(ss_row8(img, r, col0 + 16 * ks + 8 * hh), of[ks], s);
+      if ((ks & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    // swap the half-D partial scores with the partner wave (the ring's barrier of the
+    // next tile orders the buffer's reuse: every read of this tile's scores is before it)
+    float4* mine = xch + wave * 64 * 4 + lane * 4;
+    const float4* other = xch + (wave ^ 1) * 64 * 4 + lane * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) mine[q] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
+    lds_barrier();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 u = other[q];
+      // the sum in D order (half 0 + half 1) on both waves: the same bits
+      s[4 * q] = half ? u.x + s[4 * q] : s[4 * q] + u.x;
+      s[4 * q + 1] = half ? u.y + s[4 * q + 1] : s[4 * q + 1] + u.y;
+      s[4 * q + 2] = half ? u.z + s[4 * q + 2] : s[4 * q + 2] + u.z;
+      s[4 * q + 3] = half ? u.w + s[4 * q + 3] : s[4 * q + 3] + u.w;
+    }
+    const bool full = tb + 32 <= nv;
+    // per half tile (elements 8 s2 .. 8 s2 + 7 = tile rows 16 s2 ..): G as bf16 hi / lo
+    // words, then that half's 16 product MFMAs
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      uint32_t gw[4], lw[4];
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) {
+        float g2[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int k = 8 * s2 + 2 * k2 + u;
+          const int tr = acc_row(k, hh), tc = tb + tr;
+          // the same item elsewhere in the batch is masked: compared on the ids' low words
+          // here (one register per score, no branch), the rare low-word matches on the
+          // high words below
+          const bool ok = ook & (full | (tc < nv)) & ((tc == oc) | (tid32[2 * tr] != olo));
+          const float pr = __builtin_amdgcn_exp2f(fmaf(s[k], p.sl2, -(olse + tlse[tr])));
+          g2[u] = ok ? (tc == oc ? pr - 1.f : pr) * coef : 0.f;
+        }
+        split2(f32x2{g2[0], g2[1]}, gw[k2], lw[k2]);
+      }
+      if (__builtin_expect(__ballot(lo_dup(tid32, olo, ohi, tb, oc, 8 * s2, hh)) != 0, 0)) {
+        // a low-word match that is not this row itself: recompute the half tile's G with
+        // the full ids (wave-uniform branch, rare: in-batch repeats of an item)
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) {
+          float g2[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int k = 8 * s2 + 2 * k2 + u;
+            const int tr = acc_row(k, hh), tc = tb + tr;
+            const bool ok = ook & (full | (tc < nv)) & ((tc == oc) | (tid[tr] != oid));
+            const float pr = __builtin_amdgcn_exp2f(fmaf(s[k], p.sl2, -(olse + tlse[tr])));
+            g2[u] = ok ? (tc == oc ? pr - 1.f : pr) * coef : 0.f;
+          }
+          split2(f32x2{g2[0], g2[1]}, gw[k2], lw[k2]);
+        }
+      }
+      const bf16x8 gh = words8(gw), gl = words8(lw);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const bf16x8 tf = ss_tr8(img, 16 * s2, col0 + 32 * dt, lane);
+        acc[dt] = mfma(tf, gh, acc[dt]);
+        acc[dt] = mfma(tf, gl, acc[dt]);
+        // at most two column blocks' fragments in flight (registers: the 128
+        // accumulators + the 64 own-row fragments leave little else)
+        if (dt & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  if (!ook) return;
+  const int pos = p.vidx[oc];
+  float* out = rows ? p.dh + (int64_t)pos * p.lddh : p.de + (int64_t)pos * p.ldde;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4)
+      *reinterpret_cast<float4*>(out + col0 + 32 * dt + 8 * g4 + 4 * hh) =
+          make_float4(acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]);
+}
+
 // which: 0 = compaction gather + forward, 1 = compaction gather + backward
 template <int D>
 static int ss_launch(const SSParams& p, int which, hipStream_t s) {
@@ -417,9 +718,18 @@ static int ss_launch(const SSParams& p, int which, hipStream_t s) {
   if (which == 0) {
     k_ss_diag<D><<<(unsigned)((p.M + 3) / 4), 256, 0, s>>>(p);
     GRK_LAUNCH_CHECK();
-    const dim3 grid((unsigned)((p.M + kSSFwdRows - 1) / kSSFwdRows), p.nslices);
-    if (p.logq) k_ss_fwd<D, true><<<grid, 256, 0, s>>>(p);
-    else k_ss_fwd<D, false><<<grid, 256, 0, s>>>(p);
+    if constexpr (D == 512) {
+      const int rblocks = (p.M + kSS2Rows - 1) / kSS2Rows;
+      const unsigned g = (unsigned)(rblocks * kSS2Slices);
+      if (p.logq) k_ss_fwd2<true><<<g, 512, 0, s>>>(p, rblocks);
+      else k_ss_fwd2<false><<<g, 512, 0, s>>>(p, rblocks);
+    } else {
+      const dim3 grid((unsigned)((p.M + kSSFwdRows - 1) / kSSFwdRows), p.nslices);
+      if (p.logq) k_ss_fwd<D, true><<<grid, 256, 0, s>>>(p);
+      else k_ss_fwd<D, false><<<grid, 256, 0, s>>>(p);
+    }
+  } else if constexpr (D == 512) {
+    k_ss_bwd2<<<dim3((unsigned)((p.M + kSSBRows - 1) / kSSBRows), 2), 512, 0, s>>>(p);
   } else {
     k_ss_bwd<D><<<dim3((unsigned)((p.M + SSB<D>::ROWS - 1) / SSB<D>::ROWS), 2), SSB<D>::NT, 0, s>>>(p);
   }
@@ -439,7 +749,8 @@ static int ss_dispatch(const SSParams& p, int dim, int which, hipStream_t s) {
   return GRK_EUNSUPPORTED;
 }
 
-static int ss_slices(int M) {
+static int ss_slices(int M, int D) {
+  if (D == 512) return kSS2Slices;   // k_ss_fwd2
   // forward column slices: ~1k workgroups when every position is valid
   // (half of them, ~2 per CU, at C2's ~53 % valid)
   const int rb = (M + kSSFwdRows - 1) / kSSFwdRows;
@@ -454,13 +765,13 @@ struct SSWs {
   int* nv;
   bf16_t *hc, *ec;
   int64_t* idc;
-  float *lqc, *pm, *pl, *diag, *partials;
+  float *lqc, *lsec, *pm, *pl, *diag, *partials;
   size_t bytes;
 };
 
 static SSWs ss_ws(char* base, int M, int D) {
   SSWs w;
-  const int ns = ss_slices(M);
+  const int ns = ss_slices(M, D);
   const int nb = (M + 255) / 256;
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -472,8 +783,9 @@ static SSWs ss_ws(char* base, int M, int D) {
   w.nv = (int*)take(4);
   w.hc = (bf16_t*)take((size_t)M * D * 2);
   w.ec = (bf16_t*)take((size_t)M * D * 2);
-  w.idc = (int64_t*)take((size_t)M * 8);
-  w.lqc = (float*)take((size_t)M * 4);
+  w.idc = (int64_t*)take((size_t)(M + kSS2Pad) * 8);   // k_ss_fwd2's meta DMA reads whole 32-row tiles
+  w.lqc = (float*)take((size_t)(M + kSS2Pad) * 4);
+  w.lsec = (float*)take((size_t)(M + kSS2Pad) * 4);
   w.pm = (float*)take((size_t)ns * M * 4);
   w.pl = (float*)take((size_t)ns * M * 4);
   w.diag = (float*)take((size_t)M * 4);
@@ -504,7 +816,7 @@ static int ss_fill(const void* h, int64_t ldh, const void* e, int64_t lde, const
   memset(p, 0, sizeof(*p));
   p->h = (const bf16_t*)h; p->ldh = ldh; p->e = (const bf16_t*)e; p->lde = lde;
   p->ids = ids; p->logq = log_q; p->M = (int)num_rows; p->sl2 = kLog2e / tau;
-  p->nslices = ss_slices(p->M);
+  p->nslices = ss_slices(p->M, dim);
   *w = ss_ws((char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), p->M, dim);
   p->vidx = w->vidx; p->nvp = w->nv; p->hc = w->hc; p->ec = w->ec; p->idc = w->idc; p->lqc = w->lqc;
   p->pm = w->pm; p->pl = w->pl; p->diag = w->diag; p->partials = w->partials;
@@ -550,6 +862,7 @@ extern "C" int grk_sampled_softmax_bwd(const void* h, int64_t ldh, const void* e
   GRK_CHECK_ARG(lddh >= dim && ldde >= dim && lddh % 4 == 0 && ldde % 4 == 0, "lddh / ldde must be >= dim, multiple of 4");
   GRK_CHECK_ARG(((uintptr_t)dh | (uintptr_t)de) % 16 == 0, "dh / de must be 16-byte aligned");
   p.lse2 = const_cast<float*>(lse2); p.grad_loss = grad_loss;
+  if (dim == 512) p.lsec = w.lsec;   // k_ss_bwd2 stages the tile rows' lse2 by DMA from a padded copy
   p.dh = dh; p.lddh = lddh; p.de = de; p.ldde = ldde;
   hipStream_t s = (hipStream_t)stream;
   // rows of positions that are not valid stay zero

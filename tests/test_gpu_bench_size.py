@@ -1,21 +1,34 @@
-"""The benched configuration at its OWN size against the oracle.
+"""The benched configuration at its OWN size against the oracle (VERDICT r4 item 1,
+VERDICT r5 item 1: also at B = 32 and at BASELINE config 4).
 
 ``bench.py`` times BASELINE config 2: O1 + HSTU d=512 (8 heads x hd 64), 4 blocks,
 maxlen 200 (T = 201), 1M-item and 1M-user bf16 tables, the jagged (span-row)
 layout, bf16 autocast GEMMs, the grouped MFMA projections, the merged
 projected-row backward, the flat dense AdamW and the deferred dense-parity table
-AdamW.  Here exactly that model and optimizer take ONE training step at B = 8
-(dropout 0: the oracle cannot draw grk's dropout masks) and are compared with
-``oracle/model_ref.py`` -- the fp32 torch-CPU restatement of the reference step
-(``model/BaseLine/main.py:163-190``: forward, BCE, backward, ``torch.optim.AdamW``
-with betas (0.9, 0.98), weight decay 0.01) -- on the same parameters and batch:
+AdamW.  Here exactly that model and optimizer take ONE training step at B = 8 and
+B = 32 (and config 4: the same model with 3 RQ-VAE semantic-id levels as O1
+item_sparse features) with dropout 0 (the oracle cannot draw grk's dropout masks),
+and are compared with ``oracle/model_ref.py`` -- the fp32 torch-CPU restatement of
+the reference step (``model/BaseLine/main.py:163-190``: forward, BCE, backward,
+``torch.optim.AdamW`` with betas (0.9, 0.98), weight decay 0.01) -- on the same
+parameters and batch:
 
-* loss, logits, every gradient (dense parameters and each table, padding rows
-  excluded), and every parameter after the update (deferred rows flushed);
+* loss and logits against the fp32 oracle;
 * the error budget is the reference's own mixed precision: the oracle step run
   under CPU bf16 autocast (the reference's ``--use_amp``, ``main.py:139-141,173``)
   is measured against the fp32 oracle on the same inputs, and grk may not exceed
   BENCH_AMP_FACTOR x that (or a floor, stated per quantity);
+* the dnn ReLUs: a pre-activation within its own rounding error of 0 takes either
+  side of the ReLU, and each such flip moves a whole table row's gradient by the
+  flipped element's gradient -- a few dozen flips among 10^5-10^6 elements decide the
+  normwise error of the tables read by few tokens (the user-side tables at B = 8: 8
+  rows; round-6 diagnosis: scripts/diag/user_grad_trace.py).  So the forward's flip
+  COUNT is held to the AMP step's (each against the fp32 oracle's own masks), and the
+  gradients / updates are compared with the fp32 and AMP oracle steps fed grk's own
+  ReLU masks (``RefBaselineModel.relu_masks``): the smooth arithmetic error, without
+  the discontinuity;
+* every gradient (dense parameters and each table, padding rows excluded), and every
+  parameter after the update (deferred rows flushed);
 * rows the batch does not touch take the g = 0 AdamW step (decay only): after the
   flush they must equal the fp32 oracle's rows rounded to bf16 BIT FOR BIT.
 
@@ -39,31 +52,20 @@ LR, BETAS, EPS, WD = 1e-3, (0.9, 0.98), 1e-8, 0.01
 
 # Bounds.  loss: the north star's 1e-3.  Everything else: BENCH_AMP_FACTOR x the
 # AMP reference's own error on the same quantity, or the floor when that is smaller.
-# Measured on MI355X (round 5, gpurun_out r5a): loss 6.9e-5 (AMP 2.7e-4), logits 3.6e-3
-# (AMP 3.7e-3), gradients <= 3.9e-2 (AMP <= 4.3e-2) except the 8 user-side feature
-# tables (sparse_emb 103-110: 3.8e-2 vs AMP 2.4e-2 -- at B = 8 each of their rows is
-# ONE user token's gradient, no averaging, and the fused step stores the projected
-# rows' gradient dP in bf16 before dE = dP W (the merged projected-row backward's
-# single rounding), a rounding the AMP step does not have); updates <= 0.21 (AMP
-# 0.22: step-1 Adam moves every element by ~lr * sign(g)); every untouched item /
-# user row bit-exact (997,611 and 999,992 rows).
 BENCH_AMP_FACTOR = 1.5
 LOSS_TOL = 1e-3
 LOGIT_FLOOR = 5e-3
-GRAD_FLOOR = 4.5e-2          # the user-side tables above (measured 3.8e-2); HSTU rab sums as the reduced test
+GRAD_FLOOR = 2.5e-2          # gradients against the oracle fed grk's ReLU masks
+RELU_FLIP_FLOOR = 16         # forward ReLU-boundary flips vs the fp32 oracle: max(1.5 x AMP's, 16)
 UPDATE_FLOOR = 2.5e-2        # the AdamW step-1 update is ~lr * sign(g): sign flips where |g| ~ its error
-ROBUST = 0.1                 # updates compared where |g_fp32| >= 0.1 x its rms (r5h: over all elements the
-                             # step-1 sign of near-zero bias gradients flipped -- biases of 0.08-0.17 -- with
-                             # every gradient inside its bound)
+ROBUST = 0.1                 # updates compared where |g_fp32| >= 0.1 x its rms (the step-1 sign of a
+                             # near-zero gradient is rounding noise for grk and the AMP step alike)
 TABLE_FLIP_FRAC = 2e-3       # bf16 tables: robust elements whose step-1 update sign flipped (beyond
-                             # BENCH_AMP_FACTOR x the AMP step's own gradient sign flips there); measured
-                             # r5k / r5fin: item 1530 of 974,656 (0.16 %), user 4 of 3,768 (0.11 %)
+                             # BENCH_AMP_FACTOR x the AMP step's own gradient sign flips there)
 OPT_TOL = 1e-3               # update vs torch AdamW of grk's own gradient (fp32 dense parameters)
 DENSE_FLIPS = (2e-3, 1)      # dense parameters: robust elements whose step-1 update sign flipped, at most
                              # max(BENCH_AMP_FACTOR x the AMP step's flips there, 0.2 % of the robust
-                             # elements, 1); the rest compared normwise (UPDATE_FLOOR).  One flipped element
-                             # of a ~1.6k-element rab alone is a normwise 0.06 (r5s: rab of layer 1 after an
-                             # ulp-level change of the forward's dnn weight)
+                             # elements, 1); the rest compared normwise (UPDATE_FLOOR)
 
 
 def nrel(a, b):
@@ -73,13 +75,15 @@ def nrel(a, b):
     return float(np.linalg.norm(a - b) / (d if d > 0 else 1.0))
 
 
-def oracle_setup(seed=5):
+def oracle_setup(seed=5, batch=None, sid=None, sid_codes=256):
     """The fp32 oracle model at the bench configuration with live parameters (reference
     init, then LayerNorm gains 1 and small random biases / rab: the reference init
     zeroes them, which makes the first step's logits identically zero), tables
-    rounded to bf16 (the fused optimizer stores them so)."""
+    rounded to bf16 (the fused optimizer stores them so).  sid: a semantic-id table
+    [items + 1, levels] (BASELINE config 4: RQ-VAE codes as O1 item_sparse features)."""
     from tencent_recommendation_2025_amd import synthetic as S
-    cfg = S.SyntheticConfig(batch_size=B, maxlen=MAXLEN, num_items=ITEMS, num_users=USERS)
+    cfg = S.SyntheticConfig(batch_size=batch or B, maxlen=MAXLEN, num_items=ITEMS, num_users=USERS,
+                            sid_table=sid, sid_codes=sid_codes)
     stats, types = S.feature_schema(cfg)
     args = S.make_args(hidden_units=D, maxlen=MAXLEN, num_blocks=BLOCKS, num_heads=HEADS, dropout_rate=0.0)
     ref = model_ref.RefBaselineModel(USERS, ITEMS, stats, types, args, variant='o1', block='hstu')
@@ -99,17 +103,33 @@ def oracle_setup(seed=5):
     return cfg, stats, types, args, ref
 
 
-def oracle_step(ref, cpu, bf16):
+def oracle_step(ref, cpu, bf16, masks=None):
     """One oracle forward + BCE + backward (fp32, or under CPU bf16 autocast): loss,
-    logits and every parameter gradient."""
+    logits, every parameter gradient, and the dnn pre-activations {(role, which):
+    [B, T, d]} (role seq / pos / neg in call order).  masks: RefBaselineModel.relu_masks
+    for the step (None: the oracle's own ReLUs)."""
     ref.zero_grad(set_to_none=True)
+    pre, order = {}, iter([('seq', 'item'), ('seq', 'user'), ('pos', 'item'), ('neg', 'item')])
+    calls = []
+
+    def hook(mod, inp, out):
+        calls.append(out.detach().float())
+    hs = [ref.itemdnn.register_forward_hook(hook), ref.userdnn.register_forward_hook(hook)]
+    ref.relu_masks = masks
     ctx = torch.autocast('cpu', dtype=torch.bfloat16) if bf16 else contextlib.nullcontext()
-    with ctx:
-        pl, nl = ref(cpu[0], cpu[1], cpu[2], cpu[3], cpu[4], cpu[6], cpu[7], cpu[8])
-        loss = model_ref.bce_loss(pl.float(), nl.float(), cpu[4])
-    loss.backward()
+    try:
+        with ctx:
+            pl, nl = ref(cpu[0], cpu[1], cpu[2], cpu[3], cpu[4], cpu[6], cpu[7], cpu[8])
+            loss = model_ref.bce_loss(pl.float(), nl.float(), cpu[4])
+        loss.backward()
+    finally:
+        ref.relu_masks = None
+        for h in hs:
+            h.remove()
+    for c in calls:
+        pre[next(order)] = c
     grads = {n: p.grad.detach().clone() for n, p in ref.named_parameters() if p.grad is not None}
-    return loss.detach(), pl.detach().float(), nl.detach().float(), grads
+    return loss.detach(), pl.detach().float(), nl.detach().float(), grads, pre
 
 
 def adamw_step1_update(p, g):
@@ -123,14 +143,41 @@ def _table_rows(grp, key, n):
     return off, off + n
 
 
-def test_bench_config_full_size_step_matches_oracle():
+def semantic_ids(levels=3, codes=256):
+    """BASELINE config 4's item tokens: an RQ-VAE (grk_rq_assign code search) trained
+    briefly on the items' mm rows and tokenising the whole 1M-item table, as bench.py
+    --semantic-ids does -> the [items + 1, levels] semantic-id table."""
+    from tencent_recommendation_2025_amd.rqvae import RQVAE, semantic_id_table
+    g = torch.Generator(device=DEV).manual_seed(81)
+    mm = torch.randn(ITEMS, 32, device=DEV, generator=g)
+    torch.manual_seed(4)
+    tok = RQVAE(32, hidden=(256, 128), latent_dim=64, levels=levels, codebook_size=codes).to(DEV)
+    tok.init_codebooks(mm[:65536], iters=5)
+    opt = torch.optim.Adam(tok.parameters(), lr=1e-3)
+    for i in range(10):
+        opt.zero_grad(set_to_none=True)
+        tok(mm[i * 16384:(i + 1) * 16384])[2]['loss'].backward()
+        opt.step()
+    return semantic_id_table(tok.tokenize(mm), ITEMS)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('bsz,sid_levels', [(8, 0), (32, 0), (8, 3)], ids=['B8', 'B32', 'C4-sid3-B8'])
+def test_bench_config_full_size_step_matches_oracle(bsz, sid_levels):
+    """batch 8 / 32: BASELINE config 2 (the bench workload); C4: config 4, the same
+    model with 3 RQ-VAE semantic-id levels of 256 codes as O1 item_sparse features
+    (model/BaseLineO1/model.py:271-280 -- the ids enter as ordinary item sparse
+    features, looked up through the projected tables)."""
     from tencent_recommendation_2025_amd import functional as G
     from tencent_recommendation_2025_amd import jagged as J
     from tencent_recommendation_2025_amd import synthetic as S
     from tencent_recommendation_2025_amd.model import BaselineModel
     from tencent_recommendation_2025_amd.optim import FusedAdamW
     torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
-    cfg, stats, types, args, ref = oracle_setup()
+    sid = semantic_ids(sid_levels) if sid_levels else None
+    cfg, stats, types, args, ref = oracle_setup(batch=bsz, sid=sid)
+    if sid is not None:
+        assert types['item_sparse'][-sid_levels:] == [f'sid{i}' for i in range(sid_levels)]
     before = {k: v.detach().clone() for k, v in ref.state_dict().items()}
     m = BaselineModel(USERS, ITEMS, stats, types, args).to(DEV)
     m.load_state_dict(ref.state_dict())
@@ -147,9 +194,29 @@ def test_bench_config_full_size_step_matches_oracle():
     n_span = J.span_rows(tt)
     jag = J.layout(tt, J.capacity_for(n_span, 512), batch[4])
     seq, pos, neg, tt_j, ntt, _nat, sf, pf, nf, _ts, pidx = J.compact(batch, jag)
-    with torch.autocast('cuda', dtype=torch.bfloat16):
-        h, pe, ne = m.encode(seq, pos, neg, tt_j, sf, pf, nf, jagged=jag, pos_idx=pidx)
-        loss = G.bce_loss(h, pe, ne, ntt)
+    # grk's dnn ReLU masks: the seq side's item / user pre-activations (the inputs of
+    # emb_combine, which applies the ReLUs), the pair side's itemdnn output (ReLU in the
+    # GEMM's store: > 0 exactly where the pre-activation is)
+    gmask = {}
+    orig_combine, orig_linear = G.emb_combine, G.linear
+
+    def combine(a, b, *rest, **kw):
+        gmask['seq', 'item'], gmask['seq', 'user'] = (a.detach() > 0), (b.detach() > 0)
+        return orig_combine(a, b, *rest, **kw)
+
+    def linear(x, weight, bias=None, addend=None, relu=False, in_place=False):
+        y = orig_linear(x, weight, bias, addend, relu, in_place)
+        if relu:
+            assert 'pair' not in gmask, 'one ReLU linear (the pair itemdnn) per forward'
+            gmask['pair'] = y.detach() > 0
+        return y
+    G.emb_combine, G.linear = combine, linear
+    try:
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            h, pe, ne = m.encode(seq, pos, neg, tt_j, sf, pf, nf, jagged=jag, pos_idx=pidx)
+            loss = G.bce_loss(h, pe, ne, ntt)
+    finally:
+        G.emb_combine, G.linear = orig_combine, orig_linear
     pl, nl = G.pair_logits(h.detach().float(), pe.detach().float(), ne.detach().float(), ntt)
     loss.backward()
     J.check_error(jag.err)
@@ -167,16 +234,38 @@ def test_bench_config_full_size_step_matches_oracle():
     after = {k: v.detach().float().cpu() for k, v in m.state_dict().items()}
     torch.cuda.synchronize()
 
-    # the oracle: fp32 step, AMP step, then torch AdamW on the fp32 gradients
-    cpu = [x.cpu() if torch.is_tensor(x) else {k: v.cpu() for k, v in x.items()} for x in batch]
-    aloss, apl, anl, agrad = oracle_step(ref, cpu, bf16=True)
-    rloss, rpl, rnl, rgrad = oracle_step(ref, cpu, bf16=False)
-    torch.optim.AdamW(ref.parameters(), lr=LR, betas=BETAS, eps=EPS, weight_decay=WD).step()
-    rafter = {k: v.detach() for k, v in ref.state_dict().items()}
-
+    # grk's masks as [B, T, d] (+ the rows they cover: the span rows of the jagged layout)
     rm = jag.row_map.cpu().long()
     live = rm >= 0
     assert int(live.sum()) == n_span
+    Bq, Tq = tt.shape
+    covered = torch.zeros(Bq * Tq, dtype=torch.bool)
+    covered[rm[live]] = True
+    covered = covered.view(Bq, Tq)
+
+    def to_bt(msk):
+        full = torch.zeros(Bq * Tq, msk.shape[-1], dtype=torch.bool)
+        full[rm[live]] = msk.reshape(-1, msk.shape[-1]).cpu()[:rm.numel()][live]
+        return full.view(Bq, Tq, -1)
+    cap = rm.numel()
+    pair = gmask.pop('pair').reshape(-1, gmask['seq', 'item'].shape[-1])
+    gmask['pos', 'item'], gmask['neg', 'item'] = pair[:cap], pair[cap:2 * cap]
+    masks = {k: (to_bt(v), covered) for k, v in gmask.items()}
+
+    # the oracle: the AMP and fp32 steps with their own ReLUs (loss, logits, the
+    # forward's ReLU flips), then both fed grk's ReLU masks (gradients), torch AdamW
+    # on the fp32 masked gradients
+    cpu = [x.cpu() if torch.is_tensor(x) else {k: v.cpu() for k, v in x.items()} for x in batch]
+    aloss, apl, anl, _, apre = oracle_step(ref, cpu, bf16=True)
+    rloss, rpl, rnl, _, rpre = oracle_step(ref, cpu, bf16=False)
+    flips = {}
+    for key, (gm, cov) in masks.items():
+        want = rpre[key] > 0
+        flips[key] = (int((gm != want)[cov].sum()), int(((apre[key] > 0) != want)[cov].sum()), int(cov.sum()))
+    agrad = oracle_step(ref, cpu, bf16=True, masks=masks)[3]
+    rgrad = oracle_step(ref, cpu, bf16=False, masks=masks)[3]
+    torch.optim.AdamW(ref.parameters(), lr=LR, betas=BETAS, eps=EPS, weight_decay=WD).step()
+    rafter = {k: v.detach() for k, v in ref.state_dict().items()}
     pl, nl = pl.cpu().reshape(-1)[live], nl.cpu().reshape(-1)[live]
     sel = rm[live]
     rpl, rnl, apl, anl = (x.reshape(-1)[sel] for x in (rpl, rnl, apl, anl))
@@ -202,7 +291,7 @@ def test_bench_config_full_size_step_matches_oracle():
 
     # parameters after the update: grk (bf16 tables, fp32 dense) vs the oracle rounded
     # alike; the change is compared (the parameters themselves are mostly unchanged)
-    u_err, u_amp, u_opt, exact_rows, ulp_off = {}, {}, {}, {}, {}
+    u_err, u_amp, u_opt, exact_rows, ulp_off, flip_over = {}, {}, {}, {}, {}, []
     for n, p0 in before.items():
         is_table = n.startswith(('item_emb', 'user_emb', 'pos_emb', 'sparse_emb.'))
         want = rafter[n].bfloat16().float() if is_table else rafter[n]
@@ -236,15 +325,15 @@ def test_bench_config_full_size_step_matches_oracle():
             # the AMP step's own sign flips of the gradient on the same elements: its budget
             amp_flips = int((((agrad[n].float() > 0) != (rg > 0)) & robust).sum()) if n in agrad else 0
             ulp_off[n] = (off, far, int(robust.sum()), amp_flips)
-            assert far <= max(BENCH_AMP_FACTOR * amp_flips, TABLE_FLIP_FRAC * int(robust.sum())), \
-                (n, far, amp_flips, int(robust.sum()))
+            if far > max(BENCH_AMP_FACTOR * amp_flips, TABLE_FLIP_FRAC * int(robust.sum())):
+                flip_over.append((n, far, amp_flips, int(robust.sum())))
             u_err[n] = 0.0
         else:
             flip = robust & ((du_grk > 0) != (du_ref > 0)) & (du_ref != 0)
             nflip = int(flip.sum())
             amp_flips = int((((agrad[n].float() > 0) != (rg > 0)) & robust).sum()) if n in agrad else 0
-            assert nflip <= max(BENCH_AMP_FACTOR * amp_flips, DENSE_FLIPS[0] * int(robust.sum()), DENSE_FLIPS[1]), \
-                (n, nflip, amp_flips, int(robust.sum()))
+            if nflip > max(BENCH_AMP_FACTOR * amp_flips, DENSE_FLIPS[0] * int(robust.sum()), DENSE_FLIPS[1]):
+                flip_over.append((n, nflip, amp_flips, int(robust.sum())))
             ulp_off[n] = (0, nflip, int(robust.sum()), amp_flips)
             keep = robust & ~flip
             u_err[n] = nrel(du_grk[keep], du_ref[keep])
@@ -259,15 +348,23 @@ def test_bench_config_full_size_step_matches_oracle():
                              int((after[n][untouched] != want[untouched]).any(1).sum()))
     worst_g = sorted(((e, g_amp[k], k) for k, e in g_err.items()), reverse=True)[:6]
     worst_u = sorted(((e, u_amp[k], k) for k, e in u_err.items()), reverse=True)[:6]
-    print(f'bench-size step (B={B}, {n_span} span rows): grk {errs}, AMP {amp}')
+    print(f'bench-size step (B={bsz}, sid levels {sid_levels}, {n_span} span rows): grk {errs}, AMP {amp}')
+    print('  dnn ReLU flips vs the fp32 oracle (grk, AMP, rows):', flips)
     print('  worst grads (grk, amp, name):', worst_g)
     print('  worst updates (grk, amp, name):', worst_u)
     print('  untouched table rows (count, mismatching):', exact_rows)
     print('  optimizer (update vs AdamW of grk gradients), worst:', max(u_opt.values()) if u_opt else None)
     print('  table + dense elements (one ulp off, sign-flipped, robust, AMP sign flips):',
           [sum(v[i] for v in ulp_off.values()) for i in range(4)])
+    print('  per table (one ulp off, sign-flipped, robust, AMP sign flips):',
+          {k: v for k, v in ulp_off.items() if k.startswith(('item_emb', 'user_emb', 'sparse_emb.'))})
+    print('  worst grads vs AMP (grk / AMP, name):',
+          sorted(((e / max(g_amp[k], 1e-30), k) for k, e in g_err.items()), reverse=True)[:8])
+    assert not flip_over, flip_over
 
     assert errs['loss'] < LOSS_TOL, (errs, amp)
+    over = [(k, f) for k, f in flips.items() if f[0] > max(BENCH_AMP_FACTOR * f[1], RELU_FLIP_FLOOR)]
+    assert not over, over
     assert errs['logits'] <= max(BENCH_AMP_FACTOR * amp['logits'], LOGIT_FLOOR), (errs, amp)
     over = [(k, e, g_amp[k]) for k, e in g_err.items() if e > max(BENCH_AMP_FACTOR * g_amp[k], GRAD_FLOOR)]
     assert not over, over

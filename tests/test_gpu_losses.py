@@ -89,7 +89,7 @@ def sampled_case(M, D, seed, frac_valid=0.6, dup_every=7):
     return h, e, ids, valid
 
 
-@pytest.mark.parametrize('M,D', [(77, 32), (600, 64), (1000, 512), (333, 128), (2100, 256)])
+@pytest.mark.parametrize('M,D', [(77, 32), (600, 64), (1000, 512), (333, 128), (2100, 256), (45, 512), (3001, 512)])
 def test_sampled_softmax_matches_oracle(K, M, D):
     """fp32 gradients of the fused backward vs the fp64 oracle at 1e-4 (the
     bf16-output gradients of the autograd path at 1e-3 below)."""
@@ -151,8 +151,9 @@ def test_sampled_softmax_logq_matches_oracle(K, M, D):
     assert torch.equal(ga[0], gb[0]) and torch.equal(ga[1], gb[1])
 
 
-def test_sampled_softmax_no_valid_rows(K):
-    M, D = 64, 64
+@pytest.mark.parametrize('D', [64, 512])
+def test_sampled_softmax_no_valid_rows(K, D):
+    M = 64
     h = torch.randn(M, D, device=DEV).bfloat16()
     ids = torch.arange(M, device=DEV)
     v8 = torch.zeros(M, dtype=torch.uint8, device=DEV)
