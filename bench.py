@@ -311,10 +311,30 @@ def item_gather_roofline(table, batch, reps):
     warm = _time(lambda: K.embedding_gather(lk, out, n), reps)  # same rows again: Infinity-Cache served
     alg = 2 * n * D * table.element_size() + 8 * n
     gbps = alg / (ms * 1e-3) / 1e9
+    # context for the fraction: a contiguous copy of the same bytes in one launch, timed
+    # the same way (cold, alone) -- at ~84 MB a launch's ramp and drain cap even that
+    # near 0.62 of the HBM peak (scripts/microbench/gather.hip sweeps)
+    src = torch.empty(n, D, dtype=table.dtype, device=table.device)
+    flush = torch.ones(128 << 20, dtype=torch.int32, device=table.device)
+    sink = torch.empty((), dtype=torch.int64, device=table.device)
+    ctot = 0.0
+    for _ in range(reps):
+        torch.sum(flush, dim=0, out=sink)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        out.copy_(src)
+        e1.record(stream)
+        e1.synchronize()
+        ctot += e0.elapsed_time(e1)
+    cms = ctot / reps
+    del flush, sink, src
     res = {'bound': 'hbm', 'kernel': 'grk::k_gather (item-table rows, 1M x 512 bf16)', 'achieved': round(gbps, 1),
            'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': round(gbps / HBM_PEAK_GBPS, 4), 'traffic': None,
            'alg_bytes_per_launch': int(alg), 'avg_launch_us': round(ms * 1e3, 2), 'rows_per_launch': int(n),
            'warm_cache_gbps': round(alg / (warm * 1e-3) / 1e9, 1),
+           'copy_same_bytes_us': round(cms * 1e3, 2),
+           'copy_same_bytes_frac': round((2 * n * D * table.element_size()) / (cms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+           'frac_of_copy': round(cms / ms, 4),
            'workload': {'rows': int(n), 'table_rows': int(table.shape[0]), 'D': int(D)}}
     p = _pmc(f'{PMC_TAG}_pmc_gather_item.json', res['workload'])
     if p is not None:
@@ -535,12 +555,10 @@ def catchup_roofline(opt, reps, batch=None):
             total += e0.elapsed_time(e1)
         return total / reps
 
-    ms = timed(lambda: K.table_adamw_catchup_slice(p, m, v, last, opt.clock, period))
-    n = hi - lo
-    moved = int((lag > 0).sum().item())
-    alg = moved * D * (p.element_size() + 8) * 2 + n * 8
-    # the batch rows' catch-up: rows the batch reads, from the state the timed region left
-    # (their lag since they were last read or flushed, at most one period)
+    # the batch rows' catch-up first: rows the batch reads, from the state the timed region
+    # left (their lag since they were last read or flushed, at most one period); then the
+    # slice, whose launches end the run's catch-ups (scripts/pmc_rooflines.py takes the
+    # PMC traffic of the last launches)
     b_ms = b_alg = 0.0
     if batch is not None:
         ids = K.batch_row_ids(*batch[:4], with_user=False)[0]
@@ -548,6 +566,10 @@ def catchup_roofline(opt, reps, batch=None):
         u = ids[ids > 0].unique()
         b_moved = int(((t - last0[u].long()) > 0).sum().item())
         b_alg = b_moved * D * (p.element_size() + 8) * 2 + ids.numel() * 8 + u.numel() * 8
+    ms = timed(lambda: K.table_adamw_catchup_slice(p, m, v, last, opt.clock, period))
+    n = hi - lo
+    moved = int((lag > 0).sum().item())
+    alg = moved * D * (p.element_size() + 8) * 2 + n * 8
     calls = len(opt._deferred)
     launches = calls * (2 if batch is not None else 1)
     tot_ms = calls * (ms + b_ms)

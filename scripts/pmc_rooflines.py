@@ -141,9 +141,11 @@ for e in entries:
             w = e['workload']
             e = dict(e, alg_bytes_per_launch=int(2 * w['K'] * (w['M'] + w['N']) + 4 * w['M'] * (w['N'] + 1)))
     elif k.startswith('k_adamw_catchup'):
-        # the rolling flush's slice launches of the roofline replays (the run's last catch-ups)
+        # the rolling flush's slice launches of the roofline replays (the run's last catch-ups;
+        # bench.py times the batch-row catch-up before them)
         fb, wb, n = traffic('k_adamw_catchup')
         name = f'{tag}_pmc_catchup.json'
+        e = dict(e, alg_bytes_per_launch=e['slice']['alg_bytes_per_launch']) if 'slice' in e else e
     else:
         continue
     out = {'kernel': k, 'workload': e['workload'], 'launches_averaged': n,

@@ -270,6 +270,7 @@ __device__ __forceinline__ bf16x8 ss_tr8(const char* img, int row0, int col0, in
   return f;
 }
 
+constexpr int kSSPre = 4;                    // fragment reads in flight ahead of their MFMA
 constexpr int kSS2Rows = 256;
 constexpr int kSS2Slices = 16;
 constexpr int kSS2Nst = 4;
@@ -323,9 +324,18 @@ __global__ void __launch_bounds__(512) k_ss_fwd2(SSParams p, int rblocks) {
     const char* img = smem + (i % NST) * kSS2Stage;
     const int64_t* tid = reinterpret_cast<const int64_t*>(img + kSS2Img);
     const float* tlq = reinterpret_cast<const float*>(img + kSS2Img + 256);
+    // the E fragments kSSPre k-steps ahead of their MFMA (a read issued right before its
+    // MFMA exposes the LDS latency on every k-step)
     f32x16 s = acc_zero();
+    bf16x8 af[kSSPre];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) s = mfma(ss_row8(img, r, 16 * ks + 8 * hh), of[ks], s);
+    for (int ks = 0; ks < kSSPre; ++ks) af[ks] = ss_row8(img, r, 16 * ks + 8 * hh);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8 a = af[ks % kSSPre];
+      if (ks + kSSPre < KS) af[ks % kSSPre] = ss_row8(img, r, 16 * (ks + kSSPre) + 8 * hh);
+      s = mfma(a, of[ks], s);
+    }
     const int jb = (tb + i) * 32;
     const bool full = jb + 32 <= nv;
     float x[16], tmax = -INFINITY;
@@ -538,57 +548,49 @@ __global__ void __launch_bounds__(SSB<D>::NT) k_ss_bwd(SSParams p) {
           make_float4(acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]);
 }
 
-// Backward at D = 512 (round 6): k_ss_bwd's math (S recomputed per tile, G = softmax -
-// onehot as bf16 hi + lo, dH = G E / dE = G^T H) with two waves per 32 own rows, each
-// owning one half of D: a wave computes the score tile over its half (16 MFMAs), the
-// pair swaps those partial tiles through LDS (ONE hand-off per tile, double-buffered),
-// both finish the full scores and G in their own lanes (the softmax VALU twice, no G
-// hand-off), and each multiplies G into its 8 column blocks (32 MFMAs).  4 row groups x
-// 2 halves = 8 waves, 128 own rows per workgroup; the other side's 32-row tiles stream
-// through a 3-stage LDS-DMA ring (k_ss_fwd2's image + meta).  The round-2 kernel: 64
-// own rows, 4 D quarters, three hand-offs per tile, tiles staged through registers.
-// Any score of elements k0 .. k0 + 7 of lane (r, hh) whose column id matches the own
-// row's id in its low word but is not the row itself (then compared in full).
-__device__ __forceinline__ bool lo_dup(const uint32_t* tid32, uint32_t olo, uint32_t ohi, int tb, int oc, int k0,
-                                       int hh) {
-  bool any = false;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int tr = acc_row(k0 + e, hh);
-    any |= (tid32[2 * tr] == olo) & (tb + tr != oc);
-  }
-  return any;
-}
-
-constexpr int kSSBRg = 4;                       // row groups
+// Backward at D = 512 (round 6): k_ss_bwd's decomposition -- 2 row groups of 32 own rows
+// x 4 D quarters = 8 waves; per tile each wave's partial scores (8 MFMAs) go to LDS, wave
+// q sums the four quarters of the EPW = 4 scores it owns (in D order), turns them into G
+// (bf16 hi + lo words) and hands them back; every wave then multiplies the whole G tile
+// into its 4 column blocks (16 MFMAs) -- the softmax VALU runs once per score.  What
+// changed from round 2: the other side's 32-row tiles stream through a 3-stage LDS-DMA
+// ring (k_ss_fwd2's padded image + meta) instead of a register round trip one tile
+// ahead behind two barriers; the hand-off buffers are laid out lane-minor (conflict-free
+// 16-byte accesses); the masks are branch-free; the fragment reads run ahead of their
+// MFMAs.
+constexpr int kSSBRg = 2;                       // row groups
+constexpr int kSSBNw = 4;                       // D quarters
+constexpr int kSSBEpw = 16 / kSSBNw;            // scores per lane each wave turns into G
 constexpr int kSSBRows = 32 * kSSBRg;
 constexpr int kSSBNst = 3;
-constexpr int kSSBXch = 8 * 64 * 16 * 4;        // [wave][lane][16 floats]
+constexpr int kSSBRed = kSSBRg * kSSBNw * 4 * 64 * 16;          // float4 partials [wave][quad][lane]
+constexpr int kSSBGx = kSSBRg * kSSBNw * (kSSBEpw / 2) * 2 * 64 * 4;   // G words [wave][word][lane]
 
 template <int P, int NST>
 __device__ __forceinline__ void ssb_wait(int ahead) { ring_wait<P, NST>(ahead); }
 
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) k_ss_bwd2(SSParams p) {
-  constexpr int D = 512, DH = D / 2, KSQ = DH / 16, NDT = DH / 32, NST = kSSBNst;
-  __shared__ __attribute__((aligned(16))) char smem[NST * kSS2Stage + kSSBXch];
-  float4* xch = reinterpret_cast<float4*>(smem + NST * kSS2Stage);
+__global__ void __launch_bounds__(512) k_ss_bwd2(SSParams p) {
+  constexpr int D = 512, NW = kSSBNw, DQ = D / NW, KSQ = DQ / 16, NDT = DQ / 32, NST = kSSBNst, EPW = kSSBEpw;
+  __shared__ __attribute__((aligned(16))) char smem[NST * kSS2Stage + kSSBRed + kSSBGx];
+  float4* red = reinterpret_cast<float4*>(smem + NST * kSS2Stage);
+  uint32_t* gx = reinterpret_cast<uint32_t*>(smem + NST * kSS2Stage + kSSBRed);
   const int nv = *p.nvp;
   const int oc0 = blockIdx.x * kSSBRows;
   if (oc0 >= nv) return;
   const bool rows = blockIdx.y == 0;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-  const int rg = wave >> 1, half = wave & 1;
+  const int rg = wave / NW, ws = wave % NW;
   const int oc = oc0 + rg * 32 + r;
   const bool ook = oc < nv;
   const int64_t oid = ook ? p.idc[oc] : -2;
-  const uint32_t olo = (uint32_t)oid, ohi = (uint32_t)((uint64_t)oid >> 32);
+  const uint32_t olo = (uint32_t)oid;
   // exponent offset of element (row i, column j) = lse2_i + log2 q_j: the own row's part
   // here, the tile row's part in the tile's meta (log2 q of e rows, or lse2 of h rows)
   const float olse = ook ? (rows ? p.lsec[oc] : p.lqc[oc]) : 0.f;
   const bf16_t* own = rows ? p.hc : p.ec;
   const bf16_t* tsrc = rows ? p.ec : p.hc;
   const float* tmeta = rows ? p.lqc : p.lsec;
-  const int col0 = half * DH;
+  const int col0 = ws * DQ;
   bf16x8 of[KSQ];
 #pragma unroll
   for (int ks = 0; ks < KSQ; ++ks) of[ks] = gload8(own + (int64_t)oc * D + col0 + 16 * ks + 8 * hh, ook);
@@ -616,6 +618,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   };
   for (int i = 0; i < NST - 1 && i < nt; ++i) issue(i, i);
+  float4* red_mine = red + wave * 4 * 64 + lane;                 // [wave][quad][lane]
+  const float4* red_q = red + (rg * NW) * 4 * 64 + ws * 64 + lane;   // quad ws of this row group's waves
+  uint32_t* gx_mine = gx + wave * EPW * 64 + lane;               // [wave][word][lane]: EPW/2 hi, EPW/2 lo
+  const uint32_t* gx_grp = gx + (rg * NW) * EPW * 64 + lane;
   for (int i = 0; i < nt; ++i) {
     if (wu == 0) ssb_wait<5, NST>(nt - 1 - i);
     else ssb_wait<4, NST>(nt - 1 - i);
@@ -626,76 +632,80 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     const float* tlse = reinterpret_cast<const float*>(img + kSS2Img + 256);
     const int tb = i * 32;
     f32x16 s = acc_zero();
+    bf16x8 af[kSSPre];
+#pragma unroll
+    for (int ks = 0; ks < kSSPre; ++ks) af[ks] = ss_row8(img, r, col0 + 16 * ks + 8 * hh);
 #pragma unroll
     for (int ks = 0; ks < KSQ; ++ks) {
-      s = mfma(ss_row8(img, r, col0 + 16 * ks + 8 * hh), of[ks], s);
-      if ((ks & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      const bf16x8 a = af[ks % kSSPre];
+      if (ks + kSSPre < KSQ) af[ks % kSSPre] = ss_row8(img, r, col0 + 16 * (ks + kSSPre) + 8 * hh);
+      s = mfma(a, of[ks], s);
     }
-    // swap the half-D partial scores with the partner wave (the ring's barrier of the
-    // next tile orders the buffer's reuse: every read of this tile's scores is before it)
-    float4* mine = xch + wave * 64 * 4 + lane * 4;
-    const float4* other = xch + (wave ^ 1) * 64 * 4 + lane * 4;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) mine[q] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
+    for (int q = 0; q < 4; ++q) red_mine[64 * q] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
+    // the product's fragments of the first half tile, read while the partials travel
+    bf16x8 tfs[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) tfs[dt] = ss_tr8(img, 0, col0 + 32 * dt, lane);
     lds_barrier();
+    // this wave's EPW scores (elements 4 ws .. 4 ws + 3 = quad ws), the quarters in D order
+    float se[EPW];
+    {
+      float4 t = red_q[0];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 u = other[q];
-      // the sum in D order (half 0 + half 1) on both waves: the same bits
-      s[4 * q] = half ? u.x + s[4 * q] : s[4 * q] + u.x;
-      s[4 * q + 1] = half ? u.y + s[4 * q + 1] : s[4 * q + 1] + u.y;
-      s[4 * q + 2] = half ? u.z + s[4 * q + 2] : s[4 * q + 2] + u.z;
-      s[4 * q + 3] = half ? u.w + s[4 * q + 3] : s[4 * q + 3] + u.w;
+      for (int w = 1; w < NW; ++w) {
+        const float4 u = red_q[w * 4 * 64];
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+      }
+      se[0] = t.x; se[1] = t.y; se[2] = t.z; se[3] = t.w;
     }
     const bool full = tb + 32 <= nv;
-    // per half tile (elements 8 s2 .. 8 s2 + 7 = tile rows 16 s2 ..): G as bf16 hi / lo
-    // words, then that half's 16 product MFMAs
+    float g[EPW];
+    bool lodup = false;
+#pragma unroll
+    for (int e = 0; e < EPW; ++e) {
+      // element k = 4 ws + e: acc_row = (k & 3) + 8 (k >> 2) + 4 hh = e + 8 ws + 4 hh
+      const int tr = e + 8 * ws + 4 * hh, tc = tb + tr;
+      const bool same = tid32[2 * tr] == olo;   // ids compared on their low words (one register)
+      const bool ok = ook & (full | (tc < nv)) & ((tc == oc) | !same);
+      lodup |= ook & same & (tc != oc);
+      const float pr = __builtin_amdgcn_exp2f(fmaf(se[e], p.sl2, -(olse + tlse[tr])));
+      g[e] = ok ? (tc == oc ? pr - 1.f : pr) * coef : 0.f;
+    }
+    if (__builtin_expect(__ballot(lodup) != 0, 0)) {   // a low-word match: the full ids decide (rare)
+#pragma unroll
+      for (int e = 0; e < EPW; ++e) {
+        const int tr = e + 8 * ws + 4 * hh, tc = tb + tr;
+        const bool ok = ook & (full | (tc < nv)) & ((tc == oc) | (tid[tr] != oid));
+        const float pr = __builtin_amdgcn_exp2f(fmaf(se[e], p.sl2, -(olse + tlse[tr])));
+        g[e] = ok ? (tc == oc ? pr - 1.f : pr) * coef : 0.f;
+      }
+    }
+#pragma unroll
+    for (int e2 = 0; e2 < EPW / 2; ++e2) {
+      uint32_t hw, lw;
+      split2(f32x2{g[2 * e2], g[2 * e2 + 1]}, hw, lw);
+      gx_mine[64 * e2] = hw;
+      gx_mine[64 * (EPW / 2 + e2)] = lw;
+    }
+    lds_barrier();
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      uint32_t gw[4], lw[4];
+      // G words of elements 8 s2 .. 8 s2 + 7: pairs 2 pp of wave w = k / EPW
+      uint32_t hw[4], lw[4];
 #pragma unroll
-      for (int k2 = 0; k2 < 4; ++k2) {
-        float g2[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int k = 8 * s2 + 2 * k2 + u;
-          const int tr = acc_row(k, hh), tc = tb + tr;
-          // the same item elsewhere in the batch is masked: compared on the ids' low words
-          // here (one register per score, no branch), the rare low-word matches on the
-          // high words below
-          const bool ok = ook & (full | (tc < nv)) & ((tc == oc) | (tid32[2 * tr] != olo));
-          const float pr = __builtin_amdgcn_exp2f(fmaf(s[k], p.sl2, -(olse + tlse[tr])));
-          g2[u] = ok ? (tc == oc ? pr - 1.f : pr) * coef : 0.f;
-        }
-        split2(f32x2{g2[0], g2[1]}, gw[k2], lw[k2]);
+      for (int pp = 0; pp < 4; ++pp) {
+        const int k = 8 * s2 + 2 * pp, w = k / EPW, kk = k % EPW;
+        hw[pp] = gx_grp[(w * EPW + kk / 2) * 64];
+        lw[pp] = gx_grp[(w * EPW + EPW / 2 + kk / 2) * 64];
       }
-      if (__builtin_expect(__ballot(lo_dup(tid32, olo, ohi, tb, oc, 8 * s2, hh)) != 0, 0)) {
-        // a low-word match that is not this row itself: recompute the half tile's G with
-        // the full ids (wave-uniform branch, rare: in-batch repeats of an item)
-#pragma unroll
-        for (int k2 = 0; k2 < 4; ++k2) {
-          float g2[2];
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int k = 8 * s2 + 2 * k2 + u;
-            const int tr = acc_row(k, hh), tc = tb + tr;
-            const bool ok = ook & (full | (tc < nv)) & ((tc == oc) | (tid[tr] != oid));
-            const float pr = __builtin_amdgcn_exp2f(fmaf(s[k], p.sl2, -(olse + tlse[tr])));
-            g2[u] = ok ? (tc == oc ? pr - 1.f : pr) * coef : 0.f;
-          }
-          split2(f32x2{g2[0], g2[1]}, gw[k2], lw[k2]);
-        }
-      }
-      const bf16x8 gh = words8(gw), gl = words8(lw);
-      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8 gh = words8(hw), gl = words8(lw);
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
-        const bf16x8 tf = ss_tr8(img, 16 * s2, col0 + 32 * dt, lane);
+        const bf16x8 tf = tfs[dt];
+        if (s2 == 0) tfs[dt] = ss_tr8(img, 16, col0 + 32 * dt, lane);   // the second half's, under these MFMAs
         acc[dt] = mfma(tf, gh, acc[dt]);
         acc[dt] = mfma(tf, gl, acc[dt]);
-        // at most two column blocks' fragments in flight (registers: the 128
-        // accumulators + the 64 own-row fragments leave little else)
-        if (dt & 1) __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
