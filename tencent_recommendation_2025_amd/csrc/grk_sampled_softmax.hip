@@ -55,6 +55,7 @@ struct SSParams {
   float* diag;          // [M] z_ii in log2 units, compact rows
   float* lse2;          // [M] log2-domain logsumexp, compact rows
   float* lsec;          // backward at D = 512: lse2 copied into the workspace ([M + kSS2Pad])
+  float* part;          // backward at D = 512: [kSSBGrid][2][64][512] partial gradients (k_ss_bwd2)
   float* partials;      // [nblocks]
   float* loss;
   const float* grad_loss;
@@ -234,12 +235,10 @@ __global__ void __launch_bounds__(256) k_ss_fwd(SSParams p) {
 //    rows' full-D fragments (128 VGPRs) for the whole column walk, so a staged
 //    32-row E tile serves 256 rows (the round-2 kernel: 128, behind two barriers
 //    and a register round trip per tile);
-//  * E tiles (32 rows x 1 KiB, the lds_off<512> swizzle, one global_load_lds_dwordx4
+//  * E tiles (32 rows x 1 KiB at the padded stride below, one global_load_lds_dwordx4
 //    per row) plus the tile's ids and log2 q (one more DMA) land in a kSS2Nst-stage
 //    ring; one barrier per tile (ring_wait);
-//  * the columns are cut into kSS2Slices slices; the slices' workgroups are dealt to
-//    the XCDs slice-major (slice s on XCD s mod 8), so an XCD streams 2/16 of E
-//    (~1.7 MB at C2) through its own 4 MiB L2 for all of its row blocks.
+//  * persistent workgroups, the columns cut into one slice per XCD (SS2Split below).
 // Per tile a wave runs 32 MFMAs (32 ds_read_b128 of the E image) and the online
 // logsumexp update of its 16 scores per lane -- the math of k_ss_fwd.
 // The D = 512 tile images: 32 rows of 1 KiB at a padded stride of kSS2Row = 1040 B, so
@@ -272,31 +271,54 @@ __device__ __forceinline__ bf16x8 ss_tr8(const char* img, int row0, int col0, in
 
 constexpr int kSSPre = 4;                    // fragment reads in flight ahead of their MFMA
 constexpr int kSS2Rows = 256;
-constexpr int kSS2Slices = 16;
 constexpr int kSS2Nst = 4;
 constexpr int kSS2Img = 32 * kSS2Row;
 constexpr int kSS2Stage = kSS2Img + 1024;   // + the tile's ids (256 B) and log2 q (128 B)
 constexpr int kSS2Pad = 64;                 // idc / lqc rows past M the meta DMA may read
 
+// Work split (stream-K, XCD-sliced): the columns are cut into 8 slices, slice x is
+// the work of XCD x's kSS2PerXcd persistent workgroups (blockIdx % 8 = x), so an XCD
+// streams only its 1/8 of E (~1.7 MB at C2) through its own 4 MiB L2; within the slice
+// the RB x tx units (256-row blocks x the slice's tiles) are cut evenly over the XCD's
+// workgroups, so no CU idles through a partial last wave of workgroups (864 fixed
+// workgroups on 256 CUs ran 4 rounds for 3.4 rounds of work).  A block's part of the
+// slice wholly inside one workgroup leaves its (max, sum) in slot F[x][block]; a part
+// cut between workgroups leaves one per piece in W[workgroup][first / last] --
+// k_ss_combine merges the pieces of every slice in a fixed order.
+constexpr int kSS2PerXcd = 32;
+constexpr int kSS2Grid = 8 * kSS2PerXcd;
+
+struct SS2Split {
+  int rb, nt, tb, tx;
+  int64_t units;
+  __device__ SS2Split(int nv, int x) : rb((nv + kSS2Rows - 1) / kSS2Rows), nt((nv + 31) / 32) {
+    tb = (int)((int64_t)x * nt / 8);
+    tx = (int)((int64_t)(x + 1) * nt / 8) - tb;
+    units = (int64_t)rb * tx;
+  }
+  __device__ int64_t start(int j) const { return (int64_t)j * units / kSS2PerXcd; }
+  __device__ int owner(int64_t u) const {
+    int j = (int)(u * kSS2PerXcd / max(units, (int64_t)1));
+    while (j + 1 < kSS2PerXcd && start(j + 1) <= u) ++j;
+    while (j > 0 && start(j) > u) --j;
+    return j;
+  }
+};
+// (max, sum) slots: F [8][rbmax * 256] then W [kSS2Grid][2][256], each as pm / pl
+__device__ __forceinline__ int64_t ss2_fslot(int x, int b, int rbmax) { return ((int64_t)x * rbmax + b) * kSS2Rows; }
+__device__ __forceinline__ int64_t ss2_wslot(int g, int last, int rbmax) {
+  return ((int64_t)8 * rbmax + 2 * g + last) * kSS2Rows;
+}
+
 template <bool LQ>
-__global__ void __launch_bounds__(512) k_ss_fwd2(SSParams p, int rblocks) {
+__global__ void __launch_bounds__(512) k_ss_fwd2(SSParams p, int rbmax) {
   constexpr int D = 512, KS = D / 16, NST = kSS2Nst, P = 5;
   __shared__ __attribute__((aligned(16))) char smem[NST * kSS2Stage];
   const int nv = *p.nvp;
-  const unsigned phys = blockIdx.x, xcd = phys & 7, q = phys >> 3;
-  const int slice = (int)(xcd + 8 * (q / rblocks)), rb = (int)(q % rblocks);
-  const int oc0 = rb * kSS2Rows;
-  if (oc0 >= nv) return;
+  const int g = blockIdx.x, x = g & 7, j = g >> 3;
+  const SS2Split sp(nv, x);
+  const int64_t u0 = sp.start(j), u1 = sp.start(j + 1);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-  const int oc = oc0 + wave * 32 + r;
-  const bool ook = oc < nv;
-  const bool wave_live = oc0 + wave * 32 < nv;
-  const int64_t oid = ook ? p.idc[oc] : -2;
-  bf16x8 of[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) of[ks] = gload8(p.hc + (int64_t)oc * D + 16 * ks + 8 * hh, ook);
-  const int tiles = (nv + 31) / 32, per = (tiles + kSS2Slices - 1) / kSS2Slices;
-  const int tb = min(tiles, slice * per), te = min(tiles, tb + per), nt = te - tb;
   const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane(
       (int)((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem));
   // this lane's DMA sources: E rows 4 wave .. 4 wave + 3 of a tile (16-byte chunk
@@ -315,52 +337,70 @@ __global__ void __launch_bounds__(512) k_ss_fwd2(SSParams p, int rblocks) {
                                                  : (const bf16_t*)(p.idc + t0 + 2 * (lane & 15));
     wg_dma16(meta, base + kSS2Img);
   };
-  for (int i = 0; i < NST - 1 && i < nt; ++i) issue(tb + i, i);
-  float m = -INFINITY, l = 0.f;
-  for (int i = 0; i < nt; ++i) {
-    ring_wait<P, NST>(nt - 1 - i);
-    if (i + NST - 1 < nt) issue(tb + i + NST - 1, (i + NST - 1) % NST);
-    if (!wave_live) continue;
-    const char* img = smem + (i % NST) * kSS2Stage;
-    const int64_t* tid = reinterpret_cast<const int64_t*>(img + kSS2Img);
-    const float* tlq = reinterpret_cast<const float*>(img + kSS2Img + 256);
-    // the E fragments kSSPre k-steps ahead of their MFMA (a read issued right before its
-    // MFMA exposes the LDS latency on every k-step)
-    f32x16 s = acc_zero();
-    bf16x8 af[kSSPre];
+  for (int64_t u = u0; u < u1;) {
+    const int b = (int)(u / sp.tx);
+    const int t0 = sp.tb + (int)(u - (int64_t)b * sp.tx);
+    const int64_t ue = min(u1, (int64_t)(b + 1) * sp.tx);
+    const int nt = (int)(ue - u);
+    const bool whole = nt == sp.tx, first = u == u0;
+    u = ue;
+    const int oc0 = b * kSS2Rows;
+    const int oc = oc0 + wave * 32 + r;
+    const bool ook = oc < nv;
+    const bool wave_live = oc0 + wave * 32 < nv;
+    const int64_t oid = ook ? p.idc[oc] : -2;
+    bf16x8 of[KS];
 #pragma unroll
-    for (int ks = 0; ks < kSSPre; ++ks) af[ks] = ss_row8(img, r, 16 * ks + 8 * hh);
+    for (int ks = 0; ks < KS; ++ks) of[ks] = gload8(p.hc + (int64_t)oc * D + 16 * ks + 8 * hh, ook);
+    lds_barrier();   // every wave is past the previous piece's reads of the ring
+    for (int i = 0; i < NST - 1 && i < nt; ++i) issue(t0 + i, i);
+    float m = -INFINITY, l = 0.f;
+    for (int i = 0; i < nt; ++i) {
+      ring_wait<P, NST>(nt - 1 - i);
+      if (i + NST - 1 < nt) issue(t0 + i + NST - 1, (i + NST - 1) % NST);
+      if (!wave_live) continue;
+      const char* img = smem + (i % NST) * kSS2Stage;
+      const int64_t* tid = reinterpret_cast<const int64_t*>(img + kSS2Img);
+      const float* tlq = reinterpret_cast<const float*>(img + kSS2Img + 256);
+      // the E fragments kSSPre k-steps ahead of their MFMA (a read issued right before its
+      // MFMA exposes the LDS latency on every k-step)
+      f32x16 s = acc_zero();
+      bf16x8 af[kSSPre];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const bf16x8 a = af[ks % kSSPre];
-      if (ks + kSSPre < KS) af[ks % kSSPre] = ss_row8(img, r, 16 * (ks + kSSPre) + 8 * hh);
-      s = mfma(a, of[ks], s);
+      for (int ks = 0; ks < kSSPre; ++ks) af[ks] = ss_row8(img, r, 16 * ks + 8 * hh);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 a = af[ks % kSSPre];
+        if (ks + kSSPre < KS) af[ks % kSSPre] = ss_row8(img, r, 16 * (ks + kSSPre) + 8 * hh);
+        s = mfma(a, of[ks], s);
+      }
+      const int jb = (t0 + i) * 32;
+      const bool full = jb + 32 <= nv;
+      float xs[16], tmax = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int jr = acc_row(k, hh), jc = jb + jr;
+        // branch-free (the id is read whatever the other terms: no per-score branch)
+        const int64_t tj = tid[jr];
+        const bool ok = (full | (jc < nv)) & ((jc == oc) | (tj != oid));
+        xs[k] = ok ? (LQ ? s[k] * p.sl2 - tlq[jr] : s[k] * p.sl2) : -INFINITY;
+        tmax = fmaxf(tmax, xs[k]);
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+      const float mn = fmaxf(m, tmax);
+      if (mn == -INFINITY) continue;
+      float rs = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) rs += __builtin_amdgcn_exp2f(xs[k] - mn);  // exp2(-inf) = 0
+      rs += __shfl_xor(rs, 32);
+      l = l * __builtin_amdgcn_exp2f(m - mn) + rs;
+      m = mn;
     }
-    const int jb = (tb + i) * 32;
-    const bool full = jb + 32 <= nv;
-    float x[16], tmax = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int jr = acc_row(k, hh), jc = jb + jr;
-      // branch-free (the id is read whatever the other terms: no per-score branch)
-      const int64_t tj = tid[jr];
-      const bool ok = (full | (jc < nv)) & ((jc == oc) | (tj != oid));
-      x[k] = ok ? (LQ ? s[k] * p.sl2 - tlq[jr] : s[k] * p.sl2) : -INFINITY;
-      tmax = fmaxf(tmax, x[k]);
+    if (hh == 0 && ook) {
+      const int64_t at = (whole ? ss2_fslot(x, b, rbmax) : ss2_wslot(g, first ? 0 : 1, rbmax)) + wave * 32 + r;
+      p.pm[at] = m;
+      p.pl[at] = l;
     }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
-    const float mn = fmaxf(m, tmax);
-    if (mn == -INFINITY) continue;
-    float rs = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) rs += __builtin_amdgcn_exp2f(x[k] - mn);  // exp2(-inf) = 0
-    rs += __shfl_xor(rs, 32);
-    l = l * __builtin_amdgcn_exp2f(m - mn) + rs;
-    m = mn;
-  }
-  if (hh == 0 && ook) {
-    p.pm[(int64_t)slice * p.M + oc] = m;
-    p.pl[(int64_t)slice * p.M + oc] = l;
   }
 }
 
@@ -379,18 +419,44 @@ __global__ void __launch_bounds__(256) k_ss_diag(SSParams p) {
 }
 
 // Merge slices -> lse2[ic]; per-block loss partials in a fixed order.
-__global__ void __launch_bounds__(256) k_ss_combine(SSParams p) {
+__device__ __forceinline__ void ss_lse_add(float& mx, float& sum, float ms, float ls) {
+  if (ms == -INFINITY) return;
+  if (ms > mx) { sum = sum * exp2f(mx - ms) + ls; mx = ms; }
+  else sum += ls * exp2f(ms - mx);
+}
+
+template <bool SPLIT>
+__global__ void __launch_bounds__(256) k_ss_combine(SSParams p, int rbmax) {
   __shared__ float red[256];
   const int nv = *p.nvp;
   const int ic = blockIdx.x * blockDim.x + threadIdx.x;
   float li = 0.f;
   if (ic < nv) {
-    float mx = -INFINITY;
-    for (int s = 0; s < p.nslices; ++s) mx = fmaxf(mx, p.pm[(int64_t)s * p.M + ic]);
-    float sum = 0.f;
-    for (int s = 0; s < p.nslices; ++s) {
-      const float ms = p.pm[(int64_t)s * p.M + ic];
-      if (ms != -INFINITY) sum += p.pl[(int64_t)s * p.M + ic] * exp2f(ms - mx);
+    float mx = -INFINITY, sum = 0.f;
+    if constexpr (SPLIT) {   // k_ss_fwd2's slots: per slice, its piece(s) in workgroup order
+      const int b = ic / kSS2Rows, row = ic % kSS2Rows;
+      for (int x = 0; x < 8; ++x) {
+        const SS2Split sp(nv, x);
+        if (sp.tx == 0) continue;
+        const int64_t x0 = (int64_t)b * sp.tx;
+        const int ja = sp.owner(x0), jb = sp.owner(x0 + sp.tx - 1);
+        if (ja == jb) {
+          const int64_t at = ss2_fslot(x, b, rbmax) + row;
+          ss_lse_add(mx, sum, p.pm[at], p.pl[at]);
+          continue;
+        }
+        for (int jj = ja; jj <= jb; ++jj) {
+          if (sp.start(jj + 1) == sp.start(jj)) continue;   // an empty range
+          const int64_t at = ss2_wslot(x + 8 * jj, sp.start(jj) >= x0 ? 0 : 1, rbmax) + row;
+          ss_lse_add(mx, sum, p.pm[at], p.pl[at]);
+        }
+      }
+    } else {
+      for (int s = 0; s < p.nslices; ++s) mx = fmaxf(mx, p.pm[(int64_t)s * p.M + ic]);
+      for (int s = 0; s < p.nslices; ++s) {
+        const float ms = p.pm[(int64_t)s * p.M + ic];
+        if (ms != -INFINITY) sum += p.pl[(int64_t)s * p.M + ic] * exp2f(ms - mx);
+      }
     }
     const float l2 = mx + log2f(sum);
     p.lse2[ic] = l2;
@@ -566,158 +632,226 @@ constexpr int kSSBNst = 3;
 constexpr int kSSBRed = kSSBRg * kSSBNw * 4 * 64 * 16;          // float4 partials [wave][quad][lane]
 constexpr int kSSBGx = kSSBRg * kSSBNw * (kSSBEpw / 2) * 2 * 64 * 4;   // G words [wave][word][lane]
 
-template <int P, int NST>
-__device__ __forceinline__ void ssb_wait(int ahead) { ring_wait<P, NST>(ahead); }
+// Work split (stream-K): the 2 x RB row blocks (RB = ceil(nv / 64) per direction) times
+// nt column tiles are one linear range of "units" cut evenly over kSSBGrid persistent
+// workgroups (one per CU; the LDS holds one), so no CU idles through a second, partial
+// wave of workgroups (426 blocks on 256 CUs at C2 ran 2 rounds for 1.66 rounds of work).
+// A workgroup's range crosses at most two block boundaries: a block wholly inside it is
+// written out directly; a block cut between workgroups leaves one partial per piece in
+// the workspace (slot 0 = the workgroup's first piece, 1 = its last) and k_ss_bwd_fix
+// sums them in workgroup order.
+constexpr int kSSBGrid = 256;
+constexpr int kSSBPart = kSSBRows * 512;        // floats per partial slot
+
+struct SSBSplit {
+  int rb, nt;
+  int64_t units;
+  __device__ SSBSplit(int nv) : rb((nv + kSSBRows - 1) / kSSBRows), nt((nv + 31) / 32) { units = (int64_t)2 * rb * nt; }
+  __device__ int64_t start(int g) const { return (int64_t)g * units / kSSBGrid; }
+  __device__ int owner(int64_t x) const {   // the workgroup whose range holds unit x
+    int g = (int)(x * kSSBGrid / max(units, (int64_t)1));
+    while (g + 1 < kSSBGrid && start(g + 1) <= x) ++g;
+    while (g > 0 && start(g) > x) --g;
+    return g;
+  }
+};
 
 __global__ void __launch_bounds__(512) k_ss_bwd2(SSParams p) {
-  constexpr int D = 512, NW = kSSBNw, DQ = D / NW, KSQ = DQ / 16, NDT = DQ / 32, NST = kSSBNst, EPW = kSSBEpw;
+  constexpr int D = 512, NW = kSSBNw, DQ = D / NW, KSQ = DQ / 16, NDT = DQ / 32, NST = kSSBNst, EPW = kSSBEpw, P = 5;
   __shared__ __attribute__((aligned(16))) char smem[NST * kSS2Stage + kSSBRed + kSSBGx];
   float4* red = reinterpret_cast<float4*>(smem + NST * kSS2Stage);
   uint32_t* gx = reinterpret_cast<uint32_t*>(smem + NST * kSS2Stage + kSSBRed);
   const int nv = *p.nvp;
-  const int oc0 = blockIdx.x * kSSBRows;
-  if (oc0 >= nv) return;
-  const bool rows = blockIdx.y == 0;
+  const SSBSplit sp(nv);
+  const int g = blockIdx.x;
+  const int64_t u0 = sp.start(g), u1 = sp.start(g + 1);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const int rg = wave / NW, ws = wave % NW;
-  const int oc = oc0 + rg * 32 + r;
-  const bool ook = oc < nv;
-  const int64_t oid = ook ? p.idc[oc] : -2;
-  const uint32_t olo = (uint32_t)oid;
-  // exponent offset of element (row i, column j) = lse2_i + log2 q_j: the own row's part
-  // here, the tile row's part in the tile's meta (log2 q of e rows, or lse2 of h rows)
-  const float olse = ook ? (rows ? p.lsec[oc] : p.lqc[oc]) : 0.f;
-  const bf16_t* own = rows ? p.hc : p.ec;
-  const bf16_t* tsrc = rows ? p.ec : p.hc;
-  const float* tmeta = rows ? p.lqc : p.lsec;
   const int col0 = ws * DQ;
-  bf16x8 of[KSQ];
-#pragma unroll
-  for (int ks = 0; ks < KSQ; ++ks) of[ks] = gload8(own + (int64_t)oc * D + col0 + 16 * ks + 8 * hh, ook);
   const float coef = (p.grad_loss ? *p.grad_loss : 1.f) / (float)max(nv, 1) * (p.sl2 / kLog2e);
-  f32x16 acc[NDT];
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) acc[dt] = acc_zero();
   const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane(
       (int)((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem));
   const int wu = __builtin_amdgcn_readfirstlane(wave);
-  const int nt = (nv + 31) / 32;
-  auto issue = [&](int t, int buf) {   // 4 tile rows per wave, the meta by wave 0
-    const unsigned base = lds0 + buf * kSS2Stage;
-    const int t0 = t * 32;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = wu * 4 + i;
-      const int srow = min(t0 + row, nv - 1);
-      wg_dma16(tsrc + (int64_t)srow * D + 8 * lane, base + row * kSS2Row);
-    }
-    if (wu == 0) {
-      const bf16_t* meta = lane >= 16 && lane < 24 ? (const bf16_t*)(tmeta + t0 + 4 * (lane - 16))
-                                                   : (const bf16_t*)(p.idc + t0 + 2 * (lane & 15));
-      wg_dma16(meta, base + kSS2Img);
-    }
-  };
-  for (int i = 0; i < NST - 1 && i < nt; ++i) issue(i, i);
   float4* red_mine = red + wave * 4 * 64 + lane;                 // [wave][quad][lane]
   const float4* red_q = red + (rg * NW) * 4 * 64 + ws * 64 + lane;   // quad ws of this row group's waves
   uint32_t* gx_mine = gx + wave * EPW * 64 + lane;               // [wave][word][lane]: EPW/2 hi, EPW/2 lo
   const uint32_t* gx_grp = gx + (rg * NW) * EPW * 64 + lane;
-  for (int i = 0; i < nt; ++i) {
-    if (wu == 0) ssb_wait<5, NST>(nt - 1 - i);
-    else ssb_wait<4, NST>(nt - 1 - i);
-    if (i + NST - 1 < nt) issue(i + NST - 1, (i + NST - 1) % NST);
-    const char* img = smem + (i % NST) * kSS2Stage;
-    const int64_t* tid = reinterpret_cast<const int64_t*>(img + kSS2Img);
-    const uint32_t* tid32 = reinterpret_cast<const uint32_t*>(img + kSS2Img);
-    const float* tlse = reinterpret_cast<const float*>(img + kSS2Img + 256);
-    const int tb = i * 32;
-    f32x16 s = acc_zero();
-    bf16x8 af[kSSPre];
+  for (int64_t u = u0; u < u1;) {
+    const int blk = (int)(u / sp.nt);
+    const int t0 = (int)(u - (int64_t)blk * sp.nt);
+    const int64_t ue = min(u1, (int64_t)(blk + 1) * sp.nt);
+    const int n = (int)(ue - u);
+    const bool first = u == u0;
+    u = ue;
+    const bool rows = blk < sp.rb;
+    const int oc0 = (rows ? blk : blk - sp.rb) * kSSBRows;
+    const int oc = oc0 + rg * 32 + r;
+    const bool ook = oc < nv;
+    const int64_t oid = ook ? p.idc[oc] : -2;
+    const uint32_t olo = (uint32_t)oid;
+    // exponent offset of element (row i, column j) = lse2_i + log2 q_j: the own row's part
+    // here, the tile row's part in the tile's meta (log2 q of e rows, or lse2 of h rows)
+    const float olse = ook ? (rows ? p.lsec[oc] : p.lqc[oc]) : 0.f;
+    const bf16_t* own = rows ? p.hc : p.ec;
+    const bf16_t* tsrc = rows ? p.ec : p.hc;
+    const float* tmeta = rows ? p.lqc : p.lsec;
+    bf16x8 of[KSQ];
 #pragma unroll
-    for (int ks = 0; ks < kSSPre; ++ks) af[ks] = ss_row8(img, r, col0 + 16 * ks + 8 * hh);
+    for (int ks = 0; ks < KSQ; ++ks) of[ks] = gload8(own + (int64_t)oc * D + col0 + 16 * ks + 8 * hh, ook);
+    f32x16 acc[NDT];
 #pragma unroll
-    for (int ks = 0; ks < KSQ; ++ks) {
-      const bf16x8 a = af[ks % kSSPre];
-      if (ks + kSSPre < KSQ) af[ks % kSSPre] = ss_row8(img, r, col0 + 16 * (ks + kSSPre) + 8 * hh);
-      s = mfma(a, of[ks], s);
-    }
+    for (int dt = 0; dt < NDT; ++dt) acc[dt] = acc_zero();
+    auto issue = [&](int t, int buf) {   // 4 tile rows per wave + the meta (every wave, same bytes)
+      const unsigned base = lds0 + buf * kSS2Stage;
+      const int tr0 = t * 32;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) red_mine[64 * q] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
-    // the product's fragments of the first half tile, read while the partials travel
-    bf16x8 tfs[NDT];
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) tfs[dt] = ss_tr8(img, 0, col0 + 32 * dt, lane);
-    lds_barrier();
-    // this wave's EPW scores (elements 4 ws .. 4 ws + 3 = quad ws), the quarters in D order
-    float se[EPW];
-    {
-      float4 t = red_q[0];
-#pragma unroll
-      for (int w = 1; w < NW; ++w) {
-        const float4 u = red_q[w * 4 * 64];
-        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+      for (int i = 0; i < 4; ++i) {
+        const int row = wu * 4 + i;
+        const int srow = min(tr0 + row, nv - 1);
+        wg_dma16(tsrc + (int64_t)srow * D + 8 * lane, base + row * kSS2Row);
       }
-      se[0] = t.x; se[1] = t.y; se[2] = t.z; se[3] = t.w;
-    }
-    const bool full = tb + 32 <= nv;
-    float g[EPW];
-    bool lodup = false;
+      const bf16_t* meta = lane >= 16 && lane < 24 ? (const bf16_t*)(tmeta + tr0 + 4 * (lane - 16))
+                                                   : (const bf16_t*)(p.idc + tr0 + 2 * (lane & 15));
+      wg_dma16(meta, base + kSS2Img);
+    };
+    // every wave is past the previous piece's reads of the ring and hand-off buffers
+    lds_barrier();
+    issue(t0, 0);
+    if (n > 1) issue(t0 + 1, 1);
+    if (n > 1) wg_wait_barrier<P>();
+    else wg_wait_barrier<0>();
+    for (int i = 0; i < n; ++i) {
+      const char* img = smem + (i % NST) * kSS2Stage;
+      const int64_t* tid = reinterpret_cast<const int64_t*>(img + kSS2Img);
+      const uint32_t* tid32 = reinterpret_cast<const uint32_t*>(img + kSS2Img);
+      const float* tlse = reinterpret_cast<const float*>(img + kSS2Img + 256);
+      const int tb = (t0 + i) * 32;
+      f32x16 s = acc_zero();
+      bf16x8 af[kSSPre];
 #pragma unroll
-    for (int e = 0; e < EPW; ++e) {
-      // element k = 4 ws + e: acc_row = (k & 3) + 8 (k >> 2) + 4 hh = e + 8 ws + 4 hh
-      const int tr = e + 8 * ws + 4 * hh, tc = tb + tr;
-      const bool same = tid32[2 * tr] == olo;   // ids compared on their low words (one register)
-      const bool ok = ook & (full | (tc < nv)) & ((tc == oc) | !same);
-      lodup |= ook & same & (tc != oc);
-      const float pr = __builtin_amdgcn_exp2f(fmaf(se[e], p.sl2, -(olse + tlse[tr])));
-      g[e] = ok ? (tc == oc ? pr - 1.f : pr) * coef : 0.f;
-    }
-    if (__builtin_expect(__ballot(lodup) != 0, 0)) {   // a low-word match: the full ids decide (rare)
+      for (int ks = 0; ks < kSSPre; ++ks) af[ks] = ss_row8(img, r, col0 + 16 * ks + 8 * hh);
+#pragma unroll
+      for (int ks = 0; ks < KSQ; ++ks) {
+        const bf16x8 a = af[ks % kSSPre];
+        if (ks + kSSPre < KSQ) af[ks % kSSPre] = ss_row8(img, r, col0 + 16 * (ks + kSSPre) + 8 * hh);
+        s = mfma(a, of[ks], s);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red_mine[64 * q] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
+      // the product's fragments of the first half tile, read while the partials travel
+      bf16x8 tfs[NDT];
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) tfs[dt] = ss_tr8(img, 0, col0 + 32 * dt, lane);
+      lds_barrier();
+      // every wave is past tile i - 1's product: its stage takes tile i + 2
+      if (i + 2 < n) issue(t0 + i + 2, (i + 2) % NST);
+      // this wave's EPW scores (elements 4 ws .. 4 ws + 3 = quad ws), the quarters in D order
+      float se[EPW];
+      {
+        float4 t = red_q[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) {
+          const float4 v = red_q[w * 4 * 64];
+          t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+        }
+        se[0] = t.x; se[1] = t.y; se[2] = t.z; se[3] = t.w;
+      }
+      const bool full = tb + 32 <= nv;
+      float gv[EPW];
+      bool lodup = false;
 #pragma unroll
       for (int e = 0; e < EPW; ++e) {
+        // element k = 4 ws + e: acc_row = (k & 3) + 8 (k >> 2) + 4 hh = e + 8 ws + 4 hh
         const int tr = e + 8 * ws + 4 * hh, tc = tb + tr;
-        const bool ok = ook & (full | (tc < nv)) & ((tc == oc) | (tid[tr] != oid));
+        const bool same = tid32[2 * tr] == olo;   // ids compared on their low words (one register)
+        const bool ok = ook & (full | (tc < nv)) & ((tc == oc) | !same);
+        lodup |= ook & same & (tc != oc);
         const float pr = __builtin_amdgcn_exp2f(fmaf(se[e], p.sl2, -(olse + tlse[tr])));
-        g[e] = ok ? (tc == oc ? pr - 1.f : pr) * coef : 0.f;
+        gv[e] = ok ? (tc == oc ? pr - 1.f : pr) * coef : 0.f;
+      }
+      if (__builtin_expect(__ballot(lodup) != 0, 0)) {   // a low-word match: the full ids decide (rare)
+#pragma unroll
+        for (int e = 0; e < EPW; ++e) {
+          const int tr = e + 8 * ws + 4 * hh, tc = tb + tr;
+          const bool ok = ook & (full | (tc < nv)) & ((tc == oc) | (tid[tr] != oid));
+          const float pr = __builtin_amdgcn_exp2f(fmaf(se[e], p.sl2, -(olse + tlse[tr])));
+          gv[e] = ok ? (tc == oc ? pr - 1.f : pr) * coef : 0.f;
+        }
+      }
+#pragma unroll
+      for (int e2 = 0; e2 < EPW / 2; ++e2) {
+        uint32_t hw, lw;
+        split2(f32x2{gv[2 * e2], gv[2 * e2 + 1]}, hw, lw);
+        gx_mine[64 * e2] = hw;
+        gx_mine[64 * (EPW / 2 + e2)] = lw;
+      }
+      // tile i + 1 landed (tile i + 2 may stay in flight) and every G word is written
+      if (i + 2 < n) wg_wait_barrier<P>();
+      else wg_wait_barrier<0>();
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        // G words of elements 8 s2 .. 8 s2 + 7: pairs 2 pp of wave w = k / EPW
+        uint32_t hw[4], lw[4];
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+          const int k = 8 * s2 + 2 * pp, w = k / EPW, kk = k % EPW;
+          hw[pp] = gx_grp[(w * EPW + kk / 2) * 64];
+          lw[pp] = gx_grp[(w * EPW + EPW / 2 + kk / 2) * 64];
+        }
+        const bf16x8 gh = words8(hw), gl = words8(lw);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const bf16x8 tf = tfs[dt];
+          if (s2 == 0) tfs[dt] = ss_tr8(img, 16, col0 + 32 * dt, lane);   // the second half's, under these MFMAs
+          acc[dt] = mfma(tf, gh, acc[dt]);
+          acc[dt] = mfma(tf, gl, acc[dt]);
+        }
       }
     }
-#pragma unroll
-    for (int e2 = 0; e2 < EPW / 2; ++e2) {
-      uint32_t hw, lw;
-      split2(f32x2{g[2 * e2], g[2 * e2 + 1]}, hw, lw);
-      gx_mine[64 * e2] = hw;
-      gx_mine[64 * (EPW / 2 + e2)] = lw;
+    if (!ook) continue;
+    float* out;
+    if (t0 == 0 && n == sp.nt) {   // the whole block in this workgroup: final rows
+      const int pos = p.vidx[oc];
+      out = rows ? p.dh + (int64_t)pos * p.lddh : p.de + (int64_t)pos * p.ldde;
+    } else {
+      out = p.part + (int64_t)(2 * g + (first ? 0 : 1)) * kSSBPart + (int64_t)(rg * 32 + r) * D;
     }
-    lds_barrier();
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      // G words of elements 8 s2 .. 8 s2 + 7: pairs 2 pp of wave w = k / EPW
-      uint32_t hw[4], lw[4];
+    for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-      for (int pp = 0; pp < 4; ++pp) {
-        const int k = 8 * s2 + 2 * pp, w = k / EPW, kk = k % EPW;
-        hw[pp] = gx_grp[(w * EPW + kk / 2) * 64];
-        lw[pp] = gx_grp[(w * EPW + EPW / 2 + kk / 2) * 64];
-      }
-      const bf16x8 gh = words8(hw), gl = words8(lw);
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const bf16x8 tf = tfs[dt];
-        if (s2 == 0) tfs[dt] = ss_tr8(img, 16, col0 + 32 * dt, lane);   // the second half's, under these MFMAs
-        acc[dt] = mfma(tf, gh, acc[dt]);
-        acc[dt] = mfma(tf, gl, acc[dt]);
-      }
-    }
+      for (int g4 = 0; g4 < 4; ++g4)
+        *reinterpret_cast<float4*>(out + col0 + 32 * dt + 8 * g4 + 4 * hh) =
+            make_float4(acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]);
   }
-  if (!ook) return;
-  const int pos = p.vidx[oc];
-  float* out = rows ? p.dh + (int64_t)pos * p.lddh : p.de + (int64_t)pos * p.ldde;
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4)
-      *reinterpret_cast<float4*>(out + col0 + 32 * dt + 8 * g4 + 4 * hh) =
-          make_float4(acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]);
+}
+
+// The blocks k_ss_bwd2 cut between workgroups: their pieces summed in workgroup order.
+// Grid: 2 x ceil(M / 64) blocks (rows, then columns), 256 threads.
+__global__ void __launch_bounds__(256) k_ss_bwd_fix(SSParams p, int rbmax) {
+  const int nv = *p.nvp;
+  const SSBSplit sp(nv);
+  const bool rows = (int)blockIdx.x < rbmax;
+  const int rb = rows ? blockIdx.x : blockIdx.x - rbmax;
+  if (rb >= sp.rb) return;
+  const int blk = rows ? rb : sp.rb + rb;
+  const int64_t x0 = (int64_t)blk * sp.nt, x1 = x0 + sp.nt - 1;
+  const int ga = sp.owner(x0), gb = sp.owner(x1);
+  if (ga == gb) return;   // written by its workgroup
+  for (int c = threadIdx.x; c < kSSBRows * 128; c += 256) {
+    const int row = c >> 7, c4 = c & 127;
+    const int oc = rb * kSSBRows + row;
+    if (oc >= nv) break;   // rows ascend with c
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int w = ga; w <= gb; ++w) {
+      if (sp.start(w + 1) == sp.start(w)) continue;   // an empty range (units < workgroups)
+      const int slot = sp.start(w) >= x0 ? 0 : 1;
+      const float4 v = reinterpret_cast<const float4*>(p.part + (int64_t)(2 * w + slot) * kSSBPart + (int64_t)row * 512)[c4];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    const int pos = p.vidx[oc];
+    float* out = rows ? p.dh + (int64_t)pos * p.lddh : p.de + (int64_t)pos * p.ldde;
+    reinterpret_cast<float4*>(out)[c4] = t;
+  }
 }
 
 // which: 0 = compaction gather + forward, 1 = compaction gather + backward
@@ -729,17 +863,19 @@ static int ss_launch(const SSParams& p, int which, hipStream_t s) {
     k_ss_diag<D><<<(unsigned)((p.M + 3) / 4), 256, 0, s>>>(p);
     GRK_LAUNCH_CHECK();
     if constexpr (D == 512) {
-      const int rblocks = (p.M + kSS2Rows - 1) / kSS2Rows;
-      const unsigned g = (unsigned)(rblocks * kSS2Slices);
-      if (p.logq) k_ss_fwd2<true><<<g, 512, 0, s>>>(p, rblocks);
-      else k_ss_fwd2<false><<<g, 512, 0, s>>>(p, rblocks);
+      const int rbmax = (p.M + kSS2Rows - 1) / kSS2Rows;
+      if (p.logq) k_ss_fwd2<true><<<kSS2Grid, 512, 0, s>>>(p, rbmax);
+      else k_ss_fwd2<false><<<kSS2Grid, 512, 0, s>>>(p, rbmax);
     } else {
       const dim3 grid((unsigned)((p.M + kSSFwdRows - 1) / kSSFwdRows), p.nslices);
       if (p.logq) k_ss_fwd<D, true><<<grid, 256, 0, s>>>(p);
       else k_ss_fwd<D, false><<<grid, 256, 0, s>>>(p);
     }
   } else if constexpr (D == 512) {
-    k_ss_bwd2<<<dim3((unsigned)((p.M + kSSBRows - 1) / kSSBRows), 2), 512, 0, s>>>(p);
+    k_ss_bwd2<<<kSSBGrid, 512, 0, s>>>(p);
+    GRK_LAUNCH_CHECK();
+    const int rbmax = (p.M + kSSBRows - 1) / kSSBRows;
+    k_ss_bwd_fix<<<(unsigned)(2 * rbmax), 256, 0, s>>>(p, rbmax);
   } else {
     k_ss_bwd<D><<<dim3((unsigned)((p.M + SSB<D>::ROWS - 1) / SSB<D>::ROWS), 2), SSB<D>::NT, 0, s>>>(p);
   }
@@ -760,7 +896,7 @@ static int ss_dispatch(const SSParams& p, int dim, int which, hipStream_t s) {
 }
 
 static int ss_slices(int M, int D) {
-  if (D == 512) return kSS2Slices;   // k_ss_fwd2
+  if (D == 512) return 8;   // k_ss_fwd2: one column slice per XCD
   // forward column slices: ~1k workgroups when every position is valid
   // (half of them, ~2 per CU, at C2's ~53 % valid)
   const int rb = (M + kSSFwdRows - 1) / kSSFwdRows;
@@ -775,7 +911,7 @@ struct SSWs {
   int* nv;
   bf16_t *hc, *ec;
   int64_t* idc;
-  float *lqc, *lsec, *pm, *pl, *diag, *partials;
+  float *lqc, *lsec, *pm, *pl, *diag, *partials, *part;
   size_t bytes;
 };
 
@@ -796,10 +932,14 @@ static SSWs ss_ws(char* base, int M, int D) {
   w.idc = (int64_t*)take((size_t)(M + kSS2Pad) * 8);   // k_ss_fwd2's meta DMA reads whole 32-row tiles
   w.lqc = (float*)take((size_t)(M + kSS2Pad) * 4);
   w.lsec = (float*)take((size_t)(M + kSS2Pad) * 4);
-  w.pm = (float*)take((size_t)ns * M * 4);
-  w.pl = (float*)take((size_t)ns * M * 4);
+  // (max, sum) slots: ns slices x M rows, or k_ss_fwd2's F + W slots
+  const size_t nslot = D == 512 ? ((size_t)8 * ((M + kSS2Rows - 1) / kSS2Rows) + 2 * kSS2Grid) * kSS2Rows
+                                : (size_t)ns * M;
+  w.pm = (float*)take(nslot * 4);
+  w.pl = (float*)take(nslot * 4);
   w.diag = (float*)take((size_t)M * 4);
   w.partials = (float*)take((size_t)nb * 4);
+  w.part = D == 512 ? (float*)take((size_t)kSSBGrid * 2 * kSSBPart * 4) : nullptr;
   w.bytes = off;
   return w;
 }
@@ -851,7 +991,8 @@ extern "C" int grk_sampled_softmax_fwd(const void* h, int64_t ldh, const void* e
   rc = ss_dispatch(p, dim, 0, s);
   if (rc) return rc;
   const int nb = (p.M + 255) / 256;
-  k_ss_combine<<<nb, 256, 0, s>>>(p);
+  if (dim == 512) k_ss_combine<true><<<nb, 256, 0, s>>>(p, (p.M + kSS2Rows - 1) / kSS2Rows);
+  else k_ss_combine<false><<<nb, 256, 0, s>>>(p, 0);
   GRK_LAUNCH_CHECK();
   k_ss_finalize<<<1, 1024, 0, s>>>(p, nb);
   GRK_LAUNCH_CHECK();
@@ -872,7 +1013,7 @@ extern "C" int grk_sampled_softmax_bwd(const void* h, int64_t ldh, const void* e
   GRK_CHECK_ARG(lddh >= dim && ldde >= dim && lddh % 4 == 0 && ldde % 4 == 0, "lddh / ldde must be >= dim, multiple of 4");
   GRK_CHECK_ARG(((uintptr_t)dh | (uintptr_t)de) % 16 == 0, "dh / de must be 16-byte aligned");
   p.lse2 = const_cast<float*>(lse2); p.grad_loss = grad_loss;
-  if (dim == 512) p.lsec = w.lsec;   // k_ss_bwd2 stages the tile rows' lse2 by DMA from a padded copy
+  if (dim == 512) { p.lsec = w.lsec; p.part = w.part; }   // k_ss_bwd2 stages the tile rows' lse2 by DMA from a padded copy
   p.dh = dh; p.lddh = lddh; p.de = de; p.ldde = ldde;
   hipStream_t s = (hipStream_t)stream;
   // rows of positions that are not valid stay zero
