@@ -764,6 +764,122 @@ __global__ void __launch_bounds__(256) k_seg_partials_combine(const unsigned* __
   store_final(acc, key, u, dim, c, dense_out, uniq_rows, row_slot);
 }
 
+// ------------------------------------ chunked mode, column-sliced by XCD ----
+// The projected feature rows' backward (dim 512, bf16 gradient rows, dense
+// output only: ~860k occurrences over ~41k distinct gradient rows per call at
+// C2).  k_seg_chunks_partial reads each occurrence's whole 1 KiB row: every XCD
+// sees random rows of the whole ~41 MB gradient, its 4 MiB L2 misses nearly all
+// of them, and PMC counted ~8x the algorithmic bytes.  Here workgroup w runs on
+// XCD w % 8 and handles only column slice x = w % 8 (64 columns = one 128-byte
+// line per row), so an XCD's working set is 1/8 of the gradient (~5 MB).  A wave
+// takes 8 consecutive chunks, one per 8-lane group (8 bf16 columns per lane);
+// each group walks its chunk exactly as k_seg_chunks_partial's wave does (same
+// pieces, same head / tail partial slots, same in-order fp32 adds per column),
+// so the output is bitwise the same.  A batch of 64 occurrences' keys and row
+// addresses per group goes through LDS (a wave's own region: no barrier).
+#ifndef GRK_COLS_PIPE
+#define GRK_COLS_PIPE 16   // rows in flight per lane (A/B builds: 8)
+#endif
+template <int CH, typename OT>
+__global__ void __launch_bounds__(256) k_seg_chunks_cols(const unsigned* __restrict__ keys,
+                                                         const unsigned long long* __restrict__ gptr, int64_t n,
+                                                         unsigned sentinel, OT* __restrict__ dense_out,
+                                                         float* __restrict__ partials) {
+  constexpr int dim = 512, PIPE = GRK_COLS_PIPE;
+  __shared__ unsigned skey[4][8][64];              // [wave][group][batch entry]
+  __shared__ unsigned long long sptr[4][8][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gi = lane >> 3, sub = lane & 7;
+  const int x = blockIdx.x & 7;
+  const int64_t chunk = ((int64_t)(blockIdx.x >> 3) * 4 + wave) * 8 + gi;
+  const int c = x * 64 + sub * 8;
+  const int64_t p0 = chunk * CH;
+  const bool live = p0 < n;
+  const int64_t p1 = live ? min(n, p0 + CH) : p0;
+  unsigned cur = live ? keys[p0] : sentinel;
+  bool done = cur == sentinel;
+  if (__ballot(!done) == 0) return;
+  const unsigned kprev = live && p0 > 0 ? keys[p0 - 1] : sentinel;
+  const unsigned knext = live && p1 < n ? keys[p1] : sentinel;
+  const unsigned long long g0 = live ? gptr[p0] : gptr[0];   // stands in past p1
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  int ps = 0, pe = 0;   // the current piece [p0 + ps, p0 + pe)
+  const int len = (int)(p1 - p0);
+  auto flush = [&]() {
+    const bool whole = (ps > 0 || kprev != cur) && (pe < len || knext != cur);
+    if (whole) {
+      OT* d = dense_out + (int64_t)cur * dim + c;
+      if constexpr (sizeof(OT) == 2) {
+        uint4 t;
+        t.x = (unsigned)f32_to_bf16(acc[0]) | ((unsigned)f32_to_bf16(acc[1]) << 16);
+        t.y = (unsigned)f32_to_bf16(acc[2]) | ((unsigned)f32_to_bf16(acc[3]) << 16);
+        t.z = (unsigned)f32_to_bf16(acc[4]) | ((unsigned)f32_to_bf16(acc[5]) << 16);
+        t.w = (unsigned)f32_to_bf16(acc[6]) | ((unsigned)f32_to_bf16(acc[7]) << 16);
+        *reinterpret_cast<uint4*>(d) = t;
+      } else {
+        *reinterpret_cast<float4*>(d) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        *reinterpret_cast<float4*>(d + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+      }
+    } else {   // the piece's sum goes to the chunk's head (0) or tail (1) slot
+      const int slot = (ps == 0 && kprev == cur) ? 0 : 1;
+      float* dst = partials + (chunk * 2 + slot) * dim + c;
+      *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    }
+  };
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+  unsigned* mk = skey[wave][gi];
+  unsigned long long* mp = sptr[wave][gi];
+#pragma unroll 1
+  for (int b = 0; b < CH; b += 64) {
+    // the group's batch: entries b .. b + 63 of its chunk, 8 per lane
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = p0 + b + 8 * k + sub;
+      mk[8 * k + sub] = i < p1 ? keys[i] : sentinel;
+      mp[8 * k + sub] = i < p1 ? gptr[i] : g0;
+    }
+    __builtin_amdgcn_wave_barrier();   // LDS accesses of one wave run in order: no barrier beyond this fence
+#pragma unroll 1
+    for (int j0 = 0; j0 < 64; j0 += PIPE) {
+      u32x4 r[PIPE];
+      unsigned kk[PIPE];
+#pragma unroll
+      for (int j = 0; j < PIPE; ++j) {
+        kk[j] = mk[j0 + j];
+        r[j] = *reinterpret_cast<gu32x4*>(mp[j0 + j] + (unsigned long long)c * 2);
+      }
+#pragma unroll
+      for (int j = 0; j < PIPE; ++j) {
+        const unsigned kj = kk[j];
+        done = done || kj == sentinel;   // sorted: the rest of the chunk is padding / past the end
+        if (!done) {
+          const int at = b + j0 + j;
+          if (kj != cur) {
+            flush();
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+            cur = kj;
+            ps = at;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc[2 * e] += __uint_as_float(r[j][e] << 16);
+            acc[2 * e + 1] += __uint_as_float(r[j][e] & 0xFFFF0000u);
+          }
+          pe = at + 1;
+        }
+      }
+      if (__ballot(!done) == 0) break;
+    }
+    if (__ballot(!done) == 0) break;
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (live && pe > ps) flush();
+}
+
 // ------------------------------------------------------------- hot rows ----
 // Rows with more than 2 * kRedChunk occurrences (the rows of cardinality-10
 // feature tables take thousands per call), summed bit-exactly in occurrence
@@ -1438,7 +1554,27 @@ extern "C" int grk_embedding_backward(const grk_lookup* lookups, int num_lookups
     k_seg_partials_combine<LW, kPartialChunk><<<ge, 256, 0, s>>>(ws.keys_out, ws.pos, ws.seg_start, ws.seg_end,  \
                                                                  total, sentinel, dim, ws.partials, dense_out,    \
                                                                  uniq_rows, row_slot)
-      if (dense_out16) {
+      const bool cols = grad_dtype == GRK_BF16 && dim == 512 && !ws.pos && !uniq_rows && !row_slot;
+      if (cols) {   // column-sliced by XCD: same pieces and adds, an eighth of the rows' bytes per XCD
+        const unsigned gc = (unsigned)(8 * ((pchunks + 31) / 32));
+        if (dense_out16)
+          k_seg_chunks_cols<kPartialChunk, bf16_t><<<gc, 256, 0, s>>>(ws.keys_out, ws.gptr_out, total, sentinel,
+                                                                      dense_out16, ws.partials);
+        else
+          k_seg_chunks_cols<kPartialChunk, float><<<gc, 256, 0, s>>>(ws.keys_out, ws.gptr_out, total, sentinel,
+                                                                     dense_out, ws.partials);
+        GRK_LAUNCH_CHECK();
+        if (ge) {
+          if (dense_out16)
+            k_seg_partials_combine<8, kPartialChunk, bf16_t><<<ge, 256, 0, s>>>(
+                ws.keys_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel, dim, ws.partials, dense_out16,
+                uniq_rows, row_slot);
+          else
+            k_seg_partials_combine<8, kPartialChunk><<<ge, 256, 0, s>>>(ws.keys_out, ws.pos, ws.seg_start,
+                                                                       ws.seg_end, total, sentinel, dim, ws.partials,
+                                                                       dense_out, uniq_rows, row_slot);
+        }
+      } else if (dense_out16) {
         k_seg_chunks_partial<bf16_t, 8, kPartialChunk, bf16_t><<<gw, 256, 0, s>>>(
             ws.keys_out, ws.gptr_out, ws.pos, ws.seg_start, ws.seg_end, total, sentinel, dim, dense_out16, uniq_rows,
             row_slot, ws.partials);

@@ -676,13 +676,20 @@ __global__ void __launch_bounds__(512) k_ss_bwd2(SSParams p) {
   const float4* red_q = red + (rg * NW) * 4 * 64 + ws * 64 + lane;   // quad ws of this row group's waves
   uint32_t* gx_mine = gx + wave * EPW * 64 + lane;               // [wave][word][lane]: EPW/2 hi, EPW/2 lo
   const uint32_t* gx_grp = gx + (rg * NW) * EPW * 64 + lane;
-  for (int64_t u = u0; u < u1;) {
+  // The range is walked from its first block boundary on ([bnd, u1), then [u0, bnd)):
+  // the blocks a workgroup starts at tile 0 then run in step with the other workgroups
+  // of its XCD, which stream the same tiles at the same time through their shared L2
+  // (walked from u0, every workgroup sat at its own tile offset: PMC 3.3 GB per launch).
+  const int64_t bnd = u0 % sp.nt == 0 ? u0 : min(u1, (u0 / sp.nt + 1) * sp.nt);
+  for (int64_t q = 0; q < u1 - u0;) {
+    const int64_t u = q < u1 - bnd ? bnd + q : u0 + (q - (u1 - bnd));
+    const int64_t uend = q < u1 - bnd ? u1 : bnd;
     const int blk = (int)(u / sp.nt);
     const int t0 = (int)(u - (int64_t)blk * sp.nt);
-    const int64_t ue = min(u1, (int64_t)(blk + 1) * sp.nt);
+    const int64_t ue = min(uend, (int64_t)(blk + 1) * sp.nt);
     const int n = (int)(ue - u);
-    const bool first = u == u0;
-    u = ue;
+    const bool first = u == u0;   // slot 0: the piece holding the range's first unit
+    q += n;
     const bool rows = blk < sp.rb;
     const int oc0 = (rows ? blk : blk - sp.rb) * kSSBRows;
     const int oc = oc0 + rg * 32 + r;

@@ -324,6 +324,30 @@ def test_backward_chunked_mode(K, D, dt):
     assert torch.equal(again, res.dense)
 
 
+@pytest.mark.parametrize('n,R', [(1, 4), (200, 50), (8192 + 77, 900), (140000, 41952)])
+def test_backward_chunked_dense_only_column_sliced(K, n, R):
+    """The dense-only chunked call at d = 512 with bf16 gradient rows (the projected
+    feature rows' backward) runs k_seg_chunks_cols: per XCD one 64-column slice, 8
+    chunks per wave.  Bit-exact against the oracle's chunk-order restatement, in fp32
+    and as the bf16 rounding of it; sizes from one occurrence to a partial last group
+    of chunks and a C2-like spread (hot rows, rows crossing chunk edges, row 0)."""
+    rng = np.random.default_rng(n)
+    D = 512
+    if n < 1000:
+        idx = rng.integers(0, R, n)
+    else:
+        idx = np.concatenate([np.full(n // 7, 3), np.repeat(np.arange(10, 30), 300),
+                              rng.integers(0, R, n - n // 7 - 6000)])
+        rng.shuffle(idx)
+    g = oemb.to_bf16_f32(rng.standard_normal((len(idx), D)).astype(np.float32))
+    src = [K.GradSource(T(idx), T(g).to(torch.bfloat16), 0)]
+    want = oemb.chunked_backward(g, idx, R, chunk=K.chunked_size())
+    got = K.embedding_backward(src, R, D, dense=True, chunked=True).dense
+    assert np.array_equal(got.cpu().numpy(), want)
+    got16 = K.embedding_backward(src, R, D, dense=True, chunked=True, dense_dtype=torch.bfloat16).dense
+    assert torch.equal(got16, T(want).to(torch.bfloat16))
+
+
 def test_backward_chunked_bf16_dense_is_the_rounded_fp32_result(K):
     """GRK_BWD_DENSE_BF16: the dense rows are the chunked fp32 result rounded
     to bf16 once (round to nearest even, as torch's cast) -- bit-exact against
