@@ -118,7 +118,7 @@ def _time(fn, reps):
     return e0.elapsed_time(e1) / reps
 
 
-PMC_TAG = 'r5'  # round tag of the committed PMC summaries (scripts/pmc_rooflines.py)
+PMC_TAG = 'r6'  # round tag of the committed PMC summaries (scripts/pmc_rooflines.py)
 
 
 def _pmc(name, match):
