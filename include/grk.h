@@ -516,6 +516,16 @@ int grk_attention_bwd(const grk_attn_args* a, const void* out, int64_t ldo, cons
  * a half does not use may be NULL (DQ: dk/dv; DKDV: dq, drab). */
 #define GRK_ATTN_BWD_DQ 1
 #define GRK_ATTN_BWD_DKDV 2
+/* Flags for the DQ half (hstu with drab):
+ *   GRK_ATTN_BWD_WS_CLEAN -- drab_ws (int64 [H, nb] + ONE extra slot, a counter)
+ *                        and drab_t_ws are zero on entry and are left zero on
+ *                        return: no reset launch, and the whole-sequence dq
+ *                        kernel's last workgroup finalizes drab (no finalize
+ *                        launch).  A caller keeps one such scratch per stream;
+ *   GRK_ATTN_BWD_DRAB_SET -- drab / drab_t are written, not accumulated (the
+ *                        caller's buffers need no zero fill). */
+#define GRK_ATTN_BWD_WS_CLEAN 4
+#define GRK_ATTN_BWD_DRAB_SET 8
 int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
                             int dout_dtype, const float* lse, float* delta_ws, void* dq, int64_t lddq, void* dk,
                             int64_t lddk, void* dv, int64_t lddv, float* drab, int64_t* drab_ws, int parts,

@@ -112,6 +112,7 @@ class GrkStoreCol(C.Structure):
 STORE_SPARSE, STORE_ARRAY, STORE_MM = 0, 1, 2
 ATTN_SOFTMAX, ATTN_HSTU = 0, 1
 ATTN_BWD_DQ, ATTN_BWD_DKDV = 1, 2
+ATTN_BWD_WS_CLEAN, ATTN_BWD_DRAB_SET = 4, 8   # grk.h: clean drab scratch kept by the caller; drab written
 ACT_NONE, ACT_SILU = 0, 1
 
 

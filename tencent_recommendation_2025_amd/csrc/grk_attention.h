@@ -46,7 +46,11 @@ struct AttnParams {
   const float* delta;
   void *dq, *dk, *dv; int64_t lddq, lddk, lddv;
   float* drab;
+  unsigned* fin_count;   // non-null: the whole-sequence dq kernel's last workgroup finalizes
+                         // drab / drab_t from the fixed-point bins and leaves bins + counter zero
+  int drab_set;          // finalize writes drab / drab_t (1) or adds to them (0)
 };
+
 
 
 // Eight consecutive elements of a q/k/v/dO row as exact fp32 (dtype GRK_F32 /
@@ -223,6 +227,14 @@ constexpr double kFixScale = 4294967296.0;
 __device__ __forceinline__ unsigned long long to_fix(float v) {
   const double d = fmin(fmax((double)v * kFixScale, -9.0e18), 9.0e18);
   return (unsigned long long)(long long)d;
+}
+
+// drab[i] (+)= fix[i] / 2^32, fix[i] = 0: the fixed-point finalize, by the threads of
+// one workgroup (the last dq workgroup) or a grid.
+__device__ __forceinline__ void drab_finalize_elem(float* drab, unsigned long long* fix, int i, bool set) {
+  const unsigned long long v = atomicExch(&fix[i], 0ull);
+  const float x = (float)((double)(long long)v * (1.0 / kFixScale));
+  drab[i] = set ? x : drab[i] + x;
 }
 
 // Launch with `lds` bytes of dynamic LDS; above 64 KiB the kernel's limit is

@@ -504,6 +504,12 @@ __global__ void k_drab_finalize(float* __restrict__ drab, const unsigned long lo
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) drab[i] += (float)((double)(long long)fix[i] * (1.0 / kFixScale));
 }
+// GRK_ATTN_BWD_WS_CLEAN when the dq kernel was not the whole-sequence one: finalize
+// (set or add) and leave the bins zero.
+__global__ void k_drab_finalize_clean(float* __restrict__ drab, unsigned long long* __restrict__ fix, int n, int set) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) drab_finalize_elem(drab, fix, i, set);
+}
 
 static int launch(const AttnParams& p, int hd, int which, hipStream_t s) {
   if (p.qkv_f8 && p.row_base) {
@@ -625,8 +631,9 @@ extern "C" int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, 
   AttnParams p;
   int rc = fill_params(a, &p);
   if (rc) return rc;
-  GRK_CHECK_ARG(parts >= 1 && parts <= (GRK_ATTN_BWD_DQ | GRK_ATTN_BWD_DKDV), "bad parts (%d)", parts);
+  GRK_CHECK_ARG((parts & 3) >= 1 && parts <= 15, "bad parts (%d)", parts);
   const bool do_dq = parts & GRK_ATTN_BWD_DQ, do_dkdv = parts & GRK_ATTN_BWD_DKDV;
+  const bool clean = parts & GRK_ATTN_BWD_WS_CLEAN, dset = parts & GRK_ATTN_BWD_DRAB_SET;
   const int64_t need = (int64_t)a->heads * a->head_dim;
   GRK_CHECK_ARG(dout && lddo >= need && lddo % 8 == 0, "bad dout / lddo");
   GRK_CHECK_ARG(dout_dtype == GRK_F32 || dout_dtype == GRK_BF16, "bad dout dtype");
@@ -647,23 +654,49 @@ extern "C" int grk_attention_bwd_parts(const grk_attn_args* a, const void* out, 
   hipStream_t s = (hipStream_t)stream;
   if (do_dq) {
     const int nfix = a->heads * a->num_buckets;
-    if (p.drab) GRK_CHECK_HIP(zero_async(drab_ws, (size_t)nfix * 8, s));
-    if (p.drab_t) GRK_CHECK_HIP(zero_async(a->drab_t_ws, (size_t)a->heads * p.nbt * 8, s));
-    if (a->kind == GRK_ATTN_SOFTMAX) {
-      // out dtype of the forward output equals out_dtype of these args
-      rc = launch(p, a->head_dim, 1, s);
+    GRK_CHECK_ARG(!clean || a->kind != GRK_ATTN_HSTU || p.drab, "GRK_ATTN_BWD_WS_CLEAN needs drab and drab_ws");
+    if (clean && p.drab) {
+      // scratch zero on entry, left zero; the counter is the extra slot after the bins
+      bool fused = false;
+      if (!p.qkv_f8) {
+        AttnParams pf = p;
+        pf.fin_count = reinterpret_cast<unsigned*>(drab_ws + nfix);
+        pf.drab_set = dset;
+        fused = attn_seq_launch(pf, a->head_dim, 2, s);
+        if (fused) GRK_LAUNCH_CHECK();
+      }
+      if (!fused) {
+        rc = launch(p, a->head_dim, 2, s);
+        if (rc) return rc;
+        k_drab_finalize_clean<<<(nfix + 255) / 256, 256, 0, s>>>(p.drab, p.drab_fix, nfix, dset);
+        GRK_LAUNCH_CHECK();
+        if (p.drab_t) {
+          const int nt = a->heads * p.nbt;
+          k_drab_finalize_clean<<<(nt + 255) / 256, 256, 0, s>>>(p.drab_t, p.drab_t_fix, nt, dset);
+          GRK_LAUNCH_CHECK();
+        }
+      }
+    } else {
+      if (p.drab) GRK_CHECK_HIP(zero_async(drab_ws, (size_t)nfix * 8, s));
+      if (p.drab_t) GRK_CHECK_HIP(zero_async(a->drab_t_ws, (size_t)a->heads * p.nbt * 8, s));
+      if (dset && p.drab) GRK_CHECK_HIP(zero_async(p.drab, (size_t)nfix * 4, s));
+      if (dset && p.drab_t) GRK_CHECK_HIP(zero_async(p.drab_t, (size_t)a->heads * p.nbt * 4, s));
+      if (a->kind == GRK_ATTN_SOFTMAX) {
+        // out dtype of the forward output equals out_dtype of these args
+        rc = launch(p, a->head_dim, 1, s);
+        if (rc) return rc;
+      }
+      rc = launch(p, a->head_dim, 2, s);
       if (rc) return rc;
-    }
-    rc = launch(p, a->head_dim, 2, s);
-    if (rc) return rc;
-    if (p.drab) {
-      k_drab_finalize<<<(nfix + 255) / 256, 256, 0, s>>>(p.drab, p.drab_fix, nfix);
-      GRK_LAUNCH_CHECK();
-    }
-    if (p.drab_t) {
-      const int nt = a->heads * p.nbt;
-      k_drab_finalize<<<(nt + 255) / 256, 256, 0, s>>>(p.drab_t, p.drab_t_fix, nt);
-      GRK_LAUNCH_CHECK();
+      if (p.drab) {
+        k_drab_finalize<<<(nfix + 255) / 256, 256, 0, s>>>(p.drab, p.drab_fix, nfix);
+        GRK_LAUNCH_CHECK();
+      }
+      if (p.drab_t) {
+        const int nt = a->heads * p.nbt;
+        k_drab_finalize<<<(nt + 255) / 256, 256, 0, s>>>(p.drab_t, p.drab_t_fix, nt);
+        GRK_LAUNCH_CHECK();
+      }
     }
   }
   return do_dkdv ? launch(p, a->head_dim, 3, s) : GRK_OK;

@@ -850,14 +850,38 @@ __global__ void __launch_bounds__(64 * kSeqWaves) k_attn_dq_seq(AttnParams p) {
     }
   if (KIND == 1 && (p.drab || p.drab_t)) {
     __syncthreads();
+    // returning atomics (their old values are folded into chk): once chk is computed,
+    // this thread's adds are performed -- the order the last-workgroup finalize needs,
+    // without __threadfence (an agent-scope fence writes back / invalidates the XCD's
+    // L2 on gfx950: with one per workgroup, dq ran 61 -> 185 us)
+    unsigned long long chk = 0ull;
     if (p.drab)
       for (int d = threadIdx.x; d < Tp; d += blockDim.x) {
         const unsigned long long q = bins[kRabPad + d];
-        if (q != 0) atomicAdd(&p.drab_fix[h * p.nb + min(d, p.nb - 1)], q);
+        if (q != 0) chk ^= atomicAdd(&p.drab_fix[h * p.nb + min(d, p.nb - 1)], q);
       }
     if (p.drab_t)
       for (int j = threadIdx.x; j < p.nbt; j += blockDim.x)
-        if (L.tbins[j] != 0ull) atomicAdd(&p.drab_t_fix[h * p.nbt + j], L.tbins[j]);
+        if (L.tbins[j] != 0ull) chk ^= atomicAdd(&p.drab_t_fix[h * p.nbt + j], L.tbins[j]);
+    if (p.fin_count) {
+      // the last workgroup to finish finalizes drab / drab_t and leaves the bins and the
+      // counter zero (GRK_ATTN_BWD_WS_CLEAN): no reset and no finalize launch per call.
+      // The flag lives in the bins' LDS, read out above.
+      int* last = reinterpret_cast<int*>(bins);
+      __syncthreads();
+      if (chk == 0x9E3779B97F4A7C15ull) last[1] = 1;   // keeps chk (and the wait on the adds) alive
+      if (threadIdx.x == 0) *last = atomicAdd(p.fin_count, 1u) == gridDim.x - 1;
+      __syncthreads();
+      if (*last) {
+        if (p.drab)
+          for (int i = threadIdx.x; i < p.H * p.nb; i += blockDim.x)
+            drab_finalize_elem(p.drab, p.drab_fix, i, p.drab_set);
+        if (p.drab_t)
+          for (int i = threadIdx.x; i < p.H * p.nbt; i += blockDim.x)
+            drab_finalize_elem(p.drab_t, p.drab_t_fix, i, p.drab_set);
+        if (threadIdx.x == 0) atomicExch(p.fin_count, 0u);
+      }
+    }
   }
 }
 

@@ -754,26 +754,48 @@ def attention_fwd(args, out, lse=None):
     L.check(rc, 'grk_attention_fwd')
 
 
+_CLEAN_WS = {}
+
+
+def _clean_ws(n, device):
+    """An int64 [n] scratch that grk leaves zero after every GRK_ATTN_BWD_WS_CLEAN call,
+    one per (device, stream, size): zeroed once here, never again per call."""
+    key = (str(device), L.stream_ptr(device), int(n))
+    t = _CLEAN_WS.get(key)
+    if t is None:
+        t = _CLEAN_WS[key] = torch.zeros(int(n), dtype=torch.int64, device=device)
+    return t
+
+
 def attention_bwd(args, out, dout, lse, delta, dq, dk, dv, drab=None, parts=L.ATTN_BWD_DQ | L.ATTN_BWD_DKDV,
-                  drab_t=None):
+                  drab_t=None, drab_set=False):
     """grk_attention_bwd(_parts): writes dq/dk/dv (args.out_dtype) and accumulates drab
     (and, with a time bias, drab_t) deterministically.  ``parts`` selects the dq half
     (L.ATTN_BWD_DQ: delta, dq, drab, drab_t) and/or the dk/dv half (L.ATTN_BWD_DKDV);
-    tensors of a half not run may be None."""
+    tensors of a half not run may be None.  drab_set: drab / drab_t are written, not
+    accumulated (no zero fill needed), through this stream's clean fixed-point scratch
+    (GRK_ATTN_BWD_WS_CLEAN: no reset launch; the whole-sequence dq kernel's last
+    workgroup finalizes them, no finalize launch)."""
     _require_cuda(dout, dq, dk, dv, drab, drab_t)
+    clean = bool(drab_set) and drab is not None and bool(parts & L.ATTN_BWD_DQ)
     wst = None
     args.drab_t, args.drab_t_ws = None, None
     if drab_t is not None:
         if args.num_time_buckets == 0 or drab_t.dtype != torch.float32 or not drab_t.is_contiguous() \
                 or drab_t.numel() != args.heads * args.num_time_buckets:
             raise L.GrkError('drab_t must be a contiguous fp32 [H, num_time_buckets] tensor of a time-bias call')
-        wst = torch.empty(drab_t.numel(), dtype=torch.int64, device=drab_t.device)
+        wst = _clean_ws(drab_t.numel(), drab_t.device) if clean else \
+            torch.empty(drab_t.numel(), dtype=torch.int64, device=drab_t.device)
         args.drab_t, args.drab_t_ws = drab_t.data_ptr(), wst.data_ptr()
     for t, n in ((dout, 'dout'), (dq, 'dq'), (dk, 'dk'), (dv, 'dv')):
         if t is not None and (t.stride(1) != 1 or t.stride(0) % 8):
             raise L.GrkError(f'{n} must be row-major with a row stride multiple of 8')
-    ws = None if drab is None or not parts & L.ATTN_BWD_DQ else torch.empty(drab.numel(), dtype=torch.int64,
-                                                                            device=drab.device)
+    if clean:   # the bins + one counter slot
+        ws = _clean_ws(drab.numel() + 1, drab.device)
+        parts |= L.ATTN_BWD_WS_CLEAN | L.ATTN_BWD_DRAB_SET
+    else:
+        ws = None if drab is None or not parts & L.ATTN_BWD_DQ else torch.empty(drab.numel(), dtype=torch.int64,
+                                                                                device=drab.device)
 
     def p_ld(t):
         return (None, 0) if t is None else (t.data_ptr(), t.stride(0))

@@ -264,12 +264,12 @@ def hstu_core_backward(gy: Tensor, pre: Tensor, o: Tensor, stats: Tensor, rab: T
     dpre = torch.empty(pre.shape[0], 4 * D, dtype=torch.bfloat16, device=pre.device)
     do, _, dw, db = K.norm_gate_bwd(g, o, pb[:, :D], ln_w.float().contiguous(), ln_b.float().contiguous(), stats,
                                     dropout_p, _seed_arg(seed, seed_dev), du=dpre[:, :D])
-    drab = torch.zeros_like(rab32)
+    drab = torch.empty_like(rab32)   # written by the backward (drab_set): no fill kernels
     rab_t32 = _f32(rab_t)
-    drab_t = torch.zeros_like(rab_t32) if rab_t is not None else None
+    drab_t = torch.empty_like(rab_t32) if rab_t is not None else None
     args = _hstu_args(pb, rab32, key_valid, heads, head_dim, inv_n, precise, seq_range, timestamps, rab_t32, row_base)
     K.attention_bwd(args, None, do, None, None, dpre[:, 2 * D:3 * D], dpre[:, 3 * D:], dpre[:, D:2 * D], drab,
-                    drab_t=drab_t)
+                    drab_t=drab_t, drab_set=True)
     drab_t = drab_t.to(rab_t.dtype) if rab_t is not None else rab.new_empty(0)
     return dpre.to(pre.dtype), drab.to(rab.dtype), dw.to(ln_w.dtype), db.to(ln_b.dtype), drab_t
 

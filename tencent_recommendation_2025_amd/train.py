@@ -196,6 +196,7 @@ class Trainer:
         self.graph, self.graph_warmup = bool(graph), int(graph_warmup)
         self.graph_audit = bool(graph_audit)  # keep the captured graph and census its nodes (graph_nodes)
         self.graph_nodes = None
+        self._seeds = {}   # cached backward seeds (_backward)
         if self.graph:
             why = self._graph_blocker()
             if why:
@@ -260,6 +261,15 @@ class Trainer:
         l2 = self.opt.l2_term() if getattr(self.opt, 'l2_emb', 0.0) else None
         return loss if l2 is None else loss + l2
 
+    def _backward(self, loss):
+        """loss.backward() seeded with a cached ones tensor: autograd's own seed is a
+        fill kernel per step (inside the captured graph too)."""
+        key = (loss.shape, loss.dtype, loss.device)
+        seed = self._seeds.get(key)
+        if seed is None:
+            seed = self._seeds[key] = torch.ones_like(loss)
+        loss.backward(seed)
+
     def eager_step(self, batch, next_batch=None):
         self.opt.zero_grad()
         if hasattr(self.opt, 'prepare'):  # row-sharded tables: fetch this batch's rows from their owners
@@ -269,7 +279,7 @@ class Trainer:
         if hasattr(self.opt, 'begin_step'):  # deferred table updates: bring this batch's rows up to date
             self.opt.begin_step(batch)
         loss = self.compute_loss(batch)
-        loss.backward()
+        self._backward(loss)
         self.opt.step()
         if self.jagged and not torch.cuda.is_current_stream_capturing():
             self.check_jagged()   # eager: one host sync per step
@@ -395,7 +405,7 @@ class Trainer:
         try:
             def fwd_bwd():
                 loss = self.compute_loss(batch)
-                loss.backward()
+                self._backward(loss)
                 G.join_side_work()
                 return loss.detach()
             loss = self._on_side(fwd_bwd)
@@ -454,7 +464,7 @@ class Trainer:
         with torch.cuda.graph(g, pool=self._pool, stream=self._side, capture_error_mode='thread_local'):
             if self._sharded:
                 loss = self.compute_loss(self._static)
-                loss.backward()
+                self._backward(loss)
                 G.join_side_work()   # every side-stream branch rejoins the capture stream
                 self._static_loss = loss.detach()
             else:

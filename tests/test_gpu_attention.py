@@ -301,6 +301,48 @@ def test_non_contiguous_key_valid(K, kind, use_ranges):
         assert err < TOL_PRECISE, f'{key}: normwise rel err {err:.2e}'
 
 
+@pytest.mark.parametrize('T,nbt', [(130, 0), (201, 16), (600, 0)])  # whole-sequence (+ time bias), chunked
+def test_bwd_drab_set_clean_scratch_equals_accumulate(K, T, nbt):
+    """GRK_ATTN_BWD_WS_CLEAN | GRK_ATTN_BWD_DRAB_SET (the model's path): drab / drab_t
+    written through the stream's clean fixed-point scratch -- finalized by the last dq
+    workgroup (whole-sequence kernel) or by the fallback launch (chunked) -- equal the
+    accumulate path into zeroed buffers bit for bit, call after call (the scratch and
+    its counter are left zero); dq / dk / dv unchanged."""
+    from tencent_recommendation_2025_amd import _lib as L
+    B, H, hd = 3, 2, 64
+    D = H * hd
+    x, valid = make_inputs(B, T, H, hd, [T, T // 2, 7], 9)
+    xd = torch.from_numpy(x).to(DEV).to(torch.bfloat16)
+    kv = torch.from_numpy(valid).to(DEV)
+    extra = dict(rab=0.3 * torch.randn(H, T, device=DEV), inv_n=1.0 / T, scale=hd ** -0.5)
+    if nbt:
+        ts = 1_700_000_000 + torch.cumsum(torch.randint(1, 100000, (B, T)), 1)
+        extra.update(timestamps=ts.to(DEV), rab_t=0.3 * torch.randn(H, nbt, device=DEV))
+    args = K.attn_args(L.ATTN_HSTU, xd[:, :D], xd[:, D:2 * D], xd[:, 2 * D:], B, T, H, hd, key_valid=kv,
+                       out_dtype=torch.bfloat16, act='silu', precise=1, **extra)
+    out = torch.empty(B * T, D, dtype=torch.bfloat16, device=DEV)
+    K.attention_fwd(args, out, torch.empty(B, H, T, device=DEV))
+    dout = torch.randn(B * T, D, device=DEV).bfloat16()
+
+    def bwd(drab_set, fill):
+        g = [torch.empty(B * T, D, dtype=torch.bfloat16, device=DEV) for _ in range(3)]
+        drab = torch.full((H, T), fill, device=DEV)
+        drab_t = torch.full((H, nbt), fill, device=DEV) if nbt else None
+        K.attention_bwd(args, None, dout, None, None, *g, drab, drab_t=drab_t, drab_set=drab_set)
+        return g, drab, drab_t
+
+    ref = bwd(False, 0.0)
+    for _ in range(3):
+        got = bwd(True, float('nan'))   # written, not accumulated: the fill never shows
+        for a, b in zip(ref[0], got[0]):
+            assert torch.equal(a, b)
+        assert torch.equal(ref[1], got[1])
+        if nbt:
+            assert torch.equal(ref[2], got[2])
+    acc = bwd(False, 1.0)   # the default still accumulates
+    assert torch.equal(acc[1], ref[1] + 1.0)
+
+
 @pytest.mark.parametrize('kind', [0, 1], ids=['softmax', 'hstu'])
 @pytest.mark.parametrize('T', [130, 600])  # whole-sequence and chunked kernels
 def test_bwd_parts_equal_full_backward(K, kind, T):
