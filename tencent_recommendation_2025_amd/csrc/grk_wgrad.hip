@@ -244,30 +244,64 @@ __global__ void __launch_bounds__(64 * WM * WN) k_wgrad_lds(const bf16_t* __rest
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
   float cs[2] = {0.f, 0.f};
+  // ring_frag's addresses, hoisted: per lane the byte offsets (within a stage) of the
+  // lo / hi halves of fragments i (A) and j (B) at k rows 0..15; rows 16..31 have the
+  // same swizzle, so k step 1 is an immediate offset (16 RB) on the same registers.
+  // Every fragment read of a step is issued before its MFMAs, so the second half's
+  // reads run under the first half's MFMAs (SQ: 34 % of wave cycles waited on
+  // instruction dependencies with a read -> wait -> MFMA sequence per k step, and
+  // ~15 VALU address ops per k step).
+  unsigned oa[2][2], ob[2][2];
+  {
+    const int g = lane >> 4, ii = lane & 15;
+    const int row = 4 * (g >> 1) + (ii >> 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ca = 64 * wm + 32 * i + 16 * (g & 1) + 4 * (ii & 3);
+      const int cb = 64 * wn + 32 * i + 16 * (g & 1) + 4 * (ii & 3);
+      oa[i][0] = row * G::RBA + 16 * ((ca >> 3) ^ wg_swz(row)) + 2 * (ca & 7);
+      oa[i][1] = (row + 8) * G::RBA + 16 * ((ca >> 3) ^ wg_swz(row + 8)) + 2 * (ca & 7);
+      ob[i][0] = G::IMGA + row * G::RBB + 16 * ((cb >> 3) ^ wg_swz(row)) + 2 * (cb & 7);
+      ob[i][1] = G::IMGA + (row + 8) * G::RBB + 16 * ((cb >> 3) ^ wg_swz(row + 8)) + 2 * (cb & 7);
+    }
+  }
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef __attribute__((address_space(3))) char lds_char;
+  auto frag = [&](const lds_char* st, unsigned lo, unsigned hi, int koff) {
+    const s16x4 l = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(st + lo + koff));
+    const s16x4 h = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(st + hi + koff));
+    const bf16x4 l4 = __builtin_bit_cast(bf16x4, l), h4 = __builtin_bit_cast(bf16x4, h);
+    bf16x8 f;
+    f[0] = l4[0]; f[1] = l4[1]; f[2] = l4[2]; f[3] = l4[3];
+    f[4] = h4[0]; f[5] = h4[1]; f[6] = h4[2]; f[7] = h4[3];
+    return f;
+  };
 
   for (int t = 0; t < NST - 1 && t < nsteps; ++t) issue(t, t);
   for (int t = 0; t < nsteps; ++t) {
     ring_wait<G::P, NST>(nsteps - 1 - t);
     if (t + NST - 1 < nsteps) issue(t + NST - 1, (t + NST - 1) % NST);
-    const char* ia = smem + (t % NST) * G::STAGE;
-    const char* ib = ia + G::IMGA;
+    const lds_char* st = (const lds_char*)smem + (t % NST) * G::STAGE;
+    bf16x8 fa[2][2], fb[2][2];   // [k step][i / j]
 #pragma unroll
     for (int ks = 0; ks < kWgK / 16; ++ks) {
-      bf16x8 fa[2], fb[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = ring_frag<G::RBA>(ia, 16 * ks, 64 * wm + 32 * i, lane);
+      for (int i = 0; i < 2; ++i) fa[ks][i] = frag(st, oa[i][0], oa[i][1], ks * 16 * G::RBA);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) fb[j] = ring_frag<G::RBB>(ib, 16 * ks, 64 * wn + 32 * j, lane);
+      for (int j = 0; j < 2; ++j) fb[ks][j] = frag(st, ob[j][0], ob[j][1], ks * 16 * G::RBB);
+    }
+#pragma unroll
+    for (int ks = 0; ks < kWgK / 16; ++ks) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fa[ks][i], fb[ks][j], acc[i][j]);
       if (do_db) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           float q = 0.f;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) q += static_cast<float>(fa[i][e]);
+          for (int e = 0; e < 8; ++e) q += static_cast<float>(fa[ks][i][e]);
           cs[i] += q;
         }
       }
