@@ -191,13 +191,15 @@ __global__ void __launch_bounds__(256) k_wgrad(const bf16_t* __restrict__ A, int
 //   * columns past M / N read a valid column instead (their outputs are
 //     never stored); K must be a multiple of 32 (no partial steps: the
 //     slices are whole steps) -- else the register-staged kernel runs.
-template <bool DB, int WM, int WN, int NST>
+// SUB: 32-row k steps per ring stage (one barrier per SUB steps; the slice length
+// is then a multiple of 32 SUB rows).
+template <bool DB, int WM, int WN, int NST, int SUB = 1>
 __global__ void __launch_bounds__(64 * WM * WN) k_wgrad_lds(const bf16_t* __restrict__ A, int64_t lda,
                                                             const bf16_t* __restrict__ B, int64_t ldb, int K, int M,
                                                             int N, int kchunk, float* __restrict__ part,
                                                             float* __restrict__ dbpart) {
   using G = WgRing<WM, WN, NST>;
-  __shared__ __attribute__((aligned(16))) char smem[NST * G::STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[NST * SUB * G::STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % WM, wn = w / WM, r = lane & 31, hh = lane >> 5;
   const unsigned nx = gridDim.x, my = gridDim.y;
@@ -207,7 +209,7 @@ __global__ void __launch_bounds__(64 * WM * WN) k_wgrad_lds(const bf16_t* __rest
   const int bx = (int)(logical % nx), by = (int)((logical / nx) % my), s = (int)(logical / (nx * my));
   const int n0 = bx * G::TN, m0 = by * G::TM;
   const int kb = s * kchunk, ke = min(K, kb + kchunk);
-  const int nsteps = ke > kb ? (ke - kb) / kWgK : 0;
+  const int nsteps = ke > kb ? (ke - kb) / (kWgK * SUB) : 0;   // ring stages of SUB steps
   const bool do_db = DB && bx == 0 && wn == 0;
   // this lane's source rows: DMA instruction q of an image covers rows [q * 1024 / RB, ...)
   const bf16_t* pa[G::PWA];
@@ -231,12 +233,15 @@ __global__ void __launch_bounds__(64 * WM * WN) k_wgrad_lds(const bf16_t* __rest
       (int)((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem));
   const unsigned wu = (unsigned)__builtin_amdgcn_readfirstlane(w);   // wave-uniform: the DMA base is an SGPR
   auto issue = [&](int step, int buf) {
-    const unsigned base = lds0 + buf * G::STAGE;
-    const int64_t ka = (int64_t)step * kWgK * lda, kbb = (int64_t)step * kWgK * ldb;
 #pragma unroll
-    for (int i = 0; i < G::PWA; ++i) wg_dma16(pa[i] + ka, base + (wu * G::PWA + i) * 1024);
+    for (int u = 0; u < SUB; ++u) {
+      const unsigned base = lds0 + (buf * SUB + u) * G::STAGE;
+      const int64_t ka = (int64_t)(step * SUB + u) * kWgK * lda, kbb = (int64_t)(step * SUB + u) * kWgK * ldb;
 #pragma unroll
-    for (int i = 0; i < G::PWB; ++i) wg_dma16(pb[i] + kbb, base + G::IMGA + (wu * G::PWB + i) * 1024);
+      for (int i = 0; i < G::PWA; ++i) wg_dma16(pa[i] + ka, base + (wu * G::PWA + i) * 1024);
+#pragma unroll
+      for (int i = 0; i < G::PWB; ++i) wg_dma16(pb[i] + kbb, base + G::IMGA + (wu * G::PWB + i) * 1024);
+    }
   };
   f32x16 acc[2][2];
 #pragma unroll
@@ -279,9 +284,11 @@ __global__ void __launch_bounds__(64 * WM * WN) k_wgrad_lds(const bf16_t* __rest
 
   for (int t = 0; t < NST - 1 && t < nsteps; ++t) issue(t, t);
   for (int t = 0; t < nsteps; ++t) {
-    ring_wait<G::P, NST>(nsteps - 1 - t);
+    ring_wait<G::P * SUB, NST>(nsteps - 1 - t);
     if (t + NST - 1 < nsteps) issue(t + NST - 1, (t + NST - 1) % NST);
-    const lds_char* st = (const lds_char*)smem + (t % NST) * G::STAGE;
+#pragma unroll
+    for (int u = 0; u < SUB; ++u) {
+    const lds_char* st = (const lds_char*)smem + ((t % NST) * SUB + u) * G::STAGE;
     bf16x8 fa[2][2], fb[2][2];   // [k step][i / j]
 #pragma unroll
     for (int ks = 0; ks < kWgK / 16; ++ks) {
@@ -305,6 +312,7 @@ __global__ void __launch_bounds__(64 * WM * WN) k_wgrad_lds(const bf16_t* __rest
           cs[i] += q;
         }
       }
+    }
     }
   }
   float* out = part + (int64_t)s * M * N;
@@ -406,6 +414,10 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(const float* __restrict__ 
 // K slices: about two workgroups per CU (latency hiding), slices of >= kSliceRows rows.
 // Measured (round 5): 256- and 128-row slices slower than 512.
 constexpr int kSliceRows = 512;
+#ifndef GRK_WGRAD_SUB2
+#define GRK_WGRAD_SUB2 1   // A/B builds: 0 = one barrier per 32-row step in the 256 x 128 ring
+#endif
+constexpr bool kWgSub2 = GRK_WGRAD_SUB2;
 int wgrad_splits(int64_t K, int64_t M, int64_t N) {
   const int64_t tiles = ((M + kWgTile - 1) / kWgTile) * ((N + kWgTile - 1) / kWgTile);
   int S = 1;
@@ -465,7 +477,9 @@ extern "C" int grk_wgrad(const void* dy, int64_t ld_dy, const void* x, int64_t l
   hipStream_t s = (hipStream_t)stream;
   float* part = (float*)workspace;
   float* dbp = part + (size_t)S * m * n;
-  const int kchunk = (int)(((k + S - 1) / S + kWgK - 1) / kWgK * kWgK);
+  // slices of whole ring stages (64 rows for the two-step 256 x 128 ring)
+  const int kq = (pl.kind == 2 && kWgSub2 && k % 64 == 0) ? 64 : kWgK;
+  const int kchunk = (int)(((k + S - 1) / S + kq - 1) / kq * kq);
   const dim3 grid((unsigned)((n + pl.tn - 1) / pl.tn), (unsigned)((m + pl.tm - 1) / pl.tm), (unsigned)S);
   const bf16_t *A = (const bf16_t*)dy, *Bx = (const bf16_t*)x;
 #define GRK_WG(KERN, THREADS)                                                                               \
@@ -473,7 +487,12 @@ extern "C" int grk_wgrad(const void* dy, int64_t ld_dy, const void* x, int64_t l
     if (db) KERN<true><<<grid, THREADS, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, dbp); \
     else KERN<false><<<grid, THREADS, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, nullptr); \
   } while (0)
-  if (pl.kind == 2) {
+  if (pl.kind == 2 && kWgSub2 && k % 64 == 0 && kchunk % 64 == 0) {
+    if (db) k_wgrad_lds<true, 4, 2, 3, 2><<<grid, 512, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part,
+                                                              dbp);
+    else k_wgrad_lds<false, 4, 2, 3, 2><<<grid, 512, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk,
+                                                             part, nullptr);
+  } else if (pl.kind == 2) {
     if (db) k_wgrad_lds<true, 4, 2, 6><<<grid, 512, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part, dbp);
     else k_wgrad_lds<false, 4, 2, 6><<<grid, 512, 0, s>>>(A, ld_dy, Bx, ld_x, (int)k, (int)m, (int)n, kchunk, part,
                                                           nullptr);
