@@ -312,8 +312,12 @@ def _one_step_grads(state, jagged, batch, quantum=128):
 # every gradient at 1e-5: test_jagged_encode_equals_padded_fp32.
 #   capacity == B*T (same GEMM shapes, so the same kernels): every parameter 1e-5
 #     normwise except the cancellation-dominated dnn / feature-table sums (1e-3);
-#   the bench's capacity rounding (128 rows here): every parameter 5e-3.
-JAGGED_STEP_TOL = dict(loss=1e-5, grad_same=1e-5, grad_sums=1e-3, grad_capacity=5e-3)
+#   the bench's capacity rounding (128 rows here): every parameter 5e-3, and the loss
+#   5e-5: the forward GEMMs of another row count may run other hipBLASLt kernels (the
+#   timed plan choice also varies by process), each output one bf16 ulp
+#   apart -- bitwise in most runs, 1.46e-5 once in round 6 (gpurun_out/r6x, after 5
+#   steps, capacity 512) with every gradient inside its 5e-3.
+JAGGED_STEP_TOL = dict(loss=1e-5, loss_capacity=5e-5, grad_same=1e-5, grad_sums=1e-3, grad_capacity=5e-3)
 DNN_SUMS = ('itemdnn.', 'userdnn.', 'emb_transform.', 'group.small', 'group.item', 'group.user')
 
 
@@ -348,7 +352,7 @@ def test_jagged_step_matches_padded_from_identical_parameters():
             print(f'after {trained} steps, batch {probe}, {name} (capacity '
                   f'{J.capacity_for(J.span_rows(batch[3]), quantum)}): loss {loss_err:.2e}',
                   [(k, f'{errs[k]:.2e}') for k in top])
-            if loss_err > JAGGED_STEP_TOL['loss']:
+            if loss_err > JAGGED_STEP_TOL['loss_capacity' if name == 'capacity' else 'loss']:
                 bad[(trained, name, 'loss')] = loss_err
             for k, v in errs.items():
                 tol = (JAGGED_STEP_TOL['grad_capacity'] if name == 'capacity' else
