@@ -128,7 +128,7 @@ for e in entries:
         # one grk_wgrad call = the ring kernel (k_wgrad_lds<, k_wgrad< before round 4) + k_wgrad_reduce;
         # round 5: the entry is the whole family, the PMC is the uvqk shape's (the 8-wave 256 x 128 ring,
         # the largest reduce grid)
-        big = 'k_wgrad_lds<true, 4, 2, 6>'
+        big = 'k_wgrad_lds<true, 4, 2, '   # the 256 x 128 ring (<..., 6> to round 5, <..., 3, 2> since round 6)
         if any(big in r['Kernel_Name'] for r in fetch):
             f1, w1, n1 = traffic(big)
             f2, w2, n2 = traffic('k_wgrad_reduce', True)
