@@ -285,6 +285,9 @@ constexpr int kSS2Pad = 64;                 // idc / lqc rows past M the meta DM
 // slice wholly inside one workgroup leaves its (max, sum) in slot F[x][block]; a part
 // cut between workgroups leaves one per piece in W[workgroup][first / last] --
 // k_ss_combine merges the pieces of every slice in a fixed order.
+#ifndef GRK_SS_FWD_PAIRS
+#define GRK_SS_FWD_PAIRS 0   // A/B builds: 1 = tile pairs, one barrier per pair
+#endif
 constexpr int kSS2PerXcd = 32;
 constexpr int kSS2Grid = 8 * kSS2PerXcd;
 
@@ -353,13 +356,34 @@ __global__ void __launch_bounds__(512) k_ss_fwd2(SSParams p, int rbmax) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) of[ks] = gload8(p.hc + (int64_t)oc * D + 16 * ks + 8 * hh, ook);
     lds_barrier();   // every wave is past the previous piece's reads of the ring
-    for (int i = 0; i < NST - 1 && i < nt; ++i) issue(t0 + i, i);
     float m = -INFINITY, l = 0.f;
+#if GRK_SS_FWD_PAIRS
+    // tile pairs: the NST = 4 slots as 2 stages of 2 tiles, one barrier per pair (the
+    // next pair loads under this pair's MFMAs); an odd piece's last pair loads its
+    // last tile twice (a constant DMA count per stage)
+    static_assert(NST == 4, "pairs of the 4 ring slots");
+    auto issue2 = [&](int st, int bf) {
+      issue(t0 + 2 * st, 2 * bf);
+      issue(t0 + min(2 * st + 1, nt - 1), 2 * bf + 1);
+    };
+    issue2(0, 0);
+    const int npair = (nt + 1) / 2;
+    for (int st = 0; st < npair; ++st) {
+      wg_wait_barrier<0>();   // this pair landed; every wave is past the previous pair
+      if (st + 1 < npair) issue2(st + 1, (st + 1) & 1);
+      for (int h2 = 0; h2 < 2; ++h2) {
+      const int i = 2 * st + h2;
+      if (i >= nt) break;
+      if (!wave_live) continue;
+      const char* img = smem + (2 * (st & 1) + h2) * kSS2Stage;
+#else
+    for (int i = 0; i < NST - 1 && i < nt; ++i) issue(t0 + i, i);
     for (int i = 0; i < nt; ++i) {
       ring_wait<P, NST>(nt - 1 - i);
       if (i + NST - 1 < nt) issue(t0 + i + NST - 1, (i + NST - 1) % NST);
       if (!wave_live) continue;
       const char* img = smem + (i % NST) * kSS2Stage;
+#endif
       const int64_t* tid = reinterpret_cast<const int64_t*>(img + kSS2Img);
       const float* tlq = reinterpret_cast<const float*>(img + kSS2Img + 256);
       // the E fragments kSSPre k-steps ahead of their MFMA (a read issued right before its
@@ -396,6 +420,9 @@ __global__ void __launch_bounds__(512) k_ss_fwd2(SSParams p, int rbmax) {
       l = l * __builtin_amdgcn_exp2f(m - mn) + rs;
       m = mn;
     }
+#if GRK_SS_FWD_PAIRS
+    }
+#endif
     if (hh == 0 && ook) {
       const int64_t at = (whole ? ss2_fslot(x, b, rbmax) : ss2_wslot(g, first ? 0 : 1, rbmax)) + wave * 32 + r;
       p.pm[at] = m;
