@@ -286,7 +286,7 @@ constexpr int kSS2Pad = 64;                 // idc / lqc rows past M the meta DM
 // cut between workgroups leaves one per piece in W[workgroup][first / last] --
 // k_ss_combine merges the pieces of every slice in a fixed order.
 #ifndef GRK_SS_FWD_PAIRS
-#define GRK_SS_FWD_PAIRS 0   // A/B builds: 1 = tile pairs, one barrier per pair
+#define GRK_SS_FWD_PAIRS 1   // A/B builds: 0 = one barrier per tile
 #endif
 constexpr int kSS2PerXcd = 32;
 constexpr int kSS2Grid = 8 * kSS2PerXcd;
