@@ -123,3 +123,11 @@ def test_write_columns_refuses_bad_blocks(lib):
     b[1] = lib.GrkColumnBlock(16, 0, 8, 32, 7, 0)                       # bad dtype
     assert h.grk_write_columns(b, 2, 10, 16, 64, lib.GRK_BF16, None) == lib.GRK_EINVAL
     assert h.grk_write_columns(b, 0, 10, 16, 64, lib.GRK_BF16, None) == lib.GRK_EINVAL
+
+
+def test_attention_backward_part_flags_match_header(lib):
+    """The Python constants of grk_attention_bwd_parts' flags are the header's values."""
+    text = HEADER.read_text()
+    want = {m.group(1): int(m.group(2)) for m in re.finditer(r'#define GRK_ATTN_BWD_([A-Z_]+) (\d+)', text)}
+    assert want == {'DQ': 1, 'DKDV': 2, 'WS_CLEAN': 4, 'DRAB_SET': 8}
+    assert (lib.ATTN_BWD_DQ, lib.ATTN_BWD_DKDV, lib.ATTN_BWD_WS_CLEAN, lib.ATTN_BWD_DRAB_SET) == (1, 2, 4, 8)
